@@ -1,0 +1,223 @@
+#!/usr/bin/env python3
+"""Benchmark: rows scanned/s of the scan-filter-aggregate query on synthetic dict-encoded fact segments.
+
+Workload (BASELINE.json configs[1]): 8 segments x 125,000,000 docs per GPU
+(1B rows), 10 fixed-bit dictionary-encoded INT columns d0..d9 with cardinalities
+{16, 100, 1000, 4096, 10000, 65536, 1000, 1000, 2^20, 1000} (bits {4,7,10,12,14,16,10,10,20,10}),
+generated in HBM (seeded splitmix64), query
+    SELECT COUNT(*), SUM(d8) FROM fact WHERE d2 BETWEEN 100 AND 599 AND d0 IN (1, 3, 5, 7)
+One step = one query over all of a rank's segments, results back on the host. With N ranks each
+GPU holds its own 8 segments (weak scaling, config 5 at N=8) and the per-rank partial aggregates are
+merged by an all-reduce over RCCL inside the timed region.
+
+Prints ONE JSON line (rank 0). Launched as `python bench.py` (N=1) or via torch.distributed.run.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "incubator-pinot_amd"))
+
+COLUMNS = [("d0", 16), ("d1", 100), ("d2", 1000), ("d3", 4096), ("d4", 10000), ("d5", 65536), ("d6", 1000),
+           ("d7", 1000), ("d8", 1 << 20), ("d9", 1000)]
+QUERY = "SELECT COUNT(*), SUM(d8) FROM fact WHERE d2 BETWEEN 100 AND 599 AND d0 IN (1, 3, 5, 7)"
+BASE_SEED = 0x5EED0000
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (8.0 TB/s spec)
+BITS = {n: max(1, (c - 1).bit_length()) for n, c in COLUMNS}
+
+
+def algorithmic_bytes(num_docs):
+    """Per-segment algorithmic HBM bytes of each kernel:
+    filter scan: d0 + d2 packed streams + bitset write; aggregate: d8 packed stream + bitset read."""
+    bitset = (num_docs + 63) // 64 * 8
+    filt = (num_docs * BITS["d0"] + 7) // 8 + (num_docs * BITS["d2"] + 7) // 8 + bitset
+    agg = (num_docs * BITS["d8"] + 7) // 8 + bitset
+    return filt, agg
+
+
+def cpu_baseline(threads, segs, docs):
+    """Reference-faithful C executor (oracle/faithful.c) on a bounded sample of the same workload."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import faithful
+    from concurrent.futures import ThreadPoolExecutor
+    faithful.load()
+    t0 = time.time()
+    # generate the sample columns in parallel (ctypes releases the GIL)
+    table = faithful.SyntheticTable(COLUMNS, docs, 0, BASE_SEED, needed=set())
+    jobs = {}
+    with ThreadPoolExecutor(threads) as ex:
+        for s in range(segs):
+            for i, (name, card) in enumerate(COLUMNS):
+                if name in ("d0", "d2", "d8"):
+                    jobs[(s, name)] = ex.submit(faithful.synth_column, BASE_SEED + s, i, card, docs)
+    table.segments = [{n: jobs[(s, n)].result() for n in ("d0", "d2", "d8")} for s in range(segs)]
+    gen_s = time.time() - t0
+    leaves = [("d2", ("RANGE", 100, 600)), ("d0", ("IN", [1, 3, 5, 7]))]
+    faithful.run_and_count_sum(table, leaves, "d8", threads)  # warm-up (page-in)
+    times = []
+    for _ in range(3):
+        t0 = time.time()
+        cnt, sm = faithful.run_and_count_sum(table, leaves, "d8", threads)
+        times.append(time.time() - t0)
+    times.sort()
+    rows = segs * docs
+    return {"value": rows / times[1], "unit": "rows/s", "cores": threads, "kind": "port",
+            "sample": "%d segments x %d docs of the same synthetic table and query (median of 3 runs, %.2fs each; "
+                      "data generated in %.1fs); oracle/faithful.c per-doc iterator executor" %
+                      (segs, docs, times[1], gen_s),
+            "check": {"count": cnt, "sum": sm}}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--segments", type=int, default=8, help="segments per GPU")
+    ap.add_argument("--docs", type=int, default=125_000_000, help="docs per segment")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-segments", type=int, default=16)
+    ap.add_argument("--cpu-docs", type=int, default=32_000_000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--verify", action="store_true", help="check the GPU result against the C oracle (slow)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    else:
+        torch.cuda.set_device(0)
+
+    from pinot_amd import GpuEngine, ServerQueryExecutor, compile_pql
+    eng = GpuEngine(local_rank if world > 1 else 0)
+    segs = []
+    t0 = time.time()
+    for s in range(args.segments):
+        gidx = rank * args.segments + s  # segment i -> GPU i // segments (round-robin by rank block)
+        segs.append(eng.register_synthetic("fact_%d" % gidx, args.docs, COLUMNS, BASE_SEED + gidx))
+    eng.synchronize()
+    load_s = time.time() - t0
+    ex = ServerQueryExecutor(eng)
+    q = compile_pql(QUERY)
+
+    part = torch.zeros(2, dtype=torch.int64, device="cuda")
+
+    def step():
+        res, st = ex.process_query(q, segs)
+        if world > 1:
+            # CombineOperator across GPUs: exact int64 partials (COUNT, integer SUM) all-reduced over RCCL
+            part[0] = res[0]
+            part[1] = int(res[1])
+            dist.all_reduce(part)
+            return int(part[0].item()), int(part[1].item()), st
+        return res[0], int(res[1]), st
+
+    for _ in range(args.warmup):
+        step()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    eng.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        cnt, sm, st = step()
+    eng.synchronize()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = elapsed * 1000.0 / args.steps
+    total_rows = world * args.segments * args.docs
+    value = total_rows * args.steps / elapsed
+
+    # per-kernel device time (HIP events on the engine stream) in a separate pass
+    eng.set_config("timing=1")
+    kt = {0: [0.0, 0], 1: [0.0, 0]}
+    reps = max(3, min(args.steps, 10))
+    for _ in range(reps):
+        ex.process_query(q, segs)
+        for k in (0, 1):
+            ms, n = eng.last_kernel_ms(k)
+            kt[k][0] += ms
+            kt[k][1] += n
+    eng.set_config("timing=0")
+    filt_b, agg_b = algorithmic_bytes(args.docs)
+    kern = {}
+    for k, name, b in ((0, "k_filter_scan", filt_b), (1, "k_aggregate", agg_b)):
+        avg_ms = kt[k][0] / max(kt[k][1], 1)
+        kern[name] = {"avg_ms": avg_ms, "launches": kt[k][1], "bytes_per_launch": b,
+                      "gbs": b / (avg_ms / 1e3) / 1e9 if avg_ms > 0 else 0.0}
+    dom = max(kern, key=lambda n: kern[n]["avg_ms"])
+    traffic = None
+    tpath = os.path.join(REPO, "profiles", "traffic.json")
+    if os.path.exists(tpath):
+        try:
+            with open(tpath) as f:
+                traffic = json.load(f).get(dom)
+        except Exception:
+            traffic = None
+    total_alg = args.segments * (filt_b + agg_b)
+    query_gbs = total_alg / (ms_per_step / 1e3) / 1e9
+
+    out = {
+        "metric": "rows scanned/sec per query",
+        "value": value,
+        "unit": "rows/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "p50_query_ms": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32 dictIds / int64 sums",
+        "data": "synthetic (seeded splitmix64 dict-encoded segments generated in HBM)",
+        "config": {"workload": "config2: %d x %d-doc segments per GPU, 10 fixed-bit INT columns, %s" %
+                   (args.segments, args.docs, QUERY),
+                   "segments_per_gpu": args.segments, "docs_per_segment": args.docs, "parallelism": "segments%d" % world},
+        "roofline": {"bound": "hbm", "achieved": kern[dom]["gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": kern[dom]["gbs"] / HBM_PEAK_GBS, "traffic": traffic, "kernel": dom,
+                     "kernels": kern, "query_algorithmic_gbs": query_gbs,
+                     "query_frac": query_gbs / HBM_PEAK_GBS},
+        "result": {"count": cnt, "sum": sm, "docs_scanned_per_rank": st.num_docs_scanned},
+        "segment_load_s": load_s,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cb = cpu_baseline(args.cpu_threads, args.cpu_segments, args.cpu_docs)
+        out["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample")}
+        out["gpu_vs_cpu"] = value / cb["value"]
+    if args.verify and rank == 0:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import faithful
+        tab = faithful.SyntheticTable(COLUMNS, args.docs, 0, BASE_SEED, needed=set())
+        tot_c, tot_s = 0, 0.0
+        for s in range(args.segments * world):
+            tab.segments = [{n: faithful.synth_column(BASE_SEED + s, i, c, args.docs)
+                             for i, (n, c) in enumerate(COLUMNS) if n in ("d0", "d2", "d8")}]
+            c, v = faithful.run_and_count_sum(tab, [("d2", ("RANGE", 100, 600)), ("d0", ("IN", [1, 3, 5, 7]))],
+                                              "d8", args.cpu_threads)
+            tot_c += c
+            tot_s += v
+        out["verify"] = {"oracle_count": tot_c, "oracle_sum": tot_s, "match": tot_c == cnt and int(tot_s) == sm}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

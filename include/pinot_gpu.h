@@ -1,0 +1,246 @@
+/*
+ * pinot_gpu.h — C-ABI of the MI355X-native Pinot segment query executor.
+ *
+ * This is the drop-in boundary between Pinot's Java operator layer and the
+ * HIP/CDNA4 kernels. A JNI shim binds these symbols; the
+ * tests and bench bind them through ctypes. No C++/torch types cross the ABI:
+ * plain structs, pointers and sizes only. Every entry point returns a
+ * pinot_status (0 = ok); on failure pinot_gpu_last_error() holds a thread-local
+ * message. Nothing aborts across the ABI.
+ *
+ * Reference interfaces replaced (PC = pinot-core/src/main/java/org/apache/pinot/core):
+ *   pinot_gpu_engine_create / destroy   QueryExecutor.init/start/shutDown   (PC/query/executor/QueryExecutor.java:32-62)
+ *   pinot_gpu_segment_register          ImmutableSegmentLoader.load + PhysicalColumnIndexContainer
+ *                                       (PC/indexsegment/immutable/ImmutableSegmentLoader.java:59-153,
+ *                                        PC/segment/index/column/PhysicalColumnIndexContainer.java:63-121)
+ *   pinot_gpu_segment_release           SegmentDataManager release / IndexSegment.destroy
+ *                                       (ServerQueryExecutorV1Impl.java:231-233)
+ *   pinot_gpu_filter                    BaseFilterOperator.nextBlock().getBlockDocIdSet()
+ *                                       (PC/plan/FilterPlanNode.java:70-126, PC/operator/filter/)
+ *   pinot_gpu_aggregate                 AggregationOperator + CombineOperator
+ *                                       (PC/operator/query/AggregationOperator.java:56-82,
+ *                                        PC/operator/CombineOperator.java:75-196)
+ *   pinot_gpu_group_by                  AggregationGroupByOperator + CombineGroupByOperator
+ *                                       (PC/operator/query/AggregationGroupByOperator.java:64-94,
+ *                                        PC/operator/CombineGroupByOperator.java:104-228)
+ */
+#ifndef PINOT_GPU_H_
+#define PINOT_GPU_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PINOT_GPU_ABI_VERSION 1
+
+/* ------------------------------------------------------------------ status */
+typedef enum {
+  PINOT_OK = 0,
+  PINOT_ERR_BAD_ARG = 1,      /* malformed descriptor / query (maps to QueryException.QUERY_EXECUTION_ERROR) */
+  PINOT_ERR_OOM = 2,          /* HBM allocation failed: caller falls back to the CPU operator */
+  PINOT_ERR_DEVICE = 3,       /* HIP runtime / kernel error */
+  PINOT_ERR_UNSUPPORTED = 4,  /* query shape not handled on the GPU: caller falls back */
+  PINOT_ERR_BAD_QUERY = 5     /* bad literal, unknown column (BadQueryRequestException) */
+} pinot_status;
+
+/* ------------------------------------------------------------------ segment */
+typedef enum {
+  PINOT_INT = 0, PINOT_LONG = 1, PINOT_FLOAT = 2, PINOT_DOUBLE = 3, PINOT_STRING = 4
+} pinot_data_type;
+
+/* One single-value dictionary-encoded column, exactly as the segment files hold it
+ * (all multi-byte fields big-endian, as PinotDataBuffer serves them). Host pointers are
+ * only read during pinot_gpu_segment_register; nothing is retained. */
+typedef struct {
+  const char *name;
+  int32_t data_type;           /* pinot_data_type */
+  int32_t cardinality;         /* dictionary length */
+  int32_t bits_per_value;      /* PinotDataBitSet.getNumBitsPerValue(card - 1) */
+  int32_t is_sorted;           /* sorted column: sorted_index present, forward_index absent */
+  int32_t has_inverted_index;  /* bitmap inverted index present (unsorted columns) */
+  int32_t string_width;        /* STRING dictionary: bytes per padded value */
+  const uint8_t *dictionary;   uint64_t dictionary_len;     /* card * width BE values */
+  const uint8_t *forward_index; uint64_t forward_index_len; /* ceil(N*b/8) bytes, MSB-first */
+  const uint8_t *sorted_index; uint64_t sorted_index_len;   /* 2*card BE int32 [start,end] */
+  const uint8_t *inverted_index; uint64_t inverted_index_len; /* (card+1) BE int32 offsets + portable roaring */
+} pinot_column_desc;
+
+typedef struct {
+  const char *name;
+  int32_t num_docs;            /* totalRawDocs, < 2^31 */
+  int32_t num_columns;
+  const pinot_column_desc *columns;
+} pinot_segment_desc;
+
+typedef struct pinot_engine pinot_engine;   /* one per GPU (HIP device) */
+typedef int64_t pinot_segment_handle;
+
+/* ------------------------------------------------------------------ query */
+/* Filter tree as Thrift FilterQuery nodes in POSTFIX order: leaves carry the
+ * operator, column and value strings exactly as the PQL compiler emits them
+ * (RANGE: one "(lo\t\thi]" string; IN/NOT_IN: values, or one "\t\t"-joined string). */
+typedef enum {
+  PINOT_FILTER_AND = 0, PINOT_FILTER_OR = 1,
+  PINOT_FILTER_EQUALITY = 2, PINOT_FILTER_NOT = 3, PINOT_FILTER_RANGE = 4,
+  PINOT_FILTER_IN = 5, PINOT_FILTER_NOT_IN = 6
+} pinot_filter_op;
+
+typedef struct {
+  int32_t op;                  /* pinot_filter_op */
+  int32_t num_children;        /* AND/OR: number of immediately preceding subtrees */
+  const char *column;          /* leaf only */
+  int32_t num_values;          /* leaf only */
+  const char *const *values;   /* leaf only */
+} pinot_filter_node;
+
+typedef enum {
+  PINOT_AGG_COUNT = 0, PINOT_AGG_SUM = 1, PINOT_AGG_MIN = 2, PINOT_AGG_MAX = 3,
+  PINOT_AGG_AVG = 4, PINOT_AGG_DISTINCTCOUNTHLL = 5
+} pinot_agg_function;
+
+typedef struct {
+  int32_t function;            /* pinot_agg_function */
+  const char *column;          /* NULL or "*" for COUNT(*) */
+} pinot_agg_spec;
+
+typedef struct {
+  int32_t num_filter_nodes;    /* 0 = no WHERE clause */
+  const pinot_filter_node *filter;
+  int32_t num_aggregations;
+  const pinot_agg_spec *aggregations;
+  int32_t num_group_by;        /* 0 = aggregation-only */
+  const char *const *group_by;
+  int32_t num_groups_limit;    /* num.groups.limit, default 100000 (InstancePlanMakerImplV2.java:55-58) */
+  int32_t max_init_group_holder_capacity; /* array-holder threshold, default 10000 */
+} pinot_query;
+
+/* Per-query statistics (ExecutionStatistics.java:35-43). num_entries_scanned_in_filter
+ * is this engine's own count (every scan leaf reads every doc), not the reference's. */
+typedef struct {
+  int64_t num_docs_scanned;
+  int64_t num_entries_scanned_in_filter;
+  int64_t num_entries_scanned_post_filter;
+  int64_t num_total_raw_docs;
+  int64_t num_segments_processed;
+  double device_ms;            /* HIP-event time of the device work of the call */
+} pinot_exec_stats;
+
+/* Intermediate result of one aggregation function over a set of segments (already
+ * combined, i.e. what CombineOperator hands to the DataTable):
+ *   COUNT:  count
+ *   SUM:    value (double, = Σ values; exact for integer columns below 2^53)
+ *   MIN/MAX: value (+inf / -inf when no doc matched)
+ *   AVG:    value = sum, count  (AvgPair)
+ *   DISTINCTCOUNTHLL: hll_registers (merged), hll_cardinality = HyperLogLog.cardinality()
+ * exact_sum / has_exact_sum: the int64 sum the device computed for INT columns. */
+typedef struct {
+  int64_t count;
+  double value;
+  int64_t exact_sum;
+  int32_t has_exact_sum;
+  int32_t reserved;
+  int64_t hll_cardinality;
+  uint8_t hll_registers[256];
+} pinot_agg_result;
+
+typedef struct pinot_groupby_result pinot_groupby_result;
+
+/* ------------------------------------------------------------------ engine */
+const char *pinot_gpu_last_error(void);
+int32_t pinot_gpu_abi_version(void);
+int32_t pinot_gpu_device_count(void);
+
+/* config: "key=value;key=value" (keys: num.groups.limit, device.scratch.mb), may be NULL */
+pinot_status pinot_gpu_engine_create(int32_t device, const char *config, pinot_engine **out);
+pinot_status pinot_gpu_engine_destroy(pinot_engine *engine);
+/* Change configuration keys at run time (e.g. "timing=1" to record per-kernel HIP events). */
+pinot_status pinot_gpu_engine_set_config(pinot_engine *engine, const char *config);
+
+/* Copies the column buffers into HBM (one-time, cold path). */
+pinot_status pinot_gpu_segment_register(pinot_engine *engine, const pinot_segment_desc *desc,
+                                        pinot_segment_handle *out);
+pinot_status pinot_gpu_segment_release(pinot_engine *engine, pinot_segment_handle handle);
+/* Bytes of HBM held by a segment. */
+pinot_status pinot_gpu_segment_device_bytes(pinot_engine *engine, pinot_segment_handle handle, uint64_t *out);
+
+/* Filter one segment: writes the dense doc bitset (bit d of word d/64 = doc d, LSB first;
+ * caller provides ceil(N/64) words, may be NULL to only count) and the matching doc count. */
+pinot_status pinot_gpu_filter(pinot_engine *engine, pinot_segment_handle segment,
+                              int32_t num_filter_nodes, const pinot_filter_node *filter,
+                              uint64_t *bitset_out, int64_t *count_out);
+
+/* Aggregation-only query over segments on this engine's GPU; out has num_aggregations entries. */
+pinot_status pinot_gpu_aggregate(pinot_engine *engine, const pinot_segment_handle *segments,
+                                 int32_t num_segments, const pinot_query *query,
+                                 pinot_agg_result *out, pinot_exec_stats *stats);
+
+/* Group-by query over segments; the result object lists the non-empty groups. */
+pinot_status pinot_gpu_group_by(pinot_engine *engine, const pinot_segment_handle *segments,
+                                int32_t num_segments, const pinot_query *query,
+                                pinot_groupby_result **out, pinot_exec_stats *stats);
+int64_t pinot_groupby_num_groups(const pinot_groupby_result *r);
+int32_t pinot_groupby_num_columns(const pinot_groupby_result *r);
+/* '\t'-joined group key string (DictionaryBasedGroupKeyGenerator.getGroupKey); NUL-terminated. */
+const char *pinot_groupby_key(const pinot_groupby_result *r, int64_t group);
+/* Per group: count (COUNT / AVG count), value (SUM / MIN / MAX / AVG sum) for function fn. */
+pinot_status pinot_groupby_values(const pinot_groupby_result *r, int32_t fn, int64_t *counts, double *values);
+/* DISTINCTCOUNTHLL: 256 registers per group (num_groups*256 bytes) and/or final cardinalities. */
+pinot_status pinot_groupby_hll(const pinot_groupby_result *r, int32_t fn, uint8_t *registers, int64_t *cardinalities);
+/* Raw dense keys in the query's global key space (column 0 least significant). */
+pinot_status pinot_groupby_raw_keys(const pinot_groupby_result *r, int64_t *keys);
+void pinot_groupby_free(pinot_groupby_result *r);
+
+/* ------------------------------------------------------------------ multi-GPU partials
+ * Group-by over a GLOBAL dense key space, for segment sharding across ranks: each rank
+ * accumulates its segments into caller-provided DEVICE arrays (one set per rank, same
+ * shape everywhere), the caller all-reduces them over RCCL (sum for counts/sums, max for
+ * HLL registers, min/max for MIN/MAX), then pinot_gpu_group_by_finalize reads the merged
+ * arrays. The key space is the product of the group-by columns' cardinalities, which must
+ * be identical dictionaries on every segment (checked). */
+typedef struct {
+  int64_t num_keys;            /* G = Π cardinalities */
+  int32_t num_aggregations;
+  int32_t reserved;
+  /* per aggregation f: accumulator kind and element size, so the caller can allocate:
+     kind 0 = int64 sum, 1 = double sum, 2 = uint64 ordered-min, 3 = uint64 ordered-max,
+     4 = uint32 HLL registers (256 per key), 5 = none (COUNT uses the shared count array) */
+  int32_t acc_kind[8];
+} pinot_partial_layout;
+
+pinot_status pinot_gpu_group_by_layout(pinot_engine *engine, const pinot_segment_handle *segments,
+                                       int32_t num_segments, const pinot_query *query,
+                                       pinot_partial_layout *layout);
+/* counts: int64[G] device; accs[f]: device array per acc_kind (NULL for kind 5). Arrays are
+ * zero/identity-initialised by this call. */
+pinot_status pinot_gpu_group_by_partial(pinot_engine *engine, const pinot_segment_handle *segments,
+                                        int32_t num_segments, const pinot_query *query,
+                                        int64_t *counts_dev, void *const *accs_dev,
+                                        pinot_exec_stats *stats);
+pinot_status pinot_gpu_group_by_finalize(pinot_engine *engine, const pinot_segment_handle *segments,
+                                         int32_t num_segments, const pinot_query *query,
+                                         const int64_t *counts_dev, void *const *accs_dev,
+                                         pinot_groupby_result **out);
+
+/* ------------------------------------------------------------------ benchmark tooling
+ * NOT part of the Java drop-in path: builds a synthetic dictionary-encoded column
+ * directly in HBM (seeded splitmix64; docs [0, card) hold values 0..card-1 so every
+ * segment has the identity dictionary [0, card)). Used by bench.py to avoid 15 GB of
+ * host→device copies; the same generator is restated on the host in oracle/. */
+pinot_status pinot_gpu_segment_register_synthetic(pinot_engine *engine, const char *name,
+                                                  int32_t num_docs, int32_t num_columns,
+                                                  const char *const *column_names,
+                                                  const int32_t *cardinalities, uint64_t seed,
+                                                  pinot_segment_handle *out);
+
+/* Synchronise the engine's stream (bench timing brackets). */
+pinot_status pinot_gpu_synchronize(pinot_engine *engine);
+/* Device time (ms) of the named kernel class in the last call, for the roofline report:
+ * kind 0 = scan/filter kernel, 1 = aggregation kernel. */
+pinot_status pinot_gpu_last_kernel_ms(pinot_engine *engine, int32_t kind, double *ms, int64_t *launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PINOT_GPU_H_ */

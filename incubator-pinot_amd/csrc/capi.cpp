@@ -1,0 +1,307 @@
+// extern "C" entry points of libpinot_gpu.so (declared in include/pinot_gpu.h).
+// Every call: validate -> take the engine lock -> run -> map exceptions to pinot_status.
+#include <cstring>
+#include <sstream>
+
+#include "engine.h"
+
+namespace pinot {
+
+Engine::~Engine() {
+  segments.clear();
+  for (auto ev : kev) (void)hipEventDestroy(ev);
+  if (ev_start) (void)hipEventDestroy(ev_start);
+  if (ev_stop) (void)hipEventDestroy(ev_stop);
+  if (stream) (void)hipStreamDestroy(stream);
+}
+
+SegmentData &Engine::seg(int64_t h) {
+  auto it = segments.find(h);
+  require(it != segments.end(), PINOT_ERR_BAD_ARG, "unknown segment handle " + std::to_string(h));
+  return *it->second;
+}
+
+}  // namespace pinot
+
+using namespace pinot;
+
+struct pinot_engine : Engine {};
+struct pinot_groupby_result : GroupByResult {};
+
+namespace {
+thread_local std::string g_last_error;
+
+template <typename F>
+pinot_status guard(F f) {
+  try {
+    f();
+    g_last_error.clear();
+    return PINOT_OK;
+  } catch (const Error &e) {
+    g_last_error = e.what();
+    return e.status;
+  } catch (const std::bad_alloc &) {
+    g_last_error = "host out of memory";
+    return PINOT_ERR_OOM;
+  } catch (const std::exception &e) {
+    g_last_error = e.what();
+    return PINOT_ERR_DEVICE;
+  }
+}
+
+void set_device(Engine &e) { PINOT_HIP(hipSetDevice(e.device)); }
+
+std::vector<SegmentData *> resolve(Engine &e, const pinot_segment_handle *segs, int32_t n) {
+  require(n >= 1 && segs != nullptr, PINOT_ERR_BAD_ARG, "at least one segment required");
+  std::vector<SegmentData *> out;
+  for (int32_t i = 0; i < n; i++) out.push_back(&e.seg(segs[i]));
+  return out;
+}
+
+void check_query(const pinot_query *q) {
+  require(q != nullptr, PINOT_ERR_BAD_ARG, "null query");
+  require(q->num_filter_nodes == 0 || q->filter != nullptr, PINOT_ERR_BAD_ARG, "filter nodes");
+  require(q->num_aggregations >= 1 && q->aggregations != nullptr, PINOT_ERR_BAD_ARG, "aggregations");
+  require(q->num_group_by == 0 || q->group_by != nullptr, PINOT_ERR_BAD_ARG, "group_by");
+}
+
+void parse_config(Engine &e, const char *cfg) {
+  if (!cfg) return;
+  std::stringstream ss(cfg);
+  std::string kv;
+  while (std::getline(ss, kv, ';')) {
+    auto p = kv.find('=');
+    if (p == std::string::npos) continue;
+    std::string k = kv.substr(0, p), v = kv.substr(p + 1);
+    if (k == "num.groups.limit") e.num_groups_limit = std::stoi(v);
+    else if (k == "filter.force") e.force_filter = v;
+    else if (k == "timing") e.timing = v == "1" || v == "true";
+    else throw Error(PINOT_ERR_BAD_ARG, "unknown config key " + k);
+  }
+}
+}  // namespace
+
+extern "C" {
+
+const char *pinot_gpu_last_error(void) { return g_last_error.c_str(); }
+int32_t pinot_gpu_abi_version(void) { return PINOT_GPU_ABI_VERSION; }
+
+int32_t pinot_gpu_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+pinot_status pinot_gpu_engine_create(int32_t device, const char *config, pinot_engine **out) {
+  return guard([&] {
+    require(out != nullptr, PINOT_ERR_BAD_ARG, "out");
+    int n = 0;
+    PINOT_HIP(hipGetDeviceCount(&n));
+    require(device >= 0 && device < n, PINOT_ERR_BAD_ARG, "no such HIP device");
+    auto e = std::make_unique<pinot_engine>();
+    e->device = device;
+    parse_config(*e, config);
+    set_device(*e);
+    PINOT_HIP(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+    PINOT_HIP(hipEventCreate(&e->ev_start));
+    PINOT_HIP(hipEventCreate(&e->ev_stop));
+    *out = e.release();
+  });
+}
+
+pinot_status pinot_gpu_engine_destroy(pinot_engine *engine) {
+  return guard([&] {
+    if (!engine) return;
+    set_device(*engine);
+    delete engine;
+  });
+}
+
+pinot_status pinot_gpu_engine_set_config(pinot_engine *engine, const char *config) {
+  return guard([&] {
+    require(engine != nullptr, PINOT_ERR_BAD_ARG, "null engine");
+    std::lock_guard<std::mutex> lk(engine->mu);
+    parse_config(*engine, config);
+  });
+}
+
+pinot_status pinot_gpu_segment_register(pinot_engine *engine, const pinot_segment_desc *desc,
+                                        pinot_segment_handle *out) {
+  return guard([&] {
+    require(engine && desc && out, PINOT_ERR_BAD_ARG, "null argument");
+    std::lock_guard<std::mutex> lk(engine->mu);
+    set_device(*engine);
+    auto seg = register_segment(*engine, *desc);
+    const int64_t h = engine->next_handle++;
+    engine->segments[h] = std::move(seg);
+    *out = h;
+  });
+}
+
+pinot_status pinot_gpu_segment_register_synthetic(pinot_engine *engine, const char *name, int32_t num_docs,
+                                                  int32_t num_columns, const char *const *column_names,
+                                                  const int32_t *cardinalities, uint64_t seed,
+                                                  pinot_segment_handle *out) {
+  return guard([&] {
+    require(engine && out, PINOT_ERR_BAD_ARG, "null argument");
+    std::lock_guard<std::mutex> lk(engine->mu);
+    set_device(*engine);
+    auto seg = register_synthetic(*engine, name, num_docs, num_columns, column_names, cardinalities, seed);
+    const int64_t h = engine->next_handle++;
+    engine->segments[h] = std::move(seg);
+    *out = h;
+  });
+}
+
+pinot_status pinot_gpu_segment_release(pinot_engine *engine, pinot_segment_handle handle) {
+  return guard([&] {
+    require(engine != nullptr, PINOT_ERR_BAD_ARG, "null engine");
+    std::lock_guard<std::mutex> lk(engine->mu);
+    set_device(*engine);
+    PINOT_HIP(hipStreamSynchronize(engine->stream));
+    require(engine->segments.erase(handle) == 1, PINOT_ERR_BAD_ARG, "unknown segment handle");
+  });
+}
+
+pinot_status pinot_gpu_segment_device_bytes(pinot_engine *engine, pinot_segment_handle handle, uint64_t *out) {
+  return guard([&] {
+    require(engine && out, PINOT_ERR_BAD_ARG, "null argument");
+    std::lock_guard<std::mutex> lk(engine->mu);
+    *out = engine->seg(handle).device_bytes;
+  });
+}
+
+pinot_status pinot_gpu_filter(pinot_engine *engine, pinot_segment_handle segment, int32_t num_filter_nodes,
+                              const pinot_filter_node *filter, uint64_t *bitset_out, int64_t *count_out) {
+  return guard([&] {
+    require(engine != nullptr, PINOT_ERR_BAD_ARG, "null engine");
+    require(num_filter_nodes == 0 || filter != nullptr, PINOT_ERR_BAD_ARG, "filter nodes");
+    std::lock_guard<std::mutex> lk(engine->mu);
+    set_device(*engine);
+    SegmentData &s = engine->seg(segment);
+    std::unique_ptr<FilterTreeInput> tree;
+    if (num_filter_nodes > 0) tree = std::make_unique<FilterTreeInput>(decode_filter(num_filter_nodes, filter));
+    exec_filter(*engine, s, tree.get(), bitset_out, count_out);
+  });
+}
+
+pinot_status pinot_gpu_aggregate(pinot_engine *engine, const pinot_segment_handle *segments, int32_t num_segments,
+                                 const pinot_query *query, pinot_agg_result *out, pinot_exec_stats *stats) {
+  return guard([&] {
+    require(engine && out, PINOT_ERR_BAD_ARG, "null argument");
+    check_query(query);
+    require(query->num_group_by == 0, PINOT_ERR_BAD_ARG, "group-by query passed to pinot_gpu_aggregate");
+    std::lock_guard<std::mutex> lk(engine->mu);
+    set_device(*engine);
+    exec_aggregate(*engine, resolve(*engine, segments, num_segments), *query, out, stats);
+  });
+}
+
+pinot_status pinot_gpu_group_by(pinot_engine *engine, const pinot_segment_handle *segments, int32_t num_segments,
+                                const pinot_query *query, pinot_groupby_result **out, pinot_exec_stats *stats) {
+  return guard([&] {
+    require(engine && out, PINOT_ERR_BAD_ARG, "null argument");
+    check_query(query);
+    require(query->num_group_by >= 1, PINOT_ERR_BAD_ARG, "aggregation-only query passed to pinot_gpu_group_by");
+    std::lock_guard<std::mutex> lk(engine->mu);
+    set_device(*engine);
+    auto r = exec_group_by(*engine, resolve(*engine, segments, num_segments), *query, stats);
+    auto *res = new pinot_groupby_result();
+    static_cast<GroupByResult &>(*res) = std::move(*r);
+    *out = res;
+  });
+}
+
+int64_t pinot_groupby_num_groups(const pinot_groupby_result *r) { return r ? (int64_t)r->raw_keys.size() : 0; }
+int32_t pinot_groupby_num_columns(const pinot_groupby_result *r) { return r ? r->num_columns : 0; }
+
+const char *pinot_groupby_key(const pinot_groupby_result *r, int64_t group) {
+  if (!r || group < 0 || group >= (int64_t)r->keys.size()) return nullptr;
+  return r->keys[group].c_str();
+}
+
+pinot_status pinot_groupby_values(const pinot_groupby_result *r, int32_t fn, int64_t *counts, double *values) {
+  return guard([&] {
+    require(r && fn >= 0 && fn < (int32_t)r->functions.size(), PINOT_ERR_BAD_ARG, "function index");
+    const size_t n = r->raw_keys.size();
+    if (counts && n) memcpy(counts, r->counts[fn].data(), n * 8);
+    if (values && n) memcpy(values, r->values[fn].data(), n * 8);
+  });
+}
+
+pinot_status pinot_groupby_hll(const pinot_groupby_result *r, int32_t fn, uint8_t *registers, int64_t *cardinalities) {
+  return guard([&] {
+    require(r && fn >= 0 && fn < (int32_t)r->functions.size(), PINOT_ERR_BAD_ARG, "function index");
+    require(r->functions[fn] == PINOT_AGG_DISTINCTCOUNTHLL, PINOT_ERR_BAD_ARG, "not a DISTINCTCOUNTHLL function");
+    const size_t n = r->raw_keys.size();
+    if (registers && n) memcpy(registers, r->hll[fn].data(), n * 256);
+    if (cardinalities)
+      for (size_t i = 0; i < n; i++) cardinalities[i] = hll_cardinality(r->hll[fn].data() + i * 256);
+  });
+}
+
+pinot_status pinot_groupby_raw_keys(const pinot_groupby_result *r, int64_t *keys) {
+  return guard([&] {
+    require(r && keys, PINOT_ERR_BAD_ARG, "null argument");
+    if (!r->raw_keys.empty()) memcpy(keys, r->raw_keys.data(), r->raw_keys.size() * 8);
+  });
+}
+
+void pinot_groupby_free(pinot_groupby_result *r) { delete r; }
+
+pinot_status pinot_gpu_group_by_layout(pinot_engine *engine, const pinot_segment_handle *segments,
+                                       int32_t num_segments, const pinot_query *query, pinot_partial_layout *layout) {
+  return guard([&] {
+    require(engine && layout, PINOT_ERR_BAD_ARG, "null argument");
+    check_query(query);
+    require(query->num_aggregations <= 8, PINOT_ERR_UNSUPPORTED, "at most 8 aggregations");
+    std::lock_guard<std::mutex> lk(engine->mu);
+    set_device(*engine);
+    exec_group_by_layout(*engine, resolve(*engine, segments, num_segments), *query, layout);
+  });
+}
+
+pinot_status pinot_gpu_group_by_partial(pinot_engine *engine, const pinot_segment_handle *segments,
+                                        int32_t num_segments, const pinot_query *query, int64_t *counts_dev,
+                                        void *const *accs_dev, pinot_exec_stats *stats) {
+  return guard([&] {
+    require(engine && counts_dev, PINOT_ERR_BAD_ARG, "null argument");
+    check_query(query);
+    std::lock_guard<std::mutex> lk(engine->mu);
+    set_device(*engine);
+    exec_group_by_partial(*engine, resolve(*engine, segments, num_segments), *query, counts_dev, accs_dev, stats);
+  });
+}
+
+pinot_status pinot_gpu_group_by_finalize(pinot_engine *engine, const pinot_segment_handle *segments,
+                                         int32_t num_segments, const pinot_query *query, const int64_t *counts_dev,
+                                         void *const *accs_dev, pinot_groupby_result **out) {
+  return guard([&] {
+    require(engine && counts_dev && out, PINOT_ERR_BAD_ARG, "null argument");
+    check_query(query);
+    std::lock_guard<std::mutex> lk(engine->mu);
+    set_device(*engine);
+    auto r = exec_group_by_finalize(*engine, resolve(*engine, segments, num_segments), *query, counts_dev, accs_dev);
+    auto *res = new pinot_groupby_result();
+    static_cast<GroupByResult &>(*res) = std::move(*r);
+    *out = res;
+  });
+}
+
+pinot_status pinot_gpu_synchronize(pinot_engine *engine) {
+  return guard([&] {
+    require(engine != nullptr, PINOT_ERR_BAD_ARG, "null engine");
+    set_device(*engine);
+    PINOT_HIP(hipStreamSynchronize(engine->stream));
+  });
+}
+
+pinot_status pinot_gpu_last_kernel_ms(pinot_engine *engine, int32_t kind, double *ms, int64_t *launches) {
+  return guard([&] {
+    require(engine && kind >= 0 && kind < 2, PINOT_ERR_BAD_ARG, "kind");
+    if (ms) *ms = engine->last_ms[kind];
+    if (launches) *launches = engine->last_launches[kind];
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,87 @@
+// Internal shared definitions of the MI355X Pinot segment executor.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "pinot_gpu.h"
+
+namespace pinot {
+
+// Exception type carried up to the C-ABI, where it becomes a pinot_status + last_error.
+struct Error : std::runtime_error {
+  pinot_status status;
+  Error(pinot_status s, const std::string &m) : std::runtime_error(m), status(s) {}
+};
+
+#define PINOT_HIP(expr)                                                                       \
+  do {                                                                                        \
+    hipError_t _e = (expr);                                                                   \
+    if (_e != hipSuccess) {                                                                   \
+      throw ::pinot::Error(_e == hipErrorOutOfMemory ? PINOT_ERR_OOM : PINOT_ERR_DEVICE,      \
+                           std::string(#expr) + ": " + hipGetErrorString(_e));                \
+    }                                                                                         \
+  } while (0)
+
+inline void require(bool ok, pinot_status s, const std::string &msg) {
+  if (!ok) throw Error(s, msg);
+}
+
+// Grow-only / owning device allocation.
+class DeviceBuffer {
+ public:
+  DeviceBuffer() = default;
+  explicit DeviceBuffer(size_t bytes) { alloc(bytes); }
+  ~DeviceBuffer() { reset(); }
+  DeviceBuffer(const DeviceBuffer &) = delete;
+  DeviceBuffer &operator=(const DeviceBuffer &) = delete;
+  DeviceBuffer(DeviceBuffer &&o) noexcept : p_(o.p_), n_(o.n_) { o.p_ = nullptr; o.n_ = 0; }
+  DeviceBuffer &operator=(DeviceBuffer &&o) noexcept {
+    if (this != &o) { reset(); p_ = o.p_; n_ = o.n_; o.p_ = nullptr; o.n_ = 0; }
+    return *this;
+  }
+  void alloc(size_t bytes) {
+    reset();
+    if (bytes == 0) return;
+    PINOT_HIP(hipMalloc(&p_, bytes));
+    n_ = bytes;
+  }
+  // Ensure capacity >= bytes (contents not preserved).
+  void reserve(size_t bytes) {
+    if (bytes > n_) alloc(bytes + bytes / 4);
+  }
+  void reset() {
+    if (p_) (void)hipFree(p_);
+    p_ = nullptr;
+    n_ = 0;
+  }
+  template <typename T = void> T *get() const { return static_cast<T *>(p_); }
+  size_t size() const { return n_; }
+
+ private:
+  void *p_ = nullptr;
+  size_t n_ = 0;
+};
+
+inline uint32_t load_be32(const uint8_t *p) {
+  return (uint32_t(p[0]) << 24) | (uint32_t(p[1]) << 16) | (uint32_t(p[2]) << 8) | uint32_t(p[3]);
+}
+inline uint64_t load_be64(const uint8_t *p) {
+  return (uint64_t(load_be32(p)) << 32) | load_be32(p + 4);
+}
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// PinotDataBitSet.getNumBitsPerValue (PinotDataBitSet.java:60-71)
+inline int num_bits_per_value(int64_t max_value) {
+  if (max_value <= 1) return 1;
+  int b = 0;
+  while (max_value > 0) { b++; max_value >>= 1; }
+  return b;
+}
+
+}  // namespace pinot

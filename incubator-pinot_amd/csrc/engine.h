@@ -1,0 +1,166 @@
+// Host-side engine: device-resident segments, query planning, execution.
+#pragma once
+#include <memory>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace pinot {
+
+// ------------------------------------------------------------------ segments
+struct ColumnData {
+  std::string name;
+  int data_type = PINOT_INT;
+  int32_t card = 0;
+  int32_t bits = 0;
+  bool is_sorted = false;
+  bool has_inverted = false;
+  int32_t string_width = 0;
+  int32_t num_docs = 0;
+
+  // host copies (dictionary-sized; used for predicate evaluation and key materialisation)
+  std::vector<uint8_t> dict_be;        // raw BE dictionary bytes
+  std::vector<int64_t> dict_int;       // INT / LONG values
+  std::vector<double> dict_dbl;        // FLOAT / DOUBLE values (float widened exactly)
+  std::vector<std::string> dict_str;   // STRING values (unpadded)
+  std::vector<int32_t> sorted_start, sorted_end;  // sorted columns
+  std::vector<int32_t> inv_dir;        // per dictId [dir[i], dir[i+1]) into containers
+  std::vector<uint64_t> inv_bytes;     // serialized roaring bytes per dictId (cost model)
+
+  // device
+  DeviceBuffer fwd;             // packed forward index (synthesised for sorted columns)
+  uint64_t fwd_bytes = 0;       // ceil(N*b/8)
+  DeviceBuffer dict_dev;        // int32 (INT) / int64 (LONG) / double (FLOAT, DOUBLE); none for STRING
+  DeviceBuffer inv_payload, inv_containers, inv_dir_dev;
+  DeviceBuffer hll_lut;         // u16 per dictId, built lazily
+
+  DevColumn dev() const { return DevColumn{fwd.get<uint8_t>(), bits, card}; }
+  int value_kind() const {  // 0 int32, 1 int64, 2 double
+    return data_type == PINOT_INT ? 0 : data_type == PINOT_LONG ? 1 : 2;
+  }
+  bool numeric() const { return data_type != PINOT_STRING; }
+  std::string string_value(int32_t id) const;  // Dictionary.getStringValue
+  double double_value(int32_t id) const;
+};
+
+struct SegmentData {
+  std::string name;
+  int32_t num_docs = 0;
+  std::vector<std::unique_ptr<ColumnData>> cols;
+  std::unordered_map<std::string, int> by_name;
+  uint64_t device_bytes = 0;
+
+  ColumnData *column(const std::string &n) const {
+    auto it = by_name.find(n);
+    if (it == by_name.end()) throw Error(PINOT_ERR_BAD_QUERY, "unknown column: " + n);
+    return cols[it->second].get();
+  }
+  int64_t nwords() const { return ceil_div(num_docs, 64); }
+};
+
+// ------------------------------------------------------------------ predicate evaluation
+// Dictionary-based predicate evaluator (PredicateEvaluatorProvider.java:37-80).
+struct Evaluator {
+  enum Kind { EQ, NEQ, IN, NOT_IN, RANGE } kind;
+  std::vector<uint8_t> matching;  // per dictId
+  int64_t num_matching = 0;
+  bool always_true = false, always_false = false;
+  bool exclusive() const { return kind == NEQ || kind == NOT_IN; }
+};
+
+Evaluator make_evaluator(const ColumnData &col, int op, const std::vector<std::string> &values);
+
+// Physical filter plan for one segment (FilterPlanNode.constructPhysicalOperator +
+// FilterOperatorUtils.getLeafFilterOperator/getAndFilterOperator/getOrFilterOperator).
+struct FilterNode {
+  enum Type { EMPTY, MATCH_ALL, SCAN, SORTED, BITMAP, AND, OR } type;
+  int col = -1;
+  std::shared_ptr<Evaluator> ev;
+  std::vector<FilterNode> children;
+};
+
+struct FilterTreeInput {  // decoded pinot_filter_node (postfix) as a tree
+  int op;
+  std::string column;
+  std::vector<std::string> values;
+  std::vector<FilterTreeInput> children;
+};
+
+FilterTreeInput decode_filter(int32_t n, const pinot_filter_node *nodes);
+FilterNode plan_filter(const SegmentData &seg, const FilterTreeInput *tree);
+
+// ------------------------------------------------------------------ engine
+struct Engine {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  int64_t next_handle = 1;
+  std::unordered_map<int64_t, std::unique_ptr<SegmentData>> segments;
+
+  // configuration
+  int num_groups_limit = 100000;
+  std::string force_filter;   // "", "scan", "index": planner override for tests
+  bool timing = false;
+
+  // scratch (grow-only)
+  DeviceBuffer bitsets;       // index-leaf slots + final bitset
+  DeviceBuffer luts;
+  DeviceBuffer small;         // counters, ranges, ids
+  DeviceBuffer partials;
+  DeviceBuffer reduced;
+  DeviceBuffer hll;
+  DeviceBuffer group_scratch;
+
+  // timing
+  hipEvent_t ev_start = nullptr, ev_stop = nullptr;
+  std::vector<hipEvent_t> kev;  // per-kernel event pairs (timing mode)
+  double last_ms[2] = {0, 0};
+  int64_t last_launches[2] = {0, 0};
+
+  ~Engine();
+  SegmentData &seg(int64_t h);
+};
+
+// execution entry points (executor.cpp)
+void exec_filter(Engine &e, SegmentData &s, const FilterTreeInput *tree, uint64_t *bitset_out, int64_t *count);
+void exec_aggregate(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q, pinot_agg_result *out,
+                    pinot_exec_stats *stats);
+
+struct GroupByResult {
+  std::vector<int64_t> raw_keys;
+  std::vector<std::string> keys;
+  int32_t num_columns = 0;
+  std::vector<int> functions;
+  std::vector<std::vector<int64_t>> counts;   // per fn
+  std::vector<std::vector<double>> values;    // per fn
+  std::vector<std::vector<uint8_t>> hll;      // per fn: groups*256
+};
+std::unique_ptr<GroupByResult> exec_group_by(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q,
+                                             pinot_exec_stats *stats);
+
+// multi-GPU partials
+void exec_group_by_layout(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q,
+                          pinot_partial_layout *layout);
+void exec_group_by_partial(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q,
+                           int64_t *counts_dev, void *const *accs_dev, pinot_exec_stats *stats);
+std::unique_ptr<GroupByResult> exec_group_by_finalize(Engine &e, const std::vector<SegmentData *> &segs,
+                                                      const pinot_query &q, const int64_t *counts_dev,
+                                                      void *const *accs_dev);
+
+// segments (segment.cpp)
+std::unique_ptr<SegmentData> register_segment(Engine &e, const pinot_segment_desc &d);
+std::unique_ptr<SegmentData> register_synthetic(Engine &e, const char *name, int32_t num_docs, int32_t ncols,
+                                                const char *const *names, const int32_t *cards, uint64_t seed);
+void ensure_hll_lut(Engine &e, ColumnData &c);
+
+// stream-lib HyperLogLog(log2m=8) helpers (hll.cpp)
+uint32_t murmur_hash_long(int64_t v);
+uint32_t murmur_hash_bytes(const uint8_t *data, int len);
+uint16_t hll_register_rank(uint32_t h);  // (register << 8) | rank
+int64_t hll_cardinality(const uint8_t *regs);
+
+}  // namespace pinot

@@ -1,0 +1,966 @@
+// Query execution on one GPU: per-segment filter programs, aggregation, group-by, combine.
+//
+// Restates, for dictionary-encoded single-value columns (PC = pinot-core/src/main/java/org/apache/pinot/core):
+//   AggregationOperator.getNextBlock / DefaultAggregationExecutor   PC/operator/query/AggregationOperator.java:56-82
+//   Count/Sum/Min/Max/Avg/DistinctCountHLL aggregation functions     PC/query/aggregation/function/*
+//   AggregationGroupByOperator / DefaultGroupByExecutor               PC/operator/query/AggregationGroupByOperator.java:64-94
+//   DictionaryBasedGroupKeyGenerator (raw keys, holder choice, limit) PC/query/aggregation/groupby/DictionaryBasedGroupKeyGenerator.java:79-437
+//   CombineOperator / CombineService.mergeTwoBlocks                   PC/operator/CombineOperator.java:75-196
+//   CombineGroupByOperator                                            PC/operator/CombineGroupByOperator.java:104-228
+//   ExecutionStatistics                                               PC/operator/ExecutionStatistics.java:24-90
+//
+// All segments of a query on this GPU are planned on the host first; every small per-query table
+// (sorted ranges, roaring id lists, IN/NOT_IN membership bitmaps) goes up in ONE host->device copy,
+// then the kernels of all segments run back to back on the engine's stream and the combined result
+// comes back in one device->host copy.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <numeric>
+#include <set>
+
+#include "engine.h"
+
+namespace pinot {
+
+namespace {
+
+struct Arena {
+  std::vector<uint8_t> bytes;
+  size_t add(const void *p, size_t n) {
+    size_t off = (bytes.size() + 15) & ~size_t(15);
+    bytes.resize(off + n);
+    if (n) memcpy(bytes.data() + off, p, n);
+    return off;
+  }
+};
+
+struct IndexLeaf {
+  int slot;
+  int kind;  // 0 sorted ranges (K2), 1 roaring (K3)
+  int col;
+  size_t off;  // arena offset: ranges (int32 pairs) or ids (int32)
+  int n;
+  int exclusive;
+};
+
+struct SegPlan {
+  SegmentData *seg = nullptr;
+  bool empty = false, match_all = false;
+  FilterProgram prog{};
+  size_t lut_off = 0;
+  std::vector<IndexLeaf> idx;
+  int64_t scan_leaves = 0;
+};
+
+std::string agg_column(const pinot_agg_spec &a) {
+  if (a.column == nullptr) return "*";
+  return a.column;
+}
+
+class Compiler {
+ public:
+  Compiler(Engine &e, SegPlan &sp, Arena &ar) : e_(e), sp_(sp), ar_(ar), seg_(*sp.seg) {}
+
+  void run(const FilterTreeInput *tree) {
+    FilterNode root = plan_filter(seg_, tree);
+    if (root.type == FilterNode::EMPTY) { sp_.empty = true; return; }
+    if (root.type == FilterNode::MATCH_ALL) { sp_.match_all = true; return; }
+    emit(root);
+    sp_.prog.n_cols = (int)colslot_.size();
+    sp_.lut_off = ar_.add(luts_.data(), luts_.size() * 4 + 16);
+  }
+
+ private:
+  int col_slot(int ci) {
+    auto it = colslot_.find(ci);
+    if (it != colslot_.end()) return it->second;
+    int s = (int)colslot_.size();
+    require(s < kMaxProgramColumns, PINOT_ERR_UNSUPPORTED, "filter references too many columns");
+    colslot_[ci] = s;
+    sp_.prog.cols[s] = seg_.cols[ci]->dev();
+    return s;
+  }
+  void push(FilterInstr in) {
+    require(sp_.prog.n_instr < kMaxProgramInstr, PINOT_ERR_UNSUPPORTED, "filter tree too large");
+    sp_.prog.ins[sp_.prog.n_instr++] = in;
+  }
+  void emit(const FilterNode &n) {
+    switch (n.type) {
+      case FilterNode::AND:
+      case FilterNode::OR: {
+        const int op = n.type == FilterNode::AND ? OP_AND : OP_OR;
+        emit(n.children[0]);
+        depth_++;
+        require(depth_ < kMaxStack, PINOT_ERR_UNSUPPORTED, "filter tree too deep");
+        for (size_t i = 1; i < n.children.size(); i++) {
+          emit(n.children[i]);
+          push(FilterInstr{op, 0, 2, 0, 0});
+        }
+        depth_--;
+        return;
+      }
+      default:
+        leaf(n);
+    }
+  }
+  void leaf(const FilterNode &n) {
+    const ColumnData &c = *seg_.cols[n.col];
+    const Evaluator &ev = *n.ev;
+    const bool force_scan = e_.force_filter == "scan";
+    const bool force_index = e_.force_filter == "index";
+    if ((n.type == FilterNode::SORTED || c.is_sorted) && !force_scan) {
+      // SortedInvertedIndexBasedFilterOperator: runs of matching dictIds -> merged [start, end] doc ranges
+      std::vector<int32_t> ranges;
+      for (int32_t i = 0; i < c.card;) {
+        if (!ev.matching[i]) { i++; continue; }
+        int32_t j = i;
+        while (j + 1 < c.card && ev.matching[j + 1]) j++;
+        const int32_t s = c.sorted_start[i], en = c.sorted_end[j];
+        if (en >= s) {
+          if (!ranges.empty() && ranges.back() + 1 == s) ranges.back() = en;
+          else { ranges.push_back(s); ranges.push_back(en); }
+        }
+        i = j + 1;
+      }
+      index_leaf(0, n.col, ranges, 0);
+      return;
+    }
+    if (n.type == FilterNode::BITMAP && !force_scan) {
+      // BitmapBasedFilterOperator: OR the bitmaps of the matching dictIds, or of the non-matching ones and flip
+      const bool excl = ev.exclusive();
+      std::vector<int32_t> ids;
+      uint64_t payload = 0;
+      for (int32_t i = 0; i < c.card; i++) {
+        if ((ev.matching[i] != 0) != excl) {
+          ids.push_back(i);
+          payload += c.inv_bytes[i];
+        }
+      }
+      // cost model: roaring payload + write/read of one bitset vs. streaming the packed column
+      const uint64_t idx_cost = payload + (uint64_t)seg_.num_docs / 4;
+      if (force_index || idx_cost < c.fwd_bytes) {
+        index_leaf(1, n.col, ids, excl ? 1 : 0);
+        return;
+      }
+    }
+    scan_leaf(n.col, ev);
+  }
+  void index_leaf(int kind, int col, const std::vector<int32_t> &data, int excl) {
+    IndexLeaf il;
+    il.slot = (int)sp_.idx.size();
+    il.kind = kind;
+    il.col = col;
+    il.n = kind == 0 ? (int)data.size() / 2 : (int)data.size();
+    il.off = ar_.add(data.data(), data.size() * 4 + 8);
+    il.exclusive = excl;
+    sp_.idx.push_back(il);
+    push(FilterInstr{OP_LEAF_BITSET, 0, il.slot, 0, 0});
+  }
+  void scan_leaf(int col, const Evaluator &ev) {
+    const ColumnData &c = *seg_.cols[col];
+    sp_.scan_leaves++;
+    const int slot = col_slot(col);
+    auto contiguous = [&](uint8_t want, int32_t &lo, int32_t &hi) {
+      int32_t first = -1, last = -1;
+      int64_t cnt = 0;
+      for (int32_t i = 0; i < c.card; i++)
+        if (ev.matching[i] == want) {
+          if (first < 0) first = i;
+          last = i;
+          cnt++;
+        }
+      if (cnt == 0 || last - first + 1 != cnt) return false;
+      lo = first;
+      hi = last + 1;
+      return true;
+    };
+    int32_t lo, hi;
+    if (contiguous(1, lo, hi)) {
+      push(FilterInstr{OP_LEAF_RANGE, slot, lo, hi, 0});
+    } else if (contiguous(0, lo, hi)) {
+      push(FilterInstr{OP_LEAF_RANGE, slot, lo, hi, 1});
+    } else {
+      const size_t words = (size_t)(c.card + 31) / 32;
+      const int32_t base = (int32_t)luts_.size();
+      luts_.resize(luts_.size() + words + 2, 0u);
+      for (int32_t i = 0; i < c.card; i++)
+        if (ev.matching[i]) luts_[base + (i >> 5)] |= 1u << (i & 31);
+      push(FilterInstr{OP_LEAF_LUT, slot, base, 0, 0});
+    }
+  }
+
+  Engine &e_;
+  SegPlan &sp_;
+  Arena &ar_;
+  const SegmentData &seg_;
+  std::map<int, int> colslot_;
+  std::vector<uint32_t> luts_;
+  int depth_ = 0;
+};
+
+// Device-side arena + bitset scratch for one query.
+struct QueryScratch {
+  uint8_t *arena = nullptr;
+  uint64_t *bitsets = nullptr;  // (max_slots + 1) * nwords_max
+  int64_t stride = 0;
+};
+
+QueryScratch prepare(Engine &e, std::vector<SegPlan> &plans, Arena &ar) {
+  QueryScratch qs;
+  size_t max_slots = 0;
+  int64_t max_words = 1;
+  for (auto &p : plans) {
+    max_slots = std::max(max_slots, p.idx.size());
+    max_words = std::max<int64_t>(max_words, p.seg->nwords());
+  }
+  e.small.reserve(std::max<size_t>(ar.bytes.size(), 256));
+  if (!ar.bytes.empty())
+    PINOT_HIP(hipMemcpyAsync(e.small.get(), ar.bytes.data(), ar.bytes.size(), hipMemcpyHostToDevice, e.stream));
+  qs.arena = e.small.get<uint8_t>();
+  qs.stride = max_words;
+  e.bitsets.reserve((max_slots + 1) * max_words * 8);
+  qs.bitsets = e.bitsets.get<uint64_t>();
+  for (auto &p : plans) {
+    p.prog.luts = reinterpret_cast<const uint32_t *>(qs.arena + p.lut_off);
+    p.prog.bitsets = qs.bitsets;
+    p.prog.bitset_stride = qs.stride;
+  }
+  return qs;
+}
+
+struct Timer {
+  Engine &e;
+  std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> marks;
+  size_t used = 0;
+  explicit Timer(Engine &en) : e(en) {}
+  std::pair<hipEvent_t, hipEvent_t> pair() {
+    if (used * 2 + 2 > e.kev.size()) {
+      hipEvent_t a, b;
+      PINOT_HIP(hipEventCreate(&a));
+      PINOT_HIP(hipEventCreate(&b));
+      e.kev.push_back(a);
+      e.kev.push_back(b);
+    }
+    auto p = std::make_pair(e.kev[used * 2], e.kev[used * 2 + 1]);
+    used++;
+    return p;
+  }
+  template <typename F>
+  void timed(int kind, F f) {
+    if (!e.timing) { f(); return; }
+    auto p = pair();
+    PINOT_HIP(hipEventRecord(p.first, e.stream));
+    f();
+    PINOT_HIP(hipEventRecord(p.second, e.stream));
+    marks.push_back({kind, p});
+  }
+  void collect() {
+    e.last_ms[0] = e.last_ms[1] = 0;
+    e.last_launches[0] = e.last_launches[1] = 0;
+    for (auto &m : marks) {
+      float ms = 0;
+      PINOT_HIP(hipEventElapsedTime(&ms, m.second.first, m.second.second));
+      e.last_ms[m.first] += ms;
+      e.last_launches[m.first]++;
+    }
+  }
+};
+
+// Runs the index leaves and the filter scan of one segment. Returns the bitset to aggregate over
+// (nullptr = all docs) and accumulates the matching-doc count into *count_dev.
+const uint64_t *run_filter(Engine &e, SegPlan &p, const QueryScratch &qs, unsigned long long *count_dev,
+                           Timer &t) {
+  SegmentData &s = *p.seg;
+  const int64_t nwords = s.nwords();
+  for (auto &il : p.idx) {
+    uint64_t *out = qs.bitsets + (int64_t)il.slot * qs.stride;
+    const ColumnData &c = *s.cols[il.col];
+    if (il.kind == 0) {
+      launch_ranges_to_bitset(reinterpret_cast<const int32_t *>(qs.arena + il.off), il.n, nwords, s.num_docs, out,
+                              e.stream);
+    } else {
+      launch_roaring_expand(c.inv_payload.get<uint8_t>(), c.inv_containers.get<RoaringContainer>(),
+                            c.inv_dir_dev.get<int32_t>(), reinterpret_cast<const int32_t *>(qs.arena + il.off), il.n,
+                            il.exclusive, nwords, s.num_docs, out, e.stream);
+    }
+    PINOT_HIP(hipGetLastError());
+  }
+  uint64_t *final_bits = qs.bitsets + (int64_t)p.idx.size() * qs.stride;
+  t.timed(0, [&] { launch_filter_scan(p.prog, nwords, s.num_docs, final_bits, count_dev, e.stream); });
+  PINOT_HIP(hipGetLastError());
+  return final_bits;
+}
+
+std::vector<SegPlan> plan_all(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q, Arena &ar,
+                              std::unique_ptr<FilterTreeInput> &tree) {
+  if (q.num_filter_nodes > 0) tree = std::make_unique<FilterTreeInput>(decode_filter(q.num_filter_nodes, q.filter));
+  std::vector<SegPlan> plans(segs.size());
+  for (size_t i = 0; i < segs.size(); i++) {
+    plans[i].seg = segs[i];
+    Compiler(e, plans[i], ar).run(tree.get());
+  }
+  return plans;
+}
+
+int64_t projected_columns(const pinot_query &q) {
+  // TransformPlanNode: distinct columns of the aggregation and group-by expressions (COUNT(*) projects none)
+  std::set<std::string> cols;
+  for (int i = 0; i < q.num_aggregations; i++) {
+    std::string c = agg_column(q.aggregations[i]);
+    if (c != "*") cols.insert(c);
+  }
+  for (int i = 0; i < q.num_group_by; i++) cols.insert(q.group_by[i]);
+  return (int64_t)cols.size();
+}
+
+void fill_stats(const pinot_query &q, const std::vector<SegPlan> &plans, const std::vector<int64_t> &counts,
+                double ms, pinot_exec_stats *st) {
+  if (!st) return;
+  memset(st, 0, sizeof(*st));
+  for (size_t i = 0; i < plans.size(); i++) {
+    st->num_docs_scanned += counts[i];
+    st->num_total_raw_docs += plans[i].seg->num_docs;
+    st->num_entries_scanned_in_filter += plans[i].scan_leaves * plans[i].seg->num_docs;
+  }
+  st->num_entries_scanned_post_filter = st->num_docs_scanned * projected_columns(q);
+  st->num_segments_processed = (int64_t)plans.size();
+  st->device_ms = ms;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ filter API
+void exec_filter(Engine &e, SegmentData &s, const FilterTreeInput *tree, uint64_t *bitset_out, int64_t *count) {
+  Arena ar;
+  std::vector<SegPlan> plans(1);
+  plans[0].seg = &s;
+  Compiler(e, plans[0], ar).run(tree);
+  QueryScratch qs = prepare(e, plans, ar);
+  const int64_t nwords = s.nwords();
+  Timer t(e);
+  if (plans[0].empty || plans[0].match_all) {
+    const int64_t c = plans[0].empty ? 0 : s.num_docs;
+    if (bitset_out) {
+      for (int64_t w = 0; w < nwords; w++) {
+        uint64_t v = plans[0].empty ? 0 : ~0ull;
+        if (w == nwords - 1 && (s.num_docs & 63)) v &= (1ull << (s.num_docs & 63)) - 1;
+        bitset_out[w] = v;
+      }
+    }
+    if (count) *count = c;
+    PINOT_HIP(hipStreamSynchronize(e.stream));
+    return;
+  }
+  e.reduced.reserve(64);
+  auto *cnt = e.reduced.get<unsigned long long>();
+  PINOT_HIP(hipMemsetAsync(cnt, 0, 8, e.stream));
+  const uint64_t *bits = run_filter(e, plans[0], qs, cnt, t);
+  unsigned long long hc = 0;
+  PINOT_HIP(hipMemcpyAsync(&hc, cnt, 8, hipMemcpyDeviceToHost, e.stream));
+  if (bitset_out && nwords)
+    PINOT_HIP(hipMemcpyAsync(bitset_out, bits, nwords * 8, hipMemcpyDeviceToHost, e.stream));
+  PINOT_HIP(hipStreamSynchronize(e.stream));
+  t.collect();
+  if (count) *count = (int64_t)hc;
+}
+
+// ------------------------------------------------------------------ aggregation-only
+void exec_aggregate(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q, pinot_agg_result *out,
+                    pinot_exec_stats *stats) {
+  const int na = q.num_aggregations;
+  require(na >= 1 && na <= kMaxAggs, PINOT_ERR_UNSUPPORTED, "1..8 aggregation functions per query");
+  Arena ar;
+  std::unique_ptr<FilterTreeInput> tree;
+  std::vector<SegPlan> plans = plan_all(e, segs, q, ar, tree);
+
+  // Aggregation programs per segment
+  std::vector<AggProgram> aprog(plans.size());
+  bool need_kernel = false;
+  int n_hll = 0;
+  for (int a = 0; a < na; a++) {
+    const int f = q.aggregations[a].function;
+    require(f >= PINOT_AGG_COUNT && f <= PINOT_AGG_DISTINCTCOUNTHLL, PINOT_ERR_UNSUPPORTED, "aggregation function");
+    if (f != PINOT_AGG_COUNT) need_kernel = true;
+    if (f == PINOT_AGG_DISTINCTCOUNTHLL) n_hll++;
+  }
+  require(n_hll <= 4, PINOT_ERR_UNSUPPORTED, "at most 4 DISTINCTCOUNTHLL per query");
+  for (size_t si = 0; si < plans.size(); si++) {
+    SegmentData &s = *plans[si].seg;
+    AggProgram &ap = aprog[si];
+    ap = AggProgram{};
+    ap.n_aggs = na;
+    std::map<int, int> slots;
+    for (int a = 0; a < na; a++) {
+      const int f = q.aggregations[a].function;
+      AggSpecDev &sd = ap.aggs[a];
+      sd.kind = AGG_NOP;
+      if (f == PINOT_AGG_COUNT) continue;
+      ColumnData &c = *s.column(agg_column(q.aggregations[a]));
+      int ci = s.by_name[c.name];
+      if (!slots.count(ci)) {
+        int k = (int)slots.size();
+        slots[ci] = k;
+        ap.cols[k] = c.dev();
+      }
+      sd.col = slots[ci];
+      sd.dict = c.dict_dev.get();
+      if (f == PINOT_AGG_DISTINCTCOUNTHLL) {
+        ensure_hll_lut(e, c);
+        sd.kind = AGG_HLL;
+        sd.hll_lut = c.hll_lut.get<uint16_t>();
+        continue;
+      }
+      require(c.numeric(), PINOT_ERR_UNSUPPORTED, "numeric aggregation over STRING column " + c.name);
+      if (f == PINOT_AGG_MIN || f == PINOT_AGG_MAX) {
+        sd.kind = AGG_MINMAX;  // sorted dictionary: min/max value = value of min/max dictId
+      } else {
+        sd.kind = c.data_type == PINOT_INT ? AGG_SUM_I32 : c.data_type == PINOT_LONG ? AGG_SUM_I64 : AGG_SUM_F64;
+      }
+    }
+    ap.n_cols = (int)slots.size();
+  }
+
+  QueryScratch qs = prepare(e, plans, ar);
+  const size_t S = plans.size();
+  int64_t max_words = 1;
+  for (auto &p : plans) max_words = std::max<int64_t>(max_words, p.seg->nwords());
+  const int grid = aggregate_grid(max_words);
+  // reduced layout: [S counters (u64)] [S * na AggPartial] [na * 256 u32 HLL]
+  const size_t off_red = ((S * 8 + 15) / 16) * 16;
+  const size_t off_hll = off_red + S * na * sizeof(AggPartial);
+  const size_t red_bytes = off_hll + (size_t)na * 256 * 4;
+  e.reduced.reserve(red_bytes);
+  e.partials.reserve((size_t)grid * na * sizeof(AggPartial));
+  uint8_t *red = e.reduced.get<uint8_t>();
+  auto *cnt_dev = reinterpret_cast<unsigned long long *>(red);
+  auto *red_dev = reinterpret_cast<AggPartial *>(red + off_red);
+  auto *hll_dev = reinterpret_cast<uint32_t *>(red + off_hll);
+  PINOT_HIP(hipEventRecord(e.ev_start, e.stream));
+  PINOT_HIP(hipMemsetAsync(red, 0, red_bytes, e.stream));
+  Timer t(e);
+  std::vector<int64_t> counts(S, 0);
+  for (size_t si = 0; si < S; si++) {
+    SegPlan &p = plans[si];
+    SegmentData &s = *p.seg;
+    if (p.empty) continue;
+    const uint64_t *bits = nullptr;
+    if (!p.match_all) bits = run_filter(e, p, qs, cnt_dev + si, t);
+    if (need_kernel) {
+      t.timed(1, [&] {
+        launch_aggregate(aprog[si], bits, s.nwords(), s.num_docs, e.partials.get<AggPartial>(), hll_dev, e.stream);
+      });
+      PINOT_HIP(hipGetLastError());
+      launch_reduce_partials(e.partials.get<AggPartial>(), grid, na, red_dev + si * na, e.stream);
+      PINOT_HIP(hipGetLastError());
+    }
+  }
+  PINOT_HIP(hipEventRecord(e.ev_stop, e.stream));
+  std::vector<uint8_t> host(red_bytes);
+  PINOT_HIP(hipMemcpyAsync(host.data(), red, red_bytes, hipMemcpyDeviceToHost, e.stream));
+  PINOT_HIP(hipStreamSynchronize(e.stream));
+  float ms = 0;
+  PINOT_HIP(hipEventElapsedTime(&ms, e.ev_start, e.ev_stop));
+  t.collect();
+
+  const auto *hcnt = reinterpret_cast<const unsigned long long *>(host.data());
+  const auto *hred = reinterpret_cast<const AggPartial *>(host.data() + off_red);
+  const auto *hhll = reinterpret_cast<const uint32_t *>(host.data() + off_hll);
+  for (size_t si = 0; si < S; si++) {
+    if (plans[si].empty) counts[si] = 0;
+    else if (plans[si].match_all) counts[si] = plans[si].seg->num_docs;
+    else counts[si] = (int64_t)hcnt[si];
+  }
+  int64_t total = 0;
+  for (auto c : counts) total += c;
+
+  // CombineService.mergeTwoBlocks over segments, in segment order
+  for (int a = 0; a < na; a++) {
+    pinot_agg_result &r = out[a];
+    memset(&r, 0, sizeof(r));
+    const int f = q.aggregations[a].function;
+    switch (f) {
+      case PINOT_AGG_COUNT:
+        r.count = total;
+        break;
+      case PINOT_AGG_SUM:
+      case PINOT_AGG_AVG: {
+        const ColumnData &c0 = *plans[0].seg->column(agg_column(q.aggregations[a]));
+        if (c0.data_type == PINOT_INT) {
+          int64_t exact = 0;
+          for (size_t si = 0; si < S; si++) exact += plans[si].empty ? 0 : hred[si * na + a].sum_i64;
+          r.exact_sum = exact;
+          r.has_exact_sum = 1;
+          r.value = (double)exact;
+        } else {
+          double v = 0.0;
+          for (size_t si = 0; si < S; si++) v += plans[si].empty ? 0.0 : hred[si * na + a].sum_f64;
+          r.value = v;
+        }
+        r.count = total;
+        break;
+      }
+      case PINOT_AGG_MIN:
+      case PINOT_AGG_MAX: {
+        const bool is_min = f == PINOT_AGG_MIN;
+        double v = is_min ? INFINITY : -INFINITY;  // Min/MaxAggregationFunction.DEFAULT_VALUE
+        for (size_t si = 0; si < S; si++) {
+          if (plans[si].empty || counts[si] == 0) continue;
+          const ColumnData &c = *plans[si].seg->column(agg_column(q.aggregations[a]));
+          const AggPartial &pp = hred[si * na + a];
+          const int32_t id = is_min ? pp.min_id : pp.max_id;
+          if (id < 0 || id >= c.card) continue;
+          const double x = c.double_value(id);
+          v = is_min ? std::min(v, x) : std::max(v, x);
+        }
+        r.value = v;
+        r.count = total;
+        break;
+      }
+      case PINOT_AGG_DISTINCTCOUNTHLL: {
+        for (int j = 0; j < 256; j++) r.hll_registers[j] = (uint8_t)hhll[a * 256 + j];
+        r.hll_cardinality = hll_cardinality(r.hll_registers);
+        r.count = total;
+        break;
+      }
+    }
+  }
+  fill_stats(q, plans, counts, ms, stats);
+}
+
+// ------------------------------------------------------------------ group-by
+namespace {
+
+struct KeySpace {
+  std::vector<int64_t> gcard;                          // global cardinality per group column
+  std::vector<std::vector<std::vector<int32_t>>> remap;  // [segment][gcol] dictId -> global id (empty = identity)
+  std::vector<std::vector<std::string>> gvalues;       // [gcol] global id -> string value
+  int64_t G = 1;
+};
+
+bool same_dictionary(const ColumnData &a, const ColumnData &b) {
+  if (a.data_type != b.data_type || a.card != b.card) return false;
+  if (a.data_type == PINOT_INT || a.data_type == PINOT_LONG) return a.dict_int == b.dict_int;
+  if (a.data_type == PINOT_STRING) return a.dict_str == b.dict_str;
+  return a.dict_dbl == b.dict_dbl;
+}
+
+// Global raw-key space over all segments (the reference merges per-segment results by string key,
+// CombineGroupByOperator.java:142-161; a dense device merge needs one key space instead).
+KeySpace build_key_space(const std::vector<SegmentData *> &segs, const pinot_query &q) {
+  KeySpace ks;
+  const int ng = q.num_group_by;
+  ks.remap.assign(segs.size(), std::vector<std::vector<int32_t>>(ng));
+  ks.gvalues.resize(ng);
+  for (int j = 0; j < ng; j++) {
+    const std::string name = q.group_by[j];
+    const ColumnData &c0 = *segs[0]->column(name);
+    bool same = true;
+    for (size_t si = 1; si < segs.size(); si++) same = same && same_dictionary(c0, *segs[si]->column(name));
+    if (same) {
+      ks.gcard.push_back(c0.card);
+      ks.gvalues[j].resize(c0.card);
+      for (int32_t i = 0; i < c0.card; i++) ks.gvalues[j][i] = c0.string_value(i);
+    } else {
+      // union dictionary in value order
+      std::vector<std::pair<double, std::string>> num;
+      std::set<std::string> strs;
+      const bool is_str = c0.data_type == PINOT_STRING;
+      std::map<std::pair<int64_t, double>, int> nmap;
+      for (auto *s : segs) {
+        const ColumnData &c = *s->column(name);
+        require(c.data_type == c0.data_type, PINOT_ERR_BAD_QUERY, "group-by column type differs across segments");
+        for (int32_t i = 0; i < c.card; i++) {
+          if (is_str) strs.insert(c.dict_str[i]);
+          else nmap[{c.data_type <= PINOT_LONG ? c.dict_int[i] : 0, c.data_type <= PINOT_LONG ? 0.0 : c.dict_dbl[i]}] = 0;
+        }
+      }
+      if (is_str) {
+        std::map<std::string, int> idx;
+        int k = 0;
+        for (auto &v : strs) { idx[v] = k++; ks.gvalues[j].push_back(v); }
+        for (size_t si = 0; si < segs.size(); si++) {
+          const ColumnData &c = *segs[si]->column(name);
+          auto &m = ks.remap[si][j];
+          m.resize(c.card);
+          for (int32_t i = 0; i < c.card; i++) m[i] = idx[c.dict_str[i]];
+        }
+      } else {
+        int k = 0;
+        for (auto &kv : nmap) kv.second = k++;
+        ks.gvalues[j].resize(nmap.size());
+        for (size_t si = 0; si < segs.size(); si++) {
+          const ColumnData &c = *segs[si]->column(name);
+          auto &m = ks.remap[si][j];
+          m.resize(c.card);
+          for (int32_t i = 0; i < c.card; i++) {
+            int g = nmap[{c.data_type <= PINOT_LONG ? c.dict_int[i] : 0, c.data_type <= PINOT_LONG ? 0.0 : c.dict_dbl[i]}];
+            m[i] = g;
+            ks.gvalues[j][g] = c.string_value(i);
+          }
+        }
+      }
+      ks.gcard.push_back((int64_t)ks.gvalues[j].size());
+    }
+  }
+  for (auto g : ks.gcard) {
+    require(ks.G <= (int64_t(1) << 40) / std::max<int64_t>(g, 1), PINOT_ERR_UNSUPPORTED,
+            "group key space too large for the dense device group-by (LONG_MAP/ARRAY_MAP shapes)");
+    ks.G *= g;
+  }
+  return ks;
+}
+
+struct GroupAccs {
+  std::vector<int> acc_kind;    // per agg
+  std::vector<size_t> acc_bytes_per_key;
+};
+
+GroupAccs group_acc_kinds(const SegmentData &s, const pinot_query &q) {
+  GroupAccs g;
+  for (int a = 0; a < q.num_aggregations; a++) {
+    const int f = q.aggregations[a].function;
+    int kind = 5;
+    size_t bytes = 0;
+    if (f != PINOT_AGG_COUNT) {
+      const ColumnData &c = *s.column(agg_column(q.aggregations[a]));
+      if (f == PINOT_AGG_DISTINCTCOUNTHLL) {
+        kind = 4;
+        bytes = 1024;
+      } else {
+        require(c.numeric(), PINOT_ERR_UNSUPPORTED, "numeric aggregation over STRING column " + c.name);
+        if (f == PINOT_AGG_MIN) kind = 2;
+        else if (f == PINOT_AGG_MAX) kind = 3;
+        else kind = c.data_type == PINOT_INT ? 0 : 1;
+        bytes = 8;
+      }
+    }
+    g.acc_kind.push_back(kind);
+    g.acc_bytes_per_key.push_back(bytes);
+  }
+  return g;
+}
+
+GroupByProgram make_group_program(Engine &e, SegmentData &s, const pinot_query &q, const GroupAccs &ga,
+                                  const KeySpace &ks, size_t si, const std::vector<DeviceBuffer> &remaps,
+                                  unsigned long long *counts, void *const *accs) {
+  GroupByProgram gp{};
+  gp.n_gcols = q.num_group_by;
+  gp.n_aggs = q.num_aggregations;
+  std::map<int, int> slots;
+  auto slot = [&](const ColumnData &c) {
+    int ci = s.by_name[c.name];
+    auto it = slots.find(ci);
+    if (it != slots.end()) return it->second;
+    int k = (int)slots.size();
+    require(k < kMaxProgramColumns, PINOT_ERR_UNSUPPORTED, "too many columns");
+    slots[ci] = k;
+    gp.cols[k] = c.dev();
+    return k;
+  };
+  long long stride = 1;
+  for (int j = 0; j < q.num_group_by; j++) {
+    const ColumnData &c = *s.column(q.group_by[j]);
+    gp.gcol[j] = slot(c);
+    gp.remap[j] = ks.remap[si][j].empty() ? nullptr : remaps[si * q.num_group_by + j].get<int32_t>();
+    gp.stride[j] = stride;
+    stride *= ks.gcard[j];
+  }
+  gp.counts = counts;
+  for (int a = 0; a < q.num_aggregations; a++) {
+    gp.acc_kind[a] = ga.acc_kind[a];
+    gp.acc[a] = accs[a];
+    AggSpecDev &sd = gp.aggs[a];
+    sd.kind = AGG_NOP;
+    if (ga.acc_kind[a] == 5) continue;
+    ColumnData &c = *s.column(agg_column(q.aggregations[a]));
+    sd.col = slot(c);
+    sd.dict = c.dict_dev.get();
+    gp.value_kind[a] = c.value_kind();
+    if (ga.acc_kind[a] == 4) {
+      ensure_hll_lut(e, c);
+      sd.hll_lut = c.hll_lut.get<uint16_t>();
+    }
+  }
+  gp.n_cols = (int)slots.size();
+  return gp;
+}
+
+double decode_ordered(uint64_t o) {
+  uint64_t u = (o & 0x8000000000000000ull) ? (o & ~0x8000000000000000ull) : ~o;
+  double d;
+  memcpy(&d, &u, 8);
+  return d;
+}
+
+std::unique_ptr<GroupByResult> finalize_groups(Engine &e, const pinot_query &q, const GroupAccs &ga,
+                                               const KeySpace &ks, GroupByProgram gp) {
+  const int na = q.num_aggregations;
+  // compact non-empty keys and gather their accumulators
+  DeviceBuffer keys_dev(std::max<int64_t>(ks.G, 1) * 8 + 16);
+  auto *n_dev = reinterpret_cast<unsigned long long *>(keys_dev.get<uint8_t>() + ks.G * 8);
+  PINOT_HIP(hipMemsetAsync(n_dev, 0, 8, e.stream));
+  launch_compact_keys(ks.G, gp.counts, keys_dev.get<long long>(), n_dev, e.stream);
+  PINOT_HIP(hipGetLastError());
+  unsigned long long n = 0;
+  PINOT_HIP(hipMemcpyAsync(&n, n_dev, 8, hipMemcpyDeviceToHost, e.stream));
+  PINOT_HIP(hipStreamSynchronize(e.stream));
+  int n_hll = 0;
+  for (int a = 0; a < na; a++) n_hll += ga.acc_kind[a] == 4;
+  auto res = std::make_unique<GroupByResult>();
+  res->num_columns = q.num_group_by;
+  res->functions.resize(na);
+  res->counts.assign(na, {});
+  res->values.assign(na, {});
+  res->hll.assign(na, {});
+  for (int a = 0; a < na; a++) res->functions[a] = q.aggregations[a].function;
+  if (n == 0) return res;
+  DeviceBuffer out(n * 8 * (1 + na) + (size_t)n_hll * n * 256 + 16);
+  auto *o_cnt = out.get<unsigned long long>();
+  auto *o_acc = o_cnt + n;
+  auto *o_hll = reinterpret_cast<uint8_t *>(o_acc + n * na);
+  launch_gather_groups(gp, keys_dev.get<long long>(), (int64_t)n, o_cnt, o_acc, o_hll, e.stream);
+  PINOT_HIP(hipGetLastError());
+  std::vector<long long> hkeys(n);
+  std::vector<unsigned long long> hcnt(n), hacc(n * na);
+  std::vector<uint8_t> hhll((size_t)n_hll * n * 256);
+  PINOT_HIP(hipMemcpyAsync(hkeys.data(), keys_dev.get(), n * 8, hipMemcpyDeviceToHost, e.stream));
+  PINOT_HIP(hipMemcpyAsync(hcnt.data(), o_cnt, n * 8, hipMemcpyDeviceToHost, e.stream));
+  PINOT_HIP(hipMemcpyAsync(hacc.data(), o_acc, n * na * 8, hipMemcpyDeviceToHost, e.stream));
+  if (n_hll) PINOT_HIP(hipMemcpyAsync(hhll.data(), o_hll, hhll.size(), hipMemcpyDeviceToHost, e.stream));
+  PINOT_HIP(hipStreamSynchronize(e.stream));
+  // order groups by raw key (the compaction order is arbitrary)
+  std::vector<size_t> order(n);
+  std::iota(order.begin(), order.end(), 0);
+  std::sort(order.begin(), order.end(), [&](size_t x, size_t y) { return hkeys[x] < hkeys[y]; });
+  res->raw_keys.resize(n);
+  res->keys.resize(n);
+  for (size_t i = 0; i < n; i++) {
+    int64_t k = hkeys[order[i]];
+    res->raw_keys[i] = k;
+    std::string s;
+    for (int j = 0; j < q.num_group_by; j++) {  // getGroupKey: column 0 first, '\t'-joined
+      if (j) s += '\t';
+      s += ks.gvalues[j][k % ks.gcard[j]];
+      k /= ks.gcard[j];
+    }
+    res->keys[i] = std::move(s);
+  }
+  int h = 0;
+  for (int a = 0; a < na; a++) {
+    auto &cv = res->counts[a];
+    auto &vv = res->values[a];
+    cv.resize(n);
+    vv.resize(n);
+    const int ak = ga.acc_kind[a];
+    if (ak == 4) res->hll[a].resize(n * 256);
+    for (size_t i = 0; i < n; i++) {
+      const size_t src = order[i];
+      cv[i] = (int64_t)hcnt[src];
+      const uint64_t raw = hacc[(size_t)a * n + src];
+      switch (ak) {
+        case 0: vv[i] = (double)(int64_t)raw; break;
+        case 1: { double d; memcpy(&d, &raw, 8); vv[i] = d; break; }
+        case 2:
+        case 3: vv[i] = decode_ordered(raw); break;
+        case 4: {
+          memcpy(res->hll[a].data() + i * 256, hhll.data() + ((size_t)h * n + src) * 256, 256);
+          vv[i] = (double)hll_cardinality(res->hll[a].data() + i * 256);
+          break;
+        }
+        default: vv[i] = (double)hcnt[src]; break;
+      }
+    }
+    if (ak == 4) h++;
+  }
+  return res;
+}
+
+// Accumulates every segment's group-by into the given device arrays (already initialised).
+void accumulate_groups(Engine &e, std::vector<SegPlan> &plans, const QueryScratch &qs, const pinot_query &q,
+                       const GroupAccs &ga, const KeySpace &ks, unsigned long long *counts, void *const *accs,
+                       unsigned long long *cnt_dev, Timer &t, std::vector<int64_t> &seg_counts, bool apply_limit) {
+  const size_t S = plans.size();
+  std::vector<DeviceBuffer> remaps(S * q.num_group_by);
+  for (size_t si = 0; si < S; si++)
+    for (int j = 0; j < q.num_group_by; j++) {
+      const auto &m = ks.remap[si][j];
+      if (m.empty()) continue;
+      remaps[si * q.num_group_by + j].alloc(m.size() * 4 + 16);
+      PINOT_HIP(hipMemcpyAsync(remaps[si * q.num_group_by + j].get(), m.data(), m.size() * 4, hipMemcpyHostToDevice,
+                               e.stream));
+    }
+  const int64_t limit = q.num_groups_limit > 0 ? q.num_groups_limit : e.num_groups_limit;
+  const int64_t array_threshold = q.max_init_group_holder_capacity > 0 ? q.max_init_group_holder_capacity : 10000;
+  DeviceBuffer first_doc, admitted;
+  for (size_t si = 0; si < S; si++) {
+    SegPlan &p = plans[si];
+    SegmentData &s = *p.seg;
+    if (p.empty) continue;
+    const uint64_t *bits = nullptr;
+    if (!p.match_all) bits = run_filter(e, p, qs, cnt_dev + si, t);
+    GroupByProgram gp = make_group_program(e, s, q, ga, ks, si, remaps, counts, accs);
+    // DictionaryBasedGroupKeyGenerator holder choice on THIS segment's cardinalities (:79-126)
+    __int128 product = 1;
+    for (int j = 0; j < q.num_group_by; j++) product *= s.column(q.group_by[j])->card;
+    int64_t upper = product > array_threshold ? limit : INT64_MAX;
+    if (product <= INT32_MAX && product > array_threshold) upper = std::min<int64_t>((int64_t)product, limit);
+    if (apply_limit && product > array_threshold && product > upper) {
+      // the cap can only bind if more than `upper` distinct keys can appear: count matching docs first
+      unsigned long long c = 0;
+      PINOT_HIP(hipMemcpyAsync(&c, cnt_dev + si, 8, hipMemcpyDeviceToHost, e.stream));
+      PINOT_HIP(hipStreamSynchronize(e.stream));
+      const int64_t matched = p.match_all ? s.num_docs : (int64_t)c;
+      if (matched > upper) {
+        // first-appearance order: keep the `upper` keys with the smallest first docId (IntMapBasedHolder :293-302)
+        first_doc.reserve(ks.G * 4);
+        PINOT_HIP(hipMemsetAsync(first_doc.get(), 0xFF, ks.G * 4, e.stream));
+        launch_first_doc(gp, bits, s.nwords(), s.num_docs, first_doc.get<uint32_t>(), e.stream);
+        std::vector<uint32_t> fd(ks.G);
+        PINOT_HIP(hipMemcpyAsync(fd.data(), first_doc.get(), ks.G * 4, hipMemcpyDeviceToHost, e.stream));
+        PINOT_HIP(hipStreamSynchronize(e.stream));
+        std::vector<std::pair<uint32_t, int64_t>> present;
+        for (int64_t k = 0; k < ks.G; k++)
+          if (fd[k] != 0xFFFFFFFFu) present.push_back({fd[k], k});
+        if ((int64_t)present.size() > upper) {
+          std::nth_element(present.begin(), present.begin() + upper, present.end());
+          present.resize(upper);
+        }
+        std::vector<uint32_t> bm((ks.G + 31) / 32 + 1, 0);
+        for (auto &pk : present) bm[pk.second >> 5] |= 1u << (pk.second & 31);
+        admitted.alloc(bm.size() * 4);
+        PINOT_HIP(hipMemcpyAsync(admitted.get(), bm.data(), bm.size() * 4, hipMemcpyHostToDevice, e.stream));
+        gp.admitted = admitted.get<uint32_t>();
+        PINOT_HIP(hipStreamSynchronize(e.stream));
+      }
+    }
+    t.timed(1, [&] { launch_group_by(gp, bits, s.nwords(), s.num_docs, e.stream); });
+    PINOT_HIP(hipGetLastError());
+    if (gp.admitted) PINOT_HIP(hipStreamSynchronize(e.stream));
+  }
+  std::vector<unsigned long long> hc(S);
+  PINOT_HIP(hipMemcpyAsync(hc.data(), cnt_dev, S * 8, hipMemcpyDeviceToHost, e.stream));
+  PINOT_HIP(hipStreamSynchronize(e.stream));
+  seg_counts.assign(S, 0);
+  for (size_t si = 0; si < S; si++)
+    seg_counts[si] = plans[si].empty ? 0 : plans[si].match_all ? plans[si].seg->num_docs : (int64_t)hc[si];
+}
+
+void init_accs(Engine &e, int64_t G, unsigned long long *counts, const GroupAccs &ga, void *const *accs) {
+  PINOT_HIP(hipMemsetAsync(counts, 0, G * 8, e.stream));
+  for (size_t a = 0; a < ga.acc_kind.size(); a++) {
+    if (ga.acc_kind[a] == 5) continue;
+    PINOT_HIP(hipMemsetAsync(accs[a], ga.acc_kind[a] == 2 ? 0xFF : 0, G * ga.acc_bytes_per_key[a], e.stream));
+  }
+}
+
+}  // namespace
+
+std::unique_ptr<GroupByResult> exec_group_by(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q,
+                                             pinot_exec_stats *stats) {
+  const int na = q.num_aggregations;
+  require(na >= 1 && na <= kMaxAggs, PINOT_ERR_UNSUPPORTED, "1..8 aggregation functions per query");
+  require(q.num_group_by >= 1 && q.num_group_by <= kMaxGroupCols, PINOT_ERR_UNSUPPORTED, "1..8 group-by columns");
+  Arena ar;
+  std::unique_ptr<FilterTreeInput> tree;
+  std::vector<SegPlan> plans = plan_all(e, segs, q, ar, tree);
+  KeySpace ks = build_key_space(segs, q);
+  GroupAccs ga = group_acc_kinds(*segs[0], q);
+  size_t per_key = 8;
+  for (auto b : ga.acc_bytes_per_key) per_key += b;
+  size_t free_b = 0, total_b = 0;
+  PINOT_HIP(hipMemGetInfo(&free_b, &total_b));
+  require((double)ks.G * per_key < 0.5 * (double)free_b, PINOT_ERR_UNSUPPORTED,
+          "dense group-by accumulators do not fit in HBM");
+  QueryScratch qs = prepare(e, plans, ar);
+  const size_t S = plans.size();
+  e.group_scratch.reserve(ks.G * per_key + 64 + S * 8);
+  uint8_t *base = e.group_scratch.get<uint8_t>();
+  auto *cnt_dev = reinterpret_cast<unsigned long long *>(base);
+  auto *counts = reinterpret_cast<unsigned long long *>(base + ((S * 8 + 63) / 64) * 64);
+  std::vector<void *> accs(na, nullptr);
+  uint8_t *p = reinterpret_cast<uint8_t *>(counts) + ks.G * 8;
+  for (int a = 0; a < na; a++) {
+    if (ga.acc_kind[a] == 5) continue;
+    accs[a] = p;
+    p += ks.G * ga.acc_bytes_per_key[a];
+  }
+  PINOT_HIP(hipEventRecord(e.ev_start, e.stream));
+  PINOT_HIP(hipMemsetAsync(cnt_dev, 0, S * 8, e.stream));
+  init_accs(e, ks.G, counts, ga, accs.data());
+  Timer t(e);
+  std::vector<int64_t> seg_counts;
+  accumulate_groups(e, plans, qs, q, ga, ks, counts, accs.data(), cnt_dev, t, seg_counts, true);
+  GroupByProgram gp{};
+  gp.n_aggs = na;
+  gp.counts = counts;
+  for (int a = 0; a < na; a++) { gp.acc[a] = accs[a]; gp.acc_kind[a] = ga.acc_kind[a]; }
+  auto res = finalize_groups(e, q, ga, ks, gp);
+  PINOT_HIP(hipEventRecord(e.ev_stop, e.stream));
+  PINOT_HIP(hipStreamSynchronize(e.stream));
+  float ms = 0;
+  PINOT_HIP(hipEventElapsedTime(&ms, e.ev_start, e.ev_stop));
+  t.collect();
+  fill_stats(q, plans, seg_counts, ms, stats);
+  return res;
+}
+
+// ------------------------------------------------------------------ multi-GPU partials
+void exec_group_by_layout(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q,
+                          pinot_partial_layout *layout) {
+  (void)e;
+  require(!segs.empty(), PINOT_ERR_BAD_ARG, "no segments");
+  KeySpace ks = build_key_space(segs, q);
+  for (auto &per_seg : ks.remap)
+    for (auto &m : per_seg)
+      require(m.empty(), PINOT_ERR_UNSUPPORTED, "partial group-by needs identical group-by dictionaries");
+  GroupAccs ga = group_acc_kinds(*segs[0], q);
+  memset(layout, 0, sizeof(*layout));
+  layout->num_keys = ks.G;
+  layout->num_aggregations = q.num_aggregations;
+  for (int a = 0; a < q.num_aggregations && a < 8; a++) layout->acc_kind[a] = ga.acc_kind[a];
+}
+
+void exec_group_by_partial(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q,
+                           int64_t *counts_dev, void *const *accs_dev, pinot_exec_stats *stats) {
+  Arena ar;
+  std::unique_ptr<FilterTreeInput> tree;
+  std::vector<SegPlan> plans = plan_all(e, segs, q, ar, tree);
+  KeySpace ks = build_key_space(segs, q);
+  GroupAccs ga = group_acc_kinds(*segs[0], q);
+  QueryScratch qs = prepare(e, plans, ar);
+  const size_t S = plans.size();
+  e.reduced.reserve(S * 8 + 16);
+  auto *cnt_dev = e.reduced.get<unsigned long long>();
+  PINOT_HIP(hipEventRecord(e.ev_start, e.stream));
+  PINOT_HIP(hipMemsetAsync(cnt_dev, 0, S * 8, e.stream));
+  auto *counts = reinterpret_cast<unsigned long long *>(counts_dev);
+  init_accs(e, ks.G, counts, ga, accs_dev);
+  Timer t(e);
+  std::vector<int64_t> seg_counts;
+  accumulate_groups(e, plans, qs, q, ga, ks, counts, accs_dev, cnt_dev, t, seg_counts, false);
+  PINOT_HIP(hipEventRecord(e.ev_stop, e.stream));
+  PINOT_HIP(hipStreamSynchronize(e.stream));
+  float ms = 0;
+  PINOT_HIP(hipEventElapsedTime(&ms, e.ev_start, e.ev_stop));
+  t.collect();
+  fill_stats(q, plans, seg_counts, ms, stats);
+}
+
+std::unique_ptr<GroupByResult> exec_group_by_finalize(Engine &e, const std::vector<SegmentData *> &segs,
+                                                      const pinot_query &q, const int64_t *counts_dev,
+                                                      void *const *accs_dev) {
+  KeySpace ks = build_key_space(segs, q);
+  GroupAccs ga = group_acc_kinds(*segs[0], q);
+  GroupByProgram gp{};
+  gp.n_aggs = q.num_aggregations;
+  gp.counts = reinterpret_cast<unsigned long long *>(const_cast<int64_t *>(counts_dev));
+  for (int a = 0; a < q.num_aggregations; a++) {
+    gp.acc[a] = accs_dev ? accs_dev[a] : nullptr;
+    gp.acc_kind[a] = ga.acc_kind[a];
+  }
+  return finalize_groups(e, q, ga, ks, gp);
+}
+
+}  // namespace pinot

@@ -1,0 +1,142 @@
+"""ctypes binding of libpinot_gpu.so (include/pinot_gpu.h).
+
+The library is the product: HIP kernels + C++ engine. There is no CPU fallback anywhere in
+this package — if the .so is missing or no HIP device exists, every entry point raises.
+"""
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpinot_gpu.so")
+
+PINOT_OK = 0
+STATUS = {0: "PINOT_OK", 1: "PINOT_ERR_BAD_ARG", 2: "PINOT_ERR_OOM", 3: "PINOT_ERR_DEVICE",
+          4: "PINOT_ERR_UNSUPPORTED", 5: "PINOT_ERR_BAD_QUERY"}
+DATA_TYPE = {"INT": 0, "LONG": 1, "FLOAT": 2, "DOUBLE": 3, "STRING": 4}
+FILTER_OP = {"AND": 0, "OR": 1, "EQUALITY": 2, "NOT": 3, "RANGE": 4, "IN": 5, "NOT_IN": 6}
+AGG_FN = {"COUNT": 0, "SUM": 1, "MIN": 2, "MAX": 3, "AVG": 4, "DISTINCTCOUNTHLL": 5}
+
+# every symbol include/pinot_gpu.h declares (checked by tests/test_abi.py)
+EXPORTED_SYMBOLS = [
+    "pinot_gpu_last_error", "pinot_gpu_abi_version", "pinot_gpu_device_count",
+    "pinot_gpu_engine_create", "pinot_gpu_engine_destroy", "pinot_gpu_engine_set_config",
+    "pinot_gpu_segment_register", "pinot_gpu_segment_release", "pinot_gpu_segment_device_bytes",
+    "pinot_gpu_filter", "pinot_gpu_aggregate", "pinot_gpu_group_by",
+    "pinot_groupby_num_groups", "pinot_groupby_num_columns", "pinot_groupby_key", "pinot_groupby_values",
+    "pinot_groupby_hll", "pinot_groupby_raw_keys", "pinot_groupby_free",
+    "pinot_gpu_group_by_layout", "pinot_gpu_group_by_partial", "pinot_gpu_group_by_finalize",
+    "pinot_gpu_segment_register_synthetic", "pinot_gpu_synchronize", "pinot_gpu_last_kernel_ms",
+]
+
+
+class PinotGpuError(RuntimeError):
+    def __init__(self, status, msg):
+        super().__init__("%s: %s" % (STATUS.get(status, status), msg))
+        self.status = status
+
+
+class ColumnDesc(C.Structure):
+    _fields_ = [("name", C.c_char_p), ("data_type", C.c_int32), ("cardinality", C.c_int32),
+                ("bits_per_value", C.c_int32), ("is_sorted", C.c_int32), ("has_inverted_index", C.c_int32),
+                ("string_width", C.c_int32),
+                ("dictionary", C.c_void_p), ("dictionary_len", C.c_uint64),
+                ("forward_index", C.c_void_p), ("forward_index_len", C.c_uint64),
+                ("sorted_index", C.c_void_p), ("sorted_index_len", C.c_uint64),
+                ("inverted_index", C.c_void_p), ("inverted_index_len", C.c_uint64)]
+
+
+class SegmentDesc(C.Structure):
+    _fields_ = [("name", C.c_char_p), ("num_docs", C.c_int32), ("num_columns", C.c_int32),
+                ("columns", C.POINTER(ColumnDesc))]
+
+
+class FilterNode(C.Structure):
+    _fields_ = [("op", C.c_int32), ("num_children", C.c_int32), ("column", C.c_char_p),
+                ("num_values", C.c_int32), ("values", C.POINTER(C.c_char_p))]
+
+
+class AggSpec(C.Structure):
+    _fields_ = [("function", C.c_int32), ("column", C.c_char_p)]
+
+
+class Query(C.Structure):
+    _fields_ = [("num_filter_nodes", C.c_int32), ("filter", C.POINTER(FilterNode)),
+                ("num_aggregations", C.c_int32), ("aggregations", C.POINTER(AggSpec)),
+                ("num_group_by", C.c_int32), ("group_by", C.POINTER(C.c_char_p)),
+                ("num_groups_limit", C.c_int32), ("max_init_group_holder_capacity", C.c_int32)]
+
+
+class ExecStats(C.Structure):
+    _fields_ = [("num_docs_scanned", C.c_int64), ("num_entries_scanned_in_filter", C.c_int64),
+                ("num_entries_scanned_post_filter", C.c_int64), ("num_total_raw_docs", C.c_int64),
+                ("num_segments_processed", C.c_int64), ("device_ms", C.c_double)]
+
+
+class AggResult(C.Structure):
+    _fields_ = [("count", C.c_int64), ("value", C.c_double), ("exact_sum", C.c_int64),
+                ("has_exact_sum", C.c_int32), ("reserved", C.c_int32), ("hll_cardinality", C.c_int64),
+                ("hll_registers", C.c_uint8 * 256)]
+
+
+class PartialLayout(C.Structure):
+    _fields_ = [("num_keys", C.c_int64), ("num_aggregations", C.c_int32), ("reserved", C.c_int32),
+                ("acc_kind", C.c_int32 * 8)]
+
+
+_lib = None
+
+
+def load(path=None):
+    """Load libpinot_gpu.so (raises if it is missing: there is no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise PinotGpuError(3, "libpinot_gpu.so not built (%s); run `make -C incubator-pinot_amd`" % p)
+    lib = C.CDLL(p)
+    P = C.c_void_p
+    i32, i64, u64 = C.c_int32, C.c_int64, C.c_uint64
+    sig = {
+        "pinot_gpu_last_error": (C.c_char_p, []),
+        "pinot_gpu_abi_version": (i32, []),
+        "pinot_gpu_device_count": (i32, []),
+        "pinot_gpu_engine_create": (i32, [i32, C.c_char_p, C.POINTER(P)]),
+        "pinot_gpu_engine_destroy": (i32, [P]),
+        "pinot_gpu_engine_set_config": (i32, [P, C.c_char_p]),
+        "pinot_gpu_segment_register": (i32, [P, C.POINTER(SegmentDesc), C.POINTER(i64)]),
+        "pinot_gpu_segment_release": (i32, [P, i64]),
+        "pinot_gpu_segment_device_bytes": (i32, [P, i64, C.POINTER(u64)]),
+        "pinot_gpu_filter": (i32, [P, i64, i32, C.POINTER(FilterNode), P, C.POINTER(i64)]),
+        "pinot_gpu_aggregate": (i32, [P, C.POINTER(i64), i32, C.POINTER(Query), C.POINTER(AggResult),
+                                      C.POINTER(ExecStats)]),
+        "pinot_gpu_group_by": (i32, [P, C.POINTER(i64), i32, C.POINTER(Query), C.POINTER(P), C.POINTER(ExecStats)]),
+        "pinot_groupby_num_groups": (i64, [P]),
+        "pinot_groupby_num_columns": (i32, [P]),
+        "pinot_groupby_key": (C.c_char_p, [P, i64]),
+        "pinot_groupby_values": (i32, [P, i32, P, P]),
+        "pinot_groupby_hll": (i32, [P, i32, P, P]),
+        "pinot_groupby_raw_keys": (i32, [P, P]),
+        "pinot_groupby_free": (None, [P]),
+        "pinot_gpu_group_by_layout": (i32, [P, C.POINTER(i64), i32, C.POINTER(Query), C.POINTER(PartialLayout)]),
+        "pinot_gpu_group_by_partial": (i32, [P, C.POINTER(i64), i32, C.POINTER(Query), P, C.POINTER(P),
+                                             C.POINTER(ExecStats)]),
+        "pinot_gpu_group_by_finalize": (i32, [P, C.POINTER(i64), i32, C.POINTER(Query), P, C.POINTER(P),
+                                              C.POINTER(P)]),
+        "pinot_gpu_segment_register_synthetic": (i32, [P, C.c_char_p, i32, i32, C.POINTER(C.c_char_p),
+                                                       C.POINTER(i32), u64, C.POINTER(i64)]),
+        "pinot_gpu_synchronize": (i32, [P]),
+        "pinot_gpu_last_kernel_ms": (i32, [P, i32, C.POINTER(C.c_double), C.POINTER(i64)]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(status):
+    if status != PINOT_OK:
+        msg = _lib.pinot_gpu_last_error().decode("utf-8", "replace") if _lib else ""
+        raise PinotGpuError(status, msg)

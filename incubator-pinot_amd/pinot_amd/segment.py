@@ -1,0 +1,242 @@
+"""Pinot immutable-segment column buffers, built in memory in Pinot's own byte format.
+
+This is the *input side* of the drop-in boundary: the C-ABI
+(`include/pinot_gpu.h`, `pinot_gpu_segment_register`) receives exactly these
+buffers — the bytes `PinotDataBuffer` would hold for a loaded v1/v3 segment — as
+host pointers, and uploads them to HBM.
+
+Byte formats (all restated from the reference's segment creator / readers):
+
+* dictionary: sorted ascending unique values, big-endian fixed width
+  (`SegmentDictionaryCreator.java:68-206`, `FixedByteValueReaderWriter`);
+  STRING values are UTF-8, zero-padded to the longest value
+  (`FixedByteValueReaderWriter.java:56-68`, padding byte 0).
+* unsorted forward index: dictIds fixed-bit packed MSB-first over a big-endian
+  byte stream, `b = getNumBitsPerValue(card - 1)` bits per doc, buffer exactly
+  ceil(N*b/8) bytes (`PinotDataBitSet.java:60-71,135-197`,
+  `FixedBitSingleValueWriter.java:32-40`, `SegmentColumnarIndexCreator.java:404`).
+* sorted forward index: 2 big-endian ints `[startDocId, endDocId]` (inclusive)
+  per dictId (`SortedIndexReaderImpl.java:34-39`).
+* bitmap inverted index: (card + 1) big-endian int offsets followed by one
+  portable-format RoaringBitmap per dictId
+  (`OffHeapBitmapInvertedIndexCreator.java:183-206`); Pinot only calls
+  `add(int)`, so containers are array (card <= 4096) or bitmap containers.
+"""
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+import numpy as np
+
+DATA_TYPES = ("INT", "LONG", "FLOAT", "DOUBLE", "STRING")
+_BE_DTYPE = {"INT": ">i4", "LONG": ">i8", "FLOAT": ">f4", "DOUBLE": ">f8"}
+# Pinot default null values (FieldSpec.java:50,54,57)
+DEFAULT_NULL_DIMENSION = {"INT": -2147483648, "LONG": -9223372036854775808,
+                          "FLOAT": float("-inf"), "DOUBLE": float("-inf"), "STRING": "null"}
+DEFAULT_NULL_METRIC = {"INT": 0, "LONG": 0, "FLOAT": 0.0, "DOUBLE": 0.0, "STRING": "null"}
+
+
+def num_bits_per_value(max_value: int) -> int:
+    """`PinotDataBitSet.getNumBitsPerValue` (PinotDataBitSet.java:60-71): at least 1 bit."""
+    if max_value <= 1:
+        return 1
+    return int(max_value).bit_length()
+
+
+def pack_fixed_bit(dict_ids: np.ndarray, bits: int) -> bytes:
+    """Pack dictIds MSB-first into a big-endian bit stream of exactly ceil(N*b/8) bytes.
+
+    Equivalent to repeated `PinotDataBitSet.writeInt(i, b, v)` (PinotDataBitSet.java:135-197).
+    """
+    ids = np.ascontiguousarray(dict_ids, dtype=np.uint32)
+    n = ids.shape[0]
+    if n == 0:
+        return b""
+    shifts = np.arange(bits - 1, -1, -1, dtype=np.uint32)
+    out = []
+    chunk = 1 << 20  # multiple of 8 values => every chunk ends on a byte boundary
+    for s in range(0, n, chunk):
+        v = ids[s:s + chunk]
+        bitmat = ((v[:, None] >> shifts[None, :]) & 1).astype(np.uint8)
+        out.append(np.packbits(bitmat.reshape(-1), bitorder="big").tobytes())
+    return b"".join(out)
+
+
+def unpack_fixed_bit(buf: bytes, n: int, bits: int) -> np.ndarray:
+    """Vectorised `FixedBitSingleValueReader.readValues` for all docs (host-side helper)."""
+    raw = np.frombuffer(buf, dtype=np.uint8)
+    padded = np.zeros(raw.shape[0] + 8, dtype=np.uint64)
+    padded[:raw.shape[0]] = raw
+    idx = np.arange(n, dtype=np.uint64)
+    bitpos = idx * np.uint64(bits)
+    b0 = (bitpos >> np.uint64(3)).astype(np.int64)
+    off = bitpos & np.uint64(7)
+    w = np.zeros(n, dtype=np.uint64)
+    for k in range(5):
+        w = (w << np.uint64(8)) | padded[b0 + k]
+    shift = np.uint64(40) - off - np.uint64(bits)
+    return ((w >> shift) & np.uint64((1 << bits) - 1)).astype(np.int32)
+
+
+# ---------------------------------------------------------------- roaring (portable format)
+SERIAL_COOKIE_NO_RUNCONTAINER = 12346
+SERIAL_COOKIE = 12347
+
+
+def roaring_serialize(doc_ids: np.ndarray) -> bytes:
+    """Portable RoaringBitmap serialisation of a sorted docId set (array + bitmap containers, no runs)."""
+    d = np.asarray(doc_ids, dtype=np.uint32)
+    if d.shape[0] == 0:
+        return np.array([SERIAL_COOKIE_NO_RUNCONTAINER, 0], dtype="<u4").tobytes()
+    keys = (d >> 16).astype(np.uint16)
+    uk, starts, counts = np.unique(keys, return_index=True, return_counts=True)
+    n = uk.shape[0]
+    header = [np.array([SERIAL_COOKIE_NO_RUNCONTAINER, n], dtype="<u4").tobytes()]
+    kc = np.empty(2 * n, dtype="<u2")
+    kc[0::2] = uk
+    kc[1::2] = (counts - 1).astype(np.uint16)
+    header.append(kc.tobytes())
+    payloads = []
+    for s, c in zip(starts, counts):
+        lows = (d[s:s + c] & 0xFFFF).astype(np.uint16)
+        if c <= 4096:
+            payloads.append(lows.astype("<u2").tobytes())
+        else:
+            words = np.zeros(1024, dtype=np.uint64)
+            np.bitwise_or.at(words, (lows >> 6).astype(np.int64), np.left_shift(np.uint64(1), (lows & 63).astype(np.uint64)))
+            payloads.append(words.astype("<u8").tobytes())
+    base = 8 + 4 * n + 4 * n
+    offs = np.zeros(n, dtype="<u4")
+    pos = base
+    for i, p in enumerate(payloads):
+        offs[i] = pos
+        pos += len(p)
+    header.append(offs.tobytes())
+    return b"".join(header) + b"".join(payloads)
+
+
+def build_inverted_index(dict_ids: np.ndarray, card: int) -> bytes:
+    """`OffHeapBitmapInvertedIndexCreator.seal` layout: (card+1) BE int offsets + roaring payloads."""
+    order = np.argsort(dict_ids, kind="stable")
+    sorted_ids = dict_ids[order]
+    bounds = np.searchsorted(sorted_ids, np.arange(card + 1))
+    blobs = []
+    for i in range(card):
+        docs = np.sort(order[bounds[i]:bounds[i + 1]])
+        blobs.append(roaring_serialize(docs))
+    offsets = np.zeros(card + 1, dtype=">i4")
+    pos = (card + 1) * 4
+    offsets[0] = pos
+    for i, b in enumerate(blobs):
+        pos += len(b)
+        offsets[i + 1] = pos
+    return offsets.tobytes() + b"".join(blobs)
+
+
+# ---------------------------------------------------------------- segment model
+@dataclass
+class Column:
+    name: str
+    data_type: str
+    cardinality: int
+    bits: int
+    is_sorted: bool
+    has_inverted_index: bool
+    num_docs: int
+    dictionary: bytes            # BE fixed-width sorted values
+    string_width: int = 0
+    fwd: Optional[bytes] = None  # fixed-bit packed forward index (unsorted columns)
+    sorted_index: Optional[bytes] = None  # 2*card BE ints (sorted columns)
+    inverted: Optional[bytes] = None      # bitmap inverted index (unsorted columns)
+    _dict_values: Optional[np.ndarray] = field(default=None, repr=False)
+    _dict_ids: Optional[np.ndarray] = field(default=None, repr=False)
+
+    def dict_values(self):
+        """Decoded dictionary (host convenience; strings unpadded like `getUnpaddedString`)."""
+        if self._dict_values is None:
+            if self.data_type == "STRING":
+                w = self.string_width
+                raw = np.frombuffer(self.dictionary, dtype=np.uint8).reshape(self.cardinality, w) if w else \
+                    np.zeros((self.cardinality, 0), dtype=np.uint8)
+                vals = []
+                for r in raw:
+                    bs = bytes(r)
+                    z = bs.find(b"\x00")
+                    vals.append((bs if z < 0 else bs[:z]).decode("utf-8"))
+                self._dict_values = np.array(vals, dtype=object)
+            else:
+                self._dict_values = np.frombuffer(self.dictionary, dtype=_BE_DTYPE[self.data_type]).astype(
+                    _BE_DTYPE[self.data_type].replace(">", "<"))
+        return self._dict_values
+
+
+@dataclass
+class Segment:
+    name: str
+    num_docs: int
+    columns: Dict[str, Column]
+
+    def column(self, name) -> Column:
+        return self.columns[name]
+
+
+def _dictionary_bytes(uniq, data_type):
+    if data_type == "STRING":
+        enc = [s.encode("utf-8") for s in uniq]
+        width = max((len(e) for e in enc), default=0)
+        buf = b"".join(e + b"\x00" * (width - len(e)) for e in enc)
+        return buf, width
+    return np.asarray(uniq).astype(_BE_DTYPE[data_type]).tobytes(), 0
+
+
+def _sorted_unique(values, data_type):
+    if data_type == "STRING":
+        # Java String.compareTo order == code-point order for BMP text; sort by UTF-8 bytes equivalently
+        uniq = sorted(set(values), key=lambda s: s.encode("utf-8"))
+        index = {v: i for i, v in enumerate(uniq)}
+        ids = np.fromiter((index[v] for v in values), dtype=np.int32, count=len(values))
+        return uniq, ids
+    arr = np.asarray(values, dtype={"INT": np.int32, "LONG": np.int64, "FLOAT": np.float32,
+                                    "DOUBLE": np.float64}[data_type])
+    uniq, ids = np.unique(arr, return_inverse=True)
+    return uniq, ids.astype(np.int32)
+
+
+def build_column(name, values, data_type, inverted=False, allow_sorted=True) -> Column:
+    """Create one column the way `SegmentColumnarIndexCreator` does for a single-value dictionary column."""
+    if data_type not in DATA_TYPES:
+        raise ValueError("unsupported data type %s" % data_type)
+    uniq, ids = _sorted_unique(values, data_type)
+    card = len(uniq)
+    n = ids.shape[0]
+    bits = num_bits_per_value(card - 1)
+    dbytes, width = _dictionary_bytes(uniq, data_type)
+    is_sorted = bool(allow_sorted and (n <= 1 or bool(np.all(ids[1:] >= ids[:-1]))))
+    col = Column(name=name, data_type=data_type, cardinality=card, bits=bits, is_sorted=is_sorted,
+                 has_inverted_index=bool(inverted) or is_sorted, num_docs=n, dictionary=dbytes,
+                 string_width=width)
+    col._dict_ids = ids
+    if is_sorted:
+        starts = np.searchsorted(ids, np.arange(card), side="left")
+        ends = np.searchsorted(ids, np.arange(card), side="right") - 1
+        pairs = np.empty(2 * card, dtype=">i4")
+        pairs[0::2] = starts
+        pairs[1::2] = ends
+        col.sorted_index = pairs.tobytes()
+    else:
+        col.fwd = pack_fixed_bit(ids, bits)
+        if inverted:
+            col.inverted = build_inverted_index(ids, card)
+    return col
+
+
+def build_segment(name, columns: Dict[str, tuple], inverted_columns=(), num_docs=None) -> Segment:
+    """columns: {name: (data_type, values)} in schema order."""
+    cols = {}
+    n = None
+    for cname, (dt, vals) in columns.items():
+        col = build_column(cname, vals, dt, inverted=cname in inverted_columns)
+        if n is None:
+            n = col.num_docs
+        elif n != col.num_docs:
+            raise ValueError("ragged columns")
+        cols[cname] = col
+    return Segment(name=name, num_docs=n if num_docs is None else num_docs, columns=cols)

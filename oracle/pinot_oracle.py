@@ -1,0 +1,595 @@
+"""CPU oracle: a numpy restatement of Pinot's segment query executor hot path.
+
+TEST INFRASTRUCTURE. Only tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg may import, call or execute anything under oracle/, and only
+as the checker — never as the thing measured or shipped. The product path
+(incubator-pinot_amd/) never imports this module.
+
+Pinning: the reference is Java and cannot be compiled or run here (no JDK; see
+SURVEY.md §8c). This restatement is pinned by the reference's own known-answer
+tests, replayed in tests/test_oracle_kats.py on the reference's own fixtures:
+  * PT/queries/InnerSegmentAggregationSingleValueQueriesTest.java:41-160
+  * PT/queries/InterSegmentAggregationSingleValueQueriesTest.java:36-206
+  * PT/query/executor/QueryExecutorTest.java:128-155
+  * PT/core/operator/filter/AndFilterOperatorTest.java / OrFilterOperatorTest.java
+  * pinot-core/src/test/resources/data/paddingNull.tar.gz (byte-level format)
+(PT = pinot-core/src/test/java/org/apache/pinot.)  Results are frozen as
+fixtures under tests/golden/ by tests/golden/make_golden.py.
+
+Each function cites the reference file:line it restates (PC =
+pinot-core/src/main/java/org/apache/pinot/core).
+
+Query representation (what the PQL compiler hands the server, i.e. the parts of
+the Thrift BrokerRequest the hot path reads, `request.thrift:26-168`):
+  {"aggregations": [{"function": "SUM", "column": "c"} ...],
+   "filter": None | {"operator": "AND"|"OR", "children": [...]}
+                   | {"operator": "EQUALITY"|"NOT"|"RANGE"|"IN"|"NOT_IN", "column": c, "values": [str]},
+   "group_by": None | {"columns": [...], "top_n": 10}}
+"""
+import math
+import numpy as np
+
+from hll import HyperLogLog, hash_long_np, hash_value, register_and_rank_np, cardinality as hll_cardinality
+
+INT_MAX = 2147483647
+INVALID_ID = -1
+
+
+# ----------------------------------------------------------------------------- L1 readers
+def read_int(buf: bytes, index: int, bits: int) -> int:
+    """Scalar `PinotDataBitSet.readInt(index, numBitsPerValue)` (PC/io/util/PinotDataBitSet.java:79-100)."""
+    bit_offset = index * bits
+    byte_offset = bit_offset // 8
+    bit_in_first = bit_offset % 8
+    cur = buf[byte_offset] & (0xFF >> bit_in_first)
+    left = bits - (8 - bit_in_first)
+    if left <= 0:
+        return cur >> -left
+    while left > 8:
+        byte_offset += 1
+        cur = (cur << 8) | buf[byte_offset]
+        left -= 8
+    return (cur << left) | (buf[byte_offset + 1] >> (8 - left))
+
+
+def read_all(buf: bytes, n: int, bits: int) -> np.ndarray:
+    """Vectorised readInt over docs [0, n) — same arithmetic as read_int, a 40-bit window per value."""
+    raw = np.frombuffer(buf, dtype=np.uint8)
+    if raw.shape[0] * 8 < n * bits:
+        raise ValueError("forward index shorter than ceil(N*b/8) (FixedBitIntReaderWriter.java:31-36)")
+    pad = np.zeros(raw.shape[0] + 8, dtype=np.uint64)
+    pad[:raw.shape[0]] = raw
+    pos = np.arange(n, dtype=np.uint64) * np.uint64(bits)
+    b0 = (pos >> np.uint64(3)).astype(np.int64)
+    w = np.zeros(n, dtype=np.uint64)
+    for k in range(5):
+        w = (w << np.uint64(8)) | pad[b0 + k]
+    sh = np.uint64(40) - (pos & np.uint64(7)) - np.uint64(bits)
+    return ((w >> sh) & np.uint64((1 << bits) - 1)).astype(np.int64)
+
+
+def sorted_pairs(col):
+    """`SortedIndexReaderImpl` (PC/io/reader/impl/v1/SortedIndexReaderImpl.java:34-39): [start,end] per dictId."""
+    p = np.frombuffer(col.sorted_index, dtype=">i4").astype(np.int64)
+    return p[0::2], p[1::2]
+
+
+def dict_ids(col) -> np.ndarray:
+    """Per-doc dictIds of a column: fixed-bit fwd index or sorted index (`PhysicalColumnIndexContainer.java:90-99`)."""
+    if col.is_sorted:
+        starts, ends = sorted_pairs(col)
+        ids = np.empty(col.num_docs, dtype=np.int64)
+        for i, (s, e) in enumerate(zip(starts, ends)):
+            ids[s:e + 1] = i
+        return ids
+    return read_all(col.fwd, col.num_docs, col.bits)
+
+
+def roaring_deserialize(blob: bytes) -> np.ndarray:
+    """Portable RoaringBitmap reader (RoaringBitmap 0.8.0 format spec; array, bitmap and run containers).
+
+    Parity of the byte format itself is unpinned (no reference fixture holds a .bitmap.inv payload).
+    """
+    mv = memoryview(blob)
+    cookie = int.from_bytes(mv[0:4], "little")
+    pos = 4
+    runs = None
+    if cookie == 12346:
+        n = int.from_bytes(mv[4:8], "little")
+        pos = 8
+        has_offsets = True
+    elif (cookie & 0xFFFF) == 12347:
+        n = (cookie >> 16) + 1
+        rb = (n + 7) // 8
+        runs = bytes(mv[pos:pos + rb])
+        pos += rb
+        has_offsets = n >= 4
+    else:
+        raise ValueError("bad roaring cookie %d" % cookie)
+    kc = np.frombuffer(blob, dtype="<u2", count=2 * n, offset=pos)
+    keys = kc[0::2].astype(np.int64)
+    cards = kc[1::2].astype(np.int64) + 1
+    pos += 4 * n
+    if has_offsets:
+        pos += 4 * n
+    out = []
+    for i in range(n):
+        is_run = runs is not None and (runs[i // 8] >> (i % 8)) & 1
+        if is_run:
+            nr = int.from_bytes(mv[pos:pos + 2], "little")
+            pos += 2
+            rl = np.frombuffer(blob, dtype="<u2", count=2 * nr, offset=pos).astype(np.int64)
+            pos += 4 * nr
+            lows = np.concatenate([np.arange(s, s + l + 1) for s, l in zip(rl[0::2], rl[1::2])]) if nr else \
+                np.zeros(0, np.int64)
+        elif cards[i] <= 4096:
+            lows = np.frombuffer(blob, dtype="<u2", count=int(cards[i]), offset=pos).astype(np.int64)
+            pos += 2 * int(cards[i])
+        else:
+            words = np.frombuffer(blob, dtype="<u8", count=1024, offset=pos)
+            pos += 8192
+            bits = np.unpackbits(words.view(np.uint8), bitorder="little")
+            lows = np.nonzero(bits)[0].astype(np.int64)
+        out.append((keys[i] << 16) | lows)
+    return np.concatenate(out) if out else np.zeros(0, dtype=np.int64)
+
+
+def inverted_doc_ids(col, dict_id: int) -> np.ndarray:
+    """`BitmapInvertedIndexReader.getDocIds` (PC/segment/index/readers/BitmapInvertedIndexReader.java:59-119)."""
+    offs = np.frombuffer(col.inverted, dtype=">i4", count=col.cardinality + 1)
+    return roaring_deserialize(col.inverted[offs[dict_id]:offs[dict_id + 1]])
+
+
+# ----------------------------------------------------------------------------- dictionaries
+def _java_parse(data_type, s):
+    s = s.strip() if data_type != "STRING" else s
+    if data_type in ("INT", "LONG"):
+        v = int(s)  # Integer.parseInt / Long.parseLong (decimal)
+        return v
+    if data_type in ("FLOAT", "DOUBLE"):
+        return float(s)
+    return s
+
+
+def insertion_index_of(col, raw: str) -> int:
+    """`ImmutableDictionaryReader.binarySearch` (PC/segment/index/readers/ImmutableDictionaryReader.java:80-180)."""
+    vals = col.dict_values()
+    v = _java_parse(col.data_type, raw)
+    if col.data_type == "FLOAT":
+        v = float(np.float32(v))
+    low, high = 0, len(vals) - 1
+    key = (lambda x: x.encode("utf-8")) if col.data_type == "STRING" else (lambda x: x)
+    kv = key(v)
+    while low <= high:
+        mid = (low + high) >> 1
+        mv = key(vals[mid])
+        if mv < kv:
+            low = mid + 1
+        elif mv > kv:
+            high = mid - 1
+        else:
+            return mid
+    return -(low + 1)
+
+
+def index_of(col, raw):
+    i = insertion_index_of(col, raw)
+    return i if i >= 0 else -1
+
+
+# ----------------------------------------------------------------------------- predicates
+class Evaluator:
+    """A dictionary-based predicate evaluator: the set of matching dictIds + alwaysTrue/alwaysFalse.
+
+    EQ   `EqualsPredicateEvaluatorFactory.java:71-102`
+    NEQ  `NotEqualsPredicateEvaluatorFactory.java:71-127`
+    IN   `InPredicateEvaluatorFactory.java:83-127`
+    NOT_IN `NotInPredicateEvaluatorFactory.java:83-145`
+    RANGE (offline) `RangePredicateEvaluatorFactory.java:79-158`
+    """
+
+    def __init__(self, kind, matching, card, always_true, always_false):
+        self.kind = kind
+        self.matching = matching  # bool[card]
+        self.card = card
+        self.always_true = always_true
+        self.always_false = always_false
+
+
+def parse_range(s):
+    """`RangePredicate` (PC/common/predicate/RangePredicate.java:41-67): "(lo\\t\\thi]" etc."""
+    s = s.strip()
+    parts = s.split("\t\t")
+    lower = parts[0][1:]
+    upper = parts[1][:-1]
+    inc_lower = True if (not s.startswith("(") or lower == "*") else False
+    inc_upper = True if (not s.endswith(")") or upper == "*") else False
+    return lower, upper, inc_lower, inc_upper
+
+
+def make_evaluator(leaf, col) -> Evaluator:
+    op = leaf["operator"]
+    card = col.cardinality
+    m = np.zeros(card, dtype=bool)
+    values = leaf["values"]
+    if op == "EQUALITY":
+        i = index_of(col, values[0])
+        if i >= 0:
+            m[i] = True
+        return Evaluator("EQ", m, card, i >= 0 and card == 1, i < 0)
+    if op == "NOT":
+        i = index_of(col, values[0])
+        m[:] = True
+        if i >= 0:
+            m[i] = False
+        # NotEqualsPredicateEvaluatorFactory: alwaysTrue if value absent, alwaysFalse if it is the only value
+        return Evaluator("NEQ", m, card, i < 0, i >= 0 and card == 1)
+    if op in ("IN", "NOT_IN"):
+        vals = values[0].split("\t\t") if len(values) == 1 else values
+        ids = {index_of(col, v) for v in vals}
+        ids.discard(-1)
+        for i in ids:
+            m[i] = True
+        if op == "IN":
+            return Evaluator("IN", m, card, len(ids) == card, len(ids) == 0)
+        return Evaluator("NOT_IN", ~m, card, len(ids) == 0, len(ids) == card)
+    if op == "RANGE":
+        lower, upper, inc_l, inc_u = parse_range(values[0])
+        if lower == "*":
+            start = 0
+        else:
+            ii = insertion_index_of(col, lower)
+            start = -(ii + 1) if ii < 0 else (ii if inc_l else ii + 1)
+        if upper == "*":
+            end = card
+        else:
+            ii = insertion_index_of(col, upper)
+            end = -(ii + 1) if ii < 0 else (ii + 1 if inc_u else ii)
+        n = end - start
+        if n > 0:
+            m[start:end] = True
+        return Evaluator("RANGE", m, card, n > 0 and n == card, n <= 0)
+    raise NotImplementedError("predicate %s" % op)
+
+
+# ----------------------------------------------------------------------------- filter
+def filter_mask(segment, tree):
+    """Docs matching the filter tree, as a bool[numDocs].
+
+    Structure follows `FilterPlanNode.constructPhysicalOperator` (PC/plan/FilterPlanNode.java:70-126) and
+    `FilterOperatorUtils` (PC/operator/filter/FilterOperatorUtils.java:43-122): alwaysTrue/alwaysFalse leaves fold
+    to MatchAll/Empty. The set semantics of every operator kind (scan / sorted / bitmap / AND / OR) are the same,
+    so the oracle evaluates each leaf on the forward index and additionally cross-checks index-backed leaves
+    against the sorted / inverted index (the path `getLeafFilterOperator` picks for non-RANGE predicates).
+    """
+    n = segment.num_docs
+    if tree is None:
+        return np.ones(n, dtype=bool)
+    op = tree["operator"]
+    if op in ("AND", "OR"):
+        ms = [filter_mask(segment, c) for c in tree["children"]]
+        out = ms[0].copy()
+        for m in ms[1:]:
+            if op == "AND":
+                out &= m
+            else:
+                out |= m
+        return out
+    col = segment.column(tree["column"])
+    ev = make_evaluator(tree, col)
+    if ev.always_false:
+        return np.zeros(n, dtype=bool)
+    if ev.always_true:
+        return np.ones(n, dtype=bool)
+    ids = dict_ids(col)
+    mask = ev.matching[ids]
+    if col.is_sorted and ev.kind != "RANGE":
+        # SortedInvertedIndexBasedFilterOperator (:59-158): union of [start,end] ranges (complement if exclusive)
+        starts, ends = sorted_pairs(col)
+        alt = np.zeros(n, dtype=bool)
+        for i in np.nonzero(ev.matching)[0]:
+            alt[starts[i]:ends[i] + 1] = True
+        assert (alt == mask).all(), "sorted-index path disagrees with scan"
+    elif col.has_inverted_index and col.inverted is not None and ev.kind != "RANGE":
+        # BitmapBasedFilterOperator + BitmapDocIdSet (:33-58): OR of matching bitmaps, flipped if exclusive
+        exclusive = ev.kind in ("NEQ", "NOT_IN")
+        alt = np.zeros(n, dtype=bool)
+        sel = ~ev.matching if exclusive else ev.matching
+        for i in np.nonzero(sel)[0]:
+            alt[inverted_doc_ids(col, int(i))] = True
+        if exclusive:
+            alt = ~alt
+        assert (alt == mask).all(), "inverted-index path disagrees with scan"
+    return mask
+
+
+# ----------------------------------------------------------------------------- aggregation functions
+NUMERIC = ("INT", "LONG", "FLOAT", "DOUBLE")
+
+
+def _values_double(col, ids):
+    vals = col.dict_values()
+    if col.data_type == "STRING":
+        return np.array([float(v) for v in vals], dtype=np.float64)[ids]
+    return vals.astype(np.float64)[ids]
+
+
+def _seq_sum(x):
+    """Sequential double accumulation (`SumAggregationFunction.java:64-72`): cumsum is left-to-right."""
+    if x.shape[0] == 0:
+        return 0.0
+    return float(np.cumsum(x)[-1])
+
+
+def aggregate_segment(segment, query, mask):
+    """`AggregationOperator.getNextBlock` (PC/operator/query/AggregationOperator.java:56-82) +
+    `DefaultAggregationExecutor.aggregate` (:56-68): one intermediate result per function.
+
+    COUNT → int; SUM/MIN/MAX → float; AVG → (sum, count); DISTINCTCOUNTHLL → HyperLogLog.
+    """
+    docs = np.nonzero(mask)[0]
+    out = []
+    for agg in query["aggregations"]:
+        f = agg["function"].upper()
+        if f == "COUNT":
+            out.append(int(docs.shape[0]))
+            continue
+        col = segment.column(agg["column"])
+        ids = dict_ids(col)[docs]
+        if f == "SUM":
+            out.append(_seq_sum(_values_double(col, ids)))
+        elif f == "MIN":
+            v = _values_double(col, ids)
+            out.append(float(v.min()) if v.shape[0] else math.inf)  # MinAggregationFunction.java:32
+        elif f == "MAX":
+            v = _values_double(col, ids)
+            out.append(float(v.max()) if v.shape[0] else -math.inf)  # MaxAggregationFunction.java:32
+        elif f == "AVG":
+            out.append((_seq_sum(_values_double(col, ids)), int(ids.shape[0])))  # AvgPair
+        elif f == "DISTINCTCOUNTHLL":
+            h = HyperLogLog()
+            h.offer_hashes(_value_hashes(col)[ids])
+            out.append(h)
+        else:
+            raise NotImplementedError(f)
+    return out
+
+
+def _value_hashes(col):
+    """MurmurHash of every dictionary value, indexed by dictId (HLL hashes the value, not the dictId)."""
+    vals = col.dict_values()
+    if col.data_type in ("INT", "LONG"):
+        return hash_long_np(vals.astype(np.int64))
+    return np.array([hash_value(v, col.data_type) & 0xFFFFFFFF for v in vals], dtype=np.uint32)
+
+
+def merge_agg(f, a, b):
+    """`AggregationFunction.merge` per function, as used by `CombineService.mergeTwoBlocks` (:48-90)."""
+    f = f.upper()
+    if f == "COUNT":
+        return a + b
+    if f == "SUM":
+        return a + b
+    if f == "MIN":
+        return min(a, b)
+    if f == "MAX":
+        return max(a, b)
+    if f == "AVG":
+        return (a[0] + b[0], a[1] + b[1])
+    if f == "DISTINCTCOUNTHLL":
+        h = HyperLogLog()
+        h.add_all(a)
+        h.add_all(b)
+        return h
+    raise NotImplementedError(f)
+
+
+def final_result(f, v):
+    """`extractFinalResult`: AVG = sum/count or -inf when count==0 (AvgAggregationFunction.java:35,222-230)."""
+    f = f.upper()
+    if f == "AVG":
+        s, c = v
+        return s / c if c else -math.inf
+    if f == "DISTINCTCOUNTHLL":
+        return v.cardinality()
+    return v
+
+
+def format_result(f, v):
+    """Broker-side string form of a final result (KAT strings such as "129268741751388.00000")."""
+    v = final_result(f, v)
+    if f.upper() in ("COUNT", "DISTINCTCOUNTHLL"):
+        return str(int(v))
+    return "%.5f" % v
+
+
+# ----------------------------------------------------------------------------- group-by
+def group_by_segment(segment, query, mask, num_groups_limit=100000):
+    """`AggregationGroupByOperator.getNextBlock` (:64-94) with `DictionaryBasedGroupKeyGenerator` (:63-437).
+
+    Raw key = fold over columns j = n-1..0 of key * card_j + dictId_j (`:200-209`), i.e. column 0 is the least
+    significant digit. Holders: ARRAY if the cardinality product <= 10,000, else INT_MAP / LONG_MAP /
+    ARRAY_MAP whose group ids are assigned at first appearance and capped at `num.groups.limit` (groups past
+    the cap get INVALID_ID and are silently dropped, `:293-302`). The ARRAY holder has no cap other than
+    min(cardinality product, limit) which the product never exceeds when it is <= 10,000.
+
+    Returns {string_key: [intermediate result per function]}.
+    """
+    gcols = [segment.column(c) for c in query["group_by"]["columns"]]
+    docs = np.nonzero(mask)[0]
+    cards = [c.cardinality for c in gcols]
+    raw = np.zeros(docs.shape[0], dtype=object if _prod(cards) > 2 ** 62 else np.int64)
+    for j in range(len(gcols) - 1, -1, -1):
+        raw = raw * cards[j] + dict_ids(gcols[j])[docs]
+    product = _prod(cards)
+    if product <= 10000:
+        keep = np.ones(docs.shape[0], dtype=bool)
+    else:
+        upper = min(product, num_groups_limit) if product <= INT_MAX else num_groups_limit
+        # first-appearance order of raw keys among the filtered docs
+        _, first = np.unique(raw, return_index=True)
+        first_sorted = np.sort(first)
+        admitted = set(raw[first_sorted[:upper]].tolist())
+        keep = np.fromiter((k in admitted for k in raw.tolist()), dtype=bool, count=raw.shape[0])
+    docs = docs[keep]
+    raw = raw[keep]
+    result = {}
+    if docs.shape[0] == 0:
+        return result
+    uniq, inv = np.unique(raw, return_inverse=True)
+    order = np.argsort(inv, kind="stable")
+    bounds = np.searchsorted(inv[order], np.arange(uniq.shape[0] + 1))
+    per_fn = []
+    for agg in query["aggregations"]:
+        f = agg["function"].upper()
+        if f == "COUNT":
+            per_fn.append(("COUNT", None, None))
+            continue
+        col = segment.column(agg["column"])
+        ids = dict_ids(col)[docs]
+        per_fn.append((f, col, ids))
+    dvals = [[c.dict_values()[i] for i in range(c.cardinality)] for c in gcols]
+    for g in range(uniq.shape[0]):
+        sel = order[bounds[g]:bounds[g + 1]]  # doc order preserved (stable)
+        key = int(uniq[g])
+        parts = []
+        for j, c in enumerate(gcols):
+            parts.append(_string_value(c, dvals[j][key % cards[j]]))
+            key //= cards[j]
+        skey = "\t".join(parts)
+        vals = []
+        for f, col, ids in per_fn:
+            if f == "COUNT":
+                vals.append(int(sel.shape[0]))
+                continue
+            gi = ids[sel]
+            if f == "SUM":
+                vals.append(_seq_sum(_values_double(col, gi)))
+            elif f == "MIN":
+                vals.append(float(_values_double(col, gi).min()))
+            elif f == "MAX":
+                vals.append(float(_values_double(col, gi).max()))
+            elif f == "AVG":
+                vals.append((_seq_sum(_values_double(col, gi)), int(gi.shape[0])))
+            elif f == "DISTINCTCOUNTHLL":
+                h = HyperLogLog()
+                h.offer_hashes(_value_hashes(col)[gi])
+                vals.append(h)
+        result[skey] = vals
+    return result
+
+
+def _prod(xs):
+    p = 1
+    for x in xs:
+        p *= int(x)
+    return p
+
+
+def _string_value(col, v):
+    """`Dictionary.getStringValue`: Integer/Long/Float/Double.toString or the unpadded string."""
+    if col.data_type in ("INT", "LONG"):
+        return str(int(v))
+    if col.data_type in ("FLOAT", "DOUBLE"):
+        return _java_double_str(float(v))
+    return v
+
+
+def _java_double_str(x):
+    r = repr(float(x))
+    if r.endswith(".0"):
+        return r
+    return r
+
+
+def combine_group_by(query, per_segment, num_groups_limit=100000):
+    """`CombineGroupByOperator.getNextBlock` (PC/operator/CombineGroupByOperator.java:104-228): merge by string key.
+
+    New groups are admitted while the merged map holds < 2 * limit groups (`:61,147`). The reference merges
+    segments concurrently, so which groups pass that cap is nondeterministic; the oracle merges in segment order.
+    """
+    fns = [a["function"].upper() for a in query["aggregations"]]
+    inter_limit = 2 * num_groups_limit
+    merged = {}
+    for seg in per_segment:
+        for k, vals in seg.items():
+            if k in merged:
+                merged[k] = [merge_agg(f, a, b) for f, a, b in zip(fns, merged[k], vals)]
+            elif len(merged) < inter_limit:
+                merged[k] = [_copy(f, v) for f, v in zip(fns, vals)]
+    return merged
+
+
+def _copy(f, v):
+    if f == "DISTINCTCOUNTHLL":
+        h = HyperLogLog()
+        h.add_all(v)
+        return h
+    return v
+
+
+def top_groups(query, merged, fn_index, top_n=None):
+    """Broker top-N for one function (`BrokerReduceService` / `AggregationGroupByTrimmingService.java:160-176`):
+    MIN ascending, everything else descending, ties broken arbitrarily. Returns [(key, final_value)]."""
+    f = query["aggregations"][fn_index]["function"].upper()
+    if top_n is None:
+        top_n = query["group_by"].get("top_n", 10)
+    items = [(k, final_result(f, v[fn_index])) for k, v in merged.items()]
+    items.sort(key=lambda kv: kv[1], reverse=(f != "MIN"))
+    return items[:top_n]
+
+
+# ----------------------------------------------------------------------------- server + broker
+def execute_segment(segment, query, num_groups_limit=100000):
+    """Per-segment plan (`InstancePlanMakerImplV2.makeInnerSegmentPlan`, :97-116): filter, then aggregate or group-by.
+    Returns (intermediate result, num_docs_scanned)."""
+    mask = filter_mask(segment, query.get("filter"))
+    scanned = int(mask.sum())
+    if query.get("group_by"):
+        return group_by_segment(segment, query, mask, num_groups_limit), scanned
+    return aggregate_segment(segment, query, mask), scanned
+
+
+def execute_server(segments, query, num_groups_limit=100000):
+    """Server-side combine over segments (`CombineOperator` / `CombineGroupByOperator`)."""
+    results = [execute_segment(s, query, num_groups_limit) for s in segments]
+    scanned = sum(r[1] for r in results)
+    fns = [a["function"].upper() for a in query["aggregations"]]
+    if query.get("group_by"):
+        return combine_group_by(query, [r[0] for r in results], num_groups_limit), scanned
+    acc = None
+    for r, _ in results:
+        acc = list(r) if acc is None else [merge_agg(f, a, b) for f, a, b in zip(fns, acc, r)]
+    return acc, scanned
+
+
+def broker_results(query, server_results):
+    """Broker reduce of several server responses; returns the KAT strings (aggregation value or top-group value)."""
+    fns = [a["function"].upper() for a in query["aggregations"]]
+    if query.get("group_by"):
+        merged = {}
+        for r in server_results:
+            for k, vals in r.items():
+                merged[k] = [merge_agg(f, a, b) for f, a, b in zip(fns, merged[k], vals)] if k in merged else \
+                    [_copy(f, v) for f, v in zip(fns, vals)]
+        out = []
+        for i, f in enumerate(fns):
+            top = top_groups(query, merged, i)
+            out.append(format_result(f, _unfinal(f, top[0][1])) if top else None)
+        return out
+    acc = None
+    for r in server_results:
+        acc = list(r) if acc is None else [merge_agg(f, a, b) for f, a, b in zip(fns, acc, r)]
+    return [format_result(f, v) for f, v in zip(fns, acc)]
+
+
+def _unfinal(f, v):
+    # top_groups already finalised the value; format_result finalises again, so wrap it back
+    if f == "AVG":
+        return (v, 1)
+    if f == "DISTINCTCOUNTHLL":
+        class _F:
+            def cardinality(self_inner):
+                return v
+        return _F()
+    return v

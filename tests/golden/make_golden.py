@@ -1,0 +1,71 @@
+"""Regenerates the committed golden fixtures from the reference's own test data.
+
+Run in the build container (needs /root/reference, read-only):  python tests/golden/make_golden.py
+
+Writes (all data, no reference source text):
+  test_data_sv.npz    the 11 columns BaseSingleValueQueriesTest builds its segment from
+                      (pinot-core/src/test/resources/data/test_data-sv.avro, 30000 rows;
+                       column list: PT/queries/BaseSingleValueQueriesTest.java:47-60,93-101)
+  simple_data.npz     dim0, dim1, met of pinot-core/src/test/resources/data/simpleData200001.avro
+                      (PT/query/executor/QueryExecutorTest.java:59-173)
+  padding_null.json   byte contents of the Java-written v1 segment paddingNull.tar.gz (dictionaries and
+                      fixed-bit forward indexes, with metadata cardinality/bits) — a byte-level format fixture
+The known answers themselves are transcribed (with file:line) in reference_kats.json.
+"""
+import io
+import json
+import os
+import sys
+import tarfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+import avro  # noqa: E402
+
+REF = "/root/reference/pinot-core/src/test/resources/data"
+SV_COLUMNS = [("column1", "INT"), ("column3", "INT"), ("column5", "STRING"), ("column6", "INT"),
+              ("column7", "INT"), ("column9", "INT"), ("column11", "STRING"), ("column12", "STRING"),
+              ("column17", "INT"), ("column18", "INT"), ("daysSinceEpoch", "INT")]
+
+
+def main():
+    names, cols = avro.read_avro(os.path.join(REF, "test_data-sv.avro"))
+    out = {}
+    for n, t in SV_COLUMNS:
+        v = cols[n]
+        assert all(x is not None for x in v), n
+        out[n] = np.array(v, dtype=np.int32) if t == "INT" else np.array(v, dtype="U")
+    np.savez_compressed(os.path.join(HERE, "test_data_sv.npz"), **out)
+
+    names, cols = avro.read_avro(os.path.join(REF, "simpleData200001.avro"))
+    np.savez_compressed(os.path.join(HERE, "simple_data.npz"),
+                        **{n: np.array(cols[n], dtype=np.int32) for n in ("dim0", "dim1", "met")})
+
+    fx = {}
+    with tarfile.open(os.path.join(REF, "paddingNull.tar.gz")) as tf:
+        files = {os.path.basename(m.name): tf.extractfile(m).read() for m in tf.getmembers() if m.isfile()}
+    meta = {}
+    for line in files["metadata.properties"].decode().splitlines():
+        if "=" in line:
+            k, v = line.split("=", 1)
+            meta[k.strip()] = v.strip()
+    for col in ("age", "name", "percent", "outgoingName1"):
+        fx[col] = {
+            "data_type": meta["column.%s.dataType" % col],
+            "cardinality": int(meta["column.%s.cardinality" % col]),
+            "bits": int(meta["column.%s.bitsPerElement" % col]),
+            "string_width": int(meta["column.%s.lengthOfEachEntry" % col]),
+            "num_docs": int(meta["segment.total.raw.docs"]),
+            "dict_hex": files[col + ".dict"].hex(),
+            "fwd_hex": files[col + ".sv.unsorted.fwd"].hex(),
+        }
+    with open(os.path.join(HERE, "padding_null.json"), "w") as f:
+        json.dump(fx, f, indent=1, sort_keys=True)
+    print("golden fixtures written to", HERE)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,45 @@
+"""The C-ABI library loads on a machine without a GPU and exports every symbol include/pinot_gpu.h declares."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from pinot_amd import _lib
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared_functions():
+    with open(os.path.join(REPO, "include", "pinot_gpu.h")) as f:
+        src = f.read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(pinot_(?:gpu|groupby)_[a-z_]+)\s*\(", src)))
+
+
+def test_library_exports_header_symbols():
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.fail("libpinot_gpu.so is not built: run __graft_entry__.build() or make -C incubator-pinot_amd")
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    declared = _declared_functions()
+    assert len(declared) >= 20
+    missing = [s for s in declared if not hasattr(lib, s)]
+    assert not missing, missing
+    assert sorted(_lib.EXPORTED_SYMBOLS) == declared
+
+
+def test_abi_version_and_error_path_without_gpu():
+    lib = _lib.load()
+    assert lib.pinot_gpu_abi_version() == 1
+    if lib.pinot_gpu_device_count() == 0:
+        ptr = ctypes.c_void_p()
+        st = lib.pinot_gpu_engine_create(0, None, ctypes.byref(ptr))
+        assert st != 0  # no device: a status, never an abort
+        assert lib.pinot_gpu_last_error()
+
+
+def test_struct_sizes_match_header():
+    # layout sanity: sizes that a JNI/ctypes binding depends on
+    assert ctypes.sizeof(_lib.AggResult) == 8 + 8 + 8 + 4 + 4 + 8 + 256
+    assert ctypes.sizeof(_lib.ExecStats) == 6 * 8
+    assert ctypes.sizeof(_lib.FilterNode) == 4 + 4 + 8 + 4 + 4 + 8

@@ -28,9 +28,10 @@ namespace {
 
 struct Arena {
   std::vector<uint8_t> bytes;
-  size_t add(const void *p, size_t n) {
+  // Copies n bytes and reserves `pad` zero bytes after them (kernels may read a little past the end).
+  size_t add(const void *p, size_t n, size_t pad = 16) {
     size_t off = (bytes.size() + 15) & ~size_t(15);
-    bytes.resize(off + n);
+    bytes.resize(off + n + pad, 0);
     if (n) memcpy(bytes.data() + off, p, n);
     return off;
   }
@@ -69,7 +70,7 @@ class Compiler {
     if (root.type == FilterNode::MATCH_ALL) { sp_.match_all = true; return; }
     emit(root);
     sp_.prog.n_cols = (int)colslot_.size();
-    sp_.lut_off = ar_.add(luts_.data(), luts_.size() * 4 + 16);
+    sp_.lut_off = ar_.add(luts_.data(), luts_.size() * 4);
   }
 
  private:
@@ -153,7 +154,7 @@ class Compiler {
     il.kind = kind;
     il.col = col;
     il.n = kind == 0 ? (int)data.size() / 2 : (int)data.size();
-    il.off = ar_.add(data.data(), data.size() * 4 + 8);
+    il.off = ar_.add(data.data(), data.size() * 4);
     il.exclusive = excl;
     sp_.idx.push_back(il);
     push(FilterInstr{OP_LEAF_BITSET, 0, il.slot, 0, 0});

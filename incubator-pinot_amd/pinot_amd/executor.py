@@ -35,7 +35,9 @@ class HyperLogLog:
     """Merged stream-lib HyperLogLog(log2m=8) registers as the device produced them."""
 
     def __init__(self, registers, cardinality):
-        self.registers = np.asarray(registers, dtype=np.uint8)
+        if isinstance(registers, (bytes, bytearray)):
+            registers = np.frombuffer(bytes(registers), dtype=np.uint8)
+        self.registers = np.array(registers, dtype=np.uint8)
         self._card = int(cardinality)
 
     def cardinality(self):

@@ -404,7 +404,7 @@ def format_result(f, v):
 
 
 # ----------------------------------------------------------------------------- group-by
-def group_by_segment(segment, query, mask, num_groups_limit=100000):
+def group_by_segment(segment, query, mask, num_groups_limit=100000, array_threshold=10000):
     """`AggregationGroupByOperator.getNextBlock` (:64-94) with `DictionaryBasedGroupKeyGenerator` (:63-437).
 
     Raw key = fold over columns j = n-1..0 of key * card_j + dictId_j (`:200-209`), i.e. column 0 is the least
@@ -422,7 +422,7 @@ def group_by_segment(segment, query, mask, num_groups_limit=100000):
     for j in range(len(gcols) - 1, -1, -1):
         raw = raw * cards[j] + dict_ids(gcols[j])[docs]
     product = _prod(cards)
-    if product <= 10000:
+    if product <= array_threshold:
         keep = np.ones(docs.shape[0], dtype=bool)
     else:
         upper = min(product, num_groups_limit) if product <= INT_MAX else num_groups_limit

@@ -279,7 +279,8 @@ def test_group_by_num_groups_limit(sv_segment):
     ex = ServerQueryExecutor(e, num_groups_limit=50, max_init_group_holder_capacity=10)
     q = compile_pql("SELECT COUNT(*), SUM(column1) FROM testTable GROUP BY column9, column11")
     got, _ = ex.process_query(q, [g], trim=False)
-    exp = O.group_by_segment(sv_segment, q, O.filter_mask(sv_segment, None), num_groups_limit=50)
+    exp = O.group_by_segment(sv_segment, q, O.filter_mask(sv_segment, None), num_groups_limit=50,
+                             array_threshold=10)
     assert set(got) == set(exp) and len(got) == 50
     for k in exp:
         assert got[k][0] == exp[k][0] and got[k][1] == exp[k][1]

@@ -76,6 +76,7 @@ void parse_config(Engine &e, const char *cfg) {
     if (k == "num.groups.limit") e.num_groups_limit = std::stoi(v);
     else if (k == "filter.force") e.force_filter = v;
     else if (k == "timing") e.timing = v == "1" || v == "true";
+    else if (k == "agg.affine") e.use_affine = v == "1" || v == "true";
     else throw Error(PINOT_ERR_BAD_ARG, "unknown config key " + k);
   }
 }

@@ -30,6 +30,10 @@ struct ColumnData {
   std::vector<int32_t> sorted_start, sorted_end;  // sorted columns
   std::vector<int32_t> inv_dir;        // per dictId [dir[i], dir[i+1]) into containers
   std::vector<uint64_t> inv_bytes;     // serialized roaring bytes per dictId (cost model)
+  // INT/LONG dictionary that is an arithmetic progression value(id) = affine_base + affine_step * id:
+  // SUM/AVG then need Σ dictId only (no dictionary gather)
+  bool affine = false;
+  int64_t affine_base = 0, affine_step = 0;
 
   // device
   DeviceBuffer fwd;             // packed forward index (synthesised for sorted columns)
@@ -104,15 +108,14 @@ struct Engine {
   // configuration
   int num_groups_limit = 100000;
   std::string force_filter;   // "", "scan", "index": planner override for tests
+  bool use_affine = true;     // agg.affine: arithmetic-progression dictionary SUM shortcut
   bool timing = false;
 
   // scratch (grow-only)
-  DeviceBuffer bitsets;       // index-leaf slots + final bitset
-  DeviceBuffer luts;
-  DeviceBuffer small;         // counters, ranges, ids
-  DeviceBuffer partials;
-  DeviceBuffer reduced;
-  DeviceBuffer hll;
+  DeviceBuffer bitsets;       // filter bitset slots (slot 0 = final)
+  DeviceBuffer small;         // per-query arena: ranges, ids, LUTs
+  DeviceBuffer partials;      // per-block partial slots
+  DeviceBuffer reduced;       // per-segment reduced slots + HLL registers
   DeviceBuffer group_scratch;
 
   // timing

@@ -1,18 +1,20 @@
-// Query execution on one GPU: per-segment filter programs, aggregation, group-by, combine.
+// Query execution on one GPU: per-segment filter plans, aggregation, group-by, combine.
 //
 // Restates, for dictionary-encoded single-value columns (PC = pinot-core/src/main/java/org/apache/pinot/core):
+//   FilterPlanNode / FilterOperatorUtils operator choice            PC/plan/FilterPlanNode.java:70-126
 //   AggregationOperator.getNextBlock / DefaultAggregationExecutor   PC/operator/query/AggregationOperator.java:56-82
-//   Count/Sum/Min/Max/Avg/DistinctCountHLL aggregation functions     PC/query/aggregation/function/*
+//   Count/Sum/Min/Max/Avg/DistinctCountHLL aggregation functions     PC/query/aggregation/function/
 //   AggregationGroupByOperator / DefaultGroupByExecutor               PC/operator/query/AggregationGroupByOperator.java:64-94
 //   DictionaryBasedGroupKeyGenerator (raw keys, holder choice, limit) PC/query/aggregation/groupby/DictionaryBasedGroupKeyGenerator.java:79-437
 //   CombineOperator / CombineService.mergeTwoBlocks                   PC/operator/CombineOperator.java:75-196
 //   CombineGroupByOperator                                            PC/operator/CombineGroupByOperator.java:104-228
 //   ExecutionStatistics                                               PC/operator/ExecutionStatistics.java:24-90
 //
-// All segments of a query on this GPU are planned on the host first; every small per-query table
-// (sorted ranges, roaring id lists, IN/NOT_IN membership bitmaps) goes up in ONE host->device copy,
-// then the kernels of all segments run back to back on the engine's stream and the combined result
-// comes back in one device->host copy.
+// A filter tree becomes a sequence of streaming leaf launches that write / AND / OR into doc bitsets in
+// HBM (slot 0 holds the final set). All segments of a query are planned on the host first; every small
+// per-query table (sorted ranges, roaring id lists, IN/NOT_IN membership bitmaps) goes up in ONE
+// host->device copy, the kernels of all segments run back to back on the engine's stream, and the
+// reduced per-segment results come back in ONE device->host copy.
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -37,21 +39,25 @@ struct Arena {
   }
 };
 
-struct IndexLeaf {
-  int slot;
-  int kind;  // 0 sorted ranges (K2), 1 roaring (K3)
-  int col;
-  size_t off;  // arena offset: ranges (int32 pairs) or ids (int32)
-  int n;
-  int exclusive;
+// One device step of a segment's filter plan.
+struct FilterStep {
+  enum Kind { SCAN, RANGES, ROARING, COMBINE, FILL } kind;
+  int col = -1;
+  int leaf_kind = LEAF_RANGE;
+  uint32_t lo = 0, span = 0;
+  uint64_t lut64 = 0;
+  size_t off = 0;  // arena offset (LUT words / ranges / ids)
+  int n = 0;
+  int negate = 0;  // SCAN: negate; ROARING: exclusive; FILL: value
+  int mode = CM_WRITE;
+  int dst = 0, src = 0;
 };
 
 struct SegPlan {
   SegmentData *seg = nullptr;
   bool empty = false, match_all = false;
-  FilterProgram prog{};
-  size_t lut_off = 0;
-  std::vector<IndexLeaf> idx;
+  std::vector<FilterStep> steps;
+  int slots = 1;
   int64_t scan_leaves = 0;
 };
 
@@ -60,6 +66,8 @@ std::string agg_column(const pinot_agg_spec &a) {
   return a.column;
 }
 
+// FilterNode tree -> step list. eval(node, dst, mode): leaves write/AND/OR straight into dst; a composite
+// child of a different operator is evaluated into a fresh slot and combined.
 class Compiler {
  public:
   Compiler(Engine &e, SegPlan &sp, Arena &ar) : e_(e), sp_(sp), ar_(ar), seg_(*sp.seg) {}
@@ -68,49 +76,44 @@ class Compiler {
     FilterNode root = plan_filter(seg_, tree);
     if (root.type == FilterNode::EMPTY) { sp_.empty = true; return; }
     if (root.type == FilterNode::MATCH_ALL) { sp_.match_all = true; return; }
-    emit(root);
-    sp_.prog.n_cols = (int)colslot_.size();
-    sp_.lut_off = ar_.add(luts_.data(), luts_.size() * 4);
+    next_slot_ = 1;
+    eval(root, 0, CM_WRITE);
   }
 
  private:
-  int col_slot(int ci) {
-    auto it = colslot_.find(ci);
-    if (it != colslot_.end()) return it->second;
-    int s = (int)colslot_.size();
-    require(s < kMaxProgramColumns, PINOT_ERR_UNSUPPORTED, "filter references too many columns");
-    colslot_[ci] = s;
-    sp_.prog.cols[s] = seg_.cols[ci]->dev();
+  int alloc_slot() {
+    const int s = next_slot_++;
+    sp_.slots = std::max(sp_.slots, next_slot_);
     return s;
   }
-  void push(FilterInstr in) {
-    require(sp_.prog.n_instr < kMaxProgramInstr, PINOT_ERR_UNSUPPORTED, "filter tree too large");
-    sp_.prog.ins[sp_.prog.n_instr++] = in;
-  }
-  void emit(const FilterNode &n) {
-    switch (n.type) {
-      case FilterNode::AND:
-      case FilterNode::OR: {
-        const int op = n.type == FilterNode::AND ? OP_AND : OP_OR;
-        emit(n.children[0]);
-        depth_++;
-        require(depth_ < kMaxStack, PINOT_ERR_UNSUPPORTED, "filter tree too deep");
-        for (size_t i = 1; i < n.children.size(); i++) {
-          emit(n.children[i]);
-          push(FilterInstr{op, 0, 2, 0, 0});
-        }
-        depth_--;
-        return;
-      }
-      default:
-        leaf(n);
+  void eval(const FilterNode &n, int dst, int mode) {
+    if (n.type != FilterNode::AND && n.type != FilterNode::OR) {
+      leaf(n, dst, mode);
+      return;
     }
+    const int op = n.type == FilterNode::AND ? CM_AND : CM_OR;
+    if (mode != CM_WRITE && mode != op) {  // e.g. OR-node into an AND accumulation: build it aside
+      const int t = alloc_slot();
+      eval(n, t, CM_WRITE);
+      FilterStep c{FilterStep::COMBINE};
+      c.dst = dst;
+      c.src = t;
+      c.mode = mode;
+      sp_.steps.push_back(c);
+      next_slot_--;
+      return;
+    }
+    for (size_t i = 0; i < n.children.size(); i++) eval(n.children[i], dst, i == 0 && mode == CM_WRITE ? CM_WRITE : op);
   }
-  void leaf(const FilterNode &n) {
+  void leaf(const FilterNode &n, int dst, int mode) {
     const ColumnData &c = *seg_.cols[n.col];
     const Evaluator &ev = *n.ev;
     const bool force_scan = e_.force_filter == "scan";
     const bool force_index = e_.force_filter == "index";
+    FilterStep st{FilterStep::SCAN};
+    st.col = n.col;
+    st.dst = dst;
+    st.mode = mode;
     if ((n.type == FilterNode::SORTED || c.is_sorted) && !force_scan) {
       // SortedInvertedIndexBasedFilterOperator: runs of matching dictIds -> merged [start, end] doc ranges
       std::vector<int32_t> ranges;
@@ -125,7 +128,10 @@ class Compiler {
         }
         i = j + 1;
       }
-      index_leaf(0, n.col, ranges, 0);
+      st.kind = FilterStep::RANGES;
+      st.n = (int)ranges.size() / 2;
+      st.off = ar_.add(ranges.data(), ranges.size() * 4);
+      sp_.steps.push_back(st);
       return;
     }
     if (n.type == FilterNode::BITMAP && !force_scan) {
@@ -139,30 +145,21 @@ class Compiler {
           payload += c.inv_bytes[i];
         }
       }
-      // cost model: roaring payload + write/read of one bitset vs. streaming the packed column
-      const uint64_t idx_cost = payload + (uint64_t)seg_.num_docs / 4;
+      // cost model: roaring payload + one bitset write vs. streaming the packed column
+      const uint64_t idx_cost = payload + (uint64_t)seg_.num_docs / 8;
       if (force_index || idx_cost < c.fwd_bytes) {
-        index_leaf(1, n.col, ids, excl ? 1 : 0);
+        st.kind = FilterStep::ROARING;
+        st.n = (int)ids.size();
+        st.negate = excl ? 1 : 0;
+        st.off = ar_.add(ids.data(), ids.size() * 4);
+        sp_.steps.push_back(st);
         return;
       }
     }
-    scan_leaf(n.col, ev);
+    scan_leaf(c, ev, st);
   }
-  void index_leaf(int kind, int col, const std::vector<int32_t> &data, int excl) {
-    IndexLeaf il;
-    il.slot = (int)sp_.idx.size();
-    il.kind = kind;
-    il.col = col;
-    il.n = kind == 0 ? (int)data.size() / 2 : (int)data.size();
-    il.off = ar_.add(data.data(), data.size() * 4);
-    il.exclusive = excl;
-    sp_.idx.push_back(il);
-    push(FilterInstr{OP_LEAF_BITSET, 0, il.slot, 0, 0});
-  }
-  void scan_leaf(int col, const Evaluator &ev) {
-    const ColumnData &c = *seg_.cols[col];
+  void scan_leaf(const ColumnData &c, const Evaluator &ev, FilterStep &st) {
     sp_.scan_leaves++;
-    const int slot = col_slot(col);
     auto contiguous = [&](uint8_t want, int32_t &lo, int32_t &hi) {
       int32_t first = -1, last = -1;
       int64_t cnt = 0;
@@ -178,56 +175,53 @@ class Compiler {
       return true;
     };
     int32_t lo, hi;
-    if (contiguous(1, lo, hi)) {
-      push(FilterInstr{OP_LEAF_RANGE, slot, lo, hi, 0});
-    } else if (contiguous(0, lo, hi)) {
-      push(FilterInstr{OP_LEAF_RANGE, slot, lo, hi, 1});
-    } else {
-      const size_t words = (size_t)(c.card + 31) / 32;
-      const int32_t base = (int32_t)luts_.size();
-      luts_.resize(luts_.size() + words + 2, 0u);
+    if (contiguous(1, lo, hi) || contiguous(0, lo, hi)) {
+      st.leaf_kind = LEAF_RANGE;
+      st.negate = ev.matching[lo] ? 0 : 1;
+      st.lo = (uint32_t)lo;
+      st.span = (uint32_t)(hi - lo);
+    } else if (c.card <= 64) {
+      st.leaf_kind = LEAF_LUT64;
       for (int32_t i = 0; i < c.card; i++)
-        if (ev.matching[i]) luts_[base + (i >> 5)] |= 1u << (i & 31);
-      push(FilterInstr{OP_LEAF_LUT, slot, base, 0, 0});
+        if (ev.matching[i]) st.lut64 |= 1ull << i;
+    } else {
+      std::vector<uint32_t> lut((c.card + 31) / 32 + 1, 0u);
+      for (int32_t i = 0; i < c.card; i++)
+        if (ev.matching[i]) lut[i >> 5] |= 1u << (i & 31);
+      st.leaf_kind = LEAF_LUT;
+      st.off = ar_.add(lut.data(), lut.size() * 4);
     }
+    sp_.steps.push_back(st);
   }
 
   Engine &e_;
   SegPlan &sp_;
   Arena &ar_;
   const SegmentData &seg_;
-  std::map<int, int> colslot_;
-  std::vector<uint32_t> luts_;
-  int depth_ = 0;
+  int next_slot_ = 1;
 };
 
-// Device-side arena + bitset scratch for one query.
 struct QueryScratch {
   uint8_t *arena = nullptr;
-  uint64_t *bitsets = nullptr;  // (max_slots + 1) * nwords_max
+  uint64_t *bitsets = nullptr;  // slots * stride words
   int64_t stride = 0;
 };
 
 QueryScratch prepare(Engine &e, std::vector<SegPlan> &plans, Arena &ar) {
   QueryScratch qs;
-  size_t max_slots = 0;
+  int slots = 1;
   int64_t max_words = 1;
   for (auto &p : plans) {
-    max_slots = std::max(max_slots, p.idx.size());
+    slots = std::max(slots, p.slots);
     max_words = std::max<int64_t>(max_words, p.seg->nwords());
   }
   e.small.reserve(std::max<size_t>(ar.bytes.size(), 256));
   if (!ar.bytes.empty())
     PINOT_HIP(hipMemcpyAsync(e.small.get(), ar.bytes.data(), ar.bytes.size(), hipMemcpyHostToDevice, e.stream));
   qs.arena = e.small.get<uint8_t>();
-  qs.stride = max_words;
-  e.bitsets.reserve((max_slots + 1) * max_words * 8);
+  qs.stride = (max_words + 31) / 32 * 32;  // 256-B aligned slots
+  e.bitsets.reserve((size_t)slots * qs.stride * 8);
   qs.bitsets = e.bitsets.get<uint64_t>();
-  for (auto &p : plans) {
-    p.prog.luts = reinterpret_cast<const uint32_t *>(qs.arena + p.lut_off);
-    p.prog.bitsets = qs.bitsets;
-    p.prog.bitset_stride = qs.stride;
-  }
   return qs;
 }
 
@@ -269,29 +263,52 @@ struct Timer {
   }
 };
 
-// Runs the index leaves and the filter scan of one segment. Returns the bitset to aggregate over
-// (nullptr = all docs) and accumulates the matching-doc count into *count_dev.
-const uint64_t *run_filter(Engine &e, SegPlan &p, const QueryScratch &qs, unsigned long long *count_dev,
-                           Timer &t) {
+// Runs the filter steps of one segment. Returns the final bitset (slot 0), or nullptr for MATCH_ALL.
+const uint64_t *run_filter(Engine &e, SegPlan &p, const QueryScratch &qs, Timer &t) {
+  if (p.match_all) return nullptr;
   SegmentData &s = *p.seg;
   const int64_t nwords = s.nwords();
-  for (auto &il : p.idx) {
-    uint64_t *out = qs.bitsets + (int64_t)il.slot * qs.stride;
-    const ColumnData &c = *s.cols[il.col];
-    if (il.kind == 0) {
-      launch_ranges_to_bitset(reinterpret_cast<const int32_t *>(qs.arena + il.off), il.n, nwords, s.num_docs, out,
-                              e.stream);
-    } else {
-      launch_roaring_expand(c.inv_payload.get<uint8_t>(), c.inv_containers.get<RoaringContainer>(),
-                            c.inv_dir_dev.get<int32_t>(), reinterpret_cast<const int32_t *>(qs.arena + il.off), il.n,
-                            il.exclusive, nwords, s.num_docs, out, e.stream);
+  auto slot = [&](int i) { return qs.bitsets + (int64_t)i * qs.stride; };
+  for (const FilterStep &st : p.steps) {
+    uint64_t *dst = slot(st.dst);
+    switch (st.kind) {
+      case FilterStep::SCAN: {
+        const ColumnData &c = *s.cols[st.col];
+        LeafArgs a{};
+        a.fwd = c.fwd.get<uint8_t>();
+        a.nwords = nwords;
+        a.num_docs = s.num_docs;
+        a.negate = st.negate;
+        a.lo = st.lo;
+        a.span = st.span;
+        a.lut64 = st.lut64;
+        a.lut = reinterpret_cast<const uint32_t *>(qs.arena + st.off);
+        a.mode = st.mode;
+        a.dst = dst;
+        t.timed(0, [&] { launch_leaf(c.bits, st.leaf_kind, a, e.stream); });
+        break;
+      }
+      case FilterStep::RANGES:
+        launch_ranges_to_bitset(reinterpret_cast<const int32_t *>(qs.arena + st.off), st.n, nwords, s.num_docs,
+                                st.mode, dst, e.stream);
+        break;
+      case FilterStep::ROARING: {
+        const ColumnData &c = *s.cols[st.col];
+        launch_roaring_expand(c.inv_payload.get<uint8_t>(), c.inv_containers.get<RoaringContainer>(),
+                              c.inv_dir_dev.get<int32_t>(), reinterpret_cast<const int32_t *>(qs.arena + st.off),
+                              st.n, st.negate, nwords, s.num_docs, st.mode, dst, e.stream);
+        break;
+      }
+      case FilterStep::COMBINE:
+        launch_bitset_combine(dst, slot(st.src), nwords, s.num_docs, st.mode, 0, e.stream);
+        break;
+      case FilterStep::FILL:
+        launch_bitset_combine(dst, nullptr, nwords, s.num_docs, st.mode, st.negate, e.stream);
+        break;
     }
     PINOT_HIP(hipGetLastError());
   }
-  uint64_t *final_bits = qs.bitsets + (int64_t)p.idx.size() * qs.stride;
-  t.timed(0, [&] { launch_filter_scan(p.prog, nwords, s.num_docs, final_bits, count_dev, e.stream); });
-  PINOT_HIP(hipGetLastError());
-  return final_bits;
+  return slot(0);
 }
 
 std::vector<SegPlan> plan_all(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q, Arena &ar,
@@ -342,7 +359,6 @@ void exec_filter(Engine &e, SegmentData &s, const FilterTreeInput *tree, uint64_
   const int64_t nwords = s.nwords();
   Timer t(e);
   if (plans[0].empty || plans[0].match_all) {
-    const int64_t c = plans[0].empty ? 0 : s.num_docs;
     if (bitset_out) {
       for (int64_t w = 0; w < nwords; w++) {
         uint64_t v = plans[0].empty ? 0 : ~0ull;
@@ -350,16 +366,23 @@ void exec_filter(Engine &e, SegmentData &s, const FilterTreeInput *tree, uint64_
         bitset_out[w] = v;
       }
     }
-    if (count) *count = c;
+    if (count) *count = plans[0].empty ? 0 : s.num_docs;
     PINOT_HIP(hipStreamSynchronize(e.stream));
     return;
   }
+  const int grid = scan_grid(nwords);
+  e.partials.reserve((size_t)grid * 8);
   e.reduced.reserve(64);
-  auto *cnt = e.reduced.get<unsigned long long>();
-  PINOT_HIP(hipMemsetAsync(cnt, 0, 8, e.stream));
-  const uint64_t *bits = run_filter(e, plans[0], qs, cnt, t);
+  const uint64_t *bits = run_filter(e, plans[0], qs, t);
+  launch_popcount(bits, nwords, s.num_docs, e.partials.get<unsigned long long>(), e.stream);
+  ReduceArgs ra{};
+  ra.in = e.partials.get<unsigned long long>();
+  ra.stride = grid;
+  ra.grid = grid;
+  ra.out = e.reduced.get<unsigned long long>();
+  launch_reduce_slots(ra, 1, e.stream);
   unsigned long long hc = 0;
-  PINOT_HIP(hipMemcpyAsync(&hc, cnt, 8, hipMemcpyDeviceToHost, e.stream));
+  PINOT_HIP(hipMemcpyAsync(&hc, ra.out, 8, hipMemcpyDeviceToHost, e.stream));
   if (bitset_out && nwords)
     PINOT_HIP(hipMemcpyAsync(bitset_out, bits, nwords * 8, hipMemcpyDeviceToHost, e.stream));
   PINOT_HIP(hipStreamSynchronize(e.stream));
@@ -368,94 +391,165 @@ void exec_filter(Engine &e, SegmentData &s, const FilterTreeInput *tree, uint64_
 }
 
 // ------------------------------------------------------------------ aggregation-only
+namespace {
+
+// How one aggregation function is computed on one segment.
+struct AggRoute {
+  enum Kind { COUNT_ONLY, IDSUM, MINMAX, GATHER, HLL } kind;
+  int col = -1;
+  int gather_kind = GA_SUM_I32;
+};
+
+AggRoute route_agg(Engine &e, SegmentData &s, const pinot_agg_spec &spec) {
+  AggRoute r{AggRoute::COUNT_ONLY};
+  const int f = spec.function;
+  if (f == PINOT_AGG_COUNT) return r;
+  ColumnData &c = *s.column(agg_column(spec));
+  r.col = s.by_name[c.name];
+  if (f == PINOT_AGG_DISTINCTCOUNTHLL) {
+    ensure_hll_lut(e, c);
+    r.kind = AggRoute::HLL;
+    return r;
+  }
+  require(c.numeric(), PINOT_ERR_UNSUPPORTED, "numeric aggregation over STRING column " + c.name);
+  if (f == PINOT_AGG_MIN || f == PINOT_AGG_MAX) {
+    r.kind = AggRoute::MINMAX;  // sorted dictionary: min/max value = value of the min/max dictId
+  } else if (c.affine && e.use_affine) {
+    r.kind = AggRoute::IDSUM;   // Σ value = base * count + step * Σ dictId
+  } else {
+    r.kind = AggRoute::GATHER;
+    r.gather_kind = c.data_type == PINOT_INT ? GA_SUM_I32 : c.data_type == PINOT_LONG ? GA_SUM_I64 : GA_SUM_F64;
+  }
+  return r;
+}
+
+}  // namespace
+
 void exec_aggregate(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q, pinot_agg_result *out,
                     pinot_exec_stats *stats) {
   const int na = q.num_aggregations;
   require(na >= 1 && na <= kMaxAggs, PINOT_ERR_UNSUPPORTED, "1..8 aggregation functions per query");
-  Arena ar;
-  std::unique_ptr<FilterTreeInput> tree;
-  std::vector<SegPlan> plans = plan_all(e, segs, q, ar, tree);
-
-  // Aggregation programs per segment
-  std::vector<AggProgram> aprog(plans.size());
-  bool need_kernel = false;
   int n_hll = 0;
   for (int a = 0; a < na; a++) {
     const int f = q.aggregations[a].function;
     require(f >= PINOT_AGG_COUNT && f <= PINOT_AGG_DISTINCTCOUNTHLL, PINOT_ERR_UNSUPPORTED, "aggregation function");
-    if (f != PINOT_AGG_COUNT) need_kernel = true;
     if (f == PINOT_AGG_DISTINCTCOUNTHLL) n_hll++;
   }
-  require(n_hll <= 4, PINOT_ERR_UNSUPPORTED, "at most 4 DISTINCTCOUNTHLL per query");
-  for (size_t si = 0; si < plans.size(); si++) {
-    SegmentData &s = *plans[si].seg;
-    AggProgram &ap = aprog[si];
-    ap = AggProgram{};
-    ap.n_aggs = na;
-    std::map<int, int> slots;
-    for (int a = 0; a < na; a++) {
-      const int f = q.aggregations[a].function;
-      AggSpecDev &sd = ap.aggs[a];
-      sd.kind = AGG_NOP;
-      if (f == PINOT_AGG_COUNT) continue;
-      ColumnData &c = *s.column(agg_column(q.aggregations[a]));
-      int ci = s.by_name[c.name];
-      if (!slots.count(ci)) {
-        int k = (int)slots.size();
-        slots[ci] = k;
-        ap.cols[k] = c.dev();
-      }
-      sd.col = slots[ci];
-      sd.dict = c.dict_dev.get();
-      if (f == PINOT_AGG_DISTINCTCOUNTHLL) {
-        ensure_hll_lut(e, c);
-        sd.kind = AGG_HLL;
-        sd.hll_lut = c.hll_lut.get<uint16_t>();
-        continue;
-      }
-      require(c.numeric(), PINOT_ERR_UNSUPPORTED, "numeric aggregation over STRING column " + c.name);
-      if (f == PINOT_AGG_MIN || f == PINOT_AGG_MAX) {
-        sd.kind = AGG_MINMAX;  // sorted dictionary: min/max value = value of min/max dictId
-      } else {
-        sd.kind = c.data_type == PINOT_INT ? AGG_SUM_I32 : c.data_type == PINOT_LONG ? AGG_SUM_I64 : AGG_SUM_F64;
-      }
-    }
-    ap.n_cols = (int)slots.size();
-  }
-
+  require(n_hll <= kMaxHll, PINOT_ERR_UNSUPPORTED, "at most 4 DISTINCTCOUNTHLL per query");
+  Arena ar;
+  std::unique_ptr<FilterTreeInput> tree;
+  std::vector<SegPlan> plans = plan_all(e, segs, q, ar, tree);
   QueryScratch qs = prepare(e, plans, ar);
   const size_t S = plans.size();
   int64_t max_words = 1;
   for (auto &p : plans) max_words = std::max<int64_t>(max_words, p.seg->nwords());
-  const int grid = aggregate_grid(max_words);
-  // reduced layout: [S counters (u64)] [S * na AggPartial] [na * 256 u32 HLL]
-  const size_t off_red = ((S * 8 + 15) / 16) * 16;
-  const size_t off_hll = off_red + S * na * sizeof(AggPartial);
+  const int grid = scan_grid(max_words);
+  // per-segment result slots: [0] count, [1 + a] aggregation a, [na + 1] discarded duplicate counts;
+  // then HLL registers [na][256] u32
+  const int nres = na + 2;
+  const size_t off_hll = ((S * nres * 8 + 255) / 256) * 256;
   const size_t red_bytes = off_hll + (size_t)na * 256 * 4;
   e.reduced.reserve(red_bytes);
-  e.partials.reserve((size_t)grid * na * sizeof(AggPartial));
+  e.partials.reserve((size_t)grid * kMaxSlots * 8);
   uint8_t *red = e.reduced.get<uint8_t>();
-  auto *cnt_dev = reinterpret_cast<unsigned long long *>(red);
-  auto *red_dev = reinterpret_cast<AggPartial *>(red + off_red);
+  auto *res_dev = reinterpret_cast<unsigned long long *>(red);
   auto *hll_dev = reinterpret_cast<uint32_t *>(red + off_hll);
+  auto *part = e.partials.get<unsigned long long>();
+
   PINOT_HIP(hipEventRecord(e.ev_start, e.stream));
   PINOT_HIP(hipMemsetAsync(red, 0, red_bytes, e.stream));
   Timer t(e);
-  std::vector<int64_t> counts(S, 0);
+  std::vector<std::vector<AggRoute>> routes(S);
   for (size_t si = 0; si < S; si++) {
     SegPlan &p = plans[si];
     SegmentData &s = *p.seg;
+    for (int a = 0; a < na; a++) routes[si].push_back(route_agg(e, s, q.aggregations[a]));
     if (p.empty) continue;
-    const uint64_t *bits = nullptr;
-    if (!p.match_all) bits = run_filter(e, p, qs, cnt_dev + si, t);
-    if (need_kernel) {
-      t.timed(1, [&] {
-        launch_aggregate(aprog[si], bits, s.nwords(), s.num_docs, e.partials.get<AggPartial>(), hll_dev, e.stream);
-      });
-      PINOT_HIP(hipGetLastError());
-      launch_reduce_partials(e.partials.get<AggPartial>(), grid, na, red_dev + si * na, e.stream);
+    const uint64_t *bits = run_filter(e, p, qs, t);
+    const int64_t nwords = s.nwords();
+    // partial slot p: part + p * grid ; slot kinds/targets for the reduction
+    ReduceArgs ra{};
+    ra.in = part;
+    ra.stride = grid;
+    ra.grid = grid;
+    ra.out = res_dev + si * nres;
+    int nslots = 0;
+    auto new_slot = [&](int kind, int target) {
+      ra.kinds[nslots] = kind;
+      ra.out_index[nslots] = target;
+      return part + (int64_t)(nslots++) * grid;
+    };
+    bool have_count = false;
+    const int discard = na + 1;
+    // one fold per column over its IDSUM / MINMAX aggregations
+    std::map<int, std::vector<int>> by_col;
+    for (int a = 0; a < na; a++)
+      if (routes[si][a].kind == AggRoute::IDSUM || routes[si][a].kind == AggRoute::MINMAX)
+        by_col[routes[si][a].col].push_back(a);
+    for (auto &kv : by_col) {
+      const ColumnData &c = *s.cols[kv.first];
+      ColAggArgs ca{};
+      ca.fwd = c.fwd.get<uint8_t>();
+      ca.bitset = bits;
+      ca.nwords = nwords;
+      ca.num_docs = s.num_docs;
+      // several aggregations of one kind on one column share the first one's slot (slot_of below)
+      int ops = 0;
+      int a_sum = -1, a_mm = -1;
+      for (int a : kv.second) {
+        if (routes[si][a].kind == AggRoute::IDSUM) {
+          ops |= COLAGG_IDSUM;
+          if (a_sum < 0) a_sum = a;
+        } else {
+          ops |= COLAGG_MINMAX;
+          if (a_mm < 0) a_mm = a;
+        }
+      }
+      ca.out_count = new_slot(SLOT_SUM_U64, have_count ? discard : 0);
+      have_count = true;
+      if (ops & COLAGG_IDSUM) ca.out_idsum = new_slot(SLOT_SUM_U64, 1 + a_sum);
+      if (ops & COLAGG_MINMAX) ca.out_minmax = new_slot(SLOT_MINMAX, 1 + a_mm);
+      t.timed(1, [&] { launch_colagg(c.bits, ops, ca, e.stream); });
       PINOT_HIP(hipGetLastError());
     }
+    // dictionary / LUT gathers
+    GatherArgs ga{};
+    ga.bitset = bits;
+    ga.nwords = nwords;
+    ga.num_docs = s.num_docs;
+    int hslot = 0;
+    for (int a = 0; a < na; a++) {
+      const AggRoute &r = routes[si][a];
+      if (r.kind != AggRoute::GATHER && r.kind != AggRoute::HLL) continue;
+      ColumnData &c = *s.cols[r.col];
+      GatherSpec &g = ga.specs[ga.n++];
+      g.bits = c.bits;
+      g.fwd = c.fwd.get<uint8_t>();
+      if (r.kind == AggRoute::HLL) {
+        g.kind = GA_HLL;
+        g.table = c.hll_lut.get();
+        g.hll_slot = hslot++;
+        g.hll_out = hll_dev + a * 256;
+      } else {
+        g.kind = r.gather_kind;
+        g.table = c.dict_dev.get();
+        g.out = new_slot(r.gather_kind == GA_SUM_I32 ? SLOT_SUM_U64 : SLOT_SUM_F64, 1 + a);
+      }
+    }
+    if (ga.n) {
+      ga.out_count = new_slot(SLOT_SUM_U64, have_count ? discard : 0);
+      have_count = true;
+      t.timed(1, [&] { launch_gather_agg(ga, e.stream); });
+      PINOT_HIP(hipGetLastError());
+    }
+    if (!have_count && bits) {
+      launch_popcount(bits, nwords, s.num_docs, new_slot(SLOT_SUM_U64, 0), e.stream);
+      PINOT_HIP(hipGetLastError());
+    }
+    require(nslots <= kMaxSlots, PINOT_ERR_UNSUPPORTED, "too many aggregation slots");
+    // one fixed-order reduction launch for all slots; the next segment reuses `part` behind it in stream order
+    launch_reduce_slots(ra, nslots, e.stream);
+    PINOT_HIP(hipGetLastError());
   }
   PINOT_HIP(hipEventRecord(e.ev_stop, e.stream));
   std::vector<uint8_t> host(red_bytes);
@@ -465,41 +559,65 @@ void exec_aggregate(Engine &e, const std::vector<SegmentData *> &segs, const pin
   PINOT_HIP(hipEventElapsedTime(&ms, e.ev_start, e.ev_stop));
   t.collect();
 
-  const auto *hcnt = reinterpret_cast<const unsigned long long *>(host.data());
-  const auto *hred = reinterpret_cast<const AggPartial *>(host.data() + off_red);
+  const auto *hres = reinterpret_cast<const unsigned long long *>(host.data());
   const auto *hhll = reinterpret_cast<const uint32_t *>(host.data() + off_hll);
+  std::vector<int64_t> counts(S, 0);
   for (size_t si = 0; si < S; si++) {
     if (plans[si].empty) counts[si] = 0;
-    else if (plans[si].match_all) counts[si] = plans[si].seg->num_docs;
-    else counts[si] = (int64_t)hcnt[si];
+    else if (plans[si].match_all && hres[si * nres] == 0) counts[si] = plans[si].seg->num_docs;
+    else counts[si] = (int64_t)hres[si * nres];
   }
   int64_t total = 0;
   for (auto c : counts) total += c;
+
+  // first aggregation index computing the same (route, column) on segment si (duplicates share one slot)
+  auto slot_of = [&](size_t si, int a) {
+    for (int b = 0; b < a; b++)
+      if (routes[si][b].kind == routes[si][a].kind && routes[si][b].col == routes[si][a].col &&
+          (routes[si][a].kind == AggRoute::IDSUM || routes[si][a].kind == AggRoute::MINMAX))
+        return b;
+    return a;
+  };
 
   // CombineService.mergeTwoBlocks over segments, in segment order
   for (int a = 0; a < na; a++) {
     pinot_agg_result &r = out[a];
     memset(&r, 0, sizeof(r));
     const int f = q.aggregations[a].function;
+    r.count = total;
     switch (f) {
       case PINOT_AGG_COUNT:
-        r.count = total;
         break;
       case PINOT_AGG_SUM:
       case PINOT_AGG_AVG: {
-        const ColumnData &c0 = *plans[0].seg->column(agg_column(q.aggregations[a]));
-        if (c0.data_type == PINOT_INT) {
-          int64_t exact = 0;
-          for (size_t si = 0; si < S; si++) exact += plans[si].empty ? 0 : hred[si * na + a].sum_i64;
-          r.exact_sum = exact;
-          r.has_exact_sum = 1;
-          r.value = (double)exact;
-        } else {
-          double v = 0.0;
-          for (size_t si = 0; si < S; si++) v += plans[si].empty ? 0.0 : hred[si * na + a].sum_f64;
-          r.value = v;
+        bool exact = true;
+        __int128 isum = 0;
+        double dsum = 0.0;
+        for (size_t si = 0; si < S; si++) {
+          if (plans[si].empty || counts[si] == 0) continue;
+          const AggRoute &rt = routes[si][a];
+          const ColumnData &c = *plans[si].seg->cols[rt.col];
+          const unsigned long long raw = hres[si * nres + 1 + slot_of(si, a)];
+          if (rt.kind == AggRoute::IDSUM) {
+            isum += (__int128)c.affine_base * counts[si] + (__int128)c.affine_step * (__int128)raw;
+          } else if (rt.gather_kind == GA_SUM_I32) {
+            isum += (__int128)(long long)raw;
+          } else {
+            double d;
+            memcpy(&d, &raw, 8);
+            dsum += d;
+            exact = false;
+          }
         }
-        r.count = total;
+        if (exact) {
+          r.value = (double)isum;
+          if (isum >= INT64_MIN && isum <= INT64_MAX) {
+            r.exact_sum = (int64_t)isum;
+            r.has_exact_sum = 1;
+          }
+        } else {
+          r.value = dsum + (double)isum;
+        }
         break;
       }
       case PINOT_AGG_MIN:
@@ -508,21 +626,19 @@ void exec_aggregate(Engine &e, const std::vector<SegmentData *> &segs, const pin
         double v = is_min ? INFINITY : -INFINITY;  // Min/MaxAggregationFunction.DEFAULT_VALUE
         for (size_t si = 0; si < S; si++) {
           if (plans[si].empty || counts[si] == 0) continue;
-          const ColumnData &c = *plans[si].seg->column(agg_column(q.aggregations[a]));
-          const AggPartial &pp = hred[si * na + a];
-          const int32_t id = is_min ? pp.min_id : pp.max_id;
-          if (id < 0 || id >= c.card) continue;
-          const double x = c.double_value(id);
+          const ColumnData &c = *plans[si].seg->cols[routes[si][a].col];
+          const unsigned long long raw = hres[si * nres + 1 + slot_of(si, a)];
+          const uint32_t id = is_min ? (uint32_t)raw : (uint32_t)(raw >> 32);
+          if (id >= (uint32_t)c.card) continue;
+          const double x = c.double_value((int32_t)id);
           v = is_min ? std::min(v, x) : std::max(v, x);
         }
         r.value = v;
-        r.count = total;
         break;
       }
       case PINOT_AGG_DISTINCTCOUNTHLL: {
         for (int j = 0; j < 256; j++) r.hll_registers[j] = (uint8_t)hhll[a * 256 + j];
         r.hll_cardinality = hll_cardinality(r.hll_registers);
-        r.count = total;
         break;
       }
     }
@@ -565,16 +681,19 @@ KeySpace build_key_space(const std::vector<SegmentData *> &segs, const pinot_que
       for (int32_t i = 0; i < c0.card; i++) ks.gvalues[j][i] = c0.string_value(i);
     } else {
       // union dictionary in value order
-      std::vector<std::pair<double, std::string>> num;
-      std::set<std::string> strs;
       const bool is_str = c0.data_type == PINOT_STRING;
+      std::set<std::string> strs;
       std::map<std::pair<int64_t, double>, int> nmap;
+      auto nkey = [](const ColumnData &c, int32_t i) {
+        return std::make_pair(c.data_type <= PINOT_LONG ? c.dict_int[i] : (int64_t)0,
+                              c.data_type <= PINOT_LONG ? 0.0 : c.dict_dbl[i]);
+      };
       for (auto *s : segs) {
         const ColumnData &c = *s->column(name);
         require(c.data_type == c0.data_type, PINOT_ERR_BAD_QUERY, "group-by column type differs across segments");
         for (int32_t i = 0; i < c.card; i++) {
           if (is_str) strs.insert(c.dict_str[i]);
-          else nmap[{c.data_type <= PINOT_LONG ? c.dict_int[i] : 0, c.data_type <= PINOT_LONG ? 0.0 : c.dict_dbl[i]}] = 0;
+          else nmap[nkey(c, i)] = 0;
         }
       }
       if (is_str) {
@@ -596,7 +715,7 @@ KeySpace build_key_space(const std::vector<SegmentData *> &segs, const pinot_que
           auto &m = ks.remap[si][j];
           m.resize(c.card);
           for (int32_t i = 0; i < c.card; i++) {
-            int g = nmap[{c.data_type <= PINOT_LONG ? c.dict_int[i] : 0, c.data_type <= PINOT_LONG ? 0.0 : c.dict_dbl[i]}];
+            const int g = nmap[nkey(c, i)];
             m[i] = g;
             ks.gvalues[j][g] = c.string_value(i);
           }
@@ -673,7 +792,7 @@ GroupByProgram make_group_program(Engine &e, SegmentData &s, const pinot_query &
     gp.acc_kind[a] = ga.acc_kind[a];
     gp.acc[a] = accs[a];
     AggSpecDev &sd = gp.aggs[a];
-    sd.kind = AGG_NOP;
+    sd.kind = 0;
     if (ga.acc_kind[a] == 5) continue;
     ColumnData &c = *s.column(agg_column(q.aggregations[a]));
     sd.col = slot(c);
@@ -778,10 +897,29 @@ std::unique_ptr<GroupByResult> finalize_groups(Engine &e, const pinot_query &q, 
   return res;
 }
 
+// Device count of the docs in a bitset (blocking; used only by the group-limit rule).
+int64_t count_docs(Engine &e, const uint64_t *bits, const SegmentData &s) {
+  if (!bits) return s.num_docs;
+  const int grid = scan_grid(s.nwords());
+  DeviceBuffer part((size_t)grid * 8 + 64);
+  auto *p = part.get<unsigned long long>();
+  launch_popcount(bits, s.nwords(), s.num_docs, p, e.stream);
+  ReduceArgs ra{};
+  ra.in = p;
+  ra.stride = grid;
+  ra.grid = grid;
+  ra.out = p + grid;
+  launch_reduce_slots(ra, 1, e.stream);
+  unsigned long long c = 0;
+  PINOT_HIP(hipMemcpyAsync(&c, p + grid, 8, hipMemcpyDeviceToHost, e.stream));
+  PINOT_HIP(hipStreamSynchronize(e.stream));
+  return (int64_t)c;
+}
+
 // Accumulates every segment's group-by into the given device arrays (already initialised).
 void accumulate_groups(Engine &e, std::vector<SegPlan> &plans, const QueryScratch &qs, const pinot_query &q,
                        const GroupAccs &ga, const KeySpace &ks, unsigned long long *counts, void *const *accs,
-                       unsigned long long *cnt_dev, Timer &t, std::vector<int64_t> &seg_counts, bool apply_limit) {
+                       Timer &t, std::vector<int64_t> &seg_counts, bool apply_limit) {
   const size_t S = plans.size();
   std::vector<DeviceBuffer> remaps(S * q.num_group_by);
   for (size_t si = 0; si < S; si++)
@@ -795,57 +933,45 @@ void accumulate_groups(Engine &e, std::vector<SegPlan> &plans, const QueryScratc
   const int64_t limit = q.num_groups_limit > 0 ? q.num_groups_limit : e.num_groups_limit;
   const int64_t array_threshold = q.max_init_group_holder_capacity > 0 ? q.max_init_group_holder_capacity : 10000;
   DeviceBuffer first_doc, admitted;
+  seg_counts.assign(S, 0);
   for (size_t si = 0; si < S; si++) {
     SegPlan &p = plans[si];
     SegmentData &s = *p.seg;
     if (p.empty) continue;
-    const uint64_t *bits = nullptr;
-    if (!p.match_all) bits = run_filter(e, p, qs, cnt_dev + si, t);
+    const uint64_t *bits = run_filter(e, p, qs, t);
+    seg_counts[si] = count_docs(e, bits, s);
     GroupByProgram gp = make_group_program(e, s, q, ga, ks, si, remaps, counts, accs);
     // DictionaryBasedGroupKeyGenerator holder choice on THIS segment's cardinalities (:79-126)
     __int128 product = 1;
     for (int j = 0; j < q.num_group_by; j++) product *= s.column(q.group_by[j])->card;
     int64_t upper = product > array_threshold ? limit : INT64_MAX;
     if (product <= INT32_MAX && product > array_threshold) upper = std::min<int64_t>((int64_t)product, limit);
-    if (apply_limit && product > array_threshold && product > upper) {
-      // the cap can only bind if more than `upper` distinct keys can appear: count matching docs first
-      unsigned long long c = 0;
-      PINOT_HIP(hipMemcpyAsync(&c, cnt_dev + si, 8, hipMemcpyDeviceToHost, e.stream));
+    if (apply_limit && product > array_threshold && product > upper && seg_counts[si] > upper) {
+      // first-appearance order: keep the `upper` keys with the smallest first docId (IntMapBasedHolder :293-302)
+      first_doc.reserve(ks.G * 4);
+      PINOT_HIP(hipMemsetAsync(first_doc.get(), 0xFF, ks.G * 4, e.stream));
+      launch_first_doc(gp, bits, s.nwords(), s.num_docs, first_doc.get<uint32_t>(), e.stream);
+      std::vector<uint32_t> fd(ks.G);
+      PINOT_HIP(hipMemcpyAsync(fd.data(), first_doc.get(), ks.G * 4, hipMemcpyDeviceToHost, e.stream));
       PINOT_HIP(hipStreamSynchronize(e.stream));
-      const int64_t matched = p.match_all ? s.num_docs : (int64_t)c;
-      if (matched > upper) {
-        // first-appearance order: keep the `upper` keys with the smallest first docId (IntMapBasedHolder :293-302)
-        first_doc.reserve(ks.G * 4);
-        PINOT_HIP(hipMemsetAsync(first_doc.get(), 0xFF, ks.G * 4, e.stream));
-        launch_first_doc(gp, bits, s.nwords(), s.num_docs, first_doc.get<uint32_t>(), e.stream);
-        std::vector<uint32_t> fd(ks.G);
-        PINOT_HIP(hipMemcpyAsync(fd.data(), first_doc.get(), ks.G * 4, hipMemcpyDeviceToHost, e.stream));
-        PINOT_HIP(hipStreamSynchronize(e.stream));
-        std::vector<std::pair<uint32_t, int64_t>> present;
-        for (int64_t k = 0; k < ks.G; k++)
-          if (fd[k] != 0xFFFFFFFFu) present.push_back({fd[k], k});
-        if ((int64_t)present.size() > upper) {
-          std::nth_element(present.begin(), present.begin() + upper, present.end());
-          present.resize(upper);
-        }
-        std::vector<uint32_t> bm((ks.G + 31) / 32 + 1, 0);
-        for (auto &pk : present) bm[pk.second >> 5] |= 1u << (pk.second & 31);
-        admitted.alloc(bm.size() * 4);
-        PINOT_HIP(hipMemcpyAsync(admitted.get(), bm.data(), bm.size() * 4, hipMemcpyHostToDevice, e.stream));
-        gp.admitted = admitted.get<uint32_t>();
-        PINOT_HIP(hipStreamSynchronize(e.stream));
+      std::vector<std::pair<uint32_t, int64_t>> present;
+      for (int64_t k = 0; k < ks.G; k++)
+        if (fd[k] != 0xFFFFFFFFu) present.push_back({fd[k], k});
+      if ((int64_t)present.size() > upper) {
+        std::nth_element(present.begin(), present.begin() + upper, present.end());
+        present.resize(upper);
       }
+      std::vector<uint32_t> bm((ks.G + 31) / 32 + 1, 0);
+      for (auto &pk : present) bm[pk.second >> 5] |= 1u << (pk.second & 31);
+      admitted.alloc(bm.size() * 4);
+      PINOT_HIP(hipMemcpyAsync(admitted.get(), bm.data(), bm.size() * 4, hipMemcpyHostToDevice, e.stream));
+      gp.admitted = admitted.get<uint32_t>();
+      PINOT_HIP(hipStreamSynchronize(e.stream));
     }
     t.timed(1, [&] { launch_group_by(gp, bits, s.nwords(), s.num_docs, e.stream); });
     PINOT_HIP(hipGetLastError());
     if (gp.admitted) PINOT_HIP(hipStreamSynchronize(e.stream));
   }
-  std::vector<unsigned long long> hc(S);
-  PINOT_HIP(hipMemcpyAsync(hc.data(), cnt_dev, S * 8, hipMemcpyDeviceToHost, e.stream));
-  PINOT_HIP(hipStreamSynchronize(e.stream));
-  seg_counts.assign(S, 0);
-  for (size_t si = 0; si < S; si++)
-    seg_counts[si] = plans[si].empty ? 0 : plans[si].match_all ? plans[si].seg->num_docs : (int64_t)hc[si];
 }
 
 void init_accs(Engine &e, int64_t G, unsigned long long *counts, const GroupAccs &ga, void *const *accs) {
@@ -875,24 +1001,21 @@ std::unique_ptr<GroupByResult> exec_group_by(Engine &e, const std::vector<Segmen
   require((double)ks.G * per_key < 0.5 * (double)free_b, PINOT_ERR_UNSUPPORTED,
           "dense group-by accumulators do not fit in HBM");
   QueryScratch qs = prepare(e, plans, ar);
-  const size_t S = plans.size();
-  e.group_scratch.reserve(ks.G * per_key + 64 + S * 8);
+  e.group_scratch.reserve(ks.G * per_key + 64);
   uint8_t *base = e.group_scratch.get<uint8_t>();
-  auto *cnt_dev = reinterpret_cast<unsigned long long *>(base);
-  auto *counts = reinterpret_cast<unsigned long long *>(base + ((S * 8 + 63) / 64) * 64);
+  auto *counts = reinterpret_cast<unsigned long long *>(base);
   std::vector<void *> accs(na, nullptr);
-  uint8_t *p = reinterpret_cast<uint8_t *>(counts) + ks.G * 8;
+  uint8_t *p = base + ks.G * 8;
   for (int a = 0; a < na; a++) {
     if (ga.acc_kind[a] == 5) continue;
     accs[a] = p;
     p += ks.G * ga.acc_bytes_per_key[a];
   }
   PINOT_HIP(hipEventRecord(e.ev_start, e.stream));
-  PINOT_HIP(hipMemsetAsync(cnt_dev, 0, S * 8, e.stream));
   init_accs(e, ks.G, counts, ga, accs.data());
   Timer t(e);
   std::vector<int64_t> seg_counts;
-  accumulate_groups(e, plans, qs, q, ga, ks, counts, accs.data(), cnt_dev, t, seg_counts, true);
+  accumulate_groups(e, plans, qs, q, ga, ks, counts, accs.data(), t, seg_counts, true);
   GroupByProgram gp{};
   gp.n_aggs = na;
   gp.counts = counts;
@@ -931,16 +1054,12 @@ void exec_group_by_partial(Engine &e, const std::vector<SegmentData *> &segs, co
   KeySpace ks = build_key_space(segs, q);
   GroupAccs ga = group_acc_kinds(*segs[0], q);
   QueryScratch qs = prepare(e, plans, ar);
-  const size_t S = plans.size();
-  e.reduced.reserve(S * 8 + 16);
-  auto *cnt_dev = e.reduced.get<unsigned long long>();
   PINOT_HIP(hipEventRecord(e.ev_start, e.stream));
-  PINOT_HIP(hipMemsetAsync(cnt_dev, 0, S * 8, e.stream));
   auto *counts = reinterpret_cast<unsigned long long *>(counts_dev);
   init_accs(e, ks.G, counts, ga, accs_dev);
   Timer t(e);
   std::vector<int64_t> seg_counts;
-  accumulate_groups(e, plans, qs, q, ga, ks, counts, accs_dev, cnt_dev, t, seg_counts, false);
+  accumulate_groups(e, plans, qs, q, ga, ks, counts, accs_dev, t, seg_counts, false);
   PINOT_HIP(hipEventRecord(e.ev_stop, e.stream));
   PINOT_HIP(hipStreamSynchronize(e.stream));
   float ms = 0;

@@ -1,4 +1,4 @@
-// Kernel argument blocks and launch entry points (implemented in kernels.hip).
+// Kernel argument blocks and launch entry points (scan.hip, kernels.hip).
 //
 // HBM layout of a segment:
 //   forward index  : the segment's own big-endian MSB-first fixed-bit stream, copied as-is,
@@ -17,6 +17,7 @@ constexpr int kMaxProgramColumns = 16;
 constexpr int kMaxProgramInstr = 48;
 constexpr int kMaxStack = 8;
 constexpr int kMaxAggs = 8;
+constexpr int kMaxHll = 4;
 constexpr int kMaxGroupCols = 8;
 constexpr int kBlock = 256;
 
@@ -26,42 +27,81 @@ struct DevColumn {
   int32_t card;
 };
 
-enum FilterOp : int32_t {
-  OP_LEAF_RANGE = 0,   // dictId in [a, b)            (flags & 1: negate)
-  OP_LEAF_LUT = 1,     // bit dictId of luts[a ..]     (flags & 1: negate)
-  OP_LEAF_BITSET = 2,  // precomputed bitset slot a
-  OP_AND = 3,          // pop a, push AND
-  OP_OR = 4,           // pop a, push OR
-  OP_ALL = 5,          // push all-ones (match all)
-  OP_NONE = 6          // push zero (empty)
+constexpr int kMaxScanGrid = 2048;  // blocks per streaming launch (8 per CU); grid-stride beyond
+
+// ---------------------------------------------------------------- streaming kernels (scan.hip)
+enum LeafKind : int32_t { LEAF_RANGE = 0, LEAF_LUT64 = 1, LEAF_LUT = 2 };
+enum CombineMode : int32_t { CM_WRITE = 0, CM_AND = 1, CM_OR = 2 };
+
+// Filter leaf on one segment column: m = pred(dictId) per doc, optionally negated, then written to /
+// AND-ed into / OR-ed into dst.
+struct LeafArgs {
+  const uint8_t *fwd;
+  int64_t nwords;
+  int32_t num_docs;
+  int32_t negate;
+  uint32_t lo, span;          // LEAF_RANGE: lo <= id < lo + span
+  uint64_t lut64;             // LEAF_LUT64: bit id (cardinality <= 64)
+  const uint32_t *lut;        // LEAF_LUT: bit id of the membership bitmap
+  int32_t mode;               // CombineMode
+  int32_t reserved;
+  uint64_t *dst;
 };
+void launch_leaf(int bits, int kind, const LeafArgs &a, hipStream_t stream);
 
-struct FilterInstr {
-  int32_t op;
-  int32_t col;  // index into FilterProgram::cols
-  int32_t a;
-  int32_t b;
-  int32_t flags;
+enum ColAggOps : int32_t { COLAGG_IDSUM = 1, COLAGG_MINMAX = 2 };
+// Per-column fold over the docs of `bitset` (null = all): per-block partials of COUNT, Σ dictId, min/max dictId.
+struct ColAggArgs {
+  const uint8_t *fwd;
+  const uint64_t *bitset;
+  int64_t nwords;
+  int32_t num_docs;
+  int32_t reserved;
+  unsigned long long *out_count, *out_idsum, *out_minmax;  // [grid] each
 };
+void launch_colagg(int bits, int ops, const ColAggArgs &a, hipStream_t stream);
 
-struct FilterProgram {
-  int32_t n_instr;
-  int32_t n_cols;
-  FilterInstr ins[kMaxProgramInstr];
-  DevColumn cols[kMaxProgramColumns];
-  const uint32_t *luts;     // concatenated dictId-membership bitmaps
-  const uint64_t *bitsets;  // slot s at bitsets + s * bitset_stride
-  int64_t bitset_stride;    // words per slot
+enum GatherKind : int32_t { GA_SUM_I32 = 0, GA_SUM_I64 = 1, GA_SUM_F64 = 2, GA_HLL = 3 };
+struct GatherSpec {
+  int32_t kind;
+  int32_t bits;
+  int32_t hll_slot;
+  int32_t reserved;
+  const uint8_t *fwd;
+  const void *table;            // int32 / int64 / double dictionary or u16 HLL (register << 8 | rank) LUT
+  unsigned long long *out;      // [grid] per-block partials (sums)
+  uint32_t *hll_out;            // 256 registers (atomicMax)
 };
+struct GatherArgs {
+  const uint64_t *bitset;
+  int64_t nwords;
+  int32_t num_docs;
+  int32_t n;
+  unsigned long long *out_count;  // [grid]
+  GatherSpec specs[kMaxAggs];
+};
+void launch_gather_agg(const GatherArgs &a, hipStream_t stream);
+void launch_popcount(const uint64_t *bitset, int64_t nwords, int32_t num_docs, unsigned long long *out,
+                     hipStream_t stream);
 
-// Filter scan: evaluates the program for every 64-doc word, writes the final bitset
-// (may be null) and adds the number of matching docs into *count.
-void launch_filter_scan(const FilterProgram &prog, int64_t nwords, int32_t num_docs, uint64_t *out_bitset,
-                        unsigned long long *count, hipStream_t stream);
+enum SlotKind : int32_t { SLOT_SUM_U64 = 0, SLOT_SUM_F64 = 1, SLOT_MINMAX = 2 };
+constexpr int kMaxSlots = 64;
+// Reduces slot s (grid partials at in + s * stride) into out[out_index[s]], fixed order.
+struct ReduceArgs {
+  const unsigned long long *in;
+  int64_t stride;
+  int32_t grid;
+  int32_t reserved;
+  unsigned long long *out;
+  int32_t kinds[kMaxSlots];
+  int32_t out_index[kMaxSlots];
+};
+void launch_reduce_slots(const ReduceArgs &a, int nslots, hipStream_t stream);
+int scan_grid(int64_t nwords);
 
-// Sorted-index leaf: ranges (inclusive [start, end], sorted, disjoint) -> bitset.
+// Sorted-index leaf: ranges (inclusive [start, end], sorted, disjoint) -> bitset (combine mode as k_leaf).
 void launch_ranges_to_bitset(const int32_t *ranges, int32_t nranges, int64_t nwords, int32_t num_docs,
-                             uint64_t *out, hipStream_t stream);
+                             int32_t mode, uint64_t *out, hipStream_t stream);
 
 // Roaring container descriptor, built on the host at segment registration.
 struct RoaringContainer {
@@ -71,46 +111,20 @@ struct RoaringContainer {
   uint16_t type;            // 0 array, 1 bitmap, 2 run (runs: cardinality = run count)
 };
 
-// Bitmap-inverted-index leaf: OR of the containers of `ids` (exclusive: flip the result).
+// Bitmap-inverted-index leaf: OR of the containers of `ids` (exclusive: flip), combined into out by mode.
 void launch_roaring_expand(const uint8_t *payload, const RoaringContainer *containers, const int32_t *dir,
                            const int32_t *ids, int32_t nids, int exclusive, int64_t nwords, int32_t num_docs,
-                           uint64_t *out, hipStream_t stream);
-
-enum AggKind : int32_t {
-  AGG_SUM_I32 = 0,   // int64 sum of an int32 dictionary
-  AGG_SUM_I64 = 1,   // double sum of an int64 dictionary
-  AGG_SUM_F64 = 2,   // double sum of a double dictionary
-  AGG_MINMAX = 3,    // min / max dictId
-  AGG_HLL = 4,       // registers via per-dictId (register << 8 | rank) LUT
-  AGG_NOP = 5
-};
+                           int32_t mode, uint64_t *out, hipStream_t stream);
+// Bitset algebra: dst = dst (op) src, or a fill (all-ones / zeros) for MATCH_ALL / EMPTY children.
+void launch_bitset_combine(uint64_t *dst, const uint64_t *src, int64_t nwords, int32_t num_docs, int32_t mode,
+                           int32_t fill, hipStream_t stream);
 
 struct AggSpecDev {
   int32_t kind;
-  int32_t col;            // index into AggProgram::cols
+  int32_t col;            // index into GroupByProgram::cols
   const void *dict;       // int32 / int64 / double dictionary
   const uint16_t *hll_lut;
 };
-
-struct AggPartial {          // one per workgroup per aggregation
-  long long sum_i64;
-  double sum_f64;
-  int32_t min_id;
-  int32_t max_id;
-};
-
-struct AggProgram {
-  int32_t n_aggs;
-  int32_t n_cols;
-  AggSpecDev aggs[kMaxAggs];
-  DevColumn cols[kMaxProgramColumns];
-};
-
-// Aggregation over docs selected by bitset (null = all docs). Writes `grid` partials per agg
-// (partials[agg * grid + block]) and HLL registers (hll_regs[agg * 256 + j], atomicMax).
-int launch_aggregate(const AggProgram &prog, const uint64_t *bitset, int64_t nwords, int32_t num_docs,
-                     AggPartial *partials, uint32_t *hll_regs, hipStream_t stream);
-int aggregate_grid(int64_t nwords);
 
 // Group-by over docs selected by bitset (null = all docs).
 struct GroupByProgram {
@@ -133,8 +147,6 @@ void launch_group_by(const GroupByProgram &prog, const uint64_t *bitset, int64_t
 // First matching doc per key (atomicMin), for the num.groups.limit first-appearance rule.
 void launch_first_doc(const GroupByProgram &prog, const uint64_t *bitset, int64_t nwords, int32_t num_docs,
                       uint32_t *first_doc, hipStream_t stream);
-
-void launch_reduce_partials(const AggPartial *in, int grid, int n_aggs, AggPartial *out, hipStream_t stream);
 // Gather counts / 64-bit accumulators (out_acc[a * n + i]) / HLL registers (u8, out_hll[(h * n + i) * 256]).
 void launch_gather_groups(const GroupByProgram &prog, const long long *keys, int64_t n, unsigned long long *out_counts,
                           unsigned long long *out_acc, uint8_t *out_hll, hipStream_t stream);

@@ -53,7 +53,9 @@ static void upload(DeviceBuffer &buf, const void *src, size_t bytes, size_t allo
   if (bytes) PINOT_HIP(hipMemcpyAsync(buf.get(), src, bytes, hipMemcpyHostToDevice, s));
 }
 
-static size_t padded(size_t bytes) { return ((bytes + 255) / 256) * 256 + 512; }
+// Forward-index allocations are padded by one full 64-word staging chunk (64 * 8 * 32 B) plus a DMA
+// piece, so the last chunk's global_load_lds pieces never leave the allocation.
+static size_t padded(size_t bytes) { return ((bytes + 255) / 256) * 256 + 16384 + 1024; }
 
 static void decode_dictionary(ColumnData &c, const pinot_column_desc &d) {
   const uint8_t *p = d.dictionary;
@@ -105,7 +107,21 @@ static void decode_dictionary(ColumnData &c, const pinot_column_desc &d) {
   c.dict_be.assign(d.dictionary, d.dictionary + d.dictionary_len);
 }
 
+// Detects value(id) = base + step * id over the whole (sorted) INT/LONG dictionary.
+static void detect_affine(ColumnData &c) {
+  c.affine = false;
+  if ((c.data_type != PINOT_INT && c.data_type != PINOT_LONG) || c.dict_int.empty()) return;
+  const int64_t base = c.dict_int[0];
+  const int64_t step = c.dict_int.size() > 1 ? c.dict_int[1] - c.dict_int[0] : 0;
+  for (size_t i = 0; i < c.dict_int.size(); i++)
+    if (c.dict_int[i] != base + step * (int64_t)i) return;
+  c.affine = true;
+  c.affine_base = base;
+  c.affine_step = step;
+}
+
 static void upload_dictionary(Engine &e, ColumnData &c) {
+  detect_affine(c);
   const int64_t card = c.card;
   if (c.data_type == PINOT_INT) {
     std::vector<int32_t> v(card);

@@ -40,8 +40,11 @@ def algorithmic_bytes(num_docs):
     return filt, agg, query
 
 
-def cpu_baseline(threads, segs, docs):
-    """Reference-faithful C executor (oracle/faithful.c) on a bounded sample of the same workload."""
+def cpu_baseline(threads, segs, docs, min_seconds=10.0):
+    """Reference-faithful C executor (oracle/faithful.c) on a bounded sample of the same workload.
+
+    The sample (segs x docs rows of the same synthetic table) is queried repeatedly until at least
+    `min_seconds` of CPU work have been timed; the median run is reported."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import faithful
     from concurrent.futures import ThreadPoolExecutor
@@ -60,16 +63,19 @@ def cpu_baseline(threads, segs, docs):
     leaves = [("d2", ("RANGE", 100, 600)), ("d0", ("IN", [1, 3, 5, 7]))]
     faithful.run_and_count_sum(table, leaves, "d8", threads)  # warm-up (page-in)
     times = []
-    for _ in range(3):
+    t_start = time.time()
+    while len(times) < 3 or time.time() - t_start < min_seconds:
         t0 = time.time()
         cnt, sm = faithful.run_and_count_sum(table, leaves, "d8", threads)
         times.append(time.time() - t0)
     times.sort()
+    med = times[len(times) // 2]
     rows = segs * docs
-    return {"value": rows / times[1], "unit": "rows/s", "cores": threads, "kind": "port",
-            "sample": "%d segments x %d docs of the same synthetic table and query (median of 3 runs, %.2fs each; "
-                      "data generated in %.1fs); oracle/faithful.c per-doc iterator executor" %
-                      (segs, docs, times[1], gen_s),
+    return {"value": rows / med, "unit": "rows/s", "cores": threads, "kind": "port",
+            "sample": "%d segments x %d docs of the same synthetic table and query, %d runs over %.1fs of CPU "
+                      "work (median %.3fs; data generated in %.1fs); oracle/faithful.c per-doc iterator executor "
+                      "(reference-faithful C restatement: the Java executor cannot run here, no JVM)" %
+                      (segs, docs, len(times), sum(times), med, gen_s),
             "check": {"count": cnt, "sum": sm}}
 
 
@@ -85,6 +91,8 @@ def main():
     ap.add_argument("--cpu-docs", type=int, default=32_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify", action="store_true", help="check the GPU result against the C oracle (slow)")
+    ap.add_argument("--engine-config", default="", help='engine keys, e.g. "exec.fused=0" (unfused launches)')
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -100,27 +108,23 @@ def main():
         torch.cuda.set_device(0)
 
     from pinot_amd import GpuEngine, ServerQueryExecutor, compile_pql
-    eng = GpuEngine(local_rank if world > 1 else 0)
+    from pinot_amd.combine import combine_aggregation
+    eng = GpuEngine(local_rank if world > 1 else 0, args.engine_config or None)
     segs = []
     t0 = time.time()
     for s in range(args.segments):
-        gidx = rank * args.segments + s  # segment i -> GPU i // segments (round-robin by rank block)
+        gidx = s * world + rank  # global segment i is served by rank i mod world
         segs.append(eng.register_synthetic("fact_%d" % gidx, args.docs, COLUMNS, BASE_SEED + gidx))
     eng.synchronize()
     load_s = time.time() - t0
     ex = ServerQueryExecutor(eng)
     q = compile_pql(QUERY)
 
-    part = torch.zeros(2, dtype=torch.int64, device="cuda")
-
     def step():
         res, st = ex.process_query(q, segs)
         if world > 1:
-            # CombineOperator across GPUs: exact int64 partials (COUNT, integer SUM) all-reduced over RCCL
-            part[0] = res[0]
-            part[1] = int(res[1])
-            dist.all_reduce(part)
-            return int(part[0].item()), int(part[1].item()), st
+            # CombineOperator across GPUs: the per-rank partial aggregates all-reduced over RCCL
+            res = combine_aggregation(q, res, device=torch.device("cuda", local_rank))
         return res[0], int(res[1]), st
 
     for _ in range(args.warmup):
@@ -130,8 +134,11 @@ def main():
     torch.cuda.synchronize()
     eng.synchronize()
     t0 = time.perf_counter()
+    step_ms = []
     for _ in range(args.steps):
-        cnt, sm, st = step()
+        ts = time.perf_counter()
+        cnt, sm, st = step()  # synchronous: results are on the host when it returns
+        step_ms.append((time.perf_counter() - ts) * 1e3)
     eng.synchronize()
     torch.cuda.synchronize()
     if dist:
@@ -158,9 +165,15 @@ def main():
     eng.set_config("timing=0")
     filt_b, agg_b, query_b = algorithmic_bytes(args.docs)
     kern = {}
-    for k, name, b in ((0, "k_leaf", filt_b), (1, "k_colagg", agg_b)):
+    if kt[1][1] == 0:
+        # fused path: ONE k_scan_query launch per query reads the three packed streams of every segment
+        # of this GPU (no bitset traffic): algorithmic bytes per launch = segments x 4.25 B/row x docs
+        names = ((0, "k_scan_query", query_b * args.segments),)
+    else:
+        names = ((0, "k_leaf", filt_b * args.segments), (1, "k_colagg", agg_b * args.segments))
+    for k, name, b in names:
         launches_per_query = max(kt[k][1] // reps, 1)
-        per_launch_b = b * args.segments / launches_per_query
+        per_launch_b = b / launches_per_query
         avg_ms = kt[k][0] / max(kt[k][1], 1)
         kern[name] = {"avg_ms": avg_ms, "launches": kt[k][1], "bytes_per_launch": per_launch_b,
                       "total_ms_per_query": kt[k][0] / reps,
@@ -202,7 +215,7 @@ def main():
         "segment_load_s": load_s,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cb = cpu_baseline(args.cpu_threads, args.cpu_segments, args.cpu_docs)
+        cb = cpu_baseline(args.cpu_threads, args.cpu_segments, args.cpu_docs, args.cpu_seconds)
         out["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample")}
         out["gpu_vs_cpu"] = value / cb["value"]
     if args.verify and rank == 0:

@@ -77,6 +77,9 @@ void parse_config(Engine &e, const char *cfg) {
     else if (k == "filter.force") e.force_filter = v;
     else if (k == "timing") e.timing = v == "1" || v == "true";
     else if (k == "agg.affine") e.use_affine = v == "1" || v == "true";
+    else if (k == "exec.fused") e.use_fused = v == "1" || v == "true";
+    else if (k == "exec.nt") e.use_nt = v == "1" || v == "true";
+    else if (k == "exec.pipe") e.use_pipe = v == "1" || v == "true";
     else throw Error(PINOT_ERR_BAD_ARG, "unknown config key " + k);
   }
 }
@@ -104,6 +107,9 @@ pinot_status pinot_gpu_engine_create(int32_t device, const char *config, pinot_e
     parse_config(*e, config);
     set_device(*e);
     PINOT_HIP(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+    hipDeviceProp_t prop;
+    PINOT_HIP(hipGetDeviceProperties(&prop, device));
+    e->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     PINOT_HIP(hipEventCreate(&e->ev_start));
     PINOT_HIP(hipEventCreate(&e->ev_stop));
     *out = e.release();

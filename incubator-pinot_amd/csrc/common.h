@@ -67,6 +67,32 @@ class DeviceBuffer {
   size_t n_ = 0;
 };
 
+// Grow-only pinned host buffer (async H2D / D2H staging of the per-query tables and results).
+class PinnedBuffer {
+ public:
+  PinnedBuffer() = default;
+  ~PinnedBuffer() { reset(); }
+  PinnedBuffer(const PinnedBuffer &) = delete;
+  PinnedBuffer &operator=(const PinnedBuffer &) = delete;
+  void reserve(size_t bytes) {
+    if (bytes <= n_) return;
+    reset();
+    const size_t want = bytes + bytes / 4;
+    PINOT_HIP(hipHostMalloc(&p_, want, hipHostMallocDefault));
+    n_ = want;
+  }
+  void reset() {
+    if (p_) (void)hipHostFree(p_);
+    p_ = nullptr;
+    n_ = 0;
+  }
+  template <typename T = void> T *get() const { return static_cast<T *>(p_); }
+
+ private:
+  void *p_ = nullptr;
+  size_t n_ = 0;
+};
+
 inline uint32_t load_be32(const uint8_t *p) {
   return (uint32_t(p[0]) << 24) | (uint32_t(p[1]) << 16) | (uint32_t(p[2]) << 8) | uint32_t(p[3]);
 }

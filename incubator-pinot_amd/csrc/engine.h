@@ -109,7 +109,11 @@ struct Engine {
   int num_groups_limit = 100000;
   std::string force_filter;   // "", "scan", "index": planner override for tests
   bool use_affine = true;     // agg.affine: arithmetic-progression dictionary SUM shortcut
+  bool use_fused = true;      // exec.fused: one k_scan_query launch per aggregation query when the shape allows
+  bool use_nt = false;        // exec.nt: non-temporal policy on the streamed column DMA
+  bool use_pipe = false;      // exec.pipe: double-buffered whole-chunk staging (k_scan_query_pipe) when a chunk fits
   bool timing = false;
+  int num_cus = 256;          // multiProcessorCount of the device
 
   // scratch (grow-only)
   DeviceBuffer bitsets;       // filter bitset slots (slot 0 = final)
@@ -117,6 +121,8 @@ struct Engine {
   DeviceBuffer partials;      // per-block partial slots
   DeviceBuffer reduced;       // per-segment reduced slots + HLL registers
   DeviceBuffer group_scratch;
+  PinnedBuffer host_arena;    // staging of the per-query arena (H2D)
+  PinnedBuffer host_result;   // staging of the reduced results (D2H)
 
   // timing
   hipEvent_t ev_start = nullptr, ev_stop = nullptr;

@@ -59,6 +59,10 @@ struct SegPlan {
   std::vector<FilterStep> steps;
   int slots = 1;
   int64_t scan_leaves = 0;
+  // fused mode: scan leaves of the top-level conjunction, evaluated inside k_scan_query; `steps`
+  // (if any) build the rest of the conjunction into slot 0, the kernel's `pre` bitset
+  std::vector<FilterStep> fused_leaves;
+  bool has_pre = false;
 };
 
 std::string agg_column(const pinot_agg_spec &a) {
@@ -78,6 +82,39 @@ class Compiler {
     if (root.type == FilterNode::MATCH_ALL) { sp_.match_all = true; return; }
     next_slot_ = 1;
     eval(root, 0, CM_WRITE);
+  }
+
+  // Fused plan: the scan leaves of the top-level conjunction (AndFilterOperator puts scans last and
+  // applies them only to the candidates of the index children, AndBlockDocIdSet.java:144-227) become
+  // k_scan_query leaves; every other conjunct is built into slot 0 = the kernel's `pre` bitset.
+  void run_fused(const FilterTreeInput *tree) {
+    FilterNode root = plan_filter(seg_, tree);
+    if (root.type == FilterNode::EMPTY) { sp_.empty = true; return; }
+    if (root.type == FilterNode::MATCH_ALL) { sp_.match_all = true; return; }
+    next_slot_ = 1;
+    std::vector<const FilterNode *> conj;
+    if (root.type == FilterNode::AND) {
+      for (const auto &c : root.children) conj.push_back(&c);
+    } else {
+      conj.push_back(&root);
+    }
+    for (const FilterNode *c : conj) {
+      const int mode = sp_.has_pre ? CM_AND : CM_WRITE;
+      if (c->type == FilterNode::AND || c->type == FilterNode::OR) {
+        eval(*c, 0, mode);
+        sp_.has_pre = true;
+        continue;
+      }
+      FilterStep st = leaf_step(*c);
+      if (st.kind == FilterStep::SCAN) {
+        sp_.fused_leaves.push_back(st);
+      } else {
+        st.dst = 0;
+        st.mode = mode;
+        sp_.steps.push_back(st);
+        sp_.has_pre = true;
+      }
+    }
   }
 
  private:
@@ -106,14 +143,19 @@ class Compiler {
     for (size_t i = 0; i < n.children.size(); i++) eval(n.children[i], dst, i == 0 && mode == CM_WRITE ? CM_WRITE : op);
   }
   void leaf(const FilterNode &n, int dst, int mode) {
+    FilterStep st = leaf_step(n);
+    st.dst = dst;
+    st.mode = mode;
+    sp_.steps.push_back(st);
+  }
+  // Physical leaf (getLeafFilterOperator + this engine's cost model): SCAN, RANGES or ROARING.
+  FilterStep leaf_step(const FilterNode &n) {
     const ColumnData &c = *seg_.cols[n.col];
     const Evaluator &ev = *n.ev;
     const bool force_scan = e_.force_filter == "scan";
     const bool force_index = e_.force_filter == "index";
     FilterStep st{FilterStep::SCAN};
     st.col = n.col;
-    st.dst = dst;
-    st.mode = mode;
     if ((n.type == FilterNode::SORTED || c.is_sorted) && !force_scan) {
       // SortedInvertedIndexBasedFilterOperator: runs of matching dictIds -> merged [start, end] doc ranges
       std::vector<int32_t> ranges;
@@ -131,8 +173,7 @@ class Compiler {
       st.kind = FilterStep::RANGES;
       st.n = (int)ranges.size() / 2;
       st.off = ar_.add(ranges.data(), ranges.size() * 4);
-      sp_.steps.push_back(st);
-      return;
+      return st;
     }
     if (n.type == FilterNode::BITMAP && !force_scan) {
       // BitmapBasedFilterOperator: OR the bitmaps of the matching dictIds, or of the non-matching ones and flip
@@ -152,11 +193,11 @@ class Compiler {
         st.n = (int)ids.size();
         st.negate = excl ? 1 : 0;
         st.off = ar_.add(ids.data(), ids.size() * 4);
-        sp_.steps.push_back(st);
-        return;
+        return st;
       }
     }
     scan_leaf(c, ev, st);
+    return st;
   }
   void scan_leaf(const ColumnData &c, const Evaluator &ev, FilterStep &st) {
     sp_.scan_leaves++;
@@ -191,7 +232,6 @@ class Compiler {
       st.leaf_kind = LEAF_LUT;
       st.off = ar_.add(lut.data(), lut.size() * 4);
     }
-    sp_.steps.push_back(st);
   }
 
   Engine &e_;
@@ -202,26 +242,43 @@ class Compiler {
 };
 
 struct QueryScratch {
-  uint8_t *arena = nullptr;
-  uint64_t *bitsets = nullptr;  // slots * stride words
+  uint8_t *arena = nullptr;     // device copy of the query arena
+  uint64_t *bitsets = nullptr;  // regions * slots * stride words
   int64_t stride = 0;
+  int slots = 1;                // bitset slots per region
 };
 
-QueryScratch prepare(Engine &e, std::vector<SegPlan> &plans, Arena &ar) {
+// Device scratch of a query: arena capacity (arena + `extra` bytes the caller appends once device
+// addresses are known) and bitset slots, one region for all segments (run one after the other) or one
+// region per segment (fused path: every `pre` bitset must exist when the single kernel runs).
+QueryScratch prepare_scratch(Engine &e, const std::vector<SegPlan> &plans, const Arena &ar, bool per_segment,
+                             size_t extra = 0) {
   QueryScratch qs;
-  int slots = 1;
   int64_t max_words = 1;
   for (auto &p : plans) {
-    slots = std::max(slots, p.slots);
+    qs.slots = std::max(qs.slots, p.slots);
     max_words = std::max<int64_t>(max_words, p.seg->nwords());
   }
-  e.small.reserve(std::max<size_t>(ar.bytes.size(), 256));
-  if (!ar.bytes.empty())
-    PINOT_HIP(hipMemcpyAsync(e.small.get(), ar.bytes.data(), ar.bytes.size(), hipMemcpyHostToDevice, e.stream));
+  e.small.reserve(std::max<size_t>(ar.bytes.size() + extra + 64, 256));
   qs.arena = e.small.get<uint8_t>();
   qs.stride = (max_words + 31) / 32 * 32;  // 256-B aligned slots
-  e.bitsets.reserve((size_t)slots * qs.stride * 8);
+  const size_t regions = per_segment ? plans.size() : 1;
+  e.bitsets.reserve(regions * (size_t)qs.slots * qs.stride * 8 + 512);  // + a chunk of `pre` words over-read
   qs.bitsets = e.bitsets.get<uint64_t>();
+  return qs;
+}
+
+// One async H2D copy of the arena through pinned staging.
+void upload_arena(Engine &e, const Arena &ar) {
+  if (ar.bytes.empty()) return;
+  e.host_arena.reserve(ar.bytes.size());
+  memcpy(e.host_arena.get(), ar.bytes.data(), ar.bytes.size());
+  PINOT_HIP(hipMemcpyAsync(e.small.get(), e.host_arena.get(), ar.bytes.size(), hipMemcpyHostToDevice, e.stream));
+}
+
+QueryScratch prepare(Engine &e, std::vector<SegPlan> &plans, Arena &ar) {
+  QueryScratch qs = prepare_scratch(e, plans, ar, false);
+  upload_arena(e, ar);
   return qs;
 }
 
@@ -264,11 +321,11 @@ struct Timer {
 };
 
 // Runs the filter steps of one segment. Returns the final bitset (slot 0), or nullptr for MATCH_ALL.
-const uint64_t *run_filter(Engine &e, SegPlan &p, const QueryScratch &qs, Timer &t) {
+const uint64_t *run_filter(Engine &e, SegPlan &p, const QueryScratch &qs, Timer &t, int64_t region = 0) {
   if (p.match_all) return nullptr;
   SegmentData &s = *p.seg;
   const int64_t nwords = s.nwords();
-  auto slot = [&](int i) { return qs.bitsets + (int64_t)i * qs.stride; };
+  auto slot = [&](int i) { return qs.bitsets + (region * qs.slots + i) * qs.stride; };
   for (const FilterStep &st : p.steps) {
     uint64_t *dst = slot(st.dst);
     switch (st.kind) {
@@ -425,6 +482,278 @@ AggRoute route_agg(Engine &e, SegmentData &s, const pinot_agg_spec &spec) {
 
 }  // namespace
 
+namespace {
+
+// Where the device left aggregation a of segment si: index into the reduced u64 results, and for
+// DISTINCTCOUNTHLL the register set (256 u32) holding its merged registers.
+struct AggResults {
+  const unsigned long long *res = nullptr;  // [S][nres]
+  const uint32_t *hll = nullptr;            // [sets][256]
+  int nres = 0;
+  std::vector<std::vector<int>> src;        // [si][a] -> slot within the segment's nres
+  std::vector<int> hll_set;                 // [a]
+};
+
+// CombineService.mergeTwoBlocks over segments (in segment order), per function.
+void merge_aggregates(const pinot_query &q, const std::vector<SegPlan> &plans,
+                      const std::vector<std::vector<AggRoute>> &routes, const std::vector<int64_t> &counts,
+                      const AggResults &R, pinot_agg_result *out) {
+  const size_t S = plans.size();
+  int64_t total = 0;
+  for (auto c : counts) total += c;
+  for (int a = 0; a < q.num_aggregations; a++) {
+    pinot_agg_result &r = out[a];
+    memset(&r, 0, sizeof(r));
+    const int f = q.aggregations[a].function;
+    r.count = total;
+    auto raw_of = [&](size_t si) { return R.res[si * R.nres + R.src[si][a]]; };
+    switch (f) {
+      case PINOT_AGG_COUNT:
+        break;
+      case PINOT_AGG_SUM:
+      case PINOT_AGG_AVG: {
+        bool exact = true;
+        __int128 isum = 0;
+        double dsum = 0.0;
+        for (size_t si = 0; si < S; si++) {
+          if (plans[si].empty || counts[si] == 0) continue;
+          const AggRoute &rt = routes[si][a];
+          const ColumnData &c = *plans[si].seg->cols[rt.col];
+          const unsigned long long raw = raw_of(si);
+          if (rt.kind == AggRoute::IDSUM) {
+            isum += (__int128)c.affine_base * counts[si] + (__int128)c.affine_step * (__int128)raw;
+          } else if (rt.gather_kind == GA_SUM_I32) {
+            isum += (__int128)(long long)raw;
+          } else {
+            double d;
+            memcpy(&d, &raw, 8);
+            dsum += d;
+            exact = false;
+          }
+        }
+        if (exact) {
+          r.value = (double)isum;
+          if (isum >= INT64_MIN && isum <= INT64_MAX) {
+            r.exact_sum = (int64_t)isum;
+            r.has_exact_sum = 1;
+          }
+        } else {
+          r.value = dsum + (double)isum;
+        }
+        break;
+      }
+      case PINOT_AGG_MIN:
+      case PINOT_AGG_MAX: {
+        const bool is_min = f == PINOT_AGG_MIN;
+        double v = is_min ? INFINITY : -INFINITY;  // Min/MaxAggregationFunction.DEFAULT_VALUE
+        for (size_t si = 0; si < S; si++) {
+          if (plans[si].empty || counts[si] == 0) continue;
+          const ColumnData &c = *plans[si].seg->cols[routes[si][a].col];
+          const unsigned long long raw = raw_of(si);
+          const uint32_t id = is_min ? (uint32_t)raw : (uint32_t)(raw >> 32);
+          if (id >= (uint32_t)c.card) continue;
+          const double x = c.double_value((int32_t)id);
+          v = is_min ? std::min(v, x) : std::max(v, x);
+        }
+        r.value = v;
+        break;
+      }
+      case PINOT_AGG_DISTINCTCOUNTHLL: {
+        const uint32_t *regs = R.hll + (size_t)R.hll_set[a] * 256;
+        for (int j = 0; j < 256; j++) r.hll_registers[j] = (uint8_t)regs[j];
+        r.hll_cardinality = hll_cardinality(r.hll_registers);
+        break;
+      }
+    }
+  }
+}
+
+// The query shape k_scan_query evaluates in one launch: every aggregation a fold over a dictId stream
+// (COUNT, Σ dictId of an arithmetic-progression dictionary, Σ int32 dictionary values, min/max dictId,
+// HLL registers via the per-dictId LUT), at most kMaxFusedFolds distinct columns and kMaxHll HLL columns.
+bool fusable(const pinot_query &q, const std::vector<std::vector<AggRoute>> &routes, std::vector<std::string> &fold_cols,
+             std::vector<std::string> &hll_cols) {
+  for (const auto &per_seg : routes)
+    for (const AggRoute &r : per_seg)
+      if (r.kind == AggRoute::GATHER && r.gather_kind != GA_SUM_I32) return false;
+  for (int a = 0; a < q.num_aggregations; a++) {
+    if (q.aggregations[a].function == PINOT_AGG_COUNT) continue;
+    const std::string c = agg_column(q.aggregations[a]);
+    if (std::find(fold_cols.begin(), fold_cols.end(), c) == fold_cols.end()) fold_cols.push_back(c);
+    if (q.aggregations[a].function == PINOT_AGG_DISTINCTCOUNTHLL &&
+        std::find(hll_cols.begin(), hll_cols.end(), c) == hll_cols.end())
+      hll_cols.push_back(c);
+  }
+  return (int)fold_cols.size() <= kMaxFusedFolds && (int)hll_cols.size() <= kMaxHll;
+}
+
+int index_of_name(const std::vector<std::string> &v, const std::string &x) {
+  return (int)(std::find(v.begin(), v.end(), x) - v.begin());
+}
+
+// Fused path: pre bitsets (index leaves / OR subtrees) per segment, then ONE k_scan_query over all
+// segments and ONE fixed-order reduction, ONE device->host copy.
+void aggregate_fused(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q,
+                     const std::vector<std::string> &fold_cols, const std::vector<std::string> &hll_cols,
+                     std::vector<std::vector<AggRoute>> &routes, pinot_agg_result *out, pinot_exec_stats *stats) {
+  const int na = q.num_aggregations;
+  const size_t S = segs.size();
+  Arena ar;
+  std::unique_ptr<FilterTreeInput> tree;
+  if (q.num_filter_nodes > 0) tree = std::make_unique<FilterTreeInput>(decode_filter(q.num_filter_nodes, q.filter));
+  std::vector<SegPlan> plans(S);
+  for (size_t si = 0; si < S; si++) {
+    plans[si].seg = segs[si];
+    Compiler(e, plans[si], ar).run_fused(tree.get());
+  }
+  const int nfolds = (int)fold_cols.size();
+  const int nslots = 1 + 2 * nfolds;
+  // steps: per segment its leaves then its folds
+  int max_bits = 1;
+  size_t nsteps = 0;
+  for (auto &p : plans) {
+    nsteps += p.fused_leaves.size() + nfolds;
+    for (auto &l : p.fused_leaves) max_bits = std::max(max_bits, p.seg->cols[l.col]->bits);
+    for (auto &c : fold_cols) max_bits = std::max(max_bits, p.seg->column(c)->bits);
+  }
+  const size_t tab_bytes = S * sizeof(FusedSegment) + nsteps * sizeof(FusedStep) + 256;  // + alignment/padding of two adds
+  QueryScratch qs = prepare_scratch(e, plans, ar, true, tab_bytes);
+  std::vector<FusedSegment> fsegs(S);
+  std::vector<FusedStep> fsteps;
+  fsteps.reserve(nsteps);
+  for (size_t si = 0; si < S; si++) {
+    SegPlan &p = plans[si];
+    SegmentData &s = *p.seg;
+    FusedSegment &fs = fsegs[si];
+    fs.pre = p.has_pre ? qs.bitsets + (int64_t)si * qs.slots * qs.stride : nullptr;
+    fs.nwords = p.empty ? 0 : s.nwords();
+    fs.num_docs = s.num_docs;
+    fs.first_step = (int32_t)fsteps.size();
+    fs.n_leaves = (int32_t)p.fused_leaves.size();
+    fs.n_folds = nfolds;
+    for (const FilterStep &l : p.fused_leaves) {
+      const ColumnData &c = *s.cols[l.col];
+      FusedStep st{};
+      st.fwd = c.fwd.get<uint8_t>();
+      st.bits = c.bits;
+      st.kind = l.leaf_kind == LEAF_RANGE ? FK_LEAF_RANGE : l.leaf_kind == LEAF_LUT64 ? FK_LEAF_LUT64 : FK_LEAF_LUT;
+      st.negate = l.negate;
+      st.lo = l.lo;
+      st.span = l.span;
+      st.lut64 = l.lut64;
+      st.table = qs.arena + l.off;
+      fsteps.push_back(st);
+    }
+    for (int f = 0; f < nfolds; f++) {
+      ColumnData &c = *s.column(fold_cols[f]);
+      FusedStep st{};
+      st.fwd = c.fwd.get<uint8_t>();
+      st.bits = c.bits;
+      st.kind = FK_FOLD;
+      st.fold = f;
+      for (int a = 0; a < na; a++) {
+        if (q.aggregations[a].function == PINOT_AGG_COUNT || agg_column(q.aggregations[a]) != fold_cols[f]) continue;
+        const AggRoute &r = routes[si][a];
+        if (r.kind == AggRoute::IDSUM) st.ops |= FOLD_IDSUM;
+        else if (r.kind == AggRoute::MINMAX) st.ops |= FOLD_MINMAX;
+        else if (r.kind == AggRoute::GATHER) { st.ops |= FOLD_DICT32; st.table = c.dict_dev.get(); }
+        else if (r.kind == AggRoute::HLL) {
+          st.ops |= FOLD_HLL;
+          st.hll_lut = c.hll_lut.get<uint16_t>();
+          st.hll_set = index_of_name(hll_cols, fold_cols[f]);
+        }
+      }
+      fsteps.push_back(st);
+    }
+  }
+  // pipelined shape: every step of a chunk gets its own 1-KiB-piece region of the wave's LDS slot
+  int slot_bytes = 0;
+  for (size_t si = 0; si < S; si++) {
+    int off = kPipePreBytes;
+    for (int i = 0; i < fsegs[si].n_leaves + fsegs[si].n_folds; i++) {
+      FusedStep &st = fsteps[fsegs[si].first_step + i];
+      st.stage_off = off;
+      off += 1024 * ((st.bits + 1) / 2);
+    }
+    slot_bytes = std::max(slot_bytes, off);
+  }
+  const bool pipelined = e.use_pipe && slot_bytes <= kMaxPipeSlotBytes;
+  const size_t off_segs = ar.add(fsegs.data(), fsegs.size() * sizeof(FusedSegment));
+  const size_t off_steps = ar.add(fsteps.data(), fsteps.size() * sizeof(FusedStep));  // may be empty (COUNT(*))
+  require(ar.bytes.size() <= e.small.size(), PINOT_ERR_DEVICE, "query arena overflow");
+
+  // grid: one resident wave of blocks, split evenly over the segments (equal work per block)
+  const int stage_bytes = pipelined ? slot_bytes : 1024 * ((max_bits + 1) / 2);
+  int64_t max_chunks = 1;
+  for (auto *sg : segs) max_chunks = std::max<int64_t>(max_chunks, (sg->nwords() + 63) / 64);
+  bool gathers = false;
+  for (const FusedStep &st : fsteps)
+    gathers = gathers || st.kind == FK_LEAF_LUT || (st.kind == FK_FOLD && (st.ops & (FOLD_DICT32 | FOLD_HLL)));
+  const int64_t resident = (int64_t)scan_query_blocks_per_cu(stage_bytes, gathers, pipelined) * e.num_cus;
+  int bps = (int)std::max<int64_t>(1, resident / (int64_t)S);
+  bps = (int)std::min<int64_t>(bps, (max_chunks + 3) / 4);
+  const int nres = kMaxFusedSlots;
+  const size_t res_bytes = S * nres * 8;
+  const size_t off_hll = (res_bytes + 255) / 256 * 256;
+  const size_t red_bytes = off_hll + (size_t)kMaxHll * 256 * 4;
+  e.reduced.reserve(red_bytes);
+  e.partials.reserve((size_t)nslots * S * bps * 8);
+  uint8_t *red = e.reduced.get<uint8_t>();
+
+  PINOT_HIP(hipEventRecord(e.ev_start, e.stream));
+  upload_arena(e, ar);
+  if (!hll_cols.empty()) PINOT_HIP(hipMemsetAsync(red + off_hll, 0, (size_t)kMaxHll * 256 * 4, e.stream));
+  Timer t(e);
+  for (size_t si = 0; si < S; si++)
+    if (plans[si].has_pre && !plans[si].empty) run_filter(e, plans[si], qs, t, (int64_t)si);
+  FusedArgs fa{};
+  fa.segs = reinterpret_cast<const FusedSegment *>(qs.arena + off_segs);
+  fa.steps = reinterpret_cast<const FusedStep *>(qs.arena + off_steps);
+  fa.part = e.partials.get<unsigned long long>();
+  fa.hll_out = reinterpret_cast<uint32_t *>(red + off_hll);
+  fa.nsegs = (int32_t)S;
+  fa.bps = bps;
+  fa.nslots = nslots;
+  fa.stage_bytes = stage_bytes;
+  fa.n_hll = (int32_t)hll_cols.size();
+  fa.nt = e.use_nt ? 1 : 0;
+  t.timed(0, [&] { launch_scan_query(fa, gathers, pipelined, e.stream); });
+  PINOT_HIP(hipGetLastError());
+  launch_reduce_fused(fa.part, (int32_t)S, bps, nslots, reinterpret_cast<unsigned long long *>(red), nres, e.stream);
+  PINOT_HIP(hipGetLastError());
+  PINOT_HIP(hipEventRecord(e.ev_stop, e.stream));
+  e.host_result.reserve(red_bytes);
+  uint8_t *host = e.host_result.get<uint8_t>();
+  PINOT_HIP(hipMemcpyAsync(host, red, red_bytes, hipMemcpyDeviceToHost, e.stream));
+  PINOT_HIP(hipStreamSynchronize(e.stream));
+  float ms = 0;
+  PINOT_HIP(hipEventElapsedTime(&ms, e.ev_start, e.ev_stop));
+  t.collect();
+
+  AggResults R;
+  R.res = reinterpret_cast<const unsigned long long *>(host);
+  R.hll = reinterpret_cast<const uint32_t *>(host + off_hll);
+  R.nres = nres;
+  R.src.assign(S, std::vector<int>(na, 0));
+  R.hll_set.assign(na, 0);
+  std::vector<int64_t> counts(S, 0);
+  for (size_t si = 0; si < S; si++) {
+    counts[si] = plans[si].empty ? 0 : (int64_t)R.res[si * nres];
+    for (int a = 0; a < na; a++) {
+      if (q.aggregations[a].function == PINOT_AGG_COUNT) continue;
+      const int f = index_of_name(fold_cols, agg_column(q.aggregations[a]));
+      R.src[si][a] = routes[si][a].kind == AggRoute::MINMAX ? 2 + 2 * f : 1 + 2 * f;
+    }
+  }
+  for (int a = 0; a < na; a++)
+    if (q.aggregations[a].function == PINOT_AGG_DISTINCTCOUNTHLL)
+      R.hll_set[a] = index_of_name(hll_cols, agg_column(q.aggregations[a]));
+  merge_aggregates(q, plans, routes, counts, R, out);
+  fill_stats(q, plans, counts, ms, stats);
+}
+
+}  // namespace
+
 void exec_aggregate(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q, pinot_agg_result *out,
                     pinot_exec_stats *stats) {
   const int na = q.num_aggregations;
@@ -436,11 +765,21 @@ void exec_aggregate(Engine &e, const std::vector<SegmentData *> &segs, const pin
     if (f == PINOT_AGG_DISTINCTCOUNTHLL) n_hll++;
   }
   require(n_hll <= kMaxHll, PINOT_ERR_UNSUPPORTED, "at most 4 DISTINCTCOUNTHLL per query");
+  const size_t S = segs.size();
+  std::vector<std::vector<AggRoute>> routes(S);
+  for (size_t si = 0; si < S; si++)
+    for (int a = 0; a < na; a++) routes[si].push_back(route_agg(e, *segs[si], q.aggregations[a]));
+  if (e.use_fused) {
+    std::vector<std::string> fold_cols, hll_cols;
+    if (fusable(q, routes, fold_cols, hll_cols)) {
+      aggregate_fused(e, segs, q, fold_cols, hll_cols, routes, out, stats);
+      return;
+    }
+  }
   Arena ar;
   std::unique_ptr<FilterTreeInput> tree;
   std::vector<SegPlan> plans = plan_all(e, segs, q, ar, tree);
   QueryScratch qs = prepare(e, plans, ar);
-  const size_t S = plans.size();
   int64_t max_words = 1;
   for (auto &p : plans) max_words = std::max<int64_t>(max_words, p.seg->nwords());
   const int grid = scan_grid(max_words);
@@ -459,11 +798,9 @@ void exec_aggregate(Engine &e, const std::vector<SegmentData *> &segs, const pin
   PINOT_HIP(hipEventRecord(e.ev_start, e.stream));
   PINOT_HIP(hipMemsetAsync(red, 0, red_bytes, e.stream));
   Timer t(e);
-  std::vector<std::vector<AggRoute>> routes(S);
   for (size_t si = 0; si < S; si++) {
     SegPlan &p = plans[si];
     SegmentData &s = *p.seg;
-    for (int a = 0; a < na; a++) routes[si].push_back(route_agg(e, s, q.aggregations[a]));
     if (p.empty) continue;
     const uint64_t *bits = run_filter(e, p, qs, t);
     const int64_t nwords = s.nwords();
@@ -493,7 +830,7 @@ void exec_aggregate(Engine &e, const std::vector<SegmentData *> &segs, const pin
       ca.bitset = bits;
       ca.nwords = nwords;
       ca.num_docs = s.num_docs;
-      // several aggregations of one kind on one column share the first one's slot (slot_of below)
+      // several aggregations of one kind on one column share the first one's slot (src below)
       int ops = 0;
       int a_sum = -1, a_mm = -1;
       for (int a : kv.second) {
@@ -552,97 +889,39 @@ void exec_aggregate(Engine &e, const std::vector<SegmentData *> &segs, const pin
     PINOT_HIP(hipGetLastError());
   }
   PINOT_HIP(hipEventRecord(e.ev_stop, e.stream));
-  std::vector<uint8_t> host(red_bytes);
-  PINOT_HIP(hipMemcpyAsync(host.data(), red, red_bytes, hipMemcpyDeviceToHost, e.stream));
+  e.host_result.reserve(red_bytes);
+  uint8_t *host = e.host_result.get<uint8_t>();
+  PINOT_HIP(hipMemcpyAsync(host, red, red_bytes, hipMemcpyDeviceToHost, e.stream));
   PINOT_HIP(hipStreamSynchronize(e.stream));
   float ms = 0;
   PINOT_HIP(hipEventElapsedTime(&ms, e.ev_start, e.ev_stop));
   t.collect();
 
-  const auto *hres = reinterpret_cast<const unsigned long long *>(host.data());
-  const auto *hhll = reinterpret_cast<const uint32_t *>(host.data() + off_hll);
+  AggResults R;
+  R.res = reinterpret_cast<const unsigned long long *>(host);
+  R.hll = reinterpret_cast<const uint32_t *>(host + off_hll);
+  R.nres = nres;
+  R.src.assign(S, std::vector<int>(na, 0));
+  R.hll_set.resize(na);
   std::vector<int64_t> counts(S, 0);
   for (size_t si = 0; si < S; si++) {
     if (plans[si].empty) counts[si] = 0;
-    else if (plans[si].match_all && hres[si * nres] == 0) counts[si] = plans[si].seg->num_docs;
-    else counts[si] = (int64_t)hres[si * nres];
-  }
-  int64_t total = 0;
-  for (auto c : counts) total += c;
-
-  // first aggregation index computing the same (route, column) on segment si (duplicates share one slot)
-  auto slot_of = [&](size_t si, int a) {
-    for (int b = 0; b < a; b++)
-      if (routes[si][b].kind == routes[si][a].kind && routes[si][b].col == routes[si][a].col &&
-          (routes[si][a].kind == AggRoute::IDSUM || routes[si][a].kind == AggRoute::MINMAX))
-        return b;
-    return a;
-  };
-
-  // CombineService.mergeTwoBlocks over segments, in segment order
-  for (int a = 0; a < na; a++) {
-    pinot_agg_result &r = out[a];
-    memset(&r, 0, sizeof(r));
-    const int f = q.aggregations[a].function;
-    r.count = total;
-    switch (f) {
-      case PINOT_AGG_COUNT:
-        break;
-      case PINOT_AGG_SUM:
-      case PINOT_AGG_AVG: {
-        bool exact = true;
-        __int128 isum = 0;
-        double dsum = 0.0;
-        for (size_t si = 0; si < S; si++) {
-          if (plans[si].empty || counts[si] == 0) continue;
-          const AggRoute &rt = routes[si][a];
-          const ColumnData &c = *plans[si].seg->cols[rt.col];
-          const unsigned long long raw = hres[si * nres + 1 + slot_of(si, a)];
-          if (rt.kind == AggRoute::IDSUM) {
-            isum += (__int128)c.affine_base * counts[si] + (__int128)c.affine_step * (__int128)raw;
-          } else if (rt.gather_kind == GA_SUM_I32) {
-            isum += (__int128)(long long)raw;
-          } else {
-            double d;
-            memcpy(&d, &raw, 8);
-            dsum += d;
-            exact = false;
-          }
+    else if (plans[si].match_all && R.res[si * nres] == 0) counts[si] = plans[si].seg->num_docs;
+    else counts[si] = (int64_t)R.res[si * nres];
+    // duplicates of one (IDSUM | MINMAX, column) share the first aggregation's slot
+    for (int a = 0; a < na; a++) {
+      int src = a;
+      for (int b = 0; b < a; b++)
+        if (routes[si][b].kind == routes[si][a].kind && routes[si][b].col == routes[si][a].col &&
+            (routes[si][a].kind == AggRoute::IDSUM || routes[si][a].kind == AggRoute::MINMAX)) {
+          src = b;
+          break;
         }
-        if (exact) {
-          r.value = (double)isum;
-          if (isum >= INT64_MIN && isum <= INT64_MAX) {
-            r.exact_sum = (int64_t)isum;
-            r.has_exact_sum = 1;
-          }
-        } else {
-          r.value = dsum + (double)isum;
-        }
-        break;
-      }
-      case PINOT_AGG_MIN:
-      case PINOT_AGG_MAX: {
-        const bool is_min = f == PINOT_AGG_MIN;
-        double v = is_min ? INFINITY : -INFINITY;  // Min/MaxAggregationFunction.DEFAULT_VALUE
-        for (size_t si = 0; si < S; si++) {
-          if (plans[si].empty || counts[si] == 0) continue;
-          const ColumnData &c = *plans[si].seg->cols[routes[si][a].col];
-          const unsigned long long raw = hres[si * nres + 1 + slot_of(si, a)];
-          const uint32_t id = is_min ? (uint32_t)raw : (uint32_t)(raw >> 32);
-          if (id >= (uint32_t)c.card) continue;
-          const double x = c.double_value((int32_t)id);
-          v = is_min ? std::min(v, x) : std::max(v, x);
-        }
-        r.value = v;
-        break;
-      }
-      case PINOT_AGG_DISTINCTCOUNTHLL: {
-        for (int j = 0; j < 256; j++) r.hll_registers[j] = (uint8_t)hhll[a * 256 + j];
-        r.hll_cardinality = hll_cardinality(r.hll_registers);
-        break;
-      }
+      R.src[si][a] = 1 + src;
     }
   }
+  for (int a = 0; a < na; a++) R.hll_set[a] = a;
+  merge_aggregates(q, plans, routes, counts, R, out);
   fill_stats(q, plans, counts, ms, stats);
 }
 

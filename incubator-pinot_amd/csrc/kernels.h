@@ -99,6 +99,65 @@ struct ReduceArgs {
 void launch_reduce_slots(const ReduceArgs &a, int nslots, hipStream_t stream);
 int scan_grid(int64_t nwords);
 
+// ---------------------------------------------------------------- fused query kernel (scan.hip)
+// ONE launch evaluates an aggregation-only query over every segment on the GPU: per 4096-doc chunk a
+// wave AND-s the scan leaves of the filter into a 64-bit mask per lane (held in registers, never
+// written to HBM), optionally starting from a `pre` bitset (index leaves / OR subtrees, evaluated by
+// the kernels below), skips the rest of the chunk as soon as the wave's mask is empty, then folds
+// the aggregated columns of the matching docs.
+enum FusedKind : int32_t { FK_LEAF_RANGE = 0, FK_LEAF_LUT64 = 1, FK_LEAF_LUT = 2, FK_FOLD = 3 };
+enum FoldOps : int32_t { FOLD_IDSUM = 1, FOLD_MINMAX = 2, FOLD_DICT32 = 4, FOLD_HLL = 8 };
+constexpr int kMaxFusedFolds = 6;                      // distinct aggregated columns per query
+constexpr int kMaxFusedSlots = 1 + 2 * kMaxFusedFolds; // slot 0 count; fold f: 1 + 2f sum, 2 + 2f min/max
+
+struct FusedStep {           // one (segment, leaf or fold) pair, built on the host per query
+  const uint8_t *fwd;        // packed forward index of the column
+  const void *table;         // FK_LEAF_LUT: u32 membership words; FOLD_DICT32: int32 dictionary
+  const uint16_t *hll_lut;   // FOLD_HLL: (register << 8 | rank) per dictId
+  uint64_t lut64;            // FK_LEAF_LUT64
+  uint32_t lo, span;         // FK_LEAF_RANGE: lo <= id < lo + span
+  int32_t bits, kind, negate, ops;
+  int32_t fold, hll_set;     // FK_FOLD: fold index (slots 1 + 2f, 2 + 2f), HLL register set
+  int32_t stage_off;         // pipelined kernel: byte offset of this step's chunk within the wave's LDS slot
+  int32_t reserved;
+};
+
+struct FusedSegment {
+  const uint64_t *pre;       // AND-ed in before the leaves; null = all docs
+  int64_t nwords;            // 0 = skip the segment (EMPTY filter)
+  int32_t num_docs;
+  int32_t first_step;        // leaves [first, first + n_leaves), then folds
+  int32_t n_leaves;
+  int32_t n_folds;
+};
+
+struct FusedArgs {
+  const FusedSegment *segs;
+  const FusedStep *steps;
+  unsigned long long *part;  // [slot][nsegs * bps] per-block partials
+  uint32_t *hll_out;         // [kMaxHll][256] registers, atomicMax (zeroed by the caller)
+  int32_t nsegs, bps;        // block b serves segment b / bps
+  int32_t nslots;            // 1 + 2 * folds
+  int32_t stage_bytes;       // stepwise: LDS bytes per wave = 1024 * ceil(max bits / 2);
+                             // pipelined: bytes of ONE chunk slot (all steps), two slots per wave
+  int32_t n_hll;
+  int32_t nt;                // pipelined: non-temporal policy on the column DMA (exec.nt)
+  int32_t reserved;
+};
+// Largest chunk slot the pipelined kernel double-buffers in LDS: 512 B of `pre` words + every step's
+// 1-KiB pieces; 4 waves x 2 slots x 18.5 KiB + the block's FusedLds fit the 160 KiB of a CU.
+constexpr int kPipePreBytes = 512;
+constexpr int kMaxPipeSlotBytes = 18 * 1024 + kPipePreBytes;
+// gathers: the program has memory-LUT leaves, FOLD_DICT32 or FOLD_HLL (selects the gather instance).
+// pipelined: whole-chunk double-buffered staging (stage_bytes = slot <= kMaxPipeSlotBytes), else stepwise.
+void launch_scan_query(const FusedArgs &a, bool gathers, bool pipelined, hipStream_t stream);
+// Resident blocks of k_scan_query per CU for a stage size (occupancy API), cached.
+int scan_query_blocks_per_cu(int stage_bytes, bool gathers, bool pipelined);
+// Fixed-order reduction of the bps partials of slot s of segment g into out[g * out_stride + s]
+// (slot 0 and odd slots: sums; even slots > 0: packed (max << 32 | min) dictIds).
+void launch_reduce_fused(const unsigned long long *part, int32_t nsegs, int32_t bps, int32_t nslots,
+                         unsigned long long *out, int32_t out_stride, hipStream_t stream);
+
 // Sorted-index leaf: ranges (inclusive [start, end], sorted, disjoint) -> bitset (combine mode as k_leaf).
 void launch_ranges_to_bitset(const int32_t *ranges, int32_t nranges, int64_t nwords, int32_t num_docs,
                              int32_t mode, uint64_t *out, hipStream_t stream);

@@ -19,21 +19,12 @@
 #include <hip/hip_runtime.h>
 #include <type_traits>
 
+#include "device.h"
 #include "kernels.h"
 
 namespace pinot {
 namespace {
-
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
-
-__device__ __forceinline__ uint64_t tail_mask(int64_t w, int64_t nwords, int32_t num_docs) {
-  if (w != nwords - 1) return ~0ull;
-  const int rem = num_docs - (int)(w * 64);
-  return rem >= 64 ? ~0ull : ((1ull << rem) - 1ull);
-}
+using namespace dev;
 
 // The packed columns are streamed once per query: non-temporal loads.
 template <int B>
@@ -65,8 +56,6 @@ __device__ __forceinline__ void load_superword(const uint8_t *__restrict__ fwd, 
 // DMA'd into the wave's LDS region with coalesced 1-KiB global_load_lds_dwordx4 pieces, then every lane
 // reads its own 8*B-byte super-word from LDS. (Loading the super-words straight from HBM with a lane
 // stride of 8*B bytes touches 64 cache lines per instruction and thrashes the 32 KiB L1.)
-typedef __attribute__((address_space(3))) void lds_void_t;
-typedef const __attribute__((address_space(1))) void glob_void_t;
 
 template <int B>
 struct Stage {
@@ -83,7 +72,6 @@ __device__ __forceinline__ void stage_chunk(const uint8_t *__restrict__ fwd, int
     __builtin_amdgcn_global_load_lds((glob_void_t *)(src + i * 1024), (lds_void_t *)(lds_wave + i * 1024), 16, 0, 0);
 }
 
-__device__ __forceinline__ void wait_stage() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 template <int B>
 __device__ __forceinline__ void lds_superword(const uint8_t *lds_wave, int lane, uint32_t (&D)[2 * B]) {
@@ -156,30 +144,6 @@ struct ColFold {
     }
   }
 };
-
-__device__ __forceinline__ unsigned long long shfl_xor_u64(unsigned long long v, int o) {
-  return (unsigned long long)__shfl_xor((long long)v, o, 64);
-}
-
-__device__ __forceinline__ unsigned long long combine(int kind, unsigned long long a, unsigned long long b) {
-  switch (kind) {
-    case SLOT_SUM_U64:
-      return a + b;
-    case SLOT_SUM_F64:
-      return (unsigned long long)__double_as_longlong(__longlong_as_double((long long)a) +
-                                                      __longlong_as_double((long long)b));
-    case SLOT_MINMAX: {
-      const uint32_t mn = min((uint32_t)a, (uint32_t)b), mx = max((uint32_t)(a >> 32), (uint32_t)(b >> 32));
-      return ((unsigned long long)mx << 32) | mn;
-    }
-    default:
-      return a;
-  }
-}
-
-__device__ __forceinline__ unsigned long long slot_init(int kind) {
-  return kind == SLOT_MINMAX ? 0x00000000FFFFFFFFull : 0ull;
-}
 
 // Block-reduces one slot value (fixed order) and writes it to out[block] (lanes 0 of each wave -> LDS).
 template <int NW>

@@ -86,6 +86,29 @@ class PartialLayout(C.Structure):
 _lib = None
 
 
+def _share_hip_runtime_with_torch():
+    """One HIP runtime per process. PyTorch-ROCm bundles its own libamdhip64 / libhsa-runtime64 (same
+    sonames as /opt/rocm's). If this library loaded /opt/rocm's copy first, torch would later load a
+    second runtime and fail to see the GPU ("No HIP GPUs are available"), which breaks the RCCL combine
+    in the same process. When torch is installed, its runtime files are loaded (RTLD_GLOBAL, without
+    importing torch) so this library binds to them, exactly as when torch is imported first.
+    PINOT_GPU_HIP_RUNTIME=system keeps /opt/rocm's runtime."""
+    if os.environ.get("PINOT_GPU_HIP_RUNTIME") == "system":
+        return
+    import importlib.util
+    try:
+        spec = importlib.util.find_spec("torch")
+    except (ImportError, ValueError):
+        return
+    if spec is None or not spec.submodule_search_locations:
+        return
+    tlib = os.path.join(list(spec.submodule_search_locations)[0], "lib")
+    for name in ("libhsa-runtime64.so", "libamdhip64.so"):
+        f = os.path.join(tlib, name)
+        if os.path.exists(f):
+            C.CDLL(f, mode=C.RTLD_GLOBAL)
+
+
 def load(path=None):
     """Load libpinot_gpu.so (raises if it is missing: there is no fallback)."""
     global _lib
@@ -94,6 +117,7 @@ def load(path=None):
     p = path or LIB_PATH
     if not os.path.exists(p):
         raise PinotGpuError(3, "libpinot_gpu.so not built (%s); run `make -C incubator-pinot_amd`" % p)
+    _share_hip_runtime_with_torch()
     lib = C.CDLL(p)
     P = C.c_void_p
     i32, i64, u64 = C.c_int32, C.c_int64, C.c_uint64

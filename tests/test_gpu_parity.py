@@ -14,13 +14,15 @@ from pinot_amd.segment import build_column, Segment
 
 pytestmark = pytest.mark.gpu
 REL = 1e-9
-FORCE_MODES = ("", "scan", "index")
+# engine configurations: default (fused single-launch path, pipelined whole-chunk staging where a chunk
+# fits), forced scan / forced index leaves, the stepwise fused kernel, the non-temporal DMA policy, and
+# the unfused per-segment launch sequence
+ENGINE_MODES = ("", "filter.force=scan", "filter.force=index", "exec.pipe=1", "exec.nt=1;exec.pipe=1", "exec.fused=0")
 
 
-@pytest.fixture(scope="module", params=FORCE_MODES)
+@pytest.fixture(scope="module", params=ENGINE_MODES)
 def engine(request):
-    cfg = "filter.force=%s" % request.param if request.param else None
-    e = GpuEngine(0, cfg)
+    e = GpuEngine(0, request.param or None)
     yield e
     e.close()
 
@@ -301,6 +303,45 @@ def test_bad_literal_is_bad_query(engine, sv_gpu):
     with pytest.raises(PinotGpuError) as ei:
         ServerQueryExecutor(engine).process_query("SELECT COUNT(*) FROM t WHERE column1 = 'abc'", [sv_gpu])
     assert ei.value.status == 5
+
+
+def test_fused_and_unfused_agree_on_selective_index_filters(sv_segment):
+    """Sorted/bitmap `pre` bitsets + scan leaves in one launch; early chunk exit on empty masks."""
+    qs = ["SELECT COUNT(*), SUM(column1), MIN(column3), MAX(column6), AVG(column7), DISTINCTCOUNTHLL(column1) "
+          "FROM t WHERE column5 = 'gFuH' AND column1 > 100000000",
+          "SELECT COUNT(*), SUM(column3) FROM t WHERE daysSinceEpoch IN (126164076, 167572854) AND column9 < 5000000",
+          "SELECT COUNT(*), MAX(column1) FROM t WHERE (column6 = 1689277 OR column11 = 'P') AND column3 > 5"]
+    e1, e0 = GpuEngine(0), GpuEngine(0, "exec.fused=0")
+    g1, g0 = e1.register(sv_segment), e0.register(sv_segment)
+    for text in qs:
+        r1, s1 = ServerQueryExecutor(e1).process_query(text, [g1, g1])
+        r0, s0 = ServerQueryExecutor(e0).process_query(text, [g0, g0])
+        exp, scanned = O.execute_server([sv_segment, sv_segment], compile_pql(text))
+        assert s1.num_docs_scanned == s0.num_docs_scanned == scanned
+        q = compile_pql(text)
+        for a, x, y, z in zip(q["aggregations"], r1, r0, exp):
+            _assert_same(a["function"], x, z)
+            _assert_same(a["function"], y, z)
+    e1.close()
+    e0.close()
+
+
+def test_distributed_group_by_single_rank(sv_segment):
+    """pinot_gpu_group_by_partial -> (no peers) -> finalize equals the one-call group-by."""
+    from pinot_amd.combine import distributed_group_by
+    e = GpuEngine(0)
+    g = e.register(sv_segment)
+    ex = ServerQueryExecutor(e)
+    q = compile_pql("SELECT COUNT(*), SUM(column1), MIN(column3), MAX(column6), AVG(column7), "
+                    "DISTINCTCOUNTHLL(column1) FROM t WHERE column1 > 100000000 GROUP BY column9, column11")
+    got, st = distributed_group_by(ex, q, [g, g])
+    exp, scanned = O.execute_server([sv_segment, sv_segment], q)
+    assert st.num_docs_scanned == scanned
+    assert set(got) == set(exp)
+    for k in exp:
+        for a, gv, ev in zip(q["aggregations"], got[k], exp[k]):
+            _assert_same(a["function"], gv, ev)
+    e.close()
 
 
 def test_synthetic_segment_matches_host_generator(engine):

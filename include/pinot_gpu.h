@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PINOT_GPU_ABI_VERSION 1
+#define PINOT_GPU_ABI_VERSION 2
 
 /* ------------------------------------------------------------------ status */
 typedef enum {
@@ -125,6 +125,7 @@ typedef struct {
   int64_t num_total_raw_docs;
   int64_t num_segments_processed;
   double device_ms;            /* HIP-event time of the device work of the call */
+  double host_ms;              /* wall time from C-ABI entry to return (results on the host) */
 } pinot_exec_stats;
 
 /* Intermediate result of one aggregation function over a set of segments (already

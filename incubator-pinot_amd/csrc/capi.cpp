@@ -1,5 +1,6 @@
 // extern "C" entry points of libpinot_gpu.so (declared in include/pinot_gpu.h).
 // Every call: validate -> take the engine lock -> run -> map exceptions to pinot_status.
+#include <chrono>
 #include <cstring>
 #include <sstream>
 
@@ -29,6 +30,10 @@ struct pinot_engine : Engine {};
 struct pinot_groupby_result : GroupByResult {};
 
 namespace {
+
+double elapsed_ms(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
 thread_local std::string g_last_error;
 
 template <typename F>
@@ -78,6 +83,8 @@ void parse_config(Engine &e, const char *cfg) {
     else if (k == "timing") e.timing = v == "1" || v == "true";
     else if (k == "agg.affine") e.use_affine = v == "1" || v == "true";
     else if (k == "exec.fused") e.use_fused = v == "1" || v == "true";
+    else if (k == "sync.poll") e.sync_poll = v == "1" || v == "true";
+    else if (k == "debug.host_phases") e.host_phases = v == "1" || v == "true";
     else if (k == "exec.nt") e.use_nt = v == "1" || v == "true";
     else if (k == "exec.pipe") e.use_pipe = v == "1" || v == "true";
     else throw Error(PINOT_ERR_BAD_ARG, "unknown config key " + k);
@@ -198,9 +205,11 @@ pinot_status pinot_gpu_aggregate(pinot_engine *engine, const pinot_segment_handl
     require(engine && out, PINOT_ERR_BAD_ARG, "null argument");
     check_query(query);
     require(query->num_group_by == 0, PINOT_ERR_BAD_ARG, "group-by query passed to pinot_gpu_aggregate");
+    const auto t0 = std::chrono::steady_clock::now();
     std::lock_guard<std::mutex> lk(engine->mu);
     set_device(*engine);
     exec_aggregate(*engine, resolve(*engine, segments, num_segments), *query, out, stats);
+    if (stats) stats->host_ms = elapsed_ms(t0);
   });
 }
 
@@ -210,9 +219,11 @@ pinot_status pinot_gpu_group_by(pinot_engine *engine, const pinot_segment_handle
     require(engine && out, PINOT_ERR_BAD_ARG, "null argument");
     check_query(query);
     require(query->num_group_by >= 1, PINOT_ERR_BAD_ARG, "aggregation-only query passed to pinot_gpu_group_by");
+    const auto t0 = std::chrono::steady_clock::now();
     std::lock_guard<std::mutex> lk(engine->mu);
     set_device(*engine);
     auto r = exec_group_by(*engine, resolve(*engine, segments, num_segments), *query, stats);
+    if (stats) stats->host_ms = elapsed_ms(t0);
     auto *res = new pinot_groupby_result();
     static_cast<GroupByResult &>(*res) = std::move(*r);
     *out = res;

@@ -39,17 +39,20 @@ class DeviceBuffer {
   ~DeviceBuffer() { reset(); }
   DeviceBuffer(const DeviceBuffer &) = delete;
   DeviceBuffer &operator=(const DeviceBuffer &) = delete;
-  DeviceBuffer(DeviceBuffer &&o) noexcept : p_(o.p_), n_(o.n_) { o.p_ = nullptr; o.n_ = 0; }
+  DeviceBuffer(DeviceBuffer &&o) noexcept : p_(o.p_), n_(o.n_), gen_(o.gen_ + 1) { o.p_ = nullptr; o.n_ = 0; o.gen_++; }
   DeviceBuffer &operator=(DeviceBuffer &&o) noexcept {
-    if (this != &o) { reset(); p_ = o.p_; n_ = o.n_; o.p_ = nullptr; o.n_ = 0; }
+    if (this != &o) { reset(); p_ = o.p_; n_ = o.n_; gen_ += o.gen_ + 1; o.p_ = nullptr; o.n_ = 0; o.gen_++; }
     return *this;
   }
   void alloc(size_t bytes) {
     reset();
+    gen_++;
     if (bytes == 0) return;
     PINOT_HIP(hipMalloc(&p_, bytes));
     n_ = bytes;
   }
+  // Bumped by every (re)allocation: contents cached by address are stale once it changes.
+  uint64_t generation() const { return gen_; }
   // Ensure capacity >= bytes (contents not preserved).
   void reserve(size_t bytes) {
     if (bytes > n_) alloc(bytes + bytes / 4);
@@ -65,6 +68,7 @@ class DeviceBuffer {
  private:
   void *p_ = nullptr;
   size_t n_ = 0;
+  uint64_t gen_ = 0;
 };
 
 // Grow-only pinned host buffer (async H2D / D2H staging of the per-query tables and results).
@@ -90,6 +94,34 @@ class PinnedBuffer {
 
  private:
   void *p_ = nullptr;
+  size_t n_ = 0;
+};
+
+// Pinned host memory the device writes directly (zero-copy results of the fused query kernel).
+class MappedBuffer {
+ public:
+  MappedBuffer() = default;
+  ~MappedBuffer() { reset(); }
+  MappedBuffer(const MappedBuffer &) = delete;
+  MappedBuffer &operator=(const MappedBuffer &) = delete;
+  void reserve(size_t bytes) {
+    if (bytes <= n_) return;
+    reset();
+    const size_t want = bytes + bytes / 4;
+    PINOT_HIP(hipHostMalloc(&p_, want, hipHostMallocMapped | hipHostMallocCoherent));
+    PINOT_HIP(hipHostGetDevicePointer(&d_, p_, 0));
+    n_ = want;
+  }
+  void reset() {
+    if (p_) (void)hipHostFree(p_);
+    p_ = d_ = nullptr;
+    n_ = 0;
+  }
+  template <typename T = void> T *host() const { return static_cast<T *>(p_); }
+  template <typename T = void> T *device() const { return static_cast<T *>(d_); }
+
+ private:
+  void *p_ = nullptr, *d_ = nullptr;
   size_t n_ = 0;
 };
 

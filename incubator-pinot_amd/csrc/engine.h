@@ -113,6 +113,8 @@ struct Engine {
   bool use_nt = false;        // exec.nt: non-temporal policy on the streamed column DMA
   bool use_pipe = false;      // exec.pipe: double-buffered whole-chunk staging (k_scan_query_pipe) when a chunk fits
   bool timing = false;
+  bool sync_poll = false;     // sync.poll: busy-poll the stream instead of hipStreamSynchronize
+  bool host_phases = false;   // debug.host_phases: print the host-side phase times of fused queries
   int num_cus = 256;          // multiProcessorCount of the device
 
   // scratch (grow-only)
@@ -122,7 +124,12 @@ struct Engine {
   DeviceBuffer reduced;       // per-segment reduced slots + HLL registers
   DeviceBuffer group_scratch;
   PinnedBuffer host_arena;    // staging of the per-query arena (H2D)
+  std::vector<uint8_t> arena_shadow;  // bytes last copied into `small` (upload_arena skips identical programs)
+  uint64_t arena_dev_gen = 0;
+  bool arena_dev_valid = false;
   PinnedBuffer host_result;   // staging of the reduced results (D2H)
+  DeviceBuffer fused_ctl;     // k_scan_query: u32 arrival counter + [kMaxHll][256] HLL registers, kept zeroed
+  MappedBuffer fused_result;  // k_scan_query's last block writes the reduced per-segment slots + HLL here
 
   // timing
   hipEvent_t ev_start = nullptr, ev_stop = nullptr;

@@ -9,7 +9,7 @@
 //   3. stops touching the chunk as soon as the wave's mask is empty (skips every remaining column),
 //   4. folds the aggregated columns over the matching docs: COUNT, Σ dictId (arithmetic-progression
 //      dictionaries), Σ int32 dictionary values, min/max dictId (sorted dictionaries), HLL registers.
-// Block partials go to HBM per segment; k_reduce_fused reduces them in a fixed order.
+// Block partials go to HBM; the last block to arrive reduces them in a fixed order into host-mapped memory.
 //
 // Restates: PinotDataBitSet.readInt (PC/io/util/PinotDataBitSet.java:79-100), SVScanDocIdIterator
 // (PC/operator/dociditerators/SVScanDocIdIterator.java:85-159), AndBlockDocIdSet (:144-227),
@@ -26,8 +26,8 @@ using namespace dev;
 
 // Runtime bit width, compile-time extraction: a wave stages the chunk of the step's column in LDS
 // (ceil(B/2) coalesced 1-KiB DMA pieces), then each lane decodes its 64 values as two halves of 32.
-// Half h of the lane's super-word is the B dwords at byte 8*B*lane + 4*B*h; the 32-way switch over B
-// selects an unrolled decoder whose shifts are constants, the evaluation after it is width-free.
+// Half h of the lane's super-word is the B dwords at byte 8*B*lane + 4*B*h; a 32-way switch over B
+// (PINOT_WIDTH_SWITCH) selects a step instance whose shifts are constants.
 template <int B, int J>
 __device__ __forceinline__ void decode_half_step(const uint32_t (&D)[B], uint32_t (&v)[32]) {
   constexpr int p = J * B, k = p >> 5, o = p & 31;
@@ -54,25 +54,6 @@ __device__ __forceinline__ void decode_half(const uint8_t *p, uint32_t (&v)[32])
   decode_half_step<B, 0>(D, v);
 }
 
-__device__ __forceinline__ void decode_half_rt(int bits, const uint8_t *p, uint32_t (&v)[32]) {
-  switch (bits) {
-#define PINOT_DECODE_CASE(B) \
-  case B:                    \
-    decode_half<B>(p, v);    \
-    break;
-    PINOT_DECODE_CASE(1) PINOT_DECODE_CASE(2) PINOT_DECODE_CASE(3) PINOT_DECODE_CASE(4) PINOT_DECODE_CASE(5)
-    PINOT_DECODE_CASE(6) PINOT_DECODE_CASE(7) PINOT_DECODE_CASE(8) PINOT_DECODE_CASE(9) PINOT_DECODE_CASE(10)
-    PINOT_DECODE_CASE(11) PINOT_DECODE_CASE(12) PINOT_DECODE_CASE(13) PINOT_DECODE_CASE(14) PINOT_DECODE_CASE(15)
-    PINOT_DECODE_CASE(16) PINOT_DECODE_CASE(17) PINOT_DECODE_CASE(18) PINOT_DECODE_CASE(19) PINOT_DECODE_CASE(20)
-    PINOT_DECODE_CASE(21) PINOT_DECODE_CASE(22) PINOT_DECODE_CASE(23) PINOT_DECODE_CASE(24) PINOT_DECODE_CASE(25)
-    PINOT_DECODE_CASE(26) PINOT_DECODE_CASE(27) PINOT_DECODE_CASE(28) PINOT_DECODE_CASE(29) PINOT_DECODE_CASE(30)
-    PINOT_DECODE_CASE(31) PINOT_DECODE_CASE(32)
-#undef PINOT_DECODE_CASE
-    default:
-      break;
-  }
-}
-
 // Stages chunk `ch` (64 words = 4096 docs, 512*B contiguous bytes) of a packed column into the wave's LDS.
 // nt: non-temporal cache policy (aux = 2) for the once-read column streams.
 __device__ __forceinline__ void stage_chunk_rt(const uint8_t *__restrict__ fwd, int bits, int64_t ch, uint8_t *lds_wave,
@@ -88,30 +69,61 @@ __device__ __forceinline__ void stage_chunk_rt(const uint8_t *__restrict__ fwd, 
   }
 }
 
+// Predicate bits of 32 decoded dictIds, bit j = value j, shifted in from j = 31 down.
+// RANGE: (v - lo) < span as the borrow of a subtract, shifted in by one v_addc: 3 VALU ops per value
+// (the compiler's own form is compare + cndmask + shift/or, 4.5).
+#define PINOT_RANGE_STEP(x) \
+  "v_sub_u32 %1, " x ", %6\n\tv_sub_co_u32 %1, vcc, %1, %7\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc\n\t"
+__device__ __forceinline__ uint32_t range_bits(const uint32_t (&v)[32], uint32_t lo, uint32_t span) {
+  uint32_t m = 0;
+#pragma unroll
+  for (int j = 31; j >= 3; j -= 4) {
+    uint32_t t;
+    asm(PINOT_RANGE_STEP("%2") PINOT_RANGE_STEP("%3") PINOT_RANGE_STEP("%4") PINOT_RANGE_STEP("%5")
+        : "+v"(m), "=&v"(t)
+        : "v"(v[j]), "v"(v[j - 1]), "v"(v[j - 2]), "v"(v[j - 3]), "v"(lo), "v"(span)
+        : "vcc");
+  }
+  return m;
+}
+#undef PINOT_RANGE_STEP
+
 template <bool G>
 __device__ __forceinline__ uint32_t leaf_half(const FusedStep &st, const uint32_t (&v)[32]) {
   uint32_t m = 0;
   if (st.kind == FK_LEAF_RANGE) {
-#pragma unroll
-    for (int j = 0; j < 32; j++) m |= ((v[j] - st.lo) < st.span ? 1u : 0u) << j;
+    m = range_bits(v, st.lo, st.span);
   } else if (!G || st.kind == FK_LEAF_LUT64) {
+    if ((st.lut64 >> 32) == 0) {  // cardinality <= 32: one 32-bit LUT word, v_bfe_u32 per value
+      const uint32_t lut = (uint32_t)st.lut64;
 #pragma unroll
-    for (int j = 0; j < 32; j++) m |= (uint32_t)((st.lut64 >> v[j]) & 1ull) << j;
+      for (int j = 31; j >= 0; j--) m = (m << 1) + __builtin_amdgcn_ubfe(lut, v[j], 1);
+    } else {
+#pragma unroll
+      for (int j = 31; j >= 0; j--) m = (m << 1) + ((uint32_t)(st.lut64 >> v[j]) & 1u);
+    }
   } else {
     const uint32_t *__restrict__ lut = static_cast<const uint32_t *>(st.table);
 #pragma unroll
-    for (int j = 0; j < 32; j++) m |= ((lut[v[j] >> 5] >> (v[j] & 31)) & 1u) << j;
+    for (int j = 31; j >= 0; j--) m = (m << 1) + __builtin_amdgcn_ubfe(lut[v[j] >> 5], v[j] & 31, 1);
   }
   return m;
 }
 
 constexpr int kFusedWaves = kBlock / 64;
 
-struct FusedLds {
-  unsigned long long sum[kMaxFusedFolds][64];  // per-lane Σ (dictId or dictionary value) of fold f
-  uint32_t mn[kMaxFusedFolds][64], mx[kMaxFusedFolds][64];
-  uint32_t hll[kMaxHll][256];
-  unsigned long long red[kFusedWaves];
+// HLL registers of the block (G programs only; atomicMax per matching doc). Everything else a block
+// reduces lives in registers until the flush, which reuses the (then idle) staging LDS as BlockRed, so a
+// streaming-only program (G = false) has no static LDS at all: 4 blocks x 4 waves x 10 KiB stages fill
+// the CU's 160 KiB at b = 20.
+typedef uint32_t HllRegs[256];
+
+struct BlockRed {
+  uint32_t last;  // this block arrived last: it reduces every block's partials
+  uint32_t pad;
+  unsigned long long cnt[kFusedWaves];
+  unsigned long long sum[kFusedWaves][kMaxFusedFolds];
+  uint32_t mn[kFusedWaves][kMaxFusedFolds], mx[kFusedWaves][kMaxFusedFolds];
 };
 
 // Per-lane fold accumulators, held in registers for the whole kernel (the fold loop is unrolled over
@@ -122,38 +134,51 @@ struct FoldAcc {
   uint32_t mn[kMaxFusedFolds], mx[kMaxFusedFolds];
 };
 
-template <bool G>
-__device__ __forceinline__ void fold_half(const FusedStep &st, uint32_t mh, const uint32_t (&v)[32],
-                                          unsigned long long &sum, uint32_t &mn, uint32_t &mx, FusedLds &L) {
+// Bit j of the match mask as an opaque 0/1 value: keeps the compiler from turning the per-value
+// masking into 32 lane-mask selects (which it hoists into SGPR pairs and then spills).
+__device__ __forceinline__ uint32_t mbit(uint32_t mh, int j) {
+  uint32_t r;
+  asm("v_bfe_u32 %0, %1, %2, 1" : "=v"(r) : "v"(mh), "i"(j));
+  return r;
+}
+
+// Fold partials of one chunk (both halves) for one aggregated column.
+struct FoldPart {
+  unsigned long long sum = 0;
+  uint32_t mn = 0xFFFFFFFFu, mx = 0;
+};
+
+template <int B, bool G>
+__device__ __forceinline__ void fold_half(const FusedStep &st, uint32_t mh, const uint32_t (&v)[32], FoldPart &r,
+                                          HllRegs *hll) {
   if (st.ops & FOLD_IDSUM) {
-    if (st.bits <= 27) {  // 32 values of <= 27 bits cannot overflow 32 bits
+    if constexpr (B <= 24) {  // v * bit + t as a 24-bit multiply-add; 32 values of <= 24 bits sum below 2^29
       uint32_t t = 0;
 #pragma unroll
-      for (int j = 0; j < 32; j++) t += ((mh >> j) & 1u) ? v[j] : 0u;
-      sum += t;
+      for (int j = 0; j < 32; j++) t += __umul24(v[j], mbit(mh, j));
+      r.sum += t;
     } else {
 #pragma unroll
-      for (int j = 0; j < 32; j++) sum += ((mh >> j) & 1u) ? (unsigned long long)v[j] : 0ull;
+      for (int j = 0; j < 32; j++) r.sum += (unsigned long long)(v[j] & (0u - mbit(mh, j)));
     }
   }
   if (G && (st.ops & FOLD_DICT32)) {
     const int32_t *__restrict__ dict = static_cast<const int32_t *>(st.table);
     long long s = 0;
 #pragma unroll
-    for (int j = 0; j < 32; j++)
-      if ((mh >> j) & 1u) s += dict[v[j]];
-    sum += (unsigned long long)s;
+    for (int j = 0; j < 32; j++) s += (long long)(dict[v[j]] & (int32_t)(0u - mbit(mh, j)));
+    r.sum += (unsigned long long)s;
   }
-  if (st.ops & FOLD_MINMAX) {
+  if (st.ops & FOLD_MINMAX) {  // max over v & m, min over v | ~m (m = all-ones when the doc matches)
 #pragma unroll
     for (int j = 0; j < 32; j++) {
-      const bool b = (mh >> j) & 1u;
-      mn = b ? min(mn, v[j]) : mn;
-      mx = b ? max(mx, v[j]) : mx;
+      const uint32_t b = mbit(mh, j);
+      r.mn = min(r.mn, v[j] | (b - 1u));
+      r.mx = max(r.mx, v[j] & (0u - b));
     }
   }
   if (G && (st.ops & FOLD_HLL)) {
-    uint32_t *regs = L.hll[st.hll_set];
+    uint32_t *regs = hll[st.hll_set];
 #pragma unroll
     for (int j = 0; j < 32; j++)
       if ((mh >> j) & 1u) {
@@ -161,6 +186,56 @@ __device__ __forceinline__ void fold_half(const FusedStep &st, uint32_t mh, cons
         atomicMax(&regs[e >> 8], e & 0xFFu);
       }
   }
+}
+
+// One step of a chunk at compile-time width B: decode the lane's two halves from LDS and apply.
+template <int B, bool G>
+__device__ __forceinline__ void leaf_step(const FusedStep &st, const uint8_t *p, uint64_t &mask) {
+  uint32_t v[32];
+  decode_half<B>(p, v);
+  const uint32_t m0 = leaf_half<G>(st, v);
+  decode_half<B>(p + 4 * B, v);
+  const uint32_t m1 = leaf_half<G>(st, v);
+  const uint64_t m = ((uint64_t)m1 << 32) | m0;
+  mask &= st.negate ? ~m : m;
+}
+
+template <int B, bool G>
+__device__ __forceinline__ void fold_step(const FusedStep &st, const uint8_t *p, uint64_t mask, FoldPart &r,
+                                          HllRegs *hll) {
+  uint32_t v[32];
+  decode_half<B>(p, v);
+  fold_half<B, G>(st, (uint32_t)mask, v, r, hll);
+  decode_half<B>(p + 4 * B, v);
+  fold_half<B, G>(st, (uint32_t)(mask >> 32), v, r, hll);
+}
+
+#define PINOT_WIDTH_SWITCH(bits, CALL)                                                                         \
+  switch (bits) {                                                                                              \
+    case 1: CALL(1); break;   case 2: CALL(2); break;   case 3: CALL(3); break;   case 4: CALL(4); break;     \
+    case 5: CALL(5); break;   case 6: CALL(6); break;   case 7: CALL(7); break;   case 8: CALL(8); break;     \
+    case 9: CALL(9); break;   case 10: CALL(10); break; case 11: CALL(11); break; case 12: CALL(12); break;   \
+    case 13: CALL(13); break; case 14: CALL(14); break; case 15: CALL(15); break; case 16: CALL(16); break;   \
+    case 17: CALL(17); break; case 18: CALL(18); break; case 19: CALL(19); break; case 20: CALL(20); break;   \
+    case 21: CALL(21); break; case 22: CALL(22); break; case 23: CALL(23); break; case 24: CALL(24); break;   \
+    case 25: CALL(25); break; case 26: CALL(26); break; case 27: CALL(27); break; case 28: CALL(28); break;   \
+    case 29: CALL(29); break; case 30: CALL(30); break; case 31: CALL(31); break; case 32: CALL(32); break;   \
+    default: break;                                                                                            \
+  }
+
+template <bool G>
+__device__ __forceinline__ void leaf_rt(const FusedStep &st, const uint8_t *p, uint64_t &mask) {
+#define PINOT_LEAF(B) leaf_step<B, G>(st, p, mask)
+  PINOT_WIDTH_SWITCH(st.bits, PINOT_LEAF)
+#undef PINOT_LEAF
+}
+
+template <bool G>
+__device__ __forceinline__ void fold_rt(const FusedStep &st, const uint8_t *p, uint64_t mask, FoldPart &r,
+                                        HllRegs *hll) {
+#define PINOT_FOLD(B) fold_step<B, G>(st, p, mask, r, hll)
+  PINOT_WIDTH_SWITCH(st.bits, PINOT_FOLD)
+#undef PINOT_FOLD
 }
 
 // The per-query program (segments, steps) is read-only for the whole launch: reading it through the
@@ -189,56 +264,86 @@ __device__ __forceinline__ void init_acc(FoldAcc &A) {
   }
 }
 
-__device__ __forceinline__ void init_lds(FusedLds &L, int tid) {
-  for (int i = tid; i < kMaxFusedFolds * 64; i += kBlock) {
-    (&L.sum[0][0])[i] = 0;
-    (&L.mn[0][0])[i] = 0xFFFFFFFFu;
-    (&L.mx[0][0])[i] = 0;
-  }
-  for (int i = tid; i < kMaxHll * 256; i += kBlock) (&L.hll[0][0])[i] = 0;
+__device__ __forceinline__ void init_hll(HllRegs *hll, int tid) {
+  for (int i = tid; i < kMaxHll * 256; i += kBlock) (&hll[0][0])[i] = 0;
   __syncthreads();
 }
 
-// block partials, fixed order: wave sums -> LDS -> thread 0; folds reduced by wave 0; HLL atomicMax
-__device__ __forceinline__ void flush_block(const FusedArgs &a, FusedLds &L, const FoldAcc &A, unsigned long long cnt,
-                                            int g, int b, int tid, int lane, int wave) {
+// Block partials: wave reductions (shuffles) -> BlockRed in the idle staging LDS -> thread 0 adds the
+// block's totals into the per-segment accumulators with memory-side integer atomics (u64 add, u32
+// min/max: exact and order-independent, so the result is deterministic). The last block to arrive copies
+// the accumulators and HLL registers into host-mapped memory and resets them to their identities for
+// the next launch (replaces a reduce launch, a memset and a D2H copy). No __threadfence: an agent-scope
+// fence writes back and invalidates the XCD's whole L2 under every still-streaming block; atomics
+// execute at the memory side, vmcnt(0) waits for their acknowledgement before the arrival atomic, and
+// the last block reads with agent-scope (L2-bypassing) loads.
+__device__ __forceinline__ void flush_block(const FusedArgs &a, uint8_t *stage_lds, HllRegs *hll, const FoldAcc &A,
+                                            unsigned long long cnt, int g, int tid, int lane, int wave) {
+  const int nfolds = (a.nslots - 1) / 2;
+  __syncthreads();  // every wave is done with its stage: reuse it
+  BlockRed &R = *reinterpret_cast<BlockRed *>(stage_lds);
+  cnt = wave_sum(cnt);
+  if (lane == 0) R.cnt[wave] = cnt;
 #pragma unroll
   for (int f = 0; f < kMaxFusedFolds; f++) {
-    if (A.sum[f]) atomicAdd(&L.sum[f][lane], A.sum[f]);
-    atomicMin(&L.mn[f][lane], A.mn[f]);
-    atomicMax(&L.mx[f][lane], A.mx[f]);
+    if (f >= nfolds) break;
+    const unsigned long long s = wave_sum(A.sum[f]);
+    uint32_t lo = A.mn[f], hi = A.mx[f];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      lo = min(lo, (uint32_t)__shfl_xor((int)lo, o, 64));
+      hi = max(hi, (uint32_t)__shfl_xor((int)hi, o, 64));
+    }
+    if (lane == 0) {
+      R.sum[wave][f] = s;
+      R.mn[wave][f] = lo;
+      R.mx[wave][f] = hi;
+    }
   }
-  cnt = wave_sum(cnt);
-  if (lane == 0) L.red[wave] = cnt;
   __syncthreads();
-  const int64_t nblk = (int64_t)a.nsegs * a.bps;
-  unsigned long long *out = a.part + (int64_t)g * a.bps + b;
+  unsigned long long *acc = a.acc + (int64_t)g * a.res_stride;
   if (tid == 0) {
     unsigned long long c = 0;
-    for (int i = 0; i < kFusedWaves; i++) c += L.red[i];
-    out[0] = c;
-  }
-  const int nfolds = (a.nslots - 1) / 2;
-  if (wave == 0) {
+    for (int w = 0; w < kFusedWaves; w++) c += R.cnt[w];
+    if (c) atomicAdd(acc, c);
     for (int f = 0; f < nfolds; f++) {
-      const unsigned long long s = wave_sum(L.sum[f][lane]);
-      uint32_t lo = L.mn[f][lane], hi = L.mx[f][lane];
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        lo = min(lo, (uint32_t)__shfl_xor((int)lo, o, 64));
-        hi = max(hi, (uint32_t)__shfl_xor((int)hi, o, 64));
+      unsigned long long s = 0;
+      uint32_t lo = 0xFFFFFFFFu, hi = 0;
+      for (int w = 0; w < kFusedWaves; w++) {
+        s += R.sum[w][f];
+        lo = min(lo, R.mn[w][f]);
+        hi = max(hi, R.mx[w][f]);
       }
-      if (lane == 0) {
-        out[(1 + 2 * f) * nblk] = s;
-        out[(2 + 2 * f) * nblk] = ((unsigned long long)hi << 32) | lo;
-      }
+      if (s) atomicAdd(acc + 1 + 2 * f, s);
+      uint32_t *mm = reinterpret_cast<uint32_t *>(acc + 2 + 2 * f);  // little-endian: [0] = min, [1] = max
+      if (lo != 0xFFFFFFFFu) atomicMin(mm, lo);
+      if (hi) atomicMax(mm + 1, hi);
     }
   }
-  for (int h = 0; h < a.n_hll; h++)
-    for (int i = tid; i < 256; i += kBlock) {
-      const uint32_t r = L.hll[h][i];
-      if (r) atomicMax(&a.hll_out[h * 256 + i], r);
-    }
+  if (hll)
+    for (int h = 0; h < a.n_hll; h++)
+      for (int i = tid; i < 256; i += kBlock) {
+        const uint32_t r = hll[h][i];
+        if (r) atomicMax(&a.hll_out[h * 256 + i], r);
+      }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const uint32_t nblk = (uint32_t)(a.nsegs * a.bps);
+  if (tid == 0) R.last = atomicAdd(a.done, 1u) == nblk - 1 ? 1u : 0u;
+  __syncthreads();
+  if (!R.last) return;
+  const int n = a.nsegs * a.res_stride;
+  for (int i = tid; i < n; i += kBlock) {
+    const int sl = i % a.res_stride;
+    a.result[i] = __hip_atomic_load(a.acc + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    a.acc[i] = slot_init((sl == 0 || (sl & 1)) ? SLOT_SUM_U64 : SLOT_MINMAX);
+  }
+  uint32_t *res_hll = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(a.result) + a.result_hll_off);
+  for (int i = tid; i < a.n_hll * 256; i += kBlock) {
+    res_hll[i] = __hip_atomic_load(&a.hll_out[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    a.hll_out[i] = 0;
+  }
+  if (tid == 0) *a.done = 0;
 }
 
 // One chunk of the segment program: leaves AND-ed into `mask` (early exit once the wave's mask is
@@ -246,31 +351,26 @@ __device__ __forceinline__ void flush_block(const FusedArgs &a, FusedLds &L, con
 // staged chunk (staging it first in the stepwise kernel). Returns the chunk's matching doc count.
 template <bool G, typename Src>
 __device__ __forceinline__ unsigned long long eval_chunk(const FusedStep *__restrict__ steps, int n_leaves,
-                                                         int n_folds, uint64_t mask, FoldAcc &A, FusedLds &L,
+                                                         int n_folds, uint64_t mask, FoldAcc &A, HllRegs *hll,
                                                          int lane, Src &&src) {
   for (int i = 0; i < n_leaves; i++) {
     if (!__any(mask != 0)) break;  // wave-uniform: nothing left in this chunk, skip its other columns
     const FusedStep st = load_const(steps + i);
-    const uint8_t *p = src(i, st) + lane * (8 * st.bits);
-    uint32_t v[32];
-    decode_half_rt(st.bits, p, v);
-    const uint32_t m0 = leaf_half<G>(st, v);
-    decode_half_rt(st.bits, p + 4 * st.bits, v);
-    const uint32_t m1 = leaf_half<G>(st, v);
-    const uint64_t m = ((uint64_t)m1 << 32) | m0;
-    mask &= st.negate ? ~m : m;
+    leaf_rt<G>(st, src(i, st) + lane * (8 * st.bits), mask);
   }
   const unsigned long long cnt = __popcll(mask);
-#pragma unroll
-  for (int i = 0; i < kMaxFusedFolds; i++) {
-    if (i >= n_folds || !__any(mask != 0)) break;
+  for (int i = 0; i < n_folds; i++) {
+    if (!__any(mask != 0)) break;
     const FusedStep st = load_const(steps + n_leaves + i);  // st.fold == i (host order)
-    const uint8_t *p = src(n_leaves + i, st) + lane * (8 * st.bits);
-    uint32_t v[32];
-    decode_half_rt(st.bits, p, v);
-    fold_half<G>(st, (uint32_t)mask, v, A.sum[i], A.mn[i], A.mx[i], L);
-    decode_half_rt(st.bits, p + 4 * st.bits, v);
-    fold_half<G>(st, (uint32_t)(mask >> 32), v, A.sum[i], A.mn[i], A.mx[i], L);
+    FoldPart r;
+    fold_rt<G>(st, src(n_leaves + i, st) + lane * (8 * st.bits), mask, r, hll);
+#pragma unroll
+    for (int f = 0; f < kMaxFusedFolds; f++)  // uniform select of the register accumulator
+      if (f == i) {
+        A.sum[f] += r.sum;
+        A.mn[f] = min(A.mn[f], r.mn);
+        A.mx[f] = max(A.mx[f], r.mx);
+      }
   }
   return cnt;
 }
@@ -286,11 +386,15 @@ __device__ __forceinline__ uint64_t chunk_word(const FusedSegment &sg, int64_t c
 // G = false: streaming-only program (RANGE / 64-entry LUT leaves, Σ dictId and min/max folds), register-light;
 // G = true: also memory-LUT leaves, dictionary-value sums and HLL (per-value gathers).
 template <bool G>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) void k_scan_query(FusedArgs a) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G ? 2 : 4))) void k_scan_query(FusedArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t stage_lds[];
-  __shared__ FusedLds L;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  init_lds(L, tid);
+  HllRegs *hll = nullptr;
+  if constexpr (G) {
+    __shared__ HllRegs hll_lds[kMaxHll];
+    hll = hll_lds;
+    init_hll(hll, tid);
+  }
   const int g = blockIdx.x / a.bps, b = blockIdx.x % a.bps;
   const FusedSegment sg = load_const(a.segs + g);
   const FusedStep *steps = a.steps + sg.first_step;
@@ -300,14 +404,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
   init_acc(A);
   const int64_t nchunks = (sg.nwords + 63) >> 6;
   for (int64_t ch = (int64_t)b * kFusedWaves + wave; ch < nchunks; ch += (int64_t)a.bps * kFusedWaves) {
-    cnt += eval_chunk<G>(steps, sg.n_leaves, sg.n_folds, chunk_word(sg, ch, lane), A, L, lane,
+    cnt += eval_chunk<G>(steps, sg.n_leaves, sg.n_folds, chunk_word(sg, ch, lane), A, hll, lane,
                          [&](int, const FusedStep &st) -> const uint8_t * {
                            stage_chunk_rt(st.fwd, st.bits, ch, lds_wave, lane);
                            wait_stage();
                            return lds_wave;
                          });
   }
-  flush_block(a, L, A, cnt, g, b, tid, lane, wave);
+  flush_block(a, stage_lds, hll, A, cnt, g, tid, lane, wave);
 }
 
 // Pipelined shape: a chunk's every column is staged at once into one of the wave's two LDS slots, and
@@ -333,9 +437,13 @@ __device__ __forceinline__ uint64_t pre_mask(const FusedSegment &sg, const uint8
 template <bool G>
 __global__ __launch_bounds__(kBlock) void k_scan_query_pipe(FusedArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t stage_lds[];
-  __shared__ FusedLds L;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  init_lds(L, tid);
+  HllRegs *hll = nullptr;
+  if constexpr (G) {
+    __shared__ HllRegs hll_lds[kMaxHll];
+    hll = hll_lds;
+    init_hll(hll, tid);
+  }
   const int g = blockIdx.x / a.bps, b = blockIdx.x % a.bps;
   const FusedSegment sg = load_const(a.segs + g);
   const FusedStep *steps = a.steps + sg.first_step;
@@ -371,33 +479,14 @@ __global__ __launch_bounds__(kBlock) void k_scan_query_pipe(FusedArgs a) {
     // cur's pre area (pre words of ch, read one iteration ago) is free again
     if (sg.pre && ch + 2 * stride < nchunks) stage_pre(sg.pre, ch + 2 * stride, cur, lane);
     if (live0)
-      cnt += eval_chunk<G>(steps, sg.n_leaves, sg.n_folds, m0, A, L, lane,
+      cnt += eval_chunk<G>(steps, sg.n_leaves, sg.n_folds, m0, A, hll, lane,
                            [&](int, const FusedStep &st) -> const uint8_t * { return cur + st.stage_off; });
     m0 = m1;
     live0 = live1;
     par ^= 1;
   }
   wait_stage();
-  flush_block(a, L, A, cnt, g, b, tid, lane, wave);
-}
-
-// One block per (segment, slot): fixed-order reduction of the segment's bps block partials.
-__global__ __launch_bounds__(kBlock) void k_reduce_fused(const unsigned long long *__restrict__ part, int32_t nsegs,
-                                                          int32_t bps, int32_t nslots, unsigned long long *out,
-                                                          int32_t out_stride) {
-  __shared__ unsigned long long sm[kBlock];
-  const int g = blockIdx.x / nslots, s = blockIdx.x % nslots, tid = threadIdx.x;
-  const int kind = (s == 0 || (s & 1)) ? SLOT_SUM_U64 : SLOT_MINMAX;
-  const unsigned long long *in = part + (int64_t)s * nsegs * bps + (int64_t)g * bps;
-  unsigned long long v = slot_init(kind);
-  for (int i = tid; i < bps; i += kBlock) v = combine(kind, v, in[i]);
-  sm[tid] = v;
-  __syncthreads();
-  for (int st = kBlock / 2; st > 0; st >>= 1) {
-    if (tid < st) sm[tid] = combine(kind, sm[tid], sm[tid + st]);
-    __syncthreads();
-  }
-  if (tid == 0) out[(int64_t)g * out_stride + s] = sm[0];
+  flush_block(a, stage_lds, hll, A, cnt, g, tid, lane, wave);
 }
 
 }  // namespace
@@ -434,11 +523,5 @@ void launch_scan_query(const FusedArgs &a, bool gathers, bool pipelined, hipStre
   }
 }
 
-void launch_reduce_fused(const unsigned long long *part, int32_t nsegs, int32_t bps, int32_t nslots,
-                         unsigned long long *out, int32_t out_stride, hipStream_t stream) {
-  if (nsegs <= 0 || nslots <= 0) return;
-  hipLaunchKernelGGL(k_reduce_fused, dim3((unsigned)(nsegs * nslots)), dim3(kBlock), 0, stream, part, nsegs, bps,
-                     nslots, out, out_stride);
-}
 
 }  // namespace pinot

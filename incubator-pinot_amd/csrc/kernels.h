@@ -134,15 +134,19 @@ struct FusedSegment {
 struct FusedArgs {
   const FusedSegment *segs;
   const FusedStep *steps;
-  unsigned long long *part;  // [slot][nsegs * bps] per-block partials
-  uint32_t *hll_out;         // [kMaxHll][256] registers, atomicMax (zeroed by the caller)
+  unsigned long long *acc;   // [nsegs][res_stride] accumulators (identity between launches: sums 0,
+                             // min/max slots min = 0xFFFFFFFF / max = 0), reset by the last block
+  uint32_t *hll_out;         // [kMaxHll][256] registers, atomicMax (zero on entry; re-zeroed by the last block)
   int32_t nsegs, bps;        // block b serves segment b / bps
   int32_t nslots;            // 1 + 2 * folds
   int32_t stage_bytes;       // stepwise: LDS bytes per wave = 1024 * ceil(max bits / 2);
                              // pipelined: bytes of ONE chunk slot (all steps), two slots per wave
   int32_t n_hll;
   int32_t nt;                // pipelined: non-temporal policy on the column DMA (exec.nt)
-  int32_t reserved;
+  int32_t res_stride;        // u64 slots per segment in `result`
+  uint32_t *done;            // arrival counter (0 between launches; the last block resets it)
+  unsigned long long *result;  // host-mapped: [nsegs][res_stride] slots, then [kMaxHll][256] u32 HLL registers
+  int64_t result_hll_off;    // byte offset of the HLL registers in `result`
 };
 // Largest chunk slot the pipelined kernel double-buffers in LDS: 512 B of `pre` words + every step's
 // 1-KiB pieces; 4 waves x 2 slots x 18.5 KiB + the block's FusedLds fit the 160 KiB of a CU.
@@ -153,10 +157,6 @@ constexpr int kMaxPipeSlotBytes = 18 * 1024 + kPipePreBytes;
 void launch_scan_query(const FusedArgs &a, bool gathers, bool pipelined, hipStream_t stream);
 // Resident blocks of k_scan_query per CU for a stage size (occupancy API), cached.
 int scan_query_blocks_per_cu(int stage_bytes, bool gathers, bool pipelined);
-// Fixed-order reduction of the bps partials of slot s of segment g into out[g * out_stride + s]
-// (slot 0 and odd slots: sums; even slots > 0: packed (max << 32 | min) dictIds).
-void launch_reduce_fused(const unsigned long long *part, int32_t nsegs, int32_t bps, int32_t nslots,
-                         unsigned long long *out, int32_t out_stride, hipStream_t stream);
 
 // Sorted-index leaf: ranges (inclusive [start, end], sorted, disjoint) -> bitset (combine mode as k_leaf).
 void launch_ranges_to_bitset(const int32_t *ranges, int32_t nranges, int64_t nwords, int32_t num_docs,

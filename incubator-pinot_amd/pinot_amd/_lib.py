@@ -69,7 +69,8 @@ class Query(C.Structure):
 class ExecStats(C.Structure):
     _fields_ = [("num_docs_scanned", C.c_int64), ("num_entries_scanned_in_filter", C.c_int64),
                 ("num_entries_scanned_post_filter", C.c_int64), ("num_total_raw_docs", C.c_int64),
-                ("num_segments_processed", C.c_int64), ("device_ms", C.c_double)]
+                ("num_segments_processed", C.c_int64), ("device_ms", C.c_double),
+                ("host_ms", C.c_double)]
 
 
 class AggResult(C.Structure):

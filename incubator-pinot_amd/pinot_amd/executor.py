@@ -53,6 +53,7 @@ class ExecutionStatistics:
     num_total_raw_docs: int
     num_segments_processed: int = 0
     device_ms: float = 0.0
+    host_ms: float = 0.0
 
 
 class GpuSegment:
@@ -273,6 +274,12 @@ def _segment_handles(segments):
     return arr
 
 
+@dataclass
+class PreparedQuery:
+    query: dict
+    marshal: "QueryMarshal"
+
+
 class ServerQueryExecutor:
     """`ServerQueryExecutorV1Impl.processQuery` over GPU-resident segments of one engine."""
 
@@ -281,11 +288,22 @@ class ServerQueryExecutor:
         self.num_groups_limit = num_groups_limit
         self.max_init = max_init_group_holder_capacity
 
-    def process_query(self, query, segments, trim=True):
+    def prepare(self, query):
+        """Compile + marshal a query once (a prepared statement); process_query accepts the result.
+        Only the ctypes argument structs are reused: every execution still plans, resolves predicates
+        against each segment's dictionary and runs the device path."""
         if isinstance(query, str):
             query = compile_pql(query)
+        return PreparedQuery(query, QueryMarshal(query, self.num_groups_limit, self.max_init))
+
+    def process_query(self, query, segments, trim=True):
+        if isinstance(query, PreparedQuery):
+            query, m = query.query, query.marshal
+        else:
+            if isinstance(query, str):
+                query = compile_pql(query)
+            m = QueryMarshal(query, self.num_groups_limit, self.max_init)
         lib = self.engine.lib
-        m = QueryMarshal(query, self.num_groups_limit, self.max_init)
         handles = _segment_handles(segments)
         stats = _lib.ExecStats()
         if query.get("group_by"):
@@ -303,7 +321,7 @@ class ServerQueryExecutor:
             res = [_agg_value(a["function"].upper(), out[i]) for i, a in enumerate(query["aggregations"])]
         st = ExecutionStatistics(stats.num_docs_scanned, stats.num_entries_scanned_in_filter,
                                  stats.num_entries_scanned_post_filter, stats.num_total_raw_docs,
-                                 stats.num_segments_processed, stats.device_ms)
+                                 stats.num_segments_processed, stats.device_ms, stats.host_ms)
         return res, st
 
     def group_by_result(self, query, segments):

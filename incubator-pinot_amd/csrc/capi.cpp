@@ -83,7 +83,11 @@ void parse_config(Engine &e, const char *cfg) {
     else if (k == "timing") e.timing = v == "1" || v == "true";
     else if (k == "agg.affine") e.use_affine = v == "1" || v == "true";
     else if (k == "exec.fused") e.use_fused = v == "1" || v == "true";
-    else if (k == "sync.poll") e.sync_poll = v == "1" || v == "true";
+    else if (k == "group.mode") {
+      require(v.empty() || v == "auto" || v == "lds" || v == "global" || v == "partition", PINOT_ERR_BAD_ARG,
+              "group.mode: auto | lds | global | partition");
+      e.group_mode = v == "auto" ? "" : v;
+    } else if (k == "sync.poll") e.sync_poll = v == "1" || v == "true";
     else if (k == "debug.host_phases") e.host_phases = v == "1" || v == "true";
     else if (k == "exec.nt") e.use_nt = v == "1" || v == "true";
     else if (k == "exec.pipe") e.use_pipe = v == "1" || v == "true";
@@ -234,8 +238,8 @@ int64_t pinot_groupby_num_groups(const pinot_groupby_result *r) { return r ? (in
 int32_t pinot_groupby_num_columns(const pinot_groupby_result *r) { return r ? r->num_columns : 0; }
 
 const char *pinot_groupby_key(const pinot_groupby_result *r, int64_t group) {
-  if (!r || group < 0 || group >= (int64_t)r->keys.size()) return nullptr;
-  return r->keys[group].c_str();
+  if (!r || group < 0 || group >= (int64_t)r->raw_keys.size()) return nullptr;
+  return r->key(group).c_str();
 }
 
 pinot_status pinot_groupby_values(const pinot_groupby_result *r, int32_t fn, int64_t *counts, double *values) {
@@ -252,9 +256,15 @@ pinot_status pinot_groupby_hll(const pinot_groupby_result *r, int32_t fn, uint8_
     require(r && fn >= 0 && fn < (int32_t)r->functions.size(), PINOT_ERR_BAD_ARG, "function index");
     require(r->functions[fn] == PINOT_AGG_DISTINCTCOUNTHLL, PINOT_ERR_BAD_ARG, "not a DISTINCTCOUNTHLL function");
     const size_t n = r->raw_keys.size();
-    if (registers && n) memcpy(registers, r->hll[fn].data(), n * 256);
-    if (cardinalities)
-      for (size_t i = 0; i < n; i++) cardinalities[i] = hll_cardinality(r->hll[fn].data() + i * 256);
+    if (registers && n) {
+      if (r->hll_dev) {
+        PINOT_HIP(hipSetDevice(r->device));
+        PINOT_HIP(hipMemcpy(registers, r->hll_dev->get<uint8_t>() + r->hll_dev_off[fn], n * 256, hipMemcpyDeviceToHost));
+      } else {
+        memcpy(registers, r->hll[fn].data(), n * 256);
+      }
+    }
+    if (cardinalities && n) memcpy(cardinalities, r->hll_card[fn].data(), n * 8);
   });
 }
 

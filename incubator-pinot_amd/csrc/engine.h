@@ -113,6 +113,7 @@ struct Engine {
   bool use_nt = false;        // exec.nt: non-temporal policy on the streamed column DMA
   bool use_pipe = false;      // exec.pipe: double-buffered whole-chunk staging (k_scan_query_pipe) when a chunk fits
   bool timing = false;
+  std::string group_mode;     // group.mode: "" (auto) | lds | global | partition (tests force a sink)
   bool sync_poll = false;     // sync.poll: busy-poll the stream instead of hipStreamSynchronize
   bool host_phases = false;   // debug.host_phases: print the host-side phase times of fused queries
   int num_cus = 256;          // multiProcessorCount of the device
@@ -122,7 +123,10 @@ struct Engine {
   DeviceBuffer small;         // per-query arena: ranges, ids, LUTs
   DeviceBuffer partials;      // per-block partial slots
   DeviceBuffer reduced;       // per-segment reduced slots + HLL registers
-  DeviceBuffer group_scratch;
+  DeviceBuffer group_scratch;  // dense group-by accumulators (+ per-segment matched counts)
+  DeviceBuffer group_part;     // partitioned plan: histogram, offsets, partition starts, scan temp
+  DeviceBuffer group_records;  // partitioned plan: (local key | dictIds) records
+  DeviceBuffer group_final;    // ordered non-empty keys + compaction scratch
   PinnedBuffer host_arena;    // staging of the per-query arena (H2D)
   std::vector<uint8_t> arena_shadow;  // bytes last copied into `small` (upload_arena skips identical programs)
   uint64_t arena_dev_gen = 0;
@@ -147,15 +151,25 @@ void exec_aggregate(Engine &e, const std::vector<SegmentData *> &segs, const pin
                     pinot_exec_stats *stats);
 
 struct GroupByResult {
-  std::vector<int64_t> raw_keys;
-  std::vector<std::string> keys;
+  std::vector<int64_t> raw_keys;              // ascending raw keys (mixed radix over global ids, column 0 least significant)
   int32_t num_columns = 0;
   std::vector<int> functions;
   std::vector<std::vector<int64_t>> counts;   // per fn
   std::vector<std::vector<double>> values;    // per fn
-  std::vector<std::vector<uint8_t>> hll;      // per fn: groups*256
-};
-std::unique_ptr<GroupByResult> exec_group_by(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q,
+  // group key strings ('\t'-joined Dictionary.getStringValue), built on first access
+  std::vector<std::vector<std::string>> gvalues;  // [gcol] global id -> string
+  std::vector<int64_t> gcard;
+  mutable std::vector<std::string> keys;
+  mutable std::vector<uint8_t> key_built;
+  const std::string &key(int64_t g) const;
+  // DISTINCTCOUNTHLL: cardinalities per fn; registers on the host (hll[fn]) or on the device
+  // (hll_dev + hll_dev_off[fn], [groups][256] u8, copied on request)
+  std::vector<std::vector<int64_t>> hll_card;
+  std::vector<std::vector<uint8_t>> hll;
+  std::shared_ptr<DeviceBuffer> hll_dev;
+  std::vector<size_t> hll_dev_off;
+  int device = 0;
+};std::unique_ptr<GroupByResult> exec_group_by(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q,
                                              pinot_exec_stats *stats);
 
 // multi-GPU partials
@@ -178,5 +192,7 @@ uint32_t murmur_hash_long(int64_t v);
 uint32_t murmur_hash_bytes(const uint8_t *data, int len);
 uint16_t hll_register_rank(uint32_t h);  // (register << 8) | rank
 int64_t hll_cardinality(const uint8_t *regs);
+// HyperLogLog.cardinality() from the exact register sum Σ 2^(32 - reg) and the zero-register count.
+int64_t hll_cardinality_from_sum(unsigned long long sum_fixed32, uint32_t zeros);
 
 }  // namespace pinot

@@ -88,7 +88,8 @@ class Compiler {
   // Fused plan: the scan leaves of the top-level conjunction (AndFilterOperator puts scans last and
   // applies them only to the candidates of the index children, AndBlockDocIdSet.java:144-227) become
   // k_scan_query leaves; every other conjunct is built into slot 0 = the kernel's `pre` bitset.
-  void run_fused(const FilterTreeInput *tree) {
+  // max_fused_bits: wider scan leaves go to the `pre` program (the group kernel's 16 wave stages are small)
+  void run_fused(const FilterTreeInput *tree, int max_fused_bits = 32) {
     FilterNode root = plan_filter(seg_, tree);
     if (root.type == FilterNode::EMPTY) { sp_.empty = true; return; }
     if (root.type == FilterNode::MATCH_ALL) { sp_.match_all = true; return; }
@@ -107,7 +108,7 @@ class Compiler {
         continue;
       }
       FilterStep st = leaf_step(*c);
-      if (st.kind == FilterStep::SCAN) {
+      if (st.kind == FilterStep::SCAN && seg_.cols[st.col]->bits <= max_fused_bits) {
         sp_.fused_leaves.push_back(st);
       } else {
         st.dst = 0;
@@ -1154,6 +1155,9 @@ std::unique_ptr<GroupByResult> finalize_groups(Engine &e, const pinot_query &q, 
   res->counts.assign(na, {});
   res->values.assign(na, {});
   res->hll.assign(na, {});
+  res->hll_card.assign(na, {});
+  res->gvalues = ks.gvalues;
+  res->gcard = ks.gcard;
   for (int a = 0; a < na; a++) res->functions[a] = q.aggregations[a].function;
   if (n == 0) return res;
   DeviceBuffer out(n * 8 * (1 + na) + (size_t)n_hll * n * 256 + 16);
@@ -1175,18 +1179,7 @@ std::unique_ptr<GroupByResult> finalize_groups(Engine &e, const pinot_query &q, 
   std::iota(order.begin(), order.end(), 0);
   std::sort(order.begin(), order.end(), [&](size_t x, size_t y) { return hkeys[x] < hkeys[y]; });
   res->raw_keys.resize(n);
-  res->keys.resize(n);
-  for (size_t i = 0; i < n; i++) {
-    int64_t k = hkeys[order[i]];
-    res->raw_keys[i] = k;
-    std::string s;
-    for (int j = 0; j < q.num_group_by; j++) {  // getGroupKey: column 0 first, '\t'-joined
-      if (j) s += '\t';
-      s += ks.gvalues[j][k % ks.gcard[j]];
-      k /= ks.gcard[j];
-    }
-    res->keys[i] = std::move(s);
-  }
+  for (size_t i = 0; i < n; i++) res->raw_keys[i] = hkeys[order[i]];
   int h = 0;
   for (int a = 0; a < na; a++) {
     auto &cv = res->counts[a];
@@ -1194,7 +1187,10 @@ std::unique_ptr<GroupByResult> finalize_groups(Engine &e, const pinot_query &q, 
     cv.resize(n);
     vv.resize(n);
     const int ak = ga.acc_kind[a];
-    if (ak == 4) res->hll[a].resize(n * 256);
+    if (ak == 4) {
+      res->hll[a].resize(n * 256);
+      res->hll_card[a].resize(n);
+    }
     for (size_t i = 0; i < n; i++) {
       const size_t src = order[i];
       cv[i] = (int64_t)hcnt[src];
@@ -1206,7 +1202,8 @@ std::unique_ptr<GroupByResult> finalize_groups(Engine &e, const pinot_query &q, 
         case 3: vv[i] = decode_ordered(raw); break;
         case 4: {
           memcpy(res->hll[a].data() + i * 256, hhll.data() + ((size_t)h * n + src) * 256, 256);
-          vv[i] = (double)hll_cardinality(res->hll[a].data() + i * 256);
+          res->hll_card[a][i] = hll_cardinality(res->hll[a].data() + i * 256);
+          vv[i] = (double)res->hll_card[a][i];
           break;
         }
         default: vv[i] = (double)hcnt[src]; break;
@@ -1304,8 +1301,435 @@ void init_accs(Engine &e, int64_t G, unsigned long long *counts, const GroupAccs
 
 }  // namespace
 
+// DictionaryBasedGroupKeyGenerator.getGroupKey (:421-437): column 0 first, values '\t'-joined.
+const std::string &GroupByResult::key(int64_t g) const {
+  if (keys.size() != raw_keys.size()) {
+    keys.assign(raw_keys.size(), std::string());
+    key_built.assign(raw_keys.size(), 0);
+  }
+  if (!key_built[g]) {
+    int64_t k = raw_keys[g];
+    std::string s;
+    for (size_t j = 0; j < gcard.size(); j++) {
+      if (j) s += '\t';
+      s += gvalues[j][k % gcard[j]];
+      k /= gcard[j];
+    }
+    keys[g] = std::move(s);
+    key_built[g] = 1;
+  }
+  return keys[g];
+}
+
+std::unique_ptr<GroupByResult> exec_group_by_legacy(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q,
+                                                    pinot_exec_stats *stats);
+
+namespace {
+
+// Fused group-by plan (GroupMode) chosen from the key space and the accumulators' per-key bytes.
+struct GroupPlan {
+  int mode = GB_GLOBAL;
+  int shift = 0;        // partitioned: 2^shift keys per partition
+  int64_t P = 0;
+  int lds_acc_bytes = 0;
+  std::vector<int> lds_off, field_shift, reduce_off;
+  int reduce_bytes = 0;
+};
+
+constexpr int kGroupMaxFusedLeafBits = 12;    // 16 wave stages x 6 KiB
+constexpr int kGroupLdsAccBudget = 60 * 1024;  // GB_LDS accumulators / GB_COUNT-EMIT partition cursors
+constexpr int kReduceLdsBudget = 128 * 1024;   // k_partition_reduce accumulators
+constexpr int64_t kMaxPartitions = kGroupLdsAccBudget / 4;
+
+size_t lds_acc_bytes_per_key(int kind, bool lds_hll_u32) {
+  if (kind == 5) return 0;
+  if (kind == 4) return lds_hll_u32 ? 1024 : 256;
+  return 8;
+}
+
+GroupPlan plan_group(const std::vector<SegmentData *> &segs, const pinot_query &q, const KeySpace &ks,
+                     const GroupAccs &ga, const std::string &force) {
+  GroupPlan gp;
+  const int na = q.num_aggregations;
+  gp.lds_off.assign(na, 0);
+  gp.field_shift.assign(na, 0);
+  gp.reduce_off.assign(na, 0);
+  // GB_LDS: counts u32 [G], then each accumulator array (8-byte aligned)
+  size_t off = ((size_t)ks.G * 4 + 7) / 8 * 8;
+  for (int a = 0; a < na; a++) {
+    gp.lds_off[a] = (int)std::min<size_t>(off, INT32_MAX);
+    off += (size_t)ks.G * lds_acc_bytes_per_key(ga.acc_kind[a], true);
+  }
+  if (off <= (size_t)kGroupLdsAccBudget && (force.empty() || force == "lds")) {
+    gp.mode = GB_LDS;
+    gp.lds_acc_bytes = (int)off;
+    return gp;
+  }
+  // partitioned: identical aggregated dictionaries on every segment (records carry dictIds) and a record
+  // (local key + each aggregated column's dictId) within 64 bits
+  bool same = true;
+  for (int a = 0; a < na && same; a++) {
+    if (ga.acc_kind[a] == 5) continue;
+    const ColumnData &c0 = *segs[0]->column(agg_column(q.aggregations[a]));
+    for (size_t si = 1; si < segs.size(); si++) same = same && same_dictionary(c0, *segs[si]->column(c0.name));
+  }
+  size_t per_key = 4;
+  for (int a = 0; a < na; a++) per_key += lds_acc_bytes_per_key(ga.acc_kind[a], true);
+  int shift = 0;
+  while (shift < 12 && ((size_t)2 << shift) * per_key <= (size_t)kReduceLdsBudget) shift++;
+  const int64_t K = int64_t(1) << shift;
+  const int64_t P = (ks.G + K - 1) / K;
+  // record layout: [shift bits local key | one field per distinct aggregated column]
+  std::map<std::string, int> col_field;
+  int bits = shift;
+  for (int a = 0; a < na; a++) {
+    if (ga.acc_kind[a] == 5) continue;
+    const std::string c = agg_column(q.aggregations[a]);
+    auto it = col_field.find(c);
+    if (it == col_field.end()) {
+      it = col_field.emplace(c, bits).first;
+      bits += segs[0]->column(c)->bits;
+    }
+    gp.field_shift[a] = it->second;
+  }
+  const bool want_part = force.empty() ? ks.G >= 4 * K : force == "partition";
+  if (same && bits <= 64 && P <= kMaxPartitions && want_part && force != "global") {
+    gp.mode = GB_EMIT;  // COUNT + EMIT + reduce
+    gp.shift = shift;
+    gp.P = P;
+    size_t roff = ((size_t)K * 4 + 7) / 8 * 8;
+    for (int a = 0; a < na; a++) {
+      gp.reduce_off[a] = (int)roff;
+      roff += (size_t)K * lds_acc_bytes_per_key(ga.acc_kind[a], true);
+    }
+    gp.reduce_bytes = (int)roff;
+    return gp;
+  }
+  gp.mode = GB_GLOBAL;
+  return gp;
+}
+
+// Segments whose holder would apply the num.groups.limit first-appearance admission
+// (IntMapBasedHolder, DictionaryBasedGroupKeyGenerator.java:293-302): those queries stay on the
+// bitset path, which implements the rule.
+bool needs_admission(const std::vector<SegmentData *> &segs, const pinot_query &q, const Engine &e) {
+  const int64_t limit = q.num_groups_limit > 0 ? q.num_groups_limit : e.num_groups_limit;
+  const int64_t threshold = q.max_init_group_holder_capacity > 0 ? q.max_init_group_holder_capacity : 10000;
+  for (auto *s : segs) {
+    __int128 product = 1;
+    for (int j = 0; j < q.num_group_by; j++) product *= s->column(q.group_by[j])->card;
+    if (product > threshold && product > limit && s->num_docs > limit) return true;
+  }
+  return false;
+}
+
+}  // namespace
+
+// Fused group-by: ONE k_group_query launch (or COUNT / EMIT / reduce for the partitioned plan) over all
+// segments, device compaction of the non-empty keys, device per-group outputs, one D2H of the arrays.
+std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q,
+                                                   const KeySpace &ks, const GroupAccs &ga, pinot_exec_stats *stats) {
+  const int na = q.num_aggregations;
+  const size_t S = segs.size();
+  const GroupPlan gp = plan_group(segs, q, ks, ga, e.group_mode);
+  Arena ar;
+  std::unique_ptr<FilterTreeInput> tree;
+  if (q.num_filter_nodes > 0) tree = std::make_unique<FilterTreeInput>(decode_filter(q.num_filter_nodes, q.filter));
+  std::vector<SegPlan> plans(S);
+  for (size_t si = 0; si < S; si++) {
+    plans[si].seg = segs[si];
+    Compiler(e, plans[si], ar).run_fused(tree.get(), kGroupMaxFusedLeafBits);
+  }
+  // remaps (dictId -> global id) travel in the arena
+  std::vector<std::vector<size_t>> remap_off(S, std::vector<size_t>(q.num_group_by, SIZE_MAX));
+  for (size_t si = 0; si < S; si++)
+    for (int j = 0; j < q.num_group_by; j++)
+      if (!ks.remap[si][j].empty()) remap_off[si][j] = ar.add(ks.remap[si][j].data(), ks.remap[si][j].size() * 4);
+  size_t n_leaves = 0;
+  for (auto &p : plans) n_leaves += p.fused_leaves.size();
+  const size_t tab_bytes = S * sizeof(GroupSegment) + n_leaves * sizeof(FusedStep) +
+                           S * q.num_group_by * sizeof(GroupColDev) + S * na * sizeof(GroupAggDev) + 512;
+  QueryScratch qs = prepare_scratch(e, plans, ar, true, tab_bytes);
+
+  // dense accumulators: counts u64 [G], then one array per aggregation (HLL: u8 [G][256])
+  std::vector<size_t> acc_bytes(na, 0);
+  size_t per_key = 8;
+  for (int a = 0; a < na; a++) {
+    acc_bytes[a] = ga.acc_kind[a] == 5 ? 0 : ga.acc_kind[a] == 4 ? 256 : 8;
+    per_key += acc_bytes[a];
+  }
+  size_t free_b = 0, total_b = 0;
+  PINOT_HIP(hipMemGetInfo(&free_b, &total_b));
+  require((double)ks.G * per_key < 0.5 * (double)free_b, PINOT_ERR_UNSUPPORTED, "dense group-by accumulators do not fit in HBM");
+  e.group_scratch.reserve(ks.G * per_key + 256 + S * 8);
+  uint8_t *base = e.group_scratch.get<uint8_t>();
+  auto *matched = reinterpret_cast<unsigned long long *>(base);
+  auto *counts = reinterpret_cast<unsigned long long *>(base + 256 + S * 8);
+  std::vector<void *> accs(na, nullptr);
+  {
+    uint8_t *p = reinterpret_cast<uint8_t *>(counts) + ks.G * 8;
+    for (int a = 0; a < na; a++) {
+      if (!acc_bytes[a]) continue;
+      accs[a] = p;
+      p += ks.G * acc_bytes[a];
+    }
+  }
+
+  // device program
+  std::vector<GroupSegment> gsegs(S);
+  std::vector<FusedStep> leaves;
+  std::vector<GroupColDev> gcols;
+  std::vector<GroupAggDev> gaggs;
+  int max_leaf_bits = 1;
+  for (size_t si = 0; si < S; si++) {
+    SegPlan &p = plans[si];
+    SegmentData &s = *p.seg;
+    GroupSegment &g = gsegs[si];
+    g.pre = p.has_pre ? qs.bitsets + (int64_t)si * qs.slots * qs.stride : nullptr;
+    g.nwords = p.empty ? 0 : s.nwords();
+    g.num_docs = s.num_docs;
+    g.first_leaf = (int32_t)leaves.size();
+    g.n_leaves = (int32_t)p.fused_leaves.size();
+    g.first_gcol = (int32_t)gcols.size();
+    g.first_agg = (int32_t)gaggs.size();
+    for (const FilterStep &l : p.fused_leaves) {
+      const ColumnData &c = *s.cols[l.col];
+      FusedStep st{};
+      st.fwd = c.fwd.get<uint8_t>();
+      st.bits = c.bits;
+      st.kind = l.leaf_kind == LEAF_RANGE ? FK_LEAF_RANGE : l.leaf_kind == LEAF_LUT64 ? FK_LEAF_LUT64 : FK_LEAF_LUT;
+      st.negate = l.negate;
+      st.lo = l.lo;
+      st.span = l.span;
+      st.lut64 = l.lut64;
+      st.table = qs.arena + l.off;
+      leaves.push_back(st);
+      max_leaf_bits = std::max(max_leaf_bits, c.bits);
+    }
+    long long stride = 1;
+    for (int j = 0; j < q.num_group_by; j++) {
+      const ColumnData &c = *s.column(q.group_by[j]);
+      GroupColDev gc{};
+      gc.fwd = c.fwd.get<uint8_t>();
+      gc.remap = remap_off[si][j] == SIZE_MAX ? nullptr : reinterpret_cast<const int32_t *>(qs.arena + remap_off[si][j]);
+      gc.stride = stride;
+      gc.bits = c.bits;
+      gcols.push_back(gc);
+      stride *= ks.gcard[j];
+    }
+    for (int a = 0; a < na; a++) {
+      GroupAggDev ag{};
+      ag.acc_kind = ga.acc_kind[a];
+      ag.acc = accs[a];
+      if (ag.acc_kind != 5) {
+        ColumnData &c = *s.column(agg_column(q.aggregations[a]));
+        ag.fwd = c.fwd.get<uint8_t>();
+        ag.dict = c.dict_dev.get();
+        ag.bits = c.bits;
+        ag.value_kind = c.value_kind();
+        if (ag.acc_kind == 4) {
+          ensure_hll_lut(e, c);
+          ag.hll_lut = c.hll_lut.get<uint16_t>();
+        }
+      }
+      ag.field_shift = gp.field_shift[a];
+      ag.lds_off = gp.lds_off[a];
+      gaggs.push_back(ag);
+    }
+  }
+  const size_t off_segs = ar.add(gsegs.data(), gsegs.size() * sizeof(GroupSegment));
+  const size_t off_leaves = ar.add(leaves.data(), leaves.size() * sizeof(FusedStep));
+  const size_t off_gcols = ar.add(gcols.data(), gcols.size() * sizeof(GroupColDev));
+  const size_t off_aggs = ar.add(gaggs.data(), gaggs.size() * sizeof(GroupAggDev));
+  require(ar.bytes.size() <= e.small.size(), PINOT_ERR_DEVICE, "query arena overflow");
+
+  GroupArgs a{};
+  a.segs = reinterpret_cast<const GroupSegment *>(qs.arena + off_segs);
+  a.leaves = reinterpret_cast<const FusedStep *>(qs.arena + off_leaves);
+  a.gcols = reinterpret_cast<const GroupColDev *>(qs.arena + off_gcols);
+  a.aggs = reinterpret_cast<const GroupAggDev *>(qs.arena + off_aggs);
+  a.nsegs = (int32_t)S;
+  a.n_gcols = q.num_group_by;
+  a.n_aggs = na;
+  a.stage_bytes = 1024 * ((max_leaf_bits + 1) / 2);
+  a.G = ks.G;
+  a.counts = counts;
+  a.matched = matched;
+  a.lds_acc_bytes = gp.lds_acc_bytes;
+  a.shift = gp.shift;
+  a.P = (int32_t)gp.P;
+  a.mode = gp.mode == GB_EMIT ? GB_COUNT : gp.mode;
+  int64_t max_chunks = 1;
+  for (auto *sg : segs) max_chunks = std::max<int64_t>(max_chunks, (sg->nwords() + 63) / 64);
+  const int64_t resident = (int64_t)group_query_blocks_per_cu(a) * e.num_cus;
+  a.bps = (int)std::max<int64_t>(1, std::min<int64_t>(resident / (int64_t)S, (max_chunks + 15) / 16));
+  const int64_t nblk = (int64_t)S * a.bps;
+
+  PINOT_HIP(hipEventRecord(e.ev_start, e.stream));
+  upload_arena(e, ar);
+  Timer t(e);
+  for (size_t si = 0; si < S; si++)
+    if (plans[si].has_pre && !plans[si].empty) run_filter(e, plans[si], qs, t, (int64_t)si);
+  PINOT_HIP(hipMemsetAsync(matched, 0, S * 8, e.stream));
+  if (gp.mode != GB_EMIT) {  // identities: counts / sums 0, min all-ones, max 0, HLL 0
+    PINOT_HIP(hipMemsetAsync(counts, 0, ks.G * 8, e.stream));
+    for (int i = 0; i < na; i++)
+      if (accs[i]) PINOT_HIP(hipMemsetAsync(accs[i], ga.acc_kind[i] == 2 ? 0xFF : 0, ks.G * acc_bytes[i], e.stream));
+    t.timed(1, [&] { launch_group_query(a, e.stream); });
+    PINOT_HIP(hipGetLastError());
+  } else {
+    const size_t hist_n = (size_t)gp.P * nblk;
+    int64_t max_records = 0;
+    for (auto *sg : segs) max_records += sg->num_docs;
+    const size_t scan_tmp = exclusive_sum_u32(nullptr, nullptr, (long long)hist_n, nullptr, 0, e.stream);
+    const size_t hist_b = (hist_n * 4 + 255) / 256 * 256, pstart_b = ((size_t)gp.P * 4 + 4 + 255) / 256 * 256;
+    e.group_part.reserve(2 * hist_b + pstart_b + scan_tmp + 256);
+    uint8_t *pb = e.group_part.get<uint8_t>();
+    auto *hist = reinterpret_cast<uint32_t *>(pb);
+    auto *offsets = reinterpret_cast<uint32_t *>(pb + hist_b);
+    auto *pstart = reinterpret_cast<uint32_t *>(pb + 2 * hist_b);
+    void *tmp = pb + 2 * hist_b + pstart_b;
+    require(max_records < (int64_t)UINT32_MAX, PINOT_ERR_UNSUPPORTED, "partitioned group-by over > 4G docs per GPU");
+    e.group_records.reserve((size_t)max_records * 8 + 64);
+    a.hist = hist;
+    a.offsets = offsets;
+    a.emit = e.group_records.get<unsigned long long>();
+    PartitionReduceArgs ra{};
+    ra.records = a.emit;
+    ra.pstart = pstart;
+    ra.P = (int32_t)gp.P;
+    ra.shift = gp.shift;
+    ra.n_aggs = na;
+    ra.lds_bytes = gp.reduce_bytes;
+    ra.G = ks.G;
+    ra.counts = counts;
+    for (int i = 0; i < na; i++) {
+      ra.aggs[i] = gaggs[i];  // segment 0's dictionary / LUT: identical on every segment (checked)
+      ra.aggs[i].lds_off = gp.reduce_off[i];
+    }
+    t.timed(1, [&] {
+      launch_group_query(a, e.stream);
+      exclusive_sum_u32(hist, offsets, (long long)hist_n, tmp, scan_tmp, e.stream);
+      launch_partition_starts(offsets, hist, (int32_t)gp.P, (int32_t)nblk, pstart, e.stream);
+      GroupArgs a2 = a;
+      a2.mode = GB_EMIT;
+      launch_group_query(a2, e.stream);
+      launch_partition_reduce(ra, e.stream);
+    });
+    PINOT_HIP(hipGetLastError());
+  }
+
+  // finalize: ordered non-empty keys, per-group outputs, one D2H
+  const size_t cscr = compact_keys_scratch_bytes(ks.G);
+  e.group_final.reserve(ks.G * 8 + 64 + cscr);
+  auto *keys_dev = e.group_final.get<long long>();
+  auto *n_dev = reinterpret_cast<unsigned long long *>(e.group_final.get<uint8_t>() + ks.G * 8);
+  launch_compact_keys_ordered(ks.G, counts, keys_dev, n_dev, e.group_final.get<uint8_t>() + ks.G * 8 + 64, cscr,
+                              e.stream);
+  PINOT_HIP(hipGetLastError());
+  std::vector<unsigned long long> hmatched(S);
+  unsigned long long n = 0;
+  PINOT_HIP(hipMemcpyAsync(&n, n_dev, 8, hipMemcpyDeviceToHost, e.stream));
+  PINOT_HIP(hipMemcpyAsync(hmatched.data(), matched, S * 8, hipMemcpyDeviceToHost, e.stream));
+  PINOT_HIP(hipStreamSynchronize(e.stream));
+  int n_hll = 0;
+  for (int i = 0; i < na; i++) n_hll += ga.acc_kind[i] == 4;
+  auto res = std::make_unique<GroupByResult>();
+  res->num_columns = q.num_group_by;
+  res->functions.resize(na);
+  for (int i = 0; i < na; i++) res->functions[i] = q.aggregations[i].function;
+  res->counts.assign(na, {});
+  res->values.assign(na, {});
+  res->hll.assign(na, {});
+  res->hll_card.assign(na, {});
+  res->hll_dev_off.assign(na, 0);
+  res->gvalues = ks.gvalues;
+  res->gcard = ks.gcard;
+  res->device = e.device;
+  if (n) {
+    const size_t out_b = n * 8 * (1 + na) + (size_t)n_hll * n * 12 + 64;
+    DeviceBuffer out(out_b);
+    auto *o_cnt = out.get<unsigned long long>();
+    auto *o_acc = o_cnt + n;
+    auto *o_hs = o_acc + n * na;
+    auto *o_hz = reinterpret_cast<uint32_t *>(o_hs + (size_t)n_hll * n);
+    launch_group_outputs(counts, gaggs.data(), na, keys_dev, (long long)n, o_cnt, o_acc, o_hs, o_hz, e.stream);
+    PINOT_HIP(hipGetLastError());
+    if (n_hll) {
+      res->hll_dev = std::make_shared<DeviceBuffer>((size_t)n_hll * n * 256 + 16);
+      int h = 0;
+      for (int i = 0; i < na; i++)
+        if (ga.acc_kind[i] == 4) {
+          res->hll_dev_off[i] = (size_t)h * n * 256;
+          launch_gather_hll(static_cast<const uint8_t *>(accs[i]), keys_dev, (long long)n,
+                            res->hll_dev->get<uint8_t>() + res->hll_dev_off[i], e.stream);
+          h++;
+        }
+      PINOT_HIP(hipGetLastError());
+    }
+    std::vector<uint8_t> host(out_b);
+    res->raw_keys.resize(n);
+    PINOT_HIP(hipMemcpyAsync(res->raw_keys.data(), keys_dev, n * 8, hipMemcpyDeviceToHost, e.stream));
+    PINOT_HIP(hipMemcpyAsync(host.data(), out.get(), out_b, hipMemcpyDeviceToHost, e.stream));
+    PINOT_HIP(hipStreamSynchronize(e.stream));
+    const auto *hc = reinterpret_cast<const unsigned long long *>(host.data());
+    const auto *hacc = hc + n;
+    const auto *hhs = hacc + n * na;
+    const auto *hhz = reinterpret_cast<const uint32_t *>(hhs + (size_t)n_hll * n);
+    int h = 0;
+    for (int i = 0; i < na; i++) {
+      auto &cv = res->counts[i];
+      auto &vv = res->values[i];
+      cv.resize(n);
+      vv.resize(n);
+      const int ak = ga.acc_kind[i];
+      if (ak == 4) res->hll_card[i].resize(n);
+      for (size_t g = 0; g < n; g++) {
+        cv[g] = (int64_t)hc[g];
+        const uint64_t raw = hacc[(size_t)i * n + g];
+        switch (ak) {
+          case 0: vv[g] = (double)(int64_t)raw; break;
+          case 1: { double d; memcpy(&d, &raw, 8); vv[g] = d; break; }
+          case 2:
+          case 3: vv[g] = decode_ordered(raw); break;
+          case 4: {
+            const int64_t c = hll_cardinality_from_sum(hhs[(size_t)h * n + g], hhz[(size_t)h * n + g]);
+            res->hll_card[i][g] = c;
+            vv[g] = (double)c;
+            break;
+          }
+          default: vv[g] = (double)hc[g]; break;
+        }
+      }
+      if (ak == 4) h++;
+    }
+  }
+  PINOT_HIP(hipEventRecord(e.ev_stop, e.stream));
+  PINOT_HIP(hipStreamSynchronize(e.stream));
+  float ms = 0;
+  PINOT_HIP(hipEventElapsedTime(&ms, e.ev_start, e.ev_stop));
+  t.collect();
+  std::vector<int64_t> seg_counts(S);
+  for (size_t si = 0; si < S; si++) seg_counts[si] = plans[si].empty ? 0 : (int64_t)hmatched[si];
+  fill_stats(q, plans, seg_counts, ms, stats);
+  return res;
+}
+
 std::unique_ptr<GroupByResult> exec_group_by(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q,
                                              pinot_exec_stats *stats) {
+  const int na = q.num_aggregations;
+  require(na >= 1 && na <= kMaxAggs, PINOT_ERR_UNSUPPORTED, "1..8 aggregation functions per query");
+  require(q.num_group_by >= 1 && q.num_group_by <= kMaxGroupCols, PINOT_ERR_UNSUPPORTED, "1..16 group-by columns");
+  if (e.use_fused && !needs_admission(segs, q, e)) {
+    KeySpace ks = build_key_space(segs, q);
+    GroupAccs ga = group_acc_kinds(*segs[0], q);
+    return exec_group_by_fused(e, segs, q, ks, ga, stats);
+  }
+  return exec_group_by_legacy(e, segs, q, stats);
+}
+
+std::unique_ptr<GroupByResult> exec_group_by_legacy(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q,
+                                                    pinot_exec_stats *stats) {
   const int na = q.num_aggregations;
   require(na >= 1 && na <= kMaxAggs, PINOT_ERR_UNSUPPORTED, "1..8 aggregation functions per query");
   require(q.num_group_by >= 1 && q.num_group_by <= kMaxGroupCols, PINOT_ERR_UNSUPPORTED, "1..8 group-by columns");

@@ -375,10 +375,11 @@ __device__ __forceinline__ unsigned long long eval_chunk(const FusedStep *__rest
   return cnt;
 }
 
-__device__ __forceinline__ uint64_t chunk_word(const FusedSegment &sg, int64_t ch, int lane) {
+__device__ __forceinline__ uint64_t chunk_word(const uint64_t *pre, int64_t nwords, int32_t num_docs, int64_t ch,
+                                               int lane) {
   const int64_t w = ch * 64 + lane;
-  if (w >= sg.nwords) return 0;
-  return (sg.pre ? sg.pre[w] : ~0ull) & tail_mask(w, sg.nwords, sg.num_docs);
+  if (w >= nwords) return 0;
+  return (pre ? pre[w] : ~0ull) & tail_mask(w, nwords, num_docs);
 }
 
 // Stepwise shape: per chunk, each step's column is staged into the wave's single LDS stage and
@@ -404,7 +405,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G ? 2 : 
   init_acc(A);
   const int64_t nchunks = (sg.nwords + 63) >> 6;
   for (int64_t ch = (int64_t)b * kFusedWaves + wave; ch < nchunks; ch += (int64_t)a.bps * kFusedWaves) {
-    cnt += eval_chunk<G>(steps, sg.n_leaves, sg.n_folds, chunk_word(sg, ch, lane), A, hll, lane,
+    cnt += eval_chunk<G>(steps, sg.n_leaves, sg.n_folds, chunk_word(sg.pre, sg.nwords, sg.num_docs, ch, lane), A, hll, lane,
                          [&](int, const FusedStep &st) -> const uint8_t * {
                            stage_chunk_rt(st.fwd, st.bits, ch, lds_wave, lane);
                            wait_stage();
@@ -489,6 +490,260 @@ __global__ __launch_bounds__(kBlock) void k_scan_query_pipe(FusedArgs a) {
   flush_block(a, stage_lds, hll, A, cnt, g, tid, lane, wave);
 }
 
+// ======================================================================== fused group-by
+// k_group_query: the filter of k_scan_query (stepwise leaves over LDS-staged chunks) followed, per
+// 64-doc word of the chunk, by one-doc-per-lane key / dictId reads straight from the packed streams
+// (a wave's 64 lanes read the 8*b contiguous bytes of the word: coalesced) and a sink (GroupMode).
+// Restates DictionaryBasedGroupKeyGenerator.getGroupKey / processSingleValue (raw key = fold of
+// key * card_j + dictId_j; PC/query/aggregation/groupby/DictionaryBasedGroupKeyGenerator.java:195-302)
+// and DefaultGroupByExecutor.process (PC/query/aggregation/groupby/DefaultGroupByExecutor.java:70-168).
+constexpr int kGroupBlock = 1024;                // 16 waves: the per-doc reads are latency-bound
+constexpr int kGroupWaves = kGroupBlock / 64;
+constexpr int kGroupUnroll = 4;                  // words whose reads are in flight together
+
+__device__ __forceinline__ uint32_t decode_doc(const uint8_t *__restrict__ fwd, int bits, int64_t doc) {
+  const uint64_t bitpos = (uint64_t)doc * (uint32_t)bits;
+  const uint32_t *p = reinterpret_cast<const uint32_t *>(fwd) + (bitpos >> 5);
+  const uint64_t x = ((uint64_t)bswap32(p[0]) << 32) | bswap32(p[1]);
+  return (uint32_t)((x << (bitpos & 31)) >> (64 - bits));
+}
+
+__device__ __forceinline__ unsigned long long ordered_bits(double d) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(d);
+  return (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
+}
+
+__device__ __forceinline__ double dict_value(const void *dict, int value_kind, uint32_t id) {
+  switch (value_kind) {
+    case 0: return (double)static_cast<const int32_t *>(dict)[id];
+    case 1: return (double)static_cast<const long long *>(dict)[id];
+    default: return static_cast<const double *>(dict)[id];
+  }
+}
+
+// HLL registers are bytes in HBM ([G][256] u8): max via CAS on the containing dword (low contention).
+__device__ __forceinline__ void hll_max_u8(uint8_t *regs, long long idx, uint32_t rank) {
+  uint32_t *word = reinterpret_cast<uint32_t *>(regs + (idx & ~3ll));
+  const int sh = (int)(idx & 3) * 8;
+  uint32_t old = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  while (((old >> sh) & 0xFFu) < rank) {
+    const uint32_t nv = (old & ~(0xFFu << sh)) | (rank << sh);
+    const uint32_t seen = atomicCAS(word, old, nv);
+    if (seen == old) break;
+    old = seen;
+  }
+}
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+  const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)v, l);
+  const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// One aggregated value into accumulator `acc` at index k (global or LDS address space by pointer).
+template <bool LDS>
+__device__ __forceinline__ void agg_update(const GroupAggDev &ag, void *acc, long long k, uint32_t id) {
+  switch (ag.acc_kind) {
+    case 0:
+      atomicAdd(static_cast<unsigned long long *>(acc) + k,
+                (unsigned long long)(long long)static_cast<const int32_t *>(ag.dict)[id]);
+      break;
+    case 1:
+      atomicAdd(static_cast<double *>(acc) + k, dict_value(ag.dict, ag.value_kind, id));
+      break;
+    case 2:
+      atomicMin(static_cast<unsigned long long *>(acc) + k, ordered_bits(dict_value(ag.dict, ag.value_kind, id)));
+      break;
+    case 3:
+      atomicMax(static_cast<unsigned long long *>(acc) + k, ordered_bits(dict_value(ag.dict, ag.value_kind, id)));
+      break;
+    case 4: {
+      const uint32_t e = ag.hll_lut[id];
+      if constexpr (LDS) atomicMax(static_cast<uint32_t *>(acc) + k * 256 + (e >> 8), e & 0xFFu);
+      else hll_max_u8(static_cast<uint8_t *>(acc), k * 256 + (e >> 8), e & 0xFFu);
+      break;
+    }
+    default:
+      break;
+  }
+}
+
+template <int MODE>
+__device__ __forceinline__ void group_chunk(const GroupArgs &a, const GroupSegment &sg, int64_t ch, uint64_t mask,
+                                            int lane, uint8_t *acc_lds, uint32_t *plds) {
+  for (int w0 = 0; w0 < 64; w0 += kGroupUnroll) {
+    uint64_t mw[kGroupUnroll];
+    bool any = false;
+#pragma unroll
+    for (int u = 0; u < kGroupUnroll; u++) {
+      mw[u] = readlane64(mask, w0 + u);
+      any = any || mw[u] != 0;
+    }
+    if (!any) continue;  // uniform
+    int64_t doc[kGroupUnroll];
+    unsigned long long key[kGroupUnroll];
+    bool act[kGroupUnroll];
+#pragma unroll
+    for (int u = 0; u < kGroupUnroll; u++) {
+      doc[u] = ((ch << 6) + w0 + u) * 64 + lane;
+      key[u] = 0;
+      act[u] = (mw[u] >> lane) & 1ull;
+    }
+    for (int j = 0; j < a.n_gcols; j++) {
+      const GroupColDev gc = load_const(a.gcols + sg.first_gcol + j);
+      uint32_t id[kGroupUnroll];
+#pragma unroll
+      for (int u = 0; u < kGroupUnroll; u++) id[u] = act[u] ? decode_doc(gc.fwd, gc.bits, doc[u]) : 0u;
+#pragma unroll
+      for (int u = 0; u < kGroupUnroll; u++) {
+        const uint32_t gid = (gc.remap && act[u]) ? (uint32_t)gc.remap[id[u]] : id[u];
+        key[u] += (unsigned long long)gid * (unsigned long long)gc.stride;
+      }
+    }
+    if (a.admitted) {
+#pragma unroll
+      for (int u = 0; u < kGroupUnroll; u++)
+        act[u] = act[u] && ((a.admitted[key[u] >> 5] >> (key[u] & 31)) & 1u);
+    }
+    if constexpr (MODE == GB_COUNT) {
+#pragma unroll
+      for (int u = 0; u < kGroupUnroll; u++)
+        if (act[u]) atomicAdd(&plds[key[u] >> a.shift], 1u);
+    } else if constexpr (MODE == GB_EMIT) {
+      unsigned long long rec[kGroupUnroll];
+#pragma unroll
+      for (int u = 0; u < kGroupUnroll; u++) rec[u] = key[u] & ((1ull << a.shift) - 1ull);
+      for (int g = 0; g < a.n_aggs; g++) {
+        const GroupAggDev ag = load_const(a.aggs + sg.first_agg + g);
+        if (ag.acc_kind == 5) continue;
+#pragma unroll
+        for (int u = 0; u < kGroupUnroll; u++)
+          if (act[u]) rec[u] |= (unsigned long long)decode_doc(ag.fwd, ag.bits, doc[u]) << ag.field_shift;
+      }
+#pragma unroll
+      for (int u = 0; u < kGroupUnroll; u++)
+        if (act[u]) {
+          const uint32_t pos = atomicAdd(&plds[key[u] >> a.shift], 1u);
+          __builtin_nontemporal_store(rec[u], a.emit + pos);
+        }
+    } else {
+      unsigned long long *cnt_g = a.counts;
+      uint32_t *cnt_l = reinterpret_cast<uint32_t *>(acc_lds);
+#pragma unroll
+      for (int u = 0; u < kGroupUnroll; u++)
+        if (act[u]) {
+          if constexpr (MODE == GB_LDS) atomicAdd(cnt_l + key[u], 1u);
+          else atomicAdd(cnt_g + key[u], 1ull);
+        }
+      for (int g = 0; g < a.n_aggs; g++) {
+        const GroupAggDev ag = load_const(a.aggs + sg.first_agg + g);
+        if (ag.acc_kind == 5) continue;
+        uint32_t id[kGroupUnroll];
+#pragma unroll
+        for (int u = 0; u < kGroupUnroll; u++) id[u] = act[u] ? decode_doc(ag.fwd, ag.bits, doc[u]) : 0u;
+        void *acc = MODE == GB_LDS ? (void *)(acc_lds + ag.lds_off) : ag.acc;
+#pragma unroll
+        for (int u = 0; u < kGroupUnroll; u++)
+          if (act[u]) agg_update<MODE == GB_LDS>(ag, acc, (long long)key[u], id[u]);
+      }
+    }
+  }
+}
+
+// LDS accumulator identities (GB_LDS): counts 0, sums 0, min all-ones, max 0, HLL 0.
+__device__ __forceinline__ void init_group_lds(const GroupArgs &a, const GroupSegment &sg, uint8_t *acc_lds, int tid) {
+  uint32_t *w = reinterpret_cast<uint32_t *>(acc_lds);
+  for (int i = tid; i < a.lds_acc_bytes / 4; i += kGroupBlock) w[i] = 0;
+  __syncthreads();
+  for (int g = 0; g < a.n_aggs; g++) {
+    const GroupAggDev ag = load_const(a.aggs + sg.first_agg + g);
+    if (ag.acc_kind == 2) {
+      unsigned long long *m = reinterpret_cast<unsigned long long *>(acc_lds + ag.lds_off);
+      for (long long i = tid; i < a.G; i += kGroupBlock) m[i] = ~0ull;
+    }
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ void flush_group_lds(const GroupArgs &a, const GroupSegment &sg, uint8_t *acc_lds, int tid) {
+  __syncthreads();
+  const uint32_t *cnt = reinterpret_cast<const uint32_t *>(acc_lds);
+  for (long long k = tid; k < a.G; k += kGroupBlock) {
+    const uint32_t c = cnt[k];
+    if (!c) continue;
+    atomicAdd(a.counts + k, (unsigned long long)c);
+    for (int g = 0; g < a.n_aggs; g++) {
+      const GroupAggDev ag = load_const(a.aggs + sg.first_agg + g);
+      const uint8_t *src = acc_lds + ag.lds_off;
+      switch (ag.acc_kind) {
+        case 0:
+          atomicAdd(static_cast<unsigned long long *>(ag.acc) + k, reinterpret_cast<const unsigned long long *>(src)[k]);
+          break;
+        case 1:
+          atomicAdd(static_cast<double *>(ag.acc) + k, reinterpret_cast<const double *>(src)[k]);
+          break;
+        case 2:
+          atomicMin(static_cast<unsigned long long *>(ag.acc) + k, reinterpret_cast<const unsigned long long *>(src)[k]);
+          break;
+        case 3:
+          atomicMax(static_cast<unsigned long long *>(ag.acc) + k, reinterpret_cast<const unsigned long long *>(src)[k]);
+          break;
+        case 4:
+          for (int r = 0; r < 256; r++) {
+            const uint32_t v = reinterpret_cast<const uint32_t *>(src)[k * 256 + r];
+            if (v) hll_max_u8(static_cast<uint8_t *>(ag.acc), k * 256 + r, v);
+          }
+          break;
+        default:
+          break;
+      }
+    }
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kGroupBlock) void k_group_query(GroupArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = blockIdx.x / a.bps, b = blockIdx.x % a.bps;
+  const int nblk = a.nsegs * a.bps;
+  const GroupSegment sg = load_const(a.segs + g);
+  const FusedStep *leaves = a.leaves + sg.first_leaf;
+  uint8_t *stage = lds + wave * a.stage_bytes;
+  uint8_t *acc_lds = lds + (size_t)kGroupWaves * a.stage_bytes;
+  uint32_t *plds = reinterpret_cast<uint32_t *>(acc_lds);
+  if constexpr (MODE == GB_LDS) init_group_lds(a, sg, acc_lds, tid);
+  if constexpr (MODE == GB_COUNT) {
+    for (int p = tid; p < a.P; p += kGroupBlock) plds[p] = 0;
+    __syncthreads();
+  }
+  if constexpr (MODE == GB_EMIT) {
+    for (int p = tid; p < a.P; p += kGroupBlock) plds[p] = a.offsets[(size_t)p * nblk + blockIdx.x];
+    __syncthreads();
+  }
+  const int64_t nchunks = (sg.nwords + 63) >> 6;
+  unsigned long long matched = 0;
+  for (int64_t ch = (int64_t)b * kGroupWaves + wave; ch < nchunks; ch += (int64_t)a.bps * kGroupWaves) {
+    uint64_t mask = chunk_word(sg.pre, sg.nwords, sg.num_docs, ch, lane);
+    for (int i = 0; i < sg.n_leaves; i++) {
+      if (!__any(mask != 0)) break;
+      const FusedStep st = load_const(leaves + i);
+      stage_chunk_rt(st.fwd, st.bits, ch, stage, lane);
+      wait_stage();
+      leaf_rt<true>(st, stage + lane * (8 * st.bits), mask);
+    }
+    matched += __popcll(mask);
+    if (__any(mask != 0)) group_chunk<MODE>(a, sg, ch, mask, lane, acc_lds, plds);
+  }
+  matched = wave_sum(matched);
+  if (lane == 0 && matched) atomicAdd(a.matched + g, matched);
+  if constexpr (MODE == GB_LDS) flush_group_lds(a, sg, acc_lds, tid);
+  if constexpr (MODE == GB_COUNT) {
+    __syncthreads();
+    for (int p = tid; p < a.P; p += kGroupBlock) a.hist[(size_t)p * nblk + blockIdx.x] = plds[p];
+  }
+}
+
 }  // namespace
 
 int scan_query_blocks_per_cu(int stage_bytes, bool gathers, bool pipelined) {
@@ -523,5 +778,37 @@ void launch_scan_query(const FusedArgs &a, bool gathers, bool pipelined, hipStre
   }
 }
 
+
+size_t group_query_lds_bytes(const GroupArgs &a) {
+  size_t acc = 0;
+  if (a.mode == GB_LDS) acc = (size_t)a.lds_acc_bytes;
+  if (a.mode == GB_COUNT || a.mode == GB_EMIT) acc = (size_t)a.P * 4;
+  return (size_t)kGroupWaves * a.stage_bytes + acc;
+}
+
+int group_query_blocks_per_cu(const GroupArgs &a) {
+  int n = 0;
+  const size_t lds = group_query_lds_bytes(a);
+  hipError_t err = hipErrorInvalidValue;
+  switch (a.mode) {
+    case GB_GLOBAL: err = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_group_query<GB_GLOBAL>, kGroupBlock, lds); break;
+    case GB_LDS: err = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_group_query<GB_LDS>, kGroupBlock, lds); break;
+    case GB_COUNT: err = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_group_query<GB_COUNT>, kGroupBlock, lds); break;
+    default: err = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_group_query<GB_EMIT>, kGroupBlock, lds); break;
+  }
+  return (err != hipSuccess || n < 1) ? 1 : n;
+}
+
+void launch_group_query(const GroupArgs &a, hipStream_t stream) {
+  if (a.nsegs <= 0 || a.bps <= 0) return;
+  const dim3 grid((unsigned)(a.nsegs * a.bps)), block(kGroupBlock);
+  const size_t lds = group_query_lds_bytes(a);
+  switch (a.mode) {
+    case GB_GLOBAL: hipLaunchKernelGGL(k_group_query<GB_GLOBAL>, grid, block, lds, stream, a); break;
+    case GB_LDS: hipLaunchKernelGGL(k_group_query<GB_LDS>, grid, block, lds, stream, a); break;
+    case GB_COUNT: hipLaunchKernelGGL(k_group_query<GB_COUNT>, grid, block, lds, stream, a); break;
+    default: hipLaunchKernelGGL(k_group_query<GB_EMIT>, grid, block, lds, stream, a); break;
+  }
+}
 
 }  // namespace pinot

@@ -1,0 +1,250 @@
+// Group-by back half (gfx950): per-partition reduction of the partitioned plan, ordered compaction of
+// the non-empty keys, and the per-group outputs the host finalises.
+//
+//   k_partition_reduce   one block owns one partition (2^shift consecutive raw keys): its records
+//                        (local key | aggregated dictIds) are folded into LDS accumulators (count,
+//                        int64 / double sums, ordered min/max, HLL registers), then written to the
+//                        dense HBM accumulators with plain stores — no HBM atomics (the keys are the
+//                        partition's alone). Restates DefaultGroupByExecutor.process + the
+//                        aggregateGroupBySV loops (PC/query/aggregation/groupby/DefaultGroupByExecutor.java:70-168).
+//   k_key_flags / k_key_scatter   counts != 0 -> ordered key list (exclusive scan in between), i.e. the
+//                        raw keys in ascending order (GroupKeyGenerator.getUniqueGroupKeys, sorted).
+//   k_group_outputs      per non-empty group: count, each 8-byte accumulator, and for HLL the exact
+//                        fixed-point Σ 2^(32 - register) and the zero-register count, from which the host
+//                        evaluates HyperLogLog.cardinality() bit-identically (the double sum of
+//                        1.0 / (1 << reg) is exact: <= 256 terms of >= 2^-25).
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include "common.h"
+#include "device.h"
+#include "kernels.h"
+
+namespace pinot {
+namespace {
+using namespace dev;
+
+constexpr int kReduceBlock = 512;
+
+__device__ __forceinline__ unsigned long long ordered_bits_r(double d) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(d);
+  return (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
+}
+
+__device__ __forceinline__ double dict_value_r(const void *dict, int value_kind, uint32_t id) {
+  switch (value_kind) {
+    case 0: return (double)static_cast<const int32_t *>(dict)[id];
+    case 1: return (double)static_cast<const long long *>(dict)[id];
+    default: return static_cast<const double *>(dict)[id];
+  }
+}
+
+__global__ __launch_bounds__(kReduceBlock) void k_partition_reduce(PartitionReduceArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int tid = threadIdx.x;
+  const int p = blockIdx.x;
+  const int K = 1 << a.shift;
+  uint32_t *cnt = reinterpret_cast<uint32_t *>(lds);
+  for (int i = tid; i < a.lds_bytes / 4; i += kReduceBlock) reinterpret_cast<uint32_t *>(lds)[i] = 0;
+  __syncthreads();
+  for (int g = 0; g < a.n_aggs; g++)
+    if (a.aggs[g].acc_kind == 2) {
+      unsigned long long *m = reinterpret_cast<unsigned long long *>(lds + a.aggs[g].lds_off);
+      for (int i = tid; i < K; i += kReduceBlock) m[i] = ~0ull;
+    }
+  __syncthreads();
+  const uint32_t b = a.pstart[p], e = a.pstart[p + 1];
+  const unsigned long long kmask = (unsigned long long)K - 1ull;
+  for (uint32_t r = b + tid; r < e; r += kReduceBlock) {
+    const unsigned long long rec = __builtin_nontemporal_load(a.records + r);
+    const uint32_t k = (uint32_t)(rec & kmask);
+    atomicAdd(cnt + k, 1u);
+#pragma unroll
+    for (int g = 0; g < kMaxGroupAggs; g++) {
+      if (g >= a.n_aggs) break;
+      const GroupAggDev &ag = a.aggs[g];
+      if (ag.acc_kind == 5) continue;
+      const uint32_t id = (uint32_t)((rec >> ag.field_shift) & ((1ull << ag.bits) - 1ull));
+      uint8_t *acc = lds + ag.lds_off;
+      switch (ag.acc_kind) {
+        case 0:
+          atomicAdd(reinterpret_cast<unsigned long long *>(acc) + k,
+                    (unsigned long long)(long long)static_cast<const int32_t *>(ag.dict)[id]);
+          break;
+        case 1:
+          atomicAdd(reinterpret_cast<double *>(acc) + k, dict_value_r(ag.dict, ag.value_kind, id));
+          break;
+        case 2:
+          atomicMin(reinterpret_cast<unsigned long long *>(acc) + k,
+                    ordered_bits_r(dict_value_r(ag.dict, ag.value_kind, id)));
+          break;
+        case 3:
+          atomicMax(reinterpret_cast<unsigned long long *>(acc) + k,
+                    ordered_bits_r(dict_value_r(ag.dict, ag.value_kind, id)));
+          break;
+        case 4: {
+          const uint32_t h = ag.hll_lut[id];
+          atomicMax(reinterpret_cast<uint32_t *>(acc) + k * 256 + (h >> 8), h & 0xFFu);
+          break;
+        }
+        default:
+          break;
+      }
+    }
+  }
+  __syncthreads();
+  const long long base = (long long)p * K;
+  for (int i = tid; i < K; i += kReduceBlock) {
+    const long long key = base + i;
+    if (key >= a.G) break;
+    a.counts[key] = cnt[i];
+  }
+  for (int g = 0; g < a.n_aggs; g++) {
+    const GroupAggDev &ag = a.aggs[g];
+    if (ag.acc_kind == 5) continue;
+    const uint8_t *acc = lds + ag.lds_off;
+    if (ag.acc_kind == 4) {
+      uint8_t *out = static_cast<uint8_t *>(ag.acc);
+      for (int i = tid; i < K * 256; i += kReduceBlock) {
+        const long long key = base + i / 256;
+        if (key < a.G) out[base * 256 + i] = (uint8_t)reinterpret_cast<const uint32_t *>(acc)[i];
+      }
+    } else {
+      unsigned long long *out = static_cast<unsigned long long *>(ag.acc);
+      for (int i = tid; i < K; i += kReduceBlock) {
+        const long long key = base + i;
+        if (key < a.G) out[key] = reinterpret_cast<const unsigned long long *>(acc)[i];
+      }
+    }
+  }
+}
+
+__global__ void k_key_flags(long long G, const unsigned long long *__restrict__ counts, uint32_t *flags) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < G; i += (long long)gridDim.x * blockDim.x)
+    flags[i] = counts[i] != 0 ? 1u : 0u;
+}
+
+__global__ void k_key_scatter(long long G, const uint32_t *__restrict__ flags, const uint32_t *__restrict__ pos,
+                              long long *keys, unsigned long long *n_out) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < G; i += (long long)gridDim.x * blockDim.x) {
+    if (flags[i]) keys[pos[i]] = i;
+    if (i == G - 1) *n_out = (unsigned long long)pos[i] + flags[i];
+  }
+}
+
+struct OutputAggs {
+  GroupAggDev aggs[kMaxGroupAggs];
+  int n;
+};
+
+__global__ void k_group_outputs(const unsigned long long *__restrict__ counts, OutputAggs oa,
+                                const long long *__restrict__ keys, long long n, unsigned long long *out_counts,
+                                unsigned long long *out_acc, unsigned long long *out_hll_sum, uint32_t *out_hll_zeros) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const long long k = keys[i];
+    out_counts[i] = counts[k];
+    int h = 0;
+    for (int g = 0; g < oa.n; g++) {
+      const GroupAggDev &ag = oa.aggs[g];
+      if (ag.acc_kind == 4) {
+        const u32x4 *r = reinterpret_cast<const u32x4 *>(static_cast<const uint8_t *>(ag.acc) + k * 256);
+        unsigned long long s = 0;
+        uint32_t z = 0;
+        for (int q = 0; q < 16; q++) {
+          const u32x4 v = r[q];
+          const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int c = 0; c < 4; c++)
+#pragma unroll
+            for (int bb = 0; bb < 4; bb++) {
+              const uint32_t reg = (w[c] >> (8 * bb)) & 0xFFu;
+              s += 1ull << (32 - reg);
+              z += reg == 0;
+            }
+        }
+        out_hll_sum[(long long)h * n + i] = s;
+        out_hll_zeros[(long long)h * n + i] = z;
+        h++;
+      } else if (ag.acc_kind != 5) {
+        out_acc[(long long)g * n + i] = static_cast<const unsigned long long *>(ag.acc)[k];
+      }
+    }
+  }
+}
+
+__global__ void k_partition_starts(const uint32_t *__restrict__ offsets, const uint32_t *__restrict__ hist, int32_t P,
+                                   int32_t nblk, uint32_t *pstart) {
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p <= P; p += gridDim.x * blockDim.x) {
+    if (p < P) pstart[p] = offsets[(size_t)p * nblk];
+    else pstart[P] = offsets[(size_t)P * nblk - 1] + hist[(size_t)P * nblk - 1];
+  }
+}
+
+__global__ void k_gather_hll(const uint8_t *__restrict__ regs, const long long *__restrict__ keys, long long n,
+                             uint8_t *__restrict__ out) {
+  // one 16-B piece per thread: 16 pieces per group
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n * 16; i += (long long)gridDim.x * blockDim.x) {
+    const long long g = i >> 4, q = i & 15;
+    reinterpret_cast<u32x4 *>(out)[i] = reinterpret_cast<const u32x4 *>(regs + keys[g] * 256)[q];
+  }
+}
+
+}  // namespace
+
+void launch_partition_starts(const uint32_t *offsets, const uint32_t *hist, int32_t P, int32_t nblk, uint32_t *pstart,
+                             hipStream_t stream) {
+  if (P <= 0) return;
+  hipLaunchKernelGGL(k_partition_starts, dim3((P + 256) / 256), dim3(256), 0, stream, offsets, hist, P, nblk, pstart);
+}
+
+void launch_gather_hll(const uint8_t *regs, const long long *keys, long long n, uint8_t *out, hipStream_t stream) {
+  if (n <= 0) return;
+  const int grid = (int)std::min<long long>((n * 16 + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_gather_hll, dim3(grid), dim3(256), 0, stream, regs, keys, n, out);
+}
+
+void launch_partition_reduce(const PartitionReduceArgs &a, hipStream_t stream) {
+  if (a.P <= 0) return;
+  hipLaunchKernelGGL(k_partition_reduce, dim3((unsigned)a.P), dim3(kReduceBlock), (size_t)a.lds_bytes, stream, a);
+}
+
+size_t exclusive_sum_u32(const uint32_t *in, uint32_t *out, long long n, void *tmp, size_t tmp_bytes,
+                         hipStream_t stream) {
+  size_t need = 0;
+  PINOT_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, need, in, out, (int)n, stream));
+  if (!tmp) return need;
+  PINOT_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, in, out, (int)n, stream));
+  return need;
+}
+
+size_t compact_keys_scratch_bytes(long long G) {
+  const size_t flags = ((size_t)G * 4 + 255) / 256 * 256;
+  return 2 * flags + exclusive_sum_u32(nullptr, nullptr, G, nullptr, 0, nullptr) + 256;
+}
+
+void launch_compact_keys_ordered(long long G, const unsigned long long *counts, long long *keys_out,
+                                 unsigned long long *n_out, void *scratch, size_t scratch_bytes, hipStream_t stream) {
+  if (G <= 0) return;
+  const size_t flags_b = ((size_t)G * 4 + 255) / 256 * 256;
+  uint32_t *flags = static_cast<uint32_t *>(scratch);
+  uint32_t *pos = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(scratch) + flags_b);
+  uint8_t *tmp = static_cast<uint8_t *>(scratch) + 2 * flags_b;
+  const int grid = (int)std::min<long long>((G + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_key_flags, dim3(grid), dim3(256), 0, stream, G, counts, flags);
+  exclusive_sum_u32(flags, pos, G, tmp, scratch_bytes - 2 * flags_b, stream);
+  hipLaunchKernelGGL(k_key_scatter, dim3(grid), dim3(256), 0, stream, G, flags, pos, keys_out, n_out);
+}
+
+void launch_group_outputs(const unsigned long long *counts, const GroupAggDev *aggs_host, int n_aggs, const long long *keys,
+                          long long n, unsigned long long *out_counts, unsigned long long *out_acc,
+                          unsigned long long *out_hll_sum, uint32_t *out_hll_zeros, hipStream_t stream) {
+  if (n <= 0) return;
+  OutputAggs oa{};
+  oa.n = n_aggs;
+  for (int g = 0; g < n_aggs && g < kMaxGroupAggs; g++) oa.aggs[g] = aggs_host[g];
+  const int grid = (int)std::min<long long>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_group_outputs, dim3(grid), dim3(256), 0, stream, counts, oa, keys, n, out_counts, out_acc,
+                     out_hll_sum, out_hll_zeros);
+}
+
+}  // namespace pinot

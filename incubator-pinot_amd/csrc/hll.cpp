@@ -83,4 +83,15 @@ int64_t hll_cardinality(const uint8_t *regs) {
   return static_cast<int64_t>(std::floor(x + 0.5));
 }
 
+int64_t hll_cardinality_from_sum(unsigned long long sum_fixed32, uint32_t zeros) {
+  const double m = 256.0;
+  const double alpha_mm = (0.7213 / (1.0 + 1.079 / m)) * m * m;
+  const double sum = std::ldexp((double)sum_fixed32, -32);  // exact: the register loop's double sum
+  const double estimate = alpha_mm * (1.0 / sum);
+  double x = estimate;
+  if (estimate <= 2.5 * m) x = zeros > 0 ? m * std::log(m / (double)zeros) : INFINITY;
+  if (std::isinf(x)) return INT64_MAX;
+  return static_cast<int64_t>(std::floor(x + 0.5));
+}
+
 }  // namespace pinot

@@ -13,12 +13,12 @@
 
 namespace pinot {
 
-constexpr int kMaxProgramColumns = 16;
+constexpr int kMaxProgramColumns = 24;
 constexpr int kMaxProgramInstr = 48;
 constexpr int kMaxStack = 8;
 constexpr int kMaxAggs = 8;
 constexpr int kMaxHll = 4;
-constexpr int kMaxGroupCols = 8;
+constexpr int kMaxGroupCols = 16;
 constexpr int kBlock = 256;
 
 struct DevColumn {
@@ -157,6 +157,104 @@ constexpr int kMaxPipeSlotBytes = 18 * 1024 + kPipePreBytes;
 void launch_scan_query(const FusedArgs &a, bool gathers, bool pipelined, hipStream_t stream);
 // Resident blocks of k_scan_query per CU for a stage size (occupancy API), cached.
 int scan_query_blocks_per_cu(int stage_bytes, bool gathers, bool pipelined);
+
+// ---------------------------------------------------------------- fused group-by (fused.hip)
+// ONE launch per group-by query over every segment on the GPU: the filter leaves are evaluated exactly
+// as in k_scan_query (LDS-staged chunks, register masks, `pre` bitsets), then every matching doc's raw
+// group key (mixed radix over the global ids of the group columns) and aggregated dictIds are read
+// straight from the packed forward indexes (one doc per lane: the 64 lanes of a wave read 8*b
+// contiguous bytes per column) and handed to a sink:
+//   GB_GLOBAL  HBM atomics into dense per-key accumulators (medium key spaces)
+//   GB_LDS     LDS-privatised per-block accumulators, flushed with HBM atomics (small key spaces)
+//   GB_COUNT   pass 1 of the partitioned plan: per-block histogram of partitions (key >> shift)
+//   GB_EMIT    pass 2: (local key | dictId fields) u64 records scattered into partition runs;
+//              k_partition_reduce then owns one partition per block (accumulators in LDS, no atomics
+//              to HBM) — the large key spaces (config 4: 1 M keys with HLL)
+enum GroupMode : int32_t { GB_GLOBAL = 0, GB_LDS = 1, GB_COUNT = 2, GB_EMIT = 3 };
+// accumulator kinds (acc_kind): 0 int64 sum, 1 double sum, 2 ordered-u64 min, 3 ordered-u64 max,
+// 4 HLL registers (u8 [G][256]), 5 none (COUNT / AVG count share `counts`)
+constexpr int kMaxGroupAggs = 8;
+
+struct GroupColDev {
+  const uint8_t *fwd;
+  const int32_t *remap;      // dictId -> global id (null = identity)
+  long long stride;          // Π global cardinalities of the previous group columns
+  int32_t bits;
+  int32_t reserved;
+};
+
+struct GroupAggDev {
+  const uint8_t *fwd;
+  const void *dict;          // int32 / int64 / double dictionary values
+  const uint16_t *hll_lut;   // acc_kind 4: (register << 8 | rank) per dictId
+  void *acc;                 // dense global accumulator array
+  int32_t bits, acc_kind, value_kind;
+  int32_t field_shift;       // GB_EMIT: bit position of this column's dictId in the record
+  int32_t lds_off;           // GB_LDS / k_partition_reduce: byte offset of its LDS accumulator array
+  int32_t reserved;
+};
+
+struct GroupSegment {
+  const uint64_t *pre;       // AND-ed in before the leaves; null = all docs
+  int64_t nwords;            // 0 = skip (EMPTY filter)
+  int32_t num_docs;
+  int32_t first_leaf, n_leaves;
+  int32_t first_gcol, first_agg;
+  int32_t reserved;
+};
+
+struct GroupArgs {
+  const GroupSegment *segs;
+  const FusedStep *leaves;
+  const GroupColDev *gcols;
+  const GroupAggDev *aggs;
+  int32_t nsegs, bps, n_gcols, n_aggs;
+  int32_t mode, stage_bytes;  // stage: LDS bytes per wave for the leaves (1024 * ceil(max leaf bits / 2))
+  long long G;
+  unsigned long long *counts;  // u64 [G]
+  unsigned long long *matched; // u64 [nsegs]: docs passing the filter per segment (numDocsScanned)
+  const uint32_t *admitted;    // bitmap over keys (num.groups.limit), null = all
+  int32_t lds_acc_bytes;       // GB_LDS: per-block accumulator bytes (counts u32 [G] at 0, aggs at lds_off)
+  int32_t shift;               // GB_COUNT / GB_EMIT: partition = key >> shift, local key = low bits
+  int32_t P;                   // partitions
+  int32_t reserved;
+  uint32_t *hist;              // GB_COUNT: [P][nblk] per-block partition counts (partition-major)
+  const uint32_t *offsets;     // GB_EMIT: [P][nblk] exclusive record offsets
+  unsigned long long *emit;    // GB_EMIT: records
+};
+void launch_group_query(const GroupArgs &a, hipStream_t stream);
+// Grid (blocks per segment x segments) the host sizes `hist` / `offsets` for.
+int group_query_blocks_per_cu(const GroupArgs &a);
+size_t group_query_lds_bytes(const GroupArgs &a);
+
+struct PartitionReduceArgs {
+  const unsigned long long *records;
+  const uint32_t *pstart;      // [P + 1] first record of each partition
+  int32_t P, shift, n_aggs, lds_bytes;
+  long long G;
+  unsigned long long *counts;
+  GroupAggDev aggs[kMaxGroupAggs];  // fwd unused; dict / hll_lut / acc / lds_off / acc_kind / field_shift / bits
+};
+void launch_partition_reduce(const PartitionReduceArgs &a, hipStream_t stream);
+// pstart[p] = offsets[p * nblk] (partition-major exclusive offsets), pstart[P] = total records.
+void launch_partition_starts(const uint32_t *offsets, const uint32_t *hist, int32_t P, int32_t nblk, uint32_t *pstart,
+                             hipStream_t stream);
+// HLL registers of the listed keys: out[i * 256 + r] = regs[keys[i] * 256 + r].
+void launch_gather_hll(const uint8_t *regs, const long long *keys, long long n, uint8_t *out, hipStream_t stream);
+
+// Device finalize of dense accumulators: ordered list of the non-empty keys (flags + exclusive scan +
+// scatter; `scratch` holds 4 * (G + 1) bytes + the scan's temporary storage) and per-group outputs.
+size_t compact_keys_scratch_bytes(long long G);
+void launch_compact_keys_ordered(long long G, const unsigned long long *counts, long long *keys_out,
+                                 unsigned long long *n_out, void *scratch, size_t scratch_bytes, hipStream_t stream);
+// out_acc[a * n + i] = 8-byte accumulator of group i; HLL (acc_kind 4): out_hll_sum[h * n + i] = Σ 2^(32 - reg)
+// (exact), out_hll_zeros[h * n + i] = #zero registers.
+void launch_group_outputs(const unsigned long long *counts, const GroupAggDev *aggs_host, int n_aggs, const long long *keys,
+                          long long n, unsigned long long *out_counts, unsigned long long *out_acc,
+                          unsigned long long *out_hll_sum, uint32_t *out_hll_zeros, hipStream_t stream);
+// Exclusive prefix sum of n u32 (hipcub); returns the temporary storage it needs when tmp == null.
+size_t exclusive_sum_u32(const uint32_t *in, uint32_t *out, long long n, void *tmp, size_t tmp_bytes,
+                         hipStream_t stream);
 
 // Sorted-index leaf: ranges (inclusive [start, end], sorted, disjoint) -> bitset (combine mode as k_leaf).
 void launch_ranges_to_bitset(const int32_t *ranges, int32_t nranges, int64_t nwords, int32_t num_docs,

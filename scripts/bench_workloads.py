@@ -1,0 +1,92 @@
+#!/usr/bin/env python3
+"""Secondary BASELINE workloads on one GPU (the headline config 2 line is bench.py's).
+
+  --workload config4   high-cardinality group-by on the config-2 table:
+                       SELECT SUM(d8), AVG(d8), DISTINCTCOUNTHLL(d5) FROM t WHERE d2 < 800 GROUP BY d6, d7
+                       (1,000,000 keys; num.groups.limit = 1,000,000 so no group is dropped).
+                       Algorithmic bytes = N x (10 + 10 + 10 + 20 + 16) / 8 = 8.25 B/row.
+                       Self-check at full size: Σ group counts / Σ group sums == the aggregation-only
+                       COUNT(*) / SUM(d8) of the same filter (an independent kernel path).
+  --workload config3   multi-predicate AND/OR over sorted + bitmap inverted indexes (config 3):
+                       s0 sorted (card 1000), b1..b4 bitmap-indexed (card 10, 100, 1000, 10000), d8, m1:
+                       SELECT SUM(d8), MAX(m1) WHERE s0 IN (10..19) AND (b1 = 3 OR b2 IN (5,6,7)) AND b3 <> 0
+
+Prints one JSON line per workload (rows/s, ms/query, kernel times, roofline fraction)."""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "incubator-pinot_amd"))
+
+COLUMNS = [("d0", 16), ("d1", 100), ("d2", 1000), ("d3", 4096), ("d4", 10000), ("d5", 65536), ("d6", 1000),
+           ("d7", 1000), ("d8", 1 << 20), ("d9", 1000)]
+BASE_SEED = 0x5EED0000
+HBM_PEAK_GBS = 8000.0
+CONFIG4 = "SELECT SUM(d8), AVG(d8), DISTINCTCOUNTHLL(d5) FROM t WHERE d2 < 800 GROUP BY d6, d7 TOP 10"
+CONFIG4_CHECK = "SELECT COUNT(*), SUM(d8) FROM t WHERE d2 < 800"
+
+
+def timed(fn, steps, warmup):
+    for _ in range(warmup):
+        fn()
+    ms = []
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        r = fn()
+        ms.append((time.perf_counter() - t0) * 1e3)
+    return r, ms
+
+
+def config4(args, eng, ex):
+    segs = [eng.register_synthetic("fact_%d" % s, args.docs, COLUMNS, BASE_SEED + s) for s in range(args.segments)]
+    eng.synchronize()
+    ex.num_groups_limit = 1_000_000
+    q = ex.prepare(CONFIG4)
+    (res, st), ms = timed(lambda: ex.process_query(q, segs, trim=False), args.steps, args.warmup)
+    chk, _ = ex.process_query(ex.prepare(CONFIG4_CHECK), segs)
+    n_groups = len(res)
+    tot_cnt = sum(v[1].count for v in res.values())
+    tot_sum = sum(v[0] for v in res.values())
+    eng.set_config("timing=1")
+    ex.process_query(q, segs, trim=False)
+    k0 = eng.last_kernel_ms(0)
+    k1 = eng.last_kernel_ms(1)
+    eng.set_config("timing=0")
+    rows = args.segments * args.docs
+    p50 = float(np.median(ms))
+    alg = rows * 8.25
+    return {"workload": "config4", "query": CONFIG4, "segments": args.segments, "docs_per_segment": args.docs,
+            "value": rows / (p50 / 1e3), "unit": "rows/s", "p50_query_ms": p50, "p50_c_abi_ms": st.host_ms,
+            "groups": n_groups, "device_ms": st.device_ms,
+            "kernels": {"filter(kind0)": {"ms": k0[0], "launches": k0[1]}, "group_by(kind1)": {"ms": k1[0], "launches": k1[1]}},
+            "roofline": {"bound": "hbm", "algorithmic_bytes": alg, "achieved_query": alg / (p50 / 1e3) / 1e9,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac_query": alg / (p50 / 1e3) / 1e9 / HBM_PEAK_GBS},
+            "check": {"sum_group_counts": tot_cnt, "filtered_count": chk[0], "sum_group_sums": tot_sum,
+                      "filtered_sum": chk[1], "match": tot_cnt == chk[0] and tot_sum == chk[1] and n_groups == 1_000_000}}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="config4", choices=("config4",))
+    ap.add_argument("--segments", type=int, default=8)
+    ap.add_argument("--docs", type=int, default=125_000_000)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--engine-config", default="")
+    args = ap.parse_args()
+    import torch
+    torch.cuda.set_device(0)
+    from pinot_amd import GpuEngine, ServerQueryExecutor
+    eng = GpuEngine(0, args.engine_config or None)
+    ex = ServerQueryExecutor(eng)
+    out = config4(args, eng, ex)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

@@ -145,6 +145,11 @@ def test_kat_and_or_filter_operators(engine, kats, inverted):
 
 # ------------------------------------------------------------------ randomized parity vs the oracle
 def _random_segment(rng, n, name="seg", n_int=5, with_strings=True, sorted_col=True, double_col=True):
+    cols, inv = _random_columns(rng, n, n_int, with_strings, sorted_col, double_col)
+    return build_segment(name, cols, inverted_columns=tuple(inv))
+
+
+def _random_columns(rng, n, n_int=5, with_strings=True, sorted_col=True, double_col=True):
     cols = {}
     inv = []
     for i in range(n_int):
@@ -167,7 +172,7 @@ def _random_segment(rng, n, name="seg", n_int=5, with_strings=True, sorted_col=T
         inv.append("s")
     if sorted_col:
         cols["srt"] = ("INT", np.sort(rng.integers(0, max(2, n // 50), size=n)).tolist())
-    return build_segment(name, cols, inverted_columns=tuple(inv))
+    return cols, inv
 
 
 def _random_leaf(rng, seg):
@@ -272,6 +277,41 @@ def test_random_group_by(engine, seed):
                 _assert_same(a["function"], gv, ev, exact)
     for g in gsegs:
         g.release()
+
+
+GROUP_SINKS = ("group.mode=lds", "group.mode=global", "group.mode=partition")
+
+
+@pytest.mark.parametrize("mode", GROUP_SINKS)
+@pytest.mark.parametrize("seed", range(3))
+def test_group_by_sinks(mode, seed):
+    """Each fused group-by sink (LDS-private, HBM atomics, partitioned COUNT/EMIT/reduce) against the oracle,
+    over two segments with identical dictionaries (rows permuted) so the partitioned plan applies."""
+    rng = np.random.default_rng(400 + seed)
+    n = int(rng.choice([777, 20000]))
+    cols, inv = _random_columns(rng, n, sorted_col=False)
+    perm = rng.permutation(n)
+    segs = [build_segment("p0", cols, inverted_columns=tuple(inv)),
+            build_segment("p1", {k: (t, [v[i] for i in perm]) for k, (t, v) in cols.items()},
+                          inverted_columns=tuple(inv))]
+    e = GpuEngine(0, mode)
+    gsegs = [e.register(x) for x in segs]
+    ex = ServerQueryExecutor(e)
+    gpool = ["i0", "i1", "i2", "s", "i3"]
+    for _ in range(4):
+        gcols = list(rng.choice(gpool, size=int(rng.integers(1, 3)), replace=False))
+        aggs = [x for x in _random_aggs(rng) if x["column"] != "srt"] or [{"function": "COUNT", "column": "*"}]
+        q = {"aggregations": aggs, "filter": _random_tree(rng, segs[0]) if rng.random() < 0.7 else None,
+             "group_by": {"columns": gcols, "top_n": 10}}
+        got, st = ex.process_query(q, gsegs, trim=False)
+        exp, scanned = O.execute_server(segs, q)
+        assert st.num_docs_scanned == scanned
+        assert set(got) == set(exp)
+        for key in exp:
+            for a, gv, ev in zip(q["aggregations"], got[key], exp[key]):
+                exact = a["column"] not in ("dbl", "flt", "lng")
+                _assert_same(a["function"], gv, ev, exact)
+    e.close()
 
 
 def test_group_by_num_groups_limit(sv_segment):

@@ -735,8 +735,8 @@ __global__ __launch_bounds__(kGroupBlock) void k_group_query(GroupArgs a) {
     matched += __popcll(mask);
     if (__any(mask != 0)) group_chunk<MODE>(a, sg, ch, mask, lane, acc_lds, plds);
   }
-  matched = wave_sum(matched);
-  if (lane == 0 && matched) atomicAdd(a.matched + g, matched);
+  matched = wave_sum(matched);  // the EMIT pass re-reads what the COUNT pass already counted
+  if (MODE != GB_EMIT && lane == 0 && matched) atomicAdd(a.matched + g, matched);
   if constexpr (MODE == GB_LDS) flush_group_lds(a, sg, acc_lds, tid);
   if constexpr (MODE == GB_COUNT) {
     __syncthreads();

@@ -1334,12 +1334,13 @@ struct GroupPlan {
   int lds_acc_bytes = 0;
   std::vector<int> lds_off, field_shift, reduce_off;
   int reduce_bytes = 0;
+  int reduce_wave_cnt_off = 0;
 };
 
 constexpr int kGroupMaxFusedLeafBits = 12;    // 16 wave stages x 6 KiB
 constexpr int kGroupLdsAccBudget = 60 * 1024;  // GB_LDS accumulators / GB_COUNT-EMIT partition cursors
 constexpr int kReduceLdsBudget = 128 * 1024;   // k_partition_reduce accumulators
-constexpr int64_t kMaxPartitions = kGroupLdsAccBudget / 4;
+constexpr int64_t kMaxPartitions = 16384;       // 64 KiB of partition cursors beside 16 x 6 KiB wave stages
 
 size_t lds_acc_bytes_per_key(int kind, bool lds_hll_u32) {
   if (kind == 5) return 0;
@@ -1373,7 +1374,7 @@ GroupPlan plan_group(const std::vector<SegmentData *> &segs, const pinot_query &
     const ColumnData &c0 = *segs[0]->column(agg_column(q.aggregations[a]));
     for (size_t si = 1; si < segs.size(); si++) same = same && same_dictionary(c0, *segs[si]->column(c0.name));
   }
-  size_t per_key = 4;
+  size_t per_key = 4 + 32;  // shared count slot + 8 per-wave count copies
   for (int a = 0; a < na; a++) per_key += lds_acc_bytes_per_key(ga.acc_kind[a], true);
   int shift = 0;
   while (shift < 12 && ((size_t)2 << shift) * per_key <= (size_t)kReduceLdsBudget) shift++;
@@ -1402,6 +1403,8 @@ GroupPlan plan_group(const std::vector<SegmentData *> &segs, const pinot_query &
       gp.reduce_off[a] = (int)roff;
       roff += (size_t)K * lds_acc_bytes_per_key(ga.acc_kind[a], true);
     }
+    gp.reduce_wave_cnt_off = (int)roff;
+    roff += (size_t)K * 4 * 8;  // k_partition_reduce: 8 waves' private count copies
     gp.reduce_bytes = (int)roff;
     return gp;
   }
@@ -1601,6 +1604,7 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     ra.shift = gp.shift;
     ra.n_aggs = na;
     ra.lds_bytes = gp.reduce_bytes;
+    ra.wave_cnt_off = gp.reduce_wave_cnt_off;
     ra.G = ks.G;
     ra.counts = counts;
     for (int i = 0; i < na; i++) {

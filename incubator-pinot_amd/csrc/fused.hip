@@ -499,7 +499,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_query_pipe(FusedArgs a) {
 // and DefaultGroupByExecutor.process (PC/query/aggregation/groupby/DefaultGroupByExecutor.java:70-168).
 constexpr int kGroupBlock = 1024;                // 16 waves: the per-doc reads are latency-bound
 constexpr int kGroupWaves = kGroupBlock / 64;
-constexpr int kGroupUnroll = 4;                  // words whose reads are in flight together
+constexpr int kGroupUnroll = 8;                  // words whose reads are in flight together
 
 __device__ __forceinline__ uint32_t decode_doc(const uint8_t *__restrict__ fwd, int bits, int64_t doc) {
   const uint64_t bitpos = (uint64_t)doc * (uint32_t)bits;
@@ -624,7 +624,7 @@ __device__ __forceinline__ void group_chunk(const GroupArgs &a, const GroupSegme
       for (int u = 0; u < kGroupUnroll; u++)
         if (act[u]) {
           const uint32_t pos = atomicAdd(&plds[key[u] >> a.shift], 1u);
-          __builtin_nontemporal_store(rec[u], a.emit + pos);
+          a.emit[pos] = rec[u];  // default policy: the partition runs' lines combine in L2
         }
     } else {
       unsigned long long *cnt_g = a.counts;

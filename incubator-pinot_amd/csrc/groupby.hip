@@ -55,10 +55,13 @@ __global__ __launch_bounds__(kReduceBlock) void k_partition_reduce(PartitionRedu
   __syncthreads();
   const uint32_t b = a.pstart[p], e = a.pstart[p + 1];
   const unsigned long long kmask = (unsigned long long)K - 1ull;
+  // counts: one private copy per wave (a partition has few keys: LDS atomics on one copy serialise)
+  const int wave = tid >> 6;
+  uint32_t *wcnt = cnt + a.wave_cnt_off / 4 + wave * K;
   for (uint32_t r = b + tid; r < e; r += kReduceBlock) {
     const unsigned long long rec = __builtin_nontemporal_load(a.records + r);
     const uint32_t k = (uint32_t)(rec & kmask);
-    atomicAdd(cnt + k, 1u);
+    atomicAdd(wcnt + k, 1u);
 #pragma unroll
     for (int g = 0; g < kMaxGroupAggs; g++) {
       if (g >= a.n_aggs) break;
@@ -97,7 +100,9 @@ __global__ __launch_bounds__(kReduceBlock) void k_partition_reduce(PartitionRedu
   for (int i = tid; i < K; i += kReduceBlock) {
     const long long key = base + i;
     if (key >= a.G) break;
-    a.counts[key] = cnt[i];
+    uint32_t c = 0;
+    for (int w = 0; w < kReduceBlock / 64; w++) c += cnt[a.wave_cnt_off / 4 + w * K + i];
+    a.counts[key] = c;
   }
   for (int g = 0; g < a.n_aggs; g++) {
     const GroupAggDev &ag = a.aggs[g];

@@ -231,6 +231,8 @@ struct PartitionReduceArgs {
   const unsigned long long *records;
   const uint32_t *pstart;      // [P + 1] first record of each partition
   int32_t P, shift, n_aggs, lds_bytes;
+  int32_t wave_cnt_off;        // LDS byte offset of the per-wave count copies (8 waves x K u32)
+  int32_t reserved;
   long long G;
   unsigned long long *counts;
   GroupAggDev aggs[kMaxGroupAggs];  // fwd unused; dict / hll_lut / acc / lds_off / acc_kind / field_shift / bits

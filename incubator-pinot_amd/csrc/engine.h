@@ -127,6 +127,7 @@ struct Engine {
   DeviceBuffer group_part;     // partitioned plan: histogram, offsets, partition starts, scan temp
   DeviceBuffer group_records;  // partitioned plan: (local key | dictIds) records
   DeviceBuffer group_final;    // ordered non-empty keys + compaction scratch
+  DeviceBuffer group_hash;     // hashed key spaces: fingerprint table + representative docs
   PinnedBuffer host_arena;    // staging of the per-query arena (H2D)
   std::vector<uint8_t> arena_shadow;  // bytes last copied into `small` (upload_arena skips identical programs)
   uint64_t arena_dev_gen = 0;
@@ -159,6 +160,7 @@ struct GroupByResult {
   // group key strings ('\t'-joined Dictionary.getStringValue), built on first access
   std::vector<std::vector<std::string>> gvalues;  // [gcol] global id -> string
   std::vector<int64_t> gcard;
+  std::vector<int32_t> key_ids;               // hashed key spaces: [groups][gcols] global ids
   mutable std::vector<std::string> keys;
   mutable std::vector<uint8_t> key_built;
   const std::string &key(int64_t g) const;

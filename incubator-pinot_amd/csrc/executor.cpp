@@ -975,7 +975,9 @@ struct KeySpace {
   std::vector<std::vector<std::vector<int32_t>>> remap;  // [segment][gcol] dictId -> global id (empty = identity)
   std::vector<std::vector<std::string>> gvalues;       // [gcol] global id -> string value
   int64_t G = 1;
+  bool hashed = false;  // Π cardinalities > kDenseKeyLimit: keys are hash-table slots (G set by the plan)
 };
+constexpr int64_t kDenseKeyLimit = int64_t(1) << 27;
 
 bool same_dictionary(const ColumnData &a, const ColumnData &b) {
   if (a.data_type != b.data_type || a.card != b.card) return false;
@@ -1045,11 +1047,16 @@ KeySpace build_key_space(const std::vector<SegmentData *> &segs, const pinot_que
       ks.gcard.push_back((int64_t)ks.gvalues[j].size());
     }
   }
+  // dense raw keys up to kDenseKeyLimit; beyond (LONG_MAP / ARRAY_MAP holder shapes) the key space is
+  // hashed: G becomes the number of hash slots, sized by the caller from the docs
   for (auto g : ks.gcard) {
-    require(ks.G <= (int64_t(1) << 40) / std::max<int64_t>(g, 1), PINOT_ERR_UNSUPPORTED,
-            "group key space too large for the dense device group-by (LONG_MAP/ARRAY_MAP shapes)");
+    if (ks.G > kDenseKeyLimit / std::max<int64_t>(g, 1)) {
+      ks.hashed = true;
+      break;
+    }
     ks.G *= g;
   }
+  if (ks.hashed) ks.G = 0;
   return ks;
 }
 
@@ -1310,10 +1317,15 @@ const std::string &GroupByResult::key(int64_t g) const {
   if (!key_built[g]) {
     int64_t k = raw_keys[g];
     std::string s;
-    for (size_t j = 0; j < gcard.size(); j++) {
+    const size_t nc = gcard.size();
+    for (size_t j = 0; j < nc; j++) {
       if (j) s += '\t';
-      s += gvalues[j][k % gcard[j]];
-      k /= gcard[j];
+      if (!key_ids.empty()) {
+        s += gvalues[j][key_ids[g * nc + j]];
+      } else {
+        s += gvalues[j][k % gcard[j]];
+        k /= gcard[j];
+      }
     }
     keys[g] = std::move(s);
     key_built[g] = 1;
@@ -1431,10 +1443,20 @@ bool needs_admission(const std::vector<SegmentData *> &segs, const pinot_query &
 // Fused group-by: ONE k_group_query launch (or COUNT / EMIT / reduce for the partitioned plan) over all
 // segments, device compaction of the non-empty keys, device per-group outputs, one D2H of the arrays.
 std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q,
-                                                   const KeySpace &ks, const GroupAccs &ga, pinot_exec_stats *stats) {
+                                                   const KeySpace &ks_in, const GroupAccs &ga, pinot_exec_stats *stats,
+                                                   int attempt = 0) {
   const int na = q.num_aggregations;
   const size_t S = segs.size();
-  const GroupPlan gp = plan_group(segs, q, ks, ga, e.group_mode);
+  KeySpace ks = ks_in;
+  int64_t hcap = 0;
+  if (ks.hashed) {  // slots: a power of two >= 2 x the docs that can match
+    int64_t docs = 0;
+    for (auto *sg : segs) docs += sg->num_docs;
+    hcap = 1024;
+    while (hcap < 2 * docs) hcap <<= 1;
+    ks.G = hcap;
+  }
+  const GroupPlan gp = plan_group(segs, q, ks, ga, ks.hashed ? std::string("global") : e.group_mode);
   Arena ar;
   std::unique_ptr<FilterTreeInput> tree;
   if (q.num_filter_nodes > 0) tree = std::make_unique<FilterTreeInput>(decode_filter(q.num_filter_nodes, q.filter));
@@ -1562,6 +1584,18 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
   a.shift = gp.shift;
   a.P = (int32_t)gp.P;
   a.mode = gp.mode == GB_EMIT ? GB_COUNT : gp.mode;
+  unsigned long long *htable = nullptr, *reps = nullptr;
+  if (ks.hashed) {
+    e.group_hash.reserve((size_t)hcap * 16 + 256);
+    htable = e.group_hash.get<unsigned long long>();
+    reps = htable + hcap;
+    a.hashed = 1;
+    a.htable = htable;
+    a.reps = reps;
+    a.hcap = hcap;
+    a.hseed = 0x5EEDF00Dull + 0x9E3779B97F4A7C15ull * (unsigned long long)attempt;
+    a.verify_err = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(matched) + S * 8 + 16);
+  }
   int64_t max_chunks = 1;
   for (auto *sg : segs) max_chunks = std::max<int64_t>(max_chunks, (sg->nwords() + 63) / 64);
   const int64_t resident = (int64_t)group_query_blocks_per_cu(a) * e.num_cus;
@@ -1578,8 +1612,19 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     PINOT_HIP(hipMemsetAsync(counts, 0, ks.G * 8, e.stream));
     for (int i = 0; i < na; i++)
       if (accs[i]) PINOT_HIP(hipMemsetAsync(accs[i], ga.acc_kind[i] == 2 ? 0xFF : 0, ks.G * acc_bytes[i], e.stream));
+    if (ks.hashed) {
+      PINOT_HIP(hipMemsetAsync(htable, 0, (size_t)hcap * 8, e.stream));
+      PINOT_HIP(hipMemsetAsync(reps, 0xFF, (size_t)hcap * 8, e.stream));
+      PINOT_HIP(hipMemsetAsync(a.verify_err, 0, 4, e.stream));
+    }
     t.timed(1, [&] { launch_group_query(a, e.stream); });
     PINOT_HIP(hipGetLastError());
+    if (ks.hashed) {  // every doc's tuple == its slot representative's tuple, or the fingerprints collided
+      GroupArgs av = a;
+      av.mode = GB_VERIFY;
+      launch_group_query(av, e.stream);
+      PINOT_HIP(hipGetLastError());
+    }
   } else {
     const size_t hist_n = (size_t)gp.P * nblk;
     int64_t max_records = 0;
@@ -1633,9 +1678,15 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
   PINOT_HIP(hipGetLastError());
   std::vector<unsigned long long> hmatched(S);
   unsigned long long n = 0;
+  uint32_t verify_err = 0;
   PINOT_HIP(hipMemcpyAsync(&n, n_dev, 8, hipMemcpyDeviceToHost, e.stream));
   PINOT_HIP(hipMemcpyAsync(hmatched.data(), matched, S * 8, hipMemcpyDeviceToHost, e.stream));
+  if (ks.hashed) PINOT_HIP(hipMemcpyAsync(&verify_err, a.verify_err, 4, hipMemcpyDeviceToHost, e.stream));
   PINOT_HIP(hipStreamSynchronize(e.stream));
+  if (verify_err) {  // 64-bit fingerprint collision: retry with another seed
+    require(attempt < 3, PINOT_ERR_DEVICE, "group-key fingerprint collisions persist");
+    return exec_group_by_fused(e, segs, q, ks_in, ga, stats, attempt + 1);
+  }
   int n_hll = 0;
   for (int i = 0; i < na; i++) n_hll += ga.acc_kind[i] == 4;
   auto res = std::make_unique<GroupByResult>();
@@ -1674,6 +1725,14 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     std::vector<uint8_t> host(out_b);
     res->raw_keys.resize(n);
     PINOT_HIP(hipMemcpyAsync(res->raw_keys.data(), keys_dev, n * 8, hipMemcpyDeviceToHost, e.stream));
+    DeviceBuffer ids;
+    if (ks.hashed) {  // group ordinals are hash slots: fetch each group's global-id tuple
+      ids.alloc(n * q.num_group_by * 4 + 16);
+      launch_hash_tuples(a, keys_dev, (long long)n, ids.get<int32_t>(), e.stream);
+      PINOT_HIP(hipGetLastError());
+      res->key_ids.resize(n * q.num_group_by);
+      PINOT_HIP(hipMemcpyAsync(res->key_ids.data(), ids.get(), n * q.num_group_by * 4, hipMemcpyDeviceToHost, e.stream));
+    }
     PINOT_HIP(hipMemcpyAsync(host.data(), out.get(), out_b, hipMemcpyDeviceToHost, e.stream));
     PINOT_HIP(hipStreamSynchronize(e.stream));
     const auto *hc = reinterpret_cast<const unsigned long long *>(host.data());
@@ -1741,6 +1800,8 @@ std::unique_ptr<GroupByResult> exec_group_by_legacy(Engine &e, const std::vector
   std::unique_ptr<FilterTreeInput> tree;
   std::vector<SegPlan> plans = plan_all(e, segs, q, ar, tree);
   KeySpace ks = build_key_space(segs, q);
+  require(!ks.hashed, PINOT_ERR_UNSUPPORTED,
+          "group key space too large for the dense bitset group-by (LONG_MAP/ARRAY_MAP shapes need the fused path)");
   GroupAccs ga = group_acc_kinds(*segs[0], q);
   size_t per_key = 8;
   for (auto b : ga.acc_bytes_per_key) per_key += b;
@@ -1784,6 +1845,7 @@ void exec_group_by_layout(Engine &e, const std::vector<SegmentData *> &segs, con
   (void)e;
   require(!segs.empty(), PINOT_ERR_BAD_ARG, "no segments");
   KeySpace ks = build_key_space(segs, q);
+  require(!ks.hashed, PINOT_ERR_UNSUPPORTED, "partial group-by needs a dense key space");
   for (auto &per_seg : ks.remap)
     for (auto &m : per_seg)
       require(m.empty(), PINOT_ERR_UNSUPPORTED, "partial group-by needs identical group-by dictionaries");
@@ -1800,6 +1862,7 @@ void exec_group_by_partial(Engine &e, const std::vector<SegmentData *> &segs, co
   std::unique_ptr<FilterTreeInput> tree;
   std::vector<SegPlan> plans = plan_all(e, segs, q, ar, tree);
   KeySpace ks = build_key_space(segs, q);
+  require(!ks.hashed, PINOT_ERR_UNSUPPORTED, "partial group-by needs a dense key space");
   GroupAccs ga = group_acc_kinds(*segs[0], q);
   QueryScratch qs = prepare(e, plans, ar);
   PINOT_HIP(hipEventRecord(e.ev_start, e.stream));
@@ -1820,6 +1883,7 @@ std::unique_ptr<GroupByResult> exec_group_by_finalize(Engine &e, const std::vect
                                                       const pinot_query &q, const int64_t *counts_dev,
                                                       void *const *accs_dev) {
   KeySpace ks = build_key_space(segs, q);
+  require(!ks.hashed, PINOT_ERR_UNSUPPORTED, "partial group-by needs a dense key space");
   GroupAccs ga = group_acc_kinds(*segs[0], q);
   GroupByProgram gp{};
   gp.n_aggs = q.num_aggregations;

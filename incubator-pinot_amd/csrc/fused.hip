@@ -568,6 +568,56 @@ __device__ __forceinline__ void agg_update(const GroupAggDev &ag, void *acc, lon
   }
 }
 
+__device__ __forceinline__ unsigned long long mix64(unsigned long long x) {  // splitmix64 finaliser
+  x ^= x >> 30;
+  x *= 0xBF58476D1CE4E5B9ull;
+  x ^= x >> 27;
+  x *= 0x94D049BB133111EBull;
+  x ^= x >> 31;
+  return x;
+}
+
+__device__ __forceinline__ long long hash_insert(const GroupArgs &a, unsigned long long fp) {
+  const unsigned long long m = (unsigned long long)a.hcap - 1ull;
+  unsigned long long slot = fp & m;
+  for (long long probe = 0; probe < a.hcap; probe++) {
+    unsigned long long cur = __hip_atomic_load(a.htable + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (cur == 0) cur = atomicCAS(a.htable + slot, 0ull, fp);
+    if (cur == 0 || cur == fp) return (long long)slot;
+    slot = (slot + 1) & m;
+  }
+  return 0;  // unreachable: hcap >= 2 x docs
+}
+
+__device__ __forceinline__ long long hash_find(const GroupArgs &a, unsigned long long fp) {
+  const unsigned long long m = (unsigned long long)a.hcap - 1ull;
+  unsigned long long slot = fp & m;
+  for (long long probe = 0; probe < a.hcap; probe++) {
+    const unsigned long long cur = __hip_atomic_load(a.htable + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (cur == fp) return (long long)slot;
+    if (cur == 0) return -1;
+    slot = (slot + 1) & m;
+  }
+  return -1;
+}
+
+__device__ __forceinline__ uint32_t tuple_id(const GroupArgs &a, int seg, int j, int64_t doc) {
+  const GroupSegment s = load_const(a.segs + seg);
+  const GroupColDev gc = load_const(a.gcols + s.first_gcol + j);
+  const uint32_t id = decode_doc(gc.fwd, gc.bits, doc);
+  return gc.remap ? (uint32_t)gc.remap[id] : id;
+}
+
+// Does doc of segment `sg` (this block's) carry the same global-id tuple as the representative `rep`?
+__device__ __forceinline__ bool same_tuple(const GroupArgs &a, const GroupSegment &sg, int64_t doc, unsigned long long rep) {
+  const int seg = (int)(rep >> 32);
+  const int64_t rdoc = (int64_t)(rep & 0xFFFFFFFFull);
+  const int mine = blockIdx.x / a.bps;
+  for (int j = 0; j < a.n_gcols; j++)
+    if (tuple_id(a, mine, j, doc) != tuple_id(a, seg, j, rdoc)) return false;
+  return true;
+}
+
 template <int MODE>
 __device__ __forceinline__ void group_chunk(const GroupArgs &a, const GroupSegment &sg, int64_t ch, uint64_t mask,
                                             int lane, uint8_t *acc_lds, uint32_t *plds) {
@@ -589,6 +639,10 @@ __device__ __forceinline__ void group_chunk(const GroupArgs &a, const GroupSegme
       key[u] = 0;
       act[u] = (mw[u] >> lane) & 1ull;
     }
+    if (a.hashed) {
+#pragma unroll
+      for (int u = 0; u < kGroupUnroll; u++) key[u] = a.hseed;
+    }
     for (int j = 0; j < a.n_gcols; j++) {
       const GroupColDev gc = load_const(a.gcols + sg.first_gcol + j);
       uint32_t id[kGroupUnroll];
@@ -597,15 +651,35 @@ __device__ __forceinline__ void group_chunk(const GroupArgs &a, const GroupSegme
 #pragma unroll
       for (int u = 0; u < kGroupUnroll; u++) {
         const uint32_t gid = (gc.remap && act[u]) ? (uint32_t)gc.remap[id[u]] : id[u];
-        key[u] += (unsigned long long)gid * (unsigned long long)gc.stride;
+        if (a.hashed) key[u] = mix64(key[u] ^ ((unsigned long long)gid + 0x9E3779B97F4A7C15ull * (unsigned long long)(j + 1)));
+        else key[u] += (unsigned long long)gid * (unsigned long long)gc.stride;
       }
+    }
+    if (a.hashed) {
+#pragma unroll
+      for (int u = 0; u < kGroupUnroll; u++)
+        if (act[u]) {
+          const unsigned long long fp = key[u] | 1ull;  // 0 marks an empty slot
+          if constexpr (MODE == GB_VERIFY) {
+            const long long slot = hash_find(a, fp);
+            if (slot < 0 || !same_tuple(a, sg, doc[u], __hip_atomic_load(a.reps + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))
+              atomicOr(a.verify_err, 1u);
+            act[u] = false;
+          } else {
+            const long long slot = hash_insert(a, fp);
+            atomicMin(a.reps + slot, ((unsigned long long)(blockIdx.x / a.bps) << 32) | (unsigned long long)doc[u]);
+            key[u] = (unsigned long long)slot;
+          }
+        }
     }
     if (a.admitted) {
 #pragma unroll
       for (int u = 0; u < kGroupUnroll; u++)
         act[u] = act[u] && ((a.admitted[key[u] >> 5] >> (key[u] & 31)) & 1u);
     }
-    if constexpr (MODE == GB_COUNT) {
+    if constexpr (MODE == GB_VERIFY) {
+      continue;
+    } else if constexpr (MODE == GB_COUNT) {
 #pragma unroll
       for (int u = 0; u < kGroupUnroll; u++)
         if (act[u]) atomicAdd(&plds[key[u] >> a.shift], 1u);
@@ -736,7 +810,7 @@ __global__ __launch_bounds__(kGroupBlock) void k_group_query(GroupArgs a) {
     if (__any(mask != 0)) group_chunk<MODE>(a, sg, ch, mask, lane, acc_lds, plds);
   }
   matched = wave_sum(matched);  // the EMIT pass re-reads what the COUNT pass already counted
-  if (MODE != GB_EMIT && lane == 0 && matched) atomicAdd(a.matched + g, matched);
+  if (MODE != GB_EMIT && MODE != GB_VERIFY && lane == 0 && matched) atomicAdd(a.matched + g, matched);
   if constexpr (MODE == GB_LDS) flush_group_lds(a, sg, acc_lds, tid);
   if constexpr (MODE == GB_COUNT) {
     __syncthreads();
@@ -807,8 +881,26 @@ void launch_group_query(const GroupArgs &a, hipStream_t stream) {
     case GB_GLOBAL: hipLaunchKernelGGL(k_group_query<GB_GLOBAL>, grid, block, lds, stream, a); break;
     case GB_LDS: hipLaunchKernelGGL(k_group_query<GB_LDS>, grid, block, lds, stream, a); break;
     case GB_COUNT: hipLaunchKernelGGL(k_group_query<GB_COUNT>, grid, block, lds, stream, a); break;
-    default: hipLaunchKernelGGL(k_group_query<GB_EMIT>, grid, block, lds, stream, a); break;
+    case GB_EMIT: hipLaunchKernelGGL(k_group_query<GB_EMIT>, grid, block, lds, stream, a); break;
+    default: hipLaunchKernelGGL(k_group_query<GB_VERIFY>, grid, block, lds, stream, a); break;
   }
+}
+
+namespace {
+__global__ void k_hash_tuples(GroupArgs a, const long long *__restrict__ slots, long long n, int32_t *ids) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const unsigned long long rep = a.reps[slots[i]];
+    const int seg = (int)(rep >> 32);
+    const int64_t doc = (int64_t)(rep & 0xFFFFFFFFull);
+    for (int j = 0; j < a.n_gcols; j++) ids[i * a.n_gcols + j] = (int32_t)tuple_id(a, seg, j, doc);
+  }
+}
+}  // namespace
+
+void launch_hash_tuples(const GroupArgs &a, const long long *slots, long long n, int32_t *ids, hipStream_t stream) {
+  if (n <= 0) return;
+  const int grid = (int)std::min<long long>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_hash_tuples, dim3(grid), dim3(256), 0, stream, a, slots, n, ids);
 }
 
 }  // namespace pinot

@@ -170,7 +170,9 @@ int scan_query_blocks_per_cu(int stage_bytes, bool gathers, bool pipelined);
 //   GB_EMIT    pass 2: (local key | dictId fields) u64 records scattered into partition runs;
 //              k_partition_reduce then owns one partition per block (accumulators in LDS, no atomics
 //              to HBM) — the large key spaces (config 4: 1 M keys with HLL)
-enum GroupMode : int32_t { GB_GLOBAL = 0, GB_LDS = 1, GB_COUNT = 2, GB_EMIT = 3 };
+//   GB_VERIFY  hashed key spaces: re-reads every matching doc's tuple and checks it against its hash
+//              slot's representative doc (a 64-bit fingerprint collision is detected, never merged)
+enum GroupMode : int32_t { GB_GLOBAL = 0, GB_LDS = 1, GB_COUNT = 2, GB_EMIT = 3, GB_VERIFY = 4 };
 // accumulator kinds (acc_kind): 0 int64 sum, 1 double sum, 2 ordered-u64 min, 3 ordered-u64 max,
 // 4 HLL registers (u8 [G][256]), 5 none (COUNT / AVG count share `counts`)
 constexpr int kMaxGroupAggs = 8;
@@ -221,6 +223,15 @@ struct GroupArgs {
   uint32_t *hist;              // GB_COUNT: [P][nblk] per-block partition counts (partition-major)
   const uint32_t *offsets;     // GB_EMIT: [P][nblk] exclusive record offsets
   unsigned long long *emit;    // GB_EMIT: records
+  // hashed key space (LONG_MAP / ARRAY_MAP shapes: Π cardinalities too large for dense arrays): the key
+  // is the slot of the tuple's 64-bit fingerprint in an open-addressing table of hcap (power of 2) slots
+  unsigned long long *htable;  // [hcap] fingerprints, 0 = empty
+  unsigned long long *reps;    // [hcap] first (segment << 32 | doc) of the slot (atomicMin)
+  long long hcap;
+  unsigned long long hseed;
+  uint32_t *verify_err;        // GB_VERIFY: set when a doc's tuple differs from its slot's representative
+  int32_t hashed;
+  int32_t reserved2;
 };
 void launch_group_query(const GroupArgs &a, hipStream_t stream);
 // Grid (blocks per segment x segments) the host sizes `hist` / `offsets` for.
@@ -241,6 +252,8 @@ void launch_partition_reduce(const PartitionReduceArgs &a, hipStream_t stream);
 // pstart[p] = offsets[p * nblk] (partition-major exclusive offsets), pstart[P] = total records.
 void launch_partition_starts(const uint32_t *offsets, const uint32_t *hist, int32_t P, int32_t nblk, uint32_t *pstart,
                              hipStream_t stream);
+// Hashed key spaces: the global-id tuple of each listed slot's representative doc, ids[i * n_gcols + j].
+void launch_hash_tuples(const GroupArgs &a, const long long *slots, long long n, int32_t *ids, hipStream_t stream);
 // HLL registers of the listed keys: out[i * 256 + r] = regs[keys[i] * 256 + r].
 void launch_gather_hll(const uint8_t *regs, const long long *keys, long long n, uint8_t *out, hipStream_t stream);
 

@@ -234,6 +234,15 @@ pinot_status pinot_gpu_segment_register_synthetic(pinot_engine *engine, const ch
                                                   const char *const *column_names,
                                                   const int32_t *cardinalities, uint64_t seed,
                                                   pinot_segment_handle *out);
+/* Same, with a kind per column (NULL = all PINOT_SYNTH_RANDOM): SORTED = value v on the docs
+ * [v*N/card, (v+1)*N/card) with a sorted index; INVERTED = the RANDOM values with a bitmap inverted index
+ * (both built on the host in Pinot's file layout and registered like a loaded segment). */
+typedef enum { PINOT_SYNTH_RANDOM = 0, PINOT_SYNTH_SORTED = 1, PINOT_SYNTH_INVERTED = 2 } pinot_synth_kind;
+pinot_status pinot_gpu_segment_register_synthetic_ex(pinot_engine *engine, const char *name,
+                                                     int32_t num_docs, int32_t num_columns,
+                                                     const char *const *column_names,
+                                                     const int32_t *cardinalities, const int32_t *kinds,
+                                                     uint64_t seed, pinot_segment_handle *out);
 
 /* Synchronise the engine's stream (bench timing brackets). */
 pinot_status pinot_gpu_synchronize(pinot_engine *engine);

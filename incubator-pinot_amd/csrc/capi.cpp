@@ -156,19 +156,27 @@ pinot_status pinot_gpu_segment_register(pinot_engine *engine, const pinot_segmen
   });
 }
 
-pinot_status pinot_gpu_segment_register_synthetic(pinot_engine *engine, const char *name, int32_t num_docs,
-                                                  int32_t num_columns, const char *const *column_names,
-                                                  const int32_t *cardinalities, uint64_t seed,
-                                                  pinot_segment_handle *out) {
+pinot_status pinot_gpu_segment_register_synthetic_ex(pinot_engine *engine, const char *name, int32_t num_docs,
+                                                     int32_t num_columns, const char *const *column_names,
+                                                     const int32_t *cardinalities, const int32_t *kinds, uint64_t seed,
+                                                     pinot_segment_handle *out) {
   return guard([&] {
     require(engine && out, PINOT_ERR_BAD_ARG, "null argument");
     std::lock_guard<std::mutex> lk(engine->mu);
     set_device(*engine);
-    auto seg = register_synthetic(*engine, name, num_docs, num_columns, column_names, cardinalities, seed);
+    auto seg = register_synthetic(*engine, name, num_docs, num_columns, column_names, cardinalities, seed, kinds);
     const int64_t h = engine->next_handle++;
     engine->segments[h] = std::move(seg);
     *out = h;
   });
+}
+
+pinot_status pinot_gpu_segment_register_synthetic(pinot_engine *engine, const char *name, int32_t num_docs,
+                                                  int32_t num_columns, const char *const *column_names,
+                                                  const int32_t *cardinalities, uint64_t seed,
+                                                  pinot_segment_handle *out) {
+  return pinot_gpu_segment_register_synthetic_ex(engine, name, num_docs, num_columns, column_names, cardinalities,
+                                                 nullptr, seed, out);
 }
 
 pinot_status pinot_gpu_segment_release(pinot_engine *engine, pinot_segment_handle handle) {

@@ -186,7 +186,8 @@ std::unique_ptr<GroupByResult> exec_group_by_finalize(Engine &e, const std::vect
 // segments (segment.cpp)
 std::unique_ptr<SegmentData> register_segment(Engine &e, const pinot_segment_desc &d);
 std::unique_ptr<SegmentData> register_synthetic(Engine &e, const char *name, int32_t num_docs, int32_t ncols,
-                                                const char *const *names, const int32_t *cards, uint64_t seed);
+                                                const char *const *names, const int32_t *cards, uint64_t seed,
+                                                const int32_t *kinds = nullptr);
 void ensure_hll_lut(Engine &e, ColumnData &c);
 
 // stream-lib HyperLogLog(log2m=8) helpers (hll.cpp)

@@ -283,13 +283,159 @@ std::unique_ptr<SegmentData> register_segment(Engine &e, const pinot_segment_des
   return seg;
 }
 
+// ---------------------------------------------------------------- synthetic sorted / inverted columns
+// Host-built Pinot-format buffers (the same bytes a segment file would hold), registered through the
+// normal descriptor path: SORTED = value v on docs [v*N/card, (v+1)*N/card); INVERTED = the HBM
+// generator's values (restated below) with a fixed-bit forward index and a bitmap inverted index
+// (OffHeapBitmapInvertedIndexCreator layout: (card+1) BE int offsets + portable roaring, array / bitmap
+// containers, no runs).
+namespace {
+
+uint64_t splitmix64_host(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+void put_be32(std::vector<uint8_t> &b, size_t off, uint32_t v) {
+  b[off] = (uint8_t)(v >> 24);
+  b[off + 1] = (uint8_t)(v >> 16);
+  b[off + 2] = (uint8_t)(v >> 8);
+  b[off + 3] = (uint8_t)v;
+}
+
+void append_le16(std::vector<uint8_t> &b, uint32_t v) {
+  b.push_back((uint8_t)v);
+  b.push_back((uint8_t)(v >> 8));
+}
+
+void append_le32(std::vector<uint8_t> &b, uint32_t v) {
+  append_le16(b, v & 0xFFFFu);
+  append_le16(b, v >> 16);
+}
+
+// Portable roaring serialisation of ascending doc ids (cookie 12346: no run containers).
+void serialize_roaring(const int32_t *docs, size_t n, std::vector<uint8_t> &out) {
+  std::vector<std::pair<uint32_t, std::pair<size_t, size_t>>> conts;  // key, [begin, end)
+  for (size_t i = 0; i < n;) {
+    const uint32_t key = (uint32_t)docs[i] >> 16;
+    size_t j = i;
+    while (j < n && ((uint32_t)docs[j] >> 16) == key) j++;
+    conts.push_back({key, {i, j}});
+    i = j;
+  }
+  const size_t base = out.size();
+  append_le32(out, 12346u);
+  append_le32(out, (uint32_t)conts.size());
+  for (auto &c : conts) {
+    append_le16(out, c.first);
+    append_le16(out, (uint32_t)(c.second.second - c.second.first - 1));
+  }
+  const size_t offs = out.size();
+  out.resize(out.size() + 4 * conts.size());
+  for (size_t k = 0; k < conts.size(); k++) {
+    const uint32_t rel = (uint32_t)(out.size() - base);
+    for (int q = 0; q < 4; q++) out[offs + 4 * k + q] = (uint8_t)(rel >> (8 * q));
+    const size_t b = conts[k].second.first, e = conts[k].second.second;
+    if (e - b > 4096) {
+      uint64_t words[1024] = {0};
+      for (size_t i = b; i < e; i++) {
+        const uint32_t lo = (uint32_t)docs[i] & 0xFFFFu;
+        words[lo >> 6] |= 1ull << (lo & 63);
+      }
+      for (int w = 0; w < 1024; w++) {
+        append_le32(out, (uint32_t)words[w]);
+        append_le32(out, (uint32_t)(words[w] >> 32));
+      }
+    } else {
+      for (size_t i = b; i < e; i++) append_le16(out, (uint32_t)docs[i] & 0xFFFFu);
+    }
+  }
+}
+
+}  // namespace
+
 std::unique_ptr<SegmentData> register_synthetic(Engine &e, const char *name, int32_t num_docs, int32_t ncols,
-                                                const char *const *names, const int32_t *cards, uint64_t seed) {
+                                                const char *const *names, const int32_t *cards, uint64_t seed,
+                                                const int32_t *kinds) {
   require(num_docs > 0 && ncols > 0 && names && cards, PINOT_ERR_BAD_ARG, "synthetic segment arguments");
   auto seg = std::make_unique<SegmentData>();
   seg->name = name ? name : "synthetic";
   seg->num_docs = num_docs;
   for (int i = 0; i < ncols; i++) {
+    const int kind = kinds ? kinds[i] : PINOT_SYNTH_RANDOM;
+    if (kind != PINOT_SYNTH_RANDOM) {
+      require(kind == PINOT_SYNTH_SORTED || kind == PINOT_SYNTH_INVERTED, PINOT_ERR_BAD_ARG, "synthetic column kind");
+      const int32_t card = cards[i];
+      require(card >= 1 && card <= num_docs, PINOT_ERR_BAD_ARG, "synthetic cardinality must be in [1, num_docs]");
+      const int bits = num_bits_per_value(card - 1);
+      std::vector<uint8_t> dict((size_t)card * 4), sorted, fwd, inv;
+      for (int32_t k = 0; k < card; k++) put_be32(dict, 4 * (size_t)k, (uint32_t)k);
+      pinot_column_desc d{};
+      d.name = names[i];
+      d.data_type = PINOT_INT;
+      d.cardinality = card;
+      d.bits_per_value = bits;
+      d.dictionary = dict.data();
+      d.dictionary_len = dict.size();
+      if (kind == PINOT_SYNTH_SORTED) {
+        sorted.resize((size_t)card * 8);
+        for (int32_t v = 0; v < card; v++) {
+          put_be32(sorted, 8 * (size_t)v, (uint32_t)((int64_t)v * num_docs / card));
+          put_be32(sorted, 8 * (size_t)v + 4, (uint32_t)((int64_t)(v + 1) * num_docs / card - 1));
+        }
+        d.is_sorted = 1;
+        d.sorted_index = sorted.data();
+        d.sorted_index_len = sorted.size();
+      } else {
+        const uint64_t cseed = seed ^ ((uint64_t)(i + 1) * 0xD1B54A32D192ED03ull);
+        std::vector<int32_t> vals(num_docs);
+        for (int64_t doc = 0; doc < num_docs; doc++)  // k_synth_column's value(d)
+          vals[doc] = doc < card ? (int32_t)doc
+                                 : (int32_t)(splitmix64_host(cseed ^ ((uint64_t)doc * 0x9E3779B97F4A7C15ull)) % (uint64_t)card);
+        fwd.assign(((size_t)num_docs * bits + 7) / 8 + 8, 0);
+        {  // PinotDataBitSet: MSB-first, big-endian, no padding between values
+          uint64_t acc = 0;
+          int nb = 0;
+          size_t o = 0;
+          for (int64_t doc = 0; doc < num_docs; doc++) {
+            acc = (acc << bits) | (uint32_t)vals[doc];
+            nb += bits;
+            while (nb >= 8) {
+              fwd[o++] = (uint8_t)(acc >> (nb - 8));
+              nb -= 8;
+            }
+            acc &= (1ull << nb) - 1ull;
+          }
+          if (nb) fwd[o] = (uint8_t)(acc << (8 - nb));
+        }
+        // counting sort of docs by value -> ascending doc lists per dictId
+        std::vector<int64_t> start((size_t)card + 1, 0);
+        for (int32_t v : vals) start[v + 1]++;
+        for (int32_t v = 0; v < card; v++) start[v + 1] += start[v];
+        std::vector<int32_t> order(num_docs);
+        {
+          std::vector<int64_t> cur(start.begin(), start.end() - 1);
+          for (int64_t doc = 0; doc < num_docs; doc++) order[cur[vals[doc]]++] = (int32_t)doc;
+        }
+        inv.assign(4 * ((size_t)card + 1), 0);
+        inv.reserve(inv.size() + (size_t)num_docs * 2 + (size_t)card * 64 + ((size_t)num_docs >> 16) * card * 8);
+        for (int32_t v = 0; v < card; v++) {
+          put_be32(inv, 4 * (size_t)v, (uint32_t)inv.size());
+          serialize_roaring(order.data() + start[v], (size_t)(start[v + 1] - start[v]), inv);
+        }
+        put_be32(inv, 4 * (size_t)card, (uint32_t)inv.size());
+        require(inv.size() < UINT32_MAX, PINOT_ERR_UNSUPPORTED, "synthetic inverted index beyond 4 GiB");
+        d.forward_index = fwd.data();
+        d.forward_index_len = fwd.size();
+        d.has_inverted_index = 1;
+        d.inverted_index = inv.data();
+        d.inverted_index_len = inv.size();
+      }
+      register_column(e, *seg, d);
+      continue;
+    }
     auto cp = std::make_unique<ColumnData>();
     ColumnData &c = *cp;
     c.name = names[i];

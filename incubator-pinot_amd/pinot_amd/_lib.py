@@ -25,7 +25,8 @@ EXPORTED_SYMBOLS = [
     "pinot_groupby_num_groups", "pinot_groupby_num_columns", "pinot_groupby_key", "pinot_groupby_values",
     "pinot_groupby_hll", "pinot_groupby_raw_keys", "pinot_groupby_free",
     "pinot_gpu_group_by_layout", "pinot_gpu_group_by_partial", "pinot_gpu_group_by_finalize",
-    "pinot_gpu_segment_register_synthetic", "pinot_gpu_synchronize", "pinot_gpu_last_kernel_ms",
+    "pinot_gpu_segment_register_synthetic", "pinot_gpu_segment_register_synthetic_ex", "pinot_gpu_synchronize",
+    "pinot_gpu_last_kernel_ms",
 ]
 
 
@@ -150,6 +151,8 @@ def load(path=None):
                                               C.POINTER(P)]),
         "pinot_gpu_segment_register_synthetic": (i32, [P, C.c_char_p, i32, i32, C.POINTER(C.c_char_p),
                                                        C.POINTER(i32), u64, C.POINTER(i64)]),
+        "pinot_gpu_segment_register_synthetic_ex": (i32, [P, C.c_char_p, i32, i32, C.POINTER(C.c_char_p),
+                                                          C.POINTER(i32), C.POINTER(i32), u64, C.POINTER(i64)]),
         "pinot_gpu_synchronize": (i32, [P]),
         "pinot_gpu_last_kernel_ms": (i32, [P, i32, C.POINTER(C.c_double), C.POINTER(i64)]),
     }

@@ -124,13 +124,17 @@ class GpuEngine:
         check(self.lib.pinot_gpu_segment_register(self.ptr, C.byref(desc), C.byref(h)))
         return GpuSegment(self, h.value, seg.name, seg.num_docs)
 
+    SYNTH_KIND = {"random": 0, "sorted": 1, "inverted": 2}
+
     def register_synthetic(self, name, num_docs, columns, seed):
-        """Bench tooling: columns = [(name, cardinality)], generated in HBM (see include/pinot_gpu.h)."""
+        """Bench tooling: columns = [(name, cardinality[, kind])] with kind "random" (generated in HBM),
+        "sorted" or "inverted" (bitmap inverted index, built on the host); see include/pinot_gpu.h."""
         names = (C.c_char_p * len(columns))(*[c[0].encode() for c in columns])
         cards = (C.c_int32 * len(columns))(*[int(c[1]) for c in columns])
+        kinds = (C.c_int32 * len(columns))(*[self.SYNTH_KIND[c[2] if len(c) > 2 else "random"] for c in columns])
         h = C.c_int64()
-        check(self.lib.pinot_gpu_segment_register_synthetic(self.ptr, name.encode(), int(num_docs), len(columns),
-                                                            names, cards, C.c_uint64(seed), C.byref(h)))
+        check(self.lib.pinot_gpu_segment_register_synthetic_ex(self.ptr, name.encode(), int(num_docs), len(columns),
+                                                               names, cards, kinds, C.c_uint64(seed), C.byref(h)))
         return GpuSegment(self, h.value, name, num_docs)
 
     def set_config(self, config):

@@ -57,3 +57,25 @@ def make_segment(name, num_docs, columns, seed):
                              has_inverted_index=False, num_docs=num_docs,
                              dictionary=np.arange(card, dtype=">i4").tobytes(), fwd=_pack(ids, bits))
     return Segment(name=name, num_docs=num_docs, columns=cols)
+
+
+def sorted_values(card, num_docs):
+    """PINOT_SYNTH_SORTED: value v on docs [v*N/card, (v+1)*N/card)."""
+    starts = (np.arange(card, dtype=np.int64) * num_docs) // card
+    return np.searchsorted(starts, np.arange(num_docs, dtype=np.int64), side="right") - 1
+
+
+def make_segment_kinds(name, num_docs, columns, seed):
+    """columns = [(name, cardinality, kind)] with kind random / sorted / inverted -> Segment via the
+    reference-format builder (sorted index, bitmap inverted indexes) from the same values."""
+    from pinot_amd.segment import build_segment  # data containers / format writer only
+    cols, inv = {}, []
+    for i, (cname, card, kind) in enumerate(columns):
+        if kind == "sorted":
+            vals = sorted_values(card, num_docs)
+        else:
+            vals = column_values(seed, i, card, 0, num_docs)
+        if kind == "inverted":
+            inv.append(cname)
+        cols[cname] = ("INT", vals.tolist())
+    return build_segment(name, cols, inverted_columns=tuple(inv))

@@ -385,6 +385,36 @@ def test_distributed_group_by_single_rank(sv_segment):
     e.close()
 
 
+CONFIG3_COLUMNS = [("s0", 1000, "sorted"), ("b1", 10, "inverted"), ("b2", 100, "inverted"), ("b3", 1000, "inverted"),
+                   ("b4", 10000, "inverted"), ("d8", 1 << 17, "random"), ("m1", 1024, "random")]
+CONFIG3_QUERY = ("SELECT SUM(d8), MAX(m1), COUNT(*) FROM t WHERE s0 IN (10,11,12,13,14,15,16,17,18,19) "
+                 "AND (b1 = 3 OR b2 IN (5, 6, 7)) AND b3 <> 0")
+
+
+def test_synthetic_index_columns_match_host_builder(engine):
+    """Synthetic sorted / bitmap-inverted columns (config 3 table) == the host format builder + oracle."""
+    import synth
+    n = 200003
+    seg = engine.register_synthetic("syn3", n, CONFIG3_COLUMNS, seed=0x5EED0011)
+    host = synth.make_segment_kinds("syn3", n, CONFIG3_COLUMNS, seed=0x5EED0011)
+    ex = ServerQueryExecutor(engine)
+    for text in (CONFIG3_QUERY, "SELECT COUNT(*), SUM(d8) FROM t WHERE b4 IN (1, 77, 9999) OR s0 = 999",
+                 "SELECT COUNT(*), MIN(m1) FROM t WHERE b2 NOT IN (1, 2) AND s0 BETWEEN 5 AND 500 GROUP BY b1"):
+        q = compile_pql(text)
+        got, st = ex.process_query(q, [seg], trim=False)
+        exp, scanned = O.execute_server([host], q)
+        assert st.num_docs_scanned == scanned
+        if q.get("group_by"):
+            assert set(got) == set(exp)
+            for k in exp:
+                for a, gv, ev in zip(q["aggregations"], got[k], exp[k]):
+                    _assert_same(a["function"], gv, ev)
+        else:
+            for a, gv, ev in zip(q["aggregations"], got, exp):
+                _assert_same(a["function"], gv, ev)
+    seg.release()
+
+
 def test_synthetic_segment_matches_host_generator(engine):
     """The HBM synthetic generator == the oracle's host restatement (bench data parity)."""
     import synth

@@ -9,8 +9,8 @@ Used to load the reference's own test fixtures
 known-answer tests of `InnerSegmentAggregationSingleValueQueriesTest` /
 `InterSegmentAggregationSingleValueQueriesTest` / `QueryExecutorTest` can be
 replayed. Only the subset of the Avro 1.x binary encoding those files use is
-implemented: records of int/long/float/double/string/boolean fields and
-["null", T] unions.
+implemented: records of int/long/float/double/string/boolean fields, arrays of those (the
+multi-value columns of pinot-tools' airlineStats_data.avro) and ["null", T] unions.
 """
 import json
 import struct
@@ -63,6 +63,21 @@ def _reader_for(t):
             return subs[buf.long()](buf)
         return rd
     if isinstance(t, dict):
+        if t.get("type") == "array":  # blocked: count (negative -> byte size follows), items, 0
+            item = _reader_for(t["items"])
+
+            def rd_array(buf):
+                out = []
+                while True:
+                    n = buf.long()
+                    if n == 0:
+                        return out
+                    if n < 0:
+                        buf.long()
+                        n = -n
+                    for _ in range(n):
+                        out.append(item(buf))
+            return rd_array
         t = t["type"]
     if t == "null":
         return lambda buf: None

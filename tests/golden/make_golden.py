@@ -8,6 +8,8 @@ Writes (all data, no reference source text):
                        column list: PT/queries/BaseSingleValueQueriesTest.java:47-60,93-101)
   simple_data.npz     dim0, dim1, met of pinot-core/src/test/resources/data/simpleData200001.avro
                       (PT/query/executor/QueryExecutorTest.java:59-173)
+  airline_stats.npz   Carrier, ArrDelay, DaysSinceEpoch of pinot-tools/src/main/resources/sample_data/
+                      airlineStats_data.avro (9746 rows; the config-1 query shape on real data)
   padding_null.json   byte contents of the Java-written v1 segment paddingNull.tar.gz (dictionaries and
                       fixed-bit forward indexes, with metadata cardinality/bits) — a byte-level format fixture
 The known answers themselves are transcribed (with file:line) in reference_kats.json.
@@ -29,6 +31,9 @@ REF = "/root/reference/pinot-core/src/test/resources/data"
 SV_COLUMNS = [("column1", "INT"), ("column3", "INT"), ("column5", "STRING"), ("column6", "INT"),
               ("column7", "INT"), ("column9", "INT"), ("column11", "STRING"), ("column12", "STRING"),
               ("column17", "INT"), ("column18", "INT"), ("daysSinceEpoch", "INT")]
+
+
+TOOLS_DATA = "/root/reference/pinot-tools/src/main/resources/sample_data"
 
 
 def main():
@@ -64,6 +69,15 @@ def main():
         }
     with open(os.path.join(HERE, "padding_null.json"), "w") as f:
         json.dump(fx, f, indent=1, sort_keys=True)
+
+    # real data for the config-1 query shape: pinot-tools' airlineStats sample, the three
+    # columns the query reads; ArrDelay is a nullable INT *dimension*, so nulls take Pinot's default
+    # dimension null value Integer.MIN_VALUE (pinot-common/.../data/FieldSpec.java:50)
+    names, cols = avro.read_avro(os.path.join(TOOLS_DATA, "airlineStats_data.avro"))
+    arr = [(-2 ** 31 if x is None else x) for x in cols["ArrDelay"]]
+    np.savez_compressed(os.path.join(HERE, "airline_stats.npz"), Carrier=np.array(cols["Carrier"], dtype="U"),
+                        ArrDelay=np.array(arr, dtype=np.int32),
+                        DaysSinceEpoch=np.array(cols["DaysSinceEpoch"], dtype=np.int32))
     print("golden fixtures written to", HERE)
 
 

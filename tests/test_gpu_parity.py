@@ -427,3 +427,56 @@ def test_synthetic_segment_matches_host_generator(engine):
     exp, _ = O.execute_server([host], q)
     assert got[0] == exp[0] and got[1] == exp[1] and got[2] == exp[2] and got[3] == exp[3]
     seg.release()
+
+
+# ------------------------------------------------------------------ config 1: the quick-start query shape
+def _assert_group_maps(q, got, exp):
+    assert set(got) == set(exp)
+    for k in exp:
+        for a, gv, ev in zip(q["aggregations"], got[k], exp[k]):
+            _assert_same(a["function"], gv, ev)
+
+
+def test_config1_airline_stats_real_data(engine):
+    """Config-1 query shape on real reference data: pinot-tools' airlineStats sample (tests/golden/airline_stats.npz,
+    9746 rows; ArrDelay nulls = Integer.MIN_VALUE, the default INT dimension null)."""
+    import os
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "airline_stats.npz"))
+    seg = build_segment("airlineStats_OFFLINE_16071_16101_0", {
+        "Carrier": ("STRING", z["Carrier"].tolist()), "ArrDelay": ("INT", z["ArrDelay"].tolist()),
+        "DaysSinceEpoch": ("INT", z["DaysSinceEpoch"].tolist())})
+    g = engine.register(seg)
+    med = int(np.median(z["DaysSinceEpoch"]))
+    ex = ServerQueryExecutor(engine)
+    for text in ("SELECT COUNT(*), SUM(ArrDelay) FROM airlineStats WHERE DaysSinceEpoch > %d GROUP BY Carrier" % med,
+                 "SELECT COUNT(*), MAX(ArrDelay), MIN(ArrDelay), AVG(ArrDelay) FROM airlineStats "
+                 "WHERE Carrier IN ('AA', 'DL') AND ArrDelay > -100 GROUP BY DaysSinceEpoch"):
+        q = compile_pql(text)
+        got, st = ex.process_query(q, [g], trim=False)
+        exp, scanned = O.execute_server([seg], q)
+        assert st.num_docs_scanned == scanned
+        _assert_group_maps(q, got, exp)
+    g.release()
+
+
+def test_config1_baseball_synthetic(engine):
+    """BASELINE config 1 (quick-start baseballStats; the CSV is absent, so a synthetic segment of the schema's
+    shape): SELECT COUNT(*), SUM(runs) WHERE yearID > 2000 GROUP BY teamID, inverted indexes on
+    playerID and teamID (baseballStats_offline_table_config.json)."""
+    rng = np.random.default_rng(1871)
+    n = 97889
+    teams = ["T%03d" % i for i in range(149)]
+    players = ["p%05d" % i for i in range(18000)]
+    runs = np.where(rng.random(n) < 0.45, 0, rng.integers(0, 193, n))
+    seg = build_segment("baseballStats_OFFLINE_0", {
+        "playerID": ("STRING", [players[i] for i in rng.integers(0, len(players), n)]),
+        "yearID": ("INT", rng.integers(1871, 2014, n).tolist()),
+        "teamID": ("STRING", [teams[i] for i in rng.integers(0, len(teams), n)]),
+        "runs": ("INT", runs.tolist())}, inverted_columns=("playerID", "teamID"))
+    g = engine.register(seg)
+    q = compile_pql("SELECT COUNT(*), SUM(runs) FROM baseballStats WHERE yearID > 2000 GROUP BY teamID")
+    got, st = ServerQueryExecutor(engine).process_query(q, [g], trim=False)
+    exp, scanned = O.execute_server([seg], q)
+    assert st.num_docs_scanned == scanned
+    _assert_group_maps(q, got, exp)
+    g.release()

@@ -1351,7 +1351,7 @@ struct GroupPlan {
 
 constexpr int kGroupMaxFusedLeafBits = 12;    // 16 wave stages x 6 KiB
 constexpr int kGroupLdsAccBudget = 60 * 1024;  // GB_LDS accumulators / GB_COUNT-EMIT partition cursors
-constexpr int kReduceLdsBudget = 128 * 1024;   // k_partition_reduce accumulators
+constexpr int kReduceLdsBudget = 152 * 1024;   // k_partition_reduce accumulators (one block per CU)
 constexpr int64_t kMaxPartitions = 16384;       // 64 KiB of partition cursors beside 16 x 6 KiB wave stages
 
 size_t lds_acc_bytes_per_key(int kind, bool lds_hll_u32) {
@@ -1386,8 +1386,8 @@ GroupPlan plan_group(const std::vector<SegmentData *> &segs, const pinot_query &
     const ColumnData &c0 = *segs[0]->column(agg_column(q.aggregations[a]));
     for (size_t si = 1; si < segs.size(); si++) same = same && same_dictionary(c0, *segs[si]->column(c0.name));
   }
-  size_t per_key = 4 + 32;  // shared count slot + 8 per-wave count copies
-  for (int a = 0; a < na; a++) per_key += lds_acc_bytes_per_key(ga.acc_kind[a], true);
+  size_t per_key = 4 + 16;  // shared count slot + 4 private count copies
+  for (int a = 0; a < na; a++) per_key += lds_acc_bytes_per_key(ga.acc_kind[a], false);  // u8 HLL registers
   int shift = 0;
   while (shift < 12 && ((size_t)2 << shift) * per_key <= (size_t)kReduceLdsBudget) shift++;
   const int64_t K = int64_t(1) << shift;
@@ -1410,13 +1410,13 @@ GroupPlan plan_group(const std::vector<SegmentData *> &segs, const pinot_query &
     gp.mode = GB_EMIT;  // COUNT + EMIT + reduce
     gp.shift = shift;
     gp.P = P;
-    size_t roff = ((size_t)K * 4 + 7) / 8 * 8;
+    size_t roff = ((size_t)K * 4 + 15) / 16 * 16;
     for (int a = 0; a < na; a++) {
       gp.reduce_off[a] = (int)roff;
-      roff += (size_t)K * lds_acc_bytes_per_key(ga.acc_kind[a], true);
+      roff += ((size_t)K * lds_acc_bytes_per_key(ga.acc_kind[a], false) + 15) / 16 * 16;
     }
     gp.reduce_wave_cnt_off = (int)roff;
-    roff += (size_t)K * 4 * 8;  // k_partition_reduce: 8 waves' private count copies
+    roff += (size_t)K * 4 * 4;  // k_partition_reduce: 4 private count copies
     gp.reduce_bytes = (int)roff;
     return gp;
   }
@@ -1448,6 +1448,20 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
   const int na = q.num_aggregations;
   const size_t S = segs.size();
   KeySpace ks = ks_in;
+  // aggregations repeating an earlier one's (accumulator kind, column) — SUM(x) and AVG(x) — share its
+  // accumulator: the device program accumulates it once (kind 5 for the duplicate)
+  std::vector<int> alias(na, -1);
+  GroupAccs gx = ga;
+  for (int a = 0; a < na; a++) {
+    if (ga.acc_kind[a] == 5) continue;
+    for (int b = 0; b < a; b++)
+      if (alias[b] < 0 && ga.acc_kind[b] == ga.acc_kind[a] &&
+          agg_column(q.aggregations[b]) == agg_column(q.aggregations[a])) {
+        alias[a] = b;
+        gx.acc_kind[a] = 5;
+        break;
+      }
+  }
   int64_t hcap = 0;
   if (ks.hashed) {  // slots: a power of two >= 2 x the docs that can match
     int64_t docs = 0;
@@ -1456,7 +1470,7 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     while (hcap < 2 * docs) hcap <<= 1;
     ks.G = hcap;
   }
-  const GroupPlan gp = plan_group(segs, q, ks, ga, ks.hashed ? std::string("global") : e.group_mode);
+  const GroupPlan gp = plan_group(segs, q, ks, gx, ks.hashed ? std::string("global") : e.group_mode);
   Arena ar;
   std::unique_ptr<FilterTreeInput> tree;
   if (q.num_filter_nodes > 0) tree = std::make_unique<FilterTreeInput>(decode_filter(q.num_filter_nodes, q.filter));
@@ -1480,24 +1494,27 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
   std::vector<size_t> acc_bytes(na, 0);
   size_t per_key = 8;
   for (int a = 0; a < na; a++) {
-    acc_bytes[a] = ga.acc_kind[a] == 5 ? 0 : ga.acc_kind[a] == 4 ? 256 : 8;
+    acc_bytes[a] = gx.acc_kind[a] == 5 ? 0 : gx.acc_kind[a] == 4 ? 256 : 8;
     per_key += acc_bytes[a];
   }
   size_t free_b = 0, total_b = 0;
   PINOT_HIP(hipMemGetInfo(&free_b, &total_b));
   require((double)ks.G * per_key < 0.5 * (double)free_b, PINOT_ERR_UNSUPPORTED, "dense group-by accumulators do not fit in HBM");
-  e.group_scratch.reserve(ks.G * per_key + 256 + S * 8);
+  const size_t head = 256 + (S * 8 + 255) / 256 * 256;  // matched [S] + verify flag, 256-B aligned arrays after
+  e.group_scratch.reserve(ks.G * per_key + head + 256 * (size_t)(na + 1));
   uint8_t *base = e.group_scratch.get<uint8_t>();
   auto *matched = reinterpret_cast<unsigned long long *>(base);
-  auto *counts = reinterpret_cast<unsigned long long *>(base + 256 + S * 8);
+  auto *counts = reinterpret_cast<unsigned long long *>(base + head);
   std::vector<void *> accs(na, nullptr);
   {
-    uint8_t *p = reinterpret_cast<uint8_t *>(counts) + ks.G * 8;
+    uint8_t *p = reinterpret_cast<uint8_t *>(counts) + (ks.G * 8 + 255) / 256 * 256;
     for (int a = 0; a < na; a++) {
       if (!acc_bytes[a]) continue;
       accs[a] = p;
-      p += ks.G * acc_bytes[a];
+      p += (ks.G * acc_bytes[a] + 255) / 256 * 256;
     }
+    for (int a = 0; a < na; a++)
+      if (alias[a] >= 0) accs[a] = accs[alias[a]];
   }
 
   // device program
@@ -1544,7 +1561,7 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     }
     for (int a = 0; a < na; a++) {
       GroupAggDev ag{};
-      ag.acc_kind = ga.acc_kind[a];
+      ag.acc_kind = gx.acc_kind[a];
       ag.acc = accs[a];
       if (ag.acc_kind != 5) {
         ColumnData &c = *s.column(agg_column(q.aggregations[a]));
@@ -1611,7 +1628,7 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
   if (gp.mode != GB_EMIT) {  // identities: counts / sums 0, min all-ones, max 0, HLL 0
     PINOT_HIP(hipMemsetAsync(counts, 0, ks.G * 8, e.stream));
     for (int i = 0; i < na; i++)
-      if (accs[i]) PINOT_HIP(hipMemsetAsync(accs[i], ga.acc_kind[i] == 2 ? 0xFF : 0, ks.G * acc_bytes[i], e.stream));
+      if (acc_bytes[i]) PINOT_HIP(hipMemsetAsync(accs[i], gx.acc_kind[i] == 2 ? 0xFF : 0, ks.G * acc_bytes[i], e.stream));
     if (ks.hashed) {
       PINOT_HIP(hipMemsetAsync(htable, 0, (size_t)hcap * 8, e.stream));
       PINOT_HIP(hipMemsetAsync(reps, 0xFF, (size_t)hcap * 8, e.stream));
@@ -1688,7 +1705,7 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     return exec_group_by_fused(e, segs, q, ks_in, ga, stats, attempt + 1);
   }
   int n_hll = 0;
-  for (int i = 0; i < na; i++) n_hll += ga.acc_kind[i] == 4;
+  for (int i = 0; i < na; i++) n_hll += gx.acc_kind[i] == 4;
   auto res = std::make_unique<GroupByResult>();
   res->num_columns = q.num_group_by;
   res->functions.resize(na);
@@ -1714,12 +1731,14 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
       res->hll_dev = std::make_shared<DeviceBuffer>((size_t)n_hll * n * 256 + 16);
       int h = 0;
       for (int i = 0; i < na; i++)
-        if (ga.acc_kind[i] == 4) {
+        if (gx.acc_kind[i] == 4) {
           res->hll_dev_off[i] = (size_t)h * n * 256;
           launch_gather_hll(static_cast<const uint8_t *>(accs[i]), keys_dev, (long long)n,
                             res->hll_dev->get<uint8_t>() + res->hll_dev_off[i], e.stream);
           h++;
         }
+      for (int i = 0; i < na; i++)
+        if (alias[i] >= 0 && ga.acc_kind[i] == 4) res->hll_dev_off[i] = res->hll_dev_off[alias[i]];
       PINOT_HIP(hipGetLastError());
     }
     std::vector<uint8_t> host(out_b);
@@ -1739,17 +1758,21 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     const auto *hacc = hc + n;
     const auto *hhs = hacc + n * na;
     const auto *hhz = reinterpret_cast<const uint32_t *>(hhs + (size_t)n_hll * n);
-    int h = 0;
+    std::vector<int> hidx(na, -1);  // HLL register-sum row of each (primary) HLL aggregation
+    for (int i = 0, h = 0; i < na; i++)
+      if (gx.acc_kind[i] == 4) hidx[i] = h++;
     for (int i = 0; i < na; i++) {
       auto &cv = res->counts[i];
       auto &vv = res->values[i];
       cv.resize(n);
       vv.resize(n);
       const int ak = ga.acc_kind[i];
+      const int src = alias[i] >= 0 ? alias[i] : i;  // the accumulator this aggregation reads
+      const int h = hidx[src];
       if (ak == 4) res->hll_card[i].resize(n);
       for (size_t g = 0; g < n; g++) {
         cv[g] = (int64_t)hc[g];
-        const uint64_t raw = hacc[(size_t)i * n + g];
+        const uint64_t raw = hacc[(size_t)src * n + g];
         switch (ak) {
           case 0: vv[g] = (double)(int64_t)raw; break;
           case 1: { double d; memcpy(&d, &raw, 8); vv[g] = d; break; }
@@ -1764,7 +1787,6 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
           default: vv[g] = (double)hc[g]; break;
         }
       }
-      if (ak == 4) h++;
     }
   }
   PINOT_HIP(hipEventRecord(e.ev_stop, e.stream));

@@ -25,6 +25,7 @@ namespace {
 using namespace dev;
 
 constexpr int kReduceBlock = 512;
+constexpr int kReduceCountCopies = 4;  // private count copies (waves w, w + 4 share one)
 
 __device__ __forceinline__ unsigned long long ordered_bits_r(double d) {
   const unsigned long long u = (unsigned long long)__double_as_longlong(d);
@@ -57,7 +58,7 @@ __global__ __launch_bounds__(kReduceBlock) void k_partition_reduce(PartitionRedu
   const unsigned long long kmask = (unsigned long long)K - 1ull;
   // counts: one private copy per wave (a partition has few keys: LDS atomics on one copy serialise)
   const int wave = tid >> 6;
-  uint32_t *wcnt = cnt + a.wave_cnt_off / 4 + wave * K;
+  uint32_t *wcnt = cnt + a.wave_cnt_off / 4 + (wave & (kReduceCountCopies - 1)) * K;
   for (uint32_t r = b + tid; r < e; r += kReduceBlock) {
     const unsigned long long rec = __builtin_nontemporal_load(a.records + r);
     const uint32_t k = (uint32_t)(rec & kmask);
@@ -85,9 +86,17 @@ __global__ __launch_bounds__(kReduceBlock) void k_partition_reduce(PartitionRedu
           atomicMax(reinterpret_cast<unsigned long long *>(acc) + k,
                     ordered_bits_r(dict_value_r(ag.dict, ag.value_kind, id)));
           break;
-        case 4: {
+        case 4: {  // u8 registers: byte max by CAS on the containing dword (conflicts are rare)
           const uint32_t h = ag.hll_lut[id];
-          atomicMax(reinterpret_cast<uint32_t *>(acc) + k * 256 + (h >> 8), h & 0xFFu);
+          const uint32_t idx = k * 256 + (h >> 8), rank = h & 0xFFu;
+          uint32_t *word = reinterpret_cast<uint32_t *>(acc) + (idx >> 2);
+          const int sh = (int)(idx & 3) * 8;
+          uint32_t old = *word;
+          while (((old >> sh) & 0xFFu) < rank) {
+            const uint32_t seen = atomicCAS(word, old, (old & ~(0xFFu << sh)) | (rank << sh));
+            if (seen == old) break;
+            old = seen;
+          }
           break;
         }
         default:
@@ -101,19 +110,17 @@ __global__ __launch_bounds__(kReduceBlock) void k_partition_reduce(PartitionRedu
     const long long key = base + i;
     if (key >= a.G) break;
     uint32_t c = 0;
-    for (int w = 0; w < kReduceBlock / 64; w++) c += cnt[a.wave_cnt_off / 4 + w * K + i];
+    for (int w = 0; w < kReduceCountCopies; w++) c += cnt[a.wave_cnt_off / 4 + w * K + i];
     a.counts[key] = c;
   }
   for (int g = 0; g < a.n_aggs; g++) {
     const GroupAggDev &ag = a.aggs[g];
     if (ag.acc_kind == 5) continue;
     const uint8_t *acc = lds + ag.lds_off;
-    if (ag.acc_kind == 4) {
-      uint8_t *out = static_cast<uint8_t *>(ag.acc);
-      for (int i = tid; i < K * 256; i += kReduceBlock) {
-        const long long key = base + i / 256;
-        if (key < a.G) out[base * 256 + i] = (uint8_t)reinterpret_cast<const uint32_t *>(acc)[i];
-      }
+    if (ag.acc_kind == 4) {  // u8 [K][256] -> u8 [G][256], 16 B per thread
+      u32x4 *out = reinterpret_cast<u32x4 *>(static_cast<uint8_t *>(ag.acc) + base * 256);
+      const long long nkeys = std::min<long long>((long long)K, a.G - base);
+      for (long long i = tid; i < nkeys * 16; i += kReduceBlock) out[i] = reinterpret_cast<const u32x4 *>(acc)[i];
     } else {
       unsigned long long *out = static_cast<unsigned long long *>(ag.acc);
       for (int i = tid; i < K; i += kReduceBlock) {

@@ -299,9 +299,15 @@ def test_group_by_sinks(mode, seed):
     gsegs = [e.register(x) for x in segs]
     ex = ServerQueryExecutor(e)
     gpool = ["i0", "i1", "i2", "s", "i3"]
-    for _ in range(4):
+    # repeated (accumulator kind, column) pairs share one device accumulator (SUM + AVG, HLL twice, MIN twice)
+    dup = [{"function": f, "column": c} for f, c in (("SUM", "i0"), ("AVG", "i0"), ("COUNT", "*"),
+                                                     ("DISTINCTCOUNTHLL", "i1"), ("DISTINCTCOUNTHLL", "i1"),
+                                                     ("MIN", "big"), ("MIN", "big"), ("AVG", "i0"))]
+    for it in range(5):
         gcols = list(rng.choice(gpool, size=int(rng.integers(1, 3)), replace=False))
         aggs = [x for x in _random_aggs(rng) if x["column"] != "srt"] or [{"function": "COUNT", "column": "*"}]
+        if it == 0:
+            aggs = dup
         q = {"aggregations": aggs, "filter": _random_tree(rng, segs[0]) if rng.random() < 0.7 else None,
              "group_by": {"columns": gcols, "top_n": 10}}
         got, st = ex.process_query(q, gsegs, trim=False)

@@ -20,6 +20,7 @@
 #include <cmath>
 #include <cstring>
 #include <map>
+#include <tuple>
 #include <numeric>
 #include <set>
 
@@ -52,7 +53,10 @@ struct FilterStep {
   int negate = 0;  // SCAN: negate; ROARING: exclusive; FILL: value
   int mode = CM_WRITE;
   int dst = 0, src = 0;
+  int join = JOIN_NEW;  // fused leaves: how the leaf joins the filter program (FusedJoin)
 };
+
+constexpr int kMaxFusedRoaringIds = 64;  // bitmap leaves with more dictIds are expanded to a `pre` bitset
 
 struct SegPlan {
   SegmentData *seg = nullptr;
@@ -88,12 +92,18 @@ class Compiler {
   // Fused plan: the scan leaves of the top-level conjunction (AndFilterOperator puts scans last and
   // applies them only to the candidates of the index children, AndBlockDocIdSet.java:144-227) become
   // k_scan_query leaves; every other conjunct is built into slot 0 = the kernel's `pre` bitset.
-  // max_fused_bits: wider scan leaves go to the `pre` program (the group kernel's 16 wave stages are small)
+  // Fused plan: the top-level conjunction (AndFilterOperator: index children first, scans last,
+  // AndBlockDocIdSet.java:144-227) becomes a program of terms evaluated per chunk in registers: a term is
+  // one leaf — scan (decoded from the staged column), sorted (doc ranges) or bitmap (roaring containers,
+  // at most kMaxFusedRoaringIds dictIds) — or an AND / OR of such leaves (OrBlockDocIdSet.java:78-120).
+  // Deeper subtrees, wider scans (> max_fused_bits: the group kernel's 16 wave stages are small) and long
+  // bitmap lists are built into slot 0 = the kernel's `pre` bitset by the launch sequence.
   void run_fused(const FilterTreeInput *tree, int max_fused_bits = 32) {
     FilterNode root = plan_filter(seg_, tree);
     if (root.type == FilterNode::EMPTY) { sp_.empty = true; return; }
     if (root.type == FilterNode::MATCH_ALL) { sp_.match_all = true; return; }
     next_slot_ = 1;
+    max_fused_bits_ = max_fused_bits;
     std::vector<const FilterNode *> conj;
     if (root.type == FilterNode::AND) {
       for (const auto &c : root.children) conj.push_back(&c);
@@ -103,12 +113,19 @@ class Compiler {
     for (const FilterNode *c : conj) {
       const int mode = sp_.has_pre ? CM_AND : CM_WRITE;
       if (c->type == FilterNode::AND || c->type == FilterNode::OR) {
+        if (fuse_term(*c)) continue;
+        eval(*c, 0, mode);
+        sp_.has_pre = true;
+        continue;
+      }
+      if (c->type == FilterNode::EMPTY || c->type == FilterNode::MATCH_ALL) {
         eval(*c, 0, mode);
         sp_.has_pre = true;
         continue;
       }
       FilterStep st = leaf_step(*c);
-      if (st.kind == FilterStep::SCAN && seg_.cols[st.col]->bits <= max_fused_bits) {
+      if (fusable(st)) {
+        st.join = JOIN_NEW;
         sp_.fused_leaves.push_back(st);
       } else {
         st.dst = 0;
@@ -120,6 +137,31 @@ class Compiler {
   }
 
  private:
+  bool fusable(const FilterStep &st) const {
+    if (st.kind == FilterStep::SCAN) return seg_.cols[st.col]->bits <= max_fused_bits_;
+    if (st.kind == FilterStep::RANGES) return true;
+    return st.kind == FilterStep::ROARING && st.n <= kMaxFusedRoaringIds;
+  }
+  // An AND / OR whose children are all fusable leaves -> one term of the fused program.
+  bool fuse_term(const FilterNode &n) {
+    for (const auto &c : n.children)
+      if (c.type == FilterNode::AND || c.type == FilterNode::OR || c.type == FilterNode::EMPTY ||
+          c.type == FilterNode::MATCH_ALL)
+        return false;
+    const int64_t scans_before = sp_.scan_leaves;
+    std::vector<FilterStep> leaves;
+    for (const auto &c : n.children) {
+      FilterStep st = leaf_step(c);
+      if (!fusable(st)) {
+        sp_.scan_leaves = scans_before;  // eval() plans these leaves again
+        return false;
+      }
+      st.join = leaves.empty() ? JOIN_NEW : (n.type == FilterNode::OR ? JOIN_OR : JOIN_AND);
+      leaves.push_back(st);
+    }
+    for (auto &st : leaves) sp_.fused_leaves.push_back(st);
+    return true;
+  }
   int alloc_slot() {
     const int s = next_slot_++;
     sp_.slots = std::max(sp_.slots, next_slot_);
@@ -236,6 +278,7 @@ class Compiler {
     }
   }
 
+  int max_fused_bits_ = 32;
   Engine &e_;
   SegPlan &sp_;
   Arena &ar_;
@@ -505,6 +548,57 @@ AggRoute route_agg(Engine &e, SegmentData &s, const pinot_agg_spec &spec) {
 
 namespace {
 
+// Chunk window of a segment's fused program: a top-level term that is a single sorted-index leaf bounds
+// the candidate docs to [first range start, last range end] (SortedInvertedIndexBasedFilterOperator's
+// docId ranges), so the kernels only visit the 4096-doc chunks inside it.
+std::pair<int64_t, int64_t> chunk_window(const SegPlan &p, const Arena &ar) {
+  const int64_t nchunks = (p.seg->nwords() + 63) / 64;
+  int64_t lo = 0, hi = nchunks;
+  const auto &L = p.fused_leaves;
+  for (size_t i = 0; i < L.size(); i++) {
+    const bool single = L[i].join == JOIN_NEW && (i + 1 == L.size() || L[i + 1].join == JOIN_NEW);
+    if (!single || L[i].kind != FilterStep::RANGES) continue;
+    if (L[i].n == 0) return {0, 0};
+    const int32_t *r = reinterpret_cast<const int32_t *>(ar.bytes.data() + L[i].off);
+    lo = std::max<int64_t>(lo, (int64_t)r[0] / 4096);
+    hi = std::min<int64_t>(hi, (int64_t)r[2 * (L[i].n - 1) + 1] / 4096 + 1);
+  }
+  return {lo, std::max(lo, hi)};
+}
+
+// A fused leaf (FilterStep) as the device step k_scan_query / k_group_query evaluate.
+FusedStep fused_leaf_step(const SegmentData &s, const FilterStep &l, const uint8_t *arena) {
+  const ColumnData &c = *s.cols[l.col];
+  FusedStep st{};
+  st.join = l.join;
+  st.negate = l.negate;
+  switch (l.kind) {
+    case FilterStep::RANGES:
+      st.kind = FK_LEAF_RANGES;
+      st.table = arena + l.off;
+      st.lo = (uint32_t)l.n;
+      break;
+    case FilterStep::ROARING:
+      st.kind = FK_LEAF_ROARING;
+      st.fwd = c.inv_payload.get<uint8_t>();
+      st.aux0 = c.inv_containers.get();
+      st.aux1 = c.inv_dir_dev.get();
+      st.table = arena + l.off;
+      st.lo = (uint32_t)l.n;
+      break;
+    default:
+      st.fwd = c.fwd.get<uint8_t>();
+      st.bits = c.bits;
+      st.kind = l.leaf_kind == LEAF_RANGE ? FK_LEAF_RANGE : l.leaf_kind == LEAF_LUT64 ? FK_LEAF_LUT64 : FK_LEAF_LUT;
+      st.lo = l.lo;
+      st.span = l.span;
+      st.lut64 = l.lut64;
+      st.table = arena + l.off;
+      break;
+  }
+  return st;
+}
+
 // Where the device left aggregation a of segment si: index into the reduced u64 results, and for
 // DISTINCTCOUNTHLL the register set (256 u32) holding its merged registers.
 struct AggResults {
@@ -635,7 +729,8 @@ void aggregate_fused(Engine &e, const std::vector<SegmentData *> &segs, const pi
   size_t nsteps = 0;
   for (auto &p : plans) {
     nsteps += p.fused_leaves.size() + nfolds;
-    for (auto &l : p.fused_leaves) max_bits = std::max(max_bits, p.seg->cols[l.col]->bits);
+    for (auto &l : p.fused_leaves)
+      if (l.kind == FilterStep::SCAN) max_bits = std::max(max_bits, p.seg->cols[l.col]->bits);
     for (auto &c : fold_cols) max_bits = std::max(max_bits, p.seg->column(c)->bits);
   }
   const size_t tab_bytes = S * sizeof(FusedSegment) + nsteps * sizeof(FusedStep) + 256;  // + alignment/padding of two adds
@@ -653,19 +748,8 @@ void aggregate_fused(Engine &e, const std::vector<SegmentData *> &segs, const pi
     fs.first_step = (int32_t)fsteps.size();
     fs.n_leaves = (int32_t)p.fused_leaves.size();
     fs.n_folds = nfolds;
-    for (const FilterStep &l : p.fused_leaves) {
-      const ColumnData &c = *s.cols[l.col];
-      FusedStep st{};
-      st.fwd = c.fwd.get<uint8_t>();
-      st.bits = c.bits;
-      st.kind = l.leaf_kind == LEAF_RANGE ? FK_LEAF_RANGE : l.leaf_kind == LEAF_LUT64 ? FK_LEAF_LUT64 : FK_LEAF_LUT;
-      st.negate = l.negate;
-      st.lo = l.lo;
-      st.span = l.span;
-      st.lut64 = l.lut64;
-      st.table = qs.arena + l.off;
-      fsteps.push_back(st);
-    }
+    std::tie(fs.ch_begin, fs.ch_end) = chunk_window(p, ar);
+    for (const FilterStep &l : p.fused_leaves) fsteps.push_back(fused_leaf_step(s, l, qs.arena));
     for (int f = 0; f < nfolds; f++) {
       ColumnData &c = *s.column(fold_cols[f]);
       FusedStep st{};
@@ -706,11 +790,12 @@ void aggregate_fused(Engine &e, const std::vector<SegmentData *> &segs, const pi
 
   // grid: one resident wave of blocks, split evenly over the segments (equal work per block)
   const int stage_bytes = pipelined ? slot_bytes : 1024 * ((max_bits + 1) / 2);
-  int64_t max_chunks = 1;
-  for (auto *sg : segs) max_chunks = std::max<int64_t>(max_chunks, (sg->nwords() + 63) / 64);
+  int64_t max_chunks = 1;  // chunks in the largest segment window
+  for (const FusedSegment &fs : fsegs) max_chunks = std::max<int64_t>(max_chunks, fs.ch_end - fs.ch_begin);
   bool gathers = false;
   for (const FusedStep &st : fsteps)
-    gathers = gathers || st.kind == FK_LEAF_LUT || (st.kind == FK_FOLD && (st.ops & (FOLD_DICT32 | FOLD_HLL)));
+    gathers = gathers || st.kind == FK_LEAF_LUT || st.kind == FK_LEAF_RANGES || st.kind == FK_LEAF_ROARING ||
+              (st.kind == FK_FOLD && (st.ops & (FOLD_DICT32 | FOLD_HLL)));
   const int64_t resident = (int64_t)scan_query_blocks_per_cu(stage_bytes, gathers, pipelined) * e.num_cus;
   int bps = (int)std::max<int64_t>(1, resident / (int64_t)S);
   bps = (int)std::min<int64_t>(bps, (max_chunks + 3) / 4);
@@ -1534,19 +1619,10 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     g.n_leaves = (int32_t)p.fused_leaves.size();
     g.first_gcol = (int32_t)gcols.size();
     g.first_agg = (int32_t)gaggs.size();
+    std::tie(g.ch_begin, g.ch_end) = chunk_window(p, ar);
     for (const FilterStep &l : p.fused_leaves) {
-      const ColumnData &c = *s.cols[l.col];
-      FusedStep st{};
-      st.fwd = c.fwd.get<uint8_t>();
-      st.bits = c.bits;
-      st.kind = l.leaf_kind == LEAF_RANGE ? FK_LEAF_RANGE : l.leaf_kind == LEAF_LUT64 ? FK_LEAF_LUT64 : FK_LEAF_LUT;
-      st.negate = l.negate;
-      st.lo = l.lo;
-      st.span = l.span;
-      st.lut64 = l.lut64;
-      st.table = qs.arena + l.off;
-      leaves.push_back(st);
-      max_leaf_bits = std::max(max_leaf_bits, c.bits);
+      leaves.push_back(fused_leaf_step(s, l, qs.arena));
+      max_leaf_bits = std::max(max_leaf_bits, leaves.back().bits);
     }
     long long stride = 1;
     for (int j = 0; j < q.num_group_by; j++) {
@@ -1613,8 +1689,8 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     a.hseed = 0x5EEDF00Dull + 0x9E3779B97F4A7C15ull * (unsigned long long)attempt;
     a.verify_err = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(matched) + S * 8 + 16);
   }
-  int64_t max_chunks = 1;
-  for (auto *sg : segs) max_chunks = std::max<int64_t>(max_chunks, (sg->nwords() + 63) / 64);
+  int64_t max_chunks = 1;  // chunks in the largest segment window
+  for (const GroupSegment &g : gsegs) max_chunks = std::max<int64_t>(max_chunks, g.ch_end - g.ch_begin);
   const int64_t resident = (int64_t)group_query_blocks_per_cu(a) * e.num_cus;
   a.bps = (int)std::max<int64_t>(1, std::min<int64_t>(resident / (int64_t)S, (max_chunks + 15) / 16));
   const int64_t nblk = (int64_t)S * a.bps;

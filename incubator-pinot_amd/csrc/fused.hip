@@ -346,18 +346,124 @@ __device__ __forceinline__ void flush_block(const FusedArgs &a, uint8_t *stage_l
   if (tid == 0) *a.done = 0;
 }
 
-// One chunk of the segment program: leaves AND-ed into `mask` (early exit once the wave's mask is
-// empty), then the folds over the surviving docs. `src(i, st)` returns the LDS address of step i's
-// staged chunk (staging it first in the stepwise kernel). Returns the chunk's matching doc count.
+// ---------------------------------------------------------------- index leaves evaluated in registers
+// The lane's 64-doc word w of a sorted-index leaf (SortedInvertedIndexBasedFilterOperator: matching
+// dictIds -> merged inclusive doc ranges) and of a bitmap-index leaf (BitmapBasedFilterOperator: OR of the
+// dictIds' roaring bitmaps, flipped when exclusive), computed on the fly from the ranges / roaring
+// containers — no dense bitset is materialised. A 4096-doc chunk lies inside one 65536-doc roaring key,
+// so the container search is wave-uniform.
+__device__ __forceinline__ uint64_t bits_between(int lo_bit, int hi_bit) {  // inclusive, 0 <= lo <= hi <= 63
+  const uint64_t upper = hi_bit == 63 ? ~0ull : ((1ull << (hi_bit + 1)) - 1ull);
+  return upper & (~0ull << lo_bit);
+}
+
+__device__ __forceinline__ uint64_t ranges_word(const int32_t *__restrict__ r, int n, int64_t w) {
+  const int64_t lo = w * 64, hi = lo + 63;
+  int l = 0, h = n;
+  while (l < h) {  // first range ending at or after lo
+    const int m = (l + h) >> 1;
+    if (r[2 * m + 1] < lo) l = m + 1;
+    else h = m;
+  }
+  uint64_t x = 0;
+  for (int i = l; i < n && r[2 * i] <= hi; i++) {
+    const int64_t s = max((int64_t)r[2 * i], lo), e = min((int64_t)r[2 * i + 1], hi);
+    x |= bits_between((int)(s - lo), (int)(e - lo));
+  }
+  return x;
+}
+
+__device__ __forceinline__ uint32_t ld16(const uint8_t *p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8); }
+
+__device__ __forceinline__ uint64_t roaring_word(const FusedStep &st, int64_t w) {
+  const uint8_t *payload = st.fwd;
+  const RoaringContainer *conts = static_cast<const RoaringContainer *>(st.aux0);
+  const int32_t *dir = static_cast<const int32_t *>(st.aux1);
+  const int32_t *ids = static_cast<const int32_t *>(st.table);
+  const uint32_t key = (uint32_t)(w >> 10);            // 1024 words per roaring key
+  const uint32_t first = (uint32_t)(w & 1023) * 64;    // the word's first low-16 doc
+  uint64_t x = 0;
+  for (int i = 0; i < (int)st.lo; i++) {
+    const int id = ids[i];
+    int l = dir[id], r = dir[id + 1];
+    const int end = r;
+    while (l < r) {
+      const int m = (l + r) >> 1;
+      if (conts[m].key < key) l = m + 1;
+      else r = m;
+    }
+    if (l >= end || conts[l].key != key) continue;
+    const RoaringContainer c = conts[l];
+    const uint8_t *p = payload + c.payload_offset;
+    if (c.type == 1) {  // bitmap container: 1024 LE u64 words
+      const uint8_t *q = p + (first >> 3);
+      x |= (uint64_t)ld16(q) | ((uint64_t)ld16(q + 2) << 16) | ((uint64_t)ld16(q + 4) << 32) |
+           ((uint64_t)ld16(q + 6) << 48);
+    } else if (c.type == 0) {  // sorted u16 array
+      int a = 0, b = (int)c.cardinality;
+      while (a < b) {
+        const int m = (a + b) >> 1;
+        if (ld16(p + 2 * m) < first) a = m + 1;
+        else b = m;
+      }
+      for (; a < (int)c.cardinality; a++) {
+        const uint32_t v = ld16(p + 2 * a);
+        if (v >= first + 64) break;
+        x |= 1ull << (v - first);
+      }
+    } else {  // run container: (start, length - 1) pairs
+      for (uint32_t k = 0; k < c.cardinality; k++) {
+        const uint32_t s0 = ld16(p + 4 * k), e0 = s0 + ld16(p + 4 * k + 2);
+        if (s0 >= first + 64) break;
+        if (e0 < first) continue;
+        x |= bits_between((int)(max(s0, first) - first), (int)(min(e0, first + 63) - first));
+      }
+    }
+  }
+  return st.negate ? ~x : x;
+}
+
+// One leaf's 64-bit word for this lane (scan leaves decode the staged chunk).
+template <bool G, typename Src>
+__device__ __forceinline__ uint64_t leaf_word(const FusedStep &st, int i, int64_t w, int lane, Src &src) {
+  if (G && st.kind == FK_LEAF_RANGES) return ranges_word(static_cast<const int32_t *>(st.table), (int)st.lo, w);
+  if (G && st.kind == FK_LEAF_ROARING) return roaring_word(st, w);
+  uint64_t x = ~0ull;
+  leaf_rt<G>(st, src(i, st) + lane * (8 * st.bits), x);
+  return x;
+}
+
+// The filter program of a chunk: terms AND-ed into `mask` (early exit once the wave's mask is empty).
+template <bool G, typename Src>
+__device__ __forceinline__ uint64_t eval_filter(const FusedStep *__restrict__ steps, int n_leaves, uint64_t mask,
+                                                int64_t w, int64_t nwords, int32_t num_docs, int lane, Src &&src) {
+  uint64_t term = ~0ull;
+  bool pending = false;
+  for (int i = 0; i < n_leaves; i++) {
+    const FusedStep st = load_const(steps + i);
+    if (st.join == JOIN_NEW) {
+      if (pending) mask &= term;
+      pending = false;
+      if (!__any(mask != 0)) return 0;  // wave-uniform: nothing left in this chunk, skip its other columns
+    }
+    uint64_t x = leaf_word<G>(st, i, w, lane, src);
+    x = w < nwords ? x & tail_mask(w, nwords, num_docs) : 0ull;
+    if (st.join == JOIN_NEW) term = x;
+    else if (st.join == JOIN_OR) term |= x;
+    else term &= x;
+    pending = true;
+  }
+  return pending ? (mask & term) : mask;
+}
+
+// One chunk of the segment program: the filter program, then the folds over the surviving docs.
+// `src(i, st)` returns the LDS address of step i's staged chunk (staging it first in the stepwise kernel). Returns the chunk's matching doc count.
 template <bool G, typename Src>
 __device__ __forceinline__ unsigned long long eval_chunk(const FusedStep *__restrict__ steps, int n_leaves,
                                                          int n_folds, uint64_t mask, FoldAcc &A, HllRegs *hll,
-                                                         int lane, Src &&src) {
-  for (int i = 0; i < n_leaves; i++) {
-    if (!__any(mask != 0)) break;  // wave-uniform: nothing left in this chunk, skip its other columns
-    const FusedStep st = load_const(steps + i);
-    leaf_rt<G>(st, src(i, st) + lane * (8 * st.bits), mask);
-  }
+                                                         int64_t w, int64_t nwords, int32_t num_docs, int lane,
+                                                         Src &&src) {
+  mask = eval_filter<G>(steps, n_leaves, mask, w, nwords, num_docs, lane, src);
   const unsigned long long cnt = __popcll(mask);
   for (int i = 0; i < n_folds; i++) {
     if (!__any(mask != 0)) break;
@@ -403,9 +509,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G ? 2 : 
   unsigned long long cnt = 0;
   FoldAcc A;
   init_acc(A);
-  const int64_t nchunks = (sg.nwords + 63) >> 6;
-  for (int64_t ch = (int64_t)b * kFusedWaves + wave; ch < nchunks; ch += (int64_t)a.bps * kFusedWaves) {
-    cnt += eval_chunk<G>(steps, sg.n_leaves, sg.n_folds, chunk_word(sg.pre, sg.nwords, sg.num_docs, ch, lane), A, hll, lane,
+  const int64_t nchunks = min((sg.nwords + 63) >> 6, sg.ch_end);
+  for (int64_t ch = sg.ch_begin + (int64_t)b * kFusedWaves + wave; ch < nchunks; ch += (int64_t)a.bps * kFusedWaves) {
+    cnt += eval_chunk<G>(steps, sg.n_leaves, sg.n_folds, chunk_word(sg.pre, sg.nwords, sg.num_docs, ch, lane), A, hll,
+                         ch * 64 + lane, sg.nwords, sg.num_docs, lane,
                          [&](int, const FusedStep &st) -> const uint8_t * {
                            stage_chunk_rt(st.fwd, st.bits, ch, lds_wave, lane);
                            wait_stage();
@@ -450,7 +557,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_query_pipe(FusedArgs a) {
   const FusedStep *steps = a.steps + sg.first_step;
   const int nsteps = sg.n_leaves + sg.n_folds;
   uint8_t *const slots = stage_lds + (size_t)wave * 2 * a.stage_bytes;
-  const int64_t nchunks = (sg.nwords + 63) >> 6;
+  const int64_t nchunks = min((sg.nwords + 63) >> 6, sg.ch_end);
   const int64_t stride = (int64_t)a.bps * kFusedWaves;
   auto slot = [&](int p) { return slots + p * a.stage_bytes; };
   auto stage_cols = [&](int64_t c, uint8_t *dst) {
@@ -462,7 +569,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_query_pipe(FusedArgs a) {
   unsigned long long cnt = 0;
   FoldAcc A;
   init_acc(A);
-  int64_t ch = (int64_t)b * kFusedWaves + wave;
+  int64_t ch = sg.ch_begin + (int64_t)b * kFusedWaves + wave;
   // prologue: pre words of ch (slot 0 area, waited for), of ch + stride (slot 1 area, read at iteration 0)
   if (sg.pre && ch < nchunks) stage_pre(sg.pre, ch, slot(0), lane);
   wait_stage();
@@ -480,7 +587,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_query_pipe(FusedArgs a) {
     // cur's pre area (pre words of ch, read one iteration ago) is free again
     if (sg.pre && ch + 2 * stride < nchunks) stage_pre(sg.pre, ch + 2 * stride, cur, lane);
     if (live0)
-      cnt += eval_chunk<G>(steps, sg.n_leaves, sg.n_folds, m0, A, hll, lane,
+      cnt += eval_chunk<G>(steps, sg.n_leaves, sg.n_folds, m0, A, hll, ch * 64 + lane, sg.nwords, sg.num_docs, lane,
                            [&](int, const FusedStep &st) -> const uint8_t * { return cur + st.stage_off; });
     m0 = m1;
     live0 = live1;
@@ -795,17 +902,16 @@ __global__ __launch_bounds__(kGroupBlock) void k_group_query(GroupArgs a) {
     for (int p = tid; p < a.P; p += kGroupBlock) plds[p] = a.offsets[(size_t)p * nblk + blockIdx.x];
     __syncthreads();
   }
-  const int64_t nchunks = (sg.nwords + 63) >> 6;
+  const int64_t nchunks = min((sg.nwords + 63) >> 6, sg.ch_end);
   unsigned long long matched = 0;
-  for (int64_t ch = (int64_t)b * kGroupWaves + wave; ch < nchunks; ch += (int64_t)a.bps * kGroupWaves) {
+  for (int64_t ch = sg.ch_begin + (int64_t)b * kGroupWaves + wave; ch < nchunks; ch += (int64_t)a.bps * kGroupWaves) {
     uint64_t mask = chunk_word(sg.pre, sg.nwords, sg.num_docs, ch, lane);
-    for (int i = 0; i < sg.n_leaves; i++) {
-      if (!__any(mask != 0)) break;
-      const FusedStep st = load_const(leaves + i);
-      stage_chunk_rt(st.fwd, st.bits, ch, stage, lane);
-      wait_stage();
-      leaf_rt<true>(st, stage + lane * (8 * st.bits), mask);
-    }
+    mask = eval_filter<true>(leaves, sg.n_leaves, mask, ch * 64 + lane, sg.nwords, sg.num_docs, lane,
+                             [&](int, const FusedStep &st) -> const uint8_t * {
+                               stage_chunk_rt(st.fwd, st.bits, ch, stage, lane);
+                               wait_stage();
+                               return stage;
+                             });
     matched += __popcll(mask);
     if (__any(mask != 0)) group_chunk<MODE>(a, sg, ch, mask, lane, acc_lds, plds);
   }

@@ -105,7 +105,16 @@ int scan_grid(int64_t nwords);
 // written to HBM), optionally starting from a `pre` bitset (index leaves / OR subtrees, evaluated by
 // the kernels below), skips the rest of the chunk as soon as the wave's mask is empty, then folds
 // the aggregated columns of the matching docs.
-enum FusedKind : int32_t { FK_LEAF_RANGE = 0, FK_LEAF_LUT64 = 1, FK_LEAF_LUT = 2, FK_FOLD = 3 };
+enum FusedKind : int32_t {
+  FK_LEAF_RANGE = 0, FK_LEAF_LUT64 = 1, FK_LEAF_LUT = 2, FK_FOLD = 3,
+  FK_LEAF_RANGES = 4,   // sorted-index leaf: inclusive [start, end] doc ranges (table, n = lo)
+  FK_LEAF_ROARING = 5   // bitmap-index leaf: OR of the dictIds' roaring bitmaps (fwd = payload, aux0 = containers,
+                        // aux1 = per-dictId container directory, table = dictIds, n = lo), negate = exclusive
+};
+// How a leaf joins the filter program (the top-level conjunction of terms, a term = one leaf or an
+// AND / OR of leaves): JOIN_NEW starts a term (the previous one is AND-ed into the mask), JOIN_OR /
+// JOIN_AND combine the leaf into the current term.
+enum FusedJoin : int32_t { JOIN_NEW = 0, JOIN_OR = 1, JOIN_AND = 2 };
 enum FoldOps : int32_t { FOLD_IDSUM = 1, FOLD_MINMAX = 2, FOLD_DICT32 = 4, FOLD_HLL = 8 };
 constexpr int kMaxFusedFolds = 6;                      // distinct aggregated columns per query
 constexpr int kMaxFusedSlots = 1 + 2 * kMaxFusedFolds; // slot 0 count; fold f: 1 + 2f sum, 2 + 2f min/max
@@ -119,7 +128,8 @@ struct FusedStep {           // one (segment, leaf or fold) pair, built on the h
   int32_t bits, kind, negate, ops;
   int32_t fold, hll_set;     // FK_FOLD: fold index (slots 1 + 2f, 2 + 2f), HLL register set
   int32_t stage_off;         // pipelined kernel: byte offset of this step's chunk within the wave's LDS slot
-  int32_t reserved;
+  int32_t join;              // leaves: FusedJoin
+  const void *aux0, *aux1;   // FK_LEAF_ROARING: containers, directory
 };
 
 struct FusedSegment {
@@ -129,6 +139,7 @@ struct FusedSegment {
   int32_t first_step;        // leaves [first, first + n_leaves), then folds
   int32_t n_leaves;
   int32_t n_folds;
+  int64_t ch_begin, ch_end;  // chunk window: a top-level sorted-index term bounds the candidate docs
 };
 
 struct FusedArgs {
@@ -203,6 +214,7 @@ struct GroupSegment {
   int32_t first_leaf, n_leaves;
   int32_t first_gcol, first_agg;
   int32_t reserved;
+  int64_t ch_begin, ch_end;  // chunk window (see FusedSegment)
 };
 
 struct GroupArgs {

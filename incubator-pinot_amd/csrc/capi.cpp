@@ -88,6 +88,7 @@ void parse_config(Engine &e, const char *cfg) {
               "group.mode: auto | lds | global | partition");
       e.group_mode = v == "auto" ? "" : v;
     } else if (k == "sync.poll") e.sync_poll = v == "1" || v == "true";
+    else if (k == "debug.emit") e.debug_emit = std::stoi(v);
     else if (k == "debug.host_phases") e.host_phases = v == "1" || v == "true";
     else if (k == "exec.nt") e.use_nt = v == "1" || v == "true";
     else if (k == "exec.pipe") e.use_pipe = v == "1" || v == "true";

@@ -115,7 +115,8 @@ struct Engine {
   bool timing = false;
   std::string group_mode;     // group.mode: "" (auto) | lds | global | partition (tests force a sink)
   bool sync_poll = false;     // sync.poll: busy-poll the stream instead of hipStreamSynchronize
-  bool host_phases = false;   // debug.host_phases: print the host-side phase times of fused queries
+  bool host_phases = false;
+  int debug_emit = 0;         // debug.emit: GB_EMIT store experiments (timing only, wrong results)   // debug.host_phases: print the host-side phase times of fused queries
   int num_cus = 256;          // multiProcessorCount of the device
 
   // scratch (grow-only)

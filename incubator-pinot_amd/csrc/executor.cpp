@@ -1677,6 +1677,7 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
   a.shift = gp.shift;
   a.P = (int32_t)gp.P;
   a.mode = gp.mode == GB_EMIT ? GB_COUNT : gp.mode;
+  a.reserved2 = e.debug_emit;  // timing experiments only (debug.emit)
   unsigned long long *htable = nullptr, *reps = nullptr;
   if (ks.hashed) {
     e.group_hash.reserve((size_t)hcap * 16 + 256);

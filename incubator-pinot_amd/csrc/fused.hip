@@ -754,10 +754,10 @@ __device__ __forceinline__ void group_chunk(const GroupArgs &a, const GroupSegme
       const GroupColDev gc = load_const(a.gcols + sg.first_gcol + j);
       uint32_t id[kGroupUnroll];
 #pragma unroll
-      for (int u = 0; u < kGroupUnroll; u++) id[u] = act[u] ? decode_doc(gc.fwd, gc.bits, doc[u]) : 0u;
+      for (int u = 0; u < kGroupUnroll; u++) id[u] = decode_doc(gc.fwd, gc.bits, doc[u]);  // all docs: loads batch
 #pragma unroll
       for (int u = 0; u < kGroupUnroll; u++) {
-        const uint32_t gid = (gc.remap && act[u]) ? (uint32_t)gc.remap[id[u]] : id[u];
+        const uint32_t gid = gc.remap ? (uint32_t)gc.remap[id[u]] : id[u];
         if (a.hashed) key[u] = mix64(key[u] ^ ((unsigned long long)gid + 0x9E3779B97F4A7C15ull * (unsigned long long)(j + 1)));
         else key[u] += (unsigned long long)gid * (unsigned long long)gc.stride;
       }
@@ -799,13 +799,19 @@ __device__ __forceinline__ void group_chunk(const GroupArgs &a, const GroupSegme
         if (ag.acc_kind == 5) continue;
 #pragma unroll
         for (int u = 0; u < kGroupUnroll; u++)
-          if (act[u]) rec[u] |= (unsigned long long)decode_doc(ag.fwd, ag.bits, doc[u]) << ag.field_shift;
+          rec[u] |= (unsigned long long)decode_doc(ag.fwd, ag.bits, doc[u]) << ag.field_shift;
       }
 #pragma unroll
       for (int u = 0; u < kGroupUnroll; u++)
         if (act[u]) {
-          const uint32_t pos = atomicAdd(&plds[key[u] >> a.shift], 1u);
-          a.emit[pos] = rec[u];  // default policy: the partition runs' lines combine in L2
+          if (a.reserved2 == 0) {
+            const uint32_t pos = atomicAdd(&plds[key[u] >> a.shift], 1u);
+            a.emit[pos] = rec[u];  // default policy: the partition runs' lines combine in L2
+          } else if (a.reserved2 == 1) {  // debug.emit=1 (timing only, wrong results): sequential stores
+            a.emit[doc[u]] = rec[u];
+          } else if (a.reserved2 == 2) {  // debug.emit=2: LDS cursor only
+            atomicAdd(&plds[key[u] >> a.shift], 1u);
+          }
         }
     } else {
       unsigned long long *cnt_g = a.counts;
@@ -821,7 +827,7 @@ __device__ __forceinline__ void group_chunk(const GroupArgs &a, const GroupSegme
         if (ag.acc_kind == 5) continue;
         uint32_t id[kGroupUnroll];
 #pragma unroll
-        for (int u = 0; u < kGroupUnroll; u++) id[u] = act[u] ? decode_doc(ag.fwd, ag.bits, doc[u]) : 0u;
+        for (int u = 0; u < kGroupUnroll; u++) id[u] = decode_doc(ag.fwd, ag.bits, doc[u]);
         void *acc = MODE == GB_LDS ? (void *)(acc_lds + ag.lds_off) : ag.acc;
 #pragma unroll
         for (int u = 0; u < kGroupUnroll; u++)

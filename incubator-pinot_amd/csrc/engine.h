@@ -116,7 +116,9 @@ struct Engine {
   std::string group_mode;     // group.mode: "" (auto) | lds | global | partition (tests force a sink)
   bool sync_poll = false;     // sync.poll: busy-poll the stream instead of hipStreamSynchronize
   bool host_phases = false;
-  int debug_emit = 0;         // debug.emit: GB_EMIT store experiments (timing only, wrong results)   // debug.host_phases: print the host-side phase times of fused queries
+  int debug_emit = 0;         // debug.emit: GB_EMIT store experiments (timing only, wrong results)
+  int group_pshift = -1;      // group.pshift: cap on log2 keys per partition (tests: many small partitions)
+  int group_split = -1;       // group.split: log2 sub-partitions per emitted run (-1 auto, 0 single-level)
   int num_cus = 256;          // multiProcessorCount of the device
 
   // scratch (grow-only)
@@ -126,8 +128,12 @@ struct Engine {
   DeviceBuffer reduced;       // per-segment reduced slots + HLL registers
   DeviceBuffer group_scratch;  // dense group-by accumulators (+ per-segment matched counts)
   DeviceBuffer group_part;     // partitioned plan: histogram, offsets, partition starts, scan temp
-  DeviceBuffer group_records;  // partitioned plan: (local key | dictIds) records
+  DeviceBuffer group_records;  // partitioned plan: (local key | dictIds) records, partition-major
+  DeviceBuffer group_runs;     // two-level plan: the same records in coarse (run, block) order
   DeviceBuffer group_final;    // ordered non-empty keys + compaction scratch
+  DeviceBuffer group_out;      // per-group outputs (counts, accumulators, HLL sums, keys) for the D2H
+  PinnedBuffer group_host;     // their pinned host copy
+  std::vector<std::shared_ptr<DeviceBuffer>> hll_pool;  // gathered HLL registers, reused once results are released
   DeviceBuffer group_hash;     // hashed key spaces: fingerprint table + representative docs
   PinnedBuffer host_arena;    // staging of the per-query arena (H2D)
   std::vector<uint8_t> arena_shadow;  // bytes last copied into `small` (upload_arena skips identical programs)

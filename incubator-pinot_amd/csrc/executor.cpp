@@ -23,6 +23,8 @@
 #include <tuple>
 #include <numeric>
 #include <set>
+#include <thread>
+#include <functional>
 
 #include "engine.h"
 
@@ -1423,10 +1425,24 @@ std::unique_ptr<GroupByResult> exec_group_by_legacy(Engine &e, const std::vector
 
 namespace {
 
+// Runs fn(0..n-1) on up to n threads (the calling thread takes task 0).
+void parallel_tasks(size_t n, const std::function<void(size_t)> &fn) {
+  if (n <= 1) {
+    if (n == 1) fn(0);
+    return;
+  }
+  std::vector<std::thread> th;
+  th.reserve(n - 1);
+  for (size_t t = 1; t < n; t++) th.emplace_back(fn, t);
+  fn(0);
+  for (auto &x : th) x.join();
+}
+
 // Fused group-by plan (GroupMode) chosen from the key space and the accumulators' per-key bytes.
 struct GroupPlan {
   int mode = GB_GLOBAL;
   int shift = 0;        // partitioned: 2^shift keys per partition
+  int split = 0;        // two-level: 2^split partitions per coarse run of the EMIT pass
   int64_t P = 0;
   int lds_acc_bytes = 0;
   std::vector<int> lds_off, field_shift, reduce_off;
@@ -1445,8 +1461,10 @@ size_t lds_acc_bytes_per_key(int kind, bool lds_hll_u32) {
   return 8;
 }
 
+constexpr int64_t kCoarseRuns = 128;  // EMIT's live partition cursors per block in the two-level plan
+
 GroupPlan plan_group(const std::vector<SegmentData *> &segs, const pinot_query &q, const KeySpace &ks,
-                     const GroupAccs &ga, const std::string &force) {
+                     const GroupAccs &ga, const std::string &force, int force_split, int max_shift) {
   GroupPlan gp;
   const int na = q.num_aggregations;
   gp.lds_off.assign(na, 0);
@@ -1475,11 +1493,26 @@ GroupPlan plan_group(const std::vector<SegmentData *> &segs, const pinot_query &
   for (int a = 0; a < na; a++) per_key += lds_acc_bytes_per_key(ga.acc_kind[a], false);  // u8 HLL registers
   int shift = 0;
   while (shift < 12 && ((size_t)2 << shift) * per_key <= (size_t)kReduceLdsBudget) shift++;
+  if (max_shift >= 0) shift = std::min(shift, max_shift);
   const int64_t K = int64_t(1) << shift;
   const int64_t P = (ks.G + K - 1) / K;
-  // record layout: [shift bits local key | one field per distinct aggregated column]
+  // two-level: EMIT scatters into ceil(P / 2^split) coarse runs (few enough live lines per block to combine
+  // in L2), k_partition_split then moves each run's records to their partitions
+  int agg_bits = 0;
+  {
+    std::set<std::string> seen;
+    for (int a = 0; a < na; a++)
+      if (ga.acc_kind[a] != 5 && seen.insert(agg_column(q.aggregations[a])).second)
+        agg_bits += segs[0]->column(agg_column(q.aggregations[a]))->bits;
+  }
+  int split = 0;
+  if (force_split >= 0) split = force_split;
+  else
+    while (split < 8 && ((P + (int64_t(1) << split) - 1) >> split) > kCoarseRuns) split++;
+  while (split > 0 && shift + split + agg_bits > 64) split--;
+  // record layout: [shift + split bits local key | one field per distinct aggregated column]
   std::map<std::string, int> col_field;
-  int bits = shift;
+  int bits = shift + split;
   for (int a = 0; a < na; a++) {
     if (ga.acc_kind[a] == 5) continue;
     const std::string c = agg_column(q.aggregations[a]);
@@ -1492,8 +1525,9 @@ GroupPlan plan_group(const std::vector<SegmentData *> &segs, const pinot_query &
   }
   const bool want_part = force.empty() ? ks.G >= 4 * K : force == "partition";
   if (same && bits <= 64 && P <= kMaxPartitions && want_part && force != "global") {
-    gp.mode = GB_EMIT;  // COUNT + EMIT + reduce
+    gp.mode = GB_EMIT;  // COUNT + EMIT (+ split) + reduce
     gp.shift = shift;
+    gp.split = split;
     gp.P = P;
     size_t roff = ((size_t)K * 4 + 15) / 16 * 16;
     for (int a = 0; a < na; a++) {
@@ -1530,6 +1564,7 @@ bool needs_admission(const std::vector<SegmentData *> &segs, const pinot_query &
 std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q,
                                                    const KeySpace &ks_in, const GroupAccs &ga, pinot_exec_stats *stats,
                                                    int attempt = 0) {
+  const auto tg0 = std::chrono::steady_clock::now();
   const int na = q.num_aggregations;
   const size_t S = segs.size();
   KeySpace ks = ks_in;
@@ -1555,7 +1590,8 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     while (hcap < 2 * docs) hcap <<= 1;
     ks.G = hcap;
   }
-  const GroupPlan gp = plan_group(segs, q, ks, gx, ks.hashed ? std::string("global") : e.group_mode);
+  const GroupPlan gp = plan_group(segs, q, ks, gx, ks.hashed ? std::string("global") : e.group_mode, e.group_split,
+                                    e.group_pshift);
   Arena ar;
   std::unique_ptr<FilterTreeInput> tree;
   if (q.num_filter_nodes > 0) tree = std::make_unique<FilterTreeInput>(decode_filter(q.num_filter_nodes, q.filter));
@@ -1582,11 +1618,14 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     acc_bytes[a] = gx.acc_kind[a] == 5 ? 0 : gx.acc_kind[a] == 4 ? 256 : 8;
     per_key += acc_bytes[a];
   }
-  size_t free_b = 0, total_b = 0;
-  PINOT_HIP(hipMemGetInfo(&free_b, &total_b));
-  require((double)ks.G * per_key < 0.5 * (double)free_b, PINOT_ERR_UNSUPPORTED, "dense group-by accumulators do not fit in HBM");
   const size_t head = 256 + (S * 8 + 255) / 256 * 256;  // matched [S] + verify flag, 256-B aligned arrays after
-  e.group_scratch.reserve(ks.G * per_key + head + 256 * (size_t)(na + 1));
+  const size_t scratch_b = ks.G * per_key + head + 256 * (size_t)(na + 1);
+  if (scratch_b > e.group_scratch.size()) {  // growing: check the free HBM first (hipMemGetInfo is a syscall)
+    size_t free_b = 0, total_b = 0;
+    PINOT_HIP(hipMemGetInfo(&free_b, &total_b));
+    require((double)ks.G * per_key < 0.5 * (double)free_b, PINOT_ERR_UNSUPPORTED, "dense group-by accumulators do not fit in HBM");
+  }
+  e.group_scratch.reserve(scratch_b);
   uint8_t *base = e.group_scratch.get<uint8_t>();
   auto *matched = reinterpret_cast<unsigned long long *>(base);
   auto *counts = reinterpret_cast<unsigned long long *>(base + head);
@@ -1696,12 +1735,14 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
   a.bps = (int)std::max<int64_t>(1, std::min<int64_t>(resident / (int64_t)S, (max_chunks + 15) / 16));
   const int64_t nblk = (int64_t)S * a.bps;
 
+  const auto tgp = std::chrono::steady_clock::now();
   PINOT_HIP(hipEventRecord(e.ev_start, e.stream));
   upload_arena(e, ar);
   Timer t(e);
   for (size_t si = 0; si < S; si++)
     if (plans[si].has_pre && !plans[si].empty) run_filter(e, plans[si], qs, t, (int64_t)si);
   PINOT_HIP(hipMemsetAsync(matched, 0, S * 8, e.stream));
+  const auto tgu = std::chrono::steady_clock::now();
   if (gp.mode != GB_EMIT) {  // identities: counts / sums 0, min all-ones, max 0, HLL 0
     PINOT_HIP(hipMemsetAsync(counts, 0, ks.G * 8, e.stream));
     for (int i = 0; i < na; i++)
@@ -1733,11 +1774,13 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     void *tmp = pb + 2 * hist_b + pstart_b;
     require(max_records < (int64_t)UINT32_MAX, PINOT_ERR_UNSUPPORTED, "partitioned group-by over > 4G docs per GPU");
     e.group_records.reserve((size_t)max_records * 8 + 64);
+    if (gp.split) e.group_runs.reserve((size_t)max_records * 8 + 64);
     a.hist = hist;
     a.offsets = offsets;
-    a.emit = e.group_records.get<unsigned long long>();
+    a.pstart = pstart;
+    a.emit = gp.split ? e.group_runs.get<unsigned long long>() : e.group_records.get<unsigned long long>();
     PartitionReduceArgs ra{};
-    ra.records = a.emit;
+    ra.records = e.group_records.get<unsigned long long>();
     ra.pstart = pstart;
     ra.P = (int32_t)gp.P;
     ra.shift = gp.shift;
@@ -1756,12 +1799,18 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
       launch_partition_starts(offsets, hist, (int32_t)gp.P, (int32_t)nblk, pstart, e.stream);
       GroupArgs a2 = a;
       a2.mode = GB_EMIT;
+      a2.split = gp.split;
       launch_group_query(a2, e.stream);
+      launch_partition_split(hist, offsets, pstart, (int32_t)gp.P, (int32_t)nblk, gp.shift, gp.split, a.emit,
+                             e.group_records.get<unsigned long long>(), e.stream);
       launch_partition_reduce(ra, e.stream);
     });
     PINOT_HIP(hipGetLastError());
   }
 
+  const auto tg1 = std::chrono::steady_clock::now();
+  if (e.host_phases) PINOT_HIP(hipStreamSynchronize(e.stream));
+  const auto tg2 = std::chrono::steady_clock::now();
   // finalize: ordered non-empty keys, per-group outputs, one D2H
   const size_t cscr = compact_keys_scratch_bytes(ks.G);
   e.group_final.reserve(ks.G * 8 + 64 + cscr);
@@ -1781,6 +1830,8 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     require(attempt < 3, PINOT_ERR_DEVICE, "group-key fingerprint collisions persist");
     return exec_group_by_fused(e, segs, q, ks_in, ga, stats, attempt + 1);
   }
+  const auto tg3 = std::chrono::steady_clock::now();
+  auto tg4 = tg3;
   int n_hll = 0;
   for (int i = 0; i < na; i++) n_hll += gx.acc_kind[i] == 4;
   auto res = std::make_unique<GroupByResult>();
@@ -1796,16 +1847,25 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
   res->gcard = ks.gcard;
   res->device = e.device;
   if (n) {
-    const size_t out_b = n * 8 * (1 + na) + (size_t)n_hll * n * 12 + 64;
-    DeviceBuffer out(out_b);
-    auto *o_cnt = out.get<unsigned long long>();
+    // device outputs and their pinned host copy live in grow-only engine buffers (no per-query allocation)
+    const size_t out_b = n * 8 * (2 + na) + (size_t)n_hll * n * 12 + 64;
+    e.group_out.reserve(out_b);
+    e.group_host.reserve(out_b);
+    auto *o_cnt = e.group_out.get<unsigned long long>();
     auto *o_acc = o_cnt + n;
     auto *o_hs = o_acc + n * na;
     auto *o_hz = reinterpret_cast<uint32_t *>(o_hs + (size_t)n_hll * n);
+    auto *o_keys = reinterpret_cast<long long *>(e.group_out.get<uint8_t>() + out_b - 64 - n * 8);
     launch_group_outputs(counts, gaggs.data(), na, keys_dev, (long long)n, o_cnt, o_acc, o_hs, o_hz, e.stream);
     PINOT_HIP(hipGetLastError());
-    if (n_hll) {
-      res->hll_dev = std::make_shared<DeviceBuffer>((size_t)n_hll * n * 256 + 16);
+    if (n_hll) {  // registers stay on the device until asked for; buffers are recycled once their result is released
+      const size_t need = (size_t)n_hll * n * 256 + 16;
+      for (auto &b : e.hll_pool)
+        if (b.use_count() == 1 && b->size() >= need) { res->hll_dev = b; break; }
+      if (!res->hll_dev) {
+        res->hll_dev = std::make_shared<DeviceBuffer>(need + need / 4);
+        if (e.hll_pool.size() < 4) e.hll_pool.push_back(res->hll_dev);
+      }
       int h = 0;
       for (int i = 0; i < na; i++)
         if (gx.acc_kind[i] == 4) {
@@ -1818,9 +1878,7 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
         if (alias[i] >= 0 && ga.acc_kind[i] == 4) res->hll_dev_off[i] = res->hll_dev_off[alias[i]];
       PINOT_HIP(hipGetLastError());
     }
-    std::vector<uint8_t> host(out_b);
-    res->raw_keys.resize(n);
-    PINOT_HIP(hipMemcpyAsync(res->raw_keys.data(), keys_dev, n * 8, hipMemcpyDeviceToHost, e.stream));
+    PINOT_HIP(hipMemcpyAsync(o_keys, keys_dev, n * 8, hipMemcpyDeviceToDevice, e.stream));
     DeviceBuffer ids;
     if (ks.hashed) {  // group ordinals are hash slots: fetch each group's global-id tuple
       ids.alloc(n * q.num_group_by * 4 + 16);
@@ -1829,45 +1887,76 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
       res->key_ids.resize(n * q.num_group_by);
       PINOT_HIP(hipMemcpyAsync(res->key_ids.data(), ids.get(), n * q.num_group_by * 4, hipMemcpyDeviceToHost, e.stream));
     }
-    PINOT_HIP(hipMemcpyAsync(host.data(), out.get(), out_b, hipMemcpyDeviceToHost, e.stream));
+    PINOT_HIP(hipMemcpyAsync(e.group_host.get(), e.group_out.get(), out_b, hipMemcpyDeviceToHost, e.stream));
     PINOT_HIP(hipStreamSynchronize(e.stream));
-    const auto *hc = reinterpret_cast<const unsigned long long *>(host.data());
+    tg4 = std::chrono::steady_clock::now();
+    const uint8_t *host = e.group_host.get<uint8_t>();
+    const auto *hc = reinterpret_cast<const unsigned long long *>(host);
     const auto *hacc = hc + n;
     const auto *hhs = hacc + n * na;
     const auto *hhz = reinterpret_cast<const uint32_t *>(hhs + (size_t)n_hll * n);
+    const auto *hkeys = reinterpret_cast<const long long *>(host + out_b - 64 - n * 8);
     std::vector<int> hidx(na, -1);  // HLL register-sum row of each (primary) HLL aggregation
     for (int i = 0, h = 0; i < na; i++)
       if (gx.acc_kind[i] == 4) hidx[i] = h++;
+    // result arrays: sized (first touch of fresh pages) and filled in parallel over the host's cores
+    std::vector<std::function<void()>> sizing;
+    sizing.push_back([&] { res->raw_keys.resize(n); });
     for (int i = 0; i < na; i++) {
-      auto &cv = res->counts[i];
-      auto &vv = res->values[i];
-      cv.resize(n);
-      vv.resize(n);
-      const int ak = ga.acc_kind[i];
-      const int src = alias[i] >= 0 ? alias[i] : i;  // the accumulator this aggregation reads
-      const int h = hidx[src];
-      if (ak == 4) res->hll_card[i].resize(n);
-      for (size_t g = 0; g < n; g++) {
-        cv[g] = (int64_t)hc[g];
-        const uint64_t raw = hacc[(size_t)src * n + g];
+      sizing.push_back([&, i] { res->counts[i].resize(n); });
+      sizing.push_back([&, i] { res->values[i].resize(n); });
+      if (ga.acc_kind[i] == 4) sizing.push_back([&, i] { res->hll_card[i].resize(n); });
+    }
+    const size_t nt = n >= (1u << 16) ? 8 : 1;  // small results: no threads
+    if (nt > 1) parallel_tasks(sizing.size(), [&](size_t t) { sizing[t](); });
+    else
+      for (auto &f : sizing) f();
+    parallel_tasks(nt, [&](size_t t) {
+      const size_t lo = n * t / nt, hi = n * (t + 1) / nt;
+      memcpy(res->raw_keys.data() + lo, hkeys + lo, (hi - lo) * 8);
+      for (int i = 0; i < na; i++) {
+        int64_t *cv = res->counts[i].data();
+        double *vv = res->values[i].data();
+        memcpy(cv + lo, hc + lo, (hi - lo) * 8);
+        const int ak = ga.acc_kind[i];
+        const int src = alias[i] >= 0 ? alias[i] : i;  // the accumulator this aggregation reads
+        const unsigned long long *raw = hacc + (size_t)src * n;
         switch (ak) {
-          case 0: vv[g] = (double)(int64_t)raw; break;
-          case 1: { double d; memcpy(&d, &raw, 8); vv[g] = d; break; }
+          case 0:
+            for (size_t g = lo; g < hi; g++) vv[g] = (double)(int64_t)raw[g];
+            break;
+          case 1:
+            memcpy(vv + lo, raw + lo, (hi - lo) * 8);
+            break;
           case 2:
-          case 3: vv[g] = decode_ordered(raw); break;
+          case 3:
+            for (size_t g = lo; g < hi; g++) vv[g] = decode_ordered(raw[g]);
+            break;
           case 4: {
-            const int64_t c = hll_cardinality_from_sum(hhs[(size_t)h * n + g], hhz[(size_t)h * n + g]);
-            res->hll_card[i][g] = c;
-            vv[g] = (double)c;
+            const int h = hidx[src];
+            int64_t *card = res->hll_card[i].data();
+            for (size_t g = lo; g < hi; g++) {
+              card[g] = hll_cardinality_from_sum(hhs[(size_t)h * n + g], hhz[(size_t)h * n + g]);
+              vv[g] = (double)card[g];
+            }
             break;
           }
-          default: vv[g] = (double)hc[g]; break;
+          default:
+            for (size_t g = lo; g < hi; g++) vv[g] = (double)hc[g];
+            break;
         }
       }
-    }
+    });
   }
   PINOT_HIP(hipEventRecord(e.ev_stop, e.stream));
   PINOT_HIP(hipStreamSynchronize(e.stream));
+  if (e.host_phases) {
+    const auto tg5 = std::chrono::steady_clock::now();
+    auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+    fprintf(stderr, "[pinot_gpu] group-by host phases (us): plan %.1f, upload %.1f, launch %.1f, kernels %.1f, "
+            "compact+sync %.1f, outputs+D2H %.1f, host finalize %.1f (%llu groups)\n", us(tg0, tgp), us(tgp, tgu),
+            us(tgu, tg1), us(tg1, tg2), us(tg2, tg3), us(tg3, tg4), us(tg4, tg5), (unsigned long long)n);
+  }
   float ms = 0;
   PINOT_HIP(hipEventElapsedTime(&ms, e.ev_start, e.ev_stop));
   t.collect();

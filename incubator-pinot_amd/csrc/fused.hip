@@ -791,9 +791,10 @@ __device__ __forceinline__ void group_chunk(const GroupArgs &a, const GroupSegme
       for (int u = 0; u < kGroupUnroll; u++)
         if (act[u]) atomicAdd(&plds[key[u] >> a.shift], 1u);
     } else if constexpr (MODE == GB_EMIT) {
+      const int rshift = a.shift + a.split;  // two-level: records go to coarse run key >> (shift + split)
       unsigned long long rec[kGroupUnroll];
 #pragma unroll
-      for (int u = 0; u < kGroupUnroll; u++) rec[u] = key[u] & ((1ull << a.shift) - 1ull);
+      for (int u = 0; u < kGroupUnroll; u++) rec[u] = key[u] & ((1ull << rshift) - 1ull);
       for (int g = 0; g < a.n_aggs; g++) {
         const GroupAggDev ag = load_const(a.aggs + sg.first_agg + g);
         if (ag.acc_kind == 5) continue;
@@ -801,13 +802,20 @@ __device__ __forceinline__ void group_chunk(const GroupArgs &a, const GroupSegme
         for (int u = 0; u < kGroupUnroll; u++)
           rec[u] |= (unsigned long long)decode_doc(ag.fwd, ag.bits, doc[u]) << ag.field_shift;
       }
+      if (a.reserved2 == 0) {
+        // all cursor claims first (inactive lanes add 0: no divergent branch around the LDS atomics, one
+        // lgkmcnt wait), then the stores; the runs' lines combine in L2
+        uint32_t pos[kGroupUnroll];
+#pragma unroll
+        for (int u = 0; u < kGroupUnroll; u++) pos[u] = atomicAdd(&plds[key[u] >> rshift], act[u] ? 1u : 0u);
+#pragma unroll
+        for (int u = 0; u < kGroupUnroll; u++)
+          if (act[u]) a.emit[pos[u]] = rec[u];
+      }
 #pragma unroll
       for (int u = 0; u < kGroupUnroll; u++)
         if (act[u]) {
-          if (a.reserved2 == 0) {
-            const uint32_t pos = atomicAdd(&plds[key[u] >> a.shift], 1u);
-            a.emit[pos] = rec[u];  // default policy: the partition runs' lines combine in L2
-          } else if (a.reserved2 == 1) {  // debug.emit=1 (timing only, wrong results): sequential stores
+          if (a.reserved2 == 1) {  // debug.emit=1 (timing only, wrong results): sequential stores
             a.emit[doc[u]] = rec[u];
           } else if (a.reserved2 == 2) {  // debug.emit=2: LDS cursor only
             atomicAdd(&plds[key[u] >> a.shift], 1u);
@@ -905,7 +913,16 @@ __global__ __launch_bounds__(kGroupBlock) void k_group_query(GroupArgs a) {
     __syncthreads();
   }
   if constexpr (MODE == GB_EMIT) {
-    for (int p = tid; p < a.P; p += kGroupBlock) plds[p] = a.offsets[(size_t)p * nblk + blockIdx.x];
+    if (a.split == 0) {
+      for (int p = tid; p < a.P; p += kGroupBlock) plds[p] = a.offsets[(size_t)p * nblk + blockIdx.x];
+    } else {  // coarse run (q, block) starts where run q starts + this block's share of q's earlier blocks
+      const int F = 1 << a.split, Q = (a.P + F - 1) >> a.split;
+      for (int q = tid; q < Q; q += kGroupBlock) {
+        uint32_t c = a.pstart[q * F];
+        for (int p = q * F; p < min(a.P, (q + 1) * F); p++) c += a.offsets[(size_t)p * nblk + blockIdx.x] - a.pstart[p];
+        plds[q] = c;
+      }
+    }
     __syncthreads();
   }
   const int64_t nchunks = min((sg.nwords + 63) >> 6, sg.ch_end);

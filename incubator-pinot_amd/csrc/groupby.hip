@@ -24,7 +24,8 @@ namespace pinot {
 namespace {
 using namespace dev;
 
-constexpr int kReduceBlock = 512;
+constexpr int kReduceBlock = 1024;
+constexpr int kReduceUnroll = 8;
 constexpr int kReduceCountCopies = 4;  // private count copies (waves w, w + 4 share one)
 
 __device__ __forceinline__ unsigned long long ordered_bits_r(double d) {
@@ -59,48 +60,74 @@ __global__ __launch_bounds__(kReduceBlock) void k_partition_reduce(PartitionRedu
   // counts: one private copy per wave (a partition has few keys: LDS atomics on one copy serialise)
   const int wave = tid >> 6;
   uint32_t *wcnt = cnt + a.wave_cnt_off / 4 + (wave & (kReduceCountCopies - 1)) * K;
-  for (uint32_t r = b + tid; r < e; r += kReduceBlock) {
-    const unsigned long long rec = __builtin_nontemporal_load(a.records + r);
-    const uint32_t k = (uint32_t)(rec & kmask);
-    atomicAdd(wcnt + k, 1u);
+  // kReduceUnroll records per thread per step, each stage batched across them (record loads, dictionary /
+  // LUT loads, LDS atomics, HLL CAS attempts): the loop is latency-bound with one record in flight
+  constexpr int U = kReduceUnroll;
+  for (uint32_t r0 = b + tid; r0 < e; r0 += (uint32_t)U * kReduceBlock) {
+    unsigned long long rec[U];
+    bool ok[U];
+    uint32_t k[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint32_t r = r0 + (uint32_t)u * kReduceBlock;
+      ok[u] = r < e;
+      rec[u] = ok[u] ? __builtin_nontemporal_load(a.records + r) : 0ull;
+      k[u] = (uint32_t)(rec[u] & kmask);
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      if (ok[u]) atomicAdd(wcnt + k[u], 1u);
 #pragma unroll
     for (int g = 0; g < kMaxGroupAggs; g++) {
       if (g >= a.n_aggs) break;
       const GroupAggDev &ag = a.aggs[g];
       if (ag.acc_kind == 5) continue;
-      const uint32_t id = (uint32_t)((rec >> ag.field_shift) & ((1ull << ag.bits) - 1ull));
+      uint32_t id[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) id[u] = ok[u] ? (uint32_t)((rec[u] >> ag.field_shift) & ((1ull << ag.bits) - 1ull)) : 0u;
       uint8_t *acc = lds + ag.lds_off;
-      switch (ag.acc_kind) {
-        case 0:
-          atomicAdd(reinterpret_cast<unsigned long long *>(acc) + k,
-                    (unsigned long long)(long long)static_cast<const int32_t *>(ag.dict)[id]);
-          break;
-        case 1:
-          atomicAdd(reinterpret_cast<double *>(acc) + k, dict_value_r(ag.dict, ag.value_kind, id));
-          break;
-        case 2:
-          atomicMin(reinterpret_cast<unsigned long long *>(acc) + k,
-                    ordered_bits_r(dict_value_r(ag.dict, ag.value_kind, id)));
-          break;
-        case 3:
-          atomicMax(reinterpret_cast<unsigned long long *>(acc) + k,
-                    ordered_bits_r(dict_value_r(ag.dict, ag.value_kind, id)));
-          break;
-        case 4: {  // u8 registers: byte max by CAS on the containing dword (conflicts are rare)
-          const uint32_t h = ag.hll_lut[id];
-          const uint32_t idx = k * 256 + (h >> 8), rank = h & 0xFFu;
-          uint32_t *word = reinterpret_cast<uint32_t *>(acc) + (idx >> 2);
-          const int sh = (int)(idx & 3) * 8;
-          uint32_t old = *word;
-          while (((old >> sh) & 0xFFu) < rank) {
-            const uint32_t seen = atomicCAS(word, old, (old & ~(0xFFu << sh)) | (rank << sh));
-            if (seen == old) break;
-            old = seen;
-          }
-          break;
+      if (ag.acc_kind == 0) {
+        long long v[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = static_cast<const int32_t *>(ag.dict)[id[u]];
+#pragma unroll
+        for (int u = 0; u < U; u++)
+          if (ok[u]) atomicAdd(reinterpret_cast<unsigned long long *>(acc) + k[u], (unsigned long long)v[u]);
+      } else if (ag.acc_kind == 4) {  // u8 registers: byte max by CAS on the containing dword
+        uint32_t h[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) h[u] = ag.hll_lut[id[u]];
+        uint32_t *word[U], old[U], rank[U];
+        int sh[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          const uint32_t idx = k[u] * 256 + (h[u] >> 8);
+          word[u] = reinterpret_cast<uint32_t *>(acc) + (idx >> 2);
+          sh[u] = (int)(idx & 3) * 8;
+          rank[u] = ok[u] ? (h[u] & 0xFFu) : 0u;
+          old[u] = *word[u];
         }
-        default:
-          break;
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          if (((old[u] >> sh[u]) & 0xFFu) >= rank[u]) continue;
+          uint32_t seen = atomicCAS(word[u], old[u], (old[u] & ~(0xFFu << sh[u])) | (rank[u] << sh[u]));
+          while (seen != old[u]) {  // another lane / wave changed the dword: retry while still below
+            old[u] = seen;
+            if (((old[u] >> sh[u]) & 0xFFu) >= rank[u]) break;
+            seen = atomicCAS(word[u], old[u], (old[u] & ~(0xFFu << sh[u])) | (rank[u] << sh[u]));
+          }
+        }
+      } else {
+        double v[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = dict_value_r(ag.dict, ag.value_kind, id[u]);
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          if (!ok[u]) continue;
+          if (ag.acc_kind == 1) atomicAdd(reinterpret_cast<double *>(acc) + k[u], v[u]);
+          else if (ag.acc_kind == 2) atomicMin(reinterpret_cast<unsigned long long *>(acc) + k[u], ordered_bits_r(v[u]));
+          else atomicMax(reinterpret_cast<unsigned long long *>(acc) + k[u], ordered_bits_r(v[u]));
+        }
       }
     }
   }
@@ -192,6 +219,39 @@ __global__ void k_partition_starts(const uint32_t *__restrict__ offsets, const u
   }
 }
 
+// Second level of the two-level partitioned plan: block (q, b) moves coarse run (q, b) — the records block b
+// of the EMIT pass wrote for partitions q*F .. q*F+F-1, in any order — to those partitions' final slots
+// offsets[p][b] (the single-level layout, partition-major then block). The live cursors are F per block, so
+// the stores of all resident blocks combine into whole lines in L2.
+__global__ __launch_bounds__(256) void k_partition_split(const uint32_t *__restrict__ hist, const uint32_t *__restrict__ offsets,
+                                                         const uint32_t *__restrict__ pstart, int32_t P, int32_t nblk,
+                                                         int32_t shift, int32_t split,
+                                                         const unsigned long long *__restrict__ runs,
+                                                         unsigned long long *__restrict__ records) {
+  __shared__ uint32_t cur[256];
+  __shared__ uint32_t run_b, run_e;
+  const int F = 1 << split;
+  const int q = blockIdx.x / nblk, b = blockIdx.x % nblk, tid = threadIdx.x;
+  if (tid == 0) {
+    uint32_t s0 = pstart[q * F], n = 0;
+    for (int p = q * F; p < min(P, (q + 1) * F); p++) {
+      const size_t i = (size_t)p * nblk + b;
+      s0 += offsets[i] - pstart[p];
+      n += hist[i];
+    }
+    run_b = s0;
+    run_e = s0 + n;
+  }
+  if (tid < F) cur[tid] = q * F + tid < P ? offsets[(size_t)(q * F + tid) * nblk + b] : 0u;
+  __syncthreads();
+  const uint32_t e = run_e;
+  for (uint32_t r = run_b + tid; r < e; r += 256) {
+    const unsigned long long rec = __builtin_nontemporal_load(runs + r);
+    const uint32_t pos = atomicAdd(&cur[(rec >> shift) & (unsigned long long)(F - 1)], 1u);
+    records[pos] = rec;
+  }
+}
+
 __global__ void k_gather_hll(const uint8_t *__restrict__ regs, const long long *__restrict__ keys, long long n,
                              uint8_t *__restrict__ out) {
   // one 16-B piece per thread: 16 pieces per group
@@ -207,6 +267,15 @@ void launch_partition_starts(const uint32_t *offsets, const uint32_t *hist, int3
                              hipStream_t stream) {
   if (P <= 0) return;
   hipLaunchKernelGGL(k_partition_starts, dim3((P + 256) / 256), dim3(256), 0, stream, offsets, hist, P, nblk, pstart);
+}
+
+void launch_partition_split(const uint32_t *hist, const uint32_t *offsets, const uint32_t *pstart, int32_t P,
+                            int32_t nblk, int32_t shift, int32_t split, const unsigned long long *runs,
+                            unsigned long long *records, hipStream_t stream) {
+  if (P <= 0 || split <= 0) return;
+  const int Q = (P + (1 << split) - 1) >> split;
+  hipLaunchKernelGGL(k_partition_split, dim3((unsigned)Q * (unsigned)nblk), dim3(256), 0, stream, hist, offsets, pstart,
+                     P, nblk, shift, split, runs, records);
 }
 
 void launch_gather_hll(const uint8_t *regs, const long long *keys, long long n, uint8_t *out, hipStream_t stream) {

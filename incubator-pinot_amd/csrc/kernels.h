@@ -231,10 +231,12 @@ struct GroupArgs {
   int32_t lds_acc_bytes;       // GB_LDS: per-block accumulator bytes (counts u32 [G] at 0, aggs at lds_off)
   int32_t shift;               // GB_COUNT / GB_EMIT: partition = key >> shift, local key = low bits
   int32_t P;                   // partitions
-  int32_t reserved;
+  int32_t split;               // GB_EMIT two-level: log2 partitions per coarse run (0 = records go straight to
+                               // their partition runs); a block emits into run (key >> (shift + split))
   uint32_t *hist;              // GB_COUNT: [P][nblk] per-block partition counts (partition-major)
   const uint32_t *offsets;     // GB_EMIT: [P][nblk] exclusive record offsets
-  unsigned long long *emit;    // GB_EMIT: records
+  const uint32_t *pstart;      // GB_EMIT two-level: [P + 1] partition starts (coarse run starts derive from them)
+  unsigned long long *emit;    // GB_EMIT: records (two-level: in coarse (run, block) order)
   // hashed key space (LONG_MAP / ARRAY_MAP shapes: Π cardinalities too large for dense arrays): the key
   // is the slot of the tuple's 64-bit fingerprint in an open-addressing table of hcap (power of 2) slots
   unsigned long long *htable;  // [hcap] fingerprints, 0 = empty
@@ -261,6 +263,11 @@ struct PartitionReduceArgs {
   GroupAggDev aggs[kMaxGroupAggs];  // fwd unused; dict / hll_lut / acc / lds_off / acc_kind / field_shift / bits
 };
 void launch_partition_reduce(const PartitionReduceArgs &a, hipStream_t stream);
+// Two-level partitioned plan, second level: coarse run (q, b) of `runs` (2^split partitions' records
+// emitted by block b) is split into the partitions' final slots offsets[p][b]... of `records`.
+void launch_partition_split(const uint32_t *hist, const uint32_t *offsets, const uint32_t *pstart, int32_t P,
+                            int32_t nblk, int32_t shift, int32_t split, const unsigned long long *runs,
+                            unsigned long long *records, hipStream_t stream);
 // pstart[p] = offsets[p * nblk] (partition-major exclusive offsets), pstart[P] = total records.
 void launch_partition_starts(const uint32_t *offsets, const uint32_t *hist, int32_t P, int32_t nblk, uint32_t *pstart,
                              hipStream_t stream);

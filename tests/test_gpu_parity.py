@@ -280,7 +280,11 @@ def test_random_group_by(engine, seed):
         g.release()
 
 
-GROUP_SINKS = ("group.mode=lds", "group.mode=global", "group.mode=partition")
+GROUP_SINKS = ("group.mode=lds", "group.mode=global", "group.mode=partition",
+               # two-level partitioned plan: many 4-key partitions, EMIT into coarse runs of 4 / 256 partitions
+               "group.mode=partition;group.pshift=2;group.split=2",
+               "group.mode=partition;group.pshift=0;group.split=8",
+               "group.mode=partition;group.pshift=1")
 
 
 @pytest.mark.parametrize("mode", GROUP_SINKS)

@@ -90,6 +90,7 @@ void parse_config(Engine &e, const char *cfg) {
     } else if (k == "sync.poll") e.sync_poll = v == "1" || v == "true";
     else if (k == "debug.emit") e.debug_emit = std::stoi(v);
     else if (k == "group.pshift") e.group_pshift = std::stoi(v);
+    else if (k == "group.prefetch") e.group_prefetch = v == "1" || v == "true";
     else if (k == "group.split") {
       e.group_split = std::stoi(v);
       require(e.group_split >= -1 && e.group_split <= 8, PINOT_ERR_BAD_ARG, "group.split: -1 (auto) .. 8");

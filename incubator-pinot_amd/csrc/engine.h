@@ -117,6 +117,7 @@ struct Engine {
   bool sync_poll = false;     // sync.poll: busy-poll the stream instead of hipStreamSynchronize
   bool host_phases = false;
   int debug_emit = 0;         // debug.emit: GB_EMIT store experiments (timing only, wrong results)
+  bool group_prefetch = true; // group.prefetch: partitioned plan loads every column of a word batch at once
   int group_pshift = -1;      // group.pshift: cap on log2 keys per partition (tests: many small partitions)
   int group_split = -1;       // group.split: log2 sub-partitions per emitted run (-1 auto, 0 single-level)
   int num_cus = 256;          // multiProcessorCount of the device

@@ -1688,6 +1688,11 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
           ensure_hll_lut(e, c);
           ag.hll_lut = c.hll_lut.get<uint16_t>();
         }
+        if (c.affine && e.use_affine && (c.data_type == PINOT_INT || c.data_type == PINOT_LONG)) {
+          ag.affine = 1;
+          ag.affine_base = c.affine_base;
+          ag.affine_step = c.affine_step;
+        }
       }
       ag.field_shift = gp.field_shift[a];
       ag.lds_off = gp.lds_off[a];
@@ -1717,6 +1722,15 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
   a.P = (int32_t)gp.P;
   a.mode = gp.mode == GB_EMIT ? GB_COUNT : gp.mode;
   a.reserved2 = e.debug_emit;  // timing experiments only (debug.emit)
+  if (gp.mode == GB_EMIT && !ks.hashed && e.group_prefetch && e.debug_emit == 0) {
+    int nc = q.num_group_by;
+    for (int i = 0; i < na && nc <= kGroupPfCols; i++)
+      if (gx.acc_kind[i] != 5) {
+        if (nc < kGroupPfCols) a.pf_agg[nc] = i;
+        nc++;
+      }
+    a.pf_nc = nc <= kGroupPfCols ? nc : 0;
+  }
   unsigned long long *htable = nullptr, *reps = nullptr;
   if (ks.hashed) {
     e.group_hash.reserve((size_t)hcap * 16 + 256);

@@ -845,6 +845,101 @@ __device__ __forceinline__ void group_chunk(const GroupArgs &a, const GroupSegme
   }
 }
 
+// GB_COUNT / GB_EMIT with every needed column prefetched: one global-memory round trip per kGroupPfUnroll
+// words instead of one per column (the per-doc reads are latency-bound).
+constexpr int kGroupPfUnroll = 4;
+
+template <int MODE>
+__device__ __forceinline__ void group_chunk_pf(const GroupArgs &a, const GroupSegment &sg, int64_t ch, uint64_t mask,
+                                               int lane, uint32_t *plds) {
+  constexpr int C = kGroupPfCols, U = kGroupPfUnroll;
+  const int nc = MODE == GB_COUNT ? a.n_gcols : a.pf_nc;
+  const uint8_t *fwd[C];
+  const int32_t *remap[C];
+  unsigned long long stride[C];
+  int bits[C], fshift[C];
+#pragma unroll
+  for (int c = 0; c < C; c++) {
+    fwd[c] = nullptr;
+    remap[c] = nullptr;
+    stride[c] = 0;
+    bits[c] = 1;
+    fshift[c] = 0;
+    if (c < a.n_gcols) {
+      const GroupColDev gc = load_const(a.gcols + sg.first_gcol + c);
+      fwd[c] = gc.fwd;
+      remap[c] = gc.remap;
+      stride[c] = (unsigned long long)gc.stride;
+      bits[c] = gc.bits;
+    } else if (c < nc) {
+      const GroupAggDev ag = load_const(a.aggs + sg.first_agg + a.pf_agg[c]);
+      fwd[c] = ag.fwd;
+      bits[c] = ag.bits;
+      fshift[c] = ag.field_shift;
+    }
+  }
+  const int rshift = a.shift + a.split;
+  for (int w0 = 0; w0 < 64; w0 += U) {
+    uint64_t mw[U];
+    bool any = false;
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      mw[u] = readlane64(mask, w0 + u);
+      any = any || mw[u] != 0;
+    }
+    if (!any) continue;  // uniform
+    int64_t doc[U];
+    bool act[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      doc[u] = ((ch << 6) + w0 + u) * 64 + lane;
+      act[u] = (mw[u] >> lane) & 1ull;
+    }
+    uint32_t lo[C][U], hi[C][U];
+#pragma unroll
+    for (int c = 0; c < C; c++)
+      if (c < nc) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          const uint32_t *p = reinterpret_cast<const uint32_t *>(fwd[c]) + (((uint64_t)doc[u] * (uint32_t)bits[c]) >> 5);
+          lo[c][u] = p[0];
+          hi[c][u] = p[1];
+        }
+      }
+    unsigned long long key[U], rec[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) key[u] = rec[u] = 0;
+#pragma unroll
+    for (int c = 0; c < C; c++)
+      if (c < nc) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          const uint64_t bitpos = (uint64_t)doc[u] * (uint32_t)bits[c];
+          const uint64_t x = ((uint64_t)bswap32(lo[c][u]) << 32) | bswap32(hi[c][u]);
+          const uint32_t id = (uint32_t)((x << (bitpos & 31)) >> (64 - bits[c]));
+          if (c < a.n_gcols) key[u] += (unsigned long long)(remap[c] ? (uint32_t)remap[c][id] : id) * stride[c];
+          else rec[u] |= (unsigned long long)id << fshift[c];
+        }
+      }
+    if (a.admitted) {
+#pragma unroll
+      for (int u = 0; u < U; u++) act[u] = act[u] && ((a.admitted[key[u] >> 5] >> (key[u] & 31)) & 1u);
+    }
+    if constexpr (MODE == GB_COUNT) {
+#pragma unroll
+      for (int u = 0; u < U; u++)
+        if (act[u]) atomicAdd(&plds[key[u] >> a.shift], 1u);
+    } else {
+      uint32_t pos[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) pos[u] = atomicAdd(&plds[key[u] >> rshift], act[u] ? 1u : 0u);
+#pragma unroll
+      for (int u = 0; u < U; u++)
+        if (act[u]) a.emit[pos[u]] = rec[u] | (key[u] & ((1ull << rshift) - 1ull));
+    }
+  }
+}
+
 // LDS accumulator identities (GB_LDS): counts 0, sums 0, min all-ones, max 0, HLL 0.
 __device__ __forceinline__ void init_group_lds(const GroupArgs &a, const GroupSegment &sg, uint8_t *acc_lds, int tid) {
   uint32_t *w = reinterpret_cast<uint32_t *>(acc_lds);
@@ -896,7 +991,7 @@ __device__ __forceinline__ void flush_group_lds(const GroupArgs &a, const GroupS
   }
 }
 
-template <int MODE>
+template <int MODE, bool PF = false>
 __global__ __launch_bounds__(kGroupBlock) void k_group_query(GroupArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -936,7 +1031,10 @@ __global__ __launch_bounds__(kGroupBlock) void k_group_query(GroupArgs a) {
                                return stage;
                              });
     matched += __popcll(mask);
-    if (__any(mask != 0)) group_chunk<MODE>(a, sg, ch, mask, lane, acc_lds, plds);
+    if (__any(mask != 0)) {
+      if constexpr (PF) group_chunk_pf<MODE>(a, sg, ch, mask, lane, plds);
+      else group_chunk<MODE>(a, sg, ch, mask, lane, acc_lds, plds);
+    }
   }
   matched = wave_sum(matched);  // the EMIT pass re-reads what the COUNT pass already counted
   if (MODE != GB_EMIT && MODE != GB_VERIFY && lane == 0 && matched) atomicAdd(a.matched + g, matched);
@@ -1009,8 +1107,11 @@ void launch_group_query(const GroupArgs &a, hipStream_t stream) {
   switch (a.mode) {
     case GB_GLOBAL: hipLaunchKernelGGL(k_group_query<GB_GLOBAL>, grid, block, lds, stream, a); break;
     case GB_LDS: hipLaunchKernelGGL(k_group_query<GB_LDS>, grid, block, lds, stream, a); break;
-    case GB_COUNT: hipLaunchKernelGGL(k_group_query<GB_COUNT>, grid, block, lds, stream, a); break;
-    case GB_EMIT: hipLaunchKernelGGL(k_group_query<GB_EMIT>, grid, block, lds, stream, a); break;
+    case GB_COUNT: hipLaunchKernelGGL(k_group_query<GB_COUNT>, grid, block, lds, stream, a); break;  // 2 columns: no gain
+    case GB_EMIT:
+      if (a.pf_nc > 0) hipLaunchKernelGGL((k_group_query<GB_EMIT, true>), grid, block, lds, stream, a);
+      else hipLaunchKernelGGL(k_group_query<GB_EMIT>, grid, block, lds, stream, a);
+      break;
     default: hipLaunchKernelGGL(k_group_query<GB_VERIFY>, grid, block, lds, stream, a); break;
   }
 }

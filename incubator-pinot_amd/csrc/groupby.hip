@@ -41,6 +41,29 @@ __device__ __forceinline__ double dict_value_r(const void *dict, int value_kind,
   }
 }
 
+// stream-lib MurmurHash.hashLong and HyperLogLog (register << 8 | rank) — the device twins of hll.cpp's
+// murmur_hash_long / hll_register_rank (bit-identical integer arithmetic).
+__device__ __forceinline__ uint32_t murmur_hash_long_d(long long data) {
+  constexpr uint32_t kM = 0x5bd1e995u;
+  const unsigned long long d = (unsigned long long)data;
+  uint32_t h = 0;
+  uint32_t k = (uint32_t)d * kM;
+  k ^= k >> 24;
+  h ^= k * kM;
+  k = (uint32_t)(d >> 32) * kM;
+  k ^= k >> 24;
+  h *= kM;
+  h ^= k * kM;
+  h ^= h >> 13;
+  h *= kM;
+  h ^= h >> 15;
+  return h;
+}
+
+__device__ __forceinline__ uint32_t hll_register_rank_d(uint32_t h) {
+  return ((h >> 24) << 8) | (uint32_t)(__builtin_clz((h << 8) | 129u) + 1);
+}
+
 __global__ __launch_bounds__(kReduceBlock) void k_partition_reduce(PartitionReduceArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int tid = threadIdx.x;
@@ -87,16 +110,18 @@ __global__ __launch_bounds__(kReduceBlock) void k_partition_reduce(PartitionRedu
       for (int u = 0; u < U; u++) id[u] = ok[u] ? (uint32_t)((rec[u] >> ag.field_shift) & ((1ull << ag.bits) - 1ull)) : 0u;
       uint8_t *acc = lds + ag.lds_off;
       if (ag.acc_kind == 0) {
-        long long v[U];
+        long long v[U];  // affine: Σ dictId here, Σ value = base * count + step * Σ dictId at the end
 #pragma unroll
-        for (int u = 0; u < U; u++) v[u] = static_cast<const int32_t *>(ag.dict)[id[u]];
+        for (int u = 0; u < U; u++) v[u] = ag.affine ? (long long)id[u] : (long long)static_cast<const int32_t *>(ag.dict)[id[u]];
 #pragma unroll
         for (int u = 0; u < U; u++)
           if (ok[u]) atomicAdd(reinterpret_cast<unsigned long long *>(acc) + k[u], (unsigned long long)v[u]);
       } else if (ag.acc_kind == 4) {  // u8 registers: byte max by CAS on the containing dword
         uint32_t h[U];
 #pragma unroll
-        for (int u = 0; u < U; u++) h[u] = ag.hll_lut[id[u]];
+        for (int u = 0; u < U; u++)
+          h[u] = ag.affine ? hll_register_rank_d(murmur_hash_long_d(ag.affine_base + ag.affine_step * (long long)id[u]))
+                           : (uint32_t)ag.hll_lut[id[u]];
         uint32_t *word[U], old[U], rank[U];
         int sh[U];
 #pragma unroll
@@ -152,7 +177,14 @@ __global__ __launch_bounds__(kReduceBlock) void k_partition_reduce(PartitionRedu
       unsigned long long *out = static_cast<unsigned long long *>(ag.acc);
       for (int i = tid; i < K; i += kReduceBlock) {
         const long long key = base + i;
-        if (key < a.G) out[key] = reinterpret_cast<const unsigned long long *>(acc)[i];
+        if (key >= a.G) continue;
+        unsigned long long v = reinterpret_cast<const unsigned long long *>(acc)[i];
+        if (ag.acc_kind == 0 && ag.affine) {
+          uint32_t c = 0;
+          for (int w = 0; w < kReduceCountCopies; w++) c += cnt[a.wave_cnt_off / 4 + w * K + i];
+          v = (unsigned long long)ag.affine_base * c + (unsigned long long)ag.affine_step * v;  // exact mod 2^64
+        }
+        out[key] = v;
       }
     }
   }
@@ -221,14 +253,19 @@ __global__ void k_partition_starts(const uint32_t *__restrict__ offsets, const u
 
 // Second level of the two-level partitioned plan: block (q, b) moves coarse run (q, b) — the records block b
 // of the EMIT pass wrote for partitions q*F .. q*F+F-1, in any order — to those partitions' final slots
-// offsets[p][b] (the single-level layout, partition-major then block). The live cursors are F per block, so
-// the stores of all resident blocks combine into whole lines in L2.
-__global__ __launch_bounds__(256) void k_partition_split(const uint32_t *__restrict__ hist, const uint32_t *__restrict__ offsets,
-                                                         const uint32_t *__restrict__ pstart, int32_t P, int32_t nblk,
-                                                         int32_t shift, int32_t split,
-                                                         const unsigned long long *__restrict__ runs,
-                                                         unsigned long long *__restrict__ records) {
-  __shared__ uint32_t cur[256];
+// offsets[p][b] (the single-level layout, partition-major then block). Tiles of kSplitTile records are
+// counting-sorted by partition in LDS first, so each partition's share of a tile leaves as one contiguous,
+// coalesced piece (a per-record scatter costs a cache-line request per record in the address unit).
+constexpr int kSplitBlock = 256;
+constexpr int kSplitTile = 2048;
+
+__global__ __launch_bounds__(kSplitBlock) void k_partition_split(const uint32_t *__restrict__ hist, const uint32_t *__restrict__ offsets,
+                                                                 const uint32_t *__restrict__ pstart, int32_t P, int32_t nblk,
+                                                                 int32_t shift, int32_t split,
+                                                                 const unsigned long long *__restrict__ runs,
+                                                                 unsigned long long *__restrict__ records) {
+  __shared__ unsigned long long sorted[kSplitTile];
+  __shared__ uint32_t cur[256], bcount[256], bstart[256];
   __shared__ uint32_t run_b, run_e;
   const int F = 1 << split;
   const int q = blockIdx.x / nblk, b = blockIdx.x % nblk, tid = threadIdx.x;
@@ -242,13 +279,65 @@ __global__ __launch_bounds__(256) void k_partition_split(const uint32_t *__restr
     run_b = s0;
     run_e = s0 + n;
   }
-  if (tid < F) cur[tid] = q * F + tid < P ? offsets[(size_t)(q * F + tid) * nblk + b] : 0u;
+  if (tid < F) {
+    cur[tid] = q * F + tid < P ? offsets[(size_t)(q * F + tid) * nblk + b] : 0u;
+    bcount[tid] = 0;
+  }
   __syncthreads();
   const uint32_t e = run_e;
-  for (uint32_t r = run_b + tid; r < e; r += 256) {
-    const unsigned long long rec = __builtin_nontemporal_load(runs + r);
-    const uint32_t pos = atomicAdd(&cur[(rec >> shift) & (unsigned long long)(F - 1)], 1u);
-    records[pos] = rec;
+  constexpr int R = kSplitTile / kSplitBlock;
+  const unsigned long long smask = (unsigned long long)(F - 1);
+  for (uint32_t t0 = run_b; t0 < e; t0 += kSplitTile) {
+    const uint32_t tn = min((uint32_t)kSplitTile, e - t0);
+    unsigned long long rec[R];
+    uint32_t rank[R];
+#pragma unroll
+    for (int i = 0; i < R; i++) {
+      const uint32_t j = (uint32_t)(i * kSplitBlock + tid);
+      rec[i] = j < tn ? __builtin_nontemporal_load(runs + t0 + j) : 0ull;
+    }
+#pragma unroll
+    for (int i = 0; i < R; i++)
+      if ((uint32_t)(i * kSplitBlock + tid) < tn) rank[i] = atomicAdd(&bcount[(rec[i] >> shift) & smask], 1u);
+    __syncthreads();
+    if (tid < 64) {  // exclusive scan of the F <= 256 bucket counts by one wave
+      uint32_t v[4], sum = 0;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int s = tid * 4 + k;
+        v[k] = s < F ? bcount[s] : 0u;
+        sum += v[k];
+      }
+      uint32_t incl = sum;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(incl, d, 64);
+        if (tid >= d) incl += o;
+      }
+      uint32_t run = incl - sum;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int s = tid * 4 + k;
+        if (s < F) bstart[s] = run;
+        run += v[k];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < R; i++)
+      if ((uint32_t)(i * kSplitBlock + tid) < tn) sorted[bstart[(rec[i] >> shift) & smask] + rank[i]] = rec[i];
+    __syncthreads();
+    for (uint32_t j = tid; j < tn; j += kSplitBlock) {
+      const unsigned long long r = sorted[j];
+      const uint32_t s = (uint32_t)((r >> shift) & smask);
+      records[cur[s] + (j - bstart[s])] = r;
+    }
+    __syncthreads();
+    if (tid < F) {
+      cur[tid] += bcount[tid];
+      bcount[tid] = 0;
+    }
+    __syncthreads();
   }
 }
 
@@ -274,7 +363,7 @@ void launch_partition_split(const uint32_t *hist, const uint32_t *offsets, const
                             unsigned long long *records, hipStream_t stream) {
   if (P <= 0 || split <= 0) return;
   const int Q = (P + (1 << split) - 1) >> split;
-  hipLaunchKernelGGL(k_partition_split, dim3((unsigned)Q * (unsigned)nblk), dim3(256), 0, stream, hist, offsets, pstart,
+  hipLaunchKernelGGL(k_partition_split, dim3((unsigned)Q * (unsigned)nblk), dim3(kSplitBlock), 0, stream, hist, offsets, pstart,
                      P, nblk, shift, split, runs, records);
 }
 

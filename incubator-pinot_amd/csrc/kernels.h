@@ -204,7 +204,9 @@ struct GroupAggDev {
   int32_t bits, acc_kind, value_kind;
   int32_t field_shift;       // GB_EMIT: bit position of this column's dictId in the record
   int32_t lds_off;           // GB_LDS / k_partition_reduce: byte offset of its LDS accumulator array
-  int32_t reserved;
+  int32_t affine;            // INT/LONG dictionary value(id) = affine_base + affine_step * id: k_partition_reduce
+                             // sums dictIds (SUM) and hashes the value arithmetically (HLL) — no gathers
+  long long affine_base, affine_step;
 };
 
 struct GroupSegment {
@@ -246,7 +248,13 @@ struct GroupArgs {
   uint32_t *verify_err;        // GB_VERIFY: set when a doc's tuple differs from its slot's representative
   int32_t hashed;
   int32_t reserved2;
+  // GB_COUNT / GB_EMIT column prefetch: every column a doc needs (group columns, then the aggregated
+  // columns pf_agg[c] for slots c >= n_gcols) is loaded for kGroupPfUnroll words before any is decoded;
+  // pf_nc = number of slots (<= kGroupPfCols), 0 = off (per-column loop)
+  int32_t pf_nc;
+  int32_t pf_agg[4];
 };
+constexpr int kGroupPfCols = 4;
 void launch_group_query(const GroupArgs &a, hipStream_t stream);
 // Grid (blocks per segment x segments) the host sizes `hist` / `offsets` for.
 int group_query_blocks_per_cu(const GroupArgs &a);

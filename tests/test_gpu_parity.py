@@ -490,3 +490,38 @@ def test_config1_baseball_synthetic(engine):
     assert st.num_docs_scanned == scanned
     _assert_group_maps(q, got, exp)
     g.release()
+
+
+@pytest.mark.parametrize("mode", ["group.mode=partition;group.pshift=3", "group.mode=partition;group.pshift=3;agg.affine=0",
+                                  "group.mode=partition;group.pshift=2;group.split=0", "group.mode=partition"])
+def test_group_by_partitioned_affine(mode):
+    """Partitioned plan over arithmetic-progression dictionaries (k_partition_reduce sums dictIds and hashes
+    value = base + step * dictId on the device) against the oracle: SUM / AVG / MAX and DISTINCTCOUNTHLL of INT
+    and LONG columns, negative bases, over two segments with identical dictionaries."""
+    rng = np.random.default_rng(77)
+    n = 30000
+
+    def ap(card, base, step):
+        ids = np.concatenate([np.arange(card), rng.integers(0, card, n - card)])  # every value present
+        return (base + step * ids).astype(np.int64).tolist()
+
+    cols = {"g0": ("INT", ap(40, 0, 1)), "g1": ("INT", ap(30, -7, 3)), "m": ("INT", ap(1000, -123456, 77)),
+            "h": ("INT", ap(5000, -2 ** 31 + 5, 1)), "l": ("LONG", ap(300, -2 ** 40, 12345))}
+    perm = rng.permutation(n)
+    segs = [build_segment("a0", cols),
+            build_segment("a1", {k: (t, [v[i] for i in perm]) for k, (t, v) in cols.items()})]
+    e = GpuEngine(0, mode)
+    gsegs = [e.register(x) for x in segs]
+    ex = ServerQueryExecutor(e)
+    for pql in ("SELECT COUNT(*), SUM(m), AVG(m), MAX(m), DISTINCTCOUNTHLL(h), DISTINCTCOUNTHLL(l) FROM t "
+                "WHERE m > -100000 GROUP BY g0, g1",
+                "SELECT SUM(m), DISTINCTCOUNTHLL(m), MIN(l) FROM t GROUP BY g1, g0"):
+        q = compile_pql(pql)
+        got, st = ex.process_query(q, gsegs, trim=False)
+        exp, scanned = O.execute_server(segs, q)
+        assert st.num_docs_scanned == scanned
+        assert set(got) == set(exp)
+        for key in exp:
+            for a, gv, ev in zip(q["aggregations"], got[key], exp[key]):
+                _assert_same(a["function"], gv, ev, True)
+    e.close()

@@ -90,6 +90,7 @@ void parse_config(Engine &e, const char *cfg) {
     } else if (k == "sync.poll") e.sync_poll = v == "1" || v == "true";
     else if (k == "debug.emit") e.debug_emit = std::stoi(v);
     else if (k == "group.pshift") e.group_pshift = std::stoi(v);
+    else if (k == "group.nt_store") e.group_nt_store = std::stoi(v) != 0;
     else if (k == "group.prefetch") e.group_prefetch = v == "1" || v == "true";
     else if (k == "group.split") {
       e.group_split = std::stoi(v);
@@ -261,7 +262,7 @@ pinot_status pinot_groupby_values(const pinot_groupby_result *r, int32_t fn, int
   return guard([&] {
     require(r && fn >= 0 && fn < (int32_t)r->functions.size(), PINOT_ERR_BAD_ARG, "function index");
     const size_t n = r->raw_keys.size();
-    if (counts && n) memcpy(counts, r->counts[fn].data(), n * 8);
+    if (counts && n) memcpy(counts, r->counts[r->counts_shared ? 0 : fn].data(), n * 8);
     if (values && n) memcpy(values, r->values[fn].data(), n * 8);
   });
 }

@@ -117,6 +117,7 @@ struct Engine {
   bool sync_poll = false;     // sync.poll: busy-poll the stream instead of hipStreamSynchronize
   bool host_phases = false;
   int debug_emit = 0;         // debug.emit: GB_EMIT store experiments (timing only, wrong results)
+  int group_nt_store = 0;     // group.nt_store: partitioned records stored non-temporally
   bool group_prefetch = true; // group.prefetch: partitioned plan loads every column of a word batch at once
   int group_pshift = -1;      // group.pshift: cap on log2 keys per partition (tests: many small partitions)
   int group_split = -1;       // group.split: log2 sub-partitions per emitted run (-1 auto, 0 single-level)
@@ -163,7 +164,8 @@ struct GroupByResult {
   std::vector<int64_t> raw_keys;              // ascending raw keys (mixed radix over global ids, column 0 least significant)
   int32_t num_columns = 0;
   std::vector<int> functions;
-  std::vector<std::vector<int64_t>> counts;   // per fn
+  std::vector<std::vector<int64_t>> counts;   // per fn (counts_shared: one vector, counts[0], for every fn)
+  bool counts_shared = false;
   std::vector<std::vector<double>> values;    // per fn
   // group key strings ('\t'-joined Dictionary.getStringValue), built on first access
   std::vector<std::vector<std::string>> gvalues;  // [gcol] global id -> string

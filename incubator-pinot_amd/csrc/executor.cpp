@@ -1068,7 +1068,12 @@ constexpr int64_t kDenseKeyLimit = int64_t(1) << 27;
 
 bool same_dictionary(const ColumnData &a, const ColumnData &b) {
   if (a.data_type != b.data_type || a.card != b.card) return false;
-  if (a.data_type == PINOT_INT || a.data_type == PINOT_LONG) return a.dict_int == b.dict_int;
+  if (a.data_type == PINOT_INT || a.data_type == PINOT_LONG) {
+    // arithmetic progressions are equal when their (base, step) are: no element-wise pass over 1M-entry
+    // dictionaries on every query
+    if (a.affine && b.affine) return a.affine_base == b.affine_base && a.affine_step == b.affine_step;
+    return a.dict_int == b.dict_int;
+  }
   if (a.data_type == PINOT_STRING) return a.dict_str == b.dict_str;
   return a.dict_dbl == b.dict_dbl;
 }
@@ -1461,7 +1466,7 @@ size_t lds_acc_bytes_per_key(int kind, bool lds_hll_u32) {
   return 8;
 }
 
-constexpr int64_t kCoarseRuns = 128;  // EMIT's live partition cursors per block in the two-level plan
+constexpr int64_t kCoarseRuns = 16;  // EMIT's live run cursors per block (16: fewest lines per scattered store, measured)
 
 GroupPlan plan_group(const std::vector<SegmentData *> &segs, const pinot_query &q, const KeySpace &ks,
                      const GroupAccs &ga, const std::string &force, int force_split, int max_shift) {
@@ -1600,6 +1605,7 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     plans[si].seg = segs[si];
     Compiler(e, plans[si], ar).run_fused(tree.get(), kGroupMaxFusedLeafBits);
   }
+  const auto tga = std::chrono::steady_clock::now();
   // remaps (dictId -> global id) travel in the arena
   std::vector<std::vector<size_t>> remap_off(S, std::vector<size_t>(q.num_group_by, SIZE_MAX));
   for (size_t si = 0; si < S; si++)
@@ -1611,6 +1617,7 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
                            S * q.num_group_by * sizeof(GroupColDev) + S * na * sizeof(GroupAggDev) + 512;
   QueryScratch qs = prepare_scratch(e, plans, ar, true, tab_bytes);
 
+  const auto tgb = std::chrono::steady_clock::now();
   // dense accumulators: counts u64 [G], then one array per aggregation (HLL: u8 [G][256])
   std::vector<size_t> acc_bytes(na, 0);
   size_t per_key = 8;
@@ -1641,6 +1648,7 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
       if (alias[a] >= 0) accs[a] = accs[alias[a]];
   }
 
+  const auto tgc = std::chrono::steady_clock::now();
   // device program
   std::vector<GroupSegment> gsegs(S);
   std::vector<FusedStep> leaves;
@@ -1722,6 +1730,7 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
   a.P = (int32_t)gp.P;
   a.mode = gp.mode == GB_EMIT ? GB_COUNT : gp.mode;
   a.reserved2 = e.debug_emit;  // timing experiments only (debug.emit)
+  a.nt_store = e.group_nt_store;
   if (gp.mode == GB_EMIT && !ks.hashed && e.group_prefetch && e.debug_emit == 0) {
     int nc = q.num_group_by;
     for (int i = 0; i < na && nc <= kGroupPfCols; i++)
@@ -1816,7 +1825,7 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
       a2.split = gp.split;
       launch_group_query(a2, e.stream);
       launch_partition_split(hist, offsets, pstart, (int32_t)gp.P, (int32_t)nblk, gp.shift, gp.split, a.emit,
-                             e.group_records.get<unsigned long long>(), e.stream);
+                             e.group_records.get<unsigned long long>(), e.group_nt_store, e.stream);
       launch_partition_reduce(ra, e.stream);
     });
     PINOT_HIP(hipGetLastError());
@@ -1916,8 +1925,9 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     // result arrays: sized (first touch of fresh pages) and filled in parallel over the host's cores
     std::vector<std::function<void()>> sizing;
     sizing.push_back([&] { res->raw_keys.resize(n); });
+    res->counts_shared = true;  // every aggregation counts the same docs per group
+    sizing.push_back([&] { res->counts[0].resize(n); });
     for (int i = 0; i < na; i++) {
-      sizing.push_back([&, i] { res->counts[i].resize(n); });
       sizing.push_back([&, i] { res->values[i].resize(n); });
       if (ga.acc_kind[i] == 4) sizing.push_back([&, i] { res->hll_card[i].resize(n); });
     }
@@ -1928,10 +1938,9 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     parallel_tasks(nt, [&](size_t t) {
       const size_t lo = n * t / nt, hi = n * (t + 1) / nt;
       memcpy(res->raw_keys.data() + lo, hkeys + lo, (hi - lo) * 8);
+      memcpy(res->counts[0].data() + lo, hc + lo, (hi - lo) * 8);
       for (int i = 0; i < na; i++) {
-        int64_t *cv = res->counts[i].data();
         double *vv = res->values[i].data();
-        memcpy(cv + lo, hc + lo, (hi - lo) * 8);
         const int ak = ga.acc_kind[i];
         const int src = alias[i] >= 0 ? alias[i] : i;  // the accumulator this aggregation reads
         const unsigned long long *raw = hacc + (size_t)src * n;
@@ -1967,6 +1976,8 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
   if (e.host_phases) {
     const auto tg5 = std::chrono::steady_clock::now();
     auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+    fprintf(stderr, "[pinot_gpu] group-by plan (us): compile %.1f, remap+scratch %.1f, accumulators %.1f, program %.1f\n",
+            us(tg0, tga), us(tga, tgb), us(tgb, tgc), us(tgc, tgp));
     fprintf(stderr, "[pinot_gpu] group-by host phases (us): plan %.1f, upload %.1f, launch %.1f, kernels %.1f, "
             "compact+sync %.1f, outputs+D2H %.1f, host finalize %.1f (%llu groups)\n", us(tg0, tgp), us(tgp, tgu),
             us(tgu, tg1), us(tg1, tg2), us(tg2, tg3), us(tg3, tg4), us(tg4, tg5), (unsigned long long)n);

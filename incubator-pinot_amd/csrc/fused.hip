@@ -935,7 +935,11 @@ __device__ __forceinline__ void group_chunk_pf(const GroupArgs &a, const GroupSe
       for (int u = 0; u < U; u++) pos[u] = atomicAdd(&plds[key[u] >> rshift], act[u] ? 1u : 0u);
 #pragma unroll
       for (int u = 0; u < U; u++)
-        if (act[u]) a.emit[pos[u]] = rec[u] | (key[u] & ((1ull << rshift) - 1ull));
+        if (act[u]) {
+          const unsigned long long r = rec[u] | (key[u] & ((1ull << rshift) - 1ull));
+          if (a.nt_store) __builtin_nontemporal_store(r, a.emit + pos[u]);
+          else a.emit[pos[u]] = r;
+        }
     }
   }
 }

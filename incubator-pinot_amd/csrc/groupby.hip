@@ -256,14 +256,14 @@ __global__ void k_partition_starts(const uint32_t *__restrict__ offsets, const u
 // offsets[p][b] (the single-level layout, partition-major then block). Tiles of kSplitTile records are
 // counting-sorted by partition in LDS first, so each partition's share of a tile leaves as one contiguous,
 // coalesced piece (a per-record scatter costs a cache-line request per record in the address unit).
-constexpr int kSplitBlock = 256;
-constexpr int kSplitTile = 2048;
+constexpr int kSplitBlock = 1024;
+constexpr int kSplitTile = 8192;
 
 __global__ __launch_bounds__(kSplitBlock) void k_partition_split(const uint32_t *__restrict__ hist, const uint32_t *__restrict__ offsets,
                                                                  const uint32_t *__restrict__ pstart, int32_t P, int32_t nblk,
                                                                  int32_t shift, int32_t split,
                                                                  const unsigned long long *__restrict__ runs,
-                                                                 unsigned long long *__restrict__ records) {
+                                                                 unsigned long long *__restrict__ records, int nt_store) {
   __shared__ unsigned long long sorted[kSplitTile];
   __shared__ uint32_t cur[256], bcount[256], bstart[256];
   __shared__ uint32_t run_b, run_e;
@@ -330,7 +330,8 @@ __global__ __launch_bounds__(kSplitBlock) void k_partition_split(const uint32_t 
     for (uint32_t j = tid; j < tn; j += kSplitBlock) {
       const unsigned long long r = sorted[j];
       const uint32_t s = (uint32_t)((r >> shift) & smask);
-      records[cur[s] + (j - bstart[s])] = r;
+      if (nt_store) __builtin_nontemporal_store(r, records + cur[s] + (j - bstart[s]));
+      else records[cur[s] + (j - bstart[s])] = r;
     }
     __syncthreads();
     if (tid < F) {
@@ -360,11 +361,11 @@ void launch_partition_starts(const uint32_t *offsets, const uint32_t *hist, int3
 
 void launch_partition_split(const uint32_t *hist, const uint32_t *offsets, const uint32_t *pstart, int32_t P,
                             int32_t nblk, int32_t shift, int32_t split, const unsigned long long *runs,
-                            unsigned long long *records, hipStream_t stream) {
+                            unsigned long long *records, int nt_store, hipStream_t stream) {
   if (P <= 0 || split <= 0) return;
   const int Q = (P + (1 << split) - 1) >> split;
   hipLaunchKernelGGL(k_partition_split, dim3((unsigned)Q * (unsigned)nblk), dim3(kSplitBlock), 0, stream, hist, offsets, pstart,
-                     P, nblk, shift, split, runs, records);
+                     P, nblk, shift, split, runs, records, nt_store);
 }
 
 void launch_gather_hll(const uint8_t *regs, const long long *keys, long long n, uint8_t *out, hipStream_t stream) {

@@ -253,6 +253,7 @@ struct GroupArgs {
   // pf_nc = number of slots (<= kGroupPfCols), 0 = off (per-column loop)
   int32_t pf_nc;
   int32_t pf_agg[4];
+  int32_t nt_store;            // GB_EMIT / split: records stored with the non-temporal (streaming) policy
 };
 constexpr int kGroupPfCols = 4;
 void launch_group_query(const GroupArgs &a, hipStream_t stream);
@@ -275,7 +276,7 @@ void launch_partition_reduce(const PartitionReduceArgs &a, hipStream_t stream);
 // emitted by block b) is split into the partitions' final slots offsets[p][b]... of `records`.
 void launch_partition_split(const uint32_t *hist, const uint32_t *offsets, const uint32_t *pstart, int32_t P,
                             int32_t nblk, int32_t shift, int32_t split, const unsigned long long *runs,
-                            unsigned long long *records, hipStream_t stream);
+                            unsigned long long *records, int nt_store, hipStream_t stream);
 // pstart[p] = offsets[p * nblk] (partition-major exclusive offsets), pstart[P] = total records.
 void launch_partition_starts(const uint32_t *offsets, const uint32_t *hist, int32_t P, int32_t nblk, uint32_t *pstart,
                              hipStream_t stream);

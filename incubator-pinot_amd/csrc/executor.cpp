@@ -1566,9 +1566,15 @@ bool needs_admission(const std::vector<SegmentData *> &segs, const pinot_query &
 
 // Fused group-by: ONE k_group_query launch (or COUNT / EMIT / reduce for the partitioned plan) over all
 // segments, device compaction of the non-empty keys, device per-group outputs, one D2H of the arrays.
+// Multi-GPU partial output (pinot_gpu_group_by_partial): the caller's dense arrays in the partial layout.
+struct PartialOut {
+  int64_t *counts;
+  void *const *accs;
+};
+
 std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q,
                                                    const KeySpace &ks_in, const GroupAccs &ga, pinot_exec_stats *stats,
-                                                   int attempt = 0) {
+                                                   int attempt = 0, const PartialOut *po = nullptr) {
   const auto tg0 = std::chrono::steady_clock::now();
   const int na = q.num_aggregations;
   const size_t S = segs.size();
@@ -1831,6 +1837,29 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     PINOT_HIP(hipGetLastError());
   }
 
+  if (po) {  // partial: the dense accumulators go out as they are (HLL registers widened to int32), no compaction
+    PINOT_HIP(hipMemcpyAsync(po->counts, counts, ks.G * 8, hipMemcpyDeviceToDevice, e.stream));
+    for (int i = 0; i < na; i++) {
+      if (ga.acc_kind[i] == 5) continue;
+      if (ga.acc_kind[i] == 4)
+        launch_widen_u8(static_cast<const uint8_t *>(accs[i]), ks.G * 256, static_cast<int32_t *>(po->accs[i]), e.stream);
+      else
+        PINOT_HIP(hipMemcpyAsync(po->accs[i], accs[i], ks.G * 8, hipMemcpyDeviceToDevice, e.stream));
+    }
+    PINOT_HIP(hipGetLastError());
+    std::vector<unsigned long long> hm(S);
+    PINOT_HIP(hipMemcpyAsync(hm.data(), matched, S * 8, hipMemcpyDeviceToHost, e.stream));
+    PINOT_HIP(hipEventRecord(e.ev_stop, e.stream));
+    PINOT_HIP(hipStreamSynchronize(e.stream));
+    float pms = 0;
+    PINOT_HIP(hipEventElapsedTime(&pms, e.ev_start, e.ev_stop));
+    t.collect();
+    std::vector<int64_t> seg_counts(S);
+    for (size_t si = 0; si < S; si++) seg_counts[si] = plans[si].empty ? 0 : (int64_t)hm[si];
+    fill_stats(q, plans, seg_counts, pms, stats);
+    return nullptr;
+  }
+
   const auto tg1 = std::chrono::steady_clock::now();
   if (e.host_phases) PINOT_HIP(hipStreamSynchronize(e.stream));
   const auto tg2 = std::chrono::steady_clock::now();
@@ -2071,12 +2100,18 @@ void exec_group_by_layout(Engine &e, const std::vector<SegmentData *> &segs, con
 
 void exec_group_by_partial(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q,
                            int64_t *counts_dev, void *const *accs_dev, pinot_exec_stats *stats) {
-  Arena ar;
-  std::unique_ptr<FilterTreeInput> tree;
-  std::vector<SegPlan> plans = plan_all(e, segs, q, ar, tree);
+  require(!segs.empty(), PINOT_ERR_BAD_ARG, "no segments");
   KeySpace ks = build_key_space(segs, q);
   require(!ks.hashed, PINOT_ERR_UNSUPPORTED, "partial group-by needs a dense key space");
   GroupAccs ga = group_acc_kinds(*segs[0], q);
+  if (e.use_fused && !needs_admission(segs, q, e)) {  // the fused sinks, stopped before compaction
+    const PartialOut po{counts_dev, accs_dev};
+    exec_group_by_fused(e, segs, q, ks, ga, stats, 0, &po);
+    return;
+  }
+  Arena ar;
+  std::unique_ptr<FilterTreeInput> tree;
+  std::vector<SegPlan> plans = plan_all(e, segs, q, ar, tree);
   QueryScratch qs = prepare(e, plans, ar);
   PINOT_HIP(hipEventRecord(e.ev_start, e.stream));
   auto *counts = reinterpret_cast<unsigned long long *>(counts_dev);

@@ -351,7 +351,27 @@ __global__ void k_gather_hll(const uint8_t *__restrict__ regs, const long long *
   }
 }
 
+__global__ void k_widen_u8(const uint8_t *__restrict__ in, long long n4, int32_t *__restrict__ out) {
+  // multi-GPU partial layout: u8 HLL registers -> int32 (4 registers per thread, one 16-B store)
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    const uint32_t w = reinterpret_cast<const uint32_t *>(in)[i];
+    u32x4 o;
+    o.x = w & 0xFF;
+    o.y = (w >> 8) & 0xFF;
+    o.z = (w >> 16) & 0xFF;
+    o.w = w >> 24;
+    reinterpret_cast<u32x4 *>(out)[i] = o;
+  }
+}
+
 }  // namespace
+
+void launch_widen_u8(const uint8_t *in, long long n, int32_t *out, hipStream_t stream) {
+  if (n <= 0) return;
+  const long long n4 = n / 4;  // n = G * 256: always a multiple of 4
+  const int grid = (int)std::min<long long>((n4 + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_widen_u8, dim3(grid), dim3(256), 0, stream, in, n4, out);
+}
 
 void launch_partition_starts(const uint32_t *offsets, const uint32_t *hist, int32_t P, int32_t nblk, uint32_t *pstart,
                              hipStream_t stream) {

@@ -130,7 +130,7 @@ def allreduce_group_partials(acc_kinds, counts, accs, group=None):
             dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
 
 
-def distributed_group_by(executor, query, segments, group=None, world=1):
+def distributed_group_by(executor, query, segments, group=None, world=1, force_collective=False, as_map=True):
     """Group-by over this rank's GPU-resident `segments`, merged with the other ranks over RCCL.
 
     Runs pinot_gpu_group_by_layout / _partial into torch CUDA tensors, all-reduces them and finalises
@@ -165,10 +165,11 @@ def distributed_group_by(executor, query, segments, group=None, world=1):
     torch.cuda.synchronize(dev)
     check(lib.pinot_gpu_group_by_partial(eng.ptr, handles, len(segments), C.byref(m.q),
                                          C.c_void_p(counts.data_ptr()), ptrs, C.byref(stats)))
-    if world > 1:
+    if world > 1 or force_collective:
         allreduce_group_partials(kinds, counts, accs, group)
         torch.cuda.synchronize(dev)
     out = C.c_void_p()
     check(lib.pinot_gpu_group_by_finalize(eng.ptr, handles, len(segments), C.byref(m.q),
                                           C.c_void_p(counts.data_ptr()), ptrs, C.byref(out)))
-    return GroupByResult(lib, out, query).to_map(), stats
+    res = GroupByResult(lib, out, query)
+    return (res.to_map() if as_map else res), stats

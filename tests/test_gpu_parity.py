@@ -377,10 +377,13 @@ def test_fused_and_unfused_agree_on_selective_index_filters(sv_segment):
     e0.close()
 
 
-def test_distributed_group_by_single_rank(sv_segment):
-    """pinot_gpu_group_by_partial -> (no peers) -> finalize equals the one-call group-by."""
+@pytest.mark.parametrize("cfg", [None, "exec.fused=0", "group.mode=lds", "group.mode=global",
+                                 "group.mode=partition;group.pshift=2;group.split=2"])
+def test_distributed_group_by_single_rank(sv_segment, cfg):
+    """pinot_gpu_group_by_partial -> (no peers) -> finalize equals the one-call group-by, through the fused
+    sinks (stopped before compaction) and the bitset path."""
     from pinot_amd.combine import distributed_group_by
-    e = GpuEngine(0)
+    e = GpuEngine(0, cfg)
     g = e.register(sv_segment)
     ex = ServerQueryExecutor(e)
     q = compile_pql("SELECT COUNT(*), SUM(column1), MIN(column3), MAX(column6), AVG(column7), "

@@ -206,7 +206,8 @@ typedef struct {
   int32_t reserved;
   /* per aggregation f: accumulator kind and element size, so the caller can allocate:
      kind 0 = int64 sum, 1 = double sum, 2 = uint64 ordered-min, 3 = uint64 ordered-max,
-     4 = uint32 HLL registers (256 per key), 5 = none (COUNT uses the shared count array) */
+     4 = uint8 HLL registers (256 bytes per key: an all-reduce MAX over uint8 moves G*256 bytes),
+     5 = none (COUNT uses the shared count array) */
   int32_t acc_kind[8];
 } pinot_partial_layout;
 

@@ -1234,14 +1234,19 @@ double decode_ordered(uint64_t o) {
   return d;
 }
 
+void parallel_tasks(size_t n, const std::function<void(size_t)> &fn);
+
+// Dense accumulators -> result arrays (bitset path and the multi-GPU partial finalize): ordered device
+// compaction of the non-empty keys, one gather, D2H into grow-only engine buffers, host fill over 8 threads.
 std::unique_ptr<GroupByResult> finalize_groups(Engine &e, const pinot_query &q, const GroupAccs &ga,
                                                const KeySpace &ks, GroupByProgram gp) {
   const int na = q.num_aggregations;
-  // compact non-empty keys and gather their accumulators
-  DeviceBuffer keys_dev(std::max<int64_t>(ks.G, 1) * 8 + 16);
-  auto *n_dev = reinterpret_cast<unsigned long long *>(keys_dev.get<uint8_t>() + ks.G * 8);
-  PINOT_HIP(hipMemsetAsync(n_dev, 0, 8, e.stream));
-  launch_compact_keys(ks.G, gp.counts, keys_dev.get<long long>(), n_dev, e.stream);
+  const size_t cscr = compact_keys_scratch_bytes(ks.G);
+  e.group_final.reserve(std::max<int64_t>(ks.G, 1) * 8 + 64 + cscr);
+  auto *keys_dev = e.group_final.get<long long>();
+  auto *n_dev = reinterpret_cast<unsigned long long *>(e.group_final.get<uint8_t>() + ks.G * 8);
+  launch_compact_keys_ordered(ks.G, gp.counts, keys_dev, n_dev, e.group_final.get<uint8_t>() + ks.G * 8 + 64, cscr,
+                              e.stream);
   PINOT_HIP(hipGetLastError());
   unsigned long long n = 0;
   PINOT_HIP(hipMemcpyAsync(&n, n_dev, 8, hipMemcpyDeviceToHost, e.stream));
@@ -1259,57 +1264,61 @@ std::unique_ptr<GroupByResult> finalize_groups(Engine &e, const pinot_query &q, 
   res->gcard = ks.gcard;
   for (int a = 0; a < na; a++) res->functions[a] = q.aggregations[a].function;
   if (n == 0) return res;
-  DeviceBuffer out(n * 8 * (1 + na) + (size_t)n_hll * n * 256 + 16);
-  auto *o_cnt = out.get<unsigned long long>();
+  // device layout == host layout: keys [n], counts [n], accs [na][n], HLL registers [n_hll][n][256]
+  const size_t out_b = n * 8 * (2 + na) + (size_t)n_hll * n * 256 + 16;
+  e.group_out.reserve(out_b);
+  e.group_host.reserve(out_b);
+  auto *o_keys = e.group_out.get<long long>();
+  auto *o_cnt = reinterpret_cast<unsigned long long *>(o_keys + n);
   auto *o_acc = o_cnt + n;
   auto *o_hll = reinterpret_cast<uint8_t *>(o_acc + n * na);
-  launch_gather_groups(gp, keys_dev.get<long long>(), (int64_t)n, o_cnt, o_acc, o_hll, e.stream);
+  PINOT_HIP(hipMemcpyAsync(o_keys, keys_dev, n * 8, hipMemcpyDeviceToDevice, e.stream));
+  launch_gather_groups(gp, keys_dev, (int64_t)n, o_cnt, o_acc, o_hll, e.stream);
   PINOT_HIP(hipGetLastError());
-  std::vector<long long> hkeys(n);
-  std::vector<unsigned long long> hcnt(n), hacc(n * na);
-  std::vector<uint8_t> hhll((size_t)n_hll * n * 256);
-  PINOT_HIP(hipMemcpyAsync(hkeys.data(), keys_dev.get(), n * 8, hipMemcpyDeviceToHost, e.stream));
-  PINOT_HIP(hipMemcpyAsync(hcnt.data(), o_cnt, n * 8, hipMemcpyDeviceToHost, e.stream));
-  PINOT_HIP(hipMemcpyAsync(hacc.data(), o_acc, n * na * 8, hipMemcpyDeviceToHost, e.stream));
-  if (n_hll) PINOT_HIP(hipMemcpyAsync(hhll.data(), o_hll, hhll.size(), hipMemcpyDeviceToHost, e.stream));
+  PINOT_HIP(hipMemcpyAsync(e.group_host.get(), e.group_out.get(), out_b, hipMemcpyDeviceToHost, e.stream));
   PINOT_HIP(hipStreamSynchronize(e.stream));
-  // order groups by raw key (the compaction order is arbitrary)
-  std::vector<size_t> order(n);
-  std::iota(order.begin(), order.end(), 0);
-  std::sort(order.begin(), order.end(), [&](size_t x, size_t y) { return hkeys[x] < hkeys[y]; });
-  res->raw_keys.resize(n);
-  for (size_t i = 0; i < n; i++) res->raw_keys[i] = hkeys[order[i]];
-  int h = 0;
-  for (int a = 0; a < na; a++) {
-    auto &cv = res->counts[a];
-    auto &vv = res->values[a];
-    cv.resize(n);
-    vv.resize(n);
-    const int ak = ga.acc_kind[a];
-    if (ak == 4) {
+  const auto *hkeys = e.group_host.get<long long>();
+  const auto *hcnt = reinterpret_cast<const unsigned long long *>(hkeys + n);
+  const auto *hacc = hcnt + n;
+  const auto *hhll = reinterpret_cast<const uint8_t *>(hacc + n * na);
+  res->raw_keys.assign(hkeys, hkeys + n);
+  std::vector<int> hidx(na, -1);
+  for (int a = 0, h = 0; a < na; a++) {
+    res->counts[a].resize(n);
+    res->values[a].resize(n);
+    if (ga.acc_kind[a] == 4) {
+      hidx[a] = h++;
       res->hll[a].resize(n * 256);
       res->hll_card[a].resize(n);
     }
-    for (size_t i = 0; i < n; i++) {
-      const size_t src = order[i];
-      cv[i] = (int64_t)hcnt[src];
-      const uint64_t raw = hacc[(size_t)a * n + src];
-      switch (ak) {
-        case 0: vv[i] = (double)(int64_t)raw; break;
-        case 1: { double d; memcpy(&d, &raw, 8); vv[i] = d; break; }
-        case 2:
-        case 3: vv[i] = decode_ordered(raw); break;
-        case 4: {
-          memcpy(res->hll[a].data() + i * 256, hhll.data() + ((size_t)h * n + src) * 256, 256);
-          res->hll_card[a][i] = hll_cardinality(res->hll[a].data() + i * 256);
-          vv[i] = (double)res->hll_card[a][i];
-          break;
+  }
+  const size_t nt = n >= (1u << 16) ? 8 : 1;
+  parallel_tasks(nt, [&](size_t t) {
+    const size_t lo = n * t / nt, hi = n * (t + 1) / nt;
+    for (int a = 0; a < na; a++) {
+      int64_t *cv = res->counts[a].data();
+      double *vv = res->values[a].data();
+      const int ak = ga.acc_kind[a];
+      for (size_t i = lo; i < hi; i++) {
+        cv[i] = (int64_t)hcnt[i];
+        const uint64_t raw = hacc[(size_t)a * n + i];
+        switch (ak) {
+          case 0: vv[i] = (double)(int64_t)raw; break;
+          case 1: { double d; memcpy(&d, &raw, 8); vv[i] = d; break; }
+          case 2:
+          case 3: vv[i] = decode_ordered(raw); break;
+          case 4: {
+            uint8_t *r = res->hll[a].data() + i * 256;
+            memcpy(r, hhll + ((size_t)hidx[a] * n + i) * 256, 256);
+            res->hll_card[a][i] = hll_cardinality(r);
+            vv[i] = (double)res->hll_card[a][i];
+            break;
+          }
+          default: vv[i] = (double)hcnt[i]; break;
         }
-        default: vv[i] = (double)hcnt[src]; break;
       }
     }
-    if (ak == 4) h++;
-  }
+  });
   return res;
 }
 
@@ -1837,15 +1846,12 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     PINOT_HIP(hipGetLastError());
   }
 
-  if (po) {  // partial: the dense accumulators go out as they are (HLL registers widened to int32), no compaction
+  if (po) {  // partial: the dense accumulators go out as they are (u8 HLL registers included), no compaction
     PINOT_HIP(hipMemcpyAsync(po->counts, counts, ks.G * 8, hipMemcpyDeviceToDevice, e.stream));
-    for (int i = 0; i < na; i++) {
-      if (ga.acc_kind[i] == 5) continue;
-      if (ga.acc_kind[i] == 4)
-        launch_widen_u8(static_cast<const uint8_t *>(accs[i]), ks.G * 256, static_cast<int32_t *>(po->accs[i]), e.stream);
-      else
-        PINOT_HIP(hipMemcpyAsync(po->accs[i], accs[i], ks.G * 8, hipMemcpyDeviceToDevice, e.stream));
-    }
+    for (int i = 0; i < na; i++)
+      if (ga.acc_kind[i] != 5)
+        PINOT_HIP(hipMemcpyAsync(po->accs[i], accs[i], ks.G * (ga.acc_kind[i] == 4 ? 256 : 8), hipMemcpyDeviceToDevice,
+                                 e.stream));
     PINOT_HIP(hipGetLastError());
     std::vector<unsigned long long> hm(S);
     PINOT_HIP(hipMemcpyAsync(hm.data(), matched, S * 8, hipMemcpyDeviceToHost, e.stream));
@@ -2113,12 +2119,24 @@ void exec_group_by_partial(Engine &e, const std::vector<SegmentData *> &segs, co
   std::unique_ptr<FilterTreeInput> tree;
   std::vector<SegPlan> plans = plan_all(e, segs, q, ar, tree);
   QueryScratch qs = prepare(e, plans, ar);
+  // the bitset path keeps u32 HLL registers: accumulate them in scratch, narrow into the caller's u8 arrays
+  std::vector<void *> accs(accs_dev, accs_dev + q.num_aggregations);
+  std::vector<DeviceBuffer> hll_tmp(q.num_aggregations);
+  for (int a = 0; a < q.num_aggregations; a++)
+    if (ga.acc_kind[a] == 4) {
+      hll_tmp[a].alloc((size_t)ks.G * 1024 + 16);
+      accs[a] = hll_tmp[a].get();
+    }
   PINOT_HIP(hipEventRecord(e.ev_start, e.stream));
   auto *counts = reinterpret_cast<unsigned long long *>(counts_dev);
-  init_accs(e, ks.G, counts, ga, accs_dev);
+  init_accs(e, ks.G, counts, ga, accs.data());
   Timer t(e);
   std::vector<int64_t> seg_counts;
-  accumulate_groups(e, plans, qs, q, ga, ks, counts, accs_dev, t, seg_counts, false);
+  accumulate_groups(e, plans, qs, q, ga, ks, counts, accs.data(), t, seg_counts, false);
+  for (int a = 0; a < q.num_aggregations; a++)
+    if (ga.acc_kind[a] == 4)
+      launch_narrow_u32(hll_tmp[a].get<uint32_t>(), ks.G * 256, static_cast<uint8_t *>(accs_dev[a]), e.stream);
+  PINOT_HIP(hipGetLastError());
   PINOT_HIP(hipEventRecord(e.ev_stop, e.stream));
   PINOT_HIP(hipStreamSynchronize(e.stream));
   float ms = 0;
@@ -2136,10 +2154,17 @@ std::unique_ptr<GroupByResult> exec_group_by_finalize(Engine &e, const std::vect
   GroupByProgram gp{};
   gp.n_aggs = q.num_aggregations;
   gp.counts = reinterpret_cast<unsigned long long *>(const_cast<int64_t *>(counts_dev));
+  std::vector<DeviceBuffer> hll_tmp(q.num_aggregations);  // u8 partial registers -> the u32 layout finalize reads
   for (int a = 0; a < q.num_aggregations; a++) {
     gp.acc[a] = accs_dev ? accs_dev[a] : nullptr;
     gp.acc_kind[a] = ga.acc_kind[a];
+    if (ga.acc_kind[a] == 4 && gp.acc[a]) {
+      hll_tmp[a].alloc((size_t)ks.G * 1024 + 16);
+      launch_widen_u8(static_cast<const uint8_t *>(gp.acc[a]), ks.G * 256, hll_tmp[a].get<int32_t>(), e.stream);
+      gp.acc[a] = hll_tmp[a].get();
+    }
   }
+  PINOT_HIP(hipGetLastError());
   return finalize_groups(e, q, ga, ks, gp);
 }
 

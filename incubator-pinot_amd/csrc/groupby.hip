@@ -352,7 +352,7 @@ __global__ void k_gather_hll(const uint8_t *__restrict__ regs, const long long *
 }
 
 __global__ void k_widen_u8(const uint8_t *__restrict__ in, long long n4, int32_t *__restrict__ out) {
-  // multi-GPU partial layout: u8 HLL registers -> int32 (4 registers per thread, one 16-B store)
+  // u8 HLL registers (fused sinks, multi-GPU partial layout) -> u32 (4 registers per thread, one 16-B store)
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
     const uint32_t w = reinterpret_cast<const uint32_t *>(in)[i];
     u32x4 o;
@@ -364,7 +364,21 @@ __global__ void k_widen_u8(const uint8_t *__restrict__ in, long long n4, int32_t
   }
 }
 
+__global__ void k_narrow_u32(const uint32_t *__restrict__ in, long long n4, uint8_t *__restrict__ out) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    const u32x4 v = reinterpret_cast<const u32x4 *>(in)[i];  // registers are <= 64: no clamping
+    reinterpret_cast<uint32_t *>(out)[i] = v.x | (v.y << 8) | (v.z << 16) | (v.w << 24);
+  }
+}
+
 }  // namespace
+
+void launch_narrow_u32(const uint32_t *in, long long n, uint8_t *out, hipStream_t stream) {
+  if (n <= 0) return;
+  const long long n4 = n / 4;
+  const int grid = (int)std::min<long long>((n4 + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_narrow_u32, dim3(grid), dim3(256), 0, stream, in, n4, out);
+}
 
 void launch_widen_u8(const uint8_t *in, long long n, int32_t *out, hipStream_t stream) {
   if (n <= 0) return;

@@ -284,8 +284,9 @@ void launch_partition_starts(const uint32_t *offsets, const uint32_t *hist, int3
 void launch_hash_tuples(const GroupArgs &a, const long long *slots, long long n, int32_t *ids, hipStream_t stream);
 // HLL registers of the listed keys: out[i * 256 + r] = regs[keys[i] * 256 + r].
 void launch_gather_hll(const uint8_t *regs, const long long *keys, long long n, uint8_t *out, hipStream_t stream);
-// out[i] = in[i] for n u8 registers (n % 4 == 0): u8 HLL accumulators -> the int32 multi-GPU partial layout
+// out[i] = in[i] for n HLL registers (n % 4 == 0): the u8 multi-GPU partial layout <-> the bitset path's u32
 void launch_widen_u8(const uint8_t *in, long long n, int32_t *out, hipStream_t stream);
+void launch_narrow_u32(const uint32_t *in, long long n, uint8_t *out, hipStream_t stream);
 
 // Device finalize of dense accumulators: ordered list of the non-empty keys (flags + exclusive scan +
 // scatter; `scratch` holds 4 * (G + 1) bytes + the scan's temporary storage) and per-group outputs.

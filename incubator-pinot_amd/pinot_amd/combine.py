@@ -115,7 +115,7 @@ def allreduce_group_partials(acc_kinds, counts, accs, group=None):
 
     counts: int64[G]; accs[f] per acc_kinds[f]: int64[G] sums (kind 0), float64[G] sums (kind 1),
     int64[G] holding uint64 order-preserving encodings of doubles (kinds 2 = MIN, 3 = MAX; unsigned
-    order is made signed by flipping the top bit around the collective), int32[G*256] HLL registers
+    order is made signed by flipping the top bit around the collective), uint8[G*256] HLL registers
     (kind 4), None (kind 5: COUNT reads `counts`)."""
     dist = _dist()
     dist.all_reduce(counts, op=dist.ReduceOp.SUM, group=group)
@@ -157,7 +157,7 @@ def distributed_group_by(executor, query, segments, group=None, world=1, force_c
         elif k == ACC_F64_SUM:
             accs.append(torch.empty(G, dtype=torch.float64, device=dev))
         elif k == ACC_HLL:
-            accs.append(torch.empty(G * 256, dtype=torch.int32, device=dev))
+            accs.append(torch.empty(G * 256, dtype=torch.uint8, device=dev))
         else:
             accs.append(torch.empty(G, dtype=torch.int64, device=dev))
     ptrs = (C.c_void_p * max(len(kinds), 1))(*[(a.data_ptr() if a is not None else None) for a in accs])

@@ -60,8 +60,7 @@ def config4(args, eng, ex):
     abi = abi[args.warmup:]
     chk, _ = ex.process_query(ex.prepare(CONFIG4_CHECK), segs)
     n_groups = len(res)
-    tot_cnt = int(res.function_values(1)[0].sum())  # AVG(d8)'s per-group counts
-    n_groups = res.num_groups()
+    tot_cnt = sum(v[1].count for v in res.values())
     tot_sum = sum(v[0] for v in res.values())
     eng.set_config("timing=1")
     ex.process_query(q, segs, trim=False)

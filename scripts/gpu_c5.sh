@@ -13,3 +13,8 @@ cat "$OUT/config4.json"
 timeout -k 10 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 scripts/bench_workloads.py --workload config5 --steps 5 --warmup 2 > "$OUT/config5.json" 2> "$OUT/config5.err" || { echo "config5 failed"; tail -20 "$OUT/config5.err"; exit 1; }
 cat "$OUT/config5.json"
 echo done
+if [ "$2" = "prof" ]; then
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/c4prof" -o run -- python3 scripts/bench_workloads.py --workload config4 --steps 2 --warmup 1 > "$OUT/c4prof.log" 2>&1 || { echo "config4 rocprof failed"; exit 1; }
+  python3 scripts/prof_kernels.py "$OUT/c4prof/run_results.db" > "$OUT/config4_rocprof_kernels.txt"
+  head -20 "$OUT/config4_rocprof_kernels.txt"
+fi

@@ -83,7 +83,7 @@ def _dense(query, result_map):
             arrays.append(np.zeros(G, dtype=np.int64))
         else:
             kinds.append(4)
-            arrays.append(np.zeros(G * 256, dtype=np.int32))
+            arrays.append(np.zeros(G * 256, dtype=np.uint8))
     for key, vals in result_map.items():
         ids = [int(x) for x in key.split("\t")]
         k, stride = 0, 1

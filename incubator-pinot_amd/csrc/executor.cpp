@@ -1575,7 +1575,9 @@ bool needs_admission(const std::vector<SegmentData *> &segs, const pinot_query &
 
 // Fused group-by: ONE k_group_query launch (or COUNT / EMIT / reduce for the partitioned plan) over all
 // segments, device compaction of the non-empty keys, device per-group outputs, one D2H of the arrays.
-// Multi-GPU partial output (pinot_gpu_group_by_partial): the caller's dense arrays in the partial layout.
+// Multi-GPU partial arrays in the partial layout: `po` = write them (pinot_gpu_group_by_partial, the kernels
+// stop before compaction), `pin` = finalize from them (pinot_gpu_group_by_finalize, no kernels: the same
+// device compaction / outputs / lazy HLL registers as a one-GPU group-by).
 struct PartialOut {
   int64_t *counts;
   void *const *accs;
@@ -1583,7 +1585,8 @@ struct PartialOut {
 
 std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q,
                                                    const KeySpace &ks_in, const GroupAccs &ga, pinot_exec_stats *stats,
-                                                   int attempt = 0, const PartialOut *po = nullptr) {
+                                                   int attempt = 0, const PartialOut *po = nullptr,
+                                                   const PartialOut *pin = nullptr) {
   const auto tg0 = std::chrono::steady_clock::now();
   const int na = q.num_aggregations;
   const size_t S = segs.size();
@@ -1661,6 +1664,10 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     }
     for (int a = 0; a < na; a++)
       if (alias[a] >= 0) accs[a] = accs[alias[a]];
+  }
+  if (pin) {  // merged partials: u64 counts, 8-byte accumulators and u8 HLL registers, as the fused sinks write them
+    counts = reinterpret_cast<unsigned long long *>(pin->counts);
+    for (int a = 0; a < na; a++) accs[a] = pin->accs[a];
   }
 
   const auto tgc = std::chrono::steady_clock::now();
@@ -1777,11 +1784,12 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
   PINOT_HIP(hipEventRecord(e.ev_start, e.stream));
   upload_arena(e, ar);
   Timer t(e);
-  for (size_t si = 0; si < S; si++)
+  for (size_t si = 0; si < S && !pin; si++)
     if (plans[si].has_pre && !plans[si].empty) run_filter(e, plans[si], qs, t, (int64_t)si);
   PINOT_HIP(hipMemsetAsync(matched, 0, S * 8, e.stream));
   const auto tgu = std::chrono::steady_clock::now();
-  if (gp.mode != GB_EMIT) {  // identities: counts / sums 0, min all-ones, max 0, HLL 0
+  if (pin) {
+  } else if (gp.mode != GB_EMIT) {  // identities: counts / sums 0, min all-ones, max 0, HLL 0
     PINOT_HIP(hipMemsetAsync(counts, 0, ks.G * 8, e.stream));
     for (int i = 0; i < na; i++)
       if (acc_bytes[i]) PINOT_HIP(hipMemsetAsync(accs[i], gx.acc_kind[i] == 2 ? 0xFF : 0, ks.G * acc_bytes[i], e.stream));
@@ -2151,6 +2159,11 @@ std::unique_ptr<GroupByResult> exec_group_by_finalize(Engine &e, const std::vect
   KeySpace ks = build_key_space(segs, q);
   require(!ks.hashed, PINOT_ERR_UNSUPPORTED, "partial group-by needs a dense key space");
   GroupAccs ga = group_acc_kinds(*segs[0], q);
+  if (e.use_fused) {
+    const PartialOut pin{const_cast<int64_t *>(counts_dev), accs_dev};
+    pinot_exec_stats st{};
+    return exec_group_by_fused(e, segs, q, ks, ga, &st, 0, nullptr, &pin);
+  }
   GroupByProgram gp{};
   gp.n_aggs = q.num_aggregations;
   gp.counts = reinterpret_cast<unsigned long long *>(const_cast<int64_t *>(counts_dev));

@@ -161,6 +161,10 @@ void exec_aggregate(Engine &e, const std::vector<SegmentData *> &segs, const pin
                     pinot_exec_stats *stats);
 
 struct GroupByResult {
+  GroupByResult() = default;
+  GroupByResult(GroupByResult &&) = default;
+  GroupByResult &operator=(GroupByResult &&) = default;
+  ~GroupByResult();  // returns its large result arrays to a process-wide pool (no page faults on the next query)
   std::vector<int64_t> raw_keys;              // ascending raw keys (mixed radix over global ids, column 0 least significant)
   int32_t num_columns = 0;
   std::vector<int> functions;

@@ -1409,6 +1409,46 @@ void init_accs(Engine &e, int64_t G, unsigned long long *counts, const GroupAccs
 
 }  // namespace
 
+// Result-array pool: a 1 M-group result is ~48 MB of fresh host pages, and first-touching them cost more than
+// filling them. Released results hand their arrays back; the next large result takes them (capacity kept).
+namespace {
+struct ResultPool {
+  std::mutex mu;
+  std::vector<std::vector<int64_t>> i64;
+  std::vector<std::vector<double>> f64;
+};
+ResultPool &result_pool() {
+  static ResultPool *p = new ResultPool;  // never destroyed: results may be released during interpreter exit
+  return *p;
+}
+template <class T>
+std::vector<T> take_pooled(std::vector<std::vector<T>> &pool, size_t n) {
+  for (size_t i = 0; i < pool.size(); i++)
+    if (pool[i].capacity() >= n) {
+      std::vector<T> v = std::move(pool[i]);
+      pool.erase(pool.begin() + i);
+      return v;
+    }
+  return {};
+}
+constexpr size_t kPoolMinElems = 1u << 16, kPoolMaxArrays = 16;
+}  // namespace
+
+GroupByResult::~GroupByResult() {
+  ResultPool &p = result_pool();
+  std::lock_guard<std::mutex> lk(p.mu);
+  auto put = [](auto &pool, auto &v) {
+    if (v.capacity() >= kPoolMinElems && pool.size() < kPoolMaxArrays) {
+      v.clear();
+      pool.push_back(std::move(v));
+    }
+  };
+  put(p.i64, raw_keys);
+  for (auto &v : counts) put(p.i64, v);
+  for (auto &v : hll_card) put(p.i64, v);
+  for (auto &v : values) put(p.f64, v);
+}
+
 // DictionaryBasedGroupKeyGenerator.getGroupKey (:421-437): column 0 first, values '\t'-joined.
 const std::string &GroupByResult::key(int64_t g) const {
   if (keys.size() != raw_keys.size()) {
@@ -1966,6 +2006,16 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     for (int i = 0, h = 0; i < na; i++)
       if (gx.acc_kind[i] == 4) hidx[i] = h++;
     // result arrays: sized (first touch of fresh pages) and filled in parallel over the host's cores
+    if (n >= kPoolMinElems) {  // recycled arrays of released results: already-mapped pages
+      ResultPool &rp = result_pool();
+      std::lock_guard<std::mutex> lk(rp.mu);
+      res->raw_keys = take_pooled(rp.i64, n);
+      res->counts[0] = take_pooled(rp.i64, n);
+      for (int i = 0; i < na; i++) {
+        res->values[i] = take_pooled(rp.f64, n);
+        if (ga.acc_kind[i] == 4) res->hll_card[i] = take_pooled(rp.i64, n);
+      }
+    }
     std::vector<std::function<void()>> sizing;
     sizing.push_back([&] { res->raw_keys.resize(n); });
     res->counts_shared = true;  // every aggregation counts the same docs per group

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PINOT_GPU_ABI_VERSION 2
+#define PINOT_GPU_ABI_VERSION 3
 
 /* ------------------------------------------------------------------ status */
 typedef enum {
@@ -42,7 +42,10 @@ typedef enum {
   PINOT_ERR_OOM = 2,          /* HBM allocation failed: caller falls back to the CPU operator */
   PINOT_ERR_DEVICE = 3,       /* HIP runtime / kernel error */
   PINOT_ERR_UNSUPPORTED = 4,  /* query shape not handled on the GPU: caller falls back */
-  PINOT_ERR_BAD_QUERY = 5     /* bad literal, unknown column (BadQueryRequestException) */
+  PINOT_ERR_BAD_QUERY = 5,    /* bad literal, unknown column (BadQueryRequestException) */
+  PINOT_ERR_TIMEOUT = 6       /* query budget exhausted: QUERY_SCHEDULING_TIMEOUT_ERROR when it was spent before
+                                 the call (ServerQueryExecutorV1Impl.java:116-126), else the combine timeout
+                                 (CombineGroupByOperator.java:174-181); device work already queued still drains */
 } pinot_status;
 
 /* ------------------------------------------------------------------ segment */
@@ -114,6 +117,9 @@ typedef struct {
   const char *const *group_by;
   int32_t num_groups_limit;    /* num.groups.limit, default 100000 (InstancePlanMakerImplV2.java:55-58) */
   int32_t max_init_group_holder_capacity; /* array-holder threshold, default 10000 */
+  int32_t timeout_ms;          /* remaining query budget = table timeout - scheduling wait
+                                  (ServerQueryExecutorV1Impl.java:113-114); 0 = none, < 0 = already spent */
+  int32_t reserved;
 } pinot_query;
 
 /* Per-query statistics (ExecutionStatistics.java:35-43). num_entries_scanned_in_filter
@@ -191,6 +197,18 @@ pinot_status pinot_groupby_values(const pinot_groupby_result *r, int32_t fn, int
 pinot_status pinot_groupby_hll(const pinot_groupby_result *r, int32_t fn, uint8_t *registers, int64_t *cardinalities);
 /* Raw dense keys in the query's global key space (column 0 least significant). */
 pinot_status pinot_groupby_raw_keys(const pinot_groupby_result *r, int64_t *keys);
+/* Every group key string in one call (what a JNI caller copies into one byte[] + int[] pair): group g's bytes
+   are buf[offsets[g], offsets[g + 1]) (no terminator); offsets has num_groups + 1 entries. buf == NULL (or too
+   short) only sets *bytes_needed. */
+pinot_status pinot_groupby_export_keys(const pinot_groupby_result *r, char *buf, uint64_t buf_len, int64_t *offsets,
+                                       uint64_t *bytes_needed);
+/* AggregationGroupByTrimmingService.trimIntermediateResultsMap (:71-116) for function fn: the groups of fn's
+   trimmed map, ascending group index. trimSize = max(5 * top_n, 5000); trimming happens only above
+   4 * trimSize groups, keeping the trimSize best final values (MIN ascending, every other function descending,
+   :160-176; ties: lower raw key first, where the reference's heap order is arbitrary). groups == NULL only sets
+   *num_out. */
+pinot_status pinot_groupby_trim(const pinot_groupby_result *r, int32_t top_n, int32_t fn, int64_t *groups,
+                                int64_t *num_out);
 void pinot_groupby_free(pinot_groupby_result *r);
 
 /* ------------------------------------------------------------------ multi-GPU partials

@@ -228,6 +228,7 @@ pinot_status pinot_gpu_aggregate(pinot_engine *engine, const pinot_segment_handl
     const auto t0 = std::chrono::steady_clock::now();
     std::lock_guard<std::mutex> lk(engine->mu);
     set_device(*engine);
+    DeadlineScope ds(*engine, query->timeout_ms);
     exec_aggregate(*engine, resolve(*engine, segments, num_segments), *query, out, stats);
     if (stats) stats->host_ms = elapsed_ms(t0);
   });
@@ -242,6 +243,7 @@ pinot_status pinot_gpu_group_by(pinot_engine *engine, const pinot_segment_handle
     const auto t0 = std::chrono::steady_clock::now();
     std::lock_guard<std::mutex> lk(engine->mu);
     set_device(*engine);
+    DeadlineScope ds(*engine, query->timeout_ms);
     auto r = exec_group_by(*engine, resolve(*engine, segments, num_segments), *query, stats);
     if (stats) stats->host_ms = elapsed_ms(t0);
     auto *res = new pinot_groupby_result();
@@ -288,6 +290,26 @@ pinot_status pinot_groupby_raw_keys(const pinot_groupby_result *r, int64_t *keys
   return guard([&] {
     require(r && keys, PINOT_ERR_BAD_ARG, "null argument");
     if (!r->raw_keys.empty()) memcpy(keys, r->raw_keys.data(), r->raw_keys.size() * 8);
+  });
+}
+
+pinot_status pinot_groupby_export_keys(const pinot_groupby_result *r, char *buf, uint64_t buf_len, int64_t *offsets,
+                                       uint64_t *bytes_needed) {
+  return guard([&] {
+    require(r != nullptr, PINOT_ERR_BAD_ARG, "null result");
+    const uint64_t need = r->export_keys(buf, buf_len, offsets);
+    if (bytes_needed) *bytes_needed = need;
+  });
+}
+
+pinot_status pinot_groupby_trim(const pinot_groupby_result *r, int32_t top_n, int32_t fn, int64_t *groups,
+                                int64_t *num_out) {
+  return guard([&] {
+    require(r && num_out && fn >= 0 && fn < (int32_t)r->functions.size(), PINOT_ERR_BAD_ARG, "function index");
+    require(top_n > 0, PINOT_ERR_BAD_ARG, "top_n must be positive (AggregationGroupByTrimmingService.java:52)");
+    const std::vector<int64_t> kept = r->trim(top_n, fn);
+    *num_out = (int64_t)kept.size();
+    if (groups && !kept.empty()) memcpy(groups, kept.data(), kept.size() * 8);
   });
 }
 

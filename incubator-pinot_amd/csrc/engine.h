@@ -1,5 +1,6 @@
 // Host-side engine: device-resident segments, query planning, execution.
 #pragma once
+#include <chrono>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -137,6 +138,7 @@ struct Engine {
   PinnedBuffer group_host;     // their pinned host copy
   std::vector<std::shared_ptr<DeviceBuffer>> hll_pool;  // gathered HLL registers, reused once results are released
   DeviceBuffer group_hash;     // hashed key spaces: fingerprint table + representative docs
+  DeviceBuffer group_admit;    // num.groups.limit admission: first docs [S][G], admitted bitmaps [S][G/32], sort scratch
   PinnedBuffer host_arena;    // staging of the per-query arena (H2D)
   std::vector<uint8_t> arena_shadow;  // bytes last copied into `small` (upload_arena skips identical programs)
   uint64_t arena_dev_gen = 0;
@@ -144,6 +146,10 @@ struct Engine {
   PinnedBuffer host_result;   // staging of the reduced results (D2H)
   DeviceBuffer fused_ctl;     // k_scan_query: u32 arrival counter + [kMaxHll][256] HLL registers, kept zeroed
   MappedBuffer fused_result;  // k_scan_query's last block writes the reduced per-segment slots + HLL here
+
+  // per-call query budget (pinot_query.timeout_ms): waits on the stream give up at the deadline
+  bool has_deadline = false;
+  std::chrono::steady_clock::time_point deadline;
 
   // timing
   hipEvent_t ev_start = nullptr, ev_stop = nullptr;
@@ -153,6 +159,14 @@ struct Engine {
 
   ~Engine();
   SegmentData &seg(int64_t h);
+};
+
+// Deadline of a query call (ServerQueryExecutorV1Impl.java:113-126: remaining = timeout - scheduling wait).
+void check_deadline(const Engine &e, const char *phase);
+struct DeadlineScope {
+  Engine &e;
+  DeadlineScope(Engine &en, int32_t timeout_ms);
+  ~DeadlineScope() { e.has_deadline = false; }
 };
 
 // execution entry points (executor.cpp)
@@ -178,6 +192,11 @@ struct GroupByResult {
   mutable std::vector<std::string> keys;
   mutable std::vector<uint8_t> key_built;
   const std::string &key(int64_t g) const;
+  // all key strings back to back (offsets[n + 1]); built in parallel on first use
+  mutable std::vector<int64_t> key_offsets;
+  uint64_t export_keys(char *buf, uint64_t buf_len, int64_t *offsets) const;
+  // AggregationGroupByTrimmingService: the groups of function fn's trimmed map (ascending)
+  std::vector<int64_t> trim(int32_t top_n, int32_t fn) const;
   // DISTINCTCOUNTHLL: cardinalities per fn; registers on the host (hll[fn]) or on the device
   // (hll_dev + hll_dev_off[fn], [groups][256] u8, copied on request)
   std::vector<std::vector<int64_t>> hll_card;

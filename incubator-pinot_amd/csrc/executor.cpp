@@ -30,6 +30,17 @@
 
 namespace pinot {
 
+void check_deadline(const Engine &e, const char *phase) {
+  if (e.has_deadline && std::chrono::steady_clock::now() >= e.deadline)
+    throw Error(PINOT_ERR_TIMEOUT, std::string("query timed out during ") + phase);
+}
+
+DeadlineScope::DeadlineScope(Engine &en, int32_t timeout_ms) : e(en) {
+  require(timeout_ms >= 0, PINOT_ERR_TIMEOUT, "query budget already spent before execution (scheduling wait >= timeout)");
+  e.has_deadline = timeout_ms > 0;
+  if (timeout_ms > 0) e.deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms);
+}
+
 namespace {
 
 struct Arena {
@@ -316,14 +327,19 @@ QueryScratch prepare_scratch(Engine &e, const std::vector<SegPlan> &plans, const
 }
 
 // Waits for the engine stream: hipStreamSynchronize, or a busy poll (sync.poll=1) that avoids the
-// runtime's sleep/wake-up latency on short queries.
+// runtime's sleep/wake-up latency on short queries. Under a query deadline the poll gives up at the deadline
+// (PINOT_ERR_TIMEOUT; the queued device work still drains in stream order before the engine's next call).
 void wait_stream(Engine &e) {
-  if (!e.sync_poll) {
-    PINOT_HIP(hipStreamSynchronize(e.stream));
+  if (!e.sync_poll && !e.has_deadline) {
+    wait_stream(e);
     return;
   }
   hipError_t st;
   while ((st = hipStreamQuery(e.stream)) == hipErrorNotReady) {
+    if (e.has_deadline) {
+      check_deadline(e, "device execution");
+      std::this_thread::yield();
+    }
   }
   PINOT_HIP(st);
 }
@@ -490,7 +506,7 @@ void exec_filter(Engine &e, SegmentData &s, const FilterTreeInput *tree, uint64_
       }
     }
     if (count) *count = plans[0].empty ? 0 : s.num_docs;
-    PINOT_HIP(hipStreamSynchronize(e.stream));
+    wait_stream(e);
     return;
   }
   const int grid = scan_grid(nwords);
@@ -508,7 +524,7 @@ void exec_filter(Engine &e, SegmentData &s, const FilterTreeInput *tree, uint64_
   PINOT_HIP(hipMemcpyAsync(&hc, ra.out, 8, hipMemcpyDeviceToHost, e.stream));
   if (bitset_out && nwords)
     PINOT_HIP(hipMemcpyAsync(bitset_out, bits, nwords * 8, hipMemcpyDeviceToHost, e.stream));
-  PINOT_HIP(hipStreamSynchronize(e.stream));
+  wait_stream(e);
   t.collect();
   if (count) *count = (int64_t)hc;
 }
@@ -822,6 +838,7 @@ void aggregate_fused(Engine &e, const std::vector<SegmentData *> &segs, const pi
   }
 
   const auto tp0 = std::chrono::steady_clock::now();
+  check_deadline(e, "planning");
   PINOT_HIP(hipEventRecord(e.ev_start, e.stream));
   upload_arena(e, ar);
   Timer t(e);
@@ -1021,7 +1038,7 @@ void exec_aggregate(Engine &e, const std::vector<SegmentData *> &segs, const pin
   e.host_result.reserve(red_bytes);
   uint8_t *host = e.host_result.get<uint8_t>();
   PINOT_HIP(hipMemcpyAsync(host, red, red_bytes, hipMemcpyDeviceToHost, e.stream));
-  PINOT_HIP(hipStreamSynchronize(e.stream));
+  wait_stream(e);
   float ms = 0;
   PINOT_HIP(hipEventElapsedTime(&ms, e.ev_start, e.ev_stop));
   t.collect();
@@ -1152,6 +1169,24 @@ KeySpace build_key_space(const std::vector<SegmentData *> &segs, const pinot_que
   return ks;
 }
 
+struct AdmissionPlan {
+  bool active = false;           // some segment's holder or the inter-segment cap can drop keys
+  bool cap_active = false;       // the 2 x limit inter-segment cap can bind
+  std::vector<int64_t> upper;    // per segment: keys its holder admits (>= G: every present key)
+  int64_t cap = 0;
+};
+struct AdmissionBuffers {
+  uint32_t *first_doc = nullptr;  // [S][G]
+  uint32_t *bitmaps = nullptr;    // [S][words]
+  int64_t words = 0;
+  void *scratch = nullptr;
+  size_t scratch_bytes = 0;
+};
+
+AdmissionPlan plan_admission(const std::vector<SegmentData *> &segs, const pinot_query &q, const Engine &e, int64_t G);
+AdmissionBuffers admission_buffers(Engine &e, size_t S, int64_t G);
+void build_admitted(Engine &e, const AdmissionPlan &ap, size_t S, int64_t G, const AdmissionBuffers &ab);
+
 struct GroupAccs {
   std::vector<int> acc_kind;    // per agg
   std::vector<size_t> acc_bytes_per_key;
@@ -1250,7 +1285,7 @@ std::unique_ptr<GroupByResult> finalize_groups(Engine &e, const pinot_query &q, 
   PINOT_HIP(hipGetLastError());
   unsigned long long n = 0;
   PINOT_HIP(hipMemcpyAsync(&n, n_dev, 8, hipMemcpyDeviceToHost, e.stream));
-  PINOT_HIP(hipStreamSynchronize(e.stream));
+  wait_stream(e);
   int n_hll = 0;
   for (int a = 0; a < na; a++) n_hll += ga.acc_kind[a] == 4;
   auto res = std::make_unique<GroupByResult>();
@@ -1276,7 +1311,7 @@ std::unique_ptr<GroupByResult> finalize_groups(Engine &e, const pinot_query &q, 
   launch_gather_groups(gp, keys_dev, (int64_t)n, o_cnt, o_acc, o_hll, e.stream);
   PINOT_HIP(hipGetLastError());
   PINOT_HIP(hipMemcpyAsync(e.group_host.get(), e.group_out.get(), out_b, hipMemcpyDeviceToHost, e.stream));
-  PINOT_HIP(hipStreamSynchronize(e.stream));
+  wait_stream(e);
   const auto *hkeys = e.group_host.get<long long>();
   const auto *hcnt = reinterpret_cast<const unsigned long long *>(hkeys + n);
   const auto *hacc = hcnt + n;
@@ -1337,7 +1372,7 @@ int64_t count_docs(Engine &e, const uint64_t *bits, const SegmentData &s) {
   launch_reduce_slots(ra, 1, e.stream);
   unsigned long long c = 0;
   PINOT_HIP(hipMemcpyAsync(&c, p + grid, 8, hipMemcpyDeviceToHost, e.stream));
-  PINOT_HIP(hipStreamSynchronize(e.stream));
+  wait_stream(e);
   return (int64_t)c;
 }
 
@@ -1355,10 +1390,25 @@ void accumulate_groups(Engine &e, std::vector<SegPlan> &plans, const QueryScratc
       PINOT_HIP(hipMemcpyAsync(remaps[si * q.num_group_by + j].get(), m.data(), m.size() * 4, hipMemcpyHostToDevice,
                                e.stream));
     }
-  const int64_t limit = q.num_groups_limit > 0 ? q.num_groups_limit : e.num_groups_limit;
-  const int64_t array_threshold = q.max_init_group_holder_capacity > 0 ? q.max_init_group_holder_capacity : 10000;
-  DeviceBuffer first_doc, admitted;
   seg_counts.assign(S, 0);
+  std::vector<SegmentData *> sv(S);
+  for (size_t si = 0; si < S; si++) sv[si] = plans[si].seg;
+  // num.groups.limit (per segment and the inter-segment cap): first doc per key of every segment, admitted bitmaps
+  const AdmissionPlan ap = apply_limit ? plan_admission(sv, q, e, ks.G) : AdmissionPlan{};
+  AdmissionBuffers ab;
+  if (ap.active) {
+    ab = admission_buffers(e, S, ks.G);
+    PINOT_HIP(hipMemsetAsync(ab.first_doc, 0xFF, (size_t)S * ks.G * 4, e.stream));
+    for (size_t si = 0; si < S; si++) {
+      SegPlan &p = plans[si];
+      if (p.empty) continue;
+      const uint64_t *bits = run_filter(e, p, qs, t);
+      GroupByProgram gp = make_group_program(e, *p.seg, q, ga, ks, si, remaps, counts, accs);
+      launch_first_doc(gp, bits, p.seg->nwords(), p.seg->num_docs, ab.first_doc + si * ks.G, e.stream);
+      PINOT_HIP(hipGetLastError());
+    }
+    build_admitted(e, ap, S, ks.G, ab);
+  }
   for (size_t si = 0; si < S; si++) {
     SegPlan &p = plans[si];
     SegmentData &s = *p.seg;
@@ -1366,36 +1416,9 @@ void accumulate_groups(Engine &e, std::vector<SegPlan> &plans, const QueryScratc
     const uint64_t *bits = run_filter(e, p, qs, t);
     seg_counts[si] = count_docs(e, bits, s);
     GroupByProgram gp = make_group_program(e, s, q, ga, ks, si, remaps, counts, accs);
-    // DictionaryBasedGroupKeyGenerator holder choice on THIS segment's cardinalities (:79-126)
-    __int128 product = 1;
-    for (int j = 0; j < q.num_group_by; j++) product *= s.column(q.group_by[j])->card;
-    int64_t upper = product > array_threshold ? limit : INT64_MAX;
-    if (product <= INT32_MAX && product > array_threshold) upper = std::min<int64_t>((int64_t)product, limit);
-    if (apply_limit && product > array_threshold && product > upper && seg_counts[si] > upper) {
-      // first-appearance order: keep the `upper` keys with the smallest first docId (IntMapBasedHolder :293-302)
-      first_doc.reserve(ks.G * 4);
-      PINOT_HIP(hipMemsetAsync(first_doc.get(), 0xFF, ks.G * 4, e.stream));
-      launch_first_doc(gp, bits, s.nwords(), s.num_docs, first_doc.get<uint32_t>(), e.stream);
-      std::vector<uint32_t> fd(ks.G);
-      PINOT_HIP(hipMemcpyAsync(fd.data(), first_doc.get(), ks.G * 4, hipMemcpyDeviceToHost, e.stream));
-      PINOT_HIP(hipStreamSynchronize(e.stream));
-      std::vector<std::pair<uint32_t, int64_t>> present;
-      for (int64_t k = 0; k < ks.G; k++)
-        if (fd[k] != 0xFFFFFFFFu) present.push_back({fd[k], k});
-      if ((int64_t)present.size() > upper) {
-        std::nth_element(present.begin(), present.begin() + upper, present.end());
-        present.resize(upper);
-      }
-      std::vector<uint32_t> bm((ks.G + 31) / 32 + 1, 0);
-      for (auto &pk : present) bm[pk.second >> 5] |= 1u << (pk.second & 31);
-      admitted.alloc(bm.size() * 4);
-      PINOT_HIP(hipMemcpyAsync(admitted.get(), bm.data(), bm.size() * 4, hipMemcpyHostToDevice, e.stream));
-      gp.admitted = admitted.get<uint32_t>();
-      PINOT_HIP(hipStreamSynchronize(e.stream));
-    }
+    if (ap.active) gp.admitted = ab.bitmaps + si * ab.words;
     t.timed(1, [&] { launch_group_by(gp, bits, s.nwords(), s.num_docs, e.stream); });
     PINOT_HIP(hipGetLastError());
-    if (gp.admitted) PINOT_HIP(hipStreamSynchronize(e.stream));
   }
 }
 
@@ -1472,6 +1495,99 @@ const std::string &GroupByResult::key(int64_t g) const {
     key_built[g] = 1;
   }
   return keys[g];
+}
+
+namespace {
+void parallel_tasks(size_t n, const std::function<void(size_t)> &fn);
+}
+
+// Bulk key export: lengths of every key (mixed-radix digits -> dictionary strings), a prefix sum, then the
+// bytes, each pass split over 8 threads for large results.
+uint64_t GroupByResult::export_keys(char *buf, uint64_t buf_len, int64_t *offsets) const {
+  const int64_t n = (int64_t)raw_keys.size();
+  const size_t nc = gcard.size();
+  const size_t nt = n >= (1 << 16) ? 8 : 1;
+  auto digit = [&](int64_t g, size_t j, int64_t &k) -> const std::string & {
+    if (!key_ids.empty()) return gvalues[j][key_ids[g * nc + j]];
+    const std::string &v = gvalues[j][k % gcard[j]];
+    k /= gcard[j];
+    return v;
+  };
+  if ((int64_t)key_offsets.size() != n + 1) {
+    std::vector<int64_t> off(n + 1, 0);
+    std::vector<int64_t> part(nt + 1, 0);
+    parallel_tasks(nt, [&](size_t t) {
+      const int64_t lo = n * t / nt, hi = n * (t + 1) / nt;
+      int64_t acc = 0;
+      for (int64_t g = lo; g < hi; g++) {
+        int64_t k = raw_keys[g], len = (int64_t)nc - 1;
+        for (size_t j = 0; j < nc; j++) len += (int64_t)digit(g, j, k).size();
+        off[g + 1] = len;
+        acc += len;
+      }
+      part[t + 1] = acc;
+    });
+    for (size_t t = 0; t < nt; t++) part[t + 1] += part[t];
+    parallel_tasks(nt, [&](size_t t) {
+      const int64_t lo = n * t / nt, hi = n * (t + 1) / nt;
+      int64_t run = part[t];
+      for (int64_t g = lo; g < hi; g++) {
+        run += off[g + 1];
+        off[g + 1] = run;
+      }
+    });
+    key_offsets.swap(off);
+  }
+  const uint64_t need = (uint64_t)key_offsets[n];
+  if (offsets) memcpy(offsets, key_offsets.data(), (size_t)(n + 1) * 8);
+  if (!buf || buf_len < need) return need;
+  parallel_tasks(nt, [&](size_t t) {
+    const int64_t lo = n * t / nt, hi = n * (t + 1) / nt;
+    for (int64_t g = lo; g < hi; g++) {
+      char *p = buf + key_offsets[g];
+      int64_t k = raw_keys[g];
+      for (size_t j = 0; j < nc; j++) {
+        if (j) *p++ = '\t';
+        const std::string &v = digit(g, j, k);
+        memcpy(p, v.data(), v.size());
+        p += v.size();
+      }
+    }
+  });
+  return need;
+}
+
+// AggregationGroupByTrimmingService.trimIntermediateResultsMap (:71-116) for one function: above
+// 4 * max(5 * topN, 5000) groups, keep the trimSize best final values — ComparableSorter (COUNT / SUM / MIN / MAX /
+// AVG: the intermediate value; AvgPair compares sum / count) or NonComparableSorter (DISTINCTCOUNTHLL: the final
+// cardinality) — MIN ascending, every other function descending (getSorter :160-176). The reference's heap keeps
+// an arbitrary member of a tie at the boundary; here the lower raw key wins.
+std::vector<int64_t> GroupByResult::trim(int32_t top_n, int32_t fn) const {
+  const int64_t n = (int64_t)raw_keys.size();
+  const int64_t trim_size = std::max<int64_t>(5 * (int64_t)top_n, 5000);
+  std::vector<int64_t> idx(n);
+  std::iota(idx.begin(), idx.end(), 0);
+  if (n <= 4 * trim_size) return idx;
+  const int f = functions[fn];
+  const std::vector<int64_t> &cnt = counts[counts_shared ? 0 : fn];
+  std::vector<double> v(n);
+  for (int64_t g = 0; g < n; g++) {
+    switch (f) {
+      case PINOT_AGG_COUNT: v[g] = (double)cnt[g]; break;
+      case PINOT_AGG_AVG: v[g] = cnt[g] ? values[fn][g] / (double)cnt[g] : -INFINITY; break;
+      case PINOT_AGG_DISTINCTCOUNTHLL: v[g] = (double)hll_card[fn][g]; break;
+      default: v[g] = values[fn][g]; break;
+    }
+  }
+  const bool asc = f == PINOT_AGG_MIN;
+  auto better = [&](int64_t a, int64_t b) {
+    if (v[a] != v[b]) return asc ? v[a] < v[b] : v[a] > v[b];
+    return a < b;
+  };
+  std::nth_element(idx.begin(), idx.begin() + trim_size, idx.end(), better);
+  idx.resize(trim_size);
+  std::sort(idx.begin(), idx.end());
+  return idx;
 }
 
 std::unique_ptr<GroupByResult> exec_group_by_legacy(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q,
@@ -1597,18 +1713,105 @@ GroupPlan plan_group(const std::vector<SegmentData *> &segs, const pinot_query &
   return gp;
 }
 
-// Segments whose holder would apply the num.groups.limit first-appearance admission
-// (IntMapBasedHolder, DictionaryBasedGroupKeyGenerator.java:293-302): those queries stay on the
-// bitset path, which implements the rule.
-bool needs_admission(const std::vector<SegmentData *> &segs, const pinot_query &q, const Engine &e) {
+// num.groups.limit, per segment and across segments:
+//   * DictionaryBasedGroupKeyGenerator (:79-126): a segment whose cardinality product exceeds
+//     max.init.group.holder.capacity uses a map holder that gives group ids to the first
+//     upper = min(product, limit) distinct keys in doc order (product > INT_MAX: limit); later keys get
+//     INVALID_ID and are dropped (IntMapBasedHolder.getGroupId :293-302);
+//   * CombineGroupByOperator (:61,147): a key enters the merged map only while it holds < 2 x limit keys.
+// The reference merges segments on a thread pool, so which keys pass the inter-segment cap depends on timing;
+// here it is the caller's segment order, ascending raw keys within a segment (the oracle's order).
+AdmissionPlan plan_admission(const std::vector<SegmentData *> &segs, const pinot_query &q, const Engine &e, int64_t G) {
+  AdmissionPlan ap;
   const int64_t limit = q.num_groups_limit > 0 ? q.num_groups_limit : e.num_groups_limit;
   const int64_t threshold = q.max_init_group_holder_capacity > 0 ? q.max_init_group_holder_capacity : 10000;
+  int64_t possible = 0;
   for (auto *s : segs) {
     __int128 product = 1;
     for (int j = 0; j < q.num_group_by; j++) product *= s->column(q.group_by[j])->card;
-    if (product > threshold && product > limit && s->num_docs > limit) return true;
+    int64_t upper = INT64_MAX;
+    if (product > threshold) upper = product <= INT32_MAX ? std::min<int64_t>((int64_t)product, limit) : limit;
+    const int64_t reach = (int64_t)std::min<__int128>(std::min<__int128>(product, (__int128)s->num_docs), (__int128)G);
+    if (upper < reach) ap.active = true;
+    else upper = G;  // cannot bind: every present key
+    ap.upper.push_back(upper);
+    possible += std::min(upper, reach);
   }
-  return false;
+  ap.cap = 2 * limit;
+  if (std::min(possible, G) > ap.cap) ap.active = ap.cap_active = true;
+  return ap;
+}
+
+// CombineGroupByOperator's inter-segment cap over the per-segment admitted bitmaps (host, [S][words] u32): keys
+// enter in segment order, ascending within a segment, until `cap` distinct keys are in; every later new key is
+// dropped from the segment that brings it.
+void apply_inter_segment_cap(std::vector<uint32_t> &bm, size_t S, int64_t words, int64_t cap) {
+  std::vector<uint32_t> merged(words, 0u);
+  int64_t n = 0;
+  bool full = false;
+  for (size_t s = 0; s < S; s++) {
+    uint32_t *b = bm.data() + s * words;
+    for (int64_t w = 0; w < words; w++) {
+      const uint32_t fresh = b[w] & ~merged[w];
+      if (!fresh) continue;
+      uint32_t kept = 0;
+      if (!full) {
+        const int64_t pc = __builtin_popcount(fresh);
+        if (n + pc <= cap) {
+          kept = fresh;
+          n += pc;
+        } else {
+          uint32_t x = fresh;  // the lowest (cap - n) new keys of this word
+          for (int64_t r = cap - n; r > 0; r--) {
+            const uint32_t low = x & (0u - x);
+            kept |= low;
+            x ^= low;
+          }
+          n = cap;
+        }
+        if (n == cap) full = true;
+      }
+      merged[w] |= kept;
+      b[w] = (b[w] & ~fresh) | kept;
+    }
+  }
+}
+
+// first_doc [S][G] (GB_FIRST / k_first_doc) -> admitted bitmaps [S][words] on the device, with the inter-segment
+// cap applied on the host when it can bind. `buf` holds first docs, bitmaps and the sort scratch.
+void build_admitted(Engine &e, const AdmissionPlan &ap, size_t S, int64_t G, const AdmissionBuffers &ab) {
+  std::vector<long long> upper(ap.upper.begin(), ap.upper.end());
+  launch_admission_bitmaps(ab.first_doc, (int)S, G, upper.data(), ab.bitmaps, ab.words, ab.scratch, ab.scratch_bytes,
+                           e.stream);
+  PINOT_HIP(hipGetLastError());
+  if (!ap.cap_active) return;
+  std::vector<uint32_t> bm(S * ab.words);
+  PINOT_HIP(hipMemcpyAsync(bm.data(), ab.bitmaps, bm.size() * 4, hipMemcpyDeviceToHost, e.stream));
+  wait_stream(e);
+  apply_inter_segment_cap(bm, S, ab.words, ap.cap);
+  e.host_arena.reserve(bm.size() * 4);  // pinned staging; the query arena is already on the device
+  memcpy(e.host_arena.get(), bm.data(), bm.size() * 4);
+  PINOT_HIP(hipMemcpyAsync(ab.bitmaps, e.host_arena.get(), bm.size() * 4, hipMemcpyHostToDevice, e.stream));
+  wait_stream(e);  // host_arena is the staging of the next query's arena
+}
+
+AdmissionBuffers admission_buffers(Engine &e, size_t S, int64_t G) {
+  AdmissionBuffers ab;
+  ab.words = (G + 31) / 32 + 1;
+  const size_t fd_b = ((size_t)S * G * 4 + 255) / 256 * 256, bm_b = ((size_t)S * ab.words * 4 + 255) / 256 * 256;
+  ab.scratch_bytes = admission_scratch_bytes(G);
+  const size_t need = fd_b + bm_b + ab.scratch_bytes;
+  if (need > e.group_admit.size()) {
+    size_t free_b = 0, total_b = 0;
+    PINOT_HIP(hipMemGetInfo(&free_b, &total_b));
+    require((double)need < 0.5 * (double)free_b, PINOT_ERR_UNSUPPORTED,
+            "num.groups.limit admission state (first docs per segment and key) does not fit in HBM");
+  }
+  e.group_admit.reserve(need);
+  ab.first_doc = e.group_admit.get<uint32_t>();
+  ab.bitmaps = reinterpret_cast<uint32_t *>(e.group_admit.get<uint8_t>() + fd_b);
+  ab.scratch = e.group_admit.get<uint8_t>() + fd_b + bm_b;
+  return ab;
 }
 
 }  // namespace
@@ -1655,6 +1858,11 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
   }
   const GroupPlan gp = plan_group(segs, q, ks, gx, ks.hashed ? std::string("global") : e.group_mode, e.group_split,
                                     e.group_pshift);
+  // num.groups.limit: per-segment first-appearance admission and the inter-segment cap (plan_admission)
+  const AdmissionPlan adm = pin ? AdmissionPlan{} : plan_admission(segs, q, e, ks.G);
+  require(!(po && adm.active), PINOT_ERR_UNSUPPORTED,
+          "multi-GPU partials with num.groups.limit admission: use the engine's own multi-device group-by");
+  const AdmissionBuffers ab = adm.active ? admission_buffers(e, S, ks.G) : AdmissionBuffers{};
   Arena ar;
   std::unique_ptr<FilterTreeInput> tree;
   if (q.num_filter_nodes > 0) tree = std::make_unique<FilterTreeInput>(decode_filter(q.num_filter_nodes, q.filter));
@@ -1728,6 +1936,7 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     g.n_leaves = (int32_t)p.fused_leaves.size();
     g.first_gcol = (int32_t)gcols.size();
     g.first_agg = (int32_t)gaggs.size();
+    g.admitted = adm.active ? ab.bitmaps + si * ab.words : nullptr;
     std::tie(g.ch_begin, g.ch_end) = chunk_window(p, ar);
     for (const FilterStep &l : p.fused_leaves) {
       leaves.push_back(fused_leaf_step(s, l, qs.arena));
@@ -1821,23 +2030,33 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
   const int64_t nblk = (int64_t)S * a.bps;
 
   const auto tgp = std::chrono::steady_clock::now();
+  check_deadline(e, "planning");
   PINOT_HIP(hipEventRecord(e.ev_start, e.stream));
   upload_arena(e, ar);
   Timer t(e);
   for (size_t si = 0; si < S && !pin; si++)
     if (plans[si].has_pre && !plans[si].empty) run_filter(e, plans[si], qs, t, (int64_t)si);
   PINOT_HIP(hipMemsetAsync(matched, 0, S * 8, e.stream));
+  if (ks.hashed && !pin && (adm.active || gp.mode != GB_EMIT)) {  // before any pass inserts keys
+    PINOT_HIP(hipMemsetAsync(htable, 0, (size_t)hcap * 8, e.stream));
+    PINOT_HIP(hipMemsetAsync(reps, 0xFF, (size_t)hcap * 8, e.stream));
+    PINOT_HIP(hipMemsetAsync(a.verify_err, 0, 4, e.stream));
+  }
+  if (adm.active) {  // first matching doc per (segment, key) -> admitted bitmaps (+ inter-segment cap)
+    PINOT_HIP(hipMemsetAsync(ab.first_doc, 0xFF, (size_t)S * ks.G * 4, e.stream));
+    GroupArgs af = a;
+    af.mode = GB_FIRST;
+    af.first_doc = ab.first_doc;
+    launch_group_query(af, e.stream);
+    PINOT_HIP(hipGetLastError());
+    build_admitted(e, adm, S, ks.G, ab);
+  }
   const auto tgu = std::chrono::steady_clock::now();
   if (pin) {
   } else if (gp.mode != GB_EMIT) {  // identities: counts / sums 0, min all-ones, max 0, HLL 0
     PINOT_HIP(hipMemsetAsync(counts, 0, ks.G * 8, e.stream));
     for (int i = 0; i < na; i++)
       if (acc_bytes[i]) PINOT_HIP(hipMemsetAsync(accs[i], gx.acc_kind[i] == 2 ? 0xFF : 0, ks.G * acc_bytes[i], e.stream));
-    if (ks.hashed) {
-      PINOT_HIP(hipMemsetAsync(htable, 0, (size_t)hcap * 8, e.stream));
-      PINOT_HIP(hipMemsetAsync(reps, 0xFF, (size_t)hcap * 8, e.stream));
-      PINOT_HIP(hipMemsetAsync(a.verify_err, 0, 4, e.stream));
-    }
     t.timed(1, [&] { launch_group_query(a, e.stream); });
     PINOT_HIP(hipGetLastError());
     if (ks.hashed) {  // every doc's tuple == its slot representative's tuple, or the fingerprints collided
@@ -1904,7 +2123,7 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     std::vector<unsigned long long> hm(S);
     PINOT_HIP(hipMemcpyAsync(hm.data(), matched, S * 8, hipMemcpyDeviceToHost, e.stream));
     PINOT_HIP(hipEventRecord(e.ev_stop, e.stream));
-    PINOT_HIP(hipStreamSynchronize(e.stream));
+    wait_stream(e);
     float pms = 0;
     PINOT_HIP(hipEventElapsedTime(&pms, e.ev_start, e.ev_stop));
     t.collect();
@@ -1915,7 +2134,7 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
   }
 
   const auto tg1 = std::chrono::steady_clock::now();
-  if (e.host_phases) PINOT_HIP(hipStreamSynchronize(e.stream));
+  if (e.host_phases) wait_stream(e);
   const auto tg2 = std::chrono::steady_clock::now();
   // finalize: ordered non-empty keys, per-group outputs, one D2H
   const size_t cscr = compact_keys_scratch_bytes(ks.G);
@@ -1931,7 +2150,7 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
   PINOT_HIP(hipMemcpyAsync(&n, n_dev, 8, hipMemcpyDeviceToHost, e.stream));
   PINOT_HIP(hipMemcpyAsync(hmatched.data(), matched, S * 8, hipMemcpyDeviceToHost, e.stream));
   if (ks.hashed) PINOT_HIP(hipMemcpyAsync(&verify_err, a.verify_err, 4, hipMemcpyDeviceToHost, e.stream));
-  PINOT_HIP(hipStreamSynchronize(e.stream));
+  wait_stream(e);
   if (verify_err) {  // 64-bit fingerprint collision: retry with another seed
     require(attempt < 3, PINOT_ERR_DEVICE, "group-key fingerprint collisions persist");
     return exec_group_by_fused(e, segs, q, ks_in, ga, stats, attempt + 1);
@@ -1994,7 +2213,7 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
       PINOT_HIP(hipMemcpyAsync(res->key_ids.data(), ids.get(), n * q.num_group_by * 4, hipMemcpyDeviceToHost, e.stream));
     }
     PINOT_HIP(hipMemcpyAsync(e.group_host.get(), e.group_out.get(), out_b, hipMemcpyDeviceToHost, e.stream));
-    PINOT_HIP(hipStreamSynchronize(e.stream));
+    wait_stream(e);
     tg4 = std::chrono::steady_clock::now();
     const uint8_t *host = e.group_host.get<uint8_t>();
     const auto *hc = reinterpret_cast<const unsigned long long *>(host);
@@ -2065,7 +2284,7 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     });
   }
   PINOT_HIP(hipEventRecord(e.ev_stop, e.stream));
-  PINOT_HIP(hipStreamSynchronize(e.stream));
+  wait_stream(e);
   if (e.host_phases) {
     const auto tg5 = std::chrono::steady_clock::now();
     auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
@@ -2089,7 +2308,7 @@ std::unique_ptr<GroupByResult> exec_group_by(Engine &e, const std::vector<Segmen
   const int na = q.num_aggregations;
   require(na >= 1 && na <= kMaxAggs, PINOT_ERR_UNSUPPORTED, "1..8 aggregation functions per query");
   require(q.num_group_by >= 1 && q.num_group_by <= kMaxGroupCols, PINOT_ERR_UNSUPPORTED, "1..16 group-by columns");
-  if (e.use_fused && !needs_admission(segs, q, e)) {
+  if (e.use_fused) {
     KeySpace ks = build_key_space(segs, q);
     GroupAccs ga = group_acc_kinds(*segs[0], q);
     return exec_group_by_fused(e, segs, q, ks, ga, stats);
@@ -2137,7 +2356,7 @@ std::unique_ptr<GroupByResult> exec_group_by_legacy(Engine &e, const std::vector
   for (int a = 0; a < na; a++) { gp.acc[a] = accs[a]; gp.acc_kind[a] = ga.acc_kind[a]; }
   auto res = finalize_groups(e, q, ga, ks, gp);
   PINOT_HIP(hipEventRecord(e.ev_stop, e.stream));
-  PINOT_HIP(hipStreamSynchronize(e.stream));
+  wait_stream(e);
   float ms = 0;
   PINOT_HIP(hipEventElapsedTime(&ms, e.ev_start, e.ev_stop));
   t.collect();
@@ -2168,7 +2387,9 @@ void exec_group_by_partial(Engine &e, const std::vector<SegmentData *> &segs, co
   KeySpace ks = build_key_space(segs, q);
   require(!ks.hashed, PINOT_ERR_UNSUPPORTED, "partial group-by needs a dense key space");
   GroupAccs ga = group_acc_kinds(*segs[0], q);
-  if (e.use_fused && !needs_admission(segs, q, e)) {  // the fused sinks, stopped before compaction
+  require(!plan_admission(segs, q, e, ks.G).active, PINOT_ERR_UNSUPPORTED,
+          "multi-GPU partials with num.groups.limit admission: use the engine's own multi-device group-by");
+  if (e.use_fused) {  // the fused sinks, stopped before compaction
     const PartialOut po{counts_dev, accs_dev};
     exec_group_by_fused(e, segs, q, ks, ga, stats, 0, &po);
     return;
@@ -2196,7 +2417,7 @@ void exec_group_by_partial(Engine &e, const std::vector<SegmentData *> &segs, co
       launch_narrow_u32(hll_tmp[a].get<uint32_t>(), ks.G * 256, static_cast<uint8_t *>(accs_dev[a]), e.stream);
   PINOT_HIP(hipGetLastError());
   PINOT_HIP(hipEventRecord(e.ev_stop, e.stream));
-  PINOT_HIP(hipStreamSynchronize(e.stream));
+  wait_stream(e);
   float ms = 0;
   PINOT_HIP(hipEventElapsedTime(&ms, e.ev_start, e.ev_stop));
   t.collect();

@@ -371,7 +371,48 @@ __global__ void k_narrow_u32(const uint32_t *__restrict__ in, long long n4, uint
   }
 }
 
+// Admission threshold of one segment: the upper-th smallest first doc (sorted ascending; 0xFFFFFFFF = absent key),
+// or every present key when the segment has at most `upper` of them.
+__global__ void k_admit_bitmap(const uint32_t *__restrict__ first_doc, long long G, const uint32_t *__restrict__ sorted,
+                               long long upper, uint32_t *__restrict__ bitmap, long long words) {
+  const uint32_t t = (sorted && upper <= G) ? sorted[upper - 1] : 0xFFFFFFFEu;
+  for (long long w = (long long)blockIdx.x * blockDim.x + threadIdx.x; w < words; w += (long long)gridDim.x * blockDim.x) {
+    uint32_t m = 0;
+    for (int b = 0; b < 32; b++) {
+      const long long k = w * 32 + b;
+      if (k >= G) break;
+      const uint32_t fd = first_doc[k];
+      m |= (fd != 0xFFFFFFFFu && fd <= t) ? (1u << b) : 0u;
+    }
+    bitmap[w] = m;
+  }
+}
+
 }  // namespace
+
+size_t admission_scratch_bytes(long long G) {
+  size_t need = 0;
+  PINOT_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, need, (const uint32_t *)nullptr, (uint32_t *)nullptr, (int)G));
+  return ((size_t)G * 4 + 255) / 256 * 256 + need + 256;
+}
+
+void launch_admission_bitmaps(const uint32_t *first_doc, int S, long long G, const long long *upper, uint32_t *bitmaps,
+                              long long words, void *scratch, size_t scratch_bytes, hipStream_t stream) {
+  uint32_t *sorted = static_cast<uint32_t *>(scratch);
+  const size_t sorted_b = ((size_t)G * 4 + 255) / 256 * 256;
+  void *tmp = static_cast<uint8_t *>(scratch) + sorted_b;
+  const int grid = (int)std::min<long long>((words + 255) / 256, 4096);
+  for (int s = 0; s < S; s++) {
+    const uint32_t *fd = first_doc + (size_t)s * G;
+    const bool limited = upper[s] < G;
+    if (limited) {
+      size_t tb = scratch_bytes - sorted_b;
+      PINOT_HIP(hipcub::DeviceRadixSort::SortKeys(tmp, tb, fd, sorted, (int)G, 0, 32, stream));
+    }
+    hipLaunchKernelGGL(k_admit_bitmap, dim3(grid), dim3(256), 0, stream, fd, G, limited ? sorted : nullptr,
+                       limited ? upper[s] : G + 1, bitmaps + (size_t)s * words, words);
+  }
+}
 
 void launch_narrow_u32(const uint32_t *in, long long n, uint8_t *out, hipStream_t stream) {
   if (n <= 0) return;

@@ -183,7 +183,9 @@ int scan_query_blocks_per_cu(int stage_bytes, bool gathers, bool pipelined);
 //              to HBM) — the large key spaces (config 4: 1 M keys with HLL)
 //   GB_VERIFY  hashed key spaces: re-reads every matching doc's tuple and checks it against its hash
 //              slot's representative doc (a 64-bit fingerprint collision is detected, never merged)
-enum GroupMode : int32_t { GB_GLOBAL = 0, GB_LDS = 1, GB_COUNT = 2, GB_EMIT = 3, GB_VERIFY = 4 };
+//   GB_FIRST   num.groups.limit admission: first_doc[segment][key] = smallest matching doc of the key
+//              (a plain read first; atomicMin only when the doc is earlier)
+enum GroupMode : int32_t { GB_GLOBAL = 0, GB_LDS = 1, GB_COUNT = 2, GB_EMIT = 3, GB_VERIFY = 4, GB_FIRST = 5 };
 // accumulator kinds (acc_kind): 0 int64 sum, 1 double sum, 2 ordered-u64 min, 3 ordered-u64 max,
 // 4 HLL registers (u8 [G][256]), 5 none (COUNT / AVG count share `counts`)
 constexpr int kMaxGroupAggs = 8;
@@ -217,6 +219,7 @@ struct GroupSegment {
   int32_t first_gcol, first_agg;
   int32_t reserved;
   int64_t ch_begin, ch_end;  // chunk window (see FusedSegment)
+  const uint32_t *admitted;  // num.groups.limit: bitmap over keys admitted for THIS segment, null = all
 };
 
 struct GroupArgs {
@@ -229,7 +232,7 @@ struct GroupArgs {
   long long G;
   unsigned long long *counts;  // u64 [G]
   unsigned long long *matched; // u64 [nsegs]: docs passing the filter per segment (numDocsScanned)
-  const uint32_t *admitted;    // bitmap over keys (num.groups.limit), null = all
+  uint32_t *first_doc;         // GB_FIRST: [nsegs][G] smallest matching doc per key (0xFFFFFFFF = absent)
   int32_t lds_acc_bytes;       // GB_LDS: per-block accumulator bytes (counts u32 [G] at 0, aggs at lds_off)
   int32_t shift;               // GB_COUNT / GB_EMIT: partition = key >> shift, local key = low bits
   int32_t P;                   // partitions
@@ -298,6 +301,14 @@ void launch_compact_keys_ordered(long long G, const unsigned long long *counts, 
 void launch_group_outputs(const unsigned long long *counts, const GroupAggDev *aggs_host, int n_aggs, const long long *keys,
                           long long n, unsigned long long *out_counts, unsigned long long *out_acc,
                           unsigned long long *out_hll_sum, uint32_t *out_hll_zeros, hipStream_t stream);
+// num.groups.limit admission (DictionaryBasedGroupKeyGenerator IntMapBasedHolder.getGroupId, first appearance):
+// segment s admits the upper[s] keys with the smallest first_doc[s][k] (first_doc values of distinct keys are
+// distinct docs). bitmaps[s] (words u32 each) gets bit k for every admitted key; upper[s] >= G admits every present
+// key. One radix sort of first_doc[s] per limited segment; the threshold never leaves the device.
+size_t admission_scratch_bytes(long long G);
+void launch_admission_bitmaps(const uint32_t *first_doc, int S, long long G, const long long *upper, uint32_t *bitmaps,
+                              long long words, void *scratch, size_t scratch_bytes, hipStream_t stream);
+
 // Exclusive prefix sum of n u32 (hipcub); returns the temporary storage it needs when tmp == null.
 size_t exclusive_sum_u32(const uint32_t *in, uint32_t *out, long long n, void *tmp, size_t tmp_bytes,
                          hipStream_t stream);

@@ -208,8 +208,11 @@ static void register_column(Engine &e, SegmentData &seg, const pinot_column_desc
   c.string_width = d.string_width;
   c.num_docs = seg.num_docs;
   require(c.card >= 1 || seg.num_docs == 0, PINOT_ERR_BAD_ARG, c.name + ": empty dictionary");
-  require(c.bits == num_bits_per_value(std::max<int64_t>(c.card - 1, 0)), PINOT_ERR_BAD_ARG,
-          c.name + ": bits_per_value != getNumBitsPerValue(cardinality - 1)");
+  // The reader takes the width from the segment metadata (column.<c>.bitsPerElement, ColumnMetadata.java:98 ->
+  // FixedBitSingleValueReader, PhysicalColumnIndexContainer.java:99); the creator writes
+  // getNumBitsPerValue(card - 1) (SegmentColumnarIndexCreator.java:404), so any wider width still decodes.
+  require(c.bits >= num_bits_per_value(std::max<int64_t>(c.card - 1, 0)), PINOT_ERR_BAD_ARG,
+          c.name + ": bits_per_value < getNumBitsPerValue(cardinality - 1)");
   require(c.bits >= 1 && c.bits <= 32, PINOT_ERR_BAD_ARG, c.name + ": bits out of range");
   decode_dictionary(c, d);
   upload_dictionary(e, c);

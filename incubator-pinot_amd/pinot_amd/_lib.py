@@ -11,7 +11,8 @@ LIB_PATH = os.path.join(_HERE, "libpinot_gpu.so")
 
 PINOT_OK = 0
 STATUS = {0: "PINOT_OK", 1: "PINOT_ERR_BAD_ARG", 2: "PINOT_ERR_OOM", 3: "PINOT_ERR_DEVICE",
-          4: "PINOT_ERR_UNSUPPORTED", 5: "PINOT_ERR_BAD_QUERY"}
+          4: "PINOT_ERR_UNSUPPORTED", 5: "PINOT_ERR_BAD_QUERY", 6: "PINOT_ERR_TIMEOUT"}
+PINOT_ERR_TIMEOUT = 6
 DATA_TYPE = {"INT": 0, "LONG": 1, "FLOAT": 2, "DOUBLE": 3, "STRING": 4}
 FILTER_OP = {"AND": 0, "OR": 1, "EQUALITY": 2, "NOT": 3, "RANGE": 4, "IN": 5, "NOT_IN": 6}
 AGG_FN = {"COUNT": 0, "SUM": 1, "MIN": 2, "MAX": 3, "AVG": 4, "DISTINCTCOUNTHLL": 5}
@@ -23,7 +24,8 @@ EXPORTED_SYMBOLS = [
     "pinot_gpu_segment_register", "pinot_gpu_segment_release", "pinot_gpu_segment_device_bytes",
     "pinot_gpu_filter", "pinot_gpu_aggregate", "pinot_gpu_group_by",
     "pinot_groupby_num_groups", "pinot_groupby_num_columns", "pinot_groupby_key", "pinot_groupby_values",
-    "pinot_groupby_hll", "pinot_groupby_raw_keys", "pinot_groupby_free",
+    "pinot_groupby_hll", "pinot_groupby_raw_keys", "pinot_groupby_export_keys", "pinot_groupby_trim",
+    "pinot_groupby_free",
     "pinot_gpu_group_by_layout", "pinot_gpu_group_by_partial", "pinot_gpu_group_by_finalize",
     "pinot_gpu_segment_register_synthetic", "pinot_gpu_segment_register_synthetic_ex", "pinot_gpu_synchronize",
     "pinot_gpu_last_kernel_ms",
@@ -64,7 +66,8 @@ class Query(C.Structure):
     _fields_ = [("num_filter_nodes", C.c_int32), ("filter", C.POINTER(FilterNode)),
                 ("num_aggregations", C.c_int32), ("aggregations", C.POINTER(AggSpec)),
                 ("num_group_by", C.c_int32), ("group_by", C.POINTER(C.c_char_p)),
-                ("num_groups_limit", C.c_int32), ("max_init_group_holder_capacity", C.c_int32)]
+                ("num_groups_limit", C.c_int32), ("max_init_group_holder_capacity", C.c_int32),
+                ("timeout_ms", C.c_int32), ("reserved", C.c_int32)]
 
 
 class ExecStats(C.Structure):
@@ -143,6 +146,8 @@ def load(path=None):
         "pinot_groupby_values": (i32, [P, i32, P, P]),
         "pinot_groupby_hll": (i32, [P, i32, P, P]),
         "pinot_groupby_raw_keys": (i32, [P, P]),
+        "pinot_groupby_export_keys": (i32, [P, P, u64, P, C.POINTER(u64)]),
+        "pinot_groupby_trim": (i32, [P, i32, i32, P, C.POINTER(i64)]),
         "pinot_groupby_free": (None, [P]),
         "pinot_gpu_group_by_layout": (i32, [P, C.POINTER(i64), i32, C.POINTER(Query), C.POINTER(PartialLayout)]),
         "pinot_gpu_group_by_partial": (i32, [P, C.POINTER(i64), i32, C.POINTER(Query), P, C.POINTER(P),

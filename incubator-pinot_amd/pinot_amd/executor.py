@@ -189,7 +189,7 @@ def _postfix(tree, out, keep):
 class QueryMarshal:
     """Query dict -> `pinot_query` (keeps every buffer alive for the duration of the call)."""
 
-    def __init__(self, query, num_groups_limit=100000, max_init_group_holder_capacity=10000):
+    def __init__(self, query, num_groups_limit=100000, max_init_group_holder_capacity=10000, timeout_ms=0):
         self.keep = []
         nodes = []
         _postfix(query.get("filter"), nodes, self.keep)
@@ -209,7 +209,7 @@ class QueryMarshal:
         self.keep.append(gcols)
         self.gcols = (C.c_char_p * max(len(gcols), 1))(*gcols)
         self.q = _lib.Query(len(nodes), self.nodes, len(aggs), self.aggs, len(gcols), self.gcols,
-                            num_groups_limit, max_init_group_holder_capacity)
+                            num_groups_limit, max_init_group_holder_capacity, int(timeout_ms), 0)
 
 
 class GroupByResult:
@@ -229,7 +229,30 @@ class GroupByResult:
         return self.lib.pinot_groupby_num_groups(self.ptr)
 
     def keys(self):
-        return [self.lib.pinot_groupby_key(self.ptr, i).decode("utf-8") for i in range(self.num_groups())]
+        """Every group key string through one bulk export call (pinot_groupby_export_keys)."""
+        buf, offs = self.key_bytes()
+        text = buf.decode("utf-8")
+        if len(text) == len(buf):  # ASCII: byte offsets are character offsets
+            return [text[offs[g]:offs[g + 1]] for g in range(offs.shape[0] - 1)]
+        return [buf[offs[g]:offs[g + 1]].decode("utf-8") for g in range(offs.shape[0] - 1)]
+
+    def key_bytes(self):
+        n = self.num_groups()
+        offs = np.zeros(n + 1, dtype=np.int64)
+        need = C.c_uint64()
+        check(self.lib.pinot_groupby_export_keys(self.ptr, None, 0, offs.ctypes.data_as(C.c_void_p), C.byref(need)))
+        buf = C.create_string_buffer(max(need.value, 1))
+        check(self.lib.pinot_groupby_export_keys(self.ptr, buf, need.value, offs.ctypes.data_as(C.c_void_p),
+                                                 C.byref(need)))
+        return buf.raw[:need.value], offs
+
+    def trimmed_groups(self, top_n, fn):
+        """Group indices of function fn's trimmed map (AggregationGroupByTrimmingService, native)."""
+        k = C.c_int64()
+        check(self.lib.pinot_groupby_trim(self.ptr, int(top_n), fn, None, C.byref(k)))
+        out = np.zeros(max(k.value, 1), dtype=np.int64)
+        check(self.lib.pinot_groupby_trim(self.ptr, int(top_n), fn, out.ctypes.data_as(C.c_void_p), C.byref(k)))
+        return out[:k.value]
 
     def raw_keys(self):
         n = self.num_groups()
@@ -253,8 +276,11 @@ class GroupByResult:
                                          cards.ctypes.data_as(C.c_void_p)))
         return regs[:n], cards[:n]
 
-    def to_map(self):
-        """{string_key: [intermediate result per function]} (the CombineGroupByOperator result map)."""
+    def to_map(self, trim_top_n=None):
+        """{string_key: [intermediate result per function]} (the CombineGroupByOperator result map).
+
+        trim_top_n: apply AggregationGroupByTrimmingService.trimIntermediateResultsMap (native): the reference
+        returns one map per function, so a group trimmed from function i's map carries None at position i."""
         keys = self.keys()
         cols = []
         for i, a in enumerate(self.query["aggregations"]):
@@ -270,7 +296,16 @@ class GroupByResult:
                 cols.append([AvgPair(float(v), int(c)) for v, c in zip(vals, counts)])
             else:
                 cols.append([float(v) for v in vals])
-        return {k: [col[g] for col in cols] for g, k in enumerate(keys)}
+        if trim_top_n is None:
+            return {k: [col[g] for col in cols] for g, k in enumerate(keys)}
+        kept = [self.trimmed_groups(trim_top_n, i) for i in range(len(cols))]
+        if all(k.shape[0] == len(keys) for k in kept):
+            return {k: [col[g] for col in cols] for g, k in enumerate(keys)}
+        out = {}
+        for i, (col, sel) in enumerate(zip(cols, kept)):
+            for g in sel.tolist():
+                out.setdefault(keys[g], [None] * len(cols))[i] = col[g]
+        return out
 
 
 def _segment_handles(segments):
@@ -287,10 +322,12 @@ class PreparedQuery:
 class ServerQueryExecutor:
     """`ServerQueryExecutorV1Impl.processQuery` over GPU-resident segments of one engine."""
 
-    def __init__(self, engine: GpuEngine, num_groups_limit=100000, max_init_group_holder_capacity=10000):
+    def __init__(self, engine: GpuEngine, num_groups_limit=100000, max_init_group_holder_capacity=10000,
+                 timeout_ms=0):
         self.engine = engine
         self.num_groups_limit = num_groups_limit
         self.max_init = max_init_group_holder_capacity
+        self.timeout_ms = timeout_ms
 
     def prepare(self, query):
         """Compile + marshal a query once (a prepared statement); process_query accepts the result.
@@ -298,7 +335,7 @@ class ServerQueryExecutor:
         against each segment's dictionary and runs the device path."""
         if isinstance(query, str):
             query = compile_pql(query)
-        return PreparedQuery(query, QueryMarshal(query, self.num_groups_limit, self.max_init))
+        return PreparedQuery(query, QueryMarshal(query, self.num_groups_limit, self.max_init, self.timeout_ms))
 
     def process_query(self, query, segments, trim=True):
         if isinstance(query, PreparedQuery):
@@ -306,7 +343,7 @@ class ServerQueryExecutor:
         else:
             if isinstance(query, str):
                 query = compile_pql(query)
-            m = QueryMarshal(query, self.num_groups_limit, self.max_init)
+            m = QueryMarshal(query, self.num_groups_limit, self.max_init, self.timeout_ms)
         lib = self.engine.lib
         handles = _segment_handles(segments)
         stats = _lib.ExecStats()
@@ -314,9 +351,8 @@ class ServerQueryExecutor:
             out = C.c_void_p()
             check(lib.pinot_gpu_group_by(self.engine.ptr, handles, len(segments), C.byref(m.q), C.byref(out),
                                          C.byref(stats)))
-            res = GroupByResult(lib, out, query).to_map()
-            if trim:
-                res = trim_intermediate_results(query, res)
+            res = GroupByResult(lib, out, query).to_map(
+                trim_top_n=query["group_by"].get("top_n", 10) if trim else None)
         else:
             n = len(query["aggregations"])
             out = (_lib.AggResult * n)()
@@ -332,7 +368,7 @@ class ServerQueryExecutor:
         """Raw device group-by result object (no trimming)."""
         if isinstance(query, str):
             query = compile_pql(query)
-        m = QueryMarshal(query, self.num_groups_limit, self.max_init)
+        m = QueryMarshal(query, self.num_groups_limit, self.max_init, self.timeout_ms)
         out = C.c_void_p()
         stats = _lib.ExecStats()
         check(self.engine.lib.pinot_gpu_group_by(self.engine.ptr, _segment_handles(segments), len(segments),
@@ -381,20 +417,21 @@ def merge(f, a, b):
 
 
 def trim_intermediate_results(query, result, trim_size=None):
-    """`AggregationGroupByTrimmingService.trimIntermediateResultsMap` (:52-116).
-
-    Trim threshold = 4 * max(5 * topN, 5000); above it keep the top max(5*topN, 5000) groups per function
-    (MIN ascending, others descending); the union of the per-function top groups survives."""
+    """`AggregationGroupByTrimmingService.trimIntermediateResultsMap` (:52-116) over an untrimmed result map, with
+    the native rule (pinot_groupby_trim): above 4 * max(5*topN, 5000) groups each function keeps its own
+    max(5*topN, 5000) best groups (MIN ascending, others descending); a group trimmed from function i's map carries
+    None at position i (the reference returns one map per function)."""
     top_n = query["group_by"].get("top_n", 10)
     keep_n = trim_size if trim_size is not None else max(5 * top_n, 5000)
     if len(result) <= 4 * keep_n:
         return result
-    keys = set()
+    out = {}
     for i, a in enumerate(query["aggregations"]):
         f = a["function"].upper()
         items = sorted(result.items(), key=lambda kv: final_result(f, kv[1][i]), reverse=(f != "MIN"))
-        keys.update(k for k, _ in items[:keep_n])
-    return {k: result[k] for k in keys}
+        for k, v in items[:keep_n]:
+            out.setdefault(k, [None] * len(v))[i] = v[i]
+    return out
 
 
 def format_value(f, v):
@@ -412,14 +449,18 @@ class BrokerReduce:
     def reduce(query, server_results):
         fns = [a["function"].upper() for a in query["aggregations"]]
         if query.get("group_by"):
-            merged = {}
+            # per function (the servers' trimmed maps are per function: None = trimmed there)
+            merged = [{} for _ in fns]
             for r in server_results:
                 for k, vals in r.items():
-                    merged[k] = [merge(f, x, y) for f, x, y in zip(fns, merged[k], vals)] if k in merged else list(vals)
+                    for i, (f, v) in enumerate(zip(fns, vals)):
+                        if v is None:
+                            continue
+                        merged[i][k] = merge(f, merged[i][k], v) if k in merged[i] else v
             top_n = query["group_by"].get("top_n", 10)
             out = []
             for i, f in enumerate(fns):
-                items = sorted(((k, final_result(f, v[i])) for k, v in merged.items()), key=lambda kv: kv[1],
+                items = sorted(((k, final_result(f, v)) for k, v in merged[i].items()), key=lambda kv: kv[1],
                                reverse=(f != "MIN"))[:top_n]
                 out.append([(k, ("%d" % v) if f in ("COUNT", "DISTINCTCOUNTHLL") else "%.5f" % v) for k, v in items])
             return out

@@ -200,14 +200,21 @@ def _sorted_unique(values, data_type):
     return uniq, ids.astype(np.int32)
 
 
-def build_column(name, values, data_type, inverted=False, allow_sorted=True) -> Column:
-    """Create one column the way `SegmentColumnarIndexCreator` does for a single-value dictionary column."""
+def build_column(name, values, data_type, inverted=False, allow_sorted=True, bits=None) -> Column:
+    """Create one column the way `SegmentColumnarIndexCreator` does for a single-value dictionary column.
+
+    `bits` (default getNumBitsPerValue(card - 1), SegmentColumnarIndexCreator.java:404) may be wider: the
+    reader takes the width from the metadata's bitsPerElement (ColumnMetadata.java:98)."""
     if data_type not in DATA_TYPES:
         raise ValueError("unsupported data type %s" % data_type)
     uniq, ids = _sorted_unique(values, data_type)
     card = len(uniq)
     n = ids.shape[0]
-    bits = num_bits_per_value(card - 1)
+    min_bits = num_bits_per_value(card - 1)
+    if bits is None:
+        bits = min_bits
+    elif not min_bits <= bits <= 32:
+        raise ValueError("bits %d outside [%d, 32]" % (bits, min_bits))
     dbytes, width = _dictionary_bytes(uniq, data_type)
     is_sorted = bool(allow_sorted and (n <= 1 or bool(np.all(ids[1:] >= ids[:-1]))))
     col = Column(name=name, data_type=data_type, cardinality=card, bits=bits, is_sorted=is_sorted,
@@ -228,12 +235,14 @@ def build_column(name, values, data_type, inverted=False, allow_sorted=True) -> 
     return col
 
 
-def build_segment(name, columns: Dict[str, tuple], inverted_columns=(), num_docs=None) -> Segment:
-    """columns: {name: (data_type, values)} in schema order."""
+def build_segment(name, columns: Dict[str, tuple], inverted_columns=(), num_docs=None, bits=None,
+                  allow_sorted=True) -> Segment:
+    """columns: {name: (data_type, values)} in schema order; bits: optional {name: bitsPerElement}."""
     cols = {}
     n = None
     for cname, (dt, vals) in columns.items():
-        col = build_column(cname, vals, dt, inverted=cname in inverted_columns)
+        col = build_column(cname, vals, dt, inverted=cname in inverted_columns, allow_sorted=allow_sorted,
+                           bits=(bits or {}).get(cname))
         if n is None:
             n = col.num_docs
         elif n != col.num_docs:

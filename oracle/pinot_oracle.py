@@ -520,6 +520,137 @@ def combine_group_by(query, per_segment, num_groups_limit=100000):
     return merged
 
 
+def cardinality_np(regs):
+    """HyperLogLog.cardinality() of every row of a uint8 [n, 256] register matrix (hll.cardinality, vectorised:
+    the sum of 2^-reg is exact in double, so the result is bit-identical to the scalar form)."""
+    from hll import ALPHA_MM, M
+    r = np.asarray(regs, dtype=np.int64)
+    s = np.ldexp(1.0, -r).sum(axis=1)
+    zeros = (r == 0).sum(axis=1).astype(np.float64)
+    est = ALPHA_MM * (1.0 / s)
+    with np.errstate(divide="ignore"):
+        lc = M * np.log(M / zeros)
+    x = np.where(est <= 2.5 * M, lc, est)
+    out = np.floor(x + 0.5)
+    big = ~np.isfinite(out) | (out >= 9.2e18)
+    res = np.where(big, 0, out).astype(np.int64)
+    res[big] = 9223372036854775807  # Math.round(+inf) = Long.MAX_VALUE
+    return res
+
+
+def _union_dictionary(cols):
+    """Global dictionary of one group-by column over segments: the union of the per-segment sorted dictionaries in
+    value order (STRING: UTF-8 byte order). Returns (values, [local dictId -> global id per segment])."""
+    if cols[0].data_type == "STRING":
+        allv = sorted({v for c in cols for v in c.dict_values()}, key=lambda s: s.encode("utf-8"))
+        index = {v: i for i, v in enumerate(allv)}
+        return allv, [np.array([index[v] for v in c.dict_values()], dtype=np.int64) for c in cols]
+    allv = np.unique(np.concatenate([c.dict_values() for c in cols]))
+    return list(allv), [np.searchsorted(allv, c.dict_values()).astype(np.int64) for c in cols]
+
+
+def execute_group_by_arrays(segments, query, num_groups_limit=100000, array_threshold=10000):
+    """Vectorised server-side group-by for large key spaces: the same semantics as execute_server() on a group-by
+    query (per-segment DictionaryBasedGroupKeyGenerator with the num.groups.limit first-appearance rule,
+    DictionaryBasedGroupKeyGenerator.java:79-126,293-302; CombineGroupByOperator merge with the 2 x limit
+    inter-segment cap in segment order, :61,147), computed with numpy scatter ops instead of a Python loop per
+    group. Pinned against execute_server() by tests/test_oracle_fast.py.
+
+    Keys are raw keys of the GLOBAL key space: global id of column j = rank of its value in the union of the
+    segments' dictionaries, raw = sum_j gid_j * prod_{k<j} gcard_k (column 0 least significant).
+    Returns dict(keys=int64[n] ascending, gcard, gvalues, scanned, fns=[dict(count, sum|min|max, hll, card)])."""
+    gnames = query["group_by"]["columns"]
+    fns = [a["function"].upper() for a in query["aggregations"]]
+    gvalues, remaps, gcard = [], [], []
+    for name in gnames:
+        vals, rm = _union_dictionary([s.column(name) for s in segments])
+        gvalues.append([_string_value(segments[0].column(name), v) for v in vals])
+        remaps.append(rm)
+        gcard.append(len(vals))
+    strides = np.cumprod([1] + gcard[:-1]).astype(np.int64)
+    if _prod(gcard) >= 2 ** 62:
+        raise ValueError("global key space too large for the vectorised oracle")
+    inter_limit = 2 * num_groups_limit
+    merged = np.zeros(0, dtype=np.int64)  # admitted global keys so far (sorted)
+    seg_docs, seg_keys = [], []
+    scanned = 0
+    for si, seg in enumerate(segments):
+        mask = filter_mask(seg, query.get("filter"))
+        scanned += int(mask.sum())
+        docs = np.nonzero(mask)[0]
+        gcols = [seg.column(c) for c in gnames]
+        cards = [c.cardinality for c in gcols]
+        ids = [dict_ids(c)[docs] for c in gcols]
+        local = np.zeros(docs.shape[0], dtype=np.int64)
+        for j in range(len(gcols) - 1, -1, -1):
+            local = local * cards[j] + ids[j]
+        product = _prod(cards)
+        if product > array_threshold:
+            upper = min(product, num_groups_limit) if product <= INT_MAX else num_groups_limit
+            uniq, first = np.unique(local, return_index=True)
+            if uniq.shape[0] > upper:
+                admitted = np.sort(local[np.sort(first)[:upper]])
+                keep = np.isin(local, admitted, assume_unique=False)
+                docs, local = docs[keep], local[keep]
+                ids = [x[keep] for x in ids]
+        gkey = np.zeros(docs.shape[0], dtype=np.int64)
+        for j in range(len(gcols)):
+            gkey += remaps[j][si][ids[j]] * strides[j]
+        # CombineGroupByOperator: new keys enter while the merged map holds < 2 x limit (segment order,
+        # ascending key order within a segment: the order this oracle's per-segment maps iterate in)
+        present = np.unique(gkey)
+        new = present[~np.isin(present, merged)]
+        room = max(inter_limit - merged.shape[0], 0)
+        merged = np.union1d(merged, new[:room])
+        seg_docs.append(docs)
+        seg_keys.append(gkey)
+    allk = np.concatenate(seg_keys) if seg_keys else np.zeros(0, dtype=np.int64)
+    keys, inv = np.unique(allk, return_inverse=True)
+    ok = np.isin(keys, merged)
+    out = {"keys": keys[ok], "gcard": gcard, "gvalues": gvalues, "scanned": scanned, "fns": []}
+    n = keys.shape[0]
+    for a, f in zip(query["aggregations"], fns):
+        r = {"count": np.bincount(inv, minlength=n)[ok].astype(np.int64)}
+        if f == "COUNT":
+            out["fns"].append(r)
+            continue
+        per_seg = []
+        for seg, docs in zip(segments, seg_docs):
+            col = seg.column(a["column"])
+            per_seg.append((col, dict_ids(col)[docs]))
+        if f == "DISTINCTCOUNTHLL":
+            h = np.concatenate([_value_hashes(c)[i] for c, i in per_seg])
+            j, rk = register_and_rank_np(h)
+            regs = np.zeros(n * 256, dtype=np.uint8)
+            np.maximum.at(regs, inv.astype(np.int64) * 256 + j, rk.astype(np.uint8))
+            regs = regs.reshape(n, 256)[ok]
+            r["hll"] = regs
+            r["card"] = cardinality_np(regs)
+        else:
+            v = np.concatenate([_values_double(c, i) for c, i in per_seg])
+            if f in ("SUM", "AVG"):
+                r["sum"] = np.bincount(inv, weights=v, minlength=n)[ok]
+            elif f == "MIN":
+                m = np.full(n, np.inf)
+                np.minimum.at(m, inv, v)
+                r["min"] = m[ok]
+            elif f == "MAX":
+                m = np.full(n, -np.inf)
+                np.maximum.at(m, inv, v)
+                r["max"] = m[ok]
+        out["fns"].append(r)
+    return out
+
+
+def key_string(arrays, raw_key):
+    """'\\t'-joined group key of a global raw key (DictionaryBasedGroupKeyGenerator.getGroupKey :421-437)."""
+    parts = []
+    for card, vals in zip(arrays["gcard"], arrays["gvalues"]):
+        parts.append(vals[raw_key % card])
+        raw_key //= card
+    return "\t".join(parts)
+
+
 def _copy(f, v):
     if f == "DISTINCTCOUNTHLL":
         h = HyperLogLog()

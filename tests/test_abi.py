@@ -30,7 +30,7 @@ def test_library_exports_header_symbols():
 
 def test_abi_version_and_error_path_without_gpu():
     lib = _lib.load()
-    assert lib.pinot_gpu_abi_version() == 2
+    assert lib.pinot_gpu_abi_version() == 3
     if lib.pinot_gpu_device_count() == 0:
         ptr = ctypes.c_void_p()
         st = lib.pinot_gpu_engine_create(0, None, ctypes.byref(ptr))
@@ -43,3 +43,4 @@ def test_struct_sizes_match_header():
     assert ctypes.sizeof(_lib.AggResult) == 8 + 8 + 8 + 4 + 4 + 8 + 256
     assert ctypes.sizeof(_lib.ExecStats) == 7 * 8
     assert ctypes.sizeof(_lib.FilterNode) == 4 + 4 + 8 + 4 + 4 + 8
+    assert ctypes.sizeof(_lib.Query) == 3 * (4 + 4 + 8) + 4 * 4  # ... num_groups_limit, max_init, timeout_ms, reserved

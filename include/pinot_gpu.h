@@ -227,6 +227,8 @@ typedef struct {
      4 = uint8 HLL registers (256 bytes per key: an all-reduce MAX over uint8 moves G*256 bytes),
      5 = none (COUNT uses the shared count array) */
   int32_t acc_kind[8];
+  uint64_t group_dictionary_fingerprint; /* FNV-1a of the group-by columns' dictionaries: ranks compare it
+                                            before merging (raw keys mean the same groups only when equal) */
 } pinot_partial_layout;
 
 pinot_status pinot_gpu_group_by_layout(pinot_engine *engine, const pinot_segment_handle *segments,
@@ -242,6 +244,38 @@ pinot_status pinot_gpu_group_by_finalize(pinot_engine *engine, const pinot_segme
                                          int32_t num_segments, const pinot_query *query,
                                          const int64_t *counts_dev, void *const *accs_dev,
                                          pinot_groupby_result **out);
+
+/* ------------------------------------------------------------------ multi-GPU server
+ * One server per node process: QueryExecutor.init with a device mask. It owns one engine per GPU and
+ * the RCCL communicators, created once (ncclCommInitAll). Segments are registered on its engines
+ * (pinot_gpu_server_engine; never pass those to pinot_gpu_engine_destroy) and queried together: the result is the
+ * combine over every GPU, as CombineOperator / CombineGroupByOperator return it (CombineOperator.java:75-196,
+ * CombineGroupByOperator.java:104-228). Group-by merges dense partials over the query's global key space (union
+ * dictionaries: per-segment dictionaries may differ) with a reduce-scatter and finalizes each key range on its GPU.
+ * Not handled across GPUs (PINOT_ERR_UNSUPPORTED: run on one engine): hashed key spaces (LONG_MAP / ARRAY_MAP) and
+ * queries where the 2 x num.groups.limit inter-segment cap can bind. */
+typedef struct pinot_server pinot_server;
+typedef struct {
+  int32_t engine;              /* index of the server engine that holds the segment */
+  int32_t reserved;
+  pinot_segment_handle handle; /* that engine's handle */
+} pinot_segment_ref;
+
+pinot_status pinot_gpu_server_create(const int32_t *devices, int32_t num_devices, const char *config, pinot_server **out);
+/* Multi-process form (one process per GPU): rank 0 makes a 128-byte id, shares it out of band; every rank then
+ * creates its server with (device, nranks, rank, id). Each rank's group-by result is its own key range of the
+ * merged result (ranks' ranges are disjoint and ascending); aggregation results are complete on every rank. Every
+ * rank must hold segments with identical group-by dictionaries; any rank's failure fails every rank (no hang). */
+pinot_status pinot_gpu_server_unique_id(uint8_t *unique_id);
+pinot_status pinot_gpu_server_create_rank(int32_t device, int32_t nranks, int32_t rank, const uint8_t *unique_id,
+                                          const char *config, pinot_server **out);
+pinot_status pinot_gpu_server_destroy(pinot_server *server);
+int32_t pinot_gpu_server_num_engines(const pinot_server *server);
+pinot_status pinot_gpu_server_engine(pinot_server *server, int32_t index, pinot_engine **out);
+pinot_status pinot_gpu_server_aggregate(pinot_server *server, const pinot_segment_ref *segments, int32_t num_segments,
+                                        const pinot_query *query, pinot_agg_result *out, pinot_exec_stats *stats);
+pinot_status pinot_gpu_server_group_by(pinot_server *server, const pinot_segment_ref *segments, int32_t num_segments,
+                                       const pinot_query *query, pinot_groupby_result **out, pinot_exec_stats *stats);
 
 /* ------------------------------------------------------------------ benchmark tooling
  * NOT part of the Java drop-in path: builds a synthetic dictionary-encoded column

@@ -26,8 +26,11 @@ SegmentData &Engine::seg(int64_t h) {
 
 using namespace pinot;
 
-struct pinot_engine : Engine {};
-struct pinot_groupby_result : GroupByResult {};
+struct pinot_server {
+  ServerImpl *impl = nullptr;
+  ~pinot_server() { server_destroy(impl); }
+};
+
 
 namespace {
 
@@ -55,6 +58,29 @@ pinot_status guard(F f) {
 }
 
 void set_device(Engine &e) { PINOT_HIP(hipSetDevice(e.device)); }
+void parse_config(Engine &e, const char *cfg);
+}  // namespace
+
+namespace pinot {
+std::unique_ptr<pinot_engine> create_engine(int32_t device, const char *config) {
+  int n = 0;
+  PINOT_HIP(hipGetDeviceCount(&n));
+  require(device >= 0 && device < n, PINOT_ERR_BAD_ARG, "no such HIP device");
+  auto e = std::make_unique<pinot_engine>();
+  e->device = device;
+  parse_config(*e, config);
+  PINOT_HIP(hipSetDevice(device));
+  PINOT_HIP(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+  hipDeviceProp_t prop;
+  PINOT_HIP(hipGetDeviceProperties(&prop, device));
+  e->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+  PINOT_HIP(hipEventCreate(&e->ev_start));
+  PINOT_HIP(hipEventCreate(&e->ev_stop));
+  return e;
+}
+}  // namespace pinot
+
+namespace {
 
 std::vector<SegmentData *> resolve(Engine &e, const pinot_segment_handle *segs, int32_t n) {
   require(n >= 1 && segs != nullptr, PINOT_ERR_BAD_ARG, "at least one segment required");
@@ -118,20 +144,7 @@ int32_t pinot_gpu_device_count(void) {
 pinot_status pinot_gpu_engine_create(int32_t device, const char *config, pinot_engine **out) {
   return guard([&] {
     require(out != nullptr, PINOT_ERR_BAD_ARG, "out");
-    int n = 0;
-    PINOT_HIP(hipGetDeviceCount(&n));
-    require(device >= 0 && device < n, PINOT_ERR_BAD_ARG, "no such HIP device");
-    auto e = std::make_unique<pinot_engine>();
-    e->device = device;
-    parse_config(*e, config);
-    set_device(*e);
-    PINOT_HIP(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
-    hipDeviceProp_t prop;
-    PINOT_HIP(hipGetDeviceProperties(&prop, device));
-    e->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
-    PINOT_HIP(hipEventCreate(&e->ev_start));
-    PINOT_HIP(hipEventCreate(&e->ev_stop));
-    *out = e.release();
+    *out = create_engine(device, config).release();
   });
 }
 
@@ -275,9 +288,13 @@ pinot_status pinot_groupby_hll(const pinot_groupby_result *r, int32_t fn, uint8_
     require(r->functions[fn] == PINOT_AGG_DISTINCTCOUNTHLL, PINOT_ERR_BAD_ARG, "not a DISTINCTCOUNTHLL function");
     const size_t n = r->raw_keys.size();
     if (registers && n) {
-      if (r->hll_dev) {
-        PINOT_HIP(hipSetDevice(r->device));
-        PINOT_HIP(hipMemcpy(registers, r->hll_dev->get<uint8_t>() + r->hll_dev_off[fn], n * 256, hipMemcpyDeviceToHost));
+      if (!r->hll_parts.empty()) {
+        for (const HllPart &p : r->hll_parts) {
+          if (!p.num_groups) continue;
+          PINOT_HIP(hipSetDevice(p.device));
+          PINOT_HIP(hipMemcpy(registers + p.group_begin * 256, p.buf->get<uint8_t>() + p.off[fn], p.num_groups * 256,
+                              hipMemcpyDeviceToHost));
+        }
       } else {
         memcpy(registers, r->hll[fn].data(), n * 256);
       }
@@ -348,6 +365,83 @@ pinot_status pinot_gpu_group_by_finalize(pinot_engine *engine, const pinot_segme
     std::lock_guard<std::mutex> lk(engine->mu);
     set_device(*engine);
     auto r = exec_group_by_finalize(*engine, resolve(*engine, segments, num_segments), *query, counts_dev, accs_dev);
+    auto *res = new pinot_groupby_result();
+    static_cast<GroupByResult &>(*res) = std::move(*r);
+    *out = res;
+  });
+}
+
+pinot_status pinot_gpu_server_create(const int32_t *devices, int32_t num_devices, const char *config, pinot_server **out) {
+  return guard([&] {
+    require(out != nullptr, PINOT_ERR_BAD_ARG, "out");
+    auto s = std::make_unique<pinot_server>();
+    s->impl = server_create(devices, num_devices, config);
+    *out = s.release();
+  });
+}
+
+pinot_status pinot_gpu_server_unique_id(uint8_t *unique_id) {
+  return guard([&] {
+    require(unique_id != nullptr, PINOT_ERR_BAD_ARG, "unique_id");
+    server_unique_id(unique_id);
+  });
+}
+
+pinot_status pinot_gpu_server_create_rank(int32_t device, int32_t nranks, int32_t rank, const uint8_t *unique_id,
+                                          const char *config, pinot_server **out) {
+  return guard([&] {
+    require(out != nullptr, PINOT_ERR_BAD_ARG, "out");
+    auto s = std::make_unique<pinot_server>();
+    s->impl = server_create_rank(device, nranks, rank, unique_id, config);
+    *out = s.release();
+  });
+}
+
+pinot_status pinot_gpu_server_destroy(pinot_server *server) {
+  return guard([&] { delete server; });
+}
+
+int32_t pinot_gpu_server_num_engines(const pinot_server *server) {
+  return server && server->impl ? server_num_engines(*server->impl) : 0;
+}
+
+pinot_status pinot_gpu_server_engine(pinot_server *server, int32_t index, pinot_engine **out) {
+  return guard([&] {
+    require(server && server->impl && out, PINOT_ERR_BAD_ARG, "null argument");
+    *out = static_cast<pinot_engine *>(server_engine(*server->impl, index));
+  });
+}
+
+static std::vector<SegmentRef> server_refs(const pinot_segment_ref *segments, int32_t n) {
+  require(n >= 0 && (n == 0 || segments != nullptr), PINOT_ERR_BAD_ARG, "segments");
+  std::vector<SegmentRef> refs;
+  for (int32_t i = 0; i < n; i++) refs.push_back(SegmentRef{segments[i].engine, segments[i].handle});
+  return refs;
+}
+
+pinot_status pinot_gpu_server_aggregate(pinot_server *server, const pinot_segment_ref *segments, int32_t num_segments,
+                                        const pinot_query *query, pinot_agg_result *out, pinot_exec_stats *stats) {
+  return guard([&] {
+    require(server && server->impl && out, PINOT_ERR_BAD_ARG, "null argument");
+    check_query(query);
+    require(query->num_group_by == 0, PINOT_ERR_BAD_ARG, "group-by query passed to pinot_gpu_server_aggregate");
+    require(query->timeout_ms >= 0, PINOT_ERR_TIMEOUT, "query budget already spent before execution");
+    const auto t0 = std::chrono::steady_clock::now();
+    server_aggregate(*server->impl, server_refs(segments, num_segments), *query, out, stats);
+    if (stats) stats->host_ms = elapsed_ms(t0);
+  });
+}
+
+pinot_status pinot_gpu_server_group_by(pinot_server *server, const pinot_segment_ref *segments, int32_t num_segments,
+                                       const pinot_query *query, pinot_groupby_result **out, pinot_exec_stats *stats) {
+  return guard([&] {
+    require(server && server->impl && out, PINOT_ERR_BAD_ARG, "null argument");
+    check_query(query);
+    require(query->num_group_by >= 1, PINOT_ERR_BAD_ARG, "aggregation-only query passed to pinot_gpu_server_group_by");
+    require(query->timeout_ms >= 0, PINOT_ERR_TIMEOUT, "query budget already spent before execution");
+    const auto t0 = std::chrono::steady_clock::now();
+    auto r = server_group_by(*server->impl, server_refs(segments, num_segments), *query, stats);
+    if (stats) stats->host_ms = elapsed_ms(t0);
     auto *res = new pinot_groupby_result();
     static_cast<GroupByResult &>(*res) = std::move(*r);
     *out = res;

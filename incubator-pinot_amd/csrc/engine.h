@@ -174,6 +174,13 @@ void exec_filter(Engine &e, SegmentData &s, const FilterTreeInput *tree, uint64_
 void exec_aggregate(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q, pinot_agg_result *out,
                     pinot_exec_stats *stats);
 
+struct HllPart {
+  int device = 0;
+  std::shared_ptr<DeviceBuffer> buf;
+  std::vector<size_t> off;        // per fn: byte offset of its [num_groups][256] registers
+  int64_t group_begin = 0, num_groups = 0;
+};
+
 struct GroupByResult {
   GroupByResult() = default;
   GroupByResult(GroupByResult &&) = default;
@@ -197,13 +204,11 @@ struct GroupByResult {
   uint64_t export_keys(char *buf, uint64_t buf_len, int64_t *offsets) const;
   // AggregationGroupByTrimmingService: the groups of function fn's trimmed map (ascending)
   std::vector<int64_t> trim(int32_t top_n, int32_t fn) const;
-  // DISTINCTCOUNTHLL: cardinalities per fn; registers on the host (hll[fn]) or on the device
-  // (hll_dev + hll_dev_off[fn], [groups][256] u8, copied on request)
+  // DISTINCTCOUNTHLL: cardinalities per fn; registers on the host (hll[fn]) or on the device in parts (one per
+  // GPU that finalized a key range: [groups][256] u8 at off[fn], copied on request)
   std::vector<std::vector<int64_t>> hll_card;
   std::vector<std::vector<uint8_t>> hll;
-  std::shared_ptr<DeviceBuffer> hll_dev;
-  std::vector<size_t> hll_dev_off;
-  int device = 0;
+  std::vector<HllPart> hll_parts;
 };std::unique_ptr<GroupByResult> exec_group_by(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q,
                                              pinot_exec_stats *stats);
 
@@ -231,4 +236,57 @@ int64_t hll_cardinality(const uint8_t *regs);
 // HyperLogLog.cardinality() from the exact register sum Σ 2^(32 - reg) and the zero-register count.
 int64_t hll_cardinality_from_sum(unsigned long long sum_fixed32, uint32_t zeros);
 
+// ------------------------------------------------------------------ multi-GPU server (server.cpp)
+// One engine per local GPU + RCCL communicators created once (ncclCommInitAll over the local devices, or one
+// rank of a multi-process communicator: ncclCommInitRank). Queries over segments of several engines run each
+// engine's part concurrently and merge on the device: reduce-scatter of the dense group-by partials, owner
+// finalize per key range (CombineGroupByOperator.java:104-228), host merge (single process) or an all-reduce
+// (multi process) of aggregation partials (CombineOperator.java:75-196).
+struct ServerImpl;
+struct SegmentRef {
+  int engine;
+  int64_t handle;
+};
+ServerImpl *server_create(const int32_t *devices, int32_t n, const char *config);
+ServerImpl *server_create_rank(int32_t device, int32_t nranks, int32_t rank, const uint8_t *id,
+                             const char *config);
+void server_unique_id(uint8_t *id);
+void server_destroy(ServerImpl *s);
+int server_num_engines(const ServerImpl &s);
+Engine *server_engine(ServerImpl &s, int i);
+void server_aggregate(ServerImpl &s, const std::vector<SegmentRef> &refs, const pinot_query &q, pinot_agg_result *out,
+                      pinot_exec_stats *stats);
+std::unique_ptr<GroupByResult> server_group_by(ServerImpl &s, const std::vector<SegmentRef> &refs, const pinot_query &q,
+                                               pinot_exec_stats *stats);
+
+// the multi-device partial step of one engine (executor.cpp): dense partials over [0, G) of the given key space
+// into counts / accs (allow_admission: per-segment num.groups.limit admission inside the partial, when the caller
+// has established that the inter-segment cap cannot bind)
+void exec_group_by_partial_ks(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q,
+                              const std::vector<int64_t> &gcard, const std::vector<std::vector<std::string>> &gvalues,
+                              const std::vector<std::vector<std::vector<int32_t>>> &remap, int64_t *counts_dev,
+                              void *const *accs_dev, pinot_exec_stats *stats);
+// owner finalize of one key range [key_base, key_base + G) of merged dense arrays
+std::unique_ptr<GroupByResult> exec_group_by_slice(Engine &e, const pinot_query &q, const std::vector<int> &acc_kind,
+                                                   const std::vector<int64_t> &gcard,
+                                                   const std::vector<std::vector<std::string>> &gvalues,
+                                                   unsigned long long *counts, const std::vector<void *> &accs,
+                                                   int64_t G, int64_t key_base);
+// global key space over segments of several engines (union dictionaries)
+void build_global_key_space(const std::vector<SegmentData *> &segs, const pinot_query &q, std::vector<int64_t> &gcard,
+                            std::vector<std::vector<std::string>> &gvalues,
+                            std::vector<std::vector<std::vector<int32_t>>> &remap, int64_t &G, bool &hashed);
+std::vector<int> group_acc_kind_list(const SegmentData &s, const pinot_query &q);
+bool admission_cap_can_bind(const std::vector<SegmentData *> &segs, const pinot_query &q, const Engine &e, int64_t G);
+uint64_t dictionary_fingerprint(const ColumnData &c);
+// CombineService.mergeTwoBlocks over per-engine aggregation results (host)
+void merge_agg_parts(const pinot_query &q, const std::vector<const pinot_agg_result *> &parts, pinot_agg_result *out);
+
+}  // namespace pinot
+
+struct pinot_engine : pinot::Engine {};
+struct pinot_groupby_result : pinot::GroupByResult {};
+
+namespace pinot {
+std::unique_ptr<pinot_engine> create_engine(int32_t device, const char *config);
 }  // namespace pinot

@@ -1826,10 +1826,185 @@ struct PartialOut {
   void *const *accs;
 };
 
+// Dense accumulators of one key range [key_base, key_base + G) -> result (the one-GPU group-by's back half, and the
+// owner finalize of a multi-GPU reduce-scatter slice): ordered compaction of the non-empty keys on the device
+// (`extra` enqueues further D2H copies ahead of the one sync), per-group outputs incl. the exact HLL register
+// sums, one D2H, host fill over the host's cores. HLL registers stay on the device until asked for.
+struct DenseGroups {
+  const pinot_query *q;
+  const KeySpace *ks;
+  const GroupAccs *ga, *gx;          // accumulator kinds per aggregation; gx: 5 where alias[i] shares another's
+  const std::vector<int> *alias;
+  unsigned long long *counts;
+  std::vector<void *> accs;
+  int64_t key_base;
+  const GroupArgs *hashed;           // hashed key spaces: the query's args (slot -> global-id tuples)
+};
+
+unsigned long long compact_dense(Engine &e, const unsigned long long *counts, int64_t G, long long *&keys_dev,
+                                 const std::function<void()> &extra) {
+  const size_t cscr = compact_keys_scratch_bytes(G);
+  e.group_final.reserve(G * 8 + 64 + cscr);
+  keys_dev = e.group_final.get<long long>();
+  auto *n_dev = reinterpret_cast<unsigned long long *>(e.group_final.get<uint8_t>() + G * 8);
+  launch_compact_keys_ordered(G, counts, keys_dev, n_dev, e.group_final.get<uint8_t>() + G * 8 + 64, cscr, e.stream);
+  PINOT_HIP(hipGetLastError());
+  unsigned long long n = 0;
+  PINOT_HIP(hipMemcpyAsync(&n, n_dev, 8, hipMemcpyDeviceToHost, e.stream));
+  if (extra) extra();
+  wait_stream(e);
+  return n;
+}
+
+std::unique_ptr<GroupByResult> build_dense_result(Engine &e, const DenseGroups &d, const long long *keys_dev,
+                                                  unsigned long long n) {
+  const pinot_query &q = *d.q;
+  const GroupAccs &ga = *d.ga, &gx = *d.gx;
+  const std::vector<int> &alias = *d.alias;
+  const int na = q.num_aggregations;
+  int n_hll = 0;
+  for (int i = 0; i < na; i++) n_hll += gx.acc_kind[i] == 4;
+  auto res = std::make_unique<GroupByResult>();
+  res->num_columns = q.num_group_by;
+  res->functions.resize(na);
+  for (int i = 0; i < na; i++) res->functions[i] = q.aggregations[i].function;
+  res->counts.assign(na, {});
+  res->values.assign(na, {});
+  res->hll.assign(na, {});
+  res->hll_card.assign(na, {});
+  res->gvalues = d.ks->gvalues;
+  res->gcard = d.ks->gcard;
+  if (!n) return res;
+  std::vector<GroupAggDev> oaggs(na);
+  for (int i = 0; i < na; i++) {
+    oaggs[i].acc_kind = gx.acc_kind[i];
+    oaggs[i].acc = d.accs[i];
+  }
+  // device outputs and their pinned host copy live in grow-only engine buffers (no per-query allocation)
+  const size_t out_b = n * 8 * (2 + na) + (size_t)n_hll * n * 12 + 64;
+  e.group_out.reserve(out_b);
+  e.group_host.reserve(out_b);
+  auto *o_cnt = e.group_out.get<unsigned long long>();
+  auto *o_acc = o_cnt + n;
+  auto *o_hs = o_acc + n * na;
+  auto *o_hz = reinterpret_cast<uint32_t *>(o_hs + (size_t)n_hll * n);
+  auto *o_keys = reinterpret_cast<long long *>(e.group_out.get<uint8_t>() + out_b - 64 - n * 8);
+  launch_group_outputs(d.counts, oaggs.data(), na, keys_dev, (long long)n, o_cnt, o_acc, o_hs, o_hz, e.stream);
+  PINOT_HIP(hipGetLastError());
+  if (n_hll) {  // registers stay on the device until asked for; buffers are recycled once their result is released
+    HllPart part;
+    part.device = e.device;
+    part.group_begin = 0;
+    part.num_groups = (int64_t)n;
+    part.off.assign(na, 0);
+    const size_t need = (size_t)n_hll * n * 256 + 16;
+    for (auto &b : e.hll_pool)
+      if (b.use_count() == 1 && b->size() >= need) { part.buf = b; break; }
+    if (!part.buf) {
+      part.buf = std::make_shared<DeviceBuffer>(need + need / 4);
+      if (e.hll_pool.size() < 4) e.hll_pool.push_back(part.buf);
+    }
+    int h = 0;
+    for (int i = 0; i < na; i++)
+      if (gx.acc_kind[i] == 4) {
+        part.off[i] = (size_t)h * n * 256;
+        launch_gather_hll(static_cast<const uint8_t *>(d.accs[i]), keys_dev, (long long)n, part.buf->get<uint8_t>() + part.off[i],
+                          e.stream);
+        h++;
+      }
+    for (int i = 0; i < na; i++)
+      if (alias[i] >= 0 && ga.acc_kind[i] == 4) part.off[i] = part.off[alias[i]];
+    PINOT_HIP(hipGetLastError());
+    res->hll_parts.push_back(std::move(part));
+  }
+  PINOT_HIP(hipMemcpyAsync(o_keys, keys_dev, n * 8, hipMemcpyDeviceToDevice, e.stream));
+  DeviceBuffer ids;
+  if (d.hashed) {  // group ordinals are hash slots: fetch each group's global-id tuple
+    ids.alloc(n * q.num_group_by * 4 + 16);
+    launch_hash_tuples(*d.hashed, keys_dev, (long long)n, ids.get<int32_t>(), e.stream);
+    PINOT_HIP(hipGetLastError());
+    res->key_ids.resize(n * q.num_group_by);
+    PINOT_HIP(hipMemcpyAsync(res->key_ids.data(), ids.get(), n * q.num_group_by * 4, hipMemcpyDeviceToHost, e.stream));
+  }
+  PINOT_HIP(hipMemcpyAsync(e.group_host.get(), e.group_out.get(), out_b, hipMemcpyDeviceToHost, e.stream));
+  wait_stream(e);
+  const uint8_t *host = e.group_host.get<uint8_t>();
+  const auto *hc = reinterpret_cast<const unsigned long long *>(host);
+  const auto *hacc = hc + n;
+  const auto *hhs = hacc + n * na;
+  const auto *hhz = reinterpret_cast<const uint32_t *>(hhs + (size_t)n_hll * n);
+  const auto *hkeys = reinterpret_cast<const long long *>(host + out_b - 64 - n * 8);
+  std::vector<int> hidx(na, -1);  // HLL register-sum row of each (primary) HLL aggregation
+  for (int i = 0, h = 0; i < na; i++)
+    if (gx.acc_kind[i] == 4) hidx[i] = h++;
+  // result arrays: sized (first touch of fresh pages) and filled in parallel over the host's cores
+  if (n >= kPoolMinElems) {  // recycled arrays of released results: already-mapped pages
+    ResultPool &rp = result_pool();
+    std::lock_guard<std::mutex> lk(rp.mu);
+    res->raw_keys = take_pooled(rp.i64, n);
+    res->counts[0] = take_pooled(rp.i64, n);
+    for (int i = 0; i < na; i++) {
+      res->values[i] = take_pooled(rp.f64, n);
+      if (ga.acc_kind[i] == 4) res->hll_card[i] = take_pooled(rp.i64, n);
+    }
+  }
+  std::vector<std::function<void()>> sizing;
+  sizing.push_back([&] { res->raw_keys.resize(n); });
+  res->counts_shared = true;  // every aggregation counts the same docs per group
+  sizing.push_back([&] { res->counts[0].resize(n); });
+  for (int i = 0; i < na; i++) {
+    sizing.push_back([&, i] { res->values[i].resize(n); });
+    if (ga.acc_kind[i] == 4) sizing.push_back([&, i] { res->hll_card[i].resize(n); });
+  }
+  const size_t nt = n >= (1u << 16) ? 8 : 1;  // small results: no threads
+  if (nt > 1) parallel_tasks(sizing.size(), [&](size_t t) { sizing[t](); });
+  else
+    for (auto &f : sizing) f();
+  const int64_t base = d.key_base;
+  parallel_tasks(nt, [&](size_t t) {
+    const size_t lo = n * t / nt, hi = n * (t + 1) / nt;
+    if (base == 0) memcpy(res->raw_keys.data() + lo, hkeys + lo, (hi - lo) * 8);
+    else
+      for (size_t g = lo; g < hi; g++) res->raw_keys[g] = hkeys[g] + base;
+    memcpy(res->counts[0].data() + lo, hc + lo, (hi - lo) * 8);
+    for (int i = 0; i < na; i++) {
+      double *vv = res->values[i].data();
+      const int ak = ga.acc_kind[i];
+      const int src = alias[i] >= 0 ? alias[i] : i;  // the accumulator this aggregation reads
+      const unsigned long long *raw = hacc + (size_t)src * n;
+      switch (ak) {
+        case 0:
+          for (size_t g = lo; g < hi; g++) vv[g] = (double)(int64_t)raw[g];
+          break;
+        case 1:
+          memcpy(vv + lo, raw + lo, (hi - lo) * 8);
+          break;
+        case 2:
+        case 3:
+          for (size_t g = lo; g < hi; g++) vv[g] = decode_ordered(raw[g]);
+          break;
+        case 4: {
+          const int h = hidx[src];
+          int64_t *card = res->hll_card[i].data();
+          for (size_t g = lo; g < hi; g++) {
+            card[g] = hll_cardinality_from_sum(hhs[(size_t)h * n + g], hhz[(size_t)h * n + g]);
+            vv[g] = (double)card[g];
+          }
+          break;
+        }
+        default:
+          for (size_t g = lo; g < hi; g++) vv[g] = (double)hc[g];
+          break;
+      }
+    }
+  });
+  return res;
+}
+
 std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q,
                                                    const KeySpace &ks_in, const GroupAccs &ga, pinot_exec_stats *stats,
                                                    int attempt = 0, const PartialOut *po = nullptr,
-                                                   const PartialOut *pin = nullptr) {
+                                                   const PartialOut *pin = nullptr, bool allow_admission = false) {
   const auto tg0 = std::chrono::steady_clock::now();
   const int na = q.num_aggregations;
   const size_t S = segs.size();
@@ -1860,7 +2035,7 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
                                     e.group_pshift);
   // num.groups.limit: per-segment first-appearance admission and the inter-segment cap (plan_admission)
   const AdmissionPlan adm = pin ? AdmissionPlan{} : plan_admission(segs, q, e, ks.G);
-  require(!(po && adm.active), PINOT_ERR_UNSUPPORTED,
+  require(!(po && adm.active && (!allow_admission || adm.cap_active)), PINOT_ERR_UNSUPPORTED,
           "multi-GPU partials with num.groups.limit admission: use the engine's own multi-device group-by");
   const AdmissionBuffers ab = adm.active ? admission_buffers(e, S, ks.G) : AdmissionBuffers{};
   Arena ar;
@@ -2137,152 +2312,21 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
   if (e.host_phases) wait_stream(e);
   const auto tg2 = std::chrono::steady_clock::now();
   // finalize: ordered non-empty keys, per-group outputs, one D2H
-  const size_t cscr = compact_keys_scratch_bytes(ks.G);
-  e.group_final.reserve(ks.G * 8 + 64 + cscr);
-  auto *keys_dev = e.group_final.get<long long>();
-  auto *n_dev = reinterpret_cast<unsigned long long *>(e.group_final.get<uint8_t>() + ks.G * 8);
-  launch_compact_keys_ordered(ks.G, counts, keys_dev, n_dev, e.group_final.get<uint8_t>() + ks.G * 8 + 64, cscr,
-                              e.stream);
-  PINOT_HIP(hipGetLastError());
   std::vector<unsigned long long> hmatched(S);
-  unsigned long long n = 0;
   uint32_t verify_err = 0;
-  PINOT_HIP(hipMemcpyAsync(&n, n_dev, 8, hipMemcpyDeviceToHost, e.stream));
-  PINOT_HIP(hipMemcpyAsync(hmatched.data(), matched, S * 8, hipMemcpyDeviceToHost, e.stream));
-  if (ks.hashed) PINOT_HIP(hipMemcpyAsync(&verify_err, a.verify_err, 4, hipMemcpyDeviceToHost, e.stream));
-  wait_stream(e);
+  long long *keys_dev = nullptr;
+  const unsigned long long n = compact_dense(e, counts, ks.G, keys_dev, [&] {
+    PINOT_HIP(hipMemcpyAsync(hmatched.data(), matched, S * 8, hipMemcpyDeviceToHost, e.stream));
+    if (ks.hashed) PINOT_HIP(hipMemcpyAsync(&verify_err, a.verify_err, 4, hipMemcpyDeviceToHost, e.stream));
+  });
   if (verify_err) {  // 64-bit fingerprint collision: retry with another seed
     require(attempt < 3, PINOT_ERR_DEVICE, "group-key fingerprint collisions persist");
     return exec_group_by_fused(e, segs, q, ks_in, ga, stats, attempt + 1);
   }
   const auto tg3 = std::chrono::steady_clock::now();
-  auto tg4 = tg3;
-  int n_hll = 0;
-  for (int i = 0; i < na; i++) n_hll += gx.acc_kind[i] == 4;
-  auto res = std::make_unique<GroupByResult>();
-  res->num_columns = q.num_group_by;
-  res->functions.resize(na);
-  for (int i = 0; i < na; i++) res->functions[i] = q.aggregations[i].function;
-  res->counts.assign(na, {});
-  res->values.assign(na, {});
-  res->hll.assign(na, {});
-  res->hll_card.assign(na, {});
-  res->hll_dev_off.assign(na, 0);
-  res->gvalues = ks.gvalues;
-  res->gcard = ks.gcard;
-  res->device = e.device;
-  if (n) {
-    // device outputs and their pinned host copy live in grow-only engine buffers (no per-query allocation)
-    const size_t out_b = n * 8 * (2 + na) + (size_t)n_hll * n * 12 + 64;
-    e.group_out.reserve(out_b);
-    e.group_host.reserve(out_b);
-    auto *o_cnt = e.group_out.get<unsigned long long>();
-    auto *o_acc = o_cnt + n;
-    auto *o_hs = o_acc + n * na;
-    auto *o_hz = reinterpret_cast<uint32_t *>(o_hs + (size_t)n_hll * n);
-    auto *o_keys = reinterpret_cast<long long *>(e.group_out.get<uint8_t>() + out_b - 64 - n * 8);
-    launch_group_outputs(counts, gaggs.data(), na, keys_dev, (long long)n, o_cnt, o_acc, o_hs, o_hz, e.stream);
-    PINOT_HIP(hipGetLastError());
-    if (n_hll) {  // registers stay on the device until asked for; buffers are recycled once their result is released
-      const size_t need = (size_t)n_hll * n * 256 + 16;
-      for (auto &b : e.hll_pool)
-        if (b.use_count() == 1 && b->size() >= need) { res->hll_dev = b; break; }
-      if (!res->hll_dev) {
-        res->hll_dev = std::make_shared<DeviceBuffer>(need + need / 4);
-        if (e.hll_pool.size() < 4) e.hll_pool.push_back(res->hll_dev);
-      }
-      int h = 0;
-      for (int i = 0; i < na; i++)
-        if (gx.acc_kind[i] == 4) {
-          res->hll_dev_off[i] = (size_t)h * n * 256;
-          launch_gather_hll(static_cast<const uint8_t *>(accs[i]), keys_dev, (long long)n,
-                            res->hll_dev->get<uint8_t>() + res->hll_dev_off[i], e.stream);
-          h++;
-        }
-      for (int i = 0; i < na; i++)
-        if (alias[i] >= 0 && ga.acc_kind[i] == 4) res->hll_dev_off[i] = res->hll_dev_off[alias[i]];
-      PINOT_HIP(hipGetLastError());
-    }
-    PINOT_HIP(hipMemcpyAsync(o_keys, keys_dev, n * 8, hipMemcpyDeviceToDevice, e.stream));
-    DeviceBuffer ids;
-    if (ks.hashed) {  // group ordinals are hash slots: fetch each group's global-id tuple
-      ids.alloc(n * q.num_group_by * 4 + 16);
-      launch_hash_tuples(a, keys_dev, (long long)n, ids.get<int32_t>(), e.stream);
-      PINOT_HIP(hipGetLastError());
-      res->key_ids.resize(n * q.num_group_by);
-      PINOT_HIP(hipMemcpyAsync(res->key_ids.data(), ids.get(), n * q.num_group_by * 4, hipMemcpyDeviceToHost, e.stream));
-    }
-    PINOT_HIP(hipMemcpyAsync(e.group_host.get(), e.group_out.get(), out_b, hipMemcpyDeviceToHost, e.stream));
-    wait_stream(e);
-    tg4 = std::chrono::steady_clock::now();
-    const uint8_t *host = e.group_host.get<uint8_t>();
-    const auto *hc = reinterpret_cast<const unsigned long long *>(host);
-    const auto *hacc = hc + n;
-    const auto *hhs = hacc + n * na;
-    const auto *hhz = reinterpret_cast<const uint32_t *>(hhs + (size_t)n_hll * n);
-    const auto *hkeys = reinterpret_cast<const long long *>(host + out_b - 64 - n * 8);
-    std::vector<int> hidx(na, -1);  // HLL register-sum row of each (primary) HLL aggregation
-    for (int i = 0, h = 0; i < na; i++)
-      if (gx.acc_kind[i] == 4) hidx[i] = h++;
-    // result arrays: sized (first touch of fresh pages) and filled in parallel over the host's cores
-    if (n >= kPoolMinElems) {  // recycled arrays of released results: already-mapped pages
-      ResultPool &rp = result_pool();
-      std::lock_guard<std::mutex> lk(rp.mu);
-      res->raw_keys = take_pooled(rp.i64, n);
-      res->counts[0] = take_pooled(rp.i64, n);
-      for (int i = 0; i < na; i++) {
-        res->values[i] = take_pooled(rp.f64, n);
-        if (ga.acc_kind[i] == 4) res->hll_card[i] = take_pooled(rp.i64, n);
-      }
-    }
-    std::vector<std::function<void()>> sizing;
-    sizing.push_back([&] { res->raw_keys.resize(n); });
-    res->counts_shared = true;  // every aggregation counts the same docs per group
-    sizing.push_back([&] { res->counts[0].resize(n); });
-    for (int i = 0; i < na; i++) {
-      sizing.push_back([&, i] { res->values[i].resize(n); });
-      if (ga.acc_kind[i] == 4) sizing.push_back([&, i] { res->hll_card[i].resize(n); });
-    }
-    const size_t nt = n >= (1u << 16) ? 8 : 1;  // small results: no threads
-    if (nt > 1) parallel_tasks(sizing.size(), [&](size_t t) { sizing[t](); });
-    else
-      for (auto &f : sizing) f();
-    parallel_tasks(nt, [&](size_t t) {
-      const size_t lo = n * t / nt, hi = n * (t + 1) / nt;
-      memcpy(res->raw_keys.data() + lo, hkeys + lo, (hi - lo) * 8);
-      memcpy(res->counts[0].data() + lo, hc + lo, (hi - lo) * 8);
-      for (int i = 0; i < na; i++) {
-        double *vv = res->values[i].data();
-        const int ak = ga.acc_kind[i];
-        const int src = alias[i] >= 0 ? alias[i] : i;  // the accumulator this aggregation reads
-        const unsigned long long *raw = hacc + (size_t)src * n;
-        switch (ak) {
-          case 0:
-            for (size_t g = lo; g < hi; g++) vv[g] = (double)(int64_t)raw[g];
-            break;
-          case 1:
-            memcpy(vv + lo, raw + lo, (hi - lo) * 8);
-            break;
-          case 2:
-          case 3:
-            for (size_t g = lo; g < hi; g++) vv[g] = decode_ordered(raw[g]);
-            break;
-          case 4: {
-            const int h = hidx[src];
-            int64_t *card = res->hll_card[i].data();
-            for (size_t g = lo; g < hi; g++) {
-              card[g] = hll_cardinality_from_sum(hhs[(size_t)h * n + g], hhz[(size_t)h * n + g]);
-              vv[g] = (double)card[g];
-            }
-            break;
-          }
-          default:
-            for (size_t g = lo; g < hi; g++) vv[g] = (double)hc[g];
-            break;
-        }
-      }
-    });
-  }
+  DenseGroups dg{&q, &ks, &ga, &gx, &alias, counts, accs, 0, ks.hashed ? &a : nullptr};
+  auto res = build_dense_result(e, dg, keys_dev, n);
+  const auto tg4 = std::chrono::steady_clock::now();
   PINOT_HIP(hipEventRecord(e.ev_stop, e.stream));
   wait_stream(e);
   if (e.host_phases) {
@@ -2379,6 +2423,9 @@ void exec_group_by_layout(Engine &e, const std::vector<SegmentData *> &segs, con
   layout->num_keys = ks.G;
   layout->num_aggregations = q.num_aggregations;
   for (int a = 0; a < q.num_aggregations && a < 8; a++) layout->acc_kind[a] = ga.acc_kind[a];
+  uint64_t fp = 0;
+  for (int j = 0; j < q.num_group_by; j++) fp = fp * 1099511628211ull + dictionary_fingerprint(*segs[0]->column(q.group_by[j]));
+  layout->group_dictionary_fingerprint = fp;
 }
 
 void exec_group_by_partial(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q,
@@ -2450,6 +2497,123 @@ std::unique_ptr<GroupByResult> exec_group_by_finalize(Engine &e, const std::vect
   }
   PINOT_HIP(hipGetLastError());
   return finalize_groups(e, q, ga, ks, gp);
+}
+
+}  // namespace pinot
+
+namespace pinot {
+
+// ------------------------------------------------------------------ pieces of the multi-GPU server (server.cpp)
+void build_global_key_space(const std::vector<SegmentData *> &segs, const pinot_query &q, std::vector<int64_t> &gcard,
+                            std::vector<std::vector<std::string>> &gvalues,
+                            std::vector<std::vector<std::vector<int32_t>>> &remap, int64_t &G, bool &hashed) {
+  KeySpace ks = build_key_space(segs, q);
+  gcard = ks.gcard;
+  gvalues = std::move(ks.gvalues);
+  remap = std::move(ks.remap);
+  G = ks.G;
+  hashed = ks.hashed;
+}
+
+std::vector<int> group_acc_kind_list(const SegmentData &s, const pinot_query &q) { return group_acc_kinds(s, q).acc_kind; }
+
+bool admission_cap_can_bind(const std::vector<SegmentData *> &segs, const pinot_query &q, const Engine &e, int64_t G) {
+  return plan_admission(segs, q, e, G).cap_active;
+}
+
+void exec_group_by_partial_ks(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q,
+                              const std::vector<int64_t> &gcard, const std::vector<std::vector<std::string>> &gvalues,
+                              const std::vector<std::vector<std::vector<int32_t>>> &remap, int64_t *counts_dev,
+                              void *const *accs_dev, pinot_exec_stats *stats) {
+  require(e.use_fused, PINOT_ERR_UNSUPPORTED, "multi-GPU group-by runs on the fused path (exec.fused=1)");
+  KeySpace ks;
+  ks.gcard = gcard;
+  ks.gvalues = gvalues;
+  ks.remap = remap;
+  ks.G = 1;
+  for (auto g : gcard) ks.G *= g;
+  GroupAccs ga = group_acc_kinds(*segs[0], q);
+  const PartialOut po{counts_dev, accs_dev};
+  exec_group_by_fused(e, segs, q, ks, ga, stats, 0, &po, nullptr, true);
+}
+
+std::unique_ptr<GroupByResult> exec_group_by_slice(Engine &e, const pinot_query &q, const std::vector<int> &acc_kind,
+                                                   const std::vector<int64_t> &gcard,
+                                                   const std::vector<std::vector<std::string>> &gvalues,
+                                                   unsigned long long *counts, const std::vector<void *> &accs,
+                                                   int64_t G, int64_t key_base) {
+  KeySpace ks;
+  ks.gcard = gcard;
+  ks.gvalues = gvalues;
+  ks.G = G;
+  GroupAccs ga;
+  ga.acc_kind = acc_kind;
+  ga.acc_bytes_per_key.assign(acc_kind.size(), 0);
+  const std::vector<int> alias(acc_kind.size(), -1);
+  long long *keys_dev = nullptr;
+  const unsigned long long n = G > 0 ? compact_dense(e, counts, G, keys_dev, nullptr) : 0;
+  DenseGroups dg{&q, &ks, &ga, &ga, &alias, counts, accs, key_base, nullptr};
+  return build_dense_result(e, dg, keys_dev, n);
+}
+
+uint64_t dictionary_fingerprint(const ColumnData &c) {
+  uint64_t h = 1469598103934665603ull;  // FNV-1a over (type, cardinality, the BE dictionary bytes)
+  auto mix = [&](uint64_t v) {
+    for (int i = 0; i < 8; i++) {
+      h ^= (v >> (8 * i)) & 0xFF;
+      h *= 1099511628211ull;
+    }
+  };
+  mix((uint64_t)c.data_type);
+  mix((uint64_t)c.card);
+  for (uint8_t b : c.dict_be) {
+    h ^= b;
+    h *= 1099511628211ull;
+  }
+  return h;
+}
+
+// CombineService.mergeTwoBlocks (:48-90) over per-engine results of the same query: counts add, exact integer
+// sums add exactly (any non-exact part makes the sum a double sum), MIN / MAX compare, HLL registers max.
+void merge_agg_parts(const pinot_query &q, const std::vector<const pinot_agg_result *> &parts, pinot_agg_result *out) {
+  for (int a = 0; a < q.num_aggregations; a++) {
+    pinot_agg_result &r = out[a];
+    memset(&r, 0, sizeof(r));
+    const int f = q.aggregations[a].function;
+    __int128 isum = 0;
+    double dsum = 0.0;
+    bool exact = true;
+    double v = f == PINOT_AGG_MIN ? INFINITY : -INFINITY;
+    for (const pinot_agg_result *p : parts) {
+      const pinot_agg_result &x = p[a];
+      r.count += x.count;
+      if (f == PINOT_AGG_SUM || f == PINOT_AGG_AVG) {
+        if (x.has_exact_sum) isum += x.exact_sum;
+        else { dsum += x.value; exact = false; }
+      } else if (f == PINOT_AGG_MIN) {
+        v = std::min(v, x.value);
+      } else if (f == PINOT_AGG_MAX) {
+        v = std::max(v, x.value);
+      } else if (f == PINOT_AGG_DISTINCTCOUNTHLL) {
+        for (int j = 0; j < 256; j++) r.hll_registers[j] = std::max(r.hll_registers[j], x.hll_registers[j]);
+      }
+    }
+    if (f == PINOT_AGG_SUM || f == PINOT_AGG_AVG) {
+      if (exact) {
+        r.value = (double)isum;
+        if (isum >= INT64_MIN && isum <= INT64_MAX) {
+          r.exact_sum = (int64_t)isum;
+          r.has_exact_sum = 1;
+        }
+      } else {
+        r.value = dsum + (double)isum;
+      }
+    } else if (f == PINOT_AGG_MIN || f == PINOT_AGG_MAX) {
+      r.value = v;
+    } else if (f == PINOT_AGG_DISTINCTCOUNTHLL) {
+      r.hll_cardinality = hll_cardinality(r.hll_registers);
+    }
+  }
 }
 
 }  // namespace pinot

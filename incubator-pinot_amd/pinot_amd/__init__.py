@@ -7,6 +7,7 @@ that library, plus the segment-format writer used to feed it.
 """
 from .segment import Segment, Column, build_segment, build_column, num_bits_per_value, pack_fixed_bit  # noqa: F401
 from .pql import compile_pql, PqlCompilationException  # noqa: F401
-from .executor import (GpuEngine, GpuSegment, ServerQueryExecutor, BrokerReduce, AvgPair, HyperLogLog,  # noqa: F401
+from .executor import (GpuEngine, GpuSegment, GpuServer, ServerExecutor, ServerQueryExecutor, BrokerReduce,  # noqa: F401
+                       AvgPair, HyperLogLog,
                        ExecutionStatistics, trim_intermediate_results, final_result, format_value)
 from ._lib import PinotGpuError, load as load_library  # noqa: F401

@@ -29,6 +29,8 @@ EXPORTED_SYMBOLS = [
     "pinot_gpu_group_by_layout", "pinot_gpu_group_by_partial", "pinot_gpu_group_by_finalize",
     "pinot_gpu_segment_register_synthetic", "pinot_gpu_segment_register_synthetic_ex", "pinot_gpu_synchronize",
     "pinot_gpu_last_kernel_ms",
+    "pinot_gpu_server_create", "pinot_gpu_server_unique_id", "pinot_gpu_server_create_rank", "pinot_gpu_server_destroy",
+    "pinot_gpu_server_num_engines", "pinot_gpu_server_engine", "pinot_gpu_server_aggregate", "pinot_gpu_server_group_by",
 ]
 
 
@@ -83,9 +85,13 @@ class AggResult(C.Structure):
                 ("hll_registers", C.c_uint8 * 256)]
 
 
+class SegmentRef(C.Structure):
+    _fields_ = [("engine", C.c_int32), ("reserved", C.c_int32), ("handle", C.c_int64)]
+
+
 class PartialLayout(C.Structure):
     _fields_ = [("num_keys", C.c_int64), ("num_aggregations", C.c_int32), ("reserved", C.c_int32),
-                ("acc_kind", C.c_int32 * 8)]
+                ("acc_kind", C.c_int32 * 8), ("group_dictionary_fingerprint", C.c_uint64)]
 
 
 _lib = None
@@ -160,6 +166,16 @@ def load(path=None):
                                                           C.POINTER(i32), C.POINTER(i32), u64, C.POINTER(i64)]),
         "pinot_gpu_synchronize": (i32, [P]),
         "pinot_gpu_last_kernel_ms": (i32, [P, i32, C.POINTER(C.c_double), C.POINTER(i64)]),
+        "pinot_gpu_server_create": (i32, [C.POINTER(i32), i32, C.c_char_p, C.POINTER(P)]),
+        "pinot_gpu_server_unique_id": (i32, [P]),
+        "pinot_gpu_server_create_rank": (i32, [i32, i32, i32, P, C.c_char_p, C.POINTER(P)]),
+        "pinot_gpu_server_destroy": (i32, [P]),
+        "pinot_gpu_server_num_engines": (i32, [P]),
+        "pinot_gpu_server_engine": (i32, [P, i32, C.POINTER(P)]),
+        "pinot_gpu_server_aggregate": (i32, [P, C.POINTER(SegmentRef), i32, C.POINTER(Query), C.POINTER(AggResult),
+                                             C.POINTER(ExecStats)]),
+        "pinot_gpu_server_group_by": (i32, [P, C.POINTER(SegmentRef), i32, C.POINTER(Query), C.POINTER(P),
+                                            C.POINTER(ExecStats)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

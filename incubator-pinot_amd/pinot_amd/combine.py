@@ -10,9 +10,12 @@ box, or gloo on CPU in the tests:
   aggregation-only   a few scalars per function: int64 SUM for COUNT and for exact integer sums,
                      float64 SUM otherwise, MIN/MAX, and MAX over the 256 HLL registers.
   group-by           dense arrays over the query's global raw-key space (identical group-by
-                     dictionaries on every segment, checked by the engine): SUM over counts / int64 /
-                     float64 sums, MIN/MAX over order-preserving encodings of doubles, MAX over HLL
-                     registers (pinot_gpu_group_by_partial -> all_reduce -> pinot_gpu_group_by_finalize).
+                     dictionaries: checked within a rank by the engine, across ranks by a fingerprint in
+                     agree_layout before any data collective): SUM over counts / int64 / float64 sums, MIN/MAX
+                     over order-preserving encodings of doubles, MAX over HLL registers
+                     (pinot_gpu_group_by_partial -> agree_layout -> all_reduce -> pinot_gpu_group_by_finalize).
+The library's multi-GPU server (pinot_gpu_server_*, include/pinot_gpu.h) does the same combine with RCCL inside
+the .so, for one process over several GPUs or one process per GPU.
 
 Integer results are exact whatever the reduction order; double sums of floating-point columns
 agree within 1e-9 relative (the reference's own merge order is nondeterministic,
@@ -130,11 +133,61 @@ def allreduce_group_partials(acc_kinds, counts, accs, group=None):
             dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
 
 
-def distributed_group_by(executor, query, segments, group=None, world=1, force_collective=False, as_map=True):
-    """Group-by over this rank's GPU-resident `segments`, merged with the other ranks over RCCL.
+def agree_layout(ok, G, kinds, fingerprint, group=None, device="cpu"):
+    """Header agreement BEFORE any data collective (a rank that failed or disagrees would otherwise leave its peers
+    blocked in all_reduce, or reduce arrays of different shapes): MIN and MAX all-reduce of
+    [ok, G, fingerprint, kinds...]. A rank without segments passes G = None: it sends the reductions' identities
+    and adopts its peers' layout. Raises on EVERY rank when any rank failed or the known fields differ.
+    Returns (G, kinds) as agreed."""
+    import torch
+    dist = _dist()
+    n = 4 + 8
+    big, small = (1 << 63) - 1, -(1 << 63)
+    known = ok and G is not None
+    vals = [1 if ok else 0, G or 0, (fingerprint or 0) & ((1 << 63) - 1), len(kinds or [])] + list(kinds or []) + \
+        [0] * (8 - len(kinds or []))
+    lo = torch.tensor([vals[0]] + [v if known else big for v in vals[1:]], dtype=torch.int64, device=device)
+    hi = torch.tensor([vals[0]] + [v if known else small for v in vals[1:]], dtype=torch.int64, device=device)
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=group)
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=group)
+    lo, hi = lo.cpu().tolist(), hi.cpu().tolist()
+    if lo[0] != 1:
+        raise RuntimeError("group-by combine: a peer rank failed before the merge")
+    if lo[1] == big:
+        raise RuntimeError("group-by combine: no rank holds a segment")
+    if lo[1:] != hi[1:]:
+        raise RuntimeError("group-by combine: ranks disagree on the key space / accumulators / group-by dictionaries "
+                           "(raw keys would name different groups)")
+    return int(lo[1]), [int(x) for x in lo[4:4 + int(lo[3])]]
 
-    Runs pinot_gpu_group_by_layout / _partial into torch CUDA tensors, all-reduces them and finalises
-    on every rank (each rank ends with the full combined result map, like CombineGroupByOperator)."""
+
+def identity_partials(G, kinds, device="cpu"):
+    """Dense partials that leave a merge unchanged (a rank without segments contributes these)."""
+    import torch
+    counts = torch.zeros(G, dtype=torch.int64, device=device)
+    accs = []
+    for k in kinds:
+        if k == ACC_NONE:
+            accs.append(None)
+        elif k == ACC_F64_SUM:
+            accs.append(torch.zeros(G, dtype=torch.float64, device=device))
+        elif k == ACC_HLL:
+            accs.append(torch.zeros(G * 256, dtype=torch.uint8, device=device))
+        elif k == ACC_MIN:
+            accs.append(torch.full((G,), -1, dtype=torch.int64, device=device))  # 0xFF.. = +inf
+        else:
+            accs.append(torch.zeros(G, dtype=torch.int64, device=device))
+    return counts, accs
+
+
+def distributed_group_by(executor, query, segments, group=None, world=1, force_collective=False, as_map=True):
+    """Group-by over this rank's GPU-resident `segments`, merged with the other ranks through torch.distributed.
+
+    Runs pinot_gpu_group_by_layout / _partial into torch tensors, agrees on the layout with every rank
+    (agree_layout), all-reduces, and finalizes on every rank that holds segments (a rank without segments
+    contributes identity partials and returns an empty result). The library's own multi-GPU server
+    (pinot_gpu_server_*) does the same merge with RCCL inside the .so; this is the path for callers that already
+    run one process per GPU under a torch process group."""
     import torch
     from .executor import GroupByResult, QueryMarshal, _segment_handles
     from .pql import compile_pql
@@ -142,32 +195,43 @@ def distributed_group_by(executor, query, segments, group=None, world=1, force_c
         query = compile_pql(query)
     eng = executor.engine
     lib = eng.lib
-    m = QueryMarshal(query, executor.num_groups_limit, executor.max_init)
-    handles = _segment_handles(segments)
-    layout = _lib.PartialLayout()
-    check(lib.pinot_gpu_group_by_layout(eng.ptr, handles, len(segments), C.byref(m.q), C.byref(layout)))
-    G = int(layout.num_keys)
-    kinds = [int(layout.acc_kind[i]) for i in range(layout.num_aggregations)]
     dev = torch.device("cuda", eng.device)
-    counts = torch.empty(G, dtype=torch.int64, device=dev)
-    accs = []
-    for k in kinds:
-        if k == ACC_NONE:
-            accs.append(None)
-        elif k == ACC_F64_SUM:
-            accs.append(torch.empty(G, dtype=torch.float64, device=dev))
-        elif k == ACC_HLL:
-            accs.append(torch.empty(G * 256, dtype=torch.uint8, device=dev))
-        else:
-            accs.append(torch.empty(G, dtype=torch.int64, device=dev))
-    ptrs = (C.c_void_p * max(len(kinds), 1))(*[(a.data_ptr() if a is not None else None) for a in accs])
+    m = QueryMarshal(query, executor.num_groups_limit, executor.max_init)
+    handles = _segment_handles(segments) if segments else None
+    collective = world > 1 or force_collective
     stats = _lib.ExecStats()
-    torch.cuda.synchronize(dev)
-    check(lib.pinot_gpu_group_by_partial(eng.ptr, handles, len(segments), C.byref(m.q),
-                                         C.c_void_p(counts.data_ptr()), ptrs, C.byref(stats)))
-    if world > 1 or force_collective:
+    ok, G, kinds, fp, err = True, None, None, None, None
+    counts = accs = None
+    try:
+        if segments:
+            layout = _lib.PartialLayout()
+            check(lib.pinot_gpu_group_by_layout(eng.ptr, handles, len(segments), C.byref(m.q), C.byref(layout)))
+            G = int(layout.num_keys)
+            kinds = [int(layout.acc_kind[i]) for i in range(layout.num_aggregations)]
+            fp = int(layout.group_dictionary_fingerprint)
+            counts, accs = identity_partials(G, kinds, dev)
+            ptrs = (C.c_void_p * max(len(kinds), 1))(*[(a.data_ptr() if a is not None else None) for a in accs])
+            torch.cuda.synchronize(dev)
+            check(lib.pinot_gpu_group_by_partial(eng.ptr, handles, len(segments), C.byref(m.q),
+                                                 C.c_void_p(counts.data_ptr()), ptrs, C.byref(stats)))
+    except Exception as ex:  # every rank must still reach the agreement, then all fail together
+        ok, err = False, ex
+        if not collective:
+            raise
+    if collective:
+        try:
+            G, kinds = agree_layout(ok, G, kinds, fp, group, device=dev)
+        except Exception:
+            if err is not None:
+                raise err
+            raise
+        if counts is None:
+            counts, accs = identity_partials(G, kinds, dev)
         allreduce_group_partials(kinds, counts, accs, group)
         torch.cuda.synchronize(dev)
+    if not segments:
+        return ({} if as_map else None), stats
+    ptrs = (C.c_void_p * max(len(kinds), 1))(*[(a.data_ptr() if a is not None else None) for a in accs])
     out = C.c_void_p()
     check(lib.pinot_gpu_group_by_finalize(eng.ptr, handles, len(segments), C.byref(m.q),
                                           C.c_void_p(counts.data_ptr()), ptrs, C.byref(out)))

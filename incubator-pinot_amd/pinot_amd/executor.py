@@ -77,17 +77,27 @@ class GpuSegment:
 class GpuEngine:
     """One engine per HIP device (`QueryExecutor.init/start/shutDown`)."""
 
-    def __init__(self, device=0, config=None):
+    def __init__(self, device=0, config=None, _server_engine=None):
         self.lib = _lib.load()
+        self.index = 0
+        self.owned = _server_engine is None
+        if _server_engine is not None:  # (server, index): an engine the server owns
+            server, self.index = _server_engine
+            ptr = C.c_void_p()
+            check(self.lib.pinot_gpu_server_engine(server.ptr, self.index, C.byref(ptr)))
+            self.ptr = ptr
+            self.device = device
+            self._server = server
+            return
         ptr = C.c_void_p()
         check(self.lib.pinot_gpu_engine_create(device, config.encode() if config else None, C.byref(ptr)))
         self.ptr = ptr
         self.device = device
 
     def close(self):
-        if self.ptr:
+        if self.ptr and self.owned:
             check(self.lib.pinot_gpu_engine_destroy(self.ptr))
-            self.ptr = None
+        self.ptr = None
 
     def __del__(self):
         try:
@@ -306,6 +316,103 @@ class GroupByResult:
             for g in sel.tolist():
                 out.setdefault(keys[g], [None] * len(cols))[i] = col[g]
         return out
+
+
+class GpuServer:
+    """Multi-GPU server (pinot_gpu_server_*): one engine per device and RCCL communicators inside the library.
+
+    GpuServer(devices=[0, 1, ...]) serves several GPUs from this process; GpuServer.rank(device, nranks, rank, uid)
+    is one rank of a multi-process server (uid from GpuServer.unique_id() on rank 0, shared out of band)."""
+
+    def __init__(self, devices=(0,), config=None, _ptr=None, _devices=None):
+        self.lib = _lib.load()
+        if _ptr is None:
+            devs = (C.c_int32 * len(devices))(*devices)
+            ptr = C.c_void_p()
+            check(self.lib.pinot_gpu_server_create(devs, len(devices), config.encode() if config else None, C.byref(ptr)))
+            _ptr, _devices = ptr, list(devices)
+        self.ptr = _ptr
+        self.engines = [GpuEngine(d, _server_engine=(self, i)) for i, d in enumerate(_devices)]
+
+    @staticmethod
+    def unique_id():
+        lib = _lib.load()
+        buf = (C.c_uint8 * 128)()
+        check(lib.pinot_gpu_server_unique_id(buf))
+        return bytes(buf)
+
+    @classmethod
+    def rank(cls, device, nranks, rank, uid, config=None):
+        lib = _lib.load()
+        ptr = C.c_void_p()
+        ub = (C.c_uint8 * 128).from_buffer_copy(uid)
+        check(lib.pinot_gpu_server_create_rank(device, nranks, rank, ub, config.encode() if config else None,
+                                               C.byref(ptr)))
+        return cls(_ptr=ptr, _devices=[device])
+
+    def close(self):
+        if self.ptr:
+            for e in self.engines:
+                e.ptr = None
+            check(self.lib.pinot_gpu_server_destroy(self.ptr))
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class ServerExecutor:
+    """`ServerQueryExecutorV1Impl.processQuery` over segments spread across a GpuServer's GPUs: the library runs
+    each GPU's share and combines them (pinot_gpu_server_aggregate / _group_by)."""
+
+    def __init__(self, server: GpuServer, num_groups_limit=100000, max_init_group_holder_capacity=10000, timeout_ms=0):
+        self.server = server
+        self.num_groups_limit = num_groups_limit
+        self.max_init = max_init_group_holder_capacity
+        self.timeout_ms = timeout_ms
+
+    def _refs(self, segments):
+        arr = (_lib.SegmentRef * max(len(segments), 1))()
+        for i, s in enumerate(segments):
+            arr[i].engine = s.engine.index
+            arr[i].handle = s.handle
+        return arr
+
+    def process_query(self, query, segments, trim=True, as_result=False):
+        if isinstance(query, PreparedQuery):
+            query, m = query.query, query.marshal
+        else:
+            if isinstance(query, str):
+                query = compile_pql(query)
+            m = QueryMarshal(query, self.num_groups_limit, self.max_init, self.timeout_ms)
+        lib = self.server.lib
+        refs = self._refs(segments)
+        stats = _lib.ExecStats()
+        if query.get("group_by"):
+            out = C.c_void_p()
+            check(lib.pinot_gpu_server_group_by(self.server.ptr, refs, len(segments), C.byref(m.q), C.byref(out),
+                                                C.byref(stats)))
+            res = GroupByResult(lib, out, query)
+            if not as_result:
+                res = res.to_map(trim_top_n=query["group_by"].get("top_n", 10) if trim else None)
+        else:
+            n = len(query["aggregations"])
+            out = (_lib.AggResult * n)()
+            check(lib.pinot_gpu_server_aggregate(self.server.ptr, refs, len(segments), C.byref(m.q), out,
+                                                 C.byref(stats)))
+            res = [_agg_value(a["function"].upper(), out[i]) for i, a in enumerate(query["aggregations"])]
+        st = ExecutionStatistics(stats.num_docs_scanned, stats.num_entries_scanned_in_filter,
+                                 stats.num_entries_scanned_post_filter, stats.num_total_raw_docs,
+                                 stats.num_segments_processed, stats.device_ms, stats.host_ms)
+        return res, st
+
+    def prepare(self, query):
+        if isinstance(query, str):
+            query = compile_pql(query)
+        return PreparedQuery(query, QueryMarshal(query, self.num_groups_limit, self.max_init, self.timeout_ms))
 
 
 def _segment_handles(segments):

@@ -145,6 +145,35 @@ def _worker(rank, world, port, q):
         for t, e in zip(ta, earrays):
             if e is not None:
                 assert (t.numpy() == e).all()
+        # layout agreement before any data collective: a rank without segments adopts the peers' layout and
+        # contributes identity partials; a disagreeing rank makes EVERY rank fail (nobody blocks in all_reduce)
+        from pinot_amd.combine import agree_layout, identity_partials
+        kinds_e, counts_e, arrays_e = _dense(query, O.execute_server(segs, query)[0])
+        G = counts_e.shape[0]
+        if rank == 0:
+            Gr, kr = agree_layout(True, G, kinds, 1234)
+            _, c0, a0 = _dense(query, part)  # (counts / arrays above were merged in place)
+            mc, ma = torch.from_numpy(c0), [torch.from_numpy(a) if a is not None else None for a in a0]
+        else:
+            Gr, kr = agree_layout(True, None, None, None)
+            mc, ma = identity_partials(Gr, kr)
+        assert (Gr, kr) == (G, kinds)
+        allreduce_group_partials(kr, mc, ma)
+        ek, ec, ea = _dense(query, O.execute_server([s for s in mine] if rank == 0 else shard_segments(segs, 0, world),
+                                                    query)[0])
+        assert (mc.numpy() == ec).all()
+        for t, e in zip(ma, ea):
+            if e is not None:
+                assert (t.numpy() == e).all()
+        for bad in ("fingerprint", "failed"):
+            try:
+                if bad == "fingerprint":
+                    agree_layout(True, G, kinds, 1234 + rank)
+                else:
+                    agree_layout(rank == 0, G if rank == 1 else None, kinds if rank == 1 else None, 1234)
+                raise AssertionError("agree_layout accepted a %s peer" % bad)
+            except RuntimeError as ex:
+                assert "failed" in str(ex) or "disagree" in str(ex)
         dist.barrier()
         dist.destroy_process_group()
         q.put((rank, "ok"))

@@ -1,14 +1,18 @@
 #!/usr/bin/env python3
-"""Benchmark: rows scanned/s of the scan-filter-aggregate query on synthetic dict-encoded fact segments.
+"""Benchmark: rows scanned/s per query on synthetic dict-encoded fact segments (BASELINE.json metric).
 
-Workload (BASELINE.json configs[1]): 8 segments x 125,000,000 docs per GPU
+Default workload (BASELINE.json configs[1]): 8 segments x 125,000,000 docs per GPU
 (1B rows), 10 fixed-bit dictionary-encoded INT columns d0..d9 with cardinalities
 {16, 100, 1000, 4096, 10000, 65536, 1000, 1000, 2^20, 1000} (bits {4,7,10,12,14,16,10,10,20,10}),
 generated in HBM (seeded splitmix64), query
     SELECT COUNT(*), SUM(d8) FROM fact WHERE d2 BETWEEN 100 AND 599 AND d0 IN (1, 3, 5, 7)
-One step = one query over all of a rank's segments, results back on the host. With N ranks each
-GPU holds its own 8 segments (weak scaling, config 5 at N=8) and the per-rank partial aggregates are
-merged by an all-reduce over RCCL inside the timed region.
+--workload config4 (BASELINE.json configs[3]): the same table, the 1M-key scan-filter-group-by
+    SELECT SUM(d8), AVG(d8), DISTINCTCOUNTHLL(d5) FROM fact WHERE d2 < 800 GROUP BY d6, d7 TOP 10
+(num.groups.limit = 1,000,000 so no group is dropped).
+One step = one query over all of a rank's segments, results back on the host. With N ranks (torch.distributed.run)
+each GPU holds its own 8 segments (weak scaling; config 5 at N = 8) and the library's multi-GPU server merges
+the ranks inside the .so over RCCL (pinot_gpu_server_create_rank; the communicator id is shared through a gloo
+process group, which also carries the barriers and the max-over-ranks timing).
 
 Prints ONE JSON line (rank 0). Launched as `python bench.py` (N=1) or via torch.distributed.run.
 """
@@ -26,6 +30,8 @@ sys.path.insert(0, os.path.join(REPO, "incubator-pinot_amd"))
 COLUMNS = [("d0", 16), ("d1", 100), ("d2", 1000), ("d3", 4096), ("d4", 10000), ("d5", 65536), ("d6", 1000),
            ("d7", 1000), ("d8", 1 << 20), ("d9", 1000)]
 QUERY = "SELECT COUNT(*), SUM(d8) FROM fact WHERE d2 BETWEEN 100 AND 599 AND d0 IN (1, 3, 5, 7)"
+CONFIG4 = "SELECT SUM(d8), AVG(d8), DISTINCTCOUNTHLL(d5) FROM fact WHERE d2 < 800 GROUP BY d6, d7 TOP 10"
+CONFIG4_BYTES_PER_ROW = (10 + 10 + 10 + 20 + 16) / 8  # d2 filter + d6, d7 keys + d8 SUM/AVG + d5 HLL
 BASE_SEED = 0x5EED0000
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (8.0 TB/s spec)
 BITS = {n: max(1, (c - 1).bit_length()) for n, c in COLUMNS}
@@ -81,37 +87,107 @@ def cpu_baseline(threads, segs, docs, min_seconds=10.0):
             "check": {"count": cnt, "sum": sm}}
 
 
+def cpu_baseline_config4(threads, segs, docs, min_seconds=10.0):
+    """Reference-faithful group-by (oracle/faithful.c: per-doc readInt, INT_MAP group ids, double / AvgPair /
+    HyperLogLog holders per group, then the CombineGroupByOperator merge) on a bounded sample of the config-4
+    workload, repeated until `min_seconds` of CPU work; the median run is reported."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import faithful
+    from concurrent.futures import ThreadPoolExecutor
+    faithful.load()
+    need = ("d2", "d5", "d6", "d7", "d8")
+    t0 = time.time()
+    table = faithful.SyntheticTable(COLUMNS, docs, 0, BASE_SEED, needed=set())
+    jobs = {}
+    with ThreadPoolExecutor(threads) as ex:
+        for s in range(segs):
+            for i, (name, card) in enumerate(COLUMNS):
+                if name in need:
+                    jobs[(s, name)] = ex.submit(faithful.synth_column, BASE_SEED + s, i, card, docs)
+    table.segments = [{n: jobs[(s, n)].result() for n in need} for s in range(segs)]
+    gen_s = time.time() - t0
+    leaves = [("d2", ("RANGE", 0, 800))]
+    times = []
+    t_start = time.time()
+    while len(times) < 2 or time.time() - t_start < min_seconds:
+        t0 = time.time()
+        groups, cnt, sm = faithful.run_group_by(table, leaves, "d6", "d7", "d8", "d5", threads)
+        times.append(time.time() - t0)
+    times.sort()
+    med = times[len(times) // 2]
+    rows = segs * docs
+    return {"value": rows / med, "unit": "rows/s", "cores": threads, "kind": "port",
+            "sample": "%d segments x %d docs of the same synthetic table and config-4 query, %d runs over %.1fs "
+                      "(median %.3fs, %d groups; data generated in %.1fs); oracle/faithful.c per-doc INT_MAP "
+                      "group-by + CombineGroupByOperator merge (reference-faithful C restatement: no JVM here)" %
+                      (segs, docs, len(times), sum(times), med, groups, gen_s)}
+
+
+def kernel_source_hash():
+    """Hash of the HIP sources the PMC traffic figures were measured on (a stale profile must not be reported)."""
+    import hashlib
+    h = hashlib.sha256()
+    csrc = os.path.join(REPO, "incubator-pinot_amd", "csrc")
+    for f in sorted(os.listdir(csrc)):
+        if f.endswith((".hip", ".h")):
+            with open(os.path.join(csrc, f), "rb") as fh:
+                h.update(f.encode() + fh.read())
+    return h.hexdigest()[:16]
+
+
+def measured_traffic(workload, kernel):
+    """HBM bytes per launch of `kernel` from profiles/traffic_<workload>.json, written by
+    scripts/pmc_traffic.py from rocprofv3 FETCH_SIZE / WRITE_SIZE passes; None unless that file was measured on
+    exactly these kernel sources."""
+    path = os.path.join(REPO, "profiles", "traffic_%s.json" % workload)
+    try:
+        with open(path) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if t.get("kernel_source_hash") != kernel_source_hash():
+        return None
+    return t.get("bytes_per_launch", {}).get(kernel)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="config2", choices=("config2", "config4"))
     ap.add_argument("--segments", type=int, default=8, help="segments per GPU")
     ap.add_argument("--docs", type=int, default=125_000_000, help="docs per segment")
     ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--cpu-segments", type=int, default=16)
-    ap.add_argument("--cpu-docs", type=int, default=32_000_000)
+    ap.add_argument("--cpu-segments", type=int, default=None)
+    ap.add_argument("--cpu-docs", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--verify", action="store_true", help="check the GPU result against the C oracle (slow)")
+    ap.add_argument("--no-verify", action="store_true",
+                    help="skip the full-size check of the GPU result against the C oracle (config 2)")
     ap.add_argument("--engine-config", default="", help='engine keys, e.g. "exec.fused=0" (unfused launches)')
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     args = ap.parse_args()
+    c4 = args.workload == "config4"
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     dist = None
+    torch.cuda.set_device(local_rank if world > 1 else 0)
+    from pinot_amd import GpuEngine, GpuServer, ServerExecutor, ServerQueryExecutor
     if world > 1:
+        # control plane only (communicator id, barriers, max-over-ranks timing); the data merge is RCCL inside the .so
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        dist.init_process_group("gloo")
+        uid = torch.tensor(list(GpuServer.unique_id()) if rank == 0 else [0] * 128, dtype=torch.uint8)
+        dist.broadcast(uid, 0)
+        server = GpuServer.rank(local_rank, world, rank, bytes(uid.tolist()), args.engine_config or None)
+        eng = server.engines[0]
+        ex = ServerExecutor(server, num_groups_limit=1_000_000)
     else:
-        torch.cuda.set_device(0)
-
-    from pinot_amd import GpuEngine, ServerQueryExecutor, compile_pql
-    from pinot_amd.combine import combine_aggregation
-    eng = GpuEngine(local_rank if world > 1 else 0, args.engine_config or None)
+        eng = GpuEngine(0, args.engine_config or None)
+        ex = ServerQueryExecutor(eng, num_groups_limit=1_000_000)
     segs = []
     t0 = time.time()
     for s in range(args.segments):
@@ -119,15 +195,16 @@ def main():
         segs.append(eng.register_synthetic("fact_%d" % gidx, args.docs, COLUMNS, BASE_SEED + gidx))
     eng.synchronize()
     load_s = time.time() - t0
-    ex = ServerQueryExecutor(eng)
-    q = ex.prepare(QUERY)  # compiled + marshalled once; every step still plans and runs the device path
+    q = ex.prepare(CONFIG4 if c4 else QUERY)  # compiled + marshalled once; every step still plans and runs the device path
 
-    def step():
-        res, st = ex.process_query(q, segs)
-        if world > 1:
-            # CombineOperator across GPUs: the per-rank partial aggregates all-reduced over RCCL
-            res = combine_aggregation(q.query, res, device=torch.device("cuda", local_rank))
-        return res[0], int(res[1]), st
+    if c4:
+        def step():
+            res, st = (ex.process_query(q, segs, as_result=True) if world > 1 else ex.group_by_result(q.query, segs))
+            return res, st
+    else:
+        def step():
+            res, st = ex.process_query(q, segs)
+            return res, st
 
     for _ in range(args.warmup):
         step()
@@ -139,7 +216,7 @@ def main():
     step_ms, abi_ms = [], []
     for _ in range(args.steps):
         ts = time.perf_counter()
-        cnt, sm, st = step()  # synchronous: results are on the host when it returns
+        res, st = step()  # synchronous: results are on the host when it returns
         step_ms.append((time.perf_counter() - ts) * 1e3)
         abi_ms.append(st.host_ms)
     eng.synchronize()
@@ -148,32 +225,39 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_per_step = elapsed * 1000.0 / args.steps
     total_rows = world * args.segments * args.docs
     value = total_rows * args.steps / elapsed
 
-    # per-kernel device time (HIP events on the engine stream) in a separate pass
+    # per-kernel device time (HIP events on the engine's own stream) in a separate pass
     eng.set_config("timing=1")
     kt = {0: [0.0, 0], 1: [0.0, 0]}
     reps = max(3, min(args.steps, 10))
     for _ in range(reps):
-        ex.process_query(q, segs)
+        step()
         for k in (0, 1):
             ms, n = eng.last_kernel_ms(k)
             kt[k][0] += ms
             kt[k][1] += n
     eng.set_config("timing=0")
-    filt_b, agg_b, query_b = algorithmic_bytes(args.docs)
     kern = {}
-    if kt[1][1] == 0:
-        # fused path: ONE k_scan_query launch per query reads the three packed streams of every segment
-        # of this GPU (no bitset traffic): algorithmic bytes per launch = segments x 4.25 B/row x docs
-        names = ((0, "k_scan_query", query_b * args.segments),)
+    if c4:
+        # the group-by pipeline of one query (COUNT histogram, scan, EMIT, split, partition reduce: one timed region)
+        alg = args.segments * args.docs * CONFIG4_BYTES_PER_ROW
+        names = ((1, "group_by_pipeline", alg),)
+        query_b = alg
     else:
-        names = ((0, "k_leaf", filt_b * args.segments), (1, "k_colagg", agg_b * args.segments))
+        filt_b, agg_b, query_b1 = algorithmic_bytes(args.docs)
+        query_b = query_b1 * args.segments
+        if kt[1][1] == 0:
+            # fused path: ONE k_scan_query launch per query reads the three packed streams of every segment
+            # of this GPU (no bitset traffic): algorithmic bytes per launch = segments x 4.25 B/row x docs
+            names = ((0, "k_scan_query", query_b),)
+        else:
+            names = ((0, "k_leaf", filt_b * args.segments), (1, "k_colagg", agg_b * args.segments))
     for k, name, b in names:
         launches_per_query = max(kt[k][1] // reps, 1)
         per_launch_b = b / launches_per_query
@@ -182,16 +266,7 @@ def main():
                       "total_ms_per_query": kt[k][0] / reps,
                       "gbs": per_launch_b / (avg_ms / 1e3) / 1e9 if avg_ms > 0 else 0.0}
     dom = max(kern, key=lambda n: kern[n]["total_ms_per_query"])
-    traffic = None
-    tpath = os.path.join(REPO, "profiles", "traffic.json")
-    if os.path.exists(tpath):
-        try:
-            with open(tpath) as f:
-                traffic = json.load(f).get(dom)
-        except Exception:
-            traffic = None
-    total_alg = args.segments * query_b
-    query_gbs = total_alg / (ms_per_step / 1e3) / 1e9
+    query_gbs = query_b / (ms_per_step / 1e3) / 1e9
 
     out = {
         "metric": "rows scanned/sec per query",
@@ -206,38 +281,69 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "u32 dictIds / int64 sums",
+        "dtype": "u32 dictIds / int64 sums" + (" / u8 HLL registers" if c4 else ""),
         "data": "synthetic (seeded splitmix64 dict-encoded segments generated in HBM)",
-        "config": {"workload": "config2: %d x %d-doc segments per GPU, 10 fixed-bit INT columns, %s" %
-                   (args.segments, args.docs, QUERY),
-                   "segments_per_gpu": args.segments, "docs_per_segment": args.docs, "parallelism": "segments%d" % world},
+        "config": {"workload": "%s: %d x %d-doc segments per GPU, 10 fixed-bit INT columns, %s" %
+                   (args.workload, args.segments, args.docs, CONFIG4 if c4 else QUERY),
+                   "segments_per_gpu": args.segments, "docs_per_segment": args.docs,
+                   "parallelism": "segments%d" % world},
         "roofline": {"bound": "hbm", "achieved": kern[dom]["gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": kern[dom]["gbs"] / HBM_PEAK_GBS, "traffic": traffic, "kernel": dom,
-                     "kernels": kern, "query_algorithmic_gbs": query_gbs,
+                     "frac": kern[dom]["gbs"] / HBM_PEAK_GBS, "traffic": measured_traffic(args.workload, dom),
+                     "kernel": dom, "kernels": kern, "query_algorithmic_gbs": query_gbs,
                      "query_frac": query_gbs / HBM_PEAK_GBS},
-        "result": {"count": cnt, "sum": sm, "docs_scanned_per_rank": st.num_docs_scanned},
         "segment_load_s": load_s,
     }
+    if c4:
+        n_groups = res.num_groups()
+        counts, sums = res.function_values(1)  # AVG(d8): per-group counts and sums
+        chk, _ = ex.process_query(ex.prepare("SELECT COUNT(*), SUM(d8) FROM fact WHERE d2 < 800"), segs)
+        tot = [int(counts.sum()), int(sums.sum())]
+        if dist:  # each rank holds its key range of the merged groups
+            t = torch.tensor([n_groups] + tot, dtype=torch.int64)
+            dist.all_reduce(t)
+            n_groups, tot = int(t[0]), [int(t[1]), int(t[2])]
+        out["result"] = {"groups": n_groups, "sum_group_counts": tot[0], "sum_group_sums": tot[1]}
+        out["verify"] = {"filtered_count": chk[0], "filtered_sum": int(chk[1]),
+                         "match": tot == [chk[0], int(chk[1])] and n_groups == 1_000_000,
+                         "how": "Σ per-group counts / sums == the aggregation-only COUNT(*) / SUM(d8) of the same "
+                                "filter (independent kernel path); group-level parity: tests/test_gpu_configs.py"}
+    else:
+        out["result"] = {"count": res[0], "sum": int(res[1]), "docs_scanned": st.num_docs_scanned}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cb = cpu_baseline(args.cpu_threads, args.cpu_segments, args.cpu_docs, args.cpu_seconds)
+        if c4:
+            cb = cpu_baseline_config4(args.cpu_threads, args.cpu_segments or 16, args.cpu_docs or 4_000_000,
+                                      args.cpu_seconds)
+        else:
+            cb = cpu_baseline(args.cpu_threads, args.cpu_segments or 16, args.cpu_docs or 32_000_000, args.cpu_seconds)
         out["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample")}
         out["gpu_vs_cpu"] = value / cb["value"]
-    if args.verify and rank == 0:
+    if not c4 and not args.no_verify and rank == 0:
+        # the full-size result against the C oracle (reference-faithful executor) over every segment of every rank
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import faithful
-        tab = faithful.SyntheticTable(COLUMNS, args.docs, 0, BASE_SEED, needed=set())
+        from concurrent.futures import ThreadPoolExecutor
         tot_c, tot_s = 0, 0.0
-        for s in range(args.segments * world):
-            tab.segments = [{n: faithful.synth_column(BASE_SEED + s, i, c, args.docs)
-                             for i, (n, c) in enumerate(COLUMNS) if n in ("d0", "d2", "d8")}]
-            c, v = faithful.run_and_count_sum(tab, [("d2", ("RANGE", 100, 600)), ("d0", ("IN", [1, 3, 5, 7]))],
-                                              "d8", args.cpu_threads)
-            tot_c += c
-            tot_s += v
-        out["verify"] = {"oracle_count": tot_c, "oracle_sum": tot_s, "match": tot_c == cnt and int(tot_s) == sm}
+        names = [(i, n, c) for i, (n, c) in enumerate(COLUMNS) if n in ("d0", "d2", "d8")]
+        tab = faithful.SyntheticTable(COLUMNS, args.docs, 0, BASE_SEED, needed=set())
+        t0 = time.time()
+        with ThreadPoolExecutor(args.cpu_threads) as pool:
+            for s in range(args.segments * world):
+                cols = {n: pool.submit(faithful.synth_column, BASE_SEED + s, i, c, args.docs) for i, n, c in names}
+                tab.segments = [{n: f.result() for n, f in cols.items()}]
+                c, v = faithful.run_and_count_sum(tab, [("d2", ("RANGE", 100, 600)), ("d0", ("IN", [1, 3, 5, 7]))],
+                                                  "d8", args.cpu_threads)
+                tot_c += c
+                tot_s += v
+        agg = out["result"]
+        if dist:
+            agg = {"count": res[0], "sum": int(res[1])}  # merged over every rank by the server
+        out["verify"] = {"oracle_count": tot_c, "oracle_sum": int(tot_s), "seconds": time.time() - t0,
+                         "match": tot_c == agg["count"] and int(tot_s) == agg["sum"]}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:
+        dist.barrier()
+        server.close()
         dist.destroy_process_group()
 
 

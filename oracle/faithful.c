@@ -192,6 +192,257 @@ void pinot_faithful_run(pinot_segment_task *tasks, int ntasks, int threads, int6
   *sum = s;
 }
 
+/* ------------------------------------------------------------------ group-by (config 4 shape)
+ * AggregationGroupByOperator with DictionaryBasedGroupKeyGenerator's INT_MAP holder (cardinality product above
+ * max.init.group.holder.capacity: raw key -> group id through an open-addressing int map, first-seen order,
+ * IntMapBasedHolder.getGroupId :293-302; no group is dropped below num.groups.limit), per 10,000-doc block:
+ * fetch the group-by dictIds (readInt per doc), build raw keys (:200-209), look up group ids; SUM / AVG:
+ * DoubleGroupByResultHolder and AvgPair (sum, count) per group (SumAggregationFunction.aggregateGroupBySV :75-82,
+ * AvgAggregationFunction :110-134); DISTINCTCOUNTHLL: a HyperLogLog(8) per group fed with MurmurHash.hashLong of
+ * each doc's INT value (DistinctCountHLLAggregationFunction.aggregateGroupBySV :121-170). Then
+ * CombineGroupByOperator merges the segments' results per group (here keyed by the raw key instead of the
+ * '\t'-joined string, which only makes the baseline cheaper). */
+static inline uint32_t murmur_hash_long(int64_t data) {
+  const uint32_t m = 0x5bd1e995u;
+  uint32_t h = 0, k = (uint32_t)data * m;
+  k ^= k >> 24;
+  h ^= k * m;
+  k = (uint32_t)((uint64_t)data >> 32) * m;
+  k ^= k >> 24;
+  h *= m;
+  h ^= k * m;
+  h ^= h >> 13;
+  h *= m;
+  h ^= h >> 15;
+  return h;
+}
+
+typedef struct {
+  int32_t num_docs;
+  int nleaves;
+  const pinot_leaf *leaves;
+  const uint8_t *g0_fwd, *g1_fwd; /* group-by columns (identity INT dictionaries) */
+  int g0_bits, g1_bits;
+  int32_t g0_card;
+  const uint8_t *m_fwd;           /* SUM / AVG column */
+  int m_bits;
+  const uint8_t *h_fwd;           /* DISTINCTCOUNTHLL column */
+  int h_bits;
+  /* outputs (owned): groups in first-seen order */
+  int32_t ngroups;
+  int64_t *keys;
+  double *sum;
+  int64_t *cnt;
+  uint8_t *regs; /* [ngroups][256] */
+} pinot_group_task;
+
+static void run_group_segment(pinot_group_task *t) {
+  scan_iter its[16];
+  for (int i = 0; i < t->nleaves; i++) {
+    its[i].leaf = &t->leaves[i];
+    its[i].cur = -1;
+    its[i].end = t->num_docs - 1;
+  }
+  and_iter a = {its, t->nleaves, -1, 0};
+  int32_t *doc_ids = (int32_t *)malloc(sizeof(int32_t) * MAX_DOCS_PER_CALL);
+  int32_t *gids = (int32_t *)malloc(sizeof(int32_t) * MAX_DOCS_PER_CALL);
+  /* Int2IntOpenHashMap: power-of-two table, linear probing, key -1 = free */
+  int64_t cap = 1 << 16, cap_groups = 1 << 14, n = 0;
+  int64_t *tk = (int64_t *)malloc(sizeof(int64_t) * cap);
+  int32_t *tv = (int32_t *)malloc(sizeof(int32_t) * cap);
+  for (int64_t i = 0; i < cap; i++) tk[i] = -1;
+  int64_t *keys = (int64_t *)malloc(sizeof(int64_t) * cap_groups);
+  double *sum = (double *)malloc(sizeof(double) * cap_groups);
+  int64_t *cnt = (int64_t *)malloc(sizeof(int64_t) * cap_groups);
+  uint8_t *regs = (uint8_t *)malloc((size_t)256 * cap_groups);
+  for (;;) {
+    int nd = 0;
+    int32_t d;
+    while (nd < MAX_DOCS_PER_CALL && (d = and_next(&a)) != EOF_DOC) doc_ids[nd++] = d;
+    if (nd == 0) break;
+    for (int i = 0; i < nd; i++) {  /* generateKeysForBlock */
+      const int64_t raw = (int64_t)read_int(t->g1_fwd, doc_ids[i], t->g1_bits) * t->g0_card +
+                          read_int(t->g0_fwd, doc_ids[i], t->g0_bits);
+      uint64_t slot = (uint64_t)(raw * 0x9E3779B97F4A7C15ull) & (uint64_t)(cap - 1);
+      while (tk[slot] != -1 && tk[slot] != raw) slot = (slot + 1) & (uint64_t)(cap - 1);
+      if (tk[slot] == -1) {
+        if (n == cap_groups) {
+          cap_groups *= 2;
+          keys = (int64_t *)realloc(keys, sizeof(int64_t) * cap_groups);
+          sum = (double *)realloc(sum, sizeof(double) * cap_groups);
+          cnt = (int64_t *)realloc(cnt, sizeof(int64_t) * cap_groups);
+          regs = (uint8_t *)realloc(regs, (size_t)256 * cap_groups);
+        }
+        tk[slot] = raw;
+        tv[slot] = (int32_t)n;
+        keys[n] = raw;
+        sum[n] = 0.0;
+        cnt[n] = 0;
+        memset(regs + (size_t)256 * n, 0, 256);
+        n++;
+        if (2 * n > cap) { /* rehash at load factor 1/2 */
+          int64_t nc = cap * 2;
+          int64_t *nk = (int64_t *)malloc(sizeof(int64_t) * nc);
+          int32_t *nv = (int32_t *)malloc(sizeof(int32_t) * nc);
+          for (int64_t j = 0; j < nc; j++) nk[j] = -1;
+          for (int64_t j = 0; j < cap; j++)
+            if (tk[j] != -1) {
+              uint64_t s2 = (uint64_t)(tk[j] * 0x9E3779B97F4A7C15ull) & (uint64_t)(nc - 1);
+              while (nk[s2] != -1) s2 = (s2 + 1) & (uint64_t)(nc - 1);
+              nk[s2] = tk[j];
+              nv[s2] = tv[j];
+            }
+          free(tk);
+          free(tv);
+          tk = nk;
+          tv = nv;
+          cap = nc;
+          slot = (uint64_t)(raw * 0x9E3779B97F4A7C15ull) & (uint64_t)(cap - 1);
+          while (tk[slot] != raw) slot = (slot + 1) & (uint64_t)(cap - 1);
+        }
+      }
+      gids[i] = tv[slot];
+    }
+    for (int i = 0; i < nd; i++) { /* SUM(m) and AVG(m): dictionary value (identity) as double */
+      const double v = (double)read_int(t->m_fwd, doc_ids[i], t->m_bits);
+      sum[gids[i]] += v;
+      cnt[gids[i]] += 1;
+    }
+    for (int i = 0; i < nd; i++) { /* DISTINCTCOUNTHLL(h): offer(hashLong(value)) */
+      const uint32_t h = murmur_hash_long(read_int(t->h_fwd, doc_ids[i], t->h_bits));
+      const uint32_t j = h >> 24;
+      const uint32_t w = (h << 8) | 129u;
+      const uint8_t r = (uint8_t)(__builtin_clz(w) + 1);
+      uint8_t *g = regs + (size_t)256 * gids[i];
+      if (g[j] < r) g[j] = r;
+    }
+    if (nd < MAX_DOCS_PER_CALL) break;
+  }
+  free(doc_ids);
+  free(gids);
+  free(tk);
+  free(tv);
+  t->ngroups = (int32_t)n;
+  t->keys = keys;
+  t->sum = sum;
+  t->cnt = cnt;
+  t->regs = regs;
+}
+
+typedef struct {
+  pinot_group_task *tasks;
+  int ntasks;
+  int next;
+  pthread_mutex_t mu;
+} gpool_t;
+
+static void *gworker(void *arg) {
+  gpool_t *p = (gpool_t *)arg;
+  for (;;) {
+    pthread_mutex_lock(&p->mu);
+    int i = p->next++;
+    pthread_mutex_unlock(&p->mu);
+    if (i >= p->ntasks) break;
+    run_group_segment(&p->tasks[i]);
+  }
+  return NULL;
+}
+
+typedef struct {
+  pinot_group_task *tasks;
+  int ntasks, nthreads;
+  int64_t *mc;
+  double *ms;
+  uint8_t *mr;
+} merge_ctx_t;
+
+typedef struct {
+  merge_ctx_t *m;
+  int worker;
+  int64_t groups;
+} merge_arg_t;
+
+static void *merge_worker(void *arg) {
+  merge_arg_t *a = (merge_arg_t *)arg;
+  merge_ctx_t *m = a->m;
+  for (int i = 0; i < m->ntasks; i++) {
+    const pinot_group_task *t = &m->tasks[i];
+    for (int32_t g = 0; g < t->ngroups; g++) {
+      const int64_t k = t->keys[g];
+      if (k % m->nthreads != a->worker) continue;
+      if (!m->mc[k]) a->groups++;
+      m->mc[k] += t->cnt[g];
+      m->ms[k] += t->sum[g];
+      uint8_t *dst = m->mr + (size_t)256 * k;
+      const uint8_t *src = t->regs + (size_t)256 * g;
+      for (int j = 0; j < 256; j++)
+        if (dst[j] < src[j]) dst[j] = src[j];
+    }
+  }
+  return NULL;
+}
+
+/* Runs the group-by tasks on `threads` workers, then the combine into a dense key space of `num_keys` (counts,
+ * sums, registers merged per key). Returns the number of groups; total count / sum for the caller's check. */
+int64_t pinot_faithful_group_run(pinot_group_task *tasks, int ntasks, int threads, int64_t num_keys, int64_t *total_count,
+                                 double *total_sum) {
+  gpool_t p;
+  p.tasks = tasks;
+  p.ntasks = ntasks;
+  p.next = 0;
+  pthread_mutex_init(&p.mu, NULL);
+  if (threads < 1) threads = 1;
+  pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * threads);
+  for (int i = 0; i < threads; i++) pthread_create(&th[i], NULL, gworker, &p);
+  for (int i = 0; i < threads; i++) pthread_join(th[i], NULL);
+  free(th);
+  pthread_mutex_destroy(&p.mu);
+  /* CombineGroupByOperator: merge every segment's groups (the reference merges concurrently into one
+     ConcurrentHashMap; here `threads` workers each own the keys k with k % threads == worker) */
+  merge_ctx_t m;
+  m.tasks = tasks;
+  m.ntasks = ntasks;
+  m.nthreads = threads;
+  m.mc = (int64_t *)calloc((size_t)num_keys, sizeof(int64_t));
+  m.ms = (double *)calloc((size_t)num_keys, sizeof(double));
+  m.mr = (uint8_t *)calloc((size_t)num_keys, 256);
+  merge_arg_t *args = (merge_arg_t *)malloc(sizeof(merge_arg_t) * threads);
+  th = (pthread_t *)malloc(sizeof(pthread_t) * threads);
+  for (int i = 0; i < threads; i++) {
+    args[i].m = &m;
+    args[i].worker = i;
+    args[i].groups = 0;
+    pthread_create(&th[i], NULL, merge_worker, &args[i]);
+  }
+  int64_t groups = 0, tc = 0;
+  double tsum = 0.0;
+  for (int i = 0; i < threads; i++) {
+    pthread_join(th[i], NULL);
+    groups += args[i].groups;
+  }
+  free(th);
+  free(args);
+  for (int i = 0; i < ntasks; i++) {
+    pinot_group_task *t = &tasks[i];
+    for (int32_t g = 0; g < t->ngroups; g++) {
+      tc += t->cnt[g];
+      tsum += t->sum[g];
+    }
+    free(t->keys);
+    free(t->sum);
+    free(t->cnt);
+    free(t->regs);
+  }
+  free(m.mc);
+  free(m.ms);
+  free(m.mr);
+  *total_count = tc;
+  *total_sum = tsum;
+  return groups;
+}
+
+int pinot_faithful_group_task_size(void) { return (int)sizeof(pinot_group_task); }
+
 int32_t pinot_faithful_read_int(const uint8_t *buf, int32_t index, int bits) { return read_int(buf, index, bits); }
 
 int pinot_faithful_task_size(void) { return (int)sizeof(pinot_segment_task); }

@@ -103,3 +103,43 @@ def run_and_count_sum(table, leaves, metric, threads):
     sm = C.c_double()
     lib.pinot_faithful_run(tasks, len(table.segments), threads, C.byref(cnt), C.byref(sm))
     return cnt.value, sm.value
+
+
+class GroupTask(C.Structure):
+    _fields_ = [("num_docs", C.c_int32), ("nleaves", C.c_int), ("leaves", C.POINTER(Leaf)),
+                ("g0_fwd", C.c_void_p), ("g1_fwd", C.c_void_p), ("g0_bits", C.c_int), ("g1_bits", C.c_int),
+                ("g0_card", C.c_int32), ("m_fwd", C.c_void_p), ("m_bits", C.c_int), ("h_fwd", C.c_void_p),
+                ("h_bits", C.c_int), ("ngroups", C.c_int32), ("keys", C.c_void_p), ("sum", C.c_void_p),
+                ("cnt", C.c_void_p), ("regs", C.c_void_p)]
+
+
+def run_group_by(table, leaves, g0, g1, metric, hll_col, threads):
+    """Config-4 shape: GROUP BY g0, g1 with SUM / AVG(metric) and DISTINCTCOUNTHLL(hll_col) per segment (INT_MAP
+    holder, per-group double sums, AvgPair, HyperLogLog), then the cross-segment combine. Returns
+    (groups, total count, total sum)."""
+    lib = load()
+    lib.pinot_faithful_group_run.argtypes = [C.POINTER(GroupTask), C.c_int, C.c_int, C.c_int64,
+                                             C.POINTER(C.c_int64), C.POINTER(C.c_double)]
+    lib.pinot_faithful_group_run.restype = C.c_int64
+    assert lib.pinot_faithful_group_task_size() == C.sizeof(GroupTask)
+    keep = []
+    tasks = (GroupTask * len(table.segments))()
+    for si, cols in enumerate(table.segments):
+        arr = (Leaf * max(1, len(leaves)))()
+        for li, (col, pred) in enumerate(leaves):
+            arr[li].fwd = cols[col].ctypes.data
+            arr[li].bits = bits_for(table.card(col))
+            arr[li].kind, arr[li].lo, arr[li].hi = 0, pred[1], pred[2]
+        keep.append(arr)
+        t = tasks[si]
+        t.num_docs = table.num_docs
+        t.nleaves = len(leaves)
+        t.leaves = arr
+        t.g0_fwd, t.g0_bits, t.g0_card = cols[g0].ctypes.data, bits_for(table.card(g0)), table.card(g0)
+        t.g1_fwd, t.g1_bits = cols[g1].ctypes.data, bits_for(table.card(g1))
+        t.m_fwd, t.m_bits = cols[metric].ctypes.data, bits_for(table.card(metric))
+        t.h_fwd, t.h_bits = cols[hll_col].ctypes.data, bits_for(table.card(hll_col))
+    tc, ts = C.c_int64(), C.c_double()
+    groups = lib.pinot_faithful_group_run(tasks, len(table.segments), threads, table.card(g0) * table.card(g1),
+                                          C.byref(tc), C.byref(ts))
+    return groups, tc.value, ts.value

@@ -169,6 +169,10 @@ pinot_status pinot_gpu_engine_set_config(pinot_engine *engine, const char *confi
 pinot_status pinot_gpu_segment_register(pinot_engine *engine, const pinot_segment_desc *desc,
                                         pinot_segment_handle *out);
 pinot_status pinot_gpu_segment_release(pinot_engine *engine, pinot_segment_handle handle);
+/* Every check pinot_gpu_segment_register makes on the descriptor's bytes (dictionaries, forward-index
+ * length, sorted-index tiling, inverted-index offsets and roaring containers), on the host only: no engine,
+ * no GPU. PINOT_ERR_BAD_ARG + pinot_gpu_last_error() name the first bad column. */
+pinot_status pinot_gpu_segment_validate(const pinot_segment_desc *desc);
 /* Bytes of HBM held by a segment. */
 pinot_status pinot_gpu_segment_device_bytes(pinot_engine *engine, pinot_segment_handle handle, uint64_t *out);
 

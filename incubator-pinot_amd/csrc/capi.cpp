@@ -118,6 +118,8 @@ void parse_config(Engine &e, const char *cfg) {
     else if (k == "group.pshift") e.group_pshift = std::stoi(v);
     else if (k == "group.nt_store") e.group_nt_store = std::stoi(v) != 0;
     else if (k == "group.prefetch") e.group_prefetch = v == "1" || v == "true";
+    else if (k == "group.bucket") e.group_bucket = v == "1" || v == "true";
+    else if (k == "group.lw") e.group_lw = v == "1" || v == "true";
     else if (k == "group.split") {
       e.group_split = std::stoi(v);
       require(e.group_split >= -1 && e.group_split <= 8, PINOT_ERR_BAD_ARG, "group.split: -1 (auto) .. 8");
@@ -207,6 +209,13 @@ pinot_status pinot_gpu_segment_release(pinot_engine *engine, pinot_segment_handl
     set_device(*engine);
     PINOT_HIP(hipStreamSynchronize(engine->stream));
     require(engine->segments.erase(handle) == 1, PINOT_ERR_BAD_ARG, "unknown segment handle");
+  });
+}
+
+pinot_status pinot_gpu_segment_validate(const pinot_segment_desc *desc) {
+  return guard([&] {
+    require(desc != nullptr, PINOT_ERR_BAD_ARG, "null descriptor");
+    validate_segment(*desc);
   });
 }
 

@@ -52,6 +52,17 @@ struct ColumnData {
   double double_value(int32_t id) const;
 };
 
+// Host-side products of parse_column that register_column uploads.
+struct ParsedIndexes {
+  std::vector<int32_t> sorted_starts;         // sorted column: card + 1 range starts (last = numDocs)
+  std::vector<RoaringContainer> containers;   // inverted index: container directory of every dictId
+};
+// segment_parse.cpp: validates and decodes one column descriptor on the host (no device work).
+void parse_column(ColumnData &c, const pinot_column_desc &d, int32_t num_docs, ParsedIndexes &out);
+void validate_segment(const pinot_segment_desc &d);
+std::string java_double_to_string(double v);  // Double.toString
+std::string java_float_to_string(float v);    // Float.toString
+
 struct SegmentData {
   std::string name;
   int32_t num_docs = 0;
@@ -122,6 +133,8 @@ struct Engine {
   bool group_prefetch = true; // group.prefetch: partitioned plan loads every column of a word batch at once
   int group_pshift = -1;      // group.pshift: cap on log2 keys per partition (tests: many small partitions)
   int group_split = -1;       // group.split: log2 sub-partitions per emitted run (-1 auto, 0 single-level)
+  bool group_lw = true;       // group.lw: partitioned plan reads each lane's whole 64-doc word (no per-doc gathers)
+  bool group_bucket = true;   // group.bucket: partitioned plan EMITs through LDS buckets into the final layout
   int num_cus = 256;          // multiProcessorCount of the device
 
   // scratch (grow-only)
@@ -133,6 +146,7 @@ struct Engine {
   DeviceBuffer group_part;     // partitioned plan: histogram, offsets, partition starts, scan temp
   DeviceBuffer group_records;  // partitioned plan: (local key | dictIds) records, partition-major
   DeviceBuffer group_runs;     // two-level plan: the same records in coarse (run, block) order
+  DeviceBuffer group_filter;   // bucketed plan: the COUNT pass's filter words per segment (read back by GB_EMIT2)
   DeviceBuffer group_final;    // ordered non-empty keys + compaction scratch
   DeviceBuffer group_out;      // per-group outputs (counts, accumulators, HLL sums, keys) for the D2H
   PinnedBuffer group_host;     // their pinned host copy

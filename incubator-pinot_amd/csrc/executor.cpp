@@ -2177,7 +2177,7 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
   a.mode = gp.mode == GB_EMIT ? GB_COUNT : gp.mode;
   a.reserved2 = e.debug_emit;  // timing experiments only (debug.emit)
   a.nt_store = e.group_nt_store;
-  if (gp.mode == GB_EMIT && !ks.hashed && e.group_prefetch && e.debug_emit == 0) {
+  if (gp.mode == GB_EMIT && !ks.hashed && e.group_prefetch && (e.debug_emit == 0 || e.debug_emit >= 3)) {
     int nc = q.num_group_by;
     for (int i = 0; i < na && nc <= kGroupPfCols; i++)
       if (gx.acc_kind[i] != 5) {
@@ -2185,6 +2185,12 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
         nc++;
       }
     a.pf_nc = nc <= kGroupPfCols ? nc : 0;
+    // lane-owns-word reads: u32 keys, every read column within the decoder's widths
+    bool lw = e.group_lw && a.pf_nc > 0 && ks.G <= (long long)UINT32_MAX;
+    for (const GroupColDev &gc : gcols) lw = lw && gc.bits <= kGroupLwMaxBits;
+    for (size_t i = 0; i < gaggs.size(); i++)
+      if (gx.acc_kind[i % na] != 5) lw = lw && gaggs[i].bits <= kGroupLwMaxBits;
+    a.lw = lw ? 1 : 0;
   }
   unsigned long long *htable = nullptr, *reps = nullptr;
   if (ks.hashed) {
@@ -2254,11 +2260,22 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     void *tmp = pb + 2 * hist_b + pstart_b;
     require(max_records < (int64_t)UINT32_MAX, PINOT_ERR_UNSUPPORTED, "partitioned group-by over > 4G docs per GPU");
     e.group_records.reserve((size_t)max_records * 8 + 64);
-    if (gp.split) e.group_runs.reserve((size_t)max_records * 8 + 64);
+    // bucketed plan: COUNT keeps the filter words, GB_EMIT2 writes whole LDS buckets into the final layout
+    const bool bucket = e.group_bucket && a.pf_nc > 0 && gp.P <= kBucketMaxPartitions &&
+                        (e.debug_emit == 0 || e.debug_emit >= 3);
+    if (gp.split && !bucket) e.group_runs.reserve((size_t)max_records * 8 + 64);
+    int64_t fstride = 0;
+    if (bucket) {
+      for (auto *sg : segs) fstride = std::max<int64_t>(fstride, sg->nwords());
+      fstride = (fstride + 63) / 64 * 64;
+      e.group_filter.reserve((size_t)S * fstride * 8 + 512);
+      a.filter_out = e.group_filter.get<uint64_t>();
+      a.filter_stride = fstride;
+    }
     a.hist = hist;
     a.offsets = offsets;
     a.pstart = pstart;
-    a.emit = gp.split ? e.group_runs.get<unsigned long long>() : e.group_records.get<unsigned long long>();
+    a.emit = gp.split && !bucket ? e.group_runs.get<unsigned long long>() : e.group_records.get<unsigned long long>();
     PartitionReduceArgs ra{};
     ra.records = e.group_records.get<unsigned long long>();
     ra.pstart = pstart;
@@ -2278,11 +2295,17 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
       exclusive_sum_u32(hist, offsets, (long long)hist_n, tmp, scan_tmp, e.stream);
       launch_partition_starts(offsets, hist, (int32_t)gp.P, (int32_t)nblk, pstart, e.stream);
       GroupArgs a2 = a;
-      a2.mode = GB_EMIT;
-      a2.split = gp.split;
-      launch_group_query(a2, e.stream);
-      launch_partition_split(hist, offsets, pstart, (int32_t)gp.P, (int32_t)nblk, gp.shift, gp.split, a.emit,
-                             e.group_records.get<unsigned long long>(), e.group_nt_store, e.stream);
+      if (bucket) {
+        a2.mode = GB_EMIT2;
+        a2.stage_bytes = 0;  // no filter re-evaluation: the COUNT pass's words
+        launch_group_query(a2, e.stream);
+      } else {
+        a2.mode = GB_EMIT;
+        a2.split = gp.split;
+        launch_group_query(a2, e.stream);
+        launch_partition_split(hist, offsets, pstart, (int32_t)gp.P, (int32_t)nblk, gp.shift, gp.split, a.emit,
+                               e.group_records.get<unsigned long long>(), e.group_nt_store, e.stream);
+      }
       launch_partition_reduce(ra, e.stream);
     });
     PINOT_HIP(hipGetLastError());

@@ -56,6 +56,24 @@ __device__ __forceinline__ void hll_max_u8(uint8_t *regs, long long idx, uint32_
   }
 }
 
+// Lane of the f-th (0-based) set bit of a 64-bit lane mask (f < popcount(m)).
+__device__ __forceinline__ int select_bit(uint64_t m, int f) {
+  int pos = 0;
+#pragma unroll
+  for (int w = 32; w >= 1; w >>= 1) {
+    const uint64_t low = m & ((1ull << w) - 1ull);
+    const int c = __popcll(low);
+    if (f >= c) {
+      f -= c;
+      m >>= w;
+      pos += w;
+    } else {
+      m = low;
+    }
+  }
+  return pos;
+}
+
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
   const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)v, l);
   const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
@@ -265,6 +283,79 @@ __device__ __forceinline__ void group_chunk(const GroupArgs &a, const GroupSegme
   }
 }
 
+// The sink of U docs per lane (act: the doc passes filter and admission; key: its raw key; rec: its aggregated
+// fields, local key bits still clear).
+template <int MODE, int U>
+__device__ __forceinline__ void group_sink(const GroupArgs &a, uint32_t *plds, const bool (&act)[U],
+                                           const unsigned long long (&key)[U], const unsigned long long (&rec)[U],
+                                           int lane) {
+  const int rshift = a.shift + a.split;
+  if constexpr (MODE == GB_COUNT) {
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      if (act[u]) atomicAdd(&plds[key[u] >> a.shift], 1u);
+  } else if constexpr (MODE == GB_EMIT2) {
+    if (a.reserved2 == 4) return;  // debug.emit=4 (timing only, wrong results): reads + decode, no sink
+    const bool st = a.reserved2 != 3;  // debug.emit=3: bucket logic without the global stores
+    // LDS [cursor P][count P][written P][bucket P x kBucketRecs]. Per batch of U words: every record claims a
+    // slot (count), writes it and bumps `written`; the record that completes a bucket (written ==
+    // kBucketRecs - 1) flushes it: the wave moves its flushers' buckets out eight lanes per bucket (one coalesced
+    // 64-B piece each) to the block's next run positions, then reopens them. A record that finds its bucket full
+    // (only when one batch brings more than kBucketRecs records of a partition) goes straight to its run slot.
+    uint32_t *cur = plds, *cnt = plds + a.P, *wrt = plds + 2 * a.P;
+    unsigned long long *bkt = reinterpret_cast<unsigned long long *>(plds + ((3 * a.P + 1) & ~1));
+    uint32_t p[U], pos[U];
+    unsigned long long r[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      p[u] = act[u] ? (uint32_t)(key[u] >> a.shift) : 0u;
+      r[u] = rec[u] | (key[u] & ((1ull << a.shift) - 1ull));
+      pos[u] = atomicAdd(&cnt[p[u]], act[u] ? 1u : 0u);
+    }
+    bool fl[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      fl[u] = false;
+      if (act[u] && pos[u] < (uint32_t)kBucketRecs) {
+        bkt[p[u] * kBucketRecs + pos[u]] = r[u];
+        fl[u] = __hip_atomic_fetch_add(&wrt[p[u]], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP) ==
+                (uint32_t)kBucketRecs - 1;
+      } else if (act[u]) {
+        const uint32_t d = atomicAdd(&cur[p[u]], 1u);
+        if (st) a.emit[d] = r[u];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t fm = __ballot(fl[u]);
+      if (!fm) continue;  // uniform
+      const uint32_t dst = fl[u] ? atomicAdd(&cur[p[u]], (uint32_t)kBucketRecs) : 0u;
+      const int nf = __popcll(fm);
+      for (int f0 = 0; f0 < nf; f0 += 64 / kBucketRecs) {  // uniform: 8 buckets per wave instruction
+        const int f = min(f0 + lane / kBucketRecs, nf - 1), i = lane % kBucketRecs;
+        const int src = select_bit(fm, f);
+        const uint32_t pf = (uint32_t)__shfl((int)p[u], src, 64), df = (uint32_t)__shfl((int)dst, src, 64);
+        if (st && f0 + lane / kBucketRecs < nf) a.emit[df + i] = bkt[pf * kBucketRecs + i];
+      }
+      if (fl[u]) {
+        __hip_atomic_store(&wrt[p[u]], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_store(&cnt[p[u]], 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
+  } else {
+    uint32_t pos[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) pos[u] = atomicAdd(&plds[key[u] >> rshift], act[u] ? 1u : 0u);
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      if (act[u]) {
+        const unsigned long long r = rec[u] | (key[u] & ((1ull << rshift) - 1ull));
+        if (a.nt_store) __builtin_nontemporal_store(r, a.emit + pos[u]);
+        else a.emit[pos[u]] = r;
+      }
+  }
+}
+
 // GB_COUNT / GB_EMIT with every needed column prefetched: one global-memory round trip per kGroupPfUnroll
 // words instead of one per column (the per-doc reads are latency-bound).
 constexpr int kGroupPfUnroll = 4;
@@ -274,6 +365,7 @@ __device__ __forceinline__ void group_chunk_pf(const GroupArgs &a, const GroupSe
                                                int lane, uint32_t *plds) {
   constexpr int C = kGroupPfCols, U = kGroupPfUnroll;
   const int nc = MODE == GB_COUNT ? a.n_gcols : a.pf_nc;
+  typedef uint32_t u32x2a __attribute__((ext_vector_type(2), aligned(4)));
   const uint8_t *fwd[C];
   const int32_t *remap[C];
   unsigned long long stride[C];
@@ -298,7 +390,6 @@ __device__ __forceinline__ void group_chunk_pf(const GroupArgs &a, const GroupSe
       fshift[c] = ag.field_shift;
     }
   }
-  const int rshift = a.shift + a.split;
   for (int w0 = 0; w0 < 64; w0 += U) {
     uint64_t mw[U];
     bool any = false;
@@ -320,10 +411,11 @@ __device__ __forceinline__ void group_chunk_pf(const GroupArgs &a, const GroupSe
     for (int c = 0; c < C; c++)
       if (c < nc) {
 #pragma unroll
-        for (int u = 0; u < U; u++) {
-          const uint32_t *p = reinterpret_cast<const uint32_t *>(fwd[c]) + (((uint64_t)doc[u] * (uint32_t)bits[c]) >> 5);
-          lo[c][u] = p[0];
-          hi[c][u] = p[1];
+        for (int u = 0; u < U; u++) {  // one 8-byte load per doc and column (the dword pair holding its bits)
+          const u32x2a x = *reinterpret_cast<const u32x2a *>(reinterpret_cast<const uint32_t *>(fwd[c]) +
+                                                             (((uint64_t)doc[u] * (uint32_t)bits[c]) >> 5));
+          lo[c][u] = x.x;
+          hi[c][u] = x.y;
         }
       }
     unsigned long long key[U], rec[U];
@@ -345,22 +437,140 @@ __device__ __forceinline__ void group_chunk_pf(const GroupArgs &a, const GroupSe
 #pragma unroll
       for (int u = 0; u < U; u++) act[u] = act[u] && ((sg.admitted[key[u] >> 5] >> (key[u] & 31)) & 1u);
     }
-    if constexpr (MODE == GB_COUNT) {
+    group_sink<MODE, U>(a, plds, act, key, rec, lane);
+  }
+}
+
+// ---------------------------------------------------------------- lane-owns-word path
+// Each lane takes the 64-doc word its filter mask already describes: per half (32 docs) and column it reads
+// the B contiguous dwords holding those docs' bits (a wave's reads cover the chunk's 256*B bytes exactly once,
+// no per-doc gathers), decodes them with compile-time shifts and folds them into the docs' keys / records; the
+// sink then walks the 32 docs of the half, four at a time across the wave.
+typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
+typedef uint32_t u32x2a_ __attribute__((ext_vector_type(2), aligned(4)));
+
+// Quarter Q (docs 16Q..16Q+15) of a half: only the dwords holding its bits are read.
+template <int B, int Q>
+__device__ __forceinline__ void load_quarter(const uint8_t *fwd, int64_t half, uint32_t (&D)[B]) {
+  constexpr int k0 = (16 * Q * B) >> 5, k1 = (16 * (Q + 1) * B - 1) >> 5;
+  const uint32_t *p = reinterpret_cast<const uint32_t *>(fwd) + half * B;
+  int k = k0;
 #pragma unroll
-      for (int u = 0; u < U; u++)
-        if (act[u]) atomicAdd(&plds[key[u] >> a.shift], 1u);
-    } else {
-      uint32_t pos[U];
+  for (; k + 3 <= k1; k += 4) {
+    const u32x4a x = *reinterpret_cast<const u32x4a *>(p + k);
+    D[k] = bswap32(x.x);
+    D[k + 1] = bswap32(x.y);
+    D[k + 2] = bswap32(x.z);
+    D[k + 3] = bswap32(x.w);
+  }
 #pragma unroll
-      for (int u = 0; u < U; u++) pos[u] = atomicAdd(&plds[key[u] >> rshift], act[u] ? 1u : 0u);
+  for (; k + 1 <= k1; k += 2) {
+    const u32x2a_ x = *reinterpret_cast<const u32x2a_ *>(p + k);
+    D[k] = bswap32(x.x);
+    D[k + 1] = bswap32(x.y);
+  }
+  if (k == k1) D[k] = bswap32(p[k]);
+}
+
+template <int B, int J, int JEND, typename F>
+__device__ __forceinline__ void decode_apply(const uint32_t (&D)[B], F &f) {
+  constexpr int q = J * B, k = q >> 5, o = q & 31;
+  constexpr uint32_t mask = (uint32_t)((1ull << B) - 1ull);
+  if constexpr (o + B <= 32) f.template put<J & 15>((D[k] >> (32 - o - B)) & mask);
+  else f.template put<J & 15>(__builtin_amdgcn_alignbit(D[k], D[k + 1], 64 - o - B) & mask);
+  if constexpr (J + 1 < JEND) decode_apply<B, J + 1, JEND>(D, f);
+}
+
+struct KeyFold {  // raw key += global id * stride (DictionaryBasedGroupKeyGenerator's mixed radix)
+  uint32_t (&key)[16];
+  const int32_t *remap;
+  uint32_t stride;
+  template <int J>
+  __device__ __forceinline__ void put(uint32_t id) {
+    key[J] += (remap ? (uint32_t)remap[id] : id) * stride;
+  }
+};
+
+struct FieldFold {  // record |= dictId << field_shift
+  unsigned long long (&rec)[16];
+  int shift;
+  template <int J>
+  __device__ __forceinline__ void put(uint32_t id) {
+    rec[J] |= (unsigned long long)id << shift;
+  }
+};
+
+template <int Q, typename F>
+__device__ __forceinline__ void decode_column_quarter(const uint8_t *fwd, int bits, int64_t half, F &f) {
+#define PINOT_LW(B)                       \
+  {                                       \
+    uint32_t D[B];                        \
+    load_quarter<B, Q>(fwd, half, D);     \
+    decode_apply<B, 16 * Q, 16 * Q + 16>(D, f); \
+  }
+  switch (bits) {  // widths up to kGroupLwMaxBits (the host routes wider columns through group_chunk_pf)
+    case 1: PINOT_LW(1); break;   case 2: PINOT_LW(2); break;   case 3: PINOT_LW(3); break;   case 4: PINOT_LW(4); break;
+    case 5: PINOT_LW(5); break;   case 6: PINOT_LW(6); break;   case 7: PINOT_LW(7); break;   case 8: PINOT_LW(8); break;
+    case 9: PINOT_LW(9); break;   case 10: PINOT_LW(10); break; case 11: PINOT_LW(11); break; case 12: PINOT_LW(12); break;
+    case 13: PINOT_LW(13); break; case 14: PINOT_LW(14); break; case 15: PINOT_LW(15); break; case 16: PINOT_LW(16); break;
+    case 17: PINOT_LW(17); break; case 18: PINOT_LW(18); break; case 19: PINOT_LW(19); break; case 20: PINOT_LW(20); break;
+    default: break;
+  }
+#undef PINOT_LW
+}
+
+template <int MODE, int Q>
+__device__ __forceinline__ void group_quarter_lw(const GroupArgs &a, const GroupSegment &sg, int64_t half, uint32_t mq,
+                                                 int lane, uint32_t *plds) {
+  constexpr int U = kGroupPfUnroll;
+  const int nc = MODE == GB_COUNT ? a.n_gcols : a.pf_nc;
+  uint32_t key[16];
+  unsigned long long rec[16];
 #pragma unroll
-      for (int u = 0; u < U; u++)
-        if (act[u]) {
-          const unsigned long long r = rec[u] | (key[u] & ((1ull << rshift) - 1ull));
-          if (a.nt_store) __builtin_nontemporal_store(r, a.emit + pos[u]);
-          else a.emit[pos[u]] = r;
-        }
+  for (int j = 0; j < 16; j++) {
+    key[j] = 0;
+    rec[j] = 0;
+  }
+#pragma unroll 1
+  for (int c = 0; c < nc; c++) {  // uniform
+    if (c < a.n_gcols) {
+      const GroupColDev gc = load_const(a.gcols + sg.first_gcol + c);
+      KeyFold f{key, gc.remap, (uint32_t)gc.stride};
+      decode_column_quarter<Q>(gc.fwd, gc.bits, half, f);
+    } else if constexpr (MODE != GB_COUNT) {
+      const int ai = c == 1 ? a.pf_agg[1] : c == 2 ? a.pf_agg[2] : a.pf_agg[3];
+      const GroupAggDev ag = load_const(a.aggs + sg.first_agg + ai);
+      FieldFold f{rec, ag.field_shift};
+      decode_column_quarter<Q>(ag.fwd, ag.bits, half, f);
     }
+  }
+#pragma unroll
+  for (int j0 = 0; j0 < 16; j0 += U) {
+    bool act[U];
+    unsigned long long k[U], r[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      act[u] = (mq >> (j0 + u)) & 1u;
+      k[u] = key[j0 + u];
+      r[u] = rec[j0 + u];
+    }
+    if (sg.admitted) {
+#pragma unroll
+      for (int u = 0; u < U; u++) act[u] = act[u] && ((sg.admitted[k[u] >> 5] >> (k[u] & 31)) & 1u);
+    }
+    group_sink<MODE, U>(a, plds, act, k, r, lane);
+  }
+}
+
+template <int MODE>
+__device__ __forceinline__ void group_chunk_lw(const GroupArgs &a, const GroupSegment &sg, int64_t ch, uint64_t mask,
+                                               int lane, uint32_t *plds) {
+  const int64_t word = ch * 64 + lane;
+#pragma unroll 1
+  for (int h = 0; h < 2; h++) {
+    const uint32_t mh = (uint32_t)(mask >> (32 * h));
+    if (__any((mh & 0xFFFFu) != 0)) group_quarter_lw<MODE, 0>(a, sg, word * 2 + h, mh & 0xFFFFu, lane, plds);
+    if (__any((mh >> 16) != 0)) group_quarter_lw<MODE, 1>(a, sg, word * 2 + h, mh >> 16, lane, plds);
   }
 }
 
@@ -415,8 +625,12 @@ __device__ __forceinline__ void flush_group_lds(const GroupArgs &a, const GroupS
   }
 }
 
-template <int MODE, bool PF = false>
-__global__ __launch_bounds__(kGroupBlock) void k_group_query(GroupArgs a) {
+// PATH: 0 = per-column loop, 1 = per-doc prefetch (group_chunk_pf), 2 = lane-owns-word (group_chunk_lw).
+// A block walks groups of kGroupWaves consecutive chunks with stride bps * kGroupWaves whatever its wave count,
+// so blocks of every BLK own the same chunks (the COUNT pass's per-block histograms stay valid for EMIT).
+template <int MODE, int PATH = 0, int BLK = kGroupBlock>
+__global__ __launch_bounds__(BLK) void k_group_query(GroupArgs a) {
+  constexpr int NW = BLK / 64;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = blockIdx.x / a.bps, b = blockIdx.x % a.bps;
@@ -424,19 +638,27 @@ __global__ __launch_bounds__(kGroupBlock) void k_group_query(GroupArgs a) {
   const GroupSegment sg = load_const(a.segs + g);
   const FusedStep *leaves = a.leaves + sg.first_leaf;
   uint8_t *stage = lds + wave * a.stage_bytes;
-  uint8_t *acc_lds = lds + (size_t)kGroupWaves * a.stage_bytes;
+  uint8_t *acc_lds = lds + (size_t)NW * a.stage_bytes;
   uint32_t *plds = reinterpret_cast<uint32_t *>(acc_lds);
   if constexpr (MODE == GB_LDS) init_group_lds(a, sg, acc_lds, tid);
   if constexpr (MODE == GB_COUNT) {
-    for (int p = tid; p < a.P; p += kGroupBlock) plds[p] = 0;
+    for (int p = tid; p < a.P; p += BLK) plds[p] = 0;
+    __syncthreads();
+  }
+  if constexpr (MODE == GB_EMIT2) {
+    for (int p = tid; p < a.P; p += BLK) {
+      plds[p] = a.offsets[(size_t)p * nblk + blockIdx.x];
+      plds[a.P + p] = 0;
+      plds[2 * a.P + p] = 0;
+    }
     __syncthreads();
   }
   if constexpr (MODE == GB_EMIT) {
     if (a.split == 0) {
-      for (int p = tid; p < a.P; p += kGroupBlock) plds[p] = a.offsets[(size_t)p * nblk + blockIdx.x];
+      for (int p = tid; p < a.P; p += BLK) plds[p] = a.offsets[(size_t)p * nblk + blockIdx.x];
     } else {  // coarse run (q, block) starts where run q starts + this block's share of q's earlier blocks
       const int F = 1 << a.split, Q = (a.P + F - 1) >> a.split;
-      for (int q = tid; q < Q; q += kGroupBlock) {
+      for (int q = tid; q < Q; q += BLK) {
         uint32_t c = a.pstart[q * F];
         for (int p = q * F; p < min(a.P, (q + 1) * F); p++) c += a.offsets[(size_t)p * nblk + blockIdx.x] - a.pstart[p];
         plds[q] = c;
@@ -446,29 +668,80 @@ __global__ __launch_bounds__(kGroupBlock) void k_group_query(GroupArgs a) {
   }
   const int64_t nchunks = min((sg.nwords + 63) >> 6, sg.ch_end);
   unsigned long long matched = 0;
-  for (int64_t ch = sg.ch_begin + (int64_t)b * kGroupWaves + wave; ch < nchunks; ch += (int64_t)a.bps * kGroupWaves) {
-    uint64_t mask = chunk_word(sg.pre, sg.nwords, sg.num_docs, ch, lane);
-    mask = eval_filter<true, 12>(leaves, sg.n_leaves, mask, ch * 64 + lane, sg.nwords, sg.num_docs, lane,
-                             [&](int, const FusedStep &st) -> const uint8_t * {
-                               stage_chunk_rt(st.fwd, st.bits, ch, stage, lane);
-                               wait_stage();
-                               return stage;
-                             });
+  for (int64_t ch0 = sg.ch_begin + (int64_t)b * kGroupWaves; ch0 < nchunks; ch0 += (int64_t)a.bps * kGroupWaves)
+  for (int i = wave; i < kGroupWaves; i += NW) {
+    const int64_t ch = ch0 + i;
+    if (ch >= nchunks) break;  // uniform
+    uint64_t mask;
+    const int64_t w = ch * 64 + lane;
+    if constexpr (MODE == GB_EMIT2) {  // the filter words the COUNT pass wrote
+      mask = w < sg.nwords ? a.filter_out[(size_t)g * a.filter_stride + w] : 0ull;
+    } else {
+      mask = chunk_word(sg.pre, sg.nwords, sg.num_docs, ch, lane);
+      mask = eval_filter<true, 12>(leaves, sg.n_leaves, mask, w, sg.nwords, sg.num_docs, lane,
+                                   [&](int, const FusedStep &st) -> const uint8_t * {
+                                     stage_chunk_rt(st.fwd, st.bits, ch, stage, lane);
+                                     wait_stage();
+                                     return stage;
+                                   });
+      if (MODE == GB_COUNT && a.filter_out && w < sg.nwords) a.filter_out[(size_t)g * a.filter_stride + w] = mask;
+    }
     matched += __popcll(mask);
     if (__any(mask != 0)) {
-      if constexpr (PF) group_chunk_pf<MODE>(a, sg, ch, mask, lane, plds);
+      if constexpr (PATH == 2) group_chunk_lw<MODE>(a, sg, ch, mask, lane, plds);
+      else if constexpr (PATH == 1) group_chunk_pf<MODE>(a, sg, ch, mask, lane, plds);
       else group_chunk<MODE>(a, sg, ch, mask, lane, acc_lds, plds);
     }
   }
   matched = wave_sum(matched);  // the EMIT pass re-reads what the COUNT pass already counted
-  if (MODE != GB_EMIT && MODE != GB_VERIFY && MODE != GB_FIRST && lane == 0 && matched) atomicAdd(a.matched + g, matched);
+  if (MODE != GB_EMIT && MODE != GB_EMIT2 && MODE != GB_VERIFY && MODE != GB_FIRST && lane == 0 && matched)
+    atomicAdd(a.matched + g, matched);
+  if constexpr (MODE == GB_EMIT2) {  // the partially filled buckets, 8 lanes per bucket
+    __syncthreads();
+    const unsigned long long *bkt = reinterpret_cast<const unsigned long long *>(plds + ((3 * a.P + 1) & ~1));
+    const int i = tid % kBucketRecs;
+    for (int p = tid / kBucketRecs; p < a.P; p += BLK / kBucketRecs)
+      if ((uint32_t)i < plds[a.P + p]) a.emit[plds[p] + i] = bkt[p * kBucketRecs + i];
+  }
   if constexpr (MODE == GB_LDS) flush_group_lds(a, sg, acc_lds, tid);
   if constexpr (MODE == GB_COUNT) {
     __syncthreads();
-    for (int p = tid; p < a.P; p += kGroupBlock) a.hist[(size_t)p * nblk + blockIdx.x] = plds[p];
+    for (int p = tid; p < a.P; p += BLK) a.hist[(size_t)p * nblk + blockIdx.x] = plds[p];
   }
 }
 
+// Lane-owns-word EMIT kernels run 512-thread blocks (their 32-doc key / record arrays need the registers).
+constexpr int kGroupLwEmitBlock = 512;
+
+static int group_block_threads(const GroupArgs &a) {
+  return (a.lw && (a.mode == GB_EMIT || a.mode == GB_EMIT2)) ? kGroupLwEmitBlock : kGroupBlock;
+}
+
+// Every instance launch_group_query may pick for `a`, through one visitor (occupancy and launch agree).
+template <typename V>
+static void with_group_kernel(const GroupArgs &a, V &&v) {
+  const bool lw = a.lw && a.pf_nc > 0;
+  switch (a.mode) {
+    case GB_GLOBAL: v(&k_group_query<GB_GLOBAL, 0, kGroupBlock>, kGroupBlock); break;
+    case GB_LDS: v(&k_group_query<GB_LDS, 0, kGroupBlock>, kGroupBlock); break;
+    case GB_COUNT:
+      if (lw) v(&k_group_query<GB_COUNT, 2, kGroupBlock>, kGroupBlock);
+      else if (a.pf_nc > 0) v(&k_group_query<GB_COUNT, 1, kGroupBlock>, kGroupBlock);
+      else v(&k_group_query<GB_COUNT, 0, kGroupBlock>, kGroupBlock);
+      break;
+    case GB_EMIT:
+      if (lw) v(&k_group_query<GB_EMIT, 2, kGroupLwEmitBlock>, kGroupLwEmitBlock);
+      else if (a.pf_nc > 0) v(&k_group_query<GB_EMIT, 1, kGroupBlock>, kGroupBlock);
+      else v(&k_group_query<GB_EMIT, 0, kGroupBlock>, kGroupBlock);
+      break;
+    case GB_FIRST: v(&k_group_query<GB_FIRST, 0, kGroupBlock>, kGroupBlock); break;
+    case GB_EMIT2:
+      if (lw) v(&k_group_query<GB_EMIT2, 2, kGroupLwEmitBlock>, kGroupLwEmitBlock);
+      else v(&k_group_query<GB_EMIT2, 1, kGroupBlock>, kGroupBlock);
+      break;
+    default: v(&k_group_query<GB_VERIFY, 0, kGroupBlock>, kGroupBlock); break;
+  }
+}
 
 }  // namespace
 
@@ -476,38 +749,24 @@ size_t group_query_lds_bytes(const GroupArgs &a) {
   size_t acc = 0;
   if (a.mode == GB_LDS) acc = (size_t)a.lds_acc_bytes;
   if (a.mode == GB_COUNT || a.mode == GB_EMIT) acc = (size_t)a.P * 4;
-  return (size_t)kGroupWaves * a.stage_bytes + acc;
+  if (a.mode == GB_EMIT2) acc = (size_t)((3 * a.P + 1) & ~1) * 4 + (size_t)a.P * 8 * kBucketRecs;
+  return (size_t)(group_block_threads(a) / 64) * a.stage_bytes + acc;
 }
 
 int group_query_blocks_per_cu(const GroupArgs &a) {
   int n = 0;
   const size_t lds = group_query_lds_bytes(a);
   hipError_t err = hipErrorInvalidValue;
-  switch (a.mode) {
-    case GB_GLOBAL: err = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_group_query<GB_GLOBAL>, kGroupBlock, lds); break;
-    case GB_LDS: err = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_group_query<GB_LDS>, kGroupBlock, lds); break;
-    case GB_COUNT: err = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_group_query<GB_COUNT>, kGroupBlock, lds); break;
-    case GB_FIRST: err = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_group_query<GB_FIRST>, kGroupBlock, lds); break;
-    default: err = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_group_query<GB_EMIT>, kGroupBlock, lds); break;
-  }
+  with_group_kernel(a, [&](auto kern, int threads) { err = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, threads, lds); });
   return (err != hipSuccess || n < 1) ? 1 : n;
 }
 
 void launch_group_query(const GroupArgs &a, hipStream_t stream) {
   if (a.nsegs <= 0 || a.bps <= 0) return;
-  const dim3 grid((unsigned)(a.nsegs * a.bps)), block(kGroupBlock);
   const size_t lds = group_query_lds_bytes(a);
-  switch (a.mode) {
-    case GB_GLOBAL: hipLaunchKernelGGL(k_group_query<GB_GLOBAL>, grid, block, lds, stream, a); break;
-    case GB_LDS: hipLaunchKernelGGL(k_group_query<GB_LDS>, grid, block, lds, stream, a); break;
-    case GB_COUNT: hipLaunchKernelGGL(k_group_query<GB_COUNT>, grid, block, lds, stream, a); break;  // 2 columns: no gain
-    case GB_EMIT:
-      if (a.pf_nc > 0) hipLaunchKernelGGL((k_group_query<GB_EMIT, true>), grid, block, lds, stream, a);
-      else hipLaunchKernelGGL(k_group_query<GB_EMIT>, grid, block, lds, stream, a);
-      break;
-    case GB_FIRST: hipLaunchKernelGGL(k_group_query<GB_FIRST>, grid, block, lds, stream, a); break;
-    default: hipLaunchKernelGGL(k_group_query<GB_VERIFY>, grid, block, lds, stream, a); break;
-  }
+  with_group_kernel(a, [&](auto kern, int threads) {
+    hipLaunchKernelGGL(kern, dim3((unsigned)(a.nsegs * a.bps)), dim3(threads), lds, stream, a);
+  });
 }
 
 namespace {

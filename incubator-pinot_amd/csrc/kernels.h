@@ -185,7 +185,12 @@ int scan_query_blocks_per_cu(int stage_bytes, bool gathers, bool pipelined);
 //              slot's representative doc (a 64-bit fingerprint collision is detected, never merged)
 //   GB_FIRST   num.groups.limit admission: first_doc[segment][key] = smallest matching doc of the key
 //              (a plain read first; atomicMin only when the doc is earlier)
-enum GroupMode : int32_t { GB_GLOBAL = 0, GB_LDS = 1, GB_COUNT = 2, GB_EMIT = 3, GB_VERIFY = 4, GB_FIRST = 5 };
+//   GB_EMIT2   pass 2 of the bucketed partitioned plan: the filter words GB_COUNT wrote (no filter re-evaluation),
+//              records appended to per-block LDS buckets of kBucketRecs records per partition and written out
+//              whole into the FINAL partition layout (offsets from GB_COUNT's histogram): no split pass
+enum GroupMode : int32_t { GB_GLOBAL = 0, GB_LDS = 1, GB_COUNT = 2, GB_EMIT = 3, GB_VERIFY = 4, GB_FIRST = 5, GB_EMIT2 = 6 };
+constexpr int kBucketRecs = 8;                                   // 64-B bucket flushes
+constexpr int kBucketMaxPartitions = 2040;                       // P x (3 x 4 + 8 x 8) B of LDS per block <= 155 KB
 // accumulator kinds (acc_kind): 0 int64 sum, 1 double sum, 2 ordered-u64 min, 3 ordered-u64 max,
 // 4 HLL registers (u8 [G][256]), 5 none (COUNT / AVG count share `counts`)
 constexpr int kMaxGroupAggs = 8;
@@ -257,8 +262,12 @@ struct GroupArgs {
   int32_t pf_nc;
   int32_t pf_agg[4];
   int32_t nt_store;            // GB_EMIT / split: records stored with the non-temporal (streaming) policy
+  int32_t lw;                  // GB_COUNT / GB_EMIT / GB_EMIT2 with pf_nc > 0: lane-owns-word reads (G < 2^32)
+  uint64_t *filter_out;        // GB_COUNT: writes each segment's filter words here (GB_EMIT2 reads them back)
+  int64_t filter_stride;       // words per segment in filter_out
 };
 constexpr int kGroupPfCols = 4;
+constexpr int kGroupLwMaxBits = 20;  // widest column the lane-owns-word decode handles
 void launch_group_query(const GroupArgs &a, hipStream_t stream);
 // Grid (blocks per segment x segments) the host sizes `hist` / `offsets` for.
 int group_query_blocks_per_cu(const GroupArgs &a);

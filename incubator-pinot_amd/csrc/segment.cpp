@@ -16,37 +16,6 @@
 
 namespace pinot {
 
-std::string ColumnData::string_value(int32_t id) const {
-  switch (data_type) {
-    case PINOT_INT:
-    case PINOT_LONG:
-      return std::to_string(dict_int[id]);
-    case PINOT_FLOAT:
-    case PINOT_DOUBLE: {
-      // Float.toString / Double.toString are not reproduced exactly for every value; group-by keys on
-      // floating-point columns use the shortest round-trip form (documented in DESIGN.md).
-      char buf[64];
-      snprintf(buf, sizeof(buf), "%.17g", dict_dbl[id]);
-      return buf;
-    }
-    default:
-      return dict_str[id];
-  }
-}
-
-double ColumnData::double_value(int32_t id) const {
-  switch (data_type) {
-    case PINOT_INT:
-    case PINOT_LONG:
-      return static_cast<double>(dict_int[id]);
-    case PINOT_FLOAT:
-    case PINOT_DOUBLE:
-      return dict_dbl[id];
-    default:
-      return std::stod(dict_str[id]);
-  }
-}
-
 static void upload(DeviceBuffer &buf, const void *src, size_t bytes, size_t alloc_bytes, hipStream_t s) {
   buf.alloc(alloc_bytes);
   if (alloc_bytes > bytes) PINOT_HIP(hipMemsetAsync(buf.get<uint8_t>() + bytes, 0, alloc_bytes - bytes, s));
@@ -56,56 +25,6 @@ static void upload(DeviceBuffer &buf, const void *src, size_t bytes, size_t allo
 // Forward-index allocations are padded by one full 64-word staging chunk (64 * 8 * 32 B) plus a DMA
 // piece, so the last chunk's global_load_lds pieces never leave the allocation.
 static size_t padded(size_t bytes) { return ((bytes + 255) / 256) * 256 + 16384 + 1024; }
-
-static void decode_dictionary(ColumnData &c, const pinot_column_desc &d) {
-  const uint8_t *p = d.dictionary;
-  const int64_t card = c.card;
-  switch (c.data_type) {
-    case PINOT_INT:
-      require(d.dictionary_len >= (uint64_t)card * 4, PINOT_ERR_BAD_ARG, c.name + ": INT dictionary too short");
-      c.dict_int.resize(card);
-      for (int64_t i = 0; i < card; i++) c.dict_int[i] = static_cast<int32_t>(load_be32(p + 4 * i));
-      break;
-    case PINOT_LONG:
-      require(d.dictionary_len >= (uint64_t)card * 8, PINOT_ERR_BAD_ARG, c.name + ": LONG dictionary too short");
-      c.dict_int.resize(card);
-      for (int64_t i = 0; i < card; i++) c.dict_int[i] = static_cast<int64_t>(load_be64(p + 8 * i));
-      break;
-    case PINOT_FLOAT:
-      require(d.dictionary_len >= (uint64_t)card * 4, PINOT_ERR_BAD_ARG, c.name + ": FLOAT dictionary too short");
-      c.dict_dbl.resize(card);
-      for (int64_t i = 0; i < card; i++) {
-        uint32_t u = load_be32(p + 4 * i);
-        float f;
-        memcpy(&f, &u, 4);
-        c.dict_dbl[i] = static_cast<double>(f);
-      }
-      break;
-    case PINOT_DOUBLE:
-      require(d.dictionary_len >= (uint64_t)card * 8, PINOT_ERR_BAD_ARG, c.name + ": DOUBLE dictionary too short");
-      c.dict_dbl.resize(card);
-      for (int64_t i = 0; i < card; i++) {
-        uint64_t u = load_be64(p + 8 * i);
-        memcpy(&c.dict_dbl[i], &u, 8);
-      }
-      break;
-    case PINOT_STRING: {
-      const int w = d.string_width;
-      require(w >= 0 && d.dictionary_len >= (uint64_t)card * w, PINOT_ERR_BAD_ARG, c.name + ": STRING dictionary");
-      c.dict_str.resize(card);
-      for (int64_t i = 0; i < card; i++) {
-        const char *s = reinterpret_cast<const char *>(p + (size_t)i * w);
-        size_t n = 0;
-        while (n < (size_t)w && s[n] != 0) n++;  // getUnpaddedString: stop at the first padding byte
-        c.dict_str[i].assign(s, n);
-      }
-      break;
-    }
-    default:
-      throw Error(PINOT_ERR_BAD_ARG, c.name + ": unknown data type");
-  }
-  c.dict_be.assign(d.dictionary, d.dictionary + d.dictionary_len);
-}
 
 // Detects value(id) = base + step * id over the whole (sorted) INT/LONG dictionary.
 static void detect_affine(ColumnData &c) {
@@ -135,133 +54,26 @@ static void upload_dictionary(Engine &e, ColumnData &c) {
   }
 }
 
-// Portable RoaringBitmap header walk (RoaringBitmap 0.8.0 RoaringArray.deserialize), building the
-// container directory the K3 kernel binary-searches. Payload bytes stay untouched in HBM.
-static void parse_roaring(const uint8_t *blob, size_t len, uint64_t base, std::vector<RoaringContainer> &out,
-                          const std::string &col) {
-  auto u16 = [&](size_t o) -> uint32_t {
-    require(o + 2 <= len, PINOT_ERR_BAD_ARG, col + ": truncated roaring bitmap");
-    return (uint32_t)blob[o] | ((uint32_t)blob[o + 1] << 8);
-  };
-  auto u32 = [&](size_t o) -> uint32_t { return u16(o) | (u16(o + 2) << 16); };
-  const uint32_t cookie = u32(0);
-  size_t pos = 4;
-  uint32_t n;
-  const uint8_t *runs = nullptr;
-  bool has_offsets;
-  if (cookie == 12346u) {
-    n = u32(4);
-    pos = 8;
-    has_offsets = true;
-  } else if ((cookie & 0xFFFFu) == 12347u) {
-    n = (cookie >> 16) + 1;
-    runs = blob + pos;
-    pos += (n + 7) / 8;
-    has_offsets = n >= 4;
-  } else {
-    throw Error(PINOT_ERR_BAD_ARG, col + ": bad roaring cookie");
-  }
-  const size_t kc = pos;
-  pos += 4 * (size_t)n;
-  const size_t offs = pos;
-  if (has_offsets) pos += 4 * (size_t)n;
-  for (uint32_t i = 0; i < n; i++) {
-    RoaringContainer c{};
-    c.key = (uint16_t)u16(kc + 4 * i);
-    const uint32_t card = u16(kc + 4 * i + 2) + 1;
-    const bool is_run = runs && ((runs[i / 8] >> (i % 8)) & 1);
-    size_t start = has_offsets ? u32(offs + 4 * i) : pos;
-    size_t size;
-    if (is_run) {
-      const uint32_t nruns = u16(start);
-      c.type = 2;
-      c.cardinality = nruns;
-      c.payload_offset = base + start + 2;
-      size = 2 + 4 * (size_t)nruns;
-    } else if (card > 4096) {
-      c.type = 1;
-      c.cardinality = card;
-      c.payload_offset = base + start;
-      size = 8192;
-    } else {
-      c.type = 0;
-      c.cardinality = card;
-      c.payload_offset = base + start;
-      size = 2 * (size_t)card;
-    }
-    require(start + size <= len, PINOT_ERR_BAD_ARG, col + ": roaring container out of bounds");
-    pos = start + size;
-    out.push_back(c);
-  }
-}
-
 static void register_column(Engine &e, SegmentData &seg, const pinot_column_desc &d) {
   auto cp = std::make_unique<ColumnData>();
   ColumnData &c = *cp;
-  require(d.name != nullptr, PINOT_ERR_BAD_ARG, "column without name");
-  c.name = d.name;
-  c.data_type = d.data_type;
-  c.card = d.cardinality;
-  c.bits = d.bits_per_value;
-  c.is_sorted = d.is_sorted != 0;
-  c.has_inverted = d.has_inverted_index != 0 || c.is_sorted;
-  c.string_width = d.string_width;
-  c.num_docs = seg.num_docs;
-  require(c.card >= 1 || seg.num_docs == 0, PINOT_ERR_BAD_ARG, c.name + ": empty dictionary");
-  // The reader takes the width from the segment metadata (column.<c>.bitsPerElement, ColumnMetadata.java:98 ->
-  // FixedBitSingleValueReader, PhysicalColumnIndexContainer.java:99); the creator writes
-  // getNumBitsPerValue(card - 1) (SegmentColumnarIndexCreator.java:404), so any wider width still decodes.
-  require(c.bits >= num_bits_per_value(std::max<int64_t>(c.card - 1, 0)), PINOT_ERR_BAD_ARG,
-          c.name + ": bits_per_value < getNumBitsPerValue(cardinality - 1)");
-  require(c.bits >= 1 && c.bits <= 32, PINOT_ERR_BAD_ARG, c.name + ": bits out of range");
-  decode_dictionary(c, d);
+  ParsedIndexes idx;
+  parse_column(c, d, seg.num_docs, idx);  // every check on the caller's bytes (segment_parse.cpp)
+  require(seg.by_name.find(c.name) == seg.by_name.end(), PINOT_ERR_BAD_ARG, "duplicate column " + c.name);
   upload_dictionary(e, c);
-
-  const int64_t n = seg.num_docs;
-  c.fwd_bytes = (uint64_t)((n * c.bits + 7) / 8);
   if (c.is_sorted) {
-    require(d.sorted_index && d.sorted_index_len >= (uint64_t)c.card * 8, PINOT_ERR_BAD_ARG,
-            c.name + ": sorted index must hold 2 ints per dictId");
-    c.sorted_start.resize(c.card);
-    c.sorted_end.resize(c.card);
-    std::vector<int32_t> starts(c.card + 1);
-    for (int32_t i = 0; i < c.card; i++) {
-      c.sorted_start[i] = static_cast<int32_t>(load_be32(d.sorted_index + 8 * i));
-      c.sorted_end[i] = static_cast<int32_t>(load_be32(d.sorted_index + 8 * i + 4));
-      starts[i] = c.sorted_start[i];
-    }
-    starts[c.card] = (int32_t)n;
-    for (int32_t i = 0; i < c.card; i++) {
-      require(c.sorted_start[i] <= c.sorted_end[i] + 1 && (i == 0 || c.sorted_start[i] == c.sorted_end[i - 1] + 1),
-              PINOT_ERR_BAD_ARG, c.name + ": sorted index ranges must tile the docs");
-    }
     DeviceBuffer dstarts;
-    upload(dstarts, starts.data(), starts.size() * 4, starts.size() * 4, e.stream);
+    upload(dstarts, idx.sorted_starts.data(), idx.sorted_starts.size() * 4, idx.sorted_starts.size() * 4, e.stream);
     c.fwd.alloc(padded(c.fwd_bytes));
     PINOT_HIP(hipMemsetAsync(c.fwd.get(), 0, c.fwd.size(), e.stream));
-    launch_sorted_to_fwd(dstarts.get<int32_t>(), c.card, c.bits, (int32_t)n, c.fwd.get<uint8_t>(), e.stream);
+    launch_sorted_to_fwd(dstarts.get<int32_t>(), c.card, c.bits, (int32_t)seg.num_docs, c.fwd.get<uint8_t>(), e.stream);
     PINOT_HIP(hipGetLastError());
     PINOT_HIP(hipStreamSynchronize(e.stream));
   } else {
-    require(d.forward_index && d.forward_index_len >= c.fwd_bytes, PINOT_ERR_BAD_ARG,
-            c.name + ": forward index shorter than ceil(N*b/8) (FixedBitIntReaderWriter.java:31-36)");
     upload(c.fwd, d.forward_index, c.fwd_bytes, padded(c.fwd_bytes), e.stream);
   }
-
   if (!c.is_sorted && c.has_inverted) {
-    require(d.inverted_index && d.inverted_index_len >= (uint64_t)(c.card + 1) * 4, PINOT_ERR_BAD_ARG,
-            c.name + ": inverted index header");
-    std::vector<RoaringContainer> conts;
-    c.inv_dir.assign(c.card + 1, 0);
-    c.inv_bytes.assign(c.card, 0);
-    for (int32_t i = 0; i < c.card; i++) {
-      const uint32_t o0 = load_be32(d.inverted_index + 4 * i), o1 = load_be32(d.inverted_index + 4 * (i + 1));
-      require(o0 <= o1 && o1 <= d.inverted_index_len, PINOT_ERR_BAD_ARG, c.name + ": inverted index offsets");
-      c.inv_dir[i] = (int32_t)conts.size();
-      c.inv_bytes[i] = o1 - o0;
-      parse_roaring(d.inverted_index + o0, o1 - o0, o0, conts, c.name);
-    }
-    c.inv_dir[c.card] = (int32_t)conts.size();
+    const std::vector<RoaringContainer> &conts = idx.containers;
     upload(c.inv_payload, d.inverted_index, d.inverted_index_len, padded(d.inverted_index_len), e.stream);
     upload(c.inv_containers, conts.data(), conts.size() * sizeof(RoaringContainer),
            std::max<size_t>(conts.size() * sizeof(RoaringContainer), 16), e.stream);
@@ -270,7 +82,6 @@ static void register_column(Engine &e, SegmentData &seg, const pinot_column_desc
   }
   seg.device_bytes += c.fwd.size() + c.dict_dev.size() + c.inv_payload.size() + c.inv_containers.size() +
                       c.inv_dir_dev.size();
-  require(seg.by_name.find(c.name) == seg.by_name.end(), PINOT_ERR_BAD_ARG, "duplicate column " + c.name);
   seg.by_name[c.name] = (int)seg.cols.size();
   seg.cols.push_back(std::move(cp));
 }

@@ -1,0 +1,323 @@
+// Host half of segment registration: every check on the caller's column bytes, with no device involved.
+// register_column (segment.cpp) runs parse_column and only then uploads; pinot_segment_validate runs it alone.
+// This file and planner.cpp are what the sanitizer build (Makefile `fuzz`, tests/fuzz/fuzz_host.cpp) exercises
+// with malformed descriptors: a bad byte must come back as PINOT_ERR_BAD_ARG, never as a fault.
+//
+// Readers restated (PC = pinot-core/src/main/java/org/apache/pinot/core):
+//   dictionaries   PC/segment/index/readers/{Int,Long,Float,Double,String}Dictionary.java (BE values, padded strings)
+//   sorted index   PC/segment/index/readers/SortedIndexReaderImpl.java:34-39 (2 BE ints per dictId)
+//   inverted index PC/segment/index/readers/BitmapInvertedIndexReader.java:92-119 (BE offsets + portable roaring)
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
+#include "engine.h"
+
+namespace pinot {
+
+// ---------------------------------------------------------------- Java Double.toString / Float.toString
+// The digits are the shortest decimal that reads back as the same double (float): the correctly rounded
+// p-digit form for the smallest p that round-trips (the Double.toString javadoc's "as many, but only as many,
+// more digits as are needed to uniquely distinguish the argument value from adjacent values"). Layout:
+// plain decimal with at least one fraction digit for 1e-3 <= |v| < 1e7, else d.dddE<exp>
+// (DoubleDictionary.getStringValue -> Double.toString, PC/segment/index/readers/DoubleDictionary.java:73-75).
+static std::string java_layout(bool neg, const std::string &digits, int exp10) {
+  std::string out = neg ? "-" : "";
+  if (exp10 >= -3 && exp10 < 7) {
+    if (exp10 >= 0) {
+      std::string ip = digits.substr(0, std::min<size_t>(digits.size(), (size_t)exp10 + 1));
+      while ((int)ip.size() < exp10 + 1) ip += '0';
+      std::string fp = (int)digits.size() > exp10 + 1 ? digits.substr(exp10 + 1) : "0";
+      out += ip + "." + fp;
+    } else {
+      out += "0." + std::string((size_t)(-exp10 - 1), '0') + digits;
+    }
+  } else {
+    out += digits.substr(0, 1) + "." + (digits.size() > 1 ? digits.substr(1) : "0") + "E" + std::to_string(exp10);
+  }
+  return out;
+}
+
+// "%.*e" output -> (digits without trailing zeros, decimal exponent)
+static void split_sci(const char *buf, std::string &digits, int &exp10) {
+  digits.clear();
+  const char *p = buf;
+  if (*p == '-') p++;
+  for (; *p && *p != 'e'; p++)
+    if (*p >= '0' && *p <= '9') digits += *p;
+  exp10 = *p == 'e' ? atoi(p + 1) : 0;
+  while (digits.size() > 1 && digits.back() == '0') digits.pop_back();
+}
+
+std::string java_double_to_string(double v) {
+  if (std::isnan(v)) return "NaN";
+  if (std::isinf(v)) return v > 0 ? "Infinity" : "-Infinity";
+  if (v == 0) return std::signbit(v) ? "-0.0" : "0.0";
+  char buf[64];
+  for (int p = 1; p <= 17; p++) {
+    snprintf(buf, sizeof(buf), "%.*e", p - 1, v);
+    if (strtod(buf, nullptr) == v) break;
+  }
+  std::string digits;
+  int e10;
+  split_sci(buf, digits, e10);
+  return java_layout(v < 0, digits, e10);
+}
+
+std::string java_float_to_string(float v) {
+  if (std::isnan(v)) return "NaN";
+  if (std::isinf(v)) return v > 0 ? "Infinity" : "-Infinity";
+  if (v == 0) return std::signbit(v) ? "-0.0" : "0.0";
+  char buf[64];
+  for (int p = 1; p <= 9; p++) {
+    snprintf(buf, sizeof(buf), "%.*e", p - 1, (double)v);
+    if (strtof(buf, nullptr) == v) break;
+  }
+  std::string digits;
+  int e10;
+  split_sci(buf, digits, e10);
+  return java_layout(v < 0, digits, e10);
+}
+
+std::string ColumnData::string_value(int32_t id) const {
+  switch (data_type) {
+    case PINOT_INT:
+    case PINOT_LONG:
+      return std::to_string(dict_int[id]);
+    case PINOT_FLOAT:  // FloatDictionary.getStringValue -> Float.toString
+      return java_float_to_string(static_cast<float>(dict_dbl[id]));
+    case PINOT_DOUBLE:
+      return java_double_to_string(dict_dbl[id]);
+    default:
+      return dict_str[id];
+  }
+}
+
+double ColumnData::double_value(int32_t id) const {
+  switch (data_type) {
+    case PINOT_INT:
+    case PINOT_LONG:
+      return static_cast<double>(dict_int[id]);
+    case PINOT_FLOAT:
+    case PINOT_DOUBLE:
+      return dict_dbl[id];
+    default:
+      return std::stod(dict_str[id]);
+  }
+}
+
+// ---------------------------------------------------------------- dictionaries
+static void decode_dictionary(ColumnData &c, const pinot_column_desc &d) {
+  const uint8_t *p = d.dictionary;
+  const int64_t card = c.card;
+  auto need = [&](uint64_t w, const char *what) {
+    require(card == 0 || (p != nullptr && d.dictionary_len / w >= (uint64_t)card), PINOT_ERR_BAD_ARG,
+            c.name + ": " + what + " dictionary too short");
+  };
+  switch (c.data_type) {
+    case PINOT_INT:
+      need(4, "INT");
+      c.dict_int.resize(card);
+      for (int64_t i = 0; i < card; i++) c.dict_int[i] = static_cast<int32_t>(load_be32(p + 4 * i));
+      break;
+    case PINOT_LONG:
+      need(8, "LONG");
+      c.dict_int.resize(card);
+      for (int64_t i = 0; i < card; i++) c.dict_int[i] = static_cast<int64_t>(load_be64(p + 8 * i));
+      break;
+    case PINOT_FLOAT:
+      need(4, "FLOAT");
+      c.dict_dbl.resize(card);
+      for (int64_t i = 0; i < card; i++) {
+        uint32_t u = load_be32(p + 4 * i);
+        float f;
+        memcpy(&f, &u, 4);
+        c.dict_dbl[i] = static_cast<double>(f);
+      }
+      break;
+    case PINOT_DOUBLE:
+      need(8, "DOUBLE");
+      c.dict_dbl.resize(card);
+      for (int64_t i = 0; i < card; i++) {
+        uint64_t u = load_be64(p + 8 * i);
+        memcpy(&c.dict_dbl[i], &u, 8);
+      }
+      break;
+    case PINOT_STRING: {
+      const int w = d.string_width;
+      require(w >= 1 && w <= (1 << 20), PINOT_ERR_BAD_ARG, c.name + ": STRING dictionary width");
+      need((uint64_t)w, "STRING");
+      c.dict_str.resize(card);
+      for (int64_t i = 0; i < card; i++) {
+        const char *s = reinterpret_cast<const char *>(p + (size_t)i * w);
+        size_t n = 0;
+        while (n < (size_t)w && s[n] != 0) n++;  // getUnpaddedString: stop at the first padding byte
+        c.dict_str[i].assign(s, n);
+      }
+      break;
+    }
+    default:
+      throw Error(PINOT_ERR_BAD_ARG, c.name + ": unknown data type");
+  }
+  if (d.dictionary_len) c.dict_be.assign(d.dictionary, d.dictionary + d.dictionary_len);
+}
+
+// ---------------------------------------------------------------- portable roaring
+// RoaringBitmap 0.8.0 RoaringArray.deserialize: the container directory the device binary-searches. Every
+// property the kernels rely on is checked here: keys strictly ascending (binary search), array values strictly
+// ascending (binary search), runs inside their 65536-doc key (the LDS tile k_roaring_expand ORs them into),
+// payloads inside the blob.
+static void parse_roaring(const uint8_t *blob, size_t len, uint64_t base, std::vector<RoaringContainer> &out,
+                          const std::string &col) {
+  auto u16 = [&](size_t o) -> uint32_t {
+    require(o <= len && len - o >= 2, PINOT_ERR_BAD_ARG, col + ": truncated roaring bitmap");
+    return (uint32_t)blob[o] | ((uint32_t)blob[o + 1] << 8);
+  };
+  auto u32 = [&](size_t o) -> uint32_t { return u16(o) | (u16(o + 2) << 16); };
+  const uint32_t cookie = u32(0);
+  size_t pos = 4;
+  uint32_t n;
+  const uint8_t *runs = nullptr;
+  bool has_offsets;
+  if (cookie == 12346u) {  // SERIAL_COOKIE_NO_RUNCONTAINER
+    n = u32(4);
+    pos = 8;
+    has_offsets = true;
+  } else if ((cookie & 0xFFFFu) == 12347u) {  // SERIAL_COOKIE
+    n = (cookie >> 16) + 1;
+    require(len - pos >= (n + 7) / 8, PINOT_ERR_BAD_ARG, col + ": truncated roaring run bitmap");
+    runs = blob + pos;
+    pos += (n + 7) / 8;
+    has_offsets = n >= 4;  // NO_OFFSET_THRESHOLD
+  } else {
+    throw Error(PINOT_ERR_BAD_ARG, col + ": bad roaring cookie");
+  }
+  require(n <= 65536, PINOT_ERR_BAD_ARG, col + ": roaring container count > 65536");
+  const size_t kc = pos;
+  pos += 4 * (size_t)n;
+  const size_t offs = pos;
+  if (has_offsets) pos += 4 * (size_t)n;
+  require(pos <= len, PINOT_ERR_BAD_ARG, col + ": truncated roaring header");
+  int64_t prev_key = -1;
+  for (uint32_t i = 0; i < n; i++) {
+    RoaringContainer c{};
+    c.key = (uint16_t)u16(kc + 4 * i);
+    require((int64_t)c.key > prev_key, PINOT_ERR_BAD_ARG, col + ": roaring keys not ascending");
+    prev_key = c.key;
+    const uint32_t card = u16(kc + 4 * i + 2) + 1;
+    const bool is_run = runs && ((runs[i / 8] >> (i % 8)) & 1);
+    const size_t start = has_offsets ? u32(offs + 4 * i) : pos;
+    size_t size;
+    if (is_run) {
+      const uint32_t nruns = u16(start);
+      c.type = 2;
+      c.cardinality = nruns;
+      c.payload_offset = base + start + 2;
+      size = 2 + 4 * (size_t)nruns;
+    } else if (card > 4096) {  // DEFAULT_MAX_SIZE: bitmap container
+      c.type = 1;
+      c.cardinality = card;
+      c.payload_offset = base + start;
+      size = 8192;
+    } else {
+      c.type = 0;
+      c.cardinality = card;
+      c.payload_offset = base + start;
+      size = 2 * (size_t)card;
+    }
+    require(start <= len && len - start >= size, PINOT_ERR_BAD_ARG, col + ": roaring container out of bounds");
+    if (c.type == 0) {
+      for (uint32_t k = 1; k < card; k++)
+        require(u16(start + 2 * k) > u16(start + 2 * (k - 1)), PINOT_ERR_BAD_ARG,
+                col + ": roaring array container not strictly ascending");
+    } else if (c.type == 2) {
+      for (uint32_t k = 0; k < c.cardinality; k++)
+        require(u16(start + 2 + 4 * k) + u16(start + 4 + 4 * k) <= 0xFFFFu, PINOT_ERR_BAD_ARG,
+                col + ": roaring run leaves its container");
+    }
+    pos = start + size;
+    out.push_back(c);
+  }
+}
+
+// ---------------------------------------------------------------- one column
+void parse_column(ColumnData &c, const pinot_column_desc &d, int32_t num_docs, ParsedIndexes &out) {
+  require(d.name != nullptr, PINOT_ERR_BAD_ARG, "column without name");
+  c.name = d.name;
+  c.data_type = d.data_type;
+  require(d.cardinality >= 0, PINOT_ERR_BAD_ARG, c.name + ": negative cardinality");
+  c.card = d.cardinality;
+  c.bits = d.bits_per_value;
+  c.is_sorted = d.is_sorted != 0;
+  c.has_inverted = d.has_inverted_index != 0 || c.is_sorted;
+  c.string_width = d.string_width;
+  c.num_docs = num_docs;
+  require(c.card >= 1 || num_docs == 0, PINOT_ERR_BAD_ARG, c.name + ": empty dictionary");
+  require(c.bits >= 1 && c.bits <= 32, PINOT_ERR_BAD_ARG, c.name + ": bits out of range");
+  // The reader takes the width from the segment metadata (column.<c>.bitsPerElement, ColumnMetadata.java:98 ->
+  // FixedBitSingleValueReader, PhysicalColumnIndexContainer.java:99); the creator writes
+  // getNumBitsPerValue(card - 1) (SegmentColumnarIndexCreator.java:404), so any wider width still decodes.
+  require(c.bits >= num_bits_per_value(std::max<int64_t>(c.card - 1, 0)), PINOT_ERR_BAD_ARG,
+          c.name + ": bits_per_value < getNumBitsPerValue(cardinality - 1)");
+  decode_dictionary(c, d);
+
+  const int64_t n = num_docs;
+  c.fwd_bytes = (uint64_t)((n * c.bits + 7) / 8);
+  out.sorted_starts.clear();
+  out.containers.clear();
+  if (c.is_sorted) {
+    require(d.sorted_index && d.sorted_index_len / 8 >= (uint64_t)c.card, PINOT_ERR_BAD_ARG,
+            c.name + ": sorted index must hold 2 ints per dictId");
+    c.sorted_start.resize(c.card);
+    c.sorted_end.resize(c.card);
+    out.sorted_starts.resize((size_t)c.card + 1);
+    for (int32_t i = 0; i < c.card; i++) {
+      c.sorted_start[i] = static_cast<int32_t>(load_be32(d.sorted_index + 8 * i));
+      c.sorted_end[i] = static_cast<int32_t>(load_be32(d.sorted_index + 8 * i + 4));
+      out.sorted_starts[i] = c.sorted_start[i];
+    }
+    out.sorted_starts[c.card] = (int32_t)n;
+    // the ranges tile [0, numDocs) in dictId order (k_sorted_to_fwd writes doc positions from them)
+    for (int32_t i = 0; i < c.card; i++) {
+      const int64_t s = c.sorted_start[i], e = c.sorted_end[i];
+      require(s == (i == 0 ? 0 : (int64_t)c.sorted_end[i - 1] + 1) && e >= s - 1 && e < n, PINOT_ERR_BAD_ARG,
+              c.name + ": sorted index ranges must tile the docs");
+    }
+    require(c.card == 0 || (int64_t)c.sorted_end[c.card - 1] == n - 1, PINOT_ERR_BAD_ARG,
+            c.name + ": sorted index ranges must tile the docs");
+  } else {
+    require(d.forward_index && d.forward_index_len >= c.fwd_bytes, PINOT_ERR_BAD_ARG,
+            c.name + ": forward index shorter than ceil(N*b/8) (FixedBitIntReaderWriter.java:31-36)");
+  }
+  if (!c.is_sorted && c.has_inverted) {
+    require(d.inverted_index && d.inverted_index_len / 4 >= (uint64_t)c.card + 1, PINOT_ERR_BAD_ARG,
+            c.name + ": inverted index header");
+    require(d.inverted_index_len < (1ull << 32), PINOT_ERR_UNSUPPORTED, c.name + ": inverted index beyond 4 GiB");
+    c.inv_dir.assign((size_t)c.card + 1, 0);
+    c.inv_bytes.assign(c.card, 0);
+    for (int32_t i = 0; i < c.card; i++) {
+      const uint32_t o0 = load_be32(d.inverted_index + 4 * i), o1 = load_be32(d.inverted_index + 4 * (i + 1));
+      require(o0 <= o1 && o1 <= d.inverted_index_len, PINOT_ERR_BAD_ARG, c.name + ": inverted index offsets");
+      c.inv_dir[i] = (int32_t)out.containers.size();
+      c.inv_bytes[i] = o1 - o0;
+      parse_roaring(d.inverted_index + o0, o1 - o0, o0, out.containers, c.name);
+    }
+    c.inv_dir[c.card] = (int32_t)out.containers.size();
+  }
+}
+
+void validate_segment(const pinot_segment_desc &d) {
+  require(d.num_docs >= 0, PINOT_ERR_BAD_ARG, "num_docs < 0");
+  require(d.num_columns >= 0 && (d.num_columns == 0 || d.columns), PINOT_ERR_BAD_ARG, "columns");
+  std::vector<std::string> names;
+  for (int i = 0; i < d.num_columns; i++) {
+    ColumnData c;
+    ParsedIndexes idx;
+    parse_column(c, d.columns[i], d.num_docs, idx);
+    for (const std::string &nm : names) require(nm != c.name, PINOT_ERR_BAD_ARG, "duplicate column " + c.name);
+    names.push_back(c.name);
+  }
+}
+
+}  // namespace pinot

@@ -9,5 +9,6 @@ from .segment import Segment, Column, build_segment, build_column, num_bits_per_
 from .pql import compile_pql, PqlCompilationException  # noqa: F401
 from .executor import (GpuEngine, GpuSegment, GpuServer, ServerExecutor, ServerQueryExecutor, BrokerReduce,  # noqa: F401
                        AvgPair, HyperLogLog,
-                       ExecutionStatistics, trim_intermediate_results, final_result, format_value)
+                       ExecutionStatistics, trim_intermediate_results, final_result, format_value,
+                       validate_segment)
 from ._lib import PinotGpuError, load as load_library  # noqa: F401

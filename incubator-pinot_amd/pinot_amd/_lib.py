@@ -21,8 +21,8 @@ AGG_FN = {"COUNT": 0, "SUM": 1, "MIN": 2, "MAX": 3, "AVG": 4, "DISTINCTCOUNTHLL"
 EXPORTED_SYMBOLS = [
     "pinot_gpu_last_error", "pinot_gpu_abi_version", "pinot_gpu_device_count",
     "pinot_gpu_engine_create", "pinot_gpu_engine_destroy", "pinot_gpu_engine_set_config",
-    "pinot_gpu_segment_register", "pinot_gpu_segment_release", "pinot_gpu_segment_device_bytes",
-    "pinot_gpu_filter", "pinot_gpu_aggregate", "pinot_gpu_group_by",
+    "pinot_gpu_segment_register", "pinot_gpu_segment_release", "pinot_gpu_segment_validate",
+    "pinot_gpu_segment_device_bytes", "pinot_gpu_filter", "pinot_gpu_aggregate", "pinot_gpu_group_by",
     "pinot_groupby_num_groups", "pinot_groupby_num_columns", "pinot_groupby_key", "pinot_groupby_values",
     "pinot_groupby_hll", "pinot_groupby_raw_keys", "pinot_groupby_export_keys", "pinot_groupby_trim",
     "pinot_groupby_free",
@@ -141,6 +141,7 @@ def load(path=None):
         "pinot_gpu_engine_set_config": (i32, [P, C.c_char_p]),
         "pinot_gpu_segment_register": (i32, [P, C.POINTER(SegmentDesc), C.POINTER(i64)]),
         "pinot_gpu_segment_release": (i32, [P, i64]),
+        "pinot_gpu_segment_validate": (i32, [C.POINTER(SegmentDesc)]),
         "pinot_gpu_segment_device_bytes": (i32, [P, i64, C.POINTER(u64)]),
         "pinot_gpu_filter": (i32, [P, i64, i32, C.POINTER(FilterNode), P, C.POINTER(i64)]),
         "pinot_gpu_aggregate": (i32, [P, C.POINTER(i64), i32, C.POINTER(Query), C.POINTER(AggResult),

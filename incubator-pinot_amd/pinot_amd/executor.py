@@ -74,6 +74,42 @@ class GpuSegment:
             self.handle = None
 
 
+def segment_desc(seg: Segment):
+    """pinot_segment_desc over the segment's column buffers; the second value keeps the buffers alive."""
+    keep = []
+    cols = (_lib.ColumnDesc * max(len(seg.columns), 1))()
+    for i, col in enumerate(seg.columns.values()):
+        d = cols[i]
+        name = col.name.encode()
+        keep.append(name)
+        d.name = name
+        d.data_type = _lib.DATA_TYPE[col.data_type]
+        d.cardinality = col.cardinality
+        d.bits_per_value = col.bits
+        d.is_sorted = int(col.is_sorted)
+        d.has_inverted_index = int(col.has_inverted_index and not col.is_sorted)
+        d.string_width = col.string_width
+        for field, data in (("dictionary", col.dictionary), ("forward_index", col.fwd),
+                            ("sorted_index", col.sorted_index), ("inverted_index", col.inverted)):
+            if data is None:
+                continue
+            buf = C.create_string_buffer(bytes(data), len(data)) if len(data) else C.create_string_buffer(1)
+            keep.append(buf)
+            setattr(d, field, C.cast(buf, C.c_void_p))
+            setattr(d, field + "_len", len(data))
+    sname = seg.name.encode()
+    keep += [sname, cols]
+    return _lib.SegmentDesc(sname, seg.num_docs, len(seg.columns), cols), keep
+
+
+def validate_segment(seg: Segment) -> None:
+    """pinot_gpu_segment_validate: the registration checks on the host alone (no engine, no GPU);
+    raises PinotGpuError (BAD_ARG) naming the first bad column."""
+    lib = _lib.load()
+    desc, _keep = segment_desc(seg)
+    check(lib.pinot_gpu_segment_validate(C.byref(desc)))
+
+
 class GpuEngine:
     """One engine per HIP device (`QueryExecutor.init/start/shutDown`)."""
 
@@ -107,29 +143,7 @@ class GpuEngine:
 
     # ---------------------------------------------------------------- segments
     def register(self, seg: Segment) -> GpuSegment:
-        keep = []
-        cols = (_lib.ColumnDesc * max(len(seg.columns), 1))()
-        for i, col in enumerate(seg.columns.values()):
-            d = cols[i]
-            name = col.name.encode()
-            keep.append(name)
-            d.name = name
-            d.data_type = _lib.DATA_TYPE[col.data_type]
-            d.cardinality = col.cardinality
-            d.bits_per_value = col.bits
-            d.is_sorted = int(col.is_sorted)
-            d.has_inverted_index = int(col.has_inverted_index and not col.is_sorted)
-            d.string_width = col.string_width
-            for field, data in (("dictionary", col.dictionary), ("forward_index", col.fwd),
-                                ("sorted_index", col.sorted_index), ("inverted_index", col.inverted)):
-                if data is None:
-                    continue
-                buf = C.create_string_buffer(bytes(data), len(data)) if len(data) else C.create_string_buffer(1)
-                keep.append(buf)
-                setattr(d, field, C.cast(buf, C.c_void_p))
-                setattr(d, field + "_len", len(data))
-        sname = seg.name.encode()
-        desc = _lib.SegmentDesc(sname, seg.num_docs, len(seg.columns), cols)
+        desc, _keep = segment_desc(seg)
         h = C.c_int64()
         check(self.lib.pinot_gpu_segment_register(self.ptr, C.byref(desc), C.byref(h)))
         return GpuSegment(self, h.value, seg.name, seg.num_docs)

@@ -12,4 +12,4 @@ timeout -k 10 300 python bench.py --workload config4 --steps 10 --warmup 3 > $ou
 tail -1 $out/bench_config4.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/prof_c4 -o run -- python bench.py --workload config4 --steps 5 --warmup 2 --no-cpu-baseline > $out/prof_c4.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/prof_c2 -o run -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-verify > $out/prof_c2.log 2>&1 || exit $?
-find $out -name "*kernel_stats.csv" | head
+python scripts/prof_kernels.py $out/prof_c4/run_results.db; python scripts/prof_kernels.py $out/prof_c2/run_results.db

@@ -1,0 +1,406 @@
+// Host-side fuzzer for the segment descriptor checks (segment_parse.cpp) and the filter planner
+// (planner.cpp), built with AddressSanitizer + UndefinedBehaviorSanitizer by `make -C incubator-pinot_amd fuzz`.
+//
+// Each iteration builds a well-formed Pinot column set (BE dictionaries, packed forward index, sorted index,
+// portable-roaring inverted index), then corrupts it: byte flips in every buffer, truncated lengths, wrong
+// widths / cardinalities / string widths, roaring cookies, container counts, offsets and run lengths. The
+// contract checked: validate_segment either accepts the descriptor or throws pinot::Error with
+// PINOT_ERR_BAD_ARG / PINOT_ERR_UNSUPPORTED, never anything else, and never touches memory outside the
+// buffers (the sanitizers abort on that). Accepted segments then go through decode_filter + plan_filter with
+// random postfix filter trees and literals; the planner must answer with pinot::Error too.
+//
+// usage: fuzz_host [iterations] [seed]   (prints one summary line; exit 1 on a contract violation)
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "engine.h"
+
+using namespace pinot;
+
+namespace {
+
+std::mt19937_64 rng;
+uint64_t rnd(uint64_t n) { return n ? rng() % n : 0; }
+bool coin(int pct) { return (int)rnd(100) < pct; }
+
+void put_be32(std::vector<uint8_t> &b, size_t off, uint32_t v) {
+  b[off] = (uint8_t)(v >> 24);
+  b[off + 1] = (uint8_t)(v >> 16);
+  b[off + 2] = (uint8_t)(v >> 8);
+  b[off + 3] = (uint8_t)v;
+}
+void app_le16(std::vector<uint8_t> &b, uint32_t v) {
+  b.push_back((uint8_t)v);
+  b.push_back((uint8_t)(v >> 8));
+}
+void app_le32(std::vector<uint8_t> &b, uint32_t v) {
+  app_le16(b, v & 0xFFFF);
+  app_le16(b, v >> 16);
+}
+
+// Portable roaring of an ascending doc list: array / bitmap containers, optionally run containers
+// (cookie 12347 with the run bitmap), otherwise cookie 12346.
+void roaring(const std::vector<int32_t> &docs, bool allow_runs, std::vector<uint8_t> &out) {
+  struct C { uint32_t key; std::vector<uint32_t> low; bool run; };
+  std::vector<C> cs;
+  for (int32_t d : docs) {
+    const uint32_t k = (uint32_t)d >> 16;
+    if (cs.empty() || cs.back().key != k) cs.push_back({k, {}, false});
+    cs.back().low.push_back((uint32_t)d & 0xFFFF);
+  }
+  for (auto &c : cs) c.run = allow_runs && coin(50);
+  const uint32_t n = (uint32_t)cs.size();
+  const bool with_runs = allow_runs && n > 0;
+  std::vector<uint8_t> hdr;
+  if (with_runs) {
+    app_le32(hdr, 12347u | ((n - 1) << 16));
+    std::vector<uint8_t> rb((n + 7) / 8, 0);
+    for (uint32_t i = 0; i < n; i++)
+      if (cs[i].run) rb[i / 8] |= (uint8_t)(1u << (i % 8));
+    hdr.insert(hdr.end(), rb.begin(), rb.end());
+  } else {
+    app_le32(hdr, 12346u);
+    app_le32(hdr, n);
+  }
+  for (auto &c : cs) {
+    app_le16(hdr, c.key);
+    app_le16(hdr, (uint32_t)c.low.size() - 1);
+  }
+  const bool offsets = !with_runs || n >= 4;
+  std::vector<std::vector<uint8_t>> bodies;
+  for (auto &c : cs) {
+    std::vector<uint8_t> b;
+    if (c.run) {
+      std::vector<std::pair<uint32_t, uint32_t>> runs;
+      for (uint32_t v : c.low) {
+        if (!runs.empty() && runs.back().first + runs.back().second + 1 == v) runs.back().second++;
+        else runs.push_back({v, 0});
+      }
+      app_le16(b, (uint32_t)runs.size());
+      for (auto &r : runs) {
+        app_le16(b, r.first);
+        app_le16(b, r.second);
+      }
+    } else if (c.low.size() > 4096) {
+      std::vector<uint64_t> words(1024, 0);
+      for (uint32_t v : c.low) words[v >> 6] |= 1ull << (v & 63);
+      for (uint64_t w : words) {
+        app_le32(b, (uint32_t)w);
+        app_le32(b, (uint32_t)(w >> 32));
+      }
+    } else {
+      for (uint32_t v : c.low) app_le16(b, v);
+    }
+    bodies.push_back(std::move(b));
+  }
+  size_t pos = out.size() + hdr.size() + (offsets ? 4 * (size_t)n : 0);
+  const size_t base = out.size();
+  out.insert(out.end(), hdr.begin(), hdr.end());
+  if (offsets)
+    for (auto &b : bodies) {
+      app_le32(out, (uint32_t)(pos - base));
+      pos += b.size();
+    }
+  for (auto &b : bodies) out.insert(out.end(), b.begin(), b.end());
+}
+
+struct ColumnBufs {
+  std::string name;
+  std::vector<uint8_t> dict, fwd, sorted, inv;
+  pinot_column_desc d{};
+};
+
+void make_column(ColumnBufs &cb, int idx, int32_t num_docs) {
+  cb.name = "c" + std::to_string(idx);
+  const int type = (int)rnd(5);  // INT LONG FLOAT DOUBLE STRING
+  const int32_t card = num_docs == 0 ? 1 : 1 + (int32_t)rnd(std::min<int32_t>(num_docs, 300));
+  int width = 0;
+  switch (type) {
+    case PINOT_INT: {
+      cb.dict.assign((size_t)card * 4, 0);
+      for (int32_t i = 0; i < card; i++) put_be32(cb.dict, 4 * (size_t)i, (uint32_t)(i * 3 - 50));
+      break;
+    }
+    case PINOT_LONG: {
+      cb.dict.assign((size_t)card * 8, 0);
+      for (int32_t i = 0; i < card; i++) {
+        const uint64_t v = (uint64_t)((int64_t)i * 1000000007ll - 5);
+        put_be32(cb.dict, 8 * (size_t)i, (uint32_t)(v >> 32));
+        put_be32(cb.dict, 8 * (size_t)i + 4, (uint32_t)v);
+      }
+      break;
+    }
+    case PINOT_FLOAT: {
+      cb.dict.assign((size_t)card * 4, 0);
+      for (int32_t i = 0; i < card; i++) {
+        float f = (float)i * 0.37f - 3.0f;
+        uint32_t u;
+        memcpy(&u, &f, 4);
+        put_be32(cb.dict, 4 * (size_t)i, u);
+      }
+      break;
+    }
+    case PINOT_DOUBLE: {
+      cb.dict.assign((size_t)card * 8, 0);
+      for (int32_t i = 0; i < card; i++) {
+        double v = (double)i * 1.25e-3 - 0.1;
+        uint64_t u;
+        memcpy(&u, &v, 8);
+        put_be32(cb.dict, 8 * (size_t)i, (uint32_t)(u >> 32));
+        put_be32(cb.dict, 8 * (size_t)i + 4, (uint32_t)u);
+      }
+      break;
+    }
+    default: {
+      width = 6;
+      cb.dict.assign((size_t)card * width, 0);
+      for (int32_t i = 0; i < card; i++) {
+        char buf[8];
+        snprintf(buf, sizeof(buf), "s%05d", i);
+        memcpy(cb.dict.data() + (size_t)i * width, buf, 6);
+      }
+    }
+  }
+  const int bits = num_bits_per_value(card - 1) + (coin(10) ? (int)rnd(3) : 0);
+  std::vector<int32_t> vals(num_docs);
+  const bool sorted = coin(25);
+  for (int32_t d = 0; d < num_docs; d++)
+    vals[d] = sorted ? (int32_t)((int64_t)d * card / std::max(num_docs, 1)) : (d < card ? d : (int32_t)rnd(card));
+  pinot_column_desc &d = cb.d;
+  d.name = cb.name.c_str();
+  d.data_type = type;
+  d.cardinality = card;
+  d.bits_per_value = bits;
+  d.string_width = width;
+  if (sorted && num_docs > 0) {
+    cb.sorted.assign((size_t)card * 8, 0);
+    std::vector<int32_t> lo(card, -1), hi(card, -2);
+    for (int32_t doc = 0; doc < num_docs; doc++) {
+      if (lo[vals[doc]] < 0) lo[vals[doc]] = doc;
+      hi[vals[doc]] = doc;
+    }
+    for (int32_t v = 0; v < card; v++) {
+      put_be32(cb.sorted, 8 * (size_t)v, (uint32_t)lo[v]);
+      put_be32(cb.sorted, 8 * (size_t)v + 4, (uint32_t)hi[v]);
+    }
+    d.is_sorted = 1;
+  } else {
+    cb.fwd.assign(((size_t)num_docs * bits + 7) / 8, 0);
+    uint64_t acc = 0;
+    int nb = 0;
+    size_t o = 0;
+    for (int32_t doc = 0; doc < num_docs; doc++) {
+      acc = (acc << bits) | (uint32_t)vals[doc];
+      nb += bits;
+      while (nb >= 8) {
+        cb.fwd[o++] = (uint8_t)(acc >> (nb - 8));
+        nb -= 8;
+      }
+      acc &= (1ull << nb) - 1ull;
+    }
+    if (nb) cb.fwd[o] = (uint8_t)(acc << (8 - nb));
+    if (coin(60)) {
+      std::vector<std::vector<int32_t>> docs(card);
+      for (int32_t doc = 0; doc < num_docs; doc++) docs[vals[doc]].push_back(doc);
+      cb.inv.assign(4 * ((size_t)card + 1), 0);
+      const bool runs = coin(50);
+      for (int32_t v = 0; v < card; v++) {
+        put_be32(cb.inv, 4 * (size_t)v, (uint32_t)cb.inv.size());
+        roaring(docs[v], runs, cb.inv);
+      }
+      put_be32(cb.inv, 4 * (size_t)card, (uint32_t)cb.inv.size());
+      d.has_inverted_index = 1;
+    }
+  }
+}
+
+void flip(std::vector<uint8_t> &b) {
+  if (b.empty()) return;
+  const int k = 1 + (int)rnd(8);
+  for (int i = 0; i < k; i++) {
+    const size_t at = rnd(b.size());
+    b[at] = coin(50) ? (uint8_t)rng() : (uint8_t)(b[at] ^ (1u << rnd(8)));
+  }
+}
+
+uint64_t trunc_len(uint64_t n) { return coin(50) ? rnd(n + 1) : n; }
+
+void mutate(ColumnBufs &cb) {
+  pinot_column_desc &d = cb.d;
+  switch (rnd(12)) {
+    case 0: flip(cb.dict); break;
+    case 1: flip(cb.fwd); break;
+    case 2: flip(cb.sorted); break;
+    case 3: case 4: case 5: flip(cb.inv); break;  // offsets, cookies, counts, container bodies
+    case 6: d.bits_per_value = (int32_t)rnd(40) - 4; break;
+    case 7: d.cardinality = coin(50) ? (int32_t)rnd(2 * (uint64_t)std::max(d.cardinality, 1) + 2) - 1 : (int32_t)rng(); break;
+    case 8: d.string_width = (int32_t)rnd(12) - 2; break;
+    case 9: d.data_type = (int32_t)rnd(7) - 1; break;
+    case 10: d.is_sorted = !d.is_sorted; break;
+    default: d.has_inverted_index = !d.has_inverted_index; break;
+  }
+}
+
+void bind(ColumnBufs &cb, bool truncate) {
+  pinot_column_desc &d = cb.d;
+  d.dictionary = cb.dict.empty() ? nullptr : cb.dict.data();
+  d.dictionary_len = truncate ? trunc_len(cb.dict.size()) : cb.dict.size();
+  d.forward_index = cb.fwd.empty() ? nullptr : cb.fwd.data();
+  d.forward_index_len = truncate ? trunc_len(cb.fwd.size()) : cb.fwd.size();
+  d.sorted_index = cb.sorted.empty() ? nullptr : cb.sorted.data();
+  d.sorted_index_len = truncate ? trunc_len(cb.sorted.size()) : cb.sorted.size();
+  d.inverted_index = cb.inv.empty() ? nullptr : cb.inv.data();
+  d.inverted_index_len = truncate ? trunc_len(cb.inv.size()) : cb.inv.size();
+}
+
+const char *kLiterals[] = {"0", "1", "-1", "7", "2147483647", "-2147483648", "9223372036854775807", "1e9", "0.5",
+                           "-0.0", "NaN", "Infinity", "abc", "", " 3", "s00002", "s99999", "*", "1.0E7", "0x10"};
+
+std::string literal(bool range) {
+  if (range || coin(15)) {  // RANGE strings: "(lo\t\thi]" with inclusive / exclusive ends and '*'
+    std::string lo = coin(20) ? "*" : kLiterals[rnd(20)], hi = coin(20) ? "*" : kLiterals[rnd(20)];
+    return std::string(coin(50) ? "(" : "[") + lo + "\t\t" + hi + (coin(50) ? ")" : "]");
+  }
+  if (coin(10)) {
+    std::string s;
+    const int n = (int)rnd(12);
+    for (int i = 0; i < n; i++) s += (char)(1 + rnd(126));
+    return s;
+  }
+  return kLiterals[rnd(20)];
+}
+
+}  // namespace
+
+int main(int argc, char **argv) {
+  const long iters = argc > 1 ? atol(argv[1]) : 2000;
+  rng.seed(argc > 2 ? strtoull(argv[2], nullptr, 10) : 12345);
+  long accepted = 0, rejected = 0, plans = 0, plan_errors = 0, violations = 0, mutated_ok = 0;
+  for (long it = 0; it < iters; it++) {
+    const int32_t num_docs = coin(5) ? 0 : (int32_t)rnd(coin(10) ? 140000 : 3000) + 1;
+    const int ncols = 1 + (int)rnd(3);
+    std::vector<ColumnBufs> cols(ncols);
+    for (int c = 0; c < ncols; c++) make_column(cols[c], c, num_docs);
+    const bool corrupt = it % 4 != 0;  // every 4th segment stays valid: the well-formed path is covered too
+    if (corrupt) {
+      const int k = 1 + (int)rnd(3);
+      for (int i = 0; i < k; i++) mutate(cols[rnd(ncols)]);
+    }
+    std::vector<pinot_column_desc> descs;
+    for (auto &cb : cols) {
+      bind(cb, corrupt && coin(30));
+      descs.push_back(cb.d);
+    }
+    pinot_segment_desc seg{};
+    seg.name = "fuzz";
+    seg.num_docs = coin(3) ? -(int32_t)rnd(5) : num_docs;
+    seg.num_columns = ncols;
+    seg.columns = descs.data();
+    bool ok = false;
+    try {
+      validate_segment(seg);
+      ok = true;
+    } catch (const Error &e) {
+      if (e.status != PINOT_ERR_BAD_ARG && e.status != PINOT_ERR_UNSUPPORTED) {
+        fprintf(stderr, "iteration %ld: validate_segment status %d (%s)\n", it, (int)e.status, e.what());
+        violations++;
+      }
+    } catch (const std::exception &e) {
+      fprintf(stderr, "iteration %ld: validate_segment threw %s\n", it, e.what());
+      violations++;
+    }
+    if (!ok) {
+      rejected++;
+      continue;
+    }
+    accepted++;
+    if (corrupt) mutated_ok++;
+    if (!corrupt && seg.num_docs != num_docs) continue;
+    // planner over the accepted segment's host columns
+    SegmentData sd;
+    sd.name = "fuzz";
+    sd.num_docs = seg.num_docs;
+    for (int c = 0; c < ncols; c++) {
+      auto cd = std::make_unique<ColumnData>();
+      ParsedIndexes idx;
+      parse_column(*cd, descs[c], seg.num_docs, idx);
+      sd.by_name[cd->name] = (int)sd.cols.size();
+      sd.cols.push_back(std::move(cd));
+    }
+    for (int t = 0; t < 8; t++) {
+      const int n = 1 + (int)rnd(7);
+      std::vector<std::vector<std::string>> vals(n);
+      std::vector<std::vector<const char *>> vptr(n);
+      std::vector<std::string> colnames(n);
+      std::vector<pinot_filter_node> nodes(n);
+      const bool shaped = coin(70);  // a well-formed postfix tree (AND/OR over what the stack holds)
+      int depth = 0;
+      for (int i = 0; i < n; i++) {
+        pinot_filter_node &nd = nodes[i];
+        if (shaped) {
+          const bool combine = depth >= 2 && (i == n - 1 || coin(40));
+          static const int32_t kLeaf[] = {PINOT_FILTER_EQUALITY, PINOT_FILTER_RANGE, PINOT_FILTER_IN,
+                                          PINOT_FILTER_NOT_IN};
+          nd.op = combine ? (int32_t)rnd(2) : kLeaf[rnd(4)];
+          nd.num_children = combine ? 2 + (int32_t)rnd(depth - 1) : 0;
+          depth = combine ? depth - nd.num_children + 1 : depth + 1;
+        } else {
+          nd.op = coin(25) ? (int32_t)rnd(2) : (int32_t)rnd(9) - 1;
+          nd.num_children = (int32_t)rnd(4);
+        }
+        colnames[i] = coin(90) ? "c" + std::to_string(rnd(ncols)) : "nope";
+        nd.column = coin(97) ? colnames[i].c_str() : nullptr;
+        const int nv = shaped ? 1 + (int)rnd(3) : (int)rnd(4);
+        for (int k = 0; k < nv; k++) vals[i].push_back(literal(shaped && nd.op == PINOT_FILTER_RANGE));
+        for (auto &s : vals[i]) vptr[i].push_back(s.c_str());
+        nd.num_values = nv;
+        nd.values = vptr[i].data();
+      }
+      try {
+        FilterTreeInput tree = decode_filter(n, nodes.data());
+        FilterNode plan = plan_filter(sd, &tree);
+        (void)plan;
+        plans++;
+      } catch (const Error &e) {
+        plan_errors++;
+        if (e.status != PINOT_ERR_BAD_ARG && e.status != PINOT_ERR_BAD_QUERY && e.status != PINOT_ERR_UNSUPPORTED) {
+          fprintf(stderr, "iteration %ld: planner status %d (%s)\n", it, (int)e.status, e.what());
+          violations++;
+        }
+      } catch (const std::exception &e) {
+        fprintf(stderr, "iteration %ld: planner threw %s\n", it, e.what());
+        violations++;
+      }
+    }
+    for (int c = 0; c < ncols; c++) {  // key strings of every dictionary entry (Double/Float.toString)
+      const ColumnData &cd = *sd.cols[c];
+      for (int32_t id = 0; id < cd.card; id++) (void)cd.string_value(id);
+    }
+  }
+  for (int i = 0; i < 20000; i++) {  // Double.toString / Float.toString over arbitrary bit patterns
+    uint64_t u = rng();
+    double dv;
+    memcpy(&dv, &u, 8);
+    const std::string s = java_double_to_string(dv);
+    if (std::isfinite(dv) && strtod(s.c_str(), nullptr) != dv) {
+      fprintf(stderr, "Double.toString round trip: %s\n", s.c_str());
+      violations++;
+    }
+    uint32_t w = (uint32_t)u;
+    float fv;
+    memcpy(&fv, &w, 4);
+    const std::string f = java_float_to_string(fv);
+    if (std::isfinite(fv) && strtof(f.c_str(), nullptr) != fv) {
+      fprintf(stderr, "Float.toString round trip: %s\n", f.c_str());
+      violations++;
+    }
+  }
+  printf("fuzz_host iterations=%ld accepted=%ld rejected=%ld mutated_accepted=%ld plans=%ld plan_errors=%ld "
+         "violations=%ld\n", iters, accepted, rejected, mutated_ok, plans, plan_errors, violations);
+  return violations ? 1 : 0;
+}

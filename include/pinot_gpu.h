@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PINOT_GPU_ABI_VERSION 3
+#define PINOT_GPU_ABI_VERSION 4
 
 /* ------------------------------------------------------------------ status */
 typedef enum {
@@ -64,6 +64,10 @@ typedef struct {
   int32_t is_sorted;           /* sorted column: sorted_index present, forward_index absent */
   int32_t has_inverted_index;  /* bitmap inverted index present (unsorted columns) */
   int32_t string_width;        /* STRING dictionary: bytes per padded value */
+  int32_t padding_byte;        /* STRING dictionary padding (segment.padding.character; '%' on legacy segments,
+                                  ColumnMetadata.java:111-115): values end at the first such byte, and a non-zero
+                                  padding compares predicate values padded (ImmutableDictionaryReader.java:152-180) */
+  int32_t reserved;
   const uint8_t *dictionary;   uint64_t dictionary_len;     /* card * width BE values */
   const uint8_t *forward_index; uint64_t forward_index_len; /* ceil(N*b/8) bytes, MSB-first */
   const uint8_t *sorted_index; uint64_t sorted_index_len;   /* 2*card BE int32 [start,end] */
@@ -169,6 +173,15 @@ pinot_status pinot_gpu_engine_set_config(pinot_engine *engine, const char *confi
 pinot_status pinot_gpu_segment_register(pinot_engine *engine, const pinot_segment_desc *desc,
                                         pinot_segment_handle *out);
 pinot_status pinot_gpu_segment_release(pinot_engine *engine, pinot_segment_handle handle);
+/* ImmutableSegmentLoader.load (PC/indexsegment/immutable/ImmutableSegmentLoader.java:59-153) of a segment
+ * directory as Pinot writes it: v1/v2 (one file per index) or v3 (v3/columns.psf + v3/index_map), metadata from
+ * metadata.properties (SegmentMetadataImpl / ColumnMetadata; V1Constants.java:54-146). The files are memory-mapped,
+ * checked like pinot_gpu_segment_register's descriptors and copied to HBM. Multi-value, raw (no-dictionary) and
+ * BYTES columns are not served and are left out. */
+pinot_status pinot_gpu_segment_load(pinot_engine *engine, const char *index_dir, pinot_segment_handle *out);
+/* The same read and checks on the host only (no engine, no GPU): docs, served columns, left-out columns. */
+pinot_status pinot_gpu_segment_dir_info(const char *index_dir, int32_t *num_docs, int32_t *num_columns,
+                                        int32_t *num_skipped);
 /* Every check pinot_gpu_segment_register makes on the descriptor's bytes (dictionaries, forward-index
  * length, sorted-index tiling, inverted-index offsets and roaring containers), on the host only: no engine,
  * no GPU. PINOT_ERR_BAD_ARG + pinot_gpu_last_error() name the first bad column. */

@@ -179,6 +179,34 @@ pinot_status pinot_gpu_segment_register(pinot_engine *engine, const pinot_segmen
   });
 }
 
+pinot_status pinot_gpu_segment_load(pinot_engine *engine, const char *index_dir, pinot_segment_handle *out) {
+  return guard([&] {
+    require(engine && index_dir && out, PINOT_ERR_BAD_ARG, "null argument");
+    SegmentDirData files;
+    read_segment_dir(index_dir, files);
+    const pinot_segment_desc desc = files.desc();
+    std::lock_guard<std::mutex> lk(engine->mu);
+    set_device(*engine);
+    auto seg = register_segment(*engine, desc);
+    const int64_t h = engine->next_handle++;
+    engine->segments[h] = std::move(seg);
+    *out = h;
+  });
+}
+
+pinot_status pinot_gpu_segment_dir_info(const char *index_dir, int32_t *num_docs, int32_t *num_columns,
+                                        int32_t *num_skipped) {
+  return guard([&] {
+    require(index_dir != nullptr, PINOT_ERR_BAD_ARG, "null argument");
+    SegmentDirData files;
+    read_segment_dir(index_dir, files);
+    validate_segment(files.desc());
+    if (num_docs) *num_docs = files.num_docs;
+    if (num_columns) *num_columns = (int32_t)files.cols.size();
+    if (num_skipped) *num_skipped = (int32_t)files.skipped.size();
+  });
+}
+
 pinot_status pinot_gpu_segment_register_synthetic_ex(pinot_engine *engine, const char *name, int32_t num_docs,
                                                      int32_t num_columns, const char *const *column_names,
                                                      const int32_t *cardinalities, const int32_t *kinds, uint64_t seed,

@@ -21,6 +21,7 @@ struct ColumnData {
   bool is_sorted = false;
   bool has_inverted = false;
   int32_t string_width = 0;
+  int32_t string_pad = 0;             // STRING padding byte (0 = '\0'; legacy segments '%')
   int32_t num_docs = 0;
 
   // host copies (dictionary-sized; used for predicate evaluation and key materialisation)
@@ -62,6 +63,26 @@ void parse_column(ColumnData &c, const pinot_column_desc &d, int32_t num_docs, P
 void validate_segment(const pinot_segment_desc &d);
 std::string java_double_to_string(double v);  // Double.toString
 std::string java_float_to_string(float v);    // Float.toString
+
+// segment_reader.cpp: a Pinot segment directory (v1 / v2 files, or v3 columns.psf + index_map) mapped read-only
+// and described as a pinot_segment_desc (ImmutableSegmentLoader.load's inputs).
+struct MappedFile {
+  const uint8_t *data = nullptr;
+  size_t size = 0;
+  explicit MappedFile(const std::string &path);
+  ~MappedFile();
+  MappedFile(const MappedFile &) = delete;
+  MappedFile &operator=(const MappedFile &) = delete;
+};
+struct SegmentDirData {
+  std::string name;
+  int32_t num_docs = 0;
+  std::vector<std::string> column_names, skipped;  // served columns; multi-value / raw / BYTES columns left out
+  std::vector<pinot_column_desc> cols;
+  std::vector<std::unique_ptr<MappedFile>> files;
+  pinot_segment_desc desc() const;
+};
+void read_segment_dir(const std::string &index_dir, SegmentDirData &out);
 
 struct SegmentData {
   std::string name;

@@ -89,12 +89,24 @@ int64_t insertion_index_of(const ColumnData &c, const std::string &raw) {
       const double v = java_parse_double(raw);
       return search([&](int64_t m) { return c.dict_dbl[m] < v ? -1 : c.dict_dbl[m] > v ? 1 : 0; });
     }
-    default:
-      // String.compareTo over unpadded values (padding byte 0); byte order == code-point order for UTF-8
+    default: {
+      // String.compareTo; byte order == code-point order for UTF-8. Padding byte 0: unpadded values. Any other
+      // padding (legacy '%' segments): the value padded to the width against the full-width entries
+      // (ImmutableDictionaryReader.binarySearch / padString, ImmutableDictionaryReader.java:152-216).
+      if (c.string_pad == 0)
+        return search([&](int64_t m) {
+          int r = c.dict_str[m].compare(raw);
+          return r < 0 ? -1 : r > 0 ? 1 : 0;
+        });
+      const size_t w = (size_t)c.string_width;
+      std::string padded = raw;
+      if (padded.size() < w) padded.append(w - padded.size(), (char)c.string_pad);
       return search([&](int64_t m) {
-        int r = c.dict_str[m].compare(raw);
+        const std::string entry(reinterpret_cast<const char *>(c.dict_be.data()) + (size_t)m * w, w);
+        int r = entry.compare(padded);
         return r < 0 ? -1 : r > 0 ? 1 : 0;
       });
+    }
   }
 }
 

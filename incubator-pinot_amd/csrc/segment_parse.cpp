@@ -17,9 +17,9 @@
 namespace pinot {
 
 // ---------------------------------------------------------------- Java Double.toString / Float.toString
-// The digits are the shortest decimal that reads back as the same double (float): the correctly rounded
-// p-digit form for the smallest p that round-trips (the Double.toString javadoc's "as many, but only as many,
-// more digits as are needed to uniquely distinguish the argument value from adjacent values"). Layout:
+// The digits are the shortest decimal that reads back as the same double (float), the closest such if several,
+// and when one digit suffices the closest of the 1- and 2-digit ones (Double.toString javadoc, JDK 19+ wording:
+// Double.MIN_VALUE -> 4.9E-324, Float.MIN_VALUE -> 1.4E-45). Layout:
 // plain decimal with at least one fraction digit for 1e-3 <= |v| < 1e7, else d.dddE<exp>
 // (DoubleDictionary.getStringValue -> Double.toString, PC/segment/index/readers/DoubleDictionary.java:73-75).
 static std::string java_layout(bool neg, const std::string &digits, int exp10) {
@@ -39,29 +39,56 @@ static std::string java_layout(bool neg, const std::string &digits, int exp10) {
   return out;
 }
 
-// "%.*e" output -> (digits without trailing zeros, decimal exponent)
-static void split_sci(const char *buf, std::string &digits, int &exp10) {
-  digits.clear();
-  const char *p = buf;
-  if (*p == '-') p++;
-  for (; *p && *p != 'e'; p++)
-    if (*p >= '0' && *p <= '9') digits += *p;
-  exp10 = *p == 'e' ? atoi(p + 1) : 0;
-  while (digits.size() > 1 && digits.back() == '0') digits.pop_back();
+// Shortest digits of a finite positive v: for p = 1, 2, ... the correctly rounded p-digit decimal D x 10^q, or, when
+// that one misses v's rounding interval (asymmetric at powers of two), its neighbour D -/+ 1 in the last place
+// if that one reads back as v. Returns the digits without trailing zeros and the exponent of the first digit.
+template <typename T>
+static void shortest_digits(T v, int max_p, std::string &digits, int &exp10) {
+  auto reads_back = [&](unsigned long long d, int q) {
+    char b[48];
+    snprintf(b, sizeof(b), "%llue%d", d, q);
+    if constexpr (sizeof(T) == 4) return strtof(b, nullptr) == v;
+    else return strtod(b, nullptr) == v;
+  };
+  char buf[64];
+  for (int p = 1; p <= max_p; p++) {
+    snprintf(buf, sizeof(buf), "%.*e", p - 1, (double)v);
+    unsigned long long d = 0;
+    const char *c = buf;
+    for (; *c && *c != 'e'; c++)
+      if (*c >= '0' && *c <= '9') d = d * 10 + (unsigned long long)(*c - '0');
+    const int e = atoi(c + 1), q = e - (p - 1);
+    unsigned long long pick = 0;
+    int pq = q;
+    if (reads_back(d, q)) pick = d;
+    else if (d > 1 && reads_back(d - 1, q)) pick = d - 1;
+    else if (reads_back(d + 1, q)) pick = d + 1;
+    if (pick && p == 1) {  // one digit suffices: the javadoc then takes the closest of the 1- and 2-digit decimals
+      snprintf(buf, sizeof(buf), "%.1e", (double)v);
+      const unsigned long long d2 = (unsigned long long)(buf[0] - '0') * 10 + (unsigned long long)(buf[2] - '0');
+      const int q2 = atoi(buf + 4) - 1;
+      if (reads_back(d2, q2)) {
+        pick = d2;
+        pq = q2;
+      }
+    }
+    if (pick || p == max_p) {
+      if (!pick) pick = d;
+      digits = std::to_string(pick);
+      exp10 = pq + (int)digits.size() - 1;
+      while (digits.size() > 1 && digits.back() == '0') digits.pop_back();
+      return;
+    }
+  }
 }
 
 std::string java_double_to_string(double v) {
   if (std::isnan(v)) return "NaN";
   if (std::isinf(v)) return v > 0 ? "Infinity" : "-Infinity";
   if (v == 0) return std::signbit(v) ? "-0.0" : "0.0";
-  char buf[64];
-  for (int p = 1; p <= 17; p++) {
-    snprintf(buf, sizeof(buf), "%.*e", p - 1, v);
-    if (strtod(buf, nullptr) == v) break;
-  }
   std::string digits;
   int e10;
-  split_sci(buf, digits, e10);
+  shortest_digits<double>(std::fabs(v), 17, digits, e10);
   return java_layout(v < 0, digits, e10);
 }
 
@@ -69,14 +96,9 @@ std::string java_float_to_string(float v) {
   if (std::isnan(v)) return "NaN";
   if (std::isinf(v)) return v > 0 ? "Infinity" : "-Infinity";
   if (v == 0) return std::signbit(v) ? "-0.0" : "0.0";
-  char buf[64];
-  for (int p = 1; p <= 9; p++) {
-    snprintf(buf, sizeof(buf), "%.*e", p - 1, (double)v);
-    if (strtof(buf, nullptr) == v) break;
-  }
   std::string digits;
   int e10;
-  split_sci(buf, digits, e10);
+  shortest_digits<float>(std::fabs(v), 9, digits, e10);
   return java_layout(v < 0, digits, e10);
 }
 
@@ -151,8 +173,8 @@ static void decode_dictionary(ColumnData &c, const pinot_column_desc &d) {
       c.dict_str.resize(card);
       for (int64_t i = 0; i < card; i++) {
         const char *s = reinterpret_cast<const char *>(p + (size_t)i * w);
-        size_t n = 0;
-        while (n < (size_t)w && s[n] != 0) n++;  // getUnpaddedString: stop at the first padding byte
+        size_t n = 0;  // getUnpaddedString: stop at the first padding byte (FixedByteValueReaderWriter.java:56-68)
+        while (n < (size_t)w && (uint8_t)s[n] != (uint8_t)c.string_pad) n++;
         c.dict_str[i].assign(s, n);
       }
       break;
@@ -252,6 +274,8 @@ void parse_column(ColumnData &c, const pinot_column_desc &d, int32_t num_docs, P
   c.is_sorted = d.is_sorted != 0;
   c.has_inverted = d.has_inverted_index != 0 || c.is_sorted;
   c.string_width = d.string_width;
+  require(d.padding_byte >= 0 && d.padding_byte <= 255, PINOT_ERR_BAD_ARG, c.name + ": padding byte out of range");
+  c.string_pad = d.padding_byte;
   c.num_docs = num_docs;
   require(c.card >= 1 || num_docs == 0, PINOT_ERR_BAD_ARG, c.name + ": empty dictionary");
   require(c.bits >= 1 && c.bits <= 32, PINOT_ERR_BAD_ARG, c.name + ": bits out of range");

@@ -1,0 +1,358 @@
+// Pinot segment directories -> pinot_segment_desc (host only; registration then uploads what it describes).
+//
+// Restates the parts of the reference's loader this path needs (PC = pinot-core/src/main/java/org/apache/pinot/core):
+//   layout         SegmentDirectoryPaths.findSegmentDirectory: <indexDir>/v3 when it exists, else <indexDir>
+//                  (PC/segment/store/SegmentDirectoryPaths.java:41-56)
+//   metadata       metadata.properties, Apache Commons PropertiesConfiguration syntax; SegmentMetadataImpl.init /
+//                  ColumnMetadata.fromPropertiesConfiguration (PC/segment/index/SegmentMetadataImpl.java:219-260,
+//                  PC/segment/index/ColumnMetadata.java:87-116); keys from V1Constants (PC/segment/creator/impl/
+//                  V1Constants.java:54-146)
+//   v1 / v2        FilePerIndexDirectory: <col>.dict, <col>.sv.unsorted.fwd | <col>.sv.sorted.fwd, <col>.bitmap.inv
+//                  (PC/segment/store/FilePerIndexDirectory.java:148-168, SegmentMetadataImpl.java:498-527)
+//   v3             SingleFileIndexDirectory: columns.psf + index_map ("<col>.<index>.startOffset|size = n"); each
+//                  entry starts with the 8-byte magic 0xdeadbeefdeafbead, counted in its size
+//                  (PC/segment/store/SingleFileIndexDirectory.java:62-320)
+// Files are memory-mapped read-only. Columns this executor does not serve (multi-value, raw / no-dictionary,
+// BYTES) are skipped and named by pinot_gpu_segment_dir_info; queries naming them fail as unknown columns.
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <cstring>
+#include <map>
+#include <set>
+
+#include "engine.h"
+
+namespace pinot {
+
+namespace {
+
+constexpr uint64_t kV3Magic = 0xdeadbeefdeafbeadull;
+
+bool is_dir(const std::string &p) {
+  struct stat st;
+  return stat(p.c_str(), &st) == 0 && S_ISDIR(st.st_mode);
+}
+bool is_file(const std::string &p) {
+  struct stat st;
+  return stat(p.c_str(), &st) == 0 && S_ISREG(st.st_mode);
+}
+
+std::string read_text(const std::string &path) {
+  const int fd = open(path.c_str(), O_RDONLY);
+  require(fd >= 0, PINOT_ERR_BAD_ARG, "cannot open " + path);
+  std::string out;
+  char buf[65536];
+  for (;;) {
+    const ssize_t n = read(fd, buf, sizeof(buf));
+    if (n <= 0) break;
+    out.append(buf, (size_t)n);
+  }
+  close(fd);
+  return out;
+}
+
+// Commons-Configuration-1.x properties: '#'/'!' comments, key and value split at the first unescaped '=', ':'
+// or whitespace, trailing-backslash continuation, Java escapes (\\, \t, \n, \r, \f, \uXXXX) in keys and values.
+std::string unescape_properties(const std::string &s) {
+  std::string o;
+  for (size_t i = 0; i < s.size(); i++) {
+    if (s[i] != '\\' || i + 1 == s.size()) {
+      o += s[i];
+      continue;
+    }
+    const char c = s[++i];
+    switch (c) {
+      case 't': o += '\t'; break;
+      case 'n': o += '\n'; break;
+      case 'r': o += '\r'; break;
+      case 'f': o += '\f'; break;
+      case 'u': {
+        require(i + 4 < s.size(), PINOT_ERR_BAD_ARG, "metadata.properties: bad \\u escape");
+        const unsigned long cp = strtoul(s.substr(i + 1, 4).c_str(), nullptr, 16);
+        i += 4;
+        if (cp < 0x80) {
+          o += (char)cp;
+        } else if (cp < 0x800) {
+          o += (char)(0xC0 | (cp >> 6));
+          o += (char)(0x80 | (cp & 0x3F));
+        } else {
+          o += (char)(0xE0 | (cp >> 12));
+          o += (char)(0x80 | ((cp >> 6) & 0x3F));
+          o += (char)(0x80 | (cp & 0x3F));
+        }
+        break;
+      }
+      default: o += c;  // \\ \= \: \, \# and any other char stand for themselves
+    }
+  }
+  return o;
+}
+
+std::string trim(const std::string &s) {
+  size_t a = 0, b = s.size();
+  while (a < b && (s[a] == ' ' || s[a] == '\t' || s[a] == '\f')) a++;
+  while (b > a && (s[b - 1] == ' ' || s[b - 1] == '\t' || s[b - 1] == '\f' || s[b - 1] == '\r')) b--;
+  return s.substr(a, b - a);
+}
+
+std::map<std::string, std::string> parse_properties(const std::string &text) {
+  std::map<std::string, std::string> kv;
+  std::vector<std::string> lines;
+  std::string cur;  // a line ending in an odd number of backslashes continues on the next (leading blanks dropped)
+  size_t i = 0;
+  while (i < text.size()) {
+    const size_t e = std::min(text.find('\n', i), text.size());
+    std::string line = text.substr(i, e - i);
+    i = e + 1;
+    if (!line.empty() && line.back() == '\r') line.pop_back();
+    if (!cur.empty()) line = trim(line);
+    size_t nbs = 0;
+    while (nbs < line.size() && line[line.size() - 1 - nbs] == '\\') nbs++;
+    if (nbs % 2 == 1) {
+      cur += line.substr(0, line.size() - 1);
+      continue;
+    }
+    lines.push_back(cur + line);
+    cur.clear();
+  }
+  if (!cur.empty()) lines.push_back(cur);
+  for (const std::string &raw : lines) {
+    const std::string line = trim(raw);
+    if (line.empty() || line[0] == '#' || line[0] == '!') continue;
+    size_t sep = std::string::npos;
+    for (size_t i = 0; i < line.size(); i++) {
+      if (line[i] == '\\') {
+        i++;
+        continue;
+      }
+      if (line[i] == '=' || line[i] == ':' || line[i] == ' ' || line[i] == '\t') {
+        sep = i;
+        break;
+      }
+    }
+    std::string key = sep == std::string::npos ? line : line.substr(0, sep);
+    std::string value = sep == std::string::npos ? "" : trim(line.substr(sep + 1));
+    if (sep != std::string::npos && (line[sep] == ' ' || line[sep] == '\t') && !value.empty() &&
+        (value[0] == '=' || value[0] == ':'))
+      value = trim(value.substr(1));
+    kv[unescape_properties(trim(key))] = value;  // values unescaped per use (lists split on unescaped ',')
+  }
+  return kv;
+}
+
+// getList: split on unescaped ',' (Commons list delimiter), each element trimmed and unescaped; empty -> none
+std::vector<std::string> prop_list(const std::map<std::string, std::string> &kv, const std::string &key) {
+  std::vector<std::string> out;
+  auto it = kv.find(key);
+  if (it == kv.end()) return out;
+  const std::string &v = it->second;
+  std::string cur;
+  for (size_t i = 0; i <= v.size(); i++) {
+    if (i == v.size() || v[i] == ',') {
+      const std::string t = trim(unescape_properties(cur));
+      if (!t.empty()) out.push_back(t);
+      cur.clear();
+    } else {
+      if (v[i] == '\\' && i + 1 < v.size()) cur += v[i++];
+      cur += v[i];
+    }
+  }
+  return out;
+}
+
+std::string prop(const std::map<std::string, std::string> &kv, const std::string &key, const char *dflt = nullptr) {
+  auto it = kv.find(key);
+  if (it == kv.end()) {
+    require(dflt != nullptr, PINOT_ERR_BAD_ARG, "metadata.properties: missing " + key);
+    return dflt;
+  }
+  return unescape_properties(it->second);
+}
+
+int64_t prop_int(const std::map<std::string, std::string> &kv, const std::string &key, const char *dflt = nullptr) {
+  const std::string v = prop(kv, key, dflt);
+  char *end = nullptr;
+  errno = 0;
+  const long long x = strtoll(v.c_str(), &end, 10);
+  require(errno == 0 && end && *end == 0 && !v.empty(), PINOT_ERR_BAD_ARG, "metadata.properties: " + key + " = " + v);
+  return x;
+}
+
+bool prop_bool(const std::map<std::string, std::string> &kv, const std::string &key, bool dflt) {
+  auto it = kv.find(key);
+  if (it == kv.end()) return dflt;
+  std::string v = trim(unescape_properties(it->second));
+  std::transform(v.begin(), v.end(), v.begin(), ::tolower);
+  return v == "true" || v == "on" || v == "yes";
+}
+
+int data_type_of(std::string t) {
+  std::transform(t.begin(), t.end(), t.begin(), ::toupper);
+  if (t == "INT") return PINOT_INT;
+  if (t == "LONG") return PINOT_LONG;
+  if (t == "FLOAT") return PINOT_FLOAT;
+  if (t == "DOUBLE") return PINOT_DOUBLE;
+  if (t == "STRING") return PINOT_STRING;
+  return -1;  // BYTES, BOOLEAN, ...: not served here
+}
+
+}  // namespace
+
+MappedFile::MappedFile(const std::string &path) {
+  const int fd = open(path.c_str(), O_RDONLY);
+  require(fd >= 0, PINOT_ERR_BAD_ARG, "cannot open " + path);
+  struct stat st;
+  if (fstat(fd, &st) != 0) {
+    close(fd);
+    throw Error(PINOT_ERR_BAD_ARG, "cannot stat " + path);
+  }
+  size = (size_t)st.st_size;
+  if (size) {
+    void *m = mmap(nullptr, size, PROT_READ, MAP_PRIVATE, fd, 0);
+    if (m == MAP_FAILED) {
+      close(fd);
+      throw Error(PINOT_ERR_BAD_ARG, "cannot map " + path);
+    }
+    data = static_cast<const uint8_t *>(m);
+  }
+  close(fd);
+}
+
+MappedFile::~MappedFile() {
+  if (data) munmap(const_cast<uint8_t *>(data), size);
+}
+
+void read_segment_dir(const std::string &index_dir, SegmentDirData &out) {
+  require(is_dir(index_dir), PINOT_ERR_BAD_ARG, "not a segment directory: " + index_dir);
+  const std::string v3 = index_dir + "/v3";
+  const std::string dir = is_dir(v3) ? v3 : index_dir;
+  const std::string meta_path = is_file(dir + "/metadata.properties") ? dir + "/metadata.properties"
+                                                                      : index_dir + "/metadata.properties";
+  const auto kv = parse_properties(read_text(meta_path));
+  const std::string version = prop(kv, "segment.index.version", "v1");
+  const bool single_file = version == "v3";
+  require(version == "v1" || version == "v2" || version == "v3", PINOT_ERR_UNSUPPORTED, "segment version " + version);
+  require(!single_file || dir == v3, PINOT_ERR_BAD_ARG, "v3 segment without a v3/ directory: " + index_dir);
+  out.name = prop(kv, "segment.name", "");
+  const int64_t total = prop_int(kv, "segment.total.docs", nullptr);
+  require(total >= 0 && total < INT32_MAX, PINOT_ERR_BAD_ARG, "segment.total.docs out of range");
+  out.num_docs = (int32_t)total;
+  // padding: segment key, else the legacy '%' (ColumnMetadata.java:111-115)
+  int pad = '%';
+  if (kv.count("segment.padding.character")) {
+    const std::string p = unescape_properties(prop(kv, "segment.padding.character"));  // unescapeJava of the value
+    require(!p.empty(), PINOT_ERR_BAD_ARG, "empty segment.padding.character");
+    pad = (uint8_t)p[0];
+  }
+
+  // physical columns in the order SegmentMetadataImpl adds them (dimensions, metrics, time, date-time)
+  std::vector<std::string> names;
+  std::set<std::string> seen;
+  for (const char *key : {"segment.dimension.column.names", "segment.metric.column.names", "segment.time.column.name",
+                          "segment.datetime.column.names"})
+    for (const std::string &c : prop_list(kv, key))
+      if (seen.insert(c).second) names.push_back(c);
+
+  // v3: index_map entries -> (offset, size) of each (column, index) inside columns.psf
+  std::map<std::string, std::pair<uint64_t, uint64_t>> entries;
+  const MappedFile *psf = nullptr;
+  if (single_file) {
+    const auto im = parse_properties(read_text(dir + "/index_map"));
+    std::map<std::string, std::pair<int64_t, int64_t>> raw;
+    for (const auto &e : im) {
+      const size_t last = e.first.rfind('.');
+      require(last != std::string::npos && last > 0, PINOT_ERR_BAD_ARG, "index_map key " + e.first);
+      const std::string what = e.first.substr(last + 1), idx = e.first.substr(0, last);
+      auto &slot = raw.emplace(idx, std::make_pair((int64_t)-1, (int64_t)-1)).first->second;
+      const int64_t v = prop_int(im, e.first);
+      if (what == "startOffset") slot.first = v;
+      else if (what == "size") slot.second = v;
+      else throw Error(PINOT_ERR_BAD_ARG, "index_map key " + e.first);
+    }
+    out.files.emplace_back(new MappedFile(dir + "/columns.psf"));
+    psf = out.files.back().get();
+    for (const auto &r : raw) {
+      const int64_t off = r.second.first, size = r.second.second;
+      require(off >= 0 && size >= 8 && (uint64_t)off <= psf->size && (uint64_t)size <= psf->size - (uint64_t)off,
+              PINOT_ERR_BAD_ARG, "index_map entry " + r.first + " outside columns.psf");
+      uint64_t magic = 0;
+      for (int i = 0; i < 8; i++) magic = (magic << 8) | psf->data[off + i];
+      require(magic == kV3Magic, PINOT_ERR_BAD_ARG, "columns.psf: missing magic marker for " + r.first);
+      entries[r.first] = {(uint64_t)off + 8, (uint64_t)size - 8};
+    }
+  }
+  auto index_bytes = [&](const std::string &col, const char *index, const std::string &v1_file, const uint8_t **p,
+                         uint64_t *n) -> bool {
+    if (single_file) {
+      auto it = entries.find(col + "." + index);
+      if (it == entries.end()) return false;
+      *p = psf->data + it->second.first;
+      *n = it->second.second;
+      return true;
+    }
+    const std::string path = dir + "/" + v1_file;
+    if (!is_file(path)) return false;
+    out.files.emplace_back(new MappedFile(path));
+    *p = out.files.back()->data;
+    *n = out.files.back()->size;
+    return true;
+  };
+
+  out.column_names.reserve(names.size());
+  for (const std::string &c : names) {
+    const std::string k = "column." + c + ".";
+    const int dt = data_type_of(prop(kv, k + "dataType"));
+    const bool single = prop_bool(kv, k + "isSingleValues", true), dict = prop_bool(kv, k + "hasDictionary", true);
+    if (dt < 0 || !single || !dict) {
+      out.skipped.push_back(c);
+      continue;
+    }
+    out.column_names.push_back(c);
+    pinot_column_desc d{};
+    d.data_type = dt;
+    const int64_t card = prop_int(kv, k + "cardinality"), bits = prop_int(kv, k + "bitsPerElement");
+    const int64_t width = prop_int(kv, k + "lengthOfEachEntry", "0");
+    require(card >= 0 && card < INT32_MAX && bits >= 0 && bits <= 64 && width >= 0 && width < INT32_MAX,
+            PINOT_ERR_BAD_ARG, c + ": column metadata out of range");
+    d.cardinality = (int32_t)card;
+    d.bits_per_value = (int32_t)bits;
+    d.string_width = (int32_t)width;
+    d.padding_byte = dt == PINOT_STRING ? pad : 0;
+    d.is_sorted = prop_bool(kv, k + "isSorted", false) ? 1 : 0;
+    require(index_bytes(c, "dictionary", c + ".dict", &d.dictionary, &d.dictionary_len), PINOT_ERR_BAD_ARG,
+            c + ": no dictionary");
+    const uint8_t *fp = nullptr;
+    uint64_t fn = 0;
+    require(index_bytes(c, "forward_index", c + (d.is_sorted ? ".sv.sorted.fwd" : ".sv.unsorted.fwd"), &fp, &fn),
+            PINOT_ERR_BAD_ARG, c + ": no forward index");
+    if (d.is_sorted) {
+      d.sorted_index = fp;
+      d.sorted_index_len = fn;
+    } else {
+      d.forward_index = fp;
+      d.forward_index_len = fn;
+      // the bitmap index is used when the segment holds one (hasInvertedIndex with no file: none was built)
+      if (prop_bool(kv, k + "hasInvertedIndex", false) &&
+          index_bytes(c, "inverted_index", c + ".bitmap.inv", &d.inverted_index, &d.inverted_index_len))
+        d.has_inverted_index = 1;
+    }
+    out.cols.push_back(d);
+  }
+  for (size_t i = 0; i < out.cols.size(); i++) out.cols[i].name = out.column_names[i].c_str();
+}
+
+pinot_segment_desc SegmentDirData::desc() const {
+  pinot_segment_desc d{};
+  d.name = name.c_str();
+  d.num_docs = num_docs;
+  d.num_columns = (int32_t)cols.size();
+  d.columns = cols.data();
+  return d;
+}
+
+}  // namespace pinot

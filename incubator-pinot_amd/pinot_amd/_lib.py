@@ -22,6 +22,7 @@ EXPORTED_SYMBOLS = [
     "pinot_gpu_last_error", "pinot_gpu_abi_version", "pinot_gpu_device_count",
     "pinot_gpu_engine_create", "pinot_gpu_engine_destroy", "pinot_gpu_engine_set_config",
     "pinot_gpu_segment_register", "pinot_gpu_segment_release", "pinot_gpu_segment_validate",
+    "pinot_gpu_segment_load", "pinot_gpu_segment_dir_info",
     "pinot_gpu_segment_device_bytes", "pinot_gpu_filter", "pinot_gpu_aggregate", "pinot_gpu_group_by",
     "pinot_groupby_num_groups", "pinot_groupby_num_columns", "pinot_groupby_key", "pinot_groupby_values",
     "pinot_groupby_hll", "pinot_groupby_raw_keys", "pinot_groupby_export_keys", "pinot_groupby_trim",
@@ -43,7 +44,7 @@ class PinotGpuError(RuntimeError):
 class ColumnDesc(C.Structure):
     _fields_ = [("name", C.c_char_p), ("data_type", C.c_int32), ("cardinality", C.c_int32),
                 ("bits_per_value", C.c_int32), ("is_sorted", C.c_int32), ("has_inverted_index", C.c_int32),
-                ("string_width", C.c_int32),
+                ("string_width", C.c_int32), ("padding_byte", C.c_int32), ("reserved", C.c_int32),
                 ("dictionary", C.c_void_p), ("dictionary_len", C.c_uint64),
                 ("forward_index", C.c_void_p), ("forward_index_len", C.c_uint64),
                 ("sorted_index", C.c_void_p), ("sorted_index_len", C.c_uint64),
@@ -142,6 +143,8 @@ def load(path=None):
         "pinot_gpu_segment_register": (i32, [P, C.POINTER(SegmentDesc), C.POINTER(i64)]),
         "pinot_gpu_segment_release": (i32, [P, i64]),
         "pinot_gpu_segment_validate": (i32, [C.POINTER(SegmentDesc)]),
+        "pinot_gpu_segment_load": (i32, [P, C.c_char_p, C.POINTER(i64)]),
+        "pinot_gpu_segment_dir_info": (i32, [C.c_char_p, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32)]),
         "pinot_gpu_segment_device_bytes": (i32, [P, i64, C.POINTER(u64)]),
         "pinot_gpu_filter": (i32, [P, i64, i32, C.POINTER(FilterNode), P, C.POINTER(i64)]),
         "pinot_gpu_aggregate": (i32, [P, C.POINTER(i64), i32, C.POINTER(Query), C.POINTER(AggResult),

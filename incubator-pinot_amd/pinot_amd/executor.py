@@ -14,6 +14,7 @@ All compute happens in libpinot_gpu.so; this module only marshals arguments.
 """
 import ctypes as C
 import math
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -89,6 +90,7 @@ def segment_desc(seg: Segment):
         d.is_sorted = int(col.is_sorted)
         d.has_inverted_index = int(col.has_inverted_index and not col.is_sorted)
         d.string_width = col.string_width
+        d.padding_byte = col.padding if col.data_type == "STRING" else 0
         for field, data in (("dictionary", col.dictionary), ("forward_index", col.fwd),
                             ("sorted_index", col.sorted_index), ("inverted_index", col.inverted)):
             if data is None:
@@ -100,6 +102,15 @@ def segment_desc(seg: Segment):
     sname = seg.name.encode()
     keep += [sname, cols]
     return _lib.SegmentDesc(sname, seg.num_docs, len(seg.columns), cols), keep
+
+
+def segment_dir_info(index_dir: str):
+    """pinot_gpu_segment_dir_info: (num_docs, served columns, left-out columns) of a segment directory, read and
+    checked on the host only."""
+    lib = _lib.load()
+    n, c, k = C.c_int32(), C.c_int32(), C.c_int32()
+    check(lib.pinot_gpu_segment_dir_info(os.fsencode(index_dir), C.byref(n), C.byref(c), C.byref(k)))
+    return n.value, c.value, k.value
 
 
 def validate_segment(seg: Segment) -> None:
@@ -147,6 +158,14 @@ class GpuEngine:
         h = C.c_int64()
         check(self.lib.pinot_gpu_segment_register(self.ptr, C.byref(desc), C.byref(h)))
         return GpuSegment(self, h.value, seg.name, seg.num_docs)
+
+    def load(self, index_dir: str) -> GpuSegment:
+        """pinot_gpu_segment_load: a Pinot segment directory (v1/v2 files or v3 columns.psf) straight to HBM."""
+        h = C.c_int64()
+        check(self.lib.pinot_gpu_segment_load(self.ptr, os.fsencode(index_dir), C.byref(h)))
+        n = C.c_int32()
+        check(self.lib.pinot_gpu_segment_dir_info(os.fsencode(index_dir), C.byref(n), None, None))
+        return GpuSegment(self, h.value, os.path.basename(os.path.normpath(index_dir)), n.value)
 
     SYNTH_KIND = {"random": 0, "sorted": 1, "inverted": 2}
 

@@ -146,6 +146,7 @@ class Column:
     fwd: Optional[bytes] = None  # fixed-bit packed forward index (unsorted columns)
     sorted_index: Optional[bytes] = None  # 2*card BE ints (sorted columns)
     inverted: Optional[bytes] = None      # bitmap inverted index (unsorted columns)
+    padding: int = 0                      # STRING padding byte (segment.padding.character; legacy segments '%')
     _dict_values: Optional[np.ndarray] = field(default=None, repr=False)
     _dict_ids: Optional[np.ndarray] = field(default=None, repr=False)
 
@@ -159,7 +160,7 @@ class Column:
                 vals = []
                 for r in raw:
                     bs = bytes(r)
-                    z = bs.find(b"\x00")
+                    z = bs.find(bytes([self.padding]))  # getUnpaddedString: up to the first padding byte
                     vals.append((bs if z < 0 else bs[:z]).decode("utf-8"))
                 self._dict_values = np.array(vals, dtype=object)
             else:

@@ -26,6 +26,8 @@ the Thrift BrokerRequest the hot path reads, `request.thrift:26-168`):
                    | {"operator": "EQUALITY"|"NOT"|"RANGE"|"IN"|"NOT_IN", "column": c, "values": [str]},
    "group_by": None | {"columns": [...], "top_n": 10}}
 """
+import decimal
+import fractions
 import math
 import numpy as np
 
@@ -160,6 +162,13 @@ def insertion_index_of(col, raw: str) -> int:
     low, high = 0, len(vals) - 1
     key = (lambda x: x.encode("utf-8")) if col.data_type == "STRING" else (lambda x: x)
     kv = key(v)
+    if col.data_type == "STRING" and getattr(col, "padding", 0):
+        # non-zero padding: the padded value against the full-width entries (ImmutableDictionaryReader.java:165-216)
+        w = col.string_width
+        if len(kv) < w:
+            kv = kv + bytes([col.padding]) * (w - len(kv))
+        vals = [col.dictionary[i * w:(i + 1) * w] for i in range(col.cardinality)]
+        key = lambda x: x  # noqa: E731
     while low <= high:
         mid = (low + high) >> 1
         mv = key(vals[mid])
@@ -487,19 +496,106 @@ def _prod(xs):
 
 
 def _string_value(col, v):
-    """`Dictionary.getStringValue`: Integer/Long/Float/Double.toString or the unpadded string."""
+    """`Dictionary.getStringValue`: Integer/Long/Float/Double.toString or the unpadded string
+    (FloatDictionary / DoubleDictionary.getStringValue, PC/segment/index/readers/DoubleDictionary.java:73-75)."""
     if col.data_type in ("INT", "LONG"):
         return str(int(v))
-    if col.data_type in ("FLOAT", "DOUBLE"):
-        return _java_double_str(float(v))
+    if col.data_type == "FLOAT":
+        return java_float_to_string(v)
+    if col.data_type == "DOUBLE":
+        return java_double_to_string(float(v))
     return v
 
 
-def _java_double_str(x):
-    r = repr(float(x))
-    if r.endswith(".0"):
-        return r
-    return r
+def _java_layout(neg, digits, exp10):
+    """Double.toString's layout of a decimal digits x 10^exp10 (one digit before the point): plain with at least
+    one fraction digit for 1e-3 <= |v| < 1e7, computerized scientific notation d.dddE<n> otherwise."""
+    out = "-" if neg else ""
+    if -3 <= exp10 < 7:
+        if exp10 >= 0:
+            ip = digits[:exp10 + 1].ljust(exp10 + 1, "0")
+            fp = digits[exp10 + 1:] or "0"
+            return out + ip + "." + fp
+        return out + "0." + "0" * (-exp10 - 1) + digits
+    return out + digits[0] + "." + (digits[1:] or "0") + "E" + str(exp10)
+
+
+def _special(x):
+    if x != x:
+        return "NaN"
+    if math.isinf(x):
+        return "Infinity" if x > 0 else "-Infinity"
+    if x == 0:
+        return "-0.0" if math.copysign(1.0, x) < 0 else "0.0"
+    return None
+
+
+def _digits_exp(s):
+    """Decimal string -> (significant digits without trailing zeros, exponent of the first digit)."""
+    sign, digs, e = decimal.Decimal(s).as_tuple()
+    exp10 = len(digs) + e - 1
+    digits = "".join(map(str, digs)).rstrip("0") or "0"
+    return digits, exp10
+
+
+def java_double_to_string(x):
+    """`Double.toString` (its javadoc: as many digits as needed to uniquely distinguish the value from the
+    adjacent doubles; among the shortest, the closest). Python's repr picks exactly that digit string."""
+    x = float(x)
+    sp = _special(x)
+    if sp is not None:
+        return sp
+    digits, exp10 = _digits_exp(repr(abs(x)))
+    if len(digits) == 1:  # one digit suffices: the closest of the 1- and 2-digit decimals (Double.MIN_VALUE -> 4.9E-324)
+        two = "%.1e" % abs(x)
+        if float(two) == abs(x):
+            digits, exp10 = _digits_exp(two)
+    return _java_layout(x < 0, digits, exp10)
+
+
+def _nearest_float32(s):
+    """Decimal string -> the float32 it rounds to (exact: no detour through a double's rounding)."""
+    q = fractions.Fraction(decimal.Decimal(s))
+    top = fractions.Fraction(float(np.finfo(np.float32).max)) + fractions.Fraction(2) ** 103  # half an ulp past MAX
+    if q >= top:
+        return np.float32(np.inf)
+    c = np.float32(float(q)) if q < top - 1 else np.finfo(np.float32).max
+    best = None
+    with np.errstate(over="ignore"):
+        cands = (np.nextafter(c, np.float32(-np.inf)), c, np.nextafter(c, np.float32(np.inf)))
+    for cand in cands:
+        if not np.isfinite(cand):
+            continue
+        d = abs(fractions.Fraction(float(cand)) - q)
+        even = (int(np.array(cand, dtype=np.float32).view(np.uint32)) & 1) == 0
+        key = (d, not even)
+        if best is None or key < best[0]:
+            best = (key, cand)
+    return best[1]
+
+
+def java_float_to_string(v):
+    """`Float.toString`: the same rule over the float32 neighbours. Per length p: the correctly rounded p-digit
+    decimal, or its last-place neighbour when only that one lies in the (asymmetric) rounding interval."""
+    f = np.float32(v)
+    sp = _special(float(f))
+    if sp is not None:
+        return sp
+    a = abs(float(f))
+    for p in range(1, 10):
+        m, e = ("%.*e" % (p - 1, a)).split("e")
+        d, q = int(m.replace(".", "")), int(e) - (p - 1)
+        pick = next((c for c in (d, d - 1, d + 1) if c > 0 and _nearest_float32("%de%d" % (c, q)) == np.float32(a)),
+                    None)
+        if pick is not None:
+            break
+    if p == 1:  # the closest of the 1- and 2-digit decimals (Float.MIN_VALUE -> 1.4E-45)
+        m2, e2 = ("%.1e" % a).split("e")
+        d2, q2 = int(m2.replace(".", "")), int(e2) - 1
+        if _nearest_float32("%de%d" % (d2, q2)) == np.float32(a):
+            pick, q = d2, q2
+    digits, exp10 = _digits_exp("%de%d" % (pick, q))
+    return _java_layout(f < 0, digits, exp10)
 
 
 def combine_group_by(query, per_segment, num_groups_limit=100000):

@@ -10,6 +10,7 @@
 // random postfix filter trees and literals; the planner must answer with pinot::Error too.
 //
 // usage: fuzz_host [iterations] [seed]   (prints one summary line; exit 1 on a contract violation)
+//        fuzz_host fmt d:<hex bits> f:<hex bits> ...   (Double/Float.toString of each, one per line)
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -278,6 +279,22 @@ std::string literal(bool range) {
 }  // namespace
 
 int main(int argc, char **argv) {
+  if (argc > 1 && strcmp(argv[1], "fmt") == 0) {  // fmt d:<16 hex> | f:<8 hex> ...: Double/Float.toString lines
+    for (int i = 2; i < argc; i++) {
+      const unsigned long long u = strtoull(argv[i] + 2, nullptr, 16);
+      if (argv[i][0] == 'd') {
+        double v;
+        memcpy(&v, &u, 8);
+        printf("%s\n", java_double_to_string(v).c_str());
+      } else {
+        const uint32_t w = (uint32_t)u;
+        float v;
+        memcpy(&v, &w, 4);
+        printf("%s\n", java_float_to_string(v).c_str());
+      }
+    }
+    return 0;
+  }
   const long iters = argc > 1 ? atol(argv[1]) : 2000;
   rng.seed(argc > 2 ? strtoull(argv[2], nullptr, 10) : 12345);
   long accepted = 0, rejected = 0, plans = 0, plan_errors = 0, violations = 0, mutated_ok = 0;

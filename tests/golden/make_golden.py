@@ -12,6 +12,8 @@ Writes (all data, no reference source text):
                       airlineStats_data.avro (9746 rows; the config-1 query shape on real data)
   padding_null.json   byte contents of the Java-written v1 segment paddingNull.tar.gz (dictionaries and
                       fixed-bit forward indexes, with metadata cardinality/bits) — a byte-level format fixture
+  segments/           the three Java-written v1 segment directories paddingNull / paddingOld / paddingPercent
+                      unpacked as they are (data files of LoaderTest.java:55-57,144-206)
 The known answers themselves are transcribed (with file:line) in reference_kats.json.
 """
 import io
@@ -69,6 +71,14 @@ def main():
         }
     with open(os.path.join(HERE, "padding_null.json"), "w") as f:
         json.dump(fx, f, indent=1, sort_keys=True)
+    for name in ("paddingNull", "paddingOld", "paddingPercent"):
+        with tarfile.open(os.path.join(REF, name + ".tar.gz")) as tf:
+            for m in tf.getmembers():
+                if m.isfile():
+                    out = os.path.join(HERE, "segments", name, os.path.basename(m.name))
+                    os.makedirs(os.path.dirname(out), exist_ok=True)
+                    with open(out, "wb") as f:
+                        f.write(tf.extractfile(m).read())
 
     # real data for the config-1 query shape: pinot-tools' airlineStats sample, the three
     # columns the query reads; ArrDelay is a nullable INT *dimension*, so nulls take Pinot's default

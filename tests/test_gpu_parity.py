@@ -280,6 +280,38 @@ def test_random_group_by(engine, seed):
         g.release()
 
 
+DOUBLE_KEYS = [1.0, 0.1, 100.0, 1e7, 9999999.0, 0.001, 1e-4, 123456789.0, -12.5, 0.1 + 0.2, 2.0 ** 63, 1e21, 5e-324,
+               1.7976931348623157e308, -3.25e-9, 65536.0, 1234567.125]
+FLOAT_KEYS = [0.1, 1e10, 3.4028235e38, 1.4e-45, 1.0 / 3.0, 16777216.0, 1e-5, -2.5, 0.001, 1e7, 7.0e-4]
+
+
+@pytest.mark.parametrize("gcols", [["dbl"], ["flt"], ["flt", "i0"], ["i0", "dbl"]])
+def test_group_by_floating_point_keys(engine, gcols):
+    """FLOAT / DOUBLE group keys are Float.toString / Double.toString of the dictionary values
+    (DoubleDictionary.getStringValue, PC/segment/index/readers/DoubleDictionary.java:73-75): plain decimals in
+    [1e-3, 1e7), computerized scientific notation outside, shortest distinguishing digits."""
+    rng = np.random.default_rng(77)
+    n = 5000
+    cols = {"dbl": ("DOUBLE", [DOUBLE_KEYS[i] for i in rng.integers(0, len(DOUBLE_KEYS), n)]),
+            "flt": ("FLOAT", np.float32([FLOAT_KEYS[i] for i in rng.integers(0, len(FLOAT_KEYS), n)]).astype(np.float64).tolist()),
+            "i0": ("INT", rng.integers(0, 3, n).tolist()),
+            "v": ("INT", rng.integers(0, 1000, n).tolist())}
+    seg = build_segment("fp", cols)
+    g = engine.register(seg)
+    q = {"aggregations": [{"function": "COUNT", "column": "*"}, {"function": "SUM", "column": "v"}],
+         "filter": None, "group_by": {"columns": gcols, "top_n": 100}}
+    got, _ = ServerQueryExecutor(engine).process_query(q, [g], trim=False)
+    exp, _ = O.execute_server([seg], q)
+    assert set(got) == set(exp)
+    for key in exp:
+        assert got[key][0] == exp[key][0] and got[key][1] == exp[key][1]
+    if gcols == ["dbl"]:
+        assert {"1.0E7", "1.0E-4", "1.23456789E8", "4.9E-324", "0.30000000000000004", "9999999.0"} <= set(got)
+    if gcols == ["flt"]:
+        assert {"0.1", "1.0E10", "3.4028235E38", "1.4E-45", "0.33333334", "1.6777216E7"} <= set(got)
+    g.release()
+
+
 GROUP_SINKS = ("group.mode=lds", "group.mode=global", "group.mode=partition",
                # two-level partitioned plan: many 4-key partitions, EMIT into coarse runs of 4 / 256 partitions
                "group.mode=partition;group.pshift=2;group.split=2",

@@ -209,3 +209,54 @@ def test_sanitizer_fuzz_of_descriptors_and_planner():
         assert "violations=0" in r.stdout, r.stdout
         stats = dict(kv.split("=") for kv in r.stdout.split()[1:])
         assert int(stats["rejected"]) > 0 and int(stats["accepted"]) > 0 and int(stats["plans"]) > 0
+
+
+# Double.toString / Float.toString (DoubleDictionary / FloatDictionary.getStringValue, the group-key strings):
+# outputs of the JDK for these values, as its javadoc specifies them
+JAVA_DOUBLE = [(1.0, "1.0"), (0.1, "0.1"), (100.0, "100.0"), (1e7, "1.0E7"), (9999999.0, "9999999.0"),
+               (0.001, "0.001"), (1e-4, "1.0E-4"), (123456789.0, "1.23456789E8"), (-0.0, "-0.0"), (0.0, "0.0"),
+               (float("nan"), "NaN"), (float("inf"), "Infinity"), (float("-inf"), "-Infinity"),
+               (1.7976931348623157e308, "1.7976931348623157E308"), (5e-324, "4.9E-324"),
+               (0.1 + 0.2, "0.30000000000000004"), (-12.5, "-12.5"), (2.0 ** 63, "9.223372036854776E18"),
+               (1e21, "1.0E21"), (1e-3 * 0.999, "9.99E-4")]
+JAVA_FLOAT = [(0.1, "0.1"), (1e10, "1.0E10"), (3.4028235e38, "3.4028235E38"), (1.4e-45, "1.4E-45"),
+              (1.0 / 3.0, "0.33333334"), (16777216.0, "1.6777216E7"), (1e-5, "1.0E-5"), (-2.5, "-2.5"),
+              (100.0, "100.0")]
+
+
+def _oracle():
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import pinot_oracle
+    return pinot_oracle
+
+
+def test_oracle_java_double_and_float_to_string():
+    o = _oracle()
+    for v, want in JAVA_DOUBLE:
+        assert o.java_double_to_string(v) == want, (v, want)
+    for v, want in JAVA_FLOAT:
+        assert o.java_float_to_string(np.float32(v)) == want, (v, want)
+
+
+@pytest.mark.skipif(not _clangxx() or shutil.which("make") is None, reason="no ROCm clang++ for the host build")
+def test_engine_key_strings_match_oracle():
+    """The engine's formatter (segment_parse.cpp, used for FLOAT/DOUBLE group keys) against the oracle's, over the
+    KATs and random bit patterns (normals, subnormals, both signs)."""
+    o = _oracle()
+    subprocess.run(["make", "-s", "-C", PKG, "fuzz"], check=True, timeout=600)
+    exe = os.path.join(PKG, "build", "fuzz_host")
+    rng = np.random.default_rng(11)
+    dbl = [v for v, _ in JAVA_DOUBLE] + list(rng.integers(0, 2 ** 63, 300, dtype=np.int64).view(np.float64)) + \
+        list(rng.integers(0, 2 ** 52, 50, dtype=np.int64).view(np.float64)) + \
+        list((rng.integers(1, 10 ** 6, 100) * 10.0 ** rng.integers(-12, 12, 100)).astype(np.float64))
+    flt = [np.float32(v) for v, _ in JAVA_FLOAT] + \
+        list(rng.integers(0, 2 ** 31, 300, dtype=np.int64).astype(np.uint32).view(np.float32)) + \
+        list((rng.integers(1, 10 ** 4, 100) * 10.0 ** rng.integers(-8, 8, 100)).astype(np.float32))
+    args = ["d:%016x" % np.array(v, dtype=np.float64).view(np.uint64) for v in dbl] + \
+        ["f:%08x" % np.array(v, dtype=np.float32).view(np.uint32) for v in flt]
+    r = subprocess.run([exe, "fmt"] + args, capture_output=True, text=True, timeout=120, check=True)
+    got = r.stdout.split("\n")[:len(args)]
+    want = [o.java_double_to_string(float(v)) for v in dbl] + [o.java_float_to_string(v) for v in flt]
+    bad = [(a, g, w) for a, g, w in zip(args, got, want) if g != w]
+    assert not bad, bad[:10]

@@ -1,0 +1,145 @@
+"""Segment directories (§8(f)1): the reference's own Java-written v1 segments (pinot-core/src/test/resources/data/
+padding{Null,Old,Percent}.tar.gz, unpacked under tests/golden/segments) and v1 / v3 directories written from
+built segments, read by the oracle's reader (oracle/segment_dir.py) and checked by the engine's C++ reader on the
+host (pinot_gpu_segment_dir_info: no GPU). Known answers: LoaderTest.testPadding
+(pinot-core/src/test/java/org/apache/pinot/core/segment/index/loader/LoaderTest.java:144-206).
+"""
+import json
+import os
+import shutil
+import struct
+
+import numpy as np
+import pytest
+
+import pinot_oracle as O
+from pinot_amd import PinotGpuError, build_segment, segment_dir_info
+from segment_dir import read_segment_dir
+from segdir_writer import write_segment_dir
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SEGS = os.path.join(HERE, "golden", "segments")
+BAD_ARG = 1
+
+
+def _names(col):
+    return [str(v) for v in col.dict_values()]
+
+
+@pytest.mark.parametrize("name", ["paddingOld", "paddingPercent"])
+def test_loader_kats_percent_padding(name):
+    seg = read_segment_dir(os.path.join(SEGS, name))
+    col = seg.column("name")
+    assert col.padding == ord("%")  # LoaderTest.java:153,174: LEGACY_STRING_PAD_CHAR
+    assert _names(col) == ["lynda 2.0", "lynda"]  # :160-163, 180-183
+    assert O.index_of(col, "lynda%") == 1 and O.index_of(col, "lynda%%") == 1  # :164-165, 184-185
+
+
+def test_loader_kats_null_padding():
+    seg = read_segment_dir(os.path.join(SEGS, "paddingNull"))
+    col = seg.column("name")
+    assert col.padding == 0  # LoaderTest.java:194: DEFAULT_STRING_PAD_CHAR
+    assert _names(col) == ["lynda", "lynda 2.0"]  # :200-203
+    assert O.insertion_index_of(col, "lynda\0") == -2 and O.insertion_index_of(col, "lynda\0\0") == -2  # :204-205
+
+
+def test_oracle_reader_matches_padding_null_fixture():
+    fx = json.load(open(os.path.join(HERE, "golden", "padding_null.json")))
+    seg = read_segment_dir(os.path.join(SEGS, "paddingNull"))
+    for c, f in fx.items():
+        col = seg.column(c)
+        assert (col.data_type, col.cardinality, col.bits, col.string_width) == \
+            (f["data_type"], f["cardinality"], f["bits"], f["string_width"])
+        assert col.dictionary.hex() == f["dict_hex"] and col.fwd.hex() == f["fwd_hex"]
+
+
+@pytest.mark.parametrize("name", ["paddingNull", "paddingOld", "paddingPercent"])
+def test_engine_reader_accepts_java_segments(name):
+    assert segment_dir_info(os.path.join(SEGS, name)) == (5, 4, 0)
+
+
+def _random_segment(seed, n=3000):
+    rng = np.random.default_rng(seed)
+    cols = {
+        "i": ("INT", rng.integers(-500, 500, n).astype(np.int32)),
+        "l": ("LONG", rng.integers(0, 1 << 40, n).astype(np.int64)),
+        "d": ("DOUBLE", rng.integers(0, 70, n) * 0.5),
+        "s": ("STRING", np.array(["v%d" % v for v in rng.integers(0, 40, n)], dtype=object)),
+        "srt": ("INT", np.sort(rng.integers(0, 100, n)).astype(np.int32)),
+    }
+    return build_segment("seg%d" % seed, cols, inverted_columns=("i", "s"))
+
+
+@pytest.mark.parametrize("version", ["v1", "v3"])
+def test_written_directories_round_trip(tmp_path, version):
+    seg = _random_segment(5)
+    d = write_segment_dir(seg, str(tmp_path / ("seg_" + version)), version=version)
+    back = read_segment_dir(d)
+    assert back.num_docs == seg.num_docs and list(back.columns) == list(seg.columns)
+    for c in seg.columns.values():
+        b = back.column(c.name)
+        assert (b.data_type, b.cardinality, b.bits, b.is_sorted, b.string_width) == \
+            (c.data_type, c.cardinality, c.bits, c.is_sorted, c.string_width)
+        assert bytes(b.dictionary) == bytes(c.dictionary)
+        assert (b.fwd, b.sorted_index, b.inverted) == (c.fwd, c.sorted_index, c.inverted)
+        assert (O.dict_ids(b) == O.dict_ids(c)).all()
+    assert segment_dir_info(d) == (seg.num_docs, len(seg.columns), 0)
+
+
+def _bad(d, match):
+    with pytest.raises(PinotGpuError) as ei:
+        segment_dir_info(d)
+    assert ei.value.status == BAD_ARG, ei.value
+    assert match in str(ei.value), str(ei.value)
+
+
+def test_missing_dictionary_file(tmp_path):
+    d = write_segment_dir(_random_segment(6), str(tmp_path / "s"))
+    os.remove(os.path.join(d, "l.dict"))
+    _bad(d, "no dictionary")
+
+
+def test_truncated_forward_index_file(tmp_path):
+    d = write_segment_dir(_random_segment(6), str(tmp_path / "s"))
+    p = os.path.join(d, "i.sv.unsorted.fwd")
+    data = open(p, "rb").read()
+    open(p, "wb").write(data[:-3])
+    _bad(d, "forward index shorter")
+
+
+def test_v3_bad_magic(tmp_path):
+    d = write_segment_dir(_random_segment(6), str(tmp_path / "s"), version="v3")
+    p = os.path.join(d, "v3", "columns.psf")
+    data = bytearray(open(p, "rb").read())
+    data[0] ^= 0xFF
+    open(p, "wb").write(bytes(data))
+    _bad(d, "magic")
+
+
+def test_v3_index_map_outside_file(tmp_path):
+    d = write_segment_dir(_random_segment(6), str(tmp_path / "s"), version="v3")
+    with open(os.path.join(d, "v3", "index_map"), "a") as f:
+        f.write("i.bloom_filter.startOffset = 999999999\ni.bloom_filter.size = 16\n")
+    _bad(d, "outside columns.psf")
+
+
+def test_missing_total_docs(tmp_path):
+    d = write_segment_dir(_random_segment(6), str(tmp_path / "s"))
+    p = os.path.join(d, "metadata.properties")
+    lines = [l for l in open(p).read().splitlines() if not l.startswith("segment.total.docs")]
+    open(p, "w").write("\n".join(lines) + "\n")
+    _bad(d, "segment.total.docs")
+
+
+def test_not_a_directory(tmp_path):
+    _bad(str(tmp_path / "nope"), "not a segment directory")
+
+
+def test_unserved_columns_are_left_out(tmp_path):
+    d = write_segment_dir(_random_segment(7), str(tmp_path / "s"))
+    p = os.path.join(d, "metadata.properties")
+    text = open(p).read().replace("column.l.isSingleValues = true", "column.l.isSingleValues = false")
+    open(p, "w").write(text)
+    n, cols, skipped = segment_dir_info(d)
+    assert (cols, skipped) == (4, 1)
+    assert "l" not in read_segment_dir(d).columns

@@ -120,6 +120,7 @@ void parse_config(Engine &e, const char *cfg) {
     else if (k == "group.prefetch") e.group_prefetch = v == "1" || v == "true";
     else if (k == "group.bucket") e.group_bucket = v == "1" || v == "true";
     else if (k == "group.lw") e.group_lw = v == "1" || v == "true";
+    else if (k == "plan.shortcut") e.use_shortcut_plans = v == "1" || v == "true";
     else if (k == "group.split") {
       e.group_split = std::stoi(v);
       require(e.group_split >= -1 && e.group_split <= 8, PINOT_ERR_BAD_ARG, "group.split: -1 (auto) .. 8");

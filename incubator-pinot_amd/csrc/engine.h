@@ -154,6 +154,7 @@ struct Engine {
   bool group_prefetch = true; // group.prefetch: partitioned plan loads every column of a word batch at once
   int group_pshift = -1;      // group.pshift: cap on log2 keys per partition (tests: many small partitions)
   int group_split = -1;       // group.split: log2 sub-partitions per emitted run (-1 auto, 0 single-level)
+  bool use_shortcut_plans = true;  // plan.shortcut: metadata / dictionary plans for unfiltered COUNT / MIN / MAX
   bool group_lw = true;       // group.lw: partitioned plan reads each lane's whole 64-doc word (no per-doc gathers)
   bool group_bucket = true;   // group.bucket: partitioned plan EMITs through LDS buckets into the final layout
   int num_cus = 256;          // multiProcessorCount of the device

@@ -900,10 +900,68 @@ void aggregate_fused(Engine &e, const std::vector<SegmentData *> &segs, const pi
 
 }  // namespace
 
+namespace {
+
+// InstancePlanMakerImplV2.makeInnerSegmentPlan (PC/plan/maker/InstancePlanMakerImplV2.java:96-110,148-211): with no
+// filter (and no group-by), all-COUNT queries take the metadata plan (MetadataBasedAggregationOperator: the
+// segment's total docs) and all-MIN/MAX queries over dictionary columns the dictionary plan
+// (DictionaryBasedAggregationOperator: dictionary value 0 / length - 1; immutable dictionaries are sorted). Both
+// report numDocsScanned = totalRawDocs and no entries scanned (MetadataBasedAggregationOperator.java:74-77,
+// DictionaryBasedAggregationOperator.java:99-102). Nothing runs on the device.
+bool shortcut_aggregate(const std::vector<SegmentData *> &segs, const pinot_query &q, pinot_agg_result *out,
+                        pinot_exec_stats *stats) {
+  if (q.num_filter_nodes != 0 || q.num_group_by != 0) return false;
+  bool all_count = true, all_minmax = true;
+  std::vector<std::vector<const ColumnData *>> cols(q.num_aggregations);
+  for (int a = 0; a < q.num_aggregations; a++) {
+    const int f = q.aggregations[a].function;
+    all_count = all_count && f == PINOT_AGG_COUNT;
+    const bool mm = f == PINOT_AGG_MIN || f == PINOT_AGG_MAX;
+    all_minmax = all_minmax && mm;
+    if (!mm) continue;
+    const std::string c = agg_column(q.aggregations[a]);
+    for (SegmentData *sg : segs) {
+      auto it = sg->by_name.find(c);
+      const ColumnData *cd = it == sg->by_name.end() ? nullptr : sg->cols[it->second].get();
+      if (!cd || !cd->numeric()) all_minmax = false;  // unknown / STRING columns: the regular plan reports it
+      cols[a].push_back(cd);
+    }
+  }
+  if (!all_count && !all_minmax) return false;
+  int64_t total = 0;
+  for (SegmentData *sg : segs) total += sg->num_docs;
+  for (int a = 0; a < q.num_aggregations; a++) {
+    pinot_agg_result &r = out[a];
+    memset(&r, 0, sizeof(r));
+    r.count = total;
+    const int f = q.aggregations[a].function;
+    if (f == PINOT_AGG_MIN || f == PINOT_AGG_MAX) {
+      const bool is_min = f == PINOT_AGG_MIN;
+      double v = is_min ? INFINITY : -INFINITY;
+      for (const ColumnData *cd : cols[a]) {
+        if (cd->card < 1 || cd->num_docs == 0) continue;
+        const double x = cd->double_value(is_min ? 0 : cd->card - 1);
+        v = is_min ? std::min(v, x) : std::max(v, x);
+      }
+      r.value = v;
+    }
+  }
+  if (stats) {
+    memset(stats, 0, sizeof(*stats));
+    stats->num_docs_scanned = total;
+    stats->num_total_raw_docs = total;
+    stats->num_segments_processed = (int64_t)segs.size();
+  }
+  return true;
+}
+
+}  // namespace
+
 void exec_aggregate(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q, pinot_agg_result *out,
                     pinot_exec_stats *stats) {
   const int na = q.num_aggregations;
   require(na >= 1 && na <= kMaxAggs, PINOT_ERR_UNSUPPORTED, "1..8 aggregation functions per query");
+  if (e.use_shortcut_plans && shortcut_aggregate(segs, q, out, stats)) return;
   int n_hll = 0;
   for (int a = 0; a < na; a++) {
     const int f = q.aggregations[a].function;

@@ -90,11 +90,16 @@ def test_kat_inter_segment(engine, sv_gpu, kats):
                                    ("unfiltered_group_by", "", k["group_by"]),
                                    ("filtered_group_by", kats["filter"], k["group_by"])):
             q = compile_pql(case["query"] + where + gb)
-            server, _ = ex.process_query(q, [sv_gpu, sv_gpu])
+            server, st = ex.process_query(q, [sv_gpu, sv_gpu])
             got = BrokerReduce.reduce(q, [server, server])
             if q.get("group_by"):
                 got = [g[0][1] for g in got]
             assert got == case[variant], (case["query"], variant)
+            # 2 servers x 2 segments: the broker sums the servers' statistics. numEntriesScannedInFilter is the
+            # iterator-protocol count (SVScanDocIdIterator.java:77-131) and is not modelled.
+            stats = [2 * st.num_docs_scanned, 2 * st.num_entries_scanned_post_filter, 2 * st.num_total_raw_docs]
+            exp = case["stats"][variant]
+            assert stats == [exp[0], exp[2], exp[3]], (case["query"], variant, stats)
 
 
 def test_kat_query_executor(engine, simple_segments, kats):

@@ -74,6 +74,9 @@ std::unique_ptr<pinot_engine> create_engine(int32_t device, const char *config) 
   hipDeviceProp_t prop;
   PINOT_HIP(hipGetDeviceProperties(&prop, device));
   e->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+  int khz = 0;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) == hipSuccess && khz > 0)
+    e->wall_clock_khz = khz;
   PINOT_HIP(hipEventCreate(&e->ev_start));
   PINOT_HIP(hipEventCreate(&e->ev_stop));
   return e;
@@ -98,6 +101,7 @@ void check_query(const pinot_query *q) {
 
 void parse_config(Engine &e, const char *cfg) {
   if (!cfg) return;
+  e.config_epoch++;
   std::stringstream ss(cfg);
   std::string kv;
   while (std::getline(ss, kv, ';')) {
@@ -114,6 +118,7 @@ void parse_config(Engine &e, const char *cfg) {
               "group.mode: auto | lds | global | partition");
       e.group_mode = v == "auto" ? "" : v;
     } else if (k == "sync.poll") e.sync_poll = v == "1" || v == "true";
+    else if (k == "sync.flag") e.sync_flag = v == "1" || v == "true";
     else if (k == "debug.emit") e.debug_emit = std::stoi(v);
     else if (k == "group.pshift") e.group_pshift = std::stoi(v);
     else if (k == "group.nt_store") e.group_nt_store = std::stoi(v) != 0;
@@ -121,6 +126,7 @@ void parse_config(Engine &e, const char *cfg) {
     else if (k == "group.bucket") e.group_bucket = v == "1" || v == "true";
     else if (k == "group.lw") e.group_lw = v == "1" || v == "true";
     else if (k == "plan.shortcut") e.use_shortcut_plans = v == "1" || v == "true";
+    else if (k == "plan.cache") e.use_plan_cache = v == "1" || v == "true";
     else if (k == "group.split") {
       e.group_split = std::stoi(v);
       require(e.group_split >= -1 && e.group_split <= 8, PINOT_ERR_BAD_ARG, "group.split: -1 (auto) .. 8");

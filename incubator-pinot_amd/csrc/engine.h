@@ -83,9 +83,11 @@ struct SegmentDirData {
   pinot_segment_desc desc() const;
 };
 void read_segment_dir(const std::string &index_dir, SegmentDirData &out);
+uint64_t next_segment_uid();
 
 struct SegmentData {
   std::string name;
+  uint64_t uid = 0;                 // process-unique (never reused, unlike addresses): plan cache keys
   int32_t num_docs = 0;
   std::vector<std::unique_ptr<ColumnData>> cols;
   std::unordered_map<std::string, int> by_name;
@@ -147,6 +149,12 @@ struct Engine {
   bool use_pipe = false;      // exec.pipe: double-buffered whole-chunk staging (k_scan_query_pipe) when a chunk fits
   bool timing = false;
   std::string group_mode;     // group.mode: "" (auto) | lds | global | partition (tests force a sink)
+  bool use_plan_cache = true;  // plan.cache: a repeated fused aggregation reuses its host plan
+  std::shared_ptr<void> fused_plan;  // executor.cpp FusedPlan of the last fused aggregation
+  uint64_t config_epoch = 0;  // bumped by every configuration change (plan cache key)
+  bool sync_flag = true;      // sync.flag: fused aggregation waits on its kernel's mapped completion flag
+  uint32_t fused_seq = 0;     // last completion sequence number handed to k_scan_query
+  int64_t wall_clock_khz = 100000;  // hipDeviceAttributeWallClockRate (device-side kernel timing)
   bool sync_poll = false;     // sync.poll: busy-poll the stream instead of hipStreamSynchronize
   bool host_phases = false;
   int debug_emit = 0;         // debug.emit: GB_EMIT store experiments (timing only, wrong results)

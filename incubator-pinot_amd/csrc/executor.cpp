@@ -16,6 +16,7 @@
 // host->device copy, the kernels of all segments run back to back on the engine's stream, and the
 // reduced per-segment results come back in ONE device->host copy.
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstring>
@@ -331,7 +332,7 @@ QueryScratch prepare_scratch(Engine &e, const std::vector<SegPlan> &plans, const
 // (PINOT_ERR_TIMEOUT; the queued device work still drains in stream order before the engine's next call).
 void wait_stream(Engine &e) {
   if (!e.sync_poll && !e.has_deadline) {
-    wait_stream(e);
+    PINOT_HIP(hipStreamSynchronize(e.stream));
     return;
   }
   hipError_t st;
@@ -342,6 +343,25 @@ void wait_stream(Engine &e) {
     }
   }
   PINOT_HIP(st);
+}
+
+constexpr size_t kCtlClockOff = 64;  // fused_ctl: u32 arrival counter at 0, u64 clock_start here, HLL from 256
+
+// Spins on a completion sequence number the kernel's last block stores (system scope, release) into mapped
+// host memory after its results: no wait for the runtime's end-of-kernel signal. Every 1024 spins the stream
+// is queried, so a device error, or a kernel that ended without the flag, still surfaces; deadlines hold.
+void wait_flag(Engine &e, volatile uint32_t *flag, uint32_t seq) {
+  for (uint64_t spins = 1;; spins++) {
+    if (*flag == seq) break;
+    if ((spins & 1023) == 0) {
+      const hipError_t st = hipStreamQuery(e.stream);
+      if (st != hipSuccess && st != hipErrorNotReady) PINOT_HIP(st);
+      if (st == hipSuccess && *flag != seq) throw Error(PINOT_ERR_DEVICE, "query kernel ended without its completion flag");
+      if (e.has_deadline) check_deadline(e, "device execution");
+    }
+    __builtin_ia32_pause();
+  }
+  std::atomic_thread_fence(std::memory_order_acquire);
 }
 
 // One async H2D copy of the arena through pinned staging. A repeated query (same program bytes at the
@@ -726,16 +746,63 @@ int index_of_name(const std::vector<std::string> &v, const std::string &x) {
 
 // Fused path: pre bitsets (index leaves / OR subtrees) per segment, then ONE k_scan_query over all
 // segments and ONE fixed-order reduction, ONE device->host copy.
-void aggregate_fused(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q,
-                     const std::vector<std::string> &fold_cols, const std::vector<std::string> &hll_cols,
-                     std::vector<std::vector<AggRoute>> &routes, pinot_agg_result *out, pinot_exec_stats *stats) {
-  const auto tq0 = std::chrono::steady_clock::now();
+// The host plan of a fused aggregation (filter compile per segment, the device program in the arena, grid and
+// LDS shape). A repeated query over the same segments (a prepared statement re-executed) reuses it: only the
+// per-segment `pre` bitsets, the launch and the merge run again.
+struct FusedPlan {
+  std::string key;                  // query shape + segment uids + engine config epoch
+  uint64_t small_gen = 0, bitsets_gen = 0;
+  std::vector<SegPlan> plans;
+  std::vector<std::vector<AggRoute>> routes;
+  std::vector<std::string> fold_cols, hll_cols;
+  Arena ar;
+  QueryScratch qs;
+  FusedArgs fa{};                   // launch-invariant fields
+  bool gathers = false, pipelined = false;
+  int nres = 0;
+  size_t off_hll = 0, off_tail = 0, red_bytes = 0, ctl_acc = 0, res_bytes = 0;
+};
+
+// Identity of a fused query: the query text as marshalled (filter nodes, aggregations), the segments' uids and
+// the engine's configuration epoch.
+std::string fused_plan_key(const Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q) {
+  std::string k;
+  auto put_i = [&k](int64_t v) { k.append(reinterpret_cast<const char *>(&v), sizeof(v)); };
+  auto put_s = [&k, &put_i](const char *s) {
+    const size_t n = s ? strlen(s) : 0;
+    put_i(s ? (int64_t)n : -1);
+    if (n) k.append(s, n);
+  };
+  put_i(e.config_epoch);
+  put_i(q.num_filter_nodes);
+  for (int i = 0; i < q.num_filter_nodes; i++) {
+    const pinot_filter_node &nd = q.filter[i];
+    put_i(nd.op);
+    put_i(nd.num_children);
+    put_s(nd.column);
+    put_i(nd.num_values);
+    for (int v = 0; v < nd.num_values; v++) put_s(nd.values ? nd.values[v] : nullptr);
+  }
+  put_i(q.num_aggregations);
+  for (int i = 0; i < q.num_aggregations; i++) {
+    put_i(q.aggregations[i].function);
+    put_s(q.aggregations[i].column);
+  }
+  put_i((int64_t)segs.size());
+  for (SegmentData *sg : segs) put_i((int64_t)sg->uid);
+  return k;
+}
+
+void plan_fused(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q, FusedPlan &fp) {
   const int na = q.num_aggregations;
   const size_t S = segs.size();
-  Arena ar;
+  std::vector<std::vector<AggRoute>> &routes = fp.routes;
+  const std::vector<std::string> &fold_cols = fp.fold_cols, &hll_cols = fp.hll_cols;
+  Arena &ar = fp.ar;
   std::unique_ptr<FilterTreeInput> tree;
   if (q.num_filter_nodes > 0) tree = std::make_unique<FilterTreeInput>(decode_filter(q.num_filter_nodes, q.filter));
-  std::vector<SegPlan> plans(S);
+  std::vector<SegPlan> &plans = fp.plans;
+  plans.assign(S, SegPlan{});
   for (size_t si = 0; si < S; si++) {
     plans[si].seg = segs[si];
     Compiler(e, plans[si], ar).run_fused(tree.get());
@@ -752,7 +819,8 @@ void aggregate_fused(Engine &e, const std::vector<SegmentData *> &segs, const pi
     for (auto &c : fold_cols) max_bits = std::max(max_bits, p.seg->column(c)->bits);
   }
   const size_t tab_bytes = S * sizeof(FusedSegment) + nsteps * sizeof(FusedStep) + 256;  // + alignment/padding of two adds
-  QueryScratch qs = prepare_scratch(e, plans, ar, true, tab_bytes);
+  fp.qs = prepare_scratch(e, plans, ar, true, tab_bytes);
+  QueryScratch &qs = fp.qs;
   std::vector<FusedSegment> fsegs(S);
   std::vector<FusedStep> fsteps;
   fsteps.reserve(nsteps);
@@ -797,41 +865,66 @@ void aggregate_fused(Engine &e, const std::vector<SegmentData *> &segs, const pi
     for (int i = 0; i < fsegs[si].n_leaves + fsegs[si].n_folds; i++) {
       FusedStep &st = fsteps[fsegs[si].first_step + i];
       st.stage_off = off;
-      off += 1024 * ((st.bits + 1) / 2);
+      off += staged_chunk_bytes(st.bits);
     }
     slot_bytes = std::max(slot_bytes, off);
   }
-  const bool pipelined = e.use_pipe && slot_bytes <= kMaxPipeSlotBytes;
+  fp.pipelined = e.use_pipe && slot_bytes <= kMaxPipeSlotBytes;
   const size_t off_segs = ar.add(fsegs.data(), fsegs.size() * sizeof(FusedSegment));
   const size_t off_steps = ar.add(fsteps.data(), fsteps.size() * sizeof(FusedStep));  // may be empty (COUNT(*))
   require(ar.bytes.size() <= e.small.size(), PINOT_ERR_DEVICE, "query arena overflow");
 
   // grid: one resident wave of blocks, split evenly over the segments (equal work per block)
-  const int stage_bytes = pipelined ? slot_bytes : 1024 * ((max_bits + 1) / 2);
+  const int stage_bytes = fp.pipelined ? slot_bytes : staged_chunk_bytes(max_bits);
   int64_t max_chunks = 1;  // chunks in the largest segment window
   for (const FusedSegment &fs : fsegs) max_chunks = std::max<int64_t>(max_chunks, fs.ch_end - fs.ch_begin);
   bool gathers = false;
   for (const FusedStep &st : fsteps)
     gathers = gathers || st.kind == FK_LEAF_LUT || st.kind == FK_LEAF_RANGES || st.kind == FK_LEAF_ROARING ||
               (st.kind == FK_FOLD && (st.ops & (FOLD_DICT32 | FOLD_HLL)));
-  const int64_t resident = (int64_t)scan_query_blocks_per_cu(stage_bytes, gathers, pipelined) * e.num_cus;
+  fp.gathers = gathers;
+  const int64_t resident = (int64_t)scan_query_blocks_per_cu(stage_bytes, gathers, fp.pipelined) * e.num_cus;
   int bps = (int)std::max<int64_t>(1, resident / (int64_t)S);
   bps = (int)std::min<int64_t>(bps, (max_chunks + 3) / 4);
-  const int nres = kMaxFusedSlots;
-  const size_t res_bytes = S * nres * 8;
-  const size_t off_hll = (res_bytes + 255) / 256 * 256;
-  const size_t red_bytes = off_hll + (size_t)kMaxHll * 256 * 4;
-  e.fused_result.reserve(red_bytes);
+  fp.nres = kMaxFusedSlots;
+  fp.res_bytes = S * fp.nres * 8;
+  fp.off_hll = (fp.res_bytes + 255) / 256 * 256;
+  fp.off_tail = fp.off_hll + (size_t)kMaxHll * 256 * 4;  // {u32 seq, u32, u64 elapsed ticks}
+  fp.red_bytes = fp.off_tail + 16;
   // arrival counter | HLL registers | per-segment accumulators: set to their identities once, the
   // kernel's last block restores them after every launch
-  const size_t ctl_acc = 256 + (size_t)kMaxHll * 256 * 4;
-  if (e.fused_ctl.size() < ctl_acc + res_bytes) {
+  fp.ctl_acc = 256 + (size_t)kMaxHll * 256 * 4;
+  FusedArgs &fa = fp.fa;
+  fa = FusedArgs{};
+  fa.segs = reinterpret_cast<const FusedSegment *>(qs.arena + off_segs);
+  fa.steps = reinterpret_cast<const FusedStep *>(qs.arena + off_steps);
+  fa.nsegs = (int32_t)S;
+  fa.bps = bps;
+  fa.nslots = nslots;
+  fa.stage_bytes = stage_bytes;
+  fa.n_hll = (int32_t)hll_cols.size();
+  fa.nt = e.use_nt ? 1 : 0;
+  fa.res_stride = fp.nres;
+  fa.result_hll_off = (int64_t)fp.off_hll;
+  fa.result_tail_off = (int64_t)fp.off_tail;
+  fp.small_gen = e.small.generation();
+  fp.bitsets_gen = e.bitsets.generation();
+}
+
+void run_fused(Engine &e, FusedPlan &fp, const pinot_query &q, pinot_agg_result *out, pinot_exec_stats *stats,
+               std::chrono::steady_clock::time_point tq0) {
+  const int na = q.num_aggregations;
+  const size_t S = fp.plans.size();
+  std::vector<SegPlan> &plans = fp.plans;
+  e.fused_result.reserve(fp.red_bytes);
+  if (e.fused_ctl.size() < fp.ctl_acc + fp.res_bytes) {
     const size_t nseg_cap = std::max<size_t>(S, 64);
-    e.fused_ctl.alloc(ctl_acc + nseg_cap * nres * 8);
+    e.fused_ctl.alloc(fp.ctl_acc + nseg_cap * fp.nres * 8);
     std::vector<uint8_t> init(e.fused_ctl.size(), 0);
-    auto *acc0 = reinterpret_cast<unsigned long long *>(init.data() + ctl_acc);
-    for (size_t i = 0; i < nseg_cap * nres; i++) {
-      const int sl = (int)(i % nres);
+    memset(init.data() + kCtlClockOff, 0xFF, 8);  // clock_start: ~0 between launches
+    auto *acc0 = reinterpret_cast<unsigned long long *>(init.data() + fp.ctl_acc);
+    for (size_t i = 0; i < nseg_cap * fp.nres; i++) {
+      const int sl = (int)(i % fp.nres);
       acc0[i] = (sl == 0 || (sl & 1)) ? 0ull : 0x00000000FFFFFFFFull;
     }
     PINOT_HIP(hipMemcpy(e.fused_ctl.get(), init.data(), init.size(), hipMemcpyHostToDevice));
@@ -839,32 +932,32 @@ void aggregate_fused(Engine &e, const std::vector<SegmentData *> &segs, const pi
 
   const auto tp0 = std::chrono::steady_clock::now();
   check_deadline(e, "planning");
-  PINOT_HIP(hipEventRecord(e.ev_start, e.stream));
-  upload_arena(e, ar);
+  // completion: spin on the flag the last block writes into mapped memory (sync.flag=1, not under timing=1,
+  // whose HIP events need the runtime's completion), else the stream wait
+  const bool flag = e.sync_flag && !e.timing;
+  if (!flag) PINOT_HIP(hipEventRecord(e.ev_start, e.stream));
+  upload_arena(e, fp.ar);
   Timer t(e);
   for (size_t si = 0; si < S; si++)
-    if (plans[si].has_pre && !plans[si].empty) run_filter(e, plans[si], qs, t, (int64_t)si);
-  FusedArgs fa{};
-  fa.segs = reinterpret_cast<const FusedSegment *>(qs.arena + off_segs);
-  fa.steps = reinterpret_cast<const FusedStep *>(qs.arena + off_steps);
-  fa.acc = reinterpret_cast<unsigned long long *>(e.fused_ctl.get<uint8_t>() + ctl_acc);
+    if (plans[si].has_pre && !plans[si].empty) run_filter(e, plans[si], fp.qs, t, (int64_t)si);
+  FusedArgs fa = fp.fa;
+  fa.acc = reinterpret_cast<unsigned long long *>(e.fused_ctl.get<uint8_t>() + fp.ctl_acc);
   fa.hll_out = reinterpret_cast<uint32_t *>(e.fused_ctl.get<uint8_t>() + 256);
-  fa.nsegs = (int32_t)S;
-  fa.bps = bps;
-  fa.nslots = nslots;
-  fa.stage_bytes = stage_bytes;
-  fa.n_hll = (int32_t)hll_cols.size();
-  fa.nt = e.use_nt ? 1 : 0;
-  fa.res_stride = nres;
   fa.done = e.fused_ctl.get<uint32_t>();
   fa.result = e.fused_result.device<unsigned long long>();
-  fa.result_hll_off = (int64_t)off_hll;
+  fa.clock_start = reinterpret_cast<unsigned long long *>(e.fused_ctl.get<uint8_t>() + kCtlClockOff);
+  volatile uint32_t *seq_flag = reinterpret_cast<volatile uint32_t *>(e.fused_result.host<uint8_t>() + fp.off_tail);
+  if (flag) {
+    if (++e.fused_seq == 0) e.fused_seq = 1;
+    fa.seq = e.fused_seq;
+  }
   const auto tp1 = std::chrono::steady_clock::now();
-  t.timed(0, [&] { launch_scan_query(fa, gathers, pipelined, e.stream); });
+  t.timed(0, [&] { launch_scan_query(fa, fp.gathers, fp.pipelined, e.stream); });
   PINOT_HIP(hipGetLastError());
-  PINOT_HIP(hipEventRecord(e.ev_stop, e.stream));
+  if (!flag) PINOT_HIP(hipEventRecord(e.ev_stop, e.stream));
   const auto tp2 = std::chrono::steady_clock::now();
-  wait_stream(e);
+  if (flag) wait_flag(e, seq_flag, fa.seq);
+  else wait_stream(e);
   if (e.host_phases) {
     const auto tp3 = std::chrono::steady_clock::now();
     auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
@@ -873,28 +966,30 @@ void aggregate_fused(Engine &e, const std::vector<SegmentData *> &segs, const pi
   }
   const uint8_t *host = e.fused_result.host<uint8_t>();
   float ms = 0;
-  PINOT_HIP(hipEventElapsedTime(&ms, e.ev_start, e.ev_stop));
+  if (flag) ms = (float)((double)reinterpret_cast<const volatile unsigned long long *>(host + fp.off_tail)[1] /
+                         (double)e.wall_clock_khz);
+  else PINOT_HIP(hipEventElapsedTime(&ms, e.ev_start, e.ev_stop));
   t.collect();
 
   AggResults R;
   R.res = reinterpret_cast<const unsigned long long *>(host);
-  R.hll = reinterpret_cast<const uint32_t *>(host + off_hll);
-  R.nres = nres;
+  R.hll = reinterpret_cast<const uint32_t *>(host + fp.off_hll);
+  R.nres = fp.nres;
   R.src.assign(S, std::vector<int>(na, 0));
   R.hll_set.assign(na, 0);
   std::vector<int64_t> counts(S, 0);
   for (size_t si = 0; si < S; si++) {
-    counts[si] = plans[si].empty ? 0 : (int64_t)R.res[si * nres];
+    counts[si] = plans[si].empty ? 0 : (int64_t)R.res[si * fp.nres];
     for (int a = 0; a < na; a++) {
       if (q.aggregations[a].function == PINOT_AGG_COUNT) continue;
-      const int f = index_of_name(fold_cols, agg_column(q.aggregations[a]));
-      R.src[si][a] = routes[si][a].kind == AggRoute::MINMAX ? 2 + 2 * f : 1 + 2 * f;
+      const int f = index_of_name(fp.fold_cols, agg_column(q.aggregations[a]));
+      R.src[si][a] = fp.routes[si][a].kind == AggRoute::MINMAX ? 2 + 2 * f : 1 + 2 * f;
     }
   }
   for (int a = 0; a < na; a++)
     if (q.aggregations[a].function == PINOT_AGG_DISTINCTCOUNTHLL)
-      R.hll_set[a] = index_of_name(hll_cols, agg_column(q.aggregations[a]));
-  merge_aggregates(q, plans, routes, counts, R, out);
+      R.hll_set[a] = index_of_name(fp.hll_cols, agg_column(q.aggregations[a]));
+  merge_aggregates(q, plans, fp.routes, counts, R, out);
   fill_stats(q, plans, counts, ms, stats);
 }
 
@@ -970,13 +1065,29 @@ void exec_aggregate(Engine &e, const std::vector<SegmentData *> &segs, const pin
   }
   require(n_hll <= kMaxHll, PINOT_ERR_UNSUPPORTED, "at most 4 DISTINCTCOUNTHLL per query");
   const size_t S = segs.size();
+  const auto tq0 = std::chrono::steady_clock::now();
+  if (e.use_fused && e.use_plan_cache) {  // a repeated fused query: its host plan as last time
+    FusedPlan *fp = static_cast<FusedPlan *>(e.fused_plan.get());
+    if (fp && fp->small_gen == e.small.generation() && fp->bitsets_gen == e.bitsets.generation() &&
+        fp->key == fused_plan_key(e, segs, q)) {
+      run_fused(e, *fp, q, out, stats, tq0);
+      return;
+    }
+  }
   std::vector<std::vector<AggRoute>> routes(S);
   for (size_t si = 0; si < S; si++)
     for (int a = 0; a < na; a++) routes[si].push_back(route_agg(e, *segs[si], q.aggregations[a]));
   if (e.use_fused) {
     std::vector<std::string> fold_cols, hll_cols;
     if (fusable(q, routes, fold_cols, hll_cols)) {
-      aggregate_fused(e, segs, q, fold_cols, hll_cols, routes, out, stats);
+      auto fp = std::make_shared<FusedPlan>();
+      fp->routes = std::move(routes);
+      fp->fold_cols = std::move(fold_cols);
+      fp->hll_cols = std::move(hll_cols);
+      plan_fused(e, segs, q, *fp);
+      fp->key = fused_plan_key(e, segs, q);
+      e.fused_plan = fp;
+      run_fused(e, *fp, q, out, stats, tq0);
       return;
     }
   }
@@ -1493,35 +1604,45 @@ void init_accs(Engine &e, int64_t G, unsigned long long *counts, const GroupAccs
 // Result-array pool: a 1 M-group result is ~48 MB of fresh host pages, and first-touching them cost more than
 // filling them. Released results hand their arrays back; the next large result takes them (capacity kept).
 namespace {
+// Recycled host result arrays (a 1M-group result allocates several 8 MB arrays per query). Bounded: at most
+// kPoolMaxBytes held in total; take = best fit, and an array more than twice the request stays pooled for a
+// larger result instead of being handed to a small one.
 struct ResultPool {
   std::mutex mu;
   std::vector<std::vector<int64_t>> i64;
   std::vector<std::vector<double>> f64;
+  size_t bytes = 0;
 };
 ResultPool &result_pool() {
   static ResultPool *p = new ResultPool;  // never destroyed: results may be released during interpreter exit
   return *p;
 }
+constexpr size_t kPoolMinElems = 1u << 16, kPoolMaxArrays = 16, kPoolMaxBytes = 256ull << 20;
 template <class T>
-std::vector<T> take_pooled(std::vector<std::vector<T>> &pool, size_t n) {
-  for (size_t i = 0; i < pool.size(); i++)
-    if (pool[i].capacity() >= n) {
-      std::vector<T> v = std::move(pool[i]);
-      pool.erase(pool.begin() + i);
-      return v;
-    }
-  return {};
+std::vector<T> take_pooled(ResultPool &rp, std::vector<std::vector<T>> &pool, size_t n) {
+  size_t best = SIZE_MAX;
+  for (size_t i = 0; i < pool.size(); i++) {
+    const size_t cap = pool[i].capacity();
+    if (cap >= n && cap <= 2 * std::max(n, kPoolMinElems) && (best == SIZE_MAX || cap < pool[best].capacity()))
+      best = i;
+  }
+  if (best == SIZE_MAX) return {};
+  std::vector<T> v = std::move(pool[best]);
+  pool.erase(pool.begin() + best);
+  rp.bytes -= v.capacity() * sizeof(T);
+  return v;
 }
-constexpr size_t kPoolMinElems = 1u << 16, kPoolMaxArrays = 16;
 }  // namespace
 
 GroupByResult::~GroupByResult() {
   ResultPool &p = result_pool();
   std::lock_guard<std::mutex> lk(p.mu);
-  auto put = [](auto &pool, auto &v) {
-    if (v.capacity() >= kPoolMinElems && pool.size() < kPoolMaxArrays) {
+  auto put = [&p](auto &pool, auto &v) {
+    const size_t b = v.capacity() * sizeof(v[0]);
+    if (v.capacity() >= kPoolMinElems && pool.size() < kPoolMaxArrays && p.bytes + b <= kPoolMaxBytes) {
       v.clear();
       pool.push_back(std::move(v));
+      p.bytes += b;
     }
   };
   put(p.i64, raw_keys);
@@ -1999,11 +2120,11 @@ std::unique_ptr<GroupByResult> build_dense_result(Engine &e, const DenseGroups &
   if (n >= kPoolMinElems) {  // recycled arrays of released results: already-mapped pages
     ResultPool &rp = result_pool();
     std::lock_guard<std::mutex> lk(rp.mu);
-    res->raw_keys = take_pooled(rp.i64, n);
-    res->counts[0] = take_pooled(rp.i64, n);
+    res->raw_keys = take_pooled(rp, rp.i64, n);
+    res->counts[0] = take_pooled(rp, rp.i64, n);
     for (int i = 0; i < na; i++) {
-      res->values[i] = take_pooled(rp.f64, n);
-      if (ga.acc_kind[i] == 4) res->hll_card[i] = take_pooled(rp.i64, n);
+      res->values[i] = take_pooled(rp, rp.f64, n);
+      if (ga.acc_kind[i] == 4) res->hll_card[i] = take_pooled(rp, rp.i64, n);
     }
   }
   std::vector<std::function<void()>> sizing;
@@ -2225,7 +2346,7 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
   a.nsegs = (int32_t)S;
   a.n_gcols = q.num_group_by;
   a.n_aggs = na;
-  a.stage_bytes = 1024 * ((max_leaf_bits + 1) / 2);
+  a.stage_bytes = staged_chunk_bytes(max_leaf_bits);
   a.G = ks.G;
   a.counts = counts;
   a.matched = matched;

@@ -105,20 +105,20 @@ __device__ __forceinline__ void fold_half(const FusedStep &st, uint32_t mh, cons
 }
 
 template <int B, bool G>
-__device__ __forceinline__ void fold_step(const FusedStep &st, const uint8_t *p, uint64_t mask, FoldPart &r,
-                                          HllRegs *hll) {
+__device__ __forceinline__ void fold_step(const FusedStep &st, const uint8_t *stage, uint32_t off, uint64_t mask,
+                                          FoldPart &r, HllRegs *hll) {
   uint32_t v[32];
-  decode_half<B>(p, v);
+  decode_half<B>(stage, off, v);
   fold_half<B, G>(st, (uint32_t)mask, v, r, hll);
-  decode_half<B>(p + 4 * B, v);
+  decode_half<B>(stage, off + 4 * B, v);
   fold_half<B, G>(st, (uint32_t)(mask >> 32), v, r, hll);
 }
 
 
 template <bool G>
-__device__ __forceinline__ void fold_rt(const FusedStep &st, const uint8_t *p, uint64_t mask, FoldPart &r,
-                                        HllRegs *hll) {
-#define PINOT_FOLD(B) fold_step<B, G>(st, p, mask, r, hll)
+__device__ __forceinline__ void fold_rt(const FusedStep &st, const uint8_t *stage, uint32_t off, uint64_t mask,
+                                        FoldPart &r, HllRegs *hll) {
+#define PINOT_FOLD(B) fold_step<B, G>(st, stage, off, mask, r, hll)
   PINOT_WIDTH_SWITCH(st.bits, PINOT_FOLD)
 #undef PINOT_FOLD
 }
@@ -213,6 +213,17 @@ __device__ __forceinline__ void flush_block(const FusedArgs &a, uint8_t *stage_l
     a.hll_out[i] = 0;
   }
   if (tid == 0) *a.done = 0;
+  if (a.seq) {
+    __threadfence_system();  // this thread's result stores, visible to the host
+    __syncthreads();
+    if (tid == 0) {
+      unsigned long long *tail = reinterpret_cast<unsigned long long *>(reinterpret_cast<uint8_t *>(a.result) +
+                                                                        a.result_tail_off);
+      tail[1] = wall_clock64() - *a.clock_start;
+      *a.clock_start = ~0ull;
+      __hip_atomic_store(reinterpret_cast<uint32_t *>(tail), a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
 }
 
 
@@ -229,7 +240,7 @@ __device__ __forceinline__ unsigned long long eval_chunk(const FusedStep *__rest
     if (!__any(mask != 0)) break;
     const FusedStep st = load_const(steps + n_leaves + i);  // st.fold == i (host order)
     FoldPart r;
-    fold_rt<G>(st, src(n_leaves + i, st) + lane * (8 * st.bits), mask, r, hll);
+    fold_rt<G>(st, src(n_leaves + i, st), (uint32_t)(lane * (8 * st.bits)), mask, r, hll);
 #pragma unroll
     for (int f = 0; f < kMaxFusedFolds; f++)  // uniform select of the register accumulator
       if (f == i) {
@@ -250,6 +261,7 @@ template <bool G>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G ? 2 : 4))) void k_scan_query(FusedArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t stage_lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (a.seq && tid == 0) atomicMin(a.clock_start, wall_clock64());  // the launch's first block start
   HllRegs *hll = nullptr;
   if constexpr (G) {
     __shared__ HllRegs hll_lds[kMaxHll];
@@ -300,6 +312,7 @@ template <bool G>
 __global__ __launch_bounds__(kBlock) void k_scan_query_pipe(FusedArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t stage_lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (a.seq && tid == 0) atomicMin(a.clock_start, wall_clock64());  // the launch's first block start
   HllRegs *hll = nullptr;
   if constexpr (G) {
     __shared__ HllRegs hll_lds[kMaxHll];

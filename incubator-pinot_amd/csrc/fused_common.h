@@ -24,19 +24,25 @@ __device__ __forceinline__ void decode_half_step(const uint32_t (&D)[B], uint32_
   if constexpr (J + 1 < 32) decode_half_step<B, J + 1>(D, v);
 }
 
+// Half of a lane's super-word at byte `off` of a staged chunk (pieces kPieceStride apart: a byte offset o of the
+// packed chunk lives at o + kPiecePad * (o >> 10); 8-byte reads never straddle a piece).
+__device__ __forceinline__ const uint8_t *staged_at(const uint8_t *stage, uint32_t o) {
+  return stage + o + kPiecePad * (o >> 10);
+}
+
 template <int B>
-__device__ __forceinline__ void decode_half(const uint8_t *p, uint32_t (&v)[32]) {
+__device__ __forceinline__ void decode_half(const uint8_t *stage, uint32_t off, uint32_t (&v)[32]) {
   uint32_t D[B];
   if constexpr (B % 2 == 0) {
 #pragma unroll
     for (int i = 0; i < B / 2; i++) {
-      const u32x2 x = *reinterpret_cast<const u32x2 *>(p + 8 * i);
+      const u32x2 x = *reinterpret_cast<const u32x2 *>(staged_at(stage, off + 8 * i));
       D[2 * i] = bswap32(x.x);
       D[2 * i + 1] = bswap32(x.y);
     }
   } else {
 #pragma unroll
-    for (int i = 0; i < B; i++) D[i] = bswap32(*reinterpret_cast<const uint32_t *>(p + 4 * i));
+    for (int i = 0; i < B; i++) D[i] = bswap32(*reinterpret_cast<const uint32_t *>(staged_at(stage, off + 4 * i)));
   }
   decode_half_step<B, 0>(D, v);
 }
@@ -49,10 +55,10 @@ __device__ __forceinline__ void stage_chunk_rt(const uint8_t *__restrict__ fwd, 
   const int pieces = (bits + 1) >> 1;
   if (nt) {
     for (int i = 0; i < pieces; i++)
-      __builtin_amdgcn_global_load_lds((glob_void_t *)(src + i * 1024), (lds_void_t *)(lds_wave + i * 1024), 16, 0, 2);
+      __builtin_amdgcn_global_load_lds((glob_void_t *)(src + i * 1024), (lds_void_t *)(lds_wave + i * kPieceStride), 16, 0, 2);
   } else {
     for (int i = 0; i < pieces; i++)
-      __builtin_amdgcn_global_load_lds((glob_void_t *)(src + i * 1024), (lds_void_t *)(lds_wave + i * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((glob_void_t *)(src + i * 1024), (lds_void_t *)(lds_wave + i * kPieceStride), 16, 0, 0);
   }
 }
 
@@ -100,11 +106,11 @@ __device__ __forceinline__ uint32_t leaf_half(const FusedStep &st, const uint32_
 
 // One step of a chunk at compile-time width B: decode the lane's two halves from LDS and apply.
 template <int B, bool G>
-__device__ __forceinline__ void leaf_step(const FusedStep &st, const uint8_t *p, uint64_t &mask) {
+__device__ __forceinline__ void leaf_step(const FusedStep &st, const uint8_t *stage, uint32_t off, uint64_t &mask) {
   uint32_t v[32];
-  decode_half<B>(p, v);
+  decode_half<B>(stage, off, v);
   const uint32_t m0 = leaf_half<G>(st, v);
-  decode_half<B>(p + 4 * B, v);
+  decode_half<B>(stage, off + 4 * B, v);
   const uint32_t m1 = leaf_half<G>(st, v);
   const uint64_t m = ((uint64_t)m1 << 32) | m0;
   mask &= st.negate ? ~m : m;
@@ -133,8 +139,8 @@ __device__ __forceinline__ void leaf_step(const FusedStep &st, const uint8_t *p,
   }
 
 template <bool G, int MAXB = 32>
-__device__ __forceinline__ void leaf_rt(const FusedStep &st, const uint8_t *p, uint64_t &mask) {
-#define PINOT_LEAF(B) leaf_step<B, G>(st, p, mask)
+__device__ __forceinline__ void leaf_rt(const FusedStep &st, const uint8_t *stage, uint32_t off, uint64_t &mask) {
+#define PINOT_LEAF(B) leaf_step<B, G>(st, stage, off, mask)
   if constexpr (MAXB <= 12) {
     PINOT_WIDTH_SWITCH_12(st.bits, PINOT_LEAF)
   } else {
@@ -243,7 +249,7 @@ __device__ __forceinline__ uint64_t leaf_word(const FusedStep &st, int i, int64_
   if (G && st.kind == FK_LEAF_RANGES) return ranges_word(static_cast<const int32_t *>(st.table), (int)st.lo, w);
   if (G && st.kind == FK_LEAF_ROARING) return roaring_word(st, w);
   uint64_t x = ~0ull;
-  leaf_rt<G, MAXB>(st, src(i, st) + lane * (8 * st.bits), x);
+  leaf_rt<G, MAXB>(st, src(i, st), (uint32_t)(lane * (8 * st.bits)), x);
   return x;
 }
 

@@ -150,7 +150,7 @@ struct FusedArgs {
   uint32_t *hll_out;         // [kMaxHll][256] registers, atomicMax (zero on entry; re-zeroed by the last block)
   int32_t nsegs, bps;        // block b serves segment b / bps
   int32_t nslots;            // 1 + 2 * folds
-  int32_t stage_bytes;       // stepwise: LDS bytes per wave = 1024 * ceil(max bits / 2);
+  int32_t stage_bytes;       // stepwise: LDS bytes per wave = staged_chunk_bytes(max bits);
                              // pipelined: bytes of ONE chunk slot (all steps), two slots per wave
   int32_t n_hll;
   int32_t nt;                // pipelined: non-temporal policy on the column DMA (exec.nt)
@@ -158,11 +158,24 @@ struct FusedArgs {
   uint32_t *done;            // arrival counter (0 between launches; the last block resets it)
   unsigned long long *result;  // host-mapped: [nsegs][res_stride] slots, then [kMaxHll][256] u32 HLL registers
   int64_t result_hll_off;    // byte offset of the HLL registers in `result`
+  // completion flag: the last block writes {elapsed wall-clock ticks, seq} at result_tail_off after every
+  // result, behind a system-scope release, so the host can spin on mapped memory instead of waiting for the
+  // runtime's completion signal (seq 0: no flag)
+  int64_t result_tail_off;
+  unsigned long long *clock_start;  // device: earliest block start (wall_clock64); ~0 between launches
+  uint32_t seq;
+  int32_t reserved;
 };
 // Largest chunk slot the pipelined kernel double-buffers in LDS: 512 B of `pre` words + every step's
 // 1-KiB pieces; 4 waves x 2 slots x 18.5 KiB + the block's FusedLds fit the 160 KiB of a CU.
 constexpr int kPipePreBytes = 512;
-constexpr int kMaxPipeSlotBytes = 18 * 1024 + kPipePreBytes;
+// A staged chunk's 1-KiB DMA pieces sit kPiecePad bytes apart in LDS: the per-lane super-word reads of the
+// decoders (lane stride 8*B bytes) then spread over all 64 banks for every width but 16 and 32 (2-way),
+// where back-to-back pieces left B = 8, 12, 20, 24, 28 2-8-way conflicted (fused_common.h decode_half).
+constexpr int kPiecePad = 8;
+constexpr int kPieceStride = 1024 + kPiecePad;
+constexpr int staged_chunk_bytes(int bits) { return kPieceStride * ((bits + 1) / 2); }
+constexpr int kMaxPipeSlotBytes = 18 * kPieceStride + kPipePreBytes;
 // gathers: the program has memory-LUT leaves, FOLD_DICT32 or FOLD_HLL (selects the gather instance).
 // pipelined: whole-chunk double-buffered staging (stage_bytes = slot <= kMaxPipeSlotBytes), else stepwise.
 void launch_scan_query(const FusedArgs &a, bool gathers, bool pipelined, hipStream_t stream);
@@ -233,7 +246,7 @@ struct GroupArgs {
   const GroupColDev *gcols;
   const GroupAggDev *aggs;
   int32_t nsegs, bps, n_gcols, n_aggs;
-  int32_t mode, stage_bytes;  // stage: LDS bytes per wave for the leaves (1024 * ceil(max leaf bits / 2))
+  int32_t mode, stage_bytes;  // stage: LDS bytes per wave for the leaves (staged_chunk_bytes(max leaf bits))
   long long G;
   unsigned long long *counts;  // u64 [G]
   unsigned long long *matched; // u64 [nsegs]: docs passing the filter per segment (numDocsScanned)

@@ -10,11 +10,17 @@
 // The packed forward index is uploaded byte-for-byte; sorted columns additionally get a packed
 // forward index synthesised on the device so aggregation/group-by kernels see one layout.
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 
 #include "engine.h"
 
 namespace pinot {
+
+uint64_t next_segment_uid() {
+  static std::atomic<uint64_t> n{0};
+  return ++n;
+}
 
 static void upload(DeviceBuffer &buf, const void *src, size_t bytes, size_t alloc_bytes, hipStream_t s) {
   buf.alloc(alloc_bytes);
@@ -90,6 +96,7 @@ std::unique_ptr<SegmentData> register_segment(Engine &e, const pinot_segment_des
   require(d.num_docs >= 0, PINOT_ERR_BAD_ARG, "num_docs < 0");
   require(d.num_columns >= 0 && (d.num_columns == 0 || d.columns), PINOT_ERR_BAD_ARG, "columns");
   auto seg = std::make_unique<SegmentData>();
+  seg->uid = next_segment_uid();
   seg->name = d.name ? d.name : "";
   seg->num_docs = d.num_docs;
   for (int i = 0; i < d.num_columns; i++) register_column(e, *seg, d.columns[i]);
@@ -175,6 +182,7 @@ std::unique_ptr<SegmentData> register_synthetic(Engine &e, const char *name, int
                                                 const int32_t *kinds) {
   require(num_docs > 0 && ncols > 0 && names && cards, PINOT_ERR_BAD_ARG, "synthetic segment arguments");
   auto seg = std::make_unique<SegmentData>();
+  seg->uid = next_segment_uid();
   seg->name = name ? name : "synthetic";
   seg->num_docs = num_docs;
   for (int i = 0; i < ncols; i++) {

@@ -124,7 +124,10 @@ void parse_config(Engine &e, const char *cfg) {
     else if (k == "group.nt_store") e.group_nt_store = std::stoi(v) != 0;
     else if (k == "group.prefetch") e.group_prefetch = v == "1" || v == "true";
     else if (k == "group.bucket") e.group_bucket = v == "1" || v == "true";
-    else if (k == "group.lw") e.group_lw = v == "1" || v == "true";
+    else if (k == "group.lw") {
+      e.group_lw = v == "true" ? 1 : std::stoi(v);
+      require(e.group_lw >= 0 && e.group_lw <= 2, PINOT_ERR_BAD_ARG, "group.lw: 0 (per doc) | 1 (lane owns word) | 2 (contiguous quarters)");
+    }
     else if (k == "plan.shortcut") e.use_shortcut_plans = v == "1" || v == "true";
     else if (k == "plan.cache") e.use_plan_cache = v == "1" || v == "true";
     else if (k == "group.split") {

@@ -24,6 +24,13 @@ __device__ __forceinline__ uint64_t tail_mask(int64_t w, int64_t nwords, int32_t
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef const __attribute__((address_space(1))) void glob_void_t;
 
+// Loads through an explicitly global pointer: a pointer read from a descriptor is generic, and a generic (flat)
+// load counts against lgkmcnt as well as vmcnt — every later LDS wait would then also wait for it.
+template <typename T>
+__device__ __forceinline__ T gload(const void *p) {
+  return *reinterpret_cast<const __attribute__((address_space(1))) T *>(reinterpret_cast<uintptr_t>(p));
+}
+
 // Waits for this wave's outstanding global loads, LDS-DMA included (the staged chunk is then readable
 // by the same wave; no other wave reads it).
 __device__ __forceinline__ void wait_stage() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }

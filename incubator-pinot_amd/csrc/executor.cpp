@@ -1797,6 +1797,7 @@ struct GroupPlan {
   std::vector<int> lds_off, field_shift, reduce_off;
   int reduce_bytes = 0;
   int reduce_wave_cnt_off = 0;
+  int record_bits = 0;  // partitioned: local key + aggregated fields (the bucketed EMIT keeps bit 63 as a valid mark)
 };
 
 constexpr int kGroupMaxFusedLeafBits = 12;    // 16 wave stages x 6 KiB
@@ -1875,6 +1876,7 @@ GroupPlan plan_group(const std::vector<SegmentData *> &segs, const pinot_query &
   const bool want_part = force.empty() ? ks.G >= 4 * K : force == "partition";
   if (same && bits <= 64 && P <= kMaxPartitions && want_part && force != "global") {
     gp.mode = GB_EMIT;  // COUNT + EMIT (+ split) + reduce
+    gp.record_bits = bits;
     gp.shift = shift;
     gp.split = split;
     gp.P = P;
@@ -2054,21 +2056,35 @@ std::unique_ptr<GroupByResult> build_dense_result(Engine &e, const DenseGroups &
   res->gvalues = d.ks->gvalues;
   res->gcard = d.ks->gcard;
   if (!n) return res;
-  std::vector<GroupAggDev> oaggs(na);
-  for (int i = 0; i < na; i++) {
-    oaggs[i].acc_kind = gx.acc_kind[i];
-    oaggs[i].acc = d.accs[i];
-  }
+  // output rows: one per primary 8-byte accumulator (aliases such as AVG(x) beside SUM(x) read their primary's row),
+  // then the HLL register sums in aggregation order
+  std::vector<GroupAggDev> oaggs;
+  std::vector<int> row(na, -1);
+  for (int i = 0; i < na; i++)
+    if (gx.acc_kind[i] >= 0 && gx.acc_kind[i] <= 3) {
+      row[i] = (int)oaggs.size();
+      oaggs.push_back(GroupAggDev{});
+      oaggs.back().acc_kind = gx.acc_kind[i];
+      oaggs.back().acc = d.accs[i];
+    }
+  const int n8 = (int)oaggs.size();
+  for (int i = 0; i < na; i++)
+    if (gx.acc_kind[i] == 4) {
+      oaggs.push_back(GroupAggDev{});
+      oaggs.back().acc_kind = 4;
+      oaggs.back().acc = d.accs[i];
+    }
   // device outputs and their pinned host copy live in grow-only engine buffers (no per-query allocation)
-  const size_t out_b = n * 8 * (2 + na) + (size_t)n_hll * n * 12 + 64;
+  const size_t out_b = n * 8 * (2 + n8) + (size_t)n_hll * n * 12 + 64;
   e.group_out.reserve(out_b);
   e.group_host.reserve(out_b);
   auto *o_cnt = e.group_out.get<unsigned long long>();
   auto *o_acc = o_cnt + n;
-  auto *o_hs = o_acc + n * na;
+  auto *o_hs = o_acc + n * n8;
   auto *o_hz = reinterpret_cast<uint32_t *>(o_hs + (size_t)n_hll * n);
   auto *o_keys = reinterpret_cast<long long *>(e.group_out.get<uint8_t>() + out_b - 64 - n * 8);
-  launch_group_outputs(d.counts, oaggs.data(), na, keys_dev, (long long)n, o_cnt, o_acc, o_hs, o_hz, e.stream);
+  launch_group_outputs(d.counts, oaggs.data(), (int)oaggs.size(), keys_dev, (long long)n, o_cnt, o_acc, o_hs, o_hz,
+                       e.stream);
   PINOT_HIP(hipGetLastError());
   if (n_hll) {  // registers stay on the device until asked for; buffers are recycled once their result is released
     HllPart part;
@@ -2110,7 +2126,7 @@ std::unique_ptr<GroupByResult> build_dense_result(Engine &e, const DenseGroups &
   const uint8_t *host = e.group_host.get<uint8_t>();
   const auto *hc = reinterpret_cast<const unsigned long long *>(host);
   const auto *hacc = hc + n;
-  const auto *hhs = hacc + n * na;
+  const auto *hhs = hacc + n * n8;
   const auto *hhz = reinterpret_cast<const uint32_t *>(hhs + (size_t)n_hll * n);
   const auto *hkeys = reinterpret_cast<const long long *>(host + out_b - 64 - n * 8);
   std::vector<int> hidx(na, -1);  // HLL register-sum row of each (primary) HLL aggregation
@@ -2150,7 +2166,7 @@ std::unique_ptr<GroupByResult> build_dense_result(Engine &e, const DenseGroups &
       double *vv = res->values[i].data();
       const int ak = ga.acc_kind[i];
       const int src = alias[i] >= 0 ? alias[i] : i;  // the accumulator this aggregation reads
-      const unsigned long long *raw = hacc + (size_t)src * n;
+      const unsigned long long *raw = row[src] >= 0 ? hacc + (size_t)row[src] * n : nullptr;
       switch (ak) {
         case 0:
           for (size_t g = lo; g < hi; g++) vv[g] = (double)(int64_t)raw[g];
@@ -2369,7 +2385,7 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     for (const GroupColDev &gc : gcols) lw = lw && gc.bits <= kGroupLwMaxBits;
     for (size_t i = 0; i < gaggs.size(); i++)
       if (gx.acc_kind[i % na] != 5) lw = lw && gaggs[i].bits <= kGroupLwMaxBits;
-    a.lw = lw ? 1 : 0;
+    a.lw = lw ? e.group_lw : 0;
   }
   unsigned long long *htable = nullptr, *reps = nullptr;
   if (ks.hashed) {
@@ -2440,7 +2456,7 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     require(max_records < (int64_t)UINT32_MAX, PINOT_ERR_UNSUPPORTED, "partitioned group-by over > 4G docs per GPU");
     e.group_records.reserve((size_t)max_records * 8 + 64);
     // bucketed plan: COUNT keeps the filter words, GB_EMIT2 writes whole LDS buckets into the final layout
-    const bool bucket = e.group_bucket && a.pf_nc > 0 && gp.P <= kBucketMaxPartitions &&
+    const bool bucket = e.group_bucket && a.pf_nc > 0 && gp.P <= kBucketMaxPartitions && gp.record_bits <= 63 &&
                         (e.debug_emit == 0 || e.debug_emit >= 3);
     if (gp.split && !bucket) e.group_runs.reserve((size_t)max_records * 8 + 64);
     int64_t fstride = 0;

@@ -574,6 +574,306 @@ __device__ __forceinline__ void group_chunk_lw(const GroupArgs &a, const GroupSe
   }
 }
 
+// ---------------------------------------------------------------- lane-owns-quarter path (contiguous)
+// Pass q of a chunk covers its docs [1024q, 1024q + 1024); lane l takes the 16 docs 1024q + 16l .. +15, i.e. the
+// packed quarter qi = 256 ch + 64q + l, whose 16*B bits start at bit 16*B*qi. A wave's loads of one column are
+// then the pass's 128*B contiguous bytes, every lane ceil(B/2) contiguous dwords: each cache line is consumed by
+// one burst of loads (the lane-owns-word quarters revisit a line after the sink work of the previous quarter, by
+// which time L2 has evicted it — twice the algorithmic bytes fetched). For odd B an odd quarter starts 16 bits
+// into its first dword: the loaded dwords are funnel-shifted by 16 first. The lane's 16 filter bits are bits
+// 16(l & 3) .. +15 of the chunk word 16q + l/4, fetched from the lane that holds it.
+template <int B>
+__device__ __forceinline__ void load_quarter_lq(const uint8_t *fwd, int64_t qi, uint32_t (&D)[(B + 1) / 2 + 1]) {
+  constexpr int N = (B + 1) / 2 + (B & 1);  // dwords covering 16*B bits from a 16-bit offset (odd B)
+  const uint32_t *p = reinterpret_cast<const uint32_t *>(fwd) + ((qi * B) >> 1);
+  uint32_t R[N];
+  int k = 0;
+#pragma unroll
+  for (; k + 4 <= N; k += 4) {
+    const u32x4a x = *reinterpret_cast<const u32x4a *>(p + k);
+    R[k] = bswap32(x.x);
+    R[k + 1] = bswap32(x.y);
+    R[k + 2] = bswap32(x.z);
+    R[k + 3] = bswap32(x.w);
+  }
+#pragma unroll
+  for (; k + 2 <= N; k += 2) {
+    const u32x2a_ x = *reinterpret_cast<const u32x2a_ *>(p + k);
+    R[k] = bswap32(x.x);
+    R[k + 1] = bswap32(x.y);
+  }
+  if (k < N) R[k] = bswap32(p[k]);
+  if constexpr (B & 1) {
+    const bool odd = qi & 1;
+#pragma unroll
+    for (int i = 0; i + 1 < N; i++) D[i] = odd ? __builtin_amdgcn_alignbit(R[i], R[i + 1], 16) : R[i];
+    D[N - 1] = R[N - 1];
+  } else {
+#pragma unroll
+    for (int i = 0; i < N; i++) D[i] = R[i];
+  }
+}
+
+template <int B, int J, typename F>
+__device__ __forceinline__ void decode_quarter_apply(const uint32_t (&D)[(B + 1) / 2 + 1], F &f) {
+  constexpr int q = J * B, k = q >> 5, o = q & 31;
+  constexpr uint32_t mask = (uint32_t)((1ull << B) - 1ull);
+  if constexpr (o + B <= 32) f.template put<J>((D[k] >> (32 - o - B)) & mask);
+  else f.template put<J>(__builtin_amdgcn_alignbit(D[k], D[k + 1], 64 - o - B) & mask);
+  if constexpr (J + 1 < 16) decode_quarter_apply<B, J + 1>(D, f);
+}
+
+template <typename F>
+__device__ __forceinline__ void decode_column_lq(const uint8_t *fwd, int bits, int64_t qi, F &f) {
+#define PINOT_LQ(B)                        \
+  {                                        \
+    uint32_t D[(B + 1) / 2 + 1];           \
+    load_quarter_lq<B>(fwd, qi, D);        \
+    decode_quarter_apply<B, 0>(D, f);      \
+  }
+  switch (bits) {  // widths up to kGroupLwMaxBits (the host routes wider columns through group_chunk_pf)
+    case 1: PINOT_LQ(1); break;   case 2: PINOT_LQ(2); break;   case 3: PINOT_LQ(3); break;   case 4: PINOT_LQ(4); break;
+    case 5: PINOT_LQ(5); break;   case 6: PINOT_LQ(6); break;   case 7: PINOT_LQ(7); break;   case 8: PINOT_LQ(8); break;
+    case 9: PINOT_LQ(9); break;   case 10: PINOT_LQ(10); break; case 11: PINOT_LQ(11); break; case 12: PINOT_LQ(12); break;
+    case 13: PINOT_LQ(13); break; case 14: PINOT_LQ(14); break; case 15: PINOT_LQ(15); break; case 16: PINOT_LQ(16); break;
+    case 17: PINOT_LQ(17); break; case 18: PINOT_LQ(18); break; case 19: PINOT_LQ(19); break; case 20: PINOT_LQ(20); break;
+    default: break;
+  }
+#undef PINOT_LQ
+}
+
+// GB_EMIT2 sink of a lane's 16 records, every stage batched over them (one LDS round trip per stage instead of
+// one per record): claim a slot of the partition's LDS bucket (count), store the record with its valid bit (bit
+// 63; records use <= 63 bits), and the record that claimed the last slot flushes the bucket once the quarter's
+// stores are issued. A flusher waits for its bucket's slots to turn valid (their writers claimed them before it
+// and store with no wait in between, so the wait ends), then eight lanes move the bucket out as one 64-B piece
+// to the block's run of the partition, clear the slots and reopen the bucket (count 0: the clears precede it in
+// this wave's LDS order). A record that finds its bucket full goes straight to its run slot.
+constexpr unsigned long long kRecValid = 1ull << 63;
+
+__device__ __forceinline__ void emit2_sink16(const GroupArgs &a, uint32_t *plds, uint32_t act,
+                                             const uint32_t (&key)[16], const unsigned long long (&rec)[16],
+                                             int lane) {
+  if (a.reserved2 == 4) return;  // debug.emit=4 (timing only, wrong results): reads + decode, no sink
+  const bool st = a.reserved2 != 3;  // debug.emit=3: bucket logic without the global stores
+  uint32_t *cur = plds, *cnt = plds + a.P;
+  unsigned long long *bkt = reinterpret_cast<unsigned long long *>(plds + ((3 * a.P + 1) & ~1));
+  const uint32_t lmask = (1u << a.shift) - 1u;
+  uint32_t pos[16];
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    pos[j] = 0;
+    if ((act >> j) & 1u) pos[j] = atomicAdd(&cnt[key[j] >> a.shift], 1u);
+  }
+  // bucket stores (no LDS returns: no waits); records that found their bucket full are marked for the run slots
+  uint32_t flush = 0, over = 0;
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    const bool in = ((act >> j) & 1u) && pos[j] < (uint32_t)kBucketRecs;
+    if (in)
+      __hip_atomic_store(&bkt[(key[j] >> a.shift) * kBucketRecs + pos[j]], rec[j] | (key[j] & lmask) | kRecValid,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    flush |= (in && pos[j] == (uint32_t)kBucketRecs - 1) ? (1u << j) : 0u;
+    over |= (((act >> j) & 1u) && !in) ? (1u << j) : 0u;
+  }
+  if (__any(over != 0)) {
+    uint32_t d[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++)
+      if ((over >> j) & 1u) d[j] = atomicAdd(&cur[key[j] >> a.shift], 1u);
+#pragma unroll
+    for (int j = 0; j < 16; j++)
+      if (((over >> j) & 1u) && st) a.emit[d[j]] = rec[j] | (key[j] & lmask);
+  }
+  while (true) {
+    const uint64_t fm = __ballot(flush != 0);
+    if (!fm) break;  // uniform
+    // this round's bucket per flushing lane: its lowest pending record
+    const int j = flush ? __builtin_ctz(flush) : 0;
+    uint32_t pk = 0;
+#pragma unroll
+    for (int t = 0; t < 16; t++) pk = t == j ? key[t] : pk;
+    const uint32_t p = pk >> a.shift;
+    const uint32_t dst = flush ? atomicAdd(&cur[p], (uint32_t)kBucketRecs) : 0u;
+    const int nf = __popcll(fm);
+    for (int f0 = 0; f0 < nf; f0 += 64 / kBucketRecs) {  // uniform: 8 buckets per wave instruction
+      const int f = min(f0 + lane / kBucketRecs, nf - 1), i = lane % kBucketRecs;
+      const int src = select_bit(fm, f);
+      const uint32_t pf = (uint32_t)__shfl((int)p, src, 64), df = (uint32_t)__shfl((int)dst, src, 64);
+      if (f0 + lane / kBucketRecs < nf) {
+        unsigned long long *slot = &bkt[pf * kBucketRecs + i];
+        unsigned long long v = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        while (!(v & kRecValid)) v = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (st) a.emit[df + i] = v & ~kRecValid;
+        __hip_atomic_store(slot, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
+    // reopen: a relaxed LDS store after the clears (one wave's LDS operations execute in issue order; the compiler
+    // fence keeps that order). A release here would wait for every outstanding HBM store of the wave (vmcnt(0)).
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    if (flush) {
+      __hip_atomic_store(&cnt[p], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      flush &= flush - 1u;
+    }
+  }
+}
+
+// Raw dwords of a lane's quarter: ceil(B/2) (+1 for odd B) from dword (qi * B) / 2, issued as up to three 16-B loads
+// so that every column's loads of a quarter are in flight before the first decode waits.
+__device__ __forceinline__ void load_raw_lq(const uint8_t *fwd, int bits, int64_t qi, uint32_t (&R)[12]) {
+  const uint32_t *p = reinterpret_cast<const uint32_t *>(fwd) + ((qi * bits) >> 1);
+  const int n = (bits + 1) / 2 + (bits & 1);
+  const u32x4a x0 = gload<u32x4a>(p);
+  R[0] = x0.x; R[1] = x0.y; R[2] = x0.z; R[3] = x0.w;
+  if (n > 4) {  // uniform
+    const u32x4a x1 = gload<u32x4a>(p + 4);
+    R[4] = x1.x; R[5] = x1.y; R[6] = x1.z; R[7] = x1.w;
+  }
+  if (n > 8) {
+    const u32x4a x2 = gload<u32x4a>(p + 8);
+    R[8] = x2.x; R[9] = x2.y; R[10] = x2.z; R[11] = x2.w;
+  }
+}
+
+struct IdOut {
+  uint32_t (&id)[16];
+  template <int J>
+  __device__ __forceinline__ void put(uint32_t v) { id[J] = v; }
+};
+
+template <int B>
+__device__ __forceinline__ void decode_raw_lq_b(const uint32_t (&R)[12], int64_t qi, uint32_t (&id)[16]) {
+  constexpr int N = (B + 1) / 2 + (B & 1);
+  uint32_t D[(B + 1) / 2 + 1];
+  if constexpr (B & 1) {
+    const bool odd = qi & 1;
+#pragma unroll
+    for (int i = 0; i + 1 < N; i++) D[i] = odd ? __builtin_amdgcn_alignbit(bswap32(R[i]), bswap32(R[i + 1]), 16) : bswap32(R[i]);
+    D[N - 1] = bswap32(R[N - 1]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < N; i++) D[i] = bswap32(R[i]);
+  }
+  IdOut f{id};
+  decode_quarter_apply<B, 0>(D, f);
+}
+
+__device__ __forceinline__ void decode_raw_lq(const uint32_t (&R)[12], int bits, int64_t qi, uint32_t (&id)[16]) {
+#define PINOT_RQ(B) decode_raw_lq_b<B>(R, qi, id)
+  switch (bits) {  // widths up to kGroupLwMaxBits (the host routes wider columns through group_chunk_pf)
+    case 1: PINOT_RQ(1); break;   case 2: PINOT_RQ(2); break;   case 3: PINOT_RQ(3); break;   case 4: PINOT_RQ(4); break;
+    case 5: PINOT_RQ(5); break;   case 6: PINOT_RQ(6); break;   case 7: PINOT_RQ(7); break;   case 8: PINOT_RQ(8); break;
+    case 9: PINOT_RQ(9); break;   case 10: PINOT_RQ(10); break; case 11: PINOT_RQ(11); break; case 12: PINOT_RQ(12); break;
+    case 13: PINOT_RQ(13); break; case 14: PINOT_RQ(14); break; case 15: PINOT_RQ(15); break; case 16: PINOT_RQ(16); break;
+    case 17: PINOT_RQ(17); break; case 18: PINOT_RQ(18); break; case 19: PINOT_RQ(19); break; case 20: PINOT_RQ(20); break;
+    default: break;
+  }
+#undef PINOT_RQ
+}
+
+template <int MODE>
+__device__ __forceinline__ void group_quarter_lq(const GroupArgs &a, const GroupSegment &sg, int64_t qi, uint32_t mq,
+                                                 int lane, uint32_t *plds) {
+  constexpr int U = kGroupPfUnroll, C = kGroupPfCols;
+  const int nc = MODE == GB_COUNT ? a.n_gcols : a.pf_nc;
+  uint32_t key[16];
+  unsigned long long rec[16];
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    key[j] = 0;
+    rec[j] = 0;
+  }
+  // column descriptors (uniform), then every column's raw loads, then the decodes
+  const uint8_t *fwd[C];
+  const int32_t *remap[C];
+  uint32_t stride[C];
+  int bits[C], fsh[C];
+#pragma unroll
+  for (int c = 0; c < C; c++) {
+    fwd[c] = nullptr;
+    remap[c] = nullptr;
+    stride[c] = 0;
+    bits[c] = 0;
+    fsh[c] = -1;  // -1: a group column (key fold)
+    if (c < nc) {
+      if (c < a.n_gcols) {
+        const GroupColDev gc = load_const(a.gcols + sg.first_gcol + c);
+        fwd[c] = gc.fwd;
+        remap[c] = gc.remap;
+        stride[c] = (uint32_t)gc.stride;
+        bits[c] = gc.bits;
+      } else if (MODE != GB_COUNT) {
+        const int ai = c == 1 ? a.pf_agg[1] : c == 2 ? a.pf_agg[2] : a.pf_agg[3];
+        const GroupAggDev ag = load_const(a.aggs + sg.first_agg + ai);
+        fwd[c] = ag.fwd;
+        bits[c] = ag.bits;
+        fsh[c] = ag.field_shift;
+      }
+    }
+  }
+  uint32_t R[C][12];
+#pragma unroll
+  for (int c = 0; c < C; c++)
+    if (bits[c]) load_raw_lq(fwd[c], bits[c], qi, R[c]);
+#pragma unroll
+  for (int c = 0; c < C; c++) {
+    if (!bits[c]) continue;
+    uint32_t id[16];
+    decode_raw_lq(R[c], bits[c], qi, id);
+    if (fsh[c] < 0) {
+      if (remap[c]) {
+#pragma unroll
+        for (int j = 0; j < 16; j++) key[j] += (uint32_t)gload<int32_t>(remap[c] + id[j]) * stride[c];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 16; j++) key[j] += id[j] * stride[c];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 16; j++) rec[j] |= (unsigned long long)id[j] << fsh[c];
+    }
+  }
+  if constexpr (MODE == GB_EMIT2) {
+    uint32_t act = mq;
+    if (sg.admitted) {
+#pragma unroll
+      for (int j = 0; j < 16; j++)
+        if (!((gload<uint32_t>(sg.admitted + (key[j] >> 5)) >> (key[j] & 31)) & 1u)) act &= ~(1u << j);
+    }
+    emit2_sink16(a, plds, act, key, rec, lane);
+    return;
+  }
+#pragma unroll
+  for (int j0 = 0; j0 < 16; j0 += U) {
+    bool act[U];
+    unsigned long long k[U], r[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      act[u] = (mq >> (j0 + u)) & 1u;
+      k[u] = key[j0 + u];
+      r[u] = rec[j0 + u];
+    }
+    if (sg.admitted) {
+#pragma unroll
+      for (int u = 0; u < U; u++) act[u] = act[u] && ((sg.admitted[k[u] >> 5] >> (k[u] & 31)) & 1u);
+    }
+    group_sink<MODE, U>(a, plds, act, k, r, lane);
+  }
+}
+
+template <int MODE>
+__device__ __forceinline__ void group_chunk_lq(const GroupArgs &a, const GroupSegment &sg, int64_t ch, uint64_t mask,
+                                               int lane, uint32_t *plds) {
+#pragma unroll 1
+  for (int q = 0; q < 4; q++) {
+    const int src = 16 * q + (lane >> 2);
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)mask, src, 64);
+    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(mask >> 32), src, 64);
+    const uint32_t mq = (((lane & 2) ? hi : lo) >> (16 * (lane & 1))) & 0xFFFFu;
+    if (__any(mq != 0)) group_quarter_lq<MODE>(a, sg, ch * 256 + 64 * q + lane, mq, lane, plds);
+  }
+}
+
 // LDS accumulator identities (GB_LDS): counts 0, sums 0, min all-ones, max 0, HLL 0.
 __device__ __forceinline__ void init_group_lds(const GroupArgs &a, const GroupSegment &sg, uint8_t *acc_lds, int tid) {
   uint32_t *w = reinterpret_cast<uint32_t *>(acc_lds);
@@ -625,7 +925,8 @@ __device__ __forceinline__ void flush_group_lds(const GroupArgs &a, const GroupS
   }
 }
 
-// PATH: 0 = per-column loop, 1 = per-doc prefetch (group_chunk_pf), 2 = lane-owns-word (group_chunk_lw).
+// PATH: 0 = per-column loop, 1 = per-doc prefetch (group_chunk_pf), 2 = lane-owns-word (group_chunk_lw),
+// 3 = lane-owns-quarter, contiguous across the wave (group_chunk_lq).
 // A block walks groups of kGroupWaves consecutive chunks with stride bps * kGroupWaves whatever its wave count,
 // so blocks of every BLK own the same chunks (the COUNT pass's per-block histograms stay valid for EMIT).
 template <int MODE, int PATH = 0, int BLK = kGroupBlock>
@@ -688,7 +989,8 @@ __global__ __launch_bounds__(BLK) void k_group_query(GroupArgs a) {
     }
     matched += __popcll(mask);
     if (__any(mask != 0)) {
-      if constexpr (PATH == 2) group_chunk_lw<MODE>(a, sg, ch, mask, lane, plds);
+      if constexpr (PATH == 3) group_chunk_lq<MODE>(a, sg, ch, mask, lane, plds);
+      else if constexpr (PATH == 2) group_chunk_lw<MODE>(a, sg, ch, mask, lane, plds);
       else if constexpr (PATH == 1) group_chunk_pf<MODE>(a, sg, ch, mask, lane, plds);
       else group_chunk<MODE>(a, sg, ch, mask, lane, acc_lds, plds);
     }
@@ -701,7 +1003,7 @@ __global__ __launch_bounds__(BLK) void k_group_query(GroupArgs a) {
     const unsigned long long *bkt = reinterpret_cast<const unsigned long long *>(plds + ((3 * a.P + 1) & ~1));
     const int i = tid % kBucketRecs;
     for (int p = tid / kBucketRecs; p < a.P; p += BLK / kBucketRecs)
-      if ((uint32_t)i < plds[a.P + p]) a.emit[plds[p] + i] = bkt[p * kBucketRecs + i];
+      if ((uint32_t)i < plds[a.P + p]) a.emit[plds[p] + i] = bkt[p * kBucketRecs + i] & ~kRecValid;
   }
   if constexpr (MODE == GB_LDS) flush_group_lds(a, sg, acc_lds, tid);
   if constexpr (MODE == GB_COUNT) {
@@ -720,23 +1022,26 @@ static int group_block_threads(const GroupArgs &a) {
 // Every instance launch_group_query may pick for `a`, through one visitor (occupancy and launch agree).
 template <typename V>
 static void with_group_kernel(const GroupArgs &a, V &&v) {
-  const bool lw = a.lw && a.pf_nc > 0;
+  const bool lw = a.lw && a.pf_nc > 0, lh = lw && a.lw == 2;
   switch (a.mode) {
     case GB_GLOBAL: v(&k_group_query<GB_GLOBAL, 0, kGroupBlock>, kGroupBlock); break;
     case GB_LDS: v(&k_group_query<GB_LDS, 0, kGroupBlock>, kGroupBlock); break;
     case GB_COUNT:
-      if (lw) v(&k_group_query<GB_COUNT, 2, kGroupBlock>, kGroupBlock);
+      if (lh) v(&k_group_query<GB_COUNT, 3, kGroupBlock>, kGroupBlock);
+      else if (lw) v(&k_group_query<GB_COUNT, 2, kGroupBlock>, kGroupBlock);
       else if (a.pf_nc > 0) v(&k_group_query<GB_COUNT, 1, kGroupBlock>, kGroupBlock);
       else v(&k_group_query<GB_COUNT, 0, kGroupBlock>, kGroupBlock);
       break;
     case GB_EMIT:
-      if (lw) v(&k_group_query<GB_EMIT, 2, kGroupLwEmitBlock>, kGroupLwEmitBlock);
+      if (lh) v(&k_group_query<GB_EMIT, 3, kGroupLwEmitBlock>, kGroupLwEmitBlock);
+      else if (lw) v(&k_group_query<GB_EMIT, 2, kGroupLwEmitBlock>, kGroupLwEmitBlock);
       else if (a.pf_nc > 0) v(&k_group_query<GB_EMIT, 1, kGroupBlock>, kGroupBlock);
       else v(&k_group_query<GB_EMIT, 0, kGroupBlock>, kGroupBlock);
       break;
     case GB_FIRST: v(&k_group_query<GB_FIRST, 0, kGroupBlock>, kGroupBlock); break;
     case GB_EMIT2:
-      if (lw) v(&k_group_query<GB_EMIT2, 2, kGroupLwEmitBlock>, kGroupLwEmitBlock);
+      if (lh) v(&k_group_query<GB_EMIT2, 3, kGroupLwEmitBlock>, kGroupLwEmitBlock);
+      else if (lw) v(&k_group_query<GB_EMIT2, 2, kGroupLwEmitBlock>, kGroupLwEmitBlock);
       else v(&k_group_query<GB_EMIT2, 1, kGroupBlock>, kGroupBlock);
       break;
     default: v(&k_group_query<GB_VERIFY, 0, kGroupBlock>, kGroupBlock); break;

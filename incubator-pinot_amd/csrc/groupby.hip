@@ -80,6 +80,17 @@ __global__ __launch_bounds__(kReduceBlock) void k_partition_reduce(PartitionRedu
   __syncthreads();
   const uint32_t b = a.pstart[p], e = a.pstart[p + 1];
   const unsigned long long kmask = (unsigned long long)K - 1ull;
+  // count folded into the first affine dictId SUM: one 64-bit LDS atomic adds (1 << sbits) + dictId, i.e. the
+  // count above a sum field of sbits = bits + cbits (n records of < 2^bits each sum to < 2^sbits), when both
+  // fields fit (block-uniform: n = this partition's records)
+  const uint32_t n = e - b;
+  const int cbits = n ? 32 - __builtin_clz(n) : 1;
+  int pk = -1, sbits = 0;
+  for (int g = 0; g < a.n_aggs; g++)
+    if (pk < 0 && a.aggs[g].acc_kind == 0 && a.aggs[g].affine && a.aggs[g].bits + 2 * cbits <= 64) {
+      pk = g;
+      sbits = a.aggs[g].bits + cbits;
+    }
   // counts: one private copy per wave (a partition has few keys: LDS atomics on one copy serialise)
   const int wave = tid >> 6;
   uint32_t *wcnt = cnt + a.wave_cnt_off / 4 + (wave & (kReduceCountCopies - 1)) * K;
@@ -97,9 +108,11 @@ __global__ __launch_bounds__(kReduceBlock) void k_partition_reduce(PartitionRedu
       rec[u] = ok[u] ? __builtin_nontemporal_load(a.records + r) : 0ull;
       k[u] = (uint32_t)(rec[u] & kmask);
     }
+    if (pk < 0) {
 #pragma unroll
-    for (int u = 0; u < U; u++)
-      if (ok[u]) atomicAdd(wcnt + k[u], 1u);
+      for (int u = 0; u < U; u++)
+        if (ok[u]) atomicAdd(wcnt + k[u], 1u);
+    }
 #pragma unroll
     for (int g = 0; g < kMaxGroupAggs; g++) {
       if (g >= a.n_aggs) break;
@@ -113,6 +126,10 @@ __global__ __launch_bounds__(kReduceBlock) void k_partition_reduce(PartitionRedu
         long long v[U];  // affine: Σ dictId here, Σ value = base * count + step * Σ dictId at the end
 #pragma unroll
         for (int u = 0; u < U; u++) v[u] = ag.affine ? (long long)id[u] : (long long)static_cast<const int32_t *>(ag.dict)[id[u]];
+        if (g == pk) {
+#pragma unroll
+          for (int u = 0; u < U; u++) v[u] += 1ll << sbits;
+        }
 #pragma unroll
         for (int u = 0; u < U; u++)
           if (ok[u]) atomicAdd(reinterpret_cast<unsigned long long *>(acc) + k[u], (unsigned long long)v[u]);
@@ -162,7 +179,9 @@ __global__ __launch_bounds__(kReduceBlock) void k_partition_reduce(PartitionRedu
     const long long key = base + i;
     if (key >= a.G) break;
     uint32_t c = 0;
-    for (int w = 0; w < kReduceCountCopies; w++) c += cnt[a.wave_cnt_off / 4 + w * K + i];
+    if (pk >= 0) c = (uint32_t)(reinterpret_cast<const unsigned long long *>(lds + a.aggs[pk].lds_off)[i] >> sbits);
+    else
+      for (int w = 0; w < kReduceCountCopies; w++) c += cnt[a.wave_cnt_off / 4 + w * K + i];
     a.counts[key] = c;
   }
   for (int g = 0; g < a.n_aggs; g++) {
@@ -181,7 +200,12 @@ __global__ __launch_bounds__(kReduceBlock) void k_partition_reduce(PartitionRedu
         unsigned long long v = reinterpret_cast<const unsigned long long *>(acc)[i];
         if (ag.acc_kind == 0 && ag.affine) {
           uint32_t c = 0;
-          for (int w = 0; w < kReduceCountCopies; w++) c += cnt[a.wave_cnt_off / 4 + w * K + i];
+          if (pk >= 0) {
+            c = (uint32_t)(reinterpret_cast<const unsigned long long *>(lds + a.aggs[pk].lds_off)[i] >> sbits);
+            if (g == pk) v &= (1ull << sbits) - 1ull;
+          } else {
+            for (int w = 0; w < kReduceCountCopies; w++) c += cnt[a.wave_cnt_off / 4 + w * K + i];
+          }
           v = (unsigned long long)ag.affine_base * c + (unsigned long long)ag.affine_step * v;  // exact mod 2^64
         }
         out[key] = v;

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PINOT_GPU_ABI_VERSION 4
+#define PINOT_GPU_ABI_VERSION 5
 
 /* ------------------------------------------------------------------ status */
 typedef enum {
@@ -136,6 +136,7 @@ typedef struct {
   int64_t num_segments_processed;
   double device_ms;            /* HIP-event time of the device work of the call */
   double host_ms;              /* wall time from C-ABI entry to return (results on the host) */
+  int64_t num_segments_matched; /* segments with at least one matching doc (ExecutionStatistics.java:42) */
 } pinot_exec_stats;
 
 /* Intermediate result of one aggregation function over a set of segments (already
@@ -227,6 +228,31 @@ pinot_status pinot_groupby_export_keys(const pinot_groupby_result *r, char *buf,
 pinot_status pinot_groupby_trim(const pinot_groupby_result *r, int32_t top_n, int32_t fn, int64_t *groups,
                                 int64_t *num_out);
 void pinot_groupby_free(pinot_groupby_result *r);
+
+/* ------------------------------------------------------------------ DataTable (server -> broker bytes)
+ * IntermediateResultsBlock.getDataTable (PC/operator/blocks/IntermediateResultsBlock.java:206-317) serialized as
+ * DataTableImplV2.toBytes (PC/common/datatable/DataTableImplV2.java:233-347), object cells per ObjectSerDeUtils
+ * (PC/common/ObjectSerDeUtils.java). Metadata: the block's statistics (attachMetadataToDataTable :298-317) and,
+ * when `server` is given, the server's own keys (ServerQueryExecutorV1Impl.java:244-245). */
+typedef struct {
+  int64_t num_segments_queried;
+  int64_t time_used_ms;
+  int64_t request_id;          /* < 0: no requestId key */
+} pinot_datatable_server;
+
+/* Aggregation-only result (getAggregationResultDataTable :234-270): *out_len = size; bytes copied when buf_len
+ * suffices (buf == NULL: size only), else PINOT_ERR_BAD_ARG. */
+pinot_status pinot_datatable_aggregation(const pinot_query *query, const pinot_agg_result *results,
+                                         const pinot_exec_stats *stats, const pinot_datatable_server *server,
+                                         uint8_t *buf, uint64_t buf_len, uint64_t *out_len);
+/* Group-by result (getAggregationGroupByResultDataTable :272-292): one row per function, its map restricted to
+ * fn_groups[fn] (fn_num_groups[fn] group indexes, e.g. pinot_groupby_trim's output) when fn_groups and
+ * fn_groups[fn] are non-NULL. The bytes are owned by the result (*data valid until the next call on it or
+ * pinot_groupby_free). */
+pinot_status pinot_datatable_group_by(const pinot_query *query, const pinot_groupby_result *result,
+                                      const int64_t *const *fn_groups, const int64_t *fn_num_groups,
+                                      const pinot_exec_stats *stats, const pinot_datatable_server *server,
+                                      const uint8_t **data, uint64_t *len);
 
 /* ------------------------------------------------------------------ multi-GPU partials
  * Group-by over a GLOBAL dense key space, for segment sharding across ranks: each rank

@@ -13,6 +13,8 @@ Engine::~Engine() {
   for (auto ev : kev) (void)hipEventDestroy(ev);
   if (ev_start) (void)hipEventDestroy(ev_start);
   if (ev_stop) (void)hipEventDestroy(ev_stop);
+  for (hipEvent_t &ev : out_ev)
+    if (ev) (void)hipEventDestroy(ev);
   if (stream) (void)hipStreamDestroy(stream);
 }
 
@@ -79,6 +81,7 @@ std::unique_ptr<pinot_engine> create_engine(int32_t device, const char *config) 
     e->wall_clock_khz = khz;
   PINOT_HIP(hipEventCreate(&e->ev_start));
   PINOT_HIP(hipEventCreate(&e->ev_stop));
+  for (hipEvent_t &ev : e->out_ev) PINOT_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
   return e;
 }
 }  // namespace pinot
@@ -334,19 +337,38 @@ pinot_status pinot_groupby_hll(const pinot_groupby_result *r, int32_t fn, uint8_
     require(r && fn >= 0 && fn < (int32_t)r->functions.size(), PINOT_ERR_BAD_ARG, "function index");
     require(r->functions[fn] == PINOT_AGG_DISTINCTCOUNTHLL, PINOT_ERR_BAD_ARG, "not a DISTINCTCOUNTHLL function");
     const size_t n = r->raw_keys.size();
-    if (registers && n) {
-      if (!r->hll_parts.empty()) {
-        for (const HllPart &p : r->hll_parts) {
-          if (!p.num_groups) continue;
-          PINOT_HIP(hipSetDevice(p.device));
-          PINOT_HIP(hipMemcpy(registers + p.group_begin * 256, p.buf->get<uint8_t>() + p.off[fn], p.num_groups * 256,
-                              hipMemcpyDeviceToHost));
-        }
-      } else {
-        memcpy(registers, r->hll[fn].data(), n * 256);
-      }
-    }
+    if (registers && n) group_by_hll_registers(*r, fn, registers);
     if (cardinalities && n) memcpy(cardinalities, r->hll_card[fn].data(), n * 8);
+  });
+}
+
+pinot_status pinot_datatable_aggregation(const pinot_query *query, const pinot_agg_result *results,
+                                         const pinot_exec_stats *stats, const pinot_datatable_server *server,
+                                         uint8_t *buf, uint64_t buf_len, uint64_t *out_len) {
+  return guard([&] {
+    require(results && stats && out_len, PINOT_ERR_BAD_ARG, "null argument");
+    check_query(query);
+    const std::vector<uint8_t> b = aggregation_datatable(*query, results, *stats, server);
+    *out_len = b.size();
+    if (!buf) return;
+    require(buf_len >= b.size(), PINOT_ERR_BAD_ARG, "DataTable buffer too small");
+    memcpy(buf, b.data(), b.size());
+  });
+}
+
+pinot_status pinot_datatable_group_by(const pinot_query *query, const pinot_groupby_result *result,
+                                      const int64_t *const *fn_groups, const int64_t *fn_num_groups,
+                                      const pinot_exec_stats *stats, const pinot_datatable_server *server,
+                                      const uint8_t **data, uint64_t *len) {
+  return guard([&] {
+    require(result && stats && data && len, PINOT_ERR_BAD_ARG, "null argument");
+    check_query(query);
+    require(query->num_aggregations == (int32_t)result->functions.size(), PINOT_ERR_BAD_ARG,
+            "query and result disagree on the aggregations");
+    require(!fn_groups || fn_num_groups, PINOT_ERR_BAD_ARG, "fn_groups without fn_num_groups");
+    result->datatable = group_by_datatable(*query, *result, fn_groups, fn_num_groups, *stats, server);
+    *data = result->datatable.data();
+    *len = result->datatable.size();
   });
 }
 

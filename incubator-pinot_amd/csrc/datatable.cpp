@@ -1,0 +1,319 @@
+// Server → broker wire format of a query's combined result: IntermediateResultsBlock.getDataTable
+// (PC/operator/blocks/IntermediateResultsBlock.java:206-317) built with DataTableBuilder
+// (PC/common/datatable/DataTableBuilder.java:72-160) and written by DataTableImplV2.toBytes
+// (PC/common/datatable/DataTableImplV2.java:233-347); object cells per ObjectSerDeUtils
+// (PC/common/ObjectSerDeUtils.java:47-98 type ids, :144-330 serializers). PC = pinot-core/src/main/java/org/apache/pinot/core.
+//
+// Layout (all integers big-endian, DataOutputStream):
+//   int VERSION (2), int numRows, int numColumns,
+//   (int start, int length) x 5 for: dictionary map, metadata, data schema, fixed-size rows, variable-size data
+//   (HEADER_SIZE = 13 ints; starts are absolute offsets), then the five sections back to back.
+// Maps the reference builds as java.util.HashMap are written in HashMap iteration order (bucket (h ^ h >>> 16) &
+// (capacity - 1) of String.hashCode / Integer.hashCode, insertion order within a bucket), so the metadata and
+// dictionary sections are byte-identical to the reference's. The group-by result maps are written in ascending raw
+// key order: the reference's map is a ConcurrentHashMap filled by concurrent segment threads, whose order is not
+// deterministic either; the broker reads it back into a HashMap (order-free).
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "engine.h"
+
+namespace pinot {
+namespace {
+
+class Out {
+ public:
+  std::vector<uint8_t> b;
+  void i32(int32_t v) {
+    const uint32_t u = (uint32_t)v;
+    const uint8_t x[4] = {(uint8_t)(u >> 24), (uint8_t)(u >> 16), (uint8_t)(u >> 8), (uint8_t)u};
+    b.insert(b.end(), x, x + 4);
+  }
+  void i64(int64_t v) {
+    i32((int32_t)((uint64_t)v >> 32));
+    i32((int32_t)(uint64_t)v);
+  }
+  void f64(double d) {  // Double.doubleToRawLongBits
+    int64_t v;
+    memcpy(&v, &d, 8);
+    i64(v);
+  }
+  void bytes(const void *p, size_t n) { b.insert(b.end(), (const uint8_t *)p, (const uint8_t *)p + n); }
+  void str(const std::string &s) {  // int length + UTF-8 bytes (StringUtil.encodeUtf8)
+    i32((int32_t)s.size());
+    bytes(s.data(), s.size());
+  }
+  void put_i32_at(size_t off, int32_t v) {
+    const uint32_t u = (uint32_t)v;
+    b[off] = (uint8_t)(u >> 24);
+    b[off + 1] = (uint8_t)(u >> 16);
+    b[off + 2] = (uint8_t)(u >> 8);
+    b[off + 3] = (uint8_t)u;
+  }
+};
+
+// java.lang.String.hashCode over the UTF-16 code units of a UTF-8 string.
+int32_t java_string_hash(const std::string &s) {
+  uint32_t h = 0;
+  for (size_t i = 0; i < s.size();) {
+    const uint8_t c = (uint8_t)s[i];
+    uint32_t cp;
+    int len;
+    if (c < 0x80) { cp = c; len = 1; }
+    else if ((c >> 5) == 6 && i + 1 < s.size()) { cp = ((c & 0x1Fu) << 6) | (s[i + 1] & 0x3Fu); len = 2; }
+    else if ((c >> 4) == 14 && i + 2 < s.size()) { cp = ((c & 0x0Fu) << 12) | ((s[i + 1] & 0x3Fu) << 6) | (s[i + 2] & 0x3Fu); len = 3; }
+    else if (i + 3 < s.size()) {
+      cp = ((c & 0x07u) << 18) | ((s[i + 1] & 0x3Fu) << 12) | ((s[i + 2] & 0x3Fu) << 6) | (s[i + 3] & 0x3Fu);
+      len = 4;
+    } else { cp = c; len = 1; }
+    i += len;
+    if (cp >= 0x10000) {  // surrogate pair
+      cp -= 0x10000;
+      h = 31u * h + (0xD800u + (cp >> 10));
+      h = 31u * h + (0xDC00u + (cp & 0x3FFu));
+    } else {
+      h = 31u * h + cp;
+    }
+  }
+  return (int32_t)h;
+}
+
+// Iteration order of a java.util.HashMap filled with keys of these hashes in this order (default capacity 16,
+// load factor 0.75, doubling; resizes keep the relative order of a bucket's entries; small maps never treeify).
+std::vector<size_t> java_hashmap_order(const std::vector<int32_t> &hashes) {
+  size_t cap = 16;
+  while ((double)hashes.size() > 0.75 * (double)cap) cap <<= 1;
+  std::vector<std::vector<size_t>> buckets(cap);
+  for (size_t i = 0; i < hashes.size(); i++) {
+    const uint32_t h = (uint32_t)hashes[i];
+    buckets[(h ^ (h >> 16)) & (cap - 1)].push_back(i);
+  }
+  std::vector<size_t> order;
+  for (auto &bk : buckets) order.insert(order.end(), bk.begin(), bk.end());
+  return order;
+}
+
+// AggregationFunction.getColumnName (CountAggregationFunction.java:43-45 "count_star"; others
+// AggregationFunctionType.getName() + "_" + column, e.g. SumAggregationFunction.java:42-44).
+std::string aggregation_column_name(const pinot_agg_spec &a) {
+  const std::string col = (a.column && *a.column) ? a.column : "*";
+  switch (a.function) {
+    case PINOT_AGG_COUNT: return "count_star";
+    case PINOT_AGG_SUM: return "sum_" + col;
+    case PINOT_AGG_MIN: return "min_" + col;
+    case PINOT_AGG_MAX: return "max_" + col;
+    case PINOT_AGG_AVG: return "avg_" + col;
+    case PINOT_AGG_DISTINCTCOUNTHLL: return "distinctCountHLL_" + col;
+    default: throw Error(PINOT_ERR_BAD_ARG, "aggregation function");
+  }
+}
+
+enum ObjType : int32_t { OBJ_STRING = 0, OBJ_LONG = 1, OBJ_DOUBLE = 2, OBJ_AVG_PAIR = 4, OBJ_HLL = 6, OBJ_MAP = 8 };
+
+// stream-lib 2.7.0 HyperLogLog.getBytes (log2m 8): int log2m, int registerSet.size * 4, then the RegisterSet's 43
+// int words, register p in word p / 6 at bit 5 * (p % 6) (RegisterSet.set; LOG2_BITS_PER_WORD 6, REGISTER_SIZE 5).
+void hll_bytes(Out &o, const uint8_t *regs) {
+  constexpr int kWords = 43;  // getSizeForCount(256): 256 / 6 = 42, not a multiple of 32 -> 43
+  uint32_t m[kWords] = {};
+  for (int p = 0; p < 256; p++) m[p / 6] |= (uint32_t)(regs[p] & 0x1F) << (5 * (p % 6));
+  o.i32(8);
+  o.i32(kWords * 4);
+  for (int w = 0; w < kWords; w++) o.i32((int32_t)m[w]);
+}
+
+// DataSchema.toBytes (pinot-common/.../utils/DataSchema.java:114-139): names, then type names.
+void schema_bytes(Out &o, const std::vector<std::string> &names, const std::vector<std::string> &types) {
+  o.i32((int32_t)names.size());
+  for (auto &n : names) o.str(n);
+  for (auto &t : types) o.str(t);
+}
+
+struct Table {
+  int32_t rows = 0, cols = 0;
+  bool has_schema = true;
+  std::vector<std::pair<std::string, std::vector<std::string>>> dictionaries;  // column -> values by dictId
+  std::vector<std::pair<std::string, std::string>> metadata;                  // insertion order
+  Out schema, fixed, var;
+};
+
+std::vector<uint8_t> table_bytes(const Table &t) {
+  Out dict;  // serializeDictionaryMap (DataTableImplV2.java:305-328): HashMap<String, HashMap<Integer, String>>
+  {
+    std::vector<int32_t> h;
+    for (auto &d : t.dictionaries) h.push_back(java_string_hash(d.first));
+    dict.i32((int32_t)t.dictionaries.size());
+    for (size_t i : java_hashmap_order(h)) {
+      const auto &d = t.dictionaries[i];
+      dict.str(d.first);
+      dict.i32((int32_t)d.second.size());
+      std::vector<int32_t> ih(d.second.size());
+      for (size_t k = 0; k < ih.size(); k++) ih[k] = (int32_t)k;  // Integer.hashCode
+      for (size_t k : java_hashmap_order(ih)) {
+        dict.i32((int32_t)k);
+        dict.str(d.second[k]);
+      }
+    }
+  }
+  Out meta;  // serializeMetadata (:330-347)
+  {
+    std::vector<int32_t> h;
+    for (auto &kv : t.metadata) h.push_back(java_string_hash(kv.first));
+    meta.i32((int32_t)t.metadata.size());
+    for (size_t i : java_hashmap_order(h)) {
+      meta.str(t.metadata[i].first);
+      meta.str(t.metadata[i].second);
+    }
+  }
+  Out o;  // toBytes (:233-303)
+  const int32_t header = 13 * 4;
+  o.i32(2);
+  o.i32(t.rows);
+  o.i32(t.cols);
+  int32_t off = header;
+  o.i32(off);
+  o.i32((int32_t)dict.b.size());
+  off += (int32_t)dict.b.size();
+  o.i32(off);
+  o.i32((int32_t)meta.b.size());
+  off += (int32_t)meta.b.size();
+  o.i32(off);
+  o.i32(t.has_schema ? (int32_t)t.schema.b.size() : 0);
+  off += t.has_schema ? (int32_t)t.schema.b.size() : 0;
+  o.i32(off);
+  o.i32((int32_t)t.fixed.b.size());
+  off += (int32_t)t.fixed.b.size();
+  o.i32(off);
+  o.i32((int32_t)t.var.b.size());
+  o.bytes(dict.b.data(), dict.b.size());
+  o.bytes(meta.b.data(), meta.b.size());
+  if (t.has_schema) o.bytes(t.schema.b.data(), t.schema.b.size());
+  o.bytes(t.fixed.b.data(), t.fixed.b.size());
+  o.bytes(t.var.b.data(), t.var.b.size());
+  require(o.b.size() < (size_t)INT32_MAX, PINOT_ERR_UNSUPPORTED, "DataTable over 2 GB (int offsets)");
+  return std::move(o.b);
+}
+
+// attachMetadataToDataTable (IntermediateResultsBlock.java:298-317) + the server's own keys
+// (ServerQueryExecutorV1Impl.java:244-245) when the caller passes them.
+void attach_metadata(Table &t, const pinot_exec_stats &s, bool groups_limit_reached, const pinot_datatable_server *srv) {
+  t.metadata.emplace_back("numDocsScanned", std::to_string(s.num_docs_scanned));
+  t.metadata.emplace_back("numEntriesScannedInFilter", std::to_string(s.num_entries_scanned_in_filter));
+  t.metadata.emplace_back("numEntriesScannedPostFilter", std::to_string(s.num_entries_scanned_post_filter));
+  t.metadata.emplace_back("numSegmentsProcessed", std::to_string(s.num_segments_processed));
+  t.metadata.emplace_back("numSegmentsMatched", std::to_string(s.num_segments_matched));
+  t.metadata.emplace_back("totalDocs", std::to_string(s.num_total_raw_docs));
+  if (groups_limit_reached) t.metadata.emplace_back("numGroupsLimitReached", "true");
+  if (srv) {
+    t.metadata.emplace_back("numSegmentsQueried", std::to_string(srv->num_segments_queried));
+    t.metadata.emplace_back("timeUsedMs", std::to_string(srv->time_used_ms));
+    if (srv->request_id >= 0) t.metadata.emplace_back("requestId", std::to_string(srv->request_id));
+  }
+}
+
+// DataTableBuilder.setColumn(int, Object) (:141-152): fixed cell = (variable offset, serialized length); variable
+// data = int object type + serialized bytes.
+template <typename F>
+void object_cell(Table &t, int32_t type, F &&serialize) {
+  Out v;
+  serialize(v);
+  t.fixed.i32((int32_t)t.var.b.size());
+  t.fixed.i32((int32_t)v.b.size());
+  t.var.i32(type);
+  t.var.bytes(v.b.data(), v.b.size());
+}
+
+}  // namespace
+
+std::vector<uint8_t> aggregation_datatable(const pinot_query &q, const pinot_agg_result *r, const pinot_exec_stats &s,
+                                           const pinot_datatable_server *srv) {
+  // getAggregationResultDataTable (:234-270): one row, one column per function (intermediate result types)
+  Table t;
+  t.rows = 1;
+  t.cols = q.num_aggregations;
+  std::vector<std::string> names, types;
+  for (int i = 0; i < q.num_aggregations; i++) {
+    names.push_back(aggregation_column_name(q.aggregations[i]));
+    const int f = q.aggregations[i].function;
+    types.push_back(f == PINOT_AGG_COUNT ? "LONG" : (f == PINOT_AGG_AVG || f == PINOT_AGG_DISTINCTCOUNTHLL) ? "OBJECT" : "DOUBLE");
+  }
+  schema_bytes(t.schema, names, types);
+  for (int i = 0; i < q.num_aggregations; i++) {
+    const pinot_agg_result &a = r[i];
+    switch (q.aggregations[i].function) {
+      case PINOT_AGG_COUNT: t.fixed.i64(a.count); break;
+      case PINOT_AGG_SUM:
+      case PINOT_AGG_MIN:
+      case PINOT_AGG_MAX: t.fixed.f64(a.value); break;
+      case PINOT_AGG_AVG:  // AvgPair.toBytes (customobject/AvgPair.java:53-58): double sum, long count
+        object_cell(t, OBJ_AVG_PAIR, [&](Out &v) { v.f64(a.value); v.i64(a.count); });
+        break;
+      default:
+        object_cell(t, OBJ_HLL, [&](Out &v) { hll_bytes(v, a.hll_registers); });
+        break;
+    }
+  }
+  attach_metadata(t, s, false, srv);
+  return table_bytes(t);
+}
+
+std::vector<uint8_t> group_by_datatable(const pinot_query &q, const GroupByResult &r, const int64_t *const *fn_groups,
+                                        const int64_t *fn_num_groups, const pinot_exec_stats &s,
+                                        const pinot_datatable_server *srv) {
+  // getAggregationGroupByResultDataTable (:272-292): per function a row (functionName STRING via the column's
+  // dictionary, GroupByResultMap OBJECT = Map<String group key, intermediate result>)
+  const int na = (int)r.functions.size();
+  const int64_t n = (int64_t)r.raw_keys.size();
+  Table t;
+  t.rows = na;
+  t.cols = 2;
+  schema_bytes(t.schema, {"functionName", "GroupByResultMap"}, {"STRING", "OBJECT"});
+  std::vector<std::string> fn_names;
+  std::vector<uint8_t> regs;
+  for (int i = 0; i < na; i++) {
+    const std::string name = aggregation_column_name(q.aggregations[i]);
+    int32_t id = (int32_t)fn_names.size();
+    for (size_t k = 0; k < fn_names.size(); k++)
+      if (fn_names[k] == name) id = (int32_t)k;
+    if (id == (int32_t)fn_names.size()) fn_names.push_back(name);
+    t.fixed.i32(id);
+    const int64_t m = fn_groups && fn_groups[i] ? fn_num_groups[i] : n;
+    auto group = [&](int64_t j) -> int64_t {
+      const int64_t g = fn_groups && fn_groups[i] ? fn_groups[i][j] : j;
+      require(g >= 0 && g < n, PINOT_ERR_BAD_ARG, "group index out of range");
+      return g;
+    };
+    const int f = r.functions[i];
+    if (f == PINOT_AGG_DISTINCTCOUNTHLL) {
+      regs.resize((size_t)n * 256);
+      group_by_hll_registers(r, i, regs.data());
+    }
+    const std::vector<int64_t> &cnt = r.counts[r.counts_shared ? 0 : i];
+    const std::vector<double> &val = r.values[i];
+    const int32_t vtype = f == PINOT_AGG_COUNT ? OBJ_LONG : f == PINOT_AGG_AVG ? OBJ_AVG_PAIR
+                          : f == PINOT_AGG_DISTINCTCOUNTHLL ? OBJ_HLL : OBJ_DOUBLE;
+    object_cell(t, OBJ_MAP, [&](Out &v) {  // MAP_SER_DE (ObjectSerDeUtils.java:262-300)
+      v.i32((int32_t)m);
+      if (m == 0) return;
+      v.i32(OBJ_STRING);
+      v.i32(vtype);
+      for (int64_t j = 0; j < m; j++) {
+        const int64_t g = group(j);
+        v.str(r.key(g));
+        switch (f) {
+          case PINOT_AGG_COUNT: v.i32(8); v.i64(cnt[g]); break;
+          case PINOT_AGG_AVG: v.i32(16); v.f64(val[g]); v.i64(cnt[g]); break;
+          case PINOT_AGG_DISTINCTCOUNTHLL: v.i32(8 + 43 * 4); hll_bytes(v, regs.data() + (size_t)g * 256); break;
+          default: v.i32(8); v.f64(val[g]); break;
+        }
+      }
+    });
+  }
+  t.dictionaries.emplace_back("functionName", fn_names);
+  // CombineGroupByOperator.java:212-214: the merged map reached the inner-segment groups limit
+  attach_metadata(t, s, n >= (int64_t)q.num_groups_limit && q.num_groups_limit > 0, srv);
+  return table_bytes(t);
+}
+
+}  // namespace pinot

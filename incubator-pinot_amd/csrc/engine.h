@@ -197,6 +197,7 @@ struct Engine {
 
   // timing
   hipEvent_t ev_start = nullptr, ev_stop = nullptr;
+  hipEvent_t out_ev[4] = {};  // group-by output chunks (D2H of chunk c complete)
   std::vector<hipEvent_t> kev;  // per-kernel event pairs (timing mode)
   double last_ms[2] = {0, 0};
   int64_t last_launches[2] = {0, 0};
@@ -253,7 +254,16 @@ struct GroupByResult {
   std::vector<std::vector<int64_t>> hll_card;
   std::vector<std::vector<uint8_t>> hll;
   std::vector<HllPart> hll_parts;
-};std::unique_ptr<GroupByResult> exec_group_by(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q,
+  mutable std::vector<uint8_t> datatable;  // pinot_datatable_group_by's bytes
+};
+// all groups' u8 HLL registers of function fn ([groups][256]) into host memory, from the device parts or the host copy
+void group_by_hll_registers(const GroupByResult &r, int fn, uint8_t *registers);
+// DataTable bytes (datatable.cpp)
+std::vector<uint8_t> aggregation_datatable(const pinot_query &q, const pinot_agg_result *r, const pinot_exec_stats &s,
+                                           const pinot_datatable_server *srv);
+std::vector<uint8_t> group_by_datatable(const pinot_query &q, const GroupByResult &r, const int64_t *const *fn_groups,
+                                        const int64_t *fn_num_groups, const pinot_exec_stats &s,
+                                        const pinot_datatable_server *srv);std::unique_ptr<GroupByResult> exec_group_by(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q,
                                              pinot_exec_stats *stats);
 
 // multi-GPU partials

@@ -503,6 +503,7 @@ void fill_stats(const pinot_query &q, const std::vector<SegPlan> &plans, const s
   }
   st->num_entries_scanned_post_filter = st->num_docs_scanned * projected_columns(q);
   st->num_segments_processed = (int64_t)plans.size();
+  for (size_t i = 0; i < plans.size(); i++) st->num_segments_matched += counts[i] > 0;
   st->device_ms = ms;
 }
 
@@ -1046,6 +1047,7 @@ bool shortcut_aggregate(const std::vector<SegmentData *> &segs, const pinot_quer
     stats->num_docs_scanned = total;
     stats->num_total_raw_docs = total;
     stats->num_segments_processed = (int64_t)segs.size();
+    for (auto *sg : segs) stats->num_segments_matched += sg->num_docs > 0;
   }
   return true;
 }
@@ -1640,7 +1642,8 @@ GroupByResult::~GroupByResult() {
   auto put = [&p](auto &pool, auto &v) {
     const size_t b = v.capacity() * sizeof(v[0]);
     if (v.capacity() >= kPoolMinElems && pool.size() < kPoolMaxArrays && p.bytes + b <= kPoolMaxBytes) {
-      v.clear();
+      // size kept: the next result's resize(n) then shrinks without touching the pages (clear() would make it
+      // zero-fill n elements the fill overwrites anyway)
       pool.push_back(std::move(v));
       p.bytes += b;
     }
@@ -1649,6 +1652,21 @@ GroupByResult::~GroupByResult() {
   for (auto &v : counts) put(p.i64, v);
   for (auto &v : hll_card) put(p.i64, v);
   for (auto &v : values) put(p.f64, v);
+}
+
+void group_by_hll_registers(const GroupByResult &r, int fn, uint8_t *registers) {
+  const size_t n = r.raw_keys.size();
+  if (!n) return;
+  if (r.hll_parts.empty()) {
+    memcpy(registers, r.hll[fn].data(), n * 256);
+    return;
+  }
+  for (const HllPart &p : r.hll_parts) {
+    if (!p.num_groups) continue;
+    PINOT_HIP(hipSetDevice(p.device));
+    PINOT_HIP(hipMemcpy(registers + p.group_begin * 256, p.buf->get<uint8_t>() + p.off[fn], p.num_groups * 256,
+                        hipMemcpyDeviceToHost));
+  }
 }
 
 // DictionaryBasedGroupKeyGenerator.getGroupKey (:421-437): column 0 first, values '\t'-joined.
@@ -2074,18 +2092,27 @@ std::unique_ptr<GroupByResult> build_dense_result(Engine &e, const DenseGroups &
       oaggs.back().acc_kind = 4;
       oaggs.back().acc = d.accs[i];
     }
-  // device outputs and their pinned host copy live in grow-only engine buffers (no per-query allocation)
-  const size_t out_b = n * 8 * (2 + n8) + (size_t)n_hll * n * 12 + 64;
+  // device outputs and their pinned host copy live in grow-only engine buffers (no per-query allocation), chunk-major
+  // (GroupOutputLayout): up to 4 chunks, each copied to the host as soon as it is ready while the host fills the
+  // result arrays from the chunks already there
+  GroupOutputLayout L{};
+  const int K = n >= (1u << 18) ? 4 : 1;
+  L.ch = (long long)((n + K - 1) / K + 63) / 64 * 64;
+  L.n8 = n8;
+  L.n_hll = n_hll;
+  L.keys_off = L.ch * 8 * (1 + n8 + n_hll) + L.ch * 4 * n_hll;
+  L.chunk_bytes = (L.keys_off + L.ch * 8 + 255) / 256 * 256;
+  const size_t out_b = (size_t)L.chunk_bytes * K;
   e.group_out.reserve(out_b);
   e.group_host.reserve(out_b);
-  auto *o_cnt = e.group_out.get<unsigned long long>();
-  auto *o_acc = o_cnt + n;
-  auto *o_hs = o_acc + n * n8;
-  auto *o_hz = reinterpret_cast<uint32_t *>(o_hs + (size_t)n_hll * n);
-  auto *o_keys = reinterpret_cast<long long *>(e.group_out.get<uint8_t>() + out_b - 64 - n * 8);
-  launch_group_outputs(d.counts, oaggs.data(), (int)oaggs.size(), keys_dev, (long long)n, o_cnt, o_acc, o_hs, o_hz,
-                       e.stream);
+  L.out = e.group_out.get<uint8_t>();
+  launch_group_outputs(d.counts, oaggs.data(), (int)oaggs.size(), keys_dev, (long long)n, L, e.stream);
   PINOT_HIP(hipGetLastError());
+  for (int c = 0; c < K; c++) {
+    PINOT_HIP(hipMemcpyAsync(e.group_host.get<uint8_t>() + (size_t)c * L.chunk_bytes, L.out + (size_t)c * L.chunk_bytes,
+                             L.chunk_bytes, hipMemcpyDeviceToHost, e.stream));
+    PINOT_HIP(hipEventRecord(e.out_ev[c], e.stream));
+  }
   if (n_hll) {  // registers stay on the device until asked for; buffers are recycled once their result is released
     HllPart part;
     part.device = e.device;
@@ -2112,7 +2139,6 @@ std::unique_ptr<GroupByResult> build_dense_result(Engine &e, const DenseGroups &
     PINOT_HIP(hipGetLastError());
     res->hll_parts.push_back(std::move(part));
   }
-  PINOT_HIP(hipMemcpyAsync(o_keys, keys_dev, n * 8, hipMemcpyDeviceToDevice, e.stream));
   DeviceBuffer ids;
   if (d.hashed) {  // group ordinals are hash slots: fetch each group's global-id tuple
     ids.alloc(n * q.num_group_by * 4 + 16);
@@ -2121,19 +2147,12 @@ std::unique_ptr<GroupByResult> build_dense_result(Engine &e, const DenseGroups &
     res->key_ids.resize(n * q.num_group_by);
     PINOT_HIP(hipMemcpyAsync(res->key_ids.data(), ids.get(), n * q.num_group_by * 4, hipMemcpyDeviceToHost, e.stream));
   }
-  PINOT_HIP(hipMemcpyAsync(e.group_host.get(), e.group_out.get(), out_b, hipMemcpyDeviceToHost, e.stream));
-  wait_stream(e);
-  const uint8_t *host = e.group_host.get<uint8_t>();
-  const auto *hc = reinterpret_cast<const unsigned long long *>(host);
-  const auto *hacc = hc + n;
-  const auto *hhs = hacc + n * n8;
-  const auto *hhz = reinterpret_cast<const uint32_t *>(hhs + (size_t)n_hll * n);
-  const auto *hkeys = reinterpret_cast<const long long *>(host + out_b - 64 - n * 8);
   std::vector<int> hidx(na, -1);  // HLL register-sum row of each (primary) HLL aggregation
   for (int i = 0, h = 0; i < na; i++)
     if (gx.acc_kind[i] == 4) hidx[i] = h++;
-  // result arrays: sized (first touch of fresh pages) and filled in parallel over the host's cores
-  if (n >= kPoolMinElems) {  // recycled arrays of released results: already-mapped pages
+  // result arrays (while the device works): recycled arrays of released results where possible (already-mapped
+  // pages), sized in parallel over the host's cores
+  if (n >= kPoolMinElems) {
     ResultPool &rp = result_pool();
     std::lock_guard<std::mutex> lk(rp.mu);
     res->raw_keys = take_pooled(rp, rp.i64, n);
@@ -2156,43 +2175,53 @@ std::unique_ptr<GroupByResult> build_dense_result(Engine &e, const DenseGroups &
   else
     for (auto &f : sizing) f();
   const int64_t base = d.key_base;
+  for (int c = 0; c < K; c++) {
+  PINOT_HIP(hipEventSynchronize(e.out_ev[c]));
+  const size_t c0 = (size_t)c * L.ch, c1 = std::min<size_t>(n, c0 + L.ch);
+  const uint8_t *cb = e.group_host.get<uint8_t>() + (size_t)c * L.chunk_bytes;
+  const auto *hc = reinterpret_cast<const unsigned long long *>(cb);  // chunk rows, indexed by g - c0
+  const auto *hacc = hc + L.ch;
+  const auto *hhs = hacc + (size_t)L.ch * n8;
+  const auto *hhz = reinterpret_cast<const uint32_t *>(hhs + (size_t)L.ch * n_hll);
+  const auto *hkeys = reinterpret_cast<const long long *>(cb + L.keys_off);
   parallel_tasks(nt, [&](size_t t) {
-    const size_t lo = n * t / nt, hi = n * (t + 1) / nt;
-    if (base == 0) memcpy(res->raw_keys.data() + lo, hkeys + lo, (hi - lo) * 8);
+    const size_t lo = c0 + (c1 - c0) * t / nt, hi = c0 + (c1 - c0) * (t + 1) / nt, m = hi - lo, o = lo - c0;
+    if (base == 0) memcpy(res->raw_keys.data() + lo, hkeys + o, m * 8);
     else
-      for (size_t g = lo; g < hi; g++) res->raw_keys[g] = hkeys[g] + base;
-    memcpy(res->counts[0].data() + lo, hc + lo, (hi - lo) * 8);
+      for (size_t g = 0; g < m; g++) res->raw_keys[lo + g] = hkeys[o + g] + base;
+    memcpy(res->counts[0].data() + lo, hc + o, m * 8);
     for (int i = 0; i < na; i++) {
-      double *vv = res->values[i].data();
+      double *vv = res->values[i].data() + lo;
       const int ak = ga.acc_kind[i];
       const int src = alias[i] >= 0 ? alias[i] : i;  // the accumulator this aggregation reads
-      const unsigned long long *raw = row[src] >= 0 ? hacc + (size_t)row[src] * n : nullptr;
+      const unsigned long long *raw = row[src] >= 0 ? hacc + (size_t)row[src] * L.ch + o : nullptr;
       switch (ak) {
         case 0:
-          for (size_t g = lo; g < hi; g++) vv[g] = (double)(int64_t)raw[g];
+          for (size_t g = 0; g < m; g++) vv[g] = (double)(int64_t)raw[g];
           break;
         case 1:
-          memcpy(vv + lo, raw + lo, (hi - lo) * 8);
+          memcpy(vv, raw, m * 8);
           break;
         case 2:
         case 3:
-          for (size_t g = lo; g < hi; g++) vv[g] = decode_ordered(raw[g]);
+          for (size_t g = 0; g < m; g++) vv[g] = decode_ordered(raw[g]);
           break;
         case 4: {
-          const int h = hidx[src];
-          int64_t *card = res->hll_card[i].data();
-          for (size_t g = lo; g < hi; g++) {
-            card[g] = hll_cardinality_from_sum(hhs[(size_t)h * n + g], hhz[(size_t)h * n + g]);
+          const size_t hr = (size_t)hidx[src] * L.ch + o;
+          int64_t *card = res->hll_card[i].data() + lo;
+          for (size_t g = 0; g < m; g++) {
+            card[g] = hll_cardinality_from_sum(hhs[hr + g], hhz[hr + g]);
             vv[g] = (double)card[g];
           }
           break;
         }
         default:
-          for (size_t g = lo; g < hi; g++) vv[g] = (double)hc[g];
+          for (size_t g = 0; g < m; g++) vv[g] = (double)hc[o + g];
           break;
       }
     }
   });
+  }
   return res;
 }
 

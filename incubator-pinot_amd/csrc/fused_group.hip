@@ -303,7 +303,7 @@ __device__ __forceinline__ void group_sink(const GroupArgs &a, uint32_t *plds, c
     // 64-B piece each) to the block's next run positions, then reopens them. A record that finds its bucket full
     // (only when one batch brings more than kBucketRecs records of a partition) goes straight to its run slot.
     uint32_t *cur = plds, *cnt = plds + a.P, *wrt = plds + 2 * a.P;
-    unsigned long long *bkt = reinterpret_cast<unsigned long long *>(plds + ((3 * a.P + 1) & ~1));
+    unsigned long long *bkt = reinterpret_cast<unsigned long long *>(plds + ((3 * a.P + 3) & ~3));
     uint32_t p[U], pos[U];
     unsigned long long r[U];
 #pragma unroll
@@ -645,10 +645,12 @@ __device__ __forceinline__ void decode_column_lq(const uint8_t *fwd, int bits, i
 // GB_EMIT2 sink of a lane's 16 records, every stage batched over them (one LDS round trip per stage instead of
 // one per record): claim a slot of the partition's LDS bucket (count), store the record with its valid bit (bit
 // 63; records use <= 63 bits), and the record that claimed the last slot flushes the bucket once the quarter's
-// stores are issued. A flusher waits for its bucket's slots to turn valid (their writers claimed them before it
-// and store with no wait in between, so the wait ends), then eight lanes move the bucket out as one 64-B piece
-// to the block's run of the partition, clear the slots and reopen the bucket (count 0: the clears precede it in
-// this wave's LDS order). A record that finds its bucket full goes straight to its run slot.
+// stores are issued. Per round every flushing lane takes one bucket: it claims the bucket's run position, lists
+// (partition, position) in the wave's LDS flush list at its rank among the flushing lanes (mbcnt), and the wave
+// then moves the listed buckets eight lanes per bucket (one coalesced 64-B piece each), waiting for a slot to turn
+// valid where its writer has not stored yet (writers claim before the flusher and store with no wait in between,
+// so the wait ends), clears the slots and reopens the buckets (count 0: the clears precede it in this wave's LDS
+// order). A record that finds its bucket full goes straight to its run slot.
 constexpr unsigned long long kRecValid = 1ull << 63;
 
 __device__ __forceinline__ void emit2_sink16(const GroupArgs &a, uint32_t *plds, uint32_t act,
@@ -657,7 +659,8 @@ __device__ __forceinline__ void emit2_sink16(const GroupArgs &a, uint32_t *plds,
   if (a.reserved2 == 4) return;  // debug.emit=4 (timing only, wrong results): reads + decode, no sink
   const bool st = a.reserved2 != 3;  // debug.emit=3: bucket logic without the global stores
   uint32_t *cur = plds, *cnt = plds + a.P;
-  unsigned long long *bkt = reinterpret_cast<unsigned long long *>(plds + ((3 * a.P + 1) & ~1));
+  unsigned long long *bkt = reinterpret_cast<unsigned long long *>(plds + ((3 * a.P + 3) & ~3));
+  unsigned long long *flist = bkt + (size_t)a.P * kBucketRecs + (threadIdx.x >> 6) * 64;
   const uint32_t lmask = (1u << a.shift) - 1u;
   uint32_t pos[16];
 #pragma unroll
@@ -688,23 +691,27 @@ __device__ __forceinline__ void emit2_sink16(const GroupArgs &a, uint32_t *plds,
   while (true) {
     const uint64_t fm = __ballot(flush != 0);
     if (!fm) break;  // uniform
-    // this round's bucket per flushing lane: its lowest pending record
-    const int j = flush ? __builtin_ctz(flush) : 0;
-    uint32_t pk = 0;
+    uint32_t p = 0;
+    if (flush) {
+      const int j = __builtin_ctz(flush);
+      uint32_t pk = 0;
 #pragma unroll
-    for (int t = 0; t < 16; t++) pk = t == j ? key[t] : pk;
-    const uint32_t p = pk >> a.shift;
-    const uint32_t dst = flush ? atomicAdd(&cur[p], (uint32_t)kBucketRecs) : 0u;
+      for (int t = 0; t < 16; t++) pk = t == j ? key[t] : pk;
+      p = pk >> a.shift;
+      const uint32_t dst = atomicAdd(&cur[p], (uint32_t)kBucketRecs);
+      const int f = __builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u));
+      flist[f] = ((unsigned long long)dst << 32) | p;
+    }
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);  // list writes before the list reads (wave LDS order)
     const int nf = __popcll(fm);
     for (int f0 = 0; f0 < nf; f0 += 64 / kBucketRecs) {  // uniform: 8 buckets per wave instruction
-      const int f = min(f0 + lane / kBucketRecs, nf - 1), i = lane % kBucketRecs;
-      const int src = select_bit(fm, f);
-      const uint32_t pf = (uint32_t)__shfl((int)p, src, 64), df = (uint32_t)__shfl((int)dst, src, 64);
-      if (f0 + lane / kBucketRecs < nf) {
-        unsigned long long *slot = &bkt[pf * kBucketRecs + i];
+      const int f = f0 + lane / kBucketRecs, i = lane % kBucketRecs;
+      if (f < nf) {
+        const unsigned long long e = flist[f];
+        unsigned long long *slot = &bkt[(uint32_t)e * kBucketRecs + i];
         unsigned long long v = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         while (!(v & kRecValid)) v = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (st) a.emit[df + i] = v & ~kRecValid;
+        if (st) a.emit[(uint32_t)(e >> 32) + i] = v & ~kRecValid;
         __hip_atomic_store(slot, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     }
@@ -771,11 +778,60 @@ __device__ __forceinline__ void decode_raw_lq(const uint32_t (&R)[12], int bits,
 #undef PINOT_RQ
 }
 
+// The columns a quarter reads (group columns, then GB_EMIT's aggregated fields): per segment, uniform. The COUNT
+// pass (128 VGPRs at 16 waves) keeps raw registers for at most kLqCountCols group columns (the host picks the
+// lane-owns-word path for more).
+constexpr int kLqCountCols = 2;
+struct LqCols {
+  const uint8_t *fwd[kGroupPfCols];
+  const int32_t *remap[kGroupPfCols];
+  uint32_t stride[kGroupPfCols];
+  int bits[kGroupPfCols], fsh[kGroupPfCols];  // bits 0 = unused slot; fsh -1 = a group column (key fold)
+};
+
 template <int MODE>
-__device__ __forceinline__ void group_quarter_lq(const GroupArgs &a, const GroupSegment &sg, int64_t qi, uint32_t mq,
-                                                 int lane, uint32_t *plds) {
-  constexpr int U = kGroupPfUnroll, C = kGroupPfCols;
+__device__ __forceinline__ LqCols lq_cols(const GroupArgs &a, const GroupSegment &sg) {
   const int nc = MODE == GB_COUNT ? a.n_gcols : a.pf_nc;
+  LqCols k;
+#pragma unroll
+  for (int c = 0; c < kGroupPfCols; c++) {
+    k.fwd[c] = nullptr;
+    k.remap[c] = nullptr;
+    k.stride[c] = 0;
+    k.bits[c] = 0;
+    k.fsh[c] = -1;
+    if (c < nc) {
+      if (c < a.n_gcols) {
+        const GroupColDev gc = load_const(a.gcols + sg.first_gcol + c);
+        k.fwd[c] = gc.fwd;
+        k.remap[c] = gc.remap;
+        k.stride[c] = (uint32_t)gc.stride;
+        k.bits[c] = gc.bits;
+      } else if (MODE != GB_COUNT) {
+        const int ai = c == 1 ? a.pf_agg[1] : c == 2 ? a.pf_agg[2] : a.pf_agg[3];
+        const GroupAggDev ag = load_const(a.aggs + sg.first_agg + ai);
+        k.fwd[c] = ag.fwd;
+        k.bits[c] = ag.bits;
+        k.fsh[c] = ag.field_shift;
+      }
+    }
+  }
+  return k;
+}
+
+template <int NC>
+__device__ __forceinline__ void lq_load(const LqCols &k, int64_t qi, uint32_t (&R)[NC][12]) {
+#pragma unroll
+  for (int c = 0; c < NC; c++)
+    if (k.bits[c]) load_raw_lq(k.fwd[c], k.bits[c], qi, R[c]);
+}
+
+// Decode a quarter's loaded columns into keys / records, then the sink.
+template <int MODE, int NC>
+__device__ __forceinline__ void lq_process(const GroupArgs &a, const GroupSegment &sg, const LqCols &k,
+                                           const uint32_t (&R)[NC][12], int64_t qi, uint32_t mq, int lane,
+                                           uint32_t *plds) {
+  constexpr int U = kGroupPfUnroll;
   uint32_t key[16];
   unsigned long long rec[16];
 #pragma unroll
@@ -783,54 +839,22 @@ __device__ __forceinline__ void group_quarter_lq(const GroupArgs &a, const Group
     key[j] = 0;
     rec[j] = 0;
   }
-  // column descriptors (uniform), then every column's raw loads, then the decodes
-  const uint8_t *fwd[C];
-  const int32_t *remap[C];
-  uint32_t stride[C];
-  int bits[C], fsh[C];
 #pragma unroll
-  for (int c = 0; c < C; c++) {
-    fwd[c] = nullptr;
-    remap[c] = nullptr;
-    stride[c] = 0;
-    bits[c] = 0;
-    fsh[c] = -1;  // -1: a group column (key fold)
-    if (c < nc) {
-      if (c < a.n_gcols) {
-        const GroupColDev gc = load_const(a.gcols + sg.first_gcol + c);
-        fwd[c] = gc.fwd;
-        remap[c] = gc.remap;
-        stride[c] = (uint32_t)gc.stride;
-        bits[c] = gc.bits;
-      } else if (MODE != GB_COUNT) {
-        const int ai = c == 1 ? a.pf_agg[1] : c == 2 ? a.pf_agg[2] : a.pf_agg[3];
-        const GroupAggDev ag = load_const(a.aggs + sg.first_agg + ai);
-        fwd[c] = ag.fwd;
-        bits[c] = ag.bits;
-        fsh[c] = ag.field_shift;
-      }
-    }
-  }
-  uint32_t R[C][12];
-#pragma unroll
-  for (int c = 0; c < C; c++)
-    if (bits[c]) load_raw_lq(fwd[c], bits[c], qi, R[c]);
-#pragma unroll
-  for (int c = 0; c < C; c++) {
-    if (!bits[c]) continue;
+  for (int c = 0; c < NC; c++) {
+    if (!k.bits[c]) continue;
     uint32_t id[16];
-    decode_raw_lq(R[c], bits[c], qi, id);
-    if (fsh[c] < 0) {
-      if (remap[c]) {
+    decode_raw_lq(R[c], k.bits[c], qi, id);
+    if (k.fsh[c] < 0) {
+      if (k.remap[c]) {
 #pragma unroll
-        for (int j = 0; j < 16; j++) key[j] += (uint32_t)gload<int32_t>(remap[c] + id[j]) * stride[c];
+        for (int j = 0; j < 16; j++) key[j] += (uint32_t)gload<int32_t>(k.remap[c] + id[j]) * k.stride[c];
       } else {
 #pragma unroll
-        for (int j = 0; j < 16; j++) key[j] += id[j] * stride[c];
+        for (int j = 0; j < 16; j++) key[j] += id[j] * k.stride[c];
       }
-    } else {
+    } else if constexpr (MODE != GB_COUNT) {
 #pragma unroll
-      for (int j = 0; j < 16; j++) rec[j] |= (unsigned long long)id[j] << fsh[c];
+      for (int j = 0; j < 16; j++) rec[j] |= (unsigned long long)id[j] << k.fsh[c];
     }
   }
   if constexpr (MODE == GB_EMIT2) {
@@ -846,31 +870,61 @@ __device__ __forceinline__ void group_quarter_lq(const GroupArgs &a, const Group
 #pragma unroll
   for (int j0 = 0; j0 < 16; j0 += U) {
     bool act[U];
-    unsigned long long k[U], r[U];
+    unsigned long long kk[U], r[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
       act[u] = (mq >> (j0 + u)) & 1u;
-      k[u] = key[j0 + u];
+      kk[u] = key[j0 + u];
       r[u] = rec[j0 + u];
     }
     if (sg.admitted) {
 #pragma unroll
-      for (int u = 0; u < U; u++) act[u] = act[u] && ((sg.admitted[k[u] >> 5] >> (k[u] & 31)) & 1u);
+      for (int u = 0; u < U; u++) act[u] = act[u] && ((gload<uint32_t>(sg.admitted + (kk[u] >> 5)) >> (kk[u] & 31)) & 1u);
     }
-    group_sink<MODE, U>(a, plds, act, k, r, lane);
+    group_sink<MODE, U>(a, plds, act, kk, r, lane);
   }
 }
 
 template <int MODE>
 __device__ __forceinline__ void group_chunk_lq(const GroupArgs &a, const GroupSegment &sg, int64_t ch, uint64_t mask,
                                                int lane, uint32_t *plds) {
+  const int64_t q0 = ch * 256 + lane;
+  if constexpr (MODE == GB_EMIT2) {
+    const LqCols k = lq_cols<MODE>(a, sg);
+    uint32_t mq[4];
+    bool any[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int src = 16 * q + (lane >> 2);
+      const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)mask, src, 64);
+      const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(mask >> 32), src, 64);
+      mq[q] = (((lane & 2) ? hi : lo) >> (16 * (lane & 1))) & 0xFFFFu;
+      any[q] = __any(mq[q] != 0);
+    }
+    // two register sets: quarter q + 1's loads are in flight while quarter q decodes and sinks
+    uint32_t R0[kGroupPfCols][12], R1[kGroupPfCols][12];
+    if (any[0]) lq_load<kGroupPfCols>(k, q0, R0);
+    if (any[1]) lq_load<kGroupPfCols>(k, q0 + 64, R1);
+    if (any[0]) lq_process<MODE, kGroupPfCols>(a, sg, k, R0, q0, mq[0], lane, plds);
+    if (any[2]) lq_load<kGroupPfCols>(k, q0 + 128, R0);
+    if (any[1]) lq_process<MODE, kGroupPfCols>(a, sg, k, R1, q0 + 64, mq[1], lane, plds);
+    if (any[3]) lq_load<kGroupPfCols>(k, q0 + 192, R1);
+    if (any[2]) lq_process<MODE, kGroupPfCols>(a, sg, k, R0, q0 + 128, mq[2], lane, plds);
+    if (any[3]) lq_process<MODE, kGroupPfCols>(a, sg, k, R1, q0 + 192, mq[3], lane, plds);
+  } else {
 #pragma unroll 1
-  for (int q = 0; q < 4; q++) {
-    const int src = 16 * q + (lane >> 2);
-    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)mask, src, 64);
-    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(mask >> 32), src, 64);
-    const uint32_t mq = (((lane & 2) ? hi : lo) >> (16 * (lane & 1))) & 0xFFFFu;
-    if (__any(mq != 0)) group_quarter_lq<MODE>(a, sg, ch * 256 + 64 * q + lane, mq, lane, plds);
+    for (int q = 0; q < 4; q++) {
+      const int src = 16 * q + (lane >> 2);
+      const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)mask, src, 64);
+      const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(mask >> 32), src, 64);
+      const uint32_t m = (((lane & 2) ? hi : lo) >> (16 * (lane & 1))) & 0xFFFFu;
+      if (!__any(m != 0)) continue;
+      const LqCols k = lq_cols<MODE>(a, sg);
+      constexpr int NC = MODE == GB_COUNT ? kLqCountCols : kGroupPfCols;  // COUNT reads the group columns only
+      uint32_t R[NC][12];
+      lq_load<NC>(k, q0 + 64 * q, R);
+      lq_process<MODE, NC>(a, sg, k, R, q0 + 64 * q, m, lane, plds);
+    }
   }
 }
 
@@ -1000,7 +1054,7 @@ __global__ __launch_bounds__(BLK) void k_group_query(GroupArgs a) {
     atomicAdd(a.matched + g, matched);
   if constexpr (MODE == GB_EMIT2) {  // the partially filled buckets, 8 lanes per bucket
     __syncthreads();
-    const unsigned long long *bkt = reinterpret_cast<const unsigned long long *>(plds + ((3 * a.P + 1) & ~1));
+    const unsigned long long *bkt = reinterpret_cast<const unsigned long long *>(plds + ((3 * a.P + 3) & ~3));
     const int i = tid % kBucketRecs;
     for (int p = tid / kBucketRecs; p < a.P; p += BLK / kBucketRecs)
       if ((uint32_t)i < plds[a.P + p]) a.emit[plds[p] + i] = bkt[p * kBucketRecs + i] & ~kRecValid;
@@ -1027,7 +1081,7 @@ static void with_group_kernel(const GroupArgs &a, V &&v) {
     case GB_GLOBAL: v(&k_group_query<GB_GLOBAL, 0, kGroupBlock>, kGroupBlock); break;
     case GB_LDS: v(&k_group_query<GB_LDS, 0, kGroupBlock>, kGroupBlock); break;
     case GB_COUNT:
-      if (lh) v(&k_group_query<GB_COUNT, 3, kGroupBlock>, kGroupBlock);
+      if (lh && a.n_gcols <= kLqCountCols) v(&k_group_query<GB_COUNT, 3, kGroupBlock>, kGroupBlock);
       else if (lw) v(&k_group_query<GB_COUNT, 2, kGroupBlock>, kGroupBlock);
       else if (a.pf_nc > 0) v(&k_group_query<GB_COUNT, 1, kGroupBlock>, kGroupBlock);
       else v(&k_group_query<GB_COUNT, 0, kGroupBlock>, kGroupBlock);
@@ -1054,7 +1108,8 @@ size_t group_query_lds_bytes(const GroupArgs &a) {
   size_t acc = 0;
   if (a.mode == GB_LDS) acc = (size_t)a.lds_acc_bytes;
   if (a.mode == GB_COUNT || a.mode == GB_EMIT) acc = (size_t)a.P * 4;
-  if (a.mode == GB_EMIT2) acc = (size_t)((3 * a.P + 1) & ~1) * 4 + (size_t)a.P * 8 * kBucketRecs;
+  if (a.mode == GB_EMIT2)  // + the per-wave flush lists of the lane-owns-quarter sink
+    acc = (size_t)((3 * a.P + 3) & ~3) * 4 + (size_t)a.P * 8 * kBucketRecs + (size_t)(group_block_threads(a) / 64) * 64 * 8;
   return (size_t)(group_block_threads(a) / 64) * a.stage_bytes + acc;
 }
 

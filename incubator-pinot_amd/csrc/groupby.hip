@@ -232,38 +232,45 @@ struct OutputAggs {
   int n;
 };
 
+// Chunk-major per-group outputs (GroupOutputLayout): group i lives in chunk i / ch at position i % ch, each chunk
+// holding its counts, 8-byte accumulator rows, HLL register sums, HLL zero counts and raw keys back to back, so a
+// chunk leaves in one D2H copy while the host fills the previous one.
 __global__ void k_group_outputs(const unsigned long long *__restrict__ counts, OutputAggs oa,
-                                const long long *__restrict__ keys, long long n, unsigned long long *out_counts,
-                                unsigned long long *out_acc, unsigned long long *out_hll_sum, uint32_t *out_hll_zeros) {
+                                const long long *__restrict__ keys, long long n, GroupOutputLayout L) {
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
     const long long k = keys[i];
-    out_counts[i] = counts[k];
-    int h = 0;
+    const long long c = i / L.ch, l = i - c * L.ch;
+    uint8_t *base = L.out + c * L.chunk_bytes;
+    unsigned long long *c8 = reinterpret_cast<unsigned long long *>(base);
+    c8[l] = counts[k];
+    int h = 0, r = 0;
     for (int g = 0; g < oa.n; g++) {
       const GroupAggDev &ag = oa.aggs[g];
       if (ag.acc_kind == 4) {
-        const u32x4 *r = reinterpret_cast<const u32x4 *>(static_cast<const uint8_t *>(ag.acc) + k * 256);
+        const u32x4 *rg = reinterpret_cast<const u32x4 *>(static_cast<const uint8_t *>(ag.acc) + k * 256);
         unsigned long long s = 0;
         uint32_t z = 0;
         for (int q = 0; q < 16; q++) {
-          const u32x4 v = r[q];
+          const u32x4 v = rg[q];
           const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-          for (int c = 0; c < 4; c++)
+          for (int cc = 0; cc < 4; cc++)
 #pragma unroll
             for (int bb = 0; bb < 4; bb++) {
-              const uint32_t reg = (w[c] >> (8 * bb)) & 0xFFu;
+              const uint32_t reg = (w[cc] >> (8 * bb)) & 0xFFu;
               s += 1ull << (32 - reg);
               z += reg == 0;
             }
         }
-        out_hll_sum[(long long)h * n + i] = s;
-        out_hll_zeros[(long long)h * n + i] = z;
+        c8[(1 + L.n8 + h) * L.ch + l] = s;
+        reinterpret_cast<uint32_t *>(c8 + (1 + L.n8 + L.n_hll) * L.ch)[h * L.ch + l] = z;
         h++;
       } else if (ag.acc_kind != 5) {
-        out_acc[(long long)g * n + i] = static_cast<const unsigned long long *>(ag.acc)[k];
+        c8[(1 + r) * L.ch + l] = static_cast<const unsigned long long *>(ag.acc)[k];
+        r++;
       }
     }
+    reinterpret_cast<long long *>(base + L.keys_off)[l] = k;
   }
 }
 
@@ -506,15 +513,13 @@ void launch_compact_keys_ordered(long long G, const unsigned long long *counts, 
 }
 
 void launch_group_outputs(const unsigned long long *counts, const GroupAggDev *aggs_host, int n_aggs, const long long *keys,
-                          long long n, unsigned long long *out_counts, unsigned long long *out_acc,
-                          unsigned long long *out_hll_sum, uint32_t *out_hll_zeros, hipStream_t stream) {
+                          long long n, const GroupOutputLayout &L, hipStream_t stream) {
   if (n <= 0) return;
   OutputAggs oa{};
   oa.n = n_aggs;
   for (int g = 0; g < n_aggs && g < kMaxGroupAggs; g++) oa.aggs[g] = aggs_host[g];
   const int grid = (int)std::min<long long>((n + 255) / 256, 4096);
-  hipLaunchKernelGGL(k_group_outputs, dim3(grid), dim3(256), 0, stream, counts, oa, keys, n, out_counts, out_acc,
-                     out_hll_sum, out_hll_zeros);
+  hipLaunchKernelGGL(k_group_outputs, dim3(grid), dim3(256), 0, stream, counts, oa, keys, n, L);
 }
 
 }  // namespace pinot

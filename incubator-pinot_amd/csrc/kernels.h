@@ -203,7 +203,7 @@ int scan_query_blocks_per_cu(int stage_bytes, bool gathers, bool pipelined);
 //              whole into the FINAL partition layout (offsets from GB_COUNT's histogram): no split pass
 enum GroupMode : int32_t { GB_GLOBAL = 0, GB_LDS = 1, GB_COUNT = 2, GB_EMIT = 3, GB_VERIFY = 4, GB_FIRST = 5, GB_EMIT2 = 6 };
 constexpr int kBucketRecs = 8;                                   // 64-B bucket flushes
-constexpr int kBucketMaxPartitions = 2040;                       // P x (3 x 4 + 8 x 8) B of LDS per block <= 155 KB
+constexpr int kBucketMaxPartitions = 2040;  // P x (3 x 4 + 8 x 8) B + 4 KiB of flush lists per block <= 160 KiB
 // accumulator kinds (acc_kind): 0 int64 sum, 1 double sum, 2 ordered-u64 min, 3 ordered-u64 max,
 // 4 HLL registers (u8 [G][256]), 5 none (COUNT / AVG count share `counts`)
 constexpr int kMaxGroupAggs = 8;
@@ -318,11 +318,17 @@ void launch_narrow_u32(const uint32_t *in, long long n, uint8_t *out, hipStream_
 size_t compact_keys_scratch_bytes(long long G);
 void launch_compact_keys_ordered(long long G, const unsigned long long *counts, long long *keys_out,
                                  unsigned long long *n_out, void *scratch, size_t scratch_bytes, hipStream_t stream);
-// out_acc[a * n + i] = 8-byte accumulator of group i; HLL (acc_kind 4): out_hll_sum[h * n + i] = Σ 2^(32 - reg)
-// (exact), out_hll_zeros[h * n + i] = #zero registers.
+// Per-group outputs, chunk-major: chunk c (groups [c * ch, (c + 1) * ch)) at out + c * chunk_bytes holds counts u64
+// [ch], the 8-byte accumulator rows u64 [n8][ch] (aggregations of kinds 0-3 in order), the HLL register sums
+// Σ 2^(32 - reg) u64 [n_hll][ch] (exact), the zero-register counts u32 [n_hll][ch], then the raw keys i64 [ch] at
+// keys_off.
+struct GroupOutputLayout {
+  uint8_t *out;
+  long long ch, chunk_bytes, keys_off;
+  int32_t n8, n_hll;
+};
 void launch_group_outputs(const unsigned long long *counts, const GroupAggDev *aggs_host, int n_aggs, const long long *keys,
-                          long long n, unsigned long long *out_counts, unsigned long long *out_acc,
-                          unsigned long long *out_hll_sum, uint32_t *out_hll_zeros, hipStream_t stream);
+                          long long n, const GroupOutputLayout &L, hipStream_t stream);
 // num.groups.limit admission (DictionaryBasedGroupKeyGenerator IntMapBasedHolder.getGroupId, first appearance):
 // segment s admits the upper[s] keys with the smallest first_doc[s][k] (first_doc values of distinct keys are
 // distinct docs). bitmaps[s] (words u32 each) gets bit k for every admitted key; upper[s] >= G admits every present

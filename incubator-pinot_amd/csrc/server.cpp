@@ -229,15 +229,16 @@ void server_aggregate(ServerImpl &s, const std::vector<SegmentRef> &refs, const 
     tot.num_entries_scanned_post_filter += x.num_entries_scanned_post_filter;
     tot.num_total_raw_docs += x.num_total_raw_docs;
     tot.num_segments_processed += x.num_segments_processed;
+    tot.num_segments_matched += x.num_segments_matched;
     tot.device_ms = std::max(tot.device_ms, x.device_ms);
   }
   if (s.multi_process) {
     // every rank all-reduces: {ok} agreement first, then per function
-    //   int64 SUM [count, exact_sum, non-exact flag] ... + the 5 stats counters, f64 SUM non-exact sums, f64 MIN of
+    //   int64 SUM [count, exact_sum, non-exact flag] ... + the 6 stats counters, f64 SUM non-exact sums, f64 MIN of
     //   MIN values, f64 MAX of MAX values, u8 MAX HLL registers
     agree_or_rethrow(s, {local_err ? 0 : 1, (int64_t)na}, {true, true}, "aggregation", local_err);
     Engine &e = *s.engines[0];
-    const size_t ni = 3 * na + 5, nd = na;
+    const size_t ni = 3 * na + 6, nd = na;
     s.small[0].reserve(8 * (ni + 3 * nd) + 256 * na + 64);
     auto *di = s.small[0].get<int64_t>();
     auto *dsum = reinterpret_cast<double *>(di + ni);
@@ -255,9 +256,9 @@ void server_aggregate(ServerImpl &s, const std::vector<SegmentRef> &refs, const 
       if (q.aggregations[a].function == PINOT_AGG_MAX) hmx[a] = out[a].value;
       memcpy(&hr[256 * a], out[a].hll_registers, 256);
     }
-    const int64_t sv[5] = {tot.num_docs_scanned, tot.num_entries_scanned_in_filter, tot.num_entries_scanned_post_filter,
-                           tot.num_total_raw_docs, tot.num_segments_processed};
-    for (int k = 0; k < 5; k++) hi[3 * na + k] = sv[k];
+    const int64_t sv[6] = {tot.num_docs_scanned, tot.num_entries_scanned_in_filter, tot.num_entries_scanned_post_filter,
+                           tot.num_total_raw_docs, tot.num_segments_processed, tot.num_segments_matched};
+    for (int k = 0; k < 6; k++) hi[3 * na + k] = sv[k];
     PINOT_HIP(hipMemcpyAsync(di, hi.data(), ni * 8, hipMemcpyHostToDevice, e.stream));
     PINOT_HIP(hipMemcpyAsync(dsum, hs.data(), nd * 8, hipMemcpyHostToDevice, e.stream));
     PINOT_HIP(hipMemcpyAsync(dmin, hmn.data(), nd * 8, hipMemcpyHostToDevice, e.stream));
@@ -299,6 +300,7 @@ void server_aggregate(ServerImpl &s, const std::vector<SegmentRef> &refs, const 
     tot.num_entries_scanned_post_filter = hi[3 * na + 2];
     tot.num_total_raw_docs = hi[3 * na + 3];
     tot.num_segments_processed = hi[3 * na + 4];
+    tot.num_segments_matched = hi[3 * na + 5];
   }
   if (stats) *stats = tot;
 }
@@ -443,6 +445,7 @@ std::unique_ptr<GroupByResult> server_group_by(ServerImpl &s, const std::vector<
     tot.num_entries_scanned_post_filter += x.num_entries_scanned_post_filter;
     tot.num_total_raw_docs += x.num_total_raw_docs;
     tot.num_segments_processed += x.num_segments_processed;
+    tot.num_segments_matched += x.num_segments_matched;
     tot.device_ms = std::max(tot.device_ms, x.device_ms);
   }
   if (stats) *stats = tot;

@@ -26,7 +26,7 @@ EXPORTED_SYMBOLS = [
     "pinot_gpu_segment_device_bytes", "pinot_gpu_filter", "pinot_gpu_aggregate", "pinot_gpu_group_by",
     "pinot_groupby_num_groups", "pinot_groupby_num_columns", "pinot_groupby_key", "pinot_groupby_values",
     "pinot_groupby_hll", "pinot_groupby_raw_keys", "pinot_groupby_export_keys", "pinot_groupby_trim",
-    "pinot_groupby_free",
+    "pinot_groupby_free", "pinot_datatable_aggregation", "pinot_datatable_group_by",
     "pinot_gpu_group_by_layout", "pinot_gpu_group_by_partial", "pinot_gpu_group_by_finalize",
     "pinot_gpu_segment_register_synthetic", "pinot_gpu_segment_register_synthetic_ex", "pinot_gpu_synchronize",
     "pinot_gpu_last_kernel_ms",
@@ -77,7 +77,11 @@ class ExecStats(C.Structure):
     _fields_ = [("num_docs_scanned", C.c_int64), ("num_entries_scanned_in_filter", C.c_int64),
                 ("num_entries_scanned_post_filter", C.c_int64), ("num_total_raw_docs", C.c_int64),
                 ("num_segments_processed", C.c_int64), ("device_ms", C.c_double),
-                ("host_ms", C.c_double)]
+                ("host_ms", C.c_double), ("num_segments_matched", C.c_int64)]
+
+
+class DataTableServer(C.Structure):
+    _fields_ = [("num_segments_queried", C.c_int64), ("time_used_ms", C.c_int64), ("request_id", C.c_int64)]
 
 
 class AggResult(C.Structure):
@@ -158,6 +162,10 @@ def load(path=None):
         "pinot_groupby_raw_keys": (i32, [P, P]),
         "pinot_groupby_export_keys": (i32, [P, P, u64, P, C.POINTER(u64)]),
         "pinot_groupby_trim": (i32, [P, i32, i32, P, C.POINTER(i64)]),
+        "pinot_datatable_aggregation": (i32, [C.POINTER(Query), P, C.POINTER(ExecStats), C.POINTER(DataTableServer),
+                                              P, u64, C.POINTER(u64)]),
+        "pinot_datatable_group_by": (i32, [C.POINTER(Query), P, P, P, C.POINTER(ExecStats),
+                                           C.POINTER(DataTableServer), C.POINTER(P), C.POINTER(u64)]),
         "pinot_groupby_free": (None, [P]),
         "pinot_gpu_group_by_layout": (i32, [P, C.POINTER(i64), i32, C.POINTER(Query), C.POINTER(PartialLayout)]),
         "pinot_gpu_group_by_partial": (i32, [P, C.POINTER(i64), i32, C.POINTER(Query), P, C.POINTER(P),

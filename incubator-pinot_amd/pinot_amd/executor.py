@@ -55,6 +55,7 @@ class ExecutionStatistics:
     num_segments_processed: int = 0
     device_ms: float = 0.0
     host_ms: float = 0.0
+    num_segments_matched: int = 0
 
 
 class GpuSegment:
@@ -319,6 +320,20 @@ class GroupByResult:
                                          cards.ctypes.data_as(C.c_void_p)))
         return regs[:n], cards[:n]
 
+    def data_table(self, marshal, stats, trim_top_n=None, server=None):
+        """DataTable bytes of this result (pinot_datatable_group_by), each function's map trimmed to its own top
+        groups (AggregationGroupByTrimmingService) when trim_top_n is given."""
+        na = len(self.query["aggregations"])
+        groups = nums = None
+        if trim_top_n is not None:
+            kept = [self.trimmed_groups(trim_top_n, i) for i in range(na)]
+            groups = (C.c_void_p * na)(*[k.ctypes.data_as(C.c_void_p) for k in kept])
+            nums = (C.c_int64 * na)(*[k.shape[0] for k in kept])
+        data, size = C.c_void_p(), C.c_uint64()
+        check(self.lib.pinot_datatable_group_by(C.byref(marshal.q), self.ptr, groups, nums, C.byref(stats), server,
+                                                C.byref(data), C.byref(size)))
+        return C.string_at(data, size.value) if size.value else b""
+
     def to_map(self, trim_top_n=None):
         """{string_key: [intermediate result per function]} (the CombineGroupByOperator result map).
 
@@ -437,10 +452,7 @@ class ServerExecutor:
             check(lib.pinot_gpu_server_aggregate(self.server.ptr, refs, len(segments), C.byref(m.q), out,
                                                  C.byref(stats)))
             res = [_agg_value(a["function"].upper(), out[i]) for i, a in enumerate(query["aggregations"])]
-        st = ExecutionStatistics(stats.num_docs_scanned, stats.num_entries_scanned_in_filter,
-                                 stats.num_entries_scanned_post_filter, stats.num_total_raw_docs,
-                                 stats.num_segments_processed, stats.device_ms, stats.host_ms)
-        return res, st
+        return res, _stats(stats)
 
     def prepare(self, query):
         if isinstance(query, str):
@@ -499,10 +511,37 @@ class ServerQueryExecutor:
             check(lib.pinot_gpu_aggregate(self.engine.ptr, handles, len(segments), C.byref(m.q), out,
                                           C.byref(stats)))
             res = [_agg_value(a["function"].upper(), out[i]) for i, a in enumerate(query["aggregations"])]
-        st = ExecutionStatistics(stats.num_docs_scanned, stats.num_entries_scanned_in_filter,
-                                 stats.num_entries_scanned_post_filter, stats.num_total_raw_docs,
-                                 stats.num_segments_processed, stats.device_ms, stats.host_ms)
-        return res, st
+        return res, _stats(stats)
+
+    def process_query_datatable(self, query, segments, trim=True, server=None):
+        """`processQuery` as the server answers the broker: the combined result as DataTable bytes
+        (IntermediateResultsBlock.getDataTable -> DataTableImplV2.toBytes, built natively by pinot_datatable_*).
+        Group-by maps are trimmed per function like CombineGroupByOperator when `trim`; `server` =
+        (numSegmentsQueried, timeUsedMs, requestId or -1) adds the server's own metadata keys."""
+        if isinstance(query, PreparedQuery):
+            query, m = query.query, query.marshal
+        else:
+            if isinstance(query, str):
+                query = compile_pql(query)
+            m = QueryMarshal(query, self.num_groups_limit, self.max_init, self.timeout_ms)
+        lib = self.engine.lib
+        handles = _segment_handles(segments)
+        stats = _lib.ExecStats()
+        srv = C.byref(_lib.DataTableServer(*server)) if server else None
+        if query.get("group_by"):
+            out = C.c_void_p()
+            check(lib.pinot_gpu_group_by(self.engine.ptr, handles, len(segments), C.byref(m.q), C.byref(out),
+                                         C.byref(stats)))
+            res = GroupByResult(lib, out, query)
+            return res.data_table(m, stats, query["group_by"].get("top_n", 10) if trim else None, srv), _stats(stats)
+        n = len(query["aggregations"])
+        out = (_lib.AggResult * n)()
+        check(lib.pinot_gpu_aggregate(self.engine.ptr, handles, len(segments), C.byref(m.q), out, C.byref(stats)))
+        need = C.c_uint64()
+        check(lib.pinot_datatable_aggregation(C.byref(m.q), out, C.byref(stats), srv, None, 0, C.byref(need)))
+        buf = C.create_string_buffer(max(need.value, 1))
+        check(lib.pinot_datatable_aggregation(C.byref(m.q), out, C.byref(stats), srv, buf, need.value, C.byref(need)))
+        return buf.raw[:need.value], _stats(stats)
 
     def group_by_result(self, query, segments):
         """Raw device group-by result object (no trimming)."""
@@ -514,6 +553,12 @@ class ServerQueryExecutor:
         check(self.engine.lib.pinot_gpu_group_by(self.engine.ptr, _segment_handles(segments), len(segments),
                                                  C.byref(m.q), C.byref(out), C.byref(stats)))
         return GroupByResult(self.engine.lib, out, query), stats
+
+
+def _stats(s):
+    return ExecutionStatistics(s.num_docs_scanned, s.num_entries_scanned_in_filter, s.num_entries_scanned_post_filter,
+                               s.num_total_raw_docs, s.num_segments_processed, s.device_ms, s.host_ms,
+                               s.num_segments_matched)
 
 
 def _agg_value(f, r):

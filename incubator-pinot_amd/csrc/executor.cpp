@@ -2092,6 +2092,7 @@ std::unique_ptr<GroupByResult> build_dense_result(Engine &e, const DenseGroups &
       oaggs.back().acc_kind = 4;
       oaggs.back().acc = d.accs[i];
     }
+  const auto tb0 = std::chrono::steady_clock::now();
   // device outputs and their pinned host copy live in grow-only engine buffers (no per-query allocation), chunk-major
   // (GroupOutputLayout): up to 4 chunks, each copied to the host as soon as it is ready while the host fills the
   // result arrays from the chunks already there
@@ -2175,8 +2176,13 @@ std::unique_ptr<GroupByResult> build_dense_result(Engine &e, const DenseGroups &
   else
     for (auto &f : sizing) f();
   const int64_t base = d.key_base;
+  const auto tf0 = std::chrono::steady_clock::now();
+  double wait_us = 0, fill_us = 0;
   for (int c = 0; c < K; c++) {
+  const auto tw = std::chrono::steady_clock::now();
   PINOT_HIP(hipEventSynchronize(e.out_ev[c]));
+  const auto tw1 = std::chrono::steady_clock::now();
+  wait_us += std::chrono::duration<double, std::micro>(tw1 - tw).count();
   const size_t c0 = (size_t)c * L.ch, c1 = std::min<size_t>(n, c0 + L.ch);
   const uint8_t *cb = e.group_host.get<uint8_t>() + (size_t)c * L.chunk_bytes;
   const auto *hc = reinterpret_cast<const unsigned long long *>(cb);  // chunk rows, indexed by g - c0
@@ -2221,7 +2227,11 @@ std::unique_ptr<GroupByResult> build_dense_result(Engine &e, const DenseGroups &
       }
     }
   });
+  fill_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tw1).count();
   }
+  if (e.host_phases)
+    fprintf(stderr, "[pinot_gpu] group-by outputs (us): enqueue+sizing %.1f, chunk waits %.1f, fill %.1f (%d chunks)\n",
+            std::chrono::duration<double, std::micro>(tf0 - tb0).count(), wait_us, fill_us, K);
   return res;
 }
 

@@ -889,29 +889,9 @@ template <int MODE>
 __device__ __forceinline__ void group_chunk_lq(const GroupArgs &a, const GroupSegment &sg, int64_t ch, uint64_t mask,
                                                int lane, uint32_t *plds) {
   const int64_t q0 = ch * 256 + lane;
-  if constexpr (MODE == GB_EMIT2) {
-    const LqCols k = lq_cols<MODE>(a, sg);
-    uint32_t mq[4];
-    bool any[4];
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-      const int src = 16 * q + (lane >> 2);
-      const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)mask, src, 64);
-      const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(mask >> 32), src, 64);
-      mq[q] = (((lane & 2) ? hi : lo) >> (16 * (lane & 1))) & 0xFFFFu;
-      any[q] = __any(mq[q] != 0);
-    }
-    // two register sets: quarter q + 1's loads are in flight while quarter q decodes and sinks
-    uint32_t R0[kGroupPfCols][12], R1[kGroupPfCols][12];
-    if (any[0]) lq_load<kGroupPfCols>(k, q0, R0);
-    if (any[1]) lq_load<kGroupPfCols>(k, q0 + 64, R1);
-    if (any[0]) lq_process<MODE, kGroupPfCols>(a, sg, k, R0, q0, mq[0], lane, plds);
-    if (any[2]) lq_load<kGroupPfCols>(k, q0 + 128, R0);
-    if (any[1]) lq_process<MODE, kGroupPfCols>(a, sg, k, R1, q0 + 64, mq[1], lane, plds);
-    if (any[3]) lq_load<kGroupPfCols>(k, q0 + 192, R1);
-    if (any[2]) lq_process<MODE, kGroupPfCols>(a, sg, k, R0, q0 + 128, mq[2], lane, plds);
-    if (any[3]) lq_process<MODE, kGroupPfCols>(a, sg, k, R1, q0 + 192, mq[3], lane, plds);
-  } else {
+  {
+    // (measured: prefetching the next quarter into a second register set was slower — the sink's data-dependent
+    // HBM stores also count in vmcnt, so the prefetched quarter's first use waits for everything: vmcnt(0))
 #pragma unroll 1
     for (int q = 0; q < 4; q++) {
       const int src = 16 * q + (lane >> 2);

@@ -13,8 +13,6 @@ Engine::~Engine() {
   for (auto ev : kev) (void)hipEventDestroy(ev);
   if (ev_start) (void)hipEventDestroy(ev_start);
   if (ev_stop) (void)hipEventDestroy(ev_stop);
-  for (hipEvent_t &ev : out_ev)
-    if (ev) (void)hipEventDestroy(ev);
   if (stream) (void)hipStreamDestroy(stream);
 }
 
@@ -81,7 +79,6 @@ std::unique_ptr<pinot_engine> create_engine(int32_t device, const char *config) 
     e->wall_clock_khz = khz;
   PINOT_HIP(hipEventCreate(&e->ev_start));
   PINOT_HIP(hipEventCreate(&e->ev_stop));
-  for (hipEvent_t &ev : e->out_ev) PINOT_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
   return e;
 }
 }  // namespace pinot
@@ -127,6 +124,7 @@ void parse_config(Engine &e, const char *cfg) {
     else if (k == "group.nt_store") e.group_nt_store = std::stoi(v) != 0;
     else if (k == "group.prefetch") e.group_prefetch = v == "1" || v == "true";
     else if (k == "group.bucket") e.group_bucket = v == "1" || v == "true";
+    else if (k == "group.aligned") e.group_aligned = v == "1" || v == "true";
     else if (k == "group.lw") {
       e.group_lw = v == "true" ? 1 : std::stoi(v);
       require(e.group_lw >= 0 && e.group_lw <= 2, PINOT_ERR_BAD_ARG, "group.lw: 0 (per doc) | 1 (lane owns word) | 2 (contiguous quarters)");

@@ -3,7 +3,9 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
+#include <new>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -124,6 +126,42 @@ class MappedBuffer {
   void *p_ = nullptr, *d_ = nullptr;
   size_t n_ = 0;
 };
+
+// Allocator of the large host result arrays: >= 1 MiB blocks are pinned (hipHostMalloc), so the device's final
+// per-group arrays are copied straight into them (no staging buffer, no host fill); smaller blocks — and any block
+// when pinning fails, e.g. without a GPU — come from malloc. A 64-byte header records which.
+template <typename T>
+struct PinnedAllocator {
+  using value_type = T;
+  PinnedAllocator() = default;
+  template <typename U>
+  PinnedAllocator(const PinnedAllocator<U> &) {}
+  T *allocate(size_t n) {
+    const size_t bytes = n * sizeof(T) + 64;
+    void *p = nullptr;
+    uint32_t tag = 0;
+    if (bytes >= (1u << 20) && hipHostMalloc(&p, bytes, hipHostMallocDefault) == hipSuccess) tag = 1;
+    else {
+      (void)hipGetLastError();
+      p = std::malloc(bytes);
+      if (!p) throw std::bad_alloc();
+    }
+    *static_cast<uint32_t *>(p) = tag;
+    return reinterpret_cast<T *>(static_cast<uint8_t *>(p) + 64);
+  }
+  void deallocate(T *q, size_t) {
+    if (!q) return;
+    void *p = reinterpret_cast<uint8_t *>(q) - 64;
+    if (*static_cast<uint32_t *>(p) == 1) (void)hipHostFree(p);
+    else std::free(p);
+  }
+  template <typename U>
+  bool operator==(const PinnedAllocator<U> &) const { return true; }
+  template <typename U>
+  bool operator!=(const PinnedAllocator<U> &) const { return false; }
+};
+template <typename T>
+using HostVec = std::vector<T, PinnedAllocator<T>>;
 
 inline uint32_t load_be32(const uint8_t *p) {
   return (uint32_t(p[0]) << 24) | (uint32_t(p[1]) << 16) | (uint32_t(p[2]) << 8) | uint32_t(p[3]);

@@ -289,8 +289,8 @@ std::vector<uint8_t> group_by_datatable(const pinot_query &q, const GroupByResul
       regs.resize((size_t)n * 256);
       group_by_hll_registers(r, i, regs.data());
     }
-    const std::vector<int64_t> &cnt = r.counts[r.counts_shared ? 0 : i];
-    const std::vector<double> &val = r.values[i];
+    const HostVec<int64_t> &cnt = r.counts[r.counts_shared ? 0 : i];
+    const HostVec<double> &val = r.values[i];
     const int32_t vtype = f == PINOT_AGG_COUNT ? OBJ_LONG : f == PINOT_AGG_AVG ? OBJ_AVG_PAIR
                           : f == PINOT_AGG_DISTINCTCOUNTHLL ? OBJ_HLL : OBJ_DOUBLE;
     object_cell(t, OBJ_MAP, [&](Out &v) {  // MAP_SER_DE (ObjectSerDeUtils.java:262-300)

@@ -163,6 +163,7 @@ struct Engine {
   int group_pshift = -1;      // group.pshift: cap on log2 keys per partition (tests: many small partitions)
   int group_split = -1;       // group.split: log2 sub-partitions per emitted run (-1 auto, 0 single-level)
   bool use_shortcut_plans = true;  // plan.shortcut: metadata / dictionary plans for unfiltered COUNT / MIN / MAX
+  bool group_aligned = true;  // group.aligned: bucketed EMIT runs padded to 64-B buckets (aligned flushes)
   int group_lw = 2;           // group.lw: partitioned plan reads 0 per doc, 1 each lane's 64-doc word, 2 contiguous quarters
   bool group_bucket = true;   // group.bucket: partitioned plan EMITs through LDS buckets into the final layout
   int num_cus = 256;          // multiProcessorCount of the device
@@ -197,7 +198,7 @@ struct Engine {
 
   // timing
   hipEvent_t ev_start = nullptr, ev_stop = nullptr;
-  hipEvent_t out_ev[4] = {};  // group-by output chunks (D2H of chunk c complete)
+  DeviceBuffer hll_linear;    // device copy of hll_linear_counting_table() (k_group_final)
   std::vector<hipEvent_t> kev;  // per-kernel event pairs (timing mode)
   double last_ms[2] = {0, 0};
   int64_t last_launches[2] = {0, 0};
@@ -231,12 +232,12 @@ struct GroupByResult {
   GroupByResult(GroupByResult &&) = default;
   GroupByResult &operator=(GroupByResult &&) = default;
   ~GroupByResult();  // returns its large result arrays to a process-wide pool (no page faults on the next query)
-  std::vector<int64_t> raw_keys;              // ascending raw keys (mixed radix over global ids, column 0 least significant)
+  HostVec<int64_t> raw_keys;                  // ascending raw keys (mixed radix over global ids, column 0 least significant)
   int32_t num_columns = 0;
   std::vector<int> functions;
-  std::vector<std::vector<int64_t>> counts;   // per fn (counts_shared: one vector, counts[0], for every fn)
+  std::vector<HostVec<int64_t>> counts;       // per fn (counts_shared: one vector, counts[0], for every fn)
   bool counts_shared = false;
-  std::vector<std::vector<double>> values;    // per fn
+  std::vector<HostVec<double>> values;        // per fn
   // group key strings ('\t'-joined Dictionary.getStringValue), built on first access
   std::vector<std::vector<std::string>> gvalues;  // [gcol] global id -> string
   std::vector<int64_t> gcard;
@@ -251,7 +252,7 @@ struct GroupByResult {
   std::vector<int64_t> trim(int32_t top_n, int32_t fn) const;
   // DISTINCTCOUNTHLL: cardinalities per fn; registers on the host (hll[fn]) or on the device in parts (one per
   // GPU that finalized a key range: [groups][256] u8 at off[fn], copied on request)
-  std::vector<std::vector<int64_t>> hll_card;
+  std::vector<HostVec<int64_t>> hll_card;
   std::vector<std::vector<uint8_t>> hll;
   std::vector<HllPart> hll_parts;
   mutable std::vector<uint8_t> datatable;  // pinot_datatable_group_by's bytes
@@ -289,6 +290,8 @@ uint16_t hll_register_rank(uint32_t h);  // (register << 8) | rank
 int64_t hll_cardinality(const uint8_t *regs);
 // HyperLogLog.cardinality() from the exact register sum Σ 2^(32 - reg) and the zero-register count.
 int64_t hll_cardinality_from_sum(unsigned long long sum_fixed32, uint32_t zeros);
+const double *hll_linear_counting_table();  // [257]: m * log(m / z), z = 0 -> +inf
+double hll_alpha_mm();
 
 // ------------------------------------------------------------------ multi-GPU server (server.cpp)
 // One engine per local GPU + RCCL communicators created once (ncclCommInitAll over the local devices, or one

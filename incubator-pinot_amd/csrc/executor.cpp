@@ -17,6 +17,9 @@
 // reduced per-segment results come back in ONE device->host copy.
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <memory>
+#include <mutex>
 #include <chrono>
 #include <cmath>
 #include <cstring>
@@ -1441,6 +1444,7 @@ double decode_ordered(uint64_t o) {
 }
 
 void parallel_tasks(size_t n, const std::function<void(size_t)> &fn);
+size_t host_threads();
 
 // Dense accumulators -> result arrays (bitset path and the multi-GPU partial finalize): ordered device
 // compaction of the non-empty keys, one gather, D2H into grow-only engine buffers, host fill over 8 threads.
@@ -1498,7 +1502,7 @@ std::unique_ptr<GroupByResult> finalize_groups(Engine &e, const pinot_query &q, 
       res->hll_card[a].resize(n);
     }
   }
-  const size_t nt = n >= (1u << 16) ? 8 : 1;
+  const size_t nt = n >= (1u << 16) ? host_threads() : 1;
   parallel_tasks(nt, [&](size_t t) {
     const size_t lo = n * t / nt, hi = n * (t + 1) / nt;
     for (int a = 0; a < na; a++) {
@@ -1611,8 +1615,8 @@ namespace {
 // larger result instead of being handed to a small one.
 struct ResultPool {
   std::mutex mu;
-  std::vector<std::vector<int64_t>> i64;
-  std::vector<std::vector<double>> f64;
+  std::vector<HostVec<int64_t>> i64;
+  std::vector<HostVec<double>> f64;
   size_t bytes = 0;
 };
 ResultPool &result_pool() {
@@ -1621,7 +1625,7 @@ ResultPool &result_pool() {
 }
 constexpr size_t kPoolMinElems = 1u << 16, kPoolMaxArrays = 16, kPoolMaxBytes = 256ull << 20;
 template <class T>
-std::vector<T> take_pooled(ResultPool &rp, std::vector<std::vector<T>> &pool, size_t n) {
+HostVec<T> take_pooled(ResultPool &rp, std::vector<HostVec<T>> &pool, size_t n) {
   size_t best = SIZE_MAX;
   for (size_t i = 0; i < pool.size(); i++) {
     const size_t cap = pool[i].capacity();
@@ -1629,7 +1633,7 @@ std::vector<T> take_pooled(ResultPool &rp, std::vector<std::vector<T>> &pool, si
       best = i;
   }
   if (best == SIZE_MAX) return {};
-  std::vector<T> v = std::move(pool[best]);
+  HostVec<T> v = std::move(pool[best]);
   pool.erase(pool.begin() + best);
   rp.bytes -= v.capacity() * sizeof(T);
   return v;
@@ -1703,7 +1707,7 @@ void parallel_tasks(size_t n, const std::function<void(size_t)> &fn);
 uint64_t GroupByResult::export_keys(char *buf, uint64_t buf_len, int64_t *offsets) const {
   const int64_t n = (int64_t)raw_keys.size();
   const size_t nc = gcard.size();
-  const size_t nt = n >= (1 << 16) ? 8 : 1;
+  const size_t nt = n >= (1 << 16) ? host_threads() : 1;
   auto digit = [&](int64_t g, size_t j, int64_t &k) -> const std::string & {
     if (!key_ids.empty()) return gvalues[j][key_ids[g * nc + j]];
     const std::string &v = gvalues[j][k % gcard[j]];
@@ -1766,7 +1770,7 @@ std::vector<int64_t> GroupByResult::trim(int32_t top_n, int32_t fn) const {
   std::iota(idx.begin(), idx.end(), 0);
   if (n <= 4 * trim_size) return idx;
   const int f = functions[fn];
-  const std::vector<int64_t> &cnt = counts[counts_shared ? 0 : fn];
+  const HostVec<int64_t> &cnt = counts[counts_shared ? 0 : fn];
   std::vector<double> v(n);
   for (int64_t g = 0; g < n; g++) {
     switch (f) {
@@ -1793,11 +1797,87 @@ std::unique_ptr<GroupByResult> exec_group_by_legacy(Engine &e, const std::vector
 namespace {
 
 // Runs fn(0..n-1) on up to n threads (the calling thread takes task 0).
+namespace {
+// Persistent host workers for the result fills (spawning threads per call cost ~0.1 ms per call, several calls per
+// query). One job at a time: a second concurrent caller (another engine's thread in the multi-GPU server) runs its
+// tasks on threads of its own instead of waiting.
+class TaskPool {
+ public:
+  static TaskPool &get() {
+    static TaskPool *p = new TaskPool();  // never destroyed: workers may outlive static destruction order
+    return *p;
+  }
+  size_t threads() const { return workers_ + 1; }
+  bool try_run(size_t n, const std::function<void(size_t)> &fn) {
+    std::unique_lock<std::mutex> busy(job_mu_, std::try_to_lock);
+    if (!busy.owns_lock()) return false;
+    auto job = std::make_shared<Job>();
+    job->fn = &fn;
+    job->n = n;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      job_ = job;
+      gen_++;
+    }
+    cv_.notify_all();
+    work(*job);  // the caller takes tasks too
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [&] { return job->done.load() == n; });
+    job_.reset();
+    return true;
+  }
+
+ private:
+  struct Job {
+    const std::function<void(size_t)> *fn = nullptr;
+    size_t n = 0;
+    std::atomic<size_t> next{0}, done{0};
+  };
+  TaskPool() {
+    const unsigned hc = std::max(1u, std::thread::hardware_concurrency());
+    workers_ = std::min<size_t>(15, hc > 1 ? hc - 1 : 0);
+    for (size_t i = 0; i < workers_; i++) std::thread([this] { loop(); }).detach();
+  }
+  void work(Job &j) {
+    for (;;) {
+      const size_t i = j.next.fetch_add(1);
+      if (i >= j.n) return;
+      (*j.fn)(i);
+      if (j.done.fetch_add(1) + 1 == j.n) {
+        std::lock_guard<std::mutex> lk(mu_);
+        done_cv_.notify_all();
+      }
+    }
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      std::shared_ptr<Job> j;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+        j = job_;
+      }
+      if (j) work(*j);
+    }
+  }
+  size_t workers_ = 0;
+  std::mutex job_mu_, mu_;
+  std::condition_variable cv_, done_cv_;
+  std::shared_ptr<Job> job_;
+  uint64_t gen_ = 0;
+};
+}  // namespace
+
+size_t host_threads() { return std::min<size_t>(16, TaskPool::get().threads()); }
+
 void parallel_tasks(size_t n, const std::function<void(size_t)> &fn) {
   if (n <= 1) {
     if (n == 1) fn(0);
     return;
   }
+  if (TaskPool::get().try_run(n, fn)) return;
   std::vector<std::thread> th;
   th.reserve(n - 1);
   for (size_t t = 1; t < n; t++) th.emplace_back(fn, t);
@@ -2074,46 +2154,59 @@ std::unique_ptr<GroupByResult> build_dense_result(Engine &e, const DenseGroups &
   res->gvalues = d.ks->gvalues;
   res->gcard = d.ks->gcard;
   if (!n) return res;
-  // output rows: one per primary 8-byte accumulator (aliases such as AVG(x) beside SUM(x) read their primary's row),
-  // then the HLL register sums in aggregation order
-  std::vector<GroupAggDev> oaggs;
-  std::vector<int> row(na, -1);
-  for (int i = 0; i < na; i++)
-    if (gx.acc_kind[i] >= 0 && gx.acc_kind[i] <= 3) {
-      row[i] = (int)oaggs.size();
-      oaggs.push_back(GroupAggDev{});
-      oaggs.back().acc_kind = gx.acc_kind[i];
-      oaggs.back().acc = d.accs[i];
-    }
-  const int n8 = (int)oaggs.size();
-  for (int i = 0; i < na; i++)
-    if (gx.acc_kind[i] == 4) {
-      oaggs.push_back(GroupAggDev{});
-      oaggs.back().acc_kind = 4;
-      oaggs.back().acc = d.accs[i];
-    }
   const auto tb0 = std::chrono::steady_clock::now();
-  // device outputs and their pinned host copy live in grow-only engine buffers (no per-query allocation), chunk-major
-  // (GroupOutputLayout): up to 4 chunks, each copied to the host as soon as it is ready while the host fills the
-  // result arrays from the chunks already there
-  GroupOutputLayout L{};
-  const int K = n >= (1u << 18) ? 4 : 1;
-  L.ch = (long long)((n + K - 1) / K + 63) / 64 * 64;
-  L.n8 = n8;
-  L.n_hll = n_hll;
-  L.keys_off = L.ch * 8 * (1 + n8 + n_hll) + L.ch * 4 * n_hll;
-  L.chunk_bytes = (L.keys_off + L.ch * 8 + 255) / 256 * 256;
-  const size_t out_b = (size_t)L.chunk_bytes * K;
-  e.group_out.reserve(out_b);
-  e.group_host.reserve(out_b);
-  L.out = e.group_out.get<uint8_t>();
-  launch_group_outputs(d.counts, oaggs.data(), (int)oaggs.size(), keys_dev, (long long)n, L, e.stream);
-  PINOT_HIP(hipGetLastError());
-  for (int c = 0; c < K; c++) {
-    PINOT_HIP(hipMemcpyAsync(e.group_host.get<uint8_t>() + (size_t)c * L.chunk_bytes, L.out + (size_t)c * L.chunk_bytes,
-                             L.chunk_bytes, hipMemcpyDeviceToHost, e.stream));
-    PINOT_HIP(hipEventRecord(e.out_ev[c], e.stream));
+  // the result arrays (pinned, recycled from released results where possible) are sized while the device works
+  auto size_results = [&] {
+    if (n >= kPoolMinElems) {
+      ResultPool &rp = result_pool();
+      std::lock_guard<std::mutex> lk(rp.mu);
+      res->raw_keys = take_pooled(rp, rp.i64, n);
+      res->counts[0] = take_pooled(rp, rp.i64, n);
+      for (int i = 0; i < na; i++) {
+        res->values[i] = take_pooled(rp, rp.f64, n);
+        if (ga.acc_kind[i] == 4) res->hll_card[i] = take_pooled(rp, rp.i64, n);
+      }
+    }
+    res->counts_shared = true;  // every aggregation counts the same docs per group
+    res->raw_keys.resize(n);
+    res->counts[0].resize(n);
+    for (int i = 0; i < na; i++) {
+      res->values[i].resize(n);
+      if (ga.acc_kind[i] == 4) res->hll_card[i].resize(n);
+    }
+  };
+  // device: the final arrays in the host layout (k_group_final), then one D2H per array straight into the result
+  if (!e.hll_linear.size()) {
+    e.hll_linear.alloc(257 * sizeof(double));
+    PINOT_HIP(hipMemcpy(e.hll_linear.get(), hll_linear_counting_table(), 257 * sizeof(double), hipMemcpyHostToDevice));
   }
+  int n_card = 0;
+  for (int i = 0; i < na; i++) n_card += ga.acc_kind[i] == 4;
+  const size_t n8 = n * 8;
+  e.group_out.reserve(n8 * (2 + na + n_card) + 256);
+  GroupFinalArgs f{};
+  f.n = na;
+  f.out_keys = e.group_out.get<long long>();
+  f.out_counts = f.out_keys + n;
+  f.key_base = d.key_base;
+  f.alpha_mm = hll_alpha_mm();
+  f.linear = e.hll_linear.get<double>();
+  {
+    double *v = reinterpret_cast<double *>(f.out_counts + n);
+    long long *c = reinterpret_cast<long long *>(v + n * na);
+    for (int i = 0; i < na; i++) {
+      const int src = alias[i] >= 0 ? alias[i] : i;  // the accumulator this aggregation reads
+      f.kind[i] = ga.acc_kind[i];
+      f.acc[i] = d.accs[src];
+      f.out_values[i] = v + n * i;
+      if (ga.acc_kind[i] == 4) {
+        f.out_card[i] = c;
+        c += n;
+      }
+    }
+  }
+  launch_group_final(d.counts, keys_dev, (long long)n, f, e.stream);
+  PINOT_HIP(hipGetLastError());
   if (n_hll) {  // registers stay on the device until asked for; buffers are recycled once their result is released
     HllPart part;
     part.device = e.device;
@@ -2148,90 +2241,20 @@ std::unique_ptr<GroupByResult> build_dense_result(Engine &e, const DenseGroups &
     res->key_ids.resize(n * q.num_group_by);
     PINOT_HIP(hipMemcpyAsync(res->key_ids.data(), ids.get(), n * q.num_group_by * 4, hipMemcpyDeviceToHost, e.stream));
   }
-  std::vector<int> hidx(na, -1);  // HLL register-sum row of each (primary) HLL aggregation
-  for (int i = 0, h = 0; i < na; i++)
-    if (gx.acc_kind[i] == 4) hidx[i] = h++;
-  // result arrays (while the device works): recycled arrays of released results where possible (already-mapped
-  // pages), sized in parallel over the host's cores
-  if (n >= kPoolMinElems) {
-    ResultPool &rp = result_pool();
-    std::lock_guard<std::mutex> lk(rp.mu);
-    res->raw_keys = take_pooled(rp, rp.i64, n);
-    res->counts[0] = take_pooled(rp, rp.i64, n);
-    for (int i = 0; i < na; i++) {
-      res->values[i] = take_pooled(rp, rp.f64, n);
-      if (ga.acc_kind[i] == 4) res->hll_card[i] = take_pooled(rp, rp.i64, n);
-    }
-  }
-  std::vector<std::function<void()>> sizing;
-  sizing.push_back([&] { res->raw_keys.resize(n); });
-  res->counts_shared = true;  // every aggregation counts the same docs per group
-  sizing.push_back([&] { res->counts[0].resize(n); });
+  size_results();
+  const auto tb1 = std::chrono::steady_clock::now();
+  PINOT_HIP(hipMemcpyAsync(res->raw_keys.data(), f.out_keys, n8, hipMemcpyDeviceToHost, e.stream));
+  PINOT_HIP(hipMemcpyAsync(res->counts[0].data(), f.out_counts, n8, hipMemcpyDeviceToHost, e.stream));
   for (int i = 0; i < na; i++) {
-    sizing.push_back([&, i] { res->values[i].resize(n); });
-    if (ga.acc_kind[i] == 4) sizing.push_back([&, i] { res->hll_card[i].resize(n); });
+    PINOT_HIP(hipMemcpyAsync(res->values[i].data(), f.out_values[i], n8, hipMemcpyDeviceToHost, e.stream));
+    if (ga.acc_kind[i] == 4)
+      PINOT_HIP(hipMemcpyAsync(res->hll_card[i].data(), f.out_card[i], n8, hipMemcpyDeviceToHost, e.stream));
   }
-  const size_t nt = n >= (1u << 16) ? 8 : 1;  // small results: no threads
-  if (nt > 1) parallel_tasks(sizing.size(), [&](size_t t) { sizing[t](); });
-  else
-    for (auto &f : sizing) f();
-  const int64_t base = d.key_base;
-  const auto tf0 = std::chrono::steady_clock::now();
-  double wait_us = 0, fill_us = 0;
-  for (int c = 0; c < K; c++) {
-  const auto tw = std::chrono::steady_clock::now();
-  PINOT_HIP(hipEventSynchronize(e.out_ev[c]));
-  const auto tw1 = std::chrono::steady_clock::now();
-  wait_us += std::chrono::duration<double, std::micro>(tw1 - tw).count();
-  const size_t c0 = (size_t)c * L.ch, c1 = std::min<size_t>(n, c0 + L.ch);
-  const uint8_t *cb = e.group_host.get<uint8_t>() + (size_t)c * L.chunk_bytes;
-  const auto *hc = reinterpret_cast<const unsigned long long *>(cb);  // chunk rows, indexed by g - c0
-  const auto *hacc = hc + L.ch;
-  const auto *hhs = hacc + (size_t)L.ch * n8;
-  const auto *hhz = reinterpret_cast<const uint32_t *>(hhs + (size_t)L.ch * n_hll);
-  const auto *hkeys = reinterpret_cast<const long long *>(cb + L.keys_off);
-  parallel_tasks(nt, [&](size_t t) {
-    const size_t lo = c0 + (c1 - c0) * t / nt, hi = c0 + (c1 - c0) * (t + 1) / nt, m = hi - lo, o = lo - c0;
-    if (base == 0) memcpy(res->raw_keys.data() + lo, hkeys + o, m * 8);
-    else
-      for (size_t g = 0; g < m; g++) res->raw_keys[lo + g] = hkeys[o + g] + base;
-    memcpy(res->counts[0].data() + lo, hc + o, m * 8);
-    for (int i = 0; i < na; i++) {
-      double *vv = res->values[i].data() + lo;
-      const int ak = ga.acc_kind[i];
-      const int src = alias[i] >= 0 ? alias[i] : i;  // the accumulator this aggregation reads
-      const unsigned long long *raw = row[src] >= 0 ? hacc + (size_t)row[src] * L.ch + o : nullptr;
-      switch (ak) {
-        case 0:
-          for (size_t g = 0; g < m; g++) vv[g] = (double)(int64_t)raw[g];
-          break;
-        case 1:
-          memcpy(vv, raw, m * 8);
-          break;
-        case 2:
-        case 3:
-          for (size_t g = 0; g < m; g++) vv[g] = decode_ordered(raw[g]);
-          break;
-        case 4: {
-          const size_t hr = (size_t)hidx[src] * L.ch + o;
-          int64_t *card = res->hll_card[i].data() + lo;
-          for (size_t g = 0; g < m; g++) {
-            card[g] = hll_cardinality_from_sum(hhs[hr + g], hhz[hr + g]);
-            vv[g] = (double)card[g];
-          }
-          break;
-        }
-        default:
-          for (size_t g = 0; g < m; g++) vv[g] = (double)hc[o + g];
-          break;
-      }
-    }
-  });
-  fill_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tw1).count();
-  }
+  wait_stream(e);
   if (e.host_phases)
-    fprintf(stderr, "[pinot_gpu] group-by outputs (us): enqueue+sizing %.1f, chunk waits %.1f, fill %.1f (%d chunks)\n",
-            std::chrono::duration<double, std::micro>(tf0 - tb0).count(), wait_us, fill_us, K);
+    fprintf(stderr, "[pinot_gpu] group-by outputs (us): launch+sizing %.1f, D2H wait %.1f\n",
+            std::chrono::duration<double, std::micro>(tb1 - tb0).count(),
+            std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tb1).count());
   return res;
 }
 
@@ -2486,17 +2509,22 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     for (auto *sg : segs) max_records += sg->num_docs;
     const size_t scan_tmp = exclusive_sum_u32(nullptr, nullptr, (long long)hist_n, nullptr, 0, e.stream);
     const size_t hist_b = (hist_n * 4 + 255) / 256 * 256, pstart_b = ((size_t)gp.P * 4 + 4 + 255) / 256 * 256;
-    e.group_part.reserve(2 * hist_b + pstart_b + scan_tmp + 256);
+    e.group_part.reserve(3 * hist_b + pstart_b + scan_tmp + 256);
     uint8_t *pb = e.group_part.get<uint8_t>();
     auto *hist = reinterpret_cast<uint32_t *>(pb);
     auto *offsets = reinterpret_cast<uint32_t *>(pb + hist_b);
     auto *pstart = reinterpret_cast<uint32_t *>(pb + 2 * hist_b);
-    void *tmp = pb + 2 * hist_b + pstart_b;
-    require(max_records < (int64_t)UINT32_MAX, PINOT_ERR_UNSUPPORTED, "partitioned group-by over > 4G docs per GPU");
-    e.group_records.reserve((size_t)max_records * 8 + 64);
-    // bucketed plan: COUNT keeps the filter words, GB_EMIT2 writes whole LDS buckets into the final layout
+    auto *padded = reinterpret_cast<uint32_t *>(pb + 2 * hist_b + pstart_b);
+    void *tmp = pb + 3 * hist_b + pstart_b;
+    // bucketed plan: COUNT keeps the filter words, GB_EMIT2 writes whole LDS buckets into the final layout; the
+    // lane-owns-quarter sink pads every (partition, block) run to whole 64-B buckets (aligned flushes)
     const bool bucket = e.group_bucket && a.pf_nc > 0 && gp.P <= kBucketMaxPartitions && gp.record_bits <= 63 &&
                         (e.debug_emit == 0 || e.debug_emit >= 3);
+    const bool aligned = bucket && a.lw == 2 && e.group_aligned;
+    const int64_t pad_records = aligned ? (int64_t)hist_n * (kBucketRecs - 1) : 0;
+    require(max_records + pad_records < (int64_t)UINT32_MAX, PINOT_ERR_UNSUPPORTED,
+            "partitioned group-by over > 4G docs per GPU");
+    e.group_records.reserve((size_t)(max_records + pad_records) * 8 + 64);
     if (gp.split && !bucket) e.group_runs.reserve((size_t)max_records * 8 + 64);
     int64_t fstride = 0;
     if (bucket) {
@@ -2518,6 +2546,8 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     ra.n_aggs = na;
     ra.lds_bytes = gp.reduce_bytes;
     ra.wave_cnt_off = gp.reduce_wave_cnt_off;
+    ra.skip_invalid = aligned ? 1 : 0;
+    a.aligned_runs = aligned ? 1 : 0;
     ra.G = ks.G;
     ra.counts = counts;
     for (int i = 0; i < na; i++) {
@@ -2526,8 +2556,9 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     }
     t.timed(1, [&] {
       launch_group_query(a, e.stream);
-      exclusive_sum_u32(hist, offsets, (long long)hist_n, tmp, scan_tmp, e.stream);
-      launch_partition_starts(offsets, hist, (int32_t)gp.P, (int32_t)nblk, pstart, e.stream);
+      if (aligned) launch_pad_counts(hist, (long long)hist_n, padded, e.stream);
+      exclusive_sum_u32(aligned ? padded : hist, offsets, (long long)hist_n, tmp, scan_tmp, e.stream);
+      launch_partition_starts(offsets, aligned ? padded : hist, (int32_t)gp.P, (int32_t)nblk, pstart, e.stream);
       GroupArgs a2 = a;
       if (bucket) {
         a2.mode = GB_EMIT2;

@@ -679,11 +679,13 @@ __device__ __forceinline__ void emit2_sink16(const GroupArgs &a, uint32_t *plds,
     flush |= (in && pos[j] == (uint32_t)kBucketRecs - 1) ? (1u << j) : 0u;
     over |= (((act >> j) & 1u) && !in) ? (1u << j) : 0u;
   }
-  if (__any(over != 0)) {
+  if (__any(over != 0)) {  // aligned runs: from the run end backwards, so the flushes stay 64-B aligned
     uint32_t d[16];
+    uint32_t *back = plds + 2 * a.P;
 #pragma unroll
     for (int j = 0; j < 16; j++)
-      if ((over >> j) & 1u) d[j] = atomicAdd(&cur[key[j] >> a.shift], 1u);
+      if ((over >> j) & 1u)
+        d[j] = a.aligned_runs ? atomicSub(&back[key[j] >> a.shift], 1u) - 1u : atomicAdd(&cur[key[j] >> a.shift], 1u);
 #pragma unroll
     for (int j = 0; j < 16; j++)
       if (((over >> j) & 1u) && st) a.emit[d[j]] = rec[j] | (key[j] & lmask);
@@ -857,14 +859,20 @@ __device__ __forceinline__ void lq_process(const GroupArgs &a, const GroupSegmen
       for (int j = 0; j < 16; j++) rec[j] |= (unsigned long long)id[j] << k.fsh[c];
     }
   }
-  if constexpr (MODE == GB_EMIT2) {
+  if constexpr (MODE == GB_EMIT2 || MODE == GB_COUNT) {
     uint32_t act = mq;
     if (sg.admitted) {
 #pragma unroll
       for (int j = 0; j < 16; j++)
         if (!((gload<uint32_t>(sg.admitted + (key[j] >> 5)) >> (key[j] & 31)) & 1u)) act &= ~(1u << j);
     }
-    emit2_sink16(a, plds, act, key, rec, lane);
+    if constexpr (MODE == GB_EMIT2) {
+      emit2_sink16(a, plds, act, key, rec, lane);
+    } else {  // partition histogram: LDS adds without return
+#pragma unroll
+      for (int j = 0; j < 16; j++)
+        if ((act >> j) & 1u) atomicAdd(&plds[key[j] >> a.shift], 1u);
+    }
     return;
   }
 #pragma unroll
@@ -980,11 +988,12 @@ __global__ __launch_bounds__(BLK) void k_group_query(GroupArgs a) {
     for (int p = tid; p < a.P; p += BLK) plds[p] = 0;
     __syncthreads();
   }
-  if constexpr (MODE == GB_EMIT2) {
+  if constexpr (MODE == GB_EMIT2) {  // [cursor P][count P][aligned runs: backward cursor = run start + count P]
     for (int p = tid; p < a.P; p += BLK) {
-      plds[p] = a.offsets[(size_t)p * nblk + blockIdx.x];
+      const size_t i = (size_t)p * nblk + blockIdx.x;
+      plds[p] = a.offsets[i];
       plds[a.P + p] = 0;
-      plds[2 * a.P + p] = 0;
+      plds[2 * a.P + p] = a.aligned_runs ? a.offsets[i] + a.hist[i] : 0u;
     }
     __syncthreads();
   }
@@ -1032,12 +1041,18 @@ __global__ __launch_bounds__(BLK) void k_group_query(GroupArgs a) {
   matched = wave_sum(matched);  // the EMIT pass re-reads what the COUNT pass already counted
   if (MODE != GB_EMIT && MODE != GB_EMIT2 && MODE != GB_VERIFY && MODE != GB_FIRST && lane == 0 && matched)
     atomicAdd(a.matched + g, matched);
-  if constexpr (MODE == GB_EMIT2) {  // the partially filled buckets, 8 lanes per bucket
+  if constexpr (MODE == GB_EMIT2) {  // the partially filled buckets, 8 lanes per bucket (+ aligned runs' padding)
     __syncthreads();
     const unsigned long long *bkt = reinterpret_cast<const unsigned long long *>(plds + ((3 * a.P + 3) & ~3));
     const int i = tid % kBucketRecs;
-    for (int p = tid / kBucketRecs; p < a.P; p += BLK / kBucketRecs)
+    for (int p = tid / kBucketRecs; p < a.P; p += BLK / kBucketRecs) {
       if ((uint32_t)i < plds[a.P + p]) a.emit[plds[p] + i] = bkt[p * kBucketRecs + i] & ~kRecValid;
+      if (a.aligned_runs) {  // run [start, start + count) is full; slots up to the next multiple of 8 are padding
+        const size_t r = (size_t)p * nblk + blockIdx.x;
+        const uint32_t end = a.offsets[r] + a.hist[r], pad = (uint32_t)(-(int32_t)a.hist[r]) & (kBucketRecs - 1);
+        if ((uint32_t)i < pad) a.emit[end + i] = kRecInvalid;
+      }
+    }
   }
   if constexpr (MODE == GB_LDS) flush_group_lds(a, sg, acc_lds, tid);
   if constexpr (MODE == GB_COUNT) {

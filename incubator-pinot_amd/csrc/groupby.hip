@@ -9,10 +9,9 @@
 //                        aggregateGroupBySV loops (PC/query/aggregation/groupby/DefaultGroupByExecutor.java:70-168).
 //   k_key_flags / k_key_scatter   counts != 0 -> ordered key list (exclusive scan in between), i.e. the
 //                        raw keys in ascending order (GroupKeyGenerator.getUniqueGroupKeys, sorted).
-//   k_group_outputs      per non-empty group: count, each 8-byte accumulator, and for HLL the exact
-//                        fixed-point Σ 2^(32 - register) and the zero-register count, from which the host
-//                        evaluates HyperLogLog.cardinality() bit-identically (the double sum of
-//                        1.0 / (1 << reg) is exact: <= 256 terms of >= 2^-25).
+//   k_group_final        per non-empty group, the host result arrays: key, count, each function's value and
+//                        HyperLogLog.cardinality() from the exact fixed-point Σ 2^(32 - register) (the double sum
+//                        of 1.0 / (1 << reg) is exact: <= 256 terms of >= 2^-25), bit-identical to the host's.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -106,6 +105,7 @@ __global__ __launch_bounds__(kReduceBlock) void k_partition_reduce(PartitionRedu
       const uint32_t r = r0 + (uint32_t)u * kReduceBlock;
       ok[u] = r < e;
       rec[u] = ok[u] ? __builtin_nontemporal_load(a.records + r) : 0ull;
+      if (a.skip_invalid) ok[u] = ok[u] && rec[u] != kRecInvalid;
       k[u] = (uint32_t)(rec[u] & kmask);
     }
     if (pk < 0) {
@@ -227,50 +227,61 @@ __global__ void k_key_scatter(long long G, const uint32_t *__restrict__ flags, c
   }
 }
 
-struct OutputAggs {
-  GroupAggDev aggs[kMaxGroupAggs];
-  int n;
-};
+// Final per-group arrays in the host result's own layout (copied straight into the pinned result arrays: no host
+// fill): raw keys (+ key_base), counts, per function its intermediate value as a double and, for DISTINCTCOUNTHLL,
+// HyperLogLog.cardinality() — the host's exact arithmetic (hll.cpp hll_cardinality_from_sum): Σ 2^(32 - reg) as an
+// exact integer scaled by 2^-32, alpha_mm * (1 / sum), linear counting m * log(m / zeros) from the host-computed
+// table when the estimate is <= 2.5 m, then floor(x + 0.5). IEEE double division / multiplication and no
+// contractable multiply-add, so the device rounds exactly as the host does.
+__device__ __forceinline__ double decode_ordered_d(unsigned long long o) {
+  const unsigned long long u = (o & 0x8000000000000000ull) ? (o & ~0x8000000000000000ull) : ~o;
+  return __longlong_as_double((long long)u);
+}
 
-// Chunk-major per-group outputs (GroupOutputLayout): group i lives in chunk i / ch at position i % ch, each chunk
-// holding its counts, 8-byte accumulator rows, HLL register sums, HLL zero counts and raw keys back to back, so a
-// chunk leaves in one D2H copy while the host fills the previous one.
-__global__ void k_group_outputs(const unsigned long long *__restrict__ counts, OutputAggs oa,
-                                const long long *__restrict__ keys, long long n, GroupOutputLayout L) {
+__global__ void k_group_final(const unsigned long long *__restrict__ counts, const long long *__restrict__ keys,
+                              long long n, GroupFinalArgs f) {
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
     const long long k = keys[i];
-    const long long c = i / L.ch, l = i - c * L.ch;
-    uint8_t *base = L.out + c * L.chunk_bytes;
-    unsigned long long *c8 = reinterpret_cast<unsigned long long *>(base);
-    c8[l] = counts[k];
-    int h = 0, r = 0;
-    for (int g = 0; g < oa.n; g++) {
-      const GroupAggDev &ag = oa.aggs[g];
-      if (ag.acc_kind == 4) {
-        const u32x4 *rg = reinterpret_cast<const u32x4 *>(static_cast<const uint8_t *>(ag.acc) + k * 256);
-        unsigned long long s = 0;
-        uint32_t z = 0;
-        for (int q = 0; q < 16; q++) {
-          const u32x4 v = rg[q];
-          const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    const unsigned long long c = counts[k];
+    f.out_keys[i] = k + f.key_base;
+    f.out_counts[i] = (long long)c;
+    for (int g = 0; g < f.n; g++) {
+      double v;
+      switch (f.kind[g]) {
+        case 0: v = (double)static_cast<const long long *>(f.acc[g])[k]; break;
+        case 1: v = static_cast<const double *>(f.acc[g])[k]; break;
+        case 2:
+        case 3: v = decode_ordered_d(static_cast<const unsigned long long *>(f.acc[g])[k]); break;
+        case 4: {
+          const u32x4 *r = reinterpret_cast<const u32x4 *>(static_cast<const uint8_t *>(f.acc[g]) + k * 256);
+          unsigned long long s = 0;
+          uint32_t z = 0;
+          for (int q = 0; q < 16; q++) {
+            const u32x4 w4 = r[q];
+            const uint32_t w[4] = {w4.x, w4.y, w4.z, w4.w};
 #pragma unroll
-          for (int cc = 0; cc < 4; cc++)
+            for (int cc = 0; cc < 4; cc++)
 #pragma unroll
-            for (int bb = 0; bb < 4; bb++) {
-              const uint32_t reg = (w[cc] >> (8 * bb)) & 0xFFu;
-              s += 1ull << (32 - reg);
-              z += reg == 0;
-            }
+              for (int bb = 0; bb < 4; bb++) {
+                const uint32_t reg = (w[cc] >> (8 * bb)) & 0xFFu;
+                s += 1ull << (32 - reg);
+                z += reg == 0;
+              }
+          }
+          const double sum = ldexp((double)s, -32);
+          const double inv = 1.0 / sum;
+          const double estimate = f.alpha_mm * inv;
+          double x = estimate;
+          if (estimate <= 640.0) x = f.linear[z];
+          const long long card = isinf(x) ? 0x7FFFFFFFFFFFFFFFll : (long long)floor(x + 0.5);
+          f.out_card[g][i] = card;
+          v = (double)card;
+          break;
         }
-        c8[(1 + L.n8 + h) * L.ch + l] = s;
-        reinterpret_cast<uint32_t *>(c8 + (1 + L.n8 + L.n_hll) * L.ch)[h * L.ch + l] = z;
-        h++;
-      } else if (ag.acc_kind != 5) {
-        c8[(1 + r) * L.ch + l] = static_cast<const unsigned long long *>(ag.acc)[k];
-        r++;
+        default: v = (double)c; break;
       }
+      f.out_values[g][i] = v;
     }
-    reinterpret_cast<long long *>(base + L.keys_off)[l] = k;
   }
 }
 
@@ -421,6 +432,13 @@ __global__ void k_admit_bitmap(const uint32_t *__restrict__ first_doc, long long
 
 }  // namespace
 
+void launch_group_final(const unsigned long long *counts, const long long *keys, long long n, const GroupFinalArgs &f,
+                        hipStream_t stream) {
+  if (n <= 0) return;
+  const int grid = (int)std::min<long long>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_group_final, dim3(grid), dim3(256), 0, stream, counts, keys, n, f);
+}
+
 size_t admission_scratch_bytes(long long G) {
   size_t need = 0;
   PINOT_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, need, (const uint32_t *)nullptr, (uint32_t *)nullptr, (int)G));
@@ -457,6 +475,17 @@ void launch_widen_u8(const uint8_t *in, long long n, int32_t *out, hipStream_t s
   const long long n4 = n / 4;  // n = G * 256: always a multiple of 4
   const int grid = (int)std::min<long long>((n4 + 255) / 256, 8192);
   hipLaunchKernelGGL(k_widen_u8, dim3(grid), dim3(256), 0, stream, in, n4, out);
+}
+
+__global__ void k_pad_counts(const uint32_t *__restrict__ in, long long n, uint32_t *__restrict__ out) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    out[i] = (in[i] + (kBucketRecs - 1)) & ~(uint32_t)(kBucketRecs - 1);
+}
+
+void launch_pad_counts(const uint32_t *in, long long n, uint32_t *out, hipStream_t stream) {
+  if (n <= 0) return;
+  const int grid = (int)std::min<long long>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_pad_counts, dim3(grid), dim3(256), 0, stream, in, n, out);
 }
 
 void launch_partition_starts(const uint32_t *offsets, const uint32_t *hist, int32_t P, int32_t nblk, uint32_t *pstart,
@@ -510,16 +539,6 @@ void launch_compact_keys_ordered(long long G, const unsigned long long *counts, 
   hipLaunchKernelGGL(k_key_flags, dim3(grid), dim3(256), 0, stream, G, counts, flags);
   exclusive_sum_u32(flags, pos, G, tmp, scratch_bytes - 2 * flags_b, stream);
   hipLaunchKernelGGL(k_key_scatter, dim3(grid), dim3(256), 0, stream, G, flags, pos, keys_out, n_out);
-}
-
-void launch_group_outputs(const unsigned long long *counts, const GroupAggDev *aggs_host, int n_aggs, const long long *keys,
-                          long long n, const GroupOutputLayout &L, hipStream_t stream) {
-  if (n <= 0) return;
-  OutputAggs oa{};
-  oa.n = n_aggs;
-  for (int g = 0; g < n_aggs && g < kMaxGroupAggs; g++) oa.aggs[g] = aggs_host[g];
-  const int grid = (int)std::min<long long>((n + 255) / 256, 4096);
-  hipLaunchKernelGGL(k_group_outputs, dim3(grid), dim3(256), 0, stream, counts, oa, keys, n, L);
 }
 
 }  // namespace pinot

@@ -96,6 +96,12 @@ struct LinearCounting {
 const LinearCounting kLinearCounting;
 }  // namespace
 
+const double *hll_linear_counting_table() { return kLinearCounting.v; }
+double hll_alpha_mm() {
+  const double m = 256.0;
+  return (0.7213 / (1.0 + 1.079 / m)) * m * m;
+}
+
 int64_t hll_cardinality_from_sum(unsigned long long sum_fixed32, uint32_t zeros) {
   const double m = 256.0;
   const double alpha_mm = (0.7213 / (1.0 + 1.079 / m)) * m * m;

@@ -203,6 +203,7 @@ int scan_query_blocks_per_cu(int stage_bytes, bool gathers, bool pipelined);
 //              whole into the FINAL partition layout (offsets from GB_COUNT's histogram): no split pass
 enum GroupMode : int32_t { GB_GLOBAL = 0, GB_LDS = 1, GB_COUNT = 2, GB_EMIT = 3, GB_VERIFY = 4, GB_FIRST = 5, GB_EMIT2 = 6 };
 constexpr int kBucketRecs = 8;                                   // 64-B bucket flushes
+constexpr unsigned long long kRecInvalid = ~0ull;                // padding slot of an aligned run (bit 63 set)
 constexpr int kBucketMaxPartitions = 2040;  // P x (3 x 4 + 8 x 8) B + 4 KiB of flush lists per block <= 160 KiB
 // accumulator kinds (acc_kind): 0 int64 sum, 1 double sum, 2 ordered-u64 min, 3 ordered-u64 max,
 // 4 HLL registers (u8 [G][256]), 5 none (COUNT / AVG count share `counts`)
@@ -277,6 +278,11 @@ struct GroupArgs {
   int32_t nt_store;            // GB_EMIT / split: records stored with the non-temporal (streaming) policy
   int32_t lw;                  // GB_COUNT / GB_EMIT / GB_EMIT2 with pf_nc > 0: lane-owns-word reads (G < 2^32)
   uint64_t *filter_out;        // GB_COUNT: writes each segment's filter words here (GB_EMIT2 reads them back)
+  int32_t aligned_runs;        // GB_EMIT2 (lane-owns-quarter sink): runs padded to multiples of kBucketRecs records
+                               // (offsets from the padded counts): bucket flushes advance from the run start in
+                               // aligned 64-B pieces, records that find their bucket full fill from the run end
+                               // backwards, and the padding slots are written with kRecInvalid
+  int32_t reserved3;
   int64_t filter_stride;       // words per segment in filter_out
 };
 constexpr int kGroupPfCols = 4;
@@ -291,7 +297,7 @@ struct PartitionReduceArgs {
   const uint32_t *pstart;      // [P + 1] first record of each partition
   int32_t P, shift, n_aggs, lds_bytes;
   int32_t wave_cnt_off;        // LDS byte offset of the per-wave count copies (8 waves x K u32)
-  int32_t reserved;
+  int32_t skip_invalid;        // records may be kRecInvalid padding (GB_EMIT2 aligned runs): skipped
   long long G;
   unsigned long long *counts;
   GroupAggDev aggs[kMaxGroupAggs];  // fwd unused; dict / hll_lut / acc / lds_off / acc_kind / field_shift / bits
@@ -305,6 +311,8 @@ void launch_partition_split(const uint32_t *hist, const uint32_t *offsets, const
 // pstart[p] = offsets[p * nblk] (partition-major exclusive offsets), pstart[P] = total records.
 void launch_partition_starts(const uint32_t *offsets, const uint32_t *hist, int32_t P, int32_t nblk, uint32_t *pstart,
                              hipStream_t stream);
+// out[i] = in[i] rounded up to a multiple of kBucketRecs (aligned runs of the bucketed EMIT)
+void launch_pad_counts(const uint32_t *in, long long n, uint32_t *out, hipStream_t stream);
 // Hashed key spaces: the global-id tuple of each listed slot's representative doc, ids[i * n_gcols + j].
 void launch_hash_tuples(const GroupArgs &a, const long long *slots, long long n, int32_t *ids, hipStream_t stream);
 // HLL registers of the listed keys: out[i * 256 + r] = regs[keys[i] * 256 + r].
@@ -318,17 +326,23 @@ void launch_narrow_u32(const uint32_t *in, long long n, uint8_t *out, hipStream_
 size_t compact_keys_scratch_bytes(long long G);
 void launch_compact_keys_ordered(long long G, const unsigned long long *counts, long long *keys_out,
                                  unsigned long long *n_out, void *scratch, size_t scratch_bytes, hipStream_t stream);
-// Per-group outputs, chunk-major: chunk c (groups [c * ch, (c + 1) * ch)) at out + c * chunk_bytes holds counts u64
-// [ch], the 8-byte accumulator rows u64 [n8][ch] (aggregations of kinds 0-3 in order), the HLL register sums
-// Σ 2^(32 - reg) u64 [n_hll][ch] (exact), the zero-register counts u32 [n_hll][ch], then the raw keys i64 [ch] at
-// keys_off.
-struct GroupOutputLayout {
-  uint8_t *out;
-  long long ch, chunk_bytes, keys_off;
-  int32_t n8, n_hll;
+// Final per-group arrays in the host result layout (k_group_final): out_keys[i] = keys[i] + key_base, out_counts,
+// out_values[fn] (the function's intermediate value as a double) and out_card[fn] (DISTINCTCOUNTHLL cardinality,
+// bit-identical to the host's hll_cardinality_from_sum). kind: 0 i64 sum, 1 f64 sum, 2/3 ordered min / max,
+// 4 HLL u8 registers [G][256], 5 the count; acc: the accumulator the function reads (its primary's for aliases).
+struct GroupFinalArgs {
+  int32_t n;
+  int32_t kind[kMaxGroupAggs];
+  const void *acc[kMaxGroupAggs];
+  double *out_values[kMaxGroupAggs];
+  long long *out_card[kMaxGroupAggs];
+  long long *out_keys, *out_counts;
+  long long key_base;
+  double alpha_mm;
+  const double *linear;  // device copy of m * log(m / z), z = 0..256 (z = 0: +inf)
 };
-void launch_group_outputs(const unsigned long long *counts, const GroupAggDev *aggs_host, int n_aggs, const long long *keys,
-                          long long n, const GroupOutputLayout &L, hipStream_t stream);
+void launch_group_final(const unsigned long long *counts, const long long *keys, long long n, const GroupFinalArgs &f,
+                        hipStream_t stream);
 // num.groups.limit admission (DictionaryBasedGroupKeyGenerator IntMapBasedHolder.getGroupId, first appearance):
 // segment s admits the upper[s] keys with the smallest first_doc[s][k] (first_doc values of distinct keys are
 // distinct docs). bitmaps[s] (words u32 each) gets bit k for every admitted key; upper[s] >= G admits every present

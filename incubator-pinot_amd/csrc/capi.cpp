@@ -125,6 +125,10 @@ void parse_config(Engine &e, const char *cfg) {
     else if (k == "group.prefetch") e.group_prefetch = v == "1" || v == "true";
     else if (k == "group.bucket") e.group_bucket = v == "1" || v == "true";
     else if (k == "group.aligned") e.group_aligned = v == "1" || v == "true";
+    else if (k == "group.emit_block") {
+      e.group_emit_block = std::stoi(v);
+      require(e.group_emit_block == 512 || e.group_emit_block == 1024, PINOT_ERR_BAD_ARG, "group.emit_block: 512 | 1024");
+    }
     else if (k == "group.lw") {
       e.group_lw = v == "true" ? 1 : std::stoi(v);
       require(e.group_lw >= 0 && e.group_lw <= 2, PINOT_ERR_BAD_ARG, "group.lw: 0 (per doc) | 1 (lane owns word) | 2 (contiguous quarters)");

@@ -2548,6 +2548,7 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     ra.wave_cnt_off = gp.reduce_wave_cnt_off;
     ra.skip_invalid = aligned ? 1 : 0;
     a.aligned_runs = aligned ? 1 : 0;
+    a.emit_block = e.group_emit_block;
     ra.G = ks.G;
     ra.counts = counts;
     for (int i = 0; i < na; i++) {

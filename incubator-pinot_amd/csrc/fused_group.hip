@@ -1063,8 +1063,11 @@ __global__ __launch_bounds__(BLK) void k_group_query(GroupArgs a) {
 
 // Lane-owns-word EMIT kernels run 512-thread blocks (their 32-doc key / record arrays need the registers).
 constexpr int kGroupLwEmitBlock = 512;
+// group.emit_block=1024: the lane-owns-quarter bucketed EMIT at 16 waves per block (the sink is LDS-latency bound)
+constexpr int kGroupLqEmitBlockWide = 1024;
 
 static int group_block_threads(const GroupArgs &a) {
+  if (a.lw == 2 && a.mode == GB_EMIT2 && a.emit_block == kGroupLqEmitBlockWide) return kGroupLqEmitBlockWide;
   return (a.lw && (a.mode == GB_EMIT || a.mode == GB_EMIT2)) ? kGroupLwEmitBlock : kGroupBlock;
 }
 
@@ -1089,7 +1092,9 @@ static void with_group_kernel(const GroupArgs &a, V &&v) {
       break;
     case GB_FIRST: v(&k_group_query<GB_FIRST, 0, kGroupBlock>, kGroupBlock); break;
     case GB_EMIT2:
-      if (lh) v(&k_group_query<GB_EMIT2, 3, kGroupLwEmitBlock>, kGroupLwEmitBlock);
+      if (lh && a.emit_block == kGroupLqEmitBlockWide)
+        v(&k_group_query<GB_EMIT2, 3, kGroupLqEmitBlockWide>, kGroupLqEmitBlockWide);
+      else if (lh) v(&k_group_query<GB_EMIT2, 3, kGroupLwEmitBlock>, kGroupLwEmitBlock);
       else if (lw) v(&k_group_query<GB_EMIT2, 2, kGroupLwEmitBlock>, kGroupLwEmitBlock);
       else v(&k_group_query<GB_EMIT2, 1, kGroupBlock>, kGroupBlock);
       break;

@@ -63,6 +63,7 @@ __device__ __forceinline__ uint32_t hll_register_rank_d(uint32_t h) {
   return ((h >> 24) << 8) | (uint32_t)(__builtin_clz((h << 8) | 129u) + 1);
 }
 
+template <bool SKIP_INVALID>
 __global__ __launch_bounds__(kReduceBlock) void k_partition_reduce(PartitionReduceArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int tid = threadIdx.x;
@@ -105,7 +106,7 @@ __global__ __launch_bounds__(kReduceBlock) void k_partition_reduce(PartitionRedu
       const uint32_t r = r0 + (uint32_t)u * kReduceBlock;
       ok[u] = r < e;
       rec[u] = ok[u] ? __builtin_nontemporal_load(a.records + r) : 0ull;
-      if (a.skip_invalid) ok[u] = ok[u] && rec[u] != kRecInvalid;
+      if constexpr (SKIP_INVALID) ok[u] = ok[u] && rec[u] != kRecInvalid;
       k[u] = (uint32_t)(rec[u] & kmask);
     }
     if (pk < 0) {
@@ -511,7 +512,10 @@ void launch_gather_hll(const uint8_t *regs, const long long *keys, long long n, 
 
 void launch_partition_reduce(const PartitionReduceArgs &a, hipStream_t stream) {
   if (a.P <= 0) return;
-  hipLaunchKernelGGL(k_partition_reduce, dim3((unsigned)a.P), dim3(kReduceBlock), (size_t)a.lds_bytes, stream, a);
+  if (a.skip_invalid)
+    hipLaunchKernelGGL(k_partition_reduce<true>, dim3((unsigned)a.P), dim3(kReduceBlock), (size_t)a.lds_bytes, stream, a);
+  else
+    hipLaunchKernelGGL(k_partition_reduce<false>, dim3((unsigned)a.P), dim3(kReduceBlock), (size_t)a.lds_bytes, stream, a);
 }
 
 size_t exclusive_sum_u32(const uint32_t *in, uint32_t *out, long long n, void *tmp, size_t tmp_bytes,

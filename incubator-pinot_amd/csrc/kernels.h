@@ -282,7 +282,7 @@ struct GroupArgs {
                                // (offsets from the padded counts): bucket flushes advance from the run start in
                                // aligned 64-B pieces, records that find their bucket full fill from the run end
                                // backwards, and the padding slots are written with kRecInvalid
-  int32_t reserved3;
+  int32_t emit_block;          // GB_EMIT2 lane-owns-quarter: threads per block (512, or 1024 = group.emit_block)
   int64_t filter_stride;       // words per segment in filter_out
 };
 constexpr int kGroupPfCols = 4;

@@ -33,6 +33,7 @@ def load():
         _lib = C.CDLL(LIB)
         _lib.pinot_faithful_run.argtypes = [C.POINTER(Task), C.c_int, C.c_int, C.POINTER(C.c_int64),
                                             C.POINTER(C.c_double)]
+        _lib.pinot_fast_run.argtypes = [C.POINTER(Task), C.c_int, C.c_int, C.POINTER(C.c_int64), C.POINTER(C.c_double)]
         _lib.pinot_synth_column.argtypes = [C.c_uint64, C.c_int, C.c_int32, C.c_int, C.c_int64, C.c_void_p]
         _lib.pinot_faithful_read_int.argtypes = [C.c_void_p, C.c_int32, C.c_int]
         _lib.pinot_faithful_read_int.restype = C.c_int32
@@ -71,8 +72,9 @@ class SyntheticTable:
         return dict(self.columns)[name]
 
 
-def run_and_count_sum(table, leaves, metric, threads):
-    """leaves: [(column, ("RANGE", lo, hi)) | (column, ("IN", [dictIds]))]; returns (count, sum)."""
+def run_and_count_sum(table, leaves, metric, threads, optimized=False):
+    """leaves: [(column, ("RANGE", lo, hi)) | (column, ("IN", [dictIds]))]; returns (count, sum).
+    optimized: the batch-unpack executor (pinot_fast_run) instead of the reference-faithful one."""
     lib = load()
     keep = []
     tasks = (Task * len(table.segments))()
@@ -101,7 +103,8 @@ def run_and_count_sum(table, leaves, metric, threads):
             t.metric_dict = metric_dict.ctypes.data
     cnt = C.c_int64()
     sm = C.c_double()
-    lib.pinot_faithful_run(tasks, len(table.segments), threads, C.byref(cnt), C.byref(sm))
+    (lib.pinot_fast_run if optimized else lib.pinot_faithful_run)(tasks, len(table.segments), threads, C.byref(cnt),
+                                                                   C.byref(sm))
     return cnt.value, sm.value
 
 

@@ -2243,14 +2243,42 @@ std::unique_ptr<GroupByResult> build_dense_result(Engine &e, const DenseGroups &
   }
   size_results();
   const auto tb1 = std::chrono::steady_clock::now();
+  // D2H (PCIe-bound, so only what the host cannot derive): keys, counts, each primary's values, cardinalities;
+  // an alias's values (AVG(x) beside SUM(x)) and an HLL function's values (= its cardinalities) are filled on the host
+  std::vector<int> derive(na, -1);  // -2: from the HLL cardinalities; >= 0: copy of that function's values
+  for (int i = 0; i < na; i++) {
+    if (ga.acc_kind[i] == 4) derive[i] = -2;
+    else if (alias[i] >= 0 && ga.acc_kind[i] == ga.acc_kind[alias[i]]) derive[i] = alias[i];
+  }
   PINOT_HIP(hipMemcpyAsync(res->raw_keys.data(), f.out_keys, n8, hipMemcpyDeviceToHost, e.stream));
   PINOT_HIP(hipMemcpyAsync(res->counts[0].data(), f.out_counts, n8, hipMemcpyDeviceToHost, e.stream));
   for (int i = 0; i < na; i++) {
-    PINOT_HIP(hipMemcpyAsync(res->values[i].data(), f.out_values[i], n8, hipMemcpyDeviceToHost, e.stream));
+    if (derive[i] == -1)
+      PINOT_HIP(hipMemcpyAsync(res->values[i].data(), f.out_values[i], n8, hipMemcpyDeviceToHost, e.stream));
     if (ga.acc_kind[i] == 4)
       PINOT_HIP(hipMemcpyAsync(res->hll_card[i].data(), f.out_card[i], n8, hipMemcpyDeviceToHost, e.stream));
   }
   wait_stream(e);
+  bool any_derived = false;
+  for (int i = 0; i < na; i++) any_derived = any_derived || derive[i] != -1;
+  if (any_derived) {
+    const size_t nt = n >= (1u << 16) ? host_threads() : 1;
+    auto fill = [&](size_t t) {
+      const size_t lo = n * t / nt, hi = n * (t + 1) / nt;
+      for (int i = 0; i < na; i++) {
+        if (derive[i] == -1) continue;
+        double *v = res->values[i].data();
+        if (derive[i] == -2) {
+          const int64_t *c = res->hll_card[i].data();
+          for (size_t g = lo; g < hi; g++) v[g] = (double)c[g];
+        } else {
+          memcpy(v + lo, res->values[derive[i]].data() + lo, (hi - lo) * 8);
+        }
+      }
+    };
+    if (nt > 1) parallel_tasks(nt, fill);
+    else fill(0);
+  }
   if (e.host_phases)
     fprintf(stderr, "[pinot_gpu] group-by outputs (us): launch+sizing %.1f, D2H wait %.1f\n",
             std::chrono::duration<double, std::micro>(tb1 - tb0).count(),

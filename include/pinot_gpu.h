@@ -23,6 +23,13 @@
  *   pinot_gpu_group_by                  AggregationGroupByOperator + CombineGroupByOperator
  *                                       (PC/operator/query/AggregationGroupByOperator.java:64-94,
  *                                        PC/operator/CombineGroupByOperator.java:104-228)
+ *   pinot_gpu_prune_segments            ServerQueryExecutorV1Impl.pruneSegments + SegmentPrunerService.prune
+ *                                       (PC/query/executor/ServerQueryExecutorV1Impl.java:183-216, :270-294,
+ *                                        PC/query/pruner/SegmentPrunerService.java:52-60)
+ *   pinot_broker_reduce                 BrokerReduceService.reduceOnDataTable (PC/query/reduce/BrokerReduceService.java:69-530)
+ *   pinot_datatable_*                   IntermediateResultsBlock.getDataTable / DataTableBuilder.buildEmptyDataTable
+ *                                       (PC/operator/blocks/IntermediateResultsBlock.java:206-317,
+ *                                        PC/common/datatable/DataTableBuilder.java:292-370)
  */
 #ifndef PINOT_GPU_H_
 #define PINOT_GPU_H_
@@ -33,7 +40,7 @@
 extern "C" {
 #endif
 
-#define PINOT_GPU_ABI_VERSION 5
+#define PINOT_GPU_ABI_VERSION 6
 
 /* ------------------------------------------------------------------ status */
 typedef enum {
@@ -229,6 +236,33 @@ pinot_status pinot_groupby_trim(const pinot_groupby_result *r, int32_t top_n, in
                                 int64_t *num_out);
 void pinot_groupby_free(pinot_groupby_result *r);
 
+/* ------------------------------------------------------------------ segment pruning
+ * The step before the plan: processQuery drops segments the query cannot match and runs the plan on the rest
+ * (ServerQueryExecutorV1Impl.java:183-216). Pruners (bit mask; applied in the server's default order,
+ * DefaultHelixStarterServerConfig.java:60-64):
+ *   DATA_SCHEMA   a query column (filter, non-COUNT aggregation, group-by) missing from the segment
+ *                 (DataSchemaSegmentPruner.java:38-41)
+ *   COLUMN_VALUE  EQUALITY / RANGE leaves outside the column's [min, max] (its dictionary's ends); AND prunes when any
+ *                 child does, OR when all do (ColumnValueSegmentPruner.java:49-200). Bloom filters and partition
+ *                 metadata are not in the descriptor: those two tests are not made.
+ *   VALID         an empty segment (ValidSegmentPruner.java:47-58)
+ * A bad literal in an EQUALITY / RANGE leaf is PINOT_ERR_BAD_QUERY (AbstractSegmentPruner.getValue); a query column
+ * the engine left out of a loaded segment (multi-value / raw / BYTES) is PINOT_ERR_UNSUPPORTED; a query whose budget
+ * is already spent (timeout_ms < 0) is PINOT_ERR_TIMEOUT, checked before pruning as processQuery does (:116-126). */
+typedef enum {
+  PINOT_PRUNER_DATA_SCHEMA = 1, PINOT_PRUNER_COLUMN_VALUE = 2, PINOT_PRUNER_VALID = 4,
+  PINOT_PRUNER_DEFAULT = 7
+} pinot_pruner;
+
+/* pruned[i] = 1 when segment i is dropped, else 0; *total_raw_docs = the docs of ALL the segments, pruned or not
+ * (the totalDocs processQuery reports, :214-215). */
+pinot_status pinot_gpu_prune_segments(pinot_engine *engine, const pinot_segment_handle *segments, int32_t num_segments,
+                                      const pinot_query *query, int32_t pruners, uint8_t *pruned,
+                                      int64_t *total_raw_docs);
+/* The same decision for one segment descriptor, on the host only (no engine, no GPU). */
+pinot_status pinot_segment_prune(const pinot_segment_desc *desc, const pinot_query *query, int32_t pruners,
+                                 int32_t *pruned);
+
 /* ------------------------------------------------------------------ DataTable (server -> broker bytes)
  * IntermediateResultsBlock.getDataTable (PC/operator/blocks/IntermediateResultsBlock.java:206-317) serialized as
  * DataTableImplV2.toBytes (PC/common/datatable/DataTableImplV2.java:233-347), object cells per ObjectSerDeUtils
@@ -253,6 +287,24 @@ pinot_status pinot_datatable_group_by(const pinot_query *query, const pinot_grou
                                       const int64_t *const *fn_groups, const int64_t *fn_num_groups,
                                       const pinot_exec_stats *stats, const pinot_datatable_server *server,
                                       const uint8_t **data, uint64_t *len);
+
+/* Every segment pruned (ServerQueryExecutorV1Impl.java:187-196): DataTableBuilder.buildEmptyDataTable (:292-370;
+ * aggregation-only: one row of the functions' empty results, group-by: one empty map per function) with totalDocs
+ * = total_docs and every other statistic 0. Buffer protocol as pinot_datatable_aggregation. */
+pinot_status pinot_datatable_empty(const pinot_query *query, int64_t total_docs, const pinot_datatable_server *server,
+                                   uint8_t *buf, uint64_t buf_len, uint64_t *out_len);
+
+/* ------------------------------------------------------------------ broker reduce
+ * BrokerReduceService.reduceOnDataTable (PC/query/reduce/BrokerReduceService.java:69-270, :347-530) over the
+ * servers' DataTable bytes for an aggregation-only or group-by query (no HAVING, no selection): statistics summed
+ * from the metadata, intermediate results merged per function (group maps by key), final results extracted, the
+ * group-by top_n kept per function (AggregationGroupByTrimmingService.trimFinalResults :123-149: MIN ascending,
+ * others descending; ties by group key) and every value formatted by AggregationFunctionUtils.formatValue
+ * (:113-128, "%1.5f" rounded half-up on the shortest digits). Writes the BrokerResponseNative JSON
+ * (BrokerResponseNative.java:42 field order; timeUsedMs 0, numServersQueried / Responded = num_tables). Buffer
+ * protocol as pinot_datatable_aggregation. */
+pinot_status pinot_broker_reduce(const pinot_query *query, int32_t num_tables, const uint8_t *const *tables,
+                                 const uint64_t *lens, int32_t top_n, char *buf, uint64_t buf_len, uint64_t *out_len);
 
 /* ------------------------------------------------------------------ multi-GPU partials
  * Group-by over a GLOBAL dense key space, for segment sharding across ranks: each rank
@@ -319,6 +371,10 @@ pinot_status pinot_gpu_server_aggregate(pinot_server *server, const pinot_segmen
                                         const pinot_query *query, pinot_agg_result *out, pinot_exec_stats *stats);
 pinot_status pinot_gpu_server_group_by(pinot_server *server, const pinot_segment_ref *segments, int32_t num_segments,
                                        const pinot_query *query, pinot_groupby_result **out, pinot_exec_stats *stats);
+/* pinot_gpu_prune_segments over segments spread across the server's engines. */
+pinot_status pinot_gpu_server_prune_segments(pinot_server *server, const pinot_segment_ref *segments,
+                                             int32_t num_segments, const pinot_query *query, int32_t pruners,
+                                             uint8_t *pruned, int64_t *total_raw_docs);
 
 /* ------------------------------------------------------------------ benchmark tooling
  * NOT part of the Java drop-in path: builds a synthetic dictionary-encoded column

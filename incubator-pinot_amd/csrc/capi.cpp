@@ -203,6 +203,7 @@ pinot_status pinot_gpu_segment_load(pinot_engine *engine, const char *index_dir,
     std::lock_guard<std::mutex> lk(engine->mu);
     set_device(*engine);
     auto seg = register_segment(*engine, desc);
+    seg->unserved = files.skipped;
     const int64_t h = engine->next_handle++;
     engine->segments[h] = std::move(seg);
     *out = h;
@@ -374,6 +375,68 @@ pinot_status pinot_datatable_group_by(const pinot_query *query, const pinot_grou
   });
 }
 
+pinot_status pinot_datatable_empty(const pinot_query *query, int64_t total_docs, const pinot_datatable_server *server,
+                                   uint8_t *buf, uint64_t buf_len, uint64_t *out_len) {
+  return guard([&] {
+    require(out_len != nullptr, PINOT_ERR_BAD_ARG, "null argument");
+    check_query(query);
+    const std::vector<uint8_t> b = empty_datatable(*query, total_docs, server);
+    *out_len = b.size();
+    if (!buf) return;
+    require(buf_len >= b.size(), PINOT_ERR_BAD_ARG, "DataTable buffer too small");
+    memcpy(buf, b.data(), b.size());
+  });
+}
+
+pinot_status pinot_broker_reduce(const pinot_query *query, int32_t num_tables, const uint8_t *const *tables,
+                                 const uint64_t *lens, int32_t top_n, char *buf, uint64_t buf_len, uint64_t *out_len) {
+  return guard([&] {
+    require(out_len != nullptr && num_tables >= 0 && (num_tables == 0 || (tables && lens)), PINOT_ERR_BAD_ARG,
+            "null argument");
+    check_query(query);
+    const std::string j = broker_reduce(*query, num_tables, tables, lens, top_n);
+    *out_len = j.size();
+    if (!buf) return;
+    require(buf_len >= j.size(), PINOT_ERR_BAD_ARG, "response buffer too small");
+    memcpy(buf, j.data(), j.size());
+  });
+}
+
+pinot_status pinot_gpu_prune_segments(pinot_engine *engine, const pinot_segment_handle *segments, int32_t num_segments,
+                                      const pinot_query *query, int32_t pruners, uint8_t *pruned,
+                                      int64_t *total_raw_docs) {
+  return guard([&] {
+    require(engine && pruned, PINOT_ERR_BAD_ARG, "null argument");
+    require(num_segments >= 0 && (num_segments == 0 || segments), PINOT_ERR_BAD_ARG, "segments");
+    check_query(query);
+    // processQuery checks the scheduling wait against the budget before it prunes (:116-126)
+    require(query->timeout_ms >= 0, PINOT_ERR_TIMEOUT, "query budget already spent before execution");
+    std::unique_ptr<FilterTreeInput> tree;
+    if (query->num_filter_nodes > 0)
+      tree = std::make_unique<FilterTreeInput>(decode_filter(query->num_filter_nodes, query->filter));
+    std::lock_guard<std::mutex> lk(engine->mu);
+    int64_t total = 0;
+    for (int32_t i = 0; i < num_segments; i++) {
+      const SegmentData &s = engine->seg(segments[i]);
+      total += s.num_docs;
+      pruned[i] = prune_segment(s, *query, tree.get(), pruners) ? 1 : 0;
+    }
+    if (total_raw_docs) *total_raw_docs = total;
+  });
+}
+
+pinot_status pinot_segment_prune(const pinot_segment_desc *desc, const pinot_query *query, int32_t pruners,
+                                 int32_t *pruned) {
+  return guard([&] {
+    require(desc && pruned, PINOT_ERR_BAD_ARG, "null argument");
+    check_query(query);
+    std::unique_ptr<FilterTreeInput> tree;
+    if (query->num_filter_nodes > 0)
+      tree = std::make_unique<FilterTreeInput>(decode_filter(query->num_filter_nodes, query->filter));
+    *pruned = prune_segment_desc(*desc, *query, tree.get(), pruners) ? 1 : 0;
+  });
+}
+
 pinot_status pinot_groupby_raw_keys(const pinot_groupby_result *r, int64_t *keys) {
   return guard([&] {
     require(r && keys, PINOT_ERR_BAD_ARG, "null argument");
@@ -516,6 +579,31 @@ pinot_status pinot_gpu_server_group_by(pinot_server *server, const pinot_segment
     auto *res = new pinot_groupby_result();
     static_cast<GroupByResult &>(*res) = std::move(*r);
     *out = res;
+  });
+}
+
+pinot_status pinot_gpu_server_prune_segments(pinot_server *server, const pinot_segment_ref *segments,
+                                             int32_t num_segments, const pinot_query *query, int32_t pruners,
+                                             uint8_t *pruned, int64_t *total_raw_docs) {
+  return guard([&] {
+    require(server && server->impl && pruned, PINOT_ERR_BAD_ARG, "null argument");
+    check_query(query);
+    require(query->timeout_ms >= 0, PINOT_ERR_TIMEOUT, "query budget already spent before execution");
+    const std::vector<SegmentRef> refs = server_refs(segments, num_segments);
+    std::unique_ptr<FilterTreeInput> tree;
+    if (query->num_filter_nodes > 0)
+      tree = std::make_unique<FilterTreeInput>(decode_filter(query->num_filter_nodes, query->filter));
+    const int32_t ne = server_num_engines(*server->impl);
+    int64_t total = 0;
+    for (size_t i = 0; i < refs.size(); i++) {
+      require(refs[i].engine >= 0 && refs[i].engine < ne, PINOT_ERR_BAD_ARG, "segment ref: no such engine");
+      Engine &e = *static_cast<Engine *>(server_engine(*server->impl, refs[i].engine));
+      std::lock_guard<std::mutex> lk(e.mu);
+      const SegmentData &s = e.seg(refs[i].handle);
+      total += s.num_docs;
+      pruned[i] = prune_segment(s, *query, tree.get(), pruners) ? 1 : 0;
+    }
+    if (total_raw_docs) *total_raw_docs = total;
   });
 }
 

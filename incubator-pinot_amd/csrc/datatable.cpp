@@ -316,4 +316,41 @@ std::vector<uint8_t> group_by_datatable(const pinot_query &q, const GroupByResul
   return table_bytes(t);
 }
 
+std::vector<uint8_t> empty_datatable(const pinot_query &q, int64_t total_docs, const pinot_datatable_server *srv) {
+  // processQuery with every segment pruned (ServerQueryExecutorV1Impl.java:187-196): buildEmptyDataTable then
+  // totalDocs and zero statistics. The keys go in as totalDocs, numDocsScanned, ... there; none of them shares a
+  // 16-slot HashMap bucket with another except numSegmentsProcessed / numSegmentsMatched, which keep their relative
+  // order, so attach_metadata's order writes the same bytes.
+  pinot_exec_stats s{};
+  s.num_total_raw_docs = total_docs;
+  if (q.num_group_by == 0) {
+    // aggregation-only (:331-369): extractAggregationResult(createAggregationResultHolder()) per function
+    std::vector<pinot_agg_result> r((size_t)q.num_aggregations);
+    for (int i = 0; i < q.num_aggregations; i++) {
+      memset(&r[i], 0, sizeof(r[i]));
+      if (q.aggregations[i].function == PINOT_AGG_MIN) r[i].value = INFINITY;    // MinAggregationFunction.java:32
+      if (q.aggregations[i].function == PINOT_AGG_MAX) r[i].value = -INFINITY;   // MaxAggregationFunction.java:32
+    }
+    return aggregation_datatable(q, r.data(), s, srv);
+  }
+  // group-by (:314-329): per function its column name and an empty HashMap
+  Table t;
+  t.rows = q.num_aggregations;
+  t.cols = 2;
+  schema_bytes(t.schema, {"functionName", "GroupByResultMap"}, {"STRING", "OBJECT"});
+  std::vector<std::string> fn_names;
+  for (int i = 0; i < q.num_aggregations; i++) {
+    const std::string name = aggregation_column_name(q.aggregations[i]);
+    int32_t id = (int32_t)fn_names.size();
+    for (size_t k = 0; k < fn_names.size(); k++)
+      if (fn_names[k] == name) id = (int32_t)k;
+    if (id == (int32_t)fn_names.size()) fn_names.push_back(name);
+    t.fixed.i32(id);
+    object_cell(t, OBJ_MAP, [](Out &v) { v.i32(0); });
+  }
+  t.dictionaries.emplace_back("functionName", fn_names);
+  attach_metadata(t, s, false, srv);
+  return table_bytes(t);
+}
+
 }  // namespace pinot

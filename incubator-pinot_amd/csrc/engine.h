@@ -91,6 +91,7 @@ struct SegmentData {
   int32_t num_docs = 0;
   std::vector<std::unique_ptr<ColumnData>> cols;
   std::unordered_map<std::string, int> by_name;
+  std::vector<std::string> unserved;  // columns the segment has but the engine does not serve (loader's left-outs)
   uint64_t device_bytes = 0;
 
   ColumnData *column(const std::string &n) const {
@@ -131,6 +132,21 @@ struct FilterTreeInput {  // decoded pinot_filter_node (postfix) as a tree
 
 FilterTreeInput decode_filter(int32_t n, const pinot_filter_node *nodes);
 FilterNode plan_filter(const SegmentData &seg, const FilterTreeInput *tree);
+
+// Literals as FieldSpec.DataType.convert reads them (Integer/Long.valueOf, Float/Double.valueOf) and RANGE strings
+// as RangePredicate splits them (planner.cpp).
+int64_t java_parse_integer(const std::string &s, int64_t lo, int64_t hi);
+double java_parse_double(const std::string &raw, bool as_float = false);
+struct RangeBounds {
+  std::string lower, upper;  // "*" = unbounded
+  bool inc_lower = true, inc_upper = true;
+};
+RangeBounds parse_range(const std::string &value);
+
+// Segment pruning before the plan (pruner.cpp): SegmentPrunerService.prune with the pruners of `mask`
+// (PINOT_PRUNER_* bits), applied in the server's default order.
+bool prune_segment(const SegmentData &s, const pinot_query &q, const FilterTreeInput *tree, int32_t mask);
+bool prune_segment_desc(const pinot_segment_desc &d, const pinot_query &q, const FilterTreeInput *tree, int32_t mask);
 
 // ------------------------------------------------------------------ engine
 struct Engine {
@@ -265,7 +281,13 @@ std::vector<uint8_t> aggregation_datatable(const pinot_query &q, const pinot_agg
                                            const pinot_datatable_server *srv);
 std::vector<uint8_t> group_by_datatable(const pinot_query &q, const GroupByResult &r, const int64_t *const *fn_groups,
                                         const int64_t *fn_num_groups, const pinot_exec_stats &s,
-                                        const pinot_datatable_server *srv);std::unique_ptr<GroupByResult> exec_group_by(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q,
+                                        const pinot_datatable_server *srv);
+// DataTableBuilder.buildEmptyDataTable + the metadata processQuery puts on it when every segment was pruned
+std::vector<uint8_t> empty_datatable(const pinot_query &q, int64_t total_docs, const pinot_datatable_server *srv);
+// BrokerReduceService over the servers' DataTable bytes -> BrokerResponseNative JSON (broker.cpp)
+std::string broker_reduce(const pinot_query &q, int32_t n, const uint8_t *const *tables, const uint64_t *lens,
+                          int32_t top_n);
+std::unique_ptr<GroupByResult> exec_group_by(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q,
                                              pinot_exec_stats *stats);
 
 // multi-GPU partials

@@ -19,8 +19,6 @@
 
 namespace pinot {
 
-namespace {
-
 // Integer.parseInt / Long.parseLong: optional sign, decimal digits, range-checked.
 int64_t java_parse_integer(const std::string &s, int64_t lo, int64_t hi) {
   require(!s.empty(), PINOT_ERR_BAD_QUERY, "NumberFormatException: empty literal");
@@ -42,22 +40,63 @@ int64_t java_parse_integer(const std::string &s, int64_t lo, int64_t hi) {
   return (int64_t)v;
 }
 
-// Double.parseDouble / Float.parseFloat (leading/trailing whitespace allowed, optional f/F/d/D suffix).
-double java_parse_double(const std::string &raw) {
+// Double.parseDouble / Float.parseFloat (leading/trailing whitespace allowed, optional f/F/d/D suffix). as_float:
+// the decimal rounded straight to float (strtof), as Float.parseFloat does, not through a double.
+double java_parse_double(const std::string &raw, bool as_float) {
   size_t b = raw.find_first_not_of(" \t\n\r\f\v");
   size_t e = raw.find_last_not_of(" \t\n\r\f\v");
   require(b != std::string::npos, PINOT_ERR_BAD_QUERY, "NumberFormatException: empty literal");
   std::string s = raw.substr(b, e - b + 1);
-  if (!s.empty() && (s.back() == 'f' || s.back() == 'F' || s.back() == 'd' || s.back() == 'D')) s.pop_back();
-  if (s == "NaN") return NAN;
-  if (s == "Infinity" || s == "+Infinity") return INFINITY;
-  if (s == "-Infinity") return -INFINITY;
+  const std::string bad = "NumberFormatException: For input string: \"" + raw + "\"";
+  const size_t sign = (s[0] == '+' || s[0] == '-') ? 1 : 0;
+  const bool neg = s[0] == '-';
+  if (s.compare(sign, std::string::npos, "NaN") == 0) return NAN;
+  if (s.compare(sign, std::string::npos, "Infinity") == 0) return neg ? -INFINITY : INFINITY;
+  if (s.back() == 'f' || s.back() == 'F' || s.back() == 'd' || s.back() == 'D') s.pop_back();
+  // FloatingDecimal.readJavaFormatString's decimal grammar: digits [. digits] (a digit somewhere) [e|E [+|-] digits].
+  // Hexadecimal literals and C's "inf" / "nan" spellings are not accepted (strtod alone would take them).
+  size_t i = sign, digits = 0;
+  while (i < s.size() && s[i] >= '0' && s[i] <= '9') i++, digits++;
+  if (i < s.size() && s[i] == '.') {
+    i++;
+    while (i < s.size() && s[i] >= '0' && s[i] <= '9') i++, digits++;
+  }
+  require(digits > 0, PINOT_ERR_BAD_QUERY, bad);
+  if (i < s.size() && (s[i] == 'e' || s[i] == 'E')) {
+    i++;
+    if (i < s.size() && (s[i] == '+' || s[i] == '-')) i++;
+    size_t ed = 0;
+    while (i < s.size() && s[i] >= '0' && s[i] <= '9') i++, ed++;
+    require(ed > 0, PINOT_ERR_BAD_QUERY, bad);
+  }
+  require(i == s.size(), PINOT_ERR_BAD_QUERY, bad);
   char *end = nullptr;
   errno = 0;
-  double v = std::strtod(s.c_str(), &end);
-  require(end && *end == 0 && !s.empty(), PINOT_ERR_BAD_QUERY, "NumberFormatException: For input string: \"" + raw + "\"");
+  // correctly rounded, like FloatingDecimal; overflow -> +-inf
+  const double v = as_float ? (double)std::strtof(s.c_str(), &end) : std::strtod(s.c_str(), &end);
+  require(end && *end == 0, PINOT_ERR_BAD_QUERY, bad);
   return v;
 }
+
+// RangePredicate(lhs, rhs) (PC/common/predicate/RangePredicate.java:41-67): "(lo\t\thi]" with "*" for unbounded;
+// "(" / ")" exclusive unless that bound is "*".
+RangeBounds parse_range(const std::string &value) {
+  std::string s = value;
+  size_t b = s.find_first_not_of(" \t\n\r");
+  size_t e = s.find_last_not_of(" \t\n\r");
+  require(b != std::string::npos, PINOT_ERR_BAD_QUERY, "empty RANGE");
+  s = s.substr(b, e - b + 1);
+  size_t d = s.find("\t\t");
+  require(d != std::string::npos && s.size() >= 2, PINOT_ERR_BAD_QUERY, "malformed RANGE: " + s);
+  RangeBounds r;
+  r.lower = s.substr(1, d - 1);
+  r.upper = s.substr(d + 2, s.size() - d - 3);
+  r.inc_lower = !(s[0] == '(') || r.lower == "*";
+  r.inc_upper = !(s.back() == ')') || r.upper == "*";
+  return r;
+}
+
+namespace {
 
 // Returns insertionIndexOf(raw): index if found, else -(insertion point + 1).
 int64_t insertion_index_of(const ColumnData &c, const std::string &raw) {
@@ -82,7 +121,7 @@ int64_t insertion_index_of(const ColumnData &c, const std::string &raw) {
       return search([&](int64_t m) { return c.dict_int[m] < v ? -1 : c.dict_int[m] > v ? 1 : 0; });
     }
     case PINOT_FLOAT: {
-      const double v = (double)(float)java_parse_double(raw);  // compared as float
+      const double v = java_parse_double(raw, true);  // compared as float
       return search([&](int64_t m) { return c.dict_dbl[m] < v ? -1 : c.dict_dbl[m] > v ? 1 : 0; });
     }
     case PINOT_DOUBLE: {
@@ -194,18 +233,9 @@ Evaluator make_evaluator(const ColumnData &c, int op, const std::vector<std::str
     }
     case PINOT_FILTER_RANGE: {
       ev.kind = Evaluator::RANGE;
-      // RangePredicate: "(lo\t\thi]" with "*" for unbounded; "(" / ")" exclusive unless the bound is "*"
-      std::string s = values[0];
-      size_t b = s.find_first_not_of(" \t\n\r");
-      size_t e = s.find_last_not_of(" \t\n\r");
-      require(b != std::string::npos, PINOT_ERR_BAD_QUERY, "empty RANGE");
-      s = s.substr(b, e - b + 1);
-      size_t d = s.find("\t\t");
-      require(d != std::string::npos && s.size() >= 2, PINOT_ERR_BAD_QUERY, "malformed RANGE: " + s);
-      const std::string lower = s.substr(1, d - 1);
-      const std::string upper = s.substr(d + 2, s.size() - d - 3);
-      const bool inc_lower = !(s[0] == '(') || lower == "*";
-      const bool inc_upper = !(s.back() == ')') || upper == "*";
+      const RangeBounds rb = parse_range(values[0]);
+      const std::string &lower = rb.lower, &upper = rb.upper;
+      const bool inc_lower = rb.inc_lower, inc_upper = rb.inc_upper;
       int64_t start, end;
       if (lower == "*") {
         start = 0;

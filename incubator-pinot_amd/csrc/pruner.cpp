@@ -1,0 +1,252 @@
+// Segment pruning, the step ServerQueryExecutorV1Impl.processQuery runs before planning
+// (PC/query/executor/ServerQueryExecutorV1Impl.java:183-216 and pruneSegments :270-294). PC = pinot-core/src/main/
+// java/org/apache/pinot/core. SegmentPrunerService.prune (PC/query/pruner/SegmentPrunerService.java:52-60) asks each
+// configured pruner in turn and drops the segment at the first "true"; the server's default list
+// (pinot-server/.../DefaultHelixStarterServerConfig.java:60-64) is restated here in that order:
+//   DataSchemaSegmentPruner   (PC/query/pruner/DataSchemaSegmentPruner.java:38-41): a query column the segment lacks
+//   ColumnValueSegmentPruner  (PC/query/pruner/ColumnValueSegmentPruner.java:49-200, AbstractSegmentPruner.java:56-105):
+//                             EQUALITY / RANGE leaves against the column's min / max value; AND prunes when any
+//                             child does, OR when every child does; other leaves never prune
+//   ValidSegmentPruner        (PC/query/pruner/ValidSegmentPruner.java:47-58): an empty segment
+// Not restated: the bloom-filter test inside ColumnValueSegmentPruner and PartitionSegmentPruner — a
+// pinot_segment_desc carries neither bloom filters nor partition metadata. Both only ever drop segments whose filter
+// matches no doc, so results are unchanged; only numSegmentsProcessed can differ.
+//
+// Min / max: the dictionary's first and last entries. Dictionaries are sorted, and the segment creator writes
+// column.<c>.minValue / maxValue from the same sorted values (ColumnMetadata.java:155-156).
+#include <cmath>
+#include <cstring>
+
+#include "engine.h"
+
+namespace pinot {
+namespace {
+
+// A column's type and value range, as ColumnMetadata exposes them to the pruner.
+struct ColumnRange {
+  int data_type = PINOT_INT;
+  bool has_range = false;  // minValue / maxValue present (a non-empty dictionary)
+  int64_t imin = 0, imax = 0;
+  double dmin = 0, dmax = 0;
+  std::string smin, smax;
+};
+
+// A literal of the column's type (AbstractSegmentPruner.getValue -> FieldSpec.DataType.convert; a bad literal is a
+// BadQueryRequestException).
+struct Literal {
+  int64_t i = 0;
+  double d = 0;
+  std::string s;
+};
+
+Literal convert(const ColumnRange &c, const std::string &raw) {
+  Literal v;
+  switch (c.data_type) {
+    case PINOT_INT: v.i = java_parse_integer(raw, INT32_MIN, INT32_MAX); break;
+    case PINOT_LONG: v.i = java_parse_integer(raw, INT64_MIN, INT64_MAX); break;
+    case PINOT_FLOAT: v.d = java_parse_double(raw, true); break;  // Float.valueOf
+    case PINOT_DOUBLE: v.d = java_parse_double(raw); break;
+    default: v.s = raw; break;
+  }
+  return v;
+}
+
+// Double.compare / Float.compare: NaN above everything (and equal to itself), -0.0 below 0.0.
+int java_double_compare(double a, double b) {
+  if (a < b) return -1;
+  if (a > b) return 1;
+  const bool an = std::isnan(a), bn = std::isnan(b);
+  if (an || bn) return an == bn ? 0 : (an ? 1 : -1);
+  const bool as = std::signbit(a), bs = std::signbit(b);
+  return as == bs ? 0 : (as ? -1 : 1);
+}
+
+// Comparable.compareTo on the column's type. STRING: byte order of the UTF-8 values, which is String.compareTo's
+// order except between supplementary characters and U+E000..U+FFFF (the planner's dictionary search has the same
+// convention).
+int compare(const ColumnRange &c, const Literal &a, const Literal &b) {
+  switch (c.data_type) {
+    case PINOT_INT:
+    case PINOT_LONG: return a.i < b.i ? -1 : a.i > b.i ? 1 : 0;
+    case PINOT_FLOAT:
+    case PINOT_DOUBLE: return java_double_compare(a.d, b.d);
+    default: {
+      const int r = a.s.compare(b.s);
+      return r < 0 ? -1 : r > 0 ? 1 : 0;
+    }
+  }
+}
+
+Literal range_min(const ColumnRange &c) { return Literal{c.imin, c.dmin, c.smin}; }
+Literal range_max(const ColumnRange &c) { return Literal{c.imax, c.dmax, c.smax}; }
+
+template <typename Lookup>
+bool prune_tree(const FilterTreeInput &t, const Lookup &lookup) {
+  if (t.op == PINOT_FILTER_AND || t.op == PINOT_FILTER_OR) {  // pruneNonLeaf (AbstractSegmentPruner.java:56-90)
+    if (t.children.empty()) return false;
+    if (t.op == PINOT_FILTER_AND) {
+      for (const auto &c : t.children)
+        if (prune_tree(c, lookup)) return true;
+      return false;
+    }
+    for (const auto &c : t.children)
+      if (!prune_tree(c, lookup)) return false;
+    return true;
+  }
+  if (t.op != PINOT_FILTER_EQUALITY && t.op != PINOT_FILTER_RANGE) return false;
+  ColumnRange c;
+  if (!lookup(t.column, c)) return true;  // "Should not reach here after DataSchemaSegmentPruner"
+  require(!t.values.empty(), PINOT_ERR_BAD_QUERY, "predicate on " + t.column + " has no value");
+  if (t.op == PINOT_FILTER_EQUALITY) {
+    const Literal v = convert(c, t.values[0]);
+    if (!c.has_range) return false;
+    return compare(c, v, range_min(c)) < 0 || compare(c, v, range_max(c)) > 0;
+  }
+  const RangeBounds rb = parse_range(t.values[0]);
+  const bool has_lo = rb.lower != "*", has_hi = rb.upper != "*";
+  Literal lo, hi;
+  if (has_lo) lo = convert(c, rb.lower);
+  if (has_hi) hi = convert(c, rb.upper);
+  if (has_lo && has_hi) {  // an empty range prunes whatever the segment holds
+    const int r = compare(c, lo, hi);
+    if (rb.inc_lower && rb.inc_upper ? r > 0 : r >= 0) return true;
+  }
+  if (!c.has_range) return false;
+  if (has_lo) {
+    const int r = compare(c, lo, range_max(c));
+    if (rb.inc_lower ? r > 0 : r >= 0) return true;
+  }
+  if (has_hi) {
+    const int r = compare(c, hi, range_min(c));
+    if (rb.inc_upper ? r < 0 : r <= 0) return true;
+  }
+  return false;
+}
+
+void filter_columns(const FilterTreeInput &t, std::vector<std::string> &out) {
+  if (t.op == PINOT_FILTER_AND || t.op == PINOT_FILTER_OR) {
+    for (const auto &c : t.children) filter_columns(c, out);
+  } else {
+    out.push_back(t.column);
+  }
+}
+
+// ServerQueryRequest.getAllColumns (PC/query/request/ServerQueryRequest.java:81-133): filter columns, the columns
+// of every aggregation except COUNT, group-by columns.
+std::vector<std::string> query_columns(const pinot_query &q, const FilterTreeInput *tree) {
+  std::vector<std::string> cols;
+  if (tree) filter_columns(*tree, cols);
+  for (int i = 0; i < q.num_aggregations; i++)
+    if (q.aggregations[i].function != PINOT_AGG_COUNT && q.aggregations[i].column)
+      cols.emplace_back(q.aggregations[i].column);
+  for (int i = 0; i < q.num_group_by; i++)
+    if (q.group_by[i]) cols.emplace_back(q.group_by[i]);
+  return cols;
+}
+
+template <typename Has, typename Lookup>
+bool prune_with(int32_t num_docs, const pinot_query &q, const FilterTreeInput *tree, int32_t mask, const Has &has,
+                const Lookup &lookup) {
+  if (mask & PINOT_PRUNER_DATA_SCHEMA)
+    for (const auto &c : query_columns(q, tree))
+      if (!has(c)) return true;
+  if ((mask & PINOT_PRUNER_COLUMN_VALUE) && tree && prune_tree(*tree, lookup)) return true;
+  if ((mask & PINOT_PRUNER_VALID) && num_docs == 0) return true;
+  return false;
+}
+
+uint64_t load_be(const uint8_t *p, int n) {
+  uint64_t v = 0;
+  for (int k = 0; k < n; k++) v = (v << 8) | p[k];
+  return v;
+}
+
+}  // namespace
+
+bool prune_segment(const SegmentData &s, const pinot_query &q, const FilterTreeInput *tree, int32_t mask) {
+  auto has = [&](const std::string &name) {
+    if (s.by_name.count(name)) return true;
+    for (const auto &u : s.unserved)
+      require(u != name, PINOT_ERR_UNSUPPORTED, "column " + name + " is multi-value / raw / BYTES: not served");
+    return false;
+  };
+  auto lookup = [&](const std::string &name, ColumnRange &c) {
+    auto it = s.by_name.find(name);
+    if (it == s.by_name.end()) return false;
+    const ColumnData &cd = *s.cols[it->second];
+    c.data_type = cd.data_type;
+    c.has_range = cd.card >= 1;
+    if (!c.has_range) return true;
+    const int32_t last = cd.card - 1;
+    switch (cd.data_type) {
+      case PINOT_INT:
+      case PINOT_LONG: c.imin = cd.dict_int[0]; c.imax = cd.dict_int[last]; break;
+      case PINOT_FLOAT:
+      case PINOT_DOUBLE: c.dmin = cd.dict_dbl[0]; c.dmax = cd.dict_dbl[last]; break;
+      default: c.smin = cd.dict_str[0]; c.smax = cd.dict_str[last]; break;
+    }
+    return true;
+  };
+  return prune_with(s.num_docs, q, tree, mask, has, lookup);
+}
+
+bool prune_segment_desc(const pinot_segment_desc &d, const pinot_query &q, const FilterTreeInput *tree, int32_t mask) {
+  require(d.num_columns >= 0 && (d.num_columns == 0 || d.columns != nullptr), PINOT_ERR_BAD_ARG, "segment columns");
+  auto find = [&](const std::string &name) -> const pinot_column_desc * {
+    for (int32_t i = 0; i < d.num_columns; i++)
+      if (d.columns[i].name && name == d.columns[i].name) return &d.columns[i];
+    return nullptr;
+  };
+  auto has = [&](const std::string &name) { return find(name) != nullptr; };
+  auto lookup = [&](const std::string &name, ColumnRange &c) {
+    const pinot_column_desc *cd = find(name);
+    if (!cd) return false;
+    c.data_type = cd->data_type;
+    const int w = cd->data_type == PINOT_INT || cd->data_type == PINOT_FLOAT ? 4
+                  : cd->data_type == PINOT_STRING ? cd->string_width : 8;
+    require(cd->data_type >= PINOT_INT && cd->data_type <= PINOT_STRING, PINOT_ERR_BAD_ARG, name + ": data type");
+    c.has_range = cd->cardinality >= 1 && w >= 1 && cd->dictionary &&
+                  cd->dictionary_len >= (uint64_t)cd->cardinality * (uint64_t)w;
+    if (!c.has_range) return true;
+    const uint8_t *first = cd->dictionary, *last = cd->dictionary + (size_t)(cd->cardinality - 1) * w;
+    switch (cd->data_type) {
+      case PINOT_INT:
+        c.imin = (int32_t)(uint32_t)load_be(first, 4);
+        c.imax = (int32_t)(uint32_t)load_be(last, 4);
+        break;
+      case PINOT_LONG:
+        c.imin = (int64_t)load_be(first, 8);
+        c.imax = (int64_t)load_be(last, 8);
+        break;
+      case PINOT_FLOAT: {
+        const uint32_t a = (uint32_t)load_be(first, 4), b = (uint32_t)load_be(last, 4);
+        float fa, fb;
+        memcpy(&fa, &a, 4);
+        memcpy(&fb, &b, 4);
+        c.dmin = fa;
+        c.dmax = fb;
+        break;
+      }
+      case PINOT_DOUBLE: {
+        const uint64_t a = load_be(first, 8), b = load_be(last, 8);
+        memcpy(&c.dmin, &a, 8);
+        memcpy(&c.dmax, &b, 8);
+        break;
+      }
+      default: {  // getUnpaddedString: up to the first padding byte
+        auto unpad = [&](const uint8_t *p) {
+          size_t n = 0;
+          while (n < (size_t)w && p[n] != (uint8_t)cd->padding_byte) n++;
+          return std::string(reinterpret_cast<const char *>(p), n);
+        };
+        c.smin = unpad(first);
+        c.smax = unpad(last);
+        break;
+      }
+    }
+    return true;
+  };
+  return prune_with(d.num_docs, q, tree, mask, has, lookup);
+}
+
+}  // namespace pinot

@@ -16,6 +16,9 @@ PINOT_ERR_TIMEOUT = 6
 DATA_TYPE = {"INT": 0, "LONG": 1, "FLOAT": 2, "DOUBLE": 3, "STRING": 4}
 FILTER_OP = {"AND": 0, "OR": 1, "EQUALITY": 2, "NOT": 3, "RANGE": 4, "IN": 5, "NOT_IN": 6}
 AGG_FN = {"COUNT": 0, "SUM": 1, "MIN": 2, "MAX": 3, "AVG": 4, "DISTINCTCOUNTHLL": 5}
+# pinot_pruner bits; the server's default list (DefaultHelixStarterServerConfig.java:60-64)
+PRUNER = {"DataSchemaSegmentPruner": 1, "ColumnValueSegmentPruner": 2, "ValidSegmentPruner": 4}
+PRUNER_DEFAULT = 7
 
 # every symbol include/pinot_gpu.h declares (checked by tests/test_abi.py)
 EXPORTED_SYMBOLS = [
@@ -26,7 +29,8 @@ EXPORTED_SYMBOLS = [
     "pinot_gpu_segment_device_bytes", "pinot_gpu_filter", "pinot_gpu_aggregate", "pinot_gpu_group_by",
     "pinot_groupby_num_groups", "pinot_groupby_num_columns", "pinot_groupby_key", "pinot_groupby_values",
     "pinot_groupby_hll", "pinot_groupby_raw_keys", "pinot_groupby_export_keys", "pinot_groupby_trim",
-    "pinot_groupby_free", "pinot_datatable_aggregation", "pinot_datatable_group_by",
+    "pinot_groupby_free", "pinot_datatable_aggregation", "pinot_datatable_group_by", "pinot_datatable_empty",
+    "pinot_gpu_prune_segments", "pinot_segment_prune", "pinot_gpu_server_prune_segments", "pinot_broker_reduce",
     "pinot_gpu_group_by_layout", "pinot_gpu_group_by_partial", "pinot_gpu_group_by_finalize",
     "pinot_gpu_segment_register_synthetic", "pinot_gpu_segment_register_synthetic_ex", "pinot_gpu_synchronize",
     "pinot_gpu_last_kernel_ms",
@@ -166,6 +170,13 @@ def load(path=None):
                                               P, u64, C.POINTER(u64)]),
         "pinot_datatable_group_by": (i32, [C.POINTER(Query), P, P, P, C.POINTER(ExecStats),
                                            C.POINTER(DataTableServer), C.POINTER(P), C.POINTER(u64)]),
+        "pinot_datatable_empty": (i32, [C.POINTER(Query), i64, C.POINTER(DataTableServer), P, u64, C.POINTER(u64)]),
+        "pinot_gpu_prune_segments": (i32, [P, C.POINTER(i64), i32, C.POINTER(Query), i32, P, C.POINTER(i64)]),
+        "pinot_segment_prune": (i32, [C.POINTER(SegmentDesc), C.POINTER(Query), i32, C.POINTER(i32)]),
+        "pinot_gpu_server_prune_segments": (i32, [P, C.POINTER(SegmentRef), i32, C.POINTER(Query), i32, P,
+                                                  C.POINTER(i64)]),
+        "pinot_broker_reduce": (i32, [C.POINTER(Query), i32, C.POINTER(P), C.POINTER(u64), i32, P, u64,
+                                      C.POINTER(u64)]),
         "pinot_groupby_free": (None, [P]),
         "pinot_gpu_group_by_layout": (i32, [P, C.POINTER(i64), i32, C.POINTER(Query), C.POINTER(PartialLayout)]),
         "pinot_gpu_group_by_partial": (i32, [P, C.POINTER(i64), i32, C.POINTER(Query), P, C.POINTER(P),

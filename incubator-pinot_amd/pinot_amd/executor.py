@@ -122,6 +122,49 @@ def validate_segment(seg: Segment) -> None:
     check(lib.pinot_gpu_segment_validate(C.byref(desc)))
 
 
+def prune_segment(seg: Segment, query, pruners=_lib.PRUNER_DEFAULT) -> bool:
+    """pinot_segment_prune: SegmentPrunerService.prune for one segment, on the host alone (no engine, no GPU)."""
+    lib = _lib.load()
+    if isinstance(query, str):
+        query = compile_pql(query)
+    desc, _keep = segment_desc(seg)
+    m = QueryMarshal(query)
+    out = C.c_int32()
+    check(lib.pinot_segment_prune(C.byref(desc), C.byref(m.q), int(pruners), C.byref(out)))
+    return bool(out.value)
+
+
+def empty_datatable(query, total_docs, server=None, num_groups_limit=100000):
+    """pinot_datatable_empty: the DataTable processQuery answers when every segment was pruned."""
+    lib = _lib.load()
+    if isinstance(query, str):
+        query = compile_pql(query)
+    m = QueryMarshal(query, num_groups_limit)
+    srv = C.byref(_lib.DataTableServer(*server)) if server else None
+    need = C.c_uint64()
+    check(lib.pinot_datatable_empty(C.byref(m.q), int(total_docs), srv, None, 0, C.byref(need)))
+    buf = C.create_string_buffer(max(need.value, 1))
+    check(lib.pinot_datatable_empty(C.byref(m.q), int(total_docs), srv, buf, need.value, C.byref(need)))
+    return buf.raw[:need.value]
+
+
+def _empty_result(query):
+    """The combined result of zero segments: the functions' empty holders (extractAggregationResult of a fresh
+    holder, DataTableBuilder.java:336-343) or an empty group map."""
+    if query.get("group_by"):
+        return {}
+    out = []
+    for a in query["aggregations"]:
+        f = a["function"].upper()
+        out.append({"COUNT": 0, "SUM": 0.0, "MIN": math.inf, "MAX": -math.inf}.get(f) if f not in (
+            "AVG", "DISTINCTCOUNTHLL") else AvgPair(0.0, 0) if f == "AVG" else HyperLogLog(bytes(256), 0))
+    return out
+
+
+def _pruned_stats(total_docs):
+    return ExecutionStatistics(0, 0, 0, total_docs, 0, 0.0, 0.0, 0)
+
+
 class GpuEngine:
     """One engine per HIP device (`QueryExecutor.init/start/shutDown`)."""
 
@@ -416,11 +459,13 @@ class ServerExecutor:
     """`ServerQueryExecutorV1Impl.processQuery` over segments spread across a GpuServer's GPUs: the library runs
     each GPU's share and combines them (pinot_gpu_server_aggregate / _group_by)."""
 
-    def __init__(self, server: GpuServer, num_groups_limit=100000, max_init_group_holder_capacity=10000, timeout_ms=0):
+    def __init__(self, server: GpuServer, num_groups_limit=100000, max_init_group_holder_capacity=10000, timeout_ms=0,
+                 pruners=_lib.PRUNER_DEFAULT):
         self.server = server
         self.num_groups_limit = num_groups_limit
         self.max_init = max_init_group_holder_capacity
         self.timeout_ms = timeout_ms
+        self.pruners = pruners
 
     def _refs(self, segments):
         arr = (_lib.SegmentRef * max(len(segments), 1))()
@@ -437,6 +482,18 @@ class ServerExecutor:
                 query = compile_pql(query)
             m = QueryMarshal(query, self.num_groups_limit, self.max_init, self.timeout_ms)
         lib = self.server.lib
+        total = None
+        if self.pruners:  # ServerQueryExecutorV1Impl.pruneSegments (:270-294)
+            pruned = (C.c_uint8 * max(len(segments), 1))()
+            tdocs = C.c_int64()
+            check(lib.pinot_gpu_server_prune_segments(self.server.ptr, self._refs(segments), len(segments),
+                                                      C.byref(m.q), int(self.pruners), pruned, C.byref(tdocs)))
+            segments = [sg for i, sg in enumerate(segments) if not pruned[i]]
+            total = tdocs.value
+            if not segments:
+                if as_result and query.get("group_by"):
+                    raise _lib.PinotGpuError(1, "every segment was pruned: no group-by result object")
+                return _empty_result(query), _pruned_stats(total)
         refs = self._refs(segments)
         stats = _lib.ExecStats()
         if query.get("group_by"):
@@ -452,6 +509,8 @@ class ServerExecutor:
             check(lib.pinot_gpu_server_aggregate(self.server.ptr, refs, len(segments), C.byref(m.q), out,
                                                  C.byref(stats)))
             res = [_agg_value(a["function"].upper(), out[i]) for i, a in enumerate(query["aggregations"])]
+        if total is not None:  # totalDocs counts the pruned segments too (:214-215)
+            stats.num_total_raw_docs = total
         return res, _stats(stats)
 
     def prepare(self, query):
@@ -475,11 +534,22 @@ class ServerQueryExecutor:
     """`ServerQueryExecutorV1Impl.processQuery` over GPU-resident segments of one engine."""
 
     def __init__(self, engine: GpuEngine, num_groups_limit=100000, max_init_group_holder_capacity=10000,
-                 timeout_ms=0):
+                 timeout_ms=0, pruners=_lib.PRUNER_DEFAULT):
         self.engine = engine
         self.num_groups_limit = num_groups_limit
         self.max_init = max_init_group_holder_capacity
         self.timeout_ms = timeout_ms
+        self.pruners = pruners  # pinot_pruner bits (0 = no pruning); default: the server's default pruner list
+
+    def prune(self, query, segments):
+        """ServerQueryExecutorV1Impl.pruneSegments (:270-294): (segments kept, totalDocs over all of them)."""
+        m = query.marshal if isinstance(query, PreparedQuery) else QueryMarshal(
+            compile_pql(query) if isinstance(query, str) else query)
+        pruned = (C.c_uint8 * max(len(segments), 1))()
+        total = C.c_int64()
+        check(self.engine.lib.pinot_gpu_prune_segments(self.engine.ptr, _segment_handles(segments), len(segments),
+                                                       C.byref(m.q), int(self.pruners), pruned, C.byref(total)))
+        return [sg for i, sg in enumerate(segments) if not pruned[i]], total.value
 
     def prepare(self, query):
         """Compile + marshal a query once (a prepared statement); process_query accepts the result.
@@ -497,6 +567,11 @@ class ServerQueryExecutor:
                 query = compile_pql(query)
             m = QueryMarshal(query, self.num_groups_limit, self.max_init, self.timeout_ms)
         lib = self.engine.lib
+        total = None
+        if self.pruners:
+            segments, total = self.prune(PreparedQuery(query, m), segments)
+            if not segments:  # every segment pruned (:187-196)
+                return _empty_result(query), _pruned_stats(total)
         handles = _segment_handles(segments)
         stats = _lib.ExecStats()
         if query.get("group_by"):
@@ -511,6 +586,8 @@ class ServerQueryExecutor:
             check(lib.pinot_gpu_aggregate(self.engine.ptr, handles, len(segments), C.byref(m.q), out,
                                           C.byref(stats)))
             res = [_agg_value(a["function"].upper(), out[i]) for i, a in enumerate(query["aggregations"])]
+        if total is not None:  # totalDocs counts the pruned segments too (:214-215)
+            stats.num_total_raw_docs = total
         return res, _stats(stats)
 
     def process_query_datatable(self, query, segments, trim=True, server=None):
@@ -525,18 +602,31 @@ class ServerQueryExecutor:
                 query = compile_pql(query)
             m = QueryMarshal(query, self.num_groups_limit, self.max_init, self.timeout_ms)
         lib = self.engine.lib
+        srv = C.byref(_lib.DataTableServer(*server)) if server else None
+        total = None
+        if self.pruners:
+            segments, total = self.prune(PreparedQuery(query, m), segments)
+            if not segments:  # every segment pruned: buildEmptyDataTable (:187-196)
+                need = C.c_uint64()
+                check(lib.pinot_datatable_empty(C.byref(m.q), total, srv, None, 0, C.byref(need)))
+                buf = C.create_string_buffer(max(need.value, 1))
+                check(lib.pinot_datatable_empty(C.byref(m.q), total, srv, buf, need.value, C.byref(need)))
+                return buf.raw[:need.value], _pruned_stats(total)
         handles = _segment_handles(segments)
         stats = _lib.ExecStats()
-        srv = C.byref(_lib.DataTableServer(*server)) if server else None
         if query.get("group_by"):
             out = C.c_void_p()
             check(lib.pinot_gpu_group_by(self.engine.ptr, handles, len(segments), C.byref(m.q), C.byref(out),
                                          C.byref(stats)))
+            if total is not None:
+                stats.num_total_raw_docs = total
             res = GroupByResult(lib, out, query)
             return res.data_table(m, stats, query["group_by"].get("top_n", 10) if trim else None, srv), _stats(stats)
         n = len(query["aggregations"])
         out = (_lib.AggResult * n)()
         check(lib.pinot_gpu_aggregate(self.engine.ptr, handles, len(segments), C.byref(m.q), out, C.byref(stats)))
+        if total is not None:
+            stats.num_total_raw_docs = total
         need = C.c_uint64()
         check(lib.pinot_datatable_aggregation(C.byref(m.q), out, C.byref(stats), srv, None, 0, C.byref(need)))
         buf = C.create_string_buffer(max(need.value, 1))
@@ -629,6 +719,27 @@ def format_value(f, v):
 
 class BrokerReduce:
     """`BrokerReduceService` over several server results of one query."""
+
+    @staticmethod
+    def reduce_datatables(query, tables, top_n=None):
+        """pinot_broker_reduce: BrokerReduceService.reduceOnDataTable over the servers' DataTable bytes, in the
+        library; returns the BrokerResponseNative as a dict (values formatted by AggregationFunctionUtils)."""
+        import json
+        lib = _lib.load()
+        if isinstance(query, str):
+            query = compile_pql(query)
+        if top_n is None:
+            top_n = (query.get("group_by") or {}).get("top_n", 10)
+        m = QueryMarshal(query)
+        n = len(tables)
+        keep = [C.create_string_buffer(bytes(t), max(len(t), 1)) for t in tables]
+        ptrs = (C.c_void_p * max(n, 1))(*[C.cast(b, C.c_void_p) for b in keep])
+        lens = (C.c_uint64 * max(n, 1))(*[len(t) for t in tables])
+        need = C.c_uint64()
+        check(lib.pinot_broker_reduce(C.byref(m.q), n, ptrs, lens, int(top_n), None, 0, C.byref(need)))
+        buf = C.create_string_buffer(max(need.value, 1))
+        check(lib.pinot_broker_reduce(C.byref(m.q), n, ptrs, lens, int(top_n), buf, need.value, C.byref(need)))
+        return json.loads(buf.raw[:need.value].decode("utf-8"))
 
     @staticmethod
     def reduce(query, server_results):

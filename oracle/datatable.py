@@ -9,6 +9,9 @@ pinot_datatable_* bytes. PC = pinot-core/src/main/java/org/apache/pinot/core.
                        DataTableImplV2.toBytes (PC/common/datatable/DataTableImplV2.java:233-347)
   decode               DataTableImplV2(ByteBuffer) (:104-171) + getters (:366-468) + ObjectSerDeUtils.deserialize
                        (PC/common/ObjectSerDeUtils.java:144-330)
+  encode_empty         DataTableBuilder.buildEmptyDataTable (PC/common/datatable/DataTableBuilder.java:292-370) with the
+                       metadata processQuery puts on it when every segment was pruned
+                       (PC/query/executor/ServerQueryExecutorV1Impl.java:187-196), keys in that insertion order
   java_hashmap_order   java.util.HashMap iteration order (String.hashCode / Integer.hashCode, spread h ^ h >>> 16,
                        capacity 16 doubling at load 0.75, insertion order within a bucket)
 
@@ -146,6 +149,77 @@ def encode_aggregation(query, values, stats, server=None):
             var += _i32(typ) + body
     return _table(1, len(aggs), [], metadata(stats, False, server), _schema([column_name(a) for a in aggs], types),
                   fixed, var)
+
+
+def encode_empty(query, total_docs, server=None):
+    md = [("totalDocs", str(total_docs)), ("numDocsScanned", "0"), ("numEntriesScannedInFilter", "0"),
+          ("numEntriesScannedPostFilter", "0"), ("numSegmentsProcessed", "0"), ("numSegmentsMatched", "0")]
+    if server:
+        md += [("numSegmentsQueried", str(server[0])), ("timeUsedMs", str(server[1]))]
+        if server[2] >= 0:
+            md.append(("requestId", str(server[2])))
+    aggs = query["aggregations"]
+    if not query.get("group_by"):
+        # one row of extractAggregationResult(createAggregationResultHolder()) per function (:331-369)
+        types, fixed, var = [], b"", b""
+        for a in aggs:
+            f = a["function"].upper()
+            if f == "COUNT":
+                types.append("LONG")
+                fixed += _i64(0)
+            elif f in ("SUM", "MIN", "MAX"):
+                types.append("DOUBLE")
+                fixed += _f64({"SUM": 0.0, "MIN": float("inf"), "MAX": float("-inf")}[f])
+            else:
+                types.append("OBJECT")
+                typ, body = (OBJ_AVG_PAIR, _f64(0.0) + _i64(0)) if f == "AVG" else (OBJ_HLL, hll_to_bytes([0] * 256))
+                fixed += _i32(len(var)) + _i32(len(body))
+                var += _i32(typ) + body
+        return _table(1, len(aggs), [], md, _schema([column_name(a) for a in aggs], types), fixed, var)
+    # group-by (:314-329): per function its name (STRING, dictionary-encoded) and an empty HashMap
+    names, fixed, var = [], b"", b""
+    for a in aggs:
+        n = column_name(a)
+        if n not in names:
+            names.append(n)
+        body = _i32(0)
+        fixed += _i32(names.index(n)) + _i32(len(var)) + _i32(len(body))
+        var += _i32(OBJ_MAP) + body
+    return _table(len(aggs), 2, [("functionName", names)], md,
+                  _schema(["functionName", "GroupByResultMap"], ["STRING", "OBJECT"]), fixed, var)
+
+
+def encode_group_by(query, result, stats, server=None):
+    """IntermediateResultsBlock.getAggregationGroupByResultDataTable (:272-292) of a combined group map
+    {key: [value per function]} (values as encode_aggregation takes them; None = trimmed from that function's map).
+    Map entries are written in ascending key order (the reference's ConcurrentHashMap order is arbitrary)."""
+    aggs = query["aggregations"]
+    names, fixed, var = [], b"", b""
+    for i, a in enumerate(aggs):
+        f = a["function"].upper()
+        n = column_name(a)
+        if n not in names:
+            names.append(n)
+        items = sorted((k, v[i]) for k, v in result.items() if v[i] is not None)
+        vt = {"COUNT": OBJ_LONG, "AVG": OBJ_AVG_PAIR, "DISTINCTCOUNTHLL": OBJ_HLL}.get(f, OBJ_DOUBLE)
+        body = _i32(len(items))
+        if items:
+            body += _i32(OBJ_STRING) + _i32(vt)
+            for k, v in items:
+                kb = k.encode("utf-8")
+                if f == "COUNT":
+                    vb = _i64(int(v))
+                elif f == "AVG":
+                    vb = _f64(float(v[0])) + _i64(int(v[1]))
+                elif f == "DISTINCTCOUNTHLL":
+                    vb = hll_to_bytes(v)
+                else:
+                    vb = _f64(float(v))
+                body += _i32(len(kb)) + kb + _i32(len(vb)) + vb
+        fixed += _i32(names.index(n)) + _i32(len(var)) + _i32(len(body))
+        var += _i32(OBJ_MAP) + body
+    return _table(len(aggs), 2, [("functionName", names)], metadata(stats, False, server),
+                  _schema(["functionName", "GroupByResultMap"], ["STRING", "OBJECT"]), fixed, var)
 
 
 # ------------------------------------------------------------------ decoding (the broker side)

@@ -14,7 +14,7 @@ def _declared_functions():
     with open(os.path.join(REPO, "include", "pinot_gpu.h")) as f:
         src = f.read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(pinot_(?:gpu|groupby|datatable)_[a-z_]+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b(pinot_(?:gpu|groupby|datatable|segment|broker)_[a-z_]+)\s*\(", src)))
 
 
 def test_library_exports_header_symbols():
@@ -30,7 +30,7 @@ def test_library_exports_header_symbols():
 
 def test_abi_version_and_error_path_without_gpu():
     lib = _lib.load()
-    assert lib.pinot_gpu_abi_version() == 5
+    assert lib.pinot_gpu_abi_version() == 6
     if lib.pinot_gpu_device_count() == 0:
         ptr = ctypes.c_void_p()
         st = lib.pinot_gpu_engine_create(0, None, ctypes.byref(ptr))

@@ -103,3 +103,26 @@ def test_group_by_datatable_trimmed_per_function_and_limit_flag(engine):
     exp, _ = O.execute_server([seg], q, num_groups_limit=50_000)
     assert len(exp) == len(keys)
     g.release()
+
+
+def test_broker_reduce_of_gpu_tables(engine, sv_segment, kats):
+    """The reference's inter-segment KAT strings (2 servers x 2 segments) from GPU-built DataTables reduced by the
+    library's pinot_broker_reduce (BrokerReduceService.reduceOnDataTable)."""
+    from pinot_amd import BrokerReduce
+    g = engine.register(sv_segment)
+    ex = ServerQueryExecutor(engine)
+    k = kats["inter_segment"]
+    for case in k["cases"]:
+        for variant, where, gb in (("unfiltered", "", ""), ("filtered", kats["filter"], ""),
+                                   ("unfiltered_group_by", "", k["group_by"]),
+                                   ("filtered_group_by", kats["filter"], k["group_by"])):
+            q = compile_pql(case["query"] + where + gb)
+            tables = [ex.process_query_datatable(q, [g, g], server=(2, 1, -1))[0] for _ in range(2)]
+            resp = BrokerReduce.reduce_datatables(q, tables)
+            got = [r["groupByResult"][0]["value"] if "groupByResult" in r else r["value"]
+                   for r in resp["aggregationResults"]]
+            assert got == case[variant], (case["query"], variant)
+            exp = case["stats"][variant]
+            assert [resp["numDocsScanned"], resp["numEntriesScannedPostFilter"], resp["totalDocs"]] == \
+                [exp[0], exp[2], exp[3]], (case["query"], variant)
+    g.release()

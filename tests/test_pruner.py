@@ -1,0 +1,204 @@
+"""Segment pruning (SegmentPrunerService.prune with the server's default pruners) and the all-pruned DataTable.
+
+The oracle (oracle/pruner.py) is pinned by the reference's ColumnValueSegmentPrunerTest.test
+(pinot-core/src/test/java/org/apache/pinot/query/pruner/ColumnValueSegmentPrunerTest.java:53-92): every one of its
+assertions is replayed below against the oracle and against the library's pinot_segment_prune (host code: no GPU).
+Randomized segments and filters then check native == oracle, and that a pruned segment never holds a matching doc.
+GPU-registered segments and the executor path: tests/test_gpu_pruner.py."""
+import math
+
+import numpy as np
+import pytest
+
+import datatable as D
+import pinot_oracle as O
+import pruner as P
+from pinot_amd import PinotGpuError, build_segment, compile_pql, empty_datatable, prune_segment
+
+BAD_QUERY = 5
+
+# ColumnValueSegmentPrunerTest.java:53-92 (query WHERE clause, expected prune)
+KAT = [
+    ("foo = 'bar'", False),
+    ("time = 0", True), ("time = 10", False), ("time = 20", False), ("time = 30", True),
+    ("time < 10", True), ("time <= 10", False), ("time >= 10", False), ("time > 20", True),
+    ("time BETWEEN 20 AND 30", False), ("time BETWEEN 30 AND 40", True),
+    ("time BETWEEN 20 AND 10", True), ("time BETWEEN 30 AND 20", True), ("time BETWEEN 10 AND 10", False),
+    ("time BETWEEN 20 AND 20", False),
+    ("time = 0 AND time > 10", True), ("time > 0 AND time < 10", True), ("time >= 0 AND time <= 10", False),
+    ("time > 20 AND time < 10", True), ("time >= 20 AND time < 30", False), ("time > 0 AND time BETWEEN 0 AND 10", False),
+    ("time = 0 OR time > 10", False), ("time = 0 OR time < 10", True), ("time >= 0 OR time <= 10", False),
+    ("time > 30 OR time < 10", True), ("time BETWEEN 0 AND 5 OR time BETWEEN 30 AND 35", True),
+]
+
+
+def _q(where, select="COUNT(*)"):
+    return compile_pql("SELECT %s FROM table%s" % (select, " WHERE " + where if where else ""))
+
+
+def test_reference_kat_oracle():
+    # the test's metadata: time INT [10, 20]; foo STRING without min / max
+    seg = {"num_docs": 100, "columns": {"time": ("INT", 10, 20), "foo": ("STRING", None, None)}}
+    for where, want in KAT:
+        assert P.column_value_prune(_q(where)["filter"], seg["columns"]) == want, where
+        assert P.prune(seg, _q(where)) == want, where
+
+
+def test_reference_kat_native():
+    # time's dictionary is [10, 20]; foo holds 'bar' only (its min / max contain 'bar': the KAT's answer is unchanged)
+    seg = build_segment("kat", {"time": ("INT", np.arange(10, 21, dtype=np.int32)),
+                                "foo": ("STRING", np.array(["bar"] * 11, dtype=object))})
+    for where, want in KAT:
+        assert prune_segment(seg, _q(where)) == want, where
+        assert prune_segment(seg, _q(where), pruners=P.COLUMN_VALUE) == want, where
+        assert not prune_segment(seg, _q(where), pruners=P.DATA_SCHEMA | P.VALID), where
+
+
+def _random_segment(rng, n, name):
+    cols = {
+        "i": ("INT", rng.integers(int(rng.integers(-100, 50)), int(rng.integers(60, 200)), n).astype(np.int32)),
+        "l": ("LONG", rng.integers(-(1 << 40), 1 << 40, n).astype(np.int64) // (1 << int(rng.integers(20, 40)))),
+        "f": ("FLOAT", (rng.integers(-40, 40, n) * 0.25).astype(np.float32)),
+        "d": ("DOUBLE", rng.integers(int(rng.integers(-90, 0)), int(rng.integers(1, 90)), n) * 0.1),
+        "s": ("STRING", np.array(["k%02d" % v for v in rng.integers(int(rng.integers(0, 40)), 80, n)], dtype=object)),
+    }
+    return build_segment(name, cols)
+
+
+def _literal(rng, seg, col):
+    c = seg.columns[col]
+    vals = c.dict_values()
+    pick = rng.integers(0, 4)
+    if pick == 0:  # a dictionary value
+        v = vals[int(rng.integers(0, c.cardinality))]
+    elif pick == 1:  # just outside
+        v = vals[0] if rng.integers(0, 2) else vals[c.cardinality - 1]
+        if c.data_type == "STRING":
+            return v[:-1] if rng.integers(0, 2) else v + "z"
+        v = v - 1 if rng.integers(0, 2) else v + 1
+    else:  # anywhere
+        if c.data_type == "STRING":
+            return "k%02d" % rng.integers(-5, 90)
+        v = rng.integers(-300, 300) * (0.25 if c.data_type in ("FLOAT", "DOUBLE") else 1)
+    if c.data_type in ("INT", "LONG"):
+        return str(int(v))
+    if c.data_type in ("FLOAT", "DOUBLE"):
+        return repr(float(v))
+    return str(v)
+
+
+def _leaf(rng, seg):
+    col = "ilfds"[int(rng.integers(0, 5))]
+    kind = int(rng.integers(0, 5))
+    a, b = _literal(rng, seg, col), _literal(rng, seg, col)
+    if kind == 0:
+        return {"operator": "EQUALITY", "column": col, "values": [a]}
+    if kind == 1:
+        return {"operator": "NOT", "column": col, "values": [a]}
+    if kind == 2:
+        return {"operator": "IN", "column": col, "values": [a, b]}
+    lo = "*" if rng.integers(0, 4) == 0 else a
+    hi = "*" if rng.integers(0, 4) == 0 else b
+    return {"operator": "RANGE", "column": col,
+            "values": ["%s%s\t\t%s%s" % ("[(" [int(rng.integers(0, 2))], lo, hi, "])"[int(rng.integers(0, 2))])]}
+
+
+def _tree(rng, seg, depth=0):
+    if depth >= 2 or rng.integers(0, 3) == 0:
+        return _leaf(rng, seg)
+    return {"operator": "AND" if rng.integers(0, 2) else "OR",
+            "children": [_tree(rng, seg, depth + 1) for _ in range(int(rng.integers(2, 4)))]}
+
+
+def test_random_native_matches_oracle_and_is_sound():
+    rng = np.random.default_rng(2024)
+    pruned_seen = kept_seen = 0
+    for k in range(12):
+        seg = _random_segment(rng, 400, "r%d" % k)
+        rs = P.ranges(seg)
+        for _ in range(40):
+            q = {"aggregations": [{"function": "COUNT", "column": "*"}], "filter": _tree(rng, seg), "group_by": None}
+            want = P.prune(rs, q)
+            assert prune_segment(seg, q) == want, q
+            if want:
+                pruned_seen += 1
+                assert int(O.filter_mask(seg, q["filter"]).sum()) == 0, q  # pruning never drops a match
+            else:
+                kept_seen += 1
+    assert pruned_seen > 50 and kept_seen > 50, (pruned_seen, kept_seen)
+
+
+def test_data_schema_and_valid_pruners():
+    seg = build_segment("s", {"a": ("INT", np.arange(5, dtype=np.int32)), "b": ("LONG", np.arange(5) * 7)})
+    assert not prune_segment(seg, _q(None))
+    assert prune_segment(seg, _q("zz = 1"))                    # filter column missing
+    assert prune_segment(seg, _q(None, "SUM(zz)"))            # aggregation column missing
+    assert not prune_segment(seg, _q(None, "COUNT(zz)"))      # COUNT's column is never required
+    assert prune_segment(seg, compile_pql("SELECT SUM(a) FROM t GROUP BY zz"))
+    assert not prune_segment(seg, _q("zz = 1"), pruners=0)
+    # ColumnValue alone: an EQUALITY / RANGE leaf on a missing column prunes, any other leaf does not
+    assert prune_segment(seg, _q("zz = 1"), pruners=P.COLUMN_VALUE)
+    assert not prune_segment(seg, _q("zz <> 1"), pruners=P.COLUMN_VALUE)
+    for q in ("zz = 1", "zz <> 1"):
+        assert P.prune({"num_docs": 5, "columns": P.ranges(seg)["columns"]}, _q(q), P.COLUMN_VALUE) == \
+            prune_segment(seg, _q(q), pruners=P.COLUMN_VALUE)
+    empty = build_segment("e", {"a": ("INT", np.arange(5, dtype=np.int32))}, num_docs=0)
+    assert prune_segment(empty, _q(None)) and P.prune(P.ranges(empty), _q(None))
+    assert not prune_segment(empty, _q(None), pruners=P.DATA_SCHEMA | P.COLUMN_VALUE)
+
+
+def test_literals_and_java_compare():
+    seg = build_segment("t", {"f": ("FLOAT", np.array([-0.0, 1.5, 2.5], dtype=np.float32)),
+                              "d": ("DOUBLE", np.array([-2.0, 0.5, 0.5])),
+                              "i": ("INT", np.array([3, 9, 9], dtype=np.int32))})
+    rs = P.ranges(seg)
+    def eq(c, v):
+        return {"aggregations": [{"function": "COUNT", "column": "*"}], "group_by": None,
+                "filter": {"operator": "EQUALITY", "column": c, "values": [v]}}
+
+    def rng_(c, v):
+        return {"aggregations": [{"function": "COUNT", "column": "*"}], "group_by": None,
+                "filter": {"operator": "RANGE", "column": c, "values": [v]}}
+
+    cases = [_q(w) for w in ("f = 1.5", "f = 2.50000001", "f = 2.6", "f = 0.0", "f < -0.0", "f <= -0.0",
+                             "d >= 0.50000001", "d BETWEEN -1e308 AND -2.0", "i = 2147483647",
+                             "i > 8 AND i < 10", "f > 1e39")]
+    cases += [eq("f", "2.5f"), eq("d", "0.5d"), eq("d", " 0.5 "), eq("d", "Infinity"), eq("d", "-Infinity"),
+              eq("f", "NaN"), eq("i", "+3"), eq("i", "-0"), rng_("d", "(*\t\tNaN)"), rng_("f", "(-0.0\t\t0.0)"),
+              rng_("f", "[-0.0\t\t0.0]"), rng_("i", "(9\t\t*)"), rng_("i", "[9\t\t*)")]
+    for q in cases:
+        assert prune_segment(seg, q) == P.prune(rs, q), q
+    for bad in (_q("i = 3.5"), _q("i = 'abc'"), _q("i = 2147483648"), _q("d = 'x'"), _q("i BETWEEN 1 AND 2e3"),
+                eq("i", " 3"), eq("d", "inf"), eq("d", "nan")):
+        with pytest.raises(PinotGpuError) as ei:
+            prune_segment(seg, bad)
+        assert ei.value.status == BAD_QUERY, bad
+        with pytest.raises(P.BadQuery):
+            P.prune(rs, bad)
+    # NOT / IN leaves never parse their literals in the pruner (no BadQuery there)
+    assert not prune_segment(seg, _q("i <> 'abc'"))
+
+
+@pytest.mark.parametrize("select,group", [
+    ("COUNT(*), SUM(m), MIN(m), MAX(m), AVG(m), DISTINCTCOUNTHLL(m)", ""),
+    ("COUNT(*)", ""),
+    ("SUM(m), COUNT(*), AVG(m), SUM(m)", " GROUP BY a, b"),
+    ("DISTINCTCOUNTHLL(m), MIN(m)", " GROUP BY a"),
+])
+@pytest.mark.parametrize("server", [None, (4, 17, -1), (12, 3, 987654321)])
+def test_empty_datatable_bytes(select, group, server):
+    q = compile_pql("SELECT %s FROM t WHERE a = 5%s" % (select, group))
+    got = empty_datatable(q, 123456789, server)
+    assert got == D.encode_empty(q, 123456789, server)
+    t = D.decode(got)
+    md = dict(t["metadata"])
+    assert md["totalDocs"] == "123456789" and md["numDocsScanned"] == "0" and md["numSegmentsProcessed"] == "0"
+    if group:
+        assert t["rows"] == len(q["aggregations"]) and all(c[1] == {} for c in t["cells"])
+    else:
+        row = t["cells"][0]
+        fns = [a["function"] for a in q["aggregations"]]
+        for f, v in zip(fns, row):
+            want = {"COUNT": 0, "SUM": 0.0, "MIN": math.inf, "MAX": -math.inf, "AVG": (0.0, 0),
+                    "DISTINCTCOUNTHLL": [0] * 256}[f]
+            assert v == want, f

@@ -545,11 +545,19 @@ class ServerQueryExecutor:
         """ServerQueryExecutorV1Impl.pruneSegments (:270-294): (segments kept, totalDocs over all of them)."""
         m = query.marshal if isinstance(query, PreparedQuery) else QueryMarshal(
             compile_pql(query) if isinstance(query, str) else query)
+        kept, total, _ = self._prune(m, segments)
+        return kept, total
+
+    def _prune(self, m, segments):
+        handles = _segment_handles(segments)
         pruned = (C.c_uint8 * max(len(segments), 1))()
         total = C.c_int64()
-        check(self.engine.lib.pinot_gpu_prune_segments(self.engine.ptr, _segment_handles(segments), len(segments),
-                                                       C.byref(m.q), int(self.pruners), pruned, C.byref(total)))
-        return [sg for i, sg in enumerate(segments) if not pruned[i]], total.value
+        check(self.engine.lib.pinot_gpu_prune_segments(self.engine.ptr, handles, len(segments), C.byref(m.q),
+                                                       int(self.pruners), pruned, C.byref(total)))
+        if not any(pruned[:len(segments)]):
+            return segments, total.value, handles  # the common case: the handle array is reused for the plan
+        kept = [sg for i, sg in enumerate(segments) if not pruned[i]]
+        return kept, total.value, (_segment_handles(kept) if kept else None)
 
     def prepare(self, query):
         """Compile + marshal a query once (a prepared statement); process_query accepts the result.
@@ -569,10 +577,11 @@ class ServerQueryExecutor:
         lib = self.engine.lib
         total = None
         if self.pruners:
-            segments, total = self.prune(PreparedQuery(query, m), segments)
+            segments, total, handles = self._prune(m, segments)
             if not segments:  # every segment pruned (:187-196)
                 return _empty_result(query), _pruned_stats(total)
-        handles = _segment_handles(segments)
+        else:
+            handles = _segment_handles(segments)
         stats = _lib.ExecStats()
         if query.get("group_by"):
             out = C.c_void_p()
@@ -604,15 +613,17 @@ class ServerQueryExecutor:
         lib = self.engine.lib
         srv = C.byref(_lib.DataTableServer(*server)) if server else None
         total = None
+        handles = None
         if self.pruners:
-            segments, total = self.prune(PreparedQuery(query, m), segments)
+            segments, total, handles = self._prune(m, segments)
             if not segments:  # every segment pruned: buildEmptyDataTable (:187-196)
                 need = C.c_uint64()
                 check(lib.pinot_datatable_empty(C.byref(m.q), total, srv, None, 0, C.byref(need)))
                 buf = C.create_string_buffer(max(need.value, 1))
                 check(lib.pinot_datatable_empty(C.byref(m.q), total, srv, buf, need.value, C.byref(need)))
                 return buf.raw[:need.value], _pruned_stats(total)
-        handles = _segment_handles(segments)
+        if handles is None:
+            handles = _segment_handles(segments)
         stats = _lib.ExecStats()
         if query.get("group_by"):
             out = C.c_void_p()

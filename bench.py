@@ -135,14 +135,18 @@ def cpu_baseline_config4(threads, segs, docs, min_seconds=10.0):
 
 
 def kernel_source_hash():
-    """Hash of the HIP sources the PMC traffic figures were measured on (a stale profile must not be reported)."""
+    """Hash of the device code's sources — every .hip file and the headers they include (csrc/common.h, device.h,
+    fused_common.h, kernels.h and include/pinot_gpu.h) — that the PMC traffic figures were measured on: a stale
+    profile must not be reported. Host-only sources (engine.h, *.cpp) do not change the kernels."""
     import hashlib
     h = hashlib.sha256()
     csrc = os.path.join(REPO, "incubator-pinot_amd", "csrc")
-    for f in sorted(os.listdir(csrc)):
-        if f.endswith((".hip", ".h")):
-            with open(os.path.join(csrc, f), "rb") as fh:
-                h.update(f.encode() + fh.read())
+    files = [f for f in sorted(os.listdir(csrc))
+             if f.endswith(".hip") or f in ("common.h", "device.h", "fused_common.h", "kernels.h")]
+    paths = [os.path.join(csrc, f) for f in files] + [os.path.join(REPO, "include", "pinot_gpu.h")]
+    for path in paths:
+        with open(path, "rb") as fh:
+            h.update(os.path.basename(path).encode() + fh.read())
     return h.hexdigest()[:16]
 
 

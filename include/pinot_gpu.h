@@ -60,6 +60,13 @@ typedef enum {
   PINOT_INT = 0, PINOT_LONG = 1, PINOT_FLOAT = 2, PINOT_DOUBLE = 3, PINOT_STRING = 4
 } pinot_data_type;
 
+/* Raw (no-dictionary) numeric columns are transcoded once at registration: the sorted distinct values become the
+ * dictionary and every doc's dictId is fixed-bit packed, so the device path reads one format. Predicates, MIN / MAX
+ * and SUM give the reference's raw-value results (RawValueBased*PredicateEvaluator) except for signed zeros and NaN
+ * in FLOAT / DOUBLE columns, which a dictionary keeps apart / orders last. The dictionary-based MIN / MAX plan is
+ * not used for them (InstancePlanMakerImplV2 requires a dictionary). Raw STRING (var-byte) columns: unsupported. */
+typedef enum { PINOT_ENCODING_DICTIONARY = 0, PINOT_ENCODING_RAW = 1 } pinot_column_encoding;
+
 /* One single-value dictionary-encoded column, exactly as the segment files hold it
  * (all multi-byte fields big-endian, as PinotDataBuffer serves them). Host pointers are
  * only read during pinot_gpu_segment_register; nothing is retained. */
@@ -74,7 +81,11 @@ typedef struct {
   int32_t padding_byte;        /* STRING dictionary padding (segment.padding.character; '%' on legacy segments,
                                   ColumnMetadata.java:111-115): values end at the first such byte, and a non-zero
                                   padding compares predicate values padded (ImmutableDictionaryReader.java:152-180) */
-  int32_t reserved;
+  int32_t encoding;            /* PINOT_ENCODING_DICTIONARY (0) or PINOT_ENCODING_RAW (1): a no-dictionary column
+                                  (PhysicalColumnIndexContainer.java:101-106); forward_index then holds the N values
+                                  themselves, BE fixed width (INT / FLOAT 4 bytes, LONG / DOUBLE 8), as the
+                                  decompressed chunks of FixedByteChunkSingleValueReader hold them; cardinality,
+                                  bits_per_value, dictionary and the indexes are ignored (0 / NULL). */
   const uint8_t *dictionary;   uint64_t dictionary_len;     /* card * width BE values */
   const uint8_t *forward_index; uint64_t forward_index_len; /* ceil(N*b/8) bytes, MSB-first */
   const uint8_t *sorted_index; uint64_t sorted_index_len;   /* 2*card BE int32 [start,end] */

@@ -23,6 +23,7 @@ struct ColumnData {
   int32_t string_width = 0;
   int32_t string_pad = 0;             // STRING padding byte (0 = '\0'; legacy segments '%')
   int32_t num_docs = 0;
+  bool raw = false;                   // registered from a raw (no-dictionary) forward index, transcoded
 
   // host copies (dictionary-sized; used for predicate evaluation and key materialisation)
   std::vector<uint8_t> dict_be;        // raw BE dictionary bytes
@@ -60,6 +61,13 @@ struct ParsedIndexes {
 };
 // segment_parse.cpp: validates and decodes one column descriptor on the host (no device work).
 void parse_column(ColumnData &c, const pinot_column_desc &d, int32_t num_docs, ParsedIndexes &out);
+// A raw column's descriptor transcoded to the dictionary-encoded form (sorted distinct values + packed dictIds);
+// false (out untouched) for a dictionary column. out.desc points into out's buffers.
+struct TranscodedColumn {
+  pinot_column_desc desc{};
+  std::vector<uint8_t> dictionary, forward_index;
+};
+bool transcode_raw(const pinot_column_desc &d, int32_t num_docs, TranscodedColumn &out);
 void validate_segment(const pinot_segment_desc &d);
 std::string java_double_to_string(double v);  // Double.toString
 std::string java_float_to_string(float v);    // Float.toString
@@ -80,6 +88,7 @@ struct SegmentDirData {
   std::vector<std::string> column_names, skipped;  // served columns; multi-value / raw / BYTES columns left out
   std::vector<pinot_column_desc> cols;
   std::vector<std::unique_ptr<MappedFile>> files;
+  std::vector<std::vector<uint8_t>> owned;  // raw columns: the decompressed chunk values
   pinot_segment_desc desc() const;
 };
 void read_segment_dir(const std::string &index_dir, SegmentDirData &out);

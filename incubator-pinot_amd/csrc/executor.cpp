@@ -1022,7 +1022,9 @@ bool shortcut_aggregate(const std::vector<SegmentData *> &segs, const pinot_quer
     for (SegmentData *sg : segs) {
       auto it = sg->by_name.find(c);
       const ColumnData *cd = it == sg->by_name.end() ? nullptr : sg->cols[it->second].get();
-      if (!cd || !cd->numeric()) all_minmax = false;  // unknown / STRING columns: the regular plan reports it
+      // unknown / STRING columns: the regular plan reports it; raw columns have no dictionary to read the ends from
+      // (InstancePlanMakerImplV2.isFitForDictionaryBasedPlan)
+      if (!cd || !cd->numeric() || cd->raw) all_minmax = false;
       cols[a].push_back(cd);
     }
   }

@@ -201,6 +201,8 @@ bool prune_segment_desc(const pinot_segment_desc &d, const pinot_query &q, const
   auto lookup = [&](const std::string &name, ColumnRange &c) {
     const pinot_column_desc *cd = find(name);
     if (!cd) return false;
+    TranscodedColumn tc;  // a raw column's min / max (its metadata's minValue / maxValue): its sorted values' ends
+    if (transcode_raw(*cd, d.num_docs, tc)) cd = &tc.desc;
     c.data_type = cd->data_type;
     const int w = cd->data_type == PINOT_INT || cd->data_type == PINOT_FLOAT ? 4
                   : cd->data_type == PINOT_STRING ? cd->string_width : 8;

@@ -60,11 +60,15 @@ static void upload_dictionary(Engine &e, ColumnData &c) {
   }
 }
 
-static void register_column(Engine &e, SegmentData &seg, const pinot_column_desc &d) {
+static void register_column(Engine &e, SegmentData &seg, const pinot_column_desc &d_in) {
+  TranscodedColumn tc;
+  const bool raw = transcode_raw(d_in, seg.num_docs, tc);  // no-dictionary column: one-time host transcoding
+  const pinot_column_desc &d = raw ? tc.desc : d_in;
   auto cp = std::make_unique<ColumnData>();
   ColumnData &c = *cp;
   ParsedIndexes idx;
   parse_column(c, d, seg.num_docs, idx);  // every check on the caller's bytes (segment_parse.cpp)
+  c.raw = raw;
   require(seg.by_name.find(c.name) == seg.by_name.end(), PINOT_ERR_BAD_ARG, "duplicate column " + c.name);
   upload_dictionary(e, c);
   if (c.is_sorted) {

@@ -7,6 +7,7 @@
 //   dictionaries   PC/segment/index/readers/{Int,Long,Float,Double,String}Dictionary.java (BE values, padded strings)
 //   sorted index   PC/segment/index/readers/SortedIndexReaderImpl.java:34-39 (2 BE ints per dictId)
 //   inverted index PC/segment/index/readers/BitmapInvertedIndexReader.java:92-119 (BE offsets + portable roaring)
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -331,6 +332,84 @@ void parse_column(ColumnData &c, const pinot_column_desc &d, int32_t num_docs, P
   }
 }
 
+// ---------------------------------------------------------------- raw (no-dictionary) columns
+// FixedByteChunkSingleValueReader values (PC/io/reader/impl/v1/FixedByteChunkSingleValueReader.java) become the
+// dictionary form the device path reads: the distinct values sorted as the segment creator sorts a dictionary
+// (Arrays.sort on the primitives: Integer / Long order, Float / Double.compare order), each doc's dictId packed at
+// getNumBitsPerValue(card - 1) bits, MSB first (FixedBitIntReaderWriter).
+bool transcode_raw(const pinot_column_desc &d, int32_t num_docs, TranscodedColumn &out) {
+  if (d.encoding == PINOT_ENCODING_DICTIONARY) return false;
+  const std::string name = d.name ? d.name : "";
+  require(d.encoding == PINOT_ENCODING_RAW, PINOT_ERR_BAD_ARG, name + ": unknown column encoding");
+  require(d.data_type >= PINOT_INT && d.data_type <= PINOT_DOUBLE, PINOT_ERR_UNSUPPORTED,
+          name + ": raw (var-byte) STRING columns are not served");
+  const int w = (d.data_type == PINOT_INT || d.data_type == PINOT_FLOAT) ? 4 : 8;
+  const uint64_t n = (uint64_t)std::max(num_docs, 0);
+  require(d.forward_index && d.forward_index_len >= n * (uint64_t)w, PINOT_ERR_BAD_ARG,
+          name + ": raw forward index shorter than numDocs values");
+  // sort keys: order-preserving u64 images of the values (sign flip for ints, IEEE total order for floats with
+  // NaN canonicalised, as Double.compare orders them)
+  auto key = [&](uint64_t i) -> uint64_t {
+    const uint8_t *p = d.forward_index + i * w;
+    uint64_t v = 0;
+    for (int k = 0; k < w; k++) v = (v << 8) | p[k];
+    switch (d.data_type) {
+      case PINOT_INT: return (uint64_t)(uint32_t)v ^ 0x80000000ull;
+      case PINOT_LONG: return v ^ 0x8000000000000000ull;
+      case PINOT_FLOAT: {
+        uint32_t b = (uint32_t)v;
+        if ((b & 0x7F800000u) == 0x7F800000u && (b & 0x7FFFFFu)) b = 0x7FC00000u;  // floatToIntBits NaN
+        return (b & 0x80000000u) ? (uint64_t)(~b) : (uint64_t)(b | 0x80000000u);
+      }
+      default: {
+        if ((v & 0x7FF0000000000000ull) == 0x7FF0000000000000ull && (v & 0xFFFFFFFFFFFFFull)) v = 0x7FF8000000000000ull;
+        return (v & 0x8000000000000000ull) ? ~v : (v | 0x8000000000000000ull);
+      }
+    }
+  };
+  std::vector<uint64_t> keys(n);
+  for (uint64_t i = 0; i < n; i++) keys[i] = key(i);
+  std::vector<uint64_t> uniq = keys;
+  std::sort(uniq.begin(), uniq.end());
+  uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
+  require(uniq.size() < (1ull << 31), PINOT_ERR_UNSUPPORTED, name + ": more than 2^31 distinct values");
+  const int64_t card = (int64_t)uniq.size();
+  const int bits = num_bits_per_value(std::max<int64_t>(card - 1, 0));
+  out.dictionary.resize((size_t)card * w);
+  for (int64_t j = 0; j < card; j++) {  // invert the key back to the BE value bytes
+    uint64_t k = uniq[j], v;
+    switch (d.data_type) {
+      case PINOT_INT: v = (k ^ 0x80000000ull) & 0xFFFFFFFFull; break;
+      case PINOT_LONG: v = k ^ 0x8000000000000000ull; break;
+      case PINOT_FLOAT: v = (k & 0x80000000ull) ? (k & 0x7FFFFFFFull) : (~k & 0xFFFFFFFFull); break;
+      default: v = (k & 0x8000000000000000ull) ? (k & 0x7FFFFFFFFFFFFFFFull) : ~k; break;
+    }
+    for (int b = 0; b < w; b++) out.dictionary[(size_t)j * w + b] = (uint8_t)(v >> (8 * (w - 1 - b)));
+  }
+  out.forward_index.assign((size_t)((n * (uint64_t)bits + 7) / 8), 0);
+  for (uint64_t i = 0; i < n; i++) {
+    const uint64_t id = (uint64_t)(std::lower_bound(uniq.begin(), uniq.end(), keys[i]) - uniq.begin());
+    const uint64_t bit0 = i * (uint64_t)bits;
+    for (int b = 0; b < bits; b++) {
+      if ((id >> (bits - 1 - b)) & 1) {
+        const uint64_t pos = bit0 + b;
+        out.forward_index[pos >> 3] |= (uint8_t)(0x80u >> (pos & 7));
+      }
+    }
+  }
+  out.desc = pinot_column_desc{};
+  out.desc.name = d.name;
+  out.desc.data_type = d.data_type;
+  out.desc.cardinality = (int32_t)card;
+  out.desc.bits_per_value = bits;
+  out.desc.encoding = PINOT_ENCODING_DICTIONARY;
+  out.desc.dictionary = out.dictionary.data();
+  out.desc.dictionary_len = out.dictionary.size();
+  out.desc.forward_index = out.forward_index.data();
+  out.desc.forward_index_len = out.forward_index.size();
+  return true;
+}
+
 void validate_segment(const pinot_segment_desc &d) {
   require(d.num_docs >= 0, PINOT_ERR_BAD_ARG, "num_docs < 0");
   require(d.num_columns >= 0 && (d.num_columns == 0 || d.columns), PINOT_ERR_BAD_ARG, "columns");
@@ -338,7 +417,8 @@ void validate_segment(const pinot_segment_desc &d) {
   for (int i = 0; i < d.num_columns; i++) {
     ColumnData c;
     ParsedIndexes idx;
-    parse_column(c, d.columns[i], d.num_docs, idx);
+    TranscodedColumn tc;
+    parse_column(c, transcode_raw(d.columns[i], d.num_docs, tc) ? tc.desc : d.columns[i], d.num_docs, idx);
     for (const std::string &nm : names) require(nm != c.name, PINOT_ERR_BAD_ARG, "duplicate column " + c.name);
     names.push_back(c.name);
   }

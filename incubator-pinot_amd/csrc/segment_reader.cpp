@@ -13,7 +13,8 @@
 //                  entry starts with the 8-byte magic 0xdeadbeefdeafbead, counted in its size
 //                  (PC/segment/store/SingleFileIndexDirectory.java:62-320)
 // Files are memory-mapped read-only. Columns this executor does not serve (multi-value, raw / no-dictionary,
-// BYTES) are skipped and named by pinot_gpu_segment_dir_info; queries naming them fail as unknown columns.
+// BYTES) are skipped and named by pinot_gpu_segment_dir_info; queries naming them fail as unknown columns. Raw
+// (no-dictionary) INT / LONG / FLOAT / DOUBLE columns are read from their chunked .sv.raw.fwd index.
 #include <fcntl.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
@@ -227,6 +228,98 @@ MappedFile::~MappedFile() {
   if (data) munmap(const_cast<uint8_t *>(data), size);
 }
 
+// Raw Snappy block (no framing), as org.xerial.snappy.Snappy.uncompress reads it: varint32 length, then literal
+// (tag & 3 == 0) and back-reference copy elements (1, 2 or 4 offset bytes).
+void snappy_uncompress(const uint8_t *p, uint64_t n, std::vector<uint8_t> &out, const std::string &what) {
+  uint64_t i = 0, len = 0;
+  for (int shift = 0;; shift += 7) {
+    require(i < n && shift <= 28, PINOT_ERR_BAD_ARG, what + ": bad Snappy length");
+    const uint8_t b = p[i++];
+    len |= (uint64_t)(b & 0x7F) << shift;
+    if (!(b & 0x80)) break;
+  }
+  const size_t base = out.size();
+  out.reserve(base + len);
+  while (i < n) {
+    const uint8_t tag = p[i++];
+    uint64_t l, off = 0;
+    switch (tag & 3) {
+      case 0: {
+        l = (uint64_t)(tag >> 2) + 1;
+        if (l > 60) {
+          const int nb = (int)l - 60;
+          require(i + nb <= n, PINOT_ERR_BAD_ARG, what + ": truncated Snappy literal");
+          l = 0;
+          for (int k = 0; k < nb; k++) l |= (uint64_t)p[i + k] << (8 * k);
+          l += 1;
+          i += nb;
+        }
+        require(l <= n - i && out.size() - base + l <= len, PINOT_ERR_BAD_ARG, what + ": Snappy literal overruns");
+        out.insert(out.end(), p + i, p + i + l);
+        i += l;
+        continue;
+      }
+      case 1:
+        require(i < n, PINOT_ERR_BAD_ARG, what + ": truncated Snappy copy");
+        l = 4 + ((tag >> 2) & 7);
+        off = ((uint64_t)(tag >> 5) << 8) | p[i++];
+        break;
+      case 2:
+        require(i + 2 <= n, PINOT_ERR_BAD_ARG, what + ": truncated Snappy copy");
+        l = 1 + (tag >> 2);
+        off = (uint64_t)p[i] | ((uint64_t)p[i + 1] << 8);
+        i += 2;
+        break;
+      default:
+        require(i + 4 <= n, PINOT_ERR_BAD_ARG, what + ": truncated Snappy copy");
+        l = 1 + (tag >> 2);
+        off = (uint64_t)p[i] | ((uint64_t)p[i + 1] << 8) | ((uint64_t)p[i + 2] << 16) | ((uint64_t)p[i + 3] << 24);
+        i += 4;
+        break;
+    }
+    const uint64_t have = out.size() - base;
+    require(off >= 1 && off <= have && have + l <= len, PINOT_ERR_BAD_ARG, what + ": bad Snappy copy");
+    for (uint64_t k = 0; k < l; k++) out.push_back(out[out.size() - off]);  // overlapping copies repeat bytes
+  }
+  require(out.size() - base == len, PINOT_ERR_BAD_ARG, what + ": Snappy length mismatch");
+}
+
+// FixedByteChunkSingleValueReader (PC/io/reader/impl/v1/BaseChunkSingleValueReader.java:57-96, :120-147): header
+// ints version, numChunks, numDocsPerChunk, lengthOfLongestEntry [, v2+: totalDocs, compressionType, dataHeaderStart],
+// then numChunks absolute chunk offsets; chunks PASS_THROUGH (0) or SNAPPY (1; version 1 is always Snappy).
+// Returns the docs' values back to back, big-endian, entry_size bytes each.
+std::vector<uint8_t> read_raw_chunks(const uint8_t *b, uint64_t n, int64_t num_docs, int entry_size,
+                                     const std::string &what) {
+  auto be32 = [&](uint64_t off) -> int64_t {
+    require(off + 4 <= n, PINOT_ERR_BAD_ARG, what + ": raw forward index header truncated");
+    return (int32_t)(((uint32_t)b[off] << 24) | ((uint32_t)b[off + 1] << 16) | ((uint32_t)b[off + 2] << 8) | b[off + 3]);
+  };
+  const int64_t version = be32(0), num_chunks = be32(4), per_chunk = be32(8), longest = be32(12);
+  require(version >= 1 && version <= 2, PINOT_ERR_UNSUPPORTED, what + ": raw forward index version");
+  require(longest == entry_size, PINOT_ERR_BAD_ARG, what + ": raw entry size differs from the data type's");
+  require(num_chunks >= 0 && per_chunk >= 1 && num_chunks * per_chunk >= num_docs, PINOT_ERR_BAD_ARG,
+          what + ": raw chunk layout does not cover the docs");
+  int64_t compression = 1, header_start = 16;
+  if (version > 1) {
+    compression = be32(20);
+    header_start = be32(24);
+  }
+  require(compression == 0 || compression == 1, PINOT_ERR_UNSUPPORTED, what + ": chunk compression type");
+  std::vector<uint8_t> values;
+  values.reserve((size_t)num_docs * entry_size);
+  for (int64_t c = 0; c < num_chunks; c++) {
+    const int64_t start = be32((uint64_t)header_start + 4 * c);
+    const int64_t end = c + 1 < num_chunks ? be32((uint64_t)header_start + 4 * (c + 1)) : (int64_t)n;
+    require(start >= header_start + 4 * num_chunks && start <= end && (uint64_t)end <= n, PINOT_ERR_BAD_ARG,
+            what + ": chunk offsets");
+    if (compression == 0) values.insert(values.end(), b + start, b + end);
+    else snappy_uncompress(b + start, (uint64_t)(end - start), values, what);
+  }
+  require(values.size() >= (size_t)num_docs * entry_size, PINOT_ERR_BAD_ARG, what + ": raw chunks hold too few docs");
+  values.resize((size_t)num_docs * entry_size);
+  return values;
+}
+
 void read_segment_dir(const std::string &index_dir, SegmentDirData &out) {
   require(is_dir(index_dir), PINOT_ERR_BAD_ARG, "not a segment directory: " + index_dir);
   const std::string v3 = index_dir + "/v3";
@@ -308,13 +401,26 @@ void read_segment_dir(const std::string &index_dir, SegmentDirData &out) {
     const std::string k = "column." + c + ".";
     const int dt = data_type_of(prop(kv, k + "dataType"));
     const bool single = prop_bool(kv, k + "isSingleValues", true), dict = prop_bool(kv, k + "hasDictionary", true);
-    if (dt < 0 || !single || !dict) {
+    if (dt < 0 || !single || (!dict && dt == PINOT_STRING)) {
       out.skipped.push_back(c);
       continue;
     }
     out.column_names.push_back(c);
     pinot_column_desc d{};
     d.data_type = dt;
+    if (!dict) {  // a raw (no-dictionary) fixed-width column: decompressed here, transcoded at registration
+      const uint8_t *fp = nullptr;
+      uint64_t fn = 0;
+      require(index_bytes(c, "forward_index", c + ".sv.raw.fwd", &fp, &fn), PINOT_ERR_BAD_ARG,
+              c + ": no raw forward index");
+      const int w = (dt == PINOT_INT || dt == PINOT_FLOAT) ? 4 : 8;
+      out.owned.push_back(read_raw_chunks(fp, fn, out.num_docs, w, c));
+      d.encoding = PINOT_ENCODING_RAW;
+      d.forward_index = out.owned.back().data();
+      d.forward_index_len = out.owned.back().size();
+      out.cols.push_back(d);
+      continue;
+    }
     const int64_t card = prop_int(kv, k + "cardinality"), bits = prop_int(kv, k + "bitsPerElement");
     const int64_t width = prop_int(kv, k + "lengthOfEachEntry", "0");
     require(card >= 0 && card < INT32_MAX && bits >= 0 && bits <= 64 && width >= 0 && width < INT32_MAX,

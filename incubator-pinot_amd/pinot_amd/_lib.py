@@ -48,7 +48,7 @@ class PinotGpuError(RuntimeError):
 class ColumnDesc(C.Structure):
     _fields_ = [("name", C.c_char_p), ("data_type", C.c_int32), ("cardinality", C.c_int32),
                 ("bits_per_value", C.c_int32), ("is_sorted", C.c_int32), ("has_inverted_index", C.c_int32),
-                ("string_width", C.c_int32), ("padding_byte", C.c_int32), ("reserved", C.c_int32),
+                ("string_width", C.c_int32), ("padding_byte", C.c_int32), ("encoding", C.c_int32),
                 ("dictionary", C.c_void_p), ("dictionary_len", C.c_uint64),
                 ("forward_index", C.c_void_p), ("forward_index_len", C.c_uint64),
                 ("sorted_index", C.c_void_p), ("sorted_index_len", C.c_uint64),

@@ -92,6 +92,7 @@ def segment_desc(seg: Segment):
         d.has_inverted_index = int(col.has_inverted_index and not col.is_sorted)
         d.string_width = col.string_width
         d.padding_byte = col.padding if col.data_type == "STRING" else 0
+        d.encoding = 1 if getattr(col, "encoding", "dictionary") == "raw" else 0
         for field, data in (("dictionary", col.dictionary), ("forward_index", col.fwd),
                             ("sorted_index", col.sorted_index), ("inverted_index", col.inverted)):
             if data is None:

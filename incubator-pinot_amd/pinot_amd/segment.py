@@ -147,6 +147,8 @@ class Column:
     sorted_index: Optional[bytes] = None  # 2*card BE ints (sorted columns)
     inverted: Optional[bytes] = None      # bitmap inverted index (unsorted columns)
     padding: int = 0                      # STRING padding byte (segment.padding.character; legacy segments '%')
+    encoding: str = "dictionary"          # "raw": no-dictionary column, fwd = BE values (cardinality / bits 0)
+    _raw_values: Optional[np.ndarray] = field(default=None, repr=False)
     _dict_values: Optional[np.ndarray] = field(default=None, repr=False)
     _dict_ids: Optional[np.ndarray] = field(default=None, repr=False)
 
@@ -201,13 +203,27 @@ def _sorted_unique(values, data_type):
     return uniq, ids.astype(np.int32)
 
 
-def build_column(name, values, data_type, inverted=False, allow_sorted=True, bits=None) -> Column:
+def build_column(name, values, data_type, inverted=False, allow_sorted=True, bits=None, raw=False) -> Column:
     """Create one column the way `SegmentColumnarIndexCreator` does for a single-value dictionary column.
 
     `bits` (default getNumBitsPerValue(card - 1), SegmentColumnarIndexCreator.java:404) may be wider: the
-    reader takes the width from the metadata's bitsPerElement (ColumnMetadata.java:98)."""
+    reader takes the width from the metadata's bitsPerElement (ColumnMetadata.java:98).
+    raw=True: a no-dictionary numeric column (encoding PINOT_ENCODING_RAW): `fwd` holds the values, BE fixed width;
+    dict_values() / _dict_ids still describe its sorted distinct values for host-side checks."""
     if data_type not in DATA_TYPES:
         raise ValueError("unsupported data type %s" % data_type)
+    if raw:
+        if data_type == "STRING":
+            raise ValueError("raw STRING columns are var-byte: not supported")
+        vals = np.asarray(values).astype(_BE_DTYPE[data_type].replace(">", "<"))
+        uniq, ids = _sorted_unique(vals, data_type)
+        col = Column(name=name, data_type=data_type, cardinality=0, bits=0, is_sorted=False, has_inverted_index=False,
+                     num_docs=int(vals.shape[0]), dictionary=b"", encoding="raw")
+        col.fwd = vals.astype(_BE_DTYPE[data_type]).tobytes()
+        col._raw_values = vals
+        col._dict_values = np.asarray(uniq).astype(vals.dtype)
+        col._dict_ids = ids
+        return col
     uniq, ids = _sorted_unique(values, data_type)
     card = len(uniq)
     n = ids.shape[0]
@@ -237,13 +253,14 @@ def build_column(name, values, data_type, inverted=False, allow_sorted=True, bit
 
 
 def build_segment(name, columns: Dict[str, tuple], inverted_columns=(), num_docs=None, bits=None,
-                  allow_sorted=True) -> Segment:
-    """columns: {name: (data_type, values)} in schema order; bits: optional {name: bitsPerElement}."""
+                  allow_sorted=True, raw_columns=()) -> Segment:
+    """columns: {name: (data_type, values)} in schema order; bits: optional {name: bitsPerElement};
+    raw_columns: names written without a dictionary."""
     cols = {}
     n = None
     for cname, (dt, vals) in columns.items():
         col = build_column(cname, vals, dt, inverted=cname in inverted_columns, allow_sorted=allow_sorted,
-                           bits=(bits or {}).get(cname))
+                           bits=(bits or {}).get(cname), raw=cname in raw_columns)
         if n is None:
             n = col.num_docs
         elif n != col.num_docs:

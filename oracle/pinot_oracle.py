@@ -77,7 +77,11 @@ def sorted_pairs(col):
 
 
 def dict_ids(col) -> np.ndarray:
-    """Per-doc dictIds of a column: fixed-bit fwd index or sorted index (`PhysicalColumnIndexContainer.java:90-99`)."""
+    """Per-doc dictIds of a column: fixed-bit fwd index or sorted index (`PhysicalColumnIndexContainer.java:90-99`).
+    A raw column has none: its values' ranks among its sorted distinct values stand in (dict_values()[ids] are the
+    values themselves), so aggregation and group-by read the same numbers the raw reader returns."""
+    if getattr(col, "encoding", "dictionary") == "raw":
+        return np.asarray(col._dict_ids, dtype=np.int64)
     if col.is_sorted:
         starts, ends = sorted_pairs(col)
         ids = np.empty(col.num_docs, dtype=np.int64)
@@ -285,6 +289,8 @@ def filter_mask(segment, tree):
                 out |= m
         return out
     col = segment.column(tree["column"])
+    if getattr(col, "encoding", "dictionary") == "raw":
+        return raw_leaf_mask(tree, col)
     ev = make_evaluator(tree, col)
     if ev.always_false:
         return np.zeros(n, dtype=bool)
@@ -310,6 +316,46 @@ def filter_mask(segment, tree):
             alt = ~alt
         assert (alt == mask).all(), "inverted-index path disagrees with scan"
     return mask
+
+
+def raw_leaf_mask(leaf, col):
+    """A leaf on a no-dictionary column: the raw-value evaluators compare the values themselves
+    (EqualsPredicateEvaluatorFactory.newRawValueBasedEvaluator, NotEquals..., In..., NotIn..., and
+    RangePredicateEvaluatorFactory's *RawValueBasedRangePredicateEvaluator: value >= / > lower and <= / < upper)."""
+    v = col._raw_values
+    dt = col.data_type
+
+    def conv(s):
+        x = _java_parse(dt, s)
+        return np.float32(x) if dt == "FLOAT" else x
+
+    op = leaf["operator"]
+    if op in ("EQUALITY", "NOT"):
+        m = v == conv(leaf["values"][0])
+        return m if op == "EQUALITY" else ~m
+    if op in ("IN", "NOT_IN"):
+        vals = leaf["values"]
+        if len(vals) == 1:  # BaseInPredicate: one value split on "\t\t", trailing empties dropped
+            vals = vals[0].split("\t\t")
+            while len(vals) > 1 and vals[-1] == "":
+                vals.pop()
+        m = np.isin(v, np.array([conv(x) for x in vals], dtype=v.dtype))
+        return m if op == "IN" else ~m
+    lower, upper, inc_lower, inc_upper = parse_range(leaf["values"][0])
+    m = np.ones(v.shape[0], dtype=bool)
+    if lower != "*":
+        lo = conv(lower)
+        m &= (v >= lo) if inc_lower else (v > lo)
+    if upper != "*":
+        hi = conv(upper)
+        m &= (v <= hi) if inc_upper else (v < hi)
+    return m
+
+
+def _card(col):
+    """Distinct values of a group-by column: the dictionary's cardinality, or a raw column's distinct values (its
+    NoDictionary*GroupKeyGenerator keys are the values; under num.groups.limit the groups are the same)."""
+    return len(col.dict_values()) if getattr(col, "encoding", "dictionary") == "raw" else col.cardinality
 
 
 # ----------------------------------------------------------------------------- aggregation functions
@@ -426,7 +472,7 @@ def group_by_segment(segment, query, mask, num_groups_limit=100000, array_thresh
     """
     gcols = [segment.column(c) for c in query["group_by"]["columns"]]
     docs = np.nonzero(mask)[0]
-    cards = [c.cardinality for c in gcols]
+    cards = [_card(c) for c in gcols]
     raw = np.zeros(docs.shape[0], dtype=object if _prod(cards) > 2 ** 62 else np.int64)
     for j in range(len(gcols) - 1, -1, -1):
         raw = raw * cards[j] + dict_ids(gcols[j])[docs]
@@ -457,7 +503,7 @@ def group_by_segment(segment, query, mask, num_groups_limit=100000, array_thresh
         col = segment.column(agg["column"])
         ids = dict_ids(col)[docs]
         per_fn.append((f, col, ids))
-    dvals = [[c.dict_values()[i] for i in range(c.cardinality)] for c in gcols]
+    dvals = [[c.dict_values()[i] for i in range(_card(c))] for c in gcols]
     for g in range(uniq.shape[0]):
         sel = order[bounds[g]:bounds[g + 1]]  # doc order preserved (stable)
         key = int(uniq[g])
@@ -675,7 +721,7 @@ def execute_group_by_arrays(segments, query, num_groups_limit=100000, array_thre
         scanned += int(mask.sum())
         docs = np.nonzero(mask)[0]
         gcols = [seg.column(c) for c in gnames]
-        cards = [c.cardinality for c in gcols]
+        cards = [_card(c) for c in gcols]
         ids = [dict_ids(c)[docs] for c in gcols]
         local = np.zeros(docs.shape[0], dtype=np.int64)
         for j in range(len(gcols) - 1, -1, -1):

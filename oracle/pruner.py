@@ -176,11 +176,11 @@ def ranges(seg):
     ends (what the segment creator writes as column.<c>.minValue / maxValue)."""
     cols = {}
     for name, c in seg.columns.items():
-        vals = c.dict_values()
-        if c.cardinality < 1:
+        vals = c.dict_values()  # a raw column: its sorted distinct values (the metadata's min / max are their ends)
+        if len(vals) < 1:
             cols[name] = (c.data_type, None, None)
             continue
-        lo, hi = vals[0], vals[c.cardinality - 1]
+        lo, hi = vals[0], vals[len(vals) - 1]
         if c.data_type in ("INT", "LONG"):
             lo, hi = int(lo), int(hi)
         elif c.data_type in ("FLOAT", "DOUBLE"):

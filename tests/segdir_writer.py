@@ -4,6 +4,8 @@ v1: metadata.properties + <col>.dict, <col>.sv.unsorted.fwd | <col>.sv.sorted.fw
 SegmentColumnarIndexCreator leaves them (file names: SegmentMetadataImpl.java:498-527, V1Constants.java:53-63).
 v3: the same buffers in v3/columns.psf, each behind the 8-byte magic marker, located by v3/index_map
 ("<col>.<index>.startOffset = o" / ".size = n", n counting the marker: SingleFileIndexDirectory.java:166-205,320-330).
+Raw (no-dictionary) columns: <col>.sv.raw.fwd as FixedByteChunkSingleValueWriter writes it
+(BaseChunkSingleValueWriter.java:62-200: header ints, absolute chunk offsets, PASS_THROUGH or Snappy chunks).
 """
 import os
 import struct
@@ -27,14 +29,85 @@ def _props(seg, version, padding):
                   k + "totalRawDocs = %d" % seg.num_docs, k + "dataType = %s" % TYPE_NAMES[c.data_type],
                   k + "bitsPerElement = %d" % c.bits, k + "lengthOfEachEntry = %d" % c.string_width,
                   k + "columnType = DIMENSION", k + "isSorted = %s" % ("true" if c.is_sorted else "false"),
-                  k + "hasNullValue = false", k + "hasDictionary = true",
+                  k + "hasNullValue = false",
+                  k + "hasDictionary = %s" % ("false" if getattr(c, "encoding", "dictionary") == "raw" else "true"),
                   k + "hasInvertedIndex = %s" % ("true" if c.inverted is not None else "false"),
                   k + "isSingleValues = true", k + "maxNumberOfMultiValues = 0",
                   k + "totalNumberOfEntries = %d" % seg.num_docs]
     return "\n".join(lines) + "\n"
 
 
+def _varint(n):
+    out = bytearray()
+    while True:
+        b = n & 0x7F
+        n >>= 7
+        out.append(b | (0x80 if n else 0))
+        if not n:
+            return bytes(out)
+
+
+def _literal(data):
+    out = bytearray()
+    for s in range(0, len(data), 65536):
+        part = data[s:s + 65536]
+        n = len(part) - 1
+        if n < 60:
+            out.append(n << 2)
+        elif n < 256:
+            out += bytes([60 << 2, n])
+        else:
+            out += bytes([61 << 2]) + struct.pack("<H", n)
+        out += part
+    return bytes(out)
+
+
+def snappy_compress(data):
+    """A valid raw Snappy block: greedy 4-byte matches emitted as 2-byte-offset copies (<= 64 bytes), else literals."""
+    data = bytes(data)
+    out = bytearray(_varint(len(data)))
+    table, i, lit = {}, 0, 0
+    while i + 4 <= len(data):
+        key = data[i:i + 4]
+        j = table.get(key)
+        table[key] = i
+        if j is not None and i - j <= 65535:
+            n = 4
+            while i + n < len(data) and n < 64 and data[j + n] == data[i + n]:
+                n += 1
+            out += _literal(data[lit:i]) if i > lit else b""
+            out += bytes([((n - 1) << 2) | 2]) + struct.pack("<H", i - j)
+            i += n
+            lit = i
+        else:
+            i += 1
+    if lit < len(data):
+        out += _literal(data[lit:])
+    return bytes(out)
+
+
+def raw_chunk_file(values_be, entry_size, num_docs, docs_per_chunk=1000, compression=1, version=2, chunks=None):
+    """FixedByteChunkSingleValueWriter bytes. chunks: optional list of already-compressed chunk bodies."""
+    chunk_bytes = docs_per_chunk * entry_size
+    raw = [bytes(values_be[s:s + chunk_bytes]) for s in range(0, num_docs * entry_size, chunk_bytes)]
+    bodies = chunks if chunks is not None else [snappy_compress(r) if compression == 1 else r for r in raw]
+    head = struct.pack(">iiii", version, len(bodies), docs_per_chunk, entry_size)
+    if version > 1:
+        head += struct.pack(">iii", num_docs, compression, len(head) + 12)
+    off = len(head) + 4 * len(bodies)
+    offs = []
+    for b in bodies:
+        offs.append(off)
+        off += len(b)
+    return head + b"".join(struct.pack(">i", o) for o in offs) + b"".join(bodies)
+
+
 def _buffers(c):
+    if getattr(c, "encoding", "dictionary") == "raw":
+        w = 4 if c.data_type in ("INT", "FLOAT") else 8
+        yield "forward_index", c.name + ".sv.raw.fwd", getattr(c, "raw_file", None) or raw_chunk_file(
+            c.fwd, w, c.num_docs)
+        return
     yield "dictionary", c.name + ".dict", c.dictionary
     if c.is_sorted:
         yield "forward_index", c.name + ".sv.sorted.fwd", c.sorted_index

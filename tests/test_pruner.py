@@ -68,11 +68,12 @@ def _random_segment(rng, n, name):
 def _literal(rng, seg, col):
     c = seg.columns[col]
     vals = c.dict_values()
+    card = len(vals)  # a raw column: its sorted distinct values
     pick = rng.integers(0, 4)
     if pick == 0:  # a dictionary value
-        v = vals[int(rng.integers(0, c.cardinality))]
+        v = vals[int(rng.integers(0, card))]
     elif pick == 1:  # just outside
-        v = vals[0] if rng.integers(0, 2) else vals[c.cardinality - 1]
+        v = vals[0] if rng.integers(0, 2) else vals[card - 1]
         if c.data_type == "STRING":
             return v[:-1] if rng.integers(0, 2) else v + "z"
         v = v - 1 if rng.integers(0, 2) else v + 1
@@ -202,3 +203,38 @@ def test_empty_datatable_bytes(select, group, server):
             want = {"COUNT": 0, "SUM": 0.0, "MIN": math.inf, "MAX": -math.inf, "AVG": (0.0, 0),
                     "DISTINCTCOUNTHLL": [0] * 256}[f]
             assert v == want, f
+
+
+def test_raw_columns_host_checks_and_pruning():
+    from pinot_amd import validate_segment
+    from pinot_amd.segment import Column
+    rng = np.random.default_rng(31)
+    vals = {"i": ("INT", rng.integers(-70, 70, 900).astype(np.int32)),
+            "l": ("LONG", rng.integers(-(1 << 50), 1 << 50, 900)),
+            "f": ("FLOAT", (rng.integers(-40, 40, 900) * 0.25).astype(np.float32)),
+            "d": ("DOUBLE", rng.integers(-400, 400, 900) * 0.125),
+            "s": ("STRING", np.array(["k%02d" % v for v in rng.integers(0, 80, 900)], dtype=object))}
+    seg = build_segment("raw", vals, raw_columns=("i", "l", "f", "d"))
+    validate_segment(seg)  # the transcoding runs on the host
+    rs = P.ranges(seg)
+    for c in "ilfd":
+        v = vals[c][1]
+        assert rs["columns"][c][1] == v.min() and rs["columns"][c][2] == v.max()
+    pruned = 0
+    for _ in range(80):
+        q = {"aggregations": [{"function": "COUNT", "column": "*"}], "filter": _tree(rng, seg), "group_by": None}
+        want = P.prune(rs, q)
+        assert prune_segment(seg, q) == want, q
+        pruned += want
+    assert pruned > 5
+    short = build_segment("short", {"l": vals["l"]}, raw_columns=("l",))
+    short.columns["l"].fwd = short.columns["l"].fwd[:-8]
+    with pytest.raises(PinotGpuError) as ei:
+        validate_segment(short)
+    assert ei.value.status == 1
+    s = build_segment("s", {"s": ("STRING", np.array(["x", "y"], dtype=object))})
+    s.columns["s"].encoding = "raw"
+    with pytest.raises(PinotGpuError) as ei:
+        validate_segment(s)
+    assert ei.value.status == 4
+

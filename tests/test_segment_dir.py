@@ -143,3 +143,35 @@ def test_unserved_columns_are_left_out(tmp_path):
     n, cols, skipped = segment_dir_info(d)
     assert (cols, skipped) == (4, 1)
     assert "l" not in read_segment_dir(d).columns
+
+
+def test_raw_columns_read_from_chunked_forward_indexes(tmp_path):
+    """.sv.raw.fwd (FixedByteChunkSingleValueReader layout): PASS_THROUGH and Snappy chunks, versions 1 and 2, v1 and
+    v3 directories: the loader decompresses them and registration transcodes them (host-side checks only here)."""
+    import numpy as np
+    from segdir_writer import raw_chunk_file
+    rng = np.random.default_rng(5)
+    n = 2500
+    cols = {"a": ("INT", rng.integers(-9, 9, n).astype(np.int32)), "m": ("LONG", rng.integers(0, 50, n) * 10 ** 12),
+            "f": ("FLOAT", (rng.integers(0, 8, n) * 0.5).astype(np.float32)), "d": ("DOUBLE", rng.normal(size=n)),
+            "s": ("STRING", np.array(["x%d" % v for v in rng.integers(0, 5, n)], dtype=object))}
+    for version, comp, fver in (("v1", 1, 2), ("v3", 0, 2), ("v1", 1, 1), ("v3", 1, 2)):
+        seg = build_segment("raw", cols, raw_columns=("a", "m", "f", "d"))
+        for c in ("a", "m", "f", "d"):
+            col = seg.columns[c]
+            w = 4 if col.data_type in ("INT", "FLOAT") else 8
+            col.raw_file = raw_chunk_file(col.fwd, w, n, docs_per_chunk=int(rng.integers(7, 900)),
+                                          compression=comp if fver > 1 else 1, version=fver)
+        d = write_segment_dir(seg, str(tmp_path / ("s_%s_%d_%d" % (version, comp, fver))), version=version)
+        assert segment_dir_info(d) == (n, 5, 0)
+    # a hand-written Snappy chunk using every element kind: literal, 1-byte-offset copy, 4-byte-offset copy
+    seg = build_segment("h", {"a": ("INT", np.full(8, 7, dtype=np.int32))}, raw_columns=("a",))
+    body = bytes([32]) + bytes([3 << 2, 0, 0, 0, 7]) + bytes([1 | (7 << 2), 4]) + bytes([3 | (16 << 2), 4, 0, 0, 0])
+    seg.columns["a"].raw_file = raw_chunk_file(seg.columns["a"].fwd, 4, 8, docs_per_chunk=8, chunks=[body])
+    assert segment_dir_info(write_segment_dir(seg, str(tmp_path / "hand"))) == (8, 1, 0)
+    # corrupt chunk streams fail as BAD_ARG, not a crash
+    for bad in (bytes([32, 3 << 2, 0, 0]), bytes([32]) + bytes([1 | (7 << 2), 9]), bytes([200])):
+        seg.columns["a"].raw_file = raw_chunk_file(seg.columns["a"].fwd, 4, 8, docs_per_chunk=8, chunks=[bad])
+        with pytest.raises(PinotGpuError) as ei:
+            segment_dir_info(write_segment_dir(seg, str(tmp_path / ("bad%d" % bad[-1]))))
+        assert ei.value.status == 1

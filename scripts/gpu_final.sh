@@ -8,7 +8,11 @@ tag=${1:-final}
 out=gpurun_out/$tag
 mkdir -p $out
 export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $out/pytest_gpu.log 2>&1 || { tail -30 $out/pytest_gpu.log; exit 1; }
+# the whole suite without -x: a failing test is reported, and the measurements below still run
+timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > $out/pytest_gpu.log 2>&1
+test_rc=$?
+case $test_rc in 124|134|137|139) tail -30 $out/pytest_gpu.log; exit 1;; esac  # timeout / abort / fault: stop
+grep -E "^FAILED|^ERROR" $out/pytest_gpu.log | head -20
 tail -1 $out/pytest_gpu.log
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1 || { tail -20 $out/smoke.log; exit 1; }
 tail -1 $out/smoke.log

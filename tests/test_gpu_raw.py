@@ -20,6 +20,14 @@ def engine():
     e.close()
 
 
+def _norm(v):
+    if hasattr(v, "registers"):  # HyperLogLog
+        return ("hll", bytes(v.registers), v.cardinality())
+    if hasattr(v, "count") and hasattr(v, "sum"):  # AvgPair
+        return ("avg", v.sum, v.count)
+    return v
+
+
 def _segments(rng, n, k):
     out = []
     for i in range(k):
@@ -90,7 +98,13 @@ def test_raw_matches_dictionary_registration(engine):
         q = compile_pql(text)
         a, _ = ex.process_query(q, [gr], trim=False)
         b, _ = ex.process_query(q, [gd], trim=False)
-        assert repr(a) == repr(b) if not q.get("group_by") else set(a) == set(b), text
+        if q.get("group_by"):
+            assert set(a) == set(b), text
+            pairs = [(a[k], b[k]) for k in a]
+        else:
+            pairs = [(a, b)]
+        for x, y in pairs:
+            assert [_norm(v) for v in x] == [_norm(v) for v in y], text
     # MIN / MAX without a filter: the dictionary plan reads a dictionary column's ends (no scan); a raw column is
     # scanned (InstancePlanMakerImplV2.isFitForDictionaryBasedPlan needs a dictionary)
     q = compile_pql("SELECT MIN(big), MAX(lng) FROM t")

@@ -195,8 +195,10 @@ pinot_status pinot_gpu_segment_release(pinot_engine *engine, pinot_segment_handl
 /* ImmutableSegmentLoader.load (PC/indexsegment/immutable/ImmutableSegmentLoader.java:59-153) of a segment
  * directory as Pinot writes it: v1/v2 (one file per index) or v3 (v3/columns.psf + v3/index_map), metadata from
  * metadata.properties (SegmentMetadataImpl / ColumnMetadata; V1Constants.java:54-146). The files are memory-mapped,
- * checked like pinot_gpu_segment_register's descriptors and copied to HBM. Multi-value, raw (no-dictionary) and
- * BYTES columns are not served and are left out. */
+ * checked like pinot_gpu_segment_register's descriptors and copied to HBM. Raw (no-dictionary) INT / LONG / FLOAT /
+ * DOUBLE columns are read from their chunked .sv.raw.fwd index (PASS_THROUGH or Snappy chunks,
+ * BaseChunkSingleValueReader.java:57-147) and registered as PINOT_ENCODING_RAW. Multi-value, raw STRING and BYTES
+ * columns are not served and are left out. */
 pinot_status pinot_gpu_segment_load(pinot_engine *engine, const char *index_dir, pinot_segment_handle *out);
 /* The same read and checks on the host only (no engine, no GPU): docs, served columns, left-out columns. */
 pinot_status pinot_gpu_segment_dir_info(const char *index_dir, int32_t *num_docs, int32_t *num_columns,

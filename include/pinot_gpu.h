@@ -90,6 +90,11 @@ typedef struct {
   const uint8_t *forward_index; uint64_t forward_index_len; /* ceil(N*b/8) bytes, MSB-first */
   const uint8_t *sorted_index; uint64_t sorted_index_len;   /* 2*card BE int32 [start,end] */
   const uint8_t *inverted_index; uint64_t inverted_index_len; /* (card+1) BE int32 offsets + portable roaring */
+  /* column.<c>.minValue / maxValue as the segment metadata holds them (ColumnMetadata.java:155-156; NULL = absent,
+     as in segments whose loader did not generate them: ColumnMinMaxValueGenerator, default mode TIME). Read only by
+     the segment pruner; parsed with the column's data type. */
+  const char *min_value;
+  const char *max_value;
 } pinot_column_desc;
 
 typedef struct {
@@ -255,7 +260,9 @@ void pinot_groupby_free(pinot_groupby_result *r);
  * DefaultHelixStarterServerConfig.java:60-64):
  *   DATA_SCHEMA   a query column (filter, non-COUNT aggregation, group-by) missing from the segment
  *                 (DataSchemaSegmentPruner.java:38-41)
- *   COLUMN_VALUE  EQUALITY / RANGE leaves outside the column's [min, max] (its dictionary's ends); AND prunes when any
+ *   COLUMN_VALUE  EQUALITY / RANGE leaves outside the column's [minValue, maxValue] metadata (a column without
+ *                 them never prunes; a loaded segment's time column gets its dictionary's ends, as the default
+ *                 ColumnMinMaxValueGenerator mode TIME does at load); AND prunes when any
  *                 child does, OR when all do (ColumnValueSegmentPruner.java:49-200). Bloom filters and partition
  *                 metadata are not in the descriptor: those two tests are not made.
  *   VALID         an empty segment (ValidSegmentPruner.java:47-58)

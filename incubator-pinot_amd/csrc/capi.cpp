@@ -204,6 +204,17 @@ pinot_status pinot_gpu_segment_load(pinot_engine *engine, const char *index_dir,
     set_device(*engine);
     auto seg = register_segment(*engine, desc);
     seg->unserved = files.skipped;
+    // ColumnMinMaxValueGenerator in its default mode (TIME, CommonConstants.java:264): the time column's min / max
+    // from its dictionary when the metadata lacks them (ColumnMinMaxValueGenerator.java:55-140)
+    auto tc = seg->by_name.find(files.time_column);
+    if (tc != seg->by_name.end()) {
+      ColumnData &c = *seg->cols[tc->second];
+      if (!c.has_minmax && c.card >= 1) {
+        c.has_minmax = true;
+        c.min_value = c.string_value(0);
+        c.max_value = c.string_value(c.card - 1);
+      }
+    }
     const int64_t h = engine->next_handle++;
     engine->segments[h] = std::move(seg);
     *out = h;

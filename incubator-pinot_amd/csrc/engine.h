@@ -1,6 +1,7 @@
 // Host-side engine: device-resident segments, query planning, execution.
 #pragma once
 #include <chrono>
+#include <deque>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -24,6 +25,8 @@ struct ColumnData {
   int32_t string_pad = 0;             // STRING padding byte (0 = '\0'; legacy segments '%')
   int32_t num_docs = 0;
   bool raw = false;                   // registered from a raw (no-dictionary) forward index, transcoded
+  bool has_minmax = false;            // metadata minValue / maxValue present (the segment pruner's only input)
+  std::string min_value, max_value;
 
   // host copies (dictionary-sized; used for predicate evaluation and key materialisation)
   std::vector<uint8_t> dict_be;        // raw BE dictionary bytes
@@ -89,6 +92,8 @@ struct SegmentDirData {
   std::vector<pinot_column_desc> cols;
   std::vector<std::unique_ptr<MappedFile>> files;
   std::vector<std::vector<uint8_t>> owned;  // raw columns: the decompressed chunk values
+  std::deque<std::string> strings;          // min / max values the descriptors point at (stable addresses)
+  std::string time_column;                  // segment.time.column.name
   pinot_segment_desc desc() const;
 };
 void read_segment_dir(const std::string &index_dir, SegmentDirData &out);

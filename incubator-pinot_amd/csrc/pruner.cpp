@@ -12,8 +12,9 @@
 // pinot_segment_desc carries neither bloom filters nor partition metadata. Both only ever drop segments whose filter
 // matches no doc, so results are unchanged; only numSegmentsProcessed can differ.
 //
-// Min / max: the dictionary's first and last entries. Dictionaries are sorted, and the segment creator writes
-// column.<c>.minValue / maxValue from the same sorted values (ColumnMetadata.java:155-156).
+// Min / max: the column metadata's minValue / maxValue strings (ColumnMetadata.java:155-156), parsed with the
+// column's type; absent (the creator does not write them; the loader's ColumnMinMaxValueGenerator adds them only
+// for the time column in its default TIME mode) means the column never prunes.
 #include <cmath>
 #include <cstring>
 
@@ -75,6 +76,17 @@ int compare(const ColumnRange &c, const Literal &a, const Literal &b) {
       return r < 0 ? -1 : r > 0 ? 1 : 0;
     }
   }
+}
+
+// ColumnMetadata's typed minValue / maxValue (Integer / Long / Float / Double.valueOf, or the string).
+void set_range(ColumnRange &c, const std::string &name, const std::string &mn, const std::string &mx) {
+  try {
+    const Literal a = convert(c, mn), b = convert(c, mx);
+    c.imin = a.i, c.imax = b.i, c.dmin = a.d, c.dmax = b.d, c.smin = a.s, c.smax = b.s;
+  } catch (const Error &) {
+    throw Error(PINOT_ERR_BAD_ARG, name + ": minValue / maxValue do not parse as the column's type");
+  }
+  c.has_range = true;
 }
 
 Literal range_min(const ColumnRange &c) { return Literal{c.imin, c.dmin, c.smin}; }
@@ -155,12 +167,6 @@ bool prune_with(int32_t num_docs, const pinot_query &q, const FilterTreeInput *t
   return false;
 }
 
-uint64_t load_be(const uint8_t *p, int n) {
-  uint64_t v = 0;
-  for (int k = 0; k < n; k++) v = (v << 8) | p[k];
-  return v;
-}
-
 }  // namespace
 
 bool prune_segment(const SegmentData &s, const pinot_query &q, const FilterTreeInput *tree, int32_t mask) {
@@ -175,16 +181,7 @@ bool prune_segment(const SegmentData &s, const pinot_query &q, const FilterTreeI
     if (it == s.by_name.end()) return false;
     const ColumnData &cd = *s.cols[it->second];
     c.data_type = cd.data_type;
-    c.has_range = cd.card >= 1;
-    if (!c.has_range) return true;
-    const int32_t last = cd.card - 1;
-    switch (cd.data_type) {
-      case PINOT_INT:
-      case PINOT_LONG: c.imin = cd.dict_int[0]; c.imax = cd.dict_int[last]; break;
-      case PINOT_FLOAT:
-      case PINOT_DOUBLE: c.dmin = cd.dict_dbl[0]; c.dmax = cd.dict_dbl[last]; break;
-      default: c.smin = cd.dict_str[0]; c.smax = cd.dict_str[last]; break;
-    }
+    if (cd.has_minmax) set_range(c, name, cd.min_value, cd.max_value);
     return true;
   };
   return prune_with(s.num_docs, q, tree, mask, has, lookup);
@@ -201,51 +198,11 @@ bool prune_segment_desc(const pinot_segment_desc &d, const pinot_query &q, const
   auto lookup = [&](const std::string &name, ColumnRange &c) {
     const pinot_column_desc *cd = find(name);
     if (!cd) return false;
-    TranscodedColumn tc;  // a raw column's min / max (its metadata's minValue / maxValue): its sorted values' ends
-    if (transcode_raw(*cd, d.num_docs, tc)) cd = &tc.desc;
-    c.data_type = cd->data_type;
-    const int w = cd->data_type == PINOT_INT || cd->data_type == PINOT_FLOAT ? 4
-                  : cd->data_type == PINOT_STRING ? cd->string_width : 8;
     require(cd->data_type >= PINOT_INT && cd->data_type <= PINOT_STRING, PINOT_ERR_BAD_ARG, name + ": data type");
-    c.has_range = cd->cardinality >= 1 && w >= 1 && cd->dictionary &&
-                  cd->dictionary_len >= (uint64_t)cd->cardinality * (uint64_t)w;
-    if (!c.has_range) return true;
-    const uint8_t *first = cd->dictionary, *last = cd->dictionary + (size_t)(cd->cardinality - 1) * w;
-    switch (cd->data_type) {
-      case PINOT_INT:
-        c.imin = (int32_t)(uint32_t)load_be(first, 4);
-        c.imax = (int32_t)(uint32_t)load_be(last, 4);
-        break;
-      case PINOT_LONG:
-        c.imin = (int64_t)load_be(first, 8);
-        c.imax = (int64_t)load_be(last, 8);
-        break;
-      case PINOT_FLOAT: {
-        const uint32_t a = (uint32_t)load_be(first, 4), b = (uint32_t)load_be(last, 4);
-        float fa, fb;
-        memcpy(&fa, &a, 4);
-        memcpy(&fb, &b, 4);
-        c.dmin = fa;
-        c.dmax = fb;
-        break;
-      }
-      case PINOT_DOUBLE: {
-        const uint64_t a = load_be(first, 8), b = load_be(last, 8);
-        memcpy(&c.dmin, &a, 8);
-        memcpy(&c.dmax, &b, 8);
-        break;
-      }
-      default: {  // getUnpaddedString: up to the first padding byte
-        auto unpad = [&](const uint8_t *p) {
-          size_t n = 0;
-          while (n < (size_t)w && p[n] != (uint8_t)cd->padding_byte) n++;
-          return std::string(reinterpret_cast<const char *>(p), n);
-        };
-        c.smin = unpad(first);
-        c.smax = unpad(last);
-        break;
-      }
-    }
+    c.data_type = cd->data_type;
+    require((cd->min_value == nullptr) == (cd->max_value == nullptr), PINOT_ERR_BAD_ARG,
+            name + ": minValue without maxValue (or the reverse)");
+    if (cd->min_value) set_range(c, name, cd->min_value, cd->max_value);
     return true;
   };
   return prune_with(d.num_docs, q, tree, mask, has, lookup);

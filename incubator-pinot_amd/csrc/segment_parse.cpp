@@ -286,6 +286,13 @@ void parse_column(ColumnData &c, const pinot_column_desc &d, int32_t num_docs, P
   require(c.bits >= num_bits_per_value(std::max<int64_t>(c.card - 1, 0)), PINOT_ERR_BAD_ARG,
           c.name + ": bits_per_value < getNumBitsPerValue(cardinality - 1)");
   decode_dictionary(c, d);
+  require((d.min_value == nullptr) == (d.max_value == nullptr), PINOT_ERR_BAD_ARG,
+          c.name + ": minValue without maxValue (or the reverse)");
+  if (d.min_value) {
+    c.has_minmax = true;
+    c.min_value = d.min_value;
+    c.max_value = d.max_value;
+  }
 
   const int64_t n = num_docs;
   c.fwd_bytes = (uint64_t)((n * c.bits + 7) / 8);
@@ -407,6 +414,8 @@ bool transcode_raw(const pinot_column_desc &d, int32_t num_docs, TranscodedColum
   out.desc.dictionary_len = out.dictionary.size();
   out.desc.forward_index = out.forward_index.data();
   out.desc.forward_index_len = out.forward_index.size();
+  out.desc.min_value = d.min_value;
+  out.desc.max_value = d.max_value;
   return true;
 }
 

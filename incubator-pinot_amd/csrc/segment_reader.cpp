@@ -332,6 +332,7 @@ void read_segment_dir(const std::string &index_dir, SegmentDirData &out) {
   require(version == "v1" || version == "v2" || version == "v3", PINOT_ERR_UNSUPPORTED, "segment version " + version);
   require(!single_file || dir == v3, PINOT_ERR_BAD_ARG, "v3 segment without a v3/ directory: " + index_dir);
   out.name = prop(kv, "segment.name", "");
+  out.time_column = prop(kv, "segment.time.column.name", "");
   const int64_t total = prop_int(kv, "segment.total.docs", nullptr);
   require(total >= 0 && total < INT32_MAX, PINOT_ERR_BAD_ARG, "segment.total.docs out of range");
   out.num_docs = (int32_t)total;
@@ -408,6 +409,12 @@ void read_segment_dir(const std::string &index_dir, SegmentDirData &out) {
     out.column_names.push_back(c);
     pinot_column_desc d{};
     d.data_type = dt;
+    if (kv.count(k + "minValue") && kv.count(k + "maxValue")) {  // ColumnMetadata.java:155-156
+      out.strings.push_back(unescape_properties(prop(kv, k + "minValue")));
+      d.min_value = out.strings.back().c_str();
+      out.strings.push_back(unescape_properties(prop(kv, k + "maxValue")));
+      d.max_value = out.strings.back().c_str();
+    }
     if (!dict) {  // a raw (no-dictionary) fixed-width column: decompressed here, transcoded at registration
       const uint8_t *fp = nullptr;
       uint64_t fn = 0;

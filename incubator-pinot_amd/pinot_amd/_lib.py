@@ -52,7 +52,8 @@ class ColumnDesc(C.Structure):
                 ("dictionary", C.c_void_p), ("dictionary_len", C.c_uint64),
                 ("forward_index", C.c_void_p), ("forward_index_len", C.c_uint64),
                 ("sorted_index", C.c_void_p), ("sorted_index_len", C.c_uint64),
-                ("inverted_index", C.c_void_p), ("inverted_index_len", C.c_uint64)]
+                ("inverted_index", C.c_void_p), ("inverted_index_len", C.c_uint64),
+                ("min_value", C.c_char_p), ("max_value", C.c_char_p)]
 
 
 class SegmentDesc(C.Structure):

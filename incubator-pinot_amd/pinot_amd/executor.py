@@ -93,6 +93,10 @@ def segment_desc(seg: Segment):
         d.string_width = col.string_width
         d.padding_byte = col.padding if col.data_type == "STRING" else 0
         d.encoding = 1 if getattr(col, "encoding", "dictionary") == "raw" else 0
+        if getattr(col, "min_value", None) is not None:
+            mn, mx = col.min_value.encode(), col.max_value.encode()
+            keep += [mn, mx]
+            d.min_value, d.max_value = mn, mx
         for field, data in (("dictionary", col.dictionary), ("forward_index", col.fwd),
                             ("sorted_index", col.sorted_index), ("inverted_index", col.inverted)):
             if data is None:

@@ -148,6 +148,8 @@ class Column:
     inverted: Optional[bytes] = None      # bitmap inverted index (unsorted columns)
     padding: int = 0                      # STRING padding byte (segment.padding.character; legacy segments '%')
     encoding: str = "dictionary"          # "raw": no-dictionary column, fwd = BE values (cardinality / bits 0)
+    min_value: Optional[str] = None       # column.<c>.minValue / maxValue metadata (None: absent, never pruned on)
+    max_value: Optional[str] = None
     _raw_values: Optional[np.ndarray] = field(default=None, repr=False)
     _dict_values: Optional[np.ndarray] = field(default=None, repr=False)
     _dict_ids: Optional[np.ndarray] = field(default=None, repr=False)
@@ -252,10 +254,17 @@ def build_column(name, values, data_type, inverted=False, allow_sorted=True, bit
     return col
 
 
+def _metadata_string(v, data_type):
+    if data_type in ("FLOAT", "DOUBLE"):
+        return repr(float(v))
+    return str(v if data_type == "STRING" else int(v))
+
+
 def build_segment(name, columns: Dict[str, tuple], inverted_columns=(), num_docs=None, bits=None,
-                  allow_sorted=True, raw_columns=()) -> Segment:
+                  allow_sorted=True, raw_columns=(), min_max=()) -> Segment:
     """columns: {name: (data_type, values)} in schema order; bits: optional {name: bitsPerElement};
-    raw_columns: names written without a dictionary."""
+    raw_columns: names written without a dictionary; min_max: names given minValue / maxValue metadata (the sorted
+    values' ends, as ColumnMinMaxValueGenerator writes them), min_max=True: every column."""
     cols = {}
     n = None
     for cname, (dt, vals) in columns.items():
@@ -265,5 +274,9 @@ def build_segment(name, columns: Dict[str, tuple], inverted_columns=(), num_docs
             n = col.num_docs
         elif n != col.num_docs:
             raise ValueError("ragged columns")
+        if (min_max is True or cname in min_max) and len(col.dict_values()):
+            vals = col.dict_values()
+            col.min_value = _metadata_string(vals[0], dt)
+            col.max_value = _metadata_string(vals[len(vals) - 1], dt)
         cols[cname] = col
     return Segment(name=name, num_docs=n if num_docs is None else num_docs, columns=cols)

@@ -172,18 +172,13 @@ def prune(segment, query, pruners=DEFAULT):
 
 
 def ranges(seg):
-    """{"num_docs", "columns": {name: (type, min, max)}} of a pinot_amd Segment: min / max = the sorted dictionary's
-    ends (what the segment creator writes as column.<c>.minValue / maxValue)."""
+    """{"num_docs", "columns": {name: (type, min, max)}} of a pinot_amd Segment: min / max = its column metadata's
+    minValue / maxValue (ColumnMetadata.java:155-156), None when absent (the creator writes none; the loader's
+    ColumnMinMaxValueGenerator adds them for the time column in its default mode)."""
     cols = {}
     for name, c in seg.columns.items():
-        vals = c.dict_values()  # a raw column: its sorted distinct values (the metadata's min / max are their ends)
-        if len(vals) < 1:
+        if getattr(c, "min_value", None) is None:
             cols[name] = (c.data_type, None, None)
             continue
-        lo, hi = vals[0], vals[len(vals) - 1]
-        if c.data_type in ("INT", "LONG"):
-            lo, hi = int(lo), int(hi)
-        elif c.data_type in ("FLOAT", "DOUBLE"):
-            lo, hi = float(lo), float(hi)
-        cols[name] = (c.data_type, lo, hi)
+        cols[name] = (c.data_type, convert(c.data_type, c.min_value), convert(c.data_type, c.max_value))
     return {"num_docs": seg.num_docs, "columns": cols}

@@ -34,6 +34,8 @@ def _props(seg, version, padding):
                   k + "hasInvertedIndex = %s" % ("true" if c.inverted is not None else "false"),
                   k + "isSingleValues = true", k + "maxNumberOfMultiValues = 0",
                   k + "totalNumberOfEntries = %d" % seg.num_docs]
+        if getattr(c, "min_value", None) is not None:
+            lines += [k + "minValue = %s" % c.min_value, k + "maxValue = %s" % c.max_value]
     return "\n".join(lines) + "\n"
 
 

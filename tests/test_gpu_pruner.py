@@ -26,7 +26,7 @@ def _segments(n=6, docs=3000, seed=5):
                 "g": ("INT", rng.integers(0, 7, docs).astype(np.int32)),
                 "m": ("LONG", rng.integers(-1000, 1000, docs).astype(np.int64)),
                 "s": ("STRING", np.array(["c%d" % (i + v) for v in rng.integers(0, 3, docs)], dtype=object))}
-        segs.append(build_segment("seg_%d" % i, cols))
+        segs.append(build_segment("seg_%d" % i, cols, min_max=("time", "s")))
     return segs
 
 

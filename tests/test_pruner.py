@@ -45,9 +45,10 @@ def test_reference_kat_oracle():
 
 
 def test_reference_kat_native():
-    # time's dictionary is [10, 20]; foo holds 'bar' only (its min / max contain 'bar': the KAT's answer is unchanged)
+    # the test's metadata: time minValue 10 / maxValue 20, foo none (ColumnValueSegmentPrunerTest.java:44-51)
     seg = build_segment("kat", {"time": ("INT", np.arange(10, 21, dtype=np.int32)),
-                                "foo": ("STRING", np.array(["bar"] * 11, dtype=object))})
+                                "foo": ("STRING", np.array(["bar"] * 11, dtype=object))}, min_max=("time",))
+    assert seg.columns["time"].min_value == "10" and seg.columns["foo"].min_value is None
     for where, want in KAT:
         assert prune_segment(seg, _q(where)) == want, where
         assert prune_segment(seg, _q(where), pruners=P.COLUMN_VALUE) == want, where
@@ -62,7 +63,7 @@ def _random_segment(rng, n, name):
         "d": ("DOUBLE", rng.integers(int(rng.integers(-90, 0)), int(rng.integers(1, 90)), n) * 0.1),
         "s": ("STRING", np.array(["k%02d" % v for v in rng.integers(int(rng.integers(0, 40)), 80, n)], dtype=object)),
     }
-    return build_segment(name, cols)
+    return build_segment(name, cols, min_max=True)
 
 
 def _literal(rng, seg, col):
@@ -143,7 +144,7 @@ def test_data_schema_and_valid_pruners():
     for q in ("zz = 1", "zz <> 1"):
         assert P.prune({"num_docs": 5, "columns": P.ranges(seg)["columns"]}, _q(q), P.COLUMN_VALUE) == \
             prune_segment(seg, _q(q), pruners=P.COLUMN_VALUE)
-    empty = build_segment("e", {"a": ("INT", np.arange(5, dtype=np.int32))}, num_docs=0)
+    empty = build_segment("e", {"a": ("INT", np.arange(5, dtype=np.int32))}, num_docs=0, min_max=True)
     assert prune_segment(empty, _q(None)) and P.prune(P.ranges(empty), _q(None))
     assert not prune_segment(empty, _q(None), pruners=P.DATA_SCHEMA | P.COLUMN_VALUE)
 
@@ -151,7 +152,7 @@ def test_data_schema_and_valid_pruners():
 def test_literals_and_java_compare():
     seg = build_segment("t", {"f": ("FLOAT", np.array([-0.0, 1.5, 2.5], dtype=np.float32)),
                               "d": ("DOUBLE", np.array([-2.0, 0.5, 0.5])),
-                              "i": ("INT", np.array([3, 9, 9], dtype=np.int32))})
+                              "i": ("INT", np.array([3, 9, 9], dtype=np.int32))}, min_max=True)
     rs = P.ranges(seg)
     def eq(c, v):
         return {"aggregations": [{"function": "COUNT", "column": "*"}], "group_by": None,
@@ -214,7 +215,7 @@ def test_raw_columns_host_checks_and_pruning():
             "f": ("FLOAT", (rng.integers(-40, 40, 900) * 0.25).astype(np.float32)),
             "d": ("DOUBLE", rng.integers(-400, 400, 900) * 0.125),
             "s": ("STRING", np.array(["k%02d" % v for v in rng.integers(0, 80, 900)], dtype=object))}
-    seg = build_segment("raw", vals, raw_columns=("i", "l", "f", "d"))
+    seg = build_segment("raw", vals, raw_columns=("i", "l", "f", "d"), min_max=True)
     validate_segment(seg)  # the transcoding runs on the host
     rs = P.ranges(seg)
     for c in "ilfd":
@@ -238,3 +239,18 @@ def test_raw_columns_host_checks_and_pruning():
         validate_segment(s)
     assert ei.value.status == 4
 
+
+
+def test_columns_without_min_max_never_prune_by_value():
+    """The segment creator writes no minValue / maxValue; without them ColumnValueSegmentPruner keeps the segment
+    (ColumnValueSegmentPruner.java:124-127, :170-173) — only the invalid-range test still prunes."""
+    seg = build_segment("n", {"a": ("INT", np.arange(10, 21, dtype=np.int32))})
+    assert seg.columns["a"].min_value is None
+    for where, want in (("a = 0", False), ("a > 100", False), ("a BETWEEN 20 AND 10", True), ("a < 5", False)):
+        assert prune_segment(seg, _q(where)) == want, where
+        assert P.prune(P.ranges(seg), _q(where)) == want, where
+    bad = build_segment("b", {"a": ("INT", np.arange(3, dtype=np.int32))}, min_max=True)
+    bad.columns["a"].min_value = "x"
+    with pytest.raises(PinotGpuError) as ei:
+        prune_segment(bad, _q("a = 1"))
+    assert ei.value.status == 1

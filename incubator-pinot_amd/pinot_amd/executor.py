@@ -444,7 +444,9 @@ class GpuServer:
         ub = (C.c_uint8 * 128).from_buffer_copy(uid)
         check(lib.pinot_gpu_server_create_rank(device, nranks, rank, ub, config.encode() if config else None,
                                                C.byref(ptr)))
-        return cls(_ptr=ptr, _devices=[device])
+        srv = cls(_ptr=ptr, _devices=[device])
+        srv.multi_process = True
+        return srv
 
     def close(self):
         if self.ptr:
@@ -493,8 +495,13 @@ class ServerExecutor:
             tdocs = C.c_int64()
             check(lib.pinot_gpu_server_prune_segments(self.server.ptr, self._refs(segments), len(segments),
                                                       C.byref(m.q), int(self.pruners), pruned, C.byref(tdocs)))
-            segments = [sg for i, sg in enumerate(segments) if not pruned[i]]
-            total = tdocs.value
+            kept = [sg for i, sg in enumerate(segments) if not pruned[i]]
+            if getattr(self.server, "multi_process", False):
+                # every rank must join the library's collectives, and its statistics are merged across ranks: a
+                # rank whose segments were all pruned still runs them (they match nothing), totals stay the library's
+                segments = kept or segments
+            else:
+                segments, total = kept, tdocs.value
             if not segments:
                 if as_result and query.get("group_by"):
                     raise _lib.PinotGpuError(1, "every segment was pruned: no group-by result object")

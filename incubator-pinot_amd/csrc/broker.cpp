@@ -212,11 +212,11 @@ int fn_of(const pinot_query &q, int i) { return q.aggregations[i].function; }
 // AvgPair.apply, HyperLogLog.addAll).
 void merge_into(int f, Value &a, const Value &b) {
   switch (f) {
-    case PINOT_AGG_COUNT: a.l += b.l; break;
+    case PINOT_AGG_COUNT: a.l = (int64_t)((uint64_t)a.l + (uint64_t)b.l); break;  // Java long arithmetic wraps
     case PINOT_AGG_SUM: a.d += b.d; break;
     case PINOT_AGG_MIN: a.d = (std::isnan(a.d) || std::isnan(b.d)) ? NAN : (a.d < b.d || (a.d == b.d && std::signbit(a.d))) ? a.d : b.d; break;
     case PINOT_AGG_MAX: a.d = (std::isnan(a.d) || std::isnan(b.d)) ? NAN : (a.d > b.d || (a.d == b.d && !std::signbit(a.d))) ? a.d : b.d; break;
-    case PINOT_AGG_AVG: a.d += b.d; a.l += b.l; break;
+    case PINOT_AGG_AVG: a.d += b.d; a.l = (int64_t)((uint64_t)a.l + (uint64_t)b.l); break;
     default:
       for (int p = 0; p < 256; p++) a.regs[p] = std::max(a.regs[p], b.regs[p]);
       break;
@@ -358,15 +358,25 @@ std::string broker_reduce(const pinot_query &q, int32_t n, const uint8_t *const 
   int64_t docs = 0, in_filter = 0, post_filter = 0, queried = 0, processed = 0, matched = 0, total = 0;
   bool limit = false;
   std::string exceptions;
-  auto add = [](int64_t &acc, const std::string *s) {
-    if (s) acc += std::stoll(*s);
+  auto parse_long = [](const std::string &s) -> int64_t {  // Long.parseLong
+    try {
+      size_t used = 0;
+      const long long v = std::stoll(s, &used);
+      require(used == s.size(), PINOT_ERR_BAD_ARG, "DataTable: metadata value is not a long: " + s);
+      return (int64_t)v;
+    } catch (const std::logic_error &) {
+      throw Error(PINOT_ERR_BAD_ARG, "DataTable: metadata value is not a long: " + s);
+    }
+  };
+  auto add = [&](int64_t &acc, const std::string *s) {
+    if (s) acc = (int64_t)((uint64_t)acc + (uint64_t)parse_long(*s));
   };
   std::vector<const Table *> with_rows;
   for (const Table &t : ts) {
     for (auto &kv : t.metadata) {
       if (kv.first.rfind("Exception", 0) == 0) {  // DataTable.EXCEPTION_METADATA_KEY + error code
         if (!exceptions.empty()) exceptions += ",";
-        exceptions += "{\"errorCode\":" + std::to_string(std::stoi(kv.first.substr(9))) + ",\"message\":";
+        exceptions += "{\"errorCode\":" + std::to_string((int32_t)parse_long(kv.first.substr(9))) + ",\"message\":";
         json_str(exceptions, kv.second);
         exceptions += "}";
       }

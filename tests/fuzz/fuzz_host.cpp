@@ -278,6 +278,58 @@ std::string literal(bool range) {
 
 }  // namespace
 
+// ---------------------------------------------------------------- DataTable bytes for the broker reduce
+struct Dt {
+  std::vector<uint8_t> b;
+  void i32(int32_t v) { for (int k = 3; k >= 0; k--) b.push_back((uint8_t)((uint32_t)v >> (8 * k))); }
+  void i64(int64_t v) { i32((int32_t)((uint64_t)v >> 32)); i32((int32_t)(uint64_t)v); }
+  void str(const std::string &s) { i32((int32_t)s.size()); b.insert(b.end(), s.begin(), s.end()); }
+};
+
+// A DataTableImplV2 (aggregation: COUNT LONG, SUM DOUBLE, AVG / HLL OBJECT; group-by: functionName STRING +
+// GroupByResultMap OBJECT), written field by field as DataTableImplV2.toBytes lays it out.
+std::vector<uint8_t> make_datatable(bool group_by, int nkeys) {
+  Dt dict, meta, schema, fixed, var;
+  meta.i32(2);
+  meta.str("numDocsScanned"); meta.str(std::to_string(rnd(1000)));
+  meta.str("totalDocs"); meta.str(std::to_string(rnd(100000)));
+  int rows, cols;
+  if (!group_by) {
+    rows = 1, cols = 4;
+    schema.i32(4);
+    for (const char *n : {"count_star", "sum_m", "avg_m", "distinctCountHLL_m"}) schema.str(n);
+    for (const char *t : {"LONG", "DOUBLE", "OBJECT", "OBJECT"}) schema.str(t);
+    fixed.i64((int64_t)rnd(1000));
+    fixed.i64((int64_t)rng());
+    Dt avg;  avg.i64((int64_t)rng()); avg.i64((int64_t)rnd(50));
+    fixed.i32((int32_t)var.b.size()); fixed.i32((int32_t)avg.b.size()); var.i32(4); var.b.insert(var.b.end(), avg.b.begin(), avg.b.end());
+    Dt hll;  hll.i32(8); hll.i32(172); for (int w = 0; w < 43; w++) hll.i32((int32_t)rng());
+    fixed.i32((int32_t)var.b.size()); fixed.i32((int32_t)hll.b.size()); var.i32(6); var.b.insert(var.b.end(), hll.b.begin(), hll.b.end());
+  } else {
+    rows = 2, cols = 2;
+    dict.i32(1); dict.str("functionName"); dict.i32(2); dict.i32(0); dict.str("sum_m"); dict.i32(1); dict.str("count_star");
+    schema.i32(2); schema.str("functionName"); schema.str("GroupByResultMap"); schema.str("STRING"); schema.str("OBJECT");
+    for (int r = 0; r < 2; r++) {
+      Dt m;
+      m.i32(nkeys);
+      if (nkeys) { m.i32(0); m.i32(r == 0 ? 2 : 1); }
+      for (int k = 0; k < nkeys; k++) {
+        m.str(std::to_string(rnd(20)) + "\t" + std::to_string(rnd(3)));
+        m.i32(8);
+        m.i64((int64_t)rng());
+      }
+      fixed.i32(r);
+      fixed.i32((int32_t)var.b.size()); fixed.i32((int32_t)m.b.size()); var.i32(8); var.b.insert(var.b.end(), m.b.begin(), m.b.end());
+    }
+  }
+  Dt o;
+  o.i32(2); o.i32(rows); o.i32(cols);
+  int32_t off = 13 * 4;
+  for (Dt *sec : {&dict, &meta, &schema, &fixed, &var}) { o.i32(off); o.i32((int32_t)sec->b.size()); off += (int32_t)sec->b.size(); }
+  for (Dt *sec : {&dict, &meta, &schema, &fixed, &var}) o.b.insert(o.b.end(), sec->b.begin(), sec->b.end());
+  return o.b;
+}
+
 int main(int argc, char **argv) {
   if (argc > 1 && strcmp(argv[1], "fmt") == 0) {  // fmt d:<16 hex> | f:<8 hex> ...: Double/Float.toString lines
     for (int i = 2; i < argc; i++) {
@@ -394,11 +446,83 @@ int main(int argc, char **argv) {
         violations++;
       }
     }
+    // segment pruning over random metadata min / max strings and random filters
+    for (int c = 0; c < ncols; c++) {
+      ColumnData &cd = *sd.cols[c];
+      cd.has_minmax = coin(60);
+      cd.min_value = literal(false);
+      cd.max_value = literal(false);
+    }
+    for (int t = 0; t < 8; t++) {
+      const std::string col = "c" + std::to_string(rnd(ncols + 1));
+      std::vector<std::string> v1 = {literal(coin(50))}, v2 = {literal(false)};
+      std::vector<const char *> p1 = {v1[0].c_str()}, p2 = {v2[0].c_str()};
+      pinot_filter_node nodes[3] = {};
+      nodes[0].op = coin(50) ? PINOT_FILTER_RANGE : PINOT_FILTER_EQUALITY;
+      nodes[0].column = col.c_str(); nodes[0].num_values = 1; nodes[0].values = p1.data();
+      nodes[1].op = coin(50) ? PINOT_FILTER_EQUALITY : PINOT_FILTER_NOT;
+      nodes[1].column = "c0"; nodes[1].num_values = 1; nodes[1].values = p2.data();
+      nodes[2].op = (int32_t)rnd(2); nodes[2].num_children = 2;
+      pinot_agg_spec agg{PINOT_AGG_SUM, "c0"};
+      pinot_query q{};
+      q.num_filter_nodes = 3; q.filter = nodes; q.num_aggregations = 1; q.aggregations = &agg;
+      try {
+        FilterTreeInput tree = decode_filter(3, nodes);
+        (void)prune_segment(sd, q, &tree, (int32_t)rnd(8));
+        (void)prune_segment_desc(seg, q, &tree, (int32_t)rnd(8));
+      } catch (const Error &e) {
+        if (e.status != PINOT_ERR_BAD_ARG && e.status != PINOT_ERR_BAD_QUERY && e.status != PINOT_ERR_UNSUPPORTED) {
+          fprintf(stderr, "iteration %ld: pruner status %d (%s)\n", it, (int)e.status, e.what());
+          violations++;
+        }
+      }
+    }
     for (int c = 0; c < ncols; c++) {  // key strings of every dictionary entry (Double/Float.toString)
       const ColumnData &cd = *sd.cols[c];
       for (int32_t id = 0; id < cd.card; id++) (void)cd.string_value(id);
     }
   }
+  long reduced = 0, reduce_errors = 0;
+  for (long it = 0; it < iters; it++) {  // broker reduce over well-formed and corrupted DataTables
+    const bool gb = coin(50);
+    const int nt = 1 + (int)rnd(3);
+    std::vector<std::vector<uint8_t>> ts;
+    for (int t = 0; t < nt; t++) {
+      ts.push_back(make_datatable(gb, (int)rnd(6)));
+      if (it % 3 != 0) {  // corrupt: flip bytes, truncate or extend
+        std::vector<uint8_t> &b = ts.back();
+        for (int k = 0, n = 1 + (int)rnd(4); k < n && !b.empty(); k++) b[rnd(b.size())] ^= (uint8_t)(1 + rnd(255));
+        if (coin(30)) b.resize(rnd(b.size() + 1));
+        if (coin(10)) b.resize(b.size() + rnd(16), (uint8_t)rnd(256));
+      }
+    }
+    std::vector<const uint8_t *> ptrs;
+    std::vector<uint64_t> lens;
+    for (auto &t : ts) { ptrs.push_back(t.data()); lens.push_back(t.size()); }
+    pinot_agg_spec aggs[4] = {{PINOT_AGG_COUNT, "*"}, {PINOT_AGG_SUM, "m"}, {PINOT_AGG_AVG, "m"},
+                              {PINOT_AGG_DISTINCTCOUNTHLL, "m"}};
+    pinot_agg_spec gaggs[2] = {{PINOT_AGG_SUM, "m"}, {PINOT_AGG_COUNT, "*"}};
+    const char *gcols[2] = {"a", "b"};
+    pinot_query q{};
+    q.num_aggregations = gb ? 2 : 4;
+    q.aggregations = gb ? gaggs : aggs;
+    q.num_group_by = gb ? 2 : 0;
+    q.group_by = gcols;
+    try {
+      (void)broker_reduce(q, nt, ptrs.data(), lens.data(), (int32_t)rnd(12));
+      reduced++;
+    } catch (const Error &e) {
+      reduce_errors++;
+      if (e.status != PINOT_ERR_BAD_ARG && e.status != PINOT_ERR_UNSUPPORTED) {
+        fprintf(stderr, "iteration %ld: broker_reduce status %d (%s)\n", it, (int)e.status, e.what());
+        violations++;
+      }
+    } catch (const std::exception &e) {
+      fprintf(stderr, "iteration %ld: broker_reduce threw %s\n", it, e.what());
+      violations++;
+    }
+  }
+  printf("broker_reduce ok=%ld rejected=%ld\n", reduced, reduce_errors);
   for (int i = 0; i < 20000; i++) {  // Double.toString / Float.toString over arbitrary bit patterns
     uint64_t u = rng();
     double dv;

@@ -200,6 +200,7 @@ def _clangxx():
 
 @pytest.mark.skipif(not _clangxx() or shutil.which("make") is None, reason="no ROCm clang++ for the sanitizer build")
 def test_sanitizer_fuzz_of_descriptors_and_planner():
+    """ASan + UBSan over the descriptor checks, the planner, the segment pruner and the broker's DataTable reader."""
     subprocess.run(["make", "-s", "-C", PKG, "fuzz"], check=True, timeout=600)
     exe = os.path.join(PKG, "build", "fuzz_host")
     for seed in (1, 2):
@@ -207,8 +208,12 @@ def test_sanitizer_fuzz_of_descriptors_and_planner():
                            env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1"))
         assert r.returncode == 0, r.stdout + r.stderr[-4000:]
         assert "violations=0" in r.stdout, r.stdout
-        stats = dict(kv.split("=") for kv in r.stdout.split()[1:])
+        lines = r.stdout.strip().splitlines()
+        stats = dict(kv.split("=") for kv in lines[-1].split()[1:])
         assert int(stats["rejected"]) > 0 and int(stats["accepted"]) > 0 and int(stats["plans"]) > 0
+        # broker reduce over well-formed and corrupted DataTable bytes: both outcomes seen, no sanitizer report
+        broker = dict(kv.split("=") for kv in lines[-2].split()[1:])
+        assert int(broker["ok"]) > 0 and int(broker["rejected"]) > 0
 
 
 # Double.toString / Float.toString (DoubleDictionary / FloatDictionary.getStringValue, the group-key strings):

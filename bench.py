@@ -296,6 +296,8 @@ def main():
         "ms_per_step": ms_per_step,
         "p50_query_ms": float(np.median(step_ms)),
         "p50_c_abi_ms": float(np.median(abi_ms)),
+        "step_ms_detail": {"min": float(np.min(step_ms)), "p90": float(np.percentile(step_ms, 90)),
+                           "max": float(np.max(step_ms)), "first": [round(x, 4) for x in step_ms[:4]]},
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,

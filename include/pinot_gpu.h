@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define PINOT_GPU_ABI_VERSION 6
+#define PINOT_GPU_ABI_VERSION 7
 
 /* ------------------------------------------------------------------ status */
 typedef enum {
@@ -146,7 +146,11 @@ typedef struct {
   int32_t max_init_group_holder_capacity; /* array-holder threshold, default 10000 */
   int32_t timeout_ms;          /* remaining query budget = table timeout - scheduling wait
                                   (ServerQueryExecutorV1Impl.java:113-114); 0 = none, < 0 = already spent */
-  int32_t reserved;
+  int32_t pruners;             /* pinot_pruner bits: the query entry points (pinot_gpu_aggregate / _group_by and the
+                                  server's) first drop the segments these pruners reject, as processQuery does
+                                  (ServerQueryExecutorV1Impl.java:183-216): numSegmentsProcessed counts the rest,
+                                  totalDocs every segment; every segment pruned gives the empty result (identities /
+                                  no group). 0 = no pruning (ABI <= 6: the reserved field) */
 } pinot_query;
 
 /* Per-query statistics (ExecutionStatistics.java:35-43). num_entries_scanned_in_filter
@@ -365,10 +369,11 @@ pinot_status pinot_gpu_group_by_finalize(pinot_engine *engine, const pinot_segme
  * the RCCL communicators, created once (ncclCommInitAll). Segments are registered on its engines
  * (pinot_gpu_server_engine; never pass those to pinot_gpu_engine_destroy) and queried together: the result is the
  * combine over every GPU, as CombineOperator / CombineGroupByOperator return it (CombineOperator.java:75-196,
- * CombineGroupByOperator.java:104-228). Group-by merges dense partials over the query's global key space (union
- * dictionaries: per-segment dictionaries may differ) with a reduce-scatter and finalizes each key range on its GPU.
- * Not handled across GPUs (PINOT_ERR_UNSUPPORTED: run on one engine): hashed key spaces (LONG_MAP / ARRAY_MAP) and
- * queries where the 2 x num.groups.limit inter-segment cap can bind. */
+ * CombineGroupByOperator.java:104-228). Group-by merges dense partials over the query's global key space (the
+ * union of every GPU's dictionaries: per-segment dictionaries may differ) with a reduce-scatter, finalizes each key
+ * range on its GPU and gathers the ranges to the first GPU. Not handled across GPUs (PINOT_ERR_UNSUPPORTED: run on
+ * one engine): hashed key spaces (LONG_MAP / ARRAY_MAP) and queries where the 2 x num.groups.limit inter-segment cap
+ * can bind. */
 typedef struct pinot_server pinot_server;
 typedef struct {
   int32_t engine;              /* index of the server engine that holds the segment */
@@ -378,9 +383,16 @@ typedef struct {
 
 pinot_status pinot_gpu_server_create(const int32_t *devices, int32_t num_devices, const char *config, pinot_server **out);
 /* Multi-process form (one process per GPU): rank 0 makes a 128-byte id, shares it out of band; every rank then
- * creates its server with (device, nranks, rank, id). Each rank's group-by result is its own key range of the
- * merged result (ranks' ranges are disjoint and ascending); aggregation results are complete on every rank. Every
- * rank must hold segments with identical group-by dictionaries; any rank's failure fails every rank (no hang). */
+ * creates its server with (device, nranks, rank, id). Every rank calls each query, with its own segments (none, or
+ * all pruned, is fine: it contributes identities). Group-by dictionaries may differ across ranks and segments: the
+ * ranks exchange their dictionaries and merge over the union. Aggregation results are complete on every rank; the
+ * group-by result is complete on rank 0 (the key ranges gathered there) and empty on the others, or with
+ * "server.gather=0" each rank's own key range (ranges disjoint and ascending). Any rank's failure (bad literal,
+ * timeout, unsupported shape) fails every rank with that status: no rank is left waiting in a collective.
+ * Server config keys (besides the engines'): server.gather=0|1, server.loopback=1 (every rank of the communicator
+ * in this process on ONE device, the collectives done by an in-library device reduce / copy: the multi-GPU merge
+ * protocol on one GPU; with pinot_gpu_server_create the devices must repeat one device, with _create_rank every
+ * rank passes the same id and device from its own thread), server.timeout_ms (in-process rendezvous timeout). */
 pinot_status pinot_gpu_server_unique_id(uint8_t *unique_id);
 pinot_status pinot_gpu_server_create_rank(int32_t device, int32_t nranks, int32_t rank, const uint8_t *unique_id,
                                           const char *config, pinot_server **out);

@@ -92,6 +92,12 @@ std::vector<SegmentData *> resolve(Engine &e, const pinot_segment_handle *segs, 
   return out;
 }
 
+int64_t total_docs(const std::vector<SegmentData *> &segs) {
+  int64_t t = 0;
+  for (auto *s : segs) t += s->num_docs;
+  return t;
+}
+
 void check_query(const pinot_query *q) {
   require(q != nullptr, PINOT_ERR_BAD_ARG, "null query");
   require(q->num_filter_nodes == 0 || q->filter != nullptr, PINOT_ERR_BAD_ARG, "filter nodes");
@@ -306,8 +312,18 @@ pinot_status pinot_gpu_aggregate(pinot_engine *engine, const pinot_segment_handl
     std::lock_guard<std::mutex> lk(engine->mu);
     set_device(*engine);
     DeadlineScope ds(*engine, query->timeout_ms);
-    exec_aggregate(*engine, resolve(*engine, segments, num_segments), *query, out, stats);
-    if (stats) stats->host_ms = elapsed_ms(t0);
+    const std::vector<SegmentData *> segs = resolve(*engine, segments, num_segments);
+    const std::vector<SegmentData *> kept = prune_for_query(segs, *query);
+    if (kept.empty()) {  // every segment pruned (ServerQueryExecutorV1Impl.java:187-196)
+      agg_identities(*query, out);
+      if (stats) memset(stats, 0, sizeof(*stats));
+    } else {
+      exec_aggregate(*engine, kept, *query, out, stats);
+    }
+    if (stats) {
+      if (query->pruners) stats->num_total_raw_docs = total_docs(segs);
+      stats->host_ms = elapsed_ms(t0);
+    }
   });
 }
 
@@ -321,8 +337,19 @@ pinot_status pinot_gpu_group_by(pinot_engine *engine, const pinot_segment_handle
     std::lock_guard<std::mutex> lk(engine->mu);
     set_device(*engine);
     DeadlineScope ds(*engine, query->timeout_ms);
-    auto r = exec_group_by(*engine, resolve(*engine, segments, num_segments), *query, stats);
-    if (stats) stats->host_ms = elapsed_ms(t0);
+    const std::vector<SegmentData *> segs = resolve(*engine, segments, num_segments);
+    const std::vector<SegmentData *> kept = prune_for_query(segs, *query);
+    std::unique_ptr<GroupByResult> r;
+    if (kept.empty()) {
+      r = empty_group_result(*query);
+      if (stats) memset(stats, 0, sizeof(*stats));
+    } else {
+      r = exec_group_by(*engine, kept, *query, stats);
+    }
+    if (stats) {
+      if (query->pruners) stats->num_total_raw_docs = total_docs(segs);
+      stats->host_ms = elapsed_ms(t0);
+    }
     auto *res = new pinot_groupby_result();
     static_cast<GroupByResult &>(*res) = std::move(*r);
     *out = res;
@@ -570,7 +597,6 @@ pinot_status pinot_gpu_server_aggregate(pinot_server *server, const pinot_segmen
     require(server && server->impl && out, PINOT_ERR_BAD_ARG, "null argument");
     check_query(query);
     require(query->num_group_by == 0, PINOT_ERR_BAD_ARG, "group-by query passed to pinot_gpu_server_aggregate");
-    require(query->timeout_ms >= 0, PINOT_ERR_TIMEOUT, "query budget already spent before execution");
     const auto t0 = std::chrono::steady_clock::now();
     server_aggregate(*server->impl, server_refs(segments, num_segments), *query, out, stats);
     if (stats) stats->host_ms = elapsed_ms(t0);
@@ -583,7 +609,6 @@ pinot_status pinot_gpu_server_group_by(pinot_server *server, const pinot_segment
     require(server && server->impl && out, PINOT_ERR_BAD_ARG, "null argument");
     check_query(query);
     require(query->num_group_by >= 1, PINOT_ERR_BAD_ARG, "aggregation-only query passed to pinot_gpu_server_group_by");
-    require(query->timeout_ms >= 0, PINOT_ERR_TIMEOUT, "query budget already spent before execution");
     const auto t0 = std::chrono::steady_clock::now();
     auto r = server_group_by(*server->impl, server_refs(segments, num_segments), *query, stats);
     if (stats) stats->host_ms = elapsed_ms(t0);

@@ -1,6 +1,7 @@
 // Host-side engine: device-resident segments, query planning, execution.
 #pragma once
 #include <chrono>
+#include <cmath>
 #include <deque>
 #include <memory>
 #include <mutex>
@@ -211,6 +212,7 @@ struct Engine {
   DeviceBuffer group_filter;   // bucketed plan: the COUNT pass's filter words per segment (read back by GB_EMIT2)
   DeviceBuffer group_final;    // ordered non-empty keys + compaction scratch
   DeviceBuffer group_out;      // per-group outputs (counts, accumulators, HLL sums, keys) for the D2H
+  DeviceBuffer group_gather;   // multi-GPU root: every rank's per-group outputs, gathered
   PinnedBuffer group_host;     // their pinned host copy
   std::vector<std::shared_ptr<DeviceBuffer>> hll_pool;  // gathered HLL registers, reused once results are released
   DeviceBuffer group_hash;     // hashed key spaces: fingerprint table + representative docs
@@ -256,6 +258,20 @@ struct HllPart {
   std::shared_ptr<DeviceBuffer> buf;
   std::vector<size_t> off;        // per fn: byte offset of its [num_groups][256] registers
   int64_t group_begin = 0, num_groups = 0;
+};
+
+// The non-empty groups of a key range on the device, array-major, as the host result will hold them (the output of
+// the owner finalize before its D2H; what a multi-GPU group-by gathers to its root rank). Per function fn: values[fn]
+// (nullptr-free; read back only where derive[fn] == -1), cards[fn] (kind 4), HLL registers [n][256] at hll_off[fn].
+struct DenseOut {
+  unsigned long long n = 0;
+  std::vector<int> kind;            // accumulator kind per fn
+  std::vector<int> derive;          // -1: read back; -2: from the HLL cardinalities; >= 0: copy of that fn's values
+  long long *keys = nullptr, *counts = nullptr;
+  std::vector<double *> values;
+  std::vector<long long *> cards;
+  std::shared_ptr<DeviceBuffer> hll;
+  std::vector<size_t> hll_off;
 };
 
 struct GroupByResult {
@@ -360,19 +376,59 @@ void exec_group_by_partial_ks(Engine &e, const std::vector<SegmentData *> &segs,
                               const std::vector<int64_t> &gcard, const std::vector<std::vector<std::string>> &gvalues,
                               const std::vector<std::vector<std::vector<int32_t>>> &remap, int64_t *counts_dev,
                               void *const *accs_dev, pinot_exec_stats *stats);
-// owner finalize of one key range [key_base, key_base + G) of merged dense arrays
-std::unique_ptr<GroupByResult> exec_group_by_slice(Engine &e, const pinot_query &q, const std::vector<int> &acc_kind,
-                                                   const std::vector<int64_t> &gcard,
-                                                   const std::vector<std::vector<std::string>> &gvalues,
-                                                   unsigned long long *counts, const std::vector<void *> &accs,
-                                                   int64_t G, int64_t key_base);
-// global key space over segments of several engines (union dictionaries)
-void build_global_key_space(const std::vector<SegmentData *> &segs, const pinot_query &q, std::vector<int64_t> &gcard,
-                            std::vector<std::vector<std::string>> &gvalues,
-                            std::vector<std::vector<std::vector<int32_t>>> &remap, int64_t &G, bool &hashed);
+// owner finalize of one key range [key_base, key_base + G) of merged dense arrays, device half: ordered compaction
+// of the non-empty keys (one sync for their count) and the group outputs on the device
+DenseOut slice_outputs(Engine &e, const pinot_query &q, const std::vector<int> &acc_kind, unsigned long long *counts,
+                       const std::vector<void *> &accs, int64_t G, int64_t key_base);
+// the device arrays of n gathered groups, in e's gather buffers, laid out as slice_outputs lays them out
+DenseOut slice_alloc(Engine &e, const pinot_query &q, const std::vector<int> &acc_kind, unsigned long long n);
+// the gatherable arrays of a DenseOut in a fixed order: (device pointer, bytes per group)
+std::vector<std::pair<void *, size_t>> slice_arrays(const DenseOut &o);
+// host half: the D2H into a result
+std::unique_ptr<GroupByResult> slice_result(Engine &e, const pinot_query &q, const std::vector<int64_t> &gcard,
+                                            const std::vector<std::vector<std::string>> &gvalues, const DenseOut &o);
+// The multi-GPU group-by key space. Each rank serializes, per group-by column, the union of its segments'
+// dictionary values (sorted, unique; an empty list of unknown type for a rank without segments); every rank merges
+// all ranks' lists into the same global dictionaries: global id = rank of the value in the union (value order:
+// integers, doubles by Double.compare, strings by bytes), and each local segment gets a dictId -> global id remap
+// (empty where its dictionary IS the union). The reference merges by string key instead because dictionaries
+// differ per segment (CombineGroupByOperator.java:142-161).
+std::vector<uint8_t> local_group_dictionaries(const std::vector<SegmentData *> &segs, const pinot_query &q);
+struct GlobalKeySpace {
+  std::vector<int64_t> gcard;
+  std::vector<std::vector<std::string>> gvalues;
+  std::vector<std::vector<std::vector<int32_t>>> remap;  // [local segment][gcol]
+  int64_t G = 1;
+  bool hashed = false;  // Π cardinalities beyond the dense limit
+  uint64_t fingerprint = 0;
+};
+GlobalKeySpace global_key_space(const std::vector<SegmentData *> &segs, const pinot_query &q,
+                                const std::vector<std::vector<uint8_t>> &rank_dicts);
 std::vector<int> group_acc_kind_list(const SegmentData &s, const pinot_query &q);
 bool admission_cap_can_bind(const std::vector<SegmentData *> &segs, const pinot_query &q, const Engine &e, int64_t G);
 uint64_t dictionary_fingerprint(const ColumnData &c);
+// SegmentPrunerService over one call's segments with the query's pruners (pinot_query.pruners; 0: all kept)
+std::vector<SegmentData *> prune_for_query(const std::vector<SegmentData *> &segs, const pinot_query &q);
+// the aggregation result of no segment (identities: MIN +inf, MAX -inf, exact zero sums, zero HLL registers)
+void agg_identities(const pinot_query &q, pinot_agg_result *out);
+// the group-by result of no segment (no group)
+std::unique_ptr<GroupByResult> empty_group_result(const pinot_query &q);
+// keys the num.groups.limit admission can let in over these segments (the 2 x limit inter-segment cap binds when
+// the total over every GPU's segments exceeds it)
+int64_t admission_possible(const std::vector<SegmentData *> &segs, const pinot_query &q, const Engine &e);
+// Math.min / Math.max (NaN wins, -0.0 < 0.0)
+inline double java_min(double a, double b) {
+  if (a != a) return a;
+  if (b != b) return b;
+  if (a == 0.0 && b == 0.0) return std::signbit(a) ? a : b;
+  return a < b ? a : b;
+}
+inline double java_max(double a, double b) {
+  if (a != a) return a;
+  if (b != b) return b;
+  if (a == 0.0 && b == 0.0) return std::signbit(a) ? b : a;
+  return a > b ? a : b;
+}
 // CombineService.mergeTwoBlocks over per-engine aggregation results (host)
 void merge_agg_parts(const pinot_query &q, const std::vector<const pinot_agg_result *> &parts, pinot_agg_result *out);
 

@@ -1042,7 +1042,7 @@ bool shortcut_aggregate(const std::vector<SegmentData *> &segs, const pinot_quer
       for (const ColumnData *cd : cols[a]) {
         if (cd->card < 1 || cd->num_docs == 0) continue;
         const double x = cd->double_value(is_min ? 0 : cd->card - 1);
-        v = is_min ? std::min(v, x) : std::max(v, x);
+        v = is_min ? java_min(v, x) : java_max(v, x);
       }
       r.value = v;
     }
@@ -2137,53 +2137,34 @@ unsigned long long compact_dense(Engine &e, const unsigned long long *counts, in
   return n;
 }
 
-std::unique_ptr<GroupByResult> build_dense_result(Engine &e, const DenseGroups &d, const long long *keys_dev,
-                                                  unsigned long long n) {
+// Device half of build_dense_result: the final arrays of the n non-empty groups in the host result's layout
+// (k_group_final) and the HLL registers gathered per group, all on the device (no sync).
+DenseOut dense_outputs(Engine &e, const DenseGroups &d, const long long *keys_dev, unsigned long long n) {
   const pinot_query &q = *d.q;
   const GroupAccs &ga = *d.ga, &gx = *d.gx;
   const std::vector<int> &alias = *d.alias;
   const int na = q.num_aggregations;
-  int n_hll = 0;
-  for (int i = 0; i < na; i++) n_hll += gx.acc_kind[i] == 4;
-  auto res = std::make_unique<GroupByResult>();
-  res->num_columns = q.num_group_by;
-  res->functions.resize(na);
-  for (int i = 0; i < na; i++) res->functions[i] = q.aggregations[i].function;
-  res->counts.assign(na, {});
-  res->values.assign(na, {});
-  res->hll.assign(na, {});
-  res->hll_card.assign(na, {});
-  res->gvalues = d.ks->gvalues;
-  res->gcard = d.ks->gcard;
-  if (!n) return res;
-  const auto tb0 = std::chrono::steady_clock::now();
-  // the result arrays (pinned, recycled from released results where possible) are sized while the device works
-  auto size_results = [&] {
-    if (n >= kPoolMinElems) {
-      ResultPool &rp = result_pool();
-      std::lock_guard<std::mutex> lk(rp.mu);
-      res->raw_keys = take_pooled(rp, rp.i64, n);
-      res->counts[0] = take_pooled(rp, rp.i64, n);
-      for (int i = 0; i < na; i++) {
-        res->values[i] = take_pooled(rp, rp.f64, n);
-        if (ga.acc_kind[i] == 4) res->hll_card[i] = take_pooled(rp, rp.i64, n);
-      }
-    }
-    res->counts_shared = true;  // every aggregation counts the same docs per group
-    res->raw_keys.resize(n);
-    res->counts[0].resize(n);
-    for (int i = 0; i < na; i++) {
-      res->values[i].resize(n);
-      if (ga.acc_kind[i] == 4) res->hll_card[i].resize(n);
-    }
-  };
-  // device: the final arrays in the host layout (k_group_final), then one D2H per array straight into the result
+  DenseOut o;
+  o.n = n;
+  o.kind = ga.acc_kind;
+  o.derive.assign(na, -1);  // -2: values from the HLL cardinalities; >= 0: copy of that function's values
+  for (int i = 0; i < na; i++) {
+    if (ga.acc_kind[i] == 4) o.derive[i] = -2;
+    else if (alias[i] >= 0 && ga.acc_kind[i] == ga.acc_kind[alias[i]]) o.derive[i] = alias[i];
+  }
+  o.hll_off.assign(na, 0);
+  o.values.assign(na, nullptr);
+  o.cards.assign(na, nullptr);
+  if (!n) return o;
   if (!e.hll_linear.size()) {
     e.hll_linear.alloc(257 * sizeof(double));
     PINOT_HIP(hipMemcpy(e.hll_linear.get(), hll_linear_counting_table(), 257 * sizeof(double), hipMemcpyHostToDevice));
   }
-  int n_card = 0;
-  for (int i = 0; i < na; i++) n_card += ga.acc_kind[i] == 4;
+  int n_card = 0, n_hll = 0;
+  for (int i = 0; i < na; i++) {
+    n_card += ga.acc_kind[i] == 4;
+    n_hll += gx.acc_kind[i] == 4;
+  }
   const size_t n8 = n * 8;
   e.group_out.reserve(n8 * (2 + na + n_card) + 256);
   GroupFinalArgs f{};
@@ -2207,74 +2188,115 @@ std::unique_ptr<GroupByResult> build_dense_result(Engine &e, const DenseGroups &
       }
     }
   }
+  o.keys = f.out_keys;
+  o.counts = f.out_counts;
+  o.values.assign(f.out_values, f.out_values + na);
+  o.cards.assign(f.out_card, f.out_card + na);
   launch_group_final(d.counts, keys_dev, (long long)n, f, e.stream);
   PINOT_HIP(hipGetLastError());
   if (n_hll) {  // registers stay on the device until asked for; buffers are recycled once their result is released
-    HllPart part;
-    part.device = e.device;
-    part.group_begin = 0;
-    part.num_groups = (int64_t)n;
-    part.off.assign(na, 0);
     const size_t need = (size_t)n_hll * n * 256 + 16;
     for (auto &b : e.hll_pool)
-      if (b.use_count() == 1 && b->size() >= need) { part.buf = b; break; }
-    if (!part.buf) {
-      part.buf = std::make_shared<DeviceBuffer>(need + need / 4);
-      if (e.hll_pool.size() < 4) e.hll_pool.push_back(part.buf);
+      if (b.use_count() == 1 && b->size() >= need) { o.hll = b; break; }
+    if (!o.hll) {
+      o.hll = std::make_shared<DeviceBuffer>(need + need / 4);
+      if (e.hll_pool.size() < 4) e.hll_pool.push_back(o.hll);
     }
     int h = 0;
     for (int i = 0; i < na; i++)
       if (gx.acc_kind[i] == 4) {
-        part.off[i] = (size_t)h * n * 256;
-        launch_gather_hll(static_cast<const uint8_t *>(d.accs[i]), keys_dev, (long long)n, part.buf->get<uint8_t>() + part.off[i],
+        o.hll_off[i] = (size_t)h * n * 256;
+        launch_gather_hll(static_cast<const uint8_t *>(d.accs[i]), keys_dev, (long long)n, o.hll->get<uint8_t>() + o.hll_off[i],
                           e.stream);
         h++;
       }
     for (int i = 0; i < na; i++)
-      if (alias[i] >= 0 && ga.acc_kind[i] == 4) part.off[i] = part.off[alias[i]];
+      if (alias[i] >= 0 && ga.acc_kind[i] == 4) o.hll_off[i] = o.hll_off[alias[i]];
     PINOT_HIP(hipGetLastError());
+  }
+  return o;
+}
+
+// Host half: one D2H per array straight into the (pinned, pooled) result arrays — only what the host cannot
+// derive: keys, counts, each primary's values, cardinalities; an alias's values (AVG(x) beside SUM(x)) and an HLL
+// function's values (= its cardinalities) are filled on the host. HLL registers stay on the device (one part).
+std::unique_ptr<GroupByResult> dense_fetch(Engine &e, const pinot_query &q, const std::vector<int64_t> &gcard,
+                                           const std::vector<std::vector<std::string>> &gvalues, const DenseOut &o,
+                                           const GroupArgs *hashed) {
+  const int na = q.num_aggregations;
+  const unsigned long long n = o.n;
+  auto res = std::make_unique<GroupByResult>();
+  res->num_columns = q.num_group_by;
+  res->functions.resize(na);
+  for (int i = 0; i < na; i++) res->functions[i] = q.aggregations[i].function;
+  res->counts.assign(na, {});
+  res->values.assign(na, {});
+  res->hll.assign(na, {});
+  res->hll_card.assign(na, {});
+  res->gvalues = gvalues;
+  res->gcard = gcard;
+  res->counts_shared = true;  // every aggregation counts the same docs per group
+  if (!n) return res;
+  const auto tb0 = std::chrono::steady_clock::now();
+  if (o.hll) {
+    HllPart part;
+    part.device = e.device;
+    part.group_begin = 0;
+    part.num_groups = (int64_t)n;
+    part.off = o.hll_off;
+    part.buf = o.hll;
     res->hll_parts.push_back(std::move(part));
   }
   DeviceBuffer ids;
-  if (d.hashed) {  // group ordinals are hash slots: fetch each group's global-id tuple
+  if (hashed) {  // group ordinals are hash slots: fetch each group's global-id tuple
     ids.alloc(n * q.num_group_by * 4 + 16);
-    launch_hash_tuples(*d.hashed, keys_dev, (long long)n, ids.get<int32_t>(), e.stream);
+    launch_hash_tuples(*hashed, o.keys, (long long)n, ids.get<int32_t>(), e.stream);
     PINOT_HIP(hipGetLastError());
     res->key_ids.resize(n * q.num_group_by);
     PINOT_HIP(hipMemcpyAsync(res->key_ids.data(), ids.get(), n * q.num_group_by * 4, hipMemcpyDeviceToHost, e.stream));
   }
-  size_results();
-  const auto tb1 = std::chrono::steady_clock::now();
-  // D2H (PCIe-bound, so only what the host cannot derive): keys, counts, each primary's values, cardinalities;
-  // an alias's values (AVG(x) beside SUM(x)) and an HLL function's values (= its cardinalities) are filled on the host
-  std::vector<int> derive(na, -1);  // -2: from the HLL cardinalities; >= 0: copy of that function's values
-  for (int i = 0; i < na; i++) {
-    if (ga.acc_kind[i] == 4) derive[i] = -2;
-    else if (alias[i] >= 0 && ga.acc_kind[i] == ga.acc_kind[alias[i]]) derive[i] = alias[i];
+  // the result arrays (pinned, recycled from released results where possible) are sized while the device works
+  if (n >= kPoolMinElems) {
+    ResultPool &rp = result_pool();
+    std::lock_guard<std::mutex> lk(rp.mu);
+    res->raw_keys = take_pooled(rp, rp.i64, n);
+    res->counts[0] = take_pooled(rp, rp.i64, n);
+    for (int i = 0; i < na; i++) {
+      res->values[i] = take_pooled(rp, rp.f64, n);
+      if (o.kind[i] == 4) res->hll_card[i] = take_pooled(rp, rp.i64, n);
+    }
   }
-  PINOT_HIP(hipMemcpyAsync(res->raw_keys.data(), f.out_keys, n8, hipMemcpyDeviceToHost, e.stream));
-  PINOT_HIP(hipMemcpyAsync(res->counts[0].data(), f.out_counts, n8, hipMemcpyDeviceToHost, e.stream));
+  res->raw_keys.resize(n);
+  res->counts[0].resize(n);
   for (int i = 0; i < na; i++) {
-    if (derive[i] == -1)
-      PINOT_HIP(hipMemcpyAsync(res->values[i].data(), f.out_values[i], n8, hipMemcpyDeviceToHost, e.stream));
-    if (ga.acc_kind[i] == 4)
-      PINOT_HIP(hipMemcpyAsync(res->hll_card[i].data(), f.out_card[i], n8, hipMemcpyDeviceToHost, e.stream));
+    res->values[i].resize(n);
+    if (o.kind[i] == 4) res->hll_card[i].resize(n);
+  }
+  const auto tb1 = std::chrono::steady_clock::now();
+  const size_t n8 = n * 8;
+  PINOT_HIP(hipMemcpyAsync(res->raw_keys.data(), o.keys, n8, hipMemcpyDeviceToHost, e.stream));
+  PINOT_HIP(hipMemcpyAsync(res->counts[0].data(), o.counts, n8, hipMemcpyDeviceToHost, e.stream));
+  for (int i = 0; i < na; i++) {
+    if (o.derive[i] == -1)
+      PINOT_HIP(hipMemcpyAsync(res->values[i].data(), o.values[i], n8, hipMemcpyDeviceToHost, e.stream));
+    if (o.kind[i] == 4)
+      PINOT_HIP(hipMemcpyAsync(res->hll_card[i].data(), o.cards[i], n8, hipMemcpyDeviceToHost, e.stream));
   }
   wait_stream(e);
   bool any_derived = false;
-  for (int i = 0; i < na; i++) any_derived = any_derived || derive[i] != -1;
+  for (int i = 0; i < na; i++) any_derived = any_derived || o.derive[i] != -1;
   if (any_derived) {
     const size_t nt = n >= (1u << 16) ? host_threads() : 1;
     auto fill = [&](size_t t) {
       const size_t lo = n * t / nt, hi = n * (t + 1) / nt;
       for (int i = 0; i < na; i++) {
-        if (derive[i] == -1) continue;
+        if (o.derive[i] == -1) continue;
         double *v = res->values[i].data();
-        if (derive[i] == -2) {
+        if (o.derive[i] == -2) {
           const int64_t *c = res->hll_card[i].data();
           for (size_t g = lo; g < hi; g++) v[g] = (double)c[g];
         } else {
-          memcpy(v + lo, res->values[derive[i]].data() + lo, (hi - lo) * 8);
+          memcpy(v + lo, res->values[o.derive[i]].data() + lo, (hi - lo) * 8);
         }
       }
     };
@@ -2282,10 +2304,16 @@ std::unique_ptr<GroupByResult> build_dense_result(Engine &e, const DenseGroups &
     else fill(0);
   }
   if (e.host_phases)
-    fprintf(stderr, "[pinot_gpu] group-by outputs (us): launch+sizing %.1f, D2H wait %.1f\n",
+    fprintf(stderr, "[pinot_gpu] group-by outputs (us): sizing %.1f, D2H wait %.1f\n",
             std::chrono::duration<double, std::micro>(tb1 - tb0).count(),
             std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tb1).count());
   return res;
+}
+
+std::unique_ptr<GroupByResult> build_dense_result(Engine &e, const DenseGroups &d, const long long *keys_dev,
+                                                  unsigned long long n) {
+  const DenseOut o = dense_outputs(e, d, keys_dev, n);
+  return dense_fetch(e, *d.q, d.ks->gcard, d.ks->gvalues, o, d.hashed);
 }
 
 std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q,
@@ -2378,6 +2406,13 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
   if (pin) {  // merged partials: u64 counts, 8-byte accumulators and u8 HLL registers, as the fused sinks write them
     counts = reinterpret_cast<unsigned long long *>(pin->counts);
     for (int a = 0; a < na; a++) accs[a] = pin->accs[a];
+  }
+  if (po) {  // partials: the sinks write the caller's dense arrays directly (an alias's array is copied after)
+    counts = reinterpret_cast<unsigned long long *>(po->counts);
+    for (int a = 0; a < na; a++)
+      if (acc_bytes[a]) accs[a] = po->accs[a];
+    for (int a = 0; a < na; a++)
+      if (alias[a] >= 0) accs[a] = accs[alias[a]];
   }
 
   const auto tgc = std::chrono::steady_clock::now();
@@ -2607,12 +2642,11 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     PINOT_HIP(hipGetLastError());
   }
 
-  if (po) {  // partial: the dense accumulators go out as they are (u8 HLL registers included), no compaction
-    PINOT_HIP(hipMemcpyAsync(po->counts, counts, ks.G * 8, hipMemcpyDeviceToDevice, e.stream));
+  if (po) {  // partial: the dense accumulators are the caller's (u8 HLL registers included), no compaction
     for (int i = 0; i < na; i++)
-      if (ga.acc_kind[i] != 5)
-        PINOT_HIP(hipMemcpyAsync(po->accs[i], accs[i], ks.G * (ga.acc_kind[i] == 4 ? 256 : 8), hipMemcpyDeviceToDevice,
-                                 e.stream));
+      if (alias[i] >= 0 && ga.acc_kind[i] != 5 && po->accs[i] != po->accs[alias[i]])
+        PINOT_HIP(hipMemcpyAsync(po->accs[i], po->accs[alias[i]], ks.G * (ga.acc_kind[i] == 4 ? 256 : 8),
+                                 hipMemcpyDeviceToDevice, e.stream));
     PINOT_HIP(hipGetLastError());
     std::vector<unsigned long long> hm(S);
     PINOT_HIP(hipMemcpyAsync(hm.data(), matched, S * 8, hipMemcpyDeviceToHost, e.stream));
@@ -2823,15 +2857,204 @@ std::unique_ptr<GroupByResult> exec_group_by_finalize(Engine &e, const std::vect
 namespace pinot {
 
 // ------------------------------------------------------------------ pieces of the multi-GPU server (server.cpp)
-void build_global_key_space(const std::vector<SegmentData *> &segs, const pinot_query &q, std::vector<int64_t> &gcard,
-                            std::vector<std::vector<std::string>> &gvalues,
-                            std::vector<std::vector<std::vector<int32_t>>> &remap, int64_t &G, bool &hashed) {
-  KeySpace ks = build_key_space(segs, q);
-  gcard = ks.gcard;
-  gvalues = std::move(ks.gvalues);
-  remap = std::move(ks.remap);
-  G = ks.G;
-  hashed = ks.hashed;
+namespace {
+
+uint64_t ordered_double_key(double d) {  // Double.compare order: -0.0 < 0.0, NaN last
+  uint64_t u;
+  memcpy(&u, &d, 8);
+  return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+}
+
+struct DictList {  // one group-by column's sorted unique values (the exchange format of local_group_dictionaries)
+  int32_t type = -1;                 // pinot_data_type; -1: this rank holds no segment
+  std::vector<int64_t> ints;         // INT / LONG
+  std::vector<double> dbls;          // FLOAT / DOUBLE (by ordered_double_key)
+  std::vector<std::string> strs;     // STRING (by bytes)
+  size_t size() const { return type < 0 ? 0 : type <= PINOT_LONG ? ints.size() : type == PINOT_STRING ? strs.size() : dbls.size(); }
+};
+
+void sort_unique(DictList &d) {
+  if (d.type <= PINOT_LONG) {
+    if (!std::is_sorted(d.ints.begin(), d.ints.end()) || std::adjacent_find(d.ints.begin(), d.ints.end()) != d.ints.end()) {
+      std::sort(d.ints.begin(), d.ints.end());
+      d.ints.erase(std::unique(d.ints.begin(), d.ints.end()), d.ints.end());
+    }
+  } else if (d.type == PINOT_STRING) {
+    std::sort(d.strs.begin(), d.strs.end());
+    d.strs.erase(std::unique(d.strs.begin(), d.strs.end()), d.strs.end());
+  } else {
+    auto lt = [](double a, double b) { return ordered_double_key(a) < ordered_double_key(b); };
+    auto eq = [](double a, double b) { return ordered_double_key(a) == ordered_double_key(b); };
+    std::sort(d.dbls.begin(), d.dbls.end(), lt);
+    d.dbls.erase(std::unique(d.dbls.begin(), d.dbls.end(), eq), d.dbls.end());
+  }
+}
+
+void put_u64(std::vector<uint8_t> &b, uint64_t v) { b.insert(b.end(), reinterpret_cast<uint8_t *>(&v), reinterpret_cast<uint8_t *>(&v) + 8); }
+
+struct Reader {
+  const std::vector<uint8_t> &b;
+  size_t p = 0;
+  uint64_t u64() {
+    require(p + 8 <= b.size(), PINOT_ERR_DEVICE, "group-by dictionary exchange: truncated payload");
+    uint64_t v;
+    memcpy(&v, b.data() + p, 8);
+    p += 8;
+    return v;
+  }
+  std::string str(size_t n) {
+    require(p + n <= b.size(), PINOT_ERR_DEVICE, "group-by dictionary exchange: truncated payload");
+    std::string s(reinterpret_cast<const char *>(b.data() + p), n);
+    p += n;
+    return s;
+  }
+};
+
+bool equals_list(const ColumnData &c, const DictList &u) {
+  if ((size_t)c.card != u.size()) return false;
+  if (c.data_type <= PINOT_LONG) return c.dict_int == u.ints;
+  if (c.data_type == PINOT_STRING) return c.dict_str == u.strs;
+  for (int32_t i = 0; i < c.card; i++)
+    if (ordered_double_key(c.dict_dbl[i]) != ordered_double_key(u.dbls[i])) return false;
+  return true;
+}
+
+}  // namespace
+
+std::vector<uint8_t> local_group_dictionaries(const std::vector<SegmentData *> &segs, const pinot_query &q) {
+  std::vector<uint8_t> out;
+  for (int j = 0; j < q.num_group_by; j++) {
+    DictList d;
+    const std::string name = q.group_by[j];
+    if (!segs.empty()) {
+      const ColumnData &c0 = *segs[0]->column(name);
+      d.type = c0.data_type;
+      bool same = true;
+      for (size_t si = 1; si < segs.size(); si++) {
+        const ColumnData &c = *segs[si]->column(name);
+        require(c.data_type == c0.data_type, PINOT_ERR_BAD_QUERY, "group-by column type differs across segments");
+        same = same && same_dictionary(c0, c);
+      }
+      for (size_t si = 0; si < (same ? 1 : segs.size()); si++) {
+        const ColumnData &c = *segs[si]->column(name);
+        if (d.type <= PINOT_LONG) d.ints.insert(d.ints.end(), c.dict_int.begin(), c.dict_int.end());
+        else if (d.type == PINOT_STRING) d.strs.insert(d.strs.end(), c.dict_str.begin(), c.dict_str.end());
+        else d.dbls.insert(d.dbls.end(), c.dict_dbl.begin(), c.dict_dbl.end());
+      }
+      sort_unique(d);
+    }
+    put_u64(out, (uint64_t)(int64_t)d.type);
+    put_u64(out, d.size());
+    if (d.type < 0) continue;
+    if (d.type <= PINOT_LONG) {
+      for (int64_t v : d.ints) put_u64(out, (uint64_t)v);
+    } else if (d.type == PINOT_STRING) {
+      for (const std::string &s : d.strs) {
+        put_u64(out, s.size());
+        out.insert(out.end(), s.begin(), s.end());
+      }
+    } else {
+      for (double v : d.dbls) {
+        uint64_t u;
+        memcpy(&u, &v, 8);
+        put_u64(out, u);
+      }
+    }
+  }
+  return out;
+}
+
+GlobalKeySpace global_key_space(const std::vector<SegmentData *> &segs, const pinot_query &q,
+                                const std::vector<std::vector<uint8_t>> &rank_dicts) {
+  const int ng = q.num_group_by;
+  std::vector<DictList> u(ng);
+  for (const auto &blob : rank_dicts) {
+    Reader r{blob};
+    for (int j = 0; j < ng; j++) {
+      const int32_t type = (int32_t)(int64_t)r.u64();
+      const uint64_t n = r.u64();
+      if (type < 0) continue;
+      require(type <= PINOT_STRING, PINOT_ERR_DEVICE, "group-by dictionary exchange: bad type");
+      require(u[j].type < 0 || u[j].type == type, PINOT_ERR_BAD_QUERY, "group-by column type differs across segments");
+      u[j].type = type;
+      for (uint64_t i = 0; i < n; i++) {
+        if (type <= PINOT_LONG) {
+          u[j].ints.push_back((int64_t)r.u64());
+        } else if (type == PINOT_STRING) {
+          const uint64_t len = r.u64();
+          u[j].strs.push_back(r.str(len));
+        } else {
+          const uint64_t bits = r.u64();
+          double v;
+          memcpy(&v, &bits, 8);
+          u[j].dbls.push_back(v);
+        }
+      }
+    }
+  }
+  GlobalKeySpace ks;
+  ks.gvalues.resize(ng);
+  ks.remap.assign(segs.size(), std::vector<std::vector<int32_t>>(ng));
+  uint64_t fp = 1469598103934665603ull;
+  auto mix = [&fp](uint64_t v) {
+    for (int i = 0; i < 8; i++) {
+      fp ^= (v >> (8 * i)) & 0xFF;
+      fp *= 1099511628211ull;
+    }
+  };
+  for (int j = 0; j < ng; j++) {
+    DictList &d = u[j];
+    if (d.type >= 0) sort_unique(d);
+    const size_t n = d.size();
+    ks.gcard.push_back((int64_t)n);
+    mix((uint64_t)(int64_t)d.type);
+    mix(n);
+    auto &gv = ks.gvalues[j];
+    gv.resize(n);
+    for (size_t i = 0; i < n; i++) {  // Dictionary.getStringValue of the value
+      if (d.type <= PINOT_LONG) {
+        gv[i] = std::to_string(d.ints[i]);
+        mix((uint64_t)d.ints[i]);
+      } else if (d.type == PINOT_STRING) {
+        gv[i] = d.strs[i];
+        for (char ch : d.strs[i]) mix((uint8_t)ch);
+      } else {
+        gv[i] = d.type == PINOT_FLOAT ? java_float_to_string((float)d.dbls[i]) : java_double_to_string(d.dbls[i]);
+        mix(ordered_double_key(d.dbls[i]));
+      }
+    }
+    const std::string name = q.group_by[j];
+    for (size_t si = 0; si < segs.size(); si++) {
+      const ColumnData &c = *segs[si]->column(name);
+      if (equals_list(c, d)) continue;  // identity
+      auto &m = ks.remap[si][j];
+      m.resize(c.card);
+      for (int32_t i = 0; i < c.card; i++) {
+        size_t g;
+        if (d.type <= PINOT_LONG) {
+          g = std::lower_bound(d.ints.begin(), d.ints.end(), c.dict_int[i]) - d.ints.begin();
+        } else if (d.type == PINOT_STRING) {
+          g = std::lower_bound(d.strs.begin(), d.strs.end(), c.dict_str[i]) - d.strs.begin();
+        } else {
+          const uint64_t key = ordered_double_key(c.dict_dbl[i]);
+          g = std::lower_bound(d.dbls.begin(), d.dbls.end(), key,
+                               [](double a, uint64_t k) { return ordered_double_key(a) < k; }) - d.dbls.begin();
+        }
+        require(g < n, PINOT_ERR_DEVICE, "group-by dictionary exchange: a local value is missing from the union");
+        m[i] = (int32_t)g;
+      }
+    }
+  }
+  ks.fingerprint = fp;
+  for (auto g : ks.gcard) {
+    if (g == 0) { ks.G = 0; break; }
+    if (ks.G > kDenseKeyLimit / g) {
+      ks.hashed = true;
+      break;
+    }
+    ks.G *= g;
+  }
+  return ks;
 }
 
 std::vector<int> group_acc_kind_list(const SegmentData &s, const pinot_query &q) { return group_acc_kinds(s, q).acc_kind; }
@@ -2856,14 +3079,9 @@ void exec_group_by_partial_ks(Engine &e, const std::vector<SegmentData *> &segs,
   exec_group_by_fused(e, segs, q, ks, ga, stats, 0, &po, nullptr, true);
 }
 
-std::unique_ptr<GroupByResult> exec_group_by_slice(Engine &e, const pinot_query &q, const std::vector<int> &acc_kind,
-                                                   const std::vector<int64_t> &gcard,
-                                                   const std::vector<std::vector<std::string>> &gvalues,
-                                                   unsigned long long *counts, const std::vector<void *> &accs,
-                                                   int64_t G, int64_t key_base) {
+DenseOut slice_outputs(Engine &e, const pinot_query &q, const std::vector<int> &acc_kind, unsigned long long *counts,
+                       const std::vector<void *> &accs, int64_t G, int64_t key_base) {
   KeySpace ks;
-  ks.gcard = gcard;
-  ks.gvalues = gvalues;
   ks.G = G;
   GroupAccs ga;
   ga.acc_kind = acc_kind;
@@ -2872,7 +3090,68 @@ std::unique_ptr<GroupByResult> exec_group_by_slice(Engine &e, const pinot_query 
   long long *keys_dev = nullptr;
   const unsigned long long n = G > 0 ? compact_dense(e, counts, G, keys_dev, nullptr) : 0;
   DenseGroups dg{&q, &ks, &ga, &ga, &alias, counts, accs, key_base, nullptr};
-  return build_dense_result(e, dg, keys_dev, n);
+  return dense_outputs(e, dg, keys_dev, n);
+}
+
+DenseOut slice_alloc(Engine &e, const pinot_query &q, const std::vector<int> &acc_kind, unsigned long long n) {
+  const int na = q.num_aggregations;
+  DenseOut o;
+  o.n = n;
+  o.kind = acc_kind;
+  o.derive.assign(na, -1);
+  o.hll_off.assign(na, 0);
+  o.values.assign(na, nullptr);
+  o.cards.assign(na, nullptr);
+  int n_card = 0;
+  for (int i = 0; i < na; i++) {
+    n_card += acc_kind[i] == 4;
+    if (acc_kind[i] == 4) o.derive[i] = -2;
+  }
+  const size_t n8 = n * 8;
+  e.group_gather.reserve(n8 * (2 + na + n_card) + 256);
+  o.keys = e.group_gather.get<long long>();
+  o.counts = o.keys + n;
+  double *v = reinterpret_cast<double *>(o.counts + n);
+  long long *c = reinterpret_cast<long long *>(v + n * na);
+  for (int i = 0; i < na; i++) {
+    o.values[i] = v + n * i;
+    if (acc_kind[i] == 4) {
+      o.cards[i] = c;
+      c += n;
+    }
+  }
+  if (n_card && n) {
+    const size_t need = (size_t)n_card * n * 256 + 16;
+    for (auto &b : e.hll_pool)
+      if (b.use_count() == 1 && b->size() >= need) { o.hll = b; break; }
+    if (!o.hll) {
+      o.hll = std::make_shared<DeviceBuffer>(need + need / 4);
+      if (e.hll_pool.size() < 4) e.hll_pool.push_back(o.hll);
+    }
+    int h = 0;
+    for (int i = 0; i < na; i++)
+      if (acc_kind[i] == 4) o.hll_off[i] = (size_t)(h++) * n * 256;
+  }
+  return o;
+}
+
+std::vector<std::pair<void *, size_t>> slice_arrays(const DenseOut &o) {
+  std::vector<std::pair<void *, size_t>> a;
+  a.push_back({o.keys, 8});
+  a.push_back({o.counts, 8});
+  for (size_t i = 0; i < o.kind.size(); i++) {
+    if (o.derive[i] == -1) a.push_back({o.values[i], 8});
+    if (o.kind[i] == 4) {
+      a.push_back({o.cards[i], 8});
+      a.push_back({o.hll ? o.hll->get<uint8_t>() + o.hll_off[i] : nullptr, 256});
+    }
+  }
+  return a;
+}
+
+std::unique_ptr<GroupByResult> slice_result(Engine &e, const pinot_query &q, const std::vector<int64_t> &gcard,
+                                            const std::vector<std::vector<std::string>> &gvalues, const DenseOut &o) {
+  return dense_fetch(e, q, gcard, gvalues, o, nullptr);
 }
 
 uint64_t dictionary_fingerprint(const ColumnData &c) {
@@ -2892,6 +3171,52 @@ uint64_t dictionary_fingerprint(const ColumnData &c) {
   return h;
 }
 
+std::vector<SegmentData *> prune_for_query(const std::vector<SegmentData *> &segs, const pinot_query &q) {
+  if (!q.pruners || segs.empty()) return segs;
+  std::unique_ptr<FilterTreeInput> tree;
+  if (q.num_filter_nodes > 0) tree = std::make_unique<FilterTreeInput>(decode_filter(q.num_filter_nodes, q.filter));
+  std::vector<SegmentData *> kept;
+  for (SegmentData *s : segs)
+    if (!prune_segment(*s, q, tree.get(), q.pruners)) kept.push_back(s);
+  return kept;
+}
+
+std::unique_ptr<GroupByResult> empty_group_result(const pinot_query &q) {
+  auto r = std::make_unique<GroupByResult>();
+  const int na = q.num_aggregations;
+  r->num_columns = q.num_group_by;
+  r->counts_shared = true;
+  for (int a = 0; a < na; a++) r->functions.push_back(q.aggregations[a].function);
+  r->counts.assign(na, {});
+  r->values.assign(na, {});
+  r->hll.assign(na, {});
+  r->hll_card.assign(na, {});
+  r->gcard.assign(q.num_group_by, 0);
+  r->gvalues.assign(q.num_group_by, {});
+  return r;
+}
+
+void agg_identities(const pinot_query &q, pinot_agg_result *out) {
+  for (int a = 0; a < q.num_aggregations; a++) {
+    memset(&out[a], 0, sizeof(pinot_agg_result));
+    out[a].has_exact_sum = 1;
+    const int f = q.aggregations[a].function;
+    out[a].value = f == PINOT_AGG_MIN ? INFINITY : f == PINOT_AGG_MAX ? -INFINITY : 0.0;
+  }
+}
+
+int64_t admission_possible(const std::vector<SegmentData *> &segs, const pinot_query &q, const Engine &e) {
+  const AdmissionPlan ap = plan_admission(segs, q, e, INT64_MAX);
+  int64_t possible = 0;
+  for (size_t i = 0; i < segs.size(); i++) {
+    __int128 product = 1;
+    for (int j = 0; j < q.num_group_by; j++) product *= segs[i]->column(q.group_by[j])->card;
+    const int64_t reach = (int64_t)std::min<__int128>(product, (__int128)segs[i]->num_docs);
+    possible += std::min(ap.upper[i], reach);
+  }
+  return possible;
+}
+
 // CombineService.mergeTwoBlocks (:48-90) over per-engine results of the same query: counts add, exact integer
 // sums add exactly (any non-exact part makes the sum a double sum), MIN / MAX compare, HLL registers max.
 void merge_agg_parts(const pinot_query &q, const std::vector<const pinot_agg_result *> &parts, pinot_agg_result *out) {
@@ -2903,16 +3228,16 @@ void merge_agg_parts(const pinot_query &q, const std::vector<const pinot_agg_res
     double dsum = 0.0;
     bool exact = true;
     double v = f == PINOT_AGG_MIN ? INFINITY : -INFINITY;
-    for (const pinot_agg_result *p : parts) {
+    for (const pinot_agg_result *p : parts) {  // Math.min / Math.max: NaN wins, -0.0 < 0.0
       const pinot_agg_result &x = p[a];
       r.count += x.count;
       if (f == PINOT_AGG_SUM || f == PINOT_AGG_AVG) {
         if (x.has_exact_sum) isum += x.exact_sum;
         else { dsum += x.value; exact = false; }
       } else if (f == PINOT_AGG_MIN) {
-        v = std::min(v, x.value);
+        v = java_min(v, x.value);
       } else if (f == PINOT_AGG_MAX) {
-        v = std::max(v, x.value);
+        v = java_max(v, x.value);
       } else if (f == PINOT_AGG_DISTINCTCOUNTHLL) {
         for (int j = 0; j < 256; j++) r.hll_registers[j] = std::max(r.hll_registers[j], x.hll_registers[j]);
       }

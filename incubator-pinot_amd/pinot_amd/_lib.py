@@ -75,7 +75,7 @@ class Query(C.Structure):
                 ("num_aggregations", C.c_int32), ("aggregations", C.POINTER(AggSpec)),
                 ("num_group_by", C.c_int32), ("group_by", C.POINTER(C.c_char_p)),
                 ("num_groups_limit", C.c_int32), ("max_init_group_holder_capacity", C.c_int32),
-                ("timeout_ms", C.c_int32), ("reserved", C.c_int32)]
+                ("timeout_ms", C.c_int32), ("pruners", C.c_int32)]
 
 
 class ExecStats(C.Structure):

@@ -281,7 +281,7 @@ def _postfix(tree, out, keep):
 class QueryMarshal:
     """Query dict -> `pinot_query` (keeps every buffer alive for the duration of the call)."""
 
-    def __init__(self, query, num_groups_limit=100000, max_init_group_holder_capacity=10000, timeout_ms=0):
+    def __init__(self, query, num_groups_limit=100000, max_init_group_holder_capacity=10000, timeout_ms=0, pruners=0):
         self.keep = []
         nodes = []
         _postfix(query.get("filter"), nodes, self.keep)
@@ -301,7 +301,7 @@ class QueryMarshal:
         self.keep.append(gcols)
         self.gcols = (C.c_char_p * max(len(gcols), 1))(*gcols)
         self.q = _lib.Query(len(nodes), self.nodes, len(aggs), self.aggs, len(gcols), self.gcols,
-                            num_groups_limit, max_init_group_holder_capacity, int(timeout_ms), 0)
+                            num_groups_limit, max_init_group_holder_capacity, int(timeout_ms), int(pruners))
 
 
 class GroupByResult:
@@ -482,30 +482,16 @@ class ServerExecutor:
         return arr
 
     def process_query(self, query, segments, trim=True, as_result=False):
+        """Every rank calls this with its own segments (possibly none): pruning (the executor's pruners, carried in
+        the query) and the merge across GPUs / ranks happen inside the library, where a failure on any rank fails
+        every rank with the same status instead of leaving peers in a collective."""
         if isinstance(query, PreparedQuery):
             query, m = query.query, query.marshal
         else:
             if isinstance(query, str):
                 query = compile_pql(query)
-            m = QueryMarshal(query, self.num_groups_limit, self.max_init, self.timeout_ms)
+            m = self._marshal(query)
         lib = self.server.lib
-        total = None
-        if self.pruners:  # ServerQueryExecutorV1Impl.pruneSegments (:270-294)
-            pruned = (C.c_uint8 * max(len(segments), 1))()
-            tdocs = C.c_int64()
-            check(lib.pinot_gpu_server_prune_segments(self.server.ptr, self._refs(segments), len(segments),
-                                                      C.byref(m.q), int(self.pruners), pruned, C.byref(tdocs)))
-            kept = [sg for i, sg in enumerate(segments) if not pruned[i]]
-            if getattr(self.server, "multi_process", False):
-                # every rank must join the library's collectives, and its statistics are merged across ranks: a
-                # rank whose segments were all pruned still runs them (they match nothing), totals stay the library's
-                segments = kept or segments
-            else:
-                segments, total = kept, tdocs.value
-            if not segments:
-                if as_result and query.get("group_by"):
-                    raise _lib.PinotGpuError(1, "every segment was pruned: no group-by result object")
-                return _empty_result(query), _pruned_stats(total)
         refs = self._refs(segments)
         stats = _lib.ExecStats()
         if query.get("group_by"):
@@ -521,14 +507,15 @@ class ServerExecutor:
             check(lib.pinot_gpu_server_aggregate(self.server.ptr, refs, len(segments), C.byref(m.q), out,
                                                  C.byref(stats)))
             res = [_agg_value(a["function"].upper(), out[i]) for i, a in enumerate(query["aggregations"])]
-        if total is not None:  # totalDocs counts the pruned segments too (:214-215)
-            stats.num_total_raw_docs = total
         return res, _stats(stats)
+
+    def _marshal(self, query):
+        return QueryMarshal(query, self.num_groups_limit, self.max_init, self.timeout_ms, self.pruners)
 
     def prepare(self, query):
         if isinstance(query, str):
             query = compile_pql(query)
-        return PreparedQuery(query, QueryMarshal(query, self.num_groups_limit, self.max_init, self.timeout_ms))
+        return PreparedQuery(query, self._marshal(query))
 
 
 def _segment_handles(segments):
@@ -577,23 +564,22 @@ class ServerQueryExecutor:
         against each segment's dictionary and runs the device path."""
         if isinstance(query, str):
             query = compile_pql(query)
-        return PreparedQuery(query, QueryMarshal(query, self.num_groups_limit, self.max_init, self.timeout_ms))
+        return PreparedQuery(query, QueryMarshal(query, self.num_groups_limit, self.max_init, self.timeout_ms,
+                                                 self.pruners))
 
     def process_query(self, query, segments, trim=True):
+        """processQuery: the library prunes (the executor's pruners travel in the query), plans and runs the rest;
+        totalDocs counts every segment, an all-pruned query gives the empty result."""
         if isinstance(query, PreparedQuery):
             query, m = query.query, query.marshal
         else:
             if isinstance(query, str):
                 query = compile_pql(query)
-            m = QueryMarshal(query, self.num_groups_limit, self.max_init, self.timeout_ms)
+            m = QueryMarshal(query, self.num_groups_limit, self.max_init, self.timeout_ms, self.pruners)
         lib = self.engine.lib
-        total = None
-        if self.pruners:
-            segments, total, handles = self._prune(m, segments)
-            if not segments:  # every segment pruned (:187-196)
-                return _empty_result(query), _pruned_stats(total)
-        else:
-            handles = _segment_handles(segments)
+        if not segments:
+            return _empty_result(query), _pruned_stats(0)
+        handles = _segment_handles(segments)
         stats = _lib.ExecStats()
         if query.get("group_by"):
             out = C.c_void_p()
@@ -607,8 +593,6 @@ class ServerQueryExecutor:
             check(lib.pinot_gpu_aggregate(self.engine.ptr, handles, len(segments), C.byref(m.q), out,
                                           C.byref(stats)))
             res = [_agg_value(a["function"].upper(), out[i]) for i, a in enumerate(query["aggregations"])]
-        if total is not None:  # totalDocs counts the pruned segments too (:214-215)
-            stats.num_total_raw_docs = total
         return res, _stats(stats)
 
     def process_query_datatable(self, query, segments, trim=True, server=None):

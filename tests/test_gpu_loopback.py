@@ -1,0 +1,247 @@
+"""The multi-GPU merge protocol with K > 1 ranks on the box's one GPU (server.loopback=1).
+
+Every rank of the communicator lives in this process on device 0 and the collectives are done by the library's
+loopback (an in-library device reduce / copy over the ranks' buffers in place of RCCL), so the code a multi-GPU
+server runs — the dictionary exchange and union key space, Gp padding, reduce-scatter slicing, per-rank owner
+finalize, the gather of every key range to rank 0, identity partials for ranks without segments, and the agreement
+that fails every rank together — executes with K = 2, 3 and 8 ranks and is checked against the oracle's
+CombineOperator / CombineGroupByOperator (CombineGroupByOperator.java:104-228, CombineOperator.java:75-196).
+
+Two forms: one server over K engines (pinot_gpu_server_create with device 0 repeated, one thread per engine inside
+the library) and K servers of the multi-process form (pinot_gpu_server_create_rank, one Python thread per rank, as
+one process per GPU would call it)."""
+import threading
+
+import numpy as np
+import pytest
+
+import pinot_oracle as O
+from pinot_amd import GpuServer, PinotGpuError, ServerExecutor, build_segment, compile_pql
+
+pytestmark = pytest.mark.gpu
+
+WORDS = ["a", "bb", "ccc", "P", "t", "zz", "Hello", "wé", "q%"]
+
+
+def _segments(rng, n, nseg, t_base=None):
+    """Segments whose group-by dictionaries differ (shifted g0 values, string subsets); t: a time-like column with
+    min / max metadata (t_base[i] + [0, 1000)) the ColumnValue pruner reads."""
+    segs = []
+    for i in range(nseg):
+        tb = 0 if t_base is None else t_base[i]
+        cols = {"g0": ("INT", (rng.integers(0, 300, n) + 7 * i).tolist()),
+                "g1": ("STRING", [WORDS[k] for k in rng.integers(0, len(WORDS) - (i % 3), n)]),
+                "m": ("INT", rng.integers(-5000, 1000000, n).tolist()),
+                "l": ("LONG", rng.integers(-2 ** 40, 2 ** 40, n).tolist()),
+                "d": ("DOUBLE", np.round(rng.normal(0, 100, n), 3).tolist()),
+                "h": ("INT", rng.integers(0, 5000, n).tolist()),
+                "t": ("INT", (rng.integers(0, 1000, n) + tb).tolist()),
+                "b": ("INT", rng.integers(0, 2, n).tolist())}
+        segs.append(build_segment("seg%d" % i, cols, inverted_columns=("g1",), min_max=True))
+    return segs
+
+
+GROUP_QUERIES = [
+    "SELECT COUNT(*), SUM(m), AVG(m), MIN(d), MAX(l), DISTINCTCOUNTHLL(h) FROM t WHERE m > 1000 GROUP BY g0, g1",
+    "SELECT SUM(d), MAX(m), COUNT(*) FROM t WHERE g1 IN ('a', 'zz', 'q%') OR h < 100 GROUP BY g1",
+    "SELECT COUNT(*), SUM(m), MIN(m), DISTINCTCOUNTHLL(l) FROM t WHERE t < 500 GROUP BY h",
+    # a key space smaller than the rank count: ranks with an empty key range
+    "SELECT COUNT(*), SUM(m), MAX(d) FROM t GROUP BY b",
+]
+AGG_QUERIES = [
+    "SELECT COUNT(*), SUM(m), AVG(l), MIN(m), MAX(d), SUM(d), DISTINCTCOUNTHLL(g1) FROM t WHERE h BETWEEN 10 AND 4000",
+    "SELECT COUNT(*), MIN(d), MAX(l) FROM t WHERE m = 123456789",
+    "SELECT COUNT(*), SUM(m), MIN(d) FROM t WHERE t < 500",
+]
+
+
+def _check_group(q, got, exp):
+    assert set(got) == set(exp), q
+    for k in exp:
+        for a, g, e in zip(q["aggregations"], got[k], exp[k]):
+            f = a["function"].upper()
+            if f == "AVG":
+                assert g.count == e[1] and abs(g.sum - e[0]) <= 1e-9 * max(1.0, abs(e[0]))
+            elif f == "DISTINCTCOUNTHLL":
+                assert g.cardinality() == e.cardinality()
+                assert (np.asarray(g.registers, dtype=np.int64) == e.reg).all()
+            elif a["column"] == "d":
+                assert abs(g - e) <= 1e-9 * max(1.0, abs(e))
+            else:
+                assert g == e, (k, a)
+
+
+def _check_agg(q, got, exp):
+    for a, g, e in zip(q["aggregations"], got, exp):
+        f = a["function"].upper()
+        if f == "AVG":
+            assert g.count == e[1] and abs(g.sum - e[0]) <= 1e-9 * max(1.0, abs(e[0]))
+        elif f == "DISTINCTCOUNTHLL":
+            assert g.cardinality() == e.cardinality()
+        elif a["column"] == "d":
+            assert g == e or abs(g - e) <= 1e-9 * max(1.0, abs(e))
+        else:
+            assert g == e, a
+
+
+def _threads(K, fn):
+    """fn(r) on K threads (ctypes releases the GIL in library calls); per rank (result, exception)."""
+    out = [None] * K
+    err = [None] * K
+
+    def run(r):
+        try:
+            out[r] = fn(r)
+        except BaseException as ex:  # noqa: BLE001 - reported per rank
+            err[r] = ex
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(K)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not any(t.is_alive() for t in th), "a rank is still blocked in the merge"
+    return out, err
+
+
+def _rank_servers(K, host_by_rank, config="server.loopback=1"):
+    uid = GpuServer.unique_id()
+    servers = [GpuServer.rank(0, K, r, uid, config) for r in range(K)]
+    segs = [[servers[r].engines[0].register(s) for s in host_by_rank[r]] for r in range(K)]
+    return servers, segs
+
+
+@pytest.mark.parametrize("K", [2, 3, 8])
+def test_loopback_one_server_k_engines(K):
+    """One server, K engines on device 0 (segment i -> engine i mod K; with 5 segments and K = 8 three engines hold
+    none), union dictionaries, pruned segments, a key space smaller than K."""
+    rng = np.random.default_rng(100 + K)
+    host = _segments(rng, 9000, 5, t_base=[0, 1000, 0, 1000, 0])
+    srv = GpuServer([0] * K, "server.loopback=1")
+    gsegs = [srv.engines[i % K].register(s) for i, s in enumerate(host)]
+    ex = ServerExecutor(srv, num_groups_limit=100000)
+    for text in GROUP_QUERIES:
+        q = compile_pql(text)
+        got, st = ex.process_query(q, gsegs, trim=False)
+        exp, scanned = O.execute_server(host, q)
+        assert st.num_docs_scanned == scanned and st.num_total_raw_docs == 5 * 9000
+        _check_group(q, got, exp)
+    for text in AGG_QUERIES:
+        q = compile_pql(text)
+        got, st = ex.process_query(q, gsegs)
+        exp, scanned = O.execute_server(host, q)
+        assert st.num_docs_scanned == scanned and st.num_total_raw_docs == 5 * 9000
+        _check_agg(q, got, exp)
+    srv.close()
+
+
+@pytest.mark.parametrize("K", [2, 3, 8])
+def test_loopback_rank_form(K):
+    """K servers of the multi-process form, one thread per rank: rank 0 returns the whole merged group-by result,
+    the others an empty one; aggregations are complete on every rank. Rank 1 holds only segments the `t < 500`
+    queries prune; with K = 8 some ranks hold no segment at all."""
+    rng = np.random.default_rng(200 + K)
+    nseg = 6
+    host = _segments(rng, 8000, nseg, t_base=[0, 1000, 0, 1000, 0, 0])
+    by_rank = [[] for _ in range(K)]
+    by_rank[1] = [host[1], host[3]]  # every segment of rank 1 is pruned by t < 500
+    rest = [host[i] for i in (0, 2, 4, 5)]
+    for i, s in enumerate(rest):
+        by_rank[(0 if K == 2 else 2 + i % (K - 2)) if K > 2 else 0].append(s)
+    servers, segs = _rank_servers(K, by_rank)
+    execs = [ServerExecutor(s, num_groups_limit=100000) for s in servers]
+    for text in GROUP_QUERIES:
+        q = compile_pql(text)
+        exp, scanned = O.execute_server(host, q)
+        out, err = _threads(K, lambda r: execs[r].process_query(q, segs[r], trim=False))
+        assert not any(err), err
+        got, st = out[0]
+        assert st.num_docs_scanned == scanned and st.num_total_raw_docs == nseg * 8000, text
+        _check_group(q, got, exp)
+        for r in range(1, K):
+            assert out[r][0] == {} and out[r][1].num_docs_scanned == scanned
+    for text in AGG_QUERIES:
+        q = compile_pql(text)
+        exp, scanned = O.execute_server(host, q)
+        out, err = _threads(K, lambda r: execs[r].process_query(q, segs[r]))
+        assert not any(err), err
+        for r in range(K):
+            got, st = out[r]
+            assert st.num_docs_scanned == scanned and st.num_total_raw_docs == nseg * 8000
+            _check_agg(q, got, exp)
+    for s in servers:
+        s.close()
+
+
+def test_loopback_key_ranges_without_gather():
+    """server.gather=0: every rank returns its own key range; the ranges are disjoint, ascend with the rank and
+    together are the oracle's result."""
+    K = 3
+    rng = np.random.default_rng(300)
+    host = _segments(rng, 7000, 4)
+    by_rank = [[host[0], host[3]], [host[1]], [host[2]]]
+    servers, segs = _rank_servers(K, by_rank, "server.loopback=1;server.gather=0")
+    q = compile_pql(GROUP_QUERIES[0])
+    exp, _ = O.execute_server(host, q)
+    from pinot_amd.executor import GroupByResult  # noqa: F401
+    out, err = _threads(K, lambda r: ServerExecutor(servers[r]).process_query(q, segs[r], trim=False, as_result=True))
+    assert not any(err), err
+    merged = {}
+    last = -1
+    for r in range(K):
+        res = out[r][0]
+        keys = res.raw_keys()
+        if len(keys):
+            assert keys[0] > last and (np.diff(keys) > 0).all()
+            last = keys[-1]
+        m = res.to_map()
+        assert not set(m) & set(merged)
+        merged.update(m)
+    _check_group(q, merged, exp)
+    for s in servers:
+        s.close()
+
+
+def test_loopback_failure_on_one_rank_fails_every_rank():
+    """A failure on one rank only — its segments lack a filter column (no pruning: unknown column, BAD_QUERY), or its
+    query budget is already spent (TIMEOUT) — fails EVERY rank with that status, and nobody hangs."""
+    K = 3
+    rng = np.random.default_rng(400)
+    host = _segments(rng, 5000, 3)
+    odd = build_segment("odd", {"g0": ("INT", rng.integers(0, 50, 5000).tolist()),
+                                "m": ("INT", rng.integers(0, 100, 5000).tolist())})
+    servers, segs = _rank_servers(K, [[host[0]], [odd], [host[1], host[2]]])
+    for text in ("SELECT COUNT(*), SUM(m) FROM t WHERE h < 100 GROUP BY g0", "SELECT COUNT(*), SUM(m) FROM t WHERE h < 100"):
+        q = compile_pql(text)
+        out, err = _threads(K, lambda r: ServerExecutor(servers[r], pruners=0).process_query(q, segs[r]))
+        assert all(isinstance(e, PinotGpuError) and e.status == 5 for e in err), err
+    q = compile_pql("SELECT COUNT(*), SUM(m) FROM t GROUP BY g0")
+    out, err = _threads(K, lambda r: ServerExecutor(servers[r], timeout_ms=(-1 if r == 2 else 0))
+                        .process_query(q, [segs[r][0]] if r != 1 else []))
+    assert all(isinstance(e, PinotGpuError) and e.status == 6 for e in err), err
+    # the communicator is still usable after a failed query (every rank left it together)
+    out, err = _threads(K, lambda r: ServerExecutor(servers[r]).process_query(q, segs[r] if r != 1 else []))
+    assert not any(err), err
+    exp, _ = O.execute_server([host[0], host[1], host[2]], q)
+    _check_group(q, out[0][0], exp)
+    for s in servers:
+        s.close()
+
+
+def test_loopback_no_rank_holds_a_segment():
+    """Every segment on every rank pruned: all ranks return the empty result (identities / no group) with totalDocs
+    over every segment."""
+    K = 2
+    rng = np.random.default_rng(500)
+    host = _segments(rng, 4000, 2, t_base=[1000, 2000])
+    servers, segs = _rank_servers(K, [[host[0]], [host[1]]])
+    q = compile_pql("SELECT COUNT(*), SUM(m) FROM t WHERE t < 500 GROUP BY g0")
+    out, err = _threads(K, lambda r: ServerExecutor(servers[r]).process_query(q, segs[r]))
+    assert not any(err), err
+    assert out[0][0] == {} and out[0][1].num_total_raw_docs == 8000 and out[0][1].num_segments_processed == 0
+    q = compile_pql("SELECT COUNT(*), SUM(m), MIN(d), MAX(d) FROM t WHERE t < 500")
+    out, err = _threads(K, lambda r: ServerExecutor(servers[r]).process_query(q, segs[r]))
+    assert not any(err), err
+    assert out[1][0] == [0, 0.0, float("inf"), float("-inf")] and out[1][1].num_total_raw_docs == 8000
+    for s in servers:
+        s.close()

@@ -1,20 +1,28 @@
 #!/usr/bin/env python3
 """Benchmark: rows scanned/s per query on synthetic dict-encoded fact segments (BASELINE.json metric).
 
-Default workload (BASELINE.json configs[1]): 8 segments x 125,000,000 docs per GPU
+Headline workload (BASELINE.json configs[1]): 8 segments x 125,000,000 docs per GPU
 (1B rows), 10 fixed-bit dictionary-encoded INT columns d0..d9 with cardinalities
 {16, 100, 1000, 4096, 10000, 65536, 1000, 1000, 2^20, 1000} (bits {4,7,10,12,14,16,10,10,20,10}),
 generated in HBM (seeded splitmix64), query
     SELECT COUNT(*), SUM(d8) FROM fact WHERE d2 BETWEEN 100 AND 599 AND d0 IN (1, 3, 5, 7)
---workload config4 (BASELINE.json configs[3]): the same table, the 1M-key scan-filter-group-by
+The same run also measures BASELINE.json configs[3] on the same segments and embeds it as "config4" in the line:
+the 1M-key scan-filter-group-by the north star's >= 70 % target names,
     SELECT SUM(d8), AVG(d8), DISTINCTCOUNTHLL(d5) FROM fact WHERE d2 < 800 GROUP BY d6, d7 TOP 10
-(num.groups.limit = 1,000,000 so no group is dropped).
-One step = one query over all of a rank's segments, results back on the host. With N ranks (torch.distributed.run)
-each GPU holds its own 8 segments (weak scaling; config 5 at N = 8) and the library's multi-GPU server merges
-the ranks inside the .so over RCCL (pinot_gpu_server_create_rank; the communicator id is shared through a gloo
-process group, which also carries the barriers and the max-over-ranks timing).
+(num.groups.limit = 1,000,000 so no group is dropped). --workload config4 makes it the headline instead.
 
-Prints ONE JSON line (rank 0). Launched as `python bench.py` (N=1) or via torch.distributed.run.
+One step = one query over all of the job's segments, results back on the host. GPUs (weak scaling, 8 segments per
+GPU, global segment i on GPU i mod N — config 5 at N = 8):
+  * N = 1 (default): one engine (pinot_gpu_aggregate / _group_by); --path server runs the same query through the
+    multi-GPU server with one GPU instead.
+  * --gpus N without WORLD_SIZE: ONE process serving N GPUs (pinot_gpu_server_create over devices 0..N-1: one
+    engine per GPU, RCCL communicators inside the library, the merge on the devices).
+  * under torch.distributed.run (WORLD_SIZE = N = --gpus): one process per GPU, each a rank of the library's
+    server (pinot_gpu_server_create_rank; the communicator id is shared through a gloo process group, which also
+    carries the barriers and the max-over-ranks timing); the merge runs over RCCL inside the library.
+The merge's own time (all-gathers, reduce-scatter, gather) is reported per phase in "merge_phases_ms".
+
+Prints ONE JSON line (rank 0).
 """
 import argparse
 import gc
@@ -36,6 +44,12 @@ CONFIG4_BYTES_PER_ROW = (10 + 10 + 10 + 20 + 16) / 8  # d2 filter + d6, d7 keys 
 BASE_SEED = 0x5EED0000
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (8.0 TB/s spec)
 BITS = {n: max(1, (c - 1).bit_length()) for n, c in COLUMNS}
+# device sources each workload's kernels are built from (a PMC traffic profile is reported only for these exact bytes)
+KERNEL_SOURCES = {
+    "config2": ("fused.hip", "scan.hip", "kernels.hip", "fused_common.h", "common.h", "device.h", "kernels.h"),
+    "config4": ("fused_group.hip", "groupby.hip", "kernels.hip", "fused_common.h", "common.h", "device.h",
+                "kernels.h"),
+}
 
 
 def algorithmic_bytes(num_docs):
@@ -47,6 +61,37 @@ def algorithmic_bytes(num_docs):
     agg = (num_docs * BITS["d8"] + 7) // 8 + bitset
     query = sum((num_docs * BITS[c] + 7) // 8 for c in ("d0", "d2", "d8"))
     return filt, agg, query
+
+
+def host_cpu_info():
+    """The host the CPU baseline runs on: CPUs this process may use (cgroup CPU quota, else the affinity mask —
+    what Java's availableProcessors() reports), the machine's count, and the CPU model (lscpu's 'Model name')."""
+    info = {"nproc": os.cpu_count()}
+    try:
+        info["affinity"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        info["affinity"] = os.cpu_count()
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) / int(period)))
+    except (OSError, ValueError):
+        pass
+    info["cgroup_cpus"] = quota
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    info["model"] = model
+    info["available_processors"] = min(x for x in (quota, info["affinity"]) if x)
+    return info
 
 
 def cpu_baseline(threads, segs, docs, min_seconds=10.0):
@@ -62,7 +107,7 @@ def cpu_baseline(threads, segs, docs, min_seconds=10.0):
     # generate the sample columns in parallel (ctypes releases the GIL)
     table = faithful.SyntheticTable(COLUMNS, docs, 0, BASE_SEED, needed=set())
     jobs = {}
-    with ThreadPoolExecutor(threads) as ex:
+    with ThreadPoolExecutor(min(threads, 32)) as ex:
         for s in range(segs):
             for i, (name, card) in enumerate(COLUMNS):
                 if name in ("d0", "d2", "d8"):
@@ -110,7 +155,7 @@ def cpu_baseline_config4(threads, segs, docs, min_seconds=10.0):
     t0 = time.time()
     table = faithful.SyntheticTable(COLUMNS, docs, 0, BASE_SEED, needed=set())
     jobs = {}
-    with ThreadPoolExecutor(threads) as ex:
+    with ThreadPoolExecutor(min(threads, 32)) as ex:
         for s in range(segs):
             for i, (name, card) in enumerate(COLUMNS):
                 if name in need:
@@ -134,19 +179,15 @@ def cpu_baseline_config4(threads, segs, docs, min_seconds=10.0):
                       (segs, docs, len(times), sum(times), med, groups, gen_s)}
 
 
-def kernel_source_hash():
-    """Hash of the device code's sources — every .hip file and the headers they include (csrc/common.h, device.h,
-    fused_common.h, kernels.h and include/pinot_gpu.h) — that the PMC traffic figures were measured on: a stale
-    profile must not be reported. Host-only sources (engine.h, *.cpp) do not change the kernels."""
+def kernel_source_hash(workload="config2"):
+    """Hash of the device code a workload's kernels are built from (KERNEL_SOURCES): the PMC traffic figures are
+    reported only while the sources still hash to the ones they were measured on."""
     import hashlib
     h = hashlib.sha256()
     csrc = os.path.join(REPO, "incubator-pinot_amd", "csrc")
-    files = [f for f in sorted(os.listdir(csrc))
-             if f.endswith(".hip") or f in ("common.h", "device.h", "fused_common.h", "kernels.h")]
-    paths = [os.path.join(csrc, f) for f in files] + [os.path.join(REPO, "include", "pinot_gpu.h")]
-    for path in paths:
-        with open(path, "rb") as fh:
-            h.update(os.path.basename(path).encode() + fh.read())
+    for f in sorted(KERNEL_SOURCES[workload]):
+        with open(os.path.join(csrc, f), "rb") as fh:
+            h.update(f.encode() + fh.read())
     return h.hexdigest()[:16]
 
 
@@ -160,122 +201,164 @@ def measured_traffic(workload, kernel):
             t = json.load(f)
     except (OSError, ValueError):
         return None
-    if t.get("kernel_source_hash") != kernel_source_hash():
+    if t.get("kernel_source_hash") != kernel_source_hash(workload):
         return None
     return t.get("bytes_per_launch", {}).get(kernel)
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=50)
-    ap.add_argument("--workload", default="config2", choices=("config2", "config4"))
-    ap.add_argument("--segments", type=int, default=8, help="segments per GPU")
-    ap.add_argument("--docs", type=int, default=125_000_000, help="docs per segment")
-    ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--cpu-segments", type=int, default=None)
-    ap.add_argument("--cpu-docs", type=int, default=None)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-verify", action="store_true",
-                    help="skip the full-size check of the GPU result against the C oracle (config 2)")
-    ap.add_argument("--engine-config", default="", help='engine keys, e.g. "exec.fused=0" (unfused launches)')
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    args = ap.parse_args()
-    c4 = args.workload == "config4"
+class Job:
+    """The GPUs and segments of this process, and how one query runs over them."""
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    def __init__(self, args, world, rank, local_rank):
+        from pinot_amd import GpuEngine, GpuServer, ServerExecutor, ServerQueryExecutor
+        cfg = args.engine_config or None
+        self.world, self.rank = world, rank
+        self.server = None
+        self.dist = None
+        if world > 1:
+            # control plane only (communicator id, barriers, max-over-ranks timing); the merge is RCCL in the .so
+            import torch
+            import torch.distributed as dist
+            dist.init_process_group("gloo")
+            self.dist = dist
+            from pinot_amd import GpuServer as GS
+            uid = torch.tensor(list(GS.unique_id()) if rank == 0 else [0] * 128, dtype=torch.uint8)
+            dist.broadcast(uid, 0)
+            self.server = GpuServer.rank(local_rank, world, rank, bytes(uid.tolist()), cfg)
+            self.path = "rank"
+        elif args.gpus > 1 or args.path == "server":
+            self.server = GpuServer(list(range(args.gpus)), cfg)
+            self.path = "server"
+        else:
+            self.engine = GpuEngine(0, cfg)
+            self.path = "engine"
+        if self.server is not None:
+            self.engines = self.server.engines
+            self.ex = ServerExecutor(self.server, num_groups_limit=1_000_000)
+        else:
+            self.engines = [self.engine]
+            self.ex = ServerQueryExecutor(self.engine, num_groups_limit=1_000_000)
+        self.n_gpus = world if world > 1 else len(self.engines)
+        self.segs = []
+        t0 = time.time()
+        local = len(self.engines)
+        for s in range(args.segments * local):
+            gidx = s * world + rank  # global segment i is served by rank i mod world (SURVEY.md §8e)
+            eng = self.engines[s % local]  # ... and by engine i mod N within one process
+            self.segs.append(eng.register_synthetic("fact_%d" % gidx, args.docs, COLUMNS, BASE_SEED + gidx))
+        for e in self.engines:
+            e.synchronize()
+        self.load_s = time.time() - t0
+        self.total_rows = self.n_gpus * args.segments * args.docs
+
+    def step_fn(self, query_text, group_by):
+        q = self.ex.prepare(query_text)  # compiled + marshalled once; every step still prunes, plans and runs
+        if not group_by:
+            return lambda: self.ex.process_query(q, self.segs)
+        if self.path == "engine":
+            return lambda: self.ex.group_by_result(q, self.segs)
+        return lambda: self.ex.process_query(q, self.segs, as_result=True)
+
+    def set_config(self, cfg):
+        for e in self.engines:
+            e.set_config(cfg)
+
+    def synchronize(self):
+        for e in self.engines:
+            e.synchronize()
+
+    def barrier(self):
+        if self.dist:
+            self.dist.barrier()
+
+    def max_over_ranks(self, x):
+        if not self.dist:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def close(self):
+        if self.dist:
+            self.dist.barrier()
+        if self.server is not None:
+            self.server.close()
+        if self.dist:
+            self.dist.destroy_process_group()
+
+
+def timed_steps(job, step, steps, warmup):
+    """W untimed warm-ups, then exactly K steps bracketed by barrier + device sync; max over ranks."""
     import torch
-    dist = None
-    torch.cuda.set_device(local_rank if world > 1 else 0)
-    from pinot_amd import GpuEngine, GpuServer, ServerExecutor, ServerQueryExecutor
-    if world > 1:
-        # control plane only (communicator id, barriers, max-over-ranks timing); the data merge is RCCL inside the .so
-        import torch.distributed as dist
-        dist.init_process_group("gloo")
-        uid = torch.tensor(list(GpuServer.unique_id()) if rank == 0 else [0] * 128, dtype=torch.uint8)
-        dist.broadcast(uid, 0)
-        server = GpuServer.rank(local_rank, world, rank, bytes(uid.tolist()), args.engine_config or None)
-        eng = server.engines[0]
-        ex = ServerExecutor(server, num_groups_limit=1_000_000)
-    else:
-        eng = GpuEngine(0, args.engine_config or None)
-        ex = ServerQueryExecutor(eng, num_groups_limit=1_000_000)
-    segs = []
-    t0 = time.time()
-    for s in range(args.segments):
-        gidx = s * world + rank  # global segment i is served by rank i mod world
-        segs.append(eng.register_synthetic("fact_%d" % gidx, args.docs, COLUMNS, BASE_SEED + gidx))
-    eng.synchronize()
-    load_s = time.time() - t0
-    q = ex.prepare(CONFIG4 if c4 else QUERY)  # compiled + marshalled once; every step still plans and runs the device path
-
-    if c4:
-        def step():
-            res, st = (ex.process_query(q, segs, as_result=True) if world > 1 else ex.group_by_result(q.query, segs))
-            return res, st
-    else:
-        def step():
-            res, st = ex.process_query(q, segs)
-            return res, st
-
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
-    if dist:
-        dist.barrier()
+    job.barrier()
     torch.cuda.synchronize()
-    eng.synchronize()
+    job.synchronize()
     gc.collect()
     gc.disable()  # the harness's own collector pauses stay out of the timed steps (the C-ABI call has none)
     t0 = time.perf_counter()
     step_ms, abi_ms = [], []
-    for _ in range(args.steps):
+    res = st = None
+    for _ in range(steps):
         ts = time.perf_counter()
         res, st = step()  # synchronous: results are on the host when it returns
         step_ms.append((time.perf_counter() - ts) * 1e3)
         abi_ms.append(st.host_ms)
-    eng.synchronize()
+    job.synchronize()
     torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
+    job.barrier()
     elapsed = time.perf_counter() - t0
     gc.enable()
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    ms_per_step = elapsed * 1000.0 / args.steps
-    total_rows = world * args.segments * args.docs
-    value = total_rows * args.steps / elapsed
+    return job.max_over_ranks(elapsed), step_ms, abi_ms, res, st
 
-    # per-kernel device time (HIP events on the engine's own stream) in a separate pass
-    eng.set_config("timing=1")
+
+def kernel_pass(job, step, reps):
+    """Per-kernel device time (HIP events on engine 0's own stream) and the server's merge phases, in a separate
+    pass with timing=1."""
+    job.set_config("timing=1")
     kt = {0: [0.0, 0], 1: [0.0, 0]}
-    reps = max(3, min(args.steps, 10))
+    phases = {}
+    eng = job.engines[0]
     for _ in range(reps):
         step()
         for k in (0, 1):
             ms, n = eng.last_kernel_ms(k)
             kt[k][0] += ms
             kt[k][1] += n
-    eng.set_config("timing=0")
+        if job.server is not None:
+            for k, v in job.server.last_phases().items():
+                phases[k] = phases.get(k, 0.0) + v / reps
+    job.set_config("timing=0")
+    return kt, phases
+
+
+def measure(job, args, workload):
+    c4 = workload == "config4"
+    step = job.step_fn(CONFIG4 if c4 else QUERY, c4)
+    steps = args.steps if not c4 or args.workload == "config4" else args.c4_steps
+    elapsed, step_ms, abi_ms, res, st = timed_steps(job, step, steps, args.warmup)
+    ms_per_step = elapsed * 1000.0 / steps
+    value = job.total_rows * steps / elapsed
+    reps = max(3, min(steps, 10))
+    kt, phases = kernel_pass(job, step, reps)
+    segs_here = args.segments  # per GPU: engine 0's share
     kern = {}
     if c4:
-        # the group-by pipeline of one query (COUNT histogram, scan, EMIT, split, partition reduce: one timed region)
-        alg = args.segments * args.docs * CONFIG4_BYTES_PER_ROW
+        alg = segs_here * args.docs * CONFIG4_BYTES_PER_ROW
+        # the group-by pipeline of one query on engine 0 (COUNT histogram, scan, EMIT, partition reduce: one region)
         names = ((1, "group_by_pipeline", alg),)
         query_b = alg
     else:
         filt_b, agg_b, query_b1 = algorithmic_bytes(args.docs)
-        query_b = query_b1 * args.segments
+        query_b = query_b1 * segs_here
         if kt[1][1] == 0:
             # fused path: ONE k_scan_query launch per query reads the three packed streams of every segment
             # of this GPU (no bitset traffic): algorithmic bytes per launch = segments x 4.25 B/row x docs
             names = ((0, "k_scan_query", query_b),)
         else:
-            names = ((0, "k_leaf", filt_b * args.segments), (1, "k_colagg", agg_b * args.segments))
+            names = ((0, "k_leaf", filt_b * segs_here), (1, "k_colagg", agg_b * segs_here))
     for k, name, b in names:
         launches_per_query = max(kt[k][1] // reps, 1)
         per_launch_b = b / launches_per_query
@@ -284,14 +367,14 @@ def main():
                       "total_ms_per_query": kt[k][0] / reps,
                       "gbs": per_launch_b / (avg_ms / 1e3) / 1e9 if avg_ms > 0 else 0.0}
     dom = max(kern, key=lambda n: kern[n]["total_ms_per_query"])
+    # per GPU: this GPU's algorithmic bytes over the query time
     query_gbs = query_b / (ms_per_step / 1e3) / 1e9
-
     out = {
         "metric": "rows scanned/sec per query",
         "value": value,
         "unit": "rows/s",
-        "n_gpus": world,
-        "steps": args.steps,
+        "n_gpus": job.n_gpus,
+        "steps": steps,
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "p50_query_ms": float(np.median(step_ms)),
@@ -304,23 +387,25 @@ def main():
         "dtype": "u32 dictIds / int64 sums" + (" / u8 HLL registers" if c4 else ""),
         "data": "synthetic (seeded splitmix64 dict-encoded segments generated in HBM)",
         "config": {"workload": "%s: %d x %d-doc segments per GPU, 10 fixed-bit INT columns, %s" %
-                   (args.workload, args.segments, args.docs, CONFIG4 if c4 else QUERY),
+                   (workload, args.segments, args.docs, CONFIG4 if c4 else QUERY),
                    "segments_per_gpu": args.segments, "docs_per_segment": args.docs,
-                   "parallelism": "segments%d" % world},
+                   "parallelism": "segments%d" % job.n_gpus, "path": job.path},
         "roofline": {"bound": "hbm", "achieved": kern[dom]["gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": kern[dom]["gbs"] / HBM_PEAK_GBS, "traffic": measured_traffic(args.workload, dom),
+                     "frac": kern[dom]["gbs"] / HBM_PEAK_GBS, "traffic": measured_traffic(workload, dom),
                      "kernel": dom, "kernels": kern, "query_algorithmic_gbs": query_gbs,
                      "query_frac": query_gbs / HBM_PEAK_GBS},
-        "segment_load_s": load_s,
     }
+    if phases:
+        out["merge_phases_ms"] = phases
     if c4:
         n_groups = res.num_groups()
         counts, sums = res.function_values(1)  # AVG(d8): per-group counts and sums
-        chk, _ = ex.process_query(ex.prepare("SELECT COUNT(*), SUM(d8) FROM fact WHERE d2 < 800"), segs)
+        chk, _ = job.ex.process_query(job.ex.prepare("SELECT COUNT(*), SUM(d8) FROM fact WHERE d2 < 800"), job.segs)
         tot = [int(counts.sum()), int(sums.sum())]
-        if dist:  # each rank holds its key range of the merged groups
+        if job.dist:  # rank 0 holds the gathered result, the other ranks none
+            import torch
             t = torch.tensor([n_groups] + tot, dtype=torch.int64)
-            dist.all_reduce(t)
+            job.dist.all_reduce(t)
             n_groups, tot = int(t[0]), [int(t[1]), int(t[2])]
         out["result"] = {"groups": n_groups, "sum_group_counts": tot[0], "sum_group_sums": tot[1]}
         out["verify"] = {"filtered_count": chk[0], "filtered_sum": int(chk[1]),
@@ -329,45 +414,101 @@ def main():
                                 "filter (independent kernel path); group-level parity: tests/test_gpu_configs.py"}
     else:
         out["result"] = {"count": res[0], "sum": int(res[1]), "docs_scanned": st.num_docs_scanned}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        if c4:
+    return out
+
+
+def verify_config2(job, args, out, res_count, res_sum):
+    """The full-size result against the C oracle (reference-faithful executor) over every segment of the job."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import faithful
+    from concurrent.futures import ThreadPoolExecutor
+    tot_c, tot_s = 0, 0.0
+    names = [(i, n, c) for i, (n, c) in enumerate(COLUMNS) if n in ("d0", "d2", "d8")]
+    tab = faithful.SyntheticTable(COLUMNS, args.docs, 0, BASE_SEED, needed=set())
+    t0 = time.time()
+    with ThreadPoolExecutor(min(args.cpu_threads, 32)) as pool:
+        for s in range(args.segments * job.n_gpus):
+            cols = {n: pool.submit(faithful.synth_column, BASE_SEED + s, i, c, args.docs) for i, n, c in names}
+            tab.segments = [{n: f.result() for n, f in cols.items()}]
+            c, v = faithful.run_and_count_sum(tab, [("d2", ("RANGE", 100, 600)), ("d0", ("IN", [1, 3, 5, 7]))],
+                                              "d8", args.cpu_threads)
+            tot_c += c
+            tot_s += v
+    return {"oracle_count": tot_c, "oracle_sum": int(tot_s), "seconds": time.time() - t0,
+            "match": tot_c == res_count and int(tot_s) == res_sum}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--workload", default="config2", choices=("config2", "config4"))
+    ap.add_argument("--no-config4", action="store_true", help="config2 line without the embedded config-4 object")
+    ap.add_argument("--c4-steps", type=int, default=None, help="timed steps of the embedded config 4 (default --steps)")
+    ap.add_argument("--path", default="auto", choices=("auto", "engine", "server"),
+                    help="N = 1: one engine (auto) or the multi-GPU server over one GPU")
+    ap.add_argument("--segments", type=int, default=8, help="segments per GPU")
+    ap.add_argument("--docs", type=int, default=125_000_000, help="docs per segment")
+    ap.add_argument("--cpu-threads", type=int, default=None,
+                    help="CPU baseline worker threads (default: 2 x available processors, ResourceManager.java:56-57)")
+    ap.add_argument("--cpu-segments", type=int, default=None)
+    ap.add_argument("--cpu-docs", type=int, default=None)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-verify", action="store_true",
+                    help="skip the full-size check of the GPU result against the C oracle (config 2)")
+    ap.add_argument("--engine-config", default="", help='engine keys, e.g. "exec.fused=0" (unfused launches)')
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    args = ap.parse_args()
+    if args.c4_steps is None:
+        args.c4_steps = args.steps
+    host = host_cpu_info()
+    if args.cpu_threads is None:
+        args.cpu_threads = min(2 * host["available_processors"], 128)
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        assert world == args.gpus, "under torch.distributed.run WORLD_SIZE (%d) must equal --gpus (%d)" % (world,
+                                                                                                        args.gpus)
+    import torch
+    torch.cuda.set_device(local_rank if world > 1 else 0)
+    job = Job(args, world, rank, local_rank)
+
+    out = measure(job, args, args.workload)
+    out["segment_load_s"] = job.load_s
+    head_res = dict(out["result"])
+    if args.workload == "config2" and not args.no_config4:
+        c4 = measure(job, args, "config4")
+        keep = ("value", "unit", "ms_per_step", "p50_query_ms", "p50_c_abi_ms", "step_ms_detail", "steps", "warmup",
+                "dtype", "config", "roofline", "merge_phases_ms", "result", "verify")
+        out["config4"] = {k: c4[k] for k in keep if k in c4}
+    cpu_ok = rank == 0 and world == 1 and job.n_gpus == 1 and not args.no_cpu_baseline
+    if cpu_ok:
+        host_desc = {"host": host, "threads": args.cpu_threads}
+        if args.workload == "config4":
             cb = cpu_baseline_config4(args.cpu_threads, args.cpu_segments or 16, args.cpu_docs or 4_000_000,
                                       args.cpu_seconds)
         else:
-            cb = cpu_baseline(args.cpu_threads, args.cpu_segments or 16, args.cpu_docs or 32_000_000, args.cpu_seconds)
+            cb = cpu_baseline(args.cpu_threads, args.cpu_segments or 16, args.cpu_docs or 32_000_000,
+                              args.cpu_seconds)
         out["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample")}
-        out["gpu_vs_cpu"] = value / cb["value"]
+        out["cpu_baseline"].update(host_desc)
+        out["gpu_vs_cpu"] = out["value"] / cb["value"]
         if "optimized" in cb:  # SURVEY §8(d)'s second CPU line
             out["cpu_baseline_optimized"] = {k: cb["optimized"][k] for k in ("value", "unit", "cores", "kind", "sample")}
-            out["gpu_vs_cpu_optimized"] = value / cb["optimized"]["value"]
-    if not c4 and not args.no_verify and rank == 0:
-        # the full-size result against the C oracle (reference-faithful executor) over every segment of every rank
-        sys.path.insert(0, os.path.join(REPO, "oracle"))
-        import faithful
-        from concurrent.futures import ThreadPoolExecutor
-        tot_c, tot_s = 0, 0.0
-        names = [(i, n, c) for i, (n, c) in enumerate(COLUMNS) if n in ("d0", "d2", "d8")]
-        tab = faithful.SyntheticTable(COLUMNS, args.docs, 0, BASE_SEED, needed=set())
-        t0 = time.time()
-        with ThreadPoolExecutor(args.cpu_threads) as pool:
-            for s in range(args.segments * world):
-                cols = {n: pool.submit(faithful.synth_column, BASE_SEED + s, i, c, args.docs) for i, n, c in names}
-                tab.segments = [{n: f.result() for n, f in cols.items()}]
-                c, v = faithful.run_and_count_sum(tab, [("d2", ("RANGE", 100, 600)), ("d0", ("IN", [1, 3, 5, 7]))],
-                                                  "d8", args.cpu_threads)
-                tot_c += c
-                tot_s += v
-        agg = out["result"]
-        if dist:
-            agg = {"count": res[0], "sum": int(res[1])}  # merged over every rank by the server
-        out["verify"] = {"oracle_count": tot_c, "oracle_sum": int(tot_s), "seconds": time.time() - t0,
-                         "match": tot_c == agg["count"] and int(tot_s) == agg["sum"]}
+            out["gpu_vs_cpu_optimized"] = out["value"] / cb["optimized"]["value"]
+        if "config4" in out:
+            cb4 = cpu_baseline_config4(args.cpu_threads, args.cpu_segments or 16, args.cpu_docs or 4_000_000,
+                                       args.cpu_seconds)
+            out["config4"]["cpu_baseline"] = dict(cb4, **host_desc)
+            out["config4"]["gpu_vs_cpu"] = out["config4"]["value"] / cb4["value"]
+    if args.workload == "config2" and not args.no_verify and rank == 0:
+        out["verify"] = verify_config2(job, args, out, head_res["count"], head_res["sum"])
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if dist:
-        dist.barrier()
-        server.close()
-        dist.destroy_process_group()
+    job.close()
 
 
 if __name__ == "__main__":

@@ -403,6 +403,12 @@ pinot_status pinot_gpu_server_aggregate(pinot_server *server, const pinot_segmen
                                         const pinot_query *query, pinot_agg_result *out, pinot_exec_stats *stats);
 pinot_status pinot_gpu_server_group_by(pinot_server *server, const pinot_segment_ref *segments, int32_t num_segments,
                                        const pinot_query *query, pinot_groupby_result **out, pinot_exec_stats *stats);
+/* Host wall time (ms) of the phases of the server's last query as its first engine's rank ran it (n <= 8 values):
+ *   [0] local work (aggregation: prune + plan + run; group-by: prune + dictionaries)  [1] all-gather of the ranks'
+ *   headers (aggregation: of their results) + the global key space  [2] group-by partials on the device
+ *   [3] agreement after the partials  [4] reduce-scatter (its device time when the engine has timing=1, else the
+ *   launch)  [5] owner finalize (compaction + outputs)  [6] gather to rank 0 + D2H  [7] total. */
+pinot_status pinot_gpu_server_last_phases(const pinot_server *server, double *ms, int32_t n);
 /* pinot_gpu_prune_segments over segments spread across the server's engines. */
 pinot_status pinot_gpu_server_prune_segments(pinot_server *server, const pinot_segment_ref *segments,
                                              int32_t num_segments, const pinot_query *query, int32_t pruners,

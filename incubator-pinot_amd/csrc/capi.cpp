@@ -573,6 +573,13 @@ pinot_status pinot_gpu_server_destroy(pinot_server *server) {
   return guard([&] { delete server; });
 }
 
+pinot_status pinot_gpu_server_last_phases(const pinot_server *server, double *ms, int32_t n) {
+  return guard([&] {
+    require(server && server->impl && ms && n >= 0, PINOT_ERR_BAD_ARG, "null argument");
+    server_last_phases(*server->impl, ms, n);
+  });
+}
+
 int32_t pinot_gpu_server_num_engines(const pinot_server *server) {
   return server && server->impl ? server_num_engines(*server->impl) : 0;
 }

@@ -362,6 +362,8 @@ ServerImpl *server_create_rank(int32_t device, int32_t nranks, int32_t rank, con
                              const char *config);
 void server_unique_id(uint8_t *id);
 void server_destroy(ServerImpl *s);
+constexpr int kServerPhases = 8;
+void server_last_phases(const ServerImpl &s, double *ms, int n);
 int server_num_engines(const ServerImpl &s);
 Engine *server_engine(ServerImpl &s, int i);
 void server_aggregate(ServerImpl &s, const std::vector<SegmentRef> &refs, const pinot_query &q, pinot_agg_result *out,

@@ -43,9 +43,30 @@ struct ServerImpl {
   bool gather = true;                                  // group-by: the whole result on rank 0
   std::mutex mu;                                       // one server call at a time (engines are locked too)
   std::vector<DeviceBuffer> partial;                   // per engine: dense group-by partials
+  double phase_ms[kServerPhases] = {};                 // last query, local engine 0's rank (server_last_phases)
 };
 
 namespace {
+
+using Clock = std::chrono::steady_clock;
+double ms_since(Clock::time_point t) { return std::chrono::duration<double, std::milli>(Clock::now() - t).count(); }
+
+// phase timer of local engine 0 (the other engines' threads pass nullptr)
+struct Phases {
+  double *ms;
+  Clock::time_point t0 = Clock::now(), last = t0;
+  explicit Phases(double *m) : ms(m) {
+    if (ms) std::fill(ms, ms + kServerPhases, 0.0);
+  }
+  void mark(int i) {
+    const auto now = Clock::now();
+    if (ms) ms[i] += std::chrono::duration<double, std::milli>(now - last).count();
+    last = now;
+  }
+  ~Phases() {
+    if (ms) ms[kServerPhases - 1] = ms_since(t0);
+  }
+};
 
 struct ServerConfig {
   bool loopback = false;
@@ -284,6 +305,10 @@ ServerImpl *server_create_rank(int32_t device, int32_t nranks, int32_t rank, con
 
 void server_destroy(ServerImpl *s) { delete s; }
 int server_num_engines(const ServerImpl &s) { return (int)s.engines.size(); }
+void server_last_phases(const ServerImpl &s, double *ms, int n) {
+  for (int i = 0; i < n && i < kServerPhases; i++) ms[i] = s.phase_ms[i];
+}
+
 Engine *server_engine(ServerImpl &s, int i) {
   require(i >= 0 && i < (int)s.engines.size(), PINOT_ERR_BAD_ARG, "engine index");
   return s.engines[i].get();
@@ -302,6 +327,7 @@ void server_aggregate(ServerImpl &s, const std::vector<SegmentRef> &refs, const 
   for_engines(s, [&](size_t i) {
     Engine &e = *s.engines[i];
     Collective &c = *s.comms[i];
+    Phases ph(i == 0 ? s.phase_ms : nullptr);
     std::vector<pinot_agg_result> part(na);
     pinot_exec_stats st{};
     const Status my = capture([&] {
@@ -316,11 +342,13 @@ void server_aggregate(ServerImpl &s, const std::vector<SegmentRef> &refs, const 
       }
       st.num_total_raw_docs = tdocs;
     });
+    ph.mark(0);
     Writer w;
     put_status(w, my);
     put_stats(w, st);
     w.raw(part.data(), sizeof(pinot_agg_result) * na);
     const auto all = c.all_gather_host(w.b, e.stream);
+    ph.mark(1);
     std::vector<Status> sts;
     std::vector<std::vector<pinot_agg_result>> parts(all.size(), std::vector<pinot_agg_result>(na));
     for (size_t r = 0; r < all.size(); r++) {
@@ -353,6 +381,7 @@ std::unique_ptr<GroupByResult> server_group_by(ServerImpl &s, const std::vector<
   for_engines(s, [&](size_t i) {
     Engine &e = *s.engines[i];
     Collective &c = *s.comms[i];
+    Phases ph(i == 0 ? s.phase_ms : nullptr);
     const int R = c.nranks(), me = c.rank();
     // A: prune, local dictionaries and accumulator kinds -> every rank's
     std::vector<SegmentData *> segs;
@@ -368,6 +397,7 @@ std::unique_ptr<GroupByResult> server_group_by(ServerImpl &s, const std::vector<
         possible = admission_possible(segs, q, e);
       }
     });
+    ph.mark(0);
     Writer wa;
     put_status(wa, my);
     wa.i64(tdocs);
@@ -398,6 +428,7 @@ std::unique_ptr<GroupByResult> server_group_by(ServerImpl &s, const std::vector<
     require(kinds_agree, PINOT_ERR_UNSUPPORTED, "multi-GPU group-by: ranks disagree on the aggregated columns' types");
     GlobalKeySpace ks;
     if (!gkinds.empty()) ks = global_key_space(segs, q, rank_dicts);  // identical on every rank (same inputs)
+    ph.mark(1);
     const int64_t limit = q.num_groups_limit > 0 ? q.num_groups_limit : e.num_groups_limit;
     require(!ks.hashed, PINOT_ERR_UNSUPPORTED,
             "multi-GPU group-by needs a dense key space (LONG_MAP / ARRAY_MAP shapes: one GPU)");
@@ -438,10 +469,12 @@ std::unique_ptr<GroupByResult> server_group_by(ServerImpl &s, const std::vector<
                                  accs.data(), &st);
       PINOT_HIP(hipStreamSynchronize(e.stream));
     });
+    ph.mark(2);
     Writer wb;
     put_status(wb, my);
     put_stats(wb, st);
     const auto all_b = c.all_gather_host(wb.b, e.stream);
+    ph.mark(3);
     sts.clear();
     for (const auto &blob : all_b) {
       Reader rd{blob};
@@ -459,6 +492,8 @@ std::unique_ptr<GroupByResult> server_group_by(ServerImpl &s, const std::vector<
         c.reduce_scatter(accs[a], (size_t)slice * (gkinds[a] == 4 ? 256 : 1), acc_ctype(gkinds[a]), acc_op(gkinds[a]),
                          e.stream);
     c.group_end();
+    if (e.timing) PINOT_HIP(hipStreamSynchronize(e.stream));  // the merge's device time on its own
+    ph.mark(4);
     // D: owner finalize of this rank's key range, then the gather to rank 0
     const int64_t base = (int64_t)me * slice;
     const int64_t g = std::max<int64_t>(0, std::min<int64_t>(slice, G - base));
@@ -466,8 +501,10 @@ std::unique_ptr<GroupByResult> server_group_by(ServerImpl &s, const std::vector<
     for (int a = 0; a < na; a++)
       if (accs[a]) sl[a] = static_cast<uint8_t *>(accs[a]) + (size_t)base * acc_unit(gkinds[a]);
     const DenseOut own = slice_outputs(e, q, gkinds, counts + base, sl, g, base);
+    ph.mark(5);
     if (!s.gather || R == 1) {
       res[i] = slice_result(e, q, ks.gcard, ks.gvalues, own);
+      ph.mark(6);
       return;
     }
     Writer wn;
@@ -497,6 +534,7 @@ std::unique_ptr<GroupByResult> server_group_by(ServerImpl &s, const std::vector<
       res[i] = slice_result(e, q, ks.gcard, ks.gvalues, none);
       PINOT_HIP(hipStreamSynchronize(e.stream));  // the sends have left this rank's buffers
     }
+    ph.mark(6);
   });
   std::unique_ptr<GroupByResult> out = std::move(res[0]);
   if (!s.gather && E > 1) {  // one process, several GPUs, key ranges kept apart: concatenate them (ascending)

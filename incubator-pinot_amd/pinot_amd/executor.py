@@ -448,6 +448,14 @@ class GpuServer:
         srv.multi_process = True
         return srv
 
+    PHASES = ("local", "exchange", "partials", "agree", "reduce_scatter", "finalize", "gather_d2h", "total")
+
+    def last_phases(self):
+        """pinot_gpu_server_last_phases: host ms per phase of the last query on the first engine's rank."""
+        ms = (C.c_double * 8)()
+        check(self.lib.pinot_gpu_server_last_phases(self.ptr, ms, 8))
+        return dict(zip(self.PHASES, list(ms)))
+
     def close(self):
         if self.ptr:
             for e in self.engines:
@@ -642,9 +650,12 @@ class ServerQueryExecutor:
 
     def group_by_result(self, query, segments):
         """Raw device group-by result object (no trimming)."""
-        if isinstance(query, str):
-            query = compile_pql(query)
-        m = QueryMarshal(query, self.num_groups_limit, self.max_init, self.timeout_ms)
+        if isinstance(query, PreparedQuery):
+            query, m = query.query, query.marshal
+        else:
+            if isinstance(query, str):
+                query = compile_pql(query)
+            m = QueryMarshal(query, self.num_groups_limit, self.max_init, self.timeout_ms, self.pruners)
         out = C.c_void_p()
         stats = _lib.ExecStats()
         check(self.engine.lib.pinot_gpu_group_by(self.engine.ptr, _segment_handles(segments), len(segments),

@@ -1,0 +1,24 @@
+"""Summarise a bench.py JSON line (last line of the file)."""
+import json
+import sys
+
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+
+
+def line(tag, x):
+    r = x["roofline"]
+    print("%s: value %.4g ms/step %.4f p50 %.4f abi %.4f kernel %s %.4f ms frac %.3f traffic %s path %s %s" % (
+        tag, x["value"], x["ms_per_step"], x["p50_query_ms"], x.get("p50_c_abi_ms", 0), r["kernel"],
+        r["kernels"][r["kernel"]]["avg_ms"], r["frac"], r.get("traffic"), x["config"].get("path"),
+        x.get("step_ms_detail")))
+    if "merge_phases_ms" in x:
+        print("   phases", {k: round(v, 3) for k, v in x["merge_phases_ms"].items()})
+    if "verify" in x:
+        print("   verify", x["verify"].get("match"))
+    if "cpu_baseline" in x:
+        print("   cpu", x["cpu_baseline"]["value"], x["cpu_baseline"].get("threads"), x["cpu_baseline"].get("host"))
+
+
+line("config2" if "config4" in d or "k_scan_query" in d["roofline"]["kernels"] else "head", d)
+if "config4" in d:
+    line("config4", d["config4"])

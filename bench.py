@@ -299,19 +299,20 @@ def timed_steps(job, step, steps, warmup):
     gc.collect()
     gc.disable()  # the harness's own collector pauses stay out of the timed steps (the C-ABI call has none)
     t0 = time.perf_counter()
-    step_ms, abi_ms = [], []
+    step_ms, abi_ms, dev_ms = [], [], []
     res = st = None
     for _ in range(steps):
         ts = time.perf_counter()
         res, st = step()  # synchronous: results are on the host when it returns
         step_ms.append((time.perf_counter() - ts) * 1e3)
         abi_ms.append(st.host_ms)
+        dev_ms.append(st.device_ms)
     job.synchronize()
     torch.cuda.synchronize()
     job.barrier()
     elapsed = time.perf_counter() - t0
     gc.enable()
-    return job.max_over_ranks(elapsed), step_ms, abi_ms, res, st
+    return job.max_over_ranks(elapsed), (step_ms, dev_ms), abi_ms, res, st
 
 
 def kernel_pass(job, step, reps):
@@ -338,7 +339,7 @@ def measure(job, args, workload):
     c4 = workload == "config4"
     step = job.step_fn(CONFIG4 if c4 else QUERY, c4)
     steps = args.steps if not c4 or args.workload == "config4" else args.c4_steps
-    elapsed, step_ms, abi_ms, res, st = timed_steps(job, step, steps, args.warmup)
+    elapsed, (step_ms, dev_ms), abi_ms, res, st = timed_steps(job, step, steps, args.warmup)
     ms_per_step = elapsed * 1000.0 / steps
     value = job.total_rows * steps / elapsed
     reps = max(3, min(steps, 10))
@@ -380,7 +381,10 @@ def measure(job, args, workload):
         "p50_query_ms": float(np.median(step_ms)),
         "p50_c_abi_ms": float(np.median(abi_ms)),
         "step_ms_detail": {"min": float(np.min(step_ms)), "p90": float(np.percentile(step_ms, 90)),
-                           "max": float(np.max(step_ms)), "first": [round(x, 4) for x in step_ms[:4]]},
+                           "max": float(np.max(step_ms)), "first": [round(x, 4) for x in step_ms[:4]],
+                           # the device's own time per step (in-kernel wall clock / events), beside the host's
+                           "device_p50": float(np.median(dev_ms)), "device_min": float(np.min(dev_ms)),
+                           "device_max": float(np.max(dev_ms))},
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,

@@ -314,12 +314,16 @@ pinot_status pinot_gpu_aggregate(pinot_engine *engine, const pinot_segment_handl
     DeadlineScope ds(*engine, query->timeout_ms);
     const std::vector<SegmentData *> segs = resolve(*engine, segments, num_segments);
     const std::vector<SegmentData *> kept = prune_for_query(segs, *query);
+    const auto t1 = std::chrono::steady_clock::now();
     if (kept.empty()) {  // every segment pruned (ServerQueryExecutorV1Impl.java:187-196)
       agg_identities(*query, out);
       if (stats) memset(stats, 0, sizeof(*stats));
     } else {
       exec_aggregate(*engine, kept, *query, out, stats);
     }
+    if (engine->host_phases)
+      fprintf(stderr, "[pinot_gpu] aggregate C-ABI phases (us): resolve+prune %.1f, execute %.1f\n",
+              std::chrono::duration<double, std::micro>(t1 - t0).count(), elapsed_ms(t1) * 1e3);
     if (stats) {
       if (query->pruners) stats->num_total_raw_docs = total_docs(segs);
       stats->host_ms = elapsed_ms(t0);

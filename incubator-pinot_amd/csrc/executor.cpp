@@ -995,6 +995,9 @@ void run_fused(Engine &e, FusedPlan &fp, const pinot_query &q, pinot_agg_result 
       R.hll_set[a] = index_of_name(fp.hll_cols, agg_column(q.aggregations[a]));
   merge_aggregates(q, plans, fp.routes, counts, R, out);
   fill_stats(q, plans, counts, ms, stats);
+  if (e.host_phases)
+    fprintf(stderr, "[pinot_gpu] fused query host phases (us): after sync %.1f\n",
+            std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tp2).count());
 }
 
 }  // namespace
@@ -1943,7 +1946,7 @@ GroupPlan plan_group(const std::vector<SegmentData *> &segs, const pinot_query &
   for (int a = 0; a < na; a++) per_key += lds_acc_bytes_per_key(ga.acc_kind[a], false);  // u8 HLL registers
   int shift = 0;
   while (shift < 12 && ((size_t)2 << shift) * per_key <= (size_t)kReduceLdsBudget) shift++;
-  if (max_shift >= 0) shift = std::min(shift, max_shift);
+  if (max_shift >= 0) shift = std::min(max_shift, 16);  // group.pshift: an explicit partition size (experiments)
   const int64_t K = int64_t(1) << shift;
   const int64_t P = (ks.G + K - 1) / K;
   // two-level: EMIT scatters into ceil(P / 2^split) coarse runs (few enough live lines per block to combine
@@ -2583,7 +2586,8 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     void *tmp = pb + 3 * hist_b + pstart_b;
     // bucketed plan: COUNT keeps the filter words, GB_EMIT2 writes whole LDS buckets into the final layout; the
     // lane-owns-quarter sink pads every (partition, block) run to whole 64-B buckets (aligned flushes)
-    const bool bucket = e.group_bucket && a.pf_nc > 0 && gp.P <= kBucketMaxPartitions && gp.record_bits <= 63 &&
+    const bool bucket = e.group_bucket && a.pf_nc > 0 && gp.P <= kBucketMaxPartitions &&
+                        gp.record_bits <= kRecPartShift && gp.P <= (int64_t(1) << (63 - kRecPartShift)) &&
                         (e.debug_emit == 0 || e.debug_emit >= 3);
     const bool aligned = bucket && a.lw == 2 && e.group_aligned;
     const int64_t pad_records = aligned ? (int64_t)hist_n * (kBucketRecs - 1) : 0;
@@ -2637,7 +2641,7 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
         launch_partition_split(hist, offsets, pstart, (int32_t)gp.P, (int32_t)nblk, gp.shift, gp.split, a.emit,
                                e.group_records.get<unsigned long long>(), e.group_nt_store, e.stream);
       }
-      launch_partition_reduce(ra, e.stream);
+      if (e.debug_emit != 5) launch_partition_reduce(ra, e.stream);  // debug.emit=5: timing of the passes before it
     });
     PINOT_HIP(hipGetLastError());
   }

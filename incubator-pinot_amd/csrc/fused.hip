@@ -280,7 +280,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G ? 2 : 
     cnt += eval_chunk<G>(steps, sg.n_leaves, sg.n_folds, chunk_word(sg.pre, sg.nwords, sg.num_docs, ch, lane), A, hll,
                          ch * 64 + lane, sg.nwords, sg.num_docs, lane,
                          [&](int, const FusedStep &st) -> const uint8_t * {
-                           stage_chunk_rt(st.fwd, st.bits, ch, lds_wave, lane);
+                           stage_chunk_rt(st.fwd, st.bits, ch, lds_wave, lane, a.nt != 0);
                            wait_stage();
                            return lds_wave;
                          });

@@ -653,20 +653,22 @@ __device__ __forceinline__ void decode_column_lq(const uint8_t *fwd, int bits, i
 // order). A record that finds its bucket full goes straight to its run slot.
 constexpr unsigned long long kRecValid = 1ull << 63;
 
+__device__ __forceinline__ uint32_t rec_partition(unsigned long long r) {
+  return (uint32_t)(r >> kRecPartShift) & ((1u << (63 - kRecPartShift)) - 1u);
+}
+
 __device__ __forceinline__ void emit2_sink16(const GroupArgs &a, uint32_t *plds, uint32_t act,
-                                             const uint32_t (&key)[16], const unsigned long long (&rec)[16],
-                                             int lane) {
+                                             const unsigned long long (&rec)[16], int lane) {
   if (a.reserved2 == 4) return;  // debug.emit=4 (timing only, wrong results): reads + decode, no sink
   const bool st = a.reserved2 != 3;  // debug.emit=3: bucket logic without the global stores
   uint32_t *cur = plds, *cnt = plds + a.P;
   unsigned long long *bkt = reinterpret_cast<unsigned long long *>(plds + ((3 * a.P + 3) & ~3));
   unsigned long long *flist = bkt + (size_t)a.P * kBucketRecs + (threadIdx.x >> 6) * 64;
-  const uint32_t lmask = (1u << a.shift) - 1u;
   uint32_t pos[16];
 #pragma unroll
   for (int j = 0; j < 16; j++) {
     pos[j] = 0;
-    if ((act >> j) & 1u) pos[j] = atomicAdd(&cnt[key[j] >> a.shift], 1u);
+    if ((act >> j) & 1u) pos[j] = atomicAdd(&cnt[rec_partition(rec[j])], 1u);
   }
   // bucket stores (no LDS returns: no waits); records that found their bucket full are marked for the run slots
   uint32_t flush = 0, over = 0;
@@ -674,8 +676,8 @@ __device__ __forceinline__ void emit2_sink16(const GroupArgs &a, uint32_t *plds,
   for (int j = 0; j < 16; j++) {
     const bool in = ((act >> j) & 1u) && pos[j] < (uint32_t)kBucketRecs;
     if (in)
-      __hip_atomic_store(&bkt[(key[j] >> a.shift) * kBucketRecs + pos[j]], rec[j] | (key[j] & lmask) | kRecValid,
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      __hip_atomic_store(&bkt[rec_partition(rec[j]) * kBucketRecs + pos[j]], rec[j] | kRecValid, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_WORKGROUP);
     flush |= (in && pos[j] == (uint32_t)kBucketRecs - 1) ? (1u << j) : 0u;
     over |= (((act >> j) & 1u) && !in) ? (1u << j) : 0u;
   }
@@ -685,10 +687,10 @@ __device__ __forceinline__ void emit2_sink16(const GroupArgs &a, uint32_t *plds,
 #pragma unroll
     for (int j = 0; j < 16; j++)
       if ((over >> j) & 1u)
-        d[j] = a.aligned_runs ? atomicSub(&back[key[j] >> a.shift], 1u) - 1u : atomicAdd(&cur[key[j] >> a.shift], 1u);
+        d[j] = a.aligned_runs ? atomicSub(&back[rec_partition(rec[j])], 1u) - 1u : atomicAdd(&cur[rec_partition(rec[j])], 1u);
 #pragma unroll
     for (int j = 0; j < 16; j++)
-      if (((over >> j) & 1u) && st) a.emit[d[j]] = rec[j] | (key[j] & lmask);
+      if (((over >> j) & 1u) && st) a.emit[d[j]] = rec[j];
   }
   while (true) {
     const uint64_t fm = __ballot(flush != 0);
@@ -696,10 +698,10 @@ __device__ __forceinline__ void emit2_sink16(const GroupArgs &a, uint32_t *plds,
     uint32_t p = 0;
     if (flush) {
       const int j = __builtin_ctz(flush);
-      uint32_t pk = 0;
+      unsigned long long pr = 0;
 #pragma unroll
-      for (int t = 0; t < 16; t++) pk = t == j ? key[t] : pk;
-      p = pk >> a.shift;
+      for (int t = 0; t < 16; t++) pr = t == j ? rec[t] : pr;
+      p = rec_partition(pr);
       const uint32_t dst = atomicAdd(&cur[p], (uint32_t)kBucketRecs);
       const int f = __builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u));
       flist[f] = ((unsigned long long)dst << 32) | p;
@@ -750,9 +752,17 @@ struct IdOut {
   __device__ __forceinline__ void put(uint32_t v) { id[J] = v; }
 };
 
+// The raw dwords pass through an empty volatile asm first: otherwise the compiler hoists the byte swaps and constant
+// shifts of every width of the switch above it (all widths' values live at once).
 template <int B>
-__device__ __forceinline__ void decode_raw_lq_b(const uint32_t (&R)[12], int64_t qi, uint32_t (&id)[16]) {
+__device__ __forceinline__ void decode_raw_lq_b(const uint32_t (&Rin)[12], int64_t qi, uint32_t (&id)[16]) {
   constexpr int N = (B + 1) / 2 + (B & 1);
+  uint32_t R[N];
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    R[i] = Rin[i];
+    asm volatile("" : "+v"(R[i]));
+  }
   uint32_t D[(B + 1) / 2 + 1];
   if constexpr (B & 1) {
     const bool odd = qi & 1;
@@ -767,8 +777,15 @@ __device__ __forceinline__ void decode_raw_lq_b(const uint32_t (&R)[12], int64_t
   decode_quarter_apply<B, 0>(D, f);
 }
 
-__device__ __forceinline__ void decode_raw_lq(const uint32_t (&R)[12], int bits, int64_t qi, uint32_t (&id)[16]) {
-#define PINOT_RQ(B) decode_raw_lq_b<B>(R, qi, id)
+// Decode a lane's 16 values and hand them to f inside the width's switch arm (only f's effects leave the switch).
+template <typename F>
+__device__ __forceinline__ void decode_raw_lq(const uint32_t (&R)[12], int bits, int64_t qi, F &&f) {
+#define PINOT_RQ(B)                   \
+  {                                   \
+    uint32_t id[16];                  \
+    decode_raw_lq_b<B>(R, qi, id);    \
+    f(id);                            \
+  }
   switch (bits) {  // widths up to kGroupLwMaxBits (the host routes wider columns through group_chunk_pf)
     case 1: PINOT_RQ(1); break;   case 2: PINOT_RQ(2); break;   case 3: PINOT_RQ(3); break;   case 4: PINOT_RQ(4); break;
     case 5: PINOT_RQ(5); break;   case 6: PINOT_RQ(6); break;   case 7: PINOT_RQ(7); break;   case 8: PINOT_RQ(8); break;
@@ -828,36 +845,31 @@ __device__ __forceinline__ void lq_load(const LqCols &k, int64_t qi, uint32_t (&
     if (k.bits[c]) load_raw_lq(k.fwd[c], k.bits[c], qi, R[c]);
 }
 
-// Decode a quarter's loaded columns into keys / records, then the sink.
+// Decode a quarter's loaded columns into keys / records, then the sink. The group columns (slots [0, n_gcols)) come
+// first; for GB_EMIT2 the key then folds into the record right away (local key | partition << kRecPartShift) so the
+// key array is dead while the aggregated columns are decoded (register pressure).
 template <int MODE, int NC>
 __device__ __forceinline__ void lq_process(const GroupArgs &a, const GroupSegment &sg, const LqCols &k,
                                            const uint32_t (&R)[NC][12], int64_t qi, uint32_t mq, int lane,
                                            uint32_t *plds) {
   constexpr int U = kGroupPfUnroll;
   uint32_t key[16];
-  unsigned long long rec[16];
 #pragma unroll
-  for (int j = 0; j < 16; j++) {
-    key[j] = 0;
-    rec[j] = 0;
-  }
+  for (int j = 0; j < 16; j++) key[j] = 0;
 #pragma unroll
   for (int c = 0; c < NC; c++) {
-    if (!k.bits[c]) continue;
-    uint32_t id[16];
-    decode_raw_lq(R[c], k.bits[c], qi, id);
-    if (k.fsh[c] < 0) {
-      if (k.remap[c]) {
+    if (!k.bits[c] || k.fsh[c] >= 0) continue;
+    const int32_t *remap = k.remap[c];
+    const uint32_t stride = k.stride[c];
+    decode_raw_lq(R[c], k.bits[c], qi, [&](const uint32_t (&id)[16]) {
+      if (remap) {
 #pragma unroll
-        for (int j = 0; j < 16; j++) key[j] += (uint32_t)gload<int32_t>(k.remap[c] + id[j]) * k.stride[c];
+        for (int j = 0; j < 16; j++) key[j] += (uint32_t)gload<int32_t>(remap + id[j]) * stride;
       } else {
 #pragma unroll
-        for (int j = 0; j < 16; j++) key[j] += id[j] * k.stride[c];
+        for (int j = 0; j < 16; j++) key[j] += id[j] * stride;
       }
-    } else if constexpr (MODE != GB_COUNT) {
-#pragma unroll
-      for (int j = 0; j < 16; j++) rec[j] |= (unsigned long long)id[j] << k.fsh[c];
-    }
+    });
   }
   if constexpr (MODE == GB_EMIT2 || MODE == GB_COUNT) {
     uint32_t act = mq;
@@ -867,13 +879,39 @@ __device__ __forceinline__ void lq_process(const GroupArgs &a, const GroupSegmen
         if (!((gload<uint32_t>(sg.admitted + (key[j] >> 5)) >> (key[j] & 31)) & 1u)) act &= ~(1u << j);
     }
     if constexpr (MODE == GB_EMIT2) {
-      emit2_sink16(a, plds, act, key, rec, lane);
+      const uint32_t lmask = (1u << a.shift) - 1u;
+      unsigned long long rec[16];
+#pragma unroll
+      for (int j = 0; j < 16; j++)
+        rec[j] = (unsigned long long)(key[j] & lmask) | ((unsigned long long)(key[j] >> a.shift) << kRecPartShift);
+#pragma unroll
+      for (int c = 0; c < NC; c++) {
+        if (!k.bits[c] || k.fsh[c] < 0) continue;
+        const int fsh = k.fsh[c];
+        decode_raw_lq(R[c], k.bits[c], qi, [&](const uint32_t (&id)[16]) {
+#pragma unroll
+          for (int j = 0; j < 16; j++) rec[j] |= (unsigned long long)id[j] << fsh;
+        });
+      }
+      emit2_sink16(a, plds, act, rec, lane);
     } else {  // partition histogram: LDS adds without return
 #pragma unroll
       for (int j = 0; j < 16; j++)
         if ((act >> j) & 1u) atomicAdd(&plds[key[j] >> a.shift], 1u);
     }
     return;
+  }
+  unsigned long long rec[16];
+#pragma unroll
+  for (int j = 0; j < 16; j++) rec[j] = 0;
+#pragma unroll
+  for (int c = 0; c < NC; c++) {
+    if (!k.bits[c] || k.fsh[c] < 0) continue;
+    const int fsh = k.fsh[c];
+    decode_raw_lq(R[c], k.bits[c], qi, [&](const uint32_t (&id)[16]) {
+#pragma unroll
+      for (int j = 0; j < 16; j++) rec[j] |= (unsigned long long)id[j] << fsh;
+    });
   }
 #pragma unroll
   for (int j0 = 0; j0 < 16; j0 += U) {

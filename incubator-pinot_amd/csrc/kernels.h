@@ -204,6 +204,7 @@ int scan_query_blocks_per_cu(int stage_bytes, bool gathers, bool pipelined);
 enum GroupMode : int32_t { GB_GLOBAL = 0, GB_LDS = 1, GB_COUNT = 2, GB_EMIT = 3, GB_VERIFY = 4, GB_FIRST = 5, GB_EMIT2 = 6 };
 constexpr int kBucketRecs = 8;                                   // 64-B bucket flushes
 constexpr unsigned long long kRecInvalid = ~0ull;                // padding slot of an aligned run (bit 63 set)
+constexpr int kRecPartShift = 52;  // GB_EMIT2 records carry their partition in bits [52, 63) (bucketed plan: <= 52 record bits)
 constexpr int kBucketMaxPartitions = 2040;  // P x (3 x 4 + 8 x 8) B + 4 KiB of flush lists per block <= 160 KiB
 // accumulator kinds (acc_kind): 0 int64 sum, 1 double sum, 2 ordered-u64 min, 3 ordered-u64 max,
 // 4 HLL registers (u8 [G][256]), 5 none (COUNT / AVG count share `counts`)

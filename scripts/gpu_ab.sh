@@ -1,13 +1,18 @@
 #!/bin/bash
-# GPU-box A/B of engine configurations on the config-2 bench (no CPU baseline), one JSON line each.
-# Usage: bash scripts/gpu_ab.sh <tag> "<cfg1>" "<cfg2>" ...   (cfg "" = defaults)
+# A/B of engine configurations on the config-2 (or --workload) bench line; optional pytest args first via PYTEST="...".
+# Usage: scripts/gpu_ab.sh <tag> <cfg> [<cfg> ...]   ("" = default engine configuration)
 set -o pipefail
-TAG=$1; shift
-OUT=gpurun_out/$TAG
-mkdir -p "$OUT"
+out=gpurun_out/$1; shift
+mkdir -p $out
+if [ -n "$PYTEST" ]; then
+  timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu $PYTEST > $out/pytest.log 2>&1 \
+    || { tail -30 $out/pytest.log; exit 1; }
+  tail -2 $out/pytest.log
+fi
 i=0
 for cfg in "$@"; do
-  timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 30 --warmup 5 --engine-config "$cfg" > "$OUT/ab_$i.json" 2> "$OUT/ab_$i.err" || { echo "bench failed: $cfg"; tail -20 "$OUT/ab_$i.err"; exit 1; }
-  python3 -c "import json,sys; d=json.load(open('$OUT/ab_$i.json')); print(repr(sys.argv[1]), 'ms/query %.4f' % d['ms_per_step'], 'kernel', {k: round(v['avg_ms'],4) for k,v in d['roofline']['kernels'].items()}, 'frac %.3f' % d['roofline']['frac'])" "$cfg"
+  timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-config4 --no-cpu-baseline --no-verify ${BENCH_ARGS} \
+    --engine-config "$cfg" > $out/bench_$i.json 2> $out/bench_$i.err || { tail -20 $out/bench_$i.err; exit 1; }
+  echo "== ${cfg:-default}"; python scripts/show_bench.py $out/bench_$i.json
   i=$((i+1))
 done

@@ -18,7 +18,7 @@ from pinot_amd import GpuEngine, ServerQueryExecutor, build_segment, compile_pql
 
 pytestmark = pytest.mark.gpu
 
-WIDTH_MODES = ("", "exec.pipe=1", "exec.fused=0")
+WIDTH_MODES = ("", "exec.nt=0", "exec.pipe=1", "exec.fused=0")
 
 
 @pytest.fixture(scope="module")
@@ -106,6 +106,9 @@ def test_fused_width_sweep(engines, b):
         "SELECT COUNT(*), MAX(w), SUM(x) FROM t WHERE w NOT IN (%d, %d) AND x > %d" % (
             int(vals_w[1]), int(vals_w[card - 1]), int(xd[card // 7])),
         "SELECT COUNT(*), SUM(x), DISTINCTCOUNTHLL(w) FROM t WHERE f <> 4",
+        # RANGE + LUT leaves with Σ dictId and min/max folds only; an OR of two leaves
+        "SELECT COUNT(*), SUM(w), MIN(w), MAX(w) FROM t WHERE w BETWEEN %d AND %d AND f IN (1, 3, 5, 7)" % (lo, hi),
+        "SELECT COUNT(*), MAX(w) FROM t WHERE f IN (2, 9) OR w < %d" % lo,
     ]
     gq = compile_pql("SELECT COUNT(*), SUM(x), MAX(x) FROM t WHERE f < 9 GROUP BY w")
     gexp = O.execute_group_by_arrays([seg], gq, num_groups_limit=1 << 22)

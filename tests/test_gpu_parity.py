@@ -17,7 +17,8 @@ REL = 1e-9
 # engine configurations: default (fused single-launch path, pipelined whole-chunk staging where a chunk
 # fits), forced scan / forced index leaves, the stepwise fused kernel, the non-temporal DMA policy, and
 # the unfused per-segment launch sequence
-ENGINE_MODES = ("", "filter.force=scan", "filter.force=index", "exec.pipe=1", "exec.nt=1;exec.pipe=1", "exec.fused=0")
+ENGINE_MODES = ("", "filter.force=scan", "filter.force=index", "exec.nt=0", "exec.pipe=1", "exec.nt=0;exec.pipe=1",
+                "exec.fused=0")
 
 
 @pytest.fixture(scope="module", params=ENGINE_MODES)

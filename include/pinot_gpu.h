@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define PINOT_GPU_ABI_VERSION 7
+#define PINOT_GPU_ABI_VERSION 8
 
 /* ------------------------------------------------------------------ status */
 typedef enum {
@@ -95,6 +95,22 @@ typedef struct {
      the segment pruner; parsed with the column's data type. */
   const char *min_value;
   const char *max_value;
+  /* Bloom filter (ABI >= 8): the column's .bloom bytes as BloomFilterReader reads them (BE int type = 1, BE int
+     version = 1, then Guava's BloomFilter.writeTo: byte strategy, byte numHashFunctions, BE int words, BE longs;
+     BloomFilterReader.java:36-50), or create_bloom_filter = 1 to build it at registration from the dictionary as
+     BloomFilterHandler does at load (BloomFilterHandler.java:107-116; dictionary columns only). Read only by the
+     COLUMN_VALUE pruner's EQUALITY test (ColumnValueSegmentPruner.java:140-144). */
+  const uint8_t *bloom_filter; uint64_t bloom_filter_len;
+  int32_t create_bloom_filter;
+  /* Partition metadata (ABI >= 8; column.<c>.partitionFunction / numPartitions / partitionValues,
+     ColumnMetadata.java:184-194): function name (Modulo / Murmur / ByteArray / HashCode, any case; NULL = none), the
+     partition count and the partitions this segment holds (ranges already expanded,
+     ColumnPartitionMetadata.extractPartitions), or num_partition_values = -1 to take the partitions of every dictionary
+     value, as the segment creator records them. Read only by the PARTITION pruner. */
+  int32_t num_partitions;
+  const char *partition_function;
+  const int32_t *partition_values; int32_t num_partition_values;
+  int32_t reserved8;
 } pinot_column_desc;
 
 typedef struct {
@@ -266,16 +282,19 @@ void pinot_groupby_free(pinot_groupby_result *r);
  *                 (DataSchemaSegmentPruner.java:38-41)
  *   COLUMN_VALUE  EQUALITY / RANGE leaves outside the column's [minValue, maxValue] metadata (a column without
  *                 them never prunes; a loaded segment's time column gets its dictionary's ends, as the default
- *                 ColumnMinMaxValueGenerator mode TIME does at load); AND prunes when any
- *                 child does, OR when all do (ColumnValueSegmentPruner.java:49-200). Bloom filters and partition
- *                 metadata are not in the descriptor: those two tests are not made.
+ *                 ColumnMinMaxValueGenerator mode TIME does at load), and an EQUALITY value the column's bloom
+ *                 filter rules out (:140-144); AND prunes when any child does, OR when all do
+ *                 (ColumnValueSegmentPruner.java:49-200, AbstractSegmentPruner.java:56-90)
  *   VALID         an empty segment (ValidSegmentPruner.java:47-58)
+ *   PARTITION     an EQUALITY value whose partition (the column's partition function) the segment does not hold
+ *                 (PartitionSegmentPruner.java:73-111); the default list has it last
+ *                 (DefaultHelixStarterServerConfig.java:60-65)
  * A bad literal in an EQUALITY / RANGE leaf is PINOT_ERR_BAD_QUERY (AbstractSegmentPruner.getValue); a query column
  * the engine left out of a loaded segment (multi-value / raw / BYTES) is PINOT_ERR_UNSUPPORTED; a query whose budget
  * is already spent (timeout_ms < 0) is PINOT_ERR_TIMEOUT, checked before pruning as processQuery does (:116-126). */
 typedef enum {
-  PINOT_PRUNER_DATA_SCHEMA = 1, PINOT_PRUNER_COLUMN_VALUE = 2, PINOT_PRUNER_VALID = 4,
-  PINOT_PRUNER_DEFAULT = 7
+  PINOT_PRUNER_DATA_SCHEMA = 1, PINOT_PRUNER_COLUMN_VALUE = 2, PINOT_PRUNER_VALID = 4, PINOT_PRUNER_PARTITION = 8,
+  PINOT_PRUNER_DEFAULT = 15
 } pinot_pruner;
 
 /* pruned[i] = 1 when segment i is dropped, else 0; *total_raw_docs = the docs of ALL the segments, pruned or not

@@ -9,6 +9,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "bloom.h"
 #include "common.h"
 #include "kernels.h"
 
@@ -28,6 +29,10 @@ struct ColumnData {
   bool raw = false;                   // registered from a raw (no-dictionary) forward index, transcoded
   bool has_minmax = false;            // metadata minValue / maxValue present (the segment pruner's only input)
   std::string min_value, max_value;
+  BloomFilter bloom;                  // empty: none (ColumnValueSegmentPruner's EQUALITY test)
+  int partition_fn = PF_NONE;         // PartitionFunctionKind of the partition metadata (PartitionSegmentPruner)
+  int32_t num_partitions = 0;
+  std::vector<int32_t> partitions;    // the partitions the segment holds, sorted
 
   // host copies (dictionary-sized; used for predicate evaluation and key materialisation)
   std::vector<uint8_t> dict_be;        // raw BE dictionary bytes
@@ -73,6 +78,9 @@ struct TranscodedColumn {
 };
 bool transcode_raw(const pinot_column_desc &d, int32_t num_docs, TranscodedColumn &out);
 void validate_segment(const pinot_segment_desc &d);
+// The pruning metadata of a column descriptor (bloom filter bytes or creation from the decoded dictionary, partition
+// metadata) into c; c's dictionary must be decoded already (parse_column calls it).
+void parse_pruning_metadata(ColumnData &c, const pinot_column_desc &d);
 std::string java_double_to_string(double v);  // Double.toString
 std::string java_float_to_string(float v);    // Float.toString
 
@@ -94,6 +102,7 @@ struct SegmentDirData {
   std::vector<std::unique_ptr<MappedFile>> files;
   std::vector<std::vector<uint8_t>> owned;  // raw columns: the decompressed chunk values
   std::deque<std::string> strings;          // min / max values the descriptors point at (stable addresses)
+  std::deque<std::vector<int32_t>> ints;    // partition values the descriptors point at
   std::string time_column;                  // segment.time.column.name
   pinot_segment_desc desc() const;
 };

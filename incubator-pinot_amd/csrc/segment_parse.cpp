@@ -293,6 +293,7 @@ void parse_column(ColumnData &c, const pinot_column_desc &d, int32_t num_docs, P
     c.min_value = d.min_value;
     c.max_value = d.max_value;
   }
+  parse_pruning_metadata(c, d);
 
   const int64_t n = num_docs;
   c.fwd_bytes = (uint64_t)((n * c.bits + 7) / 8);
@@ -336,6 +337,49 @@ void parse_column(ColumnData &c, const pinot_column_desc &d, int32_t num_docs, P
       parse_roaring(d.inverted_index + o0, o1 - o0, o0, out.containers, c.name);
     }
     c.inv_dir[c.card] = (int32_t)out.containers.size();
+  }
+}
+
+// ---------------------------------------------------------------- pruning metadata
+// Bloom filter: the .bloom bytes (BloomFilterReader), or built from the dictionary values' toString as
+// BloomFilterHandler does at load (BloomFilterHandler.java:107-116: creator.add(dictionaryReader.get(i)) for every
+// dictId; Dictionary.getStringValue is that toString for every type). Partition metadata as ColumnMetadata reads it
+// (ColumnMetadata.java:184-194).
+void parse_pruning_metadata(ColumnData &c, const pinot_column_desc &d) {
+  require(!(d.bloom_filter && d.create_bloom_filter), PINOT_ERR_BAD_ARG,
+          c.name + ": bloom filter bytes and create_bloom_filter together");
+  if (d.bloom_filter) {
+    c.bloom = parse_bloom_filter(d.bloom_filter, d.bloom_filter_len, c.name);
+  } else if (d.create_bloom_filter) {
+    c.bloom = create_bloom_filter(c.card);
+    for (int32_t i = 0; i < c.card; i++) c.bloom.put(c.string_value(i));
+  }
+  if (d.partition_function) {
+    c.partition_fn = partition_function_of(d.partition_function);
+    require(d.num_partitions > 0, PINOT_ERR_BAD_ARG, c.name + ": Number of partitions must be > 0");
+    c.num_partitions = d.num_partitions;
+    if (d.num_partition_values == -1) {  // the partitions of every dictionary value, as the creator records them
+      for (int32_t i = 0; i < c.card; i++) {
+        TypedValue v;
+        v.data_type = c.data_type;
+        if (c.data_type == PINOT_INT || c.data_type == PINOT_LONG) v.i = c.dict_int[(size_t)i];
+        else if (c.data_type != PINOT_STRING) v.d = c.dict_dbl[(size_t)i];
+        v.s = c.string_value(i);
+        try {
+          c.partitions.push_back(partition_of((PartitionFunctionKind)c.partition_fn, c.num_partitions, v));
+        } catch (const Error &e) {
+          throw Error(PINOT_ERR_BAD_ARG, c.name + ": " + e.what());
+        }
+      }
+    } else {
+      require(d.num_partition_values >= 0 && (d.num_partition_values == 0 || d.partition_values), PINOT_ERR_BAD_ARG,
+              c.name + ": partition values");
+      c.partitions.assign(d.partition_values, d.partition_values + d.num_partition_values);
+    }
+    std::sort(c.partitions.begin(), c.partitions.end());
+    c.partitions.erase(std::unique(c.partitions.begin(), c.partitions.end()), c.partitions.end());
+  } else {
+    require(d.num_partition_values == 0, PINOT_ERR_BAD_ARG, c.name + ": partition values without a partition function");
   }
 }
 
@@ -416,6 +460,13 @@ bool transcode_raw(const pinot_column_desc &d, int32_t num_docs, TranscodedColum
   out.desc.forward_index_len = out.forward_index.size();
   out.desc.min_value = d.min_value;
   out.desc.max_value = d.max_value;
+  // "Bloom filters not supported for no dictionary columns" (BloomFilterHandler.java:117-118)
+  require(!d.bloom_filter && !d.create_bloom_filter, PINOT_ERR_UNSUPPORTED,
+          name + ": bloom filters are not supported for no-dictionary columns");
+  out.desc.num_partitions = d.num_partitions;
+  out.desc.partition_function = d.partition_function;
+  out.desc.partition_values = d.partition_values;
+  out.desc.num_partition_values = d.num_partition_values;
   return true;
 }
 

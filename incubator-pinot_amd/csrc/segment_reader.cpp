@@ -415,6 +415,30 @@ void read_segment_dir(const std::string &index_dir, SegmentDirData &out) {
       out.strings.push_back(unescape_properties(prop(kv, k + "maxValue")));
       d.max_value = out.strings.back().c_str();
     }
+    if (kv.count(k + "partitionFunction")) {  // ColumnMetadata.java:184-194
+      out.strings.push_back(prop(kv, k + "partitionFunction"));
+      d.partition_function = out.strings.back().c_str();
+      const int64_t np = prop_int(kv, k + "numPartitions");
+      require(np > 0 && np < INT32_MAX, PINOT_ERR_BAD_ARG, c + ": numPartitions out of range");
+      d.num_partitions = (int32_t)np;
+      std::vector<int32_t> parts;  // ColumnPartitionMetadata.extractPartitions: "n" or "[start end]" ranges
+      for (const std::string &pv : prop_list(kv, k + "partitionValues")) {
+        require(!pv.empty(), PINOT_ERR_BAD_ARG, c + ": empty partition value");
+        if (pv[0] == '[') {
+          const size_t sp = pv.find(' ');
+          require(sp != std::string::npos && pv.back() == ']', PINOT_ERR_BAD_ARG, c + ": partition range " + pv);
+          const int64_t a = java_parse_integer(pv.substr(1, sp - 1), INT32_MIN, INT32_MAX);
+          const int64_t b = java_parse_integer(pv.substr(sp + 1, pv.size() - sp - 2), INT32_MIN, INT32_MAX);
+          require(b - a < (int64_t)1 << 20, PINOT_ERR_BAD_ARG, c + ": partition range too wide " + pv);
+          for (int64_t x = a; x <= b; x++) parts.push_back((int32_t)x);
+        } else {
+          parts.push_back((int32_t)java_parse_integer(pv, INT32_MIN, INT32_MAX));
+        }
+      }
+      out.ints.push_back(std::move(parts));
+      d.partition_values = out.ints.back().data();
+      d.num_partition_values = (int32_t)out.ints.back().size();
+    }
     if (!dict) {  // a raw (no-dictionary) fixed-width column: decompressed here, transcoded at registration
       const uint8_t *fp = nullptr;
       uint64_t fn = 0;
@@ -439,6 +463,8 @@ void read_segment_dir(const std::string &index_dir, SegmentDirData &out) {
     d.is_sorted = prop_bool(kv, k + "isSorted", false) ? 1 : 0;
     require(index_bytes(c, "dictionary", c + ".dict", &d.dictionary, &d.dictionary_len), PINOT_ERR_BAD_ARG,
             c + ": no dictionary");
+    // a bloom filter the loader built (BloomFilterHandler; v1 <col>.bloom, v3 index type bloom_filter)
+    index_bytes(c, "bloom_filter", c + ".bloom", &d.bloom_filter, &d.bloom_filter_len);
     const uint8_t *fp = nullptr;
     uint64_t fn = 0;
     require(index_bytes(c, "forward_index", c + (d.is_sorted ? ".sv.sorted.fwd" : ".sv.unsorted.fwd"), &fp, &fn),

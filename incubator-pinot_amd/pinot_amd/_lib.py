@@ -16,9 +16,10 @@ PINOT_ERR_TIMEOUT = 6
 DATA_TYPE = {"INT": 0, "LONG": 1, "FLOAT": 2, "DOUBLE": 3, "STRING": 4}
 FILTER_OP = {"AND": 0, "OR": 1, "EQUALITY": 2, "NOT": 3, "RANGE": 4, "IN": 5, "NOT_IN": 6}
 AGG_FN = {"COUNT": 0, "SUM": 1, "MIN": 2, "MAX": 3, "AVG": 4, "DISTINCTCOUNTHLL": 5}
-# pinot_pruner bits; the server's default list (DefaultHelixStarterServerConfig.java:60-64)
-PRUNER = {"DataSchemaSegmentPruner": 1, "ColumnValueSegmentPruner": 2, "ValidSegmentPruner": 4}
-PRUNER_DEFAULT = 7
+# pinot_pruner bits; the server's default list (DefaultHelixStarterServerConfig.java:60-65)
+PRUNER = {"DataSchemaSegmentPruner": 1, "ColumnValueSegmentPruner": 2, "ValidSegmentPruner": 4,
+          "PartitionSegmentPruner": 8}
+PRUNER_DEFAULT = 15
 
 # every symbol include/pinot_gpu.h declares (checked by tests/test_abi.py)
 EXPORTED_SYMBOLS = [
@@ -54,7 +55,10 @@ class ColumnDesc(C.Structure):
                 ("forward_index", C.c_void_p), ("forward_index_len", C.c_uint64),
                 ("sorted_index", C.c_void_p), ("sorted_index_len", C.c_uint64),
                 ("inverted_index", C.c_void_p), ("inverted_index_len", C.c_uint64),
-                ("min_value", C.c_char_p), ("max_value", C.c_char_p)]
+                ("min_value", C.c_char_p), ("max_value", C.c_char_p),
+                ("bloom_filter", C.c_void_p), ("bloom_filter_len", C.c_uint64), ("create_bloom_filter", C.c_int32),
+                ("num_partitions", C.c_int32), ("partition_function", C.c_char_p),
+                ("partition_values", C.c_void_p), ("num_partition_values", C.c_int32), ("reserved8", C.c_int32)]
 
 
 class SegmentDesc(C.Structure):

@@ -97,6 +97,22 @@ def segment_desc(seg: Segment):
             mn, mx = col.min_value.encode(), col.max_value.encode()
             keep += [mn, mx]
             d.min_value, d.max_value = mn, mx
+        bloom = getattr(col, "bloom_filter", None)
+        if bloom is not None:
+            bbuf = C.create_string_buffer(bytes(bloom), max(len(bloom), 1))
+            keep.append(bbuf)
+            d.bloom_filter, d.bloom_filter_len = C.cast(bbuf, C.c_void_p), len(bloom)
+        d.create_bloom_filter = int(bool(getattr(col, "create_bloom_filter", False)))
+        if getattr(col, "partition_function", None):
+            fn = col.partition_function.encode()
+            keep.append(fn)
+            d.partition_function, d.num_partitions = fn, int(col.num_partitions)
+            if col.partitions is None:
+                d.num_partition_values = -1
+            else:
+                pv = (C.c_int32 * max(len(col.partitions), 1))(*col.partitions)
+                keep.append(pv)
+                d.partition_values, d.num_partition_values = C.cast(pv, C.c_void_p), len(col.partitions)
         for field, data in (("dictionary", col.dictionary), ("forward_index", col.fwd),
                             ("sorted_index", col.sorted_index), ("inverted_index", col.inverted)):
             if data is None:

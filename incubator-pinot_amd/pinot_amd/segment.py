@@ -150,6 +150,11 @@ class Column:
     encoding: str = "dictionary"          # "raw": no-dictionary column, fwd = BE values (cardinality / bits 0)
     min_value: Optional[str] = None       # column.<c>.minValue / maxValue metadata (None: absent, never pruned on)
     max_value: Optional[str] = None
+    bloom_filter: Optional[bytes] = None  # the column's .bloom bytes (BloomFilterReader format), or
+    create_bloom_filter: bool = False     # built at registration from the dictionary (BloomFilterHandler)
+    partition_function: Optional[str] = None  # column.<c>.partitionFunction (Modulo / Murmur / ByteArray / HashCode)
+    num_partitions: int = 0
+    partitions: Optional[list] = None     # partitionValues; None with a function: every dictionary value's partition
     _raw_values: Optional[np.ndarray] = field(default=None, repr=False)
     _dict_values: Optional[np.ndarray] = field(default=None, repr=False)
     _dict_ids: Optional[np.ndarray] = field(default=None, repr=False)
@@ -261,10 +266,12 @@ def _metadata_string(v, data_type):
 
 
 def build_segment(name, columns: Dict[str, tuple], inverted_columns=(), num_docs=None, bits=None,
-                  allow_sorted=True, raw_columns=(), min_max=()) -> Segment:
+                  allow_sorted=True, raw_columns=(), min_max=(), bloom_columns=(), partitions=None) -> Segment:
     """columns: {name: (data_type, values)} in schema order; bits: optional {name: bitsPerElement};
     raw_columns: names written without a dictionary; min_max: names given minValue / maxValue metadata (the sorted
-    values' ends, as ColumnMinMaxValueGenerator writes them), min_max=True: every column."""
+    values' ends, as ColumnMinMaxValueGenerator writes them), min_max=True: every column; bloom_columns: names given a
+    bloom filter (built at registration from the dictionary, as the loader's BloomFilterHandler does); partitions:
+    {name: (function, numPartitions)} partition metadata (the partitions of the column's values)."""
     cols = {}
     n = None
     for cname, (dt, vals) in columns.items():
@@ -278,5 +285,8 @@ def build_segment(name, columns: Dict[str, tuple], inverted_columns=(), num_docs
             vals = col.dict_values()
             col.min_value = _metadata_string(vals[0], dt)
             col.max_value = _metadata_string(vals[len(vals) - 1], dt)
+        col.create_bloom_filter = cname in bloom_columns
+        if partitions and cname in partitions:
+            col.partition_function, col.num_partitions = partitions[cname]
         cols[cname] = col
     return Segment(name=name, num_docs=n if num_docs is None else num_docs, columns=cols)

@@ -11,21 +11,26 @@ pinot_segment_prune / pinot_gpu_prune_segments. PC = pinot-core/src/main/java/or
                          + AbstractSegmentPruner.pruneNonLeaf / getValue (AbstractSegmentPruner.java:56-105)
   valid_prune            ValidSegmentPruner.prune (PC/query/pruner/ValidSegmentPruner.java:47-58)
 
+  partition_prune        PartitionSegmentPruner.pruneSegment (PC/query/pruner/PartitionSegmentPruner.java:73-111)
+
 Pinned by the reference's own known-answer test, ColumnValueSegmentPrunerTest.test
 (pinot-core/src/test/java/org/apache/pinot/query/pruner/ColumnValueSegmentPrunerTest.java:53-92), replayed in
-tests/test_pruner.py. Bloom filters and PartitionSegmentPruner are not restated (no such metadata in a segment
-descriptor).
+tests/test_pruner.py. The bloom-filter test of ColumnValueSegmentPruner (:140-144) and the partition functions use
+oracle/bloom.py.
 
-A segment is described as {"num_docs": n, "columns": {name: (data_type, min, max)}} with min / max None when the
-metadata has none; `ranges(seg)` derives it from a pinot_amd Segment (the dictionary's ends).
+A segment is described as {"num_docs": n, "columns": {name: (data_type, min, max)}, "bloom": {name: BloomFilter},
+"partitions": {name: (function, numPartitions, set of partitions)}} with min / max None when the metadata has none;
+`ranges(seg)` derives it from a pinot_amd Segment (the dictionary's ends, its bloom / partition options).
 """
 import math
 import re
 
 import numpy as np
 
-DATA_SCHEMA, COLUMN_VALUE, VALID = 1, 2, 4
-DEFAULT = DATA_SCHEMA | COLUMN_VALUE | VALID
+import bloom as B
+
+DATA_SCHEMA, COLUMN_VALUE, VALID, PARTITION = 1, 2, 4, 8
+DEFAULT = DATA_SCHEMA | COLUMN_VALUE | VALID | PARTITION  # DefaultHelixStarterServerConfig.java:60-65
 
 
 class BadQuery(ValueError):
@@ -94,15 +99,37 @@ def parse_range(s):
     return lower, upper, inc_lower, inc_upper
 
 
-def column_value_prune(tree, columns):
+def java_to_string(data_type, v):
+    """Integer / Long / Float / Double.toString of the typed value, or the string (what mightContain hashes)."""
+    import pinot_oracle as O
+    if data_type in ("INT", "LONG"):
+        return str(v)
+    if data_type == "FLOAT":
+        return O.java_float_to_string(v)
+    if data_type == "DOUBLE":
+        return O.java_double_to_string(v)
+    return v
+
+
+def prune_nonleaf(tree, leaf):
+    """AbstractSegmentPruner.pruneNonLeaf (:56-90): AND prunes when any child does, OR when every child does."""
     op = tree["operator"]
     if op in ("AND", "OR"):
         kids = tree["children"]
         if not kids:
             return False
         if op == "AND":
-            return any(column_value_prune(c, columns) for c in kids)
-        return all(column_value_prune(c, columns) for c in kids)
+            return any(prune_nonleaf(c, leaf) for c in kids)
+        return all(prune_nonleaf(c, leaf) for c in kids)
+    return leaf(tree)
+
+
+def column_value_prune(tree, columns, blooms=None):
+    return prune_nonleaf(tree, lambda t: _column_value_leaf(t, columns, blooms or {}))
+
+
+def _column_value_leaf(tree, columns, blooms):
+    op = tree["operator"]
     if op not in ("EQUALITY", "RANGE"):
         return False
     if tree["column"] not in columns:
@@ -110,9 +137,10 @@ def column_value_prune(tree, columns):
     dt, mn, mx = columns[tree["column"]]
     if op == "EQUALITY":
         v = convert(dt, tree["values"][0])
-        if mn is None or mx is None:
-            return False
-        return java_compare(dt, v, mn) < 0 or java_compare(dt, v, mx) > 0
+        prune = mn is not None and mx is not None and (java_compare(dt, v, mn) < 0 or java_compare(dt, v, mx) > 0)
+        if not prune and tree["column"] in blooms:  # the bloom filter test (ColumnValueSegmentPruner.java:140-144)
+            prune = not blooms[tree["column"]].might_contain(java_to_string(dt, v))
+        return prune
     lower, upper, inc_lower, inc_upper = parse_range(tree["values"][0])
     lo = None if lower == "*" else convert(dt, lower)
     hi = None if upper == "*" else convert(dt, upper)
@@ -162,23 +190,59 @@ def valid_prune(num_docs):
     return num_docs == 0
 
 
+def partition_prune(tree, columns, partitions):
+    """PartitionSegmentPruner.pruneSegment (:85-110): EQUALITY leaves on columns with partition metadata."""
+    def leaf(t):
+        if t["operator"] != "EQUALITY":
+            return False
+        if t["column"] not in columns:
+            return True
+        if t["column"] not in partitions:
+            return False
+        dt = columns[t["column"]][0]
+        fn, n, parts = partitions[t["column"]]
+        v = convert(dt, t["values"][0])
+        return B.partition_of(fn, n, dt, v, java_to_string(dt, v)) not in parts
+    return prune_nonleaf(tree, leaf)
+
+
 def prune(segment, query, pruners=DEFAULT):
     cols = segment["columns"]
     if pruners & DATA_SCHEMA and data_schema_prune(query, cols):
         return True
-    if pruners & COLUMN_VALUE and query.get("filter") is not None and column_value_prune(query["filter"], cols):
+    if pruners & COLUMN_VALUE and query.get("filter") is not None and \
+            column_value_prune(query["filter"], cols, segment.get("bloom")):
         return True
-    return bool(pruners & VALID) and valid_prune(segment["num_docs"])
+    if pruners & VALID and valid_prune(segment["num_docs"]):
+        return True
+    return bool(pruners & PARTITION) and query.get("filter") is not None and \
+        partition_prune(query["filter"], cols, segment.get("partitions", {}))
 
 
 def ranges(seg):
     """{"num_docs", "columns": {name: (type, min, max)}} of a pinot_amd Segment: min / max = its column metadata's
     minValue / maxValue (ColumnMetadata.java:155-156), None when absent (the creator writes none; the loader's
     ColumnMinMaxValueGenerator adds them for the time column in its default mode)."""
-    cols = {}
+    cols, blooms, parts = {}, {}, {}
     for name, c in seg.columns.items():
         if getattr(c, "min_value", None) is None:
             cols[name] = (c.data_type, None, None)
-            continue
-        cols[name] = (c.data_type, convert(c.data_type, c.min_value), convert(c.data_type, c.max_value))
-    return {"num_docs": seg.num_docs, "columns": cols}
+        else:
+            cols[name] = (c.data_type, convert(c.data_type, c.min_value), convert(c.data_type, c.max_value))
+        vals = c.dict_values()
+        strings = [java_to_string(c.data_type, v.item() if hasattr(v, "item") else v) for v in vals]
+        if getattr(c, "bloom_filter", None) is not None:
+            blooms[name] = B.BloomFilter.from_bytes(c.bloom_filter)
+        elif getattr(c, "create_bloom_filter", False):  # BloomFilterHandler: every dictionary value's toString
+            bf = B.BloomFilter.for_cardinality(c.cardinality)
+            for s in strings:
+                bf.put(s)
+            blooms[name] = bf
+        if getattr(c, "partition_function", None):
+            if c.partitions is not None:
+                ps = set(c.partitions)
+            else:
+                ps = {B.partition_of(c.partition_function, c.num_partitions, c.data_type,
+                                     v.item() if hasattr(v, "item") else v, s) for v, s in zip(vals, strings)}
+            parts[name] = (c.partition_function, c.num_partitions, ps)
+    return {"num_docs": seg.num_docs, "columns": cols, "bloom": blooms, "partitions": parts}

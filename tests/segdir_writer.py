@@ -6,6 +6,9 @@ v3: the same buffers in v3/columns.psf, each behind the 8-byte magic marker, loc
 ("<col>.<index>.startOffset = o" / ".size = n", n counting the marker: SingleFileIndexDirectory.java:166-205,320-330).
 Raw (no-dictionary) columns: <col>.sv.raw.fwd as FixedByteChunkSingleValueWriter writes it
 (BaseChunkSingleValueWriter.java:62-200: header ints, absolute chunk offsets, PASS_THROUGH or Snappy chunks).
+Bloom filters: <col>.bloom (v3: index type bloom_filter) as BloomFilterHandler leaves them after a load
+(BloomFilterCreator.java:57-64; bytes from oracle/bloom.py); partition metadata: column.<c>.partitionFunction /
+numPartitions / partitionValues (V1Constants.java:135-137), the values written as "[start end]" ranges.
 """
 import os
 import struct
@@ -36,7 +39,41 @@ def _props(seg, version, padding):
                   k + "totalNumberOfEntries = %d" % seg.num_docs]
         if getattr(c, "min_value", None) is not None:
             lines += [k + "minValue = %s" % c.min_value, k + "maxValue = %s" % c.max_value]
+        if getattr(c, "partition_function", None):
+            parts = sorted(_partitions(c))
+            ranges, i = [], 0
+            while i < len(parts):  # consecutive partitions as one "[start end]" range
+                j = i
+                while j + 1 < len(parts) and parts[j + 1] == parts[j] + 1:
+                    j += 1
+                ranges.append("[%d %d]" % (parts[i], parts[j]))
+                i = j + 1
+            lines += [k + "partitionFunction = %s" % c.partition_function,
+                      k + "numPartitions = %d" % c.num_partitions, k + "partitionValues = %s" % ",".join(ranges)]
     return "\n".join(lines) + "\n"
+
+
+def _partitions(c):
+    import bloom as B
+    import pruner as P
+    if c.partitions is not None:
+        return set(c.partitions)
+    vals = [v.item() if hasattr(v, "item") else v for v in c.dict_values()]
+    return {B.partition_of(c.partition_function, c.num_partitions, c.data_type, v, P.java_to_string(c.data_type, v))
+            for v in vals}
+
+
+def _bloom_bytes(c):
+    import bloom as B
+    import pruner as P
+    if getattr(c, "bloom_filter", None) is not None:
+        return c.bloom_filter
+    if not getattr(c, "create_bloom_filter", False):
+        return None
+    bf = B.BloomFilter.for_cardinality(c.cardinality)
+    for v in c.dict_values():
+        bf.put(P.java_to_string(c.data_type, v.item() if hasattr(v, "item") else v))
+    return bf.to_bytes()
 
 
 def _varint(n):
@@ -111,6 +148,9 @@ def _buffers(c):
             c.fwd, w, c.num_docs)
         return
     yield "dictionary", c.name + ".dict", c.dictionary
+    bloom = _bloom_bytes(c)
+    if bloom is not None:
+        yield "bloom_filter", c.name + ".bloom", bloom
     if c.is_sorted:
         yield "forward_index", c.name + ".sv.sorted.fwd", c.sorted_index
     else:

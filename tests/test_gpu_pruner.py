@@ -141,3 +141,52 @@ def test_server_executor_prunes():
         assert st.num_segments_processed == len(host) - sum(P.prune(P.ranges(s), q) for s in host), text
         assert st.num_total_raw_docs == st0.num_total_raw_docs
     srv.close()
+
+
+def _partitioned_segments(tmp_path, n=4, docs=4000, seed=21):
+    """A table partitioned on pk (Modulo 4: segment i holds partition i's values) with a bloom filter on u (sparse
+    ids whose min / max ranges overlap), registered from descriptors and loaded from v1 / v3 directories written with
+    the .bloom files and partition metadata (the loaded form reads them from the files)."""
+    from segdir_writer import write_segment_dir
+    rng = np.random.default_rng(seed)
+    host, dirs = [], []
+    for i in range(n):
+        pk = (4 * rng.integers(0, 50, docs) + i).astype(np.int32)
+        u = (rng.integers(0, 200, docs) * 97 + i).astype(np.int32)
+        cols = {"pk": ("INT", pk), "u": ("INT", u), "m": ("LONG", rng.integers(-500, 500, docs).astype(np.int64)),
+                "s": ("STRING", np.array(["w%d" % (i * 10 + v) for v in rng.integers(0, 5, docs)], dtype=object))}
+        seg = build_segment("pseg_%d" % i, cols, min_max=True, bloom_columns=("u", "s"),
+                            partitions={"pk": ("Modulo", 4), "s": ("Murmur", 3)})
+        host.append(seg)
+        dirs.append(write_segment_dir(seg, str(tmp_path / ("pseg_%d" % i)), version="v3" if i % 2 else "v1"))
+    return host, dirs
+
+
+def test_bloom_and_partition_pruning(engine, tmp_path):
+    host, dirs = _partitioned_segments(tmp_path)
+    for form in ("register", "load"):
+        gsegs = [engine.register(s) for s in host] if form == "register" else [engine.load(d) for d in dirs]
+        pruning, plain = ServerQueryExecutor(engine), ServerQueryExecutor(engine, pruners=0)
+        some_pruned = 0
+        for text in ("SELECT COUNT(*), SUM(m) FROM t WHERE pk = 42", "SELECT COUNT(*), SUM(m) FROM t WHERE pk = 7",
+                     "SELECT COUNT(*), SUM(m) FROM t WHERE u = %d" % (97 * 13 + 2),
+                     "SELECT COUNT(*), SUM(m) FROM t WHERE u = %d" % (97 * 13 + 5),
+                     "SELECT COUNT(*), MAX(m) FROM t WHERE s = 'w21' OR pk = 1",
+                     "SELECT COUNT(*), SUM(m) FROM t WHERE pk = 6 AND u > 100 GROUP BY s"):
+            q = compile_pql(text)
+            want = [P.prune(P.ranges(s), q) for s in host]
+            flags, _ = _native_flags(engine, gsegs, q)
+            assert flags == want, (form, text)
+            some_pruned += sum(want)
+            for s, f in zip(host, want):
+                assert not f or int(O.filter_mask(s, q["filter"]).sum()) == 0, text
+            got, st = pruning.process_query(q, gsegs, trim=False)
+            ref, _ = plain.process_query(q, gsegs, trim=False)
+            if q.get("group_by"):
+                assert set(got) == set(ref) and all(_same(got[k], ref[k]) for k in got), text
+            else:
+                assert _same(got, ref), text
+            assert st.num_segments_processed == len(host) - sum(want), text
+        assert some_pruned >= 10, some_pruned
+        for g in gsegs:
+            g.release()

@@ -10,6 +10,7 @@ import math
 import numpy as np
 import pytest
 
+import bloom as B
 import datatable as D
 import pinot_oracle as O
 import pruner as P
@@ -63,7 +64,16 @@ def _random_segment(rng, n, name):
         "d": ("DOUBLE", rng.integers(int(rng.integers(-90, 0)), int(rng.integers(1, 90)), n) * 0.1),
         "s": ("STRING", np.array(["k%02d" % v for v in rng.integers(int(rng.integers(0, 40)), 80, n)], dtype=object)),
     }
-    return build_segment(name, cols, min_max=True)
+    # bloom filters and partition metadata on some columns (ColumnValueSegmentPruner's bloom test,
+    # PartitionSegmentPruner); each function / type pairing the creator accepts
+    bloom = [c for c in "ilfds" if rng.integers(0, 2)]
+    parts = {}
+    for c, fns in (("i", ("Modulo", "Murmur", "HashCode", "ByteArray")), ("l", ("Murmur", "HashCode", "ByteArray")),
+                   ("f", ("HashCode", "Murmur")), ("d", ("HashCode", "ByteArray")),
+                   ("s", ("Murmur", "ByteArray", "HashCode"))):
+        if rng.integers(0, 2):
+            parts[c] = (fns[int(rng.integers(0, len(fns)))], int(rng.integers(2, 9)))
+    return build_segment(name, cols, min_max=True, bloom_columns=bloom, partitions=parts)
 
 
 def _literal(rng, seg, col):
@@ -254,3 +264,117 @@ def test_columns_without_min_max_never_prune_by_value():
     with pytest.raises(PinotGpuError) as ei:
         prune_segment(bad, _q("a = 1"))
     assert ei.value.status == 1
+
+
+# ---------------------------------------------------------------- bloom filters (ColumnValueSegmentPruner :140-144)
+def test_bloom_filter_util_kats():
+    # BloomFilterCreatorTest.testBloomFilterUtil (pinot-core/src/test/.../BloomFilterCreatorTest.java:49-67)
+    assert B.compute_num_bits(1000000, 0.03) == 7298441
+    assert B.compute_num_bits(10000000, 0.03) == 72984409
+    assert B.compute_num_bits(10000000, 0.1) == 47925292
+    assert B.compute_num_hash_functions(1000000, 7298441) == 5
+    assert B.compute_num_hash_functions(10000000, 72984409) == 5
+    assert B.compute_num_hash_functions(10000000, 47925292) == 3
+    assert abs(B.compute_max_false_pos_probability(1000000, 5, 7298441) - 0.03) < 0.001
+    assert abs(B.compute_max_false_pos_probability(10000000, 5, 72984409) - 0.03) < 0.001
+    assert abs(B.compute_max_false_pos_probability(10000000, 3, 47925292) - 0.1) < 0.001
+
+
+def test_bloom_filter_creator_kats():
+    # BloomFilterCreatorTest.testBloomFilterCreator (:70-97): "0".."4" added to a cardinality-10000 filter
+    bf = B.BloomFilter.for_cardinality(10000)
+    for i in range(5):
+        bf.put(str(i))
+    back = B.BloomFilter.from_bytes(bf.to_bytes())
+    assert all(back.might_contain(str(i)) for i in range(5))
+    assert not any(back.might_contain(str(j)) for j in range(5, 10))
+    # testBloomFilterSize (:99-121): at most 1 MB + Guava's 12-byte overhead (+ Pinot's 8-byte header)
+    for card in (10, 100, 1000, 100000, 1000000, 5000000, 10000000):
+        f = B.BloomFilter.for_cardinality(card)
+        assert 8 * len(f.words) + 6 < 1024 * 1024 + 12, card
+    # MurmurHash3_x64_128 of "hello" (seed 0): the widely published (h1, h2) pair
+    assert B.murmur3_x64_128(b"hello") == (0xcbd8a7b341bd9b02, 0x5b1e906a48ae1d19)
+    assert B.murmur3_x64_128(b"") == (0, 0)
+
+
+def test_bloom_filter_prunes_inside_the_min_max_range():
+    vals = np.arange(0, 1000, 10, dtype=np.int32)  # every 10th value: min / max never rule out the gaps
+    seg = build_segment("b", {"x": ("INT", vals), "y": ("STRING", np.array(["v%d" % v for v in vals], dtype=object))},
+                        min_max=True, bloom_columns=("x", "y"))
+    rs = P.ranges(seg)
+    gaps = kept = 0
+    for v in range(-5, 1005):
+        for q in (_q("x = %d" % v), _q("y = 'v%d'" % v)):
+            want = P.prune(rs, q)
+            assert prune_segment(seg, q) == want, (v, q)
+            if v % 10 == 0 and 0 <= v < 1000:
+                assert not want, v  # no false negatives
+                kept += 1
+            elif want:
+                gaps += 1
+    assert kept == 200 and gaps > 1600, gaps  # a 5 % false-positive filter rules out most gaps
+    # the same filter handed over as .bloom bytes (BloomFilterReader) gives the same answers, and so does a
+    # MURMUR128_MITZ_32 (ordinal 0) filter read from bytes
+    for strategy in (1, 0):
+        bf = B.BloomFilter.for_cardinality(len(vals))
+        bf.strategy = strategy
+        for v in vals:
+            bf.put(str(int(v)))
+        seg.columns["x"].create_bloom_filter = False
+        seg.columns["x"].bloom_filter = bf.to_bytes()
+        rs = P.ranges(seg)
+        for v in range(-5, 1005, 3):
+            assert prune_segment(seg, _q("x = %d" % v)) == P.prune(rs, _q("x = %d" % v)), (strategy, v)
+
+
+def test_bloom_filter_rejects_malformed_bytes():
+    seg = build_segment("b", {"x": ("INT", np.arange(10, dtype=np.int32))})
+    good = B.BloomFilter.for_cardinality(10).to_bytes()
+    for bad in (good[:10], b"\x00\x00\x00\x02" + good[4:], good[:4] + b"\x00\x00\x00\x02" + good[8:],
+                good[:8] + b"\x05" + good[9:], good[:-8]):
+        seg.columns["x"].bloom_filter = bad
+        with pytest.raises(PinotGpuError):
+            prune_segment(seg, _q("x = 3"))
+
+
+# ---------------------------------------------------------------- PartitionSegmentPruner (:73-111)
+def test_partition_functions_java_semantics():
+    assert B.java_string_hash("abc") == 96354 and B.java_string_hash("hello") == 99162322
+    assert B.partition_of("Modulo", 4, "INT", -7, "-7") == -3          # Java % keeps the sign: never held
+    assert B.partition_of("modulo", 4, "STRING", "13", "13") == 1
+    assert B.partition_of("HashCode", 5, "INT", -(1 << 31), str(-(1 << 31))) == -3  # abs(MIN_VALUE) stays negative
+    assert B.partition_of("ByteArray", 5, "INT", 0, "0") == (31 + 48) % 5
+    with pytest.raises(ValueError):
+        B.partition_of("Modulo", 4, "LONG", 5, "5")
+
+
+def test_partition_pruner_native_matches_oracle():
+    rng = np.random.default_rng(77)
+    n = 300
+    checked = pruned = 0
+    for fn, dt, vals in (("Modulo", "INT", rng.integers(-50, 50, n)), ("Murmur", "INT", rng.integers(0, 1000, n)),
+                         ("HashCode", "LONG", rng.integers(-(1 << 40), 1 << 40, n)),
+                         ("ByteArray", "STRING", ["p%d" % v for v in rng.integers(0, 30, n)]),
+                         ("HashCode", "DOUBLE", rng.integers(-20, 20, n) * 0.5),
+                         ("Murmur", "FLOAT", (rng.integers(-20, 20, n) * 0.25).astype(np.float32)),
+                         ("HashCode", "STRING", ["h%d" % v for v in rng.integers(0, 30, n)])):
+        for nparts in (3, 8):
+            # a segment holding only the values of some partitions (a partitioned table's segment)
+            keep = [v for v in vals if B.partition_of(fn, nparts, dt, v.item() if hasattr(v, "item") else v,
+                                                     P.java_to_string(dt, v.item() if hasattr(v, "item") else v))
+                    in (0, 1) or fn == "Modulo"]
+            col = np.array(keep, dtype=object) if dt == "STRING" else np.asarray(keep)
+            seg = build_segment("p", {"c": (dt, col)}, partitions={"c": (fn, nparts)})
+            rs = P.ranges(seg)
+            cand = list(dict.fromkeys(list(vals[:40]) + list(keep[:10])))
+            for v in cand:
+                lit = ("'%s'" % v) if dt == "STRING" else (str(int(v)) if dt in ("INT", "LONG") else repr(float(v)))
+                q = _q("c = %s" % lit)
+                want = P.prune(rs, q)
+                assert prune_segment(seg, q) == want, (fn, dt, v)
+                assert prune_segment(seg, q, pruners=P.PARTITION) == P.prune(rs, q, P.PARTITION), (fn, dt, v)
+                checked += 1
+                pruned += want
+                if want:
+                    assert int(O.filter_mask(seg, q["filter"]).sum()) == 0, (fn, dt, v)
+    assert checked > 200 and pruned > 20, (checked, pruned)

@@ -384,7 +384,8 @@ def measure(job, args, workload):
                            "max": float(np.max(step_ms)), "first": [round(x, 4) for x in step_ms[:4]],
                            # the device's own time per step (in-kernel wall clock / events), beside the host's
                            "device_p50": float(np.median(dev_ms)), "device_min": float(np.min(dev_ms)),
-                           "device_max": float(np.max(dev_ms))},
+                           "device_max": float(np.max(dev_ms)),
+                           "device_first": [round(x, 4) for x in dev_ms[:8]]},
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define PINOT_GPU_ABI_VERSION 8
+#define PINOT_GPU_ABI_VERSION 9
 
 /* ------------------------------------------------------------------ status */
 typedef enum {
@@ -110,7 +110,14 @@ typedef struct {
   int32_t num_partitions;
   const char *partition_function;
   const int32_t *partition_values; int32_t num_partition_values;
-  int32_t reserved8;
+  /* Multi-value columns (ABI >= 9; column.<c>.isSingleValues = false): forward_index then holds the
+     FixedBitMultiValueReader layout (PC/io/reader/impl/v1/FixedBitMultiValueReader.java:30-74): BE int chunk offsets
+     (one per ceil(2048 / (entries / rows)) rows), a bitmap of entries marking each row's first value (MSB first),
+     then the entries' dictIds fixed-bit packed. total_number_of_entries / max_number_of_multi_values are the
+     metadata's totalNumberOfEntries / maxNumberOfMultiValues. Dictionary columns only; never sorted. */
+  int32_t multi_value;
+  int32_t max_number_of_multi_values;
+  int64_t total_number_of_entries;
 } pinot_column_desc;
 
 typedef struct {
@@ -143,7 +150,11 @@ typedef struct {
 
 typedef enum {
   PINOT_AGG_COUNT = 0, PINOT_AGG_SUM = 1, PINOT_AGG_MIN = 2, PINOT_AGG_MAX = 3,
-  PINOT_AGG_AVG = 4, PINOT_AGG_DISTINCTCOUNTHLL = 5
+  PINOT_AGG_AVG = 4, PINOT_AGG_DISTINCTCOUNTHLL = 5,
+  /* multi-value variants (PC/query/aggregation/function/*MVAggregationFunction.java): over every entry of the
+     matching docs' values; COUNTMV counts entries, AVGMV's count is entries */
+  PINOT_AGG_COUNTMV = 6, PINOT_AGG_SUMMV = 7, PINOT_AGG_MINMV = 8, PINOT_AGG_MAXMV = 9,
+  PINOT_AGG_AVGMV = 10, PINOT_AGG_DISTINCTCOUNTHLLMV = 11
 } pinot_agg_function;
 
 typedef struct {

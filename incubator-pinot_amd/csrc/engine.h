@@ -29,6 +29,12 @@ struct ColumnData {
   bool raw = false;                   // registered from a raw (no-dictionary) forward index, transcoded
   bool has_minmax = false;            // metadata minValue / maxValue present (the segment pruner's only input)
   std::string min_value, max_value;
+  bool mv = false;                    // multi-value column: fwd packs its entries, mv_offsets[doc] = first entry
+  int64_t num_values = 0;             // totalNumberOfEntries (MV)
+  int32_t max_mv = 0;                 // longest row (MV)
+  uint64_t mv_raw_offset = 0;         // byte offset of the packed entries in the descriptor's forward_index
+  std::vector<uint32_t> mv_offsets_host;  // numDocs + 1 row starts (host copy: oracle-free checks, key strings)
+  DeviceBuffer mv_offsets;            // u32 [numDocs + 1]
   BloomFilter bloom;                  // empty: none (ColumnValueSegmentPruner's EQUALITY test)
   int partition_fn = PF_NONE;         // PartitionFunctionKind of the partition metadata (PartitionSegmentPruner)
   int32_t num_partitions = 0;
@@ -81,6 +87,7 @@ void validate_segment(const pinot_segment_desc &d);
 // The pruning metadata of a column descriptor (bloom filter bytes or creation from the decoded dictionary, partition
 // metadata) into c; c's dictionary must be decoded already (parse_column calls it).
 void parse_pruning_metadata(ColumnData &c, const pinot_column_desc &d);
+void parse_multi_value(ColumnData &c, const pinot_column_desc &d, int32_t num_docs);
 std::string java_double_to_string(double v);  // Double.toString
 std::string java_float_to_string(float v);    // Float.toString
 

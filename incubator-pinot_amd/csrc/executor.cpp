@@ -60,7 +60,7 @@ struct Arena {
 
 // One device step of a segment's filter plan.
 struct FilterStep {
-  enum Kind { SCAN, RANGES, ROARING, COMBINE, FILL } kind;
+  enum Kind { SCAN, RANGES, ROARING, COMBINE, FILL, MV_SCAN } kind;
   int col = -1;
   int leaf_kind = LEAF_RANGE;
   uint32_t lo = 0, span = 0;
@@ -256,6 +256,16 @@ class Compiler {
         st.off = ar_.add(ids.data(), ids.size() * 4);
         return st;
       }
+    }
+    if (c.mv) {  // MVScanDocIdIterator: applyMV over each doc's entries (any / every one for exclusive predicates)
+      sp_.scan_leaves++;
+      std::vector<uint32_t> lut((c.card + 31) / 32 + 1, 0u);
+      for (int32_t i = 0; i < c.card; i++)
+        if (ev.matching[i]) lut[i >> 5] |= 1u << (i & 31);
+      st.kind = FilterStep::MV_SCAN;
+      st.negate = ev.exclusive() ? 1 : 0;
+      st.off = ar_.add(lut.data(), lut.size() * 4);
+      return st;
     }
     scan_leaf(c, ev, st);
     return st;
@@ -464,6 +474,21 @@ const uint64_t *run_filter(Engine &e, SegPlan &p, const QueryScratch &qs, Timer 
       case FilterStep::COMBINE:
         launch_bitset_combine(dst, slot(st.src), nwords, s.num_docs, st.mode, 0, e.stream);
         break;
+      case FilterStep::MV_SCAN: {
+        const ColumnData &c = *s.cols[st.col];
+        MvLeafArgs a{};
+        a.fwd = c.fwd.get<uint8_t>();
+        a.offsets = c.mv_offsets.get<uint32_t>();
+        a.bits = c.bits;
+        a.all = st.negate;
+        a.lut = reinterpret_cast<const uint32_t *>(qs.arena + st.off);
+        a.nwords = nwords;
+        a.num_docs = s.num_docs;
+        a.mode = st.mode;
+        a.dst = dst;
+        t.timed(0, [&] { launch_mv_leaf(a, e.stream); });
+        break;
+      }
       case FilterStep::FILL:
         launch_bitset_combine(dst, nullptr, nwords, s.num_docs, st.mode, st.negate, e.stream);
         break;
@@ -1062,10 +1087,191 @@ bool shortcut_aggregate(const std::vector<SegmentData *> &segs, const pinot_quer
 
 }  // namespace
 
+namespace {
+
+bool is_mv_function(int f) { return f >= PINOT_AGG_COUNTMV && f <= PINOT_AGG_DISTINCTCOUNTHLLMV; }
+
+// Does the query aggregate over a multi-value column (or with an MV function)? AggregationFunctionFactory pairs MV
+// functions with MV columns; a single-value function over an MV column reads it as single-valued and fails.
+bool touches_mv_aggregation(const std::vector<SegmentData *> &segs, const pinot_query &q) {
+  bool mv = false;
+  for (int a = 0; a < q.num_aggregations; a++) {
+    const int f = q.aggregations[a].function;
+    const std::string col = agg_column(q.aggregations[a]);
+    bool col_mv = false;
+    for (SegmentData *sg : segs) {
+      auto it = sg->by_name.find(col);
+      col_mv = col_mv || (it != sg->by_name.end() && sg->cols[it->second]->mv);
+    }
+    if (is_mv_function(f)) {
+      require(col_mv || col == "*", PINOT_ERR_BAD_QUERY, "multi-value aggregation over single-value column " + col);
+      mv = true;
+    } else if (col_mv && f != PINOT_AGG_COUNT) {
+      throw Error(PINOT_ERR_BAD_QUERY, "single-value aggregation over multi-value column " + col);
+    }
+  }
+  return mv;
+}
+
+// Aggregation-only query with multi-value functions (CountMV / SumMV / MinMV / MaxMV / AvgMV / DistinctCountHLLMV,
+// PC/query/aggregation/function/*MVAggregationFunction.java: aggregate() folds every entry of every matching doc),
+// beside any single-value functions of the same query: per segment the filter's dense bitset (the launch sequence,
+// MV scan leaves included) and ONE k_mv_aggregate over its docs; the segments' partials merged in segment order on
+// the host (CombineService.mergeTwoBlocks).
+void exec_aggregate_mv(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q, pinot_agg_result *out,
+                       pinot_exec_stats *stats) {
+  const int na = q.num_aggregations;
+  const size_t S = segs.size();
+  Arena ar;
+  std::unique_ptr<FilterTreeInput> tree;
+  std::vector<SegPlan> plans = plan_all(e, segs, q, ar, tree);
+  QueryScratch qs = prepare(e, plans, ar);
+  constexpr size_t kOut = 5 * kMaxAggs * 8, kHll = kMaxAggs * 256 * 4;
+  e.fused_result.reserve(kOut + kHll + 64);
+  uint8_t *dev = e.fused_result.device<uint8_t>();
+  const uint8_t *host = e.fused_result.host<uint8_t>();
+  std::vector<unsigned long long> init(5 * kMaxAggs, 0ull);
+  for (int g = 0; g < kMaxAggs; g++) init[5 * g + 3] = ~0ull;
+  PINOT_HIP(hipEventRecord(e.ev_start, e.stream));
+  upload_arena(e, ar);
+  Timer t(e);
+  struct Part {
+    int64_t docs = 0;
+    std::vector<unsigned long long> v;
+    std::vector<uint32_t> hll;
+  };
+  std::vector<Part> parts(S);
+  for (size_t si = 0; si < S; si++) {
+    SegPlan &p = plans[si];
+    SegmentData &sg = *p.seg;
+    if (p.empty || sg.num_docs == 0) continue;
+    const uint64_t *bits = run_filter(e, p, qs, t);
+    MvAggArgs a{};
+    a.bitset = bits;
+    a.nwords = sg.nwords();
+    a.num_docs = sg.num_docs;
+    a.n = na;
+    for (int g = 0; g < na; g++) {
+      const int f = q.aggregations[g].function;
+      MvAggSpec &sp = a.specs[g];
+      if (f == PINOT_AGG_COUNT) {
+        sp.kind = MVA_COUNT_DOCS;
+        continue;
+      }
+      ColumnData &c = *sg.column(agg_column(q.aggregations[g]));
+      sp.fwd = c.fwd.get<uint8_t>();
+      sp.offsets = c.mv ? c.mv_offsets.get<uint32_t>() : nullptr;
+      sp.dict = c.dict_dev.get();
+      sp.bits = c.bits;
+      sp.value_kind = c.value_kind();
+      sp.numeric = c.numeric() ? 1 : 0;
+      sp.kind = MVA_VALUES;
+      if (f == PINOT_AGG_DISTINCTCOUNTHLL || f == PINOT_AGG_DISTINCTCOUNTHLLMV) {
+        ensure_hll_lut(e, c);
+        sp.hll_lut = c.hll_lut.get<uint16_t>();
+        sp.kind = MVA_HLL;
+      } else {
+        require(c.numeric() || f == PINOT_AGG_COUNTMV, PINOT_ERR_BAD_QUERY,
+                "numeric aggregation over STRING column " + c.name);
+      }
+    }
+    a.out = reinterpret_cast<unsigned long long *>(dev);
+    a.hll = reinterpret_cast<uint32_t *>(dev + kOut);
+    a.docs = reinterpret_cast<unsigned long long *>(dev + kOut + kHll);
+    PINOT_HIP(hipMemcpyAsync(dev, init.data(), kOut, hipMemcpyHostToDevice, e.stream));
+    PINOT_HIP(hipMemsetAsync(dev + kOut, 0, kHll + 8, e.stream));
+    t.timed(1, [&] { launch_mv_aggregate(a, e.stream); });
+    PINOT_HIP(hipGetLastError());
+    wait_stream(e);  // the result block is reused by the next segment
+    Part &pt = parts[si];
+    pt.docs = (int64_t)*reinterpret_cast<const volatile unsigned long long *>(host + kOut + kHll);
+    pt.v.assign(reinterpret_cast<const unsigned long long *>(host),
+                reinterpret_cast<const unsigned long long *>(host) + 5 * kMaxAggs);
+    pt.hll.assign(reinterpret_cast<const uint32_t *>(host + kOut),
+                  reinterpret_cast<const uint32_t *>(host + kOut) + kMaxAggs * 256);
+  }
+  PINOT_HIP(hipEventRecord(e.ev_stop, e.stream));
+  wait_stream(e);
+  float ms = 0;
+  PINOT_HIP(hipEventElapsedTime(&ms, e.ev_start, e.ev_stop));
+  t.collect();
+  auto decode = [](unsigned long long o) {
+    const unsigned long long u = (o & 0x8000000000000000ull) ? (o & ~0x8000000000000000ull) : ~o;
+    double d;
+    memcpy(&d, &u, 8);
+    return d;
+  };
+  std::vector<int64_t> counts(S, 0);
+  for (size_t si = 0; si < S; si++) counts[si] = parts[si].docs;
+  for (int g = 0; g < na; g++) {
+    pinot_agg_result &r = out[g];
+    memset(&r, 0, sizeof(r));
+    const int f = q.aggregations[g].function;
+    const bool exact = true;
+    __int128 isum = 0;
+    double dsum = 0.0, mn = INFINITY, mx = -INFINITY;
+    int64_t entries = 0, docs = 0;
+    bool any_fp = false;
+    uint8_t regs[256] = {};
+    for (size_t si = 0; si < S; si++) {  // CombineService.mergeTwoBlocks, segment order
+      const Part &pt = parts[si];
+      if (pt.v.empty()) continue;
+      docs += pt.docs;
+      const unsigned long long *o = pt.v.data() + 5 * g;
+      if (o[0] == 0) continue;
+      entries += (int64_t)o[0];
+      isum += (__int128)(long long)o[1];
+      double d;
+      memcpy(&d, &o[2], 8);
+      if (plans[si].seg->column(agg_column(q.aggregations[g]))->value_kind() == 2) any_fp = true;
+      dsum += d;
+      mn = java_min(mn, decode(o[3]));
+      mx = java_max(mx, decode(o[4]));
+      for (int j = 0; j < 256; j++) regs[j] = std::max<uint8_t>(regs[j], (uint8_t)pt.hll[(size_t)g * 256 + j]);
+    }
+    (void)exact;
+    switch (f) {
+      case PINOT_AGG_COUNT: r.count = docs; break;
+      case PINOT_AGG_COUNTMV: r.count = entries; r.value = (double)entries; break;
+      case PINOT_AGG_SUM:
+      case PINOT_AGG_SUMMV:
+      case PINOT_AGG_AVG:
+      case PINOT_AGG_AVGMV:
+        r.count = (f == PINOT_AGG_AVG || f == PINOT_AGG_SUM) ? docs : entries;
+        if (any_fp) {
+          r.value = dsum + (double)isum;
+        } else {
+          r.value = (double)isum;
+          if (isum >= INT64_MIN && isum <= INT64_MAX) {
+            r.exact_sum = (int64_t)isum;
+            r.has_exact_sum = 1;
+          }
+        }
+        break;
+      case PINOT_AGG_MIN:
+      case PINOT_AGG_MINMV: r.count = docs; r.value = mn; break;
+      case PINOT_AGG_MAX:
+      case PINOT_AGG_MAXMV: r.count = docs; r.value = mx; break;
+      default:  // DISTINCTCOUNTHLL(MV)
+        r.count = docs;
+        memcpy(r.hll_registers, regs, 256);
+        r.hll_cardinality = hll_cardinality(r.hll_registers);
+        break;
+    }
+  }
+  fill_stats(q, plans, counts, ms, stats);
+}
+
+}  // namespace
+
 void exec_aggregate(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q, pinot_agg_result *out,
                     pinot_exec_stats *stats) {
   const int na = q.num_aggregations;
   require(na >= 1 && na <= kMaxAggs, PINOT_ERR_UNSUPPORTED, "1..8 aggregation functions per query");
+  if (touches_mv_aggregation(segs, q)) {
+    exec_aggregate_mv(e, segs, q, out, stats);
+    return;
+  }
   if (e.use_shortcut_plans && shortcut_aggregate(segs, q, out, stats)) return;
   int n_hll = 0;
   for (int a = 0; a < na; a++) {

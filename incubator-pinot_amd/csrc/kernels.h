@@ -49,6 +49,43 @@ struct LeafArgs {
 };
 void launch_leaf(int bits, int kind, const LeafArgs &a, hipStream_t stream);
 
+// Multi-value scan leaf (MVScanDocIdIterator, PC/operator/dociditerators/MVScanDocIdIterator.java:108-123, with
+// BaseDictionaryBasedPredicateEvaluator.applyMV :103-121): a doc matches when ANY entry's dictId is in lut, or for an
+// exclusive predicate (all = 1) when EVERY entry's is; written to / AND-ed into / OR-ed into dst like LeafArgs.
+struct MvLeafArgs {
+  const uint8_t *fwd;          // packed entries
+  const uint32_t *offsets;     // [num_docs + 1] row starts
+  const uint32_t *lut;         // bit dictId = applySV(dictId)
+  int64_t nwords;
+  int32_t num_docs, bits;
+  int32_t all, mode;
+  uint64_t *dst;
+};
+void launch_mv_leaf(const MvLeafArgs &a, hipStream_t stream);
+
+// Aggregations of a query that touches multi-value columns (the *MVAggregationFunction aggregate() loops, and the
+// single-value functions beside them): one lane per doc over the doc's entries. Per aggregation the kernel keeps
+// out[5 * a + k]: k = 0 entries (COUNT*: docs), 1 int64 sum, 2 double sum bits, 3 / 4 min / max as order-preserving
+// u64 images of the double value; HLL registers in hll[a * 256 + r] (atomicMax).
+enum MvAggKind : int32_t { MVA_COUNT_DOCS = 0, MVA_VALUES = 1, MVA_HLL = 2 };
+struct MvAggSpec {
+  const uint8_t *fwd;          // packed forward index (entries for MV columns)
+  const uint32_t *offsets;     // MV: [num_docs + 1] row starts; null: single-value column
+  const void *dict;            // int32 / int64 / double dictionary values
+  const uint16_t *hll_lut;     // MVA_HLL: (register << 8 | rank) per dictId
+  int32_t bits, kind, value_kind, numeric;
+};
+struct MvAggArgs {
+  const uint64_t *bitset;      // matching docs; null = all
+  int64_t nwords;
+  int32_t num_docs, n;
+  MvAggSpec specs[kMaxAggs];
+  unsigned long long *out;     // [kMaxAggs][5], identities on entry (0, 0, +0.0, ~0, 0)
+  uint32_t *hll;               // [kMaxAggs][256]
+  unsigned long long *docs;    // matching docs (one counter)
+};
+void launch_mv_aggregate(const MvAggArgs &a, hipStream_t stream);
+
 enum ColAggOps : int32_t { COLAGG_IDSUM = 1, COLAGG_MINMAX = 2 };
 // Per-column fold over the docs of `bitset` (null = all): per-block partials of COUNT, Σ dictId, min/max dictId.
 struct ColAggArgs {

@@ -11,6 +11,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 namespace pinot {
 
 namespace {
@@ -56,6 +58,136 @@ __global__ void k_ranges_to_bitset(const int32_t *__restrict__ ranges, int32_t n
     word |= (~0ull >> (63 - e)) & (~0ull << s);
   }
   store_mode(out, w, word & tail_mask(w, nwords, num_docs), mode);
+}
+
+// ------------------------------------------------------------------ multi-value scan leaf
+// Entry idx of a fixed-bit packed stream (MSB first, big-endian: PinotDataBitSet.readInt); the stream is padded, so
+// the second dword is always inside the allocation.
+__device__ __forceinline__ uint32_t read_packed(const uint8_t *__restrict__ fwd, int bits, uint64_t idx) {
+  const uint64_t bitpos = idx * (uint64_t)bits;
+  const uint32_t *p = reinterpret_cast<const uint32_t *>(fwd) + (bitpos >> 5);
+  const uint64_t x = ((uint64_t)bswap32(p[0]) << 32) | bswap32(p[1]);
+  return (uint32_t)((x << (bitpos & 31)) >> (64 - bits));
+}
+
+// One lane per doc, one wave per bitset word: the lane walks its doc's entries (applyMV: any entry in the LUT, or
+// for an exclusive predicate every entry), the wave's ballot is the word.
+__global__ __launch_bounds__(kBlock) void k_mv_leaf(MvLeafArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t w = wave0; w < a.nwords; w += nwaves) {
+    const int64_t doc = w * 64 + lane;
+    bool match = false;
+    if (doc < a.num_docs) {
+      const uint32_t b = a.offsets[doc], e = a.offsets[doc + 1];
+      match = a.all != 0;
+      for (uint32_t v = b; v < e; v++) {
+        const uint32_t id = read_packed(a.fwd, a.bits, v);
+        const bool in = (a.lut[id >> 5] >> (id & 31)) & 1u;
+        if (a.all ? !in : in) {
+          match = !a.all;
+          break;
+        }
+      }
+    }
+    const uint64_t word = __ballot(match);
+    if (lane == 0) store_mode(a.dst, w, word & tail_mask(w, a.nwords, a.num_docs), a.mode);
+  }
+}
+
+// ------------------------------------------------------------------ aggregations over multi-value columns
+__device__ __forceinline__ unsigned long long ordered_u64(double d) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(d);
+  return (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
+}
+
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
+  for (int o = 32; o > 0; o >>= 1) v += (unsigned long long)__shfl_xor((long long)v, o, 64);
+  return v;
+}
+
+// One lane per doc of the bitset (grid-stride); per aggregation register partials folded with wave reductions and
+// one memory-side atomic per wave (integer sums exact; double sums within rounding of the reference's own
+// summation order, which its combine leaves unspecified).
+__global__ __launch_bounds__(kBlock) void k_mv_aggregate(MvAggArgs a) {
+  const int lane = threadIdx.x & 63;
+  unsigned long long docs = 0;
+  unsigned long long cnt[kMaxAggs], isum[kMaxAggs], mn[kMaxAggs], mx[kMaxAggs];
+  double dsum[kMaxAggs];
+#pragma unroll
+  for (int g = 0; g < kMaxAggs; g++) {
+    cnt[g] = isum[g] = mx[g] = 0;
+    mn[g] = ~0ull;
+    dsum[g] = 0.0;
+  }
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t ndocs = ((int64_t)a.num_docs + 63) / 64 * 64;
+  for (int64_t doc = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; doc < ndocs; doc += stride) {
+    bool m = doc < a.num_docs;
+    if (m && a.bitset) m = (a.bitset[doc >> 6] >> (doc & 63)) & 1ull;
+    if (!m) continue;
+    docs++;
+#pragma unroll
+    for (int g = 0; g < kMaxAggs; g++) {
+      if (g >= a.n) break;
+      const MvAggSpec &sp = a.specs[g];
+      if (sp.kind == MVA_COUNT_DOCS) continue;
+      uint32_t b = (uint32_t)doc, e = (uint32_t)doc + 1;
+      if (sp.offsets) {
+        b = sp.offsets[doc];
+        e = sp.offsets[doc + 1];
+      }
+      for (uint32_t v = b; v < e; v++) {
+        const uint32_t id = read_packed(sp.fwd, sp.bits, v);
+        cnt[g]++;
+        if (sp.kind == MVA_HLL) {
+          const uint32_t h = sp.hll_lut[id];
+          atomicMax(a.hll + g * 256 + (h >> 8), h & 0xFFu);
+          continue;
+        }
+        if (!sp.numeric) continue;
+        double x;
+        if (sp.value_kind == 0) {
+          const long long iv = static_cast<const int32_t *>(sp.dict)[id];
+          isum[g] += (unsigned long long)iv;
+          x = (double)iv;
+        } else if (sp.value_kind == 1) {
+          const long long iv = static_cast<const long long *>(sp.dict)[id];
+          isum[g] += (unsigned long long)iv;
+          x = (double)iv;
+        } else {
+          x = static_cast<const double *>(sp.dict)[id];
+          dsum[g] += x;
+        }
+        const unsigned long long o = ordered_u64(x);
+        mn[g] = o < mn[g] ? o : mn[g];
+        mx[g] = o > mx[g] ? o : mx[g];
+      }
+    }
+  }
+  docs = wave_sum_u64(docs);
+  if (lane == 0 && docs) atomicAdd(a.docs, docs);
+  for (int g = 0; g < a.n; g++) {
+    const unsigned long long c = wave_sum_u64(cnt[g]), s = wave_sum_u64(isum[g]);
+    double d = dsum[g];
+    unsigned long long lo = mn[g], hi = mx[g];
+    for (int o = 32; o > 0; o >>= 1) {
+      d += __shfl_xor(d, o, 64);
+      const unsigned long long l2 = (unsigned long long)__shfl_xor((long long)lo, o, 64);
+      const unsigned long long h2 = (unsigned long long)__shfl_xor((long long)hi, o, 64);
+      lo = l2 < lo ? l2 : lo;
+      hi = h2 > hi ? h2 : hi;
+    }
+    if (lane == 0 && c) {
+      unsigned long long *o = a.out + 5 * g;
+      atomicAdd(o, c);
+      atomicAdd(o + 1, s);
+      if (d != 0.0) atomicAdd(reinterpret_cast<double *>(o + 2), d);
+      atomicMin(o + 3, lo);
+      atomicMax(o + 4, hi);
+    }
+  }
 }
 
 // ------------------------------------------------------------------ K3: roaring containers -> dense tile
@@ -308,6 +440,18 @@ static int grid_for(int64_t items, int per_block, int cap) {
   if (g < 1) g = 1;
   if (g > cap) g = cap;
   return (int)g;
+}
+
+void launch_mv_aggregate(const MvAggArgs &a, hipStream_t stream) {
+  if (a.num_docs <= 0) return;
+  const int64_t blocks = std::min<int64_t>(((int64_t)a.num_docs + kBlock - 1) / kBlock, 4096);
+  hipLaunchKernelGGL(k_mv_aggregate, dim3((unsigned)blocks), dim3(kBlock), 0, stream, a);
+}
+
+void launch_mv_leaf(const MvLeafArgs &a, hipStream_t stream) {
+  if (a.nwords <= 0) return;
+  const int64_t blocks = std::min<int64_t>((a.nwords * 64 + kBlock - 1) / kBlock, 8192);
+  hipLaunchKernelGGL(k_mv_leaf, dim3((unsigned)blocks), dim3(kBlock), 0, stream, a);
 }
 
 void launch_ranges_to_bitset(const int32_t *ranges, int32_t nranges, int64_t nwords, int32_t num_docs,

@@ -79,6 +79,11 @@ static void register_column(Engine &e, SegmentData &seg, const pinot_column_desc
     launch_sorted_to_fwd(dstarts.get<int32_t>(), c.card, c.bits, (int32_t)seg.num_docs, c.fwd.get<uint8_t>(), e.stream);
     PINOT_HIP(hipGetLastError());
     PINOT_HIP(hipStreamSynchronize(e.stream));
+  } else if (c.mv) {  // the packed entries, and the CSR row starts
+    upload(c.fwd, c.fwd_bytes ? d.forward_index + c.mv_raw_offset : nullptr, c.fwd_bytes, padded(c.fwd_bytes), e.stream);
+    upload(c.mv_offsets, c.mv_offsets_host.data(), c.mv_offsets_host.size() * 4, c.mv_offsets_host.size() * 4 + 16,
+           e.stream);
+    PINOT_HIP(hipStreamSynchronize(e.stream));
   } else {
     upload(c.fwd, d.forward_index, c.fwd_bytes, padded(c.fwd_bytes), e.stream);
   }
@@ -91,7 +96,7 @@ static void register_column(Engine &e, SegmentData &seg, const pinot_column_desc
     PINOT_HIP(hipStreamSynchronize(e.stream));
   }
   seg.device_bytes += c.fwd.size() + c.dict_dev.size() + c.inv_payload.size() + c.inv_containers.size() +
-                      c.inv_dir_dev.size();
+                      c.inv_dir_dev.size() + c.mv_offsets.size();
   seg.by_name[c.name] = (int)seg.cols.size();
   seg.cols.push_back(std::move(cp));
 }

@@ -299,7 +299,9 @@ void parse_column(ColumnData &c, const pinot_column_desc &d, int32_t num_docs, P
   c.fwd_bytes = (uint64_t)((n * c.bits + 7) / 8);
   out.sorted_starts.clear();
   out.containers.clear();
-  if (c.is_sorted) {
+  if (d.multi_value) {
+    parse_multi_value(c, d, num_docs);
+  } else if (c.is_sorted) {
     require(d.sorted_index && d.sorted_index_len / 8 >= (uint64_t)c.card, PINOT_ERR_BAD_ARG,
             c.name + ": sorted index must hold 2 ints per dictId");
     c.sorted_start.resize(c.card);
@@ -338,6 +340,59 @@ void parse_column(ColumnData &c, const pinot_column_desc &d, int32_t num_docs, P
     }
     c.inv_dir[c.card] = (int32_t)out.containers.size();
   }
+}
+
+// ---------------------------------------------------------------- multi-value forward index
+// FixedBitMultiValueReader (PC/io/reader/impl/v1/FixedBitMultiValueReader.java:60-74): CHUNK OFFSET (BE int per
+// chunk of numRowsPerChunk = (int) ceil((float) 2048 / (numValues / numRows)) rows: the entry index of the chunk's
+// first row), BITMAP (one bit per entry, MSB first as PinotDataBitSet reads it: set = the entry starts a row), RAW
+// DATA (the entries' dictIds at bits_per_value, FixedBitIntReaderWriter). The row starts become a CSR offset array.
+void parse_multi_value(ColumnData &c, const pinot_column_desc &d, int32_t num_docs) {
+  require(!c.is_sorted, PINOT_ERR_BAD_ARG, c.name + ": a multi-value column cannot be sorted");
+  require(d.encoding == PINOT_ENCODING_DICTIONARY, PINOT_ERR_UNSUPPORTED, c.name + ": raw multi-value columns");
+  const int64_t rows = num_docs, values = d.total_number_of_entries;
+  require(values >= rows && values < ((int64_t)1 << 32) - 1, PINOT_ERR_BAD_ARG,
+          c.name + ": totalNumberOfEntries must be >= numDocs (every row holds a value) and < 2^32");
+  c.mv = true;
+  c.num_values = values;
+  c.mv_offsets_host.assign((size_t)rows + 1, 0);
+  c.fwd_bytes = (uint64_t)((values * c.bits + 7) / 8);
+  if (rows == 0) {
+    c.mv_raw_offset = 0;
+    return;
+  }
+  const int64_t per_row = values / rows;  // Java int division
+  const float q = 2048.0f / (float)per_row;
+  const int64_t rows_per_chunk = std::max<int64_t>(1, (int64_t)std::ceil((double)q));
+  const int64_t num_chunks = (rows + rows_per_chunk - 1) / rows_per_chunk;
+  const uint64_t off_bytes = (uint64_t)num_chunks * 4, bitmap_bytes = (uint64_t)((values + 7) / 8);
+  require(d.forward_index && d.forward_index_len >= off_bytes + bitmap_bytes + c.fwd_bytes, PINOT_ERR_BAD_ARG,
+          c.name + ": multi-value forward index shorter than its chunk offsets + bitmap + packed entries");
+  const uint8_t *bitmap = d.forward_index + off_bytes;
+  int64_t row = 0, longest = 0;
+  for (uint64_t byte = 0; byte < bitmap_bytes; byte++) {
+    uint8_t b = bitmap[byte];
+    while (b) {
+      const int k = __builtin_clz((uint32_t)b) - 24;  // MSB first: bit 7 of the byte is entry 8 * byte
+      const int64_t entry = (int64_t)byte * 8 + k;
+      b &= (uint8_t)~(0x80u >> k);
+      if (entry >= values) break;
+      require(row < rows, PINOT_ERR_BAD_ARG, c.name + ": more row starts than rows");
+      require(row > 0 || entry == 0, PINOT_ERR_BAD_ARG, c.name + ": the first entry must start a row");
+      c.mv_offsets_host[(size_t)row++] = (uint32_t)entry;
+    }
+  }
+  require(row == rows, PINOT_ERR_BAD_ARG, c.name + ": fewer row starts than rows");
+  c.mv_offsets_host[(size_t)rows] = (uint32_t)values;
+  for (int64_t r = 0; r < rows; r++)
+    longest = std::max<int64_t>(longest, (int64_t)c.mv_offsets_host[(size_t)r + 1] - c.mv_offsets_host[(size_t)r]);
+  c.max_mv = (int32_t)longest;
+  require(d.max_number_of_multi_values <= 0 || longest <= d.max_number_of_multi_values, PINOT_ERR_BAD_ARG,
+          c.name + ": a row longer than maxNumberOfMultiValues");
+  for (int64_t k = 0; k < num_chunks; k++)  // each chunk offset is its first row's start (getIntArray reads them)
+    require((int64_t)load_be32(d.forward_index + 4 * k) == (int64_t)c.mv_offsets_host[(size_t)(k * rows_per_chunk)],
+            PINOT_ERR_BAD_ARG, c.name + ": chunk offset " + std::to_string(k) + " disagrees with the bitmap");
+  c.mv_raw_offset = off_bytes + bitmap_bytes;
 }
 
 // ---------------------------------------------------------------- pruning metadata

@@ -15,7 +15,8 @@ STATUS = {0: "PINOT_OK", 1: "PINOT_ERR_BAD_ARG", 2: "PINOT_ERR_OOM", 3: "PINOT_E
 PINOT_ERR_TIMEOUT = 6
 DATA_TYPE = {"INT": 0, "LONG": 1, "FLOAT": 2, "DOUBLE": 3, "STRING": 4}
 FILTER_OP = {"AND": 0, "OR": 1, "EQUALITY": 2, "NOT": 3, "RANGE": 4, "IN": 5, "NOT_IN": 6}
-AGG_FN = {"COUNT": 0, "SUM": 1, "MIN": 2, "MAX": 3, "AVG": 4, "DISTINCTCOUNTHLL": 5}
+AGG_FN = {"COUNT": 0, "SUM": 1, "MIN": 2, "MAX": 3, "AVG": 4, "DISTINCTCOUNTHLL": 5,
+          "COUNTMV": 6, "SUMMV": 7, "MINMV": 8, "MAXMV": 9, "AVGMV": 10, "DISTINCTCOUNTHLLMV": 11}
 # pinot_pruner bits; the server's default list (DefaultHelixStarterServerConfig.java:60-65)
 PRUNER = {"DataSchemaSegmentPruner": 1, "ColumnValueSegmentPruner": 2, "ValidSegmentPruner": 4,
           "PartitionSegmentPruner": 8}
@@ -58,7 +59,8 @@ class ColumnDesc(C.Structure):
                 ("min_value", C.c_char_p), ("max_value", C.c_char_p),
                 ("bloom_filter", C.c_void_p), ("bloom_filter_len", C.c_uint64), ("create_bloom_filter", C.c_int32),
                 ("num_partitions", C.c_int32), ("partition_function", C.c_char_p),
-                ("partition_values", C.c_void_p), ("num_partition_values", C.c_int32), ("reserved8", C.c_int32)]
+                ("partition_values", C.c_void_p), ("num_partition_values", C.c_int32), ("multi_value", C.c_int32),
+                ("max_number_of_multi_values", C.c_int32), ("total_number_of_entries", C.c_int64)]
 
 
 class SegmentDesc(C.Structure):

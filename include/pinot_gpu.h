@@ -151,7 +151,7 @@ typedef struct {
 typedef enum {
   PINOT_AGG_COUNT = 0, PINOT_AGG_SUM = 1, PINOT_AGG_MIN = 2, PINOT_AGG_MAX = 3,
   PINOT_AGG_AVG = 4, PINOT_AGG_DISTINCTCOUNTHLL = 5,
-  /* multi-value variants (PC/query/aggregation/function/*MVAggregationFunction.java): over every entry of the
+  /* multi-value variants (PC/query/aggregation/function/...MVAggregationFunction.java): over every entry of the
      matching docs' values; COUNTMV counts entries, AVGMV's count is entries */
   PINOT_AGG_COUNTMV = 6, PINOT_AGG_SUMMV = 7, PINOT_AGG_MINMV = 8, PINOT_AGG_MAXMV = 9,
   PINOT_AGG_AVGMV = 10, PINOT_AGG_DISTINCTCOUNTHLLMV = 11

@@ -206,7 +206,7 @@ Value get_object(const Table &t, int32_t row, int32_t col, std::vector<std::pair
   return Value{};
 }
 
-int fn_of(const pinot_query &q, int i) { return q.aggregations[i].function; }
+int fn_of(const pinot_query &q, int i) { return sv_function(q.aggregations[i].function); }
 
 // AggregationFunction.merge for each function (CountAggregationFunction.merge :…, Math.min / Math.max on doubles,
 // AvgPair.apply, HyperLogLog.addAll).

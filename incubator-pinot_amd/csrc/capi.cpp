@@ -380,7 +380,7 @@ pinot_status pinot_groupby_values(const pinot_groupby_result *r, int32_t fn, int
 pinot_status pinot_groupby_hll(const pinot_groupby_result *r, int32_t fn, uint8_t *registers, int64_t *cardinalities) {
   return guard([&] {
     require(r && fn >= 0 && fn < (int32_t)r->functions.size(), PINOT_ERR_BAD_ARG, "function index");
-    require(r->functions[fn] == PINOT_AGG_DISTINCTCOUNTHLL, PINOT_ERR_BAD_ARG, "not a DISTINCTCOUNTHLL function");
+    require(sv_function(r->functions[fn]) == PINOT_AGG_DISTINCTCOUNTHLL, PINOT_ERR_BAD_ARG, "not a DISTINCTCOUNTHLL function");
     const size_t n = r->raw_keys.size();
     if (registers && n) group_by_hll_registers(*r, fn, registers);
     if (cardinalities && n) memcpy(cardinalities, r->hll_card[fn].data(), n * 8);

@@ -106,6 +106,13 @@ std::string aggregation_column_name(const pinot_agg_spec &a) {
     case PINOT_AGG_MAX: return "max_" + col;
     case PINOT_AGG_AVG: return "avg_" + col;
     case PINOT_AGG_DISTINCTCOUNTHLL: return "distinctCountHLL_" + col;
+    // the *MVAggregationFunction overrides (e.g. CountMVAggregationFunction.java:37-40): COUNTMV.getName() + "_" + column
+    case PINOT_AGG_COUNTMV: return "countMV_" + col;
+    case PINOT_AGG_SUMMV: return "sumMV_" + col;
+    case PINOT_AGG_MINMV: return "minMV_" + col;
+    case PINOT_AGG_MAXMV: return "maxMV_" + col;
+    case PINOT_AGG_AVGMV: return "avgMV_" + col;
+    case PINOT_AGG_DISTINCTCOUNTHLLMV: return "distinctCountHLLMV_" + col;
     default: throw Error(PINOT_ERR_BAD_ARG, "aggregation function");
   }
 }
@@ -235,13 +242,13 @@ std::vector<uint8_t> aggregation_datatable(const pinot_query &q, const pinot_agg
   std::vector<std::string> names, types;
   for (int i = 0; i < q.num_aggregations; i++) {
     names.push_back(aggregation_column_name(q.aggregations[i]));
-    const int f = q.aggregations[i].function;
+    const int f = sv_function(q.aggregations[i].function);
     types.push_back(f == PINOT_AGG_COUNT ? "LONG" : (f == PINOT_AGG_AVG || f == PINOT_AGG_DISTINCTCOUNTHLL) ? "OBJECT" : "DOUBLE");
   }
   schema_bytes(t.schema, names, types);
   for (int i = 0; i < q.num_aggregations; i++) {
     const pinot_agg_result &a = r[i];
-    switch (q.aggregations[i].function) {
+    switch (sv_function(q.aggregations[i].function)) {
       case PINOT_AGG_COUNT: t.fixed.i64(a.count); break;
       case PINOT_AGG_SUM:
       case PINOT_AGG_MIN:
@@ -284,7 +291,7 @@ std::vector<uint8_t> group_by_datatable(const pinot_query &q, const GroupByResul
       require(g >= 0 && g < n, PINOT_ERR_BAD_ARG, "group index out of range");
       return g;
     };
-    const int f = r.functions[i];
+    const int f = sv_function(r.functions[i]);
     if (f == PINOT_AGG_DISTINCTCOUNTHLL) {
       regs.resize((size_t)n * 256);
       group_by_hll_registers(r, i, regs.data());
@@ -328,8 +335,9 @@ std::vector<uint8_t> empty_datatable(const pinot_query &q, int64_t total_docs, c
     std::vector<pinot_agg_result> r((size_t)q.num_aggregations);
     for (int i = 0; i < q.num_aggregations; i++) {
       memset(&r[i], 0, sizeof(r[i]));
-      if (q.aggregations[i].function == PINOT_AGG_MIN) r[i].value = INFINITY;    // MinAggregationFunction.java:32
-      if (q.aggregations[i].function == PINOT_AGG_MAX) r[i].value = -INFINITY;   // MaxAggregationFunction.java:32
+      const int f = sv_function(q.aggregations[i].function);
+      if (f == PINOT_AGG_MIN) r[i].value = INFINITY;    // MinAggregationFunction.java:32
+      if (f == PINOT_AGG_MAX) r[i].value = -INFINITY;   // MaxAggregationFunction.java:32
     }
     return aggregation_datatable(q, r.data(), s, srv);
   }

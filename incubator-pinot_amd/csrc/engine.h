@@ -291,6 +291,10 @@ struct DenseOut {
   std::vector<size_t> hll_off;
 };
 
+// The single-value function whose intermediate result / merge / final result a multi-value function shares
+// (CountMVAggregationFunction extends CountAggregationFunction, etc.).
+inline int sv_function(int f) { return f >= PINOT_AGG_COUNTMV && f <= PINOT_AGG_DISTINCTCOUNTHLLMV ? f - PINOT_AGG_COUNTMV : f; }
+
 struct GroupByResult {
   GroupByResult() = default;
   GroupByResult(GroupByResult &&) = default;

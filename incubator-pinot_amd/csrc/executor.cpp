@@ -1724,7 +1724,8 @@ std::unique_ptr<GroupByResult> finalize_groups(Engine &e, const pinot_query &q, 
         cv[i] = (int64_t)hcnt[i];
         const uint64_t raw = hacc[(size_t)a * n + i];
         switch (ak) {
-          case 0: vv[i] = (double)(int64_t)raw; break;
+          case 0:
+          case 6: vv[i] = (double)(int64_t)raw; break;
           case 1: { double d; memcpy(&d, &raw, 8); vv[i] = d; break; }
           case 2:
           case 3: vv[i] = decode_ordered(raw); break;
@@ -1980,7 +1981,7 @@ std::vector<int64_t> GroupByResult::trim(int32_t top_n, int32_t fn) const {
   std::vector<int64_t> idx(n);
   std::iota(idx.begin(), idx.end(), 0);
   if (n <= 4 * trim_size) return idx;
-  const int f = functions[fn];
+  const int f = sv_function(functions[fn]);
   const HostVec<int64_t> &cnt = counts[counts_shared ? 0 : fn];
   std::vector<double> v(n);
   for (int64_t g = 0; g < n; g++) {
@@ -2910,11 +2911,175 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
   return res;
 }
 
+namespace {
+
+bool touches_mv_group_by(const std::vector<SegmentData *> &segs, const pinot_query &q) {
+  bool mv = touches_mv_aggregation(segs, q);
+  for (int j = 0; j < q.num_group_by; j++)
+    for (SegmentData *sg : segs) {
+      auto it = sg->by_name.find(q.group_by[j]);
+      mv = mv || (it != sg->by_name.end() && sg->cols[it->second]->mv);
+    }
+  return mv;
+}
+
+// Group-by with multi-value group columns or MV functions: per segment the filter's bitset and one k_group_by_mv
+// (every doc's cartesian product of group keys, DictionaryBasedGroupKeyGenerator's MV branch) into dense
+// accumulators over the global key space, then the bitset path's finalisation. AvgMV needs its entry count beside
+// its sum: a hidden CountMV accumulator per AvgMV, folded into the function's counts after finalisation. Exact only
+// while no group is dropped: the key space must fit num.groups.limit (no first-appearance admission).
+std::unique_ptr<GroupByResult> exec_group_by_mv(Engine &e, const std::vector<SegmentData *> &segs,
+                                                const pinot_query &q, pinot_exec_stats *stats) {
+  const int na = q.num_aggregations;
+  std::vector<pinot_agg_spec> specs(q.aggregations, q.aggregations + na);
+  std::vector<int> hidden(na, -1);
+  for (int a = 0; a < na; a++)
+    if (q.aggregations[a].function == PINOT_AGG_AVGMV) {
+      require((int)specs.size() < kMaxAggs, PINOT_ERR_UNSUPPORTED, "too many aggregations with AVGMV (8 at most)");
+      pinot_agg_spec h = q.aggregations[a];
+      h.function = PINOT_AGG_COUNTMV;
+      hidden[a] = (int)specs.size();
+      specs.push_back(h);
+    }
+  pinot_query q2 = q;
+  q2.aggregations = specs.data();
+  q2.num_aggregations = (int32_t)specs.size();
+  const int nb = q2.num_aggregations;
+  Arena ar;
+  std::unique_ptr<FilterTreeInput> tree;
+  std::vector<SegPlan> plans = plan_all(e, segs, q2, ar, tree);
+  KeySpace ks = build_key_space(segs, q2);
+  const int64_t limit = q.num_groups_limit > 0 ? q.num_groups_limit : e.num_groups_limit;
+  require(!ks.hashed && ks.G <= limit, PINOT_ERR_UNSUPPORTED,
+          "multi-value group-by needs the group key space within num.groups.limit");
+  GroupAccs ga;
+  for (int a = 0; a < nb; a++) {
+    const int f = specs[a].function;
+    int kind = 5;
+    size_t bytes = 0;
+    if (f != PINOT_AGG_COUNT) {
+      const ColumnData &c = *segs[0]->column(agg_column(specs[a]));
+      bytes = 8;
+      if (f == PINOT_AGG_COUNTMV) {
+        kind = 6;
+      } else if (f == PINOT_AGG_DISTINCTCOUNTHLL || f == PINOT_AGG_DISTINCTCOUNTHLLMV) {
+        kind = 4;
+        bytes = 1024;
+      } else {
+        require(c.numeric(), PINOT_ERR_BAD_QUERY, "numeric aggregation over STRING column " + c.name);
+        const int sf = sv_function(f);
+        kind = sf == PINOT_AGG_MIN ? 2 : sf == PINOT_AGG_MAX ? 3 : c.data_type == PINOT_INT ? 0 : 1;
+      }
+    }
+    ga.acc_kind.push_back(kind);
+    ga.acc_bytes_per_key.push_back(bytes);
+  }
+  size_t per_key = 8;
+  for (auto b : ga.acc_bytes_per_key) per_key += b;
+  size_t free_b = 0, total_b = 0;
+  PINOT_HIP(hipMemGetInfo(&free_b, &total_b));
+  require((double)ks.G * per_key < 0.5 * (double)free_b, PINOT_ERR_UNSUPPORTED,
+          "dense group-by accumulators do not fit in HBM");
+  QueryScratch qs = prepare(e, plans, ar);
+  e.group_scratch.reserve(ks.G * per_key + 64);
+  uint8_t *base = e.group_scratch.get<uint8_t>();
+  auto *counts = reinterpret_cast<unsigned long long *>(base);
+  std::vector<void *> accs(nb, nullptr);
+  uint8_t *p = base + ks.G * 8;
+  for (int a = 0; a < nb; a++) {
+    if (ga.acc_kind[a] == 5) continue;
+    accs[a] = p;
+    p += ks.G * ga.acc_bytes_per_key[a];
+  }
+  PINOT_HIP(hipEventRecord(e.ev_start, e.stream));
+  init_accs(e, ks.G, counts, ga, accs.data());
+  Timer t(e);
+  const size_t S = plans.size();
+  std::vector<DeviceBuffer> remaps(S * q.num_group_by);
+  std::vector<int64_t> seg_counts(S, 0);
+  for (size_t si = 0; si < S; si++) {
+    SegPlan &pl = plans[si];
+    SegmentData &sg = *pl.seg;
+    if (pl.empty || sg.num_docs == 0) continue;
+    const uint64_t *bits = run_filter(e, pl, qs, t);
+    seg_counts[si] = count_docs(e, bits, sg);
+    MvGroupArgs a{};
+    a.n_gcols = q.num_group_by;
+    a.n_aggs = nb;
+    long long stride = 1;
+    for (int j = 0; j < q.num_group_by; j++) {
+      const ColumnData &c = *sg.column(q.group_by[j]);
+      a.gfwd[j] = c.fwd.get<uint8_t>();
+      a.goff[j] = c.mv ? c.mv_offsets.get<uint32_t>() : nullptr;
+      a.gbits[j] = c.bits;
+      const auto &m = ks.remap[si][j];
+      if (!m.empty()) {
+        DeviceBuffer &rb = remaps[si * q.num_group_by + j];
+        rb.alloc(m.size() * 4 + 16);
+        PINOT_HIP(hipMemcpyAsync(rb.get(), m.data(), m.size() * 4, hipMemcpyHostToDevice, e.stream));
+        a.remap[j] = rb.get<int32_t>();
+      }
+      a.stride[j] = stride;
+      stride *= ks.gcard[j];
+    }
+    for (int g = 0; g < nb; g++) {
+      a.acc_kind[g] = ga.acc_kind[g];
+      a.acc[g] = accs[g];
+      if (ga.acc_kind[g] == 5) continue;
+      ColumnData &c = *sg.column(agg_column(specs[g]));
+      a.afwd[g] = c.fwd.get<uint8_t>();
+      a.aoff[g] = c.mv ? c.mv_offsets.get<uint32_t>() : nullptr;
+      a.abits[g] = c.bits;
+      a.dict[g] = c.dict_dev.get();
+      a.value_kind[g] = c.value_kind();
+      if (ga.acc_kind[g] == 4) {
+        ensure_hll_lut(e, c);
+        a.hll_lut[g] = c.hll_lut.get<uint16_t>();
+      }
+    }
+    a.counts = counts;
+    a.bitset = bits;
+    a.nwords = sg.nwords();
+    a.num_docs = sg.num_docs;
+    t.timed(1, [&] { launch_group_by_mv(a, e.stream); });
+    PINOT_HIP(hipGetLastError());
+  }
+  GroupByProgram gp{};
+  gp.n_aggs = nb;
+  gp.counts = counts;
+  for (int a = 0; a < nb; a++) { gp.acc[a] = accs[a]; gp.acc_kind[a] = ga.acc_kind[a]; }
+  auto res = finalize_groups(e, q2, ga, ks, gp);
+  PINOT_HIP(hipEventRecord(e.ev_stop, e.stream));
+  wait_stream(e);
+  float ms = 0;
+  PINOT_HIP(hipEventElapsedTime(&ms, e.ev_start, e.ev_stop));
+  t.collect();
+  // CountMV: the entry count is the function's count; AvgMV: its hidden CountMV's values
+  for (int a = 0; a < na; a++) {
+    const int f = q.aggregations[a].function;
+    const int src = f == PINOT_AGG_COUNTMV ? a : hidden[a];
+    if (src < 0) continue;
+    HostVec<int64_t> &cv = res->counts[a];
+    const HostVec<double> &sv = res->values[src];
+    for (size_t i = 0; i < cv.size(); i++) cv[i] = (int64_t)sv[i];
+  }
+  res->functions.resize(na);
+  res->counts.resize(na);
+  res->values.resize(na);
+  res->hll.resize(na);
+  res->hll_card.resize(na);
+  fill_stats(q, plans, seg_counts, ms, stats);
+  return res;
+}
+
+}  // namespace
+
 std::unique_ptr<GroupByResult> exec_group_by(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q,
                                              pinot_exec_stats *stats) {
   const int na = q.num_aggregations;
   require(na >= 1 && na <= kMaxAggs, PINOT_ERR_UNSUPPORTED, "1..8 aggregation functions per query");
   require(q.num_group_by >= 1 && q.num_group_by <= kMaxGroupCols, PINOT_ERR_UNSUPPORTED, "1..16 group-by columns");
+  if (touches_mv_group_by(segs, q)) return exec_group_by_mv(e, segs, q, stats);
   if (e.use_fused) {
     KeySpace ks = build_key_space(segs, q);
     GroupAccs ga = group_acc_kinds(*segs[0], q);
@@ -2976,6 +3141,7 @@ void exec_group_by_layout(Engine &e, const std::vector<SegmentData *> &segs, con
                           pinot_partial_layout *layout) {
   (void)e;
   require(!segs.empty(), PINOT_ERR_BAD_ARG, "no segments");
+  require(!touches_mv_group_by(segs, q), PINOT_ERR_UNSUPPORTED, "multi-GPU partials of a multi-value group-by");
   KeySpace ks = build_key_space(segs, q);
   require(!ks.hashed, PINOT_ERR_UNSUPPORTED, "partial group-by needs a dense key space");
   for (auto &per_seg : ks.remap)
@@ -2994,6 +3160,7 @@ void exec_group_by_layout(Engine &e, const std::vector<SegmentData *> &segs, con
 void exec_group_by_partial(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q,
                            int64_t *counts_dev, void *const *accs_dev, pinot_exec_stats *stats) {
   require(!segs.empty(), PINOT_ERR_BAD_ARG, "no segments");
+  require(!touches_mv_group_by(segs, q), PINOT_ERR_UNSUPPORTED, "multi-GPU partials of a multi-value group-by");
   KeySpace ks = build_key_space(segs, q);
   require(!ks.hashed, PINOT_ERR_UNSUPPORTED, "partial group-by needs a dense key space");
   GroupAccs ga = group_acc_kinds(*segs[0], q);

@@ -438,6 +438,33 @@ struct GroupByProgram {
 };
 void launch_group_by(const GroupByProgram &prog, const uint64_t *bitset, int64_t nwords, int32_t num_docs,
                      hipStream_t stream);
+// Group-by over multi-value group columns and / or MV aggregations (DefaultGroupByExecutor.process with
+// DictionaryBasedGroupKeyGenerator.generateKeysForBlock(MV), :213-240, and aggregateGroupByMV): one lane per doc;
+// the doc's group keys are the cartesian product of its group columns' entries (duplicates included); every key
+// takes count + 1 and each function folds all entries of its column. acc_kind 6 adds the doc's entry count
+// (CountMV). Columns are (packed fwd, bits, row starts or null for single-value).
+struct MvGroupArgs {
+  int32_t n_gcols, n_aggs;
+  const uint8_t *gfwd[kMaxGroupCols];
+  const uint32_t *goff[kMaxGroupCols];
+  int32_t gbits[kMaxGroupCols];
+  const int32_t *remap[kMaxGroupCols];
+  long long stride[kMaxGroupCols];
+  const uint8_t *afwd[kMaxAggs];
+  const uint32_t *aoff[kMaxAggs];
+  int32_t abits[kMaxAggs];
+  const void *dict[kMaxAggs];
+  const uint16_t *hll_lut[kMaxAggs];
+  int32_t acc_kind[kMaxAggs];   // 0 i64 sum (INT), 1 f64 sum, 2 ordered min, 3 ordered max, 4 HLL u32[256], 5 none,
+                                // 6 entry count
+  int32_t value_kind[kMaxAggs];
+  unsigned long long *counts;
+  void *acc[kMaxAggs];
+  const uint64_t *bitset;       // null = all docs
+  int64_t nwords;
+  int32_t num_docs;
+};
+void launch_group_by_mv(const MvGroupArgs &a, hipStream_t stream);
 // First matching doc per key (atomicMin), for the num.groups.limit first-appearance rule.
 void launch_first_doc(const GroupByProgram &prog, const uint64_t *bitset, int64_t nwords, int32_t num_docs,
                       uint32_t *first_doc, hipStream_t stream);

@@ -331,6 +331,81 @@ __global__ __launch_bounds__(kBlock) void k_group_by(GroupByProgram prog, const 
   }
 }
 
+__device__ __forceinline__ void mv_fold(const MvGroupArgs &a, int g, long long key, uint32_t b, uint32_t e) {
+  const int ak = a.acc_kind[g];
+  if (ak == 6) {
+    atomicAdd(static_cast<unsigned long long *>(a.acc[g]) + key, (unsigned long long)(e - b));
+    return;
+  }
+  for (uint32_t v = b; v < e; v++) {
+    const uint32_t id = read_packed(a.afwd[g], a.abits[g], v);
+    switch (ak) {
+      case 0:
+        atomicAdd(static_cast<unsigned long long *>(a.acc[g]) + key,
+                  (unsigned long long)(long long)static_cast<const int32_t *>(a.dict[g])[id]);
+        break;
+      case 1:
+      case 2:
+      case 3: {
+        double x;
+        switch (a.value_kind[g]) {
+          case 0: x = (double)static_cast<const int32_t *>(a.dict[g])[id]; break;
+          case 1: x = (double)static_cast<const long long *>(a.dict[g])[id]; break;
+          default: x = static_cast<const double *>(a.dict[g])[id]; break;
+        }
+        if (ak == 1) atomicAdd(static_cast<double *>(a.acc[g]) + key, x);
+        else if (ak == 2) atomicMin(static_cast<unsigned long long *>(a.acc[g]) + key, ordered_bits(x));
+        else atomicMax(static_cast<unsigned long long *>(a.acc[g]) + key, ordered_bits(x));
+        break;
+      }
+      case 4: {
+        const uint32_t h = a.hll_lut[g][id];
+        atomicMax(static_cast<uint32_t *>(a.acc[g]) + key * 256 + (h >> 8), h & 0xFFu);
+        break;
+      }
+      default: break;
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_group_by_mv(MvGroupArgs a) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t doc = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; doc < a.num_docs; doc += stride) {
+    if (a.bitset && !((a.bitset[doc >> 6] >> (doc & 63)) & 1ull)) continue;
+    uint32_t lo[kMaxGroupCols], hi[kMaxGroupCols], cur[kMaxGroupCols];
+    bool empty = false;
+    for (int j = 0; j < a.n_gcols; j++) {
+      lo[j] = a.goff[j] ? a.goff[j][doc] : (uint32_t)doc;
+      hi[j] = a.goff[j] ? a.goff[j][doc + 1] : (uint32_t)doc + 1;
+      cur[j] = lo[j];
+      empty = empty || hi[j] <= lo[j];
+    }
+    if (empty) continue;  // a row without entries yields no group key
+    uint32_t ab[kMaxAggs], ae[kMaxAggs];
+    for (int g = 0; g < a.n_aggs; g++) {
+      ab[g] = a.aoff[g] ? a.aoff[g][doc] : (uint32_t)doc;
+      ae[g] = a.aoff[g] ? a.aoff[g][doc + 1] : (uint32_t)doc + 1;
+    }
+    while (true) {  // odometer over the product, column 0 fastest
+      long long key = 0;
+      for (int j = 0; j < a.n_gcols; j++) {
+        int32_t id = (int32_t)read_packed(a.gfwd[j], a.gbits[j], cur[j]);
+        if (a.remap[j]) id = a.remap[j][id];
+        key += (long long)id * a.stride[j];
+      }
+      atomicAdd(a.counts + key, 1ull);
+      for (int g = 0; g < a.n_aggs; g++)
+        if (a.acc_kind[g] != 5) mv_fold(a, g, key, ab[g], ae[g]);
+      int j = 0;
+      for (; j < a.n_gcols; j++) {
+        if (++cur[j] < hi[j]) break;
+        cur[j] = lo[j];
+      }
+      if (j == a.n_gcols) break;
+    }
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void k_first_doc(GroupByProgram prog, const uint64_t *__restrict__ bitset,
                                                        int64_t nwords, int32_t num_docs, uint32_t *first_doc) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -440,6 +515,12 @@ static int grid_for(int64_t items, int per_block, int cap) {
   if (g < 1) g = 1;
   if (g > cap) g = cap;
   return (int)g;
+}
+
+void launch_group_by_mv(const MvGroupArgs &a, hipStream_t stream) {
+  if (a.num_docs <= 0) return;
+  const int64_t blocks = std::min<int64_t>(((int64_t)a.num_docs + kBlock - 1) / kBlock, 4096);
+  hipLaunchKernelGGL(k_group_by_mv, dim3((unsigned)blocks), dim3(kBlock), 0, stream, a);
 }
 
 void launch_mv_aggregate(const MvAggArgs &a, hipStream_t stream) {

@@ -402,7 +402,7 @@ void read_segment_dir(const std::string &index_dir, SegmentDirData &out) {
     const std::string k = "column." + c + ".";
     const int dt = data_type_of(prop(kv, k + "dataType"));
     const bool single = prop_bool(kv, k + "isSingleValues", true), dict = prop_bool(kv, k + "hasDictionary", true);
-    if (dt < 0 || !single || (!dict && dt == PINOT_STRING)) {
+    if (dt < 0 || (!single && !dict) || (!dict && dt == PINOT_STRING)) {
       out.skipped.push_back(c);
       continue;
     }
@@ -467,7 +467,17 @@ void read_segment_dir(const std::string &index_dir, SegmentDirData &out) {
     index_bytes(c, "bloom_filter", c + ".bloom", &d.bloom_filter, &d.bloom_filter_len);
     const uint8_t *fp = nullptr;
     uint64_t fn = 0;
-    require(index_bytes(c, "forward_index", c + (d.is_sorted ? ".sv.sorted.fwd" : ".sv.unsorted.fwd"), &fp, &fn),
+    if (!single) {  // FixedBitMultiValueWriter file (<col>.mv.fwd, V1Constants.java:61)
+      d.multi_value = 1;
+      d.is_sorted = 0;
+      const int64_t entries = prop_int(kv, k + "totalNumberOfEntries");
+      const int64_t maxmv = prop_int(kv, k + "maxNumberOfMultiValues", "0");
+      require(entries >= 0 && maxmv >= 0 && maxmv < INT32_MAX, PINOT_ERR_BAD_ARG, c + ": multi-value metadata out of range");
+      d.total_number_of_entries = entries;
+      d.max_number_of_multi_values = (int32_t)maxmv;
+    }
+    require(index_bytes(c, "forward_index",
+                        c + (!single ? ".mv.fwd" : d.is_sorted ? ".sv.sorted.fwd" : ".sv.unsorted.fwd"), &fp, &fn),
             PINOT_ERR_BAD_ARG, c + ": no forward index");
     if (d.is_sorted) {
       d.sorted_index = fp;

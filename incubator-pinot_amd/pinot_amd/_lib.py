@@ -15,6 +15,13 @@ STATUS = {0: "PINOT_OK", 1: "PINOT_ERR_BAD_ARG", 2: "PINOT_ERR_OOM", 3: "PINOT_E
 PINOT_ERR_TIMEOUT = 6
 DATA_TYPE = {"INT": 0, "LONG": 1, "FLOAT": 2, "DOUBLE": 3, "STRING": 4}
 FILTER_OP = {"AND": 0, "OR": 1, "EQUALITY": 2, "NOT": 3, "RANGE": 4, "IN": 5, "NOT_IN": 6}
+def sv_name(f):
+    """The single-value function a multi-value one shares its intermediate result, merge and final result with
+    (CountMVAggregationFunction extends CountAggregationFunction, ...): "COUNTMV" -> "COUNT"."""
+    f = f.upper()
+    return f[:-2] if f.endswith("MV") and f[:-2] in ("COUNT", "SUM", "MIN", "MAX", "AVG", "DISTINCTCOUNTHLL") else f
+
+
 AGG_FN = {"COUNT": 0, "SUM": 1, "MIN": 2, "MAX": 3, "AVG": 4, "DISTINCTCOUNTHLL": 5,
           "COUNTMV": 6, "SUMMV": 7, "MINMV": 8, "MAXMV": 9, "AVGMV": 10, "DISTINCTCOUNTHLLMV": 11}
 # pinot_pruner bits; the server's default list (DefaultHelixStarterServerConfig.java:60-65)

@@ -26,7 +26,7 @@ import numpy as np
 
 from . import _lib
 from ._hll import cardinality as hll_cardinality
-from ._lib import check
+from ._lib import check, sv_name
 
 INT64_MIN = -(1 << 63)
 EXACT_LIMIT = 1 << 53  # below this an integral double sum is exact in both the reference and here
@@ -51,7 +51,7 @@ def combine_aggregation(query, partial, group=None, device="cpu"):
     import torch
     from .executor import AvgPair, HyperLogLog
     dist = _dist()
-    fns = [a["function"].upper() for a in query["aggregations"]]
+    fns = [sv_name(a["function"]) for a in query["aggregations"]]
     n = len(fns)
     isum = torch.zeros(n, dtype=torch.int64)     # COUNT, and SUM / AVG sums that are exact integers
     dsum = torch.zeros(n, dtype=torch.float64)   # SUM / AVG sums that are not

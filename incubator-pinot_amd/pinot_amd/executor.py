@@ -20,7 +20,7 @@ from dataclasses import dataclass
 import numpy as np
 
 from . import _lib
-from ._lib import check
+from ._lib import check, sv_name
 from .pql import compile_pql
 from .segment import Segment
 
@@ -103,6 +103,10 @@ def segment_desc(seg: Segment):
             keep.append(bbuf)
             d.bloom_filter, d.bloom_filter_len = C.cast(bbuf, C.c_void_p), len(bloom)
         d.create_bloom_filter = int(bool(getattr(col, "create_bloom_filter", False)))
+        if getattr(col, "multi_value", False):
+            d.multi_value = 1
+            d.total_number_of_entries = int(col.total_entries)
+            d.max_number_of_multi_values = int(col.max_multi_values)
         if getattr(col, "partition_function", None):
             fn = col.partition_function.encode()
             keep.append(fn)
@@ -176,7 +180,7 @@ def _empty_result(query):
         return {}
     out = []
     for a in query["aggregations"]:
-        f = a["function"].upper()
+        f = sv_name(a["function"])
         out.append({"COUNT": 0, "SUM": 0.0, "MIN": math.inf, "MAX": -math.inf}.get(f) if f not in (
             "AVG", "DISTINCTCOUNTHLL") else AvgPair(0.0, 0) if f == "AVG" else HyperLogLog(bytes(256), 0))
     return out
@@ -406,7 +410,7 @@ class GroupByResult:
         keys = self.keys()
         cols = []
         for i, a in enumerate(self.query["aggregations"]):
-            f = a["function"].upper()
+            f = sv_name(a["function"])
             if f == "DISTINCTCOUNTHLL":
                 regs, cards = self.hll(i)
                 cols.append([HyperLogLog(regs[g], cards[g]) for g in range(len(keys))])
@@ -530,7 +534,7 @@ class ServerExecutor:
             out = (_lib.AggResult * n)()
             check(lib.pinot_gpu_server_aggregate(self.server.ptr, refs, len(segments), C.byref(m.q), out,
                                                  C.byref(stats)))
-            res = [_agg_value(a["function"].upper(), out[i]) for i, a in enumerate(query["aggregations"])]
+            res = [_agg_value(sv_name(a["function"]), out[i]) for i, a in enumerate(query["aggregations"])]
         return res, _stats(stats)
 
     def _marshal(self, query):
@@ -616,7 +620,7 @@ class ServerQueryExecutor:
             out = (_lib.AggResult * n)()
             check(lib.pinot_gpu_aggregate(self.engine.ptr, handles, len(segments), C.byref(m.q), out,
                                           C.byref(stats)))
-            res = [_agg_value(a["function"].upper(), out[i]) for i, a in enumerate(query["aggregations"])]
+            res = [_agg_value(sv_name(a["function"]), out[i]) for i, a in enumerate(query["aggregations"])]
         return res, _stats(stats)
 
     def process_query_datatable(self, query, segments, trim=True, server=None):
@@ -700,7 +704,7 @@ def _agg_value(f, r):
 # ---------------------------------------------------------------------- results handling
 def final_result(f, v):
     """`AggregationFunction.extractFinalResult`: AVG -> sum/count or -inf (AvgAggregationFunction.java:35,222-230)."""
-    f = f.upper()
+    f = sv_name(f)
     if f == "AVG":
         return v.sum / v.count if v.count else -math.inf
     if f == "DISTINCTCOUNTHLL":
@@ -709,7 +713,7 @@ def final_result(f, v):
 
 
 def merge(f, a, b):
-    f = f.upper()
+    f = sv_name(f)
     if f in ("COUNT", "SUM"):
         return a + b
     if f == "MIN":
@@ -736,7 +740,7 @@ def trim_intermediate_results(query, result, trim_size=None):
         return result
     out = {}
     for i, a in enumerate(query["aggregations"]):
-        f = a["function"].upper()
+        f = sv_name(a["function"])
         items = sorted(result.items(), key=lambda kv: final_result(f, kv[1][i]), reverse=(f != "MIN"))
         for k, v in items[:keep_n]:
             out.setdefault(k, [None] * len(v))[i] = v[i]
@@ -746,7 +750,7 @@ def trim_intermediate_results(query, result, trim_size=None):
 def format_value(f, v):
     """Broker string form (`String.format("%.5f")` for doubles, plain integers otherwise)."""
     v = final_result(f, v)
-    if f.upper() in ("COUNT", "DISTINCTCOUNTHLL"):
+    if sv_name(f) in ("COUNT", "DISTINCTCOUNTHLL"):
         return str(int(v))
     return "%.5f" % v
 
@@ -777,7 +781,7 @@ class BrokerReduce:
 
     @staticmethod
     def reduce(query, server_results):
-        fns = [a["function"].upper() for a in query["aggregations"]]
+        fns = [sv_name(a["function"]) for a in query["aggregations"]]
         if query.get("group_by"):
             # per function (the servers' trimmed maps are per function: None = trimmed there)
             merged = [{} for _ in fns]

@@ -14,7 +14,8 @@ Supported statement: SELECT agg(col|*)[, ...] FROM t [WHERE ...] [GROUP BY c[, .
 """
 import re
 
-AGG_FUNCTIONS = ("COUNT", "SUM", "MIN", "MAX", "AVG", "DISTINCTCOUNTHLL")
+AGG_FUNCTIONS = ("COUNT", "SUM", "MIN", "MAX", "AVG", "DISTINCTCOUNTHLL", "COUNTMV", "SUMMV", "MINMV", "MAXMV", "AVGMV",
+                 "DISTINCTCOUNTHLLMV")
 _TOKEN = re.compile(r"\s*(?:(?P<num>-?\d+\.\d*(?:[eE][-+]?\d+)?|-?\d+(?:[eE][-+]?\d+)?)|"
                     r"(?P<str>'(?:[^']|'')*'|\"(?:[^\"]|\"\")*\")|"
                     r"(?P<op><>|!=|<=|>=|=|<|>|\(|\)|,|\*)|(?P<id>[A-Za-z_][A-Za-z0-9_.$]*))")

@@ -155,6 +155,10 @@ class Column:
     partition_function: Optional[str] = None  # column.<c>.partitionFunction (Modulo / Murmur / ByteArray / HashCode)
     num_partitions: int = 0
     partitions: Optional[list] = None     # partitionValues; None with a function: every dictionary value's partition
+    multi_value: bool = False             # isSingleValues = false: fwd is a FixedBitMultiValueWriter file
+    total_entries: int = 0                # totalNumberOfEntries (MV)
+    max_multi_values: int = 0             # maxNumberOfMultiValues (MV)
+    _mv_offsets: Optional[np.ndarray] = field(default=None, repr=False)  # [numDocs + 1] row starts (MV)
     _raw_values: Optional[np.ndarray] = field(default=None, repr=False)
     _dict_values: Optional[np.ndarray] = field(default=None, repr=False)
     _dict_ids: Optional[np.ndarray] = field(default=None, repr=False)
@@ -208,6 +212,63 @@ def _sorted_unique(values, data_type):
                                     "DOUBLE": np.float64}[data_type])
     uniq, ids = np.unique(arr, return_inverse=True)
     return uniq, ids.astype(np.int32)
+
+
+def multi_value_fwd(ids: np.ndarray, offsets: np.ndarray, bits: int) -> bytes:
+    """`FixedBitMultiValueWriter` file (PC/io/writer/impl/v1/FixedBitMultiValueWriter.java:61-155): CHUNK OFFSETS (BE
+    int per chunk of docsPerChunk = (int) ceil(2048 / (float) (totalNumValues / numDocs)) rows: the chunk's first
+    entry), BITSET (bit e set, MSB first, when entry e starts a row: setIntArray's customBitSet.setBit), RAW DATA (the
+    entries' dictIds, FixedBitIntReaderWriter at `bits`)."""
+    rows = offsets.shape[0] - 1
+    total = int(offsets[-1])
+    if rows == 0:
+        return b""
+    avg = np.float32(total // rows)
+    per_chunk = int(np.ceil(np.float32(2048) / avg))
+    num_chunks = (rows + per_chunk - 1) // per_chunk
+    chunk_offsets = offsets[0:rows:per_chunk][:num_chunks].astype(">i4").tobytes()
+    starts = np.zeros(total, dtype=np.uint8)
+    starts[offsets[:-1][offsets[:-1] < total]] = 1
+    bitset = np.packbits(starts, bitorder="big").tobytes()
+    return chunk_offsets + bitset + pack_fixed_bit(ids, bits)
+
+
+def build_mv_column(name, rows, data_type, bits=None, inverted=False) -> Column:
+    """A dictionary-encoded multi-value column (`SegmentColumnarIndexCreator.indexRow` with `indexOfMV`): the
+    dictionary over every entry, each row's dictIds in row order. rows: one non-empty list of values per doc."""
+    if any(len(r) == 0 for r in rows):
+        raise ValueError("every multi-value row holds at least one value (nulls become the default value)")
+    lens = np.array([len(r) for r in rows], dtype=np.int64)
+    offsets = np.zeros(len(rows) + 1, dtype=np.int64)
+    np.cumsum(lens, out=offsets[1:])
+    flat = [v for r in rows for v in r]
+    uniq, ids = _sorted_unique(flat, data_type)
+    card = len(uniq)
+    min_bits = num_bits_per_value(card - 1)
+    bits = min_bits if bits is None else bits
+    if not min_bits <= bits <= 32:
+        raise ValueError("bits %d outside [%d, 32]" % (bits, min_bits))
+    dbytes, width = _dictionary_bytes(uniq, data_type)
+    col = Column(name=name, data_type=data_type, cardinality=card, bits=bits, is_sorted=False,
+                 has_inverted_index=bool(inverted), num_docs=len(rows), dictionary=dbytes, string_width=width,
+                 multi_value=True, total_entries=int(offsets[-1]), max_multi_values=int(lens.max(initial=0)))
+    col._dict_ids = ids
+    col._mv_offsets = offsets
+    col.fwd = multi_value_fwd(ids, offsets, bits)
+    if inverted:  # MV inverted index: per dictId the docs holding it (OffHeapBitmapInvertedIndexCreator.add(int[]))
+        doc_of = np.repeat(np.arange(len(rows), dtype=np.int64), lens)
+        pairs = np.unique(np.stack([ids.astype(np.int64), doc_of], axis=1), axis=0) if len(flat) else \
+            np.zeros((0, 2), dtype=np.int64)
+        bounds = np.searchsorted(pairs[:, 0], np.arange(card + 1))
+        blobs = [roaring_serialize(pairs[bounds[i]:bounds[i + 1], 1]) for i in range(card)]
+        hdr = np.zeros(card + 1, dtype=">i4")
+        pos = (card + 1) * 4
+        hdr[0] = pos
+        for i, b in enumerate(blobs):
+            pos += len(b)
+            hdr[i + 1] = pos
+        col.inverted = hdr.tobytes() + b"".join(blobs)
+    return col
 
 
 def build_column(name, values, data_type, inverted=False, allow_sorted=True, bits=None, raw=False) -> Column:
@@ -266,17 +327,22 @@ def _metadata_string(v, data_type):
 
 
 def build_segment(name, columns: Dict[str, tuple], inverted_columns=(), num_docs=None, bits=None,
-                  allow_sorted=True, raw_columns=(), min_max=(), bloom_columns=(), partitions=None) -> Segment:
+                  allow_sorted=True, raw_columns=(), min_max=(), bloom_columns=(), partitions=None,
+                  mv_columns=()) -> Segment:
     """columns: {name: (data_type, values)} in schema order; bits: optional {name: bitsPerElement};
     raw_columns: names written without a dictionary; min_max: names given minValue / maxValue metadata (the sorted
     values' ends, as ColumnMinMaxValueGenerator writes them), min_max=True: every column; bloom_columns: names given a
     bloom filter (built at registration from the dictionary, as the loader's BloomFilterHandler does); partitions:
-    {name: (function, numPartitions)} partition metadata (the partitions of the column's values)."""
+    {name: (function, numPartitions)} partition metadata (the partitions of the column's values); mv_columns: names
+    whose values are per-doc lists (multi-value columns)."""
     cols = {}
     n = None
     for cname, (dt, vals) in columns.items():
-        col = build_column(cname, vals, dt, inverted=cname in inverted_columns, allow_sorted=allow_sorted,
-                           bits=(bits or {}).get(cname), raw=cname in raw_columns)
+        if cname in mv_columns:
+            col = build_mv_column(cname, vals, dt, bits=(bits or {}).get(cname), inverted=cname in inverted_columns)
+        else:
+            col = build_column(cname, vals, dt, inverted=cname in inverted_columns, allow_sorted=allow_sorted,
+                               bits=(bits or {}).get(cname), raw=cname in raw_columns)
         if n is None:
             n = col.num_docs
         elif n != col.num_docs:

@@ -91,6 +91,51 @@ def dict_ids(col) -> np.ndarray:
     return read_all(col.fwd, col.num_docs, col.bits)
 
 
+def sv(f):
+    """The single-value function a multi-value one shares intermediate result, merge and final result with
+    (CountMVAggregationFunction extends CountAggregationFunction, ...): "COUNTMV" -> "COUNT"."""
+    f = f.upper()
+    return f[:-2] if f.endswith("MV") and f[:-2] in ("COUNT", "SUM", "MIN", "MAX", "AVG", "DISTINCTCOUNTHLL") else f
+
+
+def is_mv(col):
+    return bool(getattr(col, "multi_value", False))
+
+
+def mv_rows(col):
+    """`FixedBitMultiValueReader` (PC/io/reader/impl/v1/FixedBitMultiValueReader.java:60-119) over the whole file:
+    CHUNK OFFSETS (BE int per chunk of rowsPerChunk = (int) ceil(2048 / (float) (totalNumValues / numRows)) rows),
+    BITMAP (entry e starts a row when its bit, MSB first, is set), RAW DATA (dictIds at bitsPerElement).
+    Returns (row starts int64[numDocs + 1], entries int64[totalNumValues])."""
+    n, total, bits = col.num_docs, int(col.total_entries), col.bits
+    if n == 0:
+        return np.zeros(1, dtype=np.int64), np.zeros(0, dtype=np.int64)
+    per_chunk = int(math.ceil(np.float32(2048) / np.float32(total // n)))
+    num_chunks = (n + per_chunk - 1) // per_chunk
+    hdr, bitmap_size = 4 * num_chunks, (total + 7) // 8
+    buf = bytes(col.fwd)
+    chunk_offsets = np.frombuffer(buf[:hdr], dtype=">i4").astype(np.int64)
+    marks = np.unpackbits(np.frombuffer(buf[hdr:hdr + bitmap_size], dtype=np.uint8), bitorder="big")[:total]
+    starts = np.nonzero(marks)[0].astype(np.int64)
+    if starts.shape[0] != n or (n and starts[0] != 0):
+        raise ValueError("multi-value bitmap does not mark one start per row")
+    if not np.array_equal(chunk_offsets, starts[::per_chunk]):
+        raise ValueError("chunk offsets disagree with the bitmap")
+    entries = read_all(buf[hdr + bitmap_size:], total, bits)
+    return np.append(starts, total), entries
+
+
+def entry_ids(col, docs):
+    """dictIds of every entry of the given docs, doc by doc (getIntArray per doc), and each doc's entry count.
+    Single-value columns: one entry per doc."""
+    if not is_mv(col):
+        return dict_ids(col)[docs], np.ones(docs.shape[0], dtype=np.int64)
+    off, ent = mv_rows(col)
+    lens = off[docs + 1] - off[docs]
+    idx = np.repeat(off[docs], lens) + (np.arange(int(lens.sum())) - np.repeat(np.cumsum(lens) - lens, lens))
+    return ent[idx], lens
+
+
 def roaring_deserialize(blob: bytes) -> np.ndarray:
     """Portable RoaringBitmap reader (RoaringBitmap 0.8.0 format spec; array, bitmap and run containers).
 
@@ -296,6 +341,8 @@ def filter_mask(segment, tree):
         return np.zeros(n, dtype=bool)
     if ev.always_true:
         return np.ones(n, dtype=bool)
+    if is_mv(col):
+        return _mv_leaf_mask(ev, col)
     ids = dict_ids(col)
     mask = ev.matching[ids]
     if col.is_sorted and ev.kind != "RANGE":
@@ -315,6 +362,28 @@ def filter_mask(segment, tree):
         if exclusive:
             alt = ~alt
         assert (alt == mask).all(), "inverted-index path disagrees with scan"
+    return mask
+
+
+def _mv_leaf_mask(ev, col):
+    """`MVScanDocIdIterator` + `BaseDictionaryBasedPredicateEvaluator.applyMV` (:104-121): a doc matches when any
+    entry matches, or for an exclusive predicate (NOT / NOT_IN) when every entry does; cross-checked against the
+    bitmap inverted index (per dictId the docs holding it) when the column has one."""
+    off, ent = mv_rows(col)
+    m = ev.matching[ent]
+    exclusive = ev.kind in ("NEQ", "NOT_IN")
+    starts = off[:-1]
+    if starts.shape[0] == 0:
+        return np.zeros(0, dtype=bool)
+    mask = (np.logical_and if exclusive else np.logical_or).reduceat(m, starts)
+    if col.has_inverted_index and col.inverted is not None:
+        alt = np.zeros(col.num_docs, dtype=bool)
+        sel = ~ev.matching if exclusive else ev.matching
+        for i in np.nonzero(sel)[0]:
+            alt[inverted_doc_ids(col, int(i))] = True
+        if exclusive:
+            alt = ~alt
+        assert (alt == mask).all(), "inverted-index path disagrees with the MV scan"
     return mask
 
 
@@ -390,8 +459,13 @@ def aggregate_segment(segment, query, mask):
             out.append(int(docs.shape[0]))
             continue
         col = segment.column(agg["column"])
-        ids = dict_ids(col)[docs]
-        if f == "SUM":
+        if is_mv(col) != (f != sv(f)):
+            raise ValueError("%s over a %s-value column" % (f, "multi" if is_mv(col) else "single"))
+        ids = entry_ids(col, docs)[0]  # *MVAggregationFunction.aggregate: every entry of every doc, doc order
+        f = sv(f)
+        if f == "COUNT":  # CountMV: the entries
+            out.append(int(ids.shape[0]))
+        elif f == "SUM":
             out.append(_seq_sum(_values_double(col, ids)))
         elif f == "MIN":
             v = _values_double(col, ids)
@@ -420,7 +494,7 @@ def _value_hashes(col):
 
 def merge_agg(f, a, b):
     """`AggregationFunction.merge` per function, as used by `CombineService.mergeTwoBlocks` (:48-90)."""
-    f = f.upper()
+    f = sv(f)
     if f == "COUNT":
         return a + b
     if f == "SUM":
@@ -441,7 +515,7 @@ def merge_agg(f, a, b):
 
 def final_result(f, v):
     """`extractFinalResult`: AVG = sum/count or -inf when count==0 (AvgAggregationFunction.java:35,222-230)."""
-    f = f.upper()
+    f = sv(f)
     if f == "AVG":
         s, c = v
         return s / c if c else -math.inf
@@ -453,7 +527,7 @@ def final_result(f, v):
 def format_result(f, v):
     """Broker-side string form of a final result (KAT strings such as "129268741751388.00000")."""
     v = final_result(f, v)
-    if f.upper() in ("COUNT", "DISTINCTCOUNTHLL"):
+    if sv(f) in ("COUNT", "DISTINCTCOUNTHLL"):
         return str(int(v))
     return "%.5f" % v
 
@@ -471,6 +545,9 @@ def group_by_segment(segment, query, mask, num_groups_limit=100000, array_thresh
     Returns {string_key: [intermediate result per function]}.
     """
     gcols = [segment.column(c) for c in query["group_by"]["columns"]]
+    if any(is_mv(c) for c in gcols) or any(sv(a["function"]) != a["function"].upper()
+                                           for a in query["aggregations"]):
+        return _group_by_segment_mv(segment, query, mask, gcols, num_groups_limit)
     docs = np.nonzero(mask)[0]
     cards = [_card(c) for c in gcols]
     raw = np.zeros(docs.shape[0], dtype=object if _prod(cards) > 2 ** 62 else np.int64)
@@ -531,6 +608,79 @@ def group_by_segment(segment, query, mask, num_groups_limit=100000, array_thresh
                 h.offer_hashes(_value_hashes(col)[gi])
                 vals.append(h)
         result[skey] = vals
+    return result
+
+
+def _group_by_segment_mv(segment, query, mask, gcols, num_groups_limit):
+    """Group-by with multi-value group columns or MV functions (`DictionaryBasedGroupKeyGenerator`'s MV branch,
+    :213-240 / getGroupKeys: a doc's keys are the cartesian product of its group columns' entries, duplicates
+    included; `aggregateGroupByMV`: each key of the doc takes COUNT + 1 and every entry of the function's column).
+    Only key spaces within num.groups.limit (no group is dropped, so first-appearance order does not matter)."""
+    cards = [_card(c) for c in gcols]
+    if _prod(cards) > num_groups_limit:
+        raise NotImplementedError("multi-value group-by beyond num.groups.limit")
+    docs = np.nonzero(mask)[0]
+    rows = []
+    for c in gcols:
+        ids, lens = entry_ids(c, docs)
+        starts = np.cumsum(lens) - lens
+        rows.append((ids, starts, lens))
+    fn_rows = []
+    for a in query["aggregations"]:
+        f = a["function"].upper()
+        if f == "COUNT":
+            fn_rows.append(None)
+            continue
+        col = segment.column(a["column"])
+        if is_mv(col) != (f != sv(f)):
+            raise ValueError("%s over a %s-value column" % (f, "multi" if is_mv(col) else "single"))
+        ids, lens = entry_ids(col, docs)
+        fn_rows.append((col, ids, np.cumsum(lens) - lens, lens))
+    per_key = {}  # raw key -> [doc count, [entry ids per function]]
+    for di in range(docs.shape[0]):
+        keys = [0]
+        for j in range(len(gcols) - 1, -1, -1):
+            ids, st, ln = rows[j]
+            vals = ids[st[di]:st[di] + ln[di]].tolist()
+            keys = [k * cards[j] + v for k in keys for v in vals]
+        for k in keys:
+            slot = per_key.setdefault(k, [0, [[] for _ in fn_rows]])
+            slot[0] += 1
+            for i, fr in enumerate(fn_rows):
+                if fr is not None:
+                    _, ids, st, ln = fr
+                    slot[1][i].extend(ids[st[di]:st[di] + ln[di]].tolist())
+    dvals = [[c.dict_values()[i] for i in range(_card(c))] for c in gcols]
+    result = {}
+    for key in sorted(per_key):
+        cnt, lists = per_key[key]
+        parts, k = [], key
+        for j, c in enumerate(gcols):
+            parts.append(_string_value(c, dvals[j][k % cards[j]]))
+            k //= cards[j]
+        vals = []
+        for a, fr, lst in zip(query["aggregations"], fn_rows, lists):
+            f = sv(a["function"])
+            if fr is None:
+                vals.append(int(cnt))
+                continue
+            col = fr[0]
+            gi = np.asarray(lst, dtype=np.int64)
+            if f == "COUNT":
+                vals.append(int(gi.shape[0]))
+            elif f == "SUM":
+                vals.append(_seq_sum(_values_double(col, gi)))
+            elif f == "MIN":
+                vals.append(float(_values_double(col, gi).min()))
+            elif f == "MAX":
+                vals.append(float(_values_double(col, gi).max()))
+            elif f == "AVG":
+                vals.append((_seq_sum(_values_double(col, gi)), int(gi.shape[0])))
+            else:
+                h = HyperLogLog()
+                h.offer_hashes(_value_hashes(col)[gi])
+                vals.append(h)
+        result["\t".join(parts)] = vals
     return result
 
 
@@ -650,7 +800,7 @@ def combine_group_by(query, per_segment, num_groups_limit=100000):
     New groups are admitted while the merged map holds < 2 * limit groups (`:61,147`). The reference merges
     segments concurrently, so which groups pass that cap is nondeterministic; the oracle merges in segment order.
     """
-    fns = [a["function"].upper() for a in query["aggregations"]]
+    fns = [sv(a["function"]) for a in query["aggregations"]]
     inter_limit = 2 * num_groups_limit
     merged = {}
     for seg in per_segment:
@@ -702,7 +852,7 @@ def execute_group_by_arrays(segments, query, num_groups_limit=100000, array_thre
     segments' dictionaries, raw = sum_j gid_j * prod_{k<j} gcard_k (column 0 least significant).
     Returns dict(keys=int64[n] ascending, gcard, gvalues, scanned, fns=[dict(count, sum|min|max, hll, card)])."""
     gnames = query["group_by"]["columns"]
-    fns = [a["function"].upper() for a in query["aggregations"]]
+    fns = [sv(a["function"]) for a in query["aggregations"]]
     gvalues, remaps, gcard = [], [], []
     for name in gnames:
         vals, rm = _union_dictionary([s.column(name) for s in segments])
@@ -804,7 +954,7 @@ def _copy(f, v):
 def top_groups(query, merged, fn_index, top_n=None):
     """Broker top-N for one function (`BrokerReduceService` / `AggregationGroupByTrimmingService.java:160-176`):
     MIN ascending, everything else descending, ties broken arbitrarily. Returns [(key, final_value)]."""
-    f = query["aggregations"][fn_index]["function"].upper()
+    f = sv(query["aggregations"][fn_index]["function"])
     if top_n is None:
         top_n = query["group_by"].get("top_n", 10)
     items = [(k, final_result(f, v[fn_index])) for k, v in merged.items()]
@@ -827,7 +977,7 @@ def execute_server(segments, query, num_groups_limit=100000):
     """Server-side combine over segments (`CombineOperator` / `CombineGroupByOperator`)."""
     results = [execute_segment(s, query, num_groups_limit) for s in segments]
     scanned = sum(r[1] for r in results)
-    fns = [a["function"].upper() for a in query["aggregations"]]
+    fns = [sv(a["function"]) for a in query["aggregations"]]
     if query.get("group_by"):
         return combine_group_by(query, [r[0] for r in results], num_groups_limit), scanned
     acc = None
@@ -838,7 +988,7 @@ def execute_server(segments, query, num_groups_limit=100000):
 
 def broker_results(query, server_results):
     """Broker reduce of several server responses; returns the KAT strings (aggregation value or top-group value)."""
-    fns = [a["function"].upper() for a in query["aggregations"]]
+    fns = [sv(a["function"]) for a in query["aggregations"]]
     if query.get("group_by"):
         merged = {}
         for r in server_results:

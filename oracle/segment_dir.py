@@ -6,7 +6,7 @@ reference's loader reads for single-value dictionary columns (PC = pinot-core/sr
   metadata.properties keys: V1Constants.MetadataKeys (PC/segment/creator/impl/V1Constants.java:81-146), read as
   SegmentMetadataImpl.init / ColumnMetadata.fromPropertiesConfiguration do (padding: segment.padding.character,
   unescapeJava, default the legacy '%': PC/segment/index/ColumnMetadata.java:111-115)
-  v1: <col>.dict / <col>.sv.unsorted.fwd / <col>.sv.sorted.fwd / <col>.bitmap.inv (FilePerIndexDirectory.java:148-168)
+  v1: <col>.dict / <col>.sv.unsorted.fwd / <col>.sv.sorted.fwd / <col>.mv.fwd / <col>.bitmap.inv (FilePerIndexDirectory.java:148-168)
   v3: columns.psf + index_map, 8-byte magic 0xdeadbeefdeafbead at each entry (SingleFileIndexDirectory.java:62-320)
 Returns pinot_amd.segment.Segment objects (the data model the oracle's query functions take).
 """
@@ -134,11 +134,12 @@ def read_segment_dir(index_dir):
     for c in names:
         k = "column.%s." % c
         dt = _unescape(props[k + "dataType"]).upper()
-        if dt not in ("INT", "LONG", "FLOAT", "DOUBLE", "STRING") or not _bool(props, k + "isSingleValues", True) \
-                or not _bool(props, k + "hasDictionary", True):
+        if dt not in ("INT", "LONG", "FLOAT", "DOUBLE", "STRING") or not _bool(props, k + "hasDictionary", True):
             continue
-        is_sorted = _bool(props, k + "isSorted")
-        fwd = index_bytes(c, "forward_index", c + (".sv.sorted.fwd" if is_sorted else ".sv.unsorted.fwd"))
+        mv = not _bool(props, k + "isSingleValues", True)
+        is_sorted = _bool(props, k + "isSorted") and not mv
+        fwd = index_bytes(c, "forward_index", c + (".mv.fwd" if mv else ".sv.sorted.fwd" if is_sorted
+                                                   else ".sv.unsorted.fwd"))
         inv = None if is_sorted or not _bool(props, k + "hasInvertedIndex") else \
             index_bytes(c, "inverted_index", c + ".bitmap.inv")
         col = Column(name=c, data_type=dt, cardinality=int(props[k + "cardinality"]),
@@ -148,5 +149,9 @@ def read_segment_dir(index_dir):
                      string_width=int(props.get(k + "lengthOfEachEntry", "0")),
                      fwd=None if is_sorted else fwd, sorted_index=fwd if is_sorted else None, inverted=inv,
                      padding=pad if dt == "STRING" else 0)
+        if mv:  # FixedBitMultiValueReader file (V1Constants.java:61)
+            col.multi_value = True
+            col.total_entries = int(props[k + "totalNumberOfEntries"])
+            col.max_multi_values = int(props.get(k + "maxNumberOfMultiValues", "0"))
         cols[c] = col
     return Segment(name=_unescape(props.get("segment.name", "")), num_docs=n, columns=cols)

@@ -1,6 +1,6 @@
 """Writes Segment objects as Pinot segment directories (test infrastructure).
 
-v1: metadata.properties + <col>.dict, <col>.sv.unsorted.fwd | <col>.sv.sorted.fwd, <col>.bitmap.inv, as
+v1: metadata.properties + <col>.dict, <col>.sv.unsorted.fwd | <col>.sv.sorted.fwd | <col>.mv.fwd, <col>.bitmap.inv, as
 SegmentColumnarIndexCreator leaves them (file names: SegmentMetadataImpl.java:498-527, V1Constants.java:53-63).
 v3: the same buffers in v3/columns.psf, each behind the 8-byte magic marker, located by v3/index_map
 ("<col>.<index>.startOffset = o" / ".size = n", n counting the marker: SingleFileIndexDirectory.java:166-205,320-330).
@@ -35,8 +35,10 @@ def _props(seg, version, padding):
                   k + "hasNullValue = false",
                   k + "hasDictionary = %s" % ("false" if getattr(c, "encoding", "dictionary") == "raw" else "true"),
                   k + "hasInvertedIndex = %s" % ("true" if c.inverted is not None else "false"),
-                  k + "isSingleValues = true", k + "maxNumberOfMultiValues = 0",
-                  k + "totalNumberOfEntries = %d" % seg.num_docs]
+                  k + "isSingleValues = %s" % ("false" if getattr(c, "multi_value", False) else "true"),
+                  k + "maxNumberOfMultiValues = %d" % getattr(c, "max_multi_values", 0),
+                  k + "totalNumberOfEntries = %d" % (c.total_entries if getattr(c, "multi_value", False)
+                                                      else seg.num_docs)]
         if getattr(c, "min_value", None) is not None:
             lines += [k + "minValue = %s" % c.min_value, k + "maxValue = %s" % c.max_value]
         if getattr(c, "partition_function", None):
@@ -151,7 +153,11 @@ def _buffers(c):
     bloom = _bloom_bytes(c)
     if bloom is not None:
         yield "bloom_filter", c.name + ".bloom", bloom
-    if c.is_sorted:
+    if getattr(c, "multi_value", False):
+        yield "forward_index", c.name + ".mv.fwd", c.fwd
+        if c.inverted is not None:
+            yield "inverted_index", c.name + ".bitmap.inv", c.inverted
+    elif c.is_sorted:
         yield "forward_index", c.name + ".sv.sorted.fwd", c.sorted_index
     else:
         yield "forward_index", c.name + ".sv.unsorted.fwd", c.fwd

@@ -138,7 +138,9 @@ def test_not_a_directory(tmp_path):
 def test_unserved_columns_are_left_out(tmp_path):
     d = write_segment_dir(_random_segment(7), str(tmp_path / "s"))
     p = os.path.join(d, "metadata.properties")
-    text = open(p).read().replace("column.l.isSingleValues = true", "column.l.isSingleValues = false")
+    # a raw (no-dictionary) multi-value column: not served, left out
+    text = open(p).read().replace("column.l.isSingleValues = true", "column.l.isSingleValues = false").replace(
+        "column.l.hasDictionary = true", "column.l.hasDictionary = false")
     open(p, "w").write(text)
     n, cols, skipped = segment_dir_info(d)
     assert (cols, skipped) == (4, 1)

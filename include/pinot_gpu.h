@@ -64,7 +64,8 @@ typedef enum {
  * dictionary and every doc's dictId is fixed-bit packed, so the device path reads one format. Predicates, MIN / MAX
  * and SUM give the reference's raw-value results (RawValueBased*PredicateEvaluator) except for signed zeros and NaN
  * in FLOAT / DOUBLE columns, which a dictionary keeps apart / orders last. The dictionary-based MIN / MAX plan is
- * not used for them (InstancePlanMakerImplV2 requires a dictionary). Raw STRING (var-byte) columns: unsupported. */
+ * not used for them (InstancePlanMakerImplV2 requires a dictionary). Raw STRING (var-byte) columns are transcoded to
+ * a dictionary sorted in UTF-8 byte order (String.compareTo's order for text without supplementary characters). */
 typedef enum { PINOT_ENCODING_DICTIONARY = 0, PINOT_ENCODING_RAW = 1 } pinot_column_encoding;
 
 /* One single-value dictionary-encoded column, exactly as the segment files hold it
@@ -84,8 +85,11 @@ typedef struct {
   int32_t encoding;            /* PINOT_ENCODING_DICTIONARY (0) or PINOT_ENCODING_RAW (1): a no-dictionary column
                                   (PhysicalColumnIndexContainer.java:101-106); forward_index then holds the N values
                                   themselves, BE fixed width (INT / FLOAT 4 bytes, LONG / DOUBLE 8), as the
-                                  decompressed chunks of FixedByteChunkSingleValueReader hold them; cardinality,
-                                  bits_per_value, dictionary and the indexes are ignored (0 / NULL). */
+                                  decompressed chunks of FixedByteChunkSingleValueReader hold them; STRING: N + 1
+                                  BE int32 offsets then the UTF-8 bytes (value i = bytes [off[i], off[i+1]), offsets
+                                  counted from the first byte after the offsets; what VarByteChunkSingleValueReader
+                                  .getBytes returns per doc); cardinality, bits_per_value, dictionary and the
+                                  indexes are ignored (0 / NULL). */
   const uint8_t *dictionary;   uint64_t dictionary_len;     /* card * width BE values */
   const uint8_t *forward_index; uint64_t forward_index_len; /* ceil(N*b/8) bytes, MSB-first */
   const uint8_t *sorted_index; uint64_t sorted_index_len;   /* 2*card BE int32 [start,end] */
@@ -233,8 +237,9 @@ pinot_status pinot_gpu_segment_release(pinot_engine *engine, pinot_segment_handl
  * metadata.properties (SegmentMetadataImpl / ColumnMetadata; V1Constants.java:54-146). The files are memory-mapped,
  * checked like pinot_gpu_segment_register's descriptors and copied to HBM. Raw (no-dictionary) INT / LONG / FLOAT /
  * DOUBLE columns are read from their chunked .sv.raw.fwd index (PASS_THROUGH or Snappy chunks,
- * BaseChunkSingleValueReader.java:57-147) and registered as PINOT_ENCODING_RAW. Multi-value, raw STRING and BYTES
- * columns are not served and are left out. */
+ * BaseChunkSingleValueReader.java:57-147), raw STRING columns from their var-byte chunks (.sv.raw.fwd,
+ * VarByteChunkSingleValueReader.java:40-115), and registered as PINOT_ENCODING_RAW; multi-value dictionary columns
+ * from <col>.mv.fwd (FixedBitMultiValueReader). Raw multi-value and BYTES columns are not served and are left out. */
 pinot_status pinot_gpu_segment_load(pinot_engine *engine, const char *index_dir, pinot_segment_handle *out);
 /* The same read and checks on the host only (no engine, no GPU): docs, served columns, left-out columns. */
 pinot_status pinot_gpu_segment_dir_info(const char *index_dir, int32_t *num_docs, int32_t *num_columns,

@@ -443,12 +443,94 @@ void parse_pruning_metadata(ColumnData &c, const pinot_column_desc &d) {
 // dictionary form the device path reads: the distinct values sorted as the segment creator sorts a dictionary
 // (Arrays.sort on the primitives: Integer / Long order, Float / Double.compare order), each doc's dictId packed at
 // getNumBitsPerValue(card - 1) bits, MSB first (FixedBitIntReaderWriter).
+namespace {
+
+void pack_ids(const std::vector<uint32_t> &ids, int bits, std::vector<uint8_t> &fwd) {
+  fwd.assign((size_t)((ids.size() * (uint64_t)bits + 7) / 8), 0);
+  for (size_t i = 0; i < ids.size(); i++) {
+    const uint64_t bit0 = i * (uint64_t)bits;
+    for (int b = 0; b < bits; b++)
+      if ((ids[i] >> (bits - 1 - b)) & 1u) {
+        const uint64_t pos = bit0 + b;
+        fwd[pos >> 3] |= (uint8_t)(0x80u >> (pos & 7));
+      }
+  }
+}
+
+void finish_transcoded(const pinot_column_desc &d, TranscodedColumn &out) {
+  out.desc.name = d.name;
+  out.desc.data_type = d.data_type;
+  out.desc.encoding = PINOT_ENCODING_DICTIONARY;
+  out.desc.dictionary = out.dictionary.data();
+  out.desc.dictionary_len = out.dictionary.size();
+  out.desc.forward_index = out.forward_index.data();
+  out.desc.forward_index_len = out.forward_index.size();
+  out.desc.min_value = d.min_value;
+  out.desc.max_value = d.max_value;
+  out.desc.num_partitions = d.num_partitions;
+  out.desc.partition_function = d.partition_function;
+  out.desc.partition_values = d.partition_values;
+  out.desc.num_partition_values = d.num_partition_values;
+}
+
+// A raw STRING column (VarByteChunkSingleValueReader.getString per doc, given flat: N + 1 BE offsets then bytes) as
+// a dictionary column: the distinct values sorted in byte order (== code-point order, the order the dictionary
+// predicate evaluators binary-search in), zero-padded to the longest; the raw-value evaluators' equals / compareTo
+// on the values then give the same docs as the dictionary evaluators on the ids. A value holding a NUL byte would
+// end at the padding: rejected.
+bool transcode_raw_string(const pinot_column_desc &d, int32_t num_docs, TranscodedColumn &out) {
+  const std::string name = d.name ? d.name : "";
+  const uint64_t n = (uint64_t)std::max(num_docs, 0);
+  const uint64_t hdr = (n + 1) * 4;
+  require(d.forward_index && d.forward_index_len >= hdr, PINOT_ERR_BAD_ARG,
+          name + ": raw STRING forward index shorter than its numDocs + 1 offsets");
+  const uint8_t *data = d.forward_index + hdr;
+  const uint64_t data_len = d.forward_index_len - hdr;
+  std::vector<std::string> vals(n);
+  uint64_t prev = load_be32(d.forward_index);
+  require(prev == 0, PINOT_ERR_BAD_ARG, name + ": raw STRING offsets must start at 0");
+  for (uint64_t i = 0; i < n; i++) {
+    const uint64_t e = load_be32(d.forward_index + 4 * (i + 1));
+    require(e >= prev && e <= data_len, PINOT_ERR_BAD_ARG, name + ": raw STRING offsets not ascending within the bytes");
+    vals[i].assign(reinterpret_cast<const char *>(data + prev), e - prev);
+    require(vals[i].find('\0') == std::string::npos, PINOT_ERR_UNSUPPORTED,
+            name + ": raw STRING value with a NUL byte (the dictionary's padding byte)");
+    prev = e;
+  }
+  std::vector<std::string> uniq = vals;
+  std::sort(uniq.begin(), uniq.end());
+  uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
+  require(uniq.size() < (1ull << 31), PINOT_ERR_UNSUPPORTED, name + ": more than 2^31 distinct values");
+  size_t width = 0;
+  for (const auto &u : uniq) width = std::max(width, u.size());
+  require(width < (size_t)INT32_MAX, PINOT_ERR_UNSUPPORTED, name + ": value too long");
+  const int64_t card = (int64_t)uniq.size();
+  out.dictionary.assign((size_t)card * width, 0);
+  for (int64_t j = 0; j < card; j++) memcpy(out.dictionary.data() + (size_t)j * width, uniq[j].data(), uniq[j].size());
+  std::vector<uint32_t> ids(n);
+  for (uint64_t i = 0; i < n; i++) ids[i] = (uint32_t)(std::lower_bound(uniq.begin(), uniq.end(), vals[i]) - uniq.begin());
+  const int bits = num_bits_per_value(std::max<int64_t>(card - 1, 0));
+  pack_ids(ids, bits, out.forward_index);
+  out.desc = pinot_column_desc{};
+  out.desc.cardinality = (int32_t)card;
+  out.desc.bits_per_value = bits;
+  out.desc.string_width = (int32_t)width;
+  out.desc.padding_byte = 0;
+  finish_transcoded(d, out);
+  return true;
+}
+
+}  // namespace
+
 bool transcode_raw(const pinot_column_desc &d, int32_t num_docs, TranscodedColumn &out) {
   if (d.encoding == PINOT_ENCODING_DICTIONARY) return false;
   const std::string name = d.name ? d.name : "";
   require(d.encoding == PINOT_ENCODING_RAW, PINOT_ERR_BAD_ARG, name + ": unknown column encoding");
-  require(d.data_type >= PINOT_INT && d.data_type <= PINOT_DOUBLE, PINOT_ERR_UNSUPPORTED,
-          name + ": raw (var-byte) STRING columns are not served");
+  require(!d.multi_value, PINOT_ERR_UNSUPPORTED, name + ": raw multi-value columns are not served");
+  require(!d.bloom_filter && !d.create_bloom_filter, PINOT_ERR_UNSUPPORTED,
+          name + ": bloom filters are not supported for no-dictionary columns");  // BloomFilterHandler.java:117-118
+  if (d.data_type == PINOT_STRING) return transcode_raw_string(d, num_docs, out);
+  require(d.data_type >= PINOT_INT && d.data_type <= PINOT_DOUBLE, PINOT_ERR_BAD_ARG, name + ": data type");
   const int w = (d.data_type == PINOT_INT || d.data_type == PINOT_FLOAT) ? 4 : 8;
   const uint64_t n = (uint64_t)std::max(num_docs, 0);
   require(d.forward_index && d.forward_index_len >= n * (uint64_t)w, PINOT_ERR_BAD_ARG,
@@ -492,36 +574,13 @@ bool transcode_raw(const pinot_column_desc &d, int32_t num_docs, TranscodedColum
     }
     for (int b = 0; b < w; b++) out.dictionary[(size_t)j * w + b] = (uint8_t)(v >> (8 * (w - 1 - b)));
   }
-  out.forward_index.assign((size_t)((n * (uint64_t)bits + 7) / 8), 0);
-  for (uint64_t i = 0; i < n; i++) {
-    const uint64_t id = (uint64_t)(std::lower_bound(uniq.begin(), uniq.end(), keys[i]) - uniq.begin());
-    const uint64_t bit0 = i * (uint64_t)bits;
-    for (int b = 0; b < bits; b++) {
-      if ((id >> (bits - 1 - b)) & 1) {
-        const uint64_t pos = bit0 + b;
-        out.forward_index[pos >> 3] |= (uint8_t)(0x80u >> (pos & 7));
-      }
-    }
-  }
+  std::vector<uint32_t> ids(n);
+  for (uint64_t i = 0; i < n; i++) ids[i] = (uint32_t)(std::lower_bound(uniq.begin(), uniq.end(), keys[i]) - uniq.begin());
+  pack_ids(ids, bits, out.forward_index);
   out.desc = pinot_column_desc{};
-  out.desc.name = d.name;
-  out.desc.data_type = d.data_type;
   out.desc.cardinality = (int32_t)card;
   out.desc.bits_per_value = bits;
-  out.desc.encoding = PINOT_ENCODING_DICTIONARY;
-  out.desc.dictionary = out.dictionary.data();
-  out.desc.dictionary_len = out.dictionary.size();
-  out.desc.forward_index = out.forward_index.data();
-  out.desc.forward_index_len = out.forward_index.size();
-  out.desc.min_value = d.min_value;
-  out.desc.max_value = d.max_value;
-  // "Bloom filters not supported for no dictionary columns" (BloomFilterHandler.java:117-118)
-  require(!d.bloom_filter && !d.create_bloom_filter, PINOT_ERR_UNSUPPORTED,
-          name + ": bloom filters are not supported for no-dictionary columns");
-  out.desc.num_partitions = d.num_partitions;
-  out.desc.partition_function = d.partition_function;
-  out.desc.partition_values = d.partition_values;
-  out.desc.num_partition_values = d.num_partition_values;
+  finish_transcoded(d, out);
   return true;
 }
 

@@ -320,6 +320,61 @@ std::vector<uint8_t> read_raw_chunks(const uint8_t *b, uint64_t n, int64_t num_d
   return values;
 }
 
+// VarByteChunkSingleValueWriter file (header as read_raw_chunks; each chunk, decompressed, = numDocsPerChunk int
+// offsets from the chunk start, then the values' bytes): per doc the bytes VarByteChunkSingleValueReader.getBytes
+// returns (VarByteChunkSingleValueReader.java:58-115: length = next offset - offset; the chunk's end for its last
+// row or when the next offset is 0, the filler of a partial chunk), flattened as the C-ABI's raw STRING form:
+// numDocs + 1 BE offsets, then the bytes.
+std::vector<uint8_t> read_var_byte_chunks(const uint8_t *b, uint64_t n, int64_t num_docs, const std::string &what) {
+  auto be32 = [&](const uint8_t *p, uint64_t len, uint64_t off) -> int64_t {
+    require(off + 4 <= len, PINOT_ERR_BAD_ARG, what + ": var-byte chunk truncated");
+    return (int32_t)(((uint32_t)p[off] << 24) | ((uint32_t)p[off + 1] << 16) | ((uint32_t)p[off + 2] << 8) | p[off + 3]);
+  };
+  const int64_t version = be32(b, n, 0), num_chunks = be32(b, n, 4), per_chunk = be32(b, n, 8);
+  require(version >= 1 && version <= 2, PINOT_ERR_UNSUPPORTED, what + ": raw forward index version");
+  require(num_chunks >= 0 && per_chunk >= 1 && num_chunks * per_chunk >= num_docs && per_chunk < (1 << 26),
+          PINOT_ERR_BAD_ARG, what + ": var-byte chunk layout does not cover the docs");
+  int64_t compression = 1, header_start = 16;
+  if (version > 1) {
+    compression = be32(b, n, 20);
+    header_start = be32(b, n, 24);
+  }
+  require(compression == 0 || compression == 1, PINOT_ERR_UNSUPPORTED, what + ": chunk compression type");
+  std::vector<uint8_t> offs((size_t)(num_docs + 1) * 4), bytes;
+  auto put_be32 = [&](int64_t i, uint64_t v) {
+    require(v < (1ull << 31), PINOT_ERR_UNSUPPORTED, what + ": raw STRING column over 2 GB");
+    for (int k = 0; k < 4; k++) offs[(size_t)i * 4 + k] = (uint8_t)(v >> (24 - 8 * k));
+  };
+  put_be32(0, 0);
+  int64_t doc = 0;
+  std::vector<uint8_t> chunk;
+  for (int64_t c = 0; c < num_chunks && doc < num_docs; c++) {
+    const int64_t start = be32(b, n, (uint64_t)header_start + 4 * c);
+    const int64_t end = c + 1 < num_chunks ? be32(b, n, (uint64_t)header_start + 4 * (c + 1)) : (int64_t)n;
+    require(start >= header_start + 4 * num_chunks && start <= end && (uint64_t)end <= n, PINOT_ERR_BAD_ARG,
+            what + ": chunk offsets");
+    chunk.clear();
+    if (compression == 0) chunk.assign(b + start, b + end);
+    else snappy_uncompress(b + start, (uint64_t)(end - start), chunk, what);
+    const uint64_t limit = chunk.size();
+    require(limit >= (uint64_t)per_chunk * 4, PINOT_ERR_BAD_ARG, what + ": var-byte chunk shorter than its offsets");
+    for (int64_t r = 0; r < per_chunk && doc < num_docs; r++, doc++) {
+      const int64_t o = be32(chunk.data(), limit, 4 * (uint64_t)r);
+      int64_t e = (int64_t)limit;
+      if (r + 1 < per_chunk) {
+        e = be32(chunk.data(), limit, 4 * (uint64_t)(r + 1));
+        if (e == 0) e = (int64_t)limit;
+      }
+      require(o >= per_chunk * 4 && o <= e && (uint64_t)e <= limit, PINOT_ERR_BAD_ARG, what + ": var-byte row offsets");
+      bytes.insert(bytes.end(), chunk.begin() + o, chunk.begin() + e);
+      put_be32(doc + 1, bytes.size());
+    }
+  }
+  require(doc == num_docs, PINOT_ERR_BAD_ARG, what + ": var-byte chunks hold too few docs");
+  offs.insert(offs.end(), bytes.begin(), bytes.end());
+  return offs;
+}
+
 void read_segment_dir(const std::string &index_dir, SegmentDirData &out) {
   require(is_dir(index_dir), PINOT_ERR_BAD_ARG, "not a segment directory: " + index_dir);
   const std::string v3 = index_dir + "/v3";
@@ -402,7 +457,7 @@ void read_segment_dir(const std::string &index_dir, SegmentDirData &out) {
     const std::string k = "column." + c + ".";
     const int dt = data_type_of(prop(kv, k + "dataType"));
     const bool single = prop_bool(kv, k + "isSingleValues", true), dict = prop_bool(kv, k + "hasDictionary", true);
-    if (dt < 0 || (!single && !dict) || (!dict && dt == PINOT_STRING)) {
+    if (dt < 0 || (!single && !dict)) {
       out.skipped.push_back(c);
       continue;
     }
@@ -444,8 +499,12 @@ void read_segment_dir(const std::string &index_dir, SegmentDirData &out) {
       uint64_t fn = 0;
       require(index_bytes(c, "forward_index", c + ".sv.raw.fwd", &fp, &fn), PINOT_ERR_BAD_ARG,
               c + ": no raw forward index");
-      const int w = (dt == PINOT_INT || dt == PINOT_FLOAT) ? 4 : 8;
-      out.owned.push_back(read_raw_chunks(fp, fn, out.num_docs, w, c));
+      if (dt == PINOT_STRING) {
+        out.owned.push_back(read_var_byte_chunks(fp, fn, out.num_docs, c));
+      } else {
+        const int w = (dt == PINOT_INT || dt == PINOT_FLOAT) ? 4 : 8;
+        out.owned.push_back(read_raw_chunks(fp, fn, out.num_docs, w, c));
+      }
       d.encoding = PINOT_ENCODING_RAW;
       d.forward_index = out.owned.back().data();
       d.forward_index_len = out.owned.back().size();

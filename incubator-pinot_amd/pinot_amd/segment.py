@@ -282,7 +282,18 @@ def build_column(name, values, data_type, inverted=False, allow_sorted=True, bit
         raise ValueError("unsupported data type %s" % data_type)
     if raw:
         if data_type == "STRING":
-            raise ValueError("raw STRING columns are var-byte: not supported")
+            # var-byte values, flat as the C-ABI takes them: numDocs + 1 BE int offsets, then the UTF-8 bytes
+            enc = [str(v).encode("utf-8") for v in values]
+            offs = np.zeros(len(enc) + 1, dtype=np.int64)
+            np.cumsum([len(e) for e in enc], out=offs[1:])
+            uniq, ids = _sorted_unique([str(v) for v in values], data_type)
+            col = Column(name=name, data_type=data_type, cardinality=0, bits=0, is_sorted=False,
+                         has_inverted_index=False, num_docs=len(enc), dictionary=b"", encoding="raw")
+            col.fwd = offs.astype(">i4").tobytes() + b"".join(enc)
+            col._raw_values = np.array([str(v) for v in values], dtype=object)
+            col._dict_values = np.array(uniq, dtype=object)
+            col._dict_ids = ids
+            return col
         vals = np.asarray(values).astype(_BE_DTYPE[data_type].replace(">", "<"))
         uniq, ids = _sorted_unique(vals, data_type)
         col = Column(name=name, data_type=data_type, cardinality=0, bits=0, is_sorted=False, has_inverted_index=False,

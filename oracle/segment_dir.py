@@ -155,3 +155,75 @@ def read_segment_dir(index_dir):
             col.max_multi_values = int(props.get(k + "maxNumberOfMultiValues", "0"))
         cols[c] = col
     return Segment(name=_unescape(props.get("segment.name", "")), num_docs=n, columns=cols)
+
+
+# ---------------------------------------------------------------- raw (var-byte) STRING forward indexes
+def snappy_uncompress(data):
+    """Raw Snappy block (format_description.txt of snappy 1.1: varint length, then literal / copy elements)."""
+    data = bytes(data)
+    n, shift, i = 0, 0, 0
+    while True:
+        b = data[i]
+        i += 1
+        n |= (b & 0x7F) << shift
+        shift += 7
+        if not b & 0x80:
+            break
+    out = bytearray()
+    while i < len(data):
+        tag = data[i]
+        i += 1
+        kind = tag & 3
+        if kind == 0:
+            ln = tag >> 2
+            if ln >= 60:
+                k = ln - 59
+                ln = int.from_bytes(data[i:i + k], "little")
+                i += k
+            ln += 1
+            out += data[i:i + ln]
+            i += ln
+            continue
+        if kind == 1:
+            ln = ((tag >> 2) & 7) + 4
+            off = ((tag >> 5) << 8) | data[i]
+            i += 1
+        elif kind == 2:
+            ln = (tag >> 2) + 1
+            off = int.from_bytes(data[i:i + 2], "little")
+            i += 2
+        else:
+            ln = (tag >> 2) + 1
+            off = int.from_bytes(data[i:i + 4], "little")
+            i += 4
+        if off == 0 or off > len(out):
+            raise ValueError("snappy copy offset")
+        for _ in range(ln):
+            out.append(out[-off])
+    if len(out) != n:
+        raise ValueError("snappy length")
+    return bytes(out)
+
+
+def read_var_byte_strings(buf, num_docs):
+    """VarByteChunkSingleValueReader.getString for docs [0, num_docs) (VarByteChunkSingleValueReader.java:58-115 over
+    BaseChunkSingleValueReader.java:57-147's header: version, numChunks, numDocsPerChunk, lengthOfLongestEntry[,
+    totalDocs, compressionType, dataHeaderStart]; version 1 is Snappy)."""
+    version, num_chunks, per_chunk, _longest = struct.unpack_from(">iiii", buf, 0)
+    comp, header = 1, 16
+    if version > 1:
+        _total, comp, header = struct.unpack_from(">iii", buf, 16)
+    offs = list(struct.unpack_from(">%di" % num_chunks, buf, header)) + [len(buf)]
+    out = []
+    for c in range(num_chunks):
+        if len(out) >= num_docs:
+            break
+        chunk = bytes(buf[offs[c]:offs[c + 1]])
+        chunk = snappy_uncompress(chunk) if comp == 1 else chunk
+        rows = struct.unpack_from(">%di" % per_chunk, chunk, 0)
+        for r in range(per_chunk):
+            if len(out) >= num_docs:
+                break
+            e = rows[r + 1] if r + 1 < per_chunk and rows[r + 1] != 0 else len(chunk)
+            out.append(chunk[rows[r]:e].decode("utf-8"))
+    return out

@@ -5,7 +5,8 @@ SegmentColumnarIndexCreator leaves them (file names: SegmentMetadataImpl.java:49
 v3: the same buffers in v3/columns.psf, each behind the 8-byte magic marker, located by v3/index_map
 ("<col>.<index>.startOffset = o" / ".size = n", n counting the marker: SingleFileIndexDirectory.java:166-205,320-330).
 Raw (no-dictionary) columns: <col>.sv.raw.fwd as FixedByteChunkSingleValueWriter writes it
-(BaseChunkSingleValueWriter.java:62-200: header ints, absolute chunk offsets, PASS_THROUGH or Snappy chunks).
+(BaseChunkSingleValueWriter.java:62-200: header ints, absolute chunk offsets, PASS_THROUGH or Snappy chunks), STRING
+ones as VarByteChunkSingleValueWriter does (per-chunk row offsets, then the bytes).
 Bloom filters: <col>.bloom (v3: index type bloom_filter) as BloomFilterHandler leaves them after a load
 (BloomFilterCreator.java:57-64; bytes from oracle/bloom.py); partition metadata: column.<c>.partitionFunction /
 numPartitions / partitionValues (V1Constants.java:135-137), the values written as "[start end]" ranges.
@@ -143,7 +144,38 @@ def raw_chunk_file(values_be, entry_size, num_docs, docs_per_chunk=1000, compres
     return head + b"".join(struct.pack(">i", o) for o in offs) + b"".join(bodies)
 
 
+def var_byte_chunk_file(values, docs_per_chunk=1000, compression=1, version=2):
+    """VarByteChunkSingleValueWriter bytes (VarByteChunkSingleValueWriter.java:50-117): per chunk numDocsPerChunk BE
+    int row offsets from the chunk start (0 for the unused rows of the last chunk), then the UTF-8 bytes; the chunk
+    written up to its last byte, PASS_THROUGH or Snappy."""
+    enc = [v.encode("utf-8") for v in values]
+    longest = max((len(e) for e in enc), default=0)
+    bodies = []
+    for s in range(0, len(enc), docs_per_chunk):
+        rows = enc[s:s + docs_per_chunk]
+        head = bytearray(4 * docs_per_chunk)
+        off = 4 * docs_per_chunk
+        for i, r in enumerate(rows):
+            head[4 * i:4 * i + 4] = struct.pack(">i", off)
+            off += len(r)
+        raw = bytes(head) + b"".join(rows)
+        bodies.append(snappy_compress(raw) if compression == 1 else raw)
+    head = struct.pack(">iiii", version, len(bodies), docs_per_chunk, longest)
+    if version > 1:
+        head += struct.pack(">iii", len(enc), compression, len(head) + 12)
+    off = len(head) + 4 * len(bodies)
+    offs = []
+    for b in bodies:
+        offs.append(off)
+        off += len(b)
+    return head + b"".join(struct.pack(">i", o) for o in offs) + b"".join(bodies)
+
+
 def _buffers(c):
+    if getattr(c, "encoding", "dictionary") == "raw" and c.data_type == "STRING":
+        yield "forward_index", c.name + ".sv.raw.fwd", getattr(c, "raw_file", None) or var_byte_chunk_file(
+            list(c._raw_values))
+        return
     if getattr(c, "encoding", "dictionary") == "raw":
         w = 4 if c.data_type in ("INT", "FLOAT") else 8
         yield "forward_index", c.name + ".sv.raw.fwd", getattr(c, "raw_file", None) or raw_chunk_file(

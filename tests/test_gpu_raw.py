@@ -10,7 +10,7 @@ from pinot_amd import GpuEngine, ServerQueryExecutor, build_segment, compile_pql
 from test_gpu_parity import _assert_same, _random_aggs, _random_columns, _random_tree
 
 pytestmark = pytest.mark.gpu
-RAW = ("big", "lng", "dbl", "flt", "i0")
+RAW = ("big", "lng", "dbl", "flt", "i0", "s")  # "s": a var-byte STRING column
 
 
 @pytest.fixture(scope="module")
@@ -114,3 +114,23 @@ def test_raw_matches_dictionary_registration(engine):
     assert sb.num_entries_scanned_post_filter == 0 and sa.num_entries_scanned_post_filter == 2 * n
     gr.release()
     gd.release()
+
+
+def test_var_byte_fixture_on_gpu(engine, tmp_path):
+    """The reference's data/varByteStrings.v1 as a raw STRING column's forward index (1009 docs cycling "abcde",
+    "fgh", "ijklmn", "12345"): loaded from a segment directory, grouped, filtered."""
+    import os
+    from segdir_writer import write_segment_dir
+    fixture = open(os.path.join(os.path.dirname(__file__), "golden", "var_byte_strings.v1"), "rb").read()
+    expected = ["abcde", "fgh", "ijklmn", "12345"]
+    vals = [expected[i % 4] for i in range(1009)]
+    seg = build_segment("vb", {"s": ("STRING", np.array(vals, dtype=object)),
+                               "i": ("INT", np.arange(1009, dtype=np.int32))}, raw_columns=("s",))
+    seg.columns["s"].raw_file = fixture
+    g = engine.load(write_segment_dir(seg, str(tmp_path / "vb"), version="v3"))
+    ex = ServerQueryExecutor(engine)
+    got, _ = ex.process_query(compile_pql("SELECT COUNT(*), SUM(i) FROM t GROUP BY s"), [g], trim=False)
+    assert got == {v: [len(range(k, 1009, 4)), float(sum(range(k, 1009, 4)))] for k, v in enumerate(expected)}
+    got, st = ex.process_query(compile_pql("SELECT COUNT(*) FROM t WHERE s BETWEEN 'abcde' AND 'fgh'"), [g])
+    assert got == [505] and st.num_docs_scanned == 505
+    g.release()

@@ -243,11 +243,13 @@ def test_raw_columns_host_checks_and_pruning():
     with pytest.raises(PinotGpuError) as ei:
         validate_segment(short)
     assert ei.value.status == 1
-    s = build_segment("s", {"s": ("STRING", np.array(["x", "y"], dtype=object))})
+    s = build_segment("s", {"s": ("INT", [[1, 2], [3]])}, mv_columns=("s",))  # raw multi-value: not served
     s.columns["s"].encoding = "raw"
     with pytest.raises(PinotGpuError) as ei:
         validate_segment(s)
     assert ei.value.status == 4
+    s = build_segment("s", {"s": ("STRING", np.array(["x", "y"], dtype=object))}, raw_columns=("s",))
+    validate_segment(s)  # raw (var-byte) STRING: transcoded
 
 
 

@@ -14,6 +14,7 @@ import pytest
 
 import pinot_oracle as O
 from pinot_amd import PinotGpuError, build_segment, segment_dir_info
+from pinot_amd.executor import validate_segment
 from segment_dir import read_segment_dir
 from segdir_writer import write_segment_dir
 
@@ -177,3 +178,50 @@ def test_raw_columns_read_from_chunked_forward_indexes(tmp_path):
         with pytest.raises(PinotGpuError) as ei:
             segment_dir_info(write_segment_dir(seg, str(tmp_path / ("bad%d" % bad[-1]))))
         assert ei.value.status == 1
+
+
+def test_var_byte_fixture_pins_the_readers(tmp_path):
+    """The reference's own var-byte file (data/varByteStrings.v1, VarByteChunkSingleValueReaderWriteTest
+    .testBackwardCompatibility: 1009 entries cycling "abcde", "fgh", "ijklmn", "12345"): the oracle's reader returns
+    those values, and the library's loader reads it as a raw STRING column's .sv.raw.fwd."""
+    import numpy as np
+    from segment_dir import read_var_byte_strings
+    fixture = open(os.path.join(os.path.dirname(__file__), "golden", "var_byte_strings.v1"), "rb").read()
+    expected = ["abcde", "fgh", "ijklmn", "12345"]
+    vals = read_var_byte_strings(fixture, 1009)
+    assert vals == [expected[i % 4] for i in range(1009)]
+    seg = build_segment("vb", {"s": ("STRING", np.array(vals, dtype=object)),
+                               "i": ("INT", np.arange(1009, dtype=np.int32))}, raw_columns=("s",))
+    seg.columns["s"].raw_file = fixture
+    assert segment_dir_info(write_segment_dir(seg, str(tmp_path / "vb"))) == (1009, 2, 0)
+
+
+@pytest.mark.parametrize("comp,version,per_chunk", [(1, 2, 7), (0, 2, 1000), (1, 1, 333), (0, 2, 1)])
+def test_raw_string_columns(tmp_path, comp, version, per_chunk):
+    """Raw STRING columns: the writer's var-byte chunks (empty strings, multi-byte UTF-8, a partial last chunk) read
+    back by the oracle's reader, and the library's loader + registration checks accept them."""
+    import numpy as np
+    from segdir_writer import var_byte_chunk_file
+    from segment_dir import read_var_byte_strings
+    rng = np.random.default_rng(per_chunk)
+    pool = ["", "a", "zz", "héllo", "日本", "x" * 40, "b7"]
+    vals = [pool[int(v)] for v in rng.integers(0, len(pool), 2001)]
+    buf = var_byte_chunk_file(vals, docs_per_chunk=per_chunk, compression=comp if version > 1 else 1,
+                              version=version)
+    assert read_var_byte_strings(buf, len(vals)) == vals
+    seg = build_segment("vs", {"s": ("STRING", np.array(vals, dtype=object))}, raw_columns=("s",))
+    seg.columns["s"].raw_file = buf
+    assert segment_dir_info(write_segment_dir(seg, str(tmp_path / "d"), version="v3")) == (2001, 1, 0)
+    validate_segment(seg)
+
+
+def test_raw_string_bad_bytes():
+    import numpy as np
+    seg = build_segment("bad", {"s": ("STRING", np.array(["ab", "c\x00d"], dtype=object))}, raw_columns=("s",))
+    with pytest.raises(PinotGpuError, match="NUL"):
+        validate_segment(seg)
+    seg = build_segment("bad", {"s": ("STRING", np.array(["ab", "cd"], dtype=object))}, raw_columns=("s",))
+    col = seg.columns["s"]
+    col.fwd = col.fwd[:4] + (9).to_bytes(4, "big") + col.fwd[8:]  # offsets not ascending within the bytes
+    with pytest.raises(PinotGpuError, match="offsets"):
+        validate_segment(seg)

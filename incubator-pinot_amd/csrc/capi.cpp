@@ -105,6 +105,16 @@ void check_query(const pinot_query *q) {
   require(q->num_group_by == 0 || q->group_by != nullptr, PINOT_ERR_BAD_ARG, "group_by");
 }
 
+// stats.exact=1: numEntriesScannedInFilter as a Java server counts it (filter_stats.cpp), summed over the processed
+// segments; the shortcut plans (no filter) scan nothing either way
+void exact_filter_stats(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q, pinot_exec_stats *st) {
+  if (!e.stats_exact || !st || q.num_filter_nodes == 0) return;
+  const FilterTreeInput tree = decode_filter(q.num_filter_nodes, q.filter);
+  int64_t n = 0;
+  for (SegmentData *s : segs) n += filter_entries_scanned(e, *s, &tree);
+  st->num_entries_scanned_in_filter = n;
+}
+
 void parse_config(Engine &e, const char *cfg) {
   if (!cfg) return;
   e.config_epoch++;
@@ -148,6 +158,7 @@ void parse_config(Engine &e, const char *cfg) {
     else if (k == "debug.host_phases") e.host_phases = v == "1" || v == "true";
     else if (k == "exec.nt") e.use_nt = v == "1" || v == "true";
     else if (k == "exec.pipe") e.use_pipe = v == "1" || v == "true";
+    else if (k == "stats.exact") e.stats_exact = v == "1" || v == "true";
     else throw Error(PINOT_ERR_BAD_ARG, "unknown config key " + k);
   }
 }
@@ -320,6 +331,7 @@ pinot_status pinot_gpu_aggregate(pinot_engine *engine, const pinot_segment_handl
       if (stats) memset(stats, 0, sizeof(*stats));
     } else {
       exec_aggregate(*engine, kept, *query, out, stats);
+      exact_filter_stats(*engine, kept, *query, stats);
     }
     if (engine->host_phases)
       fprintf(stderr, "[pinot_gpu] aggregate C-ABI phases (us): resolve+prune %.1f, execute %.1f\n",
@@ -349,6 +361,7 @@ pinot_status pinot_gpu_group_by(pinot_engine *engine, const pinot_segment_handle
       if (stats) memset(stats, 0, sizeof(*stats));
     } else {
       r = exec_group_by(*engine, kept, *query, stats);
+      exact_filter_stats(*engine, kept, *query, stats);
     }
     if (stats) {
       if (query->pruners) stats->num_total_raw_docs = total_docs(segs);

@@ -192,6 +192,7 @@ struct Engine {
   std::string force_filter;   // "", "scan", "index": planner override for tests
   bool use_affine = true;     // agg.affine: arithmetic-progression dictionary SUM shortcut
   bool use_fused = true;      // exec.fused: one k_scan_query launch per aggregation query when the shape allows
+  bool stats_exact = false;   // stats.exact: numEntriesScannedInFilter replayed per the iterator protocol (host)
   bool use_nt = true;         // exec.nt: non-temporal policy on the streamed column DMA (measured: config-2
                               // k_scan_query 0.733 -> 0.702 ms)
   bool use_pipe = false;      // exec.pipe: double-buffered whole-chunk staging (k_scan_query_pipe) when a chunk fits
@@ -267,6 +268,9 @@ struct DeadlineScope {
 
 // execution entry points (executor.cpp)
 void exec_filter(Engine &e, SegmentData &s, const FilterTreeInput *tree, uint64_t *bitset_out, int64_t *count);
+// numEntriesScannedInFilter of one segment as the reference's iterator protocol counts it (filter_stats.cpp;
+// stats.exact=1)
+int64_t filter_entries_scanned(Engine &e, SegmentData &s, const FilterTreeInput *tree);
 void exec_aggregate(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q, pinot_agg_result *out,
                     pinot_exec_stats *stats);
 

@@ -291,13 +291,15 @@ FilterTreeInput decode_filter(int32_t n, const pinot_filter_node *nodes) {
 
 namespace {
 
-int and_priority(const FilterNode &n) {  // FilterOperatorUtils.reorderAndFilterChildOperators (:130-161)
+// FilterOperatorUtils.reorderAndFilterChildOperators (:130-161): sorted, bitmap, AND, OR, scan; a multi-value scan
+// after the single-value ones (getScanBasedFilterPriority)
+int and_priority(const SegmentData &seg, const FilterNode &n) {
   switch (n.type) {
     case FilterNode::SORTED: return 0;
     case FilterNode::BITMAP: return 1;
     case FilterNode::AND: return 2;
     case FilterNode::OR: return 3;
-    default: return 4;
+    default: return n.col >= 0 && seg.cols[n.col]->mv ? 5 : 4;
   }
 }
 
@@ -320,7 +322,9 @@ FilterNode construct(const SegmentData &seg, const FilterTreeInput &t) {
     if (out.children.size() == 1) return std::move(out.children[0]);
     if (is_and)
       std::stable_sort(out.children.begin(), out.children.end(),
-                       [](const FilterNode &a, const FilterNode &b) { return and_priority(a) < and_priority(b); });
+                       [&](const FilterNode &a, const FilterNode &b) {
+                         return and_priority(seg, a) < and_priority(seg, b);
+                       });
     return out;
   }
   const int ci = seg.by_name.count(t.column) ? seg.by_name.at(t.column) : -1;

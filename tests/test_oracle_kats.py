@@ -82,3 +82,19 @@ def test_hll_estimator_edges():
 
 def test_avg_empty_is_negative_infinity():
     assert O.final_result("AVG", (0.0, 0)) == -math.inf
+
+
+def test_entries_scanned_in_filter(kats):
+    """numEntriesScannedInFilter of the reference's filtered queries (84134 per segment: 336536 over the 4 copies of
+    InterSegmentAggregationSingleValueQueriesTest, 84134 in InnerSegmentAggregationSingleValueQueriesTest) replayed by
+    oracle/iter_stats.py. The reference's segment is loaded with the default IndexLoadingConfig
+    (ImmutableSegmentLoader.load(dir, ReadMode.heap)), which brings in no bitmap inverted index: only the sorted
+    columns are index-backed, so column11's NOT IN is a scan; with column11's bitmap the count would be 63064."""
+    import iter_stats
+    from conftest import build_segment, load_sv_columns
+    seg = build_segment("testTable_126164076_167572854", load_sv_columns())
+    q = _q("SELECT COUNT(*) FROM testTable" + kats["filter"])
+    assert iter_stats.entries_scanned_in_filter(seg, q["filter"]) == 84134
+    assert kats["inner_aggregation"]["filtered"]["stats"][1] == 84134
+    assert kats["inter_segment"]["cases"][0]["stats"]["filtered"][1] == 4 * 84134
+    assert iter_stats.entries_scanned_in_filter(seg, None) == 0

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define PINOT_GPU_ABI_VERSION 9
+#define PINOT_GPU_ABI_VERSION 10
 
 /* ------------------------------------------------------------------ status */
 typedef enum {
@@ -241,6 +241,15 @@ pinot_status pinot_gpu_segment_release(pinot_engine *engine, pinot_segment_handl
  * VarByteChunkSingleValueReader.java:40-115), and registered as PINOT_ENCODING_RAW; multi-value dictionary columns
  * from <col>.mv.fwd (FixedBitMultiValueReader). Raw multi-value and BYTES columns are not served and are left out. */
 pinot_status pinot_gpu_segment_load(pinot_engine *engine, const char *index_dir, pinot_segment_handle *out);
+/* The engine's device segment cache (a server's SegmentDataManager map keyed by segment name, refreshed when the
+ * segment's CRC changes: creation.meta's crc, SegmentMetadataImpl.java:204-210, V1Constants.java:27,97). A
+ * directory whose segment name and CRC match a cached device copy returns that copy's handle (*cache_hit = 1; only
+ * metadata.properties and creation.meta are read); otherwise the directory is loaded as pinot_gpu_segment_load does,
+ * a cached copy of the same name with another CRC is released (the segment was replaced), and the new copy is
+ * cached (*cache_hit = 0). A directory without creation.meta is loaded and never cached. A cached handle stays valid
+ * until pinot_gpu_segment_release (which drops it from the cache) or its replacement. */
+pinot_status pinot_gpu_segment_acquire(pinot_engine *engine, const char *index_dir, pinot_segment_handle *out,
+                                       int32_t *cache_hit);
 /* The same read and checks on the host only (no engine, no GPU): docs, served columns, left-out columns. */
 pinot_status pinot_gpu_segment_dir_info(const char *index_dir, int32_t *num_docs, int32_t *num_columns,
                                         int32_t *num_skipped);

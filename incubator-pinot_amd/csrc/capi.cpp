@@ -211,30 +211,63 @@ pinot_status pinot_gpu_segment_register(pinot_engine *engine, const pinot_segmen
   });
 }
 
+namespace {
+// ImmutableSegmentLoader.load of a directory into a new handle (caller holds engine->mu)
+int64_t load_segment_dir(Engine &engine, const char *index_dir) {
+  SegmentDirData files;
+  read_segment_dir(index_dir, files);
+  const pinot_segment_desc desc = files.desc();
+  set_device(engine);
+  auto seg = register_segment(engine, desc);
+  seg->unserved = files.skipped;
+  // ColumnMinMaxValueGenerator in its default mode (TIME, CommonConstants.java:264): the time column's min / max
+  // from its dictionary when the metadata lacks them (ColumnMinMaxValueGenerator.java:55-140)
+  auto tc = seg->by_name.find(files.time_column);
+  if (tc != seg->by_name.end()) {
+    ColumnData &c = *seg->cols[tc->second];
+    if (!c.has_minmax && c.card >= 1) {
+      c.has_minmax = true;
+      c.min_value = c.string_value(0);
+      c.max_value = c.string_value(c.card - 1);
+    }
+  }
+  const int64_t h = engine.next_handle++;
+  engine.segments[h] = std::move(seg);
+  return h;
+}
+}  // namespace
+
 pinot_status pinot_gpu_segment_load(pinot_engine *engine, const char *index_dir, pinot_segment_handle *out) {
   return guard([&] {
     require(engine && index_dir && out, PINOT_ERR_BAD_ARG, "null argument");
-    SegmentDirData files;
-    read_segment_dir(index_dir, files);
-    const pinot_segment_desc desc = files.desc();
     std::lock_guard<std::mutex> lk(engine->mu);
-    set_device(*engine);
-    auto seg = register_segment(*engine, desc);
-    seg->unserved = files.skipped;
-    // ColumnMinMaxValueGenerator in its default mode (TIME, CommonConstants.java:264): the time column's min / max
-    // from its dictionary when the metadata lacks them (ColumnMinMaxValueGenerator.java:55-140)
-    auto tc = seg->by_name.find(files.time_column);
-    if (tc != seg->by_name.end()) {
-      ColumnData &c = *seg->cols[tc->second];
-      if (!c.has_minmax && c.card >= 1) {
-        c.has_minmax = true;
-        c.min_value = c.string_value(0);
-        c.max_value = c.string_value(c.card - 1);
-      }
+    *out = load_segment_dir(*engine, index_dir);
+  });
+}
+
+pinot_status pinot_gpu_segment_acquire(pinot_engine *engine, const char *index_dir, pinot_segment_handle *out,
+                                       int32_t *cache_hit) {
+  return guard([&] {
+    require(engine && index_dir && out, PINOT_ERR_BAD_ARG, "null argument");
+    std::string name;
+    int64_t crc = 0;
+    const bool has_crc = read_segment_identity(index_dir, name, crc);
+    std::lock_guard<std::mutex> lk(engine->mu);
+    auto it = has_crc ? engine->segment_cache.find(name) : engine->segment_cache.end();
+    if (it != engine->segment_cache.end() && it->second.first == crc && engine->segments.count(it->second.second)) {
+      *out = it->second.second;
+      if (cache_hit) *cache_hit = 1;
+      return;
     }
-    const int64_t h = engine->next_handle++;
-    engine->segments[h] = std::move(seg);
+    const int64_t h = load_segment_dir(*engine, index_dir);
+    if (it != engine->segment_cache.end()) {  // replaced: drop the stale device copy
+      PINOT_HIP(hipStreamSynchronize(engine->stream));
+      engine->segments.erase(it->second.second);
+      engine->segment_cache.erase(it);
+    }
+    if (has_crc) engine->segment_cache[name] = {crc, h};
     *out = h;
+    if (cache_hit) *cache_hit = 0;
   });
 }
 
@@ -281,6 +314,11 @@ pinot_status pinot_gpu_segment_release(pinot_engine *engine, pinot_segment_handl
     set_device(*engine);
     PINOT_HIP(hipStreamSynchronize(engine->stream));
     require(engine->segments.erase(handle) == 1, PINOT_ERR_BAD_ARG, "unknown segment handle");
+    for (auto it = engine->segment_cache.begin(); it != engine->segment_cache.end(); ++it)
+      if (it->second.second == handle) {
+        engine->segment_cache.erase(it);
+        break;
+      }
   });
 }
 

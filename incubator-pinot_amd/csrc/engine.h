@@ -114,6 +114,8 @@ struct SegmentDirData {
   pinot_segment_desc desc() const;
 };
 void read_segment_dir(const std::string &index_dir, SegmentDirData &out);
+// segment.name (metadata.properties) and creation.meta's CRC (false when the directory has no creation.meta)
+bool read_segment_identity(const std::string &index_dir, std::string &name, int64_t &crc);
 uint64_t next_segment_uid();
 
 struct SegmentData {
@@ -186,6 +188,8 @@ struct Engine {
   std::mutex mu;
   int64_t next_handle = 1;
   std::unordered_map<int64_t, std::unique_ptr<SegmentData>> segments;
+  // device segment cache: segment name -> (creation.meta CRC, handle) (pinot_gpu_segment_acquire)
+  std::unordered_map<std::string, std::pair<int64_t, int64_t>> segment_cache;
 
   // configuration
   int num_groups_limit = 100000;

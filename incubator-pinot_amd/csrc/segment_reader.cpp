@@ -375,6 +375,26 @@ std::vector<uint8_t> read_var_byte_chunks(const uint8_t *b, uint64_t n, int64_t 
   return offs;
 }
 
+bool read_segment_identity(const std::string &index_dir, std::string &name, int64_t &crc) {
+  require(is_dir(index_dir), PINOT_ERR_BAD_ARG, "not a segment directory: " + index_dir);
+  const std::string v3 = index_dir + "/v3";
+  const std::string dir = is_dir(v3) ? v3 : index_dir;
+  const std::string meta_path = is_file(dir + "/metadata.properties") ? dir + "/metadata.properties"
+                                                                      : index_dir + "/metadata.properties";
+  const auto kv = parse_properties(read_text(meta_path));
+  name = prop(kv, "segment.name", "");
+  // SegmentDirectoryPaths.findCreationMetaFile: v3/creation.meta, else the index directory's
+  std::string cm = dir + "/creation.meta";
+  if (!is_file(cm)) cm = index_dir + "/creation.meta";
+  if (!is_file(cm)) return false;
+  MappedFile f(cm);
+  require(f.size >= 8, PINOT_ERR_BAD_ARG, "creation.meta shorter than its CRC");
+  uint64_t v = 0;
+  for (int k = 0; k < 8; k++) v = (v << 8) | f.data[k];  // DataInputStream.readLong (big-endian)
+  crc = (int64_t)v;
+  return true;
+}
+
 void read_segment_dir(const std::string &index_dir, SegmentDirData &out) {
   require(is_dir(index_dir), PINOT_ERR_BAD_ARG, "not a segment directory: " + index_dir);
   const std::string v3 = index_dir + "/v3";

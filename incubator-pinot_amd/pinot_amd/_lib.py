@@ -34,7 +34,7 @@ EXPORTED_SYMBOLS = [
     "pinot_gpu_last_error", "pinot_gpu_abi_version", "pinot_gpu_device_count",
     "pinot_gpu_engine_create", "pinot_gpu_engine_destroy", "pinot_gpu_engine_set_config",
     "pinot_gpu_segment_register", "pinot_gpu_segment_release", "pinot_gpu_segment_validate",
-    "pinot_gpu_segment_load", "pinot_gpu_segment_dir_info",
+    "pinot_gpu_segment_load", "pinot_gpu_segment_acquire", "pinot_gpu_segment_dir_info",
     "pinot_gpu_segment_device_bytes", "pinot_gpu_filter", "pinot_gpu_aggregate", "pinot_gpu_group_by",
     "pinot_groupby_num_groups", "pinot_groupby_num_columns", "pinot_groupby_key", "pinot_groupby_values",
     "pinot_groupby_hll", "pinot_groupby_raw_keys", "pinot_groupby_export_keys", "pinot_groupby_trim",
@@ -167,6 +167,7 @@ def load(path=None):
         "pinot_gpu_segment_release": (i32, [P, i64]),
         "pinot_gpu_segment_validate": (i32, [C.POINTER(SegmentDesc)]),
         "pinot_gpu_segment_load": (i32, [P, C.c_char_p, C.POINTER(i64)]),
+        "pinot_gpu_segment_acquire": (i32, [P, C.c_char_p, C.POINTER(i64), C.POINTER(i32)]),
         "pinot_gpu_segment_dir_info": (i32, [C.c_char_p, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32)]),
         "pinot_gpu_segment_device_bytes": (i32, [P, i64, C.POINTER(u64)]),
         "pinot_gpu_filter": (i32, [P, i64, i32, C.POINTER(FilterNode), P, C.POINTER(i64)]),

@@ -236,6 +236,15 @@ class GpuEngine:
         check(self.lib.pinot_gpu_segment_dir_info(os.fsencode(index_dir), C.byref(n), None, None))
         return GpuSegment(self, h.value, os.path.basename(os.path.normpath(index_dir)), n.value)
 
+    def acquire(self, index_dir: str):
+        """pinot_gpu_segment_acquire: the device segment cache (segment name + creation.meta CRC). Returns
+        (GpuSegment, cache_hit); a hit is the cached copy's handle, a changed CRC replaces (releases) the old copy."""
+        h, hit = C.c_int64(), C.c_int32()
+        check(self.lib.pinot_gpu_segment_acquire(self.ptr, os.fsencode(index_dir), C.byref(h), C.byref(hit)))
+        n = C.c_int32()
+        check(self.lib.pinot_gpu_segment_dir_info(os.fsencode(index_dir), C.byref(n), None, None))
+        return GpuSegment(self, h.value, os.path.basename(os.path.normpath(index_dir)), n.value), bool(hit.value)
+
     SYNTH_KIND = {"random": 0, "sorted": 1, "inverted": 2}
 
     def register_synthetic(self, name, num_docs, columns, seed):

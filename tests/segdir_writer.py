@@ -197,9 +197,15 @@ def _buffers(c):
             yield "inverted_index", c.name + ".bitmap.inv", c.inverted
 
 
-def write_segment_dir(seg, index_dir, version="v1", padding="\\\\u0000"):
-    """padding: the metadata value as written (default the escaped NUL Pinot writes); None leaves the key out."""
+def write_segment_dir(seg, index_dir, version="v1", padding="\\\\u0000", crc=None, creation_time=0):
+    """padding: the metadata value as written (default the escaped NUL Pinot writes); None leaves the key out.
+    crc: write creation.meta (SegmentIndexCreationDriverImpl: DataOutputStream.writeLong(crc), writeLong(time))."""
     os.makedirs(index_dir, exist_ok=True)
+    if crc is not None:
+        d = os.path.join(index_dir, "v3") if version == "v3" else index_dir
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, "creation.meta"), "wb") as f:
+            f.write(struct.pack(">qq", crc, creation_time))
     if version == "v3":
         d = os.path.join(index_dir, "v3")
         os.makedirs(d, exist_ok=True)

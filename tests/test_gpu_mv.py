@@ -122,11 +122,11 @@ def test_mv_segment_dir_and_datatable(engine, tmp_path):
     got, _ = ex.process_query(q, [g], trim=False)
     exp, _ = O.execute_server([seg], q)
     _check(q, got, exp)
-    dt = ex.process_query_datatable(q, [g])
+    dt, _ = ex.process_query_datatable(q, [g])
     for name in (b"countMV_tags", b"avgMV_tagl", b"distinctCountHLLMV_tags_s"):
         assert name in dt
     qa = dict(q, group_by=None)
-    dt = ex.process_query_datatable(qa, [g])
+    dt, _ = ex.process_query_datatable(qa, [g])
     assert b"countMV_tags" in dt and b"avgMV_tagl" in dt
     g.release()
 

@@ -143,3 +143,50 @@ def test_raw_columns_loaded_from_disk(engine, tmp_path):
                 _assert_same(a["function"], g, e, exact=a["column"] not in ("d", "f"))
     for g in gsegs:
         g.release()
+
+
+@pytest.mark.parametrize("version", ["v1", "v3"])
+def test_segment_cache_by_name_and_crc(tmp_path, version):
+    """pinot_gpu_segment_acquire: the same name + creation.meta CRC is the cached device copy; a new CRC replaces it
+    (the stale handle is gone); no creation.meta is never cached; release drops the entry."""
+    from pinot_amd import PinotGpuError
+    e = GpuEngine(0)
+    try:
+        seg = _random_segment(40, 5000)
+        d1 = write_segment_dir(seg, str(tmp_path / "a"), version=version, crc=1234567890123)
+        g1, hit = e.acquire(d1)
+        assert not hit
+        g2, hit = e.acquire(d1)
+        assert hit and g2.handle == g1.handle
+        ex = ServerQueryExecutor(e)
+        q = {"aggregations": [{"function": "COUNT", "column": "*"}, {"function": "SUM", "column": "m"}],
+             "filter": {"operator": "RANGE", "column": "i", "values": ["[0\t\t*)"]}, "group_by": None}
+        exp, _ = O.execute_server([seg], q)
+        got, _ = ex.process_query(q, [g2])
+        assert got == exp
+        # a new build of the segment (another CRC): reloaded, the old copy released
+        seg_b = _random_segment(41, 6000)
+        seg_b.name = seg.name
+        d2 = write_segment_dir(seg_b, str(tmp_path / "b"), version=version, crc=-5)
+        g3, hit = e.acquire(d2)
+        assert not hit and g3.handle != g1.handle
+        with pytest.raises(PinotGpuError):
+            ex.process_query(q, [g1])
+        got, _ = ex.process_query(q, [g3])
+        assert got == O.execute_server([seg_b], q)[0]
+        g4, hit = e.acquire(d2)
+        assert hit and g4.handle == g3.handle
+        g3.release()
+        g5, hit = e.acquire(d2)
+        assert not hit and g5.handle != g3.handle
+        g4.handle = None  # same handle as g3, already released
+        g5.release()
+        # no creation.meta: loaded every time
+        d3 = write_segment_dir(seg, str(tmp_path / "c"), version=version)
+        h1, hit1 = e.acquire(d3)
+        h2, hit2 = e.acquire(d3)
+        assert not hit1 and not hit2 and h1.handle != h2.handle
+        h1.release()
+        h2.release()
+    finally:
+        e.close()

@@ -9,6 +9,7 @@
 // object cells per ObjectSerDeUtils (PC/common/ObjectSerDeUtils.java:144-330). Output: the BrokerResponseNative JSON
 // (pinot-common/.../response/broker/BrokerResponseNative.java:42 property order).
 #include <algorithm>
+#include <cctype>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -360,6 +361,9 @@ std::string broker_reduce(const pinot_query &q, int32_t n, const uint8_t *const 
   std::string exceptions;
   auto parse_long = [](const std::string &s) -> int64_t {  // Long.parseLong
     try {
+      // Long.parseLong takes an optional sign then digits only (std::stoll would skip leading whitespace)
+      require(!s.empty() && (s[0] == '-' || s[0] == '+' || (s[0] >= '0' && s[0] <= '9')), PINOT_ERR_BAD_ARG,
+              "DataTable: metadata value is not a long: " + s);
       size_t used = 0;
       const long long v = std::stoll(s, &used);
       require(used == s.size(), PINOT_ERR_BAD_ARG, "DataTable: metadata value is not a long: " + s);
@@ -389,7 +393,9 @@ std::string broker_reduce(const pinot_query &q, int32_t n, const uint8_t *const 
     add(matched, meta(t, "numSegmentsMatched"));
     add(total, meta(t, "totalDocs"));
     const std::string *gl = meta(t, "numGroupsLimitReached");
-    limit |= gl && (*gl == "true" || *gl == "TRUE" || *gl == "True");  // Boolean.valueOf: case-insensitive "true"
+    limit |= gl && gl->size() == 4 && std::equal(gl->begin(), gl->end(), "true", [](char a, char b) {
+               return std::tolower((unsigned char)a) == b;
+             });  // Boolean.valueOf: "true", ignoring case
     if (t.has_schema && t.rows > 0) with_rows.push_back(&t);
   }
   std::string results;

@@ -173,6 +173,61 @@ std::vector<std::string> split_values(const std::vector<std::string> &values) {
   return out;
 }
 
+// A raw FLOAT / DOUBLE column's RawValueBased evaluators compare primitives (FloatRawValueBasedEqPredicateEvaluator
+// `_matchingValue == value`, the range evaluators `value >= lower` ...): -0.0 equals 0.0, and NaN (as literal or value)
+// compares false, where the transcoded dictionary (Double.compare order) keeps -0.0 < 0.0 and sorts NaN last. The
+// dictionary evaluator above is right for every other entry, so only the NaN entry and the zero entries are
+// re-evaluated with the primitive rules — unless a RANGE bound is NaN (nothing compares true), which re-evaluates all.
+void raw_fp_semantics(const ColumnData &c, int op, const std::vector<std::string> &values, Evaluator &ev) {
+  const bool f32 = c.data_type == PINOT_FLOAT;
+  const int64_t card = c.card;
+  if (card == 0) return;
+  auto lit = [&](const std::string &s) { return java_parse_double(s, f32); };
+  std::vector<double> set;
+  RangeBounds rb;
+  bool lo_set = false, hi_set = false;
+  double lo = 0, hi = 0;
+  if (op == PINOT_FILTER_IN || op == PINOT_FILTER_NOT_IN) {
+    for (const auto &v : split_values(values)) set.push_back(lit(v));
+  } else if (op == PINOT_FILTER_RANGE) {
+    rb = parse_range(values[0]);
+    if (rb.lower != "*") { lo_set = true; lo = lit(rb.lower); }
+    if (rb.upper != "*") { hi_set = true; hi = lit(rb.upper); }
+  } else {
+    set.push_back(lit(values[0]));
+  }
+  auto match = [&](double v) -> bool {
+    switch (op) {
+      case PINOT_FILTER_EQUALITY: return v == set[0];
+      case PINOT_FILTER_NOT: return v != set[0];
+      case PINOT_FILTER_IN: for (double x : set) if (v == x) return true; return false;
+      case PINOT_FILTER_NOT_IN: for (double x : set) if (v == x) return false; return true;
+      default:
+        return (!lo_set || (rb.inc_lower ? v >= lo : v > lo)) && (!hi_set || (rb.inc_upper ? v <= hi : v < hi));
+    }
+  };
+  std::vector<int64_t> ids;
+  if (op == PINOT_FILTER_RANGE && ((lo_set && std::isnan(lo)) || (hi_set && std::isnan(hi)))) {
+    for (int64_t i = 0; i < card; i++) ids.push_back(i);
+  } else {
+    const bool nan_last = std::isnan(c.double_value(card - 1));
+    if (nan_last) ids.push_back(card - 1);
+    int64_t l = 0, r = card - (nan_last ? 1 : 0);  // the zero entries (-0.0, 0.0) are adjacent
+    while (l < r) {
+      const int64_t m = (l + r) / 2;
+      if (c.double_value(m) < 0.0) l = m + 1; else r = m;
+    }
+    for (int64_t i = l; i < card - (nan_last ? 1 : 0) && c.double_value(i) == 0.0; i++) ids.push_back(i);
+  }
+  for (int64_t i : ids) {
+    const uint8_t m = match(c.double_value(i)) ? 1 : 0;
+    ev.num_matching += (int64_t)m - (int64_t)ev.matching[i];
+    ev.matching[i] = m;
+  }
+  ev.always_true = ev.num_matching == card;
+  ev.always_false = ev.num_matching == 0;
+}
+
 }  // namespace
 
 Evaluator make_evaluator(const ColumnData &c, int op, const std::vector<std::string> &values) {
@@ -262,6 +317,7 @@ Evaluator make_evaluator(const ColumnData &c, int op, const std::vector<std::str
     default:
       throw Error(PINOT_ERR_UNSUPPORTED, "unsupported predicate operator");
   }
+  if (c.raw && (c.data_type == PINOT_FLOAT || c.data_type == PINOT_DOUBLE)) raw_fp_semantics(c, op, values, ev);
   return ev;
 }
 

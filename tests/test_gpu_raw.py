@@ -32,9 +32,6 @@ def _segments(rng, n, k):
     out = []
     for i in range(k):
         cols, inv = _random_columns(rng, n)
-        for c in ("dbl", "flt"):  # signed zeros: a dictionary keeps -0.0 and 0.0 apart (documented deviation)
-            t, v = cols[c]
-            cols[c] = (t, [0.0 if x == 0 else x for x in v])
         out.append(build_segment("raw%d" % i, cols, inverted_columns=tuple(x for x in inv if x not in RAW),
                                  raw_columns=RAW))
     return out
@@ -133,4 +130,30 @@ def test_var_byte_fixture_on_gpu(engine, tmp_path):
     assert got == {v: [len(range(k, 1009, 4)), float(sum(range(k, 1009, 4)))] for k, v in enumerate(expected)}
     got, st = ex.process_query(compile_pql("SELECT COUNT(*) FROM t WHERE s BETWEEN 'abcde' AND 'fgh'"), [g])
     assert got == [505] and st.num_docs_scanned == 505
+    g.release()
+
+
+def test_raw_fp_primitive_comparisons(engine):
+    """Raw FLOAT / DOUBLE predicates compare primitives (RawValueBased evaluators): -0.0 == 0.0, NaN (literal or
+    value) never compares true — unlike the transcoded dictionary's Double.compare order. Checked against the
+    oracle's raw-value evaluators (numpy IEEE comparisons)."""
+    import pinot_oracle as O
+    vals = [float("nan"), -0.0, 0.0, 1.5, -2.25, 0.0, -0.0, float("nan"), 7.0, -1.0] * 50
+    seg = build_segment("fp", {"d": ("DOUBLE", vals), "f": ("FLOAT", np.array(vals, dtype=np.float32)),
+                               "i": ("INT", np.arange(len(vals), dtype=np.int32))}, raw_columns=("d", "f"))
+    g = engine.register(seg)
+    lits = ["NaN", "0.0", "-0.0", "1.5", "-1.0"]
+    for col in ("d", "f"):
+        trees = []
+        for l in lits:
+            trees += [{"operator": op, "column": col, "values": [l]} for op in ("EQUALITY", "NOT")]
+            trees += [{"operator": op, "column": col, "values": [l + "\t\t7.0"]} for op in ("IN", "NOT_IN")]
+            trees += [{"operator": "RANGE", "column": col, "values": [r]} for r in (
+                "[%s\t\t*)" % l, "(%s\t\t*)" % l, "(*\t\t%s]" % l, "(*\t\t%s)" % l, "[-0.0\t\t%s]" % l)]
+        trees.append({"operator": "RANGE", "column": col, "values": ["(*\t\t*)"]})
+        for tree in trees:
+            exp = O.filter_mask(seg, tree)
+            bits, cnt = engine.filter(g, tree)
+            got = np.unpackbits(bits.view(np.uint8), bitorder="little")[:len(vals)].astype(bool)
+            assert cnt == int(exp.sum()) and (got == exp).all(), tree
     g.release()

@@ -13,6 +13,8 @@ Engine::~Engine() {
   for (auto ev : kev) (void)hipEventDestroy(ev);
   if (ev_start) (void)hipEventDestroy(ev_start);
   if (ev_stop) (void)hipEventDestroy(ev_stop);
+  for (auto cs : copy_streams) (void)hipStreamDestroy(cs);
+  if (ev_copy) (void)hipEventDestroy(ev_copy);
   if (stream) (void)hipStreamDestroy(stream);
 }
 
@@ -159,6 +161,10 @@ void parse_config(Engine &e, const char *cfg) {
     else if (k == "exec.nt") e.use_nt = v == "1" || v == "true";
     else if (k == "exec.pipe") e.use_pipe = v == "1" || v == "true";
     else if (k == "stats.exact") e.stats_exact = v == "1" || v == "true";
+    else if (k == "d2h.streams") {
+      e.d2h_streams = std::stoi(v);
+      require(e.d2h_streams >= 1 && e.d2h_streams <= 8, PINOT_ERR_BAD_ARG, "d2h.streams: 1 .. 8");
+    }
     else throw Error(PINOT_ERR_BAD_ARG, "unknown config key " + k);
   }
 }

@@ -185,6 +185,10 @@ bool prune_segment_desc(const pinot_segment_desc &d, const pinot_query &q, const
 struct Engine {
   int device = 0;
   hipStream_t stream = nullptr;
+  // result D2H fan-out (d2h.streams): the group-by result arrays copied on parallel streams (one SDMA queue each)
+  int d2h_streams = 4;
+  std::vector<hipStream_t> copy_streams;
+  hipEvent_t ev_copy = nullptr;
   std::mutex mu;
   int64_t next_handle = 1;
   std::unordered_map<int64_t, std::unique_ptr<SegmentData>> segments;

@@ -2484,14 +2484,32 @@ std::unique_ptr<GroupByResult> dense_fetch(Engine &e, const pinot_query &q, cons
   }
   const auto tb1 = std::chrono::steady_clock::now();
   const size_t n8 = n * 8;
-  PINOT_HIP(hipMemcpyAsync(res->raw_keys.data(), o.keys, n8, hipMemcpyDeviceToHost, e.stream));
-  PINOT_HIP(hipMemcpyAsync(res->counts[0].data(), o.counts, n8, hipMemcpyDeviceToHost, e.stream));
+  // the arrays' D2H copies fanned out over d2h.streams streams (each its own copy queue), all after the final-array
+  // kernels: one queue alone leaves PCIe half idle on a 32 MB result
+  std::vector<std::pair<void *, const void *>> copies;
+  copies.emplace_back(res->raw_keys.data(), o.keys);
+  copies.emplace_back(res->counts[0].data(), o.counts);
   for (int i = 0; i < na; i++) {
-    if (o.derive[i] == -1)
-      PINOT_HIP(hipMemcpyAsync(res->values[i].data(), o.values[i], n8, hipMemcpyDeviceToHost, e.stream));
-    if (o.kind[i] == 4)
-      PINOT_HIP(hipMemcpyAsync(res->hll_card[i].data(), o.cards[i], n8, hipMemcpyDeviceToHost, e.stream));
+    if (o.derive[i] == -1) copies.emplace_back(res->values[i].data(), o.values[i]);
+    if (o.kind[i] == 4) copies.emplace_back(res->hll_card[i].data(), o.cards[i]);
   }
+  const int ns = (n8 >= (1u << 20)) ? std::min<int>(e.d2h_streams, (int)copies.size()) : 1;
+  if (ns > 1) {
+    while ((int)e.copy_streams.size() < ns - 1) {
+      hipStream_t cs;
+      PINOT_HIP(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+      e.copy_streams.push_back(cs);
+    }
+    if (!e.ev_copy) PINOT_HIP(hipEventCreateWithFlags(&e.ev_copy, hipEventDisableTiming));
+    PINOT_HIP(hipEventRecord(e.ev_copy, e.stream));
+    for (int k = 0; k < ns - 1; k++) PINOT_HIP(hipStreamWaitEvent(e.copy_streams[k], e.ev_copy, 0));
+  }
+  for (size_t j = 0; j < copies.size(); j++) {
+    const int k = (int)(j % (size_t)ns);
+    hipStream_t st = k == 0 ? e.stream : e.copy_streams[k - 1];
+    PINOT_HIP(hipMemcpyAsync(copies[j].first, copies[j].second, n8, hipMemcpyDeviceToHost, st));
+  }
+  for (int k = 0; k < ns - 1; k++) PINOT_HIP(hipStreamSynchronize(e.copy_streams[k]));
   wait_stream(e);
   bool any_derived = false;
   for (int i = 0; i < na; i++) any_derived = any_derived || o.derive[i] != -1;

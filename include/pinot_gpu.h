@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define PINOT_GPU_ABI_VERSION 10
+#define PINOT_GPU_ABI_VERSION 11
 
 /* ------------------------------------------------------------------ status */
 typedef enum {
@@ -258,6 +258,24 @@ pinot_status pinot_gpu_segment_dir_info(const char *index_dir, int32_t *num_docs
  * no GPU. PINOT_ERR_BAD_ARG + pinot_gpu_last_error() name the first bad column. */
 pinot_status pinot_gpu_segment_validate(const pinot_segment_desc *desc);
 /* Bytes of HBM held by a segment. */
+/* A segment's star-tree v2 index (PC/startree/v2, StarTreeLoaderUtils.java:60-110): the tree as OffHeapStarTree
+ * reads it (little-endian: magic 0xBADDA55B00DAD00D, version 1, header size, (index, name) per dimension, node count,
+ * 7 int32 per node in BFS order: dimension id, dimension value (-1 = star), start doc, end doc, aggregated doc, first
+ * child, last child), and its documents as a segment descriptor: one dictionary column per split-order dimension
+ * named like the segment's column (the segment's own dictionary bytes, the star-tree's fixed-bit forward index at
+ * the segment column's bits per element, STAR stored as 0) and one raw column per function-column pair, named as
+ * AggregationFunctionColumnPair.toColumnName ("count__*" LONG; "sum__x", "min__x", "max__x" DOUBLE). Queries the
+ * tree fits (StarTreeUtils.isFitForStarTree: COUNT / SUM / MIN / MAX with their pairs, group-by and filter columns in
+ * the split order, no OR) then run on the star-tree (StarTreeFilterOperator's traversal + the pre-aggregated
+ * functions) when every queried segment has one; engine config startree.use=0 disables it (the reference's
+ * useStarTree=false debug option). */
+typedef struct {
+  const uint8_t *tree;
+  uint64_t tree_len;
+  const pinot_segment_desc *docs;
+} pinot_star_tree_desc;
+pinot_status pinot_gpu_segment_attach_star_tree(pinot_engine *engine, pinot_segment_handle handle,
+                                                const pinot_star_tree_desc *desc);
 pinot_status pinot_gpu_segment_device_bytes(pinot_engine *engine, pinot_segment_handle handle, uint64_t *out);
 
 /* Filter one segment: writes the dense doc bitset (bit d of word d/64 = doc d, LSB first;

@@ -161,6 +161,7 @@ void parse_config(Engine &e, const char *cfg) {
     else if (k == "exec.nt") e.use_nt = v == "1" || v == "true";
     else if (k == "exec.pipe") e.use_pipe = v == "1" || v == "true";
     else if (k == "stats.exact") e.stats_exact = v == "1" || v == "true";
+    else if (k == "startree.use") e.use_star_tree = v == "1" || v == "true";
     else if (k == "d2h.streams") {
       e.d2h_streams = std::stoi(v);
       require(e.d2h_streams >= 1 && e.d2h_streams <= 8, PINOT_ERR_BAD_ARG, "d2h.streams: 1 .. 8");
@@ -274,6 +275,18 @@ pinot_status pinot_gpu_segment_acquire(pinot_engine *engine, const char *index_d
     if (has_crc) engine->segment_cache[name] = {crc, h};
     *out = h;
     if (cache_hit) *cache_hit = 0;
+  });
+}
+
+pinot_status pinot_gpu_segment_attach_star_tree(pinot_engine *engine, pinot_segment_handle handle,
+                                                const pinot_star_tree_desc *desc) {
+  return guard([&] {
+    require(engine && desc, PINOT_ERR_BAD_ARG, "null argument");
+    std::lock_guard<std::mutex> lk(engine->mu);
+    set_device(*engine);
+    SegmentData &s = engine->seg(handle);
+    require(!s.star, PINOT_ERR_BAD_ARG, s.name + ": star-tree already attached");
+    attach_star_tree(*engine, s, *desc);
   });
 }
 

@@ -118,8 +118,23 @@ void read_segment_dir(const std::string &index_dir, SegmentDirData &out);
 bool read_segment_identity(const std::string &index_dir, std::string &name, int64_t &crc);
 uint64_t next_segment_uid();
 
+struct SegmentData;
+// A segment's star-tree v2 (startree.cpp): the tree (OffHeapStarTreeNode fields), the split order, the star docs as a
+// registered segment (dimension columns + metric columns) and the dimensions' dictIds on the host for the traversal's
+// remaining predicates.
+struct StarTreeNodeRec {
+  int32_t dim, value, start, end, agg, first, last;
+};
+struct StarTreeData {
+  std::vector<StarTreeNodeRec> nodes;
+  std::vector<std::string> dims;                  // split order
+  std::vector<std::vector<uint32_t>> host_dims;   // [dim][star doc] dictIds
+  std::unique_ptr<SegmentData> docs;
+};
+
 struct SegmentData {
   std::string name;
+  std::unique_ptr<StarTreeData> star;  // star-tree v2 index, when attached
   uint64_t uid = 0;                 // process-unique (never reused, unlike addresses): plan cache keys
   int32_t num_docs = 0;
   std::vector<std::unique_ptr<ColumnData>> cols;
@@ -200,6 +215,7 @@ struct Engine {
   std::string force_filter;   // "", "scan", "index": planner override for tests
   bool use_affine = true;     // agg.affine: arithmetic-progression dictionary SUM shortcut
   bool use_fused = true;      // exec.fused: one k_scan_query launch per aggregation query when the shape allows
+  bool use_star_tree = true;  // startree.use: star-tree plans for the queries a segment's tree fits
   bool stats_exact = false;   // stats.exact: numEntriesScannedInFilter replayed per the iterator protocol (host)
   bool use_nt = true;         // exec.nt: non-temporal policy on the streamed column DMA (measured: config-2
                               // k_scan_query 0.733 -> 0.702 ms)
@@ -364,6 +380,17 @@ std::unique_ptr<GroupByResult> exec_group_by_finalize(Engine &e, const std::vect
 
 // segments (segment.cpp)
 std::unique_ptr<SegmentData> register_segment(Engine &e, const pinot_segment_desc &d);
+// Star-tree v2 (startree.cpp): attach (parse + check + register the star docs), fit test, traversal.
+void attach_star_tree(Engine &e, SegmentData &seg, const pinot_star_tree_desc &d);
+bool star_tree_fits(const SegmentData &seg, const pinot_query &q);
+std::string star_pair_column(const pinot_agg_spec &a);  // "count__*", "sum__x", ... ("" when no pair exists)
+struct StarMatch {
+  bool empty = false;                  // a predicate matches nothing
+  std::vector<uint64_t> bits;          // matched star docs
+  int64_t docs = 0;
+  int64_t entries_in_filter = 0;       // remaining predicates' scanned entries (applyAnd over the bitmap answer)
+};
+StarMatch star_tree_match(const SegmentData &seg, const pinot_query &q, const FilterTreeInput *tree);
 std::unique_ptr<SegmentData> register_synthetic(Engine &e, const char *name, int32_t num_docs, int32_t ncols,
                                                 const char *const *names, const int32_t *cards, uint64_t seed,
                                                 const int32_t *kinds = nullptr);

@@ -1264,12 +1264,153 @@ void exec_aggregate_mv(Engine &e, const std::vector<SegmentData *> &segs, const 
 
 }  // namespace
 
+namespace {
+
+bool star_plan(const Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q) {
+  if (!e.use_star_tree) return false;
+  for (SegmentData *s : segs)
+    if (!star_tree_fits(*s, q)) return false;
+  return true;
+}
+
+// The star-tree plan's rewritten query: each function over its pre-aggregated pair column (COUNT sums count__*).
+struct StarQuery {
+  std::vector<std::string> names;
+  std::vector<pinot_agg_spec> specs;
+  pinot_query q{};
+};
+void star_query(const pinot_query &q, StarQuery &sq) {
+  sq.names.resize(q.num_aggregations);
+  sq.specs.assign(q.aggregations, q.aggregations + q.num_aggregations);
+  for (int a = 0; a < q.num_aggregations; a++) {
+    sq.names[a] = star_pair_column(q.aggregations[a]);
+    sq.specs[a].column = sq.names[a].c_str();
+    if (sq.specs[a].function == PINOT_AGG_COUNT) sq.specs[a].function = PINOT_AGG_SUM;
+  }
+  sq.q = q;
+  sq.q.aggregations = sq.specs.data();
+  sq.q.num_filter_nodes = 0;
+  sq.q.filter = nullptr;
+}
+
+void star_stats(const pinot_query &q2, const std::vector<SegmentData *> &segs, const std::vector<StarMatch> &m,
+                float ms, pinot_exec_stats *st) {
+  if (!st) return;
+  memset(st, 0, sizeof(*st));
+  for (size_t i = 0; i < segs.size(); i++) {
+    st->num_docs_scanned += m[i].docs;
+    st->num_entries_scanned_in_filter += m[i].entries_in_filter;
+    st->num_total_raw_docs += segs[i]->num_docs;
+    st->num_segments_matched += m[i].docs > 0;
+  }
+  // StarTreeProjectionPlanNode: the pair columns and the group-by dimensions
+  st->num_entries_scanned_post_filter = st->num_docs_scanned * projected_columns(q2);
+  st->num_segments_processed = (int64_t)segs.size();
+  st->device_ms = ms;
+}
+
+// Aggregation-only on the segments' star-trees (StarTreeAggregationExecutor): per segment the traversal's matched
+// star docs uploaded as a bitset, one k_mv_aggregate over the pair columns, merged in segment order.
+void exec_aggregate_star(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q,
+                         pinot_agg_result *out, pinot_exec_stats *stats) {
+  const int na = q.num_aggregations;
+  StarQuery sq;
+  star_query(q, sq);
+  std::unique_ptr<FilterTreeInput> tree;
+  if (q.num_filter_nodes > 0) tree = std::make_unique<FilterTreeInput>(decode_filter(q.num_filter_nodes, q.filter));
+  const size_t S = segs.size();
+  std::vector<StarMatch> m(S);
+  for (size_t si = 0; si < S; si++) m[si] = star_tree_match(*segs[si], q, tree.get());
+  constexpr size_t kOut = 5 * kMaxAggs * 8, kHll = kMaxAggs * 256 * 4;
+  e.fused_result.reserve(kOut + kHll + 64);
+  uint8_t *dev = e.fused_result.device<uint8_t>();
+  const uint8_t *host = e.fused_result.host<uint8_t>();
+  std::vector<unsigned long long> init(5 * kMaxAggs, 0ull);
+  for (int g = 0; g < kMaxAggs; g++) init[5 * g + 3] = ~0ull;
+  PINOT_HIP(hipEventRecord(e.ev_start, e.stream));
+  std::vector<std::vector<unsigned long long>> parts(S);
+  DeviceBuffer bits;
+  for (size_t si = 0; si < S; si++) {
+    if (m[si].empty || m[si].docs == 0) continue;
+    SegmentData &sd = *segs[si]->star->docs;
+    bits.reserve(m[si].bits.size() * 8 + 16);
+    PINOT_HIP(hipMemcpyAsync(bits.get(), m[si].bits.data(), m[si].bits.size() * 8, hipMemcpyHostToDevice, e.stream));
+    MvAggArgs a{};
+    a.bitset = bits.get<uint64_t>();
+    a.nwords = sd.nwords();
+    a.num_docs = sd.num_docs;
+    a.n = na;
+    for (int g = 0; g < na; g++) {
+      ColumnData &c = *sd.column(sq.names[g]);
+      MvAggSpec &sp = a.specs[g];
+      sp.fwd = c.fwd.get<uint8_t>();
+      sp.offsets = nullptr;
+      sp.dict = c.dict_dev.get();
+      sp.bits = c.bits;
+      sp.value_kind = c.value_kind();
+      sp.numeric = 1;
+      sp.kind = MVA_VALUES;
+    }
+    a.out = reinterpret_cast<unsigned long long *>(dev);
+    a.hll = reinterpret_cast<uint32_t *>(dev + kOut);
+    a.docs = reinterpret_cast<unsigned long long *>(dev + kOut + kHll);
+    PINOT_HIP(hipMemcpyAsync(dev, init.data(), kOut, hipMemcpyHostToDevice, e.stream));
+    PINOT_HIP(hipMemsetAsync(dev + kOut + kHll, 0, 8, e.stream));
+    launch_mv_aggregate(a, e.stream);
+    PINOT_HIP(hipGetLastError());
+    wait_stream(e);
+    parts[si].assign(reinterpret_cast<const unsigned long long *>(host),
+                     reinterpret_cast<const unsigned long long *>(host) + 5 * kMaxAggs);
+  }
+  PINOT_HIP(hipEventRecord(e.ev_stop, e.stream));
+  wait_stream(e);
+  float ms = 0;
+  PINOT_HIP(hipEventElapsedTime(&ms, e.ev_start, e.ev_stop));
+  auto decode_ordered_u64 = [](unsigned long long o) {
+    const unsigned long long u = (o & 0x8000000000000000ull) ? (o & ~0x8000000000000000ull) : ~o;
+    double d;
+    memcpy(&d, &u, 8);
+    return d;
+  };
+  for (int g = 0; g < na; g++) {
+    pinot_agg_result &r = out[g];
+    memset(&r, 0, sizeof(r));
+    const int f = q.aggregations[g].function;
+    int64_t isum = 0;
+    double dsum = 0.0, mn = INFINITY, mx = -INFINITY;
+    for (size_t si = 0; si < S; si++) {  // CombineService.mergeTwoBlocks, segment order
+      if (parts[si].empty()) continue;
+      const unsigned long long *o = parts[si].data() + 5 * g;
+      if (o[0] == 0) continue;
+      isum = (int64_t)((uint64_t)isum + o[1]);
+      double d;
+      memcpy(&d, &o[2], 8);
+      dsum += d;
+      mn = java_min(mn, decode_ordered_u64(o[3]));
+      mx = java_max(mx, decode_ordered_u64(o[4]));
+    }
+    switch (f) {
+      case PINOT_AGG_COUNT: r.count = isum; r.value = (double)isum; break;  // Σ count__*
+      case PINOT_AGG_SUM: r.value = dsum; break;                           // Σ sum__x (doubles)
+      case PINOT_AGG_MIN: r.value = mn; break;
+      default: r.value = mx; break;
+    }
+  }
+  star_stats(sq.q, segs, m, ms, stats);
+}
+
+}  // namespace
+
 void exec_aggregate(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q, pinot_agg_result *out,
                     pinot_exec_stats *stats) {
   const int na = q.num_aggregations;
   require(na >= 1 && na <= kMaxAggs, PINOT_ERR_UNSUPPORTED, "1..8 aggregation functions per query");
   if (touches_mv_aggregation(segs, q)) {
     exec_aggregate_mv(e, segs, q, out, stats);
+    return;
+  }
+  if (star_plan(e, segs, q)) {
+    exec_aggregate_star(e, segs, q, out, stats);
     return;
   }
   if (e.use_shortcut_plans && shortcut_aggregate(segs, q, out, stats)) return;
@@ -1725,7 +1866,8 @@ std::unique_ptr<GroupByResult> finalize_groups(Engine &e, const pinot_query &q, 
         const uint64_t raw = hacc[(size_t)a * n + i];
         switch (ak) {
           case 0:
-          case 6: vv[i] = (double)(int64_t)raw; break;
+          case 6:
+          case 7: vv[i] = (double)(int64_t)raw; break;
           case 1: { double d; memcpy(&d, &raw, 8); vv[i] = d; break; }
           case 2:
           case 3: vv[i] = decode_ordered(raw); break;
@@ -3090,6 +3232,108 @@ std::unique_ptr<GroupByResult> exec_group_by_mv(Engine &e, const std::vector<Seg
   return res;
 }
 
+// Group-by on the segments' star-trees (StarTreeGroupByExecutor): the traversal's matched star docs per segment, then
+// k_group_by_mv over the star docs' dimension columns (the segment's dictionaries, so the global key space and its
+// remaps are the segments' own) with each function over its pair column; COUNT is Σ count__* per group (exact int64).
+// Runs while the key space fits num.groups.limit (no admission); otherwise the caller takes the regular plan.
+std::unique_ptr<GroupByResult> exec_group_by_star(Engine &e, const std::vector<SegmentData *> &segs,
+                                                  const pinot_query &q, pinot_exec_stats *stats) {
+  const int na = q.num_aggregations;
+  KeySpace ks = build_key_space(segs, q);
+  const int64_t limit = q.num_groups_limit > 0 ? q.num_groups_limit : e.num_groups_limit;
+  if (ks.hashed || ks.G > limit) return nullptr;
+  StarQuery sq;
+  star_query(q, sq);
+  std::unique_ptr<FilterTreeInput> tree;
+  if (q.num_filter_nodes > 0) tree = std::make_unique<FilterTreeInput>(decode_filter(q.num_filter_nodes, q.filter));
+  const size_t S = segs.size();
+  std::vector<StarMatch> m(S);
+  for (size_t si = 0; si < S; si++) m[si] = star_tree_match(*segs[si], q, tree.get());
+  GroupAccs ga;
+  for (int a = 0; a < na; a++) {
+    const ColumnData &c = *segs[0]->star->docs->column(sq.names[a]);
+    const int f = q.aggregations[a].function;
+    ga.acc_kind.push_back(f == PINOT_AGG_COUNT ? (c.value_kind() == 2 ? 1 : 7)
+                          : f == PINOT_AGG_MIN ? 2 : f == PINOT_AGG_MAX ? 3 : (c.value_kind() == 0 ? 0 : 1));
+    ga.acc_bytes_per_key.push_back(8);
+  }
+  for (int a = 0; a < na; a++)  // an int64 SUM needs an int64 dictionary (kind 7) or an int32 one (kind 0)
+    if (ga.acc_kind[a] == 1 && q.aggregations[a].function == PINOT_AGG_SUM) {
+      const ColumnData &c = *segs[0]->star->docs->column(sq.names[a]);
+      if (c.value_kind() == 1) ga.acc_kind[a] = 7;
+    }
+  const size_t per_key = 8 + 8 * (size_t)na;
+  e.group_scratch.reserve(ks.G * per_key + 64);
+  uint8_t *base = e.group_scratch.get<uint8_t>();
+  auto *counts = reinterpret_cast<unsigned long long *>(base);
+  std::vector<void *> accs(na, nullptr);
+  for (int a = 0; a < na; a++) accs[a] = base + ks.G * 8 * (1 + a);
+  PINOT_HIP(hipEventRecord(e.ev_start, e.stream));
+  init_accs(e, ks.G, counts, ga, accs.data());
+  std::vector<DeviceBuffer> remaps(S * q.num_group_by);
+  std::vector<DeviceBuffer> bits(S);
+  for (size_t si = 0; si < S; si++) {
+    if (m[si].empty || m[si].docs == 0) continue;
+    SegmentData &sd = *segs[si]->star->docs;
+    bits[si].alloc(m[si].bits.size() * 8 + 16);
+    PINOT_HIP(hipMemcpyAsync(bits[si].get(), m[si].bits.data(), m[si].bits.size() * 8, hipMemcpyHostToDevice,
+                             e.stream));
+    MvGroupArgs a{};
+    a.n_gcols = q.num_group_by;
+    a.n_aggs = na;
+    long long stride = 1;
+    for (int j = 0; j < q.num_group_by; j++) {
+      const ColumnData &c = *sd.column(q.group_by[j]);
+      a.gfwd[j] = c.fwd.get<uint8_t>();
+      a.goff[j] = nullptr;
+      a.gbits[j] = c.bits;
+      const auto &rm = ks.remap[si][j];
+      if (!rm.empty()) {
+        DeviceBuffer &rb = remaps[si * q.num_group_by + j];
+        rb.alloc(rm.size() * 4 + 16);
+        PINOT_HIP(hipMemcpyAsync(rb.get(), rm.data(), rm.size() * 4, hipMemcpyHostToDevice, e.stream));
+        a.remap[j] = rb.get<int32_t>();
+      }
+      a.stride[j] = stride;
+      stride *= ks.gcard[j];
+    }
+    for (int g = 0; g < na; g++) {
+      ColumnData &c = *sd.column(sq.names[g]);
+      a.acc_kind[g] = ga.acc_kind[g];
+      a.acc[g] = accs[g];
+      a.afwd[g] = c.fwd.get<uint8_t>();
+      a.aoff[g] = nullptr;
+      a.abits[g] = c.bits;
+      a.dict[g] = c.dict_dev.get();
+      a.value_kind[g] = c.value_kind();
+    }
+    a.counts = counts;
+    a.bitset = bits[si].get<uint64_t>();
+    a.nwords = sd.nwords();
+    a.num_docs = sd.num_docs;
+    launch_group_by_mv(a, e.stream);
+    PINOT_HIP(hipGetLastError());
+  }
+  GroupByProgram gp{};
+  gp.n_aggs = na;
+  gp.counts = counts;
+  for (int a = 0; a < na; a++) { gp.acc[a] = accs[a]; gp.acc_kind[a] = ga.acc_kind[a]; }
+  auto res = finalize_groups(e, sq.q, ga, ks, gp);
+  PINOT_HIP(hipEventRecord(e.ev_stop, e.stream));
+  wait_stream(e);
+  float ms = 0;
+  PINOT_HIP(hipEventElapsedTime(&ms, e.ev_start, e.ev_stop));
+  for (int a = 0; a < na; a++) {
+    res->functions[a] = q.aggregations[a].function;
+    if (q.aggregations[a].function != PINOT_AGG_COUNT) continue;
+    HostVec<int64_t> &cv = res->counts[a];  // COUNT: the groups' Σ count__*
+    const HostVec<double> &v = res->values[a];
+    for (size_t i = 0; i < cv.size(); i++) cv[i] = (int64_t)v[i];
+  }
+  star_stats(sq.q, segs, m, ms, stats);
+  return res;
+}
+
 }  // namespace
 
 std::unique_ptr<GroupByResult> exec_group_by(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q,
@@ -3098,6 +3342,10 @@ std::unique_ptr<GroupByResult> exec_group_by(Engine &e, const std::vector<Segmen
   require(na >= 1 && na <= kMaxAggs, PINOT_ERR_UNSUPPORTED, "1..8 aggregation functions per query");
   require(q.num_group_by >= 1 && q.num_group_by <= kMaxGroupCols, PINOT_ERR_UNSUPPORTED, "1..16 group-by columns");
   if (touches_mv_group_by(segs, q)) return exec_group_by_mv(e, segs, q, stats);
+  if (star_plan(e, segs, q)) {
+    auto r = exec_group_by_star(e, segs, q, stats);
+    if (r) return r;
+  }
   if (e.use_fused) {
     KeySpace ks = build_key_space(segs, q);
     GroupAccs ga = group_acc_kinds(*segs[0], q);

@@ -456,7 +456,7 @@ struct MvGroupArgs {
   const void *dict[kMaxAggs];
   const uint16_t *hll_lut[kMaxAggs];
   int32_t acc_kind[kMaxAggs];   // 0 i64 sum (INT), 1 f64 sum, 2 ordered min, 3 ordered max, 4 HLL u32[256], 5 none,
-                                // 6 entry count
+                                // 6 entry count, 7 i64 sum (int64 dictionary)
   int32_t value_kind[kMaxAggs];
   unsigned long long *counts;
   void *acc[kMaxAggs];

@@ -363,6 +363,10 @@ __device__ __forceinline__ void mv_fold(const MvGroupArgs &a, int g, long long k
         atomicMax(static_cast<uint32_t *>(a.acc[g]) + key * 256 + (h >> 8), h & 0xFFu);
         break;
       }
+      case 7:  // exact int64 sum over an int64 dictionary (a star-tree's count__* column)
+        atomicAdd(static_cast<unsigned long long *>(a.acc[g]) + key,
+                  (unsigned long long)static_cast<const long long *>(a.dict[g])[id]);
+        break;
       default: break;
     }
   }

@@ -34,7 +34,8 @@ EXPORTED_SYMBOLS = [
     "pinot_gpu_last_error", "pinot_gpu_abi_version", "pinot_gpu_device_count",
     "pinot_gpu_engine_create", "pinot_gpu_engine_destroy", "pinot_gpu_engine_set_config",
     "pinot_gpu_segment_register", "pinot_gpu_segment_release", "pinot_gpu_segment_validate",
-    "pinot_gpu_segment_load", "pinot_gpu_segment_acquire", "pinot_gpu_segment_dir_info",
+    "pinot_gpu_segment_load", "pinot_gpu_segment_acquire", "pinot_gpu_segment_attach_star_tree",
+    "pinot_gpu_segment_dir_info",
     "pinot_gpu_segment_device_bytes", "pinot_gpu_filter", "pinot_gpu_aggregate", "pinot_gpu_group_by",
     "pinot_groupby_num_groups", "pinot_groupby_num_columns", "pinot_groupby_key", "pinot_groupby_values",
     "pinot_groupby_hll", "pinot_groupby_raw_keys", "pinot_groupby_export_keys", "pinot_groupby_trim",
@@ -73,6 +74,10 @@ class ColumnDesc(C.Structure):
 class SegmentDesc(C.Structure):
     _fields_ = [("name", C.c_char_p), ("num_docs", C.c_int32), ("num_columns", C.c_int32),
                 ("columns", C.POINTER(ColumnDesc))]
+
+
+class StarTreeDesc(C.Structure):
+    _fields_ = [("tree", C.c_void_p), ("tree_len", C.c_uint64), ("docs", C.POINTER(SegmentDesc))]
 
 
 class FilterNode(C.Structure):
@@ -168,6 +173,7 @@ def load(path=None):
         "pinot_gpu_segment_validate": (i32, [C.POINTER(SegmentDesc)]),
         "pinot_gpu_segment_load": (i32, [P, C.c_char_p, C.POINTER(i64)]),
         "pinot_gpu_segment_acquire": (i32, [P, C.c_char_p, C.POINTER(i64), C.POINTER(i32)]),
+        "pinot_gpu_segment_attach_star_tree": (i32, [P, i64, C.POINTER(StarTreeDesc)]),
         "pinot_gpu_segment_dir_info": (i32, [C.c_char_p, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32)]),
         "pinot_gpu_segment_device_bytes": (i32, [P, i64, C.POINTER(u64)]),
         "pinot_gpu_filter": (i32, [P, i64, i32, C.POINTER(FilterNode), P, C.POINTER(i64)]),

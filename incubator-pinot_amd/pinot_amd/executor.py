@@ -70,6 +70,29 @@ class GpuSegment:
         check(self.engine.lib.pinot_gpu_segment_device_bytes(self.engine.ptr, self.handle, C.byref(out)))
         return out.value
 
+    def attach_star_tree(self, segment: Segment, tree_bytes: bytes, dimensions, dims, metrics):
+        """pinot_gpu_segment_attach_star_tree: the segment's star-tree v2 — the OffHeapStarTree bytes, the split-order
+        dimensions' star-doc dictIds (int [num_star_docs, num_dims], STAR as 0; encoded with the segment's
+        dictionaries) and the pair columns {"count__*": int64, "sum__x" / "min__x" / "max__x": float64}."""
+        from .segment import Column, Segment as Seg, build_column, pack_fixed_bit
+        n = int(np.asarray(dims).shape[0])
+        cols = {}
+        for j, d in enumerate(dimensions):
+            pc = segment.column(d)
+            cols[d] = Column(name=d, data_type=pc.data_type, cardinality=pc.cardinality, bits=pc.bits,
+                             is_sorted=False, has_inverted_index=False, num_docs=n, dictionary=pc.dictionary,
+                             string_width=pc.string_width, fwd=pack_fixed_bit(np.asarray(dims)[:, j], pc.bits),
+                             padding=pc.padding)
+        for name, vals in metrics.items():
+            v = np.asarray(vals)
+            cols[name] = build_column(name, v, "LONG" if v.dtype.kind in "iu" else "DOUBLE", raw=True)
+        docs = Seg(name=segment.name + "$startree", num_docs=n, columns=cols)
+        desc, keep = segment_desc(docs)
+        tb = C.create_string_buffer(bytes(tree_bytes), len(tree_bytes))
+        sd = _lib.StarTreeDesc(C.cast(tb, C.c_void_p), len(tree_bytes), C.pointer(desc))
+        check(self.engine.lib.pinot_gpu_segment_attach_star_tree(self.engine.ptr, self.handle, C.byref(sd)))
+        del keep
+
     def release(self):
         if self.handle is not None:
             check(self.engine.lib.pinot_gpu_segment_release(self.engine.ptr, self.handle))

@@ -1,0 +1,80 @@
+"""Star-tree v2 plans on the GPU (pinot_gpu_segment_attach_star_tree): queries the tree fits run on the star docs —
+host traversal, device aggregation / group-by over the pair columns — and equal the oracle's star-tree plan
+(results and numDocsScanned) and the scan plan; startree.use=0 and non-fitting queries take the regular plan."""
+import numpy as np
+import pytest
+
+import pinot_oracle as O
+import startree as S
+from pinot_amd import GpuEngine, ServerQueryExecutor
+from startree_writer import build_star_tree
+from test_startree import DIMS, PAIRS, _same, random_query, st_segment
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def engine():
+    e = GpuEngine(0)
+    yield e
+    e.close()
+
+
+def _attach(engine, seg, leaf=10, skip=()):
+    st = build_star_tree(seg, DIMS, PAIRS, max_leaf_records=leaf, skip_star=skip)
+    g = engine.register(seg)
+    g.attach_star_tree(seg, st.tree_bytes, st.dimensions, st.dims, st.metrics)
+    return g, st
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_star_tree_plans(engine, seed):
+    rng = np.random.default_rng(1600 + seed)
+    segs = [st_segment(rng, int(rng.choice([50, 2000, 20000])), name="st%d" % i) for i in range(1 + seed % 2)]
+    attached = [_attach(engine, s, leaf=[1, 10, 100, 5000][seed]) for s in segs]
+    gs, sts = [a[0] for a in attached], [a[1] for a in attached]
+    ex = ServerQueryExecutor(engine)
+    for it in range(16):
+        group = [None, ["a"], ["b", "c"], ["c", "a", "b"]][it % 4]
+        q = random_query(rng, segs[0], group)
+        got, st = ex.process_query(q, gs, trim=False)
+        exp, scanned = S.execute_server(segs, sts, q)
+        _same(q, got, exp)
+        assert st.num_docs_scanned == scanned, q
+        scan, _ = O.execute_server(segs, q)
+        _same(q, got, scan)
+    engine.set_config("startree.use=0")
+    try:
+        q = random_query(rng, segs[0], ["a"])
+        got, st = ex.process_query(q, gs, trim=False)
+        exp, scanned = O.execute_server(segs, q)
+        _same(q, got, exp)
+        assert st.num_docs_scanned == scanned
+    finally:
+        engine.set_config("startree.use=1")
+    # a function without a pair (AVG) runs the regular plan
+    q = {"aggregations": [{"function": "AVG", "column": "m"}, {"function": "COUNT", "column": "*"}],
+         "filter": {"operator": "EQUALITY", "column": "a", "values": ["1"]}, "group_by": None}
+    got, st = ex.process_query(q, gs)
+    exp, scanned = O.execute_server(segs, q)
+    assert got[1] == exp[1] and got[0].count == exp[0][1] and st.num_docs_scanned == scanned
+    for g in gs:
+        g.release()
+
+
+def test_star_tree_attach_checks(engine):
+    from pinot_amd import PinotGpuError
+    rng = np.random.default_rng(1700)
+    seg = st_segment(rng, 300)
+    st = build_star_tree(seg, DIMS, PAIRS, max_leaf_records=5)
+    g = engine.register(seg)
+    bad = bytearray(st.tree_bytes)
+    bad[0] ^= 0xFF
+    with pytest.raises(PinotGpuError, match="magic"):
+        g.attach_star_tree(seg, bytes(bad), st.dimensions, st.dims, st.metrics)
+    with pytest.raises(PinotGpuError, match="size"):
+        g.attach_star_tree(seg, st.tree_bytes[:-4], st.dimensions, st.dims, st.metrics)
+    g.attach_star_tree(seg, st.tree_bytes, st.dimensions, st.dims, st.metrics)
+    with pytest.raises(PinotGpuError, match="already"):
+        g.attach_star_tree(seg, st.tree_bytes, st.dimensions, st.dims, st.metrics)
+    g.release()

@@ -162,6 +162,7 @@ void parse_config(Engine &e, const char *cfg) {
     else if (k == "exec.pipe") e.use_pipe = v == "1" || v == "true";
     else if (k == "stats.exact") e.stats_exact = v == "1" || v == "true";
     else if (k == "startree.use") e.use_star_tree = v == "1" || v == "true";
+    else if (k == "d2h.compact") e.compact_d2h = v == "1" || v == "true";
     else if (k == "d2h.streams") {
       e.d2h_streams = std::stoi(v);
       require(e.d2h_streams >= 1 && e.d2h_streams <= 8, PINOT_ERR_BAD_ARG, "d2h.streams: 1 .. 8");

@@ -201,6 +201,8 @@ struct Engine {
   int device = 0;
   hipStream_t stream = nullptr;
   // result D2H fan-out (d2h.streams): the group-by result arrays copied on parallel streams (one SDMA queue each)
+  bool compact_d2h = true;    // d2h.compact: config-4-sized group-by results read back as key bitmap + u32 arrays
+  PinnedBuffer compact_host;  // its host staging
   int d2h_streams = 1;         // measured on config 4: 1 / 2 / 4 streams all ~1.15 ms for 32 MB (PCIe-bound)
   std::vector<hipStream_t> copy_streams;
   hipEvent_t ev_copy = nullptr;
@@ -317,6 +319,14 @@ struct DenseOut {
   std::vector<long long *> cards;
   std::shared_ptr<DeviceBuffer> hll;
   std::vector<size_t> hll_off;
+  // compact read-back (dense, non-hashed key spaces of >= 64 K groups): the non-empty keys as a bitmap over [0, G),
+  // counts and HLL cardinalities as u32 (overflow flag -> the 64-bit arrays), widened on the host
+  const uint64_t *key_bits = nullptr;
+  int64_t key_words = 0;
+  long long key_base = 0;
+  unsigned int *counts32 = nullptr;
+  std::vector<unsigned int *> cards32;
+  unsigned int *overflow = nullptr;
 };
 
 // The single-value function whose intermediate result / merge / final result a multi-value function shares

@@ -2518,7 +2518,11 @@ DenseOut dense_outputs(Engine &e, const DenseGroups &d, const long long *keys_de
     n_hll += gx.acc_kind[i] == 4;
   }
   const size_t n8 = n * 8;
-  e.group_out.reserve(n8 * (2 + na + n_card) + 256);
+  // compact read-back: keys as a bitmap over [0, G), counts / cardinalities as u32 (half the PCIe bytes)
+  const bool compact = e.compact_d2h && !d.hashed && n >= (1u << 16) && d.ks->G > 0;
+  const size_t key_words = compact ? (size_t)((d.ks->G + 63) / 64) : 0;
+  const size_t compact_bytes = compact ? key_words * 8 + n * 4 * (1 + n_card) + 64 : 0;
+  e.group_out.reserve(n8 * (2 + na + n_card) + 256 + compact_bytes);
   GroupFinalArgs f{};
   f.n = na;
   f.out_keys = e.group_out.get<long long>();
@@ -2544,6 +2548,28 @@ DenseOut dense_outputs(Engine &e, const DenseGroups &d, const long long *keys_de
   o.counts = f.out_counts;
   o.values.assign(f.out_values, f.out_values + na);
   o.cards.assign(f.out_card, f.out_card + na);
+  o.cards32.assign(na, nullptr);
+  if (compact) {
+    uint8_t *cb = reinterpret_cast<uint8_t *>(f.out_counts + n) + n8 * (na + n_card);
+    cb = reinterpret_cast<uint8_t *>(((uintptr_t)cb + 15) & ~(uintptr_t)15);
+    uint64_t *kb = reinterpret_cast<uint64_t *>(cb);
+    f.overflow = reinterpret_cast<unsigned int *>(kb + key_words);
+    f.out_counts32 = f.overflow + 4;
+    unsigned int *c32 = f.out_counts32 + n;
+    for (int i = 0; i < na; i++)
+      if (ga.acc_kind[i] == 4) {
+        f.out_card32[i] = c32;
+        c32 += n;
+      }
+    PINOT_HIP(hipMemsetAsync(f.overflow, 0, 4, e.stream));
+    launch_key_bitmap(d.counts, d.ks->G, kb, e.stream);
+    o.key_bits = kb;
+    o.key_words = (int64_t)key_words;
+    o.key_base = d.key_base;
+    o.counts32 = f.out_counts32;
+    o.cards32.assign(f.out_card32, f.out_card32 + na);
+    o.overflow = f.overflow;
+  }
   launch_group_final(d.counts, keys_dev, (long long)n, f, e.stream);
   PINOT_HIP(hipGetLastError());
   if (n_hll) {  // registers stay on the device until asked for; buffers are recycled once their result is released
@@ -2567,6 +2593,70 @@ DenseOut dense_outputs(Engine &e, const DenseGroups &d, const long long *keys_de
     PINOT_HIP(hipGetLastError());
   }
   return o;
+}
+
+// The compact read-back: the key bitmap, u32 counts / cardinalities and the values straight into the result arrays,
+// then the keys listed and the u32 arrays widened over the host threads. False (nothing filled) when a count or a
+// cardinality did not fit 32 bits: the caller then reads the 64-bit arrays.
+bool compact_fetch(Engine &e, GroupByResult *res, const DenseOut &o, int na) {
+  const unsigned long long n = o.n;
+  const size_t n8 = n * 8;
+  e.compact_host.reserve((size_t)o.key_words * 8 + n * 4 * (1 + na) + 64);
+  uint8_t *h = e.compact_host.get<uint8_t>();
+  uint64_t *hbits = reinterpret_cast<uint64_t *>(h);
+  unsigned int *hover = reinterpret_cast<unsigned int *>(hbits + o.key_words);
+  unsigned int *hc32 = hover + 4;
+  std::vector<unsigned int *> hcard(na, nullptr);
+  unsigned int *p = hc32 + n;
+  for (int i = 0; i < na; i++)
+    if (o.cards32[i]) {
+      hcard[i] = p;
+      p += n;
+    }
+  PINOT_HIP(hipMemcpyAsync(hbits, o.key_bits, (size_t)o.key_words * 8, hipMemcpyDeviceToHost, e.stream));
+  PINOT_HIP(hipMemcpyAsync(hover, o.overflow, 4, hipMemcpyDeviceToHost, e.stream));
+  PINOT_HIP(hipMemcpyAsync(hc32, o.counts32, n * 4, hipMemcpyDeviceToHost, e.stream));
+  for (int i = 0; i < na; i++) {
+    if (o.derive[i] == -1) PINOT_HIP(hipMemcpyAsync(res->values[i].data(), o.values[i], n8, hipMemcpyDeviceToHost, e.stream));
+    if (hcard[i]) PINOT_HIP(hipMemcpyAsync(hcard[i], o.cards32[i], n * 4, hipMemcpyDeviceToHost, e.stream));
+  }
+  wait_stream(e);
+  if (*hover) return false;
+  const size_t nt = host_threads();
+  const size_t W = (size_t)o.key_words;
+  std::vector<size_t> base(nt + 1, 0);
+  parallel_tasks(nt, [&](size_t t) {  // set bits per word range
+    size_t c = 0;
+    for (size_t w = W * t / nt; w < W * (t + 1) / nt; w++) c += __builtin_popcountll(hbits[w]);
+    base[t + 1] = c;
+  });
+  for (size_t t = 0; t < nt; t++) base[t + 1] += base[t];
+  require(base[nt] == n, PINOT_ERR_DEVICE, "key bitmap disagrees with the compacted key count");
+  int64_t *keys = res->raw_keys.data();
+  parallel_tasks(nt, [&](size_t t) {
+    size_t i = base[t];
+    for (size_t w = W * t / nt; w < W * (t + 1) / nt; w++)
+      for (uint64_t x = hbits[w]; x; x &= x - 1) keys[i++] = (int64_t)(w * 64 + __builtin_ctzll(x)) + o.key_base;
+    const size_t lo = n * t / nt, hi = n * (t + 1) / nt;
+    int64_t *cv = res->counts[0].data();
+    for (size_t g = lo; g < hi; g++) cv[g] = hc32[g];
+    for (int f = 0; f < na; f++) {
+      if (!hcard[f]) continue;
+      int64_t *card = res->hll_card[f].data();
+      for (size_t g = lo; g < hi; g++) card[g] = hcard[f][g];
+    }
+    for (int f = 0; f < na; f++) {
+      if (o.derive[f] == -1) continue;
+      double *v = res->values[f].data();
+      if (o.derive[f] == -2) {
+        const int64_t *c = res->hll_card[f].data();
+        for (size_t g = lo; g < hi; g++) v[g] = (double)c[g];
+      } else {
+        memcpy(v + lo, res->values[o.derive[f]].data() + lo, (hi - lo) * 8);
+      }
+    }
+  });
+  return true;
 }
 
 // Host half: one D2H per array straight into the (pinned, pooled) result arrays — only what the host cannot
@@ -2626,6 +2716,13 @@ std::unique_ptr<GroupByResult> dense_fetch(Engine &e, const pinot_query &q, cons
   }
   const auto tb1 = std::chrono::steady_clock::now();
   const size_t n8 = n * 8;
+  if (o.key_bits && compact_fetch(e, res.get(), o, na)) {
+    if (e.host_phases)
+      fprintf(stderr, "[pinot_gpu] group-by outputs (us): sizing %.1f, compact D2H + widen %.1f\n",
+              std::chrono::duration<double, std::micro>(tb1 - tb0).count(),
+              std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tb1).count());
+    return res;
+  }
   // the arrays' D2H copies fanned out over d2h.streams streams (each its own copy queue), all after the final-array
   // kernels: one queue alone leaves PCIe half idle on a 32 MB result
   std::vector<std::pair<void *, const void *>> copies;

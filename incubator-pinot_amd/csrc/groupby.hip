@@ -246,10 +246,15 @@ __global__ void k_group_final(const unsigned long long *__restrict__ counts, con
     const unsigned long long c = counts[k];
     f.out_keys[i] = k + f.key_base;
     f.out_counts[i] = (long long)c;
+    if (f.out_counts32) {
+      f.out_counts32[i] = (unsigned int)c;
+      if (c >> 32) atomicOr(f.overflow, 1u);
+    }
     for (int g = 0; g < f.n; g++) {
       double v;
       switch (f.kind[g]) {
-        case 0: v = (double)static_cast<const long long *>(f.acc[g])[k]; break;
+        case 0:
+        case 7: v = (double)static_cast<const long long *>(f.acc[g])[k]; break;
         case 1: v = static_cast<const double *>(f.acc[g])[k]; break;
         case 2:
         case 3: v = decode_ordered_d(static_cast<const unsigned long long *>(f.acc[g])[k]); break;
@@ -276,6 +281,10 @@ __global__ void k_group_final(const unsigned long long *__restrict__ counts, con
           if (estimate <= 640.0) x = f.linear[z];
           const long long card = isinf(x) ? 0x7FFFFFFFFFFFFFFFll : (long long)floor(x + 0.5);
           f.out_card[g][i] = card;
+          if (f.out_card32[g]) {
+            f.out_card32[g][i] = (unsigned int)card;
+            if ((unsigned long long)card >> 32) atomicOr(f.overflow, 1u);
+          }
           v = (double)card;
           break;
         }
@@ -432,6 +441,24 @@ __global__ void k_admit_bitmap(const uint32_t *__restrict__ first_doc, long long
 }
 
 }  // namespace
+
+__global__ void k_key_bitmap(const unsigned long long *__restrict__ counts, long long G, uint64_t *bits) {
+  const long long nw = (G + 63) / 64;
+  const int lane = threadIdx.x & 63;
+  for (long long w = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6; w < nw;
+       w += ((long long)gridDim.x * blockDim.x) >> 6) {
+    const long long k = w * 64 + lane;
+    const uint64_t word = __ballot(k < G && counts[k] != 0);
+    if (lane == 0) bits[w] = word;
+  }
+}
+
+void launch_key_bitmap(const unsigned long long *counts, long long G, uint64_t *bits, hipStream_t stream) {
+  if (G <= 0) return;
+  const long long nw = (G + 63) / 64;
+  const int grid = (int)std::min<long long>((nw * 64 + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_key_bitmap, dim3(grid), dim3(256), 0, stream, counts, G, bits);
+}
 
 void launch_group_final(const unsigned long long *counts, const long long *keys, long long n, const GroupFinalArgs &f,
                         hipStream_t stream) {

@@ -378,7 +378,13 @@ struct GroupFinalArgs {
   long long key_base;
   double alpha_mm;
   const double *linear;  // device copy of m * log(m / z), z = 0..256 (z = 0: +inf)
+  // compact read-back (optional): counts and cardinalities also as u32, *overflow set when one does not fit
+  unsigned int *out_counts32;
+  unsigned int *out_card32[kMaxGroupAggs];
+  unsigned int *overflow;
 };
+// bit k of bits[k >> 6] = counts[k] != 0 (the non-empty keys the compaction lists, as a bitmap)
+void launch_key_bitmap(const unsigned long long *counts, long long G, uint64_t *bits, hipStream_t stream);
 void launch_group_final(const unsigned long long *counts, const long long *keys, long long n, const GroupFinalArgs &f,
                         hipStream_t stream);
 // num.groups.limit admission (DictionaryBasedGroupKeyGenerator IntMapBasedHolder.getGroupId, first appearance):

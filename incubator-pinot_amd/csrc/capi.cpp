@@ -239,6 +239,11 @@ int64_t load_segment_dir(Engine &engine, const char *index_dir) {
       c.max_value = c.string_value(c.card - 1);
     }
   }
+  if (files.has_star) {  // StarTreeLoaderUtils: the segment's star-tree, attached like pinot_gpu_segment_attach_star_tree
+    const pinot_segment_desc docs = files.star_desc();
+    pinot_star_tree_desc sd{files.star_tree, files.star_tree_len, &docs};
+    attach_star_tree(engine, *seg, sd);
+  }
   const int64_t h = engine.next_handle++;
   engine.segments[h] = std::move(seg);
   return h;

@@ -112,6 +112,14 @@ struct SegmentDirData {
   std::deque<std::vector<int32_t>> ints;    // partition values the descriptors point at
   std::string time_column;                  // segment.time.column.name
   pinot_segment_desc desc() const;
+  // star-tree v2 index (the first tree, startree.v2.0.*): the tree bytes and the star docs' columns
+  bool has_star = false;
+  const uint8_t *star_tree = nullptr;
+  uint64_t star_tree_len = 0;
+  int32_t star_num_docs = 0;
+  std::vector<pinot_column_desc> star_cols;
+  std::deque<std::string> star_names;
+  pinot_segment_desc star_desc() const;
 };
 void read_segment_dir(const std::string &index_dir, SegmentDirData &out);
 // segment.name (metadata.properties) and creation.meta's CRC (false when the directory has no creation.meta)

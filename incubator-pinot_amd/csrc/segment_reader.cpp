@@ -395,6 +395,8 @@ bool read_segment_identity(const std::string &index_dir, std::string &name, int6
   return true;
 }
 
+void read_star_tree(const std::string &dir, const std::map<std::string, std::string> &kv, SegmentDirData &out);
+
 void read_segment_dir(const std::string &index_dir, SegmentDirData &out) {
   require(is_dir(index_dir), PINOT_ERR_BAD_ARG, "not a segment directory: " + index_dir);
   const std::string v3 = index_dir + "/v3";
@@ -572,6 +574,81 @@ void read_segment_dir(const std::string &index_dir, SegmentDirData &out) {
     out.cols.push_back(d);
   }
   for (size_t i = 0; i < out.cols.size(); i++) out.cols[i].name = out.column_names[i].c_str();
+  read_star_tree(dir, kv, out);
+}
+
+// Star-tree v2 files (StarTreeLoaderUtils.java:60-110, StarTreeIndexMapUtils.java): star_tree_index (the combined
+// tree + forward indexes) located by star_tree_index_map ("<tree>.<column>.<STAR_TREE|FORWARD_INDEX>.<OFFSET|SIZE>",
+// the tree's column "null"), described by metadata.properties' startree.v2.* keys (StarTreeV2Metadata: total.docs,
+// split.order, function.column.pairs). Dimension forward indexes are fixed-bit at the segment column's bits;
+// the pair columns are FixedByteChunk raw indexes (LONG for count, DOUBLE otherwise). Only the first tree is read.
+void read_star_tree(const std::string &dir, const std::map<std::string, std::string> &kv, SegmentDirData &out) {
+  if (!kv.count("startree.v2.count") || prop_int(kv, "startree.v2.count") < 1) return;
+  const std::string pre = "startree.v2.0.";
+  const int64_t ndocs = prop_int(kv, pre + "total.docs");
+  require(ndocs >= 1 && ndocs < INT32_MAX, PINOT_ERR_BAD_ARG, "star-tree total.docs out of range");
+  const std::string idx_path = dir + "/star_tree_index", map_path = dir + "/star_tree_index_map";
+  require(is_file(idx_path) && is_file(map_path), PINOT_ERR_BAD_ARG, "star-tree index files missing in " + dir);
+  out.files.emplace_back(new MappedFile(idx_path));
+  const MappedFile &f = *out.files.back();
+  const auto imap = parse_properties(read_text(map_path));
+  auto range = [&](const std::string &col, const std::string &type, const uint8_t **p, uint64_t *n) {
+    const std::string k = "0." + col + "." + type + ".";
+    require(imap.count(k + "OFFSET") && imap.count(k + "SIZE"), PINOT_ERR_BAD_ARG, "star-tree index map lacks " + k);
+    const int64_t o = prop_int(imap, k + "OFFSET"), sz = prop_int(imap, k + "SIZE");
+    require(o >= 0 && sz >= 0 && (uint64_t)(o + sz) <= f.size, PINOT_ERR_BAD_ARG, "star-tree " + k + " outside star_tree_index");
+    *p = f.data + o;
+    *n = (uint64_t)sz;
+  };
+  range("null", "STAR_TREE", &out.star_tree, &out.star_tree_len);
+  out.star_num_docs = (int32_t)ndocs;
+  for (const std::string &dim : prop_list(kv, pre + "split.order")) {
+    size_t ci = 0;
+    while (ci < out.column_names.size() && out.column_names[ci] != dim) ci++;
+    require(ci < out.column_names.size(), PINOT_ERR_BAD_ARG, "star-tree dimension " + dim + " is not a served column");
+    pinot_column_desc d = out.cols[ci];  // the segment column: its dictionary, its bits
+    d.is_sorted = 0;
+    d.has_inverted_index = 0;
+    d.inverted_index = nullptr;
+    d.inverted_index_len = 0;
+    d.sorted_index = nullptr;
+    d.sorted_index_len = 0;
+    d.bloom_filter = nullptr;
+    d.bloom_filter_len = 0;
+    d.create_bloom_filter = 0;
+    d.min_value = d.max_value = nullptr;
+    d.partition_function = nullptr;
+    d.num_partitions = 0;
+    d.partition_values = nullptr;
+    d.num_partition_values = 0;
+    range(dim, "FORWARD_INDEX", &d.forward_index, &d.forward_index_len);
+    out.star_names.push_back(dim);
+    out.star_cols.push_back(d);
+  }
+  for (const std::string &pair : prop_list(kv, pre + "function.column.pairs")) {
+    pinot_column_desc d{};
+    d.data_type = pair.rfind("count__", 0) == 0 ? PINOT_LONG : PINOT_DOUBLE;
+    d.encoding = PINOT_ENCODING_RAW;
+    const uint8_t *p = nullptr;
+    uint64_t n = 0;
+    range(pair, "FORWARD_INDEX", &p, &n);
+    out.owned.push_back(read_raw_chunks(p, n, ndocs, 8, "star-tree " + pair));
+    d.forward_index = out.owned.back().data();
+    d.forward_index_len = out.owned.back().size();
+    out.star_names.push_back(pair);
+    out.star_cols.push_back(d);
+  }
+  for (size_t i = 0; i < out.star_cols.size(); i++) out.star_cols[i].name = out.star_names[i].c_str();
+  out.has_star = true;
+}
+
+pinot_segment_desc SegmentDirData::star_desc() const {
+  pinot_segment_desc d{};
+  d.name = name.c_str();
+  d.num_docs = star_num_docs;
+  d.num_columns = (int32_t)star_cols.size();
+  d.columns = star_cols.data();
+  return d;
 }
 
 pinot_segment_desc SegmentDirData::desc() const {

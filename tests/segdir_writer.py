@@ -197,7 +197,35 @@ def _buffers(c):
             yield "inverted_index", c.name + ".bitmap.inv", c.inverted
 
 
-def write_segment_dir(seg, index_dir, version="v1", padding="\\\\u0000", crc=None, creation_time=0):
+def _star_tree_files(seg, st, d):
+    """star_tree_index (the tree, then each dimension's fixed-bit forward index, then each pair's PASS_THROUGH
+    FixedByteChunk raw index: StarTreeIndexCombiner) + star_tree_index_map + the startree.v2.* metadata lines."""
+    from pinot_amd.segment import pack_fixed_bit
+    import numpy as np
+    parts = [("null", "STAR_TREE", st.tree_bytes)]
+    for j, dim in enumerate(st.dimensions):
+        parts.append((dim, "FORWARD_INDEX", pack_fixed_bit(st.dims[:, j], seg.column(dim).bits)))
+    for pair in st.pairs:
+        v = st.metrics[pair]
+        be = v.astype(">i8" if v.dtype.kind in "iu" else ">f8").tobytes()
+        parts.append((pair, "FORWARD_INDEX", raw_chunk_file(be, 8, st.num_docs, compression=0)))
+    blob, lines, off = bytearray(), [], 0
+    for col, typ, data in parts:
+        lines += ["0.%s.%s.OFFSET = %d" % (col, typ, off), "0.%s.%s.SIZE = %d" % (col, typ, len(data))]
+        blob += data
+        off += len(data)
+    with open(os.path.join(d, "star_tree_index"), "wb") as f:
+        f.write(bytes(blob))
+    with open(os.path.join(d, "star_tree_index_map"), "w") as f:
+        f.write("\n".join(lines) + "\n")
+    pre = "startree.v2.0."
+    return ["startree.v2.count = 1", pre + "total.docs = %d" % st.num_docs,
+            pre + "split.order = %s" % ",".join(st.dimensions),
+            pre + "function.column.pairs = %s" % ",".join(st.pairs),
+            pre + "max.leaf.records = %d" % st.max_leaf_records]
+
+
+def write_segment_dir(seg, index_dir, version="v1", padding="\\\\u0000", crc=None, creation_time=0, star_tree=None):
     """padding: the metadata value as written (default the escaped NUL Pinot writes); None leaves the key out.
     crc: write creation.meta (SegmentIndexCreationDriverImpl: DataOutputStream.writeLong(crc), writeLong(time))."""
     os.makedirs(index_dir, exist_ok=True)
@@ -219,13 +247,15 @@ def write_segment_dir(seg, index_dir, version="v1", padding="\\\\u0000", crc=Non
             f.write(bytes(psf))
         with open(os.path.join(d, "index_map"), "w") as f:
             f.write("\n".join(index_map) + "\n")
+        extra = _star_tree_files(seg, star_tree, d) if star_tree is not None else []
         with open(os.path.join(d, "metadata.properties"), "w") as f:
-            f.write(_props(seg, version, padding))
+            f.write(_props(seg, version, padding) + "".join(l + "\n" for l in extra))
         return index_dir
     for c in seg.columns.values():
         for _, fname, data in _buffers(c):
             with open(os.path.join(index_dir, fname), "wb") as f:
                 f.write(bytes(data))
+    extra = _star_tree_files(seg, star_tree, index_dir) if star_tree is not None else []
     with open(os.path.join(index_dir, "metadata.properties"), "w") as f:
-        f.write(_props(seg, version, padding))
+        f.write(_props(seg, version, padding) + "".join(l + "\n" for l in extra))
     return index_dir

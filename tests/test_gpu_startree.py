@@ -78,3 +78,22 @@ def test_star_tree_attach_checks(engine):
     with pytest.raises(PinotGpuError, match="already"):
         g.attach_star_tree(seg, st.tree_bytes, st.dimensions, st.dims, st.metrics)
     g.release()
+
+
+@pytest.mark.parametrize("version", ["v1", "v3"])
+def test_star_tree_from_segment_directory(engine, tmp_path, version):
+    """star_tree_index + star_tree_index_map + startree.v2.* metadata (StarTreeLoaderUtils) read by
+    pinot_gpu_segment_load: fitting queries run on the loaded tree."""
+    from segdir_writer import write_segment_dir
+    rng = np.random.default_rng(1800)
+    seg = st_segment(rng, 4000, name="stdir")
+    st = build_star_tree(seg, DIMS, PAIRS, max_leaf_records=20)
+    g = engine.load(write_segment_dir(seg, str(tmp_path / "s"), version=version, star_tree=st))
+    ex = ServerQueryExecutor(engine)
+    for it in range(8):
+        q = random_query(rng, seg, [None, ["b"]][it % 2])
+        got, stt = ex.process_query(q, [g], trim=False)
+        exp, scanned = S.execute_server([seg], [st], q)
+        _same(q, got, exp)
+        assert stt.num_docs_scanned == scanned
+    g.release()

@@ -225,3 +225,17 @@ def test_raw_string_bad_bytes():
     col.fwd = col.fwd[:4] + (9).to_bytes(4, "big") + col.fwd[8:]  # offsets not ascending within the bytes
     with pytest.raises(PinotGpuError, match="offsets"):
         validate_segment(seg)
+
+
+@pytest.mark.parametrize("version", ["v1", "v3"])
+def test_star_tree_files_read_on_the_host(tmp_path, version):
+    """The star-tree files a segment directory carries are read and checked with the segment (host only)."""
+    from startree_writer import build_star_tree
+    rng = np.random.default_rng(12)
+    seg = _random_segment(12, 2000)
+    st = build_star_tree(seg, ["i", "s"], [("COUNT", "*"), ("SUM", "l")], max_leaf_records=30)
+    d = write_segment_dir(seg, str(tmp_path / "st"), version=version, star_tree=st)
+    assert segment_dir_info(d)[0] == 2000
+    meta = os.path.join(d, "v3" if version == "v3" else "", "star_tree_index_map")
+    text = open(meta).read()
+    assert "0.null.STAR_TREE.OFFSET = 0" in text and "0.count__*.FORWARD_INDEX.SIZE" in text

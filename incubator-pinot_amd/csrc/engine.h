@@ -209,7 +209,7 @@ struct Engine {
   int device = 0;
   hipStream_t stream = nullptr;
   // result D2H fan-out (d2h.streams): the group-by result arrays copied on parallel streams (one SDMA queue each)
-  bool compact_d2h = true;    // d2h.compact: config-4-sized group-by results read back as key bitmap + u32 arrays
+  bool compact_d2h = false;   // d2h.compact: key bitmap + u32 read-back (config 4: 1.26 vs 1.19 ms, no gain: off)
   PinnedBuffer compact_host;  // its host staging
   int d2h_streams = 1;         // measured on config 4: 1 / 2 / 4 streams all ~1.15 ms for 32 MB (PCIe-bound)
   std::vector<hipStream_t> copy_streams;

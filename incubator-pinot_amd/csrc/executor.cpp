@@ -3940,7 +3940,7 @@ void agg_identities(const pinot_query &q, pinot_agg_result *out) {
   for (int a = 0; a < q.num_aggregations; a++) {
     memset(&out[a], 0, sizeof(pinot_agg_result));
     out[a].has_exact_sum = 1;
-    const int f = q.aggregations[a].function;
+    const int f = sv_function(q.aggregations[a].function);
     out[a].value = f == PINOT_AGG_MIN ? INFINITY : f == PINOT_AGG_MAX ? -INFINITY : 0.0;
   }
 }
@@ -3963,7 +3963,7 @@ void merge_agg_parts(const pinot_query &q, const std::vector<const pinot_agg_res
   for (int a = 0; a < q.num_aggregations; a++) {
     pinot_agg_result &r = out[a];
     memset(&r, 0, sizeof(r));
-    const int f = q.aggregations[a].function;
+    const int f = sv_function(q.aggregations[a].function);  // an MV function merges as its SV form
     __int128 isum = 0;
     double dsum = 0.0;
     bool exact = true;

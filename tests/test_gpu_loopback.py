@@ -245,3 +245,45 @@ def test_loopback_no_rank_holds_a_segment():
     assert out[1][0] == [0, 0.0, float("inf"), float("-inf")] and out[1][1].num_total_raw_docs == 8000
     for s in servers:
         s.close()
+
+
+def test_loopback_mv_and_star_tree_aggregations():
+    """Aggregation-only queries over multi-value columns (the MV functions merge as their single-value forms across
+    ranks) and over star-tree segments, with K = 3 loopback ranks, against the oracle."""
+    import startree as S
+    from startree_writer import build_star_tree
+    from test_mv import mv_segment
+    from test_startree import DIMS, PAIRS, st_segment
+    rng = np.random.default_rng(4242)
+    host = [mv_segment(rng, 3000, name="mv%d" % i) for i in range(4)]
+    srv = GpuServer([0] * 3, "server.loopback=1")
+    gsegs = [srv.engines[i % 3].register(s) for i, s in enumerate(host)]
+    ex = ServerExecutor(srv, pruners=0)
+    q = {"aggregations": [{"function": f, "column": c} for f, c in (
+        ("COUNTMV", "tags"), ("SUMMV", "tags"), ("MINMV", "tagl"), ("MAXMV", "tags"), ("AVGMV", "tags"),
+        ("DISTINCTCOUNTHLLMV", "tags_s"), ("COUNT", "*"))],
+         "filter": {"operator": "NOT_IN", "column": "tags_s", "values": ["t01\t\tt03"]}, "group_by": None}
+    got, st = ex.process_query(q, gsegs)
+    exp, scanned = O.execute_server(host, q)
+    assert st.num_docs_scanned == scanned
+    assert got[0] == exp[0] and got[1] == exp[1] and got[2] == exp[2] and got[3] == exp[3] and got[6] == exp[6]
+    assert (got[4].sum, got[4].count) == exp[4]
+    assert got[5].cardinality() == exp[5].cardinality()
+    srv.close()
+    # star-tree segments on every rank
+    sts_host = [st_segment(rng, 2000, name="st%d" % i) for i in range(3)]
+    trees = [build_star_tree(s, DIMS, PAIRS, max_leaf_records=10) for s in sts_host]
+    srv = GpuServer([0] * 3, "server.loopback=1")
+    gsegs = []
+    for i, (s, t) in enumerate(zip(sts_host, trees)):
+        g = srv.engines[i % 3].register(s)
+        g.attach_star_tree(s, t.tree_bytes, t.dimensions, t.dims, t.metrics)
+        gsegs.append(g)
+    ex = ServerExecutor(srv, pruners=0)
+    q = {"aggregations": [{"function": "COUNT", "column": "*"}, {"function": "SUM", "column": "m"},
+                          {"function": "MAX", "column": "x"}],
+         "filter": {"operator": "IN", "column": "c", "values": ["3\t\t9\t\t30"]}, "group_by": None}
+    got, st = ex.process_query(q, gsegs)
+    exp, scanned = S.execute_server(sts_host, trees, q)
+    assert got == exp and st.num_docs_scanned == scanned
+    srv.close()

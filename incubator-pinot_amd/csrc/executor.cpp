@@ -1268,29 +1268,50 @@ namespace {
 
 bool star_plan(const Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q) {
   if (!e.use_star_tree) return false;
+  int slots = q.num_aggregations;  // each AVG adds its AvgPair count column
+  for (int a = 0; a < q.num_aggregations; a++) slots += q.aggregations[a].function == PINOT_AGG_AVG;
+  if (slots > kMaxAggs) return false;
   for (SegmentData *s : segs)
     if (!star_tree_fits(*s, q)) return false;
   return true;
 }
 
-// The star-tree plan's rewritten query: each function over its pre-aggregated pair column (COUNT sums count__*).
+// The star-tree plan's rewritten query: each function over its pre-aggregated pair column (COUNT sums count__*; AVG
+// sums the AvgPair halves, "avg__x.sum" in its own slot and "avg__x.count" in a hidden slot after the query's).
 struct StarQuery {
-  std::vector<std::string> names;
-  std::vector<pinot_agg_spec> specs;
-  pinot_query q{};
+  std::vector<std::string> names;         // per slot: the star docs' column
+  std::vector<pinot_agg_spec> specs;      // the query's slots, then the hidden AVG count slots
+  std::vector<int> hidden;                // per query aggregation: its count slot (AVG) or -1
+  pinot_query q{};                        // the query's slots only (stats, projections)
+  pinot_query all{};                      // every slot
 };
 void star_query(const pinot_query &q, StarQuery &sq) {
-  sq.names.resize(q.num_aggregations);
-  sq.specs.assign(q.aggregations, q.aggregations + q.num_aggregations);
-  for (int a = 0; a < q.num_aggregations; a++) {
-    sq.names[a] = star_pair_column(q.aggregations[a]);
-    sq.specs[a].column = sq.names[a].c_str();
+  const int na = q.num_aggregations;
+  int nb = na;
+  for (int a = 0; a < na; a++) nb += q.aggregations[a].function == PINOT_AGG_AVG;
+  sq.names.assign(nb, "");
+  sq.specs.assign(q.aggregations, q.aggregations + na);
+  sq.hidden.assign(na, -1);
+  for (int a = 0; a < na; a++) {
+    const std::string p = star_pair_column(q.aggregations[a]);
+    sq.names[a] = q.aggregations[a].function == PINOT_AGG_AVG ? p + ".sum" : p;
     if (sq.specs[a].function == PINOT_AGG_COUNT) sq.specs[a].function = PINOT_AGG_SUM;
+    if (q.aggregations[a].function == PINOT_AGG_AVG) {
+      const int h = (int)sq.specs.size();
+      sq.names[h] = p + ".count";
+      pinot_agg_spec hs = q.aggregations[a];
+      hs.function = PINOT_AGG_SUM;
+      sq.specs.push_back(hs);
+      sq.hidden[a] = h;
+    }
   }
+  for (int b = 0; b < nb; b++) sq.specs[b].column = sq.names[b].c_str();
   sq.q = q;
   sq.q.aggregations = sq.specs.data();
   sq.q.num_filter_nodes = 0;
   sq.q.filter = nullptr;
+  sq.all = sq.q;
+  sq.all.num_aggregations = nb;
 }
 
 void star_stats(const pinot_query &q2, const std::vector<SegmentData *> &segs, const std::vector<StarMatch> &m,
@@ -1339,8 +1360,8 @@ void exec_aggregate_star(Engine &e, const std::vector<SegmentData *> &segs, cons
     a.bitset = bits.get<uint64_t>();
     a.nwords = sd.nwords();
     a.num_docs = sd.num_docs;
-    a.n = na;
-    for (int g = 0; g < na; g++) {
+    a.n = sq.all.num_aggregations;
+    for (int g = 0; g < a.n; g++) {
       ColumnData &c = *sd.column(sq.names[g]);
       MvAggSpec &sp = a.specs[g];
       sp.fwd = c.fwd.get<uint8_t>();
@@ -1376,11 +1397,12 @@ void exec_aggregate_star(Engine &e, const std::vector<SegmentData *> &segs, cons
     pinot_agg_result &r = out[g];
     memset(&r, 0, sizeof(r));
     const int f = q.aggregations[g].function;
-    int64_t isum = 0;
+    int64_t isum = 0, hcount = 0;
     double dsum = 0.0, mn = INFINITY, mx = -INFINITY;
     for (size_t si = 0; si < S; si++) {  // CombineService.mergeTwoBlocks, segment order
       if (parts[si].empty()) continue;
       const unsigned long long *o = parts[si].data() + 5 * g;
+      if (sq.hidden[g] >= 0) hcount += (int64_t)parts[si][5 * sq.hidden[g] + 1];  // Σ avg__x.count (LONG)
       if (o[0] == 0) continue;
       isum = (int64_t)((uint64_t)isum + o[1]);
       double d;
@@ -1392,6 +1414,7 @@ void exec_aggregate_star(Engine &e, const std::vector<SegmentData *> &segs, cons
     switch (f) {
       case PINOT_AGG_COUNT: r.count = isum; r.value = (double)isum; break;  // Σ count__*
       case PINOT_AGG_SUM: r.value = dsum; break;                           // Σ sum__x (doubles)
+      case PINOT_AGG_AVG: r.value = dsum; r.count = hcount; break;         // AvgPair(Σ sum, Σ count)
       case PINOT_AGG_MIN: r.value = mn; break;
       default: r.value = mx; break;
     }
@@ -3346,25 +3369,22 @@ std::unique_ptr<GroupByResult> exec_group_by_star(Engine &e, const std::vector<S
   const size_t S = segs.size();
   std::vector<StarMatch> m(S);
   for (size_t si = 0; si < S; si++) m[si] = star_tree_match(*segs[si], q, tree.get());
+  const int nb = sq.all.num_aggregations;
   GroupAccs ga;
-  for (int a = 0; a < na; a++) {
+  for (int a = 0; a < nb; a++) {
     const ColumnData &c = *segs[0]->star->docs->column(sq.names[a]);
-    const int f = q.aggregations[a].function;
-    ga.acc_kind.push_back(f == PINOT_AGG_COUNT ? (c.value_kind() == 2 ? 1 : 7)
-                          : f == PINOT_AGG_MIN ? 2 : f == PINOT_AGG_MAX ? 3 : (c.value_kind() == 0 ? 0 : 1));
+    const int f = sq.specs[a].function;  // COUNT is already SUM over count__*
+    // a LONG column sums exactly in int64 (kind 7, or kind 0 over an int32 dictionary); DOUBLE in f64 (kind 1)
+    ga.acc_kind.push_back(f == PINOT_AGG_MIN ? 2 : f == PINOT_AGG_MAX ? 3
+                          : c.value_kind() == 0 ? 0 : c.value_kind() == 1 ? 7 : 1);
     ga.acc_bytes_per_key.push_back(8);
   }
-  for (int a = 0; a < na; a++)  // an int64 SUM needs an int64 dictionary (kind 7) or an int32 one (kind 0)
-    if (ga.acc_kind[a] == 1 && q.aggregations[a].function == PINOT_AGG_SUM) {
-      const ColumnData &c = *segs[0]->star->docs->column(sq.names[a]);
-      if (c.value_kind() == 1) ga.acc_kind[a] = 7;
-    }
-  const size_t per_key = 8 + 8 * (size_t)na;
+  const size_t per_key = 8 + 8 * (size_t)nb;
   e.group_scratch.reserve(ks.G * per_key + 64);
   uint8_t *base = e.group_scratch.get<uint8_t>();
   auto *counts = reinterpret_cast<unsigned long long *>(base);
-  std::vector<void *> accs(na, nullptr);
-  for (int a = 0; a < na; a++) accs[a] = base + ks.G * 8 * (1 + a);
+  std::vector<void *> accs(nb, nullptr);
+  for (int a = 0; a < nb; a++) accs[a] = base + ks.G * 8 * (1 + a);
   PINOT_HIP(hipEventRecord(e.ev_start, e.stream));
   init_accs(e, ks.G, counts, ga, accs.data());
   std::vector<DeviceBuffer> remaps(S * q.num_group_by);
@@ -3377,7 +3397,7 @@ std::unique_ptr<GroupByResult> exec_group_by_star(Engine &e, const std::vector<S
                              e.stream));
     MvGroupArgs a{};
     a.n_gcols = q.num_group_by;
-    a.n_aggs = na;
+    a.n_aggs = nb;
     long long stride = 1;
     for (int j = 0; j < q.num_group_by; j++) {
       const ColumnData &c = *sd.column(q.group_by[j]);
@@ -3394,7 +3414,7 @@ std::unique_ptr<GroupByResult> exec_group_by_star(Engine &e, const std::vector<S
       a.stride[j] = stride;
       stride *= ks.gcard[j];
     }
-    for (int g = 0; g < na; g++) {
+    for (int g = 0; g < nb; g++) {
       ColumnData &c = *sd.column(sq.names[g]);
       a.acc_kind[g] = ga.acc_kind[g];
       a.acc[g] = accs[g];
@@ -3412,21 +3432,29 @@ std::unique_ptr<GroupByResult> exec_group_by_star(Engine &e, const std::vector<S
     PINOT_HIP(hipGetLastError());
   }
   GroupByProgram gp{};
-  gp.n_aggs = na;
+  gp.n_aggs = nb;
   gp.counts = counts;
-  for (int a = 0; a < na; a++) { gp.acc[a] = accs[a]; gp.acc_kind[a] = ga.acc_kind[a]; }
-  auto res = finalize_groups(e, sq.q, ga, ks, gp);
+  for (int a = 0; a < nb; a++) { gp.acc[a] = accs[a]; gp.acc_kind[a] = ga.acc_kind[a]; }
+  auto res = finalize_groups(e, sq.all, ga, ks, gp);
   PINOT_HIP(hipEventRecord(e.ev_stop, e.stream));
   wait_stream(e);
   float ms = 0;
   PINOT_HIP(hipEventElapsedTime(&ms, e.ev_start, e.ev_stop));
   for (int a = 0; a < na; a++) {
-    res->functions[a] = q.aggregations[a].function;
-    if (q.aggregations[a].function != PINOT_AGG_COUNT) continue;
-    HostVec<int64_t> &cv = res->counts[a];  // COUNT: the groups' Σ count__*
-    const HostVec<double> &v = res->values[a];
+    const int f = q.aggregations[a].function;
+    res->functions[a] = f;
+    // COUNT: the groups' Σ count__*; AVG: Σ avg__x.count from its hidden slot
+    const int src = f == PINOT_AGG_COUNT ? a : f == PINOT_AGG_AVG ? sq.hidden[a] : -1;
+    if (src < 0) continue;
+    HostVec<int64_t> &cv = res->counts[a];
+    const HostVec<double> &v = res->values[src];
     for (size_t i = 0; i < cv.size(); i++) cv[i] = (int64_t)v[i];
   }
+  res->functions.resize(na);
+  res->counts.resize(na);
+  res->values.resize(na);
+  res->hll.resize(na);
+  res->hll_card.resize(na);
   star_stats(sq.q, segs, m, ms, stats);
   return res;
 }

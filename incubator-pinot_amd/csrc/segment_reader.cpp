@@ -626,6 +626,38 @@ void read_star_tree(const std::string &dir, const std::map<std::string, std::str
     out.star_cols.push_back(d);
   }
   for (const std::string &pair : prop_list(kv, pre + "function.column.pairs")) {
+    if (pair.rfind("avg__", 0) == 0) {
+      // AvgValueAggregator's BYTES values (AvgPair.toBytes: double sum, long count, big-endian, 16 B) in a var-byte
+      // raw index, split into the C-ABI's two raw columns "<pair>.sum" (DOUBLE) and "<pair>.count" (LONG)
+      const uint8_t *p = nullptr;
+      uint64_t n = 0;
+      range(pair, "FORWARD_INDEX", &p, &n);
+      const std::vector<uint8_t> vb = read_var_byte_chunks(p, n, ndocs, "star-tree " + pair);
+      const uint8_t *body = vb.data() + (size_t)(ndocs + 1) * 4;
+      std::vector<uint8_t> sums((size_t)ndocs * 8), counts((size_t)ndocs * 8);
+      for (int64_t i = 0; i < ndocs; i++) {
+        auto at = [&](int64_t k) {
+          const uint8_t *q = vb.data() + 4 * k;
+          return ((uint64_t)q[0] << 24) | ((uint64_t)q[1] << 16) | ((uint64_t)q[2] << 8) | q[3];
+        };
+        const uint64_t o = at(i), e = at(i + 1);
+        require(e - o == 16, PINOT_ERR_BAD_ARG, "star-tree " + pair + ": AvgPair value is not 16 bytes");
+        memcpy(&sums[(size_t)i * 8], body + o, 8);
+        memcpy(&counts[(size_t)i * 8], body + o + 8, 8);
+      }
+      const std::string part[2] = {pair + ".sum", pair + ".count"};
+      for (int k = 0; k < 2; k++) {
+        pinot_column_desc d{};
+        d.data_type = k == 0 ? PINOT_DOUBLE : PINOT_LONG;
+        d.encoding = PINOT_ENCODING_RAW;
+        out.owned.push_back(k == 0 ? std::move(sums) : std::move(counts));
+        d.forward_index = out.owned.back().data();
+        d.forward_index_len = out.owned.back().size();
+        out.star_names.push_back(part[k]);
+        out.star_cols.push_back(d);
+      }
+      continue;
+    }
     pinot_column_desc d{};
     d.data_type = pair.rfind("count__", 0) == 0 ? PINOT_LONG : PINOT_DOUBLE;
     d.encoding = PINOT_ENCODING_RAW;

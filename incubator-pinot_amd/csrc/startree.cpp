@@ -4,8 +4,9 @@
 //   attach_star_tree   OffHeapStarTree (PC/startree/OffHeapStarTree.java:38-70) parsed and checked (little-endian
 //                      header, 7-int nodes, children in range and sorted, doc ranges inside the star docs); the star
 //                      docs registered as their own device segment (dimension columns over the segment's
-//                      dictionaries, metric columns "count__*" / "sum__x" / "min__x" / "max__x" transcoded like raw
-//                      columns); the dimensions' dictIds kept on the host for the traversal's remaining predicates.
+//                      dictionaries, metric columns "count__*" / "sum__x" / "min__x" / "max__x" and the AvgPair halves
+//                      "avg__x.sum" / "avg__x.count" transcoded like raw columns); the dimensions' dictIds kept on
+//                      the host for the traversal's remaining predicates.
 //   star_tree_fits     StarTreeUtils.isFitForStarTree (PC/startree/StarTreeUtils.java:50-95).
 //   star_tree_match    StarTreeFilterOperator (PC/startree/operator/StarTreeFilterOperator.java): evaluators on the
 //                      segment's dictionaries, the BFS over the tree, then the remaining predicates ANDed over the
@@ -53,6 +54,7 @@ std::string star_pair_column(const pinot_agg_spec &a) {
     case PINOT_AGG_SUM: return "sum__" + col;
     case PINOT_AGG_MIN: return "min__" + col;
     case PINOT_AGG_MAX: return "max__" + col;
+    case PINOT_AGG_AVG: return "avg__" + col;  // the AvgPair column, as "avg__x.sum" + "avg__x.count"
     default: return "";
   }
 }
@@ -135,7 +137,12 @@ bool star_tree_fits(const SegmentData &seg, const pinot_query &q) {
   const std::set<std::string> dims(st.dims.begin(), st.dims.end());
   for (int a = 0; a < q.num_aggregations; a++) {
     const std::string p = star_pair_column(q.aggregations[a]);
-    if (p.empty() || !st.docs->by_name.count(p)) return false;
+    if (p.empty()) return false;
+    if (q.aggregations[a].function == PINOT_AGG_AVG) {
+      if (!st.docs->by_name.count(p + ".sum") || !st.docs->by_name.count(p + ".count")) return false;
+    } else if (!st.docs->by_name.count(p)) {
+      return false;
+    }
   }
   for (int j = 0; j < q.num_group_by; j++)
     if (!dims.count(q.group_by[j])) return false;

@@ -73,7 +73,8 @@ class GpuSegment:
     def attach_star_tree(self, segment: Segment, tree_bytes: bytes, dimensions, dims, metrics):
         """pinot_gpu_segment_attach_star_tree: the segment's star-tree v2 — the OffHeapStarTree bytes, the split-order
         dimensions' star-doc dictIds (int [num_star_docs, num_dims], STAR as 0; encoded with the segment's
-        dictionaries) and the pair columns {"count__*": int64, "sum__x" / "min__x" / "max__x": float64}."""
+        dictionaries) and the pair columns {"count__*": int64, "sum__x" / "min__x" / "max__x": float64,
+        "avg__x": (sum float64, count int64)}."""
         from .segment import Column, Segment as Seg, build_column, pack_fixed_bit
         n = int(np.asarray(dims).shape[0])
         cols = {}
@@ -84,6 +85,10 @@ class GpuSegment:
                              string_width=pc.string_width, fwd=pack_fixed_bit(np.asarray(dims)[:, j], pc.bits),
                              padding=pc.padding)
         for name, vals in metrics.items():
+            if isinstance(vals, tuple):  # an AvgPair column "avg__x": its halves "avg__x.sum" / "avg__x.count"
+                cols[name + ".sum"] = build_column(name + ".sum", np.asarray(vals[0], dtype=np.float64), "DOUBLE", raw=True)
+                cols[name + ".count"] = build_column(name + ".count", np.asarray(vals[1], dtype=np.int64), "LONG", raw=True)
+                continue
             v = np.asarray(vals)
             cols[name] = build_column(name, v, "LONG" if v.dtype.kind in "iu" else "DOUBLE", raw=True)
         docs = Seg(name=segment.name + "$startree", num_docs=n, columns=cols)

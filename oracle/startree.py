@@ -10,7 +10,8 @@ PC = pinot-core/src/main/java/org/apache/pinot/core.
     child when there is one; a grouped dimension takes every non-star child), then the remaining predicates over the
     star-tree docs (AND);
   * StarTreeAggregationExecutor / StarTreeGroupByExecutor: the function applied to the pre-aggregated column
-    (COUNT sums count__*, SUM sums sum__x, MIN / MAX over min__x / max__x), the docs scanned = the matched star docs.
+    (COUNT sums count__*, SUM sums sum__x, MIN / MAX over min__x / max__x, AVG merges the avg__x AvgPairs), the
+    docs scanned = the matched star docs.
 A query the tree does not fit runs the regular plan (pinot_oracle.execute_segment).
 """
 import numpy as np
@@ -18,7 +19,7 @@ import numpy as np
 import pinot_oracle as O
 
 ALL = -1
-_FN = {"COUNT": "count", "SUM": "sum", "MIN": "min", "MAX": "max"}
+_FN = {"COUNT": "count", "SUM": "sum", "MIN": "min", "MAX": "max", "AVG": "avg"}
 
 
 def pair_of(agg):
@@ -141,6 +142,9 @@ def execute_segment(segment, st, query):
 
 def _agg(st, a, sel):
     f = a["function"].upper()
+    if f == "AVG":  # AvgAggregationFunction.aggregate over AvgPair values: sums and counts added
+        s, c = st.metrics[pair_of(a)]
+        return (O._seq_sum(s[sel]), int(c[sel].sum()))
     v = st.metrics[pair_of(a)][sel]
     if f == "COUNT":
         return int(v.sum())

@@ -148,7 +148,7 @@ def var_byte_chunk_file(values, docs_per_chunk=1000, compression=1, version=2):
     """VarByteChunkSingleValueWriter bytes (VarByteChunkSingleValueWriter.java:50-117): per chunk numDocsPerChunk BE
     int row offsets from the chunk start (0 for the unused rows of the last chunk), then the UTF-8 bytes; the chunk
     written up to its last byte, PASS_THROUGH or Snappy."""
-    enc = [v.encode("utf-8") for v in values]
+    enc = [v if isinstance(v, bytes) else v.encode("utf-8") for v in values]
     longest = max((len(e) for e in enc), default=0)
     bodies = []
     for s in range(0, len(enc), docs_per_chunk):
@@ -199,7 +199,7 @@ def _buffers(c):
 
 def _star_tree_files(seg, st, d):
     """star_tree_index (the tree, then each dimension's fixed-bit forward index, then each pair's PASS_THROUGH
-    FixedByteChunk raw index: StarTreeIndexCombiner) + star_tree_index_map + the startree.v2.* metadata lines."""
+    FixedByteChunk raw index — a var-byte one for AVG's BYTES AvgPairs: StarTreeIndexCombiner) + star_tree_index_map + the startree.v2.* metadata lines."""
     from pinot_amd.segment import pack_fixed_bit
     import numpy as np
     parts = [("null", "STAR_TREE", st.tree_bytes)]
@@ -207,6 +207,10 @@ def _star_tree_files(seg, st, d):
         parts.append((dim, "FORWARD_INDEX", pack_fixed_bit(st.dims[:, j], seg.column(dim).bits)))
     for pair in st.pairs:
         v = st.metrics[pair]
+        if isinstance(v, tuple):  # AvgPair BYTES values (AvgPair.toBytes) in a var-byte raw index
+            vals = [struct.pack(">dq", float(s), int(c)) for s, c in zip(v[0], v[1])]
+            parts.append((pair, "FORWARD_INDEX", var_byte_chunk_file(vals, docs_per_chunk=64, compression=0)))
+            continue
         be = v.astype(">i8" if v.dtype.kind in "iu" else ">f8").tobytes()
         parts.append((pair, "FORWARD_INDEX", raw_chunk_file(be, 8, st.num_docs, compression=0)))
     blob, lines, off = bytearray(), [], 0

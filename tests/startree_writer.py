@@ -12,7 +12,8 @@ count, (index, name length, UTF-8 name) per dimension, node count, then 7 ints p
 sorted by dimension value, star (-1) first). STAR is stored as 0 in the dimension forward indexes
 (StarTreeV2Constants.STAR_IN_FORWARD_INDEX). PC = pinot-core/src/main/java/org/apache/pinot/core.
 
-Metrics (ValueAggregatorFactory): COUNT -> LONG count of the records, SUM -> DOUBLE, MIN / MAX -> DOUBLE; the pair
+Metrics (ValueAggregatorFactory): COUNT -> LONG count of the records, SUM -> DOUBLE, MIN / MAX -> DOUBLE, AVG -> AvgPair
+(double sum, long count; AvgPair.toBytes as the BYTES value, 16 B big-endian); the pair
 column name is AggregationFunctionColumnPair.toColumnName: "<type>__<column>" ("count__*").
 """
 import struct
@@ -57,12 +58,15 @@ class _Node:
 def _merge(kinds, a, b):
     out = []
     for k, x, y in zip(kinds, a, b):
-        out.append(x + y if k in ("count", "sum") else (min(x, y) if k == "min" else max(x, y)))
+        if k == "avg":  # AvgValueAggregator.applyAggregatedValue: AvgPair sum + sum, count + count
+            out.append((x[0] + y[0], x[1] + y[1]))
+        else:
+            out.append(x + y if k in ("count", "sum") else (min(x, y) if k == "min" else max(x, y)))
     return out
 
 
 def build_star_tree(seg, dimensions, pairs, max_leaf_records=10000, skip_star=()):
-    """pairs: [(FUNCTION, column)] with FUNCTION in COUNT (column "*"), SUM, MIN, MAX."""
+    """pairs: [(FUNCTION, column)] with FUNCTION in COUNT (column "*"), SUM, MIN, MAX, AVG (AvgPair values)."""
     n = seg.num_docs
     k = len(dimensions)
     raw_dims = np.stack([np.asarray(seg.column(d)._dict_ids if seg.column(d)._dict_ids is not None else
@@ -90,6 +94,10 @@ def build_star_tree(seg, dimensions, pairs, max_leaf_records=10000, skip_star=()
         starts = np.nonzero(new)[0]
         recs_d = [list(map(int, sd[s])) for s in starts]
         for j, kind in enumerate(kinds):
+            if kind == "avg":  # getInitialAggregatedValue: AvgPair(value, 1)
+                recs_m.append(list(zip(np.add.reduceat(sm[j], starts).tolist(),
+                                       np.diff(np.append(starts, n)).tolist())))
+                continue
             red = {"count": np.add, "sum": np.add, "min": np.minimum, "max": np.maximum}[kind]
             v = red.reduceat(sm[j], starts)
             recs_m.append(v.tolist())
@@ -202,6 +210,9 @@ def build_star_tree(seg, dimensions, pairs, max_leaf_records=10000, skip_star=()
     metrics = {}
     for j, (name, kind) in enumerate(zip(names, kinds)):
         col = [m[j] for m in mets_list]
+        if kind == "avg":  # AvgPair per star doc: (sum double, count long)
+            metrics[name] = (np.array([x[0] for x in col], dtype=np.float64), np.array([x[1] for x in col], dtype=np.int64))
+            continue
         metrics[name] = np.array(col, dtype=np.int64 if kind == "count" else np.float64)
     st = StarTree(dimensions=list(dimensions), pairs=names, max_leaf_records=max_leaf_records, dims=dims,
                   metrics=metrics, nodes=nodes, skip_star=tuple(skip_star))

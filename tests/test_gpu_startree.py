@@ -52,8 +52,8 @@ def test_star_tree_plans(engine, seed):
         assert st.num_docs_scanned == scanned
     finally:
         engine.set_config("startree.use=1")
-    # a function without a pair (AVG) runs the regular plan
-    q = {"aggregations": [{"function": "AVG", "column": "m"}, {"function": "COUNT", "column": "*"}],
+    # a function without a pair (AVG over x) runs the regular plan
+    q = {"aggregations": [{"function": "AVG", "column": "x"}, {"function": "COUNT", "column": "*"}],
          "filter": {"operator": "EQUALITY", "column": "a", "values": ["1"]}, "group_by": None}
     got, st = ex.process_query(q, gs)
     exp, scanned = O.execute_server(segs, q)

@@ -13,7 +13,7 @@ from pinot_amd import build_segment
 from startree_writer import MAGIC, build_star_tree
 
 DIMS = ["a", "b", "c"]
-PAIRS = [("COUNT", "*"), ("SUM", "m"), ("MIN", "m"), ("MAX", "x"), ("SUM", "x")]
+PAIRS = [("COUNT", "*"), ("SUM", "m"), ("MIN", "m"), ("MAX", "x"), ("SUM", "x"), ("AVG", "m")]
 
 
 def st_segment(rng, n, name="st"):
@@ -56,6 +56,9 @@ def _same(q, got, exp):
         for a, x, y in zip(q["aggregations"], g, e):
             if a["column"] == "x" and a["function"] == "SUM":
                 assert x == pytest.approx(y, rel=1e-12)
+            elif a["function"] == "AVG":
+                xs, xc = (x.sum, x.count) if hasattr(x, "sum") else x
+                assert (xs, xc) == tuple(y), (q, a)
             else:
                 assert x == y, (q, a)
 
@@ -78,8 +81,10 @@ def test_fit_rules_and_tree_bytes():
     rng = np.random.default_rng(9)
     seg = st_segment(rng, 500)
     st = build_star_tree(seg, DIMS, PAIRS, max_leaf_records=5)
-    q = {"aggregations": [{"function": "AVG", "column": "m"}], "filter": None, "group_by": None}
-    assert not S.fits(st, q)  # no avg__m pair
+    q = {"aggregations": [{"function": "AVG", "column": "x"}], "filter": None, "group_by": None}
+    assert not S.fits(st, q)  # no avg__x pair
+    q = {"aggregations": [{"function": "DISTINCTCOUNTHLL", "column": "m"}], "filter": None, "group_by": None}
+    assert not S.fits(st, q)  # HLL pairs are not built
     q = {"aggregations": [{"function": "SUM", "column": "m"}], "group_by": None,
          "filter": {"operator": "OR", "children": [{"operator": "EQUALITY", "column": "a", "values": ["1"]},
                                                    {"operator": "EQUALITY", "column": "a", "values": ["2"]}]}}

@@ -113,7 +113,9 @@ void exact_filter_stats(Engine &e, const std::vector<SegmentData *> &segs, const
   if (!e.stats_exact || !st || q.num_filter_nodes == 0) return;
   const FilterTreeInput tree = decode_filter(q.num_filter_nodes, q.filter);
   int64_t n = 0;
-  for (SegmentData *s : segs) n += filter_entries_scanned(e, *s, &tree);
+  for (SegmentData *s : segs)  // a segment on its star-tree counts its traversal's remaining-predicate entries
+    n += std::count(e.star_answered.begin(), e.star_answered.end(), s) ? star_tree_match(*s, q, &tree).entries_in_filter
+                                                                       : filter_entries_scanned(e, *s, &tree);
   st->num_entries_scanned_in_filter = n;
 }
 
@@ -393,6 +395,7 @@ pinot_status pinot_gpu_aggregate(pinot_engine *engine, const pinot_segment_handl
       agg_identities(*query, out);
       if (stats) memset(stats, 0, sizeof(*stats));
     } else {
+      engine->star_answered.clear();
       exec_aggregate(*engine, kept, *query, out, stats);
       exact_filter_stats(*engine, kept, *query, stats);
     }
@@ -423,6 +426,7 @@ pinot_status pinot_gpu_group_by(pinot_engine *engine, const pinot_segment_handle
       r = empty_group_result(*query);
       if (stats) memset(stats, 0, sizeof(*stats));
     } else {
+      engine->star_answered.clear();
       r = exec_group_by(*engine, kept, *query, stats);
       exact_filter_stats(*engine, kept, *query, stats);
     }

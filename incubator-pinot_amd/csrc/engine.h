@@ -227,6 +227,7 @@ struct Engine {
   bool use_fused = true;      // exec.fused: one k_scan_query launch per aggregation query when the shape allows
   bool use_star_tree = true;  // startree.use: star-tree plans for the queries a segment's tree fits
   bool stats_exact = false;   // stats.exact: numEntriesScannedInFilter replayed per the iterator protocol (host)
+  std::vector<const SegmentData *> star_answered;  // the current query's segments answered on their star-trees
   bool use_nt = true;         // exec.nt: non-temporal policy on the streamed column DMA (measured: config-2
                               // k_scan_query 0.733 -> 0.702 ms)
   bool use_pipe = false;      // exec.pipe: double-buffered whole-chunk staging (k_scan_query_pipe) when a chunk fits
@@ -401,6 +402,7 @@ std::unique_ptr<SegmentData> register_segment(Engine &e, const pinot_segment_des
 // Star-tree v2 (startree.cpp): attach (parse + check + register the star docs), fit test, traversal.
 void attach_star_tree(Engine &e, SegmentData &seg, const pinot_star_tree_desc &d);
 bool star_tree_fits(const SegmentData &seg, const pinot_query &q);
+bool star_plan_fits(const Engine &e, const SegmentData &seg, const pinot_query &q);  // startree.use && the tree fits
 std::string star_pair_column(const pinot_agg_spec &a);  // "count__*", "sum__x", ... ("" when no pair exists)
 struct StarMatch {
   bool empty = false;                  // a predicate matches nothing

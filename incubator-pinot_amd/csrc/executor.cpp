@@ -1264,15 +1264,20 @@ void exec_aggregate_mv(Engine &e, const std::vector<SegmentData *> &segs, const 
 
 }  // namespace
 
-namespace {
-
-bool star_plan(const Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q) {
+// Per segment, as the reference plans each segment on its own (AggregationPlanNode / AggregationGroupByPlanNode:
+// StarTreeUtils.isFitForStarTree over that segment's trees).
+bool star_plan_fits(const Engine &e, const SegmentData &seg, const pinot_query &q) {
   if (!e.use_star_tree) return false;
   int slots = q.num_aggregations;  // each AVG adds its AvgPair count column
   for (int a = 0; a < q.num_aggregations; a++) slots += q.aggregations[a].function == PINOT_AGG_AVG;
-  if (slots > kMaxAggs) return false;
+  return slots <= kMaxAggs && star_tree_fits(seg, q);
+}
+
+namespace {
+
+bool star_plan(const Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q) {
   for (SegmentData *s : segs)
-    if (!star_tree_fits(*s, q)) return false;
+    if (!star_plan_fits(e, *s, q)) return false;
   return true;
 }
 
@@ -1342,6 +1347,7 @@ void exec_aggregate_star(Engine &e, const std::vector<SegmentData *> &segs, cons
   const size_t S = segs.size();
   std::vector<StarMatch> m(S);
   for (size_t si = 0; si < S; si++) m[si] = star_tree_match(*segs[si], q, tree.get());
+  e.star_answered.insert(e.star_answered.end(), segs.begin(), segs.end());
   constexpr size_t kOut = 5 * kMaxAggs * 8, kHll = kMaxAggs * 256 * 4;
   e.fused_result.reserve(kOut + kHll + 64);
   uint8_t *dev = e.fused_result.device<uint8_t>();
@@ -1432,8 +1438,30 @@ void exec_aggregate(Engine &e, const std::vector<SegmentData *> &segs, const pin
     exec_aggregate_mv(e, segs, q, out, stats);
     return;
   }
-  if (star_plan(e, segs, q)) {
+  std::vector<SegmentData *> on_star, on_scan;
+  for (SegmentData *s : segs) (star_plan_fits(e, *s, q) ? on_star : on_scan).push_back(s);
+  if (!on_star.empty() && on_scan.empty()) {
     exec_aggregate_star(e, segs, q, out, stats);
+    return;
+  }
+  if (!on_star.empty()) {  // mixed: each side on its plan, CombineService.mergeTwoBlocks over the two blocks
+    std::vector<pinot_agg_result> p1(na), p2(na);
+    pinot_exec_stats s1{}, s2{};
+    exec_aggregate_star(e, on_star, q, p1.data(), &s1);
+    exec_aggregate(e, on_scan, q, p2.data(), &s2);
+    merge_agg_parts(q, {p1.data(), p2.data()}, out);
+    if (stats) {
+      memset(stats, 0, sizeof(*stats));
+      for (const pinot_exec_stats *x : {&s1, &s2}) {
+        stats->num_docs_scanned += x->num_docs_scanned;
+        stats->num_entries_scanned_in_filter += x->num_entries_scanned_in_filter;
+        stats->num_entries_scanned_post_filter += x->num_entries_scanned_post_filter;
+        stats->num_total_raw_docs += x->num_total_raw_docs;
+        stats->num_segments_processed += x->num_segments_processed;
+        stats->num_segments_matched += x->num_segments_matched;
+        stats->device_ms += x->device_ms;
+      }
+    }
     return;
   }
   if (e.use_shortcut_plans && shortcut_aggregate(segs, q, out, stats)) return;
@@ -3369,6 +3397,7 @@ std::unique_ptr<GroupByResult> exec_group_by_star(Engine &e, const std::vector<S
   const size_t S = segs.size();
   std::vector<StarMatch> m(S);
   for (size_t si = 0; si < S; si++) m[si] = star_tree_match(*segs[si], q, tree.get());
+  e.star_answered.insert(e.star_answered.end(), segs.begin(), segs.end());
   const int nb = sq.all.num_aggregations;
   GroupAccs ga;
   for (int a = 0; a < nb; a++) {

@@ -97,3 +97,29 @@ def test_star_tree_from_segment_directory(engine, tmp_path, version):
         _same(q, got, exp)
         assert stt.num_docs_scanned == scanned
     g.release()
+
+
+def test_star_tree_mixed_segments(engine):
+    """Segments plan one by one (AggregationPlanNode per segment): a segment with a fitting tree runs the star-tree
+    plan, one without runs the scan plan, and the two blocks merge — numDocsScanned adds the star docs of the first
+    to the matching docs of the second. A group-by over such a mix takes the scan plan everywhere (same result)."""
+    rng = np.random.default_rng(1900)
+    segs = [st_segment(rng, 3000, name="mx%d" % i) for i in range(3)]
+    g0, st0 = _attach(engine, segs[0], leaf=10)
+    g2, st2 = _attach(engine, segs[2], leaf=100)
+    g1 = engine.register(segs[1])
+    gs, trees = [g0, g1, g2], [st0, None, st2]
+    ex = ServerQueryExecutor(engine)
+    for it in range(12):
+        q = random_query(rng, segs[0], None)
+        got, st = ex.process_query(q, gs)
+        exp, scanned = S.execute_server(segs, trees, q)
+        _same(q, got, exp)
+        assert st.num_docs_scanned == scanned, q
+    q = random_query(rng, segs[0], ["b"])
+    got, st = ex.process_query(q, gs, trim=False)
+    exp, scanned = O.execute_server(segs, q)
+    _same(q, got, exp)
+    assert st.num_docs_scanned == scanned
+    for g in gs:
+        g.release()

@@ -1531,7 +1531,7 @@ void exec_aggregate(Engine &e, const std::vector<SegmentData *> &segs, const pin
     ReduceArgs ra{};
     ra.in = part;
     ra.stride = grid;
-    ra.grid = grid;
+    ra.grid = scan_grid(nwords);  // this segment's launches: the blocks beyond it hold another segment's partials
     ra.out = res_dev + si * nres;
     int nslots = 0;
     auto new_slot = [&](int kind, int target) {

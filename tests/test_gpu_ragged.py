@@ -1,0 +1,57 @@
+"""Aggregation-only queries over segments of very different sizes and dictionaries, on the fused and the unfused
+(exec.fused=0: per-segment filter + fold / gather launches, then a fixed-order reduce of the block partials) plans.
+Regression: the reduce of a small segment once read the block partials a larger segment's launch had left beyond
+its own grid (SUM / COUNT over LONG columns taking the gather route came out wrong for mixed-size segments)."""
+import numpy as np
+import pytest
+
+import pinot_oracle as O
+from pinot_amd import GpuEngine, ServerQueryExecutor, build_segment
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def engine():
+    e = GpuEngine(0)
+    yield e
+    e.close()
+
+
+def _segment(rng, n, name):
+    cols = {"a": ("INT", rng.integers(0, 4, n).astype(np.int32)),
+            "m": ("INT", rng.integers(-500, 1000, n).astype(np.int32)),
+            "x": ("LONG", rng.integers(0, 1 << 30, n).astype(np.int64)),
+            "d": ("DOUBLE", rng.integers(-1 << 20, 1 << 20, n).astype(np.float64) / 8.0),
+            "h": ("INT", rng.integers(0, 5000, n).astype(np.int32))}
+    return build_segment(name, cols, allow_sorted=False)
+
+
+@pytest.mark.parametrize("fused", ["1", "0"])
+def test_ragged_segments(engine, fused):
+    rng = np.random.default_rng(2100)
+    sizes = [20000, 2000, 50, 70000, 1, 4097]
+    segs = [_segment(rng, n, "rg%d" % i) for i, n in enumerate(sizes)]
+    gs = [engine.register(s) for s in segs]
+    engine.set_config("exec.fused=" + fused)
+    try:
+        ex = ServerQueryExecutor(engine)
+        for order in (list(range(len(segs))), list(reversed(range(len(segs))))):
+            ss, gg = [segs[i] for i in order], [gs[i] for i in order]
+            for flt in (None, {"operator": "EQUALITY", "column": "a", "values": ["1"]},
+                        {"operator": "RANGE", "column": "m", "values": ["[0\t\t500)"]}):
+                q = {"aggregations": [{"function": "SUM", "column": "x"}, {"function": "COUNT", "column": "*"},
+                                      {"function": "AVG", "column": "m"}, {"function": "MAX", "column": "x"},
+                                      {"function": "SUM", "column": "d"}, {"function": "MIN", "column": "d"},
+                                      {"function": "DISTINCTCOUNTHLL", "column": "h"}],
+                     "filter": flt, "group_by": None}
+                got, st = ex.process_query(q, gg)
+                exp, scanned = O.execute_server(ss, q)
+                assert got[0] == exp[0] and got[1] == exp[1] and got[3] == exp[3] and got[4] == exp[4], (flt, got, exp)
+                assert (got[2].sum, got[2].count) == exp[2] and got[5] == exp[5], (flt, got, exp)
+                assert got[6].cardinality() == exp[6].cardinality()
+                assert st.num_docs_scanned == scanned
+    finally:
+        engine.set_config("exec.fused=1")
+        for g in gs:
+            g.release()

@@ -55,3 +55,51 @@ def test_ragged_segments(engine, fused):
         engine.set_config("exec.fused=1")
         for g in gs:
             g.release()
+
+
+def _same_value(f, g, e):
+    if f == "AVG":
+        assert (g.sum, g.count) == tuple(e)
+    elif f == "DISTINCTCOUNTHLL":
+        assert g.cardinality() == e.cardinality()
+    else:
+        assert g == e
+
+
+@pytest.mark.parametrize("cfg", ["", "exec.fused=0", "group.mode=lds", "group.mode=global", "group.mode=partition"])
+def test_ragged_segments_group_by(engine, cfg):
+    """Group-by over the same ragged segments (per-segment dictionaries -> the union key space and remaps), every
+    sink; group columns INT / STRING, aggregations over INT / LONG / DOUBLE."""
+    rng = np.random.default_rng(2200)
+    sizes = [20000, 2000, 50, 70000, 1, 4097]
+    segs = []
+    for i, n in enumerate(sizes):
+        cols = {"a": ("INT", rng.integers(0, 4 + i, n).astype(np.int32)),
+                "b": ("STRING", np.array(["k%d" % v for v in rng.integers(0, 30 + 7 * i, n)], dtype=object)),
+                "m": ("INT", rng.integers(-500, 1000, n).astype(np.int32)),
+                "x": ("LONG", rng.integers(0, 1 << 30, n).astype(np.int64)),
+                "d": ("DOUBLE", rng.integers(-1 << 20, 1 << 20, n).astype(np.float64) / 8.0),
+                "h": ("INT", rng.integers(0, 5000, n).astype(np.int32))}
+        segs.append(build_segment("rgg%d" % i, cols, allow_sorted=False))
+    gs = [engine.register(s) for s in segs]
+    if cfg:
+        engine.set_config(cfg)
+    try:
+        ex = ServerQueryExecutor(engine)
+        aggs = [{"function": f, "column": c} for f, c in (
+            ("COUNT", "*"), ("SUM", "x"), ("AVG", "m"), ("MIN", "d"), ("MAX", "x"), ("SUM", "d"),
+            ("DISTINCTCOUNTHLL", "h"))]
+        for gcols in (["a"], ["b"], ["b", "a"]):
+            for flt in (None, {"operator": "RANGE", "column": "m", "values": ["[0\t\t500)"]}):
+                q = {"aggregations": aggs, "filter": flt, "group_by": {"columns": gcols, "top_n": 10}}
+                got, st = ex.process_query(q, gs, trim=False)
+                exp, scanned = O.execute_server(segs, q)
+                assert st.num_docs_scanned == scanned
+                assert set(got) == set(exp), (gcols, flt)
+                for k in exp:
+                    for a, gv, ev in zip(aggs, got[k], exp[k]):
+                        _same_value(a["function"], gv, ev)
+    finally:
+        engine.set_config("exec.fused=1;group.mode=auto")
+        for g in gs:
+            g.release()

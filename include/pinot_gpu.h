@@ -265,8 +265,10 @@ pinot_status pinot_gpu_segment_validate(const pinot_segment_desc *desc);
  * named like the segment's column (the segment's own dictionary bytes, the star-tree's fixed-bit forward index at
  * the segment column's bits per element, STAR stored as 0) and one raw column per function-column pair, named as
  * AggregationFunctionColumnPair.toColumnName ("count__*" LONG; "sum__x", "min__x", "max__x" DOUBLE; AVG's AvgPair
- * BYTES column "avg__x" as its two halves "avg__x.sum" DOUBLE + "avg__x.count" LONG). Queries the tree fits
- * (StarTreeUtils.isFitForStarTree: COUNT / SUM / MIN / MAX / AVG with their pairs, group-by and filter columns in
+ * BYTES column "avg__x" as its two halves "avg__x.sum" DOUBLE + "avg__x.count" LONG; DISTINCTCOUNTHLL's
+ * "distinctCountHLL__x" as a raw STRING-layout column of HyperLogLog.getBytes values, log2m 8). Queries the tree fits
+ * (StarTreeUtils.isFitForStarTree: COUNT / SUM / MIN / MAX / AVG / DISTINCTCOUNTHLL with their pairs, group-by and
+ * filter columns in
  * the split order, no OR) then run on the star-tree (StarTreeFilterOperator's traversal + the pre-aggregated
  * functions) when every queried segment has one; engine config startree.use=0 disables it (the reference's
  * useStarTree=false debug option). */

@@ -3,6 +3,7 @@
 #include <chrono>
 #include <cmath>
 #include <deque>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -138,6 +139,7 @@ struct StarTreeData {
   std::vector<std::string> dims;                  // split order
   std::vector<std::vector<uint32_t>> host_dims;   // [dim][star doc] dictIds
   std::unique_ptr<SegmentData> docs;
+  std::map<std::string, DeviceBuffer> regs;       // "distinctCountHLL__x" -> u8 registers [star doc][256]
 };
 
 struct SegmentData {

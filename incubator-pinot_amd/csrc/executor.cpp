@@ -1133,6 +1133,7 @@ void exec_aggregate_mv(Engine &e, const std::vector<SegmentData *> &segs, const 
   std::vector<unsigned long long> init(5 * kMaxAggs, 0ull);
   for (int g = 0; g < kMaxAggs; g++) init[5 * g + 3] = ~0ull;
   PINOT_HIP(hipEventRecord(e.ev_start, e.stream));
+  PINOT_HIP(hipMemsetAsync(dev + kOut, 0, kHll, e.stream));  // HyperLogLog registers: max over every segment
   upload_arena(e, ar);
   Timer t(e);
   struct Part {
@@ -1368,8 +1369,14 @@ void exec_aggregate_star(Engine &e, const std::vector<SegmentData *> &segs, cons
     a.num_docs = sd.num_docs;
     a.n = sq.all.num_aggregations;
     for (int g = 0; g < a.n; g++) {
-      ColumnData &c = *sd.column(sq.names[g]);
       MvAggSpec &sp = a.specs[g];
+      if (sq.specs[g].function == PINOT_AGG_DISTINCTCOUNTHLL) {  // register rows, max-merged
+        sp = MvAggSpec{};
+        sp.dict = segs[si]->star->regs.at(sq.names[g]).get();
+        sp.kind = MVA_REGS;
+        continue;
+      }
+      ColumnData &c = *sd.column(sq.names[g]);
       sp.fwd = c.fwd.get<uint8_t>();
       sp.offsets = nullptr;
       sp.dict = c.dict_dev.get();
@@ -1421,6 +1428,12 @@ void exec_aggregate_star(Engine &e, const std::vector<SegmentData *> &segs, cons
       case PINOT_AGG_COUNT: r.count = isum; r.value = (double)isum; break;  // Σ count__*
       case PINOT_AGG_SUM: r.value = dsum; break;                           // Σ sum__x (doubles)
       case PINOT_AGG_AVG: r.value = dsum; r.count = hcount; break;         // AvgPair(Σ sum, Σ count)
+      case PINOT_AGG_DISTINCTCOUNTHLL: {                                   // addAll over the matched docs
+        const uint32_t *h = reinterpret_cast<const uint32_t *>(host + kOut) + (size_t)g * 256;
+        for (int j = 0; j < 256; j++) r.hll_registers[j] = (uint8_t)h[j];
+        r.hll_cardinality = hll_cardinality(r.hll_registers);
+        break;
+      }
       case PINOT_AGG_MIN: r.value = mn; break;
       default: r.value = mx; break;
     }
@@ -3401,6 +3414,11 @@ std::unique_ptr<GroupByResult> exec_group_by_star(Engine &e, const std::vector<S
   const int nb = sq.all.num_aggregations;
   GroupAccs ga;
   for (int a = 0; a < nb; a++) {
+    if (sq.specs[a].function == PINOT_AGG_DISTINCTCOUNTHLL) {  // u32 registers per key (the kernel's kind 8)
+      ga.acc_kind.push_back(4);
+      ga.acc_bytes_per_key.push_back(1024);
+      continue;
+    }
     const ColumnData &c = *segs[0]->star->docs->column(sq.names[a]);
     const int f = sq.specs[a].function;  // COUNT is already SUM over count__*
     // a LONG column sums exactly in int64 (kind 7, or kind 0 over an int32 dictionary); DOUBLE in f64 (kind 1)
@@ -3408,12 +3426,20 @@ std::unique_ptr<GroupByResult> exec_group_by_star(Engine &e, const std::vector<S
                           : c.value_kind() == 0 ? 0 : c.value_kind() == 1 ? 7 : 1);
     ga.acc_bytes_per_key.push_back(8);
   }
-  const size_t per_key = 8 + 8 * (size_t)nb;
+  size_t per_key = 8;
+  for (auto b : ga.acc_bytes_per_key) per_key += b;
+  size_t free_b = 0, total_b = 0;
+  PINOT_HIP(hipMemGetInfo(&free_b, &total_b));
+  if ((double)ks.G * per_key >= 0.5 * (double)free_b) return nullptr;  // the scan plan sizes its own sink
   e.group_scratch.reserve(ks.G * per_key + 64);
   uint8_t *base = e.group_scratch.get<uint8_t>();
   auto *counts = reinterpret_cast<unsigned long long *>(base);
   std::vector<void *> accs(nb, nullptr);
-  for (int a = 0; a < nb; a++) accs[a] = base + ks.G * 8 * (1 + a);
+  uint8_t *ap = base + ks.G * 8;
+  for (int a = 0; a < nb; a++) {
+    accs[a] = ap;
+    ap += ks.G * ga.acc_bytes_per_key[a];
+  }
   PINOT_HIP(hipEventRecord(e.ev_start, e.stream));
   init_accs(e, ks.G, counts, ga, accs.data());
   std::vector<DeviceBuffer> remaps(S * q.num_group_by);
@@ -3444,6 +3470,12 @@ std::unique_ptr<GroupByResult> exec_group_by_star(Engine &e, const std::vector<S
       stride *= ks.gcard[j];
     }
     for (int g = 0; g < nb; g++) {
+      if (ga.acc_kind[g] == 4) {  // star-tree HyperLogLog rows: the doc's registers (kind 8), not a dictId's hash
+        a.acc_kind[g] = 8;
+        a.acc[g] = accs[g];
+        a.dict[g] = segs[si]->star->regs.at(sq.names[g]).get();
+        continue;
+      }
       ColumnData &c = *sd.column(sq.names[g]);
       a.acc_kind[g] = ga.acc_kind[g];
       a.acc[g] = accs[g];

@@ -67,7 +67,8 @@ void launch_mv_leaf(const MvLeafArgs &a, hipStream_t stream);
 // single-value functions beside them): one lane per doc over the doc's entries. Per aggregation the kernel keeps
 // out[5 * a + k]: k = 0 entries (COUNT*: docs), 1 int64 sum, 2 double sum bits, 3 / 4 min / max as order-preserving
 // u64 images of the double value; HLL registers in hll[a * 256 + r] (atomicMax).
-enum MvAggKind : int32_t { MVA_COUNT_DOCS = 0, MVA_VALUES = 1, MVA_HLL = 2 };
+// MVA_REGS: a star-tree's HyperLogLog column — 256 u8 registers per doc at dict + doc * 256, max-merged.
+enum MvAggKind : int32_t { MVA_COUNT_DOCS = 0, MVA_VALUES = 1, MVA_HLL = 2, MVA_REGS = 3 };
 struct MvAggSpec {
   const uint8_t *fwd;          // packed forward index (entries for MV columns)
   const uint32_t *offsets;     // MV: [num_docs + 1] row starts; null: single-value column

@@ -133,6 +133,13 @@ __global__ __launch_bounds__(kBlock) void k_mv_aggregate(MvAggArgs a) {
       if (g >= a.n) break;
       const MvAggSpec &sp = a.specs[g];
       if (sp.kind == MVA_COUNT_DOCS) continue;
+      if (sp.kind == MVA_REGS) {  // HyperLogLog.addAll of the doc's registers
+        const uint8_t *r = static_cast<const uint8_t *>(sp.dict) + doc * 256;
+        for (int j = 0; j < 256; j++)
+          if (r[j]) atomicMax(a.hll + g * 256 + j, (uint32_t)r[j]);
+        cnt[g]++;
+        continue;
+      }
       uint32_t b = (uint32_t)doc, e = (uint32_t)doc + 1;
       if (sp.offsets) {
         b = sp.offsets[doc];
@@ -335,6 +342,12 @@ __device__ __forceinline__ void mv_fold(const MvGroupArgs &a, int g, long long k
   const int ak = a.acc_kind[g];
   if (ak == 6) {
     atomicAdd(static_cast<unsigned long long *>(a.acc[g]) + key, (unsigned long long)(e - b));
+    return;
+  }
+  if (ak == 8) {  // a star-tree's HyperLogLog column: the doc's 256 registers max-merged (HyperLogLog.addAll)
+    const uint8_t *r = static_cast<const uint8_t *>(a.dict[g]) + (size_t)b * 256;
+    for (int j = 0; j < 256; j++)
+      if (r[j]) atomicMax(static_cast<uint32_t *>(a.acc[g]) + key * 256 + j, (uint32_t)r[j]);
     return;
   }
   for (uint32_t v = b; v < e; v++) {

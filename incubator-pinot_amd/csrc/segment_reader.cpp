@@ -626,6 +626,22 @@ void read_star_tree(const std::string &dir, const std::map<std::string, std::str
     out.star_cols.push_back(d);
   }
   for (const std::string &pair : prop_list(kv, pre + "function.column.pairs")) {
+    if (pair.rfind("distinctCountHLL__", 0) == 0) {
+      // DistinctCountHLLValueAggregator's BYTES values (HyperLogLog.getBytes) in a var-byte raw index: handed over
+      // in the C-ABI's raw STRING layout (offsets + bytes); attach decodes the registers
+      const uint8_t *p = nullptr;
+      uint64_t n = 0;
+      range(pair, "FORWARD_INDEX", &p, &n);
+      out.owned.push_back(read_var_byte_chunks(p, n, ndocs, "star-tree " + pair));
+      pinot_column_desc d{};
+      d.data_type = PINOT_STRING;
+      d.encoding = PINOT_ENCODING_RAW;
+      d.forward_index = out.owned.back().data();
+      d.forward_index_len = out.owned.back().size();
+      out.star_names.push_back(pair);
+      out.star_cols.push_back(d);
+      continue;
+    }
     if (pair.rfind("avg__", 0) == 0) {
       // AvgValueAggregator's BYTES values (AvgPair.toBytes: double sum, long count, big-endian, 16 B) in a var-byte
       // raw index, split into the C-ABI's two raw columns "<pair>.sum" (DOUBLE) and "<pair>.count" (LONG)

@@ -5,8 +5,9 @@
 //                      header, 7-int nodes, children in range and sorted, doc ranges inside the star docs); the star
 //                      docs registered as their own device segment (dimension columns over the segment's
 //                      dictionaries, metric columns "count__*" / "sum__x" / "min__x" / "max__x" and the AvgPair halves
-//                      "avg__x.sum" / "avg__x.count" transcoded like raw columns); the dimensions' dictIds kept on
-//                      the host for the traversal's remaining predicates.
+//                      "avg__x.sum" / "avg__x.count" transcoded like raw columns; the HyperLogLog columns
+//                      "distinctCountHLL__x" decoded into u8 register rows); the dimensions' dictIds kept on the host
+//                      for the traversal's remaining predicates.
 //   star_tree_fits     StarTreeUtils.isFitForStarTree (PC/startree/StarTreeUtils.java:50-95).
 //   star_tree_match    StarTreeFilterOperator (PC/startree/operator/StarTreeFilterOperator.java): evaluators on the
 //                      segment's dictionaries, the BFS over the tree, then the remaining predicates ANDed over the
@@ -55,6 +56,7 @@ std::string star_pair_column(const pinot_agg_spec &a) {
     case PINOT_AGG_MIN: return "min__" + col;
     case PINOT_AGG_MAX: return "max__" + col;
     case PINOT_AGG_AVG: return "avg__" + col;  // the AvgPair column, as "avg__x.sum" + "avg__x.count"
+    case PINOT_AGG_DISTINCTCOUNTHLL: return "distinctCountHLL__" + col;
     default: return "";
   }
 }
@@ -123,7 +125,41 @@ void attach_star_tree(Engine &e, SegmentData &seg, const pinot_star_tree_desc &d
     for (int32_t i = 0; i < ndocs; i++) ids[i] = read_bits(cd->forward_index, pc.bits, (uint64_t)i);
     st->host_dims.push_back(std::move(ids));
   }
-  st->docs = register_segment(e, *d.docs);
+  // HyperLogLog pair columns ("distinctCountHLL__x": HyperLogLog.getBytes per star doc, raw var-byte layout) become
+  // u8 register rows on the device; the other columns register as the star docs' segment
+  std::vector<pinot_column_desc> plain;
+  for (int32_t k = 0; k < d.docs->num_columns; k++) {
+    const pinot_column_desc &c = d.docs->columns[k];
+    const std::string cn = c.name ? c.name : "";
+    if (cn.rfind("distinctCountHLL__", 0) != 0) {
+      plain.push_back(c);
+      continue;
+    }
+    require(c.data_type == PINOT_STRING && c.encoding == PINOT_ENCODING_RAW && c.forward_index &&
+                c.forward_index_len >= ((uint64_t)ndocs + 1) * 4,
+            PINOT_ERR_BAD_ARG, seg.name + ": star-tree HyperLogLog column " + cn + " must be raw bytes");
+    require(!st->regs.count(cn), PINOT_ERR_BAD_ARG, seg.name + ": duplicate star-tree column " + cn);
+    const uint8_t *f = c.forward_index;
+    auto be32 = [](const uint8_t *q) { return ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3]; };
+    const uint64_t body = ((uint64_t)ndocs + 1) * 4;
+    std::vector<uint8_t> regs((size_t)ndocs * 256);
+    for (int32_t i = 0; i < ndocs; i++) {
+      const uint64_t o = be32(f + 4 * (uint64_t)i), e2 = be32(f + 4 * ((uint64_t)i + 1));
+      require(e2 >= o && e2 - o == 180 && body + e2 <= c.forward_index_len, PINOT_ERR_BAD_ARG,
+              seg.name + ": " + cn + ": a HyperLogLog value is not 180 bytes (log2m 8)");
+      const uint8_t *h = f + body + o;  // HyperLogLog.getBytes: log2m, size in bytes, RegisterSet words
+      require(be32(h) == 8 && be32(h + 4) == 172, PINOT_ERR_UNSUPPORTED, seg.name + ": " + cn + ": log2m other than 8");
+      for (int p = 0; p < 256; p++) regs[(size_t)i * 256 + p] = (uint8_t)((be32(h + 8 + 4 * (p / 6)) >> (5 * (p % 6))) & 31u);
+    }
+    DeviceBuffer &db = st->regs[cn];
+    db.alloc(regs.size() + 16);
+    PINOT_HIP(hipMemcpy(db.get(), regs.data(), regs.size(), hipMemcpyHostToDevice));
+    seg.device_bytes += regs.size();
+  }
+  pinot_segment_desc plain_desc = *d.docs;
+  plain_desc.columns = plain.data();
+  plain_desc.num_columns = (int32_t)plain.size();
+  st->docs = register_segment(e, plain_desc);
   for (auto &c : st->docs->cols)
     if (c->name.find("__") != std::string::npos)
       require(c->numeric(), PINOT_ERR_BAD_ARG, seg.name + ": star-tree metric " + c->name + " must be numeric");
@@ -140,6 +176,8 @@ bool star_tree_fits(const SegmentData &seg, const pinot_query &q) {
     if (p.empty()) return false;
     if (q.aggregations[a].function == PINOT_AGG_AVG) {
       if (!st.docs->by_name.count(p + ".sum") || !st.docs->by_name.count(p + ".count")) return false;
+    } else if (q.aggregations[a].function == PINOT_AGG_DISTINCTCOUNTHLL) {
+      if (!st.regs.count(p)) return false;
     } else if (!st.docs->by_name.count(p)) {
       return false;
     }

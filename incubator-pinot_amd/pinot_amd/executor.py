@@ -74,7 +74,8 @@ class GpuSegment:
         """pinot_gpu_segment_attach_star_tree: the segment's star-tree v2 — the OffHeapStarTree bytes, the split-order
         dimensions' star-doc dictIds (int [num_star_docs, num_dims], STAR as 0; encoded with the segment's
         dictionaries) and the pair columns {"count__*": int64, "sum__x" / "min__x" / "max__x": float64,
-        "avg__x": (sum float64, count int64)}."""
+        "avg__x": (sum float64, count int64), "distinctCountHLL__x": uint8 registers [num_star_docs, 256]}; the
+        HyperLogLogs travel as their HyperLogLog.getBytes values in a raw STRING-layout column."""
         from .segment import Column, Segment as Seg, build_column, pack_fixed_bit
         n = int(np.asarray(dims).shape[0])
         cols = {}
@@ -85,6 +86,15 @@ class GpuSegment:
                              string_width=pc.string_width, fwd=pack_fixed_bit(np.asarray(dims)[:, j], pc.bits),
                              padding=pc.padding)
         for name, vals in metrics.items():
+            if getattr(vals, "ndim", 1) == 2:  # HyperLogLog registers [n, 256] -> getBytes values, raw var-byte
+                enc = [_hll_bytes(r) for r in np.asarray(vals)]
+                offs = np.zeros(n + 1, dtype=np.int64)
+                offs[1:] = np.cumsum([len(b) for b in enc])
+                c = Column(name=name, data_type="STRING", cardinality=0, bits=0, is_sorted=False,
+                           has_inverted_index=False, num_docs=n, dictionary=b"", encoding="raw")
+                c.fwd = offs.astype(">i4").tobytes() + b"".join(enc)
+                cols[name] = c
+                continue
             if isinstance(vals, tuple):  # an AvgPair column "avg__x": its halves "avg__x.sum" / "avg__x.count"
                 cols[name + ".sum"] = build_column(name + ".sum", np.asarray(vals[0], dtype=np.float64), "DOUBLE", raw=True)
                 cols[name + ".count"] = build_column(name + ".count", np.asarray(vals[1], dtype=np.int64), "LONG", raw=True)
@@ -102,6 +112,15 @@ class GpuSegment:
         if self.handle is not None:
             check(self.engine.lib.pinot_gpu_segment_release(self.engine.ptr, self.handle))
             self.handle = None
+
+
+def _hll_bytes(regs):
+    """stream-lib HyperLogLog.getBytes (log2m 8): BE int 8, BE int 172, the RegisterSet's 43 BE int words (register p
+    at bit 5 * (p % 6) of word p / 6)."""
+    r = np.zeros(258, dtype=np.uint32)
+    r[:256] = np.asarray(regs, dtype=np.uint32)
+    words = (r.reshape(43, 6) << (5 * np.arange(6, dtype=np.uint32))).sum(axis=1, dtype=np.uint32)
+    return np.array([8, 172], dtype=">i4").tobytes() + words.astype(">u4").tobytes()
 
 
 def segment_desc(seg: Segment):

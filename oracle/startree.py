@@ -10,8 +10,8 @@ PC = pinot-core/src/main/java/org/apache/pinot/core.
     child when there is one; a grouped dimension takes every non-star child), then the remaining predicates over the
     star-tree docs (AND);
   * StarTreeAggregationExecutor / StarTreeGroupByExecutor: the function applied to the pre-aggregated column
-    (COUNT sums count__*, SUM sums sum__x, MIN / MAX over min__x / max__x, AVG merges the avg__x AvgPairs), the
-    docs scanned = the matched star docs.
+    (COUNT sums count__*, SUM sums sum__x, MIN / MAX over min__x / max__x, AVG merges the avg__x AvgPairs,
+    DISTINCTCOUNTHLL merges the distinctCountHLL__x HyperLogLogs), the docs scanned = the matched star docs.
 A query the tree does not fit runs the regular plan (pinot_oracle.execute_segment).
 """
 import numpy as np
@@ -19,7 +19,7 @@ import numpy as np
 import pinot_oracle as O
 
 ALL = -1
-_FN = {"COUNT": "count", "SUM": "sum", "MIN": "min", "MAX": "max", "AVG": "avg"}
+_FN = {"COUNT": "count", "SUM": "sum", "MIN": "min", "MAX": "max", "AVG": "avg", "DISTINCTCOUNTHLL": "distinctCountHLL"}
 
 
 def pair_of(agg):
@@ -145,6 +145,12 @@ def _agg(st, a, sel):
     if f == "AVG":  # AvgAggregationFunction.aggregate over AvgPair values: sums and counts added
         s, c = st.metrics[pair_of(a)]
         return (O._seq_sum(s[sel]), int(c[sel].sum()))
+    if f == "DISTINCTCOUNTHLL":  # DistinctCountHLLAggregationFunction over HyperLogLog values: addAll
+        h = O.HyperLogLog()
+        regs = st.metrics[pair_of(a)][sel]
+        if regs.shape[0]:
+            h.reg = regs.max(axis=0).astype(np.int32)
+        return h
     v = st.metrics[pair_of(a)][sel]
     if f == "COUNT":
         return int(v.sum())

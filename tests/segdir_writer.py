@@ -207,6 +207,11 @@ def _star_tree_files(seg, st, d):
         parts.append((dim, "FORWARD_INDEX", pack_fixed_bit(st.dims[:, j], seg.column(dim).bits)))
     for pair in st.pairs:
         v = st.metrics[pair]
+        if getattr(v, "ndim", 1) == 2:  # HyperLogLog BYTES values (HyperLogLog.getBytes) in a var-byte raw index
+            from startree_writer import hll_bytes
+            parts.append((pair, "FORWARD_INDEX", var_byte_chunk_file([hll_bytes(r) for r in v], docs_per_chunk=64,
+                                                                     compression=1)))
+            continue
         if isinstance(v, tuple):  # AvgPair BYTES values (AvgPair.toBytes) in a var-byte raw index
             vals = [struct.pack(">dq", float(s), int(c)) for s, c in zip(v[0], v[1])]
             parts.append((pair, "FORWARD_INDEX", var_byte_chunk_file(vals, docs_per_chunk=64, compression=0)))

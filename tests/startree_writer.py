@@ -13,7 +13,8 @@ sorted by dimension value, star (-1) first). STAR is stored as 0 in the dimensio
 (StarTreeV2Constants.STAR_IN_FORWARD_INDEX). PC = pinot-core/src/main/java/org/apache/pinot/core.
 
 Metrics (ValueAggregatorFactory): COUNT -> LONG count of the records, SUM -> DOUBLE, MIN / MAX -> DOUBLE, AVG -> AvgPair
-(double sum, long count; AvgPair.toBytes as the BYTES value, 16 B big-endian); the pair
+(double sum, long count; AvgPair.toBytes as the BYTES value, 16 B big-endian), DISTINCTCOUNTHLL -> HyperLogLog
+(log2m 8; HyperLogLog.getBytes as the BYTES value: int log2m, int 172, the RegisterSet's 43 BE ints); the pair
 column name is AggregationFunctionColumnPair.toColumnName: "<type>__<column>" ("count__*").
 """
 import struct
@@ -60,13 +61,16 @@ def _merge(kinds, a, b):
     for k, x, y in zip(kinds, a, b):
         if k == "avg":  # AvgValueAggregator.applyAggregatedValue: AvgPair sum + sum, count + count
             out.append((x[0] + y[0], x[1] + y[1]))
+        elif k == "distinctcounthll":  # DistinctCountHLLValueAggregator: HyperLogLog.addAll (register max)
+            out.append(np.maximum(x, y))
         else:
             out.append(x + y if k in ("count", "sum") else (min(x, y) if k == "min" else max(x, y)))
     return out
 
 
 def build_star_tree(seg, dimensions, pairs, max_leaf_records=10000, skip_star=()):
-    """pairs: [(FUNCTION, column)] with FUNCTION in COUNT (column "*"), SUM, MIN, MAX, AVG (AvgPair values)."""
+    """pairs: [(FUNCTION, column)] with FUNCTION in COUNT (column "*"), SUM, MIN, MAX, AVG (AvgPair values),
+    DISTINCTCOUNTHLL (HyperLogLog registers)."""
     n = seg.num_docs
     k = len(dimensions)
     raw_dims = np.stack([np.asarray(seg.column(d)._dict_ids if seg.column(d)._dict_ids is not None else
@@ -78,6 +82,14 @@ def build_star_tree(seg, dimensions, pairs, max_leaf_records=10000, skip_star=()
     for f, c in pairs:
         if f.upper() == "COUNT":
             raw_metrics.append(np.ones(n, dtype=np.int64))
+        elif f.upper() == "DISTINCTCOUNTHLL":  # getInitialAggregatedValue: a HyperLogLog offered the value
+            import pinot_oracle as O
+            from hll import register_and_rank_np
+            col = seg.column(c)
+            j, r = register_and_rank_np(O._value_hashes(col)[np.asarray(O.dict_ids(col))])
+            regs = np.zeros((n, 256), dtype=np.uint8)
+            regs[np.arange(n), j] = r
+            raw_metrics.append(regs)
         else:
             col = seg.column(c)
             raw_metrics.append(np.asarray(col.dict_values(), dtype=np.float64)[np.asarray(col._dict_ids)])
@@ -94,6 +106,9 @@ def build_star_tree(seg, dimensions, pairs, max_leaf_records=10000, skip_star=()
         starts = np.nonzero(new)[0]
         recs_d = [list(map(int, sd[s])) for s in starts]
         for j, kind in enumerate(kinds):
+            if kind == "distinctcounthll":
+                recs_m.append(list(np.maximum.reduceat(sm[j], starts, axis=0)))
+                continue
             if kind == "avg":  # getInitialAggregatedValue: AvgPair(value, 1)
                 recs_m.append(list(zip(np.add.reduceat(sm[j], starts).tolist(),
                                        np.diff(np.append(starts, n)).tolist())))
@@ -210,6 +225,9 @@ def build_star_tree(seg, dimensions, pairs, max_leaf_records=10000, skip_star=()
     metrics = {}
     for j, (name, kind) in enumerate(zip(names, kinds)):
         col = [m[j] for m in mets_list]
+        if kind == "distinctcounthll":  # HyperLogLog registers per star doc, uint8 [num_docs, 256]
+            metrics[name] = np.stack(col).astype(np.uint8) if col else np.zeros((0, 256), dtype=np.uint8)
+            continue
         if kind == "avg":  # AvgPair per star doc: (sum double, count long)
             metrics[name] = (np.array([x[0] for x in col], dtype=np.float64), np.array([x[1] for x in col], dtype=np.int64))
             continue
@@ -223,6 +241,15 @@ def build_star_tree(seg, dimensions, pairs, max_leaf_records=10000, skip_star=()
 def _read_ids(col):
     import pinot_oracle as O
     return O.dict_ids(col)
+
+
+def hll_bytes(regs):
+    """stream-lib HyperLogLog.getBytes of 256 registers: BE int log2m (8), BE int size in bytes (43 words * 4),
+    then the RegisterSet words (register p at bit 5 * (p % 6) of word p / 6)."""
+    words = [0] * 43
+    for p_, r in enumerate(regs):
+        words[p_ // 6] |= int(r) << (5 * (p_ % 6))
+    return struct.pack(">ii", 8, 172) + struct.pack(">43i", *[w - (1 << 32) if w >= 1 << 31 else w for w in words])
 
 
 def serialize_tree(dimensions, nodes):

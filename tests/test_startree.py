@@ -13,7 +13,8 @@ from pinot_amd import build_segment
 from startree_writer import MAGIC, build_star_tree
 
 DIMS = ["a", "b", "c"]
-PAIRS = [("COUNT", "*"), ("SUM", "m"), ("MIN", "m"), ("MAX", "x"), ("SUM", "x"), ("AVG", "m")]
+PAIRS = [("COUNT", "*"), ("SUM", "m"), ("MIN", "m"), ("MAX", "x"), ("SUM", "x"), ("AVG", "m"),
+         ("DISTINCTCOUNTHLL", "c")]
 
 
 def st_segment(rng, n, name="st"):
@@ -56,6 +57,10 @@ def _same(q, got, exp):
         for a, x, y in zip(q["aggregations"], g, e):
             if a["column"] == "x" and a["function"] == "SUM":
                 assert x == pytest.approx(y, rel=1e-12)
+            elif a["function"] == "DISTINCTCOUNTHLL":
+                assert x.cardinality() == y.cardinality(), (q, a)
+                if hasattr(x, "reg"):
+                    assert list(x.reg) == list(y.reg), (q, a)
             elif a["function"] == "AVG":
                 xs, xc = (x.sum, x.count) if hasattr(x, "sum") else x
                 assert (xs, xc) == tuple(y), (q, a)
@@ -84,7 +89,7 @@ def test_fit_rules_and_tree_bytes():
     q = {"aggregations": [{"function": "AVG", "column": "x"}], "filter": None, "group_by": None}
     assert not S.fits(st, q)  # no avg__x pair
     q = {"aggregations": [{"function": "DISTINCTCOUNTHLL", "column": "m"}], "filter": None, "group_by": None}
-    assert not S.fits(st, q)  # HLL pairs are not built
+    assert not S.fits(st, q)  # no distinctCountHLL__m pair
     q = {"aggregations": [{"function": "SUM", "column": "m"}], "group_by": None,
          "filter": {"operator": "OR", "children": [{"operator": "EQUALITY", "column": "a", "values": ["1"]},
                                                    {"operator": "EQUALITY", "column": "a", "values": ["2"]}]}}
@@ -103,3 +108,14 @@ def test_fit_rules_and_tree_bytes():
     q = {"aggregations": [{"function": "COUNT", "column": "*"}], "filter": None, "group_by": None}
     res, scanned = S.execute_segment(seg, st, q)
     assert res == [500] and scanned == 1
+
+
+def test_hll_bytes_layout():
+    """HyperLogLog.getBytes as DataTable's serializer writes it (datatable.cpp) and the star-tree stores it."""
+    from startree_writer import hll_bytes
+    regs = np.zeros(256, dtype=np.uint8)
+    regs[0], regs[5], regs[6], regs[255] = 3, 31, 1, 7
+    b = hll_bytes(regs)
+    assert len(b) == 180 and struct.unpack_from(">ii", b, 0) == (8, 172)
+    w = struct.unpack_from(">43i", b, 8)
+    assert w[0] == 3 | (31 << 25) and w[1] == 1 and w[42] == 7 << 15

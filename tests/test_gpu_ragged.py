@@ -103,3 +103,70 @@ def test_ragged_segments_group_by(engine, cfg):
         engine.set_config("exec.fused=1;group.mode=auto")
         for g in gs:
             g.release()
+
+
+RAGGED_CONFIGS = ["", "exec.fused=0", "group.mode=lds", "group.mode=global", "plan.cache=0;agg.affine=0"]
+
+
+@pytest.mark.parametrize("cfg", RAGGED_CONFIGS)
+@pytest.mark.parametrize("seed", range(3))
+def test_random_ragged(engine, cfg, seed):
+    """Random filters (nested AND / OR over every predicate kind, sorted / bitmap / scan leaves), aggregations and
+    group-bys over 2-4 segments of independent sizes and dictionaries, on each plan, against the oracle."""
+    from test_gpu_parity import _assert_same, _random_aggs, _random_segment, _random_tree
+    rng = np.random.default_rng(2300 + seed)
+    sizes = [int(rng.choice([1, 63, 64, 65, 999, 4097, 40000])) for _ in range(int(rng.integers(2, 5)))]
+    segs = [_random_segment(rng, n, name="rr%d" % i) for i, n in enumerate(sizes)]
+    gs = [engine.register(s) for s in segs]
+    if cfg:
+        engine.set_config(cfg)
+    try:
+        ex = ServerQueryExecutor(engine)
+        for it in range(10):
+            group = None
+            if it % 2:
+                gcols = list(rng.choice(["i0", "i1", "i2", "s", "srt", "i3"], size=int(rng.integers(1, 3)), replace=False))
+                group = {"columns": gcols, "top_n": 10}
+            q = {"aggregations": _random_aggs(rng),
+                 "filter": _random_tree(rng, segs[int(rng.integers(0, len(segs)))]) if rng.random() < 0.8 else None,
+                 "group_by": group}
+            got, st = ex.process_query(q, gs, trim=False) if group else ex.process_query(q, gs)
+            exp, scanned = O.execute_server(segs, q)
+            assert st.num_docs_scanned == scanned, (sizes, q)
+            rows = [(got[k], exp[k]) for k in exp] if group else [(got, exp)]
+            if group:
+                assert set(got) == set(exp), (sizes, q)
+            for gv_row, ev_row in rows:
+                for a, gv, ev in zip(q["aggregations"], gv_row, ev_row):
+                    _assert_same(a["function"], gv, ev, a["column"] not in ("dbl", "flt", "lng"))
+    finally:
+        engine.set_config("exec.fused=1;group.mode=auto;plan.cache=1;agg.affine=1")
+        for g in gs:
+            g.release()
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_random_ragged_multi_value(engine, seed):
+    """The multi-value plans (MV leaves, *MV functions, cartesian-product group keys) over segments of independent
+    sizes, entry counts and dictionaries."""
+    from test_gpu_mv import _aggs, _check, _tree
+    from test_mv import mv_segment
+    rng = np.random.default_rng(2400 + seed)
+    sizes = [int(rng.choice([1, 7, 64, 65, 999, 20000])) for _ in range(int(rng.integers(2, 5)))]
+    segs = [mv_segment(rng, n, name="rm%d" % i) for i, n in enumerate(sizes)]
+    gs = [engine.register(s) for s in segs]
+    ex = ServerQueryExecutor(engine)
+    shapes = [None, ["tags"], ["g"], ["tags_s", "g"], None, ["s", "tagl"]]
+    try:
+        for it in range(12):
+            cols = shapes[it % len(shapes)]
+            q = {"aggregations": _aggs(rng),
+                 "filter": _tree(rng, segs[int(rng.integers(0, len(segs)))]) if rng.random() < 0.7 else None,
+                 "group_by": {"columns": cols, "top_n": 10} if cols else None}
+            got, st = ex.process_query(q, gs, trim=False) if cols else ex.process_query(q, gs)
+            exp, scanned = O.execute_server(segs, q)
+            assert st.num_docs_scanned == scanned, (sizes, q)
+            _check(q, got, exp)
+    finally:
+        for g in gs:
+            g.release()

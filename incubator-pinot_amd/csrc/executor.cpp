@@ -3396,9 +3396,13 @@ std::unique_ptr<GroupByResult> exec_group_by_mv(Engine &e, const std::vector<Seg
 // Group-by on the segments' star-trees (StarTreeGroupByExecutor): the traversal's matched star docs per segment, then
 // k_group_by_mv over the star docs' dimension columns (the segment's dictionaries, so the global key space and its
 // remaps are the segments' own) with each function over its pair column; COUNT is Σ count__* per group (exact int64).
-// Runs while the key space fits num.groups.limit (no admission); otherwise the caller takes the regular plan.
+// Segments whose tree does not fit (on_star[si] false) run their own filter and fold their columns into the same
+// accumulators (COUNT and AVG's count: +1 per doc; SUM / AVG as doubles, as the pair columns hold them; HLL by value
+// hash) — each segment on its own plan, as InstancePlanMakerImplV2 plans them. Runs while the key space fits
+// num.groups.limit (no admission); otherwise the caller takes the regular plan.
 std::unique_ptr<GroupByResult> exec_group_by_star(Engine &e, const std::vector<SegmentData *> &segs,
-                                                  const pinot_query &q, pinot_exec_stats *stats) {
+                                                  const std::vector<bool> &on_star, const pinot_query &q,
+                                                  pinot_exec_stats *stats) {
   const int na = q.num_aggregations;
   KeySpace ks = build_key_space(segs, q);
   const int64_t limit = q.num_groups_limit > 0 ? q.num_groups_limit : e.num_groups_limit;
@@ -3409,8 +3413,20 @@ std::unique_ptr<GroupByResult> exec_group_by_star(Engine &e, const std::vector<S
   if (q.num_filter_nodes > 0) tree = std::make_unique<FilterTreeInput>(decode_filter(q.num_filter_nodes, q.filter));
   const size_t S = segs.size();
   std::vector<StarMatch> m(S);
-  for (size_t si = 0; si < S; si++) m[si] = star_tree_match(*segs[si], q, tree.get());
-  e.star_answered.insert(e.star_answered.end(), segs.begin(), segs.end());
+  std::vector<SegmentData *> star_segs, scan_segs;
+  std::vector<StarMatch> star_m;
+  const SegmentData *first_star = nullptr;
+  for (size_t si = 0; si < S; si++) {
+    if (!on_star[si]) {
+      scan_segs.push_back(segs[si]);
+      continue;
+    }
+    m[si] = star_tree_match(*segs[si], q, tree.get());
+    star_segs.push_back(segs[si]);
+    star_m.push_back(m[si]);
+    if (!first_star) first_star = segs[si];
+  }
+  require(first_star != nullptr, PINOT_ERR_BAD_ARG, "star-tree group-by without a star-tree segment");
   const int nb = sq.all.num_aggregations;
   GroupAccs ga;
   for (int a = 0; a < nb; a++) {
@@ -3419,18 +3435,33 @@ std::unique_ptr<GroupByResult> exec_group_by_star(Engine &e, const std::vector<S
       ga.acc_bytes_per_key.push_back(1024);
       continue;
     }
-    const ColumnData &c = *segs[0]->star->docs->column(sq.names[a]);
+    const ColumnData &c = *first_star->star->docs->column(sq.names[a]);
     const int f = sq.specs[a].function;  // COUNT is already SUM over count__*
     // a LONG column sums exactly in int64 (kind 7, or kind 0 over an int32 dictionary); DOUBLE in f64 (kind 1)
     ga.acc_kind.push_back(f == PINOT_AGG_MIN ? 2 : f == PINOT_AGG_MAX ? 3
                           : c.value_kind() == 0 ? 0 : c.value_kind() == 1 ? 7 : 1);
     ga.acc_bytes_per_key.push_back(8);
   }
+  for (int a = 0; a < na; a++)  // the scan side adds exactly one per doc where the star side adds counts
+    if (q.aggregations[a].function == PINOT_AGG_COUNT || q.aggregations[a].function == PINOT_AGG_AVG) {
+      const int slot = q.aggregations[a].function == PINOT_AGG_COUNT ? a : sq.hidden[a];
+      if (!scan_segs.empty() && ga.acc_kind[slot] == 0) return nullptr;  // int32 count column: not this plan
+    }
   size_t per_key = 8;
   for (auto b : ga.acc_bytes_per_key) per_key += b;
   size_t free_b = 0, total_b = 0;
   PINOT_HIP(hipMemGetInfo(&free_b, &total_b));
   if ((double)ks.G * per_key >= 0.5 * (double)free_b) return nullptr;  // the scan plan sizes its own sink
+  // the scan side's filters (plans over its segments; bitsets produced per segment before its fold)
+  Arena ar;
+  std::unique_ptr<FilterTreeInput> scan_tree;
+  std::vector<SegPlan> plans;
+  QueryScratch qs;
+  if (!scan_segs.empty()) {
+    plans = plan_all(e, scan_segs, q, ar, scan_tree);
+    qs = prepare(e, plans, ar);
+  }
+  e.star_answered.insert(e.star_answered.end(), star_segs.begin(), star_segs.end());
   e.group_scratch.reserve(ks.G * per_key + 64);
   uint8_t *base = e.group_scratch.get<uint8_t>();
   auto *counts = reinterpret_cast<unsigned long long *>(base);
@@ -3442,14 +3473,27 @@ std::unique_ptr<GroupByResult> exec_group_by_star(Engine &e, const std::vector<S
   }
   PINOT_HIP(hipEventRecord(e.ev_start, e.stream));
   init_accs(e, ks.G, counts, ga, accs.data());
+  Timer t(e);
   std::vector<DeviceBuffer> remaps(S * q.num_group_by);
   std::vector<DeviceBuffer> bits(S);
+  std::vector<int64_t> seg_counts(scan_segs.size(), 0);
+  size_t pi = 0;
   for (size_t si = 0; si < S; si++) {
-    if (m[si].empty || m[si].docs == 0) continue;
-    SegmentData &sd = *segs[si]->star->docs;
-    bits[si].alloc(m[si].bits.size() * 8 + 16);
-    PINOT_HIP(hipMemcpyAsync(bits[si].get(), m[si].bits.data(), m[si].bits.size() * 8, hipMemcpyHostToDevice,
-                             e.stream));
+    const bool star = on_star[si];
+    const uint64_t *bitset = nullptr;
+    SegPlan *pl = star ? nullptr : &plans[pi++];
+    if (star) {
+      if (m[si].empty || m[si].docs == 0) continue;
+      bits[si].alloc(m[si].bits.size() * 8 + 16);
+      PINOT_HIP(hipMemcpyAsync(bits[si].get(), m[si].bits.data(), m[si].bits.size() * 8, hipMemcpyHostToDevice,
+                               e.stream));
+      bitset = bits[si].get<uint64_t>();
+    } else {
+      if (pl->empty || pl->seg->num_docs == 0) continue;
+      bitset = run_filter(e, *pl, qs, t);
+      seg_counts[pi - 1] = count_docs(e, bitset, *pl->seg);
+    }
+    SegmentData &sd = star ? *segs[si]->star->docs : *segs[si];
     MvGroupArgs a{};
     a.n_gcols = q.num_group_by;
     a.n_aggs = nb;
@@ -3470,15 +3514,29 @@ std::unique_ptr<GroupByResult> exec_group_by_star(Engine &e, const std::vector<S
       stride *= ks.gcard[j];
     }
     for (int g = 0; g < nb; g++) {
-      if (ga.acc_kind[g] == 4) {  // star-tree HyperLogLog rows: the doc's registers (kind 8), not a dictId's hash
-        a.acc_kind[g] = 8;
-        a.acc[g] = accs[g];
-        a.dict[g] = segs[si]->star->regs.at(sq.names[g]).get();
+      a.acc[g] = accs[g];
+      const int f = g < na ? q.aggregations[g].function : PINOT_AGG_COUNT;  // hidden slots: AVG's counts
+      if (!star && f == PINOT_AGG_COUNT) {
+        a.acc_kind[g] = 6;  // one per doc (an SV row holds one entry)
         continue;
       }
-      ColumnData &c = *sd.column(sq.names[g]);
+      if (ga.acc_kind[g] == 4) {
+        if (star) {  // the doc's register row (kind 8)
+          a.acc_kind[g] = 8;
+          a.dict[g] = segs[si]->star->regs.at(sq.names[g]).get();
+          continue;
+        }
+        ColumnData &c = *sd.column(agg_column(q.aggregations[g]));
+        ensure_hll_lut(e, c);
+        a.acc_kind[g] = 4;
+        a.afwd[g] = c.fwd.get<uint8_t>();
+        a.abits[g] = c.bits;
+        a.hll_lut[g] = c.hll_lut.get<uint16_t>();
+        continue;
+      }
+      ColumnData &c = *sd.column(star ? sq.names[g] : agg_column(q.aggregations[g]));
+      require(star || c.numeric(), PINOT_ERR_BAD_QUERY, "numeric aggregation over STRING column " + c.name);
       a.acc_kind[g] = ga.acc_kind[g];
-      a.acc[g] = accs[g];
       a.afwd[g] = c.fwd.get<uint8_t>();
       a.aoff[g] = nullptr;
       a.abits[g] = c.bits;
@@ -3486,7 +3544,7 @@ std::unique_ptr<GroupByResult> exec_group_by_star(Engine &e, const std::vector<S
       a.value_kind[g] = c.value_kind();
     }
     a.counts = counts;
-    a.bitset = bits[si].get<uint64_t>();
+    a.bitset = bitset;
     a.nwords = sd.nwords();
     a.num_docs = sd.num_docs;
     launch_group_by_mv(a, e.stream);
@@ -3501,6 +3559,7 @@ std::unique_ptr<GroupByResult> exec_group_by_star(Engine &e, const std::vector<S
   wait_stream(e);
   float ms = 0;
   PINOT_HIP(hipEventElapsedTime(&ms, e.ev_start, e.ev_stop));
+  t.collect();
   for (int a = 0; a < na; a++) {
     const int f = q.aggregations[a].function;
     res->functions[a] = f;
@@ -3516,7 +3575,18 @@ std::unique_ptr<GroupByResult> exec_group_by_star(Engine &e, const std::vector<S
   res->values.resize(na);
   res->hll.resize(na);
   res->hll_card.resize(na);
-  star_stats(sq.q, segs, m, ms, stats);
+  pinot_exec_stats s1{}, s2{};
+  star_stats(sq.q, star_segs, star_m, ms, &s1);
+  if (!scan_segs.empty()) fill_stats(q, plans, seg_counts, 0.0f, &s2);
+  if (stats) {
+    *stats = s1;
+    stats->num_docs_scanned += s2.num_docs_scanned;
+    stats->num_entries_scanned_in_filter += s2.num_entries_scanned_in_filter;
+    stats->num_entries_scanned_post_filter += s2.num_entries_scanned_post_filter;
+    stats->num_total_raw_docs += s2.num_total_raw_docs;
+    stats->num_segments_processed += s2.num_segments_processed;
+    stats->num_segments_matched += s2.num_segments_matched;
+  }
   return res;
 }
 
@@ -3528,8 +3598,11 @@ std::unique_ptr<GroupByResult> exec_group_by(Engine &e, const std::vector<Segmen
   require(na >= 1 && na <= kMaxAggs, PINOT_ERR_UNSUPPORTED, "1..8 aggregation functions per query");
   require(q.num_group_by >= 1 && q.num_group_by <= kMaxGroupCols, PINOT_ERR_UNSUPPORTED, "1..16 group-by columns");
   if (touches_mv_group_by(segs, q)) return exec_group_by_mv(e, segs, q, stats);
-  if (star_plan(e, segs, q)) {
-    auto r = exec_group_by_star(e, segs, q, stats);
+  std::vector<bool> on_star(segs.size());
+  bool any_star = false;
+  for (size_t i = 0; i < segs.size(); i++) any_star |= (on_star[i] = star_plan_fits(e, *segs[i], q));
+  if (any_star) {  // each segment on its own plan (star-tree where its tree fits)
+    auto r = exec_group_by_star(e, segs, on_star, q, stats);
     if (r) return r;
   }
   if (e.use_fused) {

@@ -102,7 +102,7 @@ def test_star_tree_from_segment_directory(engine, tmp_path, version):
 def test_star_tree_mixed_segments(engine):
     """Segments plan one by one (AggregationPlanNode per segment): a segment with a fitting tree runs the star-tree
     plan, one without runs the scan plan, and the two blocks merge — numDocsScanned adds the star docs of the first
-    to the matching docs of the second. A group-by over such a mix takes the scan plan everywhere (same result)."""
+    to the matching docs of the second; group-bys likewise fold both kinds of segment into one key space."""
     rng = np.random.default_rng(1900)
     segs = [st_segment(rng, 3000, name="mx%d" % i) for i in range(3)]
     g0, st0 = _attach(engine, segs[0], leaf=10)
@@ -116,10 +116,13 @@ def test_star_tree_mixed_segments(engine):
         exp, scanned = S.execute_server(segs, trees, q)
         _same(q, got, exp)
         assert st.num_docs_scanned == scanned, q
-    q = random_query(rng, segs[0], ["b"])
-    got, st = ex.process_query(q, gs, trim=False)
-    exp, scanned = O.execute_server(segs, q)
-    _same(q, got, exp)
-    assert st.num_docs_scanned == scanned
+    for it in range(12):
+        q = random_query(rng, segs[0], [["b"], ["a", "c"], ["c"]][it % 3])
+        got, st = ex.process_query(q, gs, trim=False)
+        exp, scanned = S.execute_server(segs, trees, q)
+        _same(q, got, exp)
+        assert st.num_docs_scanned == scanned, q
+        scan, _ = O.execute_server(segs, q)
+        _same(q, got, scan)
     for g in gs:
         g.release()

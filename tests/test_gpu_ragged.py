@@ -170,3 +170,35 @@ def test_random_ragged_multi_value(engine, seed):
     finally:
         for g in gs:
             g.release()
+
+
+@pytest.mark.parametrize("K", [2, 5])
+def test_ragged_loopback_server(K):
+    """The multi-GPU merge (server.loopback=1: K engines on device 0) over segments of independent sizes: union
+    dictionaries, per-engine partials of ragged segments, the reduce-scatter and gather."""
+    from pinot_amd import GpuServer, ServerExecutor, compile_pql
+    from test_gpu_loopback import AGG_QUERIES, GROUP_QUERIES, _check_agg, _check_group, _segments
+    rng = np.random.default_rng(2500 + K)
+    host = []
+    for i, n in enumerate([int(rng.choice([1, 65, 999, 4097, 30000])) for _ in range(6)]):
+        s = _segments(rng, n, 1, t_base=[1000 * (i % 2)])[0]
+        s.name = "rl%d" % i
+        host.append(s)
+    srv = GpuServer([0] * K, "server.loopback=1")
+    try:
+        gsegs = [srv.engines[i % K].register(s) for i, s in enumerate(host)]
+        ex = ServerExecutor(srv, num_groups_limit=100000)
+        for text in GROUP_QUERIES:
+            q = compile_pql(text)
+            got, st = ex.process_query(q, gsegs, trim=False)
+            exp, scanned = O.execute_server(host, q)
+            assert st.num_docs_scanned == scanned, text
+            _check_group(q, got, exp)
+        for text in AGG_QUERIES:
+            q = compile_pql(text)
+            got, st = ex.process_query(q, gsegs)
+            exp, scanned = O.execute_server(host, q)
+            assert st.num_docs_scanned == scanned, text
+            _check_agg(q, got, exp)
+    finally:
+        srv.close()

@@ -84,6 +84,8 @@ struct TranscodedColumn {
   std::vector<uint8_t> dictionary, forward_index;
 };
 bool transcode_raw(const pinot_column_desc &d, int32_t num_docs, TranscodedColumn &out);
+// Same, on `threads` host threads (0: one per 1 M docs, at most 16); the output does not depend on the count.
+bool transcode_raw_threads(const pinot_column_desc &d, int32_t num_docs, TranscodedColumn &out, size_t threads);
 void validate_segment(const pinot_segment_desc &d);
 // The pruning metadata of a column descriptor (bloom filter bytes or creation from the decoded dictionary, partition
 // metadata) into c; c's dictionary must be decoded already (parse_column calls it).

@@ -12,6 +12,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <thread>
 
 #include "engine.h"
 
@@ -445,16 +447,91 @@ void parse_pruning_metadata(ColumnData &c, const pinot_column_desc &d) {
 // getNumBitsPerValue(card - 1) bits, MSB first (FixedBitIntReaderWriter).
 namespace {
 
-void pack_ids(const std::vector<uint32_t> &ids, int bits, std::vector<uint8_t> &fwd) {
-  fwd.assign((size_t)((ids.size() * (uint64_t)bits + 7) / 8), 0);
-  for (size_t i = 0; i < ids.size(); i++) {
-    const uint64_t bit0 = i * (uint64_t)bits;
-    for (int b = 0; b < bits; b++)
-      if ((ids[i] >> (bits - 1 - b)) & 1u) {
-        const uint64_t pos = bit0 + b;
-        fwd[pos >> 3] |= (uint8_t)(0x80u >> (pos & 7));
-      }
+// fn(t) for t in [0, T) on T threads (registration is a cold path: plain threads, no pool)
+void run_threads(size_t T, const std::function<void(size_t)> &fn) {
+  if (T <= 1) {
+    fn(0);
+    return;
   }
+  std::vector<std::thread> th;
+  th.reserve(T - 1);
+  for (size_t t = 1; t < T; t++) th.emplace_back(fn, t);
+  fn(0);
+  for (auto &x : th) x.join();
+}
+
+size_t transcode_threads(uint64_t n, size_t requested) {
+  if (requested) return requested;
+  const size_t hw = std::max<size_t>(1, std::thread::hardware_concurrency());
+  return (size_t)std::max<uint64_t>(1, std::min<uint64_t>({n >> 20, 16, hw}));
+}
+
+// Chunk t of T over [0, n) with boundaries on multiples of `align`.
+void chunk_of(uint64_t n, size_t T, size_t t, uint64_t align, uint64_t &lo, uint64_t &hi) {
+  auto at = [&](size_t k) { return k >= T ? n : std::min<uint64_t>(n, (n * k / T) / align * align); };
+  lo = at(t);
+  hi = at(t + 1);
+}
+
+// The distinct values of v in ascending order: chunks sorted and deduplicated in parallel, then merged pairwise
+// (each round's merges in parallel).
+template <class V>
+std::vector<V> sorted_unique(std::vector<V> v, size_t T) {
+  const uint64_t n = v.size();
+  if (T > n / 2) T = std::max<size_t>(1, (size_t)(n / 2));
+  std::vector<std::vector<V>> parts(T);
+  run_threads(T, [&](size_t t) {
+    uint64_t lo, hi;
+    chunk_of(n, T, t, 1, lo, hi);
+    std::vector<V> &p = parts[t];
+    p.assign(std::make_move_iterator(v.begin() + lo), std::make_move_iterator(v.begin() + hi));
+    std::sort(p.begin(), p.end());
+    p.erase(std::unique(p.begin(), p.end()), p.end());
+  });
+  v.clear();
+  v.shrink_to_fit();
+  while (parts.size() > 1) {
+    std::vector<std::vector<V>> next((parts.size() + 1) / 2);
+    run_threads(next.size(), [&](size_t k) {
+      if (2 * k + 1 == parts.size()) {
+        next[k] = std::move(parts[2 * k]);
+        return;
+      }
+      std::vector<V> &a = parts[2 * k], &b = parts[2 * k + 1], &o = next[k];
+      o.reserve(a.size() + b.size());
+      std::merge(std::make_move_iterator(a.begin()), std::make_move_iterator(a.end()),
+                 std::make_move_iterator(b.begin()), std::make_move_iterator(b.end()), std::back_inserter(o));
+      o.erase(std::unique(o.begin(), o.end()), o.end());
+      std::vector<V>().swap(a);
+      std::vector<V>().swap(b);
+    });
+    parts = std::move(next);
+  }
+  return parts.empty() ? std::vector<V>() : std::move(parts[0]);
+}
+
+// dictIds packed MSB-first at `bits` per value (FixedBitIntReaderWriter), chunks of 8-doc multiples in parallel
+// (each chunk owns whole bytes)
+void pack_ids(const std::vector<uint32_t> &ids, int bits, std::vector<uint8_t> &fwd, size_t T = 1) {
+  const uint64_t n = ids.size();
+  fwd.assign((size_t)((n * (uint64_t)bits + 7) / 8), 0);
+  run_threads(T, [&](size_t t) {
+    uint64_t lo, hi;
+    chunk_of(n, T, t, 8, lo, hi);
+    uint64_t acc = 0;  // pending bits, right-aligned
+    int have = 0;
+    size_t out = (size_t)(lo * (uint64_t)bits / 8);
+    for (uint64_t i = lo; i < hi; i++) {
+      acc = (acc << bits) | ids[i];
+      have += bits;
+      while (have >= 8) {
+        have -= 8;
+        fwd[out++] = (uint8_t)(acc >> have);
+      }
+      acc &= have ? ((1ull << have) - 1) : 0;
+    }
+    if (have) fwd[out] = (uint8_t)(acc << (8 - have));
+  });
 }
 
 void finish_transcoded(const pinot_column_desc &d, TranscodedColumn &out) {
@@ -478,7 +555,7 @@ void finish_transcoded(const pinot_column_desc &d, TranscodedColumn &out) {
 // predicate evaluators binary-search in), zero-padded to the longest; the raw-value evaluators' equals / compareTo
 // on the values then give the same docs as the dictionary evaluators on the ids. A value holding a NUL byte would
 // end at the padding: rejected.
-bool transcode_raw_string(const pinot_column_desc &d, int32_t num_docs, TranscodedColumn &out) {
+bool transcode_raw_string(const pinot_column_desc &d, int32_t num_docs, TranscodedColumn &out, size_t T) {
   const std::string name = d.name ? d.name : "";
   const uint64_t n = (uint64_t)std::max(num_docs, 0);
   const uint64_t hdr = (n + 1) * 4;
@@ -497,9 +574,7 @@ bool transcode_raw_string(const pinot_column_desc &d, int32_t num_docs, Transcod
             name + ": raw STRING value with a NUL byte (the dictionary's padding byte)");
     prev = e;
   }
-  std::vector<std::string> uniq = vals;
-  std::sort(uniq.begin(), uniq.end());
-  uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
+  const std::vector<std::string> uniq = sorted_unique(vals, T);
   require(uniq.size() < (1ull << 31), PINOT_ERR_UNSUPPORTED, name + ": more than 2^31 distinct values");
   size_t width = 0;
   for (const auto &u : uniq) width = std::max(width, u.size());
@@ -508,9 +583,14 @@ bool transcode_raw_string(const pinot_column_desc &d, int32_t num_docs, Transcod
   out.dictionary.assign((size_t)card * width, 0);
   for (int64_t j = 0; j < card; j++) memcpy(out.dictionary.data() + (size_t)j * width, uniq[j].data(), uniq[j].size());
   std::vector<uint32_t> ids(n);
-  for (uint64_t i = 0; i < n; i++) ids[i] = (uint32_t)(std::lower_bound(uniq.begin(), uniq.end(), vals[i]) - uniq.begin());
+  run_threads(T, [&](size_t t) {
+    uint64_t lo, hi;
+    chunk_of(n, T, t, 1, lo, hi);
+    for (uint64_t i = lo; i < hi; i++)
+      ids[i] = (uint32_t)(std::lower_bound(uniq.begin(), uniq.end(), vals[i]) - uniq.begin());
+  });
   const int bits = num_bits_per_value(std::max<int64_t>(card - 1, 0));
-  pack_ids(ids, bits, out.forward_index);
+  pack_ids(ids, bits, out.forward_index, T);
   out.desc = pinot_column_desc{};
   out.desc.cardinality = (int32_t)card;
   out.desc.bits_per_value = bits;
@@ -523,13 +603,18 @@ bool transcode_raw_string(const pinot_column_desc &d, int32_t num_docs, Transcod
 }  // namespace
 
 bool transcode_raw(const pinot_column_desc &d, int32_t num_docs, TranscodedColumn &out) {
+  return transcode_raw_threads(d, num_docs, out, 0);
+}
+
+bool transcode_raw_threads(const pinot_column_desc &d, int32_t num_docs, TranscodedColumn &out, size_t threads) {
   if (d.encoding == PINOT_ENCODING_DICTIONARY) return false;
+  const size_t T = transcode_threads((uint64_t)std::max(num_docs, 0), threads);
   const std::string name = d.name ? d.name : "";
   require(d.encoding == PINOT_ENCODING_RAW, PINOT_ERR_BAD_ARG, name + ": unknown column encoding");
   require(!d.multi_value, PINOT_ERR_UNSUPPORTED, name + ": raw multi-value columns are not served");
   require(!d.bloom_filter && !d.create_bloom_filter, PINOT_ERR_UNSUPPORTED,
           name + ": bloom filters are not supported for no-dictionary columns");  // BloomFilterHandler.java:117-118
-  if (d.data_type == PINOT_STRING) return transcode_raw_string(d, num_docs, out);
+  if (d.data_type == PINOT_STRING) return transcode_raw_string(d, num_docs, out, T);
   require(d.data_type >= PINOT_INT && d.data_type <= PINOT_DOUBLE, PINOT_ERR_BAD_ARG, name + ": data type");
   const int w = (d.data_type == PINOT_INT || d.data_type == PINOT_FLOAT) ? 4 : 8;
   const uint64_t n = (uint64_t)std::max(num_docs, 0);
@@ -556,10 +641,12 @@ bool transcode_raw(const pinot_column_desc &d, int32_t num_docs, TranscodedColum
     }
   };
   std::vector<uint64_t> keys(n);
-  for (uint64_t i = 0; i < n; i++) keys[i] = key(i);
-  std::vector<uint64_t> uniq = keys;
-  std::sort(uniq.begin(), uniq.end());
-  uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
+  run_threads(T, [&](size_t t) {
+    uint64_t lo, hi;
+    chunk_of(n, T, t, 1, lo, hi);
+    for (uint64_t i = lo; i < hi; i++) keys[i] = key(i);
+  });
+  const std::vector<uint64_t> uniq = sorted_unique(keys, T);
   require(uniq.size() < (1ull << 31), PINOT_ERR_UNSUPPORTED, name + ": more than 2^31 distinct values");
   const int64_t card = (int64_t)uniq.size();
   const int bits = num_bits_per_value(std::max<int64_t>(card - 1, 0));
@@ -575,8 +662,13 @@ bool transcode_raw(const pinot_column_desc &d, int32_t num_docs, TranscodedColum
     for (int b = 0; b < w; b++) out.dictionary[(size_t)j * w + b] = (uint8_t)(v >> (8 * (w - 1 - b)));
   }
   std::vector<uint32_t> ids(n);
-  for (uint64_t i = 0; i < n; i++) ids[i] = (uint32_t)(std::lower_bound(uniq.begin(), uniq.end(), keys[i]) - uniq.begin());
-  pack_ids(ids, bits, out.forward_index);
+  run_threads(T, [&](size_t t) {
+    uint64_t lo, hi;
+    chunk_of(n, T, t, 1, lo, hi);
+    for (uint64_t i = lo; i < hi; i++)
+      ids[i] = (uint32_t)(std::lower_bound(uniq.begin(), uniq.end(), keys[i]) - uniq.begin());
+  });
+  pack_ids(ids, bits, out.forward_index, T);
   out.desc = pinot_column_desc{};
   out.desc.cardinality = (int32_t)card;
   out.desc.bits_per_value = bits;

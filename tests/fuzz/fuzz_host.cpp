@@ -11,6 +11,7 @@
 //
 // usage: fuzz_host [iterations] [seed]   (prints one summary line; exit 1 on a contract violation)
 //        fuzz_host fmt d:<hex bits> f:<hex bits> ...   (Double/Float.toString of each, one per line)
+//        fuzz_host transcode [iterations] [seed]   (raw-column transcoding: 1 vs many host threads, read-back)
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -330,7 +331,98 @@ std::vector<uint8_t> make_datatable(bool group_by, int nkeys) {
   return o.b;
 }
 
+// transcode [iters] [seed]: raw columns (INT / LONG / FLOAT / DOUBLE with NaN payloads and signed zeros, STRING)
+// transcoded on 1 and on several host threads must give identical bytes, and every doc's packed dictId must read
+// back (MSB-first, bit by bit) to a dictionary entry equal to the doc's value, the dictionary strictly ascending.
+int transcode_check(long iters, uint64_t seed) {
+  rng.seed(seed);
+  long bad = 0, cols = 0;
+  for (long it = 0; it < iters; it++) {
+    const int type = (int)rnd(5);  // PINOT_INT .. PINOT_STRING
+    const int32_t n = 1 + (int32_t)(coin(20) ? rnd(70) : rnd(coin(30) ? 300000 : 5000));
+    const uint64_t card = 1 + rnd(coin(50) ? 40 : 100000);
+    const int w = type == PINOT_INT || type == PINOT_FLOAT ? 4 : 8;
+    std::vector<uint64_t> pool(card);
+    for (auto &v : pool) {
+      v = rng();
+      if (type == PINOT_FLOAT && coin(10)) v = coin(50) ? 0x7FC00001u + rnd(5) : (coin(50) ? 0x80000000u : 0u);
+      if (type == PINOT_DOUBLE && coin(10)) v = coin(50) ? 0xFFF8000000000003ull + rnd(5) : (coin(50) ? 0x8000000000000000ull : 0ull);
+      if (w == 4) v &= 0xFFFFFFFFull;
+    }
+    std::vector<uint8_t> fwd;
+    std::vector<std::string> strs;
+    if (type == PINOT_STRING) {
+      fwd.assign((size_t)(n + 1) * 4, 0);
+      uint32_t off = 0;
+      std::string body;
+      for (int32_t i = 0; i < n; i++) {
+        const uint64_t v = pool[rnd(card)];
+        std::string sv;
+        for (int k = 0; k < (int)(v % 7); k++) sv += (char)('a' + (v >> (5 * k)) % 26);
+        strs.push_back(sv);
+        body += sv;
+        off += (uint32_t)sv.size();
+        put_be32(fwd, 4 * (size_t)(i + 1), off);
+      }
+      fwd.insert(fwd.end(), body.begin(), body.end());
+    } else {
+      fwd.resize((size_t)n * w);
+      for (int32_t i = 0; i < n; i++) {
+        const uint64_t v = pool[rnd(card)];
+        for (int k = 0; k < w; k++) fwd[(size_t)i * w + k] = (uint8_t)(v >> (8 * (w - 1 - k)));
+      }
+    }
+    pinot_column_desc d{};
+    d.name = "c";
+    d.data_type = type;
+    d.encoding = PINOT_ENCODING_RAW;
+    d.forward_index = fwd.data();
+    d.forward_index_len = fwd.size();
+    TranscodedColumn one, many;
+    transcode_raw_threads(d, n, one, 1);
+    transcode_raw_threads(d, n, many, 2 + rnd(15));
+    cols++;
+    bool ok = one.dictionary == many.dictionary && one.forward_index == many.forward_index &&
+              one.desc.cardinality == many.desc.cardinality && one.desc.bits_per_value == many.desc.bits_per_value;
+    const int bits = one.desc.bits_per_value;
+    const int64_t dcard = one.desc.cardinality;
+    const size_t dw = type == PINOT_STRING ? (size_t)one.desc.string_width : (size_t)w;
+    auto is_nan = [&](const uint8_t *p) {
+      uint64_t v = 0;
+      for (int k = 0; k < w; k++) v = (v << 8) | p[k];
+      return type == PINOT_FLOAT ? ((v & 0x7F800000u) == 0x7F800000u && (v & 0x7FFFFFu))
+                                 : ((v & 0x7FF0000000000000ull) == 0x7FF0000000000000ull && (v & 0xFFFFFFFFFFFFFull));
+    };
+    for (int32_t i = 0; ok && i < n; i++) {
+      uint64_t id = 0;
+      for (int b = 0; b < bits; b++) {
+        const uint64_t pos = (uint64_t)i * bits + b;
+        id = (id << 1) | ((one.forward_index[pos >> 3] >> (7 - (pos & 7))) & 1u);
+      }
+      if ((int64_t)id >= dcard) { ok = false; break; }
+      const uint8_t *e = one.dictionary.data() + id * dw;
+      if (type == PINOT_STRING) {
+        ok = strs[i] == std::string(reinterpret_cast<const char *>(e), strnlen(reinterpret_cast<const char *>(e), dw));
+      } else if ((type == PINOT_FLOAT || type == PINOT_DOUBLE) && is_nan(&fwd[(size_t)i * w])) {
+        ok = is_nan(e);
+      } else {
+        ok = memcmp(e, &fwd[(size_t)i * w], w) == 0;
+      }
+    }
+    for (int64_t j = 1; ok && j < dcard; j++)  // strictly ascending: distinct entries
+      ok = memcmp(one.dictionary.data() + (j - 1) * dw, one.dictionary.data() + j * dw, dw) != 0;
+    if (!ok) {
+      bad++;
+      fprintf(stderr, "transcode mismatch: iter %ld type %d n %d card %llu\n", it, type, n, (unsigned long long)card);
+    }
+  }
+  printf("transcode columns=%ld mismatches=%ld\n", cols, bad);
+  return bad ? 1 : 0;
+}
+
 int main(int argc, char **argv) {
+  if (argc > 1 && strcmp(argv[1], "transcode") == 0)
+    return transcode_check(argc > 2 ? atol(argv[2]) : 200, argc > 3 ? strtoull(argv[3], nullptr, 10) : 7);
   if (argc > 1 && strcmp(argv[1], "fmt") == 0) {  // fmt d:<16 hex> | f:<8 hex> ...: Double/Float.toString lines
     for (int i = 2; i < argc; i++) {
       const unsigned long long u = strtoull(argv[i] + 2, nullptr, 16);

@@ -216,6 +216,19 @@ def test_sanitizer_fuzz_of_descriptors_and_planner():
         assert int(broker["ok"]) > 0 and int(broker["rejected"]) > 0
 
 
+@pytest.mark.skipif(not _clangxx() or shutil.which("make") is None, reason="no ROCm clang++ for the sanitizer build")
+def test_parallel_raw_transcode_matches_serial():
+    """Raw-column transcoding (registration's host step, segment_parse.cpp) on several threads: byte-identical to
+    one thread, every doc's dictId reads back to its value, dictionary strictly ascending — INT / LONG / FLOAT /
+    DOUBLE with NaN payloads and signed zeros, var-byte STRING; under ASan + UBSan."""
+    subprocess.run(["make", "-s", "-C", PKG, "fuzz"], check=True, timeout=600)
+    exe = os.path.join(PKG, "build", "fuzz_host")
+    r = subprocess.run([exe, "transcode", "120", "11"], capture_output=True, text=True, timeout=600,
+                       env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1"))
+    assert r.returncode == 0, r.stdout + r.stderr[-4000:]
+    assert "transcode columns=120 mismatches=0" in r.stdout, r.stdout
+
+
 # Double.toString / Float.toString (DoubleDictionary / FloatDictionary.getStringValue, the group-key strings):
 # outputs of the JDK for these values, as its javadoc specifies them
 JAVA_DOUBLE = [(1.0, "1.0"), (0.1, "0.1"), (100.0, "100.0"), (1e7, "1.0E7"), (9999999.0, "9999999.0"),

@@ -157,3 +157,39 @@ def test_raw_fp_primitive_comparisons(engine):
             got = np.unpackbits(bits.view(np.uint8), bitorder="little")[:len(vals)].astype(bool)
             assert cnt == int(exp.sum()) and (got == exp).all(), tree
     g.release()
+
+
+def test_large_raw_columns_threaded_transcode(engine):
+    """3 M-doc raw columns: registration transcodes them on several host threads (segment_parse.cpp); the result
+    answers exactly as the dictionary registration of the same values."""
+    rng = np.random.default_rng(950)
+    n = 3_000_000
+    words = np.array(["w%03d" % i for i in range(300)], dtype=object)
+    cols = {"big": ("INT", rng.integers(-2 ** 31, 2 ** 31, n).astype(np.int32)),
+            "lng": ("LONG", rng.integers(0, 1000, n).astype(np.int64) * 1_000_003 - 7),
+            "dbl": ("DOUBLE", np.where(rng.random(n) < 0.01, -0.0, np.round(rng.normal(0, 50, n), 2))),
+            "s": ("STRING", words[rng.integers(0, words.shape[0], n)]),
+            "k": ("INT", rng.integers(0, 40, n).astype(np.int32))}
+    raw = build_segment("rawbig", cols, raw_columns=("big", "lng", "dbl", "s"), allow_sorted=False)
+    dic = build_segment("dicbig", cols, allow_sorted=False)
+    gr, gd = engine.register(raw), engine.register(dic)
+    try:
+        ex = ServerQueryExecutor(engine)
+        for text in ("SELECT COUNT(*), SUM(lng), MIN(big), MAX(dbl), DISTINCTCOUNTHLL(s) FROM t WHERE big > 0 AND "
+                     "lng BETWEEN 1000003 AND 500000000 AND s IN ('w001', 'w150', 'w299', 'zz')",
+                     "SELECT SUM(dbl), MAX(lng), COUNT(*) FROM t WHERE s >= 'w100' OR k = 3",
+                     "SELECT COUNT(*), SUM(lng), MIN(dbl) FROM t WHERE big < 0 GROUP BY s, k"):
+            q = compile_pql(text)
+            a, sa = ex.process_query(q, [gr], trim=False)
+            b, sb = ex.process_query(q, [gd], trim=False)
+            assert sa.num_docs_scanned == sb.num_docs_scanned, text
+            if q.get("group_by"):
+                assert set(a) == set(b), text
+                pairs = [(a[k], b[k]) for k in a]
+            else:
+                pairs = [(a, b)]
+            for x, y in pairs:
+                assert [_norm(v) for v in x] == [_norm(v) for v in y], text
+    finally:
+        gr.release()
+        gd.release()

@@ -202,3 +202,27 @@ def test_ragged_loopback_server(K):
             _check_agg(q, got, exp)
     finally:
         srv.close()
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_ragged_exact_filter_stats(seed):
+    """stats.exact=1 over segments of independent sizes and dictionaries: numEntriesScannedInFilter is the sum of
+    each segment's replay of the iterator protocol (oracle/iter_stats.py), for aggregation and group-by plans."""
+    import iter_stats
+    from test_gpu_parity import _random_aggs, _random_segment, _random_tree
+    rng = np.random.default_rng(2600 + seed)
+    sizes = [int(rng.choice([1, 64, 777, 5000, 20000])) for _ in range(int(rng.integers(2, 4)))]
+    segs = [_random_segment(rng, n, name="rs%d" % i) for i, n in enumerate(sizes)]
+    e = GpuEngine(0, "stats.exact=1")
+    try:
+        gs = [e.register(s) for s in segs]
+        ex = ServerQueryExecutor(e)
+        for it in range(10):
+            tree = _random_tree(rng, segs[int(rng.integers(0, len(segs)))])
+            group = {"columns": ["i0"], "top_n": 10} if it % 2 else None
+            q = {"aggregations": _random_aggs(rng), "filter": tree, "group_by": group}
+            _, st = ex.process_query(q, gs, trim=False) if group else ex.process_query(q, gs)
+            want = sum(iter_stats.entries_scanned_in_filter(s, tree) for s in segs)
+            assert st.num_entries_scanned_in_filter == want, (sizes, tree)
+    finally:
+        e.close()

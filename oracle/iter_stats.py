@@ -268,7 +268,7 @@ class OrIt:
 
 class Set:
     def __init__(self, kind, mask=None, n=0, mv=False):
-        self.kind, self.mask, self.kids, self.mv = kind, mask, [], mv
+        self.kind, self.mask, self.kids, self.mv, self.n = kind, mask, [], mv, n
         self.minv, self.maxv = 0, n - 1
         self.pairs = []
         if kind == "SORTED":
@@ -350,7 +350,7 @@ class Set:
                 rest.append(k.iterator())
         if not sorted_ and not bitmaps:
             return AndIt([k.iterator() for k in self.kids])
-        n = self.kids[0].mask.shape[0]
+        n = self.n
         answer = None
         for s in sorted_:
             m = self._pairs_mask(s.pairs, n)
@@ -365,7 +365,7 @@ class Set:
     def _or_iterator(self):
         its = []
         if any(k.kind == "BITMAP" for k in self.kids):
-            n = self.kids[0].mask.shape[0]
+            n = self.n
             u = np.zeros(n, dtype=bool)
             for k in self.kids:
                 if k.kind == "SORTED":

@@ -291,13 +291,15 @@ class Job:
 def timed_steps(job, step, steps, warmup):
     """W untimed warm-ups, then exactly K steps bracketed by barrier + device sync; max over ranks."""
     import torch
+    # the harness's own collector pauses stay out of the timed steps (the C-ABI call has none); collected before the
+    # warm-ups so the timed steps follow them with no idle gap on the device
+    gc.collect()
+    gc.disable()
     for _ in range(warmup):
         step()
     job.barrier()
     torch.cuda.synchronize()
     job.synchronize()
-    gc.collect()
-    gc.disable()  # the harness's own collector pauses stay out of the timed steps (the C-ABI call has none)
     t0 = time.perf_counter()
     step_ms, abi_ms, dev_ms = [], [], []
     res = st = None

@@ -226,3 +226,4 @@ def test_ragged_exact_filter_stats(seed):
             assert st.num_entries_scanned_in_filter == want, (sizes, tree)
     finally:
         e.close()
+

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define PINOT_GPU_ABI_VERSION 11
+#define PINOT_GPU_ABI_VERSION 12
 
 /* ------------------------------------------------------------------ status */
 typedef enum {
@@ -246,8 +246,11 @@ pinot_status pinot_gpu_segment_load(pinot_engine *engine, const char *index_dir,
  * directory whose segment name and CRC match a cached device copy returns that copy's handle (*cache_hit = 1; only
  * metadata.properties and creation.meta are read); otherwise the directory is loaded as pinot_gpu_segment_load does,
  * a cached copy of the same name with another CRC is released (the segment was replaced), and the new copy is
- * cached (*cache_hit = 0). A directory without creation.meta is loaded and never cached. A cached handle stays valid
- * until pinot_gpu_segment_release (which drops it from the cache) or its replacement. */
+ * cached (*cache_hit = 0). A directory without creation.meta is loaded and never cached. Acquires are reference-counted
+ * like SegmentDataManager.increaseReferenceCount / releaseSegment (BaseTableDataManager.java): every acquire of a
+ * handle takes one reference, pinot_gpu_segment_release returns one, and the device copy is dropped when the last
+ * reference returns. A replaced copy (new CRC) leaves the cache at once but stays valid for its holders until they
+ * release it. */
 pinot_status pinot_gpu_segment_acquire(pinot_engine *engine, const char *index_dir, pinot_segment_handle *out,
                                        int32_t *cache_hit);
 /* The same read and checks on the host only (no engine, no GPU): docs, served columns, left-out columns. */
@@ -296,6 +299,16 @@ pinot_status pinot_gpu_aggregate(pinot_engine *engine, const pinot_segment_handl
 pinot_status pinot_gpu_group_by(pinot_engine *engine, const pinot_segment_handle *segments,
                                 int32_t num_segments, const pinot_query *query,
                                 pinot_groupby_result **out, pinot_exec_stats *stats);
+/* The group-by as the server hands it to the DataTable: CombineGroupByOperator's trim
+ * (AggregationGroupByTrimmingService.trimIntermediateResultsMap, :71-116; CombineGroupByOperator.java:184-215) runs on
+ * the device before any group leaves it. Above 4 x trimSize groups (trimSize = max(5 * top_n, 5000)) the result holds
+ * only the union of the functions' trimmed maps (pinot_groupby_trim with the same top_n lists each function's groups;
+ * another top_n is PINOT_ERR_BAD_ARG); otherwise every group, as pinot_gpu_group_by. Ties: lower raw key first. The
+ * device trim applies to dense key spaces; hashed, multi-value and star-tree group-bys return every group and trim
+ * on the host (pinot_groupby_trim). */
+pinot_status pinot_gpu_group_by_top(pinot_engine *engine, const pinot_segment_handle *segments,
+                                    int32_t num_segments, const pinot_query *query, int32_t top_n,
+                                    pinot_groupby_result **out, pinot_exec_stats *stats);
 int64_t pinot_groupby_num_groups(const pinot_groupby_result *r);
 int32_t pinot_groupby_num_columns(const pinot_groupby_result *r);
 /* '\t'-joined group key string (DictionaryBasedGroupKeyGenerator.getGroupKey); NUL-terminated. */
@@ -504,6 +517,9 @@ pinot_status pinot_gpu_synchronize(pinot_engine *engine);
 /* Device time (ms) of the named kernel class in the last call, for the roofline report:
  * kind 0 = scan/filter kernel, 1 = aggregation kernel. */
 pinot_status pinot_gpu_last_kernel_ms(pinot_engine *engine, int32_t kind, double *ms, int64_t *launches);
+/* Engine counters (diagnostics, no Java counterpart): "group.ring_queries" = group-bys answered on the ring plan,
+ * "group.ring_fallbacks" = ring-plan group-bys re-answered on the counted plan (a region overflowed: skewed keys). */
+pinot_status pinot_gpu_engine_stat(pinot_engine *engine, const char *name, int64_t *value);
 
 #ifdef __cplusplus
 }

@@ -144,6 +144,7 @@ void parse_config(Engine &e, const char *cfg) {
     else if (k == "group.nt_store") e.group_nt_store = std::stoi(v) != 0;
     else if (k == "group.prefetch") e.group_prefetch = v == "1" || v == "true";
     else if (k == "group.bucket") e.group_bucket = v == "1" || v == "true";
+    else if (k == "group.ring") e.group_ring = v == "1" || v == "true";
     else if (k == "group.aligned") e.group_aligned = v == "1" || v == "true";
     else if (k == "group.emit_block") {
       e.group_emit_block = std::stoi(v);
@@ -271,16 +272,23 @@ pinot_status pinot_gpu_segment_acquire(pinot_engine *engine, const char *index_d
     auto it = has_crc ? engine->segment_cache.find(name) : engine->segment_cache.end();
     if (it != engine->segment_cache.end() && it->second.first == crc && engine->segments.count(it->second.second)) {
       *out = it->second.second;
+      engine->acquire_refs[*out]++;
       if (cache_hit) *cache_hit = 1;
       return;
     }
     const int64_t h = load_segment_dir(*engine, index_dir);
-    if (it != engine->segment_cache.end()) {  // replaced: drop the stale device copy
-      PINOT_HIP(hipStreamSynchronize(engine->stream));
-      engine->segments.erase(it->second.second);
+    if (it != engine->segment_cache.end()) {  // replaced: out of the cache now, dropped once its holders release it
+      const int64_t old = it->second.second;
       engine->segment_cache.erase(it);
+      auto r = engine->acquire_refs.find(old);
+      if (r == engine->acquire_refs.end() || r->second <= 0) {
+        PINOT_HIP(hipStreamSynchronize(engine->stream));
+        engine->segments.erase(old);
+        if (r != engine->acquire_refs.end()) engine->acquire_refs.erase(r);
+      }
     }
     if (has_crc) engine->segment_cache[name] = {crc, h};
+    engine->acquire_refs[h] = 1;
     *out = h;
     if (cache_hit) *cache_hit = 0;
   });
@@ -339,8 +347,14 @@ pinot_status pinot_gpu_segment_release(pinot_engine *engine, pinot_segment_handl
     require(engine != nullptr, PINOT_ERR_BAD_ARG, "null engine");
     std::lock_guard<std::mutex> lk(engine->mu);
     set_device(*engine);
+    require(engine->segments.count(handle) == 1, PINOT_ERR_BAD_ARG, "unknown segment handle");
+    auto r = engine->acquire_refs.find(handle);
+    if (r != engine->acquire_refs.end()) {  // an acquired handle: the last reference drops the device copy
+      if (--r->second > 0) return;
+      engine->acquire_refs.erase(r);
+    }
     PINOT_HIP(hipStreamSynchronize(engine->stream));
-    require(engine->segments.erase(handle) == 1, PINOT_ERR_BAD_ARG, "unknown segment handle");
+    engine->segments.erase(handle);
     for (auto it = engine->segment_cache.begin(); it != engine->segment_cache.end(); ++it)
       if (it->second.second == handle) {
         engine->segment_cache.erase(it);
@@ -409,10 +423,12 @@ pinot_status pinot_gpu_aggregate(pinot_engine *engine, const pinot_segment_handl
   });
 }
 
-pinot_status pinot_gpu_group_by(pinot_engine *engine, const pinot_segment_handle *segments, int32_t num_segments,
-                                const pinot_query *query, pinot_groupby_result **out, pinot_exec_stats *stats) {
+namespace {
+pinot_status group_by_call(pinot_engine *engine, const pinot_segment_handle *segments, int32_t num_segments,
+                           const pinot_query *query, int32_t top_n, pinot_groupby_result **out, pinot_exec_stats *stats) {
   return guard([&] {
     require(engine && out, PINOT_ERR_BAD_ARG, "null argument");
+    require(top_n >= 0, PINOT_ERR_BAD_ARG, "top_n must be positive (AggregationGroupByTrimmingService.java:52)");
     check_query(query);
     require(query->num_group_by >= 1, PINOT_ERR_BAD_ARG, "aggregation-only query passed to pinot_gpu_group_by");
     const auto t0 = std::chrono::steady_clock::now();
@@ -427,6 +443,11 @@ pinot_status pinot_gpu_group_by(pinot_engine *engine, const pinot_segment_handle
       if (stats) memset(stats, 0, sizeof(*stats));
     } else {
       engine->star_answered.clear();
+      struct TrimScope {
+        Engine &e;
+        ~TrimScope() { e.trim_top_n = 0; }
+      } ts{*engine};
+      engine->trim_top_n = top_n;
       r = exec_group_by(*engine, kept, *query, stats);
       exact_filter_stats(*engine, kept, *query, stats);
     }
@@ -438,6 +459,20 @@ pinot_status pinot_gpu_group_by(pinot_engine *engine, const pinot_segment_handle
     static_cast<GroupByResult &>(*res) = std::move(*r);
     *out = res;
   });
+}
+}  // namespace
+
+pinot_status pinot_gpu_group_by(pinot_engine *engine, const pinot_segment_handle *segments, int32_t num_segments,
+                                const pinot_query *query, pinot_groupby_result **out, pinot_exec_stats *stats) {
+  return group_by_call(engine, segments, num_segments, query, 0, out, stats);
+}
+
+pinot_status pinot_gpu_group_by_top(pinot_engine *engine, const pinot_segment_handle *segments, int32_t num_segments,
+                                    const pinot_query *query, int32_t top_n, pinot_groupby_result **out,
+                                    pinot_exec_stats *stats) {
+  if (top_n <= 0)
+    return guard([&] { require(false, PINOT_ERR_BAD_ARG, "top_n must be positive (AggregationGroupByTrimmingService.java:52)"); });
+  return group_by_call(engine, segments, num_segments, query, top_n, out, stats);
 }
 
 int64_t pinot_groupby_num_groups(const pinot_groupby_result *r) { return r ? (int64_t)r->raw_keys.size() : 0; }
@@ -747,6 +782,16 @@ pinot_status pinot_gpu_last_kernel_ms(pinot_engine *engine, int32_t kind, double
     require(engine && kind >= 0 && kind < 2, PINOT_ERR_BAD_ARG, "kind");
     if (ms) *ms = engine->last_ms[kind];
     if (launches) *launches = engine->last_launches[kind];
+  });
+}
+
+pinot_status pinot_gpu_engine_stat(pinot_engine *engine, const char *name, int64_t *value) {
+  return guard([&] {
+    require(engine && name && value, PINOT_ERR_BAD_ARG, "engine, name, value");
+    const std::string n = name;
+    if (n == "group.ring_queries") *value = engine->ring_queries;
+    else if (n == "group.ring_fallbacks") *value = engine->ring_fallbacks;
+    else require(false, PINOT_ERR_BAD_ARG, "unknown engine stat");
   });
 }
 

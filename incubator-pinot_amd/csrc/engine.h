@@ -90,6 +90,7 @@ void validate_segment(const pinot_segment_desc &d);
 // The pruning metadata of a column descriptor (bloom filter bytes or creation from the decoded dictionary, partition
 // metadata) into c; c's dictionary must be decoded already (parse_column calls it).
 void parse_pruning_metadata(ColumnData &c, const pinot_column_desc &d);
+void parse_dictionary_only(ColumnData &c, const pinot_column_desc &d);  // dictionary + pruning metadata only
 void parse_multi_value(ColumnData &c, const pinot_column_desc &d, int32_t num_docs);
 std::string java_double_to_string(double v);  // Double.toString
 std::string java_float_to_string(float v);    // Float.toString
@@ -223,6 +224,7 @@ struct Engine {
   std::unordered_map<int64_t, std::unique_ptr<SegmentData>> segments;
   // device segment cache: segment name -> (creation.meta CRC, handle) (pinot_gpu_segment_acquire)
   std::unordered_map<std::string, std::pair<int64_t, int64_t>> segment_cache;
+  std::unordered_map<int64_t, int64_t> acquire_refs;  // handle -> references taken by pinot_gpu_segment_acquire
 
   // configuration
   int num_groups_limit = 100000;
@@ -255,6 +257,10 @@ struct Engine {
   bool group_aligned = false; // group.aligned: bucketed EMIT runs padded to 64-B buckets (measured: EMIT -1.6%, reduce slower)
   int group_lw = 2;           // group.lw: partitioned plan reads 0 per doc, 1 each lane's 64-doc word, 2 contiguous quarters
   bool group_bucket = true;   // group.bucket: partitioned plan EMITs through LDS buckets into the final layout
+  bool group_ring = true;     // group.ring: large dense key spaces take the ring plan (no histogram pass; group_ring.hip)
+  int32_t trim_top_n = 0;      // per call (pinot_gpu_group_by_top): trim the group-by on the device for this TOP n
+  int64_t ring_queries = 0;    // group-bys launched on the ring plan
+  int64_t ring_fallbacks = 0;  // ring-plan queries re-answered on the counted plan (a region overflowed: skewed keys)
   int num_cus = 256;          // multiProcessorCount of the device
 
   // scratch (grow-only)
@@ -272,6 +278,7 @@ struct Engine {
   DeviceBuffer group_gather;   // multi-GPU root: every rank's per-group outputs, gathered
   PinnedBuffer group_host;     // their pinned host copy
   std::vector<std::shared_ptr<DeviceBuffer>> hll_pool;  // gathered HLL registers, reused once results are released
+  DeviceBuffer group_trim;     // device trim: union keys, per-group function bits, sort / scan scratch
   DeviceBuffer group_hash;     // hashed key spaces: fingerprint table + representative docs
   DeviceBuffer group_admit;    // num.groups.limit admission: first docs [S][G], admitted bitmaps [S][G/32], sort scratch
   PinnedBuffer host_arena;    // staging of the per-query arena (H2D)
@@ -369,6 +376,10 @@ struct GroupByResult {
   uint64_t export_keys(char *buf, uint64_t buf_len, int64_t *offsets) const;
   // AggregationGroupByTrimmingService: the groups of function fn's trimmed map (ascending)
   std::vector<int64_t> trim(int32_t top_n, int32_t fn) const;
+  // trimmed on the device (pinot_gpu_group_by_top): the result holds the union of the functions' trimmed maps and
+  // fn_kept[fn] lists fn's groups; 0 = not trimmed (every group)
+  int32_t trimmed_top_n = 0;
+  std::vector<std::vector<int64_t>> fn_kept;
   // DISTINCTCOUNTHLL: cardinalities per fn; registers on the host (hll[fn]) or on the device in parts (one per
   // GPU that finalized a key range: [groups][256] u8 at off[fn], copied on request)
   std::vector<HostVec<int64_t>> hll_card;

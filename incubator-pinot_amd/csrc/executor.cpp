@@ -1356,6 +1356,9 @@ void exec_aggregate_star(Engine &e, const std::vector<SegmentData *> &segs, cons
   std::vector<unsigned long long> init(5 * kMaxAggs, 0ull);
   for (int g = 0; g < kMaxAggs; g++) init[5 * g + 3] = ~0ull;
   PINOT_HIP(hipEventRecord(e.ev_start, e.stream));
+  // the HLL register block is max-merged across the segments: zero it once (the fused, MV and earlier star queries
+  // leave their registers in the same buffer)
+  PINOT_HIP(hipMemsetAsync(dev + kOut, 0, kHll, e.stream));
   std::vector<std::vector<unsigned long long>> parts(S);
   DeviceBuffer bits;
   for (size_t si = 0; si < S; si++) {
@@ -2182,6 +2185,10 @@ uint64_t GroupByResult::export_keys(char *buf, uint64_t buf_len, int64_t *offset
 // cardinality) — MIN ascending, every other function descending (getSorter :160-176). The reference's heap keeps
 // an arbitrary member of a tie at the boundary; here the lower raw key wins.
 std::vector<int64_t> GroupByResult::trim(int32_t top_n, int32_t fn) const {
+  if (trimmed_top_n) {  // the device already kept each function's trimSize best groups
+    require(top_n == trimmed_top_n, PINOT_ERR_BAD_ARG, "result was trimmed on the device for another TOP n");
+    return fn_kept.at(fn);
+  }
   const int64_t n = (int64_t)raw_keys.size();
   const int64_t trim_size = std::max<int64_t>(5 * (int64_t)top_n, 5000);
   std::vector<int64_t> idx(n);
@@ -2410,6 +2417,95 @@ GroupPlan plan_group(const std::vector<SegmentData *> &segs, const pinot_query &
   return gp;
 }
 
+// Ring plan (group_ring.hip): the partitioned plan without its histogram pass. Applies to dense key spaces whose
+// partitions of K <= 1024 keys number at most kRingMaxPartitions (k_group_ring's LDS rings), read through the
+// lane-owns-quarter decoder (<= 4 columns of <= 20 bits) with records of <= 53 bits.
+constexpr int64_t kRingMaxPartitions = 1024;
+constexpr size_t kRingReduceLds = 160 * 1024;
+struct RingPlan {
+  bool on = false;
+  int shift = 0;
+  int64_t P = 0;
+  std::vector<int> field_shift, lds_off;
+  int cnt_off = 0, hist_off = 0, exc_off = 0, lds_bytes = 0;
+  uint32_t cap = 0;        // records per region the allocation holds
+  int64_t nblk = 0;
+  int64_t total_chunks = 0;
+};
+
+RingPlan plan_ring(const Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q, const KeySpace &ks,
+                   const GroupAccs &gx, int64_t total_chunks) {
+  RingPlan rp;
+  const int na = q.num_aggregations;
+  if (ks.G <= 0 || ks.G > (int64_t)UINT32_MAX || total_chunks <= 0) return rp;
+  // columns: the group columns, then one slot per distinct accumulator (as the EMIT prefetch lists them)
+  int nc = q.num_group_by;
+  for (int a = 0; a < na; a++) nc += gx.acc_kind[a] != 5;
+  if (nc > kGroupPfCols) return rp;
+  for (auto *s : segs) {
+    for (int j = 0; j < q.num_group_by; j++)
+      if (s->column(q.group_by[j])->bits > kGroupLwMaxBits) return rp;
+    for (int a = 0; a < na; a++)
+      if (gx.acc_kind[a] != 5 && s->column(agg_column(q.aggregations[a]))->bits > kGroupLwMaxBits) return rp;
+  }
+  const size_t nblk = (size_t)e.num_cus;
+  const size_t fixed = nblk * 4 + (4 + (size_t)ring_reduce_exceptions()) * 4 + 256;
+  size_t per_key = 4;
+  for (int a = 0; a < na; a++)
+    if (gx.acc_kind[a] != 5) per_key += gx.acc_kind[a] == 4 ? 128 : 8;
+  int s = 10;
+  while (s > 0 && ((size_t)1 << s) * per_key + fixed > kRingReduceLds) s--;
+  const int64_t need = (ks.G + kRingMaxPartitions - 1) / kRingMaxPartitions;  // K >= G / max partitions
+  if (((int64_t)1 << s) < need) return rp;
+  while (s > 5 && ((ks.G + ((int64_t)1 << (s - 1)) - 1) >> (s - 1)) <= kRingMaxPartitions &&
+         ((ks.G + ((int64_t)1 << s) - 1) >> s) < 2 * (int64_t)nblk)
+    s--;  // small key spaces: more, smaller partitions for the reduce's grid
+  const int64_t K = (int64_t)1 << s;
+  rp.P = (ks.G + K - 1) / K;
+  if (rp.P > kRingMaxPartitions || ring_lds_bytes((int)rp.P) > kRingReduceLds) return rp;
+  // record layout: [s bits local key | one field per distinct aggregated column]
+  rp.field_shift.assign(na, 0);
+  std::map<std::string, int> col_field;
+  int bits = s;
+  for (int a = 0; a < na; a++) {
+    if (gx.acc_kind[a] == 5) continue;
+    const std::string c = agg_column(q.aggregations[a]);
+    auto it = col_field.find(c);
+    if (it == col_field.end()) {
+      it = col_field.emplace(c, bits).first;
+      bits += segs[0]->column(c)->bits;
+    }
+    rp.field_shift[a] = it->second;
+  }
+  if (bits > 53) return rp;
+  // allocation: every doc of the largest block matching
+  const int64_t max_docs = (total_chunks + (int64_t)nblk - 1) / (int64_t)nblk * 4096;
+  const uint32_t cap = ring_region_records((uint64_t)max_docs, K, ks.G, UINT32_MAX);
+  if (cap > (1u << 20)) return rp;
+  rp.cap = cap;
+  // reduce LDS: accumulators (nibble HLL [K][128 B], 8-B others), counts u32 [K], hist row, exception list
+  rp.lds_off.assign(na, 0);
+  size_t off = 0;
+  for (int a = 0; a < na; a++) {
+    if (gx.acc_kind[a] == 5) continue;
+    rp.lds_off[a] = (int)off;
+    off += ((size_t)K * (gx.acc_kind[a] == 4 ? 128 : 8) + 15) / 16 * 16;
+  }
+  rp.cnt_off = (int)off;
+  off += (size_t)K * 4;
+  rp.hist_off = (int)off;
+  off += (nblk * 4 + 15) / 16 * 16;
+  rp.exc_off = (int)off;
+  off += (4 + (size_t)ring_reduce_exceptions()) * 4;
+  if (off > kRingReduceLds) return rp;
+  rp.lds_bytes = (int)off;
+  rp.shift = s;
+  rp.nblk = (int64_t)nblk;
+  rp.total_chunks = total_chunks;
+  rp.on = true;
+  return rp;
+}
+
 // num.groups.limit, per segment and across segments:
 //   * DictionaryBasedGroupKeyGenerator (:79-126): a segment whose cardinality product exceeds
 //     max.init.group.holder.capacity uses a map holder that gives group ids to the first
@@ -2555,7 +2651,8 @@ unsigned long long compact_dense(Engine &e, const unsigned long long *counts, in
 
 // Device half of build_dense_result: the final arrays of the n non-empty groups in the host result's layout
 // (k_group_final) and the HLL registers gathered per group, all on the device (no sync).
-DenseOut dense_outputs(Engine &e, const DenseGroups &d, const long long *keys_dev, unsigned long long n) {
+DenseOut dense_outputs(Engine &e, const DenseGroups &d, const long long *keys_dev, unsigned long long n,
+                       bool gather_hll = true) {
   const pinot_query &q = *d.q;
   const GroupAccs &ga = *d.ga, &gx = *d.gx;
   const std::vector<int> &alias = *d.alias;
@@ -2636,7 +2733,7 @@ DenseOut dense_outputs(Engine &e, const DenseGroups &d, const long long *keys_de
   }
   launch_group_final(d.counts, keys_dev, (long long)n, f, e.stream);
   PINOT_HIP(hipGetLastError());
-  if (n_hll) {  // registers stay on the device until asked for; buffers are recycled once their result is released
+  if (n_hll && gather_hll) {  // registers stay on the device until asked for; buffers are recycled once released
     const size_t need = (size_t)n_hll * n * 256 + 16;
     for (auto &b : e.hll_pool)
       if (b.use_count() == 1 && b->size() >= need) { o.hll = b; break; }
@@ -2847,6 +2944,49 @@ std::unique_ptr<GroupByResult> build_dense_result(Engine &e, const DenseGroups &
   return dense_fetch(e, *d.q, d.ks->gcard, d.ks->gvalues, o, d.hashed);
 }
 
+// CombineGroupByOperator's trim (AggregationGroupByTrimmingService.trimIntermediateResultsMap :71-116) on the device,
+// before anything leaves it: above 4 x trimSize groups (trimSize = max(5 * TOP, 5000)) every function keeps its
+// trimSize best groups (getSorter :160-176: MIN ascending, the others descending; AVG by sum / count, HLL by
+// cardinality; ties in ascending raw key order); the result holds the union of the kept groups and each function's
+// list. Returns the union's keys (device) and sets n to its size; `kept` stays empty when nothing is trimmed.
+const long long *device_trim(Engine &e, const DenseGroups &d, const long long *keys_dev, unsigned long long &n,
+                             int32_t top_n, std::vector<std::vector<int64_t>> &kept) {
+  const int64_t T = std::max<int64_t>(5 * (int64_t)top_n, 5000);
+  if ((int64_t)n <= 4 * T || d.hashed) return keys_dev;
+  const pinot_query &q = *d.q;
+  const int na = q.num_aggregations;
+  const DenseOut o = dense_outputs(e, d, keys_dev, n, false);  // comparable values of every group, no registers
+  const size_t scr = trim_scratch_bytes((long long)n);
+  const size_t a8 = ((size_t)n * 8 + 255) / 256 * 256, a4 = ((size_t)n * 4 + 255) / 256 * 256;
+  e.group_trim.reserve(a8 + 2 * a4 + 256 + scr);
+  uint8_t *p = e.group_trim.get<uint8_t>();
+  auto *ukeys = reinterpret_cast<long long *>(p);
+  auto *flags = reinterpret_cast<uint32_t *>(p + a8);
+  auto *uflags = reinterpret_cast<uint32_t *>(p + a8 + a4);
+  auto *n_dev = reinterpret_cast<unsigned long long *>(p + a8 + 2 * a4);
+  void *tmp = p + a8 + 2 * a4 + 256;
+  PINOT_HIP(hipMemsetAsync(flags, 0, (size_t)n * 4, e.stream));
+  for (int i = 0; i < na; i++) {
+    const int f = sv_function(q.aggregations[i].function);
+    launch_trim_select(o.values[i], o.counts, f == PINOT_AGG_AVG, f == PINOT_AGG_MIN, (long long)n, T, 1u << i, flags,
+                       tmp, scr, e.stream);
+  }
+  launch_trim_union(flags, keys_dev, (long long)n, ukeys, uflags, n_dev, tmp, scr, e.stream);
+  PINOT_HIP(hipGetLastError());
+  unsigned long long nu = 0;
+  PINOT_HIP(hipMemcpyAsync(&nu, n_dev, 8, hipMemcpyDeviceToHost, e.stream));
+  wait_stream(e);
+  std::vector<uint32_t> hf(nu);
+  if (nu) PINOT_HIP(hipMemcpyAsync(hf.data(), uflags, nu * 4, hipMemcpyDeviceToHost, e.stream));
+  wait_stream(e);
+  kept.assign(na, {});
+  for (int i = 0; i < na; i++) kept[i].reserve((size_t)T);
+  for (unsigned long long g = 0; g < nu; g++)
+    for (uint32_t x = hf[g]; x; x &= x - 1u) kept[__builtin_ctz(x)].push_back((int64_t)g);
+  n = nu;
+  return ukeys;
+}
+
 std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q,
                                                    const KeySpace &ks_in, const GroupAccs &ga, pinot_exec_stats *stats,
                                                    int attempt = 0, const PartialOut *po = nullptr,
@@ -2892,6 +3032,31 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     plans[si].seg = segs[si];
     Compiler(e, plans[si], ar).run_fused(tree.get(), kGroupMaxFusedLeafBits);
   }
+  // chunk windows (a single sorted leaf bounds the chunks a segment's program visits), concatenated: the ring plan's
+  // blocks split the global chunk list evenly
+  std::vector<std::pair<int64_t, int64_t>> windows(S);
+  std::vector<int64_t> cstart(S + 1, 0);
+  for (size_t si = 0; si < S; si++) {
+    windows[si] = chunk_window(plans[si], ar);
+    const int64_t nch = plans[si].empty ? 0 : (plans[si].seg->nwords() + 63) / 64;
+    const int64_t n = std::max<int64_t>(0, std::min(nch, windows[si].second) - windows[si].first);
+    cstart[si + 1] = cstart[si] + n;
+  }
+  RingPlan rp;
+  if (e.group_ring && gp.mode == GB_EMIT && !ks.hashed && !adm.active && !pin && e.debug_emit == 0 && e.group_prefetch &&
+      e.group_lw == 2 && e.group_bucket && e.group_pshift < 0)
+    rp = plan_ring(e, segs, q, ks, gx, cstart[S]);
+  // a ring region overflowed (keys skewed beyond the regions' slack) or a bound tripped: the counted plan answers
+  auto ring_fallback = [&]() {
+    e.ring_fallbacks++;
+    struct Restore {
+      Engine &e;
+      bool v;
+      ~Restore() { e.group_ring = v; }
+    } restore{e, e.group_ring};
+    e.group_ring = false;
+    return exec_group_by_fused(e, segs, q, ks_in, ga, stats, attempt, po, pin, allow_admission);
+  };
   const auto tga = std::chrono::steady_clock::now();
   // remaps (dictId -> global id) travel in the arena
   std::vector<std::vector<size_t>> remap_off(S, std::vector<size_t>(q.num_group_by, SIZE_MAX));
@@ -2900,7 +3065,7 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
       if (!ks.remap[si][j].empty()) remap_off[si][j] = ar.add(ks.remap[si][j].data(), ks.remap[si][j].size() * 4);
   size_t n_leaves = 0;
   for (auto &p : plans) n_leaves += p.fused_leaves.size();
-  const size_t tab_bytes = S * sizeof(GroupSegment) + n_leaves * sizeof(FusedStep) +
+  const size_t tab_bytes = (S + 1) * 8 + 32 + S * sizeof(GroupSegment) + n_leaves * sizeof(FusedStep) +
                            S * q.num_group_by * sizeof(GroupColDev) + S * na * sizeof(GroupAggDev) + 512;
   QueryScratch qs = prepare_scratch(e, plans, ar, true, tab_bytes);
 
@@ -2965,7 +3130,7 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     g.first_gcol = (int32_t)gcols.size();
     g.first_agg = (int32_t)gaggs.size();
     g.admitted = adm.active ? ab.bitmaps + si * ab.words : nullptr;
-    std::tie(g.ch_begin, g.ch_end) = chunk_window(p, ar);
+    std::tie(g.ch_begin, g.ch_end) = windows[si];
     for (const FilterStep &l : p.fused_leaves) {
       leaves.push_back(fused_leaf_step(s, l, qs.arena));
       max_leaf_bits = std::max(max_leaf_bits, leaves.back().bits);
@@ -3001,7 +3166,7 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
           ag.affine_step = c.affine_step;
         }
       }
-      ag.field_shift = gp.field_shift[a];
+      ag.field_shift = rp.on ? rp.field_shift[a] : gp.field_shift[a];
       ag.lds_off = gp.lds_off[a];
       gaggs.push_back(ag);
     }
@@ -3010,6 +3175,7 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
   const size_t off_leaves = ar.add(leaves.data(), leaves.size() * sizeof(FusedStep));
   const size_t off_gcols = ar.add(gcols.data(), gcols.size() * sizeof(GroupColDev));
   const size_t off_aggs = ar.add(gaggs.data(), gaggs.size() * sizeof(GroupAggDev));
+  const size_t off_cstart = ar.add(cstart.data(), cstart.size() * 8);
   require(ar.bytes.size() <= e.small.size(), PINOT_ERR_DEVICE, "query arena overflow");
 
   GroupArgs a{};
@@ -3086,7 +3252,80 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     build_admitted(e, adm, S, ks.G, ab);
   }
   const auto tgu = std::chrono::steady_clock::now();
+  uint32_t *ring_status = nullptr;  // ring plan: [0] status bits, [1] region records (k_group_ring)
   if (pin) {
+  } else if (rp.on) {  // GB_FILTER -> k_group_ring -> k_ring_reduce (group_ring.hip): every key written, no memset
+    const size_t nblk = (size_t)rp.nblk;
+    const size_t hist_n = (size_t)rp.P * nblk;
+    const size_t hist_b = (hist_n * 4 + 255) / 256 * 256, bm_b = (nblk * 4 + 255) / 256 * 256;
+    e.group_part.reserve(hist_b + bm_b + 256);
+    uint8_t *pb = e.group_part.get<uint8_t>();
+    auto *hist = reinterpret_cast<uint32_t *>(pb);
+    auto *blk_matched = reinterpret_cast<uint32_t *>(pb + hist_b);
+    ring_status = reinterpret_cast<uint32_t *>(pb + hist_b + bm_b);
+    e.group_records.reserve((size_t)rp.P * nblk * rp.cap * 8 + 64);
+    int64_t fstride = 0;
+    for (auto *sg : segs) fstride = std::max<int64_t>(fstride, sg->nwords());
+    fstride = (fstride + 63) / 64 * 64;
+    e.group_filter.reserve((size_t)S * fstride * 8 + 512);
+    GroupArgs af = a;
+    af.mode = GB_FILTER;
+    af.filter_out = e.group_filter.get<uint64_t>();
+    af.filter_stride = fstride;
+    af.cstart = reinterpret_cast<const int64_t *>(qs.arena + off_cstart);
+    af.total_chunks = rp.total_chunks;
+    af.ring_blocks = (int32_t)nblk;
+    af.blk_matched = blk_matched;
+    RingArgs ra{};
+    ra.segs = a.segs;
+    ra.gcols = a.gcols;
+    ra.aggs = a.aggs;
+    ra.cstart = af.cstart;
+    ra.filter = af.filter_out;
+    ra.filter_stride = fstride;
+    ra.total_chunks = rp.total_chunks;
+    ra.G = ks.G;
+    ra.nsegs = (int32_t)S;
+    ra.n_gcols = q.num_group_by;
+    ra.nc = a.pf_nc;
+    for (int i = 0; i < 4; i++) ra.pf_agg[i] = a.pf_agg[i];
+    ra.P = (int32_t)rp.P;
+    ra.shift = rp.shift;
+    ra.nblk = (int32_t)nblk;
+    ra.cap = rp.cap;
+    ra.blk_matched = blk_matched;
+    ra.records = e.group_records.get<unsigned long long>();
+    ra.hist = hist;
+    ra.status = ring_status;
+    ra.region = ring_status + 1;
+    RingReduceArgs rr{};
+    rr.records = ra.records;
+    rr.hist = hist;
+    rr.region = ra.region;
+    rr.P = (int32_t)rp.P;
+    rr.shift = rp.shift;
+    rr.n_aggs = na;
+    rr.nblk = (int32_t)nblk;
+    rr.lds_bytes = rr.lds_zero_bytes = rp.lds_bytes;
+    rr.cnt_off = rp.cnt_off;
+    rr.hist_off = rp.hist_off;
+    rr.exc_off = rp.exc_off;
+    rr.G = ks.G;
+    rr.counts = counts;
+    rr.status = ring_status;
+    for (int i = 0; i < na; i++) {
+      rr.aggs[i] = gaggs[i];  // segment 0's dictionary / LUT: identical on every segment (checked by plan_group)
+      rr.aggs[i].lds_off = rp.lds_off[i];
+    }
+    require(a.pf_nc > 0, PINOT_ERR_DEVICE, "ring plan without its column list");
+    PINOT_HIP(hipMemsetAsync(blk_matched, 0, bm_b + 256, e.stream));
+    e.ring_queries++;
+    t.timed(1, [&] {
+      launch_group_query(af, e.stream);
+      launch_group_ring(ra, e.stream);
+      launch_ring_reduce(rr, e.stream);
+    });
+    PINOT_HIP(hipGetLastError());
   } else if (gp.mode != GB_EMIT) {  // identities: counts / sums 0, min all-ones, max 0, HLL 0
     PINOT_HIP(hipMemsetAsync(counts, 0, ks.G * 8, e.stream));
     for (int i = 0; i < na; i++)
@@ -3181,9 +3420,12 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
                                  hipMemcpyDeviceToDevice, e.stream));
     PINOT_HIP(hipGetLastError());
     std::vector<unsigned long long> hm(S);
+    uint32_t rstat = 0;
     PINOT_HIP(hipMemcpyAsync(hm.data(), matched, S * 8, hipMemcpyDeviceToHost, e.stream));
+    if (ring_status) PINOT_HIP(hipMemcpyAsync(&rstat, ring_status, 4, hipMemcpyDeviceToHost, e.stream));
     PINOT_HIP(hipEventRecord(e.ev_stop, e.stream));
     wait_stream(e);
+    if (rstat) return ring_fallback();
     float pms = 0;
     PINOT_HIP(hipEventElapsedTime(&pms, e.ev_start, e.ev_stop));
     t.collect();
@@ -3200,17 +3442,28 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
   std::vector<unsigned long long> hmatched(S);
   uint32_t verify_err = 0;
   long long *keys_dev = nullptr;
+  uint32_t rstat = 0;
   const unsigned long long n = compact_dense(e, counts, ks.G, keys_dev, [&] {
     PINOT_HIP(hipMemcpyAsync(hmatched.data(), matched, S * 8, hipMemcpyDeviceToHost, e.stream));
     if (ks.hashed) PINOT_HIP(hipMemcpyAsync(&verify_err, a.verify_err, 4, hipMemcpyDeviceToHost, e.stream));
+    if (ring_status) PINOT_HIP(hipMemcpyAsync(&rstat, ring_status, 4, hipMemcpyDeviceToHost, e.stream));
   });
+  if (rstat) return ring_fallback();
   if (verify_err) {  // 64-bit fingerprint collision: retry with another seed
     require(attempt < 3, PINOT_ERR_DEVICE, "group-key fingerprint collisions persist");
     return exec_group_by_fused(e, segs, q, ks_in, ga, stats, attempt + 1);
   }
   const auto tg3 = std::chrono::steady_clock::now();
   DenseGroups dg{&q, &ks, &ga, &gx, &alias, counts, accs, 0, ks.hashed ? &a : nullptr};
-  auto res = build_dense_result(e, dg, keys_dev, n);
+  std::vector<std::vector<int64_t>> kept;
+  unsigned long long nres = n;
+  const long long *rkeys = keys_dev;
+  if (e.trim_top_n > 0) rkeys = device_trim(e, dg, keys_dev, nres, e.trim_top_n, kept);
+  auto res = build_dense_result(e, dg, rkeys, nres);
+  if (!kept.empty()) {
+    res->trimmed_top_n = e.trim_top_n;
+    res->fn_kept = std::move(kept);
+  }
   const auto tg4 = std::chrono::steady_clock::now();
   PINOT_HIP(hipEventRecord(e.ev_stop, e.stream));
   wait_stream(e);

@@ -440,7 +440,87 @@ __global__ void k_admit_bitmap(const uint32_t *__restrict__ first_doc, long long
   }
 }
 
+// AggregationGroupByTrimmingService's per-function selection on the device: the sort key of each group is its
+// comparable value (COUNT / SUM / MIN / MAX the intermediate value, AVG sum / count, DISTINCTCOUNTHLL the cardinality:
+// k_group_final's out_values, getSorter :160-176) as an order-preserving u64, flipped for the descending functions; a
+// stable radix sort then ranks the groups with ties in ascending raw key order (the group index order).
+__global__ void k_trim_keys(const double *__restrict__ vals, const long long *__restrict__ counts, int avg, int asc,
+                            long long n, unsigned long long *__restrict__ keys, uint32_t *__restrict__ idx) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    double v = vals[i];
+    if (avg) v = v / (double)counts[i];
+    if (v == 0.0) v = 0.0;  // -0.0 ties with 0.0, as the host's comparison does
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    const unsigned long long o = (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
+    keys[i] = asc ? o : ~o;
+    idx[i] = (uint32_t)i;
+  }
+}
+
+__global__ void k_trim_mark(const uint32_t *__restrict__ idx, long long T, uint32_t bit, uint32_t *__restrict__ flags) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < T; i += (long long)gridDim.x * blockDim.x)
+    flags[idx[i]] |= bit;  // one function per launch: no two threads touch one group
+}
+
+__global__ void k_nonzero(const uint32_t *__restrict__ flags, long long n, uint32_t *__restrict__ out) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    out[i] = flags[i] != 0u;
+}
+
+__global__ void k_union_scatter(const uint32_t *__restrict__ flags, const uint32_t *__restrict__ pos,
+                                const long long *__restrict__ keys, long long n, long long *__restrict__ keys_out,
+                                uint32_t *__restrict__ flags_out, unsigned long long *__restrict__ n_out) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const uint32_t f = flags[i];
+    if (f) {
+      keys_out[pos[i]] = keys[i];
+      flags_out[pos[i]] = f;
+    }
+    if (i == n - 1) *n_out = (unsigned long long)pos[i] + (f != 0u);
+  }
+}
+
 }  // namespace
+
+size_t trim_scratch_bytes(long long n) {
+  size_t sort = 0, scan = 0;
+  PINOT_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, sort, (const unsigned long long *)nullptr,
+                                               (unsigned long long *)nullptr, (const uint32_t *)nullptr,
+                                               (uint32_t *)nullptr, (int)n));
+  scan = exclusive_sum_u32(nullptr, nullptr, n, nullptr, 0, nullptr);
+  const size_t a8 = ((size_t)n * 8 + 255) / 256 * 256, a4 = ((size_t)n * 4 + 255) / 256 * 256;
+  return 2 * a8 + 2 * a4 + std::max(sort, scan) + 256;
+}
+
+void launch_trim_select(const double *vals, const long long *counts, int avg, int asc, long long n, long long T,
+                        uint32_t bit, uint32_t *flags, void *scratch, size_t scratch_bytes, hipStream_t stream) {
+  if (n <= 0) return;
+  const size_t a8 = ((size_t)n * 8 + 255) / 256 * 256, a4 = ((size_t)n * 4 + 255) / 256 * 256;
+  uint8_t *p = static_cast<uint8_t *>(scratch);
+  auto *k_in = reinterpret_cast<unsigned long long *>(p), *k_out = reinterpret_cast<unsigned long long *>(p + a8);
+  auto *i_in = reinterpret_cast<uint32_t *>(p + 2 * a8), *i_out = reinterpret_cast<uint32_t *>(p + 2 * a8 + a4);
+  void *tmp = p + 2 * a8 + 2 * a4;
+  size_t tb = scratch_bytes - (2 * a8 + 2 * a4);
+  const int grid = (int)std::min<long long>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_trim_keys, dim3(grid), dim3(256), 0, stream, vals, counts, avg, asc, n, k_in, i_in);
+  PINOT_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tb, k_in, k_out, i_in, i_out, (int)n, 0, 64, stream));
+  const long long t = std::min(T, n);
+  hipLaunchKernelGGL(k_trim_mark, dim3((int)std::min<long long>((t + 255) / 256, 4096)), dim3(256), 0, stream, i_out, t,
+                     bit, flags);
+}
+
+void launch_trim_union(const uint32_t *flags, const long long *keys, long long n, long long *keys_out,
+                       uint32_t *flags_out, unsigned long long *n_out, void *scratch, size_t scratch_bytes,
+                       hipStream_t stream) {
+  if (n <= 0) return;
+  const size_t a4 = ((size_t)n * 4 + 255) / 256 * 256;
+  uint8_t *p = static_cast<uint8_t *>(scratch);
+  auto *nz = reinterpret_cast<uint32_t *>(p), *pos = reinterpret_cast<uint32_t *>(p + a4);
+  const int grid = (int)std::min<long long>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_nonzero, dim3(grid), dim3(256), 0, stream, flags, n, nz);
+  exclusive_sum_u32(nz, pos, n, p + 2 * a4, scratch_bytes - 2 * a4, stream);
+  hipLaunchKernelGGL(k_union_scatter, dim3(grid), dim3(256), 0, stream, flags, pos, keys, n, keys_out, flags_out, n_out);
+}
 
 __global__ void k_key_bitmap(const unsigned long long *__restrict__ counts, long long G, uint64_t *bits) {
   const long long nw = (G + 63) / 64;

@@ -239,7 +239,10 @@ int scan_query_blocks_per_cu(int stage_bytes, bool gathers, bool pipelined);
 //   GB_EMIT2   pass 2 of the bucketed partitioned plan: the filter words GB_COUNT wrote (no filter re-evaluation),
 //              records appended to per-block LDS buckets of kBucketRecs records per partition and written out
 //              whole into the FINAL partition layout (offsets from GB_COUNT's histogram): no split pass
-enum GroupMode : int32_t { GB_GLOBAL = 0, GB_LDS = 1, GB_COUNT = 2, GB_EMIT = 3, GB_VERIFY = 4, GB_FIRST = 5, GB_EMIT2 = 6 };
+//   GB_FILTER  the ring plan's first pass (group_ring.hip): the filter program alone, its words per segment into
+//              filter_out and every ring block's matching docs into blk_matched (the ring regions' size)
+enum GroupMode : int32_t { GB_GLOBAL = 0, GB_LDS = 1, GB_COUNT = 2, GB_EMIT = 3, GB_VERIFY = 4, GB_FIRST = 5, GB_EMIT2 = 6,
+                           GB_FILTER = 7 };
 constexpr int kBucketRecs = 8;                                   // 64-B bucket flushes
 constexpr unsigned long long kRecInvalid = ~0ull;                // padding slot of an aligned run (bit 63 set)
 constexpr int kRecPartShift = 52;  // GB_EMIT2 records carry their partition in bits [52, 63) (bucketed plan: <= 52 record bits)
@@ -323,6 +326,13 @@ struct GroupArgs {
                                // backwards, and the padding slots are written with kRecInvalid
   int32_t emit_block;          // GB_EMIT2 lane-owns-quarter: threads per block (512, or 1024 = group.emit_block)
   int64_t filter_stride;       // words per segment in filter_out
+  // GB_FILTER: chunk c of segment g's window is global chunk cstart[g] + (c - ch_begin); global chunk i belongs to
+  // ring block i * ring_blocks / total_chunks, whose matching docs accumulate in blk_matched
+  const int64_t *cstart;
+  int64_t total_chunks;
+  int32_t ring_blocks;
+  int32_t reserved3;
+  uint32_t *blk_matched;
 };
 constexpr int kGroupPfCols = 4;
 constexpr int kGroupLwMaxBits = 20;  // widest column the lane-owns-word decode handles
@@ -342,6 +352,48 @@ struct PartitionReduceArgs {
   GroupAggDev aggs[kMaxGroupAggs];  // fwd unused; dict / hll_lut / acc / lds_off / acc_kind / field_shift / bits
 };
 void launch_partition_reduce(const PartitionReduceArgs &a, hipStream_t stream);
+
+// ---------------------------------------------------------------- ring plan (group_ring.hip)
+// Large dense key spaces without a histogram pass: GB_FILTER -> k_group_ring (records into fixed-capacity regions
+// [P][nblk][C], C from the busiest block's matching docs) -> k_ring_reduce (one block per partition of 2^shift keys).
+struct RingArgs {
+  const GroupSegment *segs;
+  const GroupColDev *gcols;
+  const GroupAggDev *aggs;
+  const int64_t *cstart;         // [nsegs + 1]: first global chunk of each segment's chunk window
+  const uint64_t *filter;        // GB_FILTER's words, [nsegs][filter_stride]
+  int64_t filter_stride;
+  int64_t total_chunks;
+  long long G;
+  int32_t nsegs, n_gcols, nc, P;  // nc: columns read per doc (the group columns, then the pf_agg fields)
+  int32_t pf_agg[4];
+  int32_t shift, nblk;            // nblk: blocks of the launch (one per CU): block b owns chunks [T b / nblk, T (b+1) / nblk)
+  uint32_t cap;                   // records per region the allocation holds
+  int32_t reserved;
+  const uint32_t *blk_matched;    // [nblk] matching docs per block (GB_FILTER)
+  unsigned long long *records;    // [P][nblk][C] (local key | dictId fields)
+  uint32_t *hist;                 // [P][nblk] records claimed per region (> C: overflow)
+  uint32_t *status;               // |= 1 a region overflowed, 2 a spin bound was hit, 4 HLL exception list full
+  uint32_t *region;               // C, written by block 0 (read by k_ring_reduce)
+};
+struct RingReduceArgs {
+  const unsigned long long *records;
+  const uint32_t *hist;
+  const uint32_t *region;
+  int32_t P, shift, n_aggs, nblk;
+  int32_t lds_bytes, lds_zero_bytes;
+  int32_t cnt_off, hist_off, exc_off;  // LDS: counts u32 [K], hist row u32 [nblk], exceptions (count + entries)
+  int32_t reserved;
+  long long G;
+  unsigned long long *counts;
+  uint32_t *status;
+  GroupAggDev aggs[kMaxGroupAggs];  // lds_off / acc_kind / field_shift / bits / dict / hll_lut / affine / acc
+};
+__host__ __device__ uint32_t ring_region_records(uint64_t max_block_docs, int64_t K, int64_t G, uint32_t cap);
+size_t ring_lds_bytes(int P);  // k_group_ring's dynamic LDS
+void launch_group_ring(const RingArgs &a, hipStream_t stream);
+void launch_ring_reduce(const RingReduceArgs &a, hipStream_t stream);
+int ring_reduce_exceptions();  // LDS exception entries per partition
 // Two-level partitioned plan, second level: coarse run (q, b) of `runs` (2^split partitions' records
 // emitted by block b) is split into the partitions' final slots offsets[p][b]... of `records`.
 void launch_partition_split(const uint32_t *hist, const uint32_t *offsets, const uint32_t *pstart, int32_t P,
@@ -384,6 +436,15 @@ struct GroupFinalArgs {
   unsigned int *out_card32[kMaxGroupAggs];
   unsigned int *overflow;
 };
+// Server-side trimming on the device (AggregationGroupByTrimmingService.trimIntermediateResultsMap :71-116): per function,
+// flags[g] |= bit for the T best groups of its comparable values (vals = k_group_final's out_values; avg: / counts;
+// asc: MIN), ties in ascending group order; then the union of flagged groups compacted in group order.
+size_t trim_scratch_bytes(long long n);
+void launch_trim_select(const double *vals, const long long *counts, int avg, int asc, long long n, long long T,
+                        uint32_t bit, uint32_t *flags, void *scratch, size_t scratch_bytes, hipStream_t stream);
+void launch_trim_union(const uint32_t *flags, const long long *keys, long long n, long long *keys_out,
+                       uint32_t *flags_out, unsigned long long *n_out, void *scratch, size_t scratch_bytes,
+                       hipStream_t stream);
 // bit k of bits[k >> 6] = counts[k] != 0 (the non-empty keys the compaction lists, as a bitmap)
 void launch_key_bitmap(const unsigned long long *counts, long long G, uint64_t *bits, hipStream_t stream);
 void launch_group_final(const unsigned long long *counts, const long long *keys, long long n, const GroupFinalArgs &f,

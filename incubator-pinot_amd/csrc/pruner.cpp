@@ -264,9 +264,11 @@ bool prune_segment_desc(const pinot_segment_desc &d, const pinot_query &q, const
       if (it == meta.end()) {
         ColumnData &m = meta[name];
         if (cd->create_bloom_filter || cd->num_partition_values == -1) {  // built from the decoded dictionary
-          ParsedIndexes idx;
+          // a dictionary column decodes its dictionary only; a raw column needs its values sorted into one (the
+          // transcode registration does: O(N log N) per call, not cached — register the segment to pay it once)
           TranscodedColumn tc;
-          parse_column(m, transcode_raw(*cd, d.num_docs, tc) ? tc.desc : *cd, d.num_docs, idx);
+          if (transcode_raw(*cd, d.num_docs, tc)) parse_dictionary_only(m, tc.desc);
+          else parse_dictionary_only(m, *cd);
         } else {
           m.name = name;
           m.data_type = cd->data_type;

@@ -402,6 +402,21 @@ void parse_multi_value(ColumnData &c, const pinot_column_desc &d, int32_t num_do
 // BloomFilterHandler does at load (BloomFilterHandler.java:107-116: creator.add(dictionaryReader.get(i)) for every
 // dictId; Dictionary.getStringValue is that toString for every type). Partition metadata as ColumnMetadata reads it
 // (ColumnMetadata.java:184-194).
+// The dictionary and pruning metadata of a dictionary-encoded column, nothing else (no forward or inverted index):
+// the stateless pruning call builds bloom filters / partition lists from it (pruner.cpp prune_segment_desc).
+void parse_dictionary_only(ColumnData &c, const pinot_column_desc &d) {
+  require(d.name != nullptr, PINOT_ERR_BAD_ARG, "column without name");
+  c.name = d.name;
+  c.data_type = d.data_type;
+  require(d.cardinality >= 0, PINOT_ERR_BAD_ARG, c.name + ": negative cardinality");
+  c.card = d.cardinality;
+  c.string_width = d.string_width;
+  require(d.padding_byte >= 0 && d.padding_byte <= 255, PINOT_ERR_BAD_ARG, c.name + ": padding byte out of range");
+  c.string_pad = d.padding_byte;
+  decode_dictionary(c, d);
+  parse_pruning_metadata(c, d);
+}
+
 void parse_pruning_metadata(ColumnData &c, const pinot_column_desc &d) {
   require(!(d.bloom_filter && d.create_bloom_filter), PINOT_ERR_BAD_ARG,
           c.name + ": bloom filter bytes and create_bloom_filter together");

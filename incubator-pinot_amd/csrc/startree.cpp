@@ -160,9 +160,19 @@ void attach_star_tree(Engine &e, SegmentData &seg, const pinot_star_tree_desc &d
   plain_desc.columns = plain.data();
   plain_desc.num_columns = (int32_t)plain.size();
   st->docs = register_segment(e, plain_desc);
+  // ValueAggregatorFactory's value types: COUNT (and AvgPair's count half) LONG, SUM / MIN / MAX (and AvgPair's sum
+  // half) DOUBLE — the star aggregation reads the counts as exact integers and the others as doubles
+  auto ends_with = [](const std::string &a, const char *b) {
+    const size_t n = strlen(b);
+    return a.size() >= n && a.compare(a.size() - n, n, b) == 0;
+  };
   for (auto &c : st->docs->cols)
-    if (c->name.find("__") != std::string::npos)
+    if (c->name.find("__") != std::string::npos) {
       require(c->numeric(), PINOT_ERR_BAD_ARG, seg.name + ": star-tree metric " + c->name + " must be numeric");
+      const bool count = c->name.rfind("count__", 0) == 0 || ends_with(c->name, ".count");
+      require(count ? c->data_type == PINOT_LONG : c->data_type == PINOT_DOUBLE, PINOT_ERR_BAD_ARG,
+              seg.name + ": star-tree metric " + c->name + (count ? " must be LONG" : " must be DOUBLE"));
+    }
   seg.device_bytes += st->docs->device_bytes;
   seg.star = std::move(st);
 }

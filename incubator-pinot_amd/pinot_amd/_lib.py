@@ -36,14 +36,14 @@ EXPORTED_SYMBOLS = [
     "pinot_gpu_segment_register", "pinot_gpu_segment_release", "pinot_gpu_segment_validate",
     "pinot_gpu_segment_load", "pinot_gpu_segment_acquire", "pinot_gpu_segment_attach_star_tree",
     "pinot_gpu_segment_dir_info",
-    "pinot_gpu_segment_device_bytes", "pinot_gpu_filter", "pinot_gpu_aggregate", "pinot_gpu_group_by",
+    "pinot_gpu_segment_device_bytes", "pinot_gpu_filter", "pinot_gpu_aggregate", "pinot_gpu_group_by", "pinot_gpu_group_by_top",
     "pinot_groupby_num_groups", "pinot_groupby_num_columns", "pinot_groupby_key", "pinot_groupby_values",
     "pinot_groupby_hll", "pinot_groupby_raw_keys", "pinot_groupby_export_keys", "pinot_groupby_trim",
     "pinot_groupby_free", "pinot_datatable_aggregation", "pinot_datatable_group_by", "pinot_datatable_empty",
     "pinot_gpu_prune_segments", "pinot_segment_prune", "pinot_gpu_server_prune_segments", "pinot_broker_reduce",
     "pinot_gpu_group_by_layout", "pinot_gpu_group_by_partial", "pinot_gpu_group_by_finalize",
     "pinot_gpu_segment_register_synthetic", "pinot_gpu_segment_register_synthetic_ex", "pinot_gpu_synchronize",
-    "pinot_gpu_last_kernel_ms",
+    "pinot_gpu_last_kernel_ms", "pinot_gpu_engine_stat",
     "pinot_gpu_server_create", "pinot_gpu_server_unique_id", "pinot_gpu_server_create_rank", "pinot_gpu_server_destroy",
     "pinot_gpu_server_num_engines", "pinot_gpu_server_engine", "pinot_gpu_server_aggregate", "pinot_gpu_server_group_by",
     "pinot_gpu_server_last_phases",
@@ -180,6 +180,8 @@ def load(path=None):
         "pinot_gpu_aggregate": (i32, [P, C.POINTER(i64), i32, C.POINTER(Query), C.POINTER(AggResult),
                                       C.POINTER(ExecStats)]),
         "pinot_gpu_group_by": (i32, [P, C.POINTER(i64), i32, C.POINTER(Query), C.POINTER(P), C.POINTER(ExecStats)]),
+        "pinot_gpu_group_by_top": (i32, [P, C.POINTER(i64), i32, C.POINTER(Query), i32, C.POINTER(P),
+                                         C.POINTER(ExecStats)]),
         "pinot_groupby_num_groups": (i64, [P]),
         "pinot_groupby_num_columns": (i32, [P]),
         "pinot_groupby_key": (C.c_char_p, [P, i64]),
@@ -211,6 +213,7 @@ def load(path=None):
                                                           C.POINTER(i32), C.POINTER(i32), u64, C.POINTER(i64)]),
         "pinot_gpu_synchronize": (i32, [P]),
         "pinot_gpu_last_kernel_ms": (i32, [P, i32, C.POINTER(C.c_double), C.POINTER(i64)]),
+        "pinot_gpu_engine_stat": (i32, [P, C.c_char_p, C.POINTER(i64)]),
         "pinot_gpu_server_create": (i32, [C.POINTER(i32), i32, C.c_char_p, C.POINTER(P)]),
         "pinot_gpu_server_unique_id": (i32, [P]),
         "pinot_gpu_server_create_rank": (i32, [i32, i32, i32, P, C.c_char_p, C.POINTER(P)]),

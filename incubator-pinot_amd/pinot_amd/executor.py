@@ -285,7 +285,8 @@ class GpuEngine:
 
     def acquire(self, index_dir: str):
         """pinot_gpu_segment_acquire: the device segment cache (segment name + creation.meta CRC). Returns
-        (GpuSegment, cache_hit); a hit is the cached copy's handle, a changed CRC replaces (releases) the old copy."""
+        (GpuSegment, cache_hit); a hit is the cached copy's handle, a changed CRC replaces the old copy in the cache.
+        Every returned GpuSegment holds one reference: release() returns it, the last one drops the device copy."""
         h, hit = C.c_int64(), C.c_int32()
         check(self.lib.pinot_gpu_segment_acquire(self.ptr, os.fsencode(index_dir), C.byref(h), C.byref(hit)))
         n = C.c_int32()
@@ -316,6 +317,12 @@ class GpuEngine:
         n = C.c_int64()
         check(self.lib.pinot_gpu_last_kernel_ms(self.ptr, kind, C.byref(ms), C.byref(n)))
         return ms.value, n.value
+
+    def stat(self, name):
+        """Engine counter (pinot_gpu_engine_stat): "group.ring_queries", "group.ring_fallbacks"."""
+        v = C.c_int64()
+        check(self.lib.pinot_gpu_engine_stat(self.ptr, name.encode(), C.byref(v)))
+        return v.value
 
     # ---------------------------------------------------------------- filter
     def filter(self, seg: GpuSegment, filter_tree):
@@ -667,10 +674,14 @@ class ServerQueryExecutor:
         stats = _lib.ExecStats()
         if query.get("group_by"):
             out = C.c_void_p()
-            check(lib.pinot_gpu_group_by(self.engine.ptr, handles, len(segments), C.byref(m.q), C.byref(out),
-                                         C.byref(stats)))
-            res = GroupByResult(lib, out, query).to_map(
-                trim_top_n=query["group_by"].get("top_n", 10) if trim else None)
+            top_n = query["group_by"].get("top_n", 10) if trim else None
+            if top_n:  # CombineGroupByOperator's trim on the device: only the kept groups leave it
+                check(lib.pinot_gpu_group_by_top(self.engine.ptr, handles, len(segments), C.byref(m.q), top_n,
+                                                 C.byref(out), C.byref(stats)))
+            else:
+                check(lib.pinot_gpu_group_by(self.engine.ptr, handles, len(segments), C.byref(m.q), C.byref(out),
+                                             C.byref(stats)))
+            res = GroupByResult(lib, out, query).to_map(trim_top_n=top_n)
         else:
             n = len(query["aggregations"])
             out = (_lib.AggResult * n)()
@@ -707,12 +718,17 @@ class ServerQueryExecutor:
         stats = _lib.ExecStats()
         if query.get("group_by"):
             out = C.c_void_p()
-            check(lib.pinot_gpu_group_by(self.engine.ptr, handles, len(segments), C.byref(m.q), C.byref(out),
-                                         C.byref(stats)))
+            top_n = query["group_by"].get("top_n", 10) if trim else None
+            if top_n:
+                check(lib.pinot_gpu_group_by_top(self.engine.ptr, handles, len(segments), C.byref(m.q), top_n,
+                                                 C.byref(out), C.byref(stats)))
+            else:
+                check(lib.pinot_gpu_group_by(self.engine.ptr, handles, len(segments), C.byref(m.q), C.byref(out),
+                                             C.byref(stats)))
             if total is not None:
                 stats.num_total_raw_docs = total
             res = GroupByResult(lib, out, query)
-            return res.data_table(m, stats, query["group_by"].get("top_n", 10) if trim else None, srv), _stats(stats)
+            return res.data_table(m, stats, top_n, srv), _stats(stats)
         n = len(query["aggregations"])
         out = (_lib.AggResult * n)()
         check(lib.pinot_gpu_aggregate(self.engine.ptr, handles, len(segments), C.byref(m.q), out, C.byref(stats)))
@@ -724,8 +740,9 @@ class ServerQueryExecutor:
         check(lib.pinot_datatable_aggregation(C.byref(m.q), out, C.byref(stats), srv, buf, need.value, C.byref(need)))
         return buf.raw[:need.value], _stats(stats)
 
-    def group_by_result(self, query, segments):
-        """Raw device group-by result object (no trimming)."""
+    def group_by_result(self, query, segments, top_n=None):
+        """Raw device group-by result object: every group, or with top_n the device-trimmed result the server hands to
+        its DataTable (pinot_gpu_group_by_top: the union of the functions' trimmed maps)."""
         if isinstance(query, PreparedQuery):
             query, m = query.query, query.marshal
         else:
@@ -734,8 +751,12 @@ class ServerQueryExecutor:
             m = QueryMarshal(query, self.num_groups_limit, self.max_init, self.timeout_ms, self.pruners)
         out = C.c_void_p()
         stats = _lib.ExecStats()
-        check(self.engine.lib.pinot_gpu_group_by(self.engine.ptr, _segment_handles(segments), len(segments),
-                                                 C.byref(m.q), C.byref(out), C.byref(stats)))
+        if top_n:
+            check(self.engine.lib.pinot_gpu_group_by_top(self.engine.ptr, _segment_handles(segments), len(segments),
+                                                         C.byref(m.q), int(top_n), C.byref(out), C.byref(stats)))
+        else:
+            check(self.engine.lib.pinot_gpu_group_by(self.engine.ptr, _segment_handles(segments), len(segments),
+                                                     C.byref(m.q), C.byref(out), C.byref(stats)))
         return GroupByResult(self.engine.lib, out, query), stats
 
 

@@ -241,6 +241,42 @@ def test_server_trim_and_bulk_export_1m_groups():
     e.close()
 
 
+def test_device_trim_equals_host_trim():
+    """pinot_gpu_group_by_top (CombineGroupByOperator's trim on the device, AggregationGroupByTrimmingService
+    :71-116): each function's kept groups equal the oracle's trim of the full arrays, the result holds only their
+    union, and the server's DataTable bytes equal the host-trimmed DataTable of the untrimmed result."""
+    e = GpuEngine(0)
+    gsegs, host = _synthetic(e, 2, 2_000_000)
+    q = compile_pql("SELECT COUNT(*), SUM(d8), MIN(d4), MAX(d3), AVG(d9), DISTINCTCOUNTHLL(d5) FROM fact "
+                    "WHERE d2 < 800 GROUP BY d6, d7 TOP 10")
+    exp = O.execute_group_by_arrays(host, q, num_groups_limit=1_000_000)
+    ex = ServerQueryExecutor(e, num_groups_limit=1_000_000)
+    top, st = ex.group_by_result(q, gsegs, top_n=10)
+    assert st.num_docs_scanned == exp["scanned"]
+    ukeys = top.raw_keys()
+    union = set()
+    for fn in range(len(q["aggregations"])):
+        kept = top.trimmed_groups(10, fn)
+        want = exp["keys"][_oracle_trim(exp, q, fn, 10)]
+        assert kept.shape[0] == 5000 and (ukeys[kept] == want).all(), q["aggregations"][fn]
+        union |= set(want.tolist())
+    assert sorted(union) == ukeys.tolist()
+    # the kept groups' values are the full result's
+    pos = np.searchsorted(exp["keys"], ukeys)
+    c, v = top.function_values(1)
+    assert (c == exp["fns"][1]["count"][pos]).all() and (v == exp["fns"][1]["sum"][pos]).all()
+    regs, cards = top.hll(5)
+    assert (cards == exp["fns"][5]["card"][pos]).all() and (regs == exp["fns"][5]["hll"][pos]).all()
+    # DataTable: device trim == host trim of the untrimmed result
+    got, _ = ex.process_query_datatable(q, gsegs, trim=True)
+    full, st2 = ex.group_by_result(q, gsegs)
+    m = ex.prepare(q).marshal
+    ref = full.data_table(m, st2, 10)
+    assert got == ref
+    del top, full
+    e.close()
+
+
 def test_query_timeout_status():
     """pinot_query.timeout_ms: a budget already spent returns PINOT_ERR_TIMEOUT before any device work
     (ServerQueryExecutorV1Impl.java:116-126); a budget shorter than the device work times out in the wait

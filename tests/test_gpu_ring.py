@@ -1,0 +1,135 @@
+"""GPU parity of the ring-partitioned group-by plan (group_ring.hip: GB_FILTER -> k_group_ring -> k_ring_reduce), the
+plan config 4's 1M-key GROUP BY runs on: every group's count, integer sum, ordered MIN / MAX, double sum and HLL
+registers bit-exact against the oracle (DictionaryBasedGroupKeyGenerator.java:195-302,
+DefaultGroupByExecutor.java:70-168), including
+* the HLL registers whose rank exceeds the reduce's 4-bit nibbles (the exception list);
+* chunk windows from a sorted-index leaf, where one block gets all the matching docs (regions sized by the busiest
+  block);
+* per-segment dictionaries of the group columns (dictId -> global id remaps) and ragged segment sizes;
+* skewed keys that overflow a region: the counted plan answers instead (group.ring_fallbacks), same results."""
+import numpy as np
+import pytest
+
+import pinot_oracle as O
+import synth
+from pinot_amd import GpuEngine, ServerQueryExecutor, build_segment, compile_pql
+
+pytestmark = pytest.mark.gpu
+
+CONFIG_COLUMNS = [("d0", 16), ("d1", 100), ("d2", 1000), ("d3", 4096), ("d4", 10000), ("d5", 65536), ("d6", 1000),
+                  ("d7", 1000), ("d8", 1 << 20), ("d9", 1000)]
+BASE_SEED = 0x5EED0000
+CONFIG4 = "SELECT SUM(d8), AVG(d8), DISTINCTCOUNTHLL(d5) FROM fact WHERE d2 < 800 GROUP BY d6, d7 TOP 10"
+
+
+def _assert_group_arrays(res, exp, q):
+    keys = res.raw_keys()
+    assert keys.shape == exp["keys"].shape
+    assert (keys == exp["keys"]).all()
+    for i, (a, r) in enumerate(zip(q["aggregations"], exp["fns"])):
+        f = a["function"].upper()
+        if f == "DISTINCTCOUNTHLL":
+            regs, cards = res.hll(i)
+            assert (cards == r["card"]).all()
+            assert (regs == r["hll"]).all()
+            continue
+        counts, vals = res.function_values(i)
+        assert (counts == r["count"]).all()
+        if f in ("SUM", "AVG"):
+            if np.issubdtype(np.asarray(r["sum"]).dtype, np.floating) and not (vals == r["sum"]).all():
+                np.testing.assert_allclose(vals, r["sum"], rtol=1e-9)  # double sums: 1e-9 relative (north star)
+            else:
+                assert (vals == r["sum"]).all()
+        elif f == "MIN":
+            assert (vals == r["min"]).all()
+        elif f == "MAX":
+            assert (vals == r["max"]).all()
+
+
+def _run(e, q, gsegs, host, limit=1 << 22):
+    exp = O.execute_group_by_arrays(host, q, num_groups_limit=limit)
+    before = e.stat("group.ring_queries"), e.stat("group.ring_fallbacks")
+    res, st = ServerQueryExecutor(e, num_groups_limit=limit).group_by_result(q, gsegs)
+    assert st.num_docs_scanned == exp["scanned"]
+    _assert_group_arrays(res, exp, q)
+    del res
+    return e.stat("group.ring_queries") - before[0], e.stat("group.ring_fallbacks") - before[1]
+
+
+def test_ring_config4_shape():
+    """Config 4's query and table at 2 x 2M docs: 1M keys in 977 partitions of 1024, SUM / AVG over the 20-bit d8
+    (count packed beside the dictId sum), HLL over the 16-bit d5 (~120 ranks > 15 across the groups)."""
+    e = GpuEngine(0)
+    gsegs = [e.register_synthetic("fact_%d" % s, 2_000_000, CONFIG_COLUMNS, BASE_SEED + s) for s in range(2)]
+    host = [synth.make_segment("fact_%d" % s, 2_000_000, CONFIG_COLUMNS, BASE_SEED + s) for s in range(2)]
+    ran, fell = _run(e, compile_pql(CONFIG4), gsegs, host, limit=1_000_000)
+    assert (ran, fell) == (1, 0)
+    # the counted plan on the same engine (group.ring=0) gives the same arrays
+    e.set_config("group.ring=0")
+    ran, fell = _run(e, compile_pql(CONFIG4), gsegs, host, limit=1_000_000)
+    assert (ran, fell) == (0, 0)
+    e.close()
+
+
+def _mixed_segment(name, n, seed, k1_vals, k2_vals, sorted_ts=False):
+    rng = np.random.default_rng(seed)
+    cols = {
+        "k1": ("INT", rng.choice(k1_vals, n).tolist()),
+        "k2": ("STRING", ["s%04d" % v for v in rng.choice(k2_vals, n)]),
+        "f": ("INT", rng.integers(0, 100, n).tolist()),
+        "lv": ("LONG", (rng.integers(-(1 << 40), 1 << 40, n) * 7).tolist()),
+        "dv": ("DOUBLE", (rng.standard_normal(n) * 1e6).round(3).tolist()),
+        "h": ("INT", rng.integers(0, 50000, n).tolist()),
+    }
+    if sorted_ts:
+        cols["ts"] = ("INT", (np.arange(n) // 997).tolist())
+    return build_segment(name, cols)
+
+
+@pytest.mark.parametrize("text", [
+    "SELECT MIN(dv), MAX(lv) FROM t WHERE f < 70 GROUP BY k1, k2",
+    "SELECT SUM(dv), COUNT(*) FROM t WHERE f >= 10 GROUP BY k2, k1",
+    "SELECT SUM(lv), DISTINCTCOUNTHLL(h) FROM t WHERE f <> 5 GROUP BY k1, k2",
+])
+def test_ring_remap_ragged_kinds(text):
+    """Three segments of different sizes whose group dictionaries differ (remapped to the union key space), every
+    accumulator kind the ring reduce folds: ordered MIN / MAX, double and int64 sums, counts, HLL."""
+    segs = [_mixed_segment("r0", 70_001, 1, np.arange(0, 90), np.arange(0, 80)),
+            _mixed_segment("r1", 33_333, 2, np.arange(20, 120), np.arange(10, 95)),
+            _mixed_segment("r2", 120_017, 3, np.arange(5, 100), np.arange(0, 90))]
+    e = GpuEngine(0, "group.mode=partition")
+    gsegs = [e.register(s) for s in segs]
+    ran, fell = _run(e, compile_pql(text), gsegs, segs)
+    assert (ran, fell) == (1, 0)
+    e.close()
+
+
+def test_ring_sorted_window_busiest_block():
+    """A sorted-index leaf bounds each segment's chunk window: all matching docs fall into a few blocks' chunk
+    ranges, so the regions are sized from the busiest block's matches (blk_matched), not the average."""
+    segs = [_mixed_segment("w0", 400_000, 11, np.arange(0, 100), np.arange(0, 100), sorted_ts=True),
+            _mixed_segment("w1", 250_000, 12, np.arange(0, 100), np.arange(0, 100), sorted_ts=True)]
+    e = GpuEngine(0, "group.mode=partition")
+    gsegs = [e.register(s) for s in segs]
+    q = compile_pql("SELECT SUM(lv), MAX(dv) FROM t WHERE ts BETWEEN 40 AND 90 AND f < 95 GROUP BY k1, k2")
+    ran, fell = _run(e, q, gsegs, segs)
+    assert (ran, fell) == (1, 0)
+    e.close()
+
+
+def test_ring_skewed_keys_fall_back():
+    """90 % of the docs on one key: its partition's records overflow every block's region; the query is re-answered
+    on the counted plan with identical results."""
+    n = 600_000
+    rng = np.random.default_rng(5)
+    k1 = np.where(rng.random(n) < 0.9, 3, rng.integers(0, 100, n))
+    k2 = np.where(k1 == 3, 7, rng.integers(0, 100, n))
+    seg = build_segment("skew", {"k1": ("INT", k1.tolist()), "k2": ("INT", k2.tolist()),
+                                 "x": ("INT", rng.integers(0, 1000, n).tolist()),
+                                 "f": ("INT", rng.integers(0, 10, n).tolist())})
+    e = GpuEngine(0, "group.mode=partition")
+    g = e.register(seg)
+    q = compile_pql("SELECT SUM(x), MAX(x) FROM t WHERE f < 8 GROUP BY k1, k2")
+    ran, fell = _run(e, q, [g], [seg])
+    assert (ran, fell) == (1, 1)
+    e.close()

@@ -147,8 +147,9 @@ def test_raw_columns_loaded_from_disk(engine, tmp_path):
 
 @pytest.mark.parametrize("version", ["v1", "v3"])
 def test_segment_cache_by_name_and_crc(tmp_path, version):
-    """pinot_gpu_segment_acquire: the same name + creation.meta CRC is the cached device copy; a new CRC replaces it
-    (the stale handle is gone); no creation.meta is never cached; release drops the entry."""
+    """pinot_gpu_segment_acquire: the same name + creation.meta CRC is the cached device copy; acquires are
+    reference-counted (SegmentDataManager reference counts): a new CRC replaces the cache entry while the old copy
+    stays valid for its holders until the last release; no creation.meta is never cached."""
     from pinot_amd import PinotGpuError
     e = GpuEngine(0)
     try:
@@ -164,23 +165,37 @@ def test_segment_cache_by_name_and_crc(tmp_path, version):
         exp, _ = O.execute_server([seg], q)
         got, _ = ex.process_query(q, [g2])
         assert got == exp
-        # a new build of the segment (another CRC): reloaded, the old copy released
+        # a new build of the segment (another CRC): reloaded and cached; the old copy serves its two holders
         seg_b = _random_segment(41, 6000)
         seg_b.name = seg.name
         d2 = write_segment_dir(seg_b, str(tmp_path / "b"), version=version, crc=-5)
         g3, hit = e.acquire(d2)
         assert not hit and g3.handle != g1.handle
+        got, _ = ex.process_query(q, [g1])
+        assert got == exp
+        old = g1.handle
+        g1.release()
+        got, _ = ex.process_query(q, [g2])
+        assert got == exp
+        g2.release()  # last reference of the replaced copy: dropped
+        g1.handle = old
         with pytest.raises(PinotGpuError):
             ex.process_query(q, [g1])
+        g1.handle = None
         got, _ = ex.process_query(q, [g3])
         assert got == O.execute_server([seg_b], q)[0]
         g4, hit = e.acquire(d2)
         assert hit and g4.handle == g3.handle
-        g3.release()
+        g3.release()  # g4 still holds it: cached, valid
+        got, _ = ex.process_query(q, [g4])
+        assert got == O.execute_server([seg_b], q)[0]
         g5, hit = e.acquire(d2)
-        assert not hit and g5.handle != g3.handle
-        g4.handle = None  # same handle as g3, already released
-        g5.release()
+        assert hit and g5.handle == g4.handle
+        g4.release()
+        g5.release()  # the last reference: the next acquire loads again
+        g6, hit = e.acquire(d2)
+        assert not hit
+        g6.release()
         # no creation.meta: loaded every time
         d3 = write_segment_dir(seg, str(tmp_path / "c"), version=version)
         h1, hit1 = e.acquire(d3)

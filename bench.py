@@ -132,7 +132,8 @@ def cpu_baseline(threads, segs, docs, min_seconds=10.0):
                 "oracle/faithful.c per-doc iterator executor (reference-faithful C restatement: the Java executor "
                 "cannot run here, no JVM)")
         out["optimized" if optimized else "faithful"] = {
-            "value": rows / med, "unit": "rows/s", "cores": threads, "kind": "port",
+            "value": rows / med, "unit": "rows/s", "cores": host_cpu_info()["available_processors"],
+            "threads": threads, "kind": "port",
             "sample": "%d segments x %d docs of the same synthetic table and query, %d runs over %.1fs of CPU work "
                       "(median %.3fs; data generated in %.1fs); %s" % (segs, docs, len(times), sum(times), med, gen_s,
                                                                        what),
@@ -172,7 +173,8 @@ def cpu_baseline_config4(threads, segs, docs, min_seconds=10.0):
     times.sort()
     med = times[len(times) // 2]
     rows = segs * docs
-    return {"value": rows / med, "unit": "rows/s", "cores": threads, "kind": "port",
+    return {"value": rows / med, "unit": "rows/s", "cores": host_cpu_info()["available_processors"], "threads": threads,
+            "kind": "port",
             "sample": "%d segments x %d docs of the same synthetic table and config-4 query, %d runs over %.1fs "
                       "(median %.3fs, %d groups; data generated in %.1fs); oracle/faithful.c per-doc INT_MAP "
                       "group-by + CombineGroupByOperator merge (reference-faithful C restatement: no JVM here)" %
@@ -256,7 +258,9 @@ class Job:
         if not group_by:
             return lambda: self.ex.process_query(q, self.segs)
         if self.path == "engine":
-            return lambda: self.ex.group_by_result(q, self.segs)
+            # what the server hands the broker: the group-by trimmed on the device (CombineGroupByOperator's
+            # AggregationGroupByTrimmingService, TOP 10 -> 5,000 groups per function) serialized as DataTable bytes
+            return lambda: self.ex.process_query_datatable(q, self.segs, trim=True)
         return lambda: self.ex.process_query(q, self.segs, as_result=True)
 
     def set_config(self, cfg):
@@ -405,6 +409,9 @@ def measure(job, args, workload):
     if phases:
         out["merge_phases_ms"] = phases
     if c4:
+        if job.path == "engine":  # the timed step returned DataTable bytes; the full result once for the check
+            out["datatable_bytes"] = len(res)
+            res, _ = job.ex.group_by_result(job.ex.prepare(CONFIG4), job.segs)
         n_groups = res.num_groups()
         counts, sums = res.function_values(1)  # AVG(d8): per-group counts and sums
         chk, _ = job.ex.process_query(job.ex.prepare("SELECT COUNT(*), SUM(d8) FROM fact WHERE d2 < 800"), job.segs)
@@ -500,11 +507,12 @@ def main():
         else:
             cb = cpu_baseline(args.cpu_threads, args.cpu_segments or 16, args.cpu_docs or 32_000_000,
                               args.cpu_seconds)
-        out["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample")}
+        out["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "threads", "kind", "sample")}
         out["cpu_baseline"].update(host_desc)
         out["gpu_vs_cpu"] = out["value"] / cb["value"]
         if "optimized" in cb:  # SURVEY §8(d)'s second CPU line
-            out["cpu_baseline_optimized"] = {k: cb["optimized"][k] for k in ("value", "unit", "cores", "kind", "sample")}
+            out["cpu_baseline_optimized"] = {k: cb["optimized"][k] for k in ("value", "unit", "cores", "threads", "kind",
+                                                                             "sample")}
             out["gpu_vs_cpu_optimized"] = out["value"] / cb["optimized"]["value"]
         if "config4" in out:
             cb4 = cpu_baseline_config4(args.cpu_threads, args.cpu_segments or 16, args.cpu_docs or 4_000_000,

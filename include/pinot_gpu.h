@@ -256,6 +256,12 @@ pinot_status pinot_gpu_segment_acquire(pinot_engine *engine, const char *index_d
 /* The same read and checks on the host only (no engine, no GPU): docs, served columns, left-out columns. */
 pinot_status pinot_gpu_segment_dir_info(const char *index_dir, int32_t *num_docs, int32_t *num_columns,
                                         int32_t *num_skipped);
+/* A raw (no-dictionary) fixed-width forward index file's values, host only: FixedByteChunkSingleValueReader over the
+ * file's bytes (BaseChunkSingleValueReader.java:57-96 header, version 1 always Snappy, version 2 PASS_THROUGH or
+ * Snappy chunks; FixedByteChunkSingleValueReader.getInt / getLong / getFloat / getDouble), as the segment loader reads
+ * .sv.raw.fwd. data_type INT / LONG / FLOAT / DOUBLE; values receives num_docs native-endian values. */
+pinot_status pinot_segment_read_raw_forward_index(const uint8_t *bytes, uint64_t len, int32_t data_type, int32_t num_docs,
+                                          void *values);
 /* Every check pinot_gpu_segment_register makes on the descriptor's bytes (dictionaries, forward-index
  * length, sorted-index tiling, inverted-index offsets and roaring containers), on the host only: no engine,
  * no GPU. PINOT_ERR_BAD_ARG + pinot_gpu_last_error() name the first bad column. */

@@ -306,6 +306,19 @@ pinot_status pinot_gpu_segment_attach_star_tree(pinot_engine *engine, pinot_segm
   });
 }
 
+pinot_status pinot_segment_read_raw_forward_index(const uint8_t *bytes, uint64_t len, int32_t data_type, int32_t num_docs,
+                                          void *values) {
+  return guard([&] {
+    require(bytes && values && num_docs >= 0, PINOT_ERR_BAD_ARG, "null argument");
+    require(data_type >= PINOT_INT && data_type <= PINOT_DOUBLE, PINOT_ERR_BAD_ARG, "fixed-width data type");
+    const int w = (data_type == PINOT_INT || data_type == PINOT_FLOAT) ? 4 : 8;
+    const std::vector<uint8_t> be = read_raw_chunks(bytes, len, num_docs, w, "raw forward index");
+    uint8_t *out = static_cast<uint8_t *>(values);
+    for (size_t i = 0; i < (size_t)num_docs; i++)
+      for (int k = 0; k < w; k++) out[i * w + k] = be[i * w + (w - 1 - k)];  // big-endian -> host (little-endian)
+  });
+}
+
 pinot_status pinot_gpu_segment_dir_info(const char *index_dir, int32_t *num_docs, int32_t *num_columns,
                                         int32_t *num_skipped) {
   return guard([&] {

@@ -91,6 +91,8 @@ void validate_segment(const pinot_segment_desc &d);
 // metadata) into c; c's dictionary must be decoded already (parse_column calls it).
 void parse_pruning_metadata(ColumnData &c, const pinot_column_desc &d);
 void parse_dictionary_only(ColumnData &c, const pinot_column_desc &d);  // dictionary + pruning metadata only
+// FixedByteChunkSingleValueReader over a .sv.raw.fwd file: the docs' values back to back, big-endian (segment_reader.cpp)
+std::vector<uint8_t> read_raw_chunks(const uint8_t *b, uint64_t n, int64_t num_docs, int entry_size, const std::string &what);
 void parse_multi_value(ColumnData &c, const pinot_column_desc &d, int32_t num_docs);
 std::string java_double_to_string(double v);  // Double.toString
 std::string java_float_to_string(float v);    // Float.toString

@@ -10,5 +10,6 @@ from .pql import compile_pql, PqlCompilationException  # noqa: F401
 from .executor import (GpuEngine, GpuSegment, GpuServer, ServerExecutor, ServerQueryExecutor, BrokerReduce,  # noqa: F401
                        AvgPair, HyperLogLog,
                        ExecutionStatistics, trim_intermediate_results, final_result, format_value,
-                       validate_segment, segment_dir_info, prune_segment, empty_datatable)
+                       validate_segment, segment_dir_info, raw_forward_index_values, prune_segment,
+                       empty_datatable)
 from ._lib import PinotGpuError, load as load_library  # noqa: F401

@@ -43,7 +43,7 @@ EXPORTED_SYMBOLS = [
     "pinot_gpu_prune_segments", "pinot_segment_prune", "pinot_gpu_server_prune_segments", "pinot_broker_reduce",
     "pinot_gpu_group_by_layout", "pinot_gpu_group_by_partial", "pinot_gpu_group_by_finalize",
     "pinot_gpu_segment_register_synthetic", "pinot_gpu_segment_register_synthetic_ex", "pinot_gpu_synchronize",
-    "pinot_gpu_last_kernel_ms", "pinot_gpu_engine_stat",
+    "pinot_gpu_last_kernel_ms", "pinot_gpu_engine_stat", "pinot_segment_read_raw_forward_index",
     "pinot_gpu_server_create", "pinot_gpu_server_unique_id", "pinot_gpu_server_create_rank", "pinot_gpu_server_destroy",
     "pinot_gpu_server_num_engines", "pinot_gpu_server_engine", "pinot_gpu_server_aggregate", "pinot_gpu_server_group_by",
     "pinot_gpu_server_last_phases",
@@ -214,6 +214,7 @@ def load(path=None):
         "pinot_gpu_synchronize": (i32, [P]),
         "pinot_gpu_last_kernel_ms": (i32, [P, i32, C.POINTER(C.c_double), C.POINTER(i64)]),
         "pinot_gpu_engine_stat": (i32, [P, C.c_char_p, C.POINTER(i64)]),
+        "pinot_segment_read_raw_forward_index": (i32, [C.c_char_p, u64, i32, i32, P]),
         "pinot_gpu_server_create": (i32, [C.POINTER(i32), i32, C.c_char_p, C.POINTER(P)]),
         "pinot_gpu_server_unique_id": (i32, [P]),
         "pinot_gpu_server_create_rank": (i32, [i32, i32, i32, P, C.c_char_p, C.POINTER(P)]),

@@ -186,6 +186,16 @@ def segment_dir_info(index_dir: str):
     return n.value, c.value, k.value
 
 
+def raw_forward_index_values(buf: bytes, data_type: str, num_docs: int):
+    """pinot_segment_read_raw_forward_index: a fixed-width raw forward index file (.sv.raw.fwd) read by the library's
+    FixedByteChunkSingleValueReader restatement on the host, as a numpy array."""
+    dt = {"INT": (0, np.int32), "LONG": (1, np.int64), "FLOAT": (2, np.float32), "DOUBLE": (3, np.float64)}[data_type]
+    out = np.zeros(max(num_docs, 1), dtype=dt[1])
+    check(_lib.load().pinot_segment_read_raw_forward_index(bytes(buf), len(buf), dt[0], num_docs,
+                                                    out.ctypes.data_as(C.c_void_p)))
+    return out[:num_docs]
+
+
 def validate_segment(seg: Segment) -> None:
     """pinot_gpu_segment_validate: the registration checks on the host alone (no engine, no GPU);
     raises PinotGpuError (BAD_ARG) naming the first bad column."""

@@ -227,3 +227,26 @@ def read_var_byte_strings(buf, num_docs):
             e = rows[r + 1] if r + 1 < per_chunk and rows[r + 1] != 0 else len(chunk)
             out.append(chunk[rows[r]:e].decode("utf-8"))
     return out
+
+
+# ---------------------------------------------------------------- raw fixed-width forward indexes
+def read_fixed_byte_values(buf, num_docs, fmt):
+    """FixedByteChunkSingleValueReader.getInt / getLong / getFloat / getDouble for docs [0, num_docs)
+    (FixedByteChunkSingleValueReader.java over BaseChunkSingleValueReader.java:57-96's header; version 1 is always
+    Snappy): each decompressed chunk holds numDocsPerChunk big-endian values of lengthOfLongestEntry bytes.
+    fmt: the struct code of one value ("i", "q", "f", "d")."""
+    version, num_chunks, per_chunk, longest = struct.unpack_from(">iiii", buf, 0)
+    assert longest == struct.calcsize(">" + fmt)
+    comp, header = 1, 16
+    if version > 1:
+        _total, comp, header = struct.unpack_from(">iii", buf, 16)
+    offs = list(struct.unpack_from(">%di" % num_chunks, buf, header)) + [len(buf)]
+    out = []
+    for c in range(num_chunks):
+        if len(out) >= num_docs:
+            break
+        chunk = bytes(buf[offs[c]:offs[c + 1]])
+        chunk = snappy_uncompress(chunk) if comp == 1 else chunk
+        k = min(per_chunk, num_docs - len(out), len(chunk) // longest)
+        out.extend(struct.unpack_from(">%d%s" % (k, fmt), chunk, 0))
+    return out

@@ -1,14 +1,16 @@
 #!/bin/bash
-# Ring-plan iteration: its GPU parity tests + config-4 shapes, then the config-4 bench line and a rocprofv3 summary.
+# Ring-plan iteration: its GPU parity tests + config-4 shapes + this round's other GPU tests, then the config-4 bench
+# line and a rocprofv3 summary.
 set -o pipefail
 tag=${1:-ring}
 out=gpurun_out/$tag
 mkdir -p $out
-timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_gpu_ring.py \
-  tests/test_gpu_configs.py -k "ring or config4 or trim" > $out/pytest.log 2>&1 || { tail -60 $out/pytest.log; exit 1; }
+timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_gpu_ring.py \
+  tests/test_gpu_configs.py tests/test_gpu_raw.py tests/test_gpu_segment_dir.py tests/test_gpu_startree.py \
+  -k "ring or config4 or trim or fixture or cache or hll or HLL" > $out/pytest.log 2>&1 || { tail -60 $out/pytest.log; exit 1; }
 grep -E "passed|failed" $out/pytest.log | tail -2
 timeout -k 10 300 python bench.py --workload config4 --steps 10 --warmup 3 --cpu-seconds 5 > $out/bench_config4.json 2> $out/bench_config4.err || { tail -20 $out/bench_config4.err; exit 1; }
-tail -1 $out/bench_config4.json | cut -c1-1500
+tail -1 $out/bench_config4.json | cut -c1-2500
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/prof -o run -- python bench.py --workload config4 --steps 5 --warmup 2 --no-cpu-baseline > $out/prof.log 2>&1 || { tail -20 $out/prof.log; exit 1; }
 python scripts/prof_kernels.py $out/prof/run_results.db > $out/kernels.txt 2>&1; head -24 $out/kernels.txt

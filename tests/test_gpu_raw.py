@@ -133,6 +133,39 @@ def test_var_byte_fixture_on_gpu(engine, tmp_path):
     g.release()
 
 
+def test_fixed_byte_fixture_on_gpu(engine, tmp_path):
+    """The reference's data/fixedByteSVRDoubles.v1 (version 1, Snappy; doc i = (double) i for 10,009 docs) as a raw
+    DOUBLE column loaded from a segment directory: every doc's value through a range filter, aggregations and a
+    group-by, against the oracle over the same values."""
+    import os
+    from segdir_writer import write_segment_dir
+    fixture = open(os.path.join(os.path.dirname(__file__), "golden", "fixed_byte_svr_doubles.v1"), "rb").read()
+    n = 10009
+    cols = {"d": ("DOUBLE", np.arange(n, dtype=np.float64)), "k": ("INT", (np.arange(n) % 7).astype(np.int32))}
+    seg = build_segment("fb", cols, raw_columns=("d",))
+    seg.columns["d"].raw_file = fixture
+    g = engine.load(write_segment_dir(seg, str(tmp_path / "fb"), version="v3"))
+    ex = ServerQueryExecutor(engine)
+    for text in ("SELECT COUNT(*), SUM(d), MIN(d), MAX(d), AVG(d) FROM t",
+                 "SELECT COUNT(*), SUM(d), MAX(d) FROM t WHERE d BETWEEN 100.5 AND 5000",
+                 "SELECT COUNT(*), MIN(d) FROM t WHERE d > 9000 OR d < 3",
+                 "SELECT SUM(d), MAX(d) FROM t WHERE d >= 17 GROUP BY k"):
+        q = compile_pql(text)
+        got, st = ex.process_query(q, [g], trim=False)
+        exp, scanned = O.execute_server([seg], q)
+        assert st.num_docs_scanned == scanned, text
+        if isinstance(exp, dict):
+            assert {k: [_norm(v) for v in x] for k, x in got.items()} == \
+                   {k: [_norm(v) for v in x] for k, x in exp.items()}, text
+        else:
+            assert [_norm(v) for v in got] == [_norm(v) for v in exp], text
+    # every doc's value: d == i exactly (a per-doc equality filter over a sample of docs)
+    for i in (0, 1, 4095, 4096, 8191, 10008):
+        got, _ = ex.process_query(compile_pql("SELECT COUNT(*), SUM(d) FROM t WHERE d = %d" % i), [g])
+        assert got == [1, float(i)], i
+    g.release()
+
+
 def test_raw_fp_primitive_comparisons(engine):
     """Raw FLOAT / DOUBLE predicates compare primitives (RawValueBased evaluators): -0.0 == 0.0, NaN (literal or
     value) never compares true — unlike the transcoded dictionary's Double.compare order. Checked against the

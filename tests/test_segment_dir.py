@@ -13,7 +13,7 @@ import numpy as np
 import pytest
 
 import pinot_oracle as O
-from pinot_amd import PinotGpuError, build_segment, segment_dir_info
+from pinot_amd import PinotGpuError, build_segment, raw_forward_index_values, segment_dir_info
 from pinot_amd.executor import validate_segment
 from segment_dir import read_segment_dir
 from segdir_writer import write_segment_dir
@@ -239,3 +239,27 @@ def test_star_tree_files_read_on_the_host(tmp_path, version):
     meta = os.path.join(d, "v3" if version == "v3" else "", "star_tree_index_map")
     text = open(meta).read()
     assert "0.null.STAR_TREE.OFFSET = 0" in text and "0.count__*.FORWARD_INDEX.SIZE" in text
+
+
+def test_fixed_byte_fixture_pins_the_raw_reader(tmp_path):
+    """The reference's own fixed-width raw file (data/fixedByteSVRDoubles.v1,
+    FixedByteChunkSingleValueReaderWriteTest.testBackwardCompatibility :263-284: a version-1 FixedByteChunk file —
+    always Snappy — of 10,009 doubles, doc i = (double) i): the oracle's reader and the library's host reader
+    (pinot_segment_read_raw_forward_index = segment_reader.cpp read_raw_chunks + its Snappy decoder) return i for every doc,
+    and the segment loader reads it as a raw DOUBLE column's .sv.raw.fwd."""
+    from segment_dir import read_fixed_byte_values
+    fixture = open(os.path.join(HERE, "golden", "fixed_byte_svr_doubles.v1"), "rb").read()
+    assert len(fixture) == 44397 and struct.unpack_from(">i", fixture, 0)[0] == 1  # version 1: Snappy chunks
+    n = 10009
+    assert read_fixed_byte_values(fixture, n, "d") == [float(i) for i in range(n)]
+    got = raw_forward_index_values(fixture, "DOUBLE", n)
+    assert got.dtype == np.float64 and (got == np.arange(n, dtype=np.float64)).all()
+    seg = build_segment("fb", {"d": ("DOUBLE", np.arange(n, dtype=np.float64)),
+                               "i": ("INT", np.arange(n, dtype=np.int32))}, raw_columns=("d",))
+    seg.columns["d"].raw_file = fixture
+    assert segment_dir_info(write_segment_dir(seg, str(tmp_path / "fb"))) == (n, 2, 0)
+    # damaged copies are refused with a status: a truncated chunk, a wrong entry width
+    with pytest.raises(PinotGpuError):
+        raw_forward_index_values(fixture[:-200], "DOUBLE", n)
+    with pytest.raises(PinotGpuError):
+        raw_forward_index_values(fixture, "INT", n)

@@ -471,10 +471,21 @@ std::unique_ptr<GroupByResult> server_group_by(ServerImpl &s, const std::vector<
 // the multi-device partial step of one engine (executor.cpp): dense partials over [0, G) of the given key space
 // into counts / accs (allow_admission: per-segment num.groups.limit admission inside the partial, when the caller
 // has established that the inter-segment cap cannot bind)
+// The server's num.groups.limit inter-segment cap across ranks (CombineGroupByOperator.java:80,147 over every rank's
+// segments): mode 1 exports each local segment's first-appearance admitted keys ([segments][words] u32 bitmaps over
+// the global key space, DictionaryBasedGroupKeyGenerator's per-segment holder rule applied, no cap) and runs no
+// group-by; mode 2 imports the capped bitmaps and runs the partial with them.
+struct AdmissionIO {
+  int mode = 0;
+  int64_t words = 0;
+  std::vector<uint32_t> bitmaps;
+};
 void exec_group_by_partial_ks(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q,
                               const std::vector<int64_t> &gcard, const std::vector<std::vector<std::string>> &gvalues,
                               const std::vector<std::vector<std::vector<int32_t>>> &remap, int64_t *counts_dev,
-                              void *const *accs_dev, pinot_exec_stats *stats);
+                              void *const *accs_dev, pinot_exec_stats *stats, AdmissionIO *aio = nullptr);
+// CombineGroupByOperator's cap over [S][words] admitted bitmaps in segment order: keys enter until `cap` are in
+void inter_segment_cap(std::vector<uint32_t> &bm, size_t S, int64_t words, int64_t cap);
 // owner finalize of one key range [key_base, key_base + G) of merged dense arrays, device half: ordered compaction
 // of the non-empty keys (one sync for their count) and the group outputs on the device
 DenseOut slice_outputs(Engine &e, const pinot_query &q, const std::vector<int> &acc_kind, unsigned long long *counts,

@@ -2990,7 +2990,8 @@ const long long *device_trim(Engine &e, const DenseGroups &d, const long long *k
 std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q,
                                                    const KeySpace &ks_in, const GroupAccs &ga, pinot_exec_stats *stats,
                                                    int attempt = 0, const PartialOut *po = nullptr,
-                                                   const PartialOut *pin = nullptr, bool allow_admission = false) {
+                                                   const PartialOut *pin = nullptr, bool allow_admission = false,
+                                                   AdmissionIO *aio = nullptr) {
   const auto tg0 = std::chrono::steady_clock::now();
   const int na = q.num_aggregations;
   const size_t S = segs.size();
@@ -3020,7 +3021,11 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
   const GroupPlan gp = plan_group(segs, q, ks, gx, ks.hashed ? std::string("global") : e.group_mode, e.group_split,
                                     e.group_pshift);
   // num.groups.limit: per-segment first-appearance admission and the inter-segment cap (plan_admission)
-  const AdmissionPlan adm = pin ? AdmissionPlan{} : plan_admission(segs, q, e, ks.G);
+  AdmissionPlan adm = pin ? AdmissionPlan{} : plan_admission(segs, q, e, ks.G);
+  if (aio && !pin) {  // the server applies the inter-segment cap across ranks (AdmissionIO): every segment's keys
+    adm.active = true;
+    adm.cap_active = false;
+  }
   require(!(po && adm.active && (!allow_admission || adm.cap_active)), PINOT_ERR_UNSUPPORTED,
           "multi-GPU partials with num.groups.limit admission: use the engine's own multi-device group-by");
   const AdmissionBuffers ab = adm.active ? admission_buffers(e, S, ks.G) : AdmissionBuffers{};
@@ -3055,7 +3060,7 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
       ~Restore() { e.group_ring = v; }
     } restore{e, e.group_ring};
     e.group_ring = false;
-    return exec_group_by_fused(e, segs, q, ks_in, ga, stats, attempt, po, pin, allow_admission);
+    return exec_group_by_fused(e, segs, q, ks_in, ga, stats, attempt, po, pin, allow_admission, aio);
   };
   const auto tga = std::chrono::steady_clock::now();
   // remaps (dictId -> global id) travel in the arena
@@ -3242,7 +3247,14 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     PINOT_HIP(hipMemsetAsync(reps, 0xFF, (size_t)hcap * 8, e.stream));
     PINOT_HIP(hipMemsetAsync(a.verify_err, 0, 4, e.stream));
   }
-  if (adm.active) {  // first matching doc per (segment, key) -> admitted bitmaps (+ inter-segment cap)
+  if (adm.active && aio && aio->mode == 2) {  // the server's capped bitmaps for these segments
+    require(aio->words == ab.words && aio->bitmaps.size() == S * (size_t)ab.words, PINOT_ERR_DEVICE,
+            "admitted bitmaps of another shape");
+    e.host_arena.reserve(aio->bitmaps.size() * 4);
+    memcpy(e.host_arena.get(), aio->bitmaps.data(), aio->bitmaps.size() * 4);
+    PINOT_HIP(hipMemcpyAsync(ab.bitmaps, e.host_arena.get(), aio->bitmaps.size() * 4, hipMemcpyHostToDevice, e.stream));
+    wait_stream(e);  // host_arena stages the next query's arena
+  } else if (adm.active) {  // first matching doc per (segment, key) -> admitted bitmaps (+ inter-segment cap)
     PINOT_HIP(hipMemsetAsync(ab.first_doc, 0xFF, (size_t)S * ks.G * 4, e.stream));
     GroupArgs af = a;
     af.mode = GB_FIRST;
@@ -3250,6 +3262,13 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     launch_group_query(af, e.stream);
     PINOT_HIP(hipGetLastError());
     build_admitted(e, adm, S, ks.G, ab);
+    if (aio && aio->mode == 1) {  // export for the server's cap; no group-by here
+      aio->words = ab.words;
+      aio->bitmaps.assign(S * (size_t)ab.words, 0u);
+      PINOT_HIP(hipMemcpyAsync(aio->bitmaps.data(), ab.bitmaps, aio->bitmaps.size() * 4, hipMemcpyDeviceToHost, e.stream));
+      wait_stream(e);
+      return nullptr;
+    }
   }
   const auto tgu = std::chrono::steady_clock::now();
   uint32_t *ring_status = nullptr;  // ring plan: [0] status bits, [1] region records (k_group_ring)
@@ -3524,8 +3543,30 @@ std::unique_ptr<GroupByResult> exec_group_by_mv(Engine &e, const std::vector<Seg
   std::vector<SegPlan> plans = plan_all(e, segs, q2, ar, tree);
   KeySpace ks = build_key_space(segs, q2);
   const int64_t limit = q.num_groups_limit > 0 ? q.num_groups_limit : e.num_groups_limit;
-  require(!ks.hashed && ks.G <= limit, PINOT_ERR_UNSUPPORTED,
-          "multi-value group-by needs the group key space within num.groups.limit");
+  require(!ks.hashed, PINOT_ERR_UNSUPPORTED,
+          "multi-value group-by over a hashed key space (LONG_MAP / ARRAY_MAP holder shapes)");
+  // num.groups.limit (DictionaryBasedGroupKeyGenerator :79-126, IntMapBasedHolder.processMultiValue :282-300): a segment
+  // whose cardinality product exceeds max.init.group.holder.capacity admits the first min(product, limit) distinct keys
+  // in doc order, each doc's keys in getIntRawKeys order; then CombineGroupByOperator's 2 x limit cap in segment order
+  const size_t S = segs.size();
+  AdmissionPlan adm;
+  {
+    const int64_t threshold = q.max_init_group_holder_capacity > 0 ? q.max_init_group_holder_capacity : 10000;
+    int64_t possible = 0;
+    for (auto *sg : segs) {
+      __int128 product = 1;
+      for (int j = 0; j < q.num_group_by; j++) product *= sg->column(q.group_by[j])->card;
+      int64_t upper = INT64_MAX;
+      if (product > threshold) upper = product <= INT32_MAX ? std::min<int64_t>((int64_t)product, limit) : limit;
+      const int64_t reach = (int64_t)std::min<__int128>(product, (__int128)ks.G);  // a doc yields several keys
+      if (upper < reach) adm.active = true;
+      else upper = ks.G;
+      adm.upper.push_back(upper);
+      possible += std::min(upper, reach);
+    }
+    adm.cap = 2 * limit;
+    if (std::min(possible, ks.G) > adm.cap) adm.active = adm.cap_active = true;
+  }
   GroupAccs ga;
   for (int a = 0; a < nb; a++) {
     const int f = specs[a].function;
@@ -3568,15 +3609,10 @@ std::unique_ptr<GroupByResult> exec_group_by_mv(Engine &e, const std::vector<Seg
   PINOT_HIP(hipEventRecord(e.ev_start, e.stream));
   init_accs(e, ks.G, counts, ga, accs.data());
   Timer t(e);
-  const size_t S = plans.size();
   std::vector<DeviceBuffer> remaps(S * q.num_group_by);
   std::vector<int64_t> seg_counts(S, 0);
-  for (size_t si = 0; si < S; si++) {
-    SegPlan &pl = plans[si];
-    SegmentData &sg = *pl.seg;
-    if (pl.empty || sg.num_docs == 0) continue;
-    const uint64_t *bits = run_filter(e, pl, qs, t);
-    seg_counts[si] = count_docs(e, bits, sg);
+  auto mv_args = [&](size_t si, const uint64_t *bits) {
+    SegmentData &sg = *plans[si].seg;
     MvGroupArgs a{};
     a.n_gcols = q.num_group_by;
     a.n_aggs = nb;
@@ -3589,8 +3625,10 @@ std::unique_ptr<GroupByResult> exec_group_by_mv(Engine &e, const std::vector<Seg
       const auto &m = ks.remap[si][j];
       if (!m.empty()) {
         DeviceBuffer &rb = remaps[si * q.num_group_by + j];
-        rb.alloc(m.size() * 4 + 16);
-        PINOT_HIP(hipMemcpyAsync(rb.get(), m.data(), m.size() * 4, hipMemcpyHostToDevice, e.stream));
+        if (!rb.size()) {  // uploaded once per query (the admission pass and the accumulation pass share it)
+          rb.alloc(m.size() * 4 + 16);
+          PINOT_HIP(hipMemcpyAsync(rb.get(), m.data(), m.size() * 4, hipMemcpyHostToDevice, e.stream));
+        }
         a.remap[j] = rb.get<int32_t>();
       }
       a.stride[j] = stride;
@@ -3615,6 +3653,48 @@ std::unique_ptr<GroupByResult> exec_group_by_mv(Engine &e, const std::vector<Seg
     a.bitset = bits;
     a.nwords = sg.nwords();
     a.num_docs = sg.num_docs;
+    return a;
+  };
+  // admission: every segment's first-appearance bitmap (first positions, one radix sort each), then the cap
+  DeviceBuffer adm_buf;
+  int64_t words = 0;
+  if (adm.active) {
+    words = (ks.G + 31) / 32 + 1;
+    const size_t fp_b = ((size_t)ks.G * 8 + 255) / 256 * 256, bm_b = ((size_t)S * words * 4 + 255) / 256 * 256;
+    const size_t scr = admission_scratch_bytes_u64(ks.G);
+    adm_buf.alloc(fp_b + bm_b + scr);
+    auto *first_pos = adm_buf.get<unsigned long long>();
+    auto *bitmaps = reinterpret_cast<uint32_t *>(adm_buf.get<uint8_t>() + fp_b);
+    PINOT_HIP(hipMemsetAsync(bitmaps, 0, (size_t)S * words * 4, e.stream));
+    for (size_t si = 0; si < S; si++) {
+      SegPlan &pl = plans[si];
+      if (pl.empty || pl.seg->num_docs == 0) continue;
+      const MvGroupArgs a = mv_args(si, run_filter(e, pl, qs, t));
+      PINOT_HIP(hipMemsetAsync(first_pos, 0xFF, (size_t)ks.G * 8, e.stream));
+      launch_first_pos_mv(a, first_pos, e.stream);
+      launch_admission_bitmap_u64(first_pos, ks.G, adm.upper[si], bitmaps + si * words, words,
+                                  adm_buf.get<uint8_t>() + fp_b + bm_b, scr, e.stream);
+      PINOT_HIP(hipGetLastError());
+    }
+    if (adm.cap_active) {
+      std::vector<uint32_t> bm(S * words);
+      PINOT_HIP(hipMemcpyAsync(bm.data(), bitmaps, bm.size() * 4, hipMemcpyDeviceToHost, e.stream));
+      wait_stream(e);
+      apply_inter_segment_cap(bm, S, words, adm.cap);
+      PINOT_HIP(hipMemcpyAsync(bitmaps, bm.data(), bm.size() * 4, hipMemcpyHostToDevice, e.stream));
+      wait_stream(e);
+    }
+  }
+  for (size_t si = 0; si < S; si++) {
+    SegPlan &pl = plans[si];
+    SegmentData &sg = *pl.seg;
+    if (pl.empty || sg.num_docs == 0) continue;
+    const uint64_t *bits = run_filter(e, pl, qs, t);
+    seg_counts[si] = count_docs(e, bits, sg);
+    MvGroupArgs a = mv_args(si, bits);
+    if (adm.active)
+      a.admitted = reinterpret_cast<const uint32_t *>(adm_buf.get<uint8_t>() + ((size_t)ks.G * 8 + 255) / 256 * 256) +
+                   si * words;
     t.timed(1, [&] { launch_group_by_mv(a, e.stream); });
     PINOT_HIP(hipGetLastError());
   }
@@ -4221,7 +4301,7 @@ bool admission_cap_can_bind(const std::vector<SegmentData *> &segs, const pinot_
 void exec_group_by_partial_ks(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q,
                               const std::vector<int64_t> &gcard, const std::vector<std::vector<std::string>> &gvalues,
                               const std::vector<std::vector<std::vector<int32_t>>> &remap, int64_t *counts_dev,
-                              void *const *accs_dev, pinot_exec_stats *stats) {
+                              void *const *accs_dev, pinot_exec_stats *stats, AdmissionIO *aio) {
   require(e.use_fused, PINOT_ERR_UNSUPPORTED, "multi-GPU group-by runs on the fused path (exec.fused=1)");
   KeySpace ks;
   ks.gcard = gcard;
@@ -4230,8 +4310,13 @@ void exec_group_by_partial_ks(Engine &e, const std::vector<SegmentData *> &segs,
   ks.G = 1;
   for (auto g : gcard) ks.G *= g;
   GroupAccs ga = group_acc_kinds(*segs[0], q);
-  const PartialOut po{counts_dev, accs_dev};
-  exec_group_by_fused(e, segs, q, ks, ga, stats, 0, &po, nullptr, true);
+  std::vector<void *> no_accs(q.num_aggregations, nullptr);  // export: the partial arrays are never touched
+  const PartialOut po{counts_dev, accs_dev ? accs_dev : no_accs.data()};
+  exec_group_by_fused(e, segs, q, ks, ga, stats, 0, &po, nullptr, true, aio);
+}
+
+void inter_segment_cap(std::vector<uint32_t> &bm, size_t S, int64_t words, int64_t cap) {
+  apply_inter_segment_cap(bm, S, words, cap);
 }
 
 DenseOut slice_outputs(Engine &e, const pinot_query &q, const std::vector<int> &acc_kind, unsigned long long *counts,

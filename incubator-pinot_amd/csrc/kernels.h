@@ -531,8 +531,18 @@ struct MvGroupArgs {
   const uint64_t *bitset;       // null = all docs
   int64_t nwords;
   int32_t num_docs;
+  int32_t reserved;
+  const uint32_t *admitted;     // num.groups.limit: keys admitted for this segment (bitmap), null = all
 };
 void launch_group_by_mv(const MvGroupArgs &a, hipStream_t stream);
+// MV first appearance (DictionaryBasedGroupKeyGenerator IntMapBasedHolder.processMultiValue :282-300 over getIntRawKeys
+// :344-410): first_pos[key] = min over matching docs of (doc << 32 | position of the key in the doc's raw-key list),
+// the list ordered as getIntRawKeys builds it (the highest-index multi-value column fastest).
+void launch_first_pos_mv(const MvGroupArgs &a, unsigned long long *first_pos, hipStream_t stream);
+// admitted bit k = first_pos[k] among the `upper` smallest (every present key when upper >= G); one radix sort
+size_t admission_scratch_bytes_u64(long long G);
+void launch_admission_bitmap_u64(const unsigned long long *first_pos, long long G, long long upper, uint32_t *bitmap,
+                                 long long words, void *scratch, size_t scratch_bytes, hipStream_t stream);
 // First matching doc per key (atomicMin), for the num.groups.limit first-appearance rule.
 void launch_first_doc(const GroupByProgram &prog, const uint64_t *bitset, int64_t nwords, int32_t num_docs,
                       uint32_t *first_doc, hipStream_t stream);

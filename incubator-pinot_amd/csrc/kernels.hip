@@ -8,8 +8,10 @@
 // K7 HLL update       DistinctCountHLLAggregationFunction (register/rank precomputed per dictId on the host)
 // plus the device-side packers (synthetic bench columns, sorted-column forward index).
 #include "kernels.h"
+#include "common.h"
 
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 
@@ -410,6 +412,15 @@ __global__ __launch_bounds__(kBlock) void k_group_by_mv(MvGroupArgs a) {
         if (a.remap[j]) id = a.remap[j][id];
         key += (long long)id * a.stride[j];
       }
+      if (a.admitted && !((a.admitted[key >> 5] >> (key & 31)) & 1u)) {  // dropped: INVALID_ID (holder full)
+        int j = 0;
+        for (; j < a.n_gcols; j++) {
+          if (++cur[j] < hi[j]) break;
+          cur[j] = lo[j];
+        }
+        if (j == a.n_gcols) break;
+        continue;
+      }
       atomicAdd(a.counts + key, 1ull);
       for (int g = 0; g < a.n_aggs; g++)
         if (a.acc_kind[g] != 5) mv_fold(a, g, key, ab[g], ae[g]);
@@ -420,6 +431,58 @@ __global__ __launch_bounds__(kBlock) void k_group_by_mv(MvGroupArgs a) {
       }
       if (j == a.n_gcols) break;
     }
+  }
+}
+
+// Keys of a doc in getIntRawKeys order: the highest-index multi-value column fastest (its values outermost-first
+// build the array, each lower-index column's values then repeat the array: DictionaryBasedGroupKeyGenerator
+// .java:344-410); position = the key's index in that list. Keys repeat when a row repeats a value; the first one counts.
+__global__ __launch_bounds__(kBlock) void k_first_pos_mv(MvGroupArgs a, unsigned long long *first_pos) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t doc = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; doc < a.num_docs; doc += stride) {
+    if (a.bitset && !((a.bitset[doc >> 6] >> (doc & 63)) & 1ull)) continue;
+    uint32_t lo[kMaxGroupCols], hi[kMaxGroupCols], cur[kMaxGroupCols];
+    bool empty = false;
+    for (int j = 0; j < a.n_gcols; j++) {
+      lo[j] = a.goff[j] ? a.goff[j][doc] : (uint32_t)doc;
+      hi[j] = a.goff[j] ? a.goff[j][doc + 1] : (uint32_t)doc + 1;
+      cur[j] = lo[j];
+      empty = empty || hi[j] <= lo[j];
+    }
+    if (empty) continue;
+    unsigned long long pos = (unsigned long long)doc << 32;
+    while (true) {
+      long long key = 0;
+      for (int j = 0; j < a.n_gcols; j++) {
+        int32_t id = (int32_t)read_packed(a.gfwd[j], a.gbits[j], cur[j]);
+        if (a.remap[j]) id = a.remap[j][id];
+        key += (long long)id * a.stride[j];
+      }
+      if (first_pos[key] > pos) atomicMin(first_pos + key, pos);  // values only decrease: a stale read still takes it
+      pos++;
+      int j = a.n_gcols - 1;
+      for (; j >= 0; j--) {
+        if (++cur[j] < hi[j]) break;
+        cur[j] = lo[j];
+      }
+      if (j < 0) break;
+    }
+  }
+}
+
+__global__ void k_admit_bitmap_u64(const unsigned long long *__restrict__ first_pos, long long G,
+                                   const unsigned long long *__restrict__ sorted, long long upper,
+                                   uint32_t *__restrict__ bitmap, long long words) {
+  const unsigned long long t = (sorted && upper <= G) ? sorted[upper - 1] : ~0ull - 1ull;
+  for (long long w = (long long)blockIdx.x * blockDim.x + threadIdx.x; w < words; w += (long long)gridDim.x * blockDim.x) {
+    uint32_t m = 0;
+    for (int b = 0; b < 32; b++) {
+      const long long k = w * 32 + b;
+      if (k >= G) break;
+      const unsigned long long fp = first_pos[k];
+      m |= (fp != ~0ull && fp <= t) ? (1u << b) : 0u;
+    }
+    bitmap[w] = m;
   }
 }
 
@@ -538,6 +601,34 @@ void launch_group_by_mv(const MvGroupArgs &a, hipStream_t stream) {
   if (a.num_docs <= 0) return;
   const int64_t blocks = std::min<int64_t>(((int64_t)a.num_docs + kBlock - 1) / kBlock, 4096);
   hipLaunchKernelGGL(k_group_by_mv, dim3((unsigned)blocks), dim3(kBlock), 0, stream, a);
+}
+
+void launch_first_pos_mv(const MvGroupArgs &a, unsigned long long *first_pos, hipStream_t stream) {
+  if (a.num_docs <= 0) return;
+  const int64_t blocks = std::min<int64_t>(((int64_t)a.num_docs + kBlock - 1) / kBlock, 4096);
+  hipLaunchKernelGGL(k_first_pos_mv, dim3((unsigned)blocks), dim3(kBlock), 0, stream, a, first_pos);
+}
+
+size_t admission_scratch_bytes_u64(long long G) {
+  size_t need = 0;
+  PINOT_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, need, (const unsigned long long *)nullptr,
+                                              (unsigned long long *)nullptr, (int)G));
+  return ((size_t)G * 8 + 255) / 256 * 256 + need + 256;
+}
+
+void launch_admission_bitmap_u64(const unsigned long long *first_pos, long long G, long long upper, uint32_t *bitmap,
+                                 long long words, void *scratch, size_t scratch_bytes, hipStream_t stream) {
+  auto *sorted = static_cast<unsigned long long *>(scratch);
+  const size_t sorted_b = ((size_t)G * 8 + 255) / 256 * 256;
+  const bool limited = upper < G;
+  if (limited) {
+    size_t tb = scratch_bytes - sorted_b;
+    PINOT_HIP(hipcub::DeviceRadixSort::SortKeys(static_cast<uint8_t *>(scratch) + sorted_b, tb, first_pos, sorted,
+                                                (int)G, 0, 64, stream));
+  }
+  const int grid = (int)std::min<long long>((words + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_admit_bitmap_u64, dim3(grid), dim3(256), 0, stream, first_pos, G, limited ? sorted : nullptr,
+                     limited ? upper : G + 1, bitmap, words);
 }
 
 void launch_mv_aggregate(const MvAggArgs &a, hipStream_t stream) {

@@ -432,12 +432,63 @@ std::unique_ptr<GroupByResult> server_group_by(ServerImpl &s, const std::vector<
     const int64_t limit = q.num_groups_limit > 0 ? q.num_groups_limit : e.num_groups_limit;
     require(!ks.hashed, PINOT_ERR_UNSUPPORTED,
             "multi-GPU group-by needs a dense key space (LONG_MAP / ARRAY_MAP shapes: one GPU)");
-    require(gkinds.empty() || std::min(total_possible, ks.G) <= 2 * limit, PINOT_ERR_UNSUPPORTED,
-            "multi-GPU group-by where the 2 x num.groups.limit inter-segment cap can bind: one GPU");
     if (gkinds.empty() || ks.G == 0) {  // no rank holds a segment after pruning: no group
       res[i] = empty_group_result(q);
       tot[i].num_total_raw_docs = total_docs;
       return;
+    }
+    // A2: the 2 x num.groups.limit inter-segment cap (CombineGroupByOperator.java:80,147) when it can bind: every
+    // rank's segments' first-appearance admitted keys (each segment's holder rule applied on its own rank,
+    // DictionaryBasedGroupKeyGenerator.java:293-302) -> every rank; keys enter the merged map in rank order, then each
+    // rank's own segment order (the reference's thread-pool order is nondeterministic; this one is fixed), until
+    // 2 x limit keys are in; each rank then runs its partials with its segments' capped bitmaps
+    AdmissionIO admit;
+    if (std::min(total_possible, ks.G) > 2 * limit) {
+      AdmissionIO ex;
+      ex.mode = 1;
+      my = capture([&] {
+        std::lock_guard<std::mutex> el(e.mu);
+        DeadlineScope ds(e, q.timeout_ms);
+        if (!segs.empty()) exec_group_by_partial_ks(e, segs, q, ks.gcard, ks.gvalues, ks.remap, nullptr, nullptr, nullptr, &ex);
+      });
+      Writer wc;
+      put_status(wc, my);
+      wc.i64((int64_t)(segs.empty() ? 0 : segs.size()));
+      wc.i64(ex.words);
+      std::vector<uint8_t> raw(ex.bitmaps.size() * 4);
+      if (!raw.empty()) memcpy(raw.data(), ex.bitmaps.data(), raw.size());
+      wc.bytes(raw);
+      const auto all_c = c.all_gather_host(wc.b, e.stream);
+      sts.clear();
+      std::vector<int64_t> nseg(R, 0);
+      std::vector<std::vector<uint8_t>> rank_bm(R);
+      int64_t words = 0;
+      for (int r = 0; r < R; r++) {
+        Reader rd{all_c[r]};
+        sts.push_back(get_status(rd));
+        nseg[r] = rd.i64();
+        const int64_t w = rd.i64();
+        rank_bm[r] = rd.bytes();
+        if (nseg[r] > 0) words = std::max(words, w);
+      }
+      fail_together(sts, me, "group-by admission");
+      std::vector<uint32_t> bm;
+      int64_t S_all = 0, mine = 0;
+      for (int r = 0; r < R; r++) {
+        if (nseg[r] <= 0) continue;
+        require((int64_t)rank_bm[r].size() == nseg[r] * words * 4, PINOT_ERR_DEVICE, "admitted bitmaps of another shape");
+        if (r == me) mine = S_all;
+        const size_t at = bm.size();
+        bm.resize(at + (size_t)nseg[r] * words);
+        memcpy(bm.data() + at, rank_bm[r].data(), rank_bm[r].size());
+        S_all += nseg[r];
+      }
+      inter_segment_cap(bm, (size_t)S_all, words, 2 * limit);
+      if (!segs.empty()) {
+        admit.mode = 2;
+        admit.words = words;
+        admit.bitmaps.assign(bm.begin() + mine * words, bm.begin() + (mine + (int64_t)segs.size()) * words);
+      }
     }
     const int64_t G = ks.G, slice = (G + R - 1) / R, Gp = slice * R;
     // B: dense partials over [0, G), identities on the padding (everywhere without segments)
@@ -466,7 +517,7 @@ std::unique_ptr<GroupByResult> server_group_by(ServerImpl &s, const std::vector<
                                    gkinds[a] == 2 ? 0xFF : 0, (size_t)(Gp - from) * acc_unit(gkinds[a]), e.stream));
       if (!segs.empty())
         exec_group_by_partial_ks(e, segs, q, ks.gcard, ks.gvalues, ks.remap, reinterpret_cast<int64_t *>(counts),
-                                 accs.data(), &st);
+                                 accs.data(), &st, admit.mode ? &admit : nullptr);
       PINOT_HIP(hipStreamSynchronize(e.stream));
     });
     ph.mark(2);

@@ -547,7 +547,7 @@ def group_by_segment(segment, query, mask, num_groups_limit=100000, array_thresh
     gcols = [segment.column(c) for c in query["group_by"]["columns"]]
     if any(is_mv(c) for c in gcols) or any(sv(a["function"]) != a["function"].upper()
                                            for a in query["aggregations"]):
-        return _group_by_segment_mv(segment, query, mask, gcols, num_groups_limit)
+        return _group_by_segment_mv(segment, query, mask, gcols, num_groups_limit, array_threshold)
     docs = np.nonzero(mask)[0]
     cards = [_card(c) for c in gcols]
     raw = np.zeros(docs.shape[0], dtype=object if _prod(cards) > 2 ** 62 else np.int64)
@@ -611,14 +611,20 @@ def group_by_segment(segment, query, mask, num_groups_limit=100000, array_thresh
     return result
 
 
-def _group_by_segment_mv(segment, query, mask, gcols, num_groups_limit):
+def _group_by_segment_mv(segment, query, mask, gcols, num_groups_limit, array_threshold=10000):
     """Group-by with multi-value group columns or MV functions (`DictionaryBasedGroupKeyGenerator`'s MV branch,
     :213-240 / getGroupKeys: a doc's keys are the cartesian product of its group columns' entries, duplicates
     included; `aggregateGroupByMV`: each key of the doc takes COUNT + 1 and every entry of the function's column).
-    Only key spaces within num.groups.limit (no group is dropped, so first-appearance order does not matter)."""
+    A doc's keys come in getIntRawKeys order (:344-410: columns folded from the last to the first, each multi-value
+    column's entries outermost, so the highest-index multi-value column varies fastest); above the array threshold
+    the holder admits keys at first appearance up to min(product, limit) (IntMapBasedHolder.processMultiValue
+    :282-300 / getGroupId :293-302) and later keys are dropped (INVALID_ID)."""
     cards = [_card(c) for c in gcols]
-    if _prod(cards) > num_groups_limit:
-        raise NotImplementedError("multi-value group-by beyond num.groups.limit")
+    product = _prod(cards)
+    upper = None
+    if product > array_threshold:
+        upper = min(product, num_groups_limit) if product <= INT_MAX else num_groups_limit
+    admitted = set()
     docs = np.nonzero(mask)[0]
     rows = []
     for c in gcols:
@@ -642,8 +648,12 @@ def _group_by_segment_mv(segment, query, mask, gcols, num_groups_limit):
         for j in range(len(gcols) - 1, -1, -1):
             ids, st, ln = rows[j]
             vals = ids[st[di]:st[di] + ln[di]].tolist()
-            keys = [k * cards[j] + v for k in keys for v in vals]
+            keys = [k * cards[j] + v for v in vals for k in keys]
         for k in keys:
+            if upper is not None and k not in admitted:
+                if len(admitted) >= upper:
+                    continue  # INVALID_ID: the holder is full
+                admitted.add(k)
             slot = per_key.setdefault(k, [0, [[] for _ in fn_rows]])
             slot[0] += 1
             for i, fr in enumerate(fn_rows):
@@ -963,19 +973,20 @@ def top_groups(query, merged, fn_index, top_n=None):
 
 
 # ----------------------------------------------------------------------------- server + broker
-def execute_segment(segment, query, num_groups_limit=100000):
+def execute_segment(segment, query, num_groups_limit=100000, array_threshold=10000):
     """Per-segment plan (`InstancePlanMakerImplV2.makeInnerSegmentPlan`, :97-116): filter, then aggregate or group-by.
-    Returns (intermediate result, num_docs_scanned)."""
+    array_threshold: max.init.group.holder.capacity (the ARRAY holder's bound). Returns (intermediate result,
+    num_docs_scanned)."""
     mask = filter_mask(segment, query.get("filter"))
     scanned = int(mask.sum())
     if query.get("group_by"):
-        return group_by_segment(segment, query, mask, num_groups_limit), scanned
+        return group_by_segment(segment, query, mask, num_groups_limit, array_threshold), scanned
     return aggregate_segment(segment, query, mask), scanned
 
 
-def execute_server(segments, query, num_groups_limit=100000):
+def execute_server(segments, query, num_groups_limit=100000, array_threshold=10000):
     """Server-side combine over segments (`CombineOperator` / `CombineGroupByOperator`)."""
-    results = [execute_segment(s, query, num_groups_limit) for s in segments]
+    results = [execute_segment(s, query, num_groups_limit, array_threshold) for s in segments]
     scanned = sum(r[1] for r in results)
     fns = [sv(a["function"]) for a in query["aggregations"]]
     if query.get("group_by"):

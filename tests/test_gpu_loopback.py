@@ -173,6 +173,52 @@ def test_loopback_rank_form(K):
         s.close()
 
 
+def _wide_segments(rng, n, nseg):
+    """Segments of n docs over a ~1M-key space (g0, g1 ~1000 values each, g0 shifted per segment: dictionaries
+    differ): tens of thousands of distinct keys per segment, so the 2 x num.groups.limit inter-segment cap binds."""
+    segs = []
+    for i in range(nseg):
+        cols = {"g0": ("INT", (rng.integers(0, 990, n) + 3 * i).tolist()),
+                "g1": ("INT", rng.integers(0, 1000, n).tolist()),
+                "m": ("INT", rng.integers(-5000, 1000000, n).tolist()),
+                "d": ("DOUBLE", np.round(rng.normal(0, 100, n), 3).tolist()),
+                "h": ("INT", rng.integers(0, 5000, n).tolist()),
+                "f": ("INT", rng.integers(0, 10, n).tolist())}
+        segs.append(build_segment("wide%d" % i, cols))
+    return segs
+
+
+@pytest.mark.parametrize("K,limit", [(2, 100_000), (3, 100_000), (8, 100_000), (3, 20_000)])
+def test_loopback_num_groups_limit_across_ranks(K, limit):
+    """num.groups.limit across GPUs: each rank applies its segments' first-appearance holder rule
+    (DictionaryBasedGroupKeyGenerator.java:293-302; at limit 20,000 it binds inside every segment), then the 2 x limit
+    inter-segment cap (CombineGroupByOperator.java:80,147) over every rank's segments in rank order, then each rank's
+    own segment order: the admitted key set and every group's values equal the oracle's one-server combine over the
+    segments in that order (more than 200,000 possible keys)."""
+    rng = np.random.default_rng(400 + K + limit)
+    nseg = 7
+    host = _wide_segments(rng, 60_000, nseg)
+    srv = GpuServer([0] * K, "server.loopback=1")
+    gsegs = [srv.engines[i % K].register(s) for i, s in enumerate(host)]
+    ordered = [host[i] for r in range(K) for i in range(nseg) if i % K == r]  # rank order, then each rank's order
+    ex = ServerExecutor(srv, num_groups_limit=limit)
+    q = compile_pql("SELECT COUNT(*), SUM(m), MAX(d), DISTINCTCOUNTHLL(h) FROM t WHERE f < 9 GROUP BY g0, g1")
+    exp = O.execute_group_by_arrays(ordered, q, num_groups_limit=limit)
+    assert exp["keys"].shape[0] == 2 * limit  # the cap bound
+    res, st = ex.process_query(q, gsegs, as_result=True)
+    assert st.num_docs_scanned == exp["scanned"]
+    keys = res.raw_keys()
+    assert keys.shape == exp["keys"].shape and (keys == exp["keys"]).all()
+    c, v = res.function_values(1)
+    assert (c == exp["fns"][1]["count"]).all() and (v == exp["fns"][1]["sum"]).all()
+    _, v = res.function_values(2)
+    assert (v == exp["fns"][2]["max"]).all()
+    regs, cards = res.hll(3)
+    assert (cards == exp["fns"][3]["card"]).all() and (regs == exp["fns"][3]["hll"]).all()
+    del res
+    srv.close()
+
+
 def test_loopback_key_ranges_without_gather():
     """server.gather=0: every rank returns its own key range; the ranges are disjoint, ascend with the rank and
     together are the oracle's result."""

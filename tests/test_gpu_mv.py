@@ -109,6 +109,32 @@ def test_mv_group_by(engine, seed):
         g.release()
 
 
+@pytest.mark.parametrize("seed", range(3))
+def test_mv_group_by_admission(engine, seed):
+    """MV group-by beyond num.groups.limit: each segment's holder admits keys at first appearance (doc order, each
+    doc's keys in getIntRawKeys order) up to min(product, limit), then the 2 x limit inter-segment cap in segment order
+    (DictionaryBasedGroupKeyGenerator.java:282-302, CombineGroupByOperator.java:80,147); small limits and holder
+    thresholds (max.init.group.holder.capacity) make both rules bind on small segments."""
+    rng = np.random.default_rng(1500 + seed)
+    segs = [mv_segment(rng, int(rng.choice([600, 3000])), name="a%d" % i) for i in range(int(rng.integers(2, 4)))]
+    gsegs = [engine.register(s) for s in segs]
+    shapes = [["tags", "tags_s"], ["tags", "g"], ["tags_s", "tagl"], ["g", "tags"]]
+    for it, cols in enumerate(shapes):
+        limit, thr = [(40, 10), (120, 60), (25, 5), (300, 10)][it]
+        aggs = [{"function": "COUNT", "column": "*"}, {"function": "SUM", "column": "m"},
+                {"function": "MAXMV", "column": "tags"}, {"function": "AVGMV", "column": "tagl"}]
+        q = {"aggregations": aggs, "filter": _tree(rng, segs[0]) if it % 2 else None,
+             "group_by": {"columns": cols, "top_n": 10}}
+        ex = ServerQueryExecutor(engine, num_groups_limit=limit, max_init_group_holder_capacity=thr)
+        got, st = ex.process_query(q, gsegs, trim=False)
+        exp, scanned = O.execute_server(segs, q, num_groups_limit=limit, array_threshold=thr)
+        assert st.num_docs_scanned == scanned
+        assert len(exp) <= 2 * limit
+        _check(q, got, exp)
+    for g in gsegs:
+        g.release()
+
+
 def test_mv_segment_dir_and_datatable(engine, tmp_path):
     rng = np.random.default_rng(1200)
     seg = mv_segment(rng, 5000)

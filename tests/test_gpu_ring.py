@@ -71,15 +71,28 @@ def test_ring_config4_shape():
     e.close()
 
 
+_POOL = np.random.default_rng(77)
+LV_POOL = _POOL.integers(-(1 << 40), 1 << 40, 3000) * 7
+DV_POOL = (_POOL.standard_normal(2000) * 1e6).round(3)
+H_POOL = np.arange(0, 50000, 7)
+
+
+def _from_pool(rng, pool, n):
+    """n values from pool, every pool value present (the partitioned plans carry dictIds: the aggregated columns'
+    dictionaries must be identical on every segment)."""
+    v = np.concatenate([pool, rng.choice(pool, n - pool.shape[0])])
+    return v[rng.permutation(n)]
+
+
 def _mixed_segment(name, n, seed, k1_vals, k2_vals, sorted_ts=False):
     rng = np.random.default_rng(seed)
     cols = {
         "k1": ("INT", rng.choice(k1_vals, n).tolist()),
         "k2": ("STRING", ["s%04d" % v for v in rng.choice(k2_vals, n)]),
         "f": ("INT", rng.integers(0, 100, n).tolist()),
-        "lv": ("LONG", (rng.integers(-(1 << 40), 1 << 40, n) * 7).tolist()),
-        "dv": ("DOUBLE", (rng.standard_normal(n) * 1e6).round(3).tolist()),
-        "h": ("INT", rng.integers(0, 50000, n).tolist()),
+        "lv": ("LONG", _from_pool(rng, LV_POOL, n).tolist()),
+        "dv": ("DOUBLE", _from_pool(rng, DV_POOL, n).tolist()),
+        "h": ("INT", _from_pool(rng, H_POOL, n).tolist()),
     }
     if sorted_ts:
         cols["ts"] = ("INT", (np.arange(n) // 997).tolist())

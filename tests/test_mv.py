@@ -117,6 +117,28 @@ def test_mv_group_by_cartesian_with_duplicates():
     assert len(r) == 6
 
 
+def test_mv_group_by_first_appearance_admission():
+    """IntMapBasedHolder.processMultiValue (DictionaryBasedGroupKeyGenerator.java:282-300): above the array threshold
+    a doc's keys take group ids in getIntRawKeys order (:344-410: the highest-index multi-value column fastest) until
+    the holder holds min(product, limit) keys; later keys are dropped for every doc (INVALID_ID)."""
+    seg = build_segment("adm", {
+        "a": ("INT", [[2, 1], [3], [1, 3], [1, 2]]),
+        "b": ("INT", [[7, 8], [8], [7], [9, 7]]),
+        "x": ("INT", np.array([10, 20, 30, 40], dtype=np.int32)),
+    }, mv_columns=("a", "b"), allow_sorted=False)
+    q = {"aggregations": [{"function": "COUNT", "column": "*"}, {"function": "SUM", "column": "x"}],
+         "filter": None, "group_by": {"columns": ["a", "b"], "top_n": 10}}
+    mask = np.ones(4, dtype=bool)
+    # doc 0 keys in order: (2,7) (2,8) (1,7) (1,8) — column b (index 1) fastest; the holder admits 5 keys:
+    # doc 0's four, then doc 1's (3,8); doc 2's (1,7) exists, (3,7) is dropped; doc 3's (1,9) dropped, (1,7) exists,
+    # (2,9) dropped, (2,7) exists
+    r = O.group_by_segment(seg, q, mask, num_groups_limit=5, array_threshold=2)
+    assert r == {"2\t7": [2, 50.0], "2\t8": [1, 10.0], "1\t7": [3, 80.0], "1\t8": [1, 10.0], "3\t8": [1, 20.0]}
+    # without a binding limit every key of the cartesian products counts
+    full = O.group_by_segment(seg, q, mask, num_groups_limit=100, array_threshold=2)
+    assert len(full) == 8 and full["3\t7"] == [1, 30.0] and full["1\t9"] == [1, 40.0]
+
+
 # ------------------------------------------------------------------ segment directories + host validation
 @pytest.mark.parametrize("version", ["v1", "v3"])
 def test_segment_dir_round_trip(tmp_path, version):

@@ -262,6 +262,7 @@ struct Engine {
   bool group_ring = true;     // group.ring: large dense key spaces take the ring plan (no histogram pass; group_ring.hip)
   int32_t trim_top_n = 0;      // per call (pinot_gpu_group_by_top): trim the group-by on the device for this TOP n
   int64_t ring_queries = 0;    // group-bys launched on the ring plan
+  int64_t last_pre_segments = 0;  // segments of the last fused query whose filter needed a `pre` bitset (launch sequence)
   int64_t ring_fallbacks = 0;  // ring-plan queries re-answered on the counted plan (a region overflowed: skewed keys)
   int num_cus = 256;          // multiProcessorCount of the device
 

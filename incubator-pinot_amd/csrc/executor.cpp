@@ -60,7 +60,7 @@ struct Arena {
 
 // One device step of a segment's filter plan.
 struct FilterStep {
-  enum Kind { SCAN, RANGES, ROARING, COMBINE, FILL, MV_SCAN } kind;
+  enum Kind { SCAN, RANGES, ROARING, COMBINE, FILL, MV_SCAN, FUSED_OP } kind;  // FUSED_OP: a nested term's close
   int col = -1;
   int leaf_kind = LEAF_RANGE;
   uint32_t lo = 0, span = 0;
@@ -73,7 +73,7 @@ struct FilterStep {
   int join = JOIN_NEW;  // fused leaves: how the leaf joins the filter program (FusedJoin)
 };
 
-constexpr int kMaxFusedRoaringIds = 64;  // bitmap leaves with more dictIds are expanded to a `pre` bitset
+constexpr int kMaxFusedRoaringIds = 256;  // bitmap leaves with more dictIds are expanded to a `pre` bitset
 
 struct SegPlan {
   SegmentData *seg = nullptr;
@@ -159,24 +159,48 @@ class Compiler {
     if (st.kind == FilterStep::RANGES) return true;
     return st.kind == FilterStep::ROARING && st.n <= kMaxFusedRoaringIds;
   }
-  // An AND / OR whose children are all fusable leaves -> one term of the fused program.
-  bool fuse_term(const FilterNode &n) {
-    for (const auto &c : n.children)
-      if (c.type == FilterNode::AND || c.type == FilterNode::OR || c.type == FilterNode::EMPTY ||
-          c.type == FilterNode::MATCH_ALL)
-        return false;
-    const int64_t scans_before = sp_.scan_leaves;
-    std::vector<FilterStep> leaves;
-    for (const auto &c : n.children) {
-      FilterStep st = leaf_step(c);
-      if (!fusable(st)) {
-        sp_.scan_leaves = scans_before;  // eval() plans these leaves again
-        return false;
-      }
-      st.join = leaves.empty() ? JOIN_NEW : (n.type == FilterNode::OR ? JOIN_OR : JOIN_AND);
-      leaves.push_back(st);
+  // An AND / OR tree of fusable leaves -> one term of the fused program, in postfix over the kernel's register stack
+  // (JOIN_PUSH / FUSED_OP: a child whose operator differs from its parent's is built above the parent's running
+  // term, then combined). Trees deeper than the stack, or with an unfusable leaf, take the `pre` bitset instead.
+  enum GenMode { GEN_START, GEN_PUSH, GEN_COMBINE };
+  bool gen_term(const FilterNode &n, GenMode mode, int op, std::vector<FilterStep> &out, int &depth, int &max_depth) {
+    if (n.type == FilterNode::EMPTY || n.type == FilterNode::MATCH_ALL) return false;
+    if (n.type != FilterNode::AND && n.type != FilterNode::OR) {
+      FilterStep st = leaf_step(n);
+      if (!fusable(st)) return false;
+      st.join = mode == GEN_START ? JOIN_NEW : mode == GEN_PUSH ? JOIN_PUSH : op;
+      if (mode == GEN_PUSH) max_depth = std::max(max_depth, ++depth);
+      out.push_back(st);
+      return true;
     }
-    for (auto &st : leaves) sp_.fused_leaves.push_back(st);
+    if (n.children.empty()) return false;
+    const int nop = n.type == FilterNode::OR ? JOIN_OR : JOIN_AND;
+    if (mode == GEN_COMBINE && nop == op) {  // the parent's operator: its children join the running term directly
+      for (const auto &c : n.children)
+        if (!gen_term(c, GEN_COMBINE, op, out, depth, max_depth)) return false;
+      return true;
+    }
+    const bool nested = mode == GEN_COMBINE;
+    if (!gen_term(n.children[0], nested ? GEN_PUSH : mode, -1, out, depth, max_depth)) return false;
+    for (size_t i = 1; i < n.children.size(); i++)
+      if (!gen_term(n.children[i], GEN_COMBINE, nop, out, depth, max_depth)) return false;
+    if (nested) {  // close: term = (the parent's running term) op term
+      FilterStep cl{FilterStep::FUSED_OP};
+      cl.join = op;
+      out.push_back(cl);
+      depth--;
+    }
+    return true;
+  }
+  bool fuse_term(const FilterNode &n) {
+    const int64_t scans_before = sp_.scan_leaves;
+    std::vector<FilterStep> steps;
+    int depth = 0, max_depth = 0;
+    if (!gen_term(n, GEN_START, -1, steps, depth, max_depth) || max_depth > kMaxFusedStack) {
+      sp_.scan_leaves = scans_before;  // eval() plans these leaves again
+      return false;
+    }
+    for (auto &st : steps) sp_.fused_leaves.push_back(st);
     return true;
   }
   int alloc_slot() {
@@ -635,10 +659,14 @@ std::pair<int64_t, int64_t> chunk_window(const SegPlan &p, const Arena &ar) {
 
 // A fused leaf (FilterStep) as the device step k_scan_query / k_group_query evaluate.
 FusedStep fused_leaf_step(const SegmentData &s, const FilterStep &l, const uint8_t *arena) {
-  const ColumnData &c = *s.cols[l.col];
   FusedStep st{};
   st.join = l.join;
   st.negate = l.negate;
+  if (l.kind == FilterStep::FUSED_OP) {  // no column: the close of a nested term
+    st.kind = FK_OP;
+    return st;
+  }
+  const ColumnData &c = *s.cols[l.col];
   switch (l.kind) {
     case FilterStep::RANGES:
       st.kind = FK_LEAF_RANGES;
@@ -836,6 +864,8 @@ void plan_fused(Engine &e, const std::vector<SegmentData *> &segs, const pinot_q
     plans[si].seg = segs[si];
     Compiler(e, plans[si], ar).run_fused(tree.get());
   }
+  e.last_pre_segments = 0;
+  for (auto &p : plans) e.last_pre_segments += p.has_pre && !p.empty;
   const int nfolds = (int)fold_cols.size();
   const int nslots = 1 + 2 * nfolds;
   // steps: per segment its leaves then its folds
@@ -3037,6 +3067,8 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     plans[si].seg = segs[si];
     Compiler(e, plans[si], ar).run_fused(tree.get(), kGroupMaxFusedLeafBits);
   }
+  e.last_pre_segments = 0;
+  for (auto &p : plans) e.last_pre_segments += p.has_pre && !p.empty;
   // chunk windows (a single sorted leaf bounds the chunks a segment's program visits), concatenated: the ring plan's
   // blocks split the global chunk list evenly
   std::vector<std::pair<int64_t, int64_t>> windows(S);

@@ -200,20 +200,23 @@ __device__ __forceinline__ uint64_t roaring_word(const FusedStep &st, int64_t w)
   const RoaringContainer *conts = static_cast<const RoaringContainer *>(st.aux0);
   const int32_t *dir = static_cast<const int32_t *>(st.aux1);
   const int32_t *ids = static_cast<const int32_t *>(st.table);
-  const uint32_t key = (uint32_t)(w >> 10);            // 1024 words per roaring key
+  // a chunk's 64 words lie in one 1024-word roaring key: the key, each id's container search and the container header
+  // are wave-uniform (scalar loads); only the word inside the container is per lane
+  const uint32_t key = (uint32_t)__builtin_amdgcn_readfirstlane((int)(w >> 10));
   const uint32_t first = (uint32_t)(w & 1023) * 64;    // the word's first low-16 doc
   uint64_t x = 0;
   for (int i = 0; i < (int)st.lo; i++) {
-    const int id = ids[i];
-    int l = dir[id], r = dir[id + 1];
+    const int id = load_const(ids + i);
+    int l = load_const(dir + id), r = load_const(dir + id + 1);
     const int end = r;
     while (l < r) {
       const int m = (l + r) >> 1;
-      if (conts[m].key < key) l = m + 1;
+      if (load_const(conts + m).key < key) l = m + 1;
       else r = m;
     }
-    if (l >= end || conts[l].key != key) continue;
-    const RoaringContainer c = conts[l];
+    if (l >= end) continue;
+    const RoaringContainer c = load_const(conts + l);
+    if (c.key != key) continue;
     const uint8_t *p = payload + c.payload_offset;
     if (c.type == 1) {  // bitmap container: 1024 LE u64 words
       const uint8_t *q = p + (first >> 3);
@@ -253,14 +256,22 @@ __device__ __forceinline__ uint64_t leaf_word(const FusedStep &st, int i, int64_
   return x;
 }
 
-// The filter program of a chunk: terms AND-ed into `mask` (early exit once the wave's mask is empty).
+// The filter program of a chunk: terms AND-ed into `mask` (early exit once the wave's mask is empty). A term is an
+// AND / OR tree in postfix over a register stack (s0..s2 below the running term): nested subtrees of the filter
+// (FilterOperatorUtils.java:74-122 builds them with AndFilterOperator / OrFilterOperator) stay in registers.
 template <bool G, int MAXB = 32, typename Src>
 __device__ __forceinline__ uint64_t eval_filter(const FusedStep *__restrict__ steps, int n_leaves, uint64_t mask,
                                                 int64_t w, int64_t nwords, int32_t num_docs, int lane, Src &&src) {
-  uint64_t term = ~0ull;
+  uint64_t term = ~0ull, s0 = 0, s1 = 0, s2 = 0;
   bool pending = false;
   for (int i = 0; i < n_leaves; i++) {
     const FusedStep st = load_const(steps + i);
+    if (st.kind == FK_OP) {  // uniform: the nested term closes into the entry below it
+      term = st.join == JOIN_OR ? (s0 | term) : (s0 & term);
+      s0 = s1;
+      s1 = s2;
+      continue;
+    }
     if (st.join == JOIN_NEW) {
       if (pending) mask &= term;
       pending = false;
@@ -270,7 +281,13 @@ __device__ __forceinline__ uint64_t eval_filter(const FusedStep *__restrict__ st
     x = w < nwords ? x & tail_mask(w, nwords, num_docs) : 0ull;
     if (st.join == JOIN_NEW) term = x;
     else if (st.join == JOIN_OR) term |= x;
-    else term &= x;
+    else if (st.join == JOIN_AND) term &= x;
+    else {  // JOIN_PUSH
+      s2 = s1;
+      s1 = s0;
+      s0 = term;
+      term = x;
+    }
     pending = true;
   }
   return pending ? (mask & term) : mask;

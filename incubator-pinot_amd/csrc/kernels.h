@@ -146,13 +146,16 @@ int scan_grid(int64_t nwords);
 enum FusedKind : int32_t {
   FK_LEAF_RANGE = 0, FK_LEAF_LUT64 = 1, FK_LEAF_LUT = 2, FK_FOLD = 3,
   FK_LEAF_RANGES = 4,   // sorted-index leaf: inclusive [start, end] doc ranges (table, n = lo)
-  FK_LEAF_ROARING = 5   // bitmap-index leaf: OR of the dictIds' roaring bitmaps (fwd = payload, aux0 = containers,
+  FK_LEAF_ROARING = 5,  // bitmap-index leaf: OR of the dictIds' roaring bitmaps (fwd = payload, aux0 = containers,
                         // aux1 = per-dictId container directory, table = dictIds, n = lo), negate = exclusive
+  FK_OP = 6             // nested AND / OR: term = (popped entry) op term, op in `join` (JOIN_AND / JOIN_OR)
 };
-// How a leaf joins the filter program (the top-level conjunction of terms, a term = one leaf or an
-// AND / OR of leaves): JOIN_NEW starts a term (the previous one is AND-ed into the mask), JOIN_OR /
-// JOIN_AND combine the leaf into the current term.
-enum FusedJoin : int32_t { JOIN_NEW = 0, JOIN_OR = 1, JOIN_AND = 2 };
+// How a leaf joins the filter program (the top-level conjunction of terms, a term = an AND / OR tree of leaves in
+// postfix): JOIN_NEW starts a term (the previous one is AND-ed into the mask), JOIN_OR / JOIN_AND combine the leaf
+// into the running term, JOIN_PUSH pushes the running term onto a register stack and starts a nested one (an FK_OP
+// step pops it and combines). kMaxFusedStack entries below the running term.
+enum FusedJoin : int32_t { JOIN_NEW = 0, JOIN_OR = 1, JOIN_AND = 2, JOIN_PUSH = 3 };
+constexpr int kMaxFusedStack = 3;
 enum FoldOps : int32_t { FOLD_IDSUM = 1, FOLD_MINMAX = 2, FOLD_DICT32 = 4, FOLD_HLL = 8 };
 constexpr int kMaxFusedFolds = 6;                      // distinct aggregated columns per query
 constexpr int kMaxFusedSlots = 1 + 2 * kMaxFusedFolds; // slot 0 count; fold f: 1 + 2f sum, 2 + 2f min/max

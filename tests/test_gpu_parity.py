@@ -242,6 +242,83 @@ def test_random_filter_bitsets(engine, seed):
     g.release()
 
 
+def _small_leaf(rng, seg):
+    """A leaf the fused kernel evaluates in registers: EQ / NOT / IN / NOT_IN of a few literals (scan, sorted or
+    bitmap leaf by the planner's cost model) or a RANGE."""
+    while True:
+        leaf = _random_leaf(rng, seg)
+        if leaf["operator"] != "RANGE" or leaf["column"] not in ("s",) and not leaf["column"].startswith("i"):
+            return leaf
+
+
+def _deep_tree(rng, seg, depth=0, max_depth=4):
+    """AND / OR levels alternating down to max_depth (every level nests: FilterOperatorUtils builds one operator per
+    level, FilterOperatorUtils.java:74-122)."""
+    if depth >= max_depth or (depth >= 2 and rng.random() < 0.3):
+        return _small_leaf(rng, seg)
+    op = ("AND", "OR")[(depth + int(rng.integers(0, 2)) * (depth == 0)) % 2]
+    k = int(rng.integers(2, 4))
+    return {"operator": op, "children": [_deep_tree(rng, seg, depth + 1, max_depth) for _ in range(k)]}
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_deep_filter_trees_in_registers(seed):
+    """Filter trees nested four levels deep (alternating AND / OR) run inside the fused kernel's register program
+    (postfix terms over its register stack): no segment's filter goes through the dense-bitset launch sequence
+    (exec.last_pre_segments == 0), and the aggregations equal the oracle's."""
+    rng = np.random.default_rng(2100 + seed)
+    n = int(rng.choice([1000, 70001]))
+    segs = [_random_segment(rng, n, name="d%d" % i) for i in range(2)]
+    e = GpuEngine(0)
+    gsegs = [e.register(s) for s in segs]
+    ex = ServerQueryExecutor(e)
+    for _ in range(10):
+        tree = _deep_tree(rng, segs[0])
+        q = {"aggregations": [{"function": "COUNT", "column": "*"}, {"function": "SUM", "column": "big"},
+                              {"function": "MAX", "column": "lng"}], "filter": tree, "group_by": None}
+        got, st = ex.process_query(q, gsegs)
+        exp, scanned = O.execute_server(segs, q)
+        assert st.num_docs_scanned == scanned, tree
+        for a, gv, ev in zip(q["aggregations"], got, exp):
+            _assert_same(a["function"], gv, ev, True)
+        assert e.stat("exec.last_pre_segments") == 0, tree
+        # the same tree through the filter API (the dense-bitset launch path) agrees doc for doc
+        bits, cnt = e.filter(gsegs[0], tree)
+        m = O.filter_mask(segs[0], tree)
+        assert cnt == int(m.sum())
+    e.close()
+
+
+def test_wide_bitmap_leaf_in_registers():
+    """A bitmap-indexed leaf over 200 dictIds (a config-3 variant: b4 IN (200 values)) is evaluated from the roaring
+    containers inside the fused kernel, one launch with no `pre` bitset, equal to the oracle and to the forced-scan
+    plan."""
+    rng = np.random.default_rng(2200)
+    n = 300_000
+    cols = {"s0": ("INT", np.sort(rng.integers(0, 400, n)).tolist()),
+            "b4": ("INT", rng.integers(0, 1000, n).tolist()),
+            "b1": ("INT", rng.integers(0, 50, n).tolist()),
+            "m": ("INT", rng.integers(-1000, 100000, n).tolist())}
+    seg = build_segment("cfg3", cols, inverted_columns=("b4", "b1"))
+    e = GpuEngine(0, "filter.force=index")
+    g = e.register(seg)
+    ex = ServerQueryExecutor(e)
+    vals = "\t\t".join(str(v) for v in sorted(rng.choice(1000, 200, replace=False)))
+    for tree in ({"operator": "IN", "column": "b4", "values": [vals]},
+                 {"operator": "AND", "children": [
+                     {"operator": "RANGE", "column": "s0", "values": ["[10\t\t300)"]},
+                     {"operator": "OR", "children": [{"operator": "IN", "column": "b4", "values": [vals]},
+                                                     {"operator": "EQUALITY", "column": "b1", "values": ["3"]}]}]},
+                 {"operator": "NOT_IN", "column": "b4", "values": [vals]}):
+        q = {"aggregations": [{"function": "COUNT", "column": "*"}, {"function": "SUM", "column": "m"},
+                              {"function": "MAX", "column": "m"}], "filter": tree, "group_by": None}
+        got, st = ex.process_query(q, [g])
+        exp, scanned = O.execute_server([seg], q)
+        assert st.num_docs_scanned == scanned and got == exp, tree
+        assert e.stat("exec.last_pre_segments") == 0, tree
+    e.close()
+
+
 @pytest.mark.parametrize("seed", range(6))
 def test_random_aggregations(engine, seed):
     rng = np.random.default_rng(200 + seed)

@@ -516,6 +516,8 @@ const uint64_t *run_filter(Engine &e, SegPlan &p, const QueryScratch &qs, Timer 
       case FilterStep::FILL:
         launch_bitset_combine(dst, nullptr, nwords, s.num_docs, st.mode, st.negate, e.stream);
         break;
+      case FilterStep::FUSED_OP:  // only in fused programs, never in a launch sequence
+        throw Error(PINOT_ERR_DEVICE, "fused program step in a filter launch sequence");
     }
     PINOT_HIP(hipGetLastError());
   }

@@ -9,6 +9,11 @@
 namespace pinot {
 
 Engine::~Engine() {
+  // drain every queue first: result copies (copy streams, async D2H of pooled results) still in flight at teardown
+  // would complete after their buffers and streams are gone
+  if (stream) (void)hipStreamSynchronize(stream);
+  for (auto cs : copy_streams) (void)hipStreamSynchronize(cs);
+  (void)hipDeviceSynchronize();
   segments.clear();
   for (auto ev : kev) (void)hipEventDestroy(ev);
   if (ev_start) (void)hipEventDestroy(ev_start);

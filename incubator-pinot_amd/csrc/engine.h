@@ -487,6 +487,21 @@ void exec_group_by_partial_ks(Engine &e, const std::vector<SegmentData *> &segs,
                               void *const *accs_dev, pinot_exec_stats *stats, AdmissionIO *aio = nullptr);
 // CombineGroupByOperator's cap over [S][words] admitted bitmaps in segment order: keys enter until `cap` are in
 void inter_segment_cap(std::vector<uint32_t> &bm, size_t S, int64_t words, int64_t cap);
+// Multi-value group-by (MV group columns or *MV functions): the extended function list (a hidden CountMV after the
+// functions for every AvgMV, whose entry count it carries), and the fold of those counts into the final result.
+std::vector<pinot_agg_spec> mv_extended_specs(const pinot_query &q, std::vector<int> &hidden);
+void fold_mv_counts(GroupByResult &res, const pinot_query &q, const std::vector<int> &hidden);
+bool touches_mv_group_by(const std::vector<SegmentData *> &segs, const pinot_query &q);
+struct MvPartial {  // the server's MV partial step: global key space, its dense arrays (extended function list)
+  const std::vector<int64_t> *gcard;
+  const std::vector<std::vector<std::string>> *gvalues;
+  const std::vector<std::vector<std::vector<int32_t>>> *remap;
+  int64_t *counts;
+  void *const *accs;
+  AdmissionIO *aio;
+};
+void exec_group_by_mv_partial(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q,
+                              const MvPartial &mp, pinot_exec_stats *stats);
 // owner finalize of one key range [key_base, key_base + G) of merged dense arrays, device half: ordered compaction
 // of the non-empty keys (one sync for their count) and the group outputs on the device
 DenseOut slice_outputs(Engine &e, const pinot_query &q, const std::vector<int> &acc_kind, unsigned long long *counts,

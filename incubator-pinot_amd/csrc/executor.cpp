@@ -1820,18 +1820,21 @@ struct GroupAccs {
 GroupAccs group_acc_kinds(const SegmentData &s, const pinot_query &q) {
   GroupAccs g;
   for (int a = 0; a < q.num_aggregations; a++) {
-    const int f = q.aggregations[a].function;
+    const int f = q.aggregations[a].function, sf = sv_function(f);
     int kind = 5;
     size_t bytes = 0;
-    if (f != PINOT_AGG_COUNT) {
+    if (f == PINOT_AGG_COUNTMV) {  // entries per group (an int64 sum)
+      kind = 6;
+      bytes = 8;
+    } else if (f != PINOT_AGG_COUNT) {
       const ColumnData &c = *s.column(agg_column(q.aggregations[a]));
-      if (f == PINOT_AGG_DISTINCTCOUNTHLL) {
+      if (sf == PINOT_AGG_DISTINCTCOUNTHLL) {
         kind = 4;
         bytes = 1024;
       } else {
         require(c.numeric(), PINOT_ERR_UNSUPPORTED, "numeric aggregation over STRING column " + c.name);
-        if (f == PINOT_AGG_MIN) kind = 2;
-        else if (f == PINOT_AGG_MAX) kind = 3;
+        if (sf == PINOT_AGG_MIN) kind = 2;
+        else if (sf == PINOT_AGG_MAX) kind = 3;
         else kind = c.data_type == PINOT_INT ? 0 : 1;
         bytes = 8;
       }
@@ -3538,8 +3541,6 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
   return res;
 }
 
-namespace {
-
 bool touches_mv_group_by(const std::vector<SegmentData *> &segs, const pinot_query &q) {
   bool mv = touches_mv_aggregation(segs, q);
   for (int j = 0; j < q.num_group_by; j++)
@@ -3550,16 +3551,11 @@ bool touches_mv_group_by(const std::vector<SegmentData *> &segs, const pinot_que
   return mv;
 }
 
-// Group-by with multi-value group columns or MV functions: per segment the filter's bitset and one k_group_by_mv
-// (every doc's cartesian product of group keys, DictionaryBasedGroupKeyGenerator's MV branch) into dense
-// accumulators over the global key space, then the bitset path's finalisation. AvgMV needs its entry count beside
-// its sum: a hidden CountMV accumulator per AvgMV, folded into the function's counts after finalisation. Exact only
-// while no group is dropped: the key space must fit num.groups.limit (no first-appearance admission).
-std::unique_ptr<GroupByResult> exec_group_by_mv(Engine &e, const std::vector<SegmentData *> &segs,
-                                                const pinot_query &q, pinot_exec_stats *stats) {
+
+std::vector<pinot_agg_spec> mv_extended_specs(const pinot_query &q, std::vector<int> &hidden) {
   const int na = q.num_aggregations;
   std::vector<pinot_agg_spec> specs(q.aggregations, q.aggregations + na);
-  std::vector<int> hidden(na, -1);
+  hidden.assign(na, -1);
   for (int a = 0; a < na; a++)
     if (q.aggregations[a].function == PINOT_AGG_AVGMV) {
       require((int)specs.size() < kMaxAggs, PINOT_ERR_UNSUPPORTED, "too many aggregations with AVGMV (8 at most)");
@@ -3568,6 +3564,46 @@ std::unique_ptr<GroupByResult> exec_group_by_mv(Engine &e, const std::vector<Seg
       hidden[a] = (int)specs.size();
       specs.push_back(h);
     }
+  return specs;
+}
+
+void fold_mv_counts(GroupByResult &res, const pinot_query &q, const std::vector<int> &hidden) {
+  const int na = q.num_aggregations;
+  if (res.counts_shared) {  // one count vector for every function: split it before the MV functions take theirs
+    res.counts.resize(res.functions.size());
+    for (size_t a = 1; a < res.counts.size(); a++) res.counts[a] = res.counts[0];
+    res.counts_shared = false;
+  }
+  for (int a = 0; a < na; a++) {
+    const int f = q.aggregations[a].function;
+    const int src = f == PINOT_AGG_COUNTMV ? a : hidden[a];
+    if (src < 0) continue;
+    HostVec<int64_t> &cv = res.counts[a];
+    const HostVec<double> &sv = res.values[src];
+    cv.resize(sv.size());
+    for (size_t i = 0; i < cv.size(); i++) cv[i] = (int64_t)sv[i];
+  }
+  res.functions.resize(na);
+  res.counts.resize(na);
+  res.values.resize(na);
+  res.hll.resize(na);
+  res.hll_card.resize(na);
+  for (HllPart &part : res.hll_parts) part.off.resize(na);
+}
+
+namespace {
+
+// Group-by with multi-value group columns or MV functions: per segment the filter's bitset and one k_group_by_mv
+// (every doc's cartesian product of group keys, DictionaryBasedGroupKeyGenerator's MV branch) into dense
+// accumulators over the global key space, then the bitset path's finalisation. AvgMV needs its entry count beside
+// its sum: a hidden CountMV accumulator per AvgMV, folded into the function's counts after finalisation. num.groups.limit:
+// first-appearance admission per segment, then the 2 x limit cap (here, or the server's across ranks: `mp`).
+std::unique_ptr<GroupByResult> exec_group_by_mv(Engine &e, const std::vector<SegmentData *> &segs,
+                                                const pinot_query &q, pinot_exec_stats *stats,
+                                                const MvPartial *mp = nullptr) {
+  const int na = q.num_aggregations;
+  std::vector<int> hidden;
+  std::vector<pinot_agg_spec> specs = mv_extended_specs(q, hidden);
   pinot_query q2 = q;
   q2.aggregations = specs.data();
   q2.num_aggregations = (int32_t)specs.size();
@@ -3575,7 +3611,16 @@ std::unique_ptr<GroupByResult> exec_group_by_mv(Engine &e, const std::vector<Seg
   Arena ar;
   std::unique_ptr<FilterTreeInput> tree;
   std::vector<SegPlan> plans = plan_all(e, segs, q2, ar, tree);
-  KeySpace ks = build_key_space(segs, q2);
+  KeySpace ks;
+  if (mp) {  // the server's global key space (union dictionaries over every rank)
+    ks.gcard = *mp->gcard;
+    ks.gvalues = *mp->gvalues;
+    ks.remap = *mp->remap;
+    ks.G = 1;
+    for (auto g : ks.gcard) ks.G *= g;
+  } else {
+    ks = build_key_space(segs, q2);
+  }
   const int64_t limit = q.num_groups_limit > 0 ? q.num_groups_limit : e.num_groups_limit;
   require(!ks.hashed, PINOT_ERR_UNSUPPORTED,
           "multi-value group-by over a hashed key space (LONG_MAP / ARRAY_MAP holder shapes)");
@@ -3600,6 +3645,12 @@ std::unique_ptr<GroupByResult> exec_group_by_mv(Engine &e, const std::vector<Seg
     }
     adm.cap = 2 * limit;
     if (std::min(possible, ks.G) > adm.cap) adm.active = adm.cap_active = true;
+    if (mp && mp->aio) {  // the server applies the cap across ranks
+      adm.active = true;
+      adm.cap_active = false;
+    } else if (mp) {
+      require(!adm.cap_active, PINOT_ERR_DEVICE, "multi-GPU MV group-by partial without the server's cap exchange");
+    }
   }
   GroupAccs ga;
   for (int a = 0; a < nb; a++) {
@@ -3640,8 +3691,13 @@ std::unique_ptr<GroupByResult> exec_group_by_mv(Engine &e, const std::vector<Seg
     accs[a] = p;
     p += ks.G * ga.acc_bytes_per_key[a];
   }
+  if (mp) {  // partial: the server's arrays (HLL registers accumulate as u32 here, narrowed into its u8 layout)
+    counts = reinterpret_cast<unsigned long long *>(mp->counts);
+    for (int a = 0; a < nb; a++)
+      if (ga.acc_kind[a] != 5 && ga.acc_kind[a] != 4) accs[a] = mp->accs[a];
+  }
   PINOT_HIP(hipEventRecord(e.ev_start, e.stream));
-  init_accs(e, ks.G, counts, ga, accs.data());
+  if (!(mp && mp->aio && mp->aio->mode == 1)) init_accs(e, ks.G, counts, ga, accs.data());  // (export: no arrays)
   Timer t(e);
   std::vector<DeviceBuffer> remaps(S * q.num_group_by);
   std::vector<int64_t> seg_counts(S, 0);
@@ -3692,7 +3748,17 @@ std::unique_ptr<GroupByResult> exec_group_by_mv(Engine &e, const std::vector<Seg
   // admission: every segment's first-appearance bitmap (first positions, one radix sort each), then the cap
   DeviceBuffer adm_buf;
   int64_t words = 0;
-  if (adm.active) {
+  AdmissionIO *aio = mp ? mp->aio : nullptr;
+  if (adm.active && aio && aio->mode == 2) {  // the server's capped bitmaps for these segments
+    words = (ks.G + 31) / 32 + 1;
+    require(aio->words == words && aio->bitmaps.size() == S * (size_t)words, PINOT_ERR_DEVICE,
+            "admitted bitmaps of another shape");
+    const size_t fp_b = ((size_t)ks.G * 8 + 255) / 256 * 256;
+    adm_buf.alloc(fp_b + aio->bitmaps.size() * 4 + 256);
+    PINOT_HIP(hipMemcpyAsync(adm_buf.get<uint8_t>() + fp_b, aio->bitmaps.data(), aio->bitmaps.size() * 4,
+                             hipMemcpyHostToDevice, e.stream));
+    wait_stream(e);
+  } else if (adm.active) {
     words = (ks.G + 31) / 32 + 1;
     const size_t fp_b = ((size_t)ks.G * 8 + 255) / 256 * 256, bm_b = ((size_t)S * words * 4 + 255) / 256 * 256;
     const size_t scr = admission_scratch_bytes_u64(ks.G);
@@ -3709,6 +3775,13 @@ std::unique_ptr<GroupByResult> exec_group_by_mv(Engine &e, const std::vector<Seg
       launch_admission_bitmap_u64(first_pos, ks.G, adm.upper[si], bitmaps + si * words, words,
                                   adm_buf.get<uint8_t>() + fp_b + bm_b, scr, e.stream);
       PINOT_HIP(hipGetLastError());
+    }
+    if (aio && aio->mode == 1) {  // export for the server's cap: no accumulation here
+      aio->words = words;
+      aio->bitmaps.assign(S * (size_t)words, 0u);
+      PINOT_HIP(hipMemcpyAsync(aio->bitmaps.data(), bitmaps, aio->bitmaps.size() * 4, hipMemcpyDeviceToHost, e.stream));
+      wait_stream(e);
+      return nullptr;
     }
     if (adm.cap_active) {
       std::vector<uint32_t> bm(S * words);
@@ -3732,6 +3805,19 @@ std::unique_ptr<GroupByResult> exec_group_by_mv(Engine &e, const std::vector<Seg
     t.timed(1, [&] { launch_group_by_mv(a, e.stream); });
     PINOT_HIP(hipGetLastError());
   }
+  if (mp) {  // partial: the u32 registers into the server's u8 layout, the statistics, no finalisation
+    for (int a = 0; a < nb; a++)
+      if (ga.acc_kind[a] == 4) launch_narrow_u32(static_cast<const uint32_t *>(accs[a]), ks.G * 256,
+                                                 static_cast<uint8_t *>(mp->accs[a]), e.stream);
+    PINOT_HIP(hipGetLastError());
+    PINOT_HIP(hipEventRecord(e.ev_stop, e.stream));
+    wait_stream(e);
+    float ms = 0;
+    PINOT_HIP(hipEventElapsedTime(&ms, e.ev_start, e.ev_stop));
+    t.collect();
+    fill_stats(q, plans, seg_counts, ms, stats);
+    return nullptr;
+  }
   GroupByProgram gp{};
   gp.n_aggs = nb;
   gp.counts = counts;
@@ -3743,19 +3829,7 @@ std::unique_ptr<GroupByResult> exec_group_by_mv(Engine &e, const std::vector<Seg
   PINOT_HIP(hipEventElapsedTime(&ms, e.ev_start, e.ev_stop));
   t.collect();
   // CountMV: the entry count is the function's count; AvgMV: its hidden CountMV's values
-  for (int a = 0; a < na; a++) {
-    const int f = q.aggregations[a].function;
-    const int src = f == PINOT_AGG_COUNTMV ? a : hidden[a];
-    if (src < 0) continue;
-    HostVec<int64_t> &cv = res->counts[a];
-    const HostVec<double> &sv = res->values[src];
-    for (size_t i = 0; i < cv.size(); i++) cv[i] = (int64_t)sv[i];
-  }
-  res->functions.resize(na);
-  res->counts.resize(na);
-  res->values.resize(na);
-  res->hll.resize(na);
-  res->hll_card.resize(na);
+  fold_mv_counts(*res, q, hidden);
   fill_stats(q, plans, seg_counts, ms, stats);
   return res;
 }
@@ -4481,11 +4555,12 @@ void agg_identities(const pinot_query &q, pinot_agg_result *out) {
 
 int64_t admission_possible(const std::vector<SegmentData *> &segs, const pinot_query &q, const Engine &e) {
   const AdmissionPlan ap = plan_admission(segs, q, e, INT64_MAX);
+  const bool mv = touches_mv_group_by(segs, q);  // a multi-value doc yields several keys: no docs bound
   int64_t possible = 0;
   for (size_t i = 0; i < segs.size(); i++) {
     __int128 product = 1;
     for (int j = 0; j < q.num_group_by; j++) product *= segs[i]->column(q.group_by[j])->card;
-    const int64_t reach = (int64_t)std::min<__int128>(product, (__int128)segs[i]->num_docs);
+    const int64_t reach = (int64_t)std::min<__int128>(product, mv ? (__int128)INT64_MAX : (__int128)segs[i]->num_docs);
     possible += std::min(ap.upper[i], reach);
   }
   return possible;
@@ -4534,4 +4609,11 @@ void merge_agg_parts(const pinot_query &q, const std::vector<const pinot_agg_res
   }
 }
 
+}  // namespace pinot
+
+namespace pinot {
+void exec_group_by_mv_partial(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q,
+                              const MvPartial &mp, pinot_exec_stats *stats) {
+  exec_group_by_mv(e, segs, q, stats, &mp);
+}
 }  // namespace pinot

@@ -254,6 +254,7 @@ __global__ void k_group_final(const unsigned long long *__restrict__ counts, con
       double v;
       switch (f.kind[g]) {
         case 0:
+        case 6:
         case 7: v = (double)static_cast<const long long *>(f.acc[g])[k]; break;
         case 1: v = static_cast<const double *>(f.acc[g])[k]; break;
         case 2:

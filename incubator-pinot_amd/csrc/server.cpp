@@ -367,13 +367,24 @@ void server_aggregate(ServerImpl &s, const std::vector<SegmentRef> &refs, const 
 }
 
 // ------------------------------------------------------------------ group-by
-std::unique_ptr<GroupByResult> server_group_by(ServerImpl &s, const std::vector<SegmentRef> &refs, const pinot_query &q,
+std::unique_ptr<GroupByResult> server_group_by(ServerImpl &s, const std::vector<SegmentRef> &refs, const pinot_query &q0,
                                                pinot_exec_stats *stats) {
   std::lock_guard<std::mutex> lk(s.mu);
   for (const SegmentRef &r : refs)
     require(r.engine >= 0 && r.engine < (int)s.engines.size(), PINOT_ERR_BAD_ARG, "segment ref: no such engine");
+  require(q0.num_aggregations >= 1 && q0.num_aggregations <= kMaxAggs, PINOT_ERR_UNSUPPORTED,
+          "1..8 aggregation functions per query");
+  // the partials run on the extended function list (a hidden CountMV per AvgMV carries its entry count), folded
+  // back into the query's functions at the end
+  std::vector<int> hidden;
+  const std::vector<pinot_agg_spec> xspecs = mv_extended_specs(q0, hidden);
+  pinot_query qx = q0;
+  qx.aggregations = xspecs.data();
+  qx.num_aggregations = (int32_t)xspecs.size();
+  const pinot_query &q = qx;
   const int na = q.num_aggregations;
-  require(na >= 1 && na <= kMaxAggs, PINOT_ERR_UNSUPPORTED, "1..8 aggregation functions per query");
+  bool mv_counts = na != q0.num_aggregations;
+  for (int a = 0; a < q0.num_aggregations; a++) mv_counts = mv_counts || q0.aggregations[a].function == PINOT_AGG_COUNTMV;
   require(q.num_group_by >= 1 && q.num_group_by <= kMaxGroupCols, PINOT_ERR_UNSUPPORTED, "1..16 group-by columns");
   const size_t E = s.engines.size();
   std::vector<std::unique_ptr<GroupByResult>> res(E);
@@ -388,6 +399,7 @@ std::unique_ptr<GroupByResult> server_group_by(ServerImpl &s, const std::vector<
     int64_t tdocs = 0, possible = 0;
     std::vector<int> kinds;
     std::vector<uint8_t> dicts;
+    bool mv = false;  // this rank's segments take the multi-value partial (MV group columns or MV functions)
     Status my = capture([&] {
       std::lock_guard<std::mutex> el(e.mu);
       segs = rank_segments(e, i, refs, q, tdocs);
@@ -395,6 +407,7 @@ std::unique_ptr<GroupByResult> server_group_by(ServerImpl &s, const std::vector<
       if (!segs.empty()) {
         kinds = group_acc_kind_list(*segs[0], q);
         possible = admission_possible(segs, q, e);
+        mv = touches_mv_group_by(segs, q0);
       }
     });
     ph.mark(0);
@@ -449,7 +462,12 @@ std::unique_ptr<GroupByResult> server_group_by(ServerImpl &s, const std::vector<
       my = capture([&] {
         std::lock_guard<std::mutex> el(e.mu);
         DeadlineScope ds(e, q.timeout_ms);
-        if (!segs.empty()) exec_group_by_partial_ks(e, segs, q, ks.gcard, ks.gvalues, ks.remap, nullptr, nullptr, nullptr, &ex);
+        if (segs.empty()) return;
+        if (mv)
+          exec_group_by_mv_partial(e, segs, q0, MvPartial{&ks.gcard, &ks.gvalues, &ks.remap, nullptr, nullptr, &ex},
+                                   nullptr);
+        else
+          exec_group_by_partial_ks(e, segs, q, ks.gcard, ks.gvalues, ks.remap, nullptr, nullptr, nullptr, &ex);
       });
       Writer wc;
       put_status(wc, my);
@@ -515,7 +533,12 @@ std::unique_ptr<GroupByResult> server_group_by(ServerImpl &s, const std::vector<
         if (accs[a])
           PINOT_HIP(hipMemsetAsync(static_cast<uint8_t *>(accs[a]) + (size_t)from * acc_unit(gkinds[a]),
                                    gkinds[a] == 2 ? 0xFF : 0, (size_t)(Gp - from) * acc_unit(gkinds[a]), e.stream));
-      if (!segs.empty())
+      if (!segs.empty() && mv)
+        exec_group_by_mv_partial(e, segs, q0,
+                                 MvPartial{&ks.gcard, &ks.gvalues, &ks.remap, reinterpret_cast<int64_t *>(counts),
+                                           accs.data(), admit.mode ? &admit : nullptr},
+                                 &st);
+      else if (!segs.empty())
         exec_group_by_partial_ks(e, segs, q, ks.gcard, ks.gvalues, ks.remap, reinterpret_cast<int64_t *>(counts),
                                  accs.data(), &st, admit.mode ? &admit : nullptr);
       PINOT_HIP(hipStreamSynchronize(e.stream));
@@ -605,6 +628,7 @@ std::unique_ptr<GroupByResult> server_group_by(ServerImpl &s, const std::vector<
     }
   }
   out->counts_shared = true;
+  if (mv_counts) fold_mv_counts(*out, q0, hidden);  // CountMV / AvgMV counts: entries, not docs
   if (stats) *stats = tot[0];
   return out;
 }

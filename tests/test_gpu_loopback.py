@@ -333,3 +333,35 @@ def test_loopback_mv_and_star_tree_aggregations():
     exp, scanned = S.execute_server(sts_host, trees, q)
     assert got[:3] == exp[:3] and (got[3].sum, got[3].count) == exp[3] and st.num_docs_scanned == scanned
     srv.close()
+
+
+@pytest.mark.parametrize("K", [2, 3])
+def test_loopback_mv_group_by(K):
+    """Group-by over multi-value group columns and with *MV functions across K loopback ranks: each rank's
+    k_group_by_mv partial over the union key space (AvgMV's entry count in a hidden CountMV array through the
+    reduce-scatter), then, with a binding num.groups.limit, each segment's first-appearance holder (getIntRawKeys
+    order) and the 2 x limit cap over every rank's segments in rank order, then each rank's segment order
+    (DictionaryBasedGroupKeyGenerator.java:282-302, CombineGroupByOperator.java:80,147)."""
+    from test_gpu_mv import _check
+    from test_mv import mv_segment
+    rng = np.random.default_rng(4600 + K)
+    nseg = 5
+    host = [mv_segment(rng, int(rng.choice([800, 2500])), name="lm%d" % i) for i in range(nseg)]
+    srv = GpuServer([0] * K, "server.loopback=1")
+    gsegs = [srv.engines[i % K].register(s) for i, s in enumerate(host)]
+    ordered = [host[i] for r in range(K) for i in range(nseg) if i % K == r]
+    aggs = [{"function": "COUNT", "column": "*"}, {"function": "SUM", "column": "m"},
+            {"function": "MAXMV", "column": "tags"}, {"function": "AVGMV", "column": "tagl"},
+            {"function": "COUNTMV", "column": "tags_s"}, {"function": "DISTINCTCOUNTHLLMV", "column": "tagd"}]
+    for cols, limit, thr in ((["tags", "g"], 100_000, 10_000), (["tags_s", "g"], 100_000, 10_000),
+                             (["g"], 100_000, 10_000), (["tags", "tags_s"], 60, 10), (["tagl", "tags"], 150, 40)):
+        q = {"aggregations": aggs, "filter": {"operator": "RANGE", "column": "m", "values": ["[-900\t\t*)"]},
+             "group_by": {"columns": cols, "top_n": 10}}
+        ex = ServerExecutor(srv, num_groups_limit=limit, max_init_group_holder_capacity=thr, pruners=0)
+        got, st = ex.process_query(q, gsegs, trim=False)
+        exp, scanned = O.execute_server(ordered, q, num_groups_limit=limit, array_threshold=thr)
+        assert st.num_docs_scanned == scanned
+        if limit < 1000:
+            assert len(exp) == 2 * limit  # the cap binds
+        _check(q, got, exp)
+    srv.close()

@@ -41,15 +41,20 @@ COLUMNS = [("d0", 16), ("d1", 100), ("d2", 1000), ("d3", 4096), ("d4", 10000), (
 QUERY = "SELECT COUNT(*), SUM(d8) FROM fact WHERE d2 BETWEEN 100 AND 599 AND d0 IN (1, 3, 5, 7)"
 CONFIG4 = "SELECT SUM(d8), AVG(d8), DISTINCTCOUNTHLL(d5) FROM fact WHERE d2 < 800 GROUP BY d6, d7 TOP 10"
 CONFIG4_BYTES_PER_ROW = (10 + 10 + 10 + 20 + 16) / 8  # d2 filter + d6, d7 keys + d8 SUM/AVG + d5 HLL
+# the small-key-space group-by (1,600 groups): per-block LDS-privatised accumulators, one launch (GB_LDS)
+LDS_QUERY = "SELECT COUNT(*), SUM(d8), AVG(d8) FROM fact WHERE d2 < 800 GROUP BY d0, d1 TOP 10"
+LDS_BYTES_PER_ROW = (10 + 4 + 7 + 20) / 8  # d2 filter + d0, d1 keys + d8 SUM/AVG
 BASE_SEED = 0x5EED0000
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (8.0 TB/s spec)
 BITS = {n: max(1, (c - 1).bit_length()) for n, c in COLUMNS}
 # device sources each workload's kernels are built from (a PMC traffic profile is reported only for these exact bytes)
 KERNEL_SOURCES = {
     "config2": ("fused.hip", "scan.hip", "kernels.hip", "fused_common.h", "common.h", "device.h", "kernels.h"),
-    "config4": ("fused_group.hip", "groupby.hip", "kernels.hip", "fused_common.h", "common.h", "device.h",
-                "kernels.h"),
+    "config4": ("fused_group.hip", "group_ring.hip", "group_lq.h", "groupby.hip", "kernels.hip", "fused_common.h",
+                "common.h", "device.h", "kernels.h"),
+    "lds": ("fused_group.hip", "group_lq.h", "groupby.hip", "fused_common.h", "common.h", "device.h", "kernels.h"),
 }
+WORKLOAD_QUERY = {"config2": QUERY, "config4": CONFIG4, "lds": LDS_QUERY}
 
 
 def algorithmic_bytes(num_docs):
@@ -144,15 +149,18 @@ def cpu_baseline(threads, segs, docs, min_seconds=10.0):
     return res
 
 
-def cpu_baseline_config4(threads, segs, docs, min_seconds=10.0):
+def cpu_baseline_config4(threads, segs, docs, min_seconds=10.0, workload="config4"):
     """Reference-faithful group-by (oracle/faithful.c: per-doc readInt, INT_MAP group ids, double / AvgPair /
     HyperLogLog holders per group, then the CombineGroupByOperator merge) on a bounded sample of the config-4
-    workload, repeated until `min_seconds` of CPU work; the median run is reported."""
+    workload (or the LDS one: GROUP BY d0, d1, no HLL), repeated until `min_seconds` of CPU work; the median run
+    is reported."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import faithful
     from concurrent.futures import ThreadPoolExecutor
     faithful.load()
-    need = ("d2", "d5", "d6", "d7", "d8")
+    c4 = workload == "config4"
+    g0, g1, hcol = ("d6", "d7", "d5") if c4 else ("d0", "d1", None)
+    need = ("d2", "d8", g0, g1) + ((hcol,) if hcol else ())
     t0 = time.time()
     table = faithful.SyntheticTable(COLUMNS, docs, 0, BASE_SEED, needed=set())
     jobs = {}
@@ -168,17 +176,17 @@ def cpu_baseline_config4(threads, segs, docs, min_seconds=10.0):
     t_start = time.time()
     while len(times) < 2 or time.time() - t_start < min_seconds:
         t0 = time.time()
-        groups, cnt, sm = faithful.run_group_by(table, leaves, "d6", "d7", "d8", "d5", threads)
+        groups, cnt, sm = faithful.run_group_by(table, leaves, g0, g1, "d8", hcol, threads)
         times.append(time.time() - t0)
     times.sort()
     med = times[len(times) // 2]
     rows = segs * docs
     return {"value": rows / med, "unit": "rows/s", "cores": host_cpu_info()["available_processors"], "threads": threads,
             "kind": "port",
-            "sample": "%d segments x %d docs of the same synthetic table and config-4 query, %d runs over %.1fs "
+            "sample": "%d segments x %d docs of the same synthetic table and %s query, %d runs over %.1fs "
                       "(median %.3fs, %d groups; data generated in %.1fs); oracle/faithful.c per-doc INT_MAP "
                       "group-by + CombineGroupByOperator merge (reference-faithful C restatement: no JVM here)" %
-                      (segs, docs, len(times), sum(times), med, groups, gen_s)}
+                      (segs, docs, workload, len(times), sum(times), med, groups, gen_s)}
 
 
 def kernel_source_hash(workload="config2"):
@@ -342,9 +350,11 @@ def kernel_pass(job, step, reps):
 
 
 def measure(job, args, workload):
+    gb = workload != "config2"  # a group-by workload (config 4, or the LDS-privatised small-key-space one)
     c4 = workload == "config4"
-    step = job.step_fn(CONFIG4 if c4 else QUERY, c4)
-    steps = args.steps if not c4 or args.workload == "config4" else args.c4_steps
+    text = WORKLOAD_QUERY[workload]
+    step = job.step_fn(text, gb)
+    steps = args.steps if workload == args.workload else args.c4_steps
     elapsed, (step_ms, dev_ms), abi_ms, res, st = timed_steps(job, step, steps, args.warmup)
     ms_per_step = elapsed * 1000.0 / steps
     value = job.total_rows * steps / elapsed
@@ -354,8 +364,12 @@ def measure(job, args, workload):
     kern = {}
     if c4:
         alg = segs_here * args.docs * CONFIG4_BYTES_PER_ROW
-        # the group-by pipeline of one query on engine 0 (COUNT histogram, scan, EMIT, partition reduce: one region)
+        # the group-by pipeline of one query on engine 0 (filter, ring partition, ring reduce: one timed region)
         names = ((1, "group_by_pipeline", alg),)
+        query_b = alg
+    elif gb:
+        alg = segs_here * args.docs * LDS_BYTES_PER_ROW
+        names = ((1, "k_group_query_lds", alg),)  # ONE launch over every segment: LDS accumulators per block
         query_b = alg
     else:
         filt_b, agg_b, query_b1 = algorithmic_bytes(args.docs)
@@ -398,7 +412,7 @@ def measure(job, args, workload):
         "dtype": "u32 dictIds / int64 sums" + (" / u8 HLL registers" if c4 else ""),
         "data": "synthetic (seeded splitmix64 dict-encoded segments generated in HBM)",
         "config": {"workload": "%s: %d x %d-doc segments per GPU, 10 fixed-bit INT columns, %s" %
-                   (workload, args.segments, args.docs, CONFIG4 if c4 else QUERY),
+                   (workload, args.segments, args.docs, text),
                    "segments_per_gpu": args.segments, "docs_per_segment": args.docs,
                    "parallelism": "segments%d" % job.n_gpus, "path": job.path},
         "roofline": {"bound": "hbm", "achieved": kern[dom]["gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -408,12 +422,12 @@ def measure(job, args, workload):
     }
     if phases:
         out["merge_phases_ms"] = phases
-    if c4:
+    if gb:
         if job.path == "engine":  # the timed step returned DataTable bytes; the full result once for the check
             out["datatable_bytes"] = len(res)
-            res, _ = job.ex.group_by_result(job.ex.prepare(CONFIG4), job.segs)
+            res, _ = job.ex.group_by_result(job.ex.prepare(text), job.segs)
         n_groups = res.num_groups()
-        counts, sums = res.function_values(1)  # AVG(d8): per-group counts and sums
+        counts, sums = res.function_values(1 if c4 else 2)  # AVG(d8): per-group counts and sums
         chk, _ = job.ex.process_query(job.ex.prepare("SELECT COUNT(*), SUM(d8) FROM fact WHERE d2 < 800"), job.segs)
         tot = [int(counts.sum()), int(sums.sum())]
         if job.dist:  # rank 0 holds the gathered result, the other ranks none
@@ -423,7 +437,7 @@ def measure(job, args, workload):
             n_groups, tot = int(t[0]), [int(t[1]), int(t[2])]
         out["result"] = {"groups": n_groups, "sum_group_counts": tot[0], "sum_group_sums": tot[1]}
         out["verify"] = {"filtered_count": chk[0], "filtered_sum": int(chk[1]),
-                         "match": tot == [chk[0], int(chk[1])] and n_groups == 1_000_000,
+                         "match": tot == [chk[0], int(chk[1])] and n_groups == (1_000_000 if c4 else 1_600),
                          "how": "Σ per-group counts / sums == the aggregation-only COUNT(*) / SUM(d8) of the same "
                                 "filter (independent kernel path); group-level parity: tests/test_gpu_configs.py"}
     else:
@@ -457,8 +471,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=50)
-    ap.add_argument("--workload", default="config2", choices=("config2", "config4"))
+    ap.add_argument("--workload", default="config2", choices=("config2", "config4", "lds"))
     ap.add_argument("--no-config4", action="store_true", help="config2 line without the embedded config-4 object")
+    ap.add_argument("--no-lds", action="store_true", help="config2 line without the embedded LDS group-by object")
     ap.add_argument("--c4-steps", type=int, default=None, help="timed steps of the embedded config 4 (default --steps)")
     ap.add_argument("--path", default="auto", choices=("auto", "engine", "server"),
                     help="N = 1: one engine (auto) or the multi-GPU server over one GPU")
@@ -498,12 +513,17 @@ def main():
         keep = ("value", "unit", "ms_per_step", "p50_query_ms", "p50_c_abi_ms", "step_ms_detail", "steps", "warmup",
                 "dtype", "config", "roofline", "merge_phases_ms", "result", "verify")
         out["config4"] = {k: c4[k] for k in keep if k in c4}
+    if args.workload == "config2" and not args.no_lds:
+        lds = measure(job, args, "lds")
+        keep = ("value", "unit", "ms_per_step", "p50_query_ms", "step_ms_detail", "steps", "dtype", "config",
+                "roofline", "result", "verify")
+        out["lds_group_by"] = {k: lds[k] for k in keep if k in lds}
     cpu_ok = rank == 0 and world == 1 and job.n_gpus == 1 and not args.no_cpu_baseline
     if cpu_ok:
         host_desc = {"host": host, "threads": args.cpu_threads}
-        if args.workload == "config4":
+        if args.workload != "config2":
             cb = cpu_baseline_config4(args.cpu_threads, args.cpu_segments or 16, args.cpu_docs or 4_000_000,
-                                      args.cpu_seconds)
+                                      args.cpu_seconds, workload=args.workload)
         else:
             cb = cpu_baseline(args.cpu_threads, args.cpu_segments or 16, args.cpu_docs or 32_000_000,
                               args.cpu_seconds)
@@ -519,6 +539,11 @@ def main():
                                        args.cpu_seconds)
             out["config4"]["cpu_baseline"] = dict(cb4, **host_desc)
             out["config4"]["gpu_vs_cpu"] = out["config4"]["value"] / cb4["value"]
+        if "lds_group_by" in out:
+            cbl = cpu_baseline_config4(args.cpu_threads, args.cpu_segments or 16, args.cpu_docs or 8_000_000,
+                                       args.cpu_seconds, workload="lds")
+            out["lds_group_by"]["cpu_baseline"] = dict(cbl, **host_desc)
+            out["lds_group_by"]["gpu_vs_cpu"] = out["lds_group_by"]["value"] / cbl["value"]
     if args.workload == "config2" and not args.no_verify and rank == 0:
         out["verify"] = verify_config2(job, args, out, head_res["count"], head_res["sum"])
     if rank == 0:

@@ -350,7 +350,7 @@ typedef struct {
   int32_t g0_card;
   const uint8_t *m_fwd;           /* SUM / AVG column */
   int m_bits;
-  const uint8_t *h_fwd;           /* DISTINCTCOUNTHLL column */
+  const uint8_t *h_fwd;           /* DISTINCTCOUNTHLL column (NULL: the query has none) */
   int h_bits;
   /* outputs (owned): groups in first-seen order */
   int32_t ngroups;
@@ -432,7 +432,7 @@ static void run_group_segment(pinot_group_task *t) {
       sum[gids[i]] += v;
       cnt[gids[i]] += 1;
     }
-    for (int i = 0; i < nd; i++) { /* DISTINCTCOUNTHLL(h): offer(hashLong(value)) */
+    for (int i = 0; t->h_fwd && i < nd; i++) { /* DISTINCTCOUNTHLL(h): offer(hashLong(value)) */
       const uint32_t h = murmur_hash_long(read_int(t->h_fwd, doc_ids[i], t->h_bits));
       const uint32_t j = h >> 24;
       const uint32_t w = (h << 8) | 129u;
@@ -497,6 +497,7 @@ static void *merge_worker(void *arg) {
       if (!m->mc[k]) a->groups++;
       m->mc[k] += t->cnt[g];
       m->ms[k] += t->sum[g];
+      if (!t->h_fwd) continue;
       uint8_t *dst = m->mr + (size_t)256 * k;
       const uint8_t *src = t->regs + (size_t)256 * g;
       for (int j = 0; j < 256; j++)

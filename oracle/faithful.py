@@ -141,7 +141,8 @@ def run_group_by(table, leaves, g0, g1, metric, hll_col, threads):
         t.g0_fwd, t.g0_bits, t.g0_card = cols[g0].ctypes.data, bits_for(table.card(g0)), table.card(g0)
         t.g1_fwd, t.g1_bits = cols[g1].ctypes.data, bits_for(table.card(g1))
         t.m_fwd, t.m_bits = cols[metric].ctypes.data, bits_for(table.card(metric))
-        t.h_fwd, t.h_bits = cols[hll_col].ctypes.data, bits_for(table.card(hll_col))
+        if hll_col is not None:  # None: no DISTINCTCOUNTHLL in the query
+            t.h_fwd, t.h_bits = cols[hll_col].ctypes.data, bits_for(table.card(hll_col))
     tc, ts = C.c_int64(), C.c_double()
     groups = lib.pinot_faithful_group_run(tasks, len(table.segments), threads, table.card(g0) * table.card(g1),
                                           C.byref(tc), C.byref(ts))

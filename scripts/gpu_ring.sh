@@ -5,9 +5,11 @@ set -o pipefail
 tag=${1:-ring}
 out=gpurun_out/$tag
 mkdir -p $out
-timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_gpu_ring.py \
+timeout -k 10 900 python -u -m pytest --maxfail=6 -v --timeout 300 --timeout-method thread -m gpu tests/test_gpu_ring.py \
   tests/test_gpu_configs.py tests/test_gpu_raw.py tests/test_gpu_segment_dir.py tests/test_gpu_startree.py tests/test_gpu_loopback.py tests/test_gpu_mv.py tests/test_gpu_parity.py \
-  -k "ring or config4 or trim or fixture or cache or hll or HLL or limit or admission or loopback_mv or deep_filter or wide_bitmap" > $out/pytest.log 2>&1 || { tail -60 $out/pytest.log; exit 1; }
+  -k "fixed_byte or ring or config4 or trim or fixture or cache or hll or HLL or limit or admission or loopback_mv or deep_filter or wide_bitmap" > $out/pytest.log 2>&1; rc=$?
+grep -E "FAILED|Error" $out/pytest.log | head -20
+[ $rc -eq 0 ] || [ $rc -eq 1 ] || { tail -40 $out/pytest.log; exit 1; }  # 1 = test failures (bench still runs)
 grep -E "passed|failed" $out/pytest.log | tail -2
 timeout -k 10 300 python bench.py --workload config4 --steps 10 --warmup 3 --cpu-seconds 5 > $out/bench_config4.json 2> $out/bench_config4.err || { tail -20 $out/bench_config4.err; exit 1; }
 tail -1 $out/bench_config4.json | cut -c1-2500

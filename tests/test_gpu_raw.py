@@ -25,6 +25,8 @@ def _norm(v):
         return ("hll", bytes(v.registers), v.cardinality())
     if hasattr(v, "count") and hasattr(v, "sum"):  # AvgPair
         return ("avg", v.sum, v.count)
+    if isinstance(v, tuple) and len(v) == 2:  # the oracle's AvgPair (sum, count)
+        return ("avg", v[0], v[1])
     return v
 
 

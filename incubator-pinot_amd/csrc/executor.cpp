@@ -3238,7 +3238,9 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
   a.mode = gp.mode == GB_EMIT ? GB_COUNT : gp.mode;
   a.reserved2 = e.debug_emit;  // timing experiments only (debug.emit)
   a.nt_store = e.group_nt_store;
-  if (gp.mode == GB_EMIT && !ks.hashed && e.group_prefetch && (e.debug_emit == 0 || e.debug_emit >= 3)) {
+  // the prefetched column list: GB_EMIT's record fields, or GB_LDS's lane-owns-quarter reads (group.lw=2)
+  if (((gp.mode == GB_EMIT && (e.debug_emit == 0 || e.debug_emit >= 3)) || (gp.mode == GB_LDS && e.group_lw == 2)) &&
+      !ks.hashed && e.group_prefetch) {
     int nc = q.num_group_by;
     for (int i = 0; i < na && nc <= kGroupPfCols; i++)
       if (gx.acc_kind[i] != 5) {
@@ -3349,6 +3351,7 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     ra.shift = rp.shift;
     ra.nblk = (int32_t)nblk;
     ra.cap = rp.cap;
+    ra.debug = e.debug_ring;
     ra.blk_matched = blk_matched;
     ra.records = e.group_records.get<unsigned long long>();
     ra.hist = hist;
@@ -3476,12 +3479,14 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
                                  hipMemcpyDeviceToDevice, e.stream));
     PINOT_HIP(hipGetLastError());
     std::vector<unsigned long long> hm(S);
-    uint32_t rstat = 0;
+    uint32_t rs[4] = {0, 0, 0, 0};
     PINOT_HIP(hipMemcpyAsync(hm.data(), matched, S * 8, hipMemcpyDeviceToHost, e.stream));
-    if (ring_status) PINOT_HIP(hipMemcpyAsync(&rstat, ring_status, 4, hipMemcpyDeviceToHost, e.stream));
+    if (ring_status) PINOT_HIP(hipMemcpyAsync(rs, ring_status, 16, hipMemcpyDeviceToHost, e.stream));
     PINOT_HIP(hipEventRecord(e.ev_stop, e.stream));
     wait_stream(e);
-    if (rstat) return ring_fallback();
+    e.ring_waits += rs[2];
+    e.ring_sleeps += rs[3];
+    if (rs[0]) return ring_fallback();
     float pms = 0;
     PINOT_HIP(hipEventElapsedTime(&pms, e.ev_start, e.ev_stop));
     t.collect();
@@ -3498,13 +3503,15 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
   std::vector<unsigned long long> hmatched(S);
   uint32_t verify_err = 0;
   long long *keys_dev = nullptr;
-  uint32_t rstat = 0;
+  uint32_t rs[4] = {0, 0, 0, 0};
   const unsigned long long n = compact_dense(e, counts, ks.G, keys_dev, [&] {
     PINOT_HIP(hipMemcpyAsync(hmatched.data(), matched, S * 8, hipMemcpyDeviceToHost, e.stream));
     if (ks.hashed) PINOT_HIP(hipMemcpyAsync(&verify_err, a.verify_err, 4, hipMemcpyDeviceToHost, e.stream));
-    if (ring_status) PINOT_HIP(hipMemcpyAsync(&rstat, ring_status, 4, hipMemcpyDeviceToHost, e.stream));
+    if (ring_status) PINOT_HIP(hipMemcpyAsync(rs, ring_status, 16, hipMemcpyDeviceToHost, e.stream));
   });
-  if (rstat) return ring_fallback();
+  e.ring_waits += rs[2];
+  e.ring_sleeps += rs[3];
+  if (rs[0]) return ring_fallback();
   if (verify_err) {  // 64-bit fingerprint collision: retry with another seed
     require(attempt < 3, PINOT_ERR_DEVICE, "group-key fingerprint collisions persist");
     return exec_group_by_fused(e, segs, q, ks_in, ga, stats, attempt + 1);
@@ -3601,7 +3608,6 @@ namespace {
 std::unique_ptr<GroupByResult> exec_group_by_mv(Engine &e, const std::vector<SegmentData *> &segs,
                                                 const pinot_query &q, pinot_exec_stats *stats,
                                                 const MvPartial *mp = nullptr) {
-  const int na = q.num_aggregations;
   std::vector<int> hidden;
   std::vector<pinot_agg_spec> specs = mv_extended_specs(q, hidden);
   pinot_query q2 = q;

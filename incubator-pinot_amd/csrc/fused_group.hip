@@ -85,9 +85,10 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
 template <bool LDS>
 __device__ __forceinline__ void agg_update(const GroupAggDev &ag, void *acc, long long k, uint32_t id) {
   switch (ag.acc_kind) {
-    case 0:
+    case 0:  // LDS + affine dictionary: Σ dictId here, Σ value = base * count + step * Σ dictId at the flush
       atomicAdd(static_cast<unsigned long long *>(acc) + k,
-                (unsigned long long)(long long)static_cast<const int32_t *>(ag.dict)[id]);
+                LDS && ag.affine ? (unsigned long long)id
+                                 : (unsigned long long)(long long)static_cast<const int32_t *>(ag.dict)[id]);
       break;
     case 1:
       atomicAdd(static_cast<double *>(acc) + k, dict_value(ag.dict, ag.value_kind, id));
@@ -770,6 +771,30 @@ __device__ __forceinline__ void lq_load(const LqCols &k, int64_t qi, uint32_t (&
     if (k.bits[c]) load_raw_lq(k.fwd[c], k.bits[c], qi, R[c]);
 }
 
+// GB_LDS: column slot C (an aggregated column, compile-time so its raw registers stay registers) folded into the
+// block's LDS accumulators of its function, 16 docs per lane.
+template <int C, int NC>
+__device__ __forceinline__ void lds_sink_col(const GroupArgs &a, const GroupSegment &sg, const LqCols &k,
+                                             const uint32_t (&R)[NC][12], int64_t qi, uint32_t act,
+                                             const uint32_t (&key)[16], uint32_t *plds) {
+  if constexpr (C < NC) {
+    if (!k.bits[C] || k.fsh[C] < 0) return;
+    const GroupAggDev ag = load_const(a.aggs + sg.first_agg + a.pf_agg[C]);
+    uint8_t *acc = reinterpret_cast<uint8_t *>(plds) + ag.lds_off;
+    decode_raw_lq(R[C], k.bits[C], qi, [&](const uint32_t (&id)[16]) {
+      if (ag.acc_kind == 0 && ag.affine) {  // Σ dictId (converted at the flush)
+#pragma unroll
+        for (int j = 0; j < 16; j++)
+          if ((act >> j) & 1u) atomicAdd(reinterpret_cast<unsigned long long *>(acc) + key[j], (unsigned long long)id[j]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 16; j++)
+          if ((act >> j) & 1u) agg_update<true>(ag, acc, (long long)key[j], id[j]);
+      }
+    });
+  }
+}
+
 // Decode a quarter's loaded columns into keys / records, then the sink. The group columns (slots [0, n_gcols)) come
 // first; for GB_EMIT2 the key then folds into the record right away (local key | partition << kRecPartShift) so the
 // key array is dead while the aggregated columns are decoded (register pressure).
@@ -795,6 +820,21 @@ __device__ __forceinline__ void lq_process(const GroupArgs &a, const GroupSegmen
         for (int j = 0; j < 16; j++) key[j] += id[j] * stride;
       }
     });
+  }
+  if constexpr (MODE == GB_LDS) {  // block-private LDS accumulators: the count, then each aggregated column's slot
+    uint32_t act = mq;
+    if (sg.admitted) {
+#pragma unroll
+      for (int j = 0; j < 16; j++)
+        if (!((gload<uint32_t>(sg.admitted + (key[j] >> 5)) >> (key[j] & 31)) & 1u)) act &= ~(1u << j);
+    }
+#pragma unroll
+    for (int j = 0; j < 16; j++)
+      if ((act >> j) & 1u) atomicAdd(plds + key[j], 1u);
+    lds_sink_col<1, NC>(a, sg, k, R, qi, act, key, plds);
+    lds_sink_col<2, NC>(a, sg, k, R, qi, act, key, plds);
+    lds_sink_col<3, NC>(a, sg, k, R, qi, act, key, plds);
+    return;
   }
   if constexpr (MODE == GB_EMIT2 || MODE == GB_COUNT) {
     uint32_t act = mq;
@@ -905,9 +945,12 @@ __device__ __forceinline__ void flush_group_lds(const GroupArgs &a, const GroupS
       const GroupAggDev ag = load_const(a.aggs + sg.first_agg + g);
       const uint8_t *src = acc_lds + ag.lds_off;
       switch (ag.acc_kind) {
-        case 0:
-          atomicAdd(static_cast<unsigned long long *>(ag.acc) + k, reinterpret_cast<const unsigned long long *>(src)[k]);
+        case 0: {
+          unsigned long long v = reinterpret_cast<const unsigned long long *>(src)[k];
+          if (ag.affine) v = (unsigned long long)ag.affine_base * c + (unsigned long long)ag.affine_step * v;  // mod 2^64
+          atomicAdd(static_cast<unsigned long long *>(ag.acc) + k, v);
           break;
+        }
         case 1:
           atomicAdd(static_cast<double *>(ag.acc) + k, reinterpret_cast<const double *>(src)[k]);
           break;
@@ -1039,6 +1082,7 @@ constexpr int kGroupLwEmitBlock = 512;
 constexpr int kGroupLqEmitBlockWide = 1024;
 
 static int group_block_threads(const GroupArgs &a) {
+  if (a.mode == GB_LDS && a.lw == 2 && a.pf_nc > 0) return kGroupLwEmitBlock;  // lane-owns-quarter registers
   if (a.lw == 2 && a.mode == GB_EMIT2 && a.emit_block == kGroupLqEmitBlockWide) return kGroupLqEmitBlockWide;
   return (a.lw && (a.mode == GB_EMIT || a.mode == GB_EMIT2)) ? kGroupLwEmitBlock : kGroupBlock;
 }
@@ -1049,7 +1093,10 @@ static void with_group_kernel(const GroupArgs &a, V &&v) {
   const bool lw = a.lw && a.pf_nc > 0, lh = lw && a.lw == 2;
   switch (a.mode) {
     case GB_GLOBAL: v(&k_group_query<GB_GLOBAL, 0, kGroupBlock>, kGroupBlock); break;
-    case GB_LDS: v(&k_group_query<GB_LDS, 0, kGroupBlock>, kGroupBlock); break;
+    case GB_LDS:
+      if (lh) v(&k_group_query<GB_LDS, 3, kGroupLwEmitBlock>, kGroupLwEmitBlock);
+      else v(&k_group_query<GB_LDS, 0, kGroupBlock>, kGroupBlock);
+      break;
     case GB_COUNT:
       if (lh && a.n_gcols <= kLqCountCols) v(&k_group_query<GB_COUNT, 3, kGroupBlock>, kGroupBlock);
       else if (lw) v(&k_group_query<GB_COUNT, 2, kGroupBlock>, kGroupBlock);

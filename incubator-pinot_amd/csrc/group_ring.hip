@@ -64,6 +64,7 @@ __device__ __forceinline__ uint32_t rec_part(unsigned long long r) { return (uin
 // this round's flushing lanes, then the wave stores eight halves per instruction (8 lanes x 8 B each). The laps-flushed
 // bump follows the ring reads in this wave's LDS order, so a writer of the next lap (which waits for the bump) never
 // overwrites a slot before it has been read.
+template <int DBG>
 __device__ __forceinline__ void ring_flush(const RingArgs &a, const RingLds &L, uint32_t *fl, uint32_t comp,
                                            const uint32_t (&pos)[16], const unsigned long long (&rec)[16],
                                            unsigned long long *region0, uint32_t C, int lane) {
@@ -91,7 +92,7 @@ __device__ __forceinline__ void ring_flush(const RingArgs &a, const RingLds &L, 
         const uint32_t e = fl[f];
         const uint32_t p = e >> 18, m = e & 0x3FFFFu, h = m & 1u;
         const unsigned long long v = L.ring[p * 16 + h * 8 + r];
-        __builtin_nontemporal_store(v, region0 + ((size_t)p * a.nblk) * C + (size_t)m * 8 + r);
+        if (DBG == 0 || a.debug != 2) __builtin_nontemporal_store(v, region0 + ((size_t)p * a.nblk) * C + (size_t)m * 8 + r);
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
         if (r == 0) __hip_atomic_fetch_add(L.meta + p, 1ull << (32 + 16 * h), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
@@ -100,10 +101,12 @@ __device__ __forceinline__ void ring_flush(const RingArgs &a, const RingLds &L, 
   }
 }
 
-// Sink of a lane's 16 records (act: bit j = record j is live), in two batches of 8 claims.
+// Sink of a lane's 16 records (act: bit j = record j is live), in two batches of 8 claims. DBG = 1: the instrumented
+// instance (debug.ring modes and the wait counters), never the production one.
+template <int DBG>
 __device__ __forceinline__ void ring_sink(const RingArgs &a, const RingLds &L, uint32_t *fl, uint32_t act,
                                           const unsigned long long (&rec)[16], unsigned long long *region0, uint32_t C,
-                                          int lane, uint32_t &over) {
+                                          int lane, uint32_t &over, uint32_t &waits, uint32_t &sleeps) {
   uint32_t pos[16];
   uint32_t todo = 0, pend = 0;
   // claims: one 64-bit LDS add returns the claim index and both halves' flushed-lap counts
@@ -129,6 +132,8 @@ __device__ __forceinline__ void ring_sink(const RingArgs &a, const RingLds &L, u
       else pend |= 1u << (j0 + j);
     }
   }
+  if (DBG && a.debug == 3) return;  // claims only
+  if (DBG && __any(pend != 0)) waits++;
   // records whose slot still holds the previous lap (its half not yet moved out) wait for the bump and go in a later
   // round; every wave moves out what it completed before it waits, so the half it waits for always drains
   uint32_t spins = 0;
@@ -145,13 +150,14 @@ __device__ __forceinline__ void ring_sink(const RingArgs &a, const RingLds &L, u
                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         comp |= ((w & 7u) == 7u) ? (1u << j) : 0u;
       }
-    ring_flush(a, L, fl, comp, pos, rec, region0, C, lane);
+    ring_flush<DBG>(a, L, fl, comp, pos, rec, region0, C, lane);
     if (!__any(pend != 0)) break;  // uniform
     if (++spins > (1u << 22)) {  // bounded: a protocol fault ends the launch with a status, never a hang
       over |= 2u;
       break;
     }
     __builtin_amdgcn_s_sleep(2);
+    if (DBG) sleeps++;
     todo = 0;
     for (uint32_t x = pend; x; x &= x - 1u) {
       const int j = __builtin_ctz(x);
@@ -268,6 +274,7 @@ __device__ __forceinline__ int64_t ring_qi(const RingArgs &a, const RingCursor &
   return ch * 256 + 64 * cu.q + lane;
 }
 
+template <int DBG>
 __global__ __launch_bounds__(kRingBlock) void k_group_ring(RingArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -293,7 +300,7 @@ __global__ __launch_bounds__(kRingBlock) void k_group_ring(RingArgs a) {
   unsigned long long *region0 = a.records + (size_t)b * C;  // region (p, b) at ((p * nblk + b) * C)
   uint32_t *fl = L.flist + wave * 64;
   const int64_t c0 = a.total_chunks * b / a.nblk, c1 = a.total_chunks * (b + 1) / a.nblk;
-  uint32_t over = 0;
+  uint32_t over = 0, waits = 0, sleeps = 0;
   RingCursor cu;
   cu.cn = c0 + wave;
   cu.wn = ring_word(a, cu.cn, c1, lane);
@@ -355,8 +362,17 @@ __global__ __launch_bounds__(kRingBlock) void k_group_ring(RingArgs a) {
       for (int c = 0; c < kGroupPfCols; c++)
         if (k.bits[c]) load_raw_lq(k.fwd[c], k.bits[c], qi, R[c]);
     }
-    ring_sink(a, L, fl, act, rec, region0, C, lane, over);
+    if (DBG && a.debug == 1) {  // decode only: keep the records alive without the sink
+      unsigned long long x = 0;
+#pragma unroll
+      for (int j = 0; j < 16; j++) x ^= ((act >> j) & 1u) ? rec[j] : 0ull;
+      if (x == 0x0123456789ABCDEFull) over |= 8u;
+      continue;
+    }
+    ring_sink<DBG>(a, L, fl, act, rec, region0, C, lane, over, waits, sleeps);
   }
+  if (DBG && lane == 0 && waits) atomicAdd(a.status + 2, waits);
+  if (DBG && lane == 0 && sleeps) atomicAdd(a.status + 3, sleeps);
   __syncthreads();
   // every complete half is out; the partial last half of each partition and the region's record count remain
   for (int p = tid; p < a.P; p += kRingBlock) {
@@ -622,7 +638,8 @@ size_t ring_lds_bytes(int P) { return (size_t)P * (16 * 8 + 8 + 8) + (size_t)kRi
 
 void launch_group_ring(const RingArgs &a, hipStream_t stream) {
   if (a.nblk <= 0 || a.total_chunks <= 0) return;
-  hipLaunchKernelGGL(k_group_ring, dim3((unsigned)a.nblk), dim3(kRingBlock), ring_lds_bytes(a.P), stream, a);
+  if (a.debug) hipLaunchKernelGGL(k_group_ring<1>, dim3((unsigned)a.nblk), dim3(kRingBlock), ring_lds_bytes(a.P), stream, a);
+  else hipLaunchKernelGGL(k_group_ring<0>, dim3((unsigned)a.nblk), dim3(kRingBlock), ring_lds_bytes(a.P), stream, a);
 }
 
 void launch_ring_reduce(const RingReduceArgs &a, hipStream_t stream) {

@@ -3697,13 +3697,14 @@ std::unique_ptr<GroupByResult> exec_group_by_mv(Engine &e, const std::vector<Seg
     accs[a] = p;
     p += ks.G * ga.acc_bytes_per_key[a];
   }
-  if (mp) {  // partial: the server's arrays (HLL registers accumulate as u32 here, narrowed into its u8 layout)
+  if (mp && mp->accs) {  // partial: the server's arrays (HLL registers accumulate as u32 here, narrowed into its u8
+                         // layout); the admission export (no arrays) keeps the scratch ones
     counts = reinterpret_cast<unsigned long long *>(mp->counts);
     for (int a = 0; a < nb; a++)
       if (ga.acc_kind[a] != 5 && ga.acc_kind[a] != 4) accs[a] = mp->accs[a];
   }
   PINOT_HIP(hipEventRecord(e.ev_start, e.stream));
-  if (!(mp && mp->aio && mp->aio->mode == 1)) init_accs(e, ks.G, counts, ga, accs.data());  // (export: no arrays)
+  if (!(mp && !mp->accs)) init_accs(e, ks.G, counts, ga, accs.data());  // (the admission export: no arrays)
   Timer t(e);
   std::vector<DeviceBuffer> remaps(S * q.num_group_by);
   std::vector<int64_t> seg_counts(S, 0);

@@ -810,8 +810,7 @@ pinot_status pinot_gpu_engine_stat(pinot_engine *engine, const char *name, int64
     const std::string n = name;
     if (n == "group.ring_queries") *value = engine->ring_queries;
     else if (n == "group.ring_fallbacks") *value = engine->ring_fallbacks;
-    else if (n == "group.ring_waits") *value = engine->ring_waits;
-    else if (n == "group.ring_sleeps") *value = engine->ring_sleeps;
+    else if (n == "group.ring_direct") *value = engine->ring_direct;
     else if (n == "exec.last_pre_segments") *value = engine->last_pre_segments;
     else require(false, PINOT_ERR_BAD_ARG, "unknown engine stat");
   });

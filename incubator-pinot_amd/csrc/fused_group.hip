@@ -922,13 +922,13 @@ __device__ __forceinline__ void group_chunk_lq(const GroupArgs &a, const GroupSe
 // LDS accumulator identities (GB_LDS): counts 0, sums 0, min all-ones, max 0, HLL 0.
 __device__ __forceinline__ void init_group_lds(const GroupArgs &a, const GroupSegment &sg, uint8_t *acc_lds, int tid) {
   uint32_t *w = reinterpret_cast<uint32_t *>(acc_lds);
-  for (int i = tid; i < a.lds_acc_bytes / 4; i += kGroupBlock) w[i] = 0;
+  for (int i = tid; i < a.lds_acc_bytes / 4; i += (int)blockDim.x) w[i] = 0;
   __syncthreads();
   for (int g = 0; g < a.n_aggs; g++) {
     const GroupAggDev ag = load_const(a.aggs + sg.first_agg + g);
     if (ag.acc_kind == 2) {
       unsigned long long *m = reinterpret_cast<unsigned long long *>(acc_lds + ag.lds_off);
-      for (long long i = tid; i < a.G; i += kGroupBlock) m[i] = ~0ull;
+      for (long long i = tid; i < a.G; i += (long long)blockDim.x) m[i] = ~0ull;
     }
   }
   __syncthreads();
@@ -937,7 +937,7 @@ __device__ __forceinline__ void init_group_lds(const GroupArgs &a, const GroupSe
 __device__ __forceinline__ void flush_group_lds(const GroupArgs &a, const GroupSegment &sg, uint8_t *acc_lds, int tid) {
   __syncthreads();
   const uint32_t *cnt = reinterpret_cast<const uint32_t *>(acc_lds);
-  for (long long k = tid; k < a.G; k += kGroupBlock) {
+  for (long long k = tid; k < a.G; k += (long long)blockDim.x) {
     const uint32_t c = cnt[k];
     if (!c) continue;
     atomicAdd(a.counts + k, (unsigned long long)c);

@@ -3272,6 +3272,27 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
   const int64_t resident = (int64_t)group_query_blocks_per_cu(a) * e.num_cus;
   a.bps = (int)std::max<int64_t>(1, std::min<int64_t>(resident / (int64_t)S, (max_chunks + 15) / 16));
   const int64_t nblk = (int64_t)S * a.bps;
+  // GB_LDS on the lane-owns-quarter path: the count packed into an affine dictId sum when both fields fit 64 bits
+  // (a block's docs < 2^cbits; Σ dictId < 2^(bits + cbits))
+  a.lds_pack = -1;
+  if (gp.mode == GB_LDS && a.lw == 2 && a.pf_nc > 0 && !pin) {
+    const int64_t blk_docs = ((max_chunks + 16 * a.bps - 1) / (16 * a.bps)) * 16 * 4096;
+    const int cbits = 64 - __builtin_clzll((unsigned long long)blk_docs);
+    for (int c = q.num_group_by; c < a.pf_nc && a.lds_pack < 0; c++) {
+      const int i = a.pf_agg[c];
+      if (gx.acc_kind[i] != 0) continue;
+      bool affine = true;
+      int bits = 0;
+      for (size_t si = 0; si < S; si++) {
+        affine = affine && gaggs[si * na + i].affine;
+        bits = std::max(bits, gaggs[si * na + i].bits);
+      }
+      if (affine && bits + 2 * cbits <= 64) {
+        a.lds_pack = i;
+        a.lds_sbits = bits + cbits;
+      }
+    }
+  }
 
   const auto tgp = std::chrono::steady_clock::now();
   check_deadline(e, "planning");

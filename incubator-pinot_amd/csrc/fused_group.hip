@@ -781,8 +781,14 @@ __device__ __forceinline__ void lds_sink_col(const GroupArgs &a, const GroupSegm
     if (!k.bits[C] || k.fsh[C] < 0) return;
     const GroupAggDev ag = load_const(a.aggs + sg.first_agg + a.pf_agg[C]);
     uint8_t *acc = reinterpret_cast<uint8_t *>(plds) + ag.lds_off;
+    const bool pack = a.lds_pack == a.pf_agg[C];
     decode_raw_lq(R[C], k.bits[C], qi, [&](const uint32_t (&id)[16]) {
-      if (ag.acc_kind == 0 && ag.affine) {  // Σ dictId (converted at the flush)
+      if (pack) {  // count << sbits + Σ dictId in one 64-bit add
+#pragma unroll
+        for (int j = 0; j < 16; j++)
+          if ((act >> j) & 1u)
+            atomicAdd(reinterpret_cast<unsigned long long *>(acc) + key[j], (1ull << a.lds_sbits) + (unsigned long long)id[j]);
+      } else if (ag.acc_kind == 0 && ag.affine) {  // Σ dictId (converted at the flush)
 #pragma unroll
         for (int j = 0; j < 16; j++)
           if ((act >> j) & 1u) atomicAdd(reinterpret_cast<unsigned long long *>(acc) + key[j], (unsigned long long)id[j]);
@@ -828,9 +834,11 @@ __device__ __forceinline__ void lq_process(const GroupArgs &a, const GroupSegmen
       for (int j = 0; j < 16; j++)
         if (!((gload<uint32_t>(sg.admitted + (key[j] >> 5)) >> (key[j] & 31)) & 1u)) act &= ~(1u << j);
     }
+    if (a.lds_pack < 0) {
 #pragma unroll
-    for (int j = 0; j < 16; j++)
-      if ((act >> j) & 1u) atomicAdd(plds + key[j], 1u);
+      for (int j = 0; j < 16; j++)
+        if ((act >> j) & 1u) atomicAdd(plds + key[j], 1u);
+    }
     lds_sink_col<1, NC>(a, sg, k, R, qi, act, key, plds);
     lds_sink_col<2, NC>(a, sg, k, R, qi, act, key, plds);
     lds_sink_col<3, NC>(a, sg, k, R, qi, act, key, plds);
@@ -937,8 +945,12 @@ __device__ __forceinline__ void init_group_lds(const GroupArgs &a, const GroupSe
 __device__ __forceinline__ void flush_group_lds(const GroupArgs &a, const GroupSegment &sg, uint8_t *acc_lds, int tid) {
   __syncthreads();
   const uint32_t *cnt = reinterpret_cast<const uint32_t *>(acc_lds);
+  const unsigned long long *packed =
+      a.lds_pack >= 0 ? reinterpret_cast<const unsigned long long *>(acc_lds + load_const(a.aggs + sg.first_agg + a.lds_pack).lds_off)
+                      : nullptr;
+  const unsigned long long low = a.lds_pack >= 0 ? (1ull << a.lds_sbits) - 1ull : ~0ull;
   for (long long k = tid; k < a.G; k += (long long)blockDim.x) {
-    const uint32_t c = cnt[k];
+    const uint32_t c = packed ? (uint32_t)(packed[k] >> a.lds_sbits) : cnt[k];
     if (!c) continue;
     atomicAdd(a.counts + k, (unsigned long long)c);
     for (int g = 0; g < a.n_aggs; g++) {
@@ -947,6 +959,7 @@ __device__ __forceinline__ void flush_group_lds(const GroupArgs &a, const GroupS
       switch (ag.acc_kind) {
         case 0: {
           unsigned long long v = reinterpret_cast<const unsigned long long *>(src)[k];
+          if (g == a.lds_pack) v &= low;
           if (ag.affine) v = (unsigned long long)ag.affine_base * c + (unsigned long long)ag.affine_step * v;  // mod 2^64
           atomicAdd(static_cast<unsigned long long *>(ag.acc) + k, v);
           break;

@@ -336,6 +336,9 @@ struct GroupArgs {
   int32_t ring_blocks;
   int32_t reserved3;
   uint32_t *blk_matched;
+  // GB_LDS lane-owns-quarter: the doc count rides in the high bits of aggregation lds_pack's affine dictId sum
+  // ((1 << lds_sbits) + dictId per doc: one LDS atomic for both); -1 = separate u32 counts
+  int32_t lds_pack, lds_sbits;
 };
 constexpr int kGroupPfCols = 4;
 constexpr int kGroupLwMaxBits = 20;  // widest column the lane-owns-word decode handles

@@ -525,7 +525,8 @@ pinot_status pinot_gpu_synchronize(pinot_engine *engine);
 pinot_status pinot_gpu_last_kernel_ms(pinot_engine *engine, int32_t kind, double *ms, int64_t *launches);
 /* Engine counters (diagnostics, no Java counterpart): "group.ring_queries" = group-bys answered on the ring plan,
  * "group.ring_fallbacks" = ring-plan group-bys re-answered on the counted plan (a region overflowed: skewed keys),
- * "group.ring_direct" = records the ring sink wrote straight to their region (counted under debug.ring only),
+ * "group.ring_waits" / "group.ring_sleeps" = ring-sink rounds that waited for a ring half to drain / their spins
+ * (counted under debug.ring only),
  * "exec.last_pre_segments" = segments of the last fused query whose filter was built as a dense `pre` bitset by the
  * launch sequence instead of inside the fused kernel's register program. */
 pinot_status pinot_gpu_engine_stat(pinot_engine *engine, const char *name, int64_t *value);

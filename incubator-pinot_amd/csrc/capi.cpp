@@ -456,6 +456,7 @@ pinot_status group_by_call(pinot_engine *engine, const pinot_segment_handle *seg
     DeadlineScope ds(*engine, query->timeout_ms);
     const std::vector<SegmentData *> segs = resolve(*engine, segments, num_segments);
     const std::vector<SegmentData *> kept = prune_for_query(segs, *query);
+    const auto t1 = std::chrono::steady_clock::now();
     std::unique_ptr<GroupByResult> r;
     if (kept.empty()) {
       r = empty_group_result(*query);
@@ -474,9 +475,15 @@ pinot_status group_by_call(pinot_engine *engine, const pinot_segment_handle *seg
       if (query->pruners) stats->num_total_raw_docs = total_docs(segs);
       stats->host_ms = elapsed_ms(t0);
     }
+    const auto t2 = std::chrono::steady_clock::now();
     auto *res = new pinot_groupby_result();
     static_cast<GroupByResult &>(*res) = std::move(*r);
     *out = res;
+    if (engine->host_phases) {
+      auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+      fprintf(stderr, "[pinot_gpu] group-by C-ABI phases (us): resolve+prune %.1f, execute %.1f, result %.1f\n",
+              us(t0, t1), us(t1, t2), us(t2, std::chrono::steady_clock::now()));
+    }
   });
 }
 }  // namespace
@@ -810,7 +817,8 @@ pinot_status pinot_gpu_engine_stat(pinot_engine *engine, const char *name, int64
     const std::string n = name;
     if (n == "group.ring_queries") *value = engine->ring_queries;
     else if (n == "group.ring_fallbacks") *value = engine->ring_fallbacks;
-    else if (n == "group.ring_direct") *value = engine->ring_direct;
+    else if (n == "group.ring_waits") *value = engine->ring_waits;
+    else if (n == "group.ring_sleeps") *value = engine->ring_sleeps;
     else if (n == "exec.last_pre_segments") *value = engine->last_pre_segments;
     else require(false, PINOT_ERR_BAD_ARG, "unknown engine stat");
   });

@@ -8,6 +8,7 @@
 #include <new>
 #include <stdexcept>
 #include <string>
+#include <mutex>
 #include <vector>
 
 #include "pinot_gpu.h"
@@ -127,9 +128,42 @@ class MappedBuffer {
   size_t n_ = 0;
 };
 
-// Allocator of the large host result arrays: >= 1 MiB blocks are pinned (hipHostMalloc), so the device's final
-// per-group arrays are copied straight into them (no staging buffer, no host fill); smaller blocks — and any block
-// when pinning fails, e.g. without a GPU — come from malloc. A 64-byte header records which.
+// Pinned host blocks are slow to get and to give back (hipHostMalloc / hipHostFree: milliseconds for the result
+// arrays of a 1M-group query, and the free waits for the device), so freed blocks are kept for reuse: one free list
+// per power-of-two size class, at most kPinnedCacheBytes held in all.
+struct PinnedCache {
+  static constexpr size_t kPinnedCacheBytes = size_t(4) << 30;
+  std::mutex mu;
+  std::vector<void *> lists[64];
+  size_t held = 0;
+  static PinnedCache &get() {
+    static PinnedCache *c = new PinnedCache();  // never destroyed: blocks may be returned during static teardown
+    return *c;
+  }
+  static int size_class(size_t bytes) { return 64 - __builtin_clzll((unsigned long long)(bytes - 1)); }
+  void *take(size_t bytes) {  // a block of 2^size_class(bytes) bytes, or nullptr
+    std::lock_guard<std::mutex> lk(mu);
+    auto &l = lists[size_class(bytes)];
+    if (l.empty()) return nullptr;
+    void *p = l.back();
+    l.pop_back();
+    held -= size_t(1) << size_class(bytes);
+    return p;
+  }
+  bool give(void *p, size_t bytes) {
+    std::lock_guard<std::mutex> lk(mu);
+    const size_t sz = size_t(1) << size_class(bytes);
+    if (held + sz > kPinnedCacheBytes) return false;
+    lists[size_class(bytes)].push_back(p);
+    held += sz;
+    return true;
+  }
+};
+
+// Allocator of the large host result arrays: >= 1 MiB blocks are pinned (hipHostMalloc, rounded up to their size class
+// and cached by PinnedCache), so the device's final per-group arrays are copied straight into them (no staging
+// buffer, no host fill); smaller blocks — and any block when pinning fails, e.g. without a GPU — come from malloc. A
+// 64-byte header records which (and the pinned block's size).
 template <typename T>
 struct PinnedAllocator {
   using value_type = T;
@@ -137,23 +171,31 @@ struct PinnedAllocator {
   template <typename U>
   PinnedAllocator(const PinnedAllocator<U> &) {}
   T *allocate(size_t n) {
-    const size_t bytes = n * sizeof(T) + 64;
+    size_t bytes = n * sizeof(T) + 64;
     void *p = nullptr;
     uint32_t tag = 0;
-    if (bytes >= (1u << 20) && hipHostMalloc(&p, bytes, hipHostMallocDefault) == hipSuccess) tag = 1;
-    else {
+    if (bytes >= (1u << 20)) {
+      bytes = size_t(1) << PinnedCache::size_class(bytes);
+      p = PinnedCache::get().take(bytes);
+      if (p || hipHostMalloc(&p, bytes, hipHostMallocDefault) == hipSuccess) tag = 1;
+    }
+    if (!tag) {
       (void)hipGetLastError();
       p = std::malloc(bytes);
       if (!p) throw std::bad_alloc();
     }
-    *static_cast<uint32_t *>(p) = tag;
+    static_cast<uint32_t *>(p)[0] = tag;
+    reinterpret_cast<uint64_t *>(p)[1] = bytes;
     return reinterpret_cast<T *>(static_cast<uint8_t *>(p) + 64);
   }
   void deallocate(T *q, size_t) {
     if (!q) return;
     void *p = reinterpret_cast<uint8_t *>(q) - 64;
-    if (*static_cast<uint32_t *>(p) == 1) (void)hipHostFree(p);
-    else std::free(p);
+    if (static_cast<uint32_t *>(p)[0] == 1) {
+      if (!PinnedCache::get().give(p, reinterpret_cast<uint64_t *>(p)[1])) (void)hipHostFree(p);
+    } else {
+      std::free(p);
+    }
   }
   template <typename U>
   bool operator==(const PinnedAllocator<U> &) const { return true; }

@@ -264,7 +264,8 @@ struct Engine {
   int32_t trim_top_n = 0;      // per call (pinot_gpu_group_by_top): trim the group-by on the device for this TOP n
   int64_t ring_queries = 0;    // group-bys launched on the ring plan
   int64_t last_pre_segments = 0;  // segments of the last fused query whose filter needed a `pre` bitset (launch sequence)
-  int64_t ring_direct = 0;     // records k_group_ring wrote straight to their region (group.ring_direct; debug.ring)
+  int64_t ring_waits = 0;      // k_group_ring sink rounds that waited for a ring half to drain (group.ring_waits)
+  int64_t ring_sleeps = 0;     // ... and their s_sleep spins (group.ring_sleeps)
   int64_t ring_fallbacks = 0;  // ring-plan queries re-answered on the counted plan (a region overflowed: skewed keys)
   int num_cus = 256;          // multiProcessorCount of the device
 

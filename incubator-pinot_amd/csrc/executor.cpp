@@ -3011,7 +3011,7 @@ const long long *device_trim(Engine &e, const DenseGroups &d, const long long *k
   unsigned long long nu = 0;
   PINOT_HIP(hipMemcpyAsync(&nu, n_dev, 8, hipMemcpyDeviceToHost, e.stream));
   wait_stream(e);
-  std::vector<uint32_t> hf(nu);
+  HostVec<uint32_t> hf(nu);
   if (nu) PINOT_HIP(hipMemcpyAsync(hf.data(), uflags, nu * 4, hipMemcpyDeviceToHost, e.stream));
   wait_stream(e);
   kept.assign(na, {});
@@ -3505,7 +3505,8 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     if (ring_status) PINOT_HIP(hipMemcpyAsync(rs, ring_status, 16, hipMemcpyDeviceToHost, e.stream));
     PINOT_HIP(hipEventRecord(e.ev_stop, e.stream));
     wait_stream(e);
-    e.ring_direct += rs[2];
+    e.ring_waits += rs[2];
+    e.ring_sleeps += rs[3];
     if (rs[0]) return ring_fallback();
     float pms = 0;
     PINOT_HIP(hipEventElapsedTime(&pms, e.ev_start, e.ev_stop));
@@ -3529,7 +3530,8 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     if (ks.hashed) PINOT_HIP(hipMemcpyAsync(&verify_err, a.verify_err, 4, hipMemcpyDeviceToHost, e.stream));
     if (ring_status) PINOT_HIP(hipMemcpyAsync(rs, ring_status, 16, hipMemcpyDeviceToHost, e.stream));
   });
-  e.ring_direct += rs[2];
+  e.ring_waits += rs[2];
+  e.ring_sleeps += rs[3];
   if (rs[0]) return ring_fallback();
   if (verify_err) {  // 64-bit fingerprint collision: retry with another seed
     require(attempt < 3, PINOT_ERR_DEVICE, "group-key fingerprint collisions persist");
@@ -4073,8 +4075,12 @@ std::unique_ptr<GroupByResult> exec_group_by(Engine &e, const std::vector<Segmen
     if (r) return r;
   }
   if (e.use_fused) {
+    const auto t0 = std::chrono::steady_clock::now();
     KeySpace ks = build_key_space(segs, q);
     GroupAccs ga = group_acc_kinds(*segs[0], q);
+    if (e.host_phases)
+      fprintf(stderr, "[pinot_gpu] group-by key space (us): %.1f\n",
+              std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
     return exec_group_by_fused(e, segs, q, ks, ga, stats);
   }
   return exec_group_by_legacy(e, segs, q, stats);

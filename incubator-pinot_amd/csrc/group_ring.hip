@@ -6,10 +6,9 @@
 //                        group key and aggregated dictIds (lane-owns-quarter reads, the next quarter's loads in
 //                        flight while this one is sunk) into u64 records (local key | dictId fields | partition) and
 //                        appends them to its partition's LDS ring of 16 slots (two halves of 8). The lane whose
-//                        record completes a half moves it to the block's region of that partition as one aligned 64-B
+//                        write completes a half moves it to the block's region of that partition as one aligned 64-B
 //                        piece: region (p, block) holds records [0, n) in claim order, so every flush lands on its own
-//                        64-B sector and no histogram, scan or cursor leaves the CU. A record whose ring slot still
-//                        holds the previous lap goes straight to its region position instead (nobody waits).
+//                        64-B sector and no histogram, scan or cursor leaves the CU.
 //   k_ring_reduce        one block per partition of K <= 1024 consecutive keys: the partition's records from every
 //                        block's region folded into LDS accumulators (count packed beside the first affine dictId
 //                        SUM, int64 / double sums, ordered min / max, HLL registers as 4-bit nibbles with the rare
@@ -41,9 +40,7 @@ using namespace dev;
 
 constexpr int kRingBlock = 512;  // 8 waves: the 16-record sink and the next quarter's raw loads need the registers
 constexpr int kRingWaves = kRingBlock / 64;
-constexpr int kRecPShift = 53;  // records carry their partition in bits [53, 64); ring slots their lap's low bits
-constexpr unsigned long long kRecMask = (1ull << kRecPShift) - 1ull;
-constexpr uint32_t kLapMask = (1u << (64 - kRecPShift)) - 1u;
+constexpr int kRecPShift = 53;  // records carry their partition in bits [53, 64)
 
 struct RingLds {
   unsigned long long *ring;  // [P][16]
@@ -64,14 +61,13 @@ __device__ __forceinline__ RingLds ring_lds(uint8_t *lds, int P) {
 __device__ __forceinline__ uint32_t rec_part(unsigned long long r) { return (uint32_t)(r >> kRecPShift); }
 
 // Move the listed completed halves out: every lane that completed one lists (partition, half-lap) at its rank among
-// this round's flushing lanes, then the wave stores eight halves per instruction (8 lanes x 8 B each). A slot whose lap
-// tag is not the half's lap was written straight to the region by its record (the slot still held an older lap), so
-// its lane stores nothing. The laps-flushed bump follows the ring reads in this wave's LDS order, so a writer of the
-// next lap (which checks the bump at its claim) never overwrites a slot before it has been read.
+// this round's flushing lanes, then the wave stores eight halves per instruction (8 lanes x 8 B each). The laps-flushed
+// bump follows the ring reads in this wave's LDS order, so a writer of the next lap (which waits for the bump) never
+// overwrites a slot before it has been read.
 template <int DBG>
 __device__ __forceinline__ void ring_flush(const RingArgs &a, const RingLds &L, uint32_t *fl, uint32_t comp,
-                                          const uint32_t (&pos)[16], const unsigned long long (&rec)[16],
-                                          unsigned long long *region0, uint32_t C, int lane) {
+                                           const uint32_t (&pos)[16], const unsigned long long (&rec)[16],
+                                           unsigned long long *region0, uint32_t C, int lane) {
   while (true) {
     const uint64_t fm = __ballot(comp != 0);
     if (!fm) break;  // uniform
@@ -96,8 +92,7 @@ __device__ __forceinline__ void ring_flush(const RingArgs &a, const RingLds &L, 
         const uint32_t e = fl[f];
         const uint32_t p = e >> 18, m = e & 0x3FFFFu, h = m & 1u;
         const unsigned long long v = L.ring[p * 16 + h * 8 + r];
-        if ((uint32_t)(v >> kRecPShift) == ((m >> 1) & kLapMask) && (DBG == 0 || a.debug != 2))
-          __builtin_nontemporal_store(v & kRecMask, region0 + ((size_t)p * a.nblk) * C + (size_t)m * 8 + r);
+        if (DBG == 0 || a.debug != 2) __builtin_nontemporal_store(v, region0 + ((size_t)p * a.nblk) * C + (size_t)m * 8 + r);
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
         if (r == 0) __hip_atomic_fetch_add(L.meta + p, 1ull << (32 + 16 * h), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
@@ -106,17 +101,15 @@ __device__ __forceinline__ void ring_flush(const RingArgs &a, const RingLds &L, 
   }
 }
 
-// Sink of a lane's 16 records (act: bit j = record j is live), in two batches of 8 claims. A claim returns the
-// record's position in its partition's region and both ring halves' flushed-lap counts: a record whose slot has been
-// moved out for the previous lap goes into the ring (tagged with its lap), else straight to its region position (no
-// wait); either way it counts toward its half's completion, and the lane whose count completes a half flushes it.
-// DBG = 1: the instrumented instance (debug.ring modes and the direct-write counter), never the production one.
+// Sink of a lane's 16 records (act: bit j = record j is live), in two batches of 8 claims. DBG = 1: the instrumented
+// instance (debug.ring modes and the wait counters), never the production one.
 template <int DBG>
 __device__ __forceinline__ void ring_sink(const RingArgs &a, const RingLds &L, uint32_t *fl, uint32_t act,
                                           const unsigned long long (&rec)[16], unsigned long long *region0, uint32_t C,
-                                          int lane, uint32_t &over, uint32_t &direct) {
+                                          int lane, uint32_t &over, uint32_t &waits, uint32_t &sleeps) {
   uint32_t pos[16];
-  uint32_t ring = 0, live = 0;
+  uint32_t todo = 0, pend = 0;
+  // claims: one 64-bit LDS add returns the claim index and both halves' flushed-lap counts
 #pragma unroll
   for (int j0 = 0; j0 < 16; j0 += 8) {
     unsigned long long old[8];
@@ -133,35 +126,54 @@ __device__ __forceinline__ void ring_sink(const RingArgs &a, const RingLds &L, u
         over |= 1u;
         continue;
       }
-      live |= 1u << (j0 + j);
       const uint32_t h = (pos[j0 + j] >> 3) & 1u, lap = (pos[j0 + j] >> 4) & 0xFFFFu;
-      if (((uint32_t)(old[j] >> (32 + 16 * h)) & 0xFFFFu) == lap) ring |= 1u << (j0 + j);
+      const uint32_t flh = (uint32_t)(old[j] >> (32 + 16 * h)) & 0xFFFFu;
+      if (flh == lap) todo |= 1u << (j0 + j);
+      else pend |= 1u << (j0 + j);
     }
   }
   if (DBG && a.debug == 3) return;  // claims only
-  const size_t pstride = (size_t)a.nblk * C;
+  if (DBG && __any(pend != 0)) waits++;
+  // records whose slot still holds the previous lap (its half not yet moved out) wait for the bump and go in a later
+  // round; every wave moves out what it completed before it waits, so the half it waits for always drains
+  uint32_t spins = 0;
+  while (true) {
+    uint32_t comp = 0;
 #pragma unroll
-  for (int j = 0; j < 16; j++) {
-    if (!((live >> j) & 1u)) continue;
-    const uint32_t p = rec_part(rec[j]);
-    const unsigned long long r = rec[j] & kRecMask;
-    if ((ring >> j) & 1u) {
-      L.ring[p * 16 + (pos[j] & 15u)] = r | ((unsigned long long)((pos[j] >> 4) & kLapMask) << kRecPShift);
-    } else if (DBG == 0 || a.debug != 2) {
-      region0[p * pstride + pos[j]] = r;
+    for (int j = 0; j < 16; j++)
+      if ((todo >> j) & 1u) L.ring[rec_part(rec[j]) * 16 + (pos[j] & 15u)] = rec[j] & ((1ull << kRecPShift) - 1ull);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+#pragma unroll
+    for (int j = 0; j < 16; j++)
+      if ((todo >> j) & 1u) {
+        const uint32_t w = __hip_atomic_fetch_add(L.wr + rec_part(rec[j]) * 2 + ((pos[j] >> 3) & 1u), 1u,
+                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        comp |= ((w & 7u) == 7u) ? (1u << j) : 0u;
+      }
+    ring_flush<DBG>(a, L, fl, comp, pos, rec, region0, C, lane);
+    if (!__any(pend != 0)) break;  // uniform
+    if (++spins > (1u << 22)) {  // bounded: a protocol fault ends the launch with a status, never a hang
+      over |= 2u;
+      break;
     }
+    __builtin_amdgcn_s_sleep(2);
+    if (DBG) sleeps++;
+    todo = 0;
+    for (uint32_t x = pend; x; x &= x - 1u) {
+      const int j = __builtin_ctz(x);
+      uint32_t pj = 0, psj = 0;
+#pragma unroll
+      for (int t = 0; t < 16; t++)
+        if (t == j) {
+          pj = rec_part(rec[t]);
+          psj = pos[t];
+        }
+      const unsigned long long m = __hip_atomic_load(L.meta + pj, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      const uint32_t h = (psj >> 3) & 1u, lap = (psj >> 4) & 0xFFFFu;
+      if (((uint32_t)(m >> (32 + 16 * h)) & 0xFFFFu) == lap) todo |= 1u << j;
+    }
+    pend &= ~todo;
   }
-  if (DBG) direct += __popc(live & ~ring);
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);
-  uint32_t comp = 0;
-#pragma unroll
-  for (int j = 0; j < 16; j++)
-    if ((live >> j) & 1u) {
-      const uint32_t w = __hip_atomic_fetch_add(L.wr + rec_part(rec[j]) * 2 + ((pos[j] >> 3) & 1u), 1u,
-                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      comp |= ((w & 7u) == 7u) ? (1u << j) : 0u;
-    }
-  ring_flush<DBG>(a, L, fl, comp, pos, rec, region0, C, lane);
 }
 
 // Segment of global chunk c (the chunk windows of the segments, concatenated in order): uniform scalar scan.
@@ -288,7 +300,7 @@ __global__ __launch_bounds__(kRingBlock) void k_group_ring(RingArgs a) {
   unsigned long long *region0 = a.records + (size_t)b * C;  // region (p, b) at ((p * nblk + b) * C)
   uint32_t *fl = L.flist + wave * 64;
   const int64_t c0 = a.total_chunks * b / a.nblk, c1 = a.total_chunks * (b + 1) / a.nblk;
-  uint32_t over = 0, direct = 0;
+  uint32_t over = 0, waits = 0, sleeps = 0;
   RingCursor cu;
   cu.cn = c0 + wave;
   cu.wn = ring_word(a, cu.cn, c1, lane);
@@ -357,9 +369,10 @@ __global__ __launch_bounds__(kRingBlock) void k_group_ring(RingArgs a) {
       if (x == 0x0123456789ABCDEFull) over |= 8u;
       continue;
     }
-    ring_sink<DBG>(a, L, fl, act, rec, region0, C, lane, over, direct);
+    ring_sink<DBG>(a, L, fl, act, rec, region0, C, lane, over, waits, sleeps);
   }
-  if (DBG && direct) atomicAdd(a.status + 2, direct);
+  if (DBG && lane == 0 && waits) atomicAdd(a.status + 2, waits);
+  if (DBG && lane == 0 && sleeps) atomicAdd(a.status + 3, sleeps);
   __syncthreads();
   // every complete half is out; the partial last half of each partition and the region's record count remain
   for (int p = tid; p < a.P; p += kRingBlock) {
@@ -370,11 +383,8 @@ __global__ __launch_bounds__(kRingBlock) void k_group_ring(RingArgs a) {
       continue;
     }
     const uint32_t kk = n & 7u, h = (n >> 3) & 1u, m = n >> 3;
-    for (uint32_t r = 0; r < kk; r++) {  // slots of another lap were written straight to the region
-      const unsigned long long v = L.ring[p * 16 + h * 8 + r];
-      if ((uint32_t)(v >> kRecPShift) == ((m >> 1) & kLapMask))
-        region0[((size_t)p * a.nblk) * C + (size_t)m * 8 + r] = v & kRecMask;
-    }
+    for (uint32_t r = 0; r < kk; r++)
+      region0[((size_t)p * a.nblk) * C + (size_t)m * 8 + r] = L.ring[p * 16 + h * 8 + r];
   }
   if (over) atomicOr(a.status, over);
 }
@@ -542,59 +552,26 @@ __global__ __launch_bounds__(kRingReduceBlock) void k_ring_reduce(RingReduceArgs
   uint32_t status = 0;
   const unsigned long long *base = a.records + (size_t)p * a.nblk * C;
   constexpr int RB = kRingReduceRegions, U = kRingReduceUnroll, N = RB * U;
-  // steps (b0, r0): RB regions' records [r0, r0 + U * block) each; the next step's loads are issued before this step
-  // is folded (the fold is LDS work only: the loads' latency hides behind it)
-  auto hmax_of = [&](int b0) {
-    uint32_t h = 0;
+  for (int b0 = 0; b0 < a.nblk; b0 += RB) {
+    uint32_t hmax = 0;
 #pragma unroll
-    for (int r = 0; r < RB; r++) h = max(h, b0 + r < a.nblk ? hrow[b0 + r] : 0u);
-    return min(h, C);
-  };
-  auto load = [&](int b0, uint32_t r0, unsigned long long (&rec)[N], bool (&ok)[N]) {
+    for (int r = 0; r < RB; r++) hmax = max(hmax, b0 + r < a.nblk ? hrow[b0 + r] : 0u);
+    hmax = min(hmax, C);
+    for (uint32_t r0 = 0; r0 < hmax; r0 += (uint32_t)U * kRingReduceBlock) {
+      unsigned long long rec[N];
+      bool ok[N];
 #pragma unroll
-    for (int r = 0; r < RB; r++)
+      for (int r = 0; r < RB; r++)
 #pragma unroll
-      for (int u = 0; u < U; u++) {
-        const int bb = b0 + r;
-        const uint32_t i = r0 + (uint32_t)(u * kRingReduceBlock + tid);
-        const bool v = bb < a.nblk && i < min(hrow[bb < a.nblk ? bb : 0], C);
-        ok[r * U + u] = v;
-        rec[r * U + u] = v ? __builtin_nontemporal_load(base + (size_t)bb * C + i) : 0ull;
-      }
-  };
-  int b0 = 0;
-  uint32_t r0 = 0;
-  while (b0 < a.nblk && hmax_of(b0) == 0) b0 += RB;  // uniform
-  unsigned long long rec[N];
-  bool ok[N];
-  if (b0 < a.nblk) load(b0, 0, rec, ok);
-  while (b0 < a.nblk) {  // uniform
-    int nb = b0;
-    uint32_t nr = r0 + (uint32_t)U * kRingReduceBlock;
-    if (nr >= hmax_of(b0)) {
-      nb = b0 + RB;
-      nr = 0;
-      while (nb < a.nblk && hmax_of(nb) == 0) nb += RB;
+        for (int u = 0; u < U; u++) {
+          const int bb = b0 + r;
+          const uint32_t i = r0 + (uint32_t)(u * kRingReduceBlock + tid);
+          const bool v = bb < a.nblk && i < min(hrow[bb < a.nblk ? bb : 0], C);
+          ok[r * U + u] = v;
+          rec[r * U + u] = v ? __builtin_nontemporal_load(base + (size_t)bb * C + i) : 0ull;
+        }
+      ring_fold<N>(a, lds, cnt, exc_n, exc, rec, ok, pk, sbits, status);
     }
-    unsigned long long rn[N];
-    bool on[N];
-    if (nb < a.nblk) {
-      load(nb, nr, rn, on);
-    } else {
-#pragma unroll
-      for (int i = 0; i < N; i++) {
-        rn[i] = 0;
-        on[i] = false;
-      }
-    }
-    ring_fold<N>(a, lds, cnt, exc_n, exc, rec, ok, pk, sbits, status);
-#pragma unroll
-    for (int i = 0; i < N; i++) {
-      rec[i] = rn[i];
-      ok[i] = on[i];
-    }
-    b0 = nb;
-    r0 = nr;
   }
   __syncthreads();
   const long long kbase = (long long)p * K;

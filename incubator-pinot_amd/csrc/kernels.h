@@ -375,13 +375,13 @@ struct RingArgs {
   int32_t pf_agg[4];
   int32_t shift, nblk;            // nblk: blocks of the launch (one per CU): block b owns chunks [T b / nblk, T (b+1) / nblk)
   uint32_t cap;                   // records per region the allocation holds
-  int32_t debug;                  // debug.ring: the instrumented instance (direct counter); 1 decode without the sink,
+  int32_t debug;                  // debug.ring: the instrumented instance (wait counters); 1 decode without the sink,
                                   // 2 sink without the HBM stores, 3 claims only (timing only, wrong results), 4 as 0
   const uint32_t *blk_matched;    // [nblk] matching docs per block (GB_FILTER)
   unsigned long long *records;    // [P][nblk][C] (local key | dictId fields)
   uint32_t *hist;                 // [P][nblk] records claimed per region (> C: overflow)
   uint32_t *status;               // |= 1 a region overflowed, 2 a spin bound was hit, 4 HLL exception list full;
-                                  // status[2]: records written straight to their region (instrumented instance)
+                                  // status[2]: sink rounds that waited for a half to drain, status[3]: s_sleep spins
   uint32_t *region;               // C, written by block 0 (read by k_ring_reduce)
 };
 struct RingReduceArgs {

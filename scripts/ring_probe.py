@@ -2,7 +2,7 @@
 """Config-4 ring-plan probe (timing experiments, run under rocprofv3 --kernel-trace): the full-size config-4 group-by
 on the engine with each debug.ring mode in turn, R queries per mode, in this order:
 
-    0 production  |  4 instrumented (direct-write counter)  |  1 decode only  |  2 sink without HBM stores  |  3 claims only
+    0 production  |  4 instrumented (wait counters)  |  1 decode only  |  2 sink without HBM stores  |  3 claims only
 
 Modes 1-3 give wrong results (timing only). Prints one JSON line per mode: the engine's HIP-event time of the timed
 group-by region (filter + ring + reduce) per query and the ring-sink wait counters; the per-kernel split comes from
@@ -35,7 +35,7 @@ ex = ServerQueryExecutor(e, num_groups_limit=1_000_000)
 q = ex.prepare(args.query)
 for mode in [int(m) for m in args.modes.split(",")]:
     e.set_config("debug.ring=%d;timing=1" % mode)
-    d0 = e.stat("group.ring_direct")
+    w0, s0 = e.stat("group.ring_waits"), e.stat("group.ring_sleeps")
     ms = []
     t0 = time.time()
     for _ in range(args.reps):
@@ -44,6 +44,7 @@ for mode in [int(m) for m in args.modes.split(",")]:
         del res
     print(json.dumps({"debug_ring": mode, "region_ms": ms, "wall_s": time.time() - t0,
                       "ring_queries": e.stat("group.ring_queries"), "fallbacks": e.stat("group.ring_fallbacks"),
-                      "direct_per_query": (e.stat("group.ring_direct") - d0) / args.reps}), flush=True)
+                      "waits_per_query": (e.stat("group.ring_waits") - w0) / args.reps,
+                      "sleeps_per_query": (e.stat("group.ring_sleeps") - s0) / args.reps}), flush=True)
 e.set_config("debug.ring=0;timing=0")
 e.close()

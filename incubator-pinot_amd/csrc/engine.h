@@ -260,7 +260,8 @@ struct Engine {
   bool group_aligned = false; // group.aligned: bucketed EMIT runs padded to 64-B buckets (measured: EMIT -1.6%, reduce slower)
   int group_lw = 2;           // group.lw: partitioned plan reads 0 per doc, 1 each lane's 64-doc word, 2 contiguous quarters
   bool group_bucket = true;   // group.bucket: partitioned plan EMITs through LDS buckets into the final layout
-  bool group_ring = true;     // group.ring: large dense key spaces take the ring plan (no histogram pass; group_ring.hip)
+  bool group_ring = false;    // group.ring: large dense key spaces take the ring plan (no histogram pass; group_ring.hip;
+                              // measured 0.1-1 ms slower than the counted plan at config 4, so off by default)
   int32_t trim_top_n = 0;      // per call (pinot_gpu_group_by_top): trim the group-by on the device for this TOP n
   int64_t ring_queries = 0;    // group-bys launched on the ring plan
   int64_t last_pre_segments = 0;  // segments of the last fused query whose filter needed a `pre` bitset (launch sequence)

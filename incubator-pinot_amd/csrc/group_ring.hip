@@ -176,9 +176,10 @@ __device__ __forceinline__ void ring_sink(const RingArgs &a, const RingLds &L, u
   }
 }
 
-// Segment of global chunk c (the chunk windows of the segments, concatenated in order): uniform scalar scan.
-__device__ __forceinline__ int ring_segment(const RingArgs &a, int64_t c) {
-  int g = 0;
+// Segment of global chunk c (the chunk windows of the segments, concatenated in order): uniform scalar scan forward
+// from g0, a segment at or before c's (a wave's chunks ascend, so the scan usually stops at once).
+__device__ __forceinline__ int ring_segment(const RingArgs &a, int64_t c, int g0 = 0) {
+  int g = g0;
   while (g + 1 < a.nsegs && load_const(a.cstart + g + 1) <= c) g++;
   return g;
 }
@@ -190,11 +191,12 @@ struct RingCursor {
   uint64_t wn;    // ... of chunk cn (prefetched)
   int q;          // quarter of c
   uint32_t m;     // this lane's 16 filter bits of quarter q
+  int gn;         // segment of chunk cn (a wave's chunks ascend)
 };
 
-__device__ __forceinline__ uint64_t ring_word(const RingArgs &a, int64_t c, int64_t end, int lane) {
+__device__ __forceinline__ uint64_t ring_word(const RingArgs &a, int64_t c, int64_t end, int lane, int &gs) {
   if (c >= end) return 0ull;
-  const int g = ring_segment(a, c);
+  const int g = gs = ring_segment(a, c, gs);
   const GroupSegment sg = load_const(a.segs + g);
   const int64_t ch = sg.ch_begin + (c - load_const(a.cstart + g));
   const int64_t w = ch * 64 + lane;
@@ -217,7 +219,7 @@ __device__ __forceinline__ void ring_advance(const RingArgs &a, RingCursor &cu, 
       cu.c = cu.cn;
       cu.wc = cu.wn;
       cu.cn += kRingWaves;
-      cu.wn = ring_word(a, cu.cn, end, lane);
+      cu.wn = ring_word(a, cu.cn, end, lane, cu.gn);
       cu.q = 0;
       if (cu.c >= end) return;
       if (!__any(cu.wc != 0)) {  // uniform: nothing in this chunk
@@ -268,7 +270,7 @@ __device__ __forceinline__ RingColsDev ring_cols(const RingArgs &a, int g) {
 }
 
 __device__ __forceinline__ int64_t ring_qi(const RingArgs &a, const RingCursor &cu, int lane, int &g) {
-  g = ring_segment(a, cu.c);
+  g = ring_segment(a, cu.c, g);
   const GroupSegment sg = load_const(a.segs + g);
   const int64_t ch = sg.ch_begin + (cu.c - load_const(a.cstart + g));
   return ch * 256 + 64 * cu.q + lane;
@@ -303,7 +305,8 @@ __global__ __launch_bounds__(kRingBlock) void k_group_ring(RingArgs a) {
   uint32_t over = 0, waits = 0, sleeps = 0;
   RingCursor cu;
   cu.cn = c0 + wave;
-  cu.wn = ring_word(a, cu.cn, c1, lane);
+  cu.gn = 0;
+  cu.wn = ring_word(a, cu.cn, c1, lane, cu.gn);
   cu.q = 3;
   cu.c = -1;
   ring_advance(a, cu, c1, lane);
@@ -356,8 +359,9 @@ __global__ __launch_bounds__(kRingBlock) void k_group_ring(RingArgs a) {
     // the next quarter's loads go out before this one is sunk (the sink issues LDS work and 64-B stores only)
     ring_advance(a, cu, c1, lane);
     if (cu.c < c1) {
+      const int gp = g;
       qi = ring_qi(a, cu, lane, g);
-      k = ring_cols(a, g);
+      if (g != gp) k = ring_cols(a, g);  // uniform: the column descriptors change with the segment only
 #pragma unroll
       for (int c = 0; c < kGroupPfCols; c++)
         if (k.bits[c]) load_raw_lq(k.fwd[c], k.bits[c], qi, R[c]);

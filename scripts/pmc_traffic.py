@@ -18,8 +18,10 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from bench import kernel_source_hash  # noqa: E402
 
 PIPELINE = {"config2": ("k_scan_query",),
-            "config4": ("k_group_query", "k_pad_counts", "k_partition_starts", "k_partition_split", "k_partition_reduce")}
-NAME = {"config2": "k_scan_query", "config4": "group_by_pipeline"}
+            "config4": ("k_group_query", "k_pad_counts", "k_partition_starts", "k_partition_split", "k_partition_reduce",
+                        "k_group_ring", "k_ring_reduce"),
+            "lds": ("k_group_query",)}
+NAME = {"config2": "k_scan_query", "config4": "group_by_pipeline", "lds": "k_group_query_lds"}
 
 
 def per_kernel(db, counter):

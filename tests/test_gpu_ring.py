@@ -59,7 +59,7 @@ def _run(e, q, gsegs, host, limit=1 << 22):
 def test_ring_config4_shape():
     """Config 4's query and table at 2 x 2M docs: 1M keys in 977 partitions of 1024, SUM / AVG over the 20-bit d8
     (count packed beside the dictId sum), HLL over the 16-bit d5 (~120 ranks > 15 across the groups)."""
-    e = GpuEngine(0)
+    e = GpuEngine(0, "group.ring=1")
     gsegs = [e.register_synthetic("fact_%d" % s, 2_000_000, CONFIG_COLUMNS, BASE_SEED + s) for s in range(2)]
     host = [synth.make_segment("fact_%d" % s, 2_000_000, CONFIG_COLUMNS, BASE_SEED + s) for s in range(2)]
     ran, fell = _run(e, compile_pql(CONFIG4), gsegs, host, limit=1_000_000)
@@ -110,7 +110,7 @@ def test_ring_remap_ragged_kinds(text):
     segs = [_mixed_segment("r0", 70_001, 1, np.arange(0, 90), np.arange(0, 80)),
             _mixed_segment("r1", 33_333, 2, np.arange(20, 120), np.arange(10, 95)),
             _mixed_segment("r2", 120_017, 3, np.arange(5, 100), np.arange(0, 90))]
-    e = GpuEngine(0, "group.mode=partition")
+    e = GpuEngine(0, "group.mode=partition;group.ring=1")
     gsegs = [e.register(s) for s in segs]
     ran, fell = _run(e, compile_pql(text), gsegs, segs)
     assert (ran, fell) == (1, 0)
@@ -122,7 +122,7 @@ def test_ring_sorted_window_busiest_block():
     ranges, so the regions are sized from the busiest block's matches (blk_matched), not the average."""
     segs = [_mixed_segment("w0", 400_000, 11, np.arange(0, 100), np.arange(0, 100), sorted_ts=True),
             _mixed_segment("w1", 250_000, 12, np.arange(0, 100), np.arange(0, 100), sorted_ts=True)]
-    e = GpuEngine(0, "group.mode=partition")
+    e = GpuEngine(0, "group.mode=partition;group.ring=1")
     gsegs = [e.register(s) for s in segs]
     q = compile_pql("SELECT SUM(lv), MAX(dv) FROM t WHERE ts BETWEEN 40 AND 90 AND f < 95 GROUP BY k1, k2")
     ran, fell = _run(e, q, gsegs, segs)
@@ -140,7 +140,7 @@ def test_ring_skewed_keys_fall_back():
     seg = build_segment("skew", {"k1": ("INT", k1.tolist()), "k2": ("INT", k2.tolist()),
                                  "x": ("INT", rng.integers(0, 1000, n).tolist()),
                                  "f": ("INT", rng.integers(0, 10, n).tolist())})
-    e = GpuEngine(0, "group.mode=partition")
+    e = GpuEngine(0, "group.mode=partition;group.ring=1")
     g = e.register(seg)
     q = compile_pql("SELECT SUM(x), MAX(x) FROM t WHERE f < 8 GROUP BY k1, k2")
     ran, fell = _run(e, q, [g], [seg])

@@ -10,7 +10,7 @@ mkdir -p $out
 export TMPDIR=/tmp
 for wl in $wls; do
   for c in FETCH_SIZE WRITE_SIZE; do
-    timeout -s KILL 150 rocprofv3 --pmc $c -d $out/pmc_${wl}_$c -o run -- python3 bench.py --workload $wl --steps 3 --warmup 1 \
+    timeout -s KILL 150 rocprofv3 --pmc $c -d $out/pmc_${wl}_$c -o run -- python3 bench.py --workload $wl --steps 3 --warmup 1 --no-config4 --no-lds \
       --no-cpu-baseline --no-verify > $out/pmc_${wl}_$c.log 2>&1 || { tail -20 $out/pmc_${wl}_$c.log; exit 1; }
   done
   python3 scripts/pmc_traffic.py $wl $out/pmc_${wl}_FETCH_SIZE/run_results.db $out/pmc_${wl}_WRITE_SIZE/run_results.db \

@@ -13,6 +13,7 @@
 // dictionary sections are byte-identical to the reference's. The group-by result maps are written in ascending raw
 // key order: the reference's map is a ConcurrentHashMap filled by concurrent segment threads, whose order is not
 // deterministic either; the broker reads it back into a HashMap (order-free).
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <string>
@@ -26,21 +27,33 @@ namespace {
 class Out {
  public:
   std::vector<uint8_t> b;
+  uint8_t *grow(size_t n) {  // n more bytes at the end (amortised doubling)
+    const size_t at = b.size();
+    if (at + n > b.capacity()) b.reserve(std::max<size_t>(2 * b.capacity(), at + n + 4096));
+    b.resize(at + n);
+    return b.data() + at;
+  }
   void i32(int32_t v) {
     const uint32_t u = (uint32_t)v;
-    const uint8_t x[4] = {(uint8_t)(u >> 24), (uint8_t)(u >> 16), (uint8_t)(u >> 8), (uint8_t)u};
-    b.insert(b.end(), x, x + 4);
+    uint8_t *x = grow(4);
+    x[0] = (uint8_t)(u >> 24);
+    x[1] = (uint8_t)(u >> 16);
+    x[2] = (uint8_t)(u >> 8);
+    x[3] = (uint8_t)u;
   }
   void i64(int64_t v) {
-    i32((int32_t)((uint64_t)v >> 32));
-    i32((int32_t)(uint64_t)v);
+    const uint64_t u = (uint64_t)v;
+    uint8_t *x = grow(8);
+    for (int i = 0; i < 8; i++) x[i] = (uint8_t)(u >> (56 - 8 * i));
   }
   void f64(double d) {  // Double.doubleToRawLongBits
     int64_t v;
     memcpy(&v, &d, 8);
     i64(v);
   }
-  void bytes(const void *p, size_t n) { b.insert(b.end(), (const uint8_t *)p, (const uint8_t *)p + n); }
+  void bytes(const void *p, size_t n) {
+    if (n) memcpy(grow(n), p, n);
+  }
   void str(const std::string &s) {  // int length + UTF-8 bytes (StringUtil.encodeUtf8)
     i32((int32_t)s.size());
     bytes(s.data(), s.size());
@@ -125,9 +138,15 @@ void hll_bytes(Out &o, const uint8_t *regs) {
   constexpr int kWords = 43;  // getSizeForCount(256): 256 / 6 = 42, not a multiple of 32 -> 43
   uint32_t m[kWords] = {};
   for (int p = 0; p < 256; p++) m[p / 6] |= (uint32_t)(regs[p] & 0x1F) << (5 * (p % 6));
-  o.i32(8);
-  o.i32(kWords * 4);
-  for (int w = 0; w < kWords; w++) o.i32((int32_t)m[w]);
+  uint8_t *x = o.grow(8 + 4 * kWords);
+  const uint32_t head[2] = {8u, (uint32_t)(kWords * 4)};
+  for (int w = 0; w < 2 + kWords; w++) {
+    const uint32_t u = w < 2 ? head[w] : m[w - 2];
+    x[4 * w] = (uint8_t)(u >> 24);
+    x[4 * w + 1] = (uint8_t)(u >> 16);
+    x[4 * w + 2] = (uint8_t)(u >> 8);
+    x[4 * w + 3] = (uint8_t)u;
+  }
 }
 
 // DataSchema.toBytes (pinot-common/.../utils/DataSchema.java:114-139): names, then type names.

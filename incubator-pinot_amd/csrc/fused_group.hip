@@ -990,8 +990,8 @@ __device__ __forceinline__ void flush_group_lds(const GroupArgs &a, const GroupS
 // 3 = lane-owns-quarter, contiguous across the wave (group_chunk_lq).
 // A block walks groups of kGroupWaves consecutive chunks with stride bps * kGroupWaves whatever its wave count,
 // so blocks of every BLK own the same chunks (the COUNT pass's per-block histograms stay valid for EMIT).
-template <int MODE, int PATH = 0, int BLK = kGroupBlock>
-__global__ __launch_bounds__(BLK) void k_group_query(GroupArgs a) {
+template <int MODE, int PATH = 0, int BLK = kGroupBlock, int MINW = 1>  // MINW: minimum waves per SIMD
+__global__ __launch_bounds__(BLK, MINW) void k_group_query(GroupArgs a) {
   constexpr int NW = BLK / 64;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1107,7 +1107,7 @@ static void with_group_kernel(const GroupArgs &a, V &&v) {
   switch (a.mode) {
     case GB_GLOBAL: v(&k_group_query<GB_GLOBAL, 0, kGroupBlock>, kGroupBlock); break;
     case GB_LDS:
-      if (lh) v(&k_group_query<GB_LDS, 3, kGroupLwEmitBlock>, kGroupLwEmitBlock);
+      if (lh) v(&k_group_query<GB_LDS, 3, kGroupLwEmitBlock, 4>, kGroupLwEmitBlock);  // 4 waves per SIMD: 2 blocks per CU
       else v(&k_group_query<GB_LDS, 0, kGroupBlock>, kGroupBlock);
       break;
     case GB_COUNT:

@@ -339,7 +339,8 @@ std::vector<uint8_t> group_by_datatable(const pinot_query &q, const GroupByResul
   }
   t.dictionaries.emplace_back("functionName", fn_names);
   // CombineGroupByOperator.java:212-214: the merged map reached the inner-segment groups limit
-  attach_metadata(t, s, n >= (int64_t)q.num_groups_limit && q.num_groups_limit > 0, srv);
+  const int64_t merged = r.merged_groups >= 0 ? r.merged_groups : n;  // the device trim keeps fewer than it merged
+  attach_metadata(t, s, merged >= (int64_t)q.num_groups_limit && q.num_groups_limit > 0, srv);
   return table_bytes(t);
 }
 

@@ -386,6 +386,7 @@ struct GroupByResult {
   // trimmed on the device (pinot_gpu_group_by_top): the result holds the union of the functions' trimmed maps and
   // fn_kept[fn] lists fn's groups; 0 = not trimmed (every group)
   int32_t trimmed_top_n = 0;
+  int64_t merged_groups = -1;  // groups of the merged map before a device trim (-1: raw_keys.size())
   std::vector<std::vector<int64_t>> fn_kept;
   // DISTINCTCOUNTHLL: cardinalities per fn; registers on the host (hll[fn]) or on the device in parts (one per
   // GPU that finalized a key range: [groups][256] u8 at off[fn], copied on request)

@@ -3544,6 +3544,7 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
   const long long *rkeys = keys_dev;
   if (e.trim_top_n > 0) rkeys = device_trim(e, dg, keys_dev, nres, e.trim_top_n, kept);
   auto res = build_dense_result(e, dg, rkeys, nres);
+  res->merged_groups = (int64_t)n;  // before the trim: CombineGroupByOperator's numGroupsLimitReached test
   if (!kept.empty()) {
     res->trimmed_top_n = e.trim_top_n;
     res->fn_kept = std::move(kept);

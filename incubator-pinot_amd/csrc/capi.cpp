@@ -152,7 +152,10 @@ void parse_config(Engine &e, const char *cfg) {
     else if (k == "group.bucket") e.group_bucket = v == "1" || v == "true";
     else if (k == "group.ring") e.group_ring = v == "1" || v == "true";
     else if (k == "group.aligned") e.group_aligned = v == "1" || v == "true";
-    else if (k == "group.emit_block") {
+    else if (k == "group.lds_block") {
+      e.group_lds_block = std::stoi(v);
+      require(e.group_lds_block == 256 || e.group_lds_block == 512, PINOT_ERR_BAD_ARG, "group.lds_block: 256 | 512");
+    } else if (k == "group.emit_block") {
       e.group_emit_block = std::stoi(v);
       require(e.group_emit_block == 512 || e.group_emit_block == 1024, PINOT_ERR_BAD_ARG, "group.emit_block: 512 | 1024");
     }

@@ -136,8 +136,14 @@ enum ObjType : int32_t { OBJ_STRING = 0, OBJ_LONG = 1, OBJ_DOUBLE = 2, OBJ_AVG_P
 // int words, register p in word p / 6 at bit 5 * (p % 6) (RegisterSet.set; LOG2_BITS_PER_WORD 6, REGISTER_SIZE 5).
 void hll_bytes(Out &o, const uint8_t *regs) {
   constexpr int kWords = 43;  // getSizeForCount(256): 256 / 6 = 42, not a multiple of 32 -> 43
-  uint32_t m[kWords] = {};
-  for (int p = 0; p < 256; p++) m[p / 6] |= (uint32_t)(regs[p] & 0x1F) << (5 * (p % 6));
+  uint32_t m[kWords];
+  for (int w = 0; w < 42; w++) {  // six 5-bit registers per word, no division in the loop
+    const uint8_t *r = regs + 6 * w;
+    m[w] = (uint32_t)(r[0] & 0x1F) | (uint32_t)(r[1] & 0x1F) << 5 | (uint32_t)(r[2] & 0x1F) << 10 |
+           (uint32_t)(r[3] & 0x1F) << 15 | (uint32_t)(r[4] & 0x1F) << 20 | (uint32_t)(r[5] & 0x1F) << 25;
+  }
+  m[42] = (uint32_t)(regs[252] & 0x1F) | (uint32_t)(regs[253] & 0x1F) << 5 | (uint32_t)(regs[254] & 0x1F) << 10 |
+          (uint32_t)(regs[255] & 0x1F) << 15;
   uint8_t *x = o.grow(8 + 4 * kWords);
   const uint32_t head[2] = {8u, (uint32_t)(kWords * 4)};
   for (int w = 0; w < 2 + kWords; w++) {
@@ -314,7 +320,7 @@ std::vector<uint8_t> group_by_datatable(const pinot_query &q, const GroupByResul
     const int f = sv_function(r.functions[i]);
     if (f == PINOT_AGG_DISTINCTCOUNTHLL) {
       regs.resize((size_t)n * 256);
-      group_by_hll_registers(r, i, regs.data());
+      group_by_hll_registers(r, i, regs.data(), true);
     }
     const HostVec<int64_t> &cnt = r.counts[r.counts_shared ? 0 : i];
     const HostVec<double> &val = r.values[i];

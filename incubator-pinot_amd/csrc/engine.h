@@ -257,6 +257,7 @@ struct Engine {
   int group_split = -1;       // group.split: log2 sub-partitions per emitted run (-1 auto, 0 single-level)
   bool use_shortcut_plans = true;  // plan.shortcut: metadata / dictionary plans for unfiltered COUNT / MIN / MAX
   int group_emit_block = 512;  // group.emit_block: 512 | 1024 threads per bucketed lane-owns-quarter EMIT block
+  int group_lds_block = 512;   // group.lds_block: 256 | 512 threads per lane-owns-quarter GB_LDS block
   bool group_aligned = false; // group.aligned: bucketed EMIT runs padded to 64-B buckets (measured: EMIT -1.6%, reduce slower)
   int group_lw = 2;           // group.lw: partitioned plan reads 0 per doc, 1 each lane's 64-doc word, 2 contiguous quarters
   bool group_bucket = true;   // group.bucket: partitioned plan EMITs through LDS buckets into the final layout
@@ -396,7 +397,7 @@ struct GroupByResult {
   mutable std::vector<uint8_t> datatable;  // pinot_datatable_group_by's bytes
 };
 // all groups' u8 HLL registers of function fn ([groups][256]) into host memory, from the device parts or the host copy
-void group_by_hll_registers(const GroupByResult &r, int fn, uint8_t *registers);
+void group_by_hll_registers(const GroupByResult &r, int fn, uint8_t *registers, bool pinned_dst = false);
 // DataTable bytes (datatable.cpp)
 std::vector<uint8_t> aggregation_datatable(const pinot_query &q, const pinot_agg_result *r, const pinot_exec_stats &s,
                                            const pinot_datatable_server *srv);

@@ -2114,19 +2114,28 @@ GroupByResult::~GroupByResult() {
   for (auto &v : values) put(p.f64, v);
 }
 
-void group_by_hll_registers(const GroupByResult &r, int fn, uint8_t *registers) {
+void group_by_hll_registers(const GroupByResult &r, int fn, uint8_t *registers, bool pinned_dst) {
   const size_t n = r.raw_keys.size();
   if (!n) return;
   if (r.hll_parts.empty()) {
     memcpy(registers, r.hll[fn].data(), n * 256);
     return;
   }
+  // a caller's (pageable) buffer is never the copy target: the runtime would pin it in place, and its later unmap
+  // stalls the GPU queues; the registers pass through a pinned, cached staging block instead
+  HostVec<uint8_t> stage;
+  uint8_t *dst = registers;
+  if (!pinned_dst) {
+    stage.resize(n * 256);
+    dst = stage.data();
+  }
   for (const HllPart &p : r.hll_parts) {
     if (!p.num_groups) continue;
     PINOT_HIP(hipSetDevice(p.device));
-    PINOT_HIP(hipMemcpy(registers + p.group_begin * 256, p.buf->get<uint8_t>() + p.off[fn], p.num_groups * 256,
+    PINOT_HIP(hipMemcpy(dst + p.group_begin * 256, p.buf->get<uint8_t>() + p.off[fn], p.num_groups * 256,
                         hipMemcpyDeviceToHost));
   }
+  if (!pinned_dst) memcpy(registers, dst, n * 256);
 }
 
 // DictionaryBasedGroupKeyGenerator.getGroupKey (:421-437): column 0 first, values '\t'-joined.
@@ -3267,6 +3276,7 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     a.hseed = 0x5EEDF00Dull + 0x9E3779B97F4A7C15ull * (unsigned long long)attempt;
     a.verify_err = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(matched) + S * 8 + 16);
   }
+  if (gp.mode == GB_LDS) a.emit_block = e.group_lds_block;  // block size of the lane-owns-quarter GB_LDS instance
   int64_t max_chunks = 1;  // chunks in the largest segment window
   for (const GroupSegment &g : gsegs) max_chunks = std::max<int64_t>(max_chunks, g.ch_end - g.ch_begin);
   const int64_t resident = (int64_t)group_query_blocks_per_cu(a) * e.num_cus;

@@ -1095,7 +1095,7 @@ constexpr int kGroupLwEmitBlock = 512;
 constexpr int kGroupLqEmitBlockWide = 1024;
 
 static int group_block_threads(const GroupArgs &a) {
-  if (a.mode == GB_LDS && a.lw == 2 && a.pf_nc > 0) return kGroupLwEmitBlock;  // lane-owns-quarter registers
+  if (a.mode == GB_LDS && a.lw == 2 && a.pf_nc > 0) return a.emit_block == 256 ? 256 : kGroupLwEmitBlock;
   if (a.lw == 2 && a.mode == GB_EMIT2 && a.emit_block == kGroupLqEmitBlockWide) return kGroupLqEmitBlockWide;
   return (a.lw && (a.mode == GB_EMIT || a.mode == GB_EMIT2)) ? kGroupLwEmitBlock : kGroupBlock;
 }
@@ -1107,7 +1107,8 @@ static void with_group_kernel(const GroupArgs &a, V &&v) {
   switch (a.mode) {
     case GB_GLOBAL: v(&k_group_query<GB_GLOBAL, 0, kGroupBlock>, kGroupBlock); break;
     case GB_LDS:
-      if (lh) v(&k_group_query<GB_LDS, 3, kGroupLwEmitBlock, 4>, kGroupLwEmitBlock);  // 4 waves per SIMD: 2 blocks per CU
+      if (lh && a.emit_block == 256) v(&k_group_query<GB_LDS, 3, 256, 3>, 256);  // 3 blocks of 4 waves per CU
+      else if (lh) v(&k_group_query<GB_LDS, 3, kGroupLwEmitBlock, 4>, kGroupLwEmitBlock);  // 4 waves per SIMD: 2 blocks per CU
       else v(&k_group_query<GB_LDS, 0, kGroupBlock>, kGroupBlock);
       break;
     case GB_COUNT:

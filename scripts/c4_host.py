@@ -26,8 +26,16 @@ for i in range(10):
     t1 = time.perf_counter()
     res, st = ex.group_by_result(q, kept, top_n=10)
     t2 = time.perf_counter()
+    ta = time.perf_counter()
+    kept = [res.trimmed_groups(10, i) for i in range(3)]
+    tb = time.perf_counter()
+    regs = res.hll(2)
+    tc = time.perf_counter()
+    keys = res.raw_keys()
+    td = time.perf_counter()
     dt = res.data_table(q.marshal, st, 10, None)
     t3 = time.perf_counter()
+    print(json.dumps({"trim_lists_ms": (tb - ta) * 1e3, "hll_fetch_ms": (tc - tb) * 1e3, "raw_keys_ms": (td - tc) * 1e3}))
     del res
     t4 = time.perf_counter()
     print(json.dumps({"step": i, "prune_ms": (t1 - t0) * 1e3, "group_by_top_ms": (t2 - t1) * 1e3,

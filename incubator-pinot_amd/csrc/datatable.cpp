@@ -155,6 +155,31 @@ void hll_bytes(Out &o, const uint8_t *regs) {
   }
 }
 
+// A group key as a serialized String (int length + UTF-8 bytes) written straight from the columns' value strings:
+// GroupByResult::key's '\t'-joined value, without building it (DictionaryBasedGroupKeyGenerator.java:421-437).
+void put_group_key(Out &o, const GroupByResult &r, int64_t g) {
+  const size_t nc = r.gcard.size();
+  const std::string *part[kMaxGroupCols];
+  size_t len = nc ? nc - 1 : 0;
+  int64_t k = r.raw_keys[g];
+  for (size_t j = 0; j < nc; j++) {
+    if (!r.key_ids.empty()) {
+      part[j] = &r.gvalues[j][r.key_ids[g * nc + j]];
+    } else {
+      part[j] = &r.gvalues[j][k % r.gcard[j]];
+      k /= r.gcard[j];
+    }
+    len += part[j]->size();
+  }
+  o.i32((int32_t)len);
+  uint8_t *x = o.grow(len);
+  for (size_t j = 0; j < nc; j++) {
+    if (j) *x++ = '\t';
+    memcpy(x, part[j]->data(), part[j]->size());
+    x += part[j]->size();
+  }
+}
+
 // DataSchema.toBytes (pinot-common/.../utils/DataSchema.java:114-139): names, then type names.
 void schema_bytes(Out &o, const std::vector<std::string> &names, const std::vector<std::string> &types) {
   o.i32((int32_t)names.size());
@@ -333,7 +358,7 @@ std::vector<uint8_t> group_by_datatable(const pinot_query &q, const GroupByResul
       v.i32(vtype);
       for (int64_t j = 0; j < m; j++) {
         const int64_t g = group(j);
-        v.str(r.key(g));
+        put_group_key(v, r, g);
         switch (f) {
           case PINOT_AGG_COUNT: v.i32(8); v.i64(cnt[g]); break;
           case PINOT_AGG_AVG: v.i32(16); v.f64(val[g]); v.i64(cnt[g]); break;

@@ -109,16 +109,20 @@ def test_server_two_ranks_on_one_device():
     srv.close()
 
 
-def test_server_refuses_binding_inter_segment_cap():
-    """The 2 x num.groups.limit cap orders keys across GPUs: refused (status 4) instead of a wrong answer."""
+def test_server_binding_inter_segment_cap():
+    """The 2 x num.groups.limit cap through the RCCL server (one rank): each segment's first-appearance holder
+    (max.init.group.holder.capacity 10 makes it bind) and the inter-segment cap in segment order
+    (CombineGroupByOperator.java:80,147), against the oracle's one-server combine."""
     rng = np.random.default_rng(14)
     host = _segments(rng, 8000, 3)
     srv = GpuServer([0])
     gsegs = [srv.engines[0].register(s) for s in host]
     q = compile_pql("SELECT COUNT(*) FROM t GROUP BY g0, h")
-    with pytest.raises(PinotGpuError) as ei:
-        ServerExecutor(srv, num_groups_limit=100, max_init_group_holder_capacity=10).process_query(q, gsegs)
-    assert ei.value.status == 4
+    got, st = ServerExecutor(srv, num_groups_limit=100, max_init_group_holder_capacity=10).process_query(
+        q, gsegs, trim=False)
+    exp, scanned = O.execute_server(host, q, num_groups_limit=100, array_threshold=10)
+    assert st.num_docs_scanned == scanned and len(exp) == 200
+    assert got == exp
     srv.close()
 
 

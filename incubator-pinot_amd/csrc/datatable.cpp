@@ -16,7 +16,9 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <exception>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "engine.h"
@@ -326,32 +328,30 @@ std::vector<uint8_t> group_by_datatable(const pinot_query &q, const GroupByResul
   t.rows = na;
   t.cols = 2;
   schema_bytes(t.schema, {"functionName", "GroupByResultMap"}, {"STRING", "OBJECT"});
-  std::vector<std::string> fn_names;
-  HostVec<uint8_t> regs;  // pinned: a large pageable copy target is pinned in place by the runtime, and its later
-                          // unmap stalls the GPU's queues (measured: ~20 ms on the next query)
-  for (int i = 0; i < na; i++) {
-    const std::string name = aggregation_column_name(q.aggregations[i]);
-    int32_t id = (int32_t)fn_names.size();
-    for (size_t k = 0; k < fn_names.size(); k++)
-      if (fn_names[k] == name) id = (int32_t)k;
-    if (id == (int32_t)fn_names.size()) fn_names.push_back(name);
-    t.fixed.i32(id);
-    const int64_t m = fn_groups && fn_groups[i] ? fn_num_groups[i] : n;
-    auto group = [&](int64_t j) -> int64_t {
-      const int64_t g = fn_groups && fn_groups[i] ? fn_groups[i][j] : j;
-      require(g >= 0 && g < n, PINOT_ERR_BAD_ARG, "group index out of range");
-      return g;
-    };
-    const int f = sv_function(r.functions[i]);
-    if (f == PINOT_AGG_DISTINCTCOUNTHLL) {
-      regs.resize((size_t)n * 256);
-      group_by_hll_registers(r, i, regs.data(), true);
-    }
-    const HostVec<int64_t> &cnt = r.counts[r.counts_shared ? 0 : i];
-    const HostVec<double> &val = r.values[i];
-    const int32_t vtype = f == PINOT_AGG_COUNT ? OBJ_LONG : f == PINOT_AGG_AVG ? OBJ_AVG_PAIR
-                          : f == PINOT_AGG_DISTINCTCOUNTHLL ? OBJ_HLL : OBJ_DOUBLE;
-    object_cell(t, OBJ_MAP, [&](Out &v) {  // MAP_SER_DE (ObjectSerDeUtils.java:262-300)
+  // each function's map serialized on its own thread (they are independent; large trimmed results take ms each),
+  // then the rows appended in function order
+  std::vector<Out> cells(na);
+  std::vector<std::exception_ptr> errs(na);
+  auto build = [&](int i) {
+    try {
+      const int64_t m = fn_groups && fn_groups[i] ? fn_num_groups[i] : n;
+      auto group = [&](int64_t j) -> int64_t {
+        const int64_t g = fn_groups && fn_groups[i] ? fn_groups[i][j] : j;
+        require(g >= 0 && g < n, PINOT_ERR_BAD_ARG, "group index out of range");
+        return g;
+      };
+      const int f = sv_function(r.functions[i]);
+      HostVec<uint8_t> regs;  // pinned: a large pageable copy target is pinned in place by the runtime, and its later
+                              // unmap stalls the GPU's queues (measured: ~20 ms on the next query)
+      if (f == PINOT_AGG_DISTINCTCOUNTHLL) {
+        regs.resize((size_t)n * 256);
+        group_by_hll_registers(r, i, regs.data(), true);
+      }
+      const HostVec<int64_t> &cnt = r.counts[r.counts_shared ? 0 : i];
+      const HostVec<double> &val = r.values[i];
+      const int32_t vtype = f == PINOT_AGG_COUNT ? OBJ_LONG : f == PINOT_AGG_AVG ? OBJ_AVG_PAIR
+                            : f == PINOT_AGG_DISTINCTCOUNTHLL ? OBJ_HLL : OBJ_DOUBLE;
+      Out &v = cells[i];  // MAP_SER_DE (ObjectSerDeUtils.java:262-300)
       v.i32((int32_t)m);
       if (m == 0) return;
       v.i32(OBJ_STRING);
@@ -366,7 +366,29 @@ std::vector<uint8_t> group_by_datatable(const pinot_query &q, const GroupByResul
           default: v.i32(8); v.f64(val[g]); break;
         }
       }
-    });
+    } catch (...) {
+      errs[i] = std::current_exception();
+    }
+  };
+  if (na > 1 && n >= 4096) {
+    std::vector<std::thread> th;
+    for (int i = 1; i < na; i++) th.emplace_back(build, i);
+    build(0);
+    for (auto &x : th) x.join();
+  } else {
+    for (int i = 0; i < na; i++) build(i);
+  }
+  for (auto &e : errs)
+    if (e) std::rethrow_exception(e);
+  std::vector<std::string> fn_names;
+  for (int i = 0; i < na; i++) {
+    const std::string name = aggregation_column_name(q.aggregations[i]);
+    int32_t id = (int32_t)fn_names.size();
+    for (size_t k = 0; k < fn_names.size(); k++)
+      if (fn_names[k] == name) id = (int32_t)k;
+    if (id == (int32_t)fn_names.size()) fn_names.push_back(name);
+    t.fixed.i32(id);
+    object_cell(t, OBJ_MAP, [&](Out &v) { v.b.swap(cells[i].b); });
   }
   t.dictionaries.emplace_back("functionName", fn_names);
   // CombineGroupByOperator.java:212-214: the merged map reached the inner-segment groups limit

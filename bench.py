@@ -385,8 +385,15 @@ def measure(job, args, workload):
         per_launch_b = b / launches_per_query
         avg_ms = kt[k][0] / max(kt[k][1], 1)
         kern[name] = {"avg_ms": avg_ms, "launches": kt[k][1], "bytes_per_launch": per_launch_b,
-                      "total_ms_per_query": kt[k][0] / reps,
+                      "total_ms_per_query": kt[k][0] / reps, "timing": "HIP events, separate timing pass",
                       "gbs": per_launch_b / (avg_ms / 1e3) / 1e9 if avg_ms > 0 else 0.0}
+        if name == "k_scan_query" and dev_ms:
+            # the one launch per step, timed inside the timed steps themselves: its in-kernel wall clock (first block
+            # start to last block end, s_memrealtime) every step; the separate timing pass is kept beside it
+            win = float(np.mean(dev_ms))
+            kern[name].update({"avg_ms": win, "timing": "in-kernel wall clock of every timed step (mean)",
+                               "timing_pass_avg_ms": avg_ms,
+                               "gbs": per_launch_b / (win / 1e3) / 1e9 if win > 0 else 0.0})
     dom = max(kern, key=lambda n: kern[n]["total_ms_per_query"])
     # per GPU: this GPU's algorithmic bytes over the query time
     query_gbs = query_b / (ms_per_step / 1e3) / 1e9

@@ -6,6 +6,8 @@ tag=${1:-r04final}
 out=gpurun_out/$tag
 mkdir -p $out
 export TMPDIR=/tmp
+timeout -k 10 150 python -u -m pytest -v --timeout 100 --timeout-method thread -m gpu tests/test_gpu_datatable.py > $out/pytest_dt.log 2>&1 || { tail -30 $out/pytest_dt.log; exit 1; }
+tail -1 $out/pytest_dt.log
 timeout -k 10 600 python bench.py --steps 20 --warmup 5 > $out/bench_default.json 2> $out/bench_default.err || { tail -20 $out/bench_default.err; exit 1; }
 python scripts/show_bench.py $out/bench_default.json | head -20
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/prof -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-verify > $out/prof.log 2>&1 || { tail -20 $out/prof.log; exit 1; }

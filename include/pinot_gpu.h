@@ -225,7 +225,11 @@ int32_t pinot_gpu_device_count(void);
 /* config: "key=value;key=value" (keys: num.groups.limit, device.scratch.mb), may be NULL */
 pinot_status pinot_gpu_engine_create(int32_t device, const char *config, pinot_engine **out);
 pinot_status pinot_gpu_engine_destroy(pinot_engine *engine);
-/* Change configuration keys at run time (e.g. "timing=1" to record per-kernel HIP events). */
+/* Change configuration keys at run time (e.g. "timing=1" to record per-kernel HIP events). Plan keys (defaults are
+ * the measured-fastest plans; the others stay for experiments and parity tests): exec.fused, filter.force,
+ * group.mode (lds | global | partition), group.ring (1: the ring-partitioned group-by plan), group.lds_block
+ * (256 | 512), group.emit_block, stats.exact, startree.use; diagnostics: debug.host_phases (stderr phase times),
+ * debug.ring (ring-kernel timing modes, wrong results). */
 pinot_status pinot_gpu_engine_set_config(pinot_engine *engine, const char *config);
 
 /* Copies the column buffers into HBM (one-time, cold path). */

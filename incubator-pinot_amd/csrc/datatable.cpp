@@ -17,6 +17,7 @@
 #include <cmath>
 #include <cstring>
 #include <exception>
+#include <memory>
 #include <string>
 #include <thread>
 #include <vector>
@@ -68,6 +69,18 @@ class Out {
     b[off + 3] = (uint8_t)u;
   }
 };
+
+inline uint8_t *put_be32(uint8_t *x, uint32_t u) {
+  x[0] = (uint8_t)(u >> 24);
+  x[1] = (uint8_t)(u >> 16);
+  x[2] = (uint8_t)(u >> 8);
+  x[3] = (uint8_t)u;
+  return x + 4;
+}
+inline uint8_t *put_be64(uint8_t *x, uint64_t u) {
+  for (int i = 0; i < 8; i++) x[i] = (uint8_t)(u >> (56 - 8 * i));
+  return x + 8;
+}
 
 // java.lang.String.hashCode over the UTF-16 code units of a UTF-8 string.
 int32_t java_string_hash(const std::string &s) {
@@ -136,6 +149,18 @@ enum ObjType : int32_t { OBJ_STRING = 0, OBJ_LONG = 1, OBJ_DOUBLE = 2, OBJ_AVG_P
 
 // stream-lib 2.7.0 HyperLogLog.getBytes (log2m 8): int log2m, int registerSet.size * 4, then the RegisterSet's 43
 // int words, register p in word p / 6 at bit 5 * (p % 6) (RegisterSet.set; LOG2_BITS_PER_WORD 6, REGISTER_SIZE 5).
+// HyperLogLog.getBytes into x (8 + 43 * 4 bytes): log2m, register-set size, the 43 words of six 5-bit registers.
+void hll_bytes_at(uint8_t *x, const uint8_t *regs) {
+  x = put_be32(put_be32(x, 8u), 43u * 4u);
+  for (int w = 0; w < 42; w++) {
+    const uint8_t *r = regs + 6 * w;
+    x = put_be32(x, (uint32_t)(r[0] & 0x1F) | (uint32_t)(r[1] & 0x1F) << 5 | (uint32_t)(r[2] & 0x1F) << 10 |
+                        (uint32_t)(r[3] & 0x1F) << 15 | (uint32_t)(r[4] & 0x1F) << 20 | (uint32_t)(r[5] & 0x1F) << 25);
+  }
+  put_be32(x, (uint32_t)(regs[252] & 0x1F) | (uint32_t)(regs[253] & 0x1F) << 5 | (uint32_t)(regs[254] & 0x1F) << 10 |
+                  (uint32_t)(regs[255] & 0x1F) << 15);
+}
+
 void hll_bytes(Out &o, const uint8_t *regs) {
   constexpr int kWords = 43;  // getSizeForCount(256): 256 / 6 = 42, not a multiple of 32 -> 43
   uint32_t m[kWords];
@@ -155,6 +180,65 @@ void hll_bytes(Out &o, const uint8_t *regs) {
     x[4 * w + 2] = (uint8_t)(u >> 8);
     x[4 * w + 3] = (uint8_t)u;
   }
+}
+
+// Uninitialised pinned staging bytes (PinnedCache-backed): the device registers' copy target.
+struct PinnedBytes {
+  void *p = nullptr;
+  size_t bytes = 0;
+  bool pinned = false;
+  explicit PinnedBytes(size_t n) {
+    bytes = size_t(1) << PinnedCache::size_class(n < 4096 ? 4096 : n);
+    p = PinnedCache::get().take(bytes);
+    pinned = p != nullptr || hipHostMalloc(&p, bytes, hipHostMallocDefault) == hipSuccess;
+    if (!pinned) {
+      (void)hipGetLastError();
+      p = std::malloc(bytes);
+      if (!p) throw std::bad_alloc();
+    }
+  }
+  ~PinnedBytes() {
+    if (!pinned) std::free(p);
+    else if (!PinnedCache::get().give(p, bytes)) (void)hipHostFree(p);
+  }
+  PinnedBytes(const PinnedBytes &) = delete;
+  PinnedBytes &operator=(const PinnedBytes &) = delete;
+  uint8_t *data() { return static_cast<uint8_t *>(p); }
+};
+
+// A group key's value strings (GroupByResult::key's '\t'-joined parts); returns the joined length.
+size_t group_key_parts(const GroupByResult &r, int64_t g, const std::string **part) {
+  const size_t nc = r.gcard.size();
+  size_t len = nc ? nc - 1 : 0;
+  int64_t k = r.raw_keys[g];
+  for (size_t j = 0; j < nc; j++) {
+    if (!r.key_ids.empty()) {
+      part[j] = &r.gvalues[j][r.key_ids[g * nc + j]];
+    } else {
+      part[j] = &r.gvalues[j][k % r.gcard[j]];
+      k /= r.gcard[j];
+    }
+    len += part[j]->size();
+  }
+  return len;
+}
+
+// One map entry (MAP_SER_DE: key String, then the value's int length and bytes) appended with one buffer growth:
+// the key written straight from the columns' value strings, without building it
+// (DictionaryBasedGroupKeyGenerator.java:421-437).
+template <typename F>
+void put_entry(Out &o, const GroupByResult &r, int64_t g, size_t vbytes, F &&value) {
+  const std::string *part[kMaxGroupCols];
+  const size_t nc = r.gcard.size();
+  const size_t klen = group_key_parts(r, g, part);
+  uint8_t *x = put_be32(o.grow(4 + klen + 4 + vbytes), (uint32_t)klen);
+  for (size_t j = 0; j < nc; j++) {
+    if (j) *x++ = '\t';
+    memcpy(x, part[j]->data(), part[j]->size());
+    x += part[j]->size();
+  }
+  x = put_be32(x, (uint32_t)vbytes);
+  value(x);
 }
 
 // A group key as a serialized String (int length + UTF-8 bytes) written straight from the columns' value strings:
@@ -341,11 +425,18 @@ std::vector<uint8_t> group_by_datatable(const pinot_query &q, const GroupByResul
         return g;
       };
       const int f = sv_function(r.functions[i]);
-      HostVec<uint8_t> regs;  // pinned: a large pageable copy target is pinned in place by the runtime, and its later
-                              // unmap stalls the GPU's queues (measured: ~20 ms on the next query)
+      // registers: the host copy as it is, or the device parts through pinned staging (a large pageable copy target
+      // is pinned in place by the runtime, and its later unmap stalls the GPU's queues: ~20 ms on the next query)
+      std::unique_ptr<PinnedBytes> stage;
+      const uint8_t *regs = nullptr;
       if (f == PINOT_AGG_DISTINCTCOUNTHLL) {
-        regs.resize((size_t)n * 256);
-        group_by_hll_registers(r, i, regs.data(), true);
+        if (r.hll_parts.empty()) {
+          regs = r.hll[i].data();
+        } else {
+          stage.reset(new PinnedBytes((size_t)n * 256));
+          group_by_hll_registers(r, i, stage->data(), true);
+          regs = stage->data();
+        }
       }
       const HostVec<int64_t> &cnt = r.counts[r.counts_shared ? 0 : i];
       const HostVec<double> &val = r.values[i];
@@ -356,14 +447,23 @@ std::vector<uint8_t> group_by_datatable(const pinot_query &q, const GroupByResul
       if (m == 0) return;
       v.i32(OBJ_STRING);
       v.i32(vtype);
+      v.b.reserve(v.b.size() + (size_t)m * (16 + (f == PINOT_AGG_DISTINCTCOUNTHLL ? 8 + 43 * 4 : 16)));
+      auto bits = [](double d) {
+        uint64_t u;
+        memcpy(&u, &d, 8);
+        return u;
+      };
       for (int64_t j = 0; j < m; j++) {
         const int64_t g = group(j);
-        put_group_key(v, r, g);
         switch (f) {
-          case PINOT_AGG_COUNT: v.i32(8); v.i64(cnt[g]); break;
-          case PINOT_AGG_AVG: v.i32(16); v.f64(val[g]); v.i64(cnt[g]); break;
-          case PINOT_AGG_DISTINCTCOUNTHLL: v.i32(8 + 43 * 4); hll_bytes(v, regs.data() + (size_t)g * 256); break;
-          default: v.i32(8); v.f64(val[g]); break;
+          case PINOT_AGG_COUNT: put_entry(v, r, g, 8, [&](uint8_t *x) { put_be64(x, (uint64_t)cnt[g]); }); break;
+          case PINOT_AGG_AVG:
+            put_entry(v, r, g, 16, [&](uint8_t *x) { put_be64(put_be64(x, bits(val[g])), (uint64_t)cnt[g]); });
+            break;
+          case PINOT_AGG_DISTINCTCOUNTHLL:
+            put_entry(v, r, g, 8 + 43 * 4, [&](uint8_t *x) { hll_bytes_at(x, regs + (size_t)g * 256); });
+            break;
+          default: put_entry(v, r, g, 8, [&](uint8_t *x) { put_be64(x, bits(val[g])); }); break;
         }
       }
     } catch (...) {

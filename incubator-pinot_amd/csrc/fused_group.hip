@@ -904,7 +904,7 @@ __device__ __forceinline__ void lq_process(const GroupArgs &a, const GroupSegmen
   }
 }
 
-template <int MODE>
+template <int MODE, int NCOL = kGroupPfCols>
 __device__ __forceinline__ void group_chunk_lq(const GroupArgs &a, const GroupSegment &sg, int64_t ch, uint64_t mask,
                                                int lane, uint32_t *plds) {
   const int64_t q0 = ch * 256 + lane;
@@ -919,7 +919,7 @@ __device__ __forceinline__ void group_chunk_lq(const GroupArgs &a, const GroupSe
       const uint32_t m = (((lane & 2) ? hi : lo) >> (16 * (lane & 1))) & 0xFFFFu;
       if (!__any(m != 0)) continue;
       const LqCols k = lq_cols<MODE>(a, sg);
-      constexpr int NC = MODE == GB_COUNT ? kLqCountCols : kGroupPfCols;  // COUNT reads the group columns only
+      constexpr int NC = MODE == GB_COUNT ? kLqCountCols : NCOL;  // COUNT reads the group columns only
       uint32_t R[NC][12];
       lq_load<NC>(k, q0 + 64 * q, R);
       lq_process<MODE, NC>(a, sg, k, R, q0 + 64 * q, m, lane, plds);
@@ -1061,6 +1061,7 @@ __global__ __launch_bounds__(BLK, MINW) void k_group_query(GroupArgs a) {
     }
     if (__any(mask != 0)) {
       if constexpr (PATH == 3) group_chunk_lq<MODE>(a, sg, ch, mask, lane, plds);
+      else if constexpr (PATH == 4) group_chunk_lq<MODE, 3>(a, sg, ch, mask, lane, plds);  // <= 3 columns read
       else if constexpr (PATH == 2) group_chunk_lw<MODE>(a, sg, ch, mask, lane, plds);
       else if constexpr (PATH == 1) group_chunk_pf<MODE>(a, sg, ch, mask, lane, plds);
       else group_chunk<MODE>(a, sg, ch, mask, lane, acc_lds, plds);
@@ -1108,6 +1109,7 @@ static void with_group_kernel(const GroupArgs &a, V &&v) {
     case GB_GLOBAL: v(&k_group_query<GB_GLOBAL, 0, kGroupBlock>, kGroupBlock); break;
     case GB_LDS:
       if (lh && a.emit_block == 256) v(&k_group_query<GB_LDS, 3, 256, 3>, 256);  // 3 blocks of 4 waves per CU
+      else if (lh && a.pf_nc <= 3) v(&k_group_query<GB_LDS, 4, kGroupLwEmitBlock, 4>, kGroupLwEmitBlock);
       else if (lh) v(&k_group_query<GB_LDS, 3, kGroupLwEmitBlock, 4>, kGroupLwEmitBlock);  // 4 waves per SIMD: 2 blocks per CU
       else v(&k_group_query<GB_LDS, 0, kGroupBlock>, kGroupBlock);
       break;

@@ -126,3 +126,26 @@ def test_star_tree_mixed_segments(engine):
         _same(q, got, scan)
     for g in gs:
         g.release()
+
+
+def test_star_tree_hll_after_other_plans(engine):
+    """A star-tree DISTINCTCOUNTHLL right after scan-plan and star-tree HLL queries that filled the shared register
+    block: the star plan starts from cleared registers (a narrower filter, and one matching nothing, equal the oracle
+    rather than the earlier queries' registers)."""
+    rng = np.random.default_rng(1700)
+    seg = st_segment(rng, 20000, name="sth")
+    g, st = _attach(engine, seg, leaf=10)
+    ex = ServerQueryExecutor(engine)
+    wide = {"aggregations": [{"function": "DISTINCTCOUNTHLL", "column": "m"}], "filter": None, "group_by": None}
+    got, _ = ex.process_query(wide, [g])  # m has no HLL pair: the regular (scan) plan
+    assert got[0].cardinality() == O.execute_server([seg], wide)[0][0].cardinality()
+    for flt in (None, {"operator": "EQUALITY", "column": "a", "values": ["1"]},
+                {"operator": "EQUALITY", "column": "a", "values": ["123456789"]}):
+        q = {"aggregations": [{"function": "DISTINCTCOUNTHLL", "column": "c"}, {"function": "COUNT", "column": "*"}],
+             "filter": flt, "group_by": None}
+        got, stats = ex.process_query(q, [g])
+        exp, scanned = S.execute_server([seg], [st], q)
+        assert got[1] == exp[1] and stats.num_docs_scanned == scanned, flt
+        assert got[0].cardinality() == exp[0].cardinality(), flt
+        assert (np.asarray(got[0].registers, dtype=np.int64) == np.asarray(exp[0].reg, dtype=np.int64)).all(), flt
+    g.release()

@@ -364,7 +364,8 @@ def measure(job, args, workload):
     kern = {}
     if c4:
         alg = segs_here * args.docs * CONFIG4_BYTES_PER_ROW
-        # the group-by pipeline of one query on engine 0 (filter, ring partition, ring reduce: one timed region)
+        # the group-by pipeline of one query on engine 0, one timed region: the ring plan (k_group_ring ->
+        # k_ring_reduce) or the counted plan (COUNT -> scan -> EMIT2 -> k_partition_reduce), as `plan` says
         names = ((1, "group_by_pipeline", alg),)
         query_b = alg
     elif gb:
@@ -429,6 +430,10 @@ def measure(job, args, workload):
     }
     if phases:
         out["merge_phases_ms"] = phases
+    if gb and job.engines:
+        inst = job.engines[0].stat("group.last_instance")
+        out["plan"] = {"instance": inst, "name": "ring" if inst == 90000 else
+                       "counted" if inst // 10000 in (3, 6) else "lds" if inst // 10000 == 1 else "other"}
     if gb:
         if job.path == "engine":  # the timed step returned DataTable bytes; the full result once for the check
             out["datatable_bytes"] = len(res)
@@ -446,7 +451,10 @@ def measure(job, args, workload):
         out["verify"] = {"filtered_count": chk[0], "filtered_sum": int(chk[1]),
                          "match": tot == [chk[0], int(chk[1])] and n_groups == (1_000_000 if c4 else 1_600),
                          "how": "Σ per-group counts / sums == the aggregation-only COUNT(*) / SUM(d8) of the same "
-                                "filter (independent kernel path); group-level parity: tests/test_gpu_configs.py"}
+                                "filter (independent kernel path) at full size; group-level parity against the oracle "
+                                "at 2 x 2M docs: " + ("tests/test_gpu_configs.py::test_config4_shape, "
+                                                      "tests/test_gpu_ring.py::test_ring_config4_shape" if c4 else
+                                                      "tests/test_gpu_configs.py::test_lds_shape")}
     else:
         out["result"] = {"count": res[0], "sum": int(res[1]), "docs_scanned": st.num_docs_scanned}
     return out
@@ -518,12 +526,12 @@ def main():
     if args.workload == "config2" and not args.no_config4:
         c4 = measure(job, args, "config4")
         keep = ("value", "unit", "ms_per_step", "p50_query_ms", "p50_c_abi_ms", "step_ms_detail", "steps", "warmup",
-                "dtype", "config", "roofline", "merge_phases_ms", "result", "verify")
+                "dtype", "config", "roofline", "merge_phases_ms", "result", "verify", "plan")
         out["config4"] = {k: c4[k] for k in keep if k in c4}
     if args.workload == "config2" and not args.no_lds:
         lds = measure(job, args, "lds")
         keep = ("value", "unit", "ms_per_step", "p50_query_ms", "step_ms_detail", "steps", "dtype", "config",
-                "roofline", "result", "verify")
+                "roofline", "result", "verify", "plan")
         out["lds_group_by"] = {k: lds[k] for k in keep if k in lds}
     cpu_ok = rank == 0 and world == 1 and job.n_gpus == 1 and not args.no_cpu_baseline
     if cpu_ok:

@@ -144,13 +144,12 @@ void parse_config(Engine &e, const char *cfg) {
       e.group_mode = v == "auto" ? "" : v;
     } else if (k == "sync.poll") e.sync_poll = v == "1" || v == "true";
     else if (k == "sync.flag") e.sync_flag = v == "1" || v == "true";
-    else if (k == "debug.emit") e.debug_emit = std::stoi(v);
-    else if (k == "debug.ring") e.debug_ring = std::stoi(v);
     else if (k == "group.pshift") e.group_pshift = std::stoi(v);
     else if (k == "group.nt_store") e.group_nt_store = std::stoi(v) != 0;
     else if (k == "group.prefetch") e.group_prefetch = v == "1" || v == "true";
     else if (k == "group.bucket") e.group_bucket = v == "1" || v == "true";
     else if (k == "group.ring") e.group_ring = v == "1" || v == "true";
+    else if (k == "group.ring_qfilter") e.group_ring_qfilter = v == "1" || v == "true";
     else if (k == "group.aligned") e.group_aligned = v == "1" || v == "true";
     else if (k == "group.lds_block") {
       e.group_lds_block = std::stoi(v);
@@ -820,8 +819,8 @@ pinot_status pinot_gpu_engine_stat(pinot_engine *engine, const char *name, int64
     const std::string n = name;
     if (n == "group.ring_queries") *value = engine->ring_queries;
     else if (n == "group.ring_fallbacks") *value = engine->ring_fallbacks;
-    else if (n == "group.ring_waits") *value = engine->ring_waits;
-    else if (n == "group.ring_sleeps") *value = engine->ring_sleeps;
+    else if (n == "group.ring_qfilter_queries") *value = engine->ring_qfilter_queries;
+    else if (n == "group.last_instance") *value = engine->last_group_instance;
     else if (n == "exec.last_pre_segments") *value = engine->last_pre_segments;
     else require(false, PINOT_ERR_BAD_ARG, "unknown engine stat");
   });

@@ -17,6 +17,7 @@
 #include <cmath>
 #include <cstring>
 #include <exception>
+#include <functional>
 #include <memory>
 #include <string>
 #include <thread>
@@ -26,6 +27,22 @@
 
 namespace pinot {
 namespace {
+// fn(0) .. fn(n - 1) on n threads (fn(0) on the caller's); every started thread is joined, also when starting one or
+// fn(0) throws
+void run_parallel(size_t n, const std::function<void(size_t)> &fn) {
+  std::vector<std::thread> th;
+  struct Join {
+    std::vector<std::thread> &t;
+    ~Join() {
+      for (auto &x : t)
+        if (x.joinable()) x.join();
+    }
+  } join{th};
+  th.reserve(n ? n - 1 : 0);
+  for (size_t t = 1; t < n; t++) th.emplace_back(fn, t);
+  if (n) fn(0);
+}
+
 
 class Out {
  public:
@@ -161,26 +178,7 @@ void hll_bytes_at(uint8_t *x, const uint8_t *regs) {
                   (uint32_t)(regs[255] & 0x1F) << 15);
 }
 
-void hll_bytes(Out &o, const uint8_t *regs) {
-  constexpr int kWords = 43;  // getSizeForCount(256): 256 / 6 = 42, not a multiple of 32 -> 43
-  uint32_t m[kWords];
-  for (int w = 0; w < 42; w++) {  // six 5-bit registers per word, no division in the loop
-    const uint8_t *r = regs + 6 * w;
-    m[w] = (uint32_t)(r[0] & 0x1F) | (uint32_t)(r[1] & 0x1F) << 5 | (uint32_t)(r[2] & 0x1F) << 10 |
-           (uint32_t)(r[3] & 0x1F) << 15 | (uint32_t)(r[4] & 0x1F) << 20 | (uint32_t)(r[5] & 0x1F) << 25;
-  }
-  m[42] = (uint32_t)(regs[252] & 0x1F) | (uint32_t)(regs[253] & 0x1F) << 5 | (uint32_t)(regs[254] & 0x1F) << 10 |
-          (uint32_t)(regs[255] & 0x1F) << 15;
-  uint8_t *x = o.grow(8 + 4 * kWords);
-  const uint32_t head[2] = {8u, (uint32_t)(kWords * 4)};
-  for (int w = 0; w < 2 + kWords; w++) {
-    const uint32_t u = w < 2 ? head[w] : m[w - 2];
-    x[4 * w] = (uint8_t)(u >> 24);
-    x[4 * w + 1] = (uint8_t)(u >> 16);
-    x[4 * w + 2] = (uint8_t)(u >> 8);
-    x[4 * w + 3] = (uint8_t)u;
-  }
-}
+void hll_bytes(Out &o, const uint8_t *regs) { hll_bytes_at(o.grow(8 + 43 * 4), regs); }
 
 // Uninitialised pinned staging bytes (PinnedCache-backed): the device registers' copy target.
 struct PinnedBytes {
@@ -239,31 +237,6 @@ void put_entry(Out &o, const GroupByResult &r, int64_t g, size_t vbytes, F &&val
   }
   x = put_be32(x, (uint32_t)vbytes);
   value(x);
-}
-
-// A group key as a serialized String (int length + UTF-8 bytes) written straight from the columns' value strings:
-// GroupByResult::key's '\t'-joined value, without building it (DictionaryBasedGroupKeyGenerator.java:421-437).
-void put_group_key(Out &o, const GroupByResult &r, int64_t g) {
-  const size_t nc = r.gcard.size();
-  const std::string *part[kMaxGroupCols];
-  size_t len = nc ? nc - 1 : 0;
-  int64_t k = r.raw_keys[g];
-  for (size_t j = 0; j < nc; j++) {
-    if (!r.key_ids.empty()) {
-      part[j] = &r.gvalues[j][r.key_ids[g * nc + j]];
-    } else {
-      part[j] = &r.gvalues[j][k % r.gcard[j]];
-      k /= r.gcard[j];
-    }
-    len += part[j]->size();
-  }
-  o.i32((int32_t)len);
-  uint8_t *x = o.grow(len);
-  for (size_t j = 0; j < nc; j++) {
-    if (j) *x++ = '\t';
-    memcpy(x, part[j]->data(), part[j]->size());
-    x += part[j]->size();
-  }
 }
 
 // DataSchema.toBytes (pinot-common/.../utils/DataSchema.java:114-139): names, then type names.
@@ -429,7 +402,12 @@ std::vector<uint8_t> group_by_datatable(const pinot_query &q, const GroupByResul
       // is pinned in place by the runtime, and its later unmap stalls the GPU's queues: ~20 ms on the next query)
       std::unique_ptr<PinnedBytes> stage;
       const uint8_t *regs = nullptr;
-      if (f == PINOT_AGG_DISTINCTCOUNTHLL) {
+      // a device-trimmed result carries each HLL function's getBytes rows (hll_serde.hip): copied as they are
+      const uint8_t *ser = (f == PINOT_AGG_DISTINCTCOUNTHLL && (size_t)i < r.hll_bytes.size() &&
+                            r.hll_bytes[i].size() == (size_t)n * 180)
+                               ? r.hll_bytes[i].data()
+                               : nullptr;
+      if (f == PINOT_AGG_DISTINCTCOUNTHLL && !ser) {
         if (r.hll_parts.empty()) {
           regs = r.hll[i].data();
         } else {
@@ -461,7 +439,8 @@ std::vector<uint8_t> group_by_datatable(const pinot_query &q, const GroupByResul
             put_entry(v, r, g, 16, [&](uint8_t *x) { put_be64(put_be64(x, bits(val[g])), (uint64_t)cnt[g]); });
             break;
           case PINOT_AGG_DISTINCTCOUNTHLL:
-            put_entry(v, r, g, 8 + 43 * 4, [&](uint8_t *x) { hll_bytes_at(x, regs + (size_t)g * 256); });
+            if (ser) put_entry(v, r, g, 8 + 43 * 4, [&](uint8_t *x) { memcpy(x, ser + (size_t)g * 180, 180); });
+            else put_entry(v, r, g, 8 + 43 * 4, [&](uint8_t *x) { hll_bytes_at(x, regs + (size_t)g * 256); });
             break;
           default: put_entry(v, r, g, 8, [&](uint8_t *x) { put_be64(x, bits(val[g])); }); break;
         }
@@ -470,14 +449,9 @@ std::vector<uint8_t> group_by_datatable(const pinot_query &q, const GroupByResul
       errs[i] = std::current_exception();
     }
   };
-  if (na > 1 && n >= 4096) {
-    std::vector<std::thread> th;
-    for (int i = 1; i < na; i++) th.emplace_back(build, i);
-    build(0);
-    for (auto &x : th) x.join();
-  } else {
+  if (na > 1 && n >= 4096) run_parallel((size_t)na, [&](size_t i) { build((int)i); });
+  else
     for (int i = 0; i < na; i++) build(i);
-  }
   for (auto &e : errs)
     if (e) std::rethrow_exception(e);
   std::vector<std::string> fn_names;

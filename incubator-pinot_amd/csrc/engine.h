@@ -249,8 +249,6 @@ struct Engine {
   int64_t wall_clock_khz = 100000;  // hipDeviceAttributeWallClockRate (device-side kernel timing)
   bool sync_poll = false;     // sync.poll: busy-poll the stream instead of hipStreamSynchronize
   bool host_phases = false;
-  int debug_ring = 0;         // debug.ring: k_group_ring experiments (timing only, wrong results; RingArgs.debug)
-  int debug_emit = 0;         // debug.emit: GB_EMIT store experiments (timing only, wrong results)
   int group_nt_store = 0;     // group.nt_store: partitioned records stored non-temporally
   bool group_prefetch = true; // group.prefetch: partitioned plan loads every column of a word batch at once
   int group_pshift = -1;      // group.pshift: cap on log2 keys per partition (tests: many small partitions)
@@ -261,13 +259,14 @@ struct Engine {
   bool group_aligned = false; // group.aligned: bucketed EMIT runs padded to 64-B buckets (measured: EMIT -1.6%, reduce slower)
   int group_lw = 2;           // group.lw: partitioned plan reads 0 per doc, 1 each lane's 64-doc word, 2 contiguous quarters
   bool group_bucket = true;   // group.bucket: partitioned plan EMITs through LDS buckets into the final layout
-  bool group_ring = false;    // group.ring: large dense key spaces take the ring plan (no histogram pass; group_ring.hip;
-                              // measured 0.1-1 ms slower than the counted plan at config 4, so off by default)
+  bool group_ring = true;     // group.ring: large dense key spaces take the ring plan (no histogram pass; group_ring.hip);
+                              // 0: the counted plan (COUNT -> scan -> EMIT2 -> k_partition_reduce)
+  bool group_ring_qfilter = true;  // group.ring_qfilter: the ring kernel evaluates simple filters itself (else GB_FILTER)
   int32_t trim_top_n = 0;      // per call (pinot_gpu_group_by_top): trim the group-by on the device for this TOP n
   int64_t ring_queries = 0;    // group-bys launched on the ring plan
+  int64_t last_group_instance = 0;  // the last fused group-by's main kernel instance (group.last_instance)
   int64_t last_pre_segments = 0;  // segments of the last fused query whose filter needed a `pre` bitset (launch sequence)
-  int64_t ring_waits = 0;      // k_group_ring sink rounds that waited for a ring half to drain (group.ring_waits)
-  int64_t ring_sleeps = 0;     // ... and their s_sleep spins (group.ring_sleeps)
+  int64_t ring_qfilter_queries = 0;  // ... of them with the filter evaluated inside k_group_ring (no GB_FILTER pass)
   int64_t ring_fallbacks = 0;  // ring-plan queries re-answered on the counted plan (a region overflowed: skewed keys)
   int num_cus = 256;          // multiProcessorCount of the device
 
@@ -286,6 +285,7 @@ struct Engine {
   DeviceBuffer group_gather;   // multi-GPU root: every rank's per-group outputs, gathered
   PinnedBuffer group_host;     // their pinned host copy
   std::vector<std::shared_ptr<DeviceBuffer>> hll_pool;  // gathered HLL registers, reused once results are released
+  std::shared_ptr<DeviceBuffer> hll_ser;  // HyperLogLog.getBytes rows of a device-trimmed result (copied back at once)
   DeviceBuffer group_trim;     // device trim: union keys, per-group function bits, sort / scan scratch
   DeviceBuffer group_hash;     // hashed key spaces: fingerprint table + representative docs
   DeviceBuffer group_admit;    // num.groups.limit admission: first docs [S][G], admitted bitmaps [S][G/32], sort scratch
@@ -347,6 +347,10 @@ struct DenseOut {
   std::vector<long long *> cards;
   std::shared_ptr<DeviceBuffer> hll;
   std::vector<size_t> hll_off;
+  // device-trimmed results: each HLL function's HyperLogLog.getBytes rows ([n][180] B, hll_serde.hip) in hll_ser at
+  // hll_ser_off[fn], copied back with the other arrays
+  std::shared_ptr<DeviceBuffer> hll_ser;
+  std::vector<size_t> hll_ser_off;
   // compact read-back (dense, non-hashed key spaces of >= 64 K groups): the non-empty keys as a bitmap over [0, G),
   // counts and HLL cardinalities as u32 (overflow flag -> the 64-bit arrays), widened on the host
   const uint64_t *key_bits = nullptr;
@@ -394,6 +398,9 @@ struct GroupByResult {
   std::vector<HostVec<int64_t>> hll_card;
   std::vector<std::vector<uint8_t>> hll;
   std::vector<HllPart> hll_parts;
+  // device-trimmed results (pinot_gpu_group_by_top): per HLL function its groups' HyperLogLog.getBytes, [n][180] B
+  // (empty: not prepared; the DataTable writer then packs the registers itself)
+  std::vector<HostVec<uint8_t>> hll_bytes;
   mutable std::vector<uint8_t> datatable;  // pinot_datatable_group_by's bytes
 };
 // all groups' u8 HLL registers of function fn ([groups][256]) into host memory, from the device parts or the host copy

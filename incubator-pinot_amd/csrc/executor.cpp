@@ -31,8 +31,13 @@
 #include <functional>
 
 #include "engine.h"
+#include "group_ring.h"
 
 namespace pinot {
+// fused_group.hip: the k_group_query instance a launch of `a` runs (mode * 10000 + read path * 1000 + threads)
+int group_query_instance(const GroupArgs &a);
+// hll_serde.hip: HyperLogLog.getBytes of n groups' u8 register rows ([n][256] -> [n][180] B)
+void launch_hll_getbytes(const uint8_t *regs, long long n, uint8_t *out, hipStream_t stream);
 
 void check_deadline(const Engine &e, const char *phase) {
   if (e.has_deadline && std::chrono::steady_clock::now() >= e.deadline)
@@ -2129,6 +2134,12 @@ void group_by_hll_registers(const GroupByResult &r, int fn, uint8_t *registers, 
     stage.resize(n * 256);
     dst = stage.data();
   }
+  int caller_dev = 0;
+  PINOT_HIP(hipGetDevice(&caller_dev));
+  struct Restore {  // the caller's current device, whatever the parts' devices were
+    int d;
+    ~Restore() { (void)hipSetDevice(d); }
+  } restore{caller_dev};
   for (const HllPart &p : r.hll_parts) {
     if (!p.num_groups) continue;
     PINOT_HIP(hipSetDevice(p.device));
@@ -2348,10 +2359,16 @@ void parallel_tasks(size_t n, const std::function<void(size_t)> &fn) {
   }
   if (TaskPool::get().try_run(n, fn)) return;
   std::vector<std::thread> th;
+  struct Join {  // every started thread is joined, also when starting one throws or fn(0) throws
+    std::vector<std::thread> &t;
+    ~Join() {
+      for (auto &x : t)
+        if (x.joinable()) x.join();
+    }
+  } join{th};
   th.reserve(n - 1);
   for (size_t t = 1; t < n; t++) th.emplace_back(fn, t);
   fn(0);
-  for (auto &x : th) x.join();
 }
 
 // Fused group-by plan (GroupMode) chosen from the key space and the accumulators' per-key bytes.
@@ -2366,6 +2383,8 @@ struct GroupPlan {
   int reduce_wave_cnt_off = 0;
   int record_bits = 0;  // partitioned: local key + aggregated fields (the bucketed EMIT keeps bit 63 as a valid mark)
 };
+
+constexpr int kRingInstanceCode = 90000;  // group.last_instance of a ring-plan query
 
 constexpr int kGroupMaxFusedLeafBits = 12;    // 16 wave stages x 6 KiB
 constexpr int kGroupLdsAccBudget = 60 * 1024;  // GB_LDS accumulators / GB_COUNT-EMIT partition cursors
@@ -2464,7 +2483,6 @@ GroupPlan plan_group(const std::vector<SegmentData *> &segs, const pinot_query &
 // Ring plan (group_ring.hip): the partitioned plan without its histogram pass. Applies to dense key spaces whose
 // partitions of K <= 1024 keys number at most kRingMaxPartitions (k_group_ring's LDS rings), read through the
 // lane-owns-quarter decoder (<= 4 columns of <= 20 bits) with records of <= 53 bits.
-constexpr int64_t kRingMaxPartitions = 1024;
 constexpr size_t kRingReduceLds = 160 * 1024;
 struct RingPlan {
   bool on = false;
@@ -2485,7 +2503,7 @@ RingPlan plan_ring(const Engine &e, const std::vector<SegmentData *> &segs, cons
   // columns: the group columns, then one slot per distinct accumulator (as the EMIT prefetch lists them)
   int nc = q.num_group_by;
   for (int a = 0; a < na; a++) nc += gx.acc_kind[a] != 5;
-  if (nc > kGroupPfCols) return rp;
+  if (nc > kGroupPfCols || q.num_group_by > kRingGroupCols || nc - q.num_group_by > kRingAggCols) return rp;
   for (auto *s : segs) {
     for (int j = 0; j < q.num_group_by; j++)
       if (s->column(q.group_by[j])->bits > kGroupLwMaxBits) return rp;
@@ -2522,7 +2540,7 @@ RingPlan plan_ring(const Engine &e, const std::vector<SegmentData *> &segs, cons
     rp.field_shift[a] = it->second;
   }
   if (bits > 53) return rp;
-  // allocation: every doc of the largest block matching
+  // regions: every doc of the largest block matching, keys spread evenly (+ slack; beyond it the counted plan answers)
   const int64_t max_docs = (total_chunks + (int64_t)nblk - 1) / (int64_t)nblk * 4096;
   const uint32_t cap = ring_region_records((uint64_t)max_docs, K, ks.G, UINT32_MAX);
   if (cap > (1u << 20)) return rp;
@@ -2695,8 +2713,10 @@ unsigned long long compact_dense(Engine &e, const unsigned long long *counts, in
 
 // Device half of build_dense_result: the final arrays of the n non-empty groups in the host result's layout
 // (k_group_final) and the HLL registers gathered per group, all on the device (no sync).
+// compact_ok: the keys are every non-empty key of [0, G) (the compact read-back lists them from a bitmap of the
+// counts); false for a subset (the device trim's kept union) or when only device arrays are wanted.
 DenseOut dense_outputs(Engine &e, const DenseGroups &d, const long long *keys_dev, unsigned long long n,
-                       bool gather_hll = true) {
+                       bool gather_hll = true, bool compact_ok = true, bool serialize_hll = false) {
   const pinot_query &q = *d.q;
   const GroupAccs &ga = *d.ga, &gx = *d.gx;
   const std::vector<int> &alias = *d.alias;
@@ -2724,7 +2744,7 @@ DenseOut dense_outputs(Engine &e, const DenseGroups &d, const long long *keys_de
   }
   const size_t n8 = n * 8;
   // compact read-back: keys as a bitmap over [0, G), counts / cardinalities as u32 (half the PCIe bytes)
-  const bool compact = e.compact_d2h && !d.hashed && n >= (1u << 16) && d.ks->G > 0;
+  const bool compact = compact_ok && e.compact_d2h && !d.hashed && n >= (1u << 16) && d.ks->G > 0;
   const size_t key_words = compact ? (size_t)((d.ks->G + 63) / 64) : 0;
   const size_t compact_bytes = compact ? key_words * 8 + n * 4 * (1 + n_card) + 64 : 0;
   e.group_out.reserve(n8 * (2 + na + n_card) + 256 + compact_bytes);
@@ -2795,6 +2815,23 @@ DenseOut dense_outputs(Engine &e, const DenseGroups &d, const long long *keys_de
       }
     for (int i = 0; i < na; i++)
       if (alias[i] >= 0 && ga.acc_kind[i] == 4) o.hll_off[i] = o.hll_off[alias[i]];
+    if (serialize_hll) {  // HyperLogLog.getBytes of every listed group, for the DataTable (hll_serde.hip)
+      const size_t need = (size_t)n_hll * n * 180 + 16;
+      if (!e.hll_ser || e.hll_ser.use_count() > 1 || e.hll_ser->size() < need)
+        e.hll_ser = std::make_shared<DeviceBuffer>(need + need / 4);
+      o.hll_ser = e.hll_ser;
+      o.hll_ser_off.assign(na, 0);
+      int s = 0;
+      for (int i = 0; i < na; i++)
+        if (gx.acc_kind[i] == 4) {
+          o.hll_ser_off[i] = (size_t)s * n * 180;
+          launch_hll_getbytes(o.hll->get<uint8_t>() + o.hll_off[i], (long long)n, o.hll_ser->get<uint8_t>() + o.hll_ser_off[i],
+                              e.stream);
+          s++;
+        }
+      for (int i = 0; i < na; i++)
+        if (alias[i] >= 0 && ga.acc_kind[i] == 4) o.hll_ser_off[i] = o.hll_ser_off[alias[i]];
+    }
     PINOT_HIP(hipGetLastError());
   }
   return o;
@@ -2919,6 +2956,15 @@ std::unique_ptr<GroupByResult> dense_fetch(Engine &e, const pinot_query &q, cons
     res->values[i].resize(n);
     if (o.kind[i] == 4) res->hll_card[i].resize(n);
   }
+  if (o.hll_ser) {  // the serialized HLL rows, in the same stream ahead of the arrays' copies and their wait
+    res->hll_bytes.assign(na, {});
+    for (int i = 0; i < na; i++)
+      if (o.kind[i] == 4) {
+        res->hll_bytes[i].resize(n * 180);
+        PINOT_HIP(hipMemcpyAsync(res->hll_bytes[i].data(), o.hll_ser->get<uint8_t>() + o.hll_ser_off[i], n * 180,
+                                 hipMemcpyDeviceToHost, e.stream));
+      }
+  }
   const auto tb1 = std::chrono::steady_clock::now();
   const size_t n8 = n * 8;
   if (o.key_bits && compact_fetch(e, res.get(), o, na)) {
@@ -2983,8 +3029,8 @@ std::unique_ptr<GroupByResult> dense_fetch(Engine &e, const pinot_query &q, cons
 }
 
 std::unique_ptr<GroupByResult> build_dense_result(Engine &e, const DenseGroups &d, const long long *keys_dev,
-                                                  unsigned long long n) {
-  const DenseOut o = dense_outputs(e, d, keys_dev, n);
+                                                  unsigned long long n, bool subset = false) {
+  const DenseOut o = dense_outputs(e, d, keys_dev, n, true, !subset, subset);
   return dense_fetch(e, *d.q, d.ks->gcard, d.ks->gvalues, o, d.hashed);
 }
 
@@ -2999,7 +3045,7 @@ const long long *device_trim(Engine &e, const DenseGroups &d, const long long *k
   if ((int64_t)n <= 4 * T || d.hashed) return keys_dev;
   const pinot_query &q = *d.q;
   const int na = q.num_aggregations;
-  const DenseOut o = dense_outputs(e, d, keys_dev, n, false);  // comparable values of every group, no registers
+  const DenseOut o = dense_outputs(e, d, keys_dev, n, false, false);  // comparable values of every group, no registers
   const size_t scr = trim_scratch_bytes((long long)n);
   const size_t a8 = ((size_t)n * 8 + 255) / 256 * 256, a4 = ((size_t)n * 4 + 255) / 256 * 256;
   e.group_trim.reserve(a8 + 2 * a4 + 256 + scr);
@@ -3094,7 +3140,7 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     cstart[si + 1] = cstart[si] + n;
   }
   RingPlan rp;
-  if (e.group_ring && gp.mode == GB_EMIT && !ks.hashed && !adm.active && !pin && e.debug_emit == 0 && e.group_prefetch &&
+  if (e.group_ring && gp.mode == GB_EMIT && !ks.hashed && !adm.active && !pin && e.group_prefetch &&
       e.group_lw == 2 && e.group_bucket && e.group_pshift < 0)
     rp = plan_ring(e, segs, q, ks, gx, cstart[S]);
   // a ring region overflowed (keys skewed beyond the regions' slack) or a bound tripped: the counted plan answers
@@ -3245,10 +3291,9 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
   a.shift = gp.shift;
   a.P = (int32_t)gp.P;
   a.mode = gp.mode == GB_EMIT ? GB_COUNT : gp.mode;
-  a.reserved2 = e.debug_emit;  // timing experiments only (debug.emit)
   a.nt_store = e.group_nt_store;
   // the prefetched column list: GB_EMIT's record fields, or GB_LDS's lane-owns-quarter reads (group.lw=2)
-  if (((gp.mode == GB_EMIT && (e.debug_emit == 0 || e.debug_emit >= 3)) || (gp.mode == GB_LDS && e.group_lw == 2)) &&
+  if ((gp.mode == GB_EMIT || (gp.mode == GB_LDS && e.group_lw == 2)) &&
       !ks.hashed && e.group_prefetch) {
     int nc = q.num_group_by;
     for (int i = 0; i < na && nc <= kGroupPfCols; i++)
@@ -3343,34 +3388,47 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
   const auto tgu = std::chrono::steady_clock::now();
   uint32_t *ring_status = nullptr;  // ring plan: [0] status bits, [1] region records (k_group_ring)
   if (pin) {
-  } else if (rp.on) {  // GB_FILTER -> k_group_ring -> k_ring_reduce (group_ring.hip): every key written, no memset
+  } else if (rp.on) {  // [GB_FILTER ->] k_group_ring -> k_ring_reduce (group_ring.hip): every key written, no memset
     const size_t nblk = (size_t)rp.nblk;
     const size_t hist_n = (size_t)rp.P * nblk;
-    const size_t hist_b = (hist_n * 4 + 255) / 256 * 256, bm_b = (nblk * 4 + 255) / 256 * 256;
-    e.group_part.reserve(hist_b + bm_b + 256);
+    const size_t hist_b = (hist_n * 4 + 255) / 256 * 256;
+    e.group_part.reserve(hist_b + 256);
     uint8_t *pb = e.group_part.get<uint8_t>();
     auto *hist = reinterpret_cast<uint32_t *>(pb);
-    auto *blk_matched = reinterpret_cast<uint32_t *>(pb + hist_b);
-    ring_status = reinterpret_cast<uint32_t *>(pb + hist_b + bm_b);
+    ring_status = reinterpret_cast<uint32_t *>(pb + hist_b);
     e.group_records.reserve((size_t)rp.P * nblk * rp.cap * 8 + 64);
-    int64_t fstride = 0;
-    for (auto *sg : segs) fstride = std::max<int64_t>(fstride, sg->nwords());
-    fstride = (fstride + 63) / 64 * 64;
-    e.group_filter.reserve((size_t)S * fstride * 8 + 512);
+    // the filter: a top-level conjunction of <= kRingMaxQuarterLeaves scan leaves (RANGE / LUT, <= 20 bits) is
+    // evaluated by the ring kernel itself on each quarter; any other program runs first as GB_FILTER
+    int nf = 0;
+    for (size_t si = 0; si < S && nf >= 0; si++) {
+      const GroupSegment &g = gsegs[si];
+      if (g.nwords == 0) continue;
+      if (g.n_leaves > kRingMaxQuarterLeaves) nf = -1;
+      for (int i = 0; i < g.n_leaves && nf >= 0; i++) {
+        const FusedStep &l = leaves[g.first_leaf + i];
+        const bool ok = l.join == JOIN_NEW && l.bits <= kGroupLwMaxBits &&
+                        (l.kind == FK_LEAF_RANGE || l.kind == FK_LEAF_LUT64 || l.kind == FK_LEAF_LUT);
+        nf = ok ? std::max(nf, g.n_leaves) : -1;
+      }
+    }
+    if (!e.group_ring_qfilter) nf = -1;
     GroupArgs af = a;
-    af.mode = GB_FILTER;
-    af.filter_out = e.group_filter.get<uint64_t>();
-    af.filter_stride = fstride;
-    af.cstart = reinterpret_cast<const int64_t *>(qs.arena + off_cstart);
-    af.total_chunks = rp.total_chunks;
-    af.ring_blocks = (int32_t)nblk;
-    af.blk_matched = blk_matched;
+    int64_t fstride = 0;
+    if (nf < 0) {
+      for (auto *sg : segs) fstride = std::max<int64_t>(fstride, sg->nwords());
+      fstride = (fstride + 63) / 64 * 64;
+      e.group_filter.reserve((size_t)S * fstride * 8 + 512);
+      af.mode = GB_FILTER;
+      af.filter_out = e.group_filter.get<uint64_t>();
+      af.filter_stride = fstride;
+    }
     RingArgs ra{};
     ra.segs = a.segs;
     ra.gcols = a.gcols;
     ra.aggs = a.aggs;
-    ra.cstart = af.cstart;
-    ra.filter = af.filter_out;
+    ra.leaves = a.leaves;
+    ra.cstart = reinterpret_cast<const int64_t *>(qs.arena + off_cstart);
+    ra.filter = nf < 0 ? af.filter_out : nullptr;
     ra.filter_stride = fstride;
     ra.total_chunks = rp.total_chunks;
     ra.G = ks.G;
@@ -3382,12 +3440,12 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     ra.shift = rp.shift;
     ra.nblk = (int32_t)nblk;
     ra.cap = rp.cap;
-    ra.debug = e.debug_ring;
-    ra.blk_matched = blk_matched;
+    ra.nf = nf;
     ra.records = e.group_records.get<unsigned long long>();
     ra.hist = hist;
     ra.status = ring_status;
     ra.region = ring_status + 1;
+    ra.matched = matched;  // the quarter-form filter counts each segment's matching docs (GB_FILTER does otherwise)
     RingReduceArgs rr{};
     rr.records = ra.records;
     rr.hist = hist;
@@ -3408,10 +3466,12 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
       rr.aggs[i].lds_off = rp.lds_off[i];
     }
     require(a.pf_nc > 0, PINOT_ERR_DEVICE, "ring plan without its column list");
-    PINOT_HIP(hipMemsetAsync(blk_matched, 0, bm_b + 256, e.stream));
+    PINOT_HIP(hipMemsetAsync(ring_status, 0, 256, e.stream));
     e.ring_queries++;
+    if (nf >= 0) e.ring_qfilter_queries++;
+    e.last_group_instance = kRingInstanceCode;
     t.timed(1, [&] {
-      launch_group_query(af, e.stream);
+      if (nf < 0) launch_group_query(af, e.stream);
       launch_group_ring(ra, e.stream);
       launch_ring_reduce(rr, e.stream);
     });
@@ -3420,6 +3480,7 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     PINOT_HIP(hipMemsetAsync(counts, 0, ks.G * 8, e.stream));
     for (int i = 0; i < na; i++)
       if (acc_bytes[i]) PINOT_HIP(hipMemsetAsync(accs[i], gx.acc_kind[i] == 2 ? 0xFF : 0, ks.G * acc_bytes[i], e.stream));
+    e.last_group_instance = group_query_instance(a);
     t.timed(1, [&] { launch_group_query(a, e.stream); });
     PINOT_HIP(hipGetLastError());
     if (ks.hashed) {  // every doc's tuple == its slot representative's tuple, or the fingerprints collided
@@ -3444,8 +3505,7 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     // bucketed plan: COUNT keeps the filter words, GB_EMIT2 writes whole LDS buckets into the final layout; the
     // lane-owns-quarter sink pads every (partition, block) run to whole 64-B buckets (aligned flushes)
     const bool bucket = e.group_bucket && a.pf_nc > 0 && gp.P <= kBucketMaxPartitions &&
-                        gp.record_bits <= kRecPartShift && gp.P <= (int64_t(1) << (63 - kRecPartShift)) &&
-                        (e.debug_emit == 0 || e.debug_emit >= 3);
+                        gp.record_bits <= kRecPartShift && gp.P <= (int64_t(1) << (63 - kRecPartShift));
     const bool aligned = bucket && a.lw == 2 && e.group_aligned;
     const int64_t pad_records = aligned ? (int64_t)hist_n * (kBucketRecs - 1) : 0;
     require(max_records + pad_records < (int64_t)UINT32_MAX, PINOT_ERR_UNSUPPORTED,
@@ -3490,15 +3550,17 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
       if (bucket) {
         a2.mode = GB_EMIT2;
         a2.stage_bytes = 0;  // no filter re-evaluation: the COUNT pass's words
+        e.last_group_instance = group_query_instance(a2);
         launch_group_query(a2, e.stream);
       } else {
         a2.mode = GB_EMIT;
         a2.split = gp.split;
+        e.last_group_instance = group_query_instance(a2);
         launch_group_query(a2, e.stream);
         launch_partition_split(hist, offsets, pstart, (int32_t)gp.P, (int32_t)nblk, gp.shift, gp.split, a.emit,
                                e.group_records.get<unsigned long long>(), e.group_nt_store, e.stream);
       }
-      if (e.debug_emit != 5) launch_partition_reduce(ra, e.stream);  // debug.emit=5: timing of the passes before it
+      launch_partition_reduce(ra, e.stream);
     });
     PINOT_HIP(hipGetLastError());
   }
@@ -3515,8 +3577,6 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     if (ring_status) PINOT_HIP(hipMemcpyAsync(rs, ring_status, 16, hipMemcpyDeviceToHost, e.stream));
     PINOT_HIP(hipEventRecord(e.ev_stop, e.stream));
     wait_stream(e);
-    e.ring_waits += rs[2];
-    e.ring_sleeps += rs[3];
     if (rs[0]) return ring_fallback();
     float pms = 0;
     PINOT_HIP(hipEventElapsedTime(&pms, e.ev_start, e.ev_stop));
@@ -3540,8 +3600,6 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     if (ks.hashed) PINOT_HIP(hipMemcpyAsync(&verify_err, a.verify_err, 4, hipMemcpyDeviceToHost, e.stream));
     if (ring_status) PINOT_HIP(hipMemcpyAsync(rs, ring_status, 16, hipMemcpyDeviceToHost, e.stream));
   });
-  e.ring_waits += rs[2];
-  e.ring_sleeps += rs[3];
   if (rs[0]) return ring_fallback();
   if (verify_err) {  // 64-bit fingerprint collision: retry with another seed
     require(attempt < 3, PINOT_ERR_DEVICE, "group-key fingerprint collisions persist");
@@ -3553,7 +3611,7 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
   unsigned long long nres = n;
   const long long *rkeys = keys_dev;
   if (e.trim_top_n > 0) rkeys = device_trim(e, dg, keys_dev, nres, e.trim_top_n, kept);
-  auto res = build_dense_result(e, dg, rkeys, nres);
+  auto res = build_dense_result(e, dg, rkeys, nres, rkeys != keys_dev);
   res->merged_groups = (int64_t)n;  // before the trim: CombineGroupByOperator's numGroupsLimitReached test
   if (!kept.empty()) {
     res->trimmed_top_n = e.trim_top_n;

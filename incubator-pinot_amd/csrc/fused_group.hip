@@ -242,25 +242,14 @@ __device__ __forceinline__ void group_chunk(const GroupArgs &a, const GroupSegme
         for (int u = 0; u < kGroupUnroll; u++)
           rec[u] |= (unsigned long long)decode_doc(ag.fwd, ag.bits, doc[u]) << ag.field_shift;
       }
-      if (a.reserved2 == 0) {
-        // all cursor claims first (inactive lanes add 0: no divergent branch around the LDS atomics, one
-        // lgkmcnt wait), then the stores; the runs' lines combine in L2
-        uint32_t pos[kGroupUnroll];
+      // all cursor claims first (inactive lanes add 0: no divergent branch around the LDS atomics, one lgkmcnt
+      // wait), then the stores; the runs' lines combine in L2
+      uint32_t pos[kGroupUnroll];
 #pragma unroll
-        for (int u = 0; u < kGroupUnroll; u++) pos[u] = atomicAdd(&plds[key[u] >> rshift], act[u] ? 1u : 0u);
-#pragma unroll
-        for (int u = 0; u < kGroupUnroll; u++)
-          if (act[u]) a.emit[pos[u]] = rec[u];
-      }
+      for (int u = 0; u < kGroupUnroll; u++) pos[u] = atomicAdd(&plds[key[u] >> rshift], act[u] ? 1u : 0u);
 #pragma unroll
       for (int u = 0; u < kGroupUnroll; u++)
-        if (act[u]) {
-          if (a.reserved2 == 1) {  // debug.emit=1 (timing only, wrong results): sequential stores
-            a.emit[doc[u]] = rec[u];
-          } else if (a.reserved2 == 2) {  // debug.emit=2: LDS cursor only
-            atomicAdd(&plds[key[u] >> a.shift], 1u);
-          }
-        }
+        if (act[u]) a.emit[pos[u]] = rec[u];
     } else {
       unsigned long long *cnt_g = a.counts;
       uint32_t *cnt_l = reinterpret_cast<uint32_t *>(acc_lds);
@@ -297,8 +286,6 @@ __device__ __forceinline__ void group_sink(const GroupArgs &a, uint32_t *plds, c
     for (int u = 0; u < U; u++)
       if (act[u]) atomicAdd(&plds[key[u] >> a.shift], 1u);
   } else if constexpr (MODE == GB_EMIT2) {
-    if (a.reserved2 == 4) return;  // debug.emit=4 (timing only, wrong results): reads + decode, no sink
-    const bool st = a.reserved2 != 3;  // debug.emit=3: bucket logic without the global stores
     // LDS [cursor P][count P][written P][bucket P x kBucketRecs]. Per batch of U words: every record claims a
     // slot (count), writes it and bumps `written`; the record that completes a bucket (written ==
     // kBucketRecs - 1) flushes it: the wave moves its flushers' buckets out eight lanes per bucket (one coalesced
@@ -324,7 +311,7 @@ __device__ __forceinline__ void group_sink(const GroupArgs &a, uint32_t *plds, c
                 (uint32_t)kBucketRecs - 1;
       } else if (act[u]) {
         const uint32_t d = atomicAdd(&cur[p[u]], 1u);
-        if (st) a.emit[d] = r[u];
+        a.emit[d] = r[u];
       }
     }
 #pragma unroll
@@ -337,7 +324,7 @@ __device__ __forceinline__ void group_sink(const GroupArgs &a, uint32_t *plds, c
         const int f = min(f0 + lane / kBucketRecs, nf - 1), i = lane % kBucketRecs;
         const int src = select_bit(fm, f);
         const uint32_t pf = (uint32_t)__shfl((int)p[u], src, 64), df = (uint32_t)__shfl((int)dst, src, 64);
-        if (st && f0 + lane / kBucketRecs < nf) a.emit[df + i] = bkt[pf * kBucketRecs + i];
+        if (f0 + lane / kBucketRecs < nf) a.emit[df + i] = bkt[pf * kBucketRecs + i];
       }
       if (fl[u]) {
         __hip_atomic_store(&wrt[p[u]], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -652,8 +639,6 @@ __device__ __forceinline__ uint32_t rec_partition(unsigned long long r) {
 
 __device__ __forceinline__ void emit2_sink16(const GroupArgs &a, uint32_t *plds, uint32_t act,
                                              const unsigned long long (&rec)[16], int lane) {
-  if (a.reserved2 == 4) return;  // debug.emit=4 (timing only, wrong results): reads + decode, no sink
-  const bool st = a.reserved2 != 3;  // debug.emit=3: bucket logic without the global stores
   uint32_t *cur = plds, *cnt = plds + a.P;
   unsigned long long *bkt = reinterpret_cast<unsigned long long *>(plds + ((3 * a.P + 3) & ~3));
   unsigned long long *flist = bkt + (size_t)a.P * kBucketRecs + (threadIdx.x >> 6) * 64;
@@ -683,7 +668,7 @@ __device__ __forceinline__ void emit2_sink16(const GroupArgs &a, uint32_t *plds,
         d[j] = a.aligned_runs ? atomicSub(&back[rec_partition(rec[j])], 1u) - 1u : atomicAdd(&cur[rec_partition(rec[j])], 1u);
 #pragma unroll
     for (int j = 0; j < 16; j++)
-      if (((over >> j) & 1u) && st) a.emit[d[j]] = rec[j];
+      if ((over >> j) & 1u) a.emit[d[j]] = rec[j];
   }
   while (true) {
     const uint64_t fm = __ballot(flush != 0);
@@ -708,7 +693,7 @@ __device__ __forceinline__ void emit2_sink16(const GroupArgs &a, uint32_t *plds,
         unsigned long long *slot = &bkt[(uint32_t)e * kBucketRecs + i];
         unsigned long long v = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         while (!(v & kRecValid)) v = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (st) a.emit[(uint32_t)(e >> 32) + i] = v & ~kRecValid;
+        a.emit[(uint32_t)(e >> 32) + i] = v & ~kRecValid;
         __hip_atomic_store(slot, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     }
@@ -1051,14 +1036,7 @@ __global__ __launch_bounds__(BLK, MINW) void k_group_query(GroupArgs a) {
         a.filter_out[(size_t)g * a.filter_stride + w] = mask;
     }
     matched += __popcll(mask);
-    if constexpr (MODE == GB_FILTER) {  // the chunk's matching docs to the ring block that will read it
-      const unsigned long long cc = wave_sum((unsigned long long)__popcll(mask));
-      if (lane == 0 && cc) {
-        const int64_t gc = load_const(a.cstart + g) + (ch - sg.ch_begin);
-        atomicAdd(a.blk_matched + (int)(gc * a.ring_blocks / a.total_chunks), (uint32_t)cc);
-      }
-      continue;
-    }
+    if constexpr (MODE == GB_FILTER) continue;  // the filter words only (the ring plan reads them)
     if (__any(mask != 0)) {
       if constexpr (PATH == 3) group_chunk_lq<MODE>(a, sg, ch, mask, lane, plds);
       else if constexpr (PATH == 4) group_chunk_lq<MODE, 3>(a, sg, ch, mask, lane, plds);  // <= 3 columns read
@@ -1101,44 +1079,52 @@ static int group_block_threads(const GroupArgs &a) {
   return (a.lw && (a.mode == GB_EMIT || a.mode == GB_EMIT2)) ? kGroupLwEmitBlock : kGroupBlock;
 }
 
-// Every instance launch_group_query may pick for `a`, through one visitor (occupancy and launch agree).
+// Every instance launch_group_query may pick for `a`, through one visitor (occupancy and launch agree); the visitor
+// also gets the instance's code (mode * 10000 + read path * 1000 + threads per block, group.last_instance).
 template <typename V>
 static void with_group_kernel(const GroupArgs &a, V &&v) {
   const bool lw = a.lw && a.pf_nc > 0, lh = lw && a.lw == 2;
+#define PINOT_GQ(M, P, B, W) v(&k_group_query<M, P, B, W>, B, (int)(M) * 10000 + (P) * 1000 + (B))
   switch (a.mode) {
-    case GB_GLOBAL: v(&k_group_query<GB_GLOBAL, 0, kGroupBlock>, kGroupBlock); break;
+    case GB_GLOBAL: PINOT_GQ(GB_GLOBAL, 0, kGroupBlock, 1); break;
     case GB_LDS:
-      if (lh && a.emit_block == 256) v(&k_group_query<GB_LDS, 3, 256, 3>, 256);  // 3 blocks of 4 waves per CU
-      else if (lh && a.pf_nc <= 3) v(&k_group_query<GB_LDS, 4, kGroupLwEmitBlock, 4>, kGroupLwEmitBlock);
-      else if (lh) v(&k_group_query<GB_LDS, 3, kGroupLwEmitBlock, 4>, kGroupLwEmitBlock);  // 4 waves per SIMD: 2 blocks per CU
-      else v(&k_group_query<GB_LDS, 0, kGroupBlock>, kGroupBlock);
+      if (lh && a.emit_block == 256) PINOT_GQ(GB_LDS, 3, 256, 3);  // 3 blocks of 4 waves per CU
+      else if (lh && a.pf_nc <= 3) PINOT_GQ(GB_LDS, 4, kGroupLwEmitBlock, 4);
+      else if (lh) PINOT_GQ(GB_LDS, 3, kGroupLwEmitBlock, 4);  // 4 waves per SIMD: 2 blocks per CU
+      else PINOT_GQ(GB_LDS, 0, kGroupBlock, 1);
       break;
     case GB_COUNT:
-      if (lh && a.n_gcols <= kLqCountCols) v(&k_group_query<GB_COUNT, 3, kGroupBlock>, kGroupBlock);
-      else if (lw) v(&k_group_query<GB_COUNT, 2, kGroupBlock>, kGroupBlock);
-      else if (a.pf_nc > 0) v(&k_group_query<GB_COUNT, 1, kGroupBlock>, kGroupBlock);
-      else v(&k_group_query<GB_COUNT, 0, kGroupBlock>, kGroupBlock);
+      if (lh && a.n_gcols <= kLqCountCols) PINOT_GQ(GB_COUNT, 3, kGroupBlock, 1);
+      else if (lw) PINOT_GQ(GB_COUNT, 2, kGroupBlock, 1);
+      else if (a.pf_nc > 0) PINOT_GQ(GB_COUNT, 1, kGroupBlock, 1);
+      else PINOT_GQ(GB_COUNT, 0, kGroupBlock, 1);
       break;
     case GB_EMIT:
-      if (lh) v(&k_group_query<GB_EMIT, 3, kGroupLwEmitBlock>, kGroupLwEmitBlock);
-      else if (lw) v(&k_group_query<GB_EMIT, 2, kGroupLwEmitBlock>, kGroupLwEmitBlock);
-      else if (a.pf_nc > 0) v(&k_group_query<GB_EMIT, 1, kGroupBlock>, kGroupBlock);
-      else v(&k_group_query<GB_EMIT, 0, kGroupBlock>, kGroupBlock);
+      if (lh) PINOT_GQ(GB_EMIT, 3, kGroupLwEmitBlock, 1);
+      else if (lw) PINOT_GQ(GB_EMIT, 2, kGroupLwEmitBlock, 1);
+      else if (a.pf_nc > 0) PINOT_GQ(GB_EMIT, 1, kGroupBlock, 1);
+      else PINOT_GQ(GB_EMIT, 0, kGroupBlock, 1);
       break;
-    case GB_FIRST: v(&k_group_query<GB_FIRST, 0, kGroupBlock>, kGroupBlock); break;
-    case GB_FILTER: v(&k_group_query<GB_FILTER, 0, kGroupBlock>, kGroupBlock); break;
+    case GB_FIRST: PINOT_GQ(GB_FIRST, 0, kGroupBlock, 1); break;
+    case GB_FILTER: PINOT_GQ(GB_FILTER, 0, kGroupBlock, 1); break;
     case GB_EMIT2:
-      if (lh && a.emit_block == kGroupLqEmitBlockWide)
-        v(&k_group_query<GB_EMIT2, 3, kGroupLqEmitBlockWide>, kGroupLqEmitBlockWide);
-      else if (lh) v(&k_group_query<GB_EMIT2, 3, kGroupLwEmitBlock>, kGroupLwEmitBlock);
-      else if (lw) v(&k_group_query<GB_EMIT2, 2, kGroupLwEmitBlock>, kGroupLwEmitBlock);
-      else v(&k_group_query<GB_EMIT2, 1, kGroupBlock>, kGroupBlock);
+      if (lh && a.emit_block == kGroupLqEmitBlockWide) PINOT_GQ(GB_EMIT2, 3, kGroupLqEmitBlockWide, 1);
+      else if (lh) PINOT_GQ(GB_EMIT2, 3, kGroupLwEmitBlock, 1);
+      else if (lw) PINOT_GQ(GB_EMIT2, 2, kGroupLwEmitBlock, 1);
+      else PINOT_GQ(GB_EMIT2, 1, kGroupBlock, 1);
       break;
-    default: v(&k_group_query<GB_VERIFY, 0, kGroupBlock>, kGroupBlock); break;
+    default: PINOT_GQ(GB_VERIFY, 0, kGroupBlock, 1); break;
   }
+#undef PINOT_GQ
 }
 
 }  // namespace
+
+int group_query_instance(const GroupArgs &a) {
+  int code = 0;
+  with_group_kernel(a, [&](auto, int, int c) { code = c; });
+  return code;
+}
 
 size_t group_query_lds_bytes(const GroupArgs &a) {
   size_t acc = 0;
@@ -1153,14 +1139,14 @@ int group_query_blocks_per_cu(const GroupArgs &a) {
   int n = 0;
   const size_t lds = group_query_lds_bytes(a);
   hipError_t err = hipErrorInvalidValue;
-  with_group_kernel(a, [&](auto kern, int threads) { err = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, threads, lds); });
+  with_group_kernel(a, [&](auto kern, int threads, int) { err = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, threads, lds); });
   return (err != hipSuccess || n < 1) ? 1 : n;
 }
 
 void launch_group_query(const GroupArgs &a, hipStream_t stream) {
   if (a.nsegs <= 0 || a.bps <= 0) return;
   const size_t lds = group_query_lds_bytes(a);
-  with_group_kernel(a, [&](auto kern, int threads) {
+  with_group_kernel(a, [&](auto kern, int threads, int) {
     hipLaunchKernelGGL(kern, dim3((unsigned)(a.nsegs * a.bps)), dim3(threads), lds, stream, a);
   });
 }

@@ -1,0 +1,10 @@
+// Shape limits of the ring-partitioned group-by plan (group_ring.hip), shared with its planner (executor.cpp).
+#pragma once
+
+namespace pinot {
+// Column slots of the ring decoder: at most kRingGroupCols group columns and kRingAggCols distinct aggregated columns
+// (a record's dictId fields), each at most kGroupLwMaxBits wide.
+constexpr int kRingGroupCols = 2, kRingAggCols = 2;
+// Partitions (of K <= 1024 consecutive keys) a ring block holds in LDS: 16 entries of 8 B + an 8-B counter each.
+constexpr int kRingMaxPartitions = 1024;
+}  // namespace pinot

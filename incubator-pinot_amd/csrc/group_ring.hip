@@ -1,14 +1,15 @@
 // Ring-partitioned group-by (the large-key-space plan, config 4): no histogram pass, fixed-capacity regions.
 //
-//   k_group_query<GB_FILTER>  (fused_group.hip) the filter program once: filter words per segment + the matching docs
-//                        of every ring block (region sizing), no group column read.
-//   k_group_ring         one block per CU, every wave a loader: per 1024-doc quarter each lane decodes its 16 docs'
-//                        group key and aggregated dictIds (lane-owns-quarter reads, the next quarter's loads in
-//                        flight while this one is sunk) into u64 records (local key | dictId fields | partition) and
-//                        appends them to its partition's LDS ring of 16 slots (two halves of 8). The lane whose
-//                        write completes a half moves it to the block's region of that partition as one aligned 64-B
-//                        piece: region (p, block) holds records [0, n) in claim order, so every flush lands on its own
-//                        64-B sector and no histogram, scan or cursor leaves the CU.
+//   k_group_ring         one block of 16 waves per CU over a contiguous range of chunks. Waves 0..13 (decoders) read
+//                        each 1024-doc quarter lane-owns-quarter (lane l: docs 16l .. 16l + 15), evaluate the
+//                        segment's top-level conjunction of scan leaves on it (or take GB_FILTER's words for other
+//                        filter shapes), decode the group key and aggregated dictIds into u64 records (local key |
+//                        dictId fields) and append each to its partition's LDS ring of 16 entries (two halves of 8):
+//                        one 64-bit LDS add claims an entry and returns how many records the partition has moved out,
+//                        so a decoder never issues an HBM store (its vmcnt holds its own loads only). Waves 14, 15
+//                        (flushers) sweep the partitions and move every completed half to the block's region of that
+//                        partition as one aligned 64-B piece: region (p, block) holds records [0, n) in claim order,
+//                        so no histogram, scan or cursor leaves the CU.
 //   k_ring_reduce        one block per partition of K <= 1024 consecutive keys: the partition's records from every
 //                        block's region folded into LDS accumulators (count packed beside the first affine dictId
 //                        SUM, int64 / double sums, ordered min / max, HLL registers as 4-bit nibbles with the rare
@@ -16,18 +17,20 @@
 //
 // Restates DictionaryBasedGroupKeyGenerator.generateKeysForBlock (raw key = mixed radix over the group columns'
 // dictIds, PC/query/aggregation/groupby/DictionaryBasedGroupKeyGenerator.java:195-302) and DefaultGroupByExecutor
-// .process / aggregateGroupBySV (PC/query/aggregation/groupby/DefaultGroupByExecutor.java:70-168). Region sizes come
-// from the filter's per-block match counts; a partition whose records exceed its region (skewed keys) sets a status
-// bit and the host answers the query on the counted plan instead (executor.cpp).
+// .process / aggregateGroupBySV (PC/query/aggregation/groupby/DefaultGroupByExecutor.java:70-168); the quarter-form
+// filter restates ScanBasedFilterOperator over the dictionary predicate evaluators (fused_common.h). Regions are sized
+// for every doc of the busiest block matching with uniform keys; a partition whose records exceed its region (skewed
+// keys) sets a status bit and the host answers the query on the counted plan instead (executor.cpp).
 #include <hip/hip_runtime.h>
 
 #include "fused_common.h"
 #include "group_lq.h"
+#include "group_ring.h"
 
 namespace pinot {
 
-// Records per region: the busiest block's matching docs spread over the partitions by key share, + 12.5 % + 64,
-// a multiple of 16 (128-B aligned regions), never above the allocation.
+// Records per region: the busiest block's docs spread over the partitions by key share, + 12.5 % + 64, a multiple of
+// 16 (128-B aligned regions), never above the allocation.
 __host__ __device__ uint32_t ring_region_records(uint64_t max_block_docs, int64_t K, int64_t G, uint32_t cap) {
   const uint64_t mean = (max_block_docs * (uint64_t)K + (uint64_t)G - 1) / (uint64_t)G;
   uint64_t c = mean + mean / 8 + 64;
@@ -38,141 +41,111 @@ __host__ __device__ uint32_t ring_region_records(uint64_t max_block_docs, int64_
 namespace {
 using namespace dev;
 
-constexpr int kRingBlock = 512;  // 8 waves: the 16-record sink and the next quarter's raw loads need the registers
+constexpr int kRingBlock = 768;                             // one block of 12 waves per CU (the buckets take the LDS)
 constexpr int kRingWaves = kRingBlock / 64;
-constexpr int kRecPShift = 53;  // records carry their partition in bits [53, 64)
+constexpr int kRingFlushWaves = 3;                           // waves 9..11: the flush phases
+constexpr int kRingDecWaves = kRingWaves - kRingFlushWaves;  // waves 0..8: filter, decode, insert
+constexpr int kRingRoundRecs = 8;                            // records per decoder lane between two flush phases
+constexpr int kRingBucket = 16;                              // entries per partition bucket (two 64-B halves)
+constexpr int kRecPShift = 53;                               // bucket entries carry their partition in bits [53, 63)
+constexpr int kRingBackBits = 12;                            // hist: front count (20 bits) | back count << 20
+static_assert(kRingRoundRecs * 2 == 16, "two rounds per pass");
+
+// RING_EXP_TIMING (experiment builds only): per-wave shader-clock totals of each phase, printed by a few blocks.
+#ifdef RING_EXP_TIMING
+#define RT_MARK(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define RT_ADD(acc, from) acc += __builtin_amdgcn_s_memtime() - (from)
+#else
+#define RT_MARK(v)
+#define RT_ADD(acc, from)
+#endif
 
 struct RingLds {
-  unsigned long long *ring;  // [P][16]
-  unsigned long long *meta;  // [P]: claims (bits 0-31) | half 0 laps flushed (32-47) | half 1 laps flushed (48-63)
-  uint32_t *wr;              // [P][2]: records written per half (mod 8 = 7 on the completing write)
-  uint32_t *flist;           // [waves][64]: this round's flushes (partition << 18 | half-lap)
+  unsigned long long *bkt;  // [P][16] bucket entries: record | partition << 53
+  uint32_t *ctr;            // [P]: entries in the bucket (bits 0-15; claims beyond 16 overflowed) | head (0 / 8) << 16
+  uint32_t *back;           // [P]: records written from the region's end (bucket overflow)
 };
 
 __device__ __forceinline__ RingLds ring_lds(uint8_t *lds, int P) {
   RingLds r;
-  r.ring = reinterpret_cast<unsigned long long *>(lds);
-  r.meta = r.ring + (size_t)P * 16;
-  r.wr = reinterpret_cast<uint32_t *>(r.meta + P);
-  r.flist = r.wr + 2 * P;
+  r.bkt = reinterpret_cast<unsigned long long *>(lds);
+  r.ctr = reinterpret_cast<uint32_t *>(r.bkt + (size_t)P * kRingBucket);
+  r.back = r.ctr + P;
   return r;
 }
 
-__device__ __forceinline__ uint32_t rec_part(unsigned long long r) { return (uint32_t)(r >> kRecPShift); }
+__device__ __forceinline__ uint32_t rec_part(unsigned long long r) { return (uint32_t)(r >> kRecPShift) & 1023u; }
 
-// Move the listed completed halves out: every lane that completed one lists (partition, half-lap) at its rank among
-// this round's flushing lanes, then the wave stores eight halves per instruction (8 lanes x 8 B each). The laps-flushed
-// bump follows the ring reads in this wave's LDS order, so a writer of the next lap (which waits for the bump) never
-// overwrites a slot before it has been read.
-template <int DBG>
-__device__ __forceinline__ void ring_flush(const RingArgs &a, const RingLds &L, uint32_t *fl, uint32_t comp,
-                                           const uint32_t (&pos)[16], const unsigned long long (&rec)[16],
-                                           unsigned long long *region0, uint32_t C, int lane) {
-  while (true) {
-    const uint64_t fm = __ballot(comp != 0);
-    if (!fm) break;  // uniform
-    if (comp) {
-      const int j = __builtin_ctz(comp);
-      uint32_t pj = 0, mj = 0;
+// Insert phase: record j of each of the lane's kRingRoundRecs records (J0 ..) claims the next entry of its partition's
+// bucket (one LDS add returns the claim index and the head) and is written at (head + claim) mod 16. No flush runs
+// during an insert phase (block barriers on both sides), so a claim below 16 always finds its entry free; a claim of
+// 16 or more (a bucket that received more than 9 records in one round; rare) goes to the back of its region instead.
+template <int J0>
+__device__ __forceinline__ void ring_insert(const RingArgs &a, const RingLds &L, uint32_t act,
+                                            const unsigned long long (&rec)[16], unsigned long long *region0,
+                                            uint32_t C) {
+  uint32_t old[kRingRoundRecs], p[kRingRoundRecs];
 #pragma unroll
-      for (int t = 0; t < 16; t++)
-        if (t == j) {
-          pj = rec_part(rec[t]);
-          mj = pos[t] >> 3;
-        }
-      const int f = __builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u));
-      fl[f] = (pj << 18) | mj;
-      comp &= comp - 1u;
-    }
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);  // list writes before the list reads (one wave's LDS order)
-    const int nf = __popcll(fm);
-    for (int f0 = 0; f0 < nf; f0 += 8) {  // uniform
-      const int f = f0 + (lane >> 3), r = lane & 7;
-      if (f < nf) {
-        const uint32_t e = fl[f];
-        const uint32_t p = e >> 18, m = e & 0x3FFFFu, h = m & 1u;
-        const unsigned long long v = L.ring[p * 16 + h * 8 + r];
-        if (DBG == 0 || a.debug != 2) __builtin_nontemporal_store(v, region0 + ((size_t)p * a.nblk) * C + (size_t)m * 8 + r);
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        if (r == 0) __hip_atomic_fetch_add(L.meta + p, 1ull << (32 + 16 * h), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  for (int j = 0; j < kRingRoundRecs; j++) {
+    const bool on = (act >> (J0 + j)) & 1u;
+    p[j] = on ? rec_part(rec[J0 + j]) : 0u;  // branch-free: an inactive record adds 0 to partition 0's counter
+    old[j] = atomicAdd(L.ctr + p[j], on ? 1u : 0u);
+  }
+  uint32_t over = 0;
+#pragma unroll
+  for (int j = 0; j < kRingRoundRecs; j++) {
+    const bool on = (act >> (J0 + j)) & 1u;
+    const uint32_t s = old[j] & 0xFFFFu, h = old[j] >> 16;
+    if (on && s < (uint32_t)kRingBucket) L.bkt[p[j] * kRingBucket + ((h + s) & (kRingBucket - 1))] = rec[J0 + j];
+    over |= (on && s >= (uint32_t)kRingBucket) ? (1u << j) : 0u;
+  }
+  if (__any(over != 0)) {  // uniform, rare
+#pragma unroll
+    for (int j = 0; j < kRingRoundRecs; j++)
+      if ((over >> j) & 1u) {
+        const uint32_t k = atomicAdd(L.back + p[j], 1u);
+        if (k < C) region0[((size_t)p[j] * a.nblk + 1) * C - 1 - k] = rec[J0 + j] & ((1ull << kRecPShift) - 1ull);
       }
-    }
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
   }
 }
 
-// Sink of a lane's 16 records (act: bit j = record j is live), in two batches of 8 claims. DBG = 1: the instrumented
-// instance (debug.ring modes and the wait counters), never the production one.
-template <int DBG>
-__device__ __forceinline__ void ring_sink(const RingArgs &a, const RingLds &L, uint32_t *fl, uint32_t act,
-                                          const unsigned long long (&rec)[16], unsigned long long *region0, uint32_t C,
-                                          int lane, uint32_t &over, uint32_t &waits, uint32_t &sleeps) {
-  uint32_t pos[16];
-  uint32_t todo = 0, pend = 0;
-  // claims: one 64-bit LDS add returns the claim index and both halves' flushed-lap counts
+// Flush phase (flusher waves only, between two block barriers): every bucket holding 8 or more entries moves its
+// oldest half (entries head .. head + 7: one aligned 64-B piece of LDS) to the front of its region at the partition's
+// front cursor (64-B aligned: regions start 128-B aligned and the front advances by 8 records), then the head moves
+// to the other half. Lane l of flusher wave fw owns partitions fw * 64 + l + 192 k and keeps their front cursors.
+template <int KP>
+__device__ __forceinline__ void ring_flush_phase(const RingArgs &a, const RingLds &L, unsigned long long *region0,
+                                                 uint32_t C, int fw, int lane, uint32_t (&front)[KP],
+                                                 uint32_t &status) {
+  uint32_t c[KP];
 #pragma unroll
-  for (int j0 = 0; j0 < 16; j0 += 8) {
-    unsigned long long old[8];
-#pragma unroll
-    for (int j = 0; j < 8; j++)
-      old[j] = ((act >> (j0 + j)) & 1u) ? __hip_atomic_fetch_add(L.meta + rec_part(rec[j0 + j]), 1ull, __ATOMIC_RELAXED,
-                                                                 __HIP_MEMORY_SCOPE_WORKGROUP)
-                                        : 0ull;
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-      pos[j0 + j] = (uint32_t)old[j];
-      if (!((act >> (j0 + j)) & 1u)) continue;
-      if (pos[j0 + j] >= C) {  // region full: the query falls back to the counted plan
-        over |= 1u;
-        continue;
-      }
-      const uint32_t h = (pos[j0 + j] >> 3) & 1u, lap = (pos[j0 + j] >> 4) & 0xFFFFu;
-      const uint32_t flh = (uint32_t)(old[j] >> (32 + 16 * h)) & 0xFFFFu;
-      if (flh == lap) todo |= 1u << (j0 + j);
-      else pend |= 1u << (j0 + j);
-    }
+  for (int k = 0; k < KP; k++) {
+    const int p = fw * 64 + lane + 64 * kRingFlushWaves * k;
+    c[k] = p < a.P ? L.ctr[p] : 0u;
   }
-  if (DBG && a.debug == 3) return;  // claims only
-  if (DBG && __any(pend != 0)) waits++;
-  // records whose slot still holds the previous lap (its half not yet moved out) wait for the bump and go in a later
-  // round; every wave moves out what it completed before it waits, so the half it waits for always drains
-  uint32_t spins = 0;
-  while (true) {
-    uint32_t comp = 0;
 #pragma unroll
-    for (int j = 0; j < 16; j++)
-      if ((todo >> j) & 1u) L.ring[rec_part(rec[j]) * 16 + (pos[j] & 15u)] = rec[j] & ((1ull << kRecPShift) - 1ull);
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-#pragma unroll
-    for (int j = 0; j < 16; j++)
-      if ((todo >> j) & 1u) {
-        const uint32_t w = __hip_atomic_fetch_add(L.wr + rec_part(rec[j]) * 2 + ((pos[j] >> 3) & 1u), 1u,
-                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        comp |= ((w & 7u) == 7u) ? (1u << j) : 0u;
+  for (int k = 0; k < KP; k++) {
+    const int p = fw * 64 + lane + 64 * kRingFlushWaves * k;
+    uint32_t n = min(c[k] & 0xFFFFu, (uint32_t)kRingBucket), h = c[k] >> 16;
+    if (n < 8u) continue;  // no complete half: the counter stays
+    while (n >= 8u) {
+      const u32x4 *src = reinterpret_cast<const u32x4 *>(L.bkt + p * kRingBucket + h);
+      const u32x4 x0 = src[0], x1 = src[1], x2 = src[2], x3 = src[3];
+      if (front[k] + 8u <= C) {
+        u32x4 *dst = reinterpret_cast<u32x4 *>(region0 + (size_t)p * a.nblk * C + front[k]);
+        const u32x4 m = {0xFFFFFFFFu, 0x001FFFFFu, 0xFFFFFFFFu, 0x001FFFFFu};  // strip the partition bits
+        __builtin_nontemporal_store(x0 & m, dst);
+        __builtin_nontemporal_store(x1 & m, dst + 1);
+        __builtin_nontemporal_store(x2 & m, dst + 2);
+        __builtin_nontemporal_store(x3 & m, dst + 3);
+      } else {
+        status |= 1u;  // region full: the query falls back to the counted plan
       }
-    ring_flush<DBG>(a, L, fl, comp, pos, rec, region0, C, lane);
-    if (!__any(pend != 0)) break;  // uniform
-    if (++spins > (1u << 22)) {  // bounded: a protocol fault ends the launch with a status, never a hang
-      over |= 2u;
-      break;
+      front[k] += 8u;
+      h ^= 8u;
+      n -= 8u;
     }
-    __builtin_amdgcn_s_sleep(2);
-    if (DBG) sleeps++;
-    todo = 0;
-    for (uint32_t x = pend; x; x &= x - 1u) {
-      const int j = __builtin_ctz(x);
-      uint32_t pj = 0, psj = 0;
-#pragma unroll
-      for (int t = 0; t < 16; t++)
-        if (t == j) {
-          pj = rec_part(rec[t]);
-          psj = pos[t];
-        }
-      const unsigned long long m = __hip_atomic_load(L.meta + pj, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      const uint32_t h = (psj >> 3) & 1u, lap = (psj >> 4) & 0xFFFFu;
-      if (((uint32_t)(m >> (32 + 16 * h)) & 0xFFFFu) == lap) todo |= 1u << j;
-    }
-    pend &= ~todo;
+    if (p < a.P) L.ctr[p] = (h << 16) | n;
   }
 }
 
@@ -184,25 +157,6 @@ __device__ __forceinline__ int ring_segment(const RingArgs &a, int64_t c, int g0
   return g;
 }
 
-struct RingCursor {
-  int64_t c;      // current chunk (global index), >= end: done
-  int64_t cn;     // next chunk of this wave
-  uint64_t wc;    // this lane's filter word of chunk c
-  uint64_t wn;    // ... of chunk cn (prefetched)
-  int q;          // quarter of c
-  uint32_t m;     // this lane's 16 filter bits of quarter q
-  int gn;         // segment of chunk cn (a wave's chunks ascend)
-};
-
-__device__ __forceinline__ uint64_t ring_word(const RingArgs &a, int64_t c, int64_t end, int lane, int &gs) {
-  if (c >= end) return 0ull;
-  const int g = gs = ring_segment(a, c, gs);
-  const GroupSegment sg = load_const(a.segs + g);
-  const int64_t ch = sg.ch_begin + (c - load_const(a.cstart + g));
-  const int64_t w = ch * 64 + lane;
-  return w < sg.nwords ? gload<uint64_t>(a.filter + (size_t)g * a.filter_stride + w) : 0ull;
-}
-
 // Lane l of quarter q takes docs 1024q + 16l .. +15: bits 16(l & 3) .. of the chunk word 16q + l/4.
 __device__ __forceinline__ uint32_t quarter_bits(uint64_t word, int q, int lane) {
   const int src = 16 * q + (lane >> 2);
@@ -211,192 +165,406 @@ __device__ __forceinline__ uint32_t quarter_bits(uint64_t word, int q, int lane)
   return (((lane & 2) ? hi : lo) >> (16 * (lane & 1))) & 0xFFFFu;
 }
 
-// Next quarter with a matching doc (possibly in a later chunk of this wave).
-__device__ __forceinline__ void ring_advance(const RingArgs &a, RingCursor &cu, int64_t end, int lane) {
-  cu.q++;
-  while (true) {
-    if (cu.q == 4) {
-      cu.c = cu.cn;
-      cu.wc = cu.wn;
-      cu.cn += kRingWaves;
-      cu.wn = ring_word(a, cu.cn, end, lane, cu.gn);
-      cu.q = 0;
-      if (cu.c >= end) return;
-      if (!__any(cu.wc != 0)) {  // uniform: nothing in this chunk
-        cu.q = 4;
-        continue;
-      }
-    }
-    cu.m = quarter_bits(cu.wc, cu.q, lane);
-    if (__any(cu.m != 0)) return;
-    cu.q++;
-  }
-}
-
+// Column slots of the ring decoder: [0, kRingGroupCols) group columns, then kRingAggCols aggregated columns (the
+// distinct accumulators' fields); bits 0 = unused slot.
 struct RingColsDev {
-  const uint8_t *fwd[kGroupPfCols];
-  const int32_t *remap[kGroupPfCols];
-  uint32_t stride[kGroupPfCols];
-  int bits[kGroupPfCols], fsh[kGroupPfCols];  // bits 0 = unused slot; fsh -1 = a group column (key fold)
+  const uint8_t *fwd[kRingGroupCols + kRingAggCols];
+  const int32_t *remap[kRingGroupCols];
+  uint32_t stride[kRingGroupCols];
+  int bits[kRingGroupCols + kRingAggCols], fsh[kRingGroupCols + kRingAggCols];
 };
 
-__device__ __forceinline__ RingColsDev ring_cols(const RingArgs &a, int g) {
-  const GroupSegment sg = load_const(a.segs + g);
+__device__ __forceinline__ RingColsDev ring_cols(const RingArgs &a, const GroupSegment &sg) {
   RingColsDev k;
 #pragma unroll
-  for (int c = 0; c < kGroupPfCols; c++) {
+  for (int c = 0; c < kRingGroupCols + kRingAggCols; c++) {
     k.fwd[c] = nullptr;
+    k.bits[c] = 0;
+    k.fsh[c] = 0;
+  }
+#pragma unroll
+  for (int c = 0; c < kRingGroupCols; c++) {
     k.remap[c] = nullptr;
     k.stride[c] = 0;
-    k.bits[c] = 0;
-    k.fsh[c] = -1;
-    if (c < a.nc) {
-      if (c < a.n_gcols) {
-        const GroupColDev gc = load_const(a.gcols + sg.first_gcol + c);
-        k.fwd[c] = gc.fwd;
-        k.remap[c] = gc.remap;
-        k.stride[c] = (uint32_t)gc.stride;
-        k.bits[c] = gc.bits;
-      } else {
-        const int ai = c == 1 ? a.pf_agg[1] : c == 2 ? a.pf_agg[2] : a.pf_agg[3];
-        const GroupAggDev ag = load_const(a.aggs + sg.first_agg + ai);
-        k.fwd[c] = ag.fwd;
-        k.bits[c] = ag.bits;
-        k.fsh[c] = ag.field_shift;
-      }
+    if (c < a.n_gcols) {
+      const GroupColDev gc = load_const(a.gcols + sg.first_gcol + c);
+      k.fwd[c] = gc.fwd;
+      k.remap[c] = gc.remap;
+      k.stride[c] = (uint32_t)gc.stride;
+      k.bits[c] = gc.bits;
     }
   }
+#pragma unroll
+  for (int c = 0; c < kRingAggCols; c++)
+    if (a.n_gcols + c < a.nc) {
+      const GroupAggDev ag = load_const(a.aggs + sg.first_agg + a.pf_agg[a.n_gcols + c]);
+      k.fwd[kRingGroupCols + c] = ag.fwd;
+      k.bits[kRingGroupCols + c] = ag.bits;
+      k.fsh[kRingGroupCols + c] = ag.field_shift;
+    }
   return k;
 }
 
-__device__ __forceinline__ int64_t ring_qi(const RingArgs &a, const RingCursor &cu, int lane, int &g) {
-  g = ring_segment(a, cu.c, g);
-  const GroupSegment sg = load_const(a.segs + g);
-  const int64_t ch = sg.ch_begin + (cu.c - load_const(a.cstart + g));
-  return ch * 256 + 64 * cu.q + lane;
+// Lane-owns-quarter decode that hands each of the lane's 16 values to f.put<J>(v) as it is extracted (no 16-value
+// array: the decoders' registers go to the raw dwords of the columns in flight). The raw dwords pass through an empty
+// volatile asm first, so the compiler cannot hoist the byte swaps of every width of the switch above it.
+template <int B, typename F>
+__device__ __forceinline__ void ring_decode_b(const uint32_t (&Rin)[12], int64_t qi, F &f) {
+  constexpr int N = (B + 1) / 2 + (B & 1);
+  uint32_t D[(B + 1) / 2 + 1];
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    uint32_t r = Rin[i];
+    asm volatile("" : "+v"(r));
+    D[i] = bswap32(r);
+  }
+  if constexpr (B & 1) {
+    if (qi & 1) {
+#pragma unroll
+      for (int i = 0; i + 1 < N; i++) D[i] = __builtin_amdgcn_alignbit(D[i], D[i + 1], 16);
+    }
+  }
+  decode_quarter_apply<B, 0>(D, f);
 }
 
-template <int DBG>
-__global__ __launch_bounds__(kRingBlock) void k_group_ring(RingArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int b = blockIdx.x;
-  const RingLds L = ring_lds(lds, a.P);
-  for (int i = tid; i < a.P; i += kRingBlock) {
-    L.meta[i] = 0;
-    L.wr[2 * i] = 0;
-    L.wr[2 * i + 1] = 0;
+template <typename F>
+__device__ __forceinline__ void ring_decode(const uint32_t (&R)[12], int bits, int64_t qi, F &f) {
+#define PINOT_RD(B) ring_decode_b<B>(R, qi, f)
+  switch (bits) {  // widths up to kGroupLwMaxBits (plan_ring checks)
+    case 1: PINOT_RD(1); break;   case 2: PINOT_RD(2); break;   case 3: PINOT_RD(3); break;   case 4: PINOT_RD(4); break;
+    case 5: PINOT_RD(5); break;   case 6: PINOT_RD(6); break;   case 7: PINOT_RD(7); break;   case 8: PINOT_RD(8); break;
+    case 9: PINOT_RD(9); break;   case 10: PINOT_RD(10); break; case 11: PINOT_RD(11); break; case 12: PINOT_RD(12); break;
+    case 13: PINOT_RD(13); break; case 14: PINOT_RD(14); break; case 15: PINOT_RD(15); break; case 16: PINOT_RD(16); break;
+    case 17: PINOT_RD(17); break; case 18: PINOT_RD(18); break; case 19: PINOT_RD(19); break; case 20: PINOT_RD(20); break;
+    default: break;
   }
-  // region size: the busiest block's matching docs (every block computes the same value)
-  __shared__ uint32_t s_max;
-  if (tid == 0) s_max = 0;
-  __syncthreads();
-  {
-    uint32_t mx = 0;
-    for (int i = tid; i < a.nblk; i += kRingBlock) mx = max(mx, a.blk_matched[i]);
-    atomicMax(&s_max, mx);
+#undef PINOT_RD
+}
+
+struct RingKeyFold {  // key += global id * stride (DictionaryBasedGroupKeyGenerator's mixed radix)
+  uint32_t (&key)[16];
+  const int32_t *remap;
+  uint32_t stride;
+  template <int J>
+  __device__ __forceinline__ void put(uint32_t id) {
+    key[J] += (remap ? (uint32_t)gload<int32_t>(remap + id) : id) * stride;
   }
-  __syncthreads();
-  const uint32_t C = ring_region_records(s_max, int64_t(1) << a.shift, a.G, a.cap);
-  if (b == 0 && tid == 0) *a.region = C;
-  unsigned long long *region0 = a.records + (size_t)b * C;  // region (p, b) at ((p * nblk + b) * C)
-  uint32_t *fl = L.flist + wave * 64;
-  const int64_t c0 = a.total_chunks * b / a.nblk, c1 = a.total_chunks * (b + 1) / a.nblk;
-  uint32_t over = 0, waits = 0, sleeps = 0;
-  RingCursor cu;
-  cu.cn = c0 + wave;
-  cu.gn = 0;
-  cu.wn = ring_word(a, cu.cn, c1, lane, cu.gn);
-  cu.q = 3;
-  cu.c = -1;
-  ring_advance(a, cu, c1, lane);
-  uint32_t R[kGroupPfCols][12];
-  int g = 0;
-  RingColsDev k{};
-  int64_t qi = 0;
-  if (cu.c < c1) {
-    qi = ring_qi(a, cu, lane, g);
-    k = ring_cols(a, g);
+};
+
+struct RingFieldFold {  // record |= dictId << field shift
+  unsigned long long (&rec)[16];
+  int shift;
+  template <int J>
+  __device__ __forceinline__ void put(uint32_t id) {
+    rec[J] |= (unsigned long long)id << shift;
+  }
+};
+
+// The fields of a quarter-form scan leaf (FusedStep) the decoders keep in scalar registers.
+struct RingLeaf {
+  const uint8_t *fwd;
+  const uint32_t *table;
+  uint64_t lut64;
+  uint32_t lo, span;
+  int32_t bits, kind, negate;
+};
+
+__device__ __forceinline__ RingLeaf ring_leaf(const FusedStep *p) {
+  RingLeaf l;
+  const FusedStep st = load_const(p);
+  l.fwd = st.fwd;
+  l.table = static_cast<const uint32_t *>(st.table);
+  l.lut64 = st.lut64;
+  l.lo = st.lo;
+  l.span = st.span;
+  l.bits = st.bits;
+  l.kind = st.kind;
+  l.negate = st.negate;
+  return l;
+}
+
+struct RingLeafFold {  // bit J of m = the leaf's predicate on value J (FusedStep, fused_common.h leaf_half)
+  const RingLeaf &st;
+  uint32_t &m;
+  template <int J>
+  __device__ __forceinline__ void put(uint32_t id) {
+    uint32_t x;
+    if (st.kind == FK_LEAF_RANGE) x = id - st.lo < st.span ? 1u : 0u;
+    else if (st.kind == FK_LEAF_LUT64) x = (uint32_t)(st.lut64 >> (id & 63u)) & 1u;
+    else x = (gload<uint32_t>(st.table + (id >> 5)) >> (id & 31u)) & 1u;
+    m |= x << J;
+  }
+};
+
+// A decoder wave's matching docs of segment g into numDocsScanned's per-segment counter.
+__device__ __forceinline__ void ring_add_matched(const RingArgs &a, int g, uint32_t n, int lane) {
+  const unsigned long long t = wave_sum((unsigned long long)n);
+  if (lane == 0 && t) atomicAdd(a.matched + g, t);
+}
+
+// What the decoders keep of a segment's descriptor (GroupSegment): ch0 = its first chunk minus its first global chunk.
+struct RingSeg {
+  const uint64_t *pre;
+  int64_t nwords, ch0;
+  int32_t num_docs, n_leaves;
+};
+
+// A lane's raw dwords of a column's quarter (group_lq.h load_raw_lq) as three unconditional loads: conditional
+// loads let the register allocator reuse a pending load's destination on the other path, and every later write of that
+// register then waits for all outstanding loads (vmcnt(0) between the columns' loads). The bytes past the quarter's
+// ceil(B / 2) + 1 dwords stay inside the forward index's padding and hit lines the wave reads anyway.
+typedef uint32_t u32x3a __attribute__((ext_vector_type(3), aligned(4)));
+__device__ __forceinline__ void ring_load_raw(const uint8_t *fwd, int bits, int64_t qi, uint32_t (&R)[12]) {
+  // 11 dwords: the most a quarter of <= 20 bits spans (a dead 12th dword would be a pending load's destination the
+  // allocator hands out again, and that write waits for every load)
+  const uint32_t *p = reinterpret_cast<const uint32_t *>(fwd) + ((qi * bits) >> 1);
+  const u32x4a x0 = gload<u32x4a>(p), x1 = gload<u32x4a>(p + 4);
+  const u32x3a x2 = gload<u32x3a>(p + 8);
+  R[0] = x0.x; R[1] = x0.y; R[2] = x0.z; R[3] = x0.w;
+  R[4] = x1.x; R[5] = x1.y; R[6] = x1.z; R[7] = x1.w;
+  R[8] = x2.x; R[9] = x2.y; R[10] = x2.z; R[11] = 0;
+}
+
+// A decoder wave's quarters: load(t) requests pass t's quarter (its filter word and the raw dwords of its filter leaves,
+// group and aggregated columns: issued, not waited for), decode() turns the requested quarter into 16 records per lane
+// (act: the docs passing the filter). The segment descriptors follow the requested quarter; a quarter past the block's
+// range (or a chunk with no candidate doc) requests nothing and decodes to no record.
+template <int NF, bool WORDS>
+struct RingDecoder {
+  int64_t c0, nq;
+  int wave, g;
+  RingSeg sg;
+  RingColsDev k;
+  RingLeaf st[NF > 0 ? NF : 1];
+  uint32_t seg_matched;  // this lane's matching docs of segment g
+  // the requested quarter
+  bool live;
+  int64_t qi;
+  uint32_t word_bits;    // the lane's 16 candidate docs (pre / filter words, tail)
+  uint32_t F[NF > 0 ? NF : 1][12];
+  uint32_t RA[kRingGroupCols][12], RB[kRingAggCols][12];
+  // the decoded quarter
+  uint32_t act;
+  unsigned long long rec[16];
+
+  __device__ __forceinline__ void init(const RingArgs &a, int64_t c0_, int64_t nq_, int wave_, int lane) {
+    c0 = c0_;
+    nq = nq_;
+    wave = wave_;
+    g = -1;
+    seg_matched = 0;
+    live = false;
+    act = 0;
 #pragma unroll
-    for (int c = 0; c < kGroupPfCols; c++)
-      if (k.bits[c]) load_raw_lq(k.fwd[c], k.bits[c], qi, R[c]);
+    for (int j = 0; j < 16; j++) rec[j] = 0;
   }
-  const uint32_t lmask = (1u << a.shift) - 1u;
-  while (cu.c < c1) {
-    // decode this quarter: group key (mixed radix over global ids), then the record's fields
+
+  __device__ __forceinline__ void load(const RingArgs &a, int64_t t) {
+    const int64_t qg = t * kRingDecWaves + wave;
+    live = qg < nq;
+    if (!live) return;  // uniform
+    const int64_t c = c0 + (qg >> 2);
+    const int q = (int)(qg & 3);
+    const int lane = threadIdx.x & 63;
+    const int gn = ring_segment(a, c, g < 0 ? 0 : g);
+    if (gn != g) {  // uniform: the descriptors change with the segment only
+      if (!WORDS && g >= 0) ring_add_matched(a, g, seg_matched, lane);
+      seg_matched = 0;
+      g = gn;
+      const GroupSegment gs = load_const(a.segs + g);
+      sg.pre = gs.pre;
+      sg.nwords = gs.nwords;
+      sg.num_docs = gs.num_docs;
+      sg.n_leaves = gs.n_leaves;
+      sg.ch0 = gs.ch_begin - load_const(a.cstart + g);
+      k = ring_cols(a, gs);
+#pragma unroll
+      for (int i = 0; i < NF; i++)
+        if (i < sg.n_leaves) st[i] = ring_leaf(a.leaves + gs.first_leaf + i);
+    }
+    const int64_t ch = sg.ch0 + c;
+    const int64_t w = ch * 64 + 16 * q + (lane >> 2);  // the chunk word holding this lane's 16 docs
+    uint64_t word;
+    if constexpr (WORDS) {
+      word = w < sg.nwords ? gload<uint64_t>(a.filter + (size_t)g * a.filter_stride + w) : 0ull;
+    } else {
+      word = w < sg.nwords ? (sg.pre ? gload<uint64_t>(sg.pre + w) : ~0ull) & tail_mask(w, sg.nwords, sg.num_docs) : 0ull;
+    }
+    word_bits = (uint32_t)(word >> (16 * (lane & 3))) & 0xFFFFu;
+    qi = ch * 256 + 64 * q + lane;
+#pragma unroll
+    for (int i = 0; i < NF; i++)
+      if (i < sg.n_leaves) ring_load_raw(st[i].fwd, st[i].bits, qi, F[i]);
+#pragma unroll
+    for (int cc = 0; cc < kRingGroupCols; cc++)
+      if (k.bits[cc]) ring_load_raw(k.fwd[cc], k.bits[cc], qi, RA[cc]);
+#pragma unroll
+    for (int cc = 0; cc < kRingAggCols; cc++)
+      if (k.bits[kRingGroupCols + cc]) ring_load_raw(k.fwd[kRingGroupCols + cc], k.bits[kRingGroupCols + cc], qi, RB[cc]);
+  }
+
+  __device__ __forceinline__ void decode(const RingArgs &a, int lane, uint32_t &status) {
+    act = live ? word_bits : 0u;
+    if (!__any(act != 0)) {  // uniform: nothing to insert
+      act = 0;
+      return;
+    }
+    if constexpr (NF > 0) {
+#pragma unroll
+      for (int i = 0; i < NF; i++)
+        if (i < sg.n_leaves) {
+          uint32_t m = 0;
+          RingLeafFold f{st[i], m};
+          ring_decode(F[i], st[i].bits, qi, f);
+          act &= (st[i].negate ? ~m : m) & 0xFFFFu;
+        }
+    }
+    if constexpr (!WORDS) seg_matched += __popc(act);
     uint32_t key[16];
 #pragma unroll
     for (int j = 0; j < 16; j++) key[j] = 0;
 #pragma unroll
-    for (int c = 0; c < kGroupPfCols; c++) {
-      if (!k.bits[c] || k.fsh[c] >= 0) continue;
-      const int32_t *remap = k.remap[c];
-      const uint32_t stride = k.stride[c];
-      decode_raw_lq(R[c], k.bits[c], qi, [&](const uint32_t (&id)[16]) {
-        if (remap) {
-#pragma unroll
-          for (int j = 0; j < 16; j++) key[j] += (uint32_t)gload<int32_t>(remap + id[j]) * stride;
-        } else {
-#pragma unroll
-          for (int j = 0; j < 16; j++) key[j] += id[j] * stride;
-        }
-      });
+    for (int cc = 0; cc < kRingGroupCols; cc++) {
+      if (!k.bits[cc]) continue;
+      RingKeyFold f{key, k.remap[cc], k.stride[cc]};
+      ring_decode(RA[cc], k.bits[cc], qi, f);
     }
-    unsigned long long rec[16];
+    const uint32_t lmask = (1u << a.shift) - 1u;
 #pragma unroll
     for (int j = 0; j < 16; j++)
       rec[j] = (unsigned long long)(key[j] & lmask) | ((unsigned long long)(key[j] >> a.shift) << kRecPShift);
 #pragma unroll
-    for (int c = 0; c < kGroupPfCols; c++) {
-      if (!k.bits[c] || k.fsh[c] < 0) continue;
-      const int fsh = k.fsh[c];
-      decode_raw_lq(R[c], k.bits[c], qi, [&](const uint32_t (&id)[16]) {
-#pragma unroll
-        for (int j = 0; j < 16; j++) rec[j] |= (unsigned long long)id[j] << fsh;
-      });
+    for (int cc = 0; cc < kRingAggCols; cc++) {
+      if (!k.bits[kRingGroupCols + cc]) continue;
+      RingFieldFold f{rec, k.fsh[kRingGroupCols + cc]};
+      ring_decode(RB[cc], k.bits[kRingGroupCols + cc], qi, f);
     }
-    const uint32_t act = cu.m;
-    // the next quarter's loads go out before this one is sunk (the sink issues LDS work and 64-B stores only)
-    ring_advance(a, cu, c1, lane);
-    if (cu.c < c1) {
-      const int gp = g;
-      qi = ring_qi(a, cu, lane, g);
-      if (g != gp) k = ring_cols(a, g);  // uniform: the column descriptors change with the segment only
-#pragma unroll
-      for (int c = 0; c < kGroupPfCols; c++)
-        if (k.bits[c]) load_raw_lq(k.fwd[c], k.bits[c], qi, R[c]);
-    }
-    if (DBG && a.debug == 1) {  // decode only: keep the records alive without the sink
-      unsigned long long x = 0;
-#pragma unroll
-      for (int j = 0; j < 16; j++) x ^= ((act >> j) & 1u) ? rec[j] : 0ull;
-      if (x == 0x0123456789ABCDEFull) over |= 8u;
-      continue;
-    }
-    ring_sink<DBG>(a, L, fl, act, rec, region0, C, lane, over, waits, sleeps);
   }
-  if (DBG && lane == 0 && waits) atomicAdd(a.status + 2, waits);
-  if (DBG && lane == 0 && sleeps) atomicAdd(a.status + 3, sleeps);
+
+  __device__ __forceinline__ void finish(const RingArgs &a, int lane) {
+    if (!WORDS && g >= 0) ring_add_matched(a, g, seg_matched, lane);
+  }
+};
+
+// WORDS: the filter words GB_FILTER wrote; else the segment's top-level conjunction of <= NF scan leaves evaluated here
+// on each quarter (lane-owns-quarter reads, like the group columns), AND-ed with the `pre` words if any.
+//
+// The block walks its quarters in passes: in pass t decoder wave w takes quarter 4 c0 + 9 t + w of the block's range
+// (none past its end: that wave inserts nothing). A pass inserts the wave's 16 records per lane in two rounds of
+// [insert phase | barrier | flush phase | barrier]; during the second flush phase the decoders decode the next pass's
+// quarter (its raw dwords requested a pass earlier) and request the one after it. Every wave executes the same
+// barriers.
+template <int NF, bool WORDS>
+__global__ __launch_bounds__(kRingBlock) void k_group_ring(RingArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: chunk indices and descriptors in SGPRs
+  const int b = blockIdx.x;
+  const RingLds L = ring_lds(lds, a.P);
+  for (int i = tid; i < a.P; i += kRingBlock) {
+    L.ctr[i] = 0;
+    L.back[i] = 0;
+  }
   __syncthreads();
-  // every complete half is out; the partial last half of each partition and the region's record count remain
-  for (int p = tid; p < a.P; p += kRingBlock) {
-    const uint32_t n = (uint32_t)L.meta[p];
-    a.hist[(size_t)p * a.nblk + b] = n;
-    if (n > C) {
-      over = 1;
-      continue;
+  const uint32_t C = a.cap;
+  if (b == 0 && tid == 0) *a.region = C;
+  unsigned long long *region0 = a.records + (size_t)b * C;  // region (p, b) at ((p * nblk + b) * C)
+  uint32_t status = 0;
+  const int64_t c0 = a.total_chunks * b / a.nblk, c1 = a.total_chunks * (b + 1) / a.nblk;
+  const int64_t nq = (c1 - c0) * 4;  // the block's quarters
+  const int64_t npass = (nq + kRingDecWaves - 1) / kRingDecWaves;
+  constexpr int KP = (kRingMaxPartitions + 64 * kRingFlushWaves - 1) / (64 * kRingFlushWaves);
+  if (wave >= kRingDecWaves) {  // flusher
+    const int fw = wave - kRingDecWaves;
+    uint32_t front[KP];
+#pragma unroll
+    for (int k = 0; k < KP; k++) front[k] = 0;
+#ifdef RING_EXP_TIMING
+    uint64_t tb = 0, tf = 0;
+    RT_MARK(t0);
+#endif
+    for (int64_t t = 0; t < npass; t++)
+#pragma unroll 1
+      for (int r = 0; r < 16 / kRingRoundRecs; r++) {
+        RT_MARK(x0);
+        __syncthreads();  // inserts of the round done
+        RT_ADD(tb, x0);
+        RT_MARK(x1);
+        ring_flush_phase<KP>(a, L, region0, C, fw, lane, front, status);
+        RT_ADD(tf, x1);
+        RT_MARK(x2);
+        __syncthreads();  // flushes done (and the decoders' next quarter decoded)
+        RT_ADD(tb, x2);
+      }
+#ifdef RING_EXP_TIMING
+    if ((b == 0 || b == a.nblk / 2) && lane == 0)
+      printf("ring-timing block %d flusher %d: total %llu barrier %llu flush %llu passes %lld\n", b, fw,
+             (unsigned long long)(__builtin_amdgcn_s_memtime() - t0), (unsigned long long)tb, (unsigned long long)tf,
+             (long long)npass);
+#endif
+    // the partial buckets (< 8 entries) to their fronts, then each region's counts
+#pragma unroll
+    for (int k = 0; k < KP; k++) {
+      const int p = fw * 64 + lane + 64 * kRingFlushWaves * k;
+      if (p >= a.P) continue;
+      const uint32_t c = L.ctr[p], n = min(c & 0xFFFFu, (uint32_t)kRingBucket), h = c >> 16, nb = L.back[p];
+      for (uint32_t i = 0; i < n; i++)
+        if (front[k] + i < C)
+          region0[(size_t)p * a.nblk * C + front[k] + i] =
+              L.bkt[p * kRingBucket + ((h + i) & (kRingBucket - 1))] & ((1ull << kRecPShift) - 1ull);
+      const uint32_t f = front[k] + n;
+      if (f + nb > C || f >= (1u << (32 - kRingBackBits)) || nb >= (1u << kRingBackBits)) status |= 1u;
+      a.hist[(size_t)p * a.nblk + b] = min(f, (1u << (32 - kRingBackBits)) - 1u) | (min(nb, (1u << kRingBackBits) - 1u) << (32 - kRingBackBits));
     }
-    const uint32_t kk = n & 7u, h = (n >> 3) & 1u, m = n >> 3;
-    for (uint32_t r = 0; r < kk; r++)
-      region0[((size_t)p * a.nblk) * C + (size_t)m * 8 + r] = L.ring[p * 16 + h * 8 + r];
+  } else {  // decoder
+    RingDecoder<NF, WORDS> d;
+    d.init(a, c0, nq, wave, lane);
+    d.load(a, 0);  // pass 0's raw dwords
+    d.decode(a, lane, status);
+    d.load(a, 1);  // in flight during pass 0's rounds
+#ifdef RING_EXP_TIMING
+    uint64_t ti = 0, tb = 0, td = 0, tl = 0;
+    RT_MARK(t0);
+#endif
+    for (int64_t t = 0; t < npass; t++) {
+      RT_MARK(x0);
+      ring_insert<0>(a, L, d.act, d.rec, region0, C);
+      RT_ADD(ti, x0);
+      RT_MARK(x1);
+      __syncthreads();  // inserts of round 0 done
+      __syncthreads();  // flush done
+      RT_ADD(tb, x1);
+      RT_MARK(x2);
+      ring_insert<kRingRoundRecs>(a, L, d.act, d.rec, region0, C);
+      RT_ADD(ti, x2);
+      RT_MARK(x3);
+      __syncthreads();  // inserts of round 1 done
+      RT_ADD(tb, x3);
+      // the next pass's quarter decoded meanwhile the flushers empty the buckets, then the one after it requested
+      RT_MARK(x4);
+      d.decode(a, lane, status);
+      RT_ADD(td, x4);
+      RT_MARK(x5);
+      d.load(a, t + 2);
+      RT_ADD(tl, x5);
+      RT_MARK(x6);
+      __syncthreads();  // flush done
+      RT_ADD(tb, x6);
+    }
+    d.finish(a, lane);
+#ifdef RING_EXP_TIMING
+    if ((b == 0 || b == a.nblk / 2) && lane == 0)
+      printf("ring-timing block %d decoder %d: total %llu insert %llu barrier %llu decode %llu load %llu\n", b, wave,
+             (unsigned long long)(__builtin_amdgcn_s_memtime() - t0), (unsigned long long)ti, (unsigned long long)tb,
+             (unsigned long long)td, (unsigned long long)tl);
+#endif
   }
-  if (over) atomicOr(a.status, over);
+  if (status) atomicOr(a.status, status);
 }
 
 // ----------------------------------------------------------------------------------------------------- reduce
 constexpr int kRingReduceBlock = 1024;
-constexpr int kRingReduceRegions = 2;  // regions read per step (8 records in flight per thread)
-constexpr int kRingReduceUnroll = 4;   // records per thread and region per step
+constexpr int kRingReduceUnroll = 4;   // 16-B loads (two records each) per lane and step
 constexpr int kRingExceptions = 512;   // HLL ranks > 15 per partition (nibble registers saturate at 15)
 
 __device__ __forceinline__ unsigned long long ordered_bits_g(double d) {
@@ -434,7 +602,9 @@ __device__ __forceinline__ uint32_t hll_register_rank_g(uint32_t h) {
   return ((h >> 24) << 8) | (uint32_t)(__builtin_clz((h << 8) | 129u) + 1);
 }
 
-template <int N>
+// GATHER = false: every aggregation is a COUNT, an affine-dictionary SUM / AVG or an affine-dictionary HLL (the host
+// checks), so the fold issues no memory loads and the records' prefetched loads are waited for exactly.
+template <int N, bool GATHER>
 __device__ __forceinline__ void ring_fold(const RingReduceArgs &a, uint8_t *lds, uint32_t *cnt, uint32_t *exc_n,
                                           uint32_t *exc, const unsigned long long (&rec)[N], const bool (&ok)[N],
                                           int pk, int sbits, uint32_t &status) {
@@ -458,7 +628,8 @@ __device__ __forceinline__ void ring_fold(const RingReduceArgs &a, uint8_t *lds,
       unsigned long long v[N];  // affine: Σ dictId here, Σ value = base * count + step * Σ dictId at the end
 #pragma unroll
       for (int u = 0; u < N; u++)
-        v[u] = ag.affine ? (unsigned long long)id[u] : (unsigned long long)(long long)gload<int32_t>(static_cast<const int32_t *>(ag.dict) + id[u]);
+        v[u] = (!GATHER || ag.affine) ? (unsigned long long)id[u]
+                                      : (unsigned long long)(long long)gload<int32_t>(static_cast<const int32_t *>(ag.dict) + id[u]);
       if (g == pk) {
 #pragma unroll
         for (int u = 0; u < N; u++) v[u] += 1ull << sbits;
@@ -470,8 +641,8 @@ __device__ __forceinline__ void ring_fold(const RingReduceArgs &a, uint8_t *lds,
       uint32_t h[N];
 #pragma unroll
       for (int u = 0; u < N; u++)
-        h[u] = ag.affine ? hll_register_rank_g(murmur_hash_long_g(ag.affine_base + ag.affine_step * (long long)id[u]))
-                         : (uint32_t)gload<uint16_t>(ag.hll_lut + id[u]);
+        h[u] = (!GATHER || ag.affine) ? hll_register_rank_g(murmur_hash_long_g(ag.affine_base + ag.affine_step * (long long)id[u]))
+                                      : (uint32_t)gload<uint16_t>(ag.hll_lut + id[u]);
       uint32_t *word[N], old[N], rk[N];
       int sh[N];
 #pragma unroll
@@ -497,7 +668,7 @@ __device__ __forceinline__ void ring_fold(const RingReduceArgs &a, uint8_t *lds,
           seen = atomicCAS(word[u], old[u], (old[u] & ~(15u << sh[u])) | (rk[u] << sh[u]));
         }
       }
-    } else {
+    } else if constexpr (GATHER) {
       double v[N];
 #pragma unroll
       for (int u = 0; u < N; u++) v[u] = ok[u] ? dict_value_g(ag.dict, ag.value_kind, id[u]) : 0.0;
@@ -512,6 +683,73 @@ __device__ __forceinline__ void ring_fold(const RingReduceArgs &a, uint8_t *lds,
   }
 }
 
+template <int U, bool GATHER>
+__device__ __forceinline__ void ring_fold_units(const RingReduceArgs &a, uint8_t *lds, uint32_t *cnt, uint32_t *exc_n,
+                                                uint32_t *exc, const u32x4 (&v)[U], const uint32_t (&n)[U], int pk,
+                                                int sbits, uint32_t &status) {
+  unsigned long long rec[2 * U];
+  bool ok[2 * U];
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    // the loaded set passes through an empty asm here, in straight-line code: the compiler waits for exactly these
+    // loads (the other set's stay in flight); a first use inside the fold's runtime loops would wait for every load
+    u32x4 x = v[u];
+    asm volatile("" : "+v"(x));
+    rec[2 * u] = ((unsigned long long)x.y << 32) | x.x;
+    rec[2 * u + 1] = ((unsigned long long)x.w << 32) | x.z;
+    ok[2 * u] = n[u] & 1u;
+    ok[2 * u + 1] = (n[u] >> 1) & 1u;
+  }
+  ring_fold<2 * U, GATHER>(a, lds, cnt, exc_n, exc, rec, ok, pk, sbits, status);
+}
+
+constexpr int kRingReduceWaves = kRingReduceBlock / 64;
+
+// A reduce wave's position in its regions' record ranges: region v, part (0: its front [0, F), 1: its back
+// [C - B, C)), next 16-B unit i of the units [i, u1) covering the range [s0, s0 + n) (a unit = records 2i, 2i + 1).
+struct RingStream {
+  int v, part;
+  uint32_t i, u1, s0, n;
+};
+
+// Loads the wave's next kRingReduceUnroll units per lane (64 lanes x 16 B consecutive per load), moving on to the
+// wave's next non-empty range when this one is done (wave w: regions w, w + 16, ..., each front then back); v >= nblk
+// once the stream is exhausted (loads then stay in bounds and count no record). cnt[u]: bit 0 / 1 = record 2i / 2i + 1
+// of the unit is in the range.
+__device__ __forceinline__ bool ring_stream_next(const RingReduceArgs &a, const uint32_t *hrow, uint32_t C,
+                                                 const unsigned long long *base, RingStream &rs, int lane,
+                                                 u32x4 (&v)[kRingReduceUnroll], uint32_t (&cnt)[kRingReduceUnroll]) {
+  while (rs.i >= rs.u1) {  // uniform
+    if (rs.part == 0) {
+      rs.part = 1;
+    } else {
+      rs.part = 0;
+      rs.v += kRingReduceWaves;
+      if (rs.v >= a.nblk) break;
+    }
+    const uint32_t h = (uint32_t)__builtin_amdgcn_readfirstlane((int)hrow[rs.v]);
+    const uint32_t f = min(h & ((1u << (32 - kRingBackBits)) - 1u), C), bk = min(h >> (32 - kRingBackBits), C - f);
+    rs.s0 = rs.part ? C - bk : 0u;
+    rs.n = rs.part ? bk : f;
+    rs.i = rs.s0 >> 1;
+    rs.u1 = (rs.s0 + rs.n + 1) >> 1;
+  }
+  const bool live = rs.v < a.nblk;
+  const u32x4 *src = reinterpret_cast<const u32x4 *>(base + (size_t)(live ? rs.v : 0) * C);
+#pragma unroll
+  for (int u = 0; u < kRingReduceUnroll; u++) {
+    const uint32_t idx = rs.i + (uint32_t)(u * 64 + lane);
+    const bool ok = live && idx < rs.u1;
+    const uint32_t r0 = 2 * idx;
+    cnt[u] = ok ? ((r0 >= rs.s0 && r0 < rs.s0 + rs.n) ? 1u : 0u) | ((r0 + 1 >= rs.s0 && r0 + 1 < rs.s0 + rs.n) ? 2u : 0u)
+                : 0u;
+    v[u] = __builtin_nontemporal_load(src + (ok ? idx : 0u));  // unconditional (a branch would cost the counted wait)
+  }
+  rs.i += 64 * kRingReduceUnroll;
+  return live;
+}
+
+template <bool GATHER>
 __global__ __launch_bounds__(kRingReduceBlock) void k_ring_reduce(RingReduceArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int tid = threadIdx.x;
@@ -537,9 +775,9 @@ __global__ __launch_bounds__(kRingReduceBlock) void k_ring_reduce(RingReduceArgs
   {
     uint32_t part = 0;
     for (int i = tid; i < a.nblk; i += kRingReduceBlock) {
-      const uint32_t h = a.hist[(size_t)p * a.nblk + i];
+      const uint32_t h = a.hist[(size_t)p * a.nblk + i];  // front | back << 20
       hrow[i] = h;
-      part += h;
+      part += (h & ((1u << (32 - kRingBackBits)) - 1u)) + (h >> (32 - kRingBackBits));
     }
     atomicAdd(&s_n, part);
   }
@@ -555,27 +793,33 @@ __global__ __launch_bounds__(kRingReduceBlock) void k_ring_reduce(RingReduceArgs
     }
   uint32_t status = 0;
   const unsigned long long *base = a.records + (size_t)p * a.nblk * C;
-  constexpr int RB = kRingReduceRegions, U = kRingReduceUnroll, N = RB * U;
-  for (int b0 = 0; b0 < a.nblk; b0 += RB) {
-    uint32_t hmax = 0;
-#pragma unroll
-    for (int r = 0; r < RB; r++) hmax = max(hmax, b0 + r < a.nblk ? hrow[b0 + r] : 0u);
-    hmax = min(hmax, C);
-    for (uint32_t r0 = 0; r0 < hmax; r0 += (uint32_t)U * kRingReduceBlock) {
-      unsigned long long rec[N];
-      bool ok[N];
-#pragma unroll
-      for (int r = 0; r < RB; r++)
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-          const int bb = b0 + r;
-          const uint32_t i = r0 + (uint32_t)(u * kRingReduceBlock + tid);
-          const bool v = bb < a.nblk && i < min(hrow[bb < a.nblk ? bb : 0], C);
-          ok[r * U + u] = v;
-          rec[r * U + u] = v ? __builtin_nontemporal_load(base + (size_t)bb * C + i) : 0ull;
-        }
-      ring_fold<N>(a, lds, cnt, exc_n, exc, rec, ok, pk, sbits, status);
-    }
+  // wave w streams record ranges w, w + 16, ... (each region's front and back): 16-B loads (two records) per lane,
+  // kRingReduceUnroll loads per lane and step, the next step's loads issued before this step's records are folded
+  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  constexpr int U = kRingReduceUnroll;
+  RingStream rs{};
+  rs.v = wave - kRingReduceWaves;
+  rs.part = 1;  // the first advance moves to region `wave`, front part
+  rs.i = 0;
+  rs.u1 = 0;
+  // two register sets, unrolled by two (no copies: a copy of a set still in flight would wait for its loads)
+  u32x4 va[U], vb[U];
+  uint32_t na[U], nb[U];
+  bool live_a = ring_stream_next(a, hrow, C, base, rs, lane, va, na);
+  while (live_a) {  // uniform; every load unconditional (an exhausted stream loads unit 0 with no record counted)
+    const bool live_b = ring_stream_next(a, hrow, C, base, rs, lane, vb, nb);
+#ifndef RING_EXP_NOFOLD
+    ring_fold_units<U, GATHER>(a, lds, cnt, exc_n, exc, va, na, pk, sbits, status);
+#else
+    for (int u = 0; u < U; u++) if (va[u].x == 0x01234567u && na[u] == 3) status |= 8u;
+#endif
+    if (!live_b) break;
+    live_a = ring_stream_next(a, hrow, C, base, rs, lane, va, na);
+#ifndef RING_EXP_NOFOLD
+    ring_fold_units<U, GATHER>(a, lds, cnt, exc_n, exc, vb, nb, pk, sbits, status);
+#else
+    for (int u = 0; u < U; u++) if (vb[u].x == 0x01234567u && nb[u] == 3) status |= 8u;
+#endif
   }
   __syncthreads();
   const long long kbase = (long long)p * K;
@@ -638,17 +882,27 @@ __global__ __launch_bounds__(kRingReduceBlock) void k_ring_reduce(RingReduceArgs
 
 }  // namespace
 
-size_t ring_lds_bytes(int P) { return (size_t)P * (16 * 8 + 8 + 8) + (size_t)kRingWaves * 64 * 4; }
+size_t ring_lds_bytes(int P) { return (size_t)P * (kRingBucket * 8 + 4 + 4) + 16; }
 
 void launch_group_ring(const RingArgs &a, hipStream_t stream) {
   if (a.nblk <= 0 || a.total_chunks <= 0) return;
-  if (a.debug) hipLaunchKernelGGL(k_group_ring<1>, dim3((unsigned)a.nblk), dim3(kRingBlock), ring_lds_bytes(a.P), stream, a);
-  else hipLaunchKernelGGL(k_group_ring<0>, dim3((unsigned)a.nblk), dim3(kRingBlock), ring_lds_bytes(a.P), stream, a);
+  const size_t lds = ring_lds_bytes(a.P);
+  const dim3 grid((unsigned)a.nblk), block(kRingBlock);
+  if (a.nf < 0) hipLaunchKernelGGL((k_group_ring<0, true>), grid, block, lds, stream, a);
+  else if (a.nf == 0) hipLaunchKernelGGL((k_group_ring<0, false>), grid, block, lds, stream, a);
+  else if (a.nf == 1) hipLaunchKernelGGL((k_group_ring<1, false>), grid, block, lds, stream, a);
+  else hipLaunchKernelGGL((k_group_ring<2, false>), grid, block, lds, stream, a);
 }
 
 void launch_ring_reduce(const RingReduceArgs &a, hipStream_t stream) {
   if (a.P <= 0) return;
-  hipLaunchKernelGGL(k_ring_reduce, dim3((unsigned)a.P), dim3(kRingReduceBlock), (size_t)a.lds_bytes, stream, a);
+  bool gather = false;  // any aggregation reading its dictionary / HLL LUT in the fold
+  for (int g = 0; g < a.n_aggs; g++) {
+    const int k = a.aggs[g].acc_kind;
+    gather = gather || k == 1 || k == 2 || k == 3 || ((k == 0 || k == 4) && !a.aggs[g].affine);
+  }
+  if (gather) hipLaunchKernelGGL(k_ring_reduce<true>, dim3((unsigned)a.P), dim3(kRingReduceBlock), (size_t)a.lds_bytes, stream, a);
+  else hipLaunchKernelGGL(k_ring_reduce<false>, dim3((unsigned)a.P), dim3(kRingReduceBlock), (size_t)a.lds_bytes, stream, a);
 }
 
 int ring_reduce_exceptions() { return kRingExceptions; }

@@ -242,8 +242,8 @@ int scan_query_blocks_per_cu(int stage_bytes, bool gathers, bool pipelined);
 //   GB_EMIT2   pass 2 of the bucketed partitioned plan: the filter words GB_COUNT wrote (no filter re-evaluation),
 //              records appended to per-block LDS buckets of kBucketRecs records per partition and written out
 //              whole into the FINAL partition layout (offsets from GB_COUNT's histogram): no split pass
-//   GB_FILTER  the ring plan's first pass (group_ring.hip): the filter program alone, its words per segment into
-//              filter_out and every ring block's matching docs into blk_matched (the ring regions' size)
+//   GB_FILTER  the ring plan's first pass for filters k_group_ring does not evaluate itself (group_ring.hip): the
+//              filter program alone, its words per segment into filter_out
 enum GroupMode : int32_t { GB_GLOBAL = 0, GB_LDS = 1, GB_COUNT = 2, GB_EMIT = 3, GB_VERIFY = 4, GB_FIRST = 5, GB_EMIT2 = 6,
                            GB_FILTER = 7 };
 constexpr int kBucketRecs = 8;                                   // 64-B bucket flushes
@@ -314,7 +314,6 @@ struct GroupArgs {
   unsigned long long hseed;
   uint32_t *verify_err;        // GB_VERIFY: set when a doc's tuple differs from its slot's representative
   int32_t hashed;
-  int32_t reserved2;
   // GB_COUNT / GB_EMIT column prefetch: every column a doc needs (group columns, then the aggregated
   // columns pf_agg[c] for slots c >= n_gcols) is loaded for kGroupPfUnroll words before any is decoded;
   // pf_nc = number of slots (<= kGroupPfCols), 0 = off (per-column loop)
@@ -329,13 +328,6 @@ struct GroupArgs {
                                // backwards, and the padding slots are written with kRecInvalid
   int32_t emit_block;          // GB_EMIT2 lane-owns-quarter: threads per block (512, or 1024 = group.emit_block)
   int64_t filter_stride;       // words per segment in filter_out
-  // GB_FILTER: chunk c of segment g's window is global chunk cstart[g] + (c - ch_begin); global chunk i belongs to
-  // ring block i * ring_blocks / total_chunks, whose matching docs accumulate in blk_matched
-  const int64_t *cstart;
-  int64_t total_chunks;
-  int32_t ring_blocks;
-  int32_t reserved3;
-  uint32_t *blk_matched;
   // GB_LDS lane-owns-quarter: the doc count rides in the high bits of aggregation lds_pack's affine dictId sum
   // ((1 << lds_sbits) + dictId per doc: one LDS atomic for both); -1 = separate u32 counts
   int32_t lds_pack, lds_sbits;
@@ -360,30 +352,31 @@ struct PartitionReduceArgs {
 void launch_partition_reduce(const PartitionReduceArgs &a, hipStream_t stream);
 
 // ---------------------------------------------------------------- ring plan (group_ring.hip)
-// Large dense key spaces without a histogram pass: GB_FILTER -> k_group_ring (records into fixed-capacity regions
-// [P][nblk][C], C from the busiest block's matching docs) -> k_ring_reduce (one block per partition of 2^shift keys).
+// Large dense key spaces without a histogram pass: k_group_ring (records into fixed-capacity regions [P][nblk][C],
+// C for the busiest block's docs all matching; the filter evaluated per quarter, or GB_FILTER's words first) ->
+// k_ring_reduce (one block per partition of 2^shift keys).
 struct RingArgs {
   const GroupSegment *segs;
   const GroupColDev *gcols;
   const GroupAggDev *aggs;
+  const FusedStep *leaves;       // nf > 0: each segment's top-level conjunction of nf scan leaves (quarter form)
   const int64_t *cstart;         // [nsegs + 1]: first global chunk of each segment's chunk window
-  const uint64_t *filter;        // GB_FILTER's words, [nsegs][filter_stride]
+  const uint64_t *filter;        // nf == 0: GB_FILTER's words, [nsegs][filter_stride]
   int64_t filter_stride;
   int64_t total_chunks;
   long long G;
   int32_t nsegs, n_gcols, nc, P;  // nc: columns read per doc (the group columns, then the pf_agg fields)
   int32_t pf_agg[4];
   int32_t shift, nblk;            // nblk: blocks of the launch (one per CU): block b owns chunks [T b / nblk, T (b+1) / nblk)
-  uint32_t cap;                   // records per region the allocation holds
-  int32_t debug;                  // debug.ring: the instrumented instance (wait counters); 1 decode without the sink,
-                                  // 2 sink without the HBM stores, 3 claims only (timing only, wrong results), 4 as 0
-  const uint32_t *blk_matched;    // [nblk] matching docs per block (GB_FILTER)
+  uint32_t cap;                   // C: records per region
+  int32_t nf;                     // < 0: the filter words; else at most nf scan leaves evaluated per quarter
   unsigned long long *records;    // [P][nblk][C] (local key | dictId fields)
   uint32_t *hist;                 // [P][nblk] records claimed per region (> C: overflow)
-  uint32_t *status;               // |= 1 a region overflowed, 2 a spin bound was hit, 4 HLL exception list full;
-                                  // status[2]: sink rounds that waited for a half to drain, status[3]: s_sleep spins
+  uint32_t *status;               // |= 1 a region overflowed, 2 a spin bound was hit, 4 HLL exception list full
   uint32_t *region;               // C, written by block 0 (read by k_ring_reduce)
+  unsigned long long *matched;    // nf >= 0: [nsegs] docs passing the filter (numDocsScanned), added by the decoders
 };
+constexpr int kRingMaxQuarterLeaves = 2;
 struct RingReduceArgs {
   const unsigned long long *records;
   const uint32_t *hist;

@@ -166,8 +166,13 @@ void attach_star_tree(Engine &e, SegmentData &seg, const pinot_star_tree_desc &d
     const size_t n = strlen(b);
     return a.size() >= n && a.compare(a.size() - n, n, b) == 0;
   };
+  auto is_metric = [](const std::string &n) {  // function-column pair columns: "<function>__<column>" (+ ".sum" / ".count")
+    for (const char *f : {"count__", "sum__", "min__", "max__", "avg__"})
+      if (n.rfind(f, 0) == 0) return true;
+    return false;
+  };
   for (auto &c : st->docs->cols)
-    if (c->name.find("__") != std::string::npos) {
+    if (is_metric(c->name)) {  // a dimension whose name merely contains "__" keeps its own type
       require(c->numeric(), PINOT_ERR_BAD_ARG, seg.name + ": star-tree metric " + c->name + " must be numeric");
       const bool count = c->name.rfind("count__", 0) == 0 || ends_with(c->name, ".count");
       require(count ? c->data_type == PINOT_LONG : c->data_type == PINOT_DOUBLE, PINOT_ERR_BAD_ARG,

@@ -154,7 +154,8 @@ def load(path=None):
     global _lib
     if _lib is not None:
         return _lib
-    p = path or LIB_PATH
+    # PINOT_GPU_LIB: another build of the same library (timing experiments on diagnostic builds); default the in-tree one
+    p = path or os.environ.get("PINOT_GPU_LIB") or LIB_PATH
     if not os.path.exists(p):
         raise PinotGpuError(3, "libpinot_gpu.so not built (%s); run `make -C incubator-pinot_amd`" % p)
     _share_hip_runtime_with_torch()

@@ -162,7 +162,8 @@ CONFIG4 = ("SELECT SUM(d8), AVG(d8), DISTINCTCOUNTHLL(d5) FROM fact WHERE d2 < 8
 
 
 @pytest.mark.parametrize("mode,limit,nseg,docs", [
-    ("", 1_000_000, 2, 2_000_000),                       # 1M keys, partitioned plan
+    ("", 1_000_000, 2, 2_000_000),                       # 1M keys, ring-partitioned plan (default)
+    ("group.ring=0", 1_000_000, 2, 2_000_000),           # 1M keys, counted partitioned plan
     ("group.mode=global", 1_000_000, 2, 2_000_000),      # HBM-atomic sink
     ("", 100_000, 3, 1_500_000),                         # reference default limit: admission + inter-segment cap
     ("exec.fused=0", 100_000, 3, 1_500_000),             # the same on the bitset path
@@ -293,4 +294,74 @@ def test_query_timeout_status():
     got, _ = ServerQueryExecutor(e, timeout_ms=60000).process_query(q2, gsegs)
     exp, _ = O.execute_server(host, q2)
     assert got[0] == exp[0] and got[1] == exp[1]
+    e.close()
+
+
+# ------------------------------------------------------------------ the LDS-privatised group-by (bench `lds_group_by`)
+LDS_QUERIES = [
+    # the bench's lds_group_by query: 1,600 keys, COUNT + SUM / AVG of the 20-bit d8 (count packed beside the dictId
+    # sum); 3 read columns -> the <= 3-column lane-owns-quarter GB_LDS instance (k_group_query<GB_LDS, 4, 512, 4>)
+    ("SELECT COUNT(*), SUM(d8), AVG(d8) FROM fact WHERE d2 < 800 GROUP BY d0, d1 TOP 10", 1 * 10000 + 4 * 1000 + 512),
+    # MIN / MAX: 4 read columns -> the general lane-owns-quarter instance (k_group_query<GB_LDS, 3, 512, 4>)
+    ("SELECT MIN(d8), MAX(d3), COUNT(*) FROM fact WHERE d2 < 800 GROUP BY d0, d1 TOP 10", 1 * 10000 + 3 * 1000 + 512),
+    ("SELECT MAX(d3), SUM(d8), AVG(d8) FROM fact WHERE d2 < 800 GROUP BY d0, d1 TOP 10", 1 * 10000 + 3 * 1000 + 512),
+    # DISTINCTCOUNTHLL: 1,600 keys x 1 KiB of LDS registers do not fit 60 KiB -> another sink (group-level parity only)
+    ("SELECT COUNT(*), SUM(d8), DISTINCTCOUNTHLL(d5) FROM fact WHERE d2 < 800 GROUP BY d0, d1 TOP 10", None),
+]
+
+
+@pytest.mark.parametrize("text,instance", LDS_QUERIES)
+def test_lds_shape(text, instance):
+    """The bench's LDS group-by workload (config 2's table, GROUP BY d0, d1: 16 x 100 keys) at 2 x 2M docs in the
+    default engine mode: every group's count, integer sum, MIN / MAX and HLL registers against the oracle's arrays,
+    and the kernel instance that ran (group.last_instance)."""
+    e = GpuEngine(0)
+    gsegs, host = _synthetic(e, 2, 2_000_000)
+    q = compile_pql(text)
+    exp = O.execute_group_by_arrays(host, q, num_groups_limit=1_000_000)
+    res, st = ServerQueryExecutor(e, num_groups_limit=1_000_000).group_by_result(q, gsegs)
+    assert st.num_docs_scanned == exp["scanned"]
+    assert exp["keys"].shape[0] == 1600
+    _assert_group_arrays(res, exp, q)
+    if instance is not None:
+        assert e.stat("group.last_instance") == instance
+    del res
+    e.close()
+
+
+def test_compact_readback_after_device_trim():
+    """d2h.compact=1 (key bitmap + u32 read-back) with a TOP large enough that the device trim's kept union holds more
+    than 65,536 groups: the result is the trimmed union (not a bitmap of every group), equal to the oracle's trim."""
+    e = GpuEngine(0, "d2h.compact=1")
+    gsegs, host = _synthetic(e, 2, 2_000_000)
+    q = compile_pql("SELECT SUM(d8), AVG(d8), DISTINCTCOUNTHLL(d5) FROM fact WHERE d2 < 800 GROUP BY d6, d7 TOP 20000")
+    exp = O.execute_group_by_arrays(host, q, num_groups_limit=1_000_000)
+    top, st = ServerQueryExecutor(e, num_groups_limit=1_000_000).group_by_result(q, gsegs, top_n=20000)
+    ukeys = top.raw_keys()
+    union = set()
+    for fn in range(len(q["aggregations"])):
+        kept = top.trimmed_groups(20000, fn)
+        want = exp["keys"][_oracle_trim(exp, q, fn, 20000)]
+        assert (ukeys[kept] == want).all(), q["aggregations"][fn]
+        union |= set(want.tolist())
+    assert len(union) >= 65536
+    assert sorted(union) == ukeys.tolist()
+    pos = np.searchsorted(exp["keys"], ukeys)
+    c, v = top.function_values(0)
+    assert (c == exp["fns"][0]["count"][pos]).all() and (v == exp["fns"][0]["sum"][pos]).all()
+    regs, cards = top.hll(2)
+    assert (cards == exp["fns"][2]["card"][pos]).all() and (regs == exp["fns"][2]["hll"][pos]).all()
+    del top
+    e.close()
+
+
+def test_diagnostic_keys_rejected():
+    """The product library has no wrong-result diagnostic modes: the former debug.emit / debug.ring keys are unknown
+    configuration keys (PINOT_ERR_BAD_ARG)."""
+    from pinot_amd import PinotGpuError
+    e = GpuEngine(0)
+    for key in ("debug.emit=4", "debug.ring=1"):
+        with pytest.raises(PinotGpuError) as ei:
+            e.set_config(key)
+        assert ei.value.status == 1
     e.close()

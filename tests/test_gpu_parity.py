@@ -395,7 +395,7 @@ def test_group_by_floating_point_keys(engine, gcols):
     g.release()
 
 
-GROUP_SINKS = ("group.mode=lds", "group.mode=global", "group.mode=partition",
+GROUP_SINKS = ("group.mode=lds", "group.mode=global", "group.mode=partition", "group.mode=partition;group.ring=0",
                # two-level partitioned plan: many 4-key partitions, EMIT into coarse runs of 4 / 256 partitions
                "group.mode=partition;group.pshift=2;group.split=2",
                "group.mode=partition;group.pshift=0;group.split=8",
@@ -611,7 +611,8 @@ def test_config1_baseball_synthetic(engine):
 
 
 @pytest.mark.parametrize("mode", ["group.mode=partition;group.pshift=3", "group.mode=partition;group.pshift=3;agg.affine=0",
-                                  "group.mode=partition;group.pshift=2;group.split=0", "group.mode=partition"])
+                                  "group.mode=partition;group.pshift=2;group.split=0", "group.mode=partition",
+                                  "group.mode=partition;group.ring=0"])
 def test_group_by_partitioned_affine(mode):
     """Partitioned plan over arithmetic-progression dictionaries (k_partition_reduce sums dictIds and hashes
     value = base + step * dictId on the device) against the oracle: SUM / AVG / MAX and DISTINCTCOUNTHLL of INT

@@ -66,7 +66,8 @@ def _same_value(f, g, e):
         assert g == e
 
 
-@pytest.mark.parametrize("cfg", ["", "exec.fused=0", "group.mode=lds", "group.mode=global", "group.mode=partition"])
+@pytest.mark.parametrize("cfg", ["", "exec.fused=0", "group.mode=lds", "group.mode=global", "group.mode=partition",
+                                 "group.mode=partition;group.ring=0"])
 def test_ragged_segments_group_by(engine, cfg):
     """Group-by over the same ragged segments (per-segment dictionaries -> the union key space and remaps), every
     sink; group columns INT / STRING, aggregations over INT / LONG / DOUBLE."""

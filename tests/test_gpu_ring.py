@@ -1,10 +1,12 @@
-"""GPU parity of the ring-partitioned group-by plan (group_ring.hip: GB_FILTER -> k_group_ring -> k_ring_reduce), the
+"""GPU parity of the ring-partitioned group-by plan (group_ring.hip: [GB_FILTER ->] k_group_ring -> k_ring_reduce), the
 plan config 4's 1M-key GROUP BY runs on: every group's count, integer sum, ordered MIN / MAX, double sum and HLL
 registers bit-exact against the oracle (DictionaryBasedGroupKeyGenerator.java:195-302,
 DefaultGroupByExecutor.java:70-168), including
 * the HLL registers whose rank exceeds the reduce's 4-bit nibbles (the exception list);
-* chunk windows from a sorted-index leaf, where one block gets all the matching docs (regions sized by the busiest
-  block);
+* the filter evaluated inside k_group_ring on each quarter (a conjunction of <= 2 scan leaves: RANGE, IN / NOT IN
+  tables, no filter at all) and every other filter shape through GB_FILTER's words (OR terms, sorted-index leaves, more
+  leaves);
+* chunk windows from a sorted-index leaf, where a few blocks get all the matching docs;
 * per-segment dictionaries of the group columns (dictId -> global id remaps) and ragged segment sizes;
 * skewed keys that overflow a region: the counted plan answers instead (group.ring_fallbacks), same results."""
 import numpy as np
@@ -46,13 +48,17 @@ def _assert_group_arrays(res, exp, q):
             assert (vals == r["max"]).all()
 
 
-def _run(e, q, gsegs, host, limit=1 << 22):
+def _run(e, q, gsegs, host, limit=1 << 22, qfilter=None):
+    """Runs q, checks it against the oracle; returns (ring-plan launches, fallbacks). qfilter: whether the ring kernel
+    must have evaluated the filter itself (True) or taken GB_FILTER's words (False)."""
     exp = O.execute_group_by_arrays(host, q, num_groups_limit=limit)
-    before = e.stat("group.ring_queries"), e.stat("group.ring_fallbacks")
+    before = e.stat("group.ring_queries"), e.stat("group.ring_fallbacks"), e.stat("group.ring_qfilter_queries")
     res, st = ServerQueryExecutor(e, num_groups_limit=limit).group_by_result(q, gsegs)
     assert st.num_docs_scanned == exp["scanned"]
     _assert_group_arrays(res, exp, q)
     del res
+    if qfilter is not None:
+        assert (e.stat("group.ring_qfilter_queries") - before[2]) == (1 if qfilter else 0)
     return e.stat("group.ring_queries") - before[0], e.stat("group.ring_fallbacks") - before[1]
 
 
@@ -62,8 +68,13 @@ def test_ring_config4_shape():
     e = GpuEngine(0, "group.ring=1")
     gsegs = [e.register_synthetic("fact_%d" % s, 2_000_000, CONFIG_COLUMNS, BASE_SEED + s) for s in range(2)]
     host = [synth.make_segment("fact_%d" % s, 2_000_000, CONFIG_COLUMNS, BASE_SEED + s) for s in range(2)]
-    ran, fell = _run(e, compile_pql(CONFIG4), gsegs, host, limit=1_000_000)
+    ran, fell = _run(e, compile_pql(CONFIG4), gsegs, host, limit=1_000_000, qfilter=True)
     assert (ran, fell) == (1, 0)
+    # the same query with the filter as GB_FILTER's words
+    e.set_config("group.ring_qfilter=0")
+    ran, fell = _run(e, compile_pql(CONFIG4), gsegs, host, limit=1_000_000, qfilter=False)
+    assert (ran, fell) == (1, 0)
+    e.set_config("group.ring_qfilter=1")
     # the counted plan on the same engine (group.ring=0) gives the same arrays
     e.set_config("group.ring=0")
     ran, fell = _run(e, compile_pql(CONFIG4), gsegs, host, limit=1_000_000)
@@ -118,14 +129,35 @@ def test_ring_remap_ragged_kinds(text):
 
 
 def test_ring_sorted_window_busiest_block():
-    """A sorted-index leaf bounds each segment's chunk window: all matching docs fall into a few blocks' chunk
-    ranges, so the regions are sized from the busiest block's matches (blk_matched), not the average."""
+    """A sorted-index leaf bounds each segment's chunk window: the blocks split the windows' chunks only (the sorted
+    leaf's ranges are not a quarter-form leaf: GB_FILTER's words)."""
     segs = [_mixed_segment("w0", 400_000, 11, np.arange(0, 100), np.arange(0, 100), sorted_ts=True),
             _mixed_segment("w1", 250_000, 12, np.arange(0, 100), np.arange(0, 100), sorted_ts=True)]
     e = GpuEngine(0, "group.mode=partition;group.ring=1")
     gsegs = [e.register(s) for s in segs]
     q = compile_pql("SELECT SUM(lv), MAX(dv) FROM t WHERE ts BETWEEN 40 AND 90 AND f < 95 GROUP BY k1, k2")
-    ran, fell = _run(e, q, gsegs, segs)
+    ran, fell = _run(e, q, gsegs, segs, qfilter=False)
+    assert (ran, fell) == (1, 0)
+    e.close()
+
+
+@pytest.mark.parametrize("qfilter", [1, 0])
+@pytest.mark.parametrize("text,qf", [
+    ("SELECT SUM(lv), COUNT(*) FROM t GROUP BY k1, k2", True),                              # no filter
+    ("SELECT SUM(lv), MAX(dv) FROM t WHERE k1 IN (3, 5, 7, 60, 61) GROUP BY k1, k2", True),  # IN: membership LUT
+    ("SELECT SUM(lv) FROM t WHERE f NOT IN (1, 2, 3) AND h > 20000 GROUP BY k2, k1", True),  # two leaves, negated
+    ("SELECT SUM(lv) FROM t WHERE f < 30 AND h > 20000 AND k1 <> 4 GROUP BY k1, k2", None),  # three leaves
+    ("SELECT SUM(lv), DISTINCTCOUNTHLL(h) FROM t WHERE f < 10 OR h < 9000 GROUP BY k1, k2", None),  # OR term
+])
+def test_ring_filter_forms(text, qf, qfilter):
+    """The filter shapes the ring kernel evaluates on each quarter (the planner may also hand it a `pre` bitset of
+    the terms it does not fuse: qf None), and every shape through GB_FILTER's words (group.ring_qfilter=0), over ragged
+    segments whose last chunk is partial (tail docs masked)."""
+    segs = [_mixed_segment("q0", 90_001, 21, np.arange(0, 90), np.arange(0, 80)),
+            _mixed_segment("q1", 41_000, 22, np.arange(10, 100), np.arange(5, 85))]
+    e = GpuEngine(0, "group.mode=partition;group.ring=1;group.ring_qfilter=%d" % qfilter)
+    gsegs = [e.register(s) for s in segs]
+    ran, fell = _run(e, compile_pql(text), gsegs, segs, qfilter=(qf if qfilter else False))
     assert (ran, fell) == (1, 0)
     e.close()
 

@@ -26,22 +26,10 @@
 #include "engine.h"
 
 namespace pinot {
+void host_parallel(size_t n, const std::function<void(size_t)> &fn);  // executor.cpp: the engine's task pool
+size_t host_parallelism();
+
 namespace {
-// fn(0) .. fn(n - 1) on n threads (fn(0) on the caller's); every started thread is joined, also when starting one or
-// fn(0) throws
-void run_parallel(size_t n, const std::function<void(size_t)> &fn) {
-  std::vector<std::thread> th;
-  struct Join {
-    std::vector<std::thread> &t;
-    ~Join() {
-      for (auto &x : t)
-        if (x.joinable()) x.join();
-    }
-  } join{th};
-  th.reserve(n ? n - 1 : 0);
-  for (size_t t = 1; t < n; t++) th.emplace_back(fn, t);
-  if (n) fn(0);
-}
 
 
 class Out {
@@ -221,24 +209,6 @@ size_t group_key_parts(const GroupByResult &r, int64_t g, const std::string **pa
   return len;
 }
 
-// One map entry (MAP_SER_DE: key String, then the value's int length and bytes) appended with one buffer growth:
-// the key written straight from the columns' value strings, without building it
-// (DictionaryBasedGroupKeyGenerator.java:421-437).
-template <typename F>
-void put_entry(Out &o, const GroupByResult &r, int64_t g, size_t vbytes, F &&value) {
-  const std::string *part[kMaxGroupCols];
-  const size_t nc = r.gcard.size();
-  const size_t klen = group_key_parts(r, g, part);
-  uint8_t *x = put_be32(o.grow(4 + klen + 4 + vbytes), (uint32_t)klen);
-  for (size_t j = 0; j < nc; j++) {
-    if (j) *x++ = '\t';
-    memcpy(x, part[j]->data(), part[j]->size());
-    x += part[j]->size();
-  }
-  x = put_be32(x, (uint32_t)vbytes);
-  value(x);
-}
-
 // DataSchema.toBytes (pinot-common/.../utils/DataSchema.java:114-139): names, then type names.
 void schema_bytes(Out &o, const std::vector<std::string> &names, const std::vector<std::string> &types) {
   o.i32((int32_t)names.size());
@@ -254,7 +224,10 @@ struct Table {
   Out schema, fixed, var;
 };
 
-std::vector<uint8_t> table_bytes(const Table &t) {
+// toBytes (DataTableImplV2.java:233-303) with the variable section written in place by write_var(dst) (var_size bytes):
+// the header, dictionary map, metadata, schema and fixed section first, then the variable section, in one buffer.
+template <typename W>
+std::vector<uint8_t> table_bytes_var(const Table &t, size_t var_size, W &&write_var) {
   Out dict;  // serializeDictionaryMap (DataTableImplV2.java:305-328): HashMap<String, HashMap<Integer, String>>
   {
     std::vector<int32_t> h;
@@ -282,33 +255,35 @@ std::vector<uint8_t> table_bytes(const Table &t) {
       meta.str(t.metadata[i].second);
     }
   }
-  Out o;  // toBytes (:233-303)
+  const size_t schema_size = t.has_schema ? t.schema.b.size() : 0;
   const int32_t header = 13 * 4;
-  o.i32(2);
-  o.i32(t.rows);
-  o.i32(t.cols);
+  const size_t total = header + dict.b.size() + meta.b.size() + schema_size + t.fixed.b.size() + var_size;
+  require(total < (size_t)INT32_MAX, PINOT_ERR_UNSUPPORTED, "DataTable over 2 GB (int offsets)");
+  std::vector<uint8_t> o(total);
+  uint8_t *x = o.data();
   int32_t off = header;
-  o.i32(off);
-  o.i32((int32_t)dict.b.size());
-  off += (int32_t)dict.b.size();
-  o.i32(off);
-  o.i32((int32_t)meta.b.size());
-  off += (int32_t)meta.b.size();
-  o.i32(off);
-  o.i32(t.has_schema ? (int32_t)t.schema.b.size() : 0);
-  off += t.has_schema ? (int32_t)t.schema.b.size() : 0;
-  o.i32(off);
-  o.i32((int32_t)t.fixed.b.size());
-  off += (int32_t)t.fixed.b.size();
-  o.i32(off);
-  o.i32((int32_t)t.var.b.size());
-  o.bytes(dict.b.data(), dict.b.size());
-  o.bytes(meta.b.data(), meta.b.size());
-  if (t.has_schema) o.bytes(t.schema.b.data(), t.schema.b.size());
-  o.bytes(t.fixed.b.data(), t.fixed.b.size());
-  o.bytes(t.var.b.data(), t.var.b.size());
-  require(o.b.size() < (size_t)INT32_MAX, PINOT_ERR_UNSUPPORTED, "DataTable over 2 GB (int offsets)");
-  return std::move(o.b);
+  const int32_t head[13] = {2, t.rows, t.cols,
+                            off, (int32_t)dict.b.size(),
+                            off + (int32_t)dict.b.size(), (int32_t)meta.b.size(),
+                            off + (int32_t)(dict.b.size() + meta.b.size()), (int32_t)schema_size,
+                            off + (int32_t)(dict.b.size() + meta.b.size() + schema_size), (int32_t)t.fixed.b.size(),
+                            off + (int32_t)(dict.b.size() + meta.b.size() + schema_size + t.fixed.b.size()),
+                            (int32_t)var_size};
+  for (int i = 0; i < 13; i++) x = put_be32(x, (uint32_t)head[i]);
+  memcpy(x, dict.b.data(), dict.b.size());
+  x += dict.b.size();
+  memcpy(x, meta.b.data(), meta.b.size());
+  x += meta.b.size();
+  if (schema_size) memcpy(x, t.schema.b.data(), schema_size);
+  x += schema_size;
+  memcpy(x, t.fixed.b.data(), t.fixed.b.size());
+  x += t.fixed.b.size();
+  write_var(x);
+  return o;
+}
+
+std::vector<uint8_t> table_bytes(const Table &t) {
+  return table_bytes_var(t, t.var.b.size(), [&](uint8_t *x) { memcpy(x, t.var.b.data(), t.var.b.size()); });
 }
 
 // attachMetadataToDataTable (IntermediateResultsBlock.java:298-317) + the server's own keys
@@ -378,83 +353,108 @@ std::vector<uint8_t> group_by_datatable(const pinot_query &q, const GroupByResul
                                         const int64_t *fn_num_groups, const pinot_exec_stats &s,
                                         const pinot_datatable_server *srv) {
   // getAggregationGroupByResultDataTable (:272-292): per function a row (functionName STRING via the column's
-  // dictionary, GroupByResultMap OBJECT = Map<String group key, intermediate result>)
+  // dictionary, GroupByResultMap OBJECT = Map<String group key, intermediate result>). The final buffer is laid out
+  // once (every map entry's size from its key's length), then the entries are written in place by the host's task
+  // pool in chunks of the concatenated entry lists.
   const int na = (int)r.functions.size();
   const int64_t n = (int64_t)r.raw_keys.size();
   Table t;
   t.rows = na;
   t.cols = 2;
   schema_bytes(t.schema, {"functionName", "GroupByResultMap"}, {"STRING", "OBJECT"});
-  // each function's map serialized on its own thread (they are independent; large trimmed results take ms each),
-  // then the rows appended in function order
-  std::vector<Out> cells(na);
-  std::vector<std::exception_ptr> errs(na);
-  auto build = [&](int i) {
-    try {
-      const int64_t m = fn_groups && fn_groups[i] ? fn_num_groups[i] : n;
-      auto group = [&](int64_t j) -> int64_t {
-        const int64_t g = fn_groups && fn_groups[i] ? fn_groups[i][j] : j;
-        require(g >= 0 && g < n, PINOT_ERR_BAD_ARG, "group index out of range");
-        return g;
-      };
-      const int f = sv_function(r.functions[i]);
-      // registers: the host copy as it is, or the device parts through pinned staging (a large pageable copy target
-      // is pinned in place by the runtime, and its later unmap stalls the GPU's queues: ~20 ms on the next query)
-      std::unique_ptr<PinnedBytes> stage;
-      const uint8_t *regs = nullptr;
-      // a device-trimmed result carries each HLL function's getBytes rows (hll_serde.hip): copied as they are
-      const uint8_t *ser = (f == PINOT_AGG_DISTINCTCOUNTHLL && (size_t)i < r.hll_bytes.size() &&
-                            r.hll_bytes[i].size() == (size_t)n * 180)
-                               ? r.hll_bytes[i].data()
-                               : nullptr;
-      if (f == PINOT_AGG_DISTINCTCOUNTHLL && !ser) {
-        if (r.hll_parts.empty()) {
-          regs = r.hll[i].data();
-        } else {
-          stage.reset(new PinnedBytes((size_t)n * 256));
-          group_by_hll_registers(r, i, stage->data(), true);
-          regs = stage->data();
-        }
-      }
-      const HostVec<int64_t> &cnt = r.counts[r.counts_shared ? 0 : i];
-      const HostVec<double> &val = r.values[i];
-      const int32_t vtype = f == PINOT_AGG_COUNT ? OBJ_LONG : f == PINOT_AGG_AVG ? OBJ_AVG_PAIR
-                            : f == PINOT_AGG_DISTINCTCOUNTHLL ? OBJ_HLL : OBJ_DOUBLE;
-      Out &v = cells[i];  // MAP_SER_DE (ObjectSerDeUtils.java:262-300)
-      v.i32((int32_t)m);
-      if (m == 0) return;
-      v.i32(OBJ_STRING);
-      v.i32(vtype);
-      v.b.reserve(v.b.size() + (size_t)m * (16 + (f == PINOT_AGG_DISTINCTCOUNTHLL ? 8 + 43 * 4 : 16)));
-      auto bits = [](double d) {
-        uint64_t u;
-        memcpy(&u, &d, 8);
-        return u;
-      };
-      for (int64_t j = 0; j < m; j++) {
-        const int64_t g = group(j);
-        switch (f) {
-          case PINOT_AGG_COUNT: put_entry(v, r, g, 8, [&](uint8_t *x) { put_be64(x, (uint64_t)cnt[g]); }); break;
-          case PINOT_AGG_AVG:
-            put_entry(v, r, g, 16, [&](uint8_t *x) { put_be64(put_be64(x, bits(val[g])), (uint64_t)cnt[g]); });
-            break;
-          case PINOT_AGG_DISTINCTCOUNTHLL:
-            if (ser) put_entry(v, r, g, 8 + 43 * 4, [&](uint8_t *x) { memcpy(x, ser + (size_t)g * 180, 180); });
-            else put_entry(v, r, g, 8 + 43 * 4, [&](uint8_t *x) { hll_bytes_at(x, regs + (size_t)g * 256); });
-            break;
-          default: put_entry(v, r, g, 8, [&](uint8_t *x) { put_be64(x, bits(val[g])); }); break;
-        }
-      }
-    } catch (...) {
-      errs[i] = std::current_exception();
-    }
+  struct Fn {
+    int64_t m = 0;           // entries of the map
+    const int64_t *sel = nullptr;  // its groups (null: 0 .. m - 1)
+    int f = 0;
+    int32_t vtype = 0, vbytes = 0;
+    const uint8_t *ser = nullptr, *regs = nullptr;  // HLL: getBytes rows / u8 register rows
+    std::unique_ptr<PinnedBytes> stage;
+    int64_t first = 0;       // index of its first entry in the concatenated list
   };
-  if (na > 1 && n >= 4096) run_parallel((size_t)na, [&](size_t i) { build((int)i); });
-  else
-    for (int i = 0; i < na; i++) build(i);
-  for (auto &e : errs)
-    if (e) std::rethrow_exception(e);
+  std::vector<Fn> fns(na);
+  int64_t total_entries = 0;
+  for (int i = 0; i < na; i++) {
+    Fn &F = fns[i];
+    F.m = fn_groups && fn_groups[i] ? fn_num_groups[i] : n;
+    F.sel = fn_groups && fn_groups[i] ? fn_groups[i] : nullptr;
+    for (int64_t j = 0; F.sel && j < F.m; j++)
+      require(F.sel[j] >= 0 && F.sel[j] < n, PINOT_ERR_BAD_ARG, "group index out of range");
+    F.f = sv_function(r.functions[i]);
+    F.vtype = F.f == PINOT_AGG_COUNT ? OBJ_LONG : F.f == PINOT_AGG_AVG ? OBJ_AVG_PAIR
+              : F.f == PINOT_AGG_DISTINCTCOUNTHLL ? OBJ_HLL : OBJ_DOUBLE;
+    F.vbytes = F.f == PINOT_AGG_AVG ? 16 : F.f == PINOT_AGG_DISTINCTCOUNTHLL ? 8 + 43 * 4 : 8;
+    if (F.f == PINOT_AGG_DISTINCTCOUNTHLL && F.m) {
+      // a device-trimmed result carries the getBytes rows (hll_serde.hip); else the registers: the host copy, or the
+      // device parts through pinned staging (a large pageable copy target is pinned in place by the runtime, and its
+      // later unmap stalls the GPU's queues)
+      if ((size_t)i < r.hll_bytes.size() && r.hll_bytes[i].size() == (size_t)n * 180) {
+        F.ser = r.hll_bytes[i].data();
+      } else if (r.hll_parts.empty()) {
+        F.regs = r.hll[i].data();
+      } else {
+        F.stage.reset(new PinnedBytes((size_t)n * 256));
+        group_by_hll_registers(r, i, F.stage->data(), true);
+        F.regs = F.stage->data();
+      }
+    }
+    F.first = total_entries;
+    total_entries += F.m;
+  }
+  // entry sizes (MAP_SER_DE, ObjectSerDeUtils.java:262-300: key String = int length + bytes, value = int length +
+  // bytes), in chunks over the pool
+  const size_t nt = total_entries >= 4096 ? std::max<size_t>(1, std::min<size_t>(host_parallelism(), 16)) : 1;
+  std::vector<uint32_t> esize((size_t)total_entries);
+  auto fn_of = [&](int64_t e) {
+    int i = 0;
+    while (i + 1 < na && fns[i + 1].first <= e) i++;
+    return i;
+  };
+  auto for_chunks = [&](const std::function<void(int64_t, int64_t)> &body) {
+    if (nt == 1) {
+      body(0, total_entries);
+      return;
+    }
+    std::vector<std::exception_ptr> errs(nt);
+    host_parallel(nt, [&](size_t c) {
+      try {
+        body(total_entries * (int64_t)c / (int64_t)nt, total_entries * (int64_t)(c + 1) / (int64_t)nt);
+      } catch (...) {
+        errs[c] = std::current_exception();
+      }
+    });
+    for (auto &e : errs)
+      if (e) std::rethrow_exception(e);
+  };
+  for_chunks([&](int64_t lo, int64_t hi) {
+    const std::string *part[kMaxGroupCols];
+    for (int64_t e = lo; e < hi;) {
+      const int i = fn_of(e);
+      const Fn &F = fns[i];
+      const int64_t end = std::min(hi, F.first + F.m);
+      for (; e < end; e++) {
+        const int64_t j = e - F.first, g = F.sel ? F.sel[j] : j;
+        esize[e] = (uint32_t)(8 + group_key_parts(r, g, part) + F.vbytes);
+      }
+    }
+  });
+  // cell sizes and the variable section's layout: per row the object type, then the map (size, key and value types,
+  // entries); the entries' offsets as one exclusive prefix sum
+  std::vector<uint64_t> eoff((size_t)total_entries + 1);
+  std::vector<int64_t> cell(na);
+  size_t var = 0;
+  for (int i = 0; i < na; i++) {
+    const Fn &F = fns[i];
+    var += 4;  // object type
+    const size_t start = var;
+    var += 4 + (F.m ? 8 : 0);
+    for (int64_t j = 0; j < F.m; j++) {
+      eoff[F.first + j] = var;
+      var += esize[F.first + j];
+    }
+    cell[i] = (int64_t)(var - start);
+  }
   std::vector<std::string> fn_names;
+  size_t vpos = 0;
   for (int i = 0; i < na; i++) {
     const std::string name = aggregation_column_name(q.aggregations[i]);
     int32_t id = (int32_t)fn_names.size();
@@ -462,13 +462,60 @@ std::vector<uint8_t> group_by_datatable(const pinot_query &q, const GroupByResul
       if (fn_names[k] == name) id = (int32_t)k;
     if (id == (int32_t)fn_names.size()) fn_names.push_back(name);
     t.fixed.i32(id);
-    object_cell(t, OBJ_MAP, [&](Out &v) { v.b.swap(cells[i].b); });
+    t.fixed.i32((int32_t)vpos);  // DataTableBuilder.setColumn(int, Object): (variable offset, serialized length)
+    t.fixed.i32((int32_t)cell[i]);
+    vpos += 4 + (size_t)cell[i];
   }
   t.dictionaries.emplace_back("functionName", fn_names);
   // CombineGroupByOperator.java:212-214: the merged map reached the inner-segment groups limit
   const int64_t merged = r.merged_groups >= 0 ? r.merged_groups : n;  // the device trim keeps fewer than it merged
   attach_metadata(t, s, merged >= (int64_t)q.num_groups_limit && q.num_groups_limit > 0, srv);
-  return table_bytes(t);
+  auto bits = [](double d) {
+    uint64_t u;
+    memcpy(&u, &d, 8);
+    return u;
+  };
+  return table_bytes_var(t, var, [&](uint8_t *v) {
+    size_t at = 0;
+    for (int i = 0; i < na; i++) {  // the rows' heads
+      uint8_t *x = put_be32(v + at, (uint32_t)OBJ_MAP);
+      x = put_be32(x, (uint32_t)fns[i].m);
+      if (fns[i].m) put_be32(put_be32(x, (uint32_t)OBJ_STRING), (uint32_t)fns[i].vtype);
+      at += 4 + (size_t)cell[i];
+    }
+    for_chunks([&](int64_t lo, int64_t hi) {
+      const std::string *part[kMaxGroupCols];
+      const size_t nc = r.gcard.size();
+      for (int64_t e = lo; e < hi;) {
+        const int i = fn_of(e);
+        const Fn &F = fns[i];
+        const HostVec<int64_t> &cnt = r.counts[r.counts_shared ? 0 : i];
+        const HostVec<double> &val = r.values[i];
+        const int64_t end = std::min(hi, F.first + F.m);
+        for (; e < end; e++) {
+          const int64_t j = e - F.first, g = F.sel ? F.sel[j] : j;
+          // the key written straight from the columns' value strings (DictionaryBasedGroupKeyGenerator.java:421-437)
+          const size_t klen = group_key_parts(r, g, part);
+          uint8_t *x = put_be32(v + eoff[e], (uint32_t)klen);
+          for (size_t c = 0; c < nc; c++) {
+            if (c) *x++ = '\t';
+            memcpy(x, part[c]->data(), part[c]->size());
+            x += part[c]->size();
+          }
+          x = put_be32(x, (uint32_t)F.vbytes);
+          switch (F.f) {
+            case PINOT_AGG_COUNT: put_be64(x, (uint64_t)cnt[g]); break;
+            case PINOT_AGG_AVG: put_be64(put_be64(x, bits(val[g])), (uint64_t)cnt[g]); break;
+            case PINOT_AGG_DISTINCTCOUNTHLL:
+              if (F.ser) memcpy(x, F.ser + (size_t)g * 180, 180);
+              else hll_bytes_at(x, F.regs + (size_t)g * 256);
+              break;
+            default: put_be64(x, bits(val[g])); break;
+          }
+        }
+      }
+    });
+  });
 }
 
 std::vector<uint8_t> empty_datatable(const pinot_query &q, int64_t total_docs, const pinot_datatable_server *srv) {

@@ -32,6 +32,7 @@
 
 #include "engine.h"
 #include "group_ring.h"
+#include "mv_hash.h"
 
 namespace pinot {
 // fused_group.hip: the k_group_query instance a launch of `a` runs (mode * 10000 + read path * 1000 + threads)
@@ -1908,7 +1909,7 @@ size_t host_threads();
 // Dense accumulators -> result arrays (bitset path and the multi-GPU partial finalize): ordered device
 // compaction of the non-empty keys, one gather, D2H into grow-only engine buffers, host fill over 8 threads.
 std::unique_ptr<GroupByResult> finalize_groups(Engine &e, const pinot_query &q, const GroupAccs &ga,
-                                               const KeySpace &ks, GroupByProgram gp) {
+                                               const KeySpace &ks, GroupByProgram gp, const MvHash *mh = nullptr) {
   const int na = q.num_aggregations;
   const size_t cscr = compact_keys_scratch_bytes(ks.G);
   e.group_final.reserve(std::max<int64_t>(ks.G, 1) * 8 + 64 + cscr);
@@ -1944,6 +1945,14 @@ std::unique_ptr<GroupByResult> finalize_groups(Engine &e, const pinot_query &q, 
   PINOT_HIP(hipMemcpyAsync(o_keys, keys_dev, n * 8, hipMemcpyDeviceToDevice, e.stream));
   launch_gather_groups(gp, keys_dev, (int64_t)n, o_cnt, o_acc, o_hll, e.stream);
   PINOT_HIP(hipGetLastError());
+  DeviceBuffer ids;
+  if (mh) {  // hashed key space: the groups are slots; their global-id tuples from the table
+    ids.alloc(n * q.num_group_by * 4 + 16);
+    launch_mv_hash_tuples(*mh, q.num_group_by, keys_dev, (long long)n, ids.get<int32_t>(), e.stream);
+    PINOT_HIP(hipGetLastError());
+    res->key_ids.resize(n * q.num_group_by);
+    PINOT_HIP(hipMemcpyAsync(res->key_ids.data(), ids.get(), n * q.num_group_by * 4, hipMemcpyDeviceToHost, e.stream));
+  }
   PINOT_HIP(hipMemcpyAsync(e.group_host.get(), e.group_out.get(), out_b, hipMemcpyDeviceToHost, e.stream));
   wait_stream(e);
   const auto *hkeys = e.group_host.get<long long>();
@@ -3697,7 +3706,7 @@ namespace {
 // first-appearance admission per segment, then the 2 x limit cap (here, or the server's across ranks: `mp`).
 std::unique_ptr<GroupByResult> exec_group_by_mv(Engine &e, const std::vector<SegmentData *> &segs,
                                                 const pinot_query &q, pinot_exec_stats *stats,
-                                                const MvPartial *mp = nullptr) {
+                                                const MvPartial *mp = nullptr, int attempt = 0) {
   std::vector<int> hidden;
   std::vector<pinot_agg_spec> specs = mv_extended_specs(q, hidden);
   pinot_query q2 = q;
@@ -3718,12 +3727,41 @@ std::unique_ptr<GroupByResult> exec_group_by_mv(Engine &e, const std::vector<Seg
     ks = build_key_space(segs, q2);
   }
   const int64_t limit = q.num_groups_limit > 0 ? q.num_groups_limit : e.num_groups_limit;
-  require(!ks.hashed, PINOT_ERR_UNSUPPORTED,
-          "multi-value group-by over a hashed key space (LONG_MAP / ARRAY_MAP holder shapes)");
+  require(!(ks.hashed && mp), PINOT_ERR_UNSUPPORTED, "multi-GPU partials of a multi-value group-by over a hashed key space");
+  const size_t S = segs.size();
+  QueryScratch qs = prepare(e, plans, ar);
+  Timer t(e);
+  // hashed key space (LONG_MAP / ARRAY_MAP holder shapes, mv_hash.h): slots = a power of two >= 2 x the keys the
+  // matching docs yield, counted on the device
+  int64_t hcap = 0;
+  if (ks.hashed) {
+    DeviceBuffer tot(64);
+    PINOT_HIP(hipMemsetAsync(tot.get(), 0, 8, e.stream));
+    for (size_t si = 0; si < S; si++) {
+      SegPlan &pl = plans[si];
+      if (pl.empty || pl.seg->num_docs == 0) continue;
+      MvGroupArgs c{};
+      c.n_gcols = q.num_group_by;
+      for (int j = 0; j < q.num_group_by; j++) {
+        const ColumnData &col = *pl.seg->column(q.group_by[j]);
+        c.goff[j] = col.mv ? col.mv_offsets.get<uint32_t>() : nullptr;
+      }
+      c.bitset = run_filter(e, pl, qs, t);
+      c.nwords = pl.seg->nwords();
+      c.num_docs = pl.seg->num_docs;
+      launch_mv_key_count(c, tot.get<unsigned long long>(), e.stream);
+      PINOT_HIP(hipGetLastError());
+    }
+    unsigned long long keys = 0;
+    PINOT_HIP(hipMemcpyAsync(&keys, tot.get(), 8, hipMemcpyDeviceToHost, e.stream));
+    wait_stream(e);
+    hcap = 1024;
+    while (hcap < 2 * (int64_t)keys) hcap <<= 1;
+    ks.G = hcap;
+  }
   // num.groups.limit (DictionaryBasedGroupKeyGenerator :79-126, IntMapBasedHolder.processMultiValue :282-300): a segment
   // whose cardinality product exceeds max.init.group.holder.capacity admits the first min(product, limit) distinct keys
   // in doc order, each doc's keys in getIntRawKeys order; then CombineGroupByOperator's 2 x limit cap in segment order
-  const size_t S = segs.size();
   AdmissionPlan adm;
   {
     const int64_t threshold = q.max_init_group_holder_capacity > 0 ? q.max_init_group_holder_capacity : 10000;
@@ -3770,13 +3808,23 @@ std::unique_ptr<GroupByResult> exec_group_by_mv(Engine &e, const std::vector<Seg
     ga.acc_kind.push_back(kind);
     ga.acc_bytes_per_key.push_back(bytes);
   }
-  size_t per_key = 8;
+  size_t per_key = 8 + (ks.hashed ? 8 + 4 * (size_t)q.num_group_by : 0);  // (+ the table's fingerprint and tuple)
   for (auto b : ga.acc_bytes_per_key) per_key += b;
   size_t free_b = 0, total_b = 0;
   PINOT_HIP(hipMemGetInfo(&free_b, &total_b));
   require((double)ks.G * per_key < 0.5 * (double)free_b, PINOT_ERR_UNSUPPORTED,
           "dense group-by accumulators do not fit in HBM");
-  QueryScratch qs = prepare(e, plans, ar);
+  MvHash mh{};
+  if (ks.hashed) {
+    e.group_hash.reserve((size_t)hcap * (8 + 4 * (size_t)q.num_group_by) + 256);
+    mh.htable = e.group_hash.get<unsigned long long>();
+    mh.tuples = reinterpret_cast<int32_t *>(mh.htable + hcap);
+    mh.verify_err = reinterpret_cast<uint32_t *>(e.group_hash.get<uint8_t>() + (size_t)hcap * (8 + 4 * (size_t)q.num_group_by));
+    mh.hcap = hcap;
+    mh.hseed = 0x5EEDF00Dull + 0x9E3779B97F4A7C15ull * (unsigned long long)(attempt + 1);
+    PINOT_HIP(hipMemsetAsync(mh.htable, 0, (size_t)hcap * 8, e.stream));
+    PINOT_HIP(hipMemsetAsync(mh.verify_err, 0, 4, e.stream));
+  }
   e.group_scratch.reserve(ks.G * per_key + 64);
   uint8_t *base = e.group_scratch.get<uint8_t>();
   auto *counts = reinterpret_cast<unsigned long long *>(base);
@@ -3795,7 +3843,6 @@ std::unique_ptr<GroupByResult> exec_group_by_mv(Engine &e, const std::vector<Seg
   }
   PINOT_HIP(hipEventRecord(e.ev_start, e.stream));
   if (!(mp && !mp->accs)) init_accs(e, ks.G, counts, ga, accs.data());  // (the admission export: no arrays)
-  Timer t(e);
   std::vector<DeviceBuffer> remaps(S * q.num_group_by);
   std::vector<int64_t> seg_counts(S, 0);
   auto mv_args = [&](size_t si, const uint64_t *bits) {
@@ -3842,6 +3889,13 @@ std::unique_ptr<GroupByResult> exec_group_by_mv(Engine &e, const std::vector<Seg
     a.num_docs = sg.num_docs;
     return a;
   };
+  if (ks.hashed)  // the table: every matching doc's keys
+    for (size_t si = 0; si < S; si++) {
+      SegPlan &pl = plans[si];
+      if (pl.empty || pl.seg->num_docs == 0) continue;
+      launch_mv_hash_insert(mv_args(si, run_filter(e, pl, qs, t)), mh, e.stream);
+      PINOT_HIP(hipGetLastError());
+    }
   // admission: every segment's first-appearance bitmap (first positions, one radix sort each), then the cap
   DeviceBuffer adm_buf;
   int64_t words = 0;
@@ -3868,7 +3922,8 @@ std::unique_ptr<GroupByResult> exec_group_by_mv(Engine &e, const std::vector<Seg
       if (pl.empty || pl.seg->num_docs == 0) continue;
       const MvGroupArgs a = mv_args(si, run_filter(e, pl, qs, t));
       PINOT_HIP(hipMemsetAsync(first_pos, 0xFF, (size_t)ks.G * 8, e.stream));
-      launch_first_pos_mv(a, first_pos, e.stream);
+      if (ks.hashed) launch_first_pos_mv_hashed(a, mh, first_pos, e.stream);
+      else launch_first_pos_mv(a, first_pos, e.stream);
       launch_admission_bitmap_u64(first_pos, ks.G, adm.upper[si], bitmaps + si * words, words,
                                   adm_buf.get<uint8_t>() + fp_b + bm_b, scr, e.stream);
       PINOT_HIP(hipGetLastError());
@@ -3899,8 +3954,20 @@ std::unique_ptr<GroupByResult> exec_group_by_mv(Engine &e, const std::vector<Seg
     if (adm.active)
       a.admitted = reinterpret_cast<const uint32_t *>(adm_buf.get<uint8_t>() + ((size_t)ks.G * 8 + 255) / 256 * 256) +
                    si * words;
-    t.timed(1, [&] { launch_group_by_mv(a, e.stream); });
+    t.timed(1, [&] {
+      if (ks.hashed) launch_group_by_mv_hashed(a, mh, e.stream);
+      else launch_group_by_mv(a, e.stream);
+    });
     PINOT_HIP(hipGetLastError());
+  }
+  if (ks.hashed) {  // a fingerprint collision: retry with another seed
+    uint32_t verify_err = 0;
+    PINOT_HIP(hipMemcpyAsync(&verify_err, mh.verify_err, 4, hipMemcpyDeviceToHost, e.stream));
+    wait_stream(e);
+    if (verify_err) {
+      require(attempt < 3, PINOT_ERR_DEVICE, "group-key fingerprint collisions persist");
+      return exec_group_by_mv(e, segs, q, stats, mp, attempt + 1);
+    }
   }
   if (mp) {  // partial: the u32 registers into the server's u8 layout, the statistics, no finalisation
     for (int a = 0; a < nb; a++)
@@ -3919,7 +3986,7 @@ std::unique_ptr<GroupByResult> exec_group_by_mv(Engine &e, const std::vector<Seg
   gp.n_aggs = nb;
   gp.counts = counts;
   for (int a = 0; a < nb; a++) { gp.acc[a] = accs[a]; gp.acc_kind[a] = ga.acc_kind[a]; }
-  auto res = finalize_groups(e, q2, ga, ks, gp);
+  auto res = finalize_groups(e, q2, ga, ks, gp, ks.hashed ? &mh : nullptr);
   PINOT_HIP(hipEventRecord(e.ev_stop, e.stream));
   wait_stream(e);
   float ms = 0;
@@ -4717,4 +4784,8 @@ void exec_group_by_mv_partial(Engine &e, const std::vector<SegmentData *> &segs,
                               const MvPartial &mp, pinot_exec_stats *stats) {
   exec_group_by_mv(e, segs, q, stats, &mp);
 }
+
+// The engine's host task pool for other translation units (datatable.cpp): fn(0) .. fn(n - 1), every task joined.
+void host_parallel(size_t n, const std::function<void(size_t)> &fn) { parallel_tasks(n, fn); }
+size_t host_parallelism() { return host_threads(); }
 }  // namespace pinot

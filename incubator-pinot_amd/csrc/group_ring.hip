@@ -117,35 +117,54 @@ template <int KP>
 __device__ __forceinline__ void ring_flush_phase(const RingArgs &a, const RingLds &L, unsigned long long *region0,
                                                  uint32_t C, int fw, int lane, uint32_t (&front)[KP],
                                                  uint32_t &status) {
+  // every counter, then the oldest half of every bucket holding 8 or more entries, then the stores: two LDS round
+  // trips per phase whatever the number of full buckets
   uint32_t c[KP];
 #pragma unroll
   for (int k = 0; k < KP; k++) {
     const int p = fw * 64 + lane + 64 * kRingFlushWaves * k;
     c[k] = p < a.P ? L.ctr[p] : 0u;
   }
+  u32x4 x[KP][4];
+#pragma unroll
+  for (int k = 0; k < KP; k++) {
+    const int p = fw * 64 + lane + 64 * kRingFlushWaves * k;
+    if ((c[k] & 0xFFFFu) >= 8u) {
+      const u32x4 *src = reinterpret_cast<const u32x4 *>(L.bkt + p * kRingBucket + (c[k] >> 16));
+#pragma unroll
+      for (int r = 0; r < 4; r++) x[k][r] = src[r];
+    }
+  }
+  const u32x4 m = {0xFFFFFFFFu, 0x001FFFFFu, 0xFFFFFFFFu, 0x001FFFFFu};  // strip the partition bits
 #pragma unroll
   for (int k = 0; k < KP; k++) {
     const int p = fw * 64 + lane + 64 * kRingFlushWaves * k;
     uint32_t n = min(c[k] & 0xFFFFu, (uint32_t)kRingBucket), h = c[k] >> 16;
     if (n < 8u) continue;  // no complete half: the counter stays
-    while (n >= 8u) {
+    if (front[k] + 8u <= C) {
+      u32x4 *dst = reinterpret_cast<u32x4 *>(region0 + (size_t)p * a.nblk * C + front[k]);
+#pragma unroll
+      for (int r = 0; r < 4; r++) __builtin_nontemporal_store(x[k][r] & m, dst + r);
+    } else {
+      status |= 1u;  // region full: the query falls back to the counted plan
+    }
+    front[k] += 8u;
+    h ^= 8u;
+    n -= 8u;
+    if (n >= 8u) {  // a full bucket (it overflowed this round): its second half too (rare)
       const u32x4 *src = reinterpret_cast<const u32x4 *>(L.bkt + p * kRingBucket + h);
-      const u32x4 x0 = src[0], x1 = src[1], x2 = src[2], x3 = src[3];
       if (front[k] + 8u <= C) {
         u32x4 *dst = reinterpret_cast<u32x4 *>(region0 + (size_t)p * a.nblk * C + front[k]);
-        const u32x4 m = {0xFFFFFFFFu, 0x001FFFFFu, 0xFFFFFFFFu, 0x001FFFFFu};  // strip the partition bits
-        __builtin_nontemporal_store(x0 & m, dst);
-        __builtin_nontemporal_store(x1 & m, dst + 1);
-        __builtin_nontemporal_store(x2 & m, dst + 2);
-        __builtin_nontemporal_store(x3 & m, dst + 3);
+#pragma unroll
+        for (int r = 0; r < 4; r++) __builtin_nontemporal_store(src[r] & m, dst + r);
       } else {
-        status |= 1u;  // region full: the query falls back to the counted plan
+        status |= 1u;
       }
       front[k] += 8u;
       h ^= 8u;
       n -= 8u;
     }
-    if (p < a.P) L.ctr[p] = (h << 16) | n;
+    L.ctr[p] = (h << 16) | n;
   }
 }
 
@@ -392,6 +411,9 @@ struct RingDecoder {
     }
     word_bits = (uint32_t)(word >> (16 * (lane & 3))) & 0xFFFFu;
     qi = ch * 256 + 64 * q + lane;
+#ifdef RING_EXP_NODEC
+    return;  // experiment: no column loads (decode() makes synthetic records)
+#endif
 #pragma unroll
     for (int i = 0; i < NF; i++)
       if (i < sg.n_leaves) ring_load_raw(st[i].fwd, st[i].bits, qi, F[i]);
@@ -409,6 +431,16 @@ struct RingDecoder {
       act = 0;
       return;
     }
+#ifdef RING_EXP_NODEC
+    {  // experiment: records of pseudo-random keys, no column data
+#pragma unroll
+      for (int j = 0; j < 16; j++) {
+        const uint32_t key = (uint32_t)((((unsigned long long)(qi * 16 + j) * 0x9E3779B97F4A7C15ull) >> 40) % (uint64_t)a.G);
+        rec[j] = (unsigned long long)(key & ((1u << a.shift) - 1u)) | ((unsigned long long)(key >> a.shift) << kRecPShift);
+      }
+      return;
+    }
+#endif
     if constexpr (NF > 0) {
 #pragma unroll
       for (int i = 0; i < NF; i++)
@@ -528,14 +560,20 @@ __global__ __launch_bounds__(kRingBlock) void k_group_ring(RingArgs a) {
 #endif
     for (int64_t t = 0; t < npass; t++) {
       RT_MARK(x0);
+#ifndef RING_EXP_NOINS
       ring_insert<0>(a, L, d.act, d.rec, region0, C);
+#endif
       RT_ADD(ti, x0);
       RT_MARK(x1);
       __syncthreads();  // inserts of round 0 done
       __syncthreads();  // flush done
       RT_ADD(tb, x1);
       RT_MARK(x2);
+#ifndef RING_EXP_NOINS
       ring_insert<kRingRoundRecs>(a, L, d.act, d.rec, region0, C);
+#else
+      if (d.rec[3] == 0x0123456789ull && d.act == 7) status |= 8u;
+#endif
       RT_ADD(ti, x2);
       RT_MARK(x3);
       __syncthreads();  // inserts of round 1 done

@@ -8,6 +8,7 @@
 // K7 HLL update       DistinctCountHLLAggregationFunction (register/rank precomputed per dictId on the host)
 // plus the device-side packers (synthetic bench columns, sorted-column forward index).
 #include "kernels.h"
+#include "mv_hash.h"
 #include "common.h"
 
 #include <hip/hip_runtime.h>
@@ -387,78 +388,169 @@ __device__ __forceinline__ void mv_fold(const MvGroupArgs &a, int g, long long k
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_group_by_mv(MvGroupArgs a) {
+__device__ __forceinline__ unsigned long long mv_mix(unsigned long long x) {
+  x ^= x >> 33;
+  x *= 0xFF51AFD7ED558CCDull;
+  x ^= x >> 33;
+  x *= 0xC4CEB9FE1A85EC53ull;
+  x ^= x >> 33;
+  return x;
+}
+
+// global id of group column j at entry position v
+__device__ __forceinline__ int32_t mv_gid(const MvGroupArgs &a, int j, uint32_t v) {
+  const int32_t id = (int32_t)read_packed(a.gfwd[j], a.gbits[j], v);
+  return a.remap[j] ? a.remap[j][id] : id;
+}
+
+// the tuple's fingerprint (never 0: 0 marks an empty slot)
+__device__ __forceinline__ unsigned long long mv_fingerprint(const MvGroupArgs &a, const MvHash &h, const uint32_t *cur) {
+  unsigned long long fp = h.hseed;
+  for (int j = 0; j < a.n_gcols; j++)
+    fp = mv_mix(fp ^ ((unsigned long long)(uint32_t)mv_gid(a, j, cur[j]) + 0x9E3779B97F4A7C15ull * (unsigned long long)(j + 1)));
+  return fp | 1ull;
+}
+
+// The key of the odometer position `cur`: the dense mixed-radix key, or (H) the slot of its tuple; -1 = the slot holds
+// another tuple under the same fingerprint (reported, the key dropped: the host retries with another seed).
+template <bool H>
+__device__ __forceinline__ long long mv_key(const MvGroupArgs &a, const MvHash &h, const uint32_t *cur) {
+  if constexpr (!H) {
+    long long key = 0;
+    for (int j = 0; j < a.n_gcols; j++) key += (long long)mv_gid(a, j, cur[j]) * a.stride[j];
+    return key;
+  } else {
+    const unsigned long long fp = mv_fingerprint(a, h, cur);
+    const unsigned long long m = (unsigned long long)h.hcap - 1ull;
+    unsigned long long slot = fp & m;
+    for (long long probe = 0; probe < h.hcap; probe++) {
+      const unsigned long long c = h.htable[slot];
+      if (c == fp) break;
+      if (c == 0) {
+        atomicOr(h.verify_err, 1u);  // inserted by the previous pass: unreachable
+        return -1;
+      }
+      slot = (slot + 1) & m;
+    }
+    const int32_t *t = h.tuples + (size_t)slot * a.n_gcols;
+    for (int j = 0; j < a.n_gcols; j++)
+      if (t[j] != mv_gid(a, j, cur[j])) {
+        atomicOr(h.verify_err, 1u);
+        return -1;
+      }
+    return (long long)slot;
+  }
+}
+
+// the doc's entry ranges per group column; false = some column has no entry (no keys)
+__device__ __forceinline__ bool mv_ranges(const MvGroupArgs &a, int64_t doc, uint32_t *lo, uint32_t *hi, uint32_t *cur) {
+  bool empty = false;
+  for (int j = 0; j < a.n_gcols; j++) {
+    lo[j] = a.goff[j] ? a.goff[j][doc] : (uint32_t)doc;
+    hi[j] = a.goff[j] ? a.goff[j][doc + 1] : (uint32_t)doc + 1;
+    cur[j] = lo[j];
+    empty = empty || hi[j] <= lo[j];
+  }
+  return !empty;
+}
+
+// odometer step, column 0 fastest; false after the last combination
+__device__ __forceinline__ bool mv_next(int n, const uint32_t *lo, const uint32_t *hi, uint32_t *cur) {
+  for (int j = 0; j < n; j++) {
+    if (++cur[j] < hi[j]) return true;
+    cur[j] = lo[j];
+  }
+  return false;
+}
+
+template <bool H>
+__global__ __launch_bounds__(kBlock) void k_group_by_mv(MvGroupArgs a, MvHash h) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t doc = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; doc < a.num_docs; doc += stride) {
     if (a.bitset && !((a.bitset[doc >> 6] >> (doc & 63)) & 1ull)) continue;
     uint32_t lo[kMaxGroupCols], hi[kMaxGroupCols], cur[kMaxGroupCols];
-    bool empty = false;
-    for (int j = 0; j < a.n_gcols; j++) {
-      lo[j] = a.goff[j] ? a.goff[j][doc] : (uint32_t)doc;
-      hi[j] = a.goff[j] ? a.goff[j][doc + 1] : (uint32_t)doc + 1;
-      cur[j] = lo[j];
-      empty = empty || hi[j] <= lo[j];
-    }
-    if (empty) continue;  // a row without entries yields no group key
+    if (!mv_ranges(a, doc, lo, hi, cur)) continue;  // a row without entries yields no group key
     uint32_t ab[kMaxAggs], ae[kMaxAggs];
     for (int g = 0; g < a.n_aggs; g++) {
       ab[g] = a.aoff[g] ? a.aoff[g][doc] : (uint32_t)doc;
       ae[g] = a.aoff[g] ? a.aoff[g][doc + 1] : (uint32_t)doc + 1;
     }
-    while (true) {  // odometer over the product, column 0 fastest
-      long long key = 0;
-      for (int j = 0; j < a.n_gcols; j++) {
-        int32_t id = (int32_t)read_packed(a.gfwd[j], a.gbits[j], cur[j]);
-        if (a.remap[j]) id = a.remap[j][id];
-        key += (long long)id * a.stride[j];
-      }
-      if (a.admitted && !((a.admitted[key >> 5] >> (key & 31)) & 1u)) {  // dropped: INVALID_ID (holder full)
-        int j = 0;
-        for (; j < a.n_gcols; j++) {
-          if (++cur[j] < hi[j]) break;
-          cur[j] = lo[j];
-        }
-        if (j == a.n_gcols) break;
-        continue;
-      }
+    do {
+      const long long key = mv_key<H>(a, h, cur);
+      // dropped: a fingerprint collision, or INVALID_ID (holder full: not admitted)
+      if (key < 0 || (a.admitted && !((a.admitted[key >> 5] >> (key & 31)) & 1u))) continue;
       atomicAdd(a.counts + key, 1ull);
       for (int g = 0; g < a.n_aggs; g++)
         if (a.acc_kind[g] != 5) mv_fold(a, g, key, ab[g], ae[g]);
-      int j = 0;
-      for (; j < a.n_gcols; j++) {
-        if (++cur[j] < hi[j]) break;
-        cur[j] = lo[j];
+    } while (mv_next(a.n_gcols, lo, hi, cur));
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_mv_key_count(MvGroupArgs a, unsigned long long *total) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  unsigned long long mine = 0;
+  for (int64_t doc = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; doc < a.num_docs; doc += stride) {
+    if (a.bitset && !((a.bitset[doc >> 6] >> (doc & 63)) & 1ull)) continue;
+    unsigned long long p = 1;
+    for (int j = 0; j < a.n_gcols; j++)
+      p *= a.goff[j] ? (unsigned long long)(a.goff[j][doc + 1] - a.goff[j][doc]) : 1ull;
+    mine += p;
+  }
+  for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o);
+  if ((threadIdx.x & 63) == 0 && mine) atomicAdd(total, mine);
+}
+
+__global__ __launch_bounds__(kBlock) void k_mv_hash_insert(MvGroupArgs a, MvHash h) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const unsigned long long m = (unsigned long long)h.hcap - 1ull;
+  for (int64_t doc = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; doc < a.num_docs; doc += stride) {
+    if (a.bitset && !((a.bitset[doc >> 6] >> (doc & 63)) & 1ull)) continue;
+    uint32_t lo[kMaxGroupCols], hi[kMaxGroupCols], cur[kMaxGroupCols];
+    if (!mv_ranges(a, doc, lo, hi, cur)) continue;
+    do {
+      const unsigned long long fp = mv_fingerprint(a, h, cur);
+      unsigned long long slot = fp & m;
+      for (long long probe = 0; probe < h.hcap; probe++) {
+        unsigned long long c = __hip_atomic_load(h.htable + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (c == 0) {
+          c = atomicCAS(h.htable + slot, 0ull, fp);
+          if (c == 0) {  // this lane owns the slot: its tuple (read by the later passes only)
+            int32_t *t = h.tuples + (size_t)slot * a.n_gcols;
+            for (int j = 0; j < a.n_gcols; j++) t[j] = mv_gid(a, j, cur[j]);
+            break;
+          }
+        }
+        if (c == fp) break;
+        slot = (slot + 1) & m;
       }
-      if (j == a.n_gcols) break;
-    }
+    } while (mv_next(a.n_gcols, lo, hi, cur));
+  }
+}
+
+__global__ void k_mv_hash_tuples(MvHash h, int n_gcols, const long long *__restrict__ slots, long long n,
+                                 int32_t *__restrict__ ids) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n * n_gcols;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long g = i / n_gcols;
+    ids[i] = h.tuples[(size_t)slots[g] * n_gcols + (i - g * n_gcols)];
   }
 }
 
 // Keys of a doc in getIntRawKeys order: the highest-index multi-value column fastest (its values outermost-first
 // build the array, each lower-index column's values then repeat the array: DictionaryBasedGroupKeyGenerator
 // .java:344-410); position = the key's index in that list. Keys repeat when a row repeats a value; the first one counts.
-__global__ __launch_bounds__(kBlock) void k_first_pos_mv(MvGroupArgs a, unsigned long long *first_pos) {
+template <bool H>
+__global__ __launch_bounds__(kBlock) void k_first_pos_mv(MvGroupArgs a, MvHash h, unsigned long long *first_pos) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t doc = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; doc < a.num_docs; doc += stride) {
     if (a.bitset && !((a.bitset[doc >> 6] >> (doc & 63)) & 1ull)) continue;
     uint32_t lo[kMaxGroupCols], hi[kMaxGroupCols], cur[kMaxGroupCols];
-    bool empty = false;
-    for (int j = 0; j < a.n_gcols; j++) {
-      lo[j] = a.goff[j] ? a.goff[j][doc] : (uint32_t)doc;
-      hi[j] = a.goff[j] ? a.goff[j][doc + 1] : (uint32_t)doc + 1;
-      cur[j] = lo[j];
-      empty = empty || hi[j] <= lo[j];
-    }
-    if (empty) continue;
+    if (!mv_ranges(a, doc, lo, hi, cur)) continue;
     unsigned long long pos = (unsigned long long)doc << 32;
     while (true) {
-      long long key = 0;
-      for (int j = 0; j < a.n_gcols; j++) {
-        int32_t id = (int32_t)read_packed(a.gfwd[j], a.gbits[j], cur[j]);
-        if (a.remap[j]) id = a.remap[j][id];
-        key += (long long)id * a.stride[j];
-      }
-      if (first_pos[key] > pos) atomicMin(first_pos + key, pos);  // values only decrease: a stale read still takes it
+      const long long key = mv_key<H>(a, h, cur);
+      // values only decrease: a stale read still takes it
+      if (key >= 0 && first_pos[key] > pos) atomicMin(first_pos + key, pos);
       pos++;
       int j = a.n_gcols - 1;
       for (; j >= 0; j--) {
@@ -597,16 +689,48 @@ static int grid_for(int64_t items, int per_block, int cap) {
   return (int)g;
 }
 
+namespace {
+unsigned mv_blocks(const MvGroupArgs &a) {
+  return (unsigned)std::min<int64_t>(((int64_t)a.num_docs + kBlock - 1) / kBlock, 4096);
+}
+}  // namespace
+
 void launch_group_by_mv(const MvGroupArgs &a, hipStream_t stream) {
   if (a.num_docs <= 0) return;
-  const int64_t blocks = std::min<int64_t>(((int64_t)a.num_docs + kBlock - 1) / kBlock, 4096);
-  hipLaunchKernelGGL(k_group_by_mv, dim3((unsigned)blocks), dim3(kBlock), 0, stream, a);
+  hipLaunchKernelGGL(k_group_by_mv<false>, dim3(mv_blocks(a)), dim3(kBlock), 0, stream, a, MvHash{});
 }
 
 void launch_first_pos_mv(const MvGroupArgs &a, unsigned long long *first_pos, hipStream_t stream) {
   if (a.num_docs <= 0) return;
-  const int64_t blocks = std::min<int64_t>(((int64_t)a.num_docs + kBlock - 1) / kBlock, 4096);
-  hipLaunchKernelGGL(k_first_pos_mv, dim3((unsigned)blocks), dim3(kBlock), 0, stream, a, first_pos);
+  hipLaunchKernelGGL(k_first_pos_mv<false>, dim3(mv_blocks(a)), dim3(kBlock), 0, stream, a, MvHash{}, first_pos);
+}
+
+void launch_mv_key_count(const MvGroupArgs &a, unsigned long long *total, hipStream_t stream) {
+  if (a.num_docs <= 0) return;
+  hipLaunchKernelGGL(k_mv_key_count, dim3(mv_blocks(a)), dim3(kBlock), 0, stream, a, total);
+}
+
+void launch_mv_hash_insert(const MvGroupArgs &a, const MvHash &h, hipStream_t stream) {
+  if (a.num_docs <= 0) return;
+  hipLaunchKernelGGL(k_mv_hash_insert, dim3(mv_blocks(a)), dim3(kBlock), 0, stream, a, h);
+}
+
+void launch_group_by_mv_hashed(const MvGroupArgs &a, const MvHash &h, hipStream_t stream) {
+  if (a.num_docs <= 0) return;
+  hipLaunchKernelGGL(k_group_by_mv<true>, dim3(mv_blocks(a)), dim3(kBlock), 0, stream, a, h);
+}
+
+void launch_first_pos_mv_hashed(const MvGroupArgs &a, const MvHash &h, unsigned long long *first_pos,
+                                hipStream_t stream) {
+  if (a.num_docs <= 0) return;
+  hipLaunchKernelGGL(k_first_pos_mv<true>, dim3(mv_blocks(a)), dim3(kBlock), 0, stream, a, h, first_pos);
+}
+
+void launch_mv_hash_tuples(const MvHash &h, int n_gcols, const long long *slots, long long n, int32_t *ids,
+                           hipStream_t stream) {
+  if (n <= 0) return;
+  const long long grid = std::min<long long>((n * n_gcols + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_mv_hash_tuples, dim3((unsigned)grid), dim3(256), 0, stream, h, n_gcols, slots, n, ids);
 }
 
 size_t admission_scratch_bytes_u64(long long G) {

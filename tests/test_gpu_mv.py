@@ -10,7 +10,8 @@ from pinot_amd import GpuEngine, ServerQueryExecutor
 from pinot_amd._lib import PinotGpuError
 from segdir_writer import write_segment_dir
 from test_gpu_parity import _assert_same, _random_leaf
-from test_mv import mv_segment
+from test_mv import mv_rows, mv_segment
+from pinot_amd import build_segment
 
 pytestmark = pytest.mark.gpu
 MV_COLS = ("tags", "tagl", "tagd", "tags_s")
@@ -131,6 +132,47 @@ def test_mv_group_by_admission(engine, seed):
         assert st.num_docs_scanned == scanned
         assert len(exp) <= 2 * limit
         _check(q, got, exp)
+    for g in gsegs:
+        g.release()
+
+
+def hashed_mv_segment(rng, n, name):
+    """Group columns whose cardinality product is beyond the dense key limit (2^27): an MV INT column of ~2n values
+    and a single-value LONG of ~n values (the LONG_MAP / ARRAY_MAP holder shapes, DictionaryBasedGroupKeyGenerator
+    .java:79-126), beside an MV aggregation column."""
+    cols = {
+        "hv": ("INT", [[int(v) for v in r] for r in mv_rows(rng, n, 4 * n, 3)]),
+        "hs": ("LONG", rng.integers(0, 10 ** 12, n).astype(np.int64)),
+        "tags": ("INT", [[int(v) * 7 - 100 for v in r] for r in mv_rows(rng, n, 40, 4)]),
+        "g": ("INT", rng.integers(0, 6, n).astype(np.int32)),
+        "m": ("INT", rng.integers(-1000, 1000, n).astype(np.int32)),
+    }
+    return build_segment(name, cols, inverted_columns=(), mv_columns=("hv", "tags"), allow_sorted=False)
+
+
+@pytest.mark.parametrize("seed", range(2))
+def test_mv_group_by_hashed_key_space(engine, seed):
+    """MV group-by over a key space past the dense limit: keys are fingerprint-table slots (mv_hash.h), the result's
+    groups carry their global-id tuples; with and without the num.groups.limit admission binding."""
+    rng = np.random.default_rng(1700 + seed)
+    segs = [hashed_mv_segment(rng, 12000, "h%d" % i) for i in range(2)]
+    gsegs = [engine.register(s) for s in segs]
+    cases = [(["hv", "hs"], None, None), (["hs", "hv", "g"], None, None), (["hv", "hs"], 500, 10)]
+    for cols, limit, thr in cases:
+        aggs = [{"function": "COUNT", "column": "*"}, {"function": "SUMMV", "column": "tags"},
+                {"function": "SUM", "column": "m"}, {"function": "DISTINCTCOUNTHLLMV", "column": "tags"}]
+        q = {"aggregations": aggs, "filter": {"operator": "RANGE", "column": "m", "values": ["[-500\t\t900)"]},
+             "group_by": {"columns": cols, "top_n": 10}}
+        kw = {} if limit is None else {"num_groups_limit": limit, "max_init_group_holder_capacity": thr}
+        ex = ServerQueryExecutor(engine, **kw)
+        got, st = ex.process_query(q, gsegs, trim=False)
+        okw = {} if limit is None else {"num_groups_limit": limit, "array_threshold": thr}
+        exp, scanned = O.execute_server(segs, q, **okw)
+        assert st.num_docs_scanned == scanned
+        assert len(exp) > (2 * limit if limit else 10000) // 2
+        _check(q, got, exp)
+        dt, _ = ex.process_query_datatable(q, gsegs)
+        assert b"sumMV_tags" in dt
     for g in gsegs:
         g.release()
 

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define PINOT_GPU_ABI_VERSION 12
+#define PINOT_GPU_ABI_VERSION 13
 
 /* ------------------------------------------------------------------ status */
 typedef enum {
@@ -266,6 +266,16 @@ pinot_status pinot_gpu_segment_dir_info(const char *index_dir, int32_t *num_docs
  * .sv.raw.fwd. data_type INT / LONG / FLOAT / DOUBLE; values receives num_docs native-endian values. */
 pinot_status pinot_segment_read_raw_forward_index(const uint8_t *bytes, uint64_t len, int32_t data_type, int32_t num_docs,
                                           void *values);
+/* A raw (no-dictionary) column's dictionary form exactly as pinot_gpu_segment_register builds it before upload
+ * (replaces the reference's raw-value reads, PhysicalColumnIndexContainer.java:101-106 / FixedByteChunkSingleValueReader,
+ * with the dictionary plans' input): numeric columns radix-sorted on the engine's GPU when on_device is 1 (config key
+ * raw.device, default on), on the host otherwise; STRING columns on the host. Outputs the cardinality, the bits per
+ * dictId, the dictionary (cardinality big-endian values, STRING zero-padded to the longest) and the MSB-first packed
+ * forward index; null buffers report the lengths only. PINOT_ERR_BAD_ARG for a dictionary-encoded column. */
+pinot_status pinot_gpu_transcode_raw(pinot_engine *engine, const pinot_column_desc *column, int32_t num_docs,
+                                     int32_t on_device, int32_t *cardinality, int32_t *bits_per_value,
+                                     uint8_t *dictionary, uint64_t dictionary_cap, uint64_t *dictionary_len,
+                                     uint8_t *forward_index, uint64_t forward_cap, uint64_t *forward_len);
 /* Every check pinot_gpu_segment_register makes on the descriptor's bytes (dictionaries, forward-index
  * length, sorted-index tiling, inverted-index offsets and roaring containers), on the host only: no engine,
  * no GPU. PINOT_ERR_BAD_ARG + pinot_gpu_last_error() name the first bad column. */

@@ -150,6 +150,7 @@ void parse_config(Engine &e, const char *cfg) {
     else if (k == "group.bucket") e.group_bucket = v == "1" || v == "true";
     else if (k == "group.ring") e.group_ring = v == "1" || v == "true";
     else if (k == "group.ring_qfilter") e.group_ring_qfilter = v == "1" || v == "true";
+    else if (k == "raw.device") e.raw_device = v == "1" || v == "true";
     else if (k == "group.aligned") e.group_aligned = v == "1" || v == "true";
     else if (k == "group.lds_block") {
       e.group_lds_block = std::stoi(v);
@@ -381,6 +382,42 @@ pinot_status pinot_gpu_segment_release(pinot_engine *engine, pinot_segment_handl
         engine->segment_cache.erase(it);
         break;
       }
+  });
+}
+
+pinot_status pinot_gpu_transcode_raw(pinot_engine *engine, const pinot_column_desc *column, int32_t num_docs,
+                                     int32_t on_device, int32_t *cardinality, int32_t *bits_per_value,
+                                     uint8_t *dictionary, uint64_t dictionary_cap, uint64_t *dictionary_len,
+                                     uint8_t *forward_index, uint64_t forward_cap, uint64_t *forward_len) {
+  return guard([&] {
+    require(engine && column && cardinality && bits_per_value && dictionary_len && forward_len, PINOT_ERR_BAD_ARG,
+            "null argument");
+    std::lock_guard<std::mutex> lk(engine->mu);
+    set_device(*engine);
+    TranscodedColumn tc;
+    const bool saved = engine->raw_device;
+    engine->raw_device = on_device != 0;
+    bool raw = false;
+    try {
+      raw = transcode_column(*engine, *column, num_docs, tc);
+    } catch (...) {
+      engine->raw_device = saved;
+      throw;
+    }
+    engine->raw_device = saved;
+    require(raw, PINOT_ERR_BAD_ARG, "not a raw column");
+    *cardinality = tc.desc.cardinality;
+    *bits_per_value = tc.desc.bits_per_value;
+    *dictionary_len = tc.dictionary.size();
+    *forward_len = tc.forward_index.size();
+    if (dictionary) {
+      require(dictionary_cap >= tc.dictionary.size(), PINOT_ERR_BAD_ARG, "dictionary buffer too small");
+      memcpy(dictionary, tc.dictionary.data(), tc.dictionary.size());
+    }
+    if (forward_index) {
+      require(forward_cap >= tc.forward_index.size(), PINOT_ERR_BAD_ARG, "forward index buffer too small");
+      memcpy(forward_index, tc.forward_index.data(), tc.forward_index.size());
+    }
   });
 }
 
@@ -820,6 +857,7 @@ pinot_status pinot_gpu_engine_stat(pinot_engine *engine, const char *name, int64
     if (n == "group.ring_queries") *value = engine->ring_queries;
     else if (n == "group.ring_fallbacks") *value = engine->ring_fallbacks;
     else if (n == "group.ring_qfilter_queries") *value = engine->ring_qfilter_queries;
+    else if (n == "raw.device_columns") *value = engine->raw_device_columns;
     else if (n == "group.last_instance") *value = engine->last_group_instance;
     else if (n == "exec.last_pre_segments") *value = engine->last_pre_segments;
     else require(false, PINOT_ERR_BAD_ARG, "unknown engine stat");

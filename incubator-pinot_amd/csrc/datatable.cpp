@@ -14,7 +14,10 @@
 // key order: the reference's map is a ConcurrentHashMap filled by concurrent segment threads, whose order is not
 // deterministic either; the broker reads it back into a HashMap (order-free).
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <exception>
 #include <functional>
@@ -358,6 +361,8 @@ std::vector<uint8_t> group_by_datatable(const pinot_query &q, const GroupByResul
   // pool in chunks of the concatenated entry lists.
   const int na = (int)r.functions.size();
   const int64_t n = (int64_t)r.raw_keys.size();
+  static const bool phases = getenv("PINOT_DATATABLE_PHASES") != nullptr;  // diagnostic timing on stderr
+  const auto t0 = std::chrono::steady_clock::now();
   Table t;
   t.rows = na;
   t.cols = 2;
@@ -400,6 +405,7 @@ std::vector<uint8_t> group_by_datatable(const pinot_query &q, const GroupByResul
     F.first = total_entries;
     total_entries += F.m;
   }
+  const auto t1 = std::chrono::steady_clock::now();
   // entry sizes (MAP_SER_DE, ObjectSerDeUtils.java:262-300: key String = int length + bytes, value = int length +
   // bytes), in chunks over the pool
   const size_t nt = total_entries >= 4096 ? std::max<size_t>(1, std::min<size_t>(host_parallelism(), 16)) : 1;
@@ -437,6 +443,7 @@ std::vector<uint8_t> group_by_datatable(const pinot_query &q, const GroupByResul
       }
     }
   });
+  const auto t2 = std::chrono::steady_clock::now();
   // cell sizes and the variable section's layout: per row the object type, then the map (size, key and value types,
   // entries); the entries' offsets as one exclusive prefix sum
   std::vector<uint64_t> eoff((size_t)total_entries + 1);
@@ -475,7 +482,10 @@ std::vector<uint8_t> group_by_datatable(const pinot_query &q, const GroupByResul
     memcpy(&u, &d, 8);
     return u;
   };
-  return table_bytes_var(t, var, [&](uint8_t *v) {
+  const auto t3 = std::chrono::steady_clock::now();
+  auto t4 = t3;
+  std::vector<uint8_t> out = table_bytes_var(t, var, [&](uint8_t *v) {
+    t4 = std::chrono::steady_clock::now();
     size_t at = 0;
     for (int i = 0; i < na; i++) {  // the rows' heads
       uint8_t *x = put_be32(v + at, (uint32_t)OBJ_MAP);
@@ -516,6 +526,14 @@ std::vector<uint8_t> group_by_datatable(const pinot_query &q, const GroupByResul
       }
     });
   });
+  if (phases) {
+    const auto t5 = std::chrono::steady_clock::now();
+    auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+    fprintf(stderr, "[pinot_gpu] datatable phases (us): stage %.1f, sizes %.1f, layout+metadata %.1f, header+alloc %.1f, "
+            "entries %.1f (%lld entries, %zu bytes)\n", us(t0, t1), us(t1, t2), us(t2, t3), us(t3, t4), us(t4, t5),
+            (long long)total_entries, out.size());
+  }
+  return out;
 }
 
 std::vector<uint8_t> empty_datatable(const pinot_query &q, int64_t total_docs, const pinot_datatable_server *srv) {

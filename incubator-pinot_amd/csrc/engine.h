@@ -84,6 +84,13 @@ struct TranscodedColumn {
   std::vector<uint8_t> dictionary, forward_index;
 };
 bool transcode_raw(const pinot_column_desc &d, int32_t num_docs, TranscodedColumn &out);
+// The checks every raw column passes; the value width (4 / 8) of a raw numeric column, 0 for STRING or dictionary.
+int raw_numeric_width(const pinot_column_desc &d, int32_t num_docs);
+// out.dictionary and out.desc from the distinct order-preserving keys (ascending); out.forward_index set by the caller.
+void transcoded_numeric_finish(const pinot_column_desc &d, const uint64_t *uniq, int64_t card, TranscodedColumn &out);
+struct Engine;
+// segment.cpp: a raw column's dictionary form as registration builds it (numeric on the device when e.raw_device).
+bool transcode_column(Engine &e, const pinot_column_desc &d, int32_t num_docs, TranscodedColumn &tc);
 // Same, on `threads` host threads (0: one per 1 M docs, at most 16); the output does not depend on the count.
 bool transcode_raw_threads(const pinot_column_desc &d, int32_t num_docs, TranscodedColumn &out, size_t threads);
 void validate_segment(const pinot_segment_desc &d);
@@ -261,6 +268,8 @@ struct Engine {
   bool group_bucket = true;   // group.bucket: partitioned plan EMITs through LDS buckets into the final layout
   bool group_ring = true;     // group.ring: large dense key spaces take the ring plan (no histogram pass; group_ring.hip);
                               // 0: the counted plan (COUNT -> scan -> EMIT2 -> k_partition_reduce)
+  bool raw_device = true;     // raw.device: raw numeric columns transcoded on the device at registration (transcode.h)
+  int64_t raw_device_columns = 0;  // columns the device transcoded
   bool group_ring_qfilter = true;  // group.ring_qfilter: the ring kernel evaluates simple filters itself (else GB_FILTER)
   int32_t trim_top_n = 0;      // per call (pinot_gpu_group_by_top): trim the group-by on the device for this TOP n
   int64_t ring_queries = 0;    // group-bys launched on the ring plan

@@ -33,6 +33,7 @@
 #include "engine.h"
 #include "group_ring.h"
 #include "mv_hash.h"
+#include "trim.h"
 
 namespace pinot {
 // fused_group.hip: the k_group_query instance a launch of `a` runs (mode * 10000 + read path * 1000 + threads)
@@ -2703,6 +2704,7 @@ struct DenseGroups {
   std::vector<void *> accs;
   int64_t key_base;
   const GroupArgs *hashed;           // hashed key spaces: the query's args (slot -> global-id tuples)
+  std::vector<const void *> hll_sum;  // per accumulator: the HLL's packed register sums (k_group_final kind 9), or null
 };
 
 unsigned long long compact_dense(Engine &e, const unsigned long long *counts, int64_t G, long long *&keys_dev,
@@ -2771,6 +2773,10 @@ DenseOut dense_outputs(Engine &e, const DenseGroups &d, const long long *keys_de
       const int src = alias[i] >= 0 ? alias[i] : i;  // the accumulator this aggregation reads
       f.kind[i] = ga.acc_kind[i];
       f.acc[i] = d.accs[src];
+      if (ga.acc_kind[i] == 4 && (size_t)src < d.hll_sum.size() && d.hll_sum[src]) {
+        f.kind[i] = 9;
+        f.acc[i] = d.hll_sum[src];
+      }
       f.out_values[i] = v + n * i;
       if (ga.acc_kind[i] == 4) {
         f.out_card[i] = c;
@@ -3055,7 +3061,7 @@ const long long *device_trim(Engine &e, const DenseGroups &d, const long long *k
   const pinot_query &q = *d.q;
   const int na = q.num_aggregations;
   const DenseOut o = dense_outputs(e, d, keys_dev, n, false, false);  // comparable values of every group, no registers
-  const size_t scr = trim_scratch_bytes((long long)n);
+  const size_t scr = std::max(trim_scratch_bytes((long long)n), trim_radix_scratch_bytes((long long)n, na));
   const size_t a8 = ((size_t)n * 8 + 255) / 256 * 256, a4 = ((size_t)n * 4 + 255) / 256 * 256;
   e.group_trim.reserve(a8 + 2 * a4 + 256 + scr);
   uint8_t *p = e.group_trim.get<uint8_t>();
@@ -3064,20 +3070,23 @@ const long long *device_trim(Engine &e, const DenseGroups &d, const long long *k
   auto *uflags = reinterpret_cast<uint32_t *>(p + a8 + a4);
   auto *n_dev = reinterpret_cast<unsigned long long *>(p + a8 + 2 * a4);
   void *tmp = p + a8 + 2 * a4 + 256;
-  PINOT_HIP(hipMemsetAsync(flags, 0, (size_t)n * 4, e.stream));
+  require(na <= kTrimMaxFns, PINOT_ERR_DEVICE, "trim over more functions than the selection holds");
+  TrimFn fns[kTrimMaxFns];
   for (int i = 0; i < na; i++) {
     const int f = sv_function(q.aggregations[i].function);
-    launch_trim_select(o.values[i], o.counts, f == PINOT_AGG_AVG, f == PINOT_AGG_MIN, (long long)n, T, 1u << i, flags,
-                       tmp, scr, e.stream);
+    fns[i] = TrimFn{o.values[i], f == PINOT_AGG_AVG, f == PINOT_AGG_MIN};
   }
+  launch_trim_radix(fns, na, o.counts, (long long)n, T, flags, tmp, scr, e.stream);  // every function's kept groups
   launch_trim_union(flags, keys_dev, (long long)n, ukeys, uflags, n_dev, tmp, scr, e.stream);
   PINOT_HIP(hipGetLastError());
+  // the union holds at most na x T groups: its count and flags in one round trip
+  const size_t max_u = std::min<size_t>((size_t)n, (size_t)na * (size_t)T);
   unsigned long long nu = 0;
+  HostVec<uint32_t> hf(max_u);
   PINOT_HIP(hipMemcpyAsync(&nu, n_dev, 8, hipMemcpyDeviceToHost, e.stream));
+  PINOT_HIP(hipMemcpyAsync(hf.data(), uflags, max_u * 4, hipMemcpyDeviceToHost, e.stream));
   wait_stream(e);
-  HostVec<uint32_t> hf(nu);
-  if (nu) PINOT_HIP(hipMemcpyAsync(hf.data(), uflags, nu * 4, hipMemcpyDeviceToHost, e.stream));
-  wait_stream(e);
+  require(nu <= max_u, PINOT_ERR_DEVICE, "trim union larger than its functions' lists");
   kept.assign(na, {});
   for (int i = 0; i < na; i++) kept[i].reserve((size_t)T);
   for (unsigned long long g = 0; g < nu; g++)
@@ -3181,7 +3190,7 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
   size_t per_key = 8;
   for (int a = 0; a < na; a++) {
     acc_bytes[a] = gx.acc_kind[a] == 5 ? 0 : gx.acc_kind[a] == 4 ? 256 : 8;
-    per_key += acc_bytes[a];
+    per_key += acc_bytes[a] + (gx.acc_kind[a] == 4 ? 8 : 0);  // HLL: + the ring reduce's packed sums u64 [G]
   }
   const size_t head = 256 + (S * 8 + 255) / 256 * 256;  // matched [S] + verify flag, 256-B aligned arrays after
   const size_t scratch_b = ks.G * per_key + head + 256 * (size_t)(na + 1);
@@ -3200,7 +3209,7 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     for (int a = 0; a < na; a++) {
       if (!acc_bytes[a]) continue;
       accs[a] = p;
-      p += (ks.G * acc_bytes[a] + 255) / 256 * 256;
+      p += (ks.G * (acc_bytes[a] + (gx.acc_kind[a] == 4 ? 8 : 0)) + 255) / 256 * 256;
     }
     for (int a = 0; a < na; a++)
       if (alias[a] >= 0) accs[a] = accs[alias[a]];
@@ -3470,6 +3479,7 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     rr.G = ks.G;
     rr.counts = counts;
     rr.status = ring_status;
+    rr.hll_sums = po ? 0 : 1;  // the engine's HLL arrays have room for the sums; a caller's partial arrays do not
     for (int i = 0; i < na; i++) {
       rr.aggs[i] = gaggs[i];  // segment 0's dictionary / LUT: identical on every segment (checked by plan_group)
       rr.aggs[i].lds_off = rp.lds_off[i];
@@ -3616,6 +3626,11 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
   }
   const auto tg3 = std::chrono::steady_clock::now();
   DenseGroups dg{&q, &ks, &ga, &gx, &alias, counts, accs, 0, ks.hashed ? &a : nullptr};
+  if (ring_status) {  // the ring reduce wrote each HLL's packed register sums after its registers
+    dg.hll_sum.assign(na, nullptr);
+    for (int i = 0; i < na; i++)
+      if (gx.acc_kind[i] == 4) dg.hll_sum[i] = static_cast<const uint8_t *>(accs[i]) + (size_t)ks.G * 256;
+  }
   std::vector<std::vector<int64_t>> kept;
   unsigned long long nres = n;
   const long long *rkeys = keys_dev;

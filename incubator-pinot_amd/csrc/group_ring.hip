@@ -1,15 +1,14 @@
 // Ring-partitioned group-by (the large-key-space plan, config 4): no histogram pass, fixed-capacity regions.
 //
-//   k_group_ring         one block of 16 waves per CU over a contiguous range of chunks. Waves 0..13 (decoders) read
-//                        each 1024-doc quarter lane-owns-quarter (lane l: docs 16l .. 16l + 15), evaluate the
+//   k_group_ring         one block of 12 waves per CU over a contiguous range of chunks. Waves 0..7 (decoders, two per
+//                        SIMD) read each 1024-doc quarter lane-owns-quarter (lane l: docs 16l .. 16l + 15), evaluate the
 //                        segment's top-level conjunction of scan leaves on it (or take GB_FILTER's words for other
 //                        filter shapes), decode the group key and aggregated dictIds into u64 records (local key |
-//                        dictId fields) and append each to its partition's LDS ring of 16 entries (two halves of 8):
-//                        one 64-bit LDS add claims an entry and returns how many records the partition has moved out,
-//                        so a decoder never issues an HBM store (its vmcnt holds its own loads only). Waves 14, 15
-//                        (flushers) sweep the partitions and move every completed half to the block's region of that
-//                        partition as one aligned 64-B piece: region (p, block) holds records [0, n) in claim order,
-//                        so no histogram, scan or cursor leaves the CU.
+//                        dictId fields) and append each to its partition's LDS bucket of 16 entries (two halves of 8):
+//                        one LDS add claims an entry, so a decoder never issues an HBM store (its vmcnt holds its own
+//                        loads only). Waves 8..11 (flushers, one per SIMD) move every completed half to the block's
+//                        region of that partition as one aligned 64-B piece, between block barriers: region
+//                        (p, block) holds records [0, n) in claim order, so no histogram, scan or cursor leaves the CU.
 //   k_ring_reduce        one block per partition of K <= 1024 consecutive keys: the partition's records from every
 //                        block's region folded into LDS accumulators (count packed beside the first affine dictId
 //                        SUM, int64 / double sums, ordered min / max, HLL registers as 4-bit nibbles with the rare
@@ -43,18 +42,32 @@ using namespace dev;
 
 constexpr int kRingBlock = 768;                             // one block of 12 waves per CU (the buckets take the LDS)
 constexpr int kRingWaves = kRingBlock / 64;
-constexpr int kRingFlushWaves = 3;                           // waves 9..11: the flush phases
-constexpr int kRingDecWaves = kRingWaves - kRingFlushWaves;  // waves 0..8: filter, decode, insert
+constexpr int kRingFlushWaves = 4;                           // waves 8..11: the flush phases (one per SIMD)
+constexpr int kRingDecWaves = kRingWaves - kRingFlushWaves;  // waves 0..7: filter, decode, insert (two per SIMD)
+#ifdef RING_EXP_ONEROUND
+constexpr int kRingRoundRecs = 16;                           // experiment: one insert phase per pass
+#else
 constexpr int kRingRoundRecs = 8;                            // records per decoder lane between two flush phases
+#endif
 constexpr int kRingBucket = 16;                              // entries per partition bucket (two 64-B halves)
+// Bucket stride in entries: 144 B = 36 dwords, so the flushers' 16-B reads of consecutive partitions start on distinct
+// banks (a 128-B stride puts every lane of a ds_read_b128 group on the same four banks) and an insert's 8-B write lands
+// on a bank set by its partition, not only by its slot.
+constexpr int kRingBucketStride = 18;
 constexpr int kRecPShift = 53;                               // bucket entries carry their partition in bits [53, 63)
 constexpr int kRingBackBits = 12;                            // hist: front count (20 bits) | back count << 20
-static_assert(kRingRoundRecs * 2 == 16, "two rounds per pass");
+static_assert(16 % kRingRoundRecs == 0, "whole rounds per pass");
 
 // RING_EXP_TIMING (experiment builds only): per-wave shader-clock totals of each phase, printed by a few blocks.
 #ifdef RING_EXP_TIMING
-#define RT_MARK(v) const uint64_t v = __builtin_amdgcn_s_memtime()
-#define RT_ADD(acc, from) acc += __builtin_amdgcn_s_memtime() - (from)
+// the shader clock, ordered against the memory operations around it (its wait also drains pending LDS operations)
+__device__ __forceinline__ uint64_t rt_cycles() {
+  uint64_t x;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(x) : : "memory");
+  return x;
+}
+#define RT_MARK(v) const uint64_t v = rt_cycles()
+#define RT_ADD(acc, from) acc += rt_cycles() - (from)
 #else
 #define RT_MARK(v)
 #define RT_ADD(acc, from)
@@ -69,7 +82,7 @@ struct RingLds {
 __device__ __forceinline__ RingLds ring_lds(uint8_t *lds, int P) {
   RingLds r;
   r.bkt = reinterpret_cast<unsigned long long *>(lds);
-  r.ctr = reinterpret_cast<uint32_t *>(r.bkt + (size_t)P * kRingBucket);
+  r.ctr = reinterpret_cast<uint32_t *>(r.bkt + (size_t)P * kRingBucketStride);
   r.back = r.ctr + P;
   return r;
 }
@@ -89,14 +102,24 @@ __device__ __forceinline__ void ring_insert(const RingArgs &a, const RingLds &L,
   for (int j = 0; j < kRingRoundRecs; j++) {
     const bool on = (act >> (J0 + j)) & 1u;
     p[j] = on ? rec_part(rec[J0 + j]) : 0u;  // branch-free: an inactive record adds 0 to partition 0's counter
+#ifdef RING_EXP_RACY
+    old[j] = L.ctr[p[j]];  // experiment: a non-atomic claim (wrong results; timing only)
+    L.ctr[p[j]] = old[j] + (on ? 1u : 0u);
+#else
     old[j] = atomicAdd(L.ctr + p[j], on ? 1u : 0u);
+#endif
   }
   uint32_t over = 0;
 #pragma unroll
   for (int j = 0; j < kRingRoundRecs; j++) {
     const bool on = (act >> (J0 + j)) & 1u;
     const uint32_t s = old[j] & 0xFFFFu, h = old[j] >> 16;
-    if (on && s < (uint32_t)kRingBucket) L.bkt[p[j] * kRingBucket + ((h + s) & (kRingBucket - 1))] = rec[J0 + j];
+#ifdef RING_EXP_NOWRITE
+    if (on && s < (uint32_t)kRingBucket && rec[J0 + j] == 0x0123456789ABCDEFull)  // experiment: no bucket writes
+#else
+    if (on && s < (uint32_t)kRingBucket)
+#endif
+      L.bkt[p[j] * kRingBucketStride + ((h + s) & (kRingBucket - 1))] = rec[J0 + j];
     over |= (on && s >= (uint32_t)kRingBucket) ? (1u << j) : 0u;
   }
   if (__any(over != 0)) {  // uniform, rare
@@ -130,7 +153,7 @@ __device__ __forceinline__ void ring_flush_phase(const RingArgs &a, const RingLd
   for (int k = 0; k < KP; k++) {
     const int p = fw * 64 + lane + 64 * kRingFlushWaves * k;
     if ((c[k] & 0xFFFFu) >= 8u) {
-      const u32x4 *src = reinterpret_cast<const u32x4 *>(L.bkt + p * kRingBucket + (c[k] >> 16));
+      const u32x4 *src = reinterpret_cast<const u32x4 *>(L.bkt + p * kRingBucketStride + (c[k] >> 16));
 #pragma unroll
       for (int r = 0; r < 4; r++) x[k][r] = src[r];
     }
@@ -141,18 +164,22 @@ __device__ __forceinline__ void ring_flush_phase(const RingArgs &a, const RingLd
     const int p = fw * 64 + lane + 64 * kRingFlushWaves * k;
     uint32_t n = min(c[k] & 0xFFFFu, (uint32_t)kRingBucket), h = c[k] >> 16;
     if (n < 8u) continue;  // no complete half: the counter stays
+#ifdef RING_EXP_NOFLUSH
+    if (front[k] + 8u <= C && x[k][0].x == 0x9E3779B9u && x[k][1].y == 0x7F4A7C15u) {  // experiment: (almost) no stores
+#else
     if (front[k] + 8u <= C) {
+#endif
       u32x4 *dst = reinterpret_cast<u32x4 *>(region0 + (size_t)p * a.nblk * C + front[k]);
 #pragma unroll
       for (int r = 0; r < 4; r++) __builtin_nontemporal_store(x[k][r] & m, dst + r);
-    } else {
+    } else if (front[k] + 8u > C) {
       status |= 1u;  // region full: the query falls back to the counted plan
     }
     front[k] += 8u;
     h ^= 8u;
     n -= 8u;
     if (n >= 8u) {  // a full bucket (it overflowed this round): its second half too (rare)
-      const u32x4 *src = reinterpret_cast<const u32x4 *>(L.bkt + p * kRingBucket + h);
+      const u32x4 *src = reinterpret_cast<const u32x4 *>(L.bkt + p * kRingBucketStride + h);
       if (front[k] + 8u <= C) {
         u32x4 *dst = reinterpret_cast<u32x4 *>(region0 + (size_t)p * a.nblk * C + front[k]);
 #pragma unroll
@@ -414,6 +441,21 @@ struct RingDecoder {
 #ifdef RING_EXP_NODEC
     return;  // experiment: no column loads (decode() makes synthetic records)
 #endif
+#ifdef RING_EXP_NOLOAD
+    {  // experiment: no column loads; the decode runs on opaque per-quarter values
+#pragma unroll
+      for (int i = 0; i < 12; i++) {
+        uint32_t v = (uint32_t)qi * 0x9E3779B1u + (uint32_t)i * 0x85EBCA77u;
+        v ^= v >> 15;
+        v *= 0x2C1B3C6Du;
+        asm volatile("" : "+v"(v));
+#pragma unroll
+        for (int f = 0; f < (NF > 0 ? NF : 1); f++) F[f][i] = v;
+        RA[0][i] = v * 3u; RA[1][i] = v * 5u; RB[0][i] = v * 7u; RB[1][i] = v * 11u;
+      }
+      return;
+    }
+#endif
 #pragma unroll
     for (int i = 0; i < NF; i++)
       if (i < sg.n_leaves) ring_load_raw(st[i].fwd, st[i].bits, qi, F[i]);
@@ -435,7 +477,10 @@ struct RingDecoder {
     {  // experiment: records of pseudo-random keys, no column data
 #pragma unroll
       for (int j = 0; j < 16; j++) {
-        const uint32_t key = (uint32_t)((((unsigned long long)(qi * 16 + j) * 0x9E3779B97F4A7C15ull) >> 40) % (uint64_t)a.G);
+        unsigned long long z = (unsigned long long)(qi * 16 + j) + 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        const uint32_t key = (uint32_t)((z ^ (z >> 31)) % (uint64_t)a.G);
         rec[j] = (unsigned long long)(key & ((1u << a.shift) - 1u)) | ((unsigned long long)(key >> a.shift) << kRecPShift);
       }
       return;
@@ -481,7 +526,7 @@ struct RingDecoder {
 // WORDS: the filter words GB_FILTER wrote; else the segment's top-level conjunction of <= NF scan leaves evaluated here
 // on each quarter (lane-owns-quarter reads, like the group columns), AND-ed with the `pre` words if any.
 //
-// The block walks its quarters in passes: in pass t decoder wave w takes quarter 4 c0 + 9 t + w of the block's range
+// The block walks its quarters in passes: in pass t decoder wave w takes quarter 4 c0 + 8 t + w of the block's range
 // (none past its end: that wave inserts nothing). A pass inserts the wave's 16 records per lane in two rounds of
 // [insert phase | barrier | flush phase | barrier]; during the second flush phase the decoders decode the next pass's
 // quarter (its raw dwords requested a pass earlier) and request the one after it. Every wave executes the same
@@ -512,13 +557,13 @@ __global__ __launch_bounds__(kRingBlock) void k_group_ring(RingArgs a) {
 #pragma unroll
     for (int k = 0; k < KP; k++) front[k] = 0;
 #ifdef RING_EXP_TIMING
-    uint64_t tb = 0, tf = 0;
-    RT_MARK(t0);
+    uint64_t tb = 0, tf = 0, tt = 0;
 #endif
     for (int64_t t = 0; t < npass; t++)
 #pragma unroll 1
       for (int r = 0; r < 16 / kRingRoundRecs; r++) {
         RT_MARK(x0);
+        RT_MARK(xt);
         __syncthreads();  // inserts of the round done
         RT_ADD(tb, x0);
         RT_MARK(x1);
@@ -527,12 +572,12 @@ __global__ __launch_bounds__(kRingBlock) void k_group_ring(RingArgs a) {
         RT_MARK(x2);
         __syncthreads();  // flushes done (and the decoders' next quarter decoded)
         RT_ADD(tb, x2);
+        RT_ADD(tt, xt);
       }
 #ifdef RING_EXP_TIMING
     if ((b == 0 || b == a.nblk / 2) && lane == 0)
       printf("ring-timing block %d flusher %d: total %llu barrier %llu flush %llu passes %lld\n", b, fw,
-             (unsigned long long)(__builtin_amdgcn_s_memtime() - t0), (unsigned long long)tb, (unsigned long long)tf,
-             (long long)npass);
+             (unsigned long long)tt, (unsigned long long)tb, (unsigned long long)tf, (long long)npass);
 #endif
     // the partial buckets (< 8 entries) to their fronts, then each region's counts
 #pragma unroll
@@ -543,7 +588,7 @@ __global__ __launch_bounds__(kRingBlock) void k_group_ring(RingArgs a) {
       for (uint32_t i = 0; i < n; i++)
         if (front[k] + i < C)
           region0[(size_t)p * a.nblk * C + front[k] + i] =
-              L.bkt[p * kRingBucket + ((h + i) & (kRingBucket - 1))] & ((1ull << kRecPShift) - 1ull);
+              L.bkt[p * kRingBucketStride + ((h + i) & (kRingBucket - 1))] & ((1ull << kRecPShift) - 1ull);
       const uint32_t f = front[k] + n;
       if (f + nb > C || f >= (1u << (32 - kRingBackBits)) || nb >= (1u << kRingBackBits)) status |= 1u;
       a.hist[(size_t)p * a.nblk + b] = min(f, (1u << (32 - kRingBackBits)) - 1u) | (min(nb, (1u << kRingBackBits) - 1u) << (32 - kRingBackBits));
@@ -555,25 +600,25 @@ __global__ __launch_bounds__(kRingBlock) void k_group_ring(RingArgs a) {
     d.decode(a, lane, status);
     d.load(a, 1);  // in flight during pass 0's rounds
 #ifdef RING_EXP_TIMING
-    uint64_t ti = 0, tb = 0, td = 0, tl = 0;
-    RT_MARK(t0);
+    uint64_t ti = 0, tb = 0, td = 0, tl = 0, tt = 0;
 #endif
     for (int64_t t = 0; t < npass; t++) {
+      RT_MARK(xt);
       RT_MARK(x0);
 #ifndef RING_EXP_NOINS
       ring_insert<0>(a, L, d.act, d.rec, region0, C);
 #endif
       RT_ADD(ti, x0);
-      RT_MARK(x1);
-      __syncthreads();  // inserts of round 0 done
-      __syncthreads();  // flush done
-      RT_ADD(tb, x1);
       RT_MARK(x2);
+      if constexpr (kRingRoundRecs < 16) {
+        __syncthreads();  // inserts of round 0 done
+        __syncthreads();  // flush done
 #ifndef RING_EXP_NOINS
-      ring_insert<kRingRoundRecs>(a, L, d.act, d.rec, region0, C);
+        ring_insert<kRingRoundRecs>(a, L, d.act, d.rec, region0, C);
 #else
-      if (d.rec[3] == 0x0123456789ull && d.act == 7) status |= 8u;
+        if (d.rec[3] == 0x0123456789ull && d.act == 7) status |= 8u;
 #endif
+      }
       RT_ADD(ti, x2);
       RT_MARK(x3);
       __syncthreads();  // inserts of round 1 done
@@ -588,13 +633,14 @@ __global__ __launch_bounds__(kRingBlock) void k_group_ring(RingArgs a) {
       RT_MARK(x6);
       __syncthreads();  // flush done
       RT_ADD(tb, x6);
+      RT_ADD(tt, xt);
     }
     d.finish(a, lane);
 #ifdef RING_EXP_TIMING
     if ((b == 0 || b == a.nblk / 2) && lane == 0)
       printf("ring-timing block %d decoder %d: total %llu insert %llu barrier %llu decode %llu load %llu\n", b, wave,
-             (unsigned long long)(__builtin_amdgcn_s_memtime() - t0), (unsigned long long)ti, (unsigned long long)tb,
-             (unsigned long long)td, (unsigned long long)tl);
+             (unsigned long long)tt, (unsigned long long)ti, (unsigned long long)tb, (unsigned long long)td,
+             (unsigned long long)tl);
 #endif
   }
   if (status) atomicOr(a.status, status);
@@ -636,6 +682,18 @@ __device__ __forceinline__ uint32_t murmur_hash_long_g(long long data) {
   return h;
 }
 
+// murmur_hash_long_g of a value in [0, 2^32): the high word's block multiplies h by kM once more
+__device__ __forceinline__ uint32_t murmur_hash_lo32_g(uint32_t lo) {
+  constexpr uint32_t kM = 0x5bd1e995u, kMM = kM * kM;
+  uint32_t k = lo * kM;
+  k ^= k >> 24;
+  uint32_t h = k * kMM;
+  h ^= h >> 13;
+  h *= kM;
+  h ^= h >> 15;
+  return h;
+}
+
 __device__ __forceinline__ uint32_t hll_register_rank_g(uint32_t h) {
   return ((h >> 24) << 8) | (uint32_t)(__builtin_clz((h << 8) | 129u) + 1);
 }
@@ -645,7 +703,7 @@ __device__ __forceinline__ uint32_t hll_register_rank_g(uint32_t h) {
 template <int N, bool GATHER>
 __device__ __forceinline__ void ring_fold(const RingReduceArgs &a, uint8_t *lds, uint32_t *cnt, uint32_t *exc_n,
                                           uint32_t *exc, const unsigned long long (&rec)[N], const bool (&ok)[N],
-                                          int pk, int sbits, uint32_t &status) {
+                                          int pk, int sbits, bool lo32, uint32_t &status) {
   const uint32_t kmask = (1u << a.shift) - 1u;
   uint32_t k[N];
 #pragma unroll
@@ -676,11 +734,19 @@ __device__ __forceinline__ void ring_fold(const RingReduceArgs &a, uint8_t *lds,
       for (int u = 0; u < N; u++)
         if (ok[u]) atomicAdd(reinterpret_cast<unsigned long long *>(acc) + k[u], v[u]);
     } else if (ag.acc_kind == 4) {  // 4-bit registers: max by CAS on the containing dword
+#ifdef RING_EXP_NOHLL
+      continue;  // experiment: no HLL fold
+#endif
       uint32_t h[N];
 #pragma unroll
       for (int u = 0; u < N; u++)
-        h[u] = (!GATHER || ag.affine) ? hll_register_rank_g(murmur_hash_long_g(ag.affine_base + ag.affine_step * (long long)id[u]))
-                                      : (uint32_t)gload<uint16_t>(ag.hll_lut + id[u]);
+#ifdef RING_EXP_CHEAPHASH
+        h[u] = hll_register_rank_g(id[u] * 0x9E3779B1u);  // experiment: one multiply instead of the hash
+#else
+        h[u] = (GATHER && !ag.affine) ? (uint32_t)gload<uint16_t>(ag.hll_lut + id[u])
+               : lo32 ? hll_register_rank_g(murmur_hash_lo32_g((uint32_t)ag.affine_base + (uint32_t)ag.affine_step * id[u]))
+                      : hll_register_rank_g(murmur_hash_long_g(ag.affine_base + ag.affine_step * (long long)id[u]));
+#endif
       uint32_t *word[N], old[N], rk[N];
       int sh[N];
 #pragma unroll
@@ -724,7 +790,7 @@ __device__ __forceinline__ void ring_fold(const RingReduceArgs &a, uint8_t *lds,
 template <int U, bool GATHER>
 __device__ __forceinline__ void ring_fold_units(const RingReduceArgs &a, uint8_t *lds, uint32_t *cnt, uint32_t *exc_n,
                                                 uint32_t *exc, const u32x4 (&v)[U], const uint32_t (&n)[U], int pk,
-                                                int sbits, uint32_t &status) {
+                                                int sbits, bool lo32, uint32_t &status) {
   unsigned long long rec[2 * U];
   bool ok[2 * U];
 #pragma unroll
@@ -738,7 +804,7 @@ __device__ __forceinline__ void ring_fold_units(const RingReduceArgs &a, uint8_t
     ok[2 * u] = n[u] & 1u;
     ok[2 * u + 1] = (n[u] >> 1) & 1u;
   }
-  ring_fold<2 * U, GATHER>(a, lds, cnt, exc_n, exc, rec, ok, pk, sbits, status);
+  ring_fold<2 * U, GATHER>(a, lds, cnt, exc_n, exc, rec, ok, pk, sbits, lo32, status);
 }
 
 constexpr int kRingReduceWaves = kRingReduceBlock / 64;
@@ -829,6 +895,14 @@ __global__ __launch_bounds__(kRingReduceBlock) void k_ring_reduce(RingReduceArgs
       pk = g;
       sbits = a.aggs[g].bits + cbits;
     }
+  // affine HLL values all in [0, 2^32): the 32-bit form of the hash (every HLL aggregation of the query)
+  bool lo32 = true;
+  for (int g = 0; g < a.n_aggs; g++)
+    if (a.aggs[g].acc_kind == 4) {
+      const GroupAggDev &ag = a.aggs[g];
+      const long long top = ag.affine_base + ag.affine_step * (long long)((1ull << ag.bits) - 1ull);
+      lo32 = lo32 && ag.affine && ag.affine_base >= 0 && ag.affine_step >= 0 && ag.bits < 32 && top < (1ll << 32);
+    }
   uint32_t status = 0;
   const unsigned long long *base = a.records + (size_t)p * a.nblk * C;
   // wave w streams record ranges w, w + 16, ... (each region's front and back): 16-B loads (two records) per lane,
@@ -847,14 +921,14 @@ __global__ __launch_bounds__(kRingReduceBlock) void k_ring_reduce(RingReduceArgs
   while (live_a) {  // uniform; every load unconditional (an exhausted stream loads unit 0 with no record counted)
     const bool live_b = ring_stream_next(a, hrow, C, base, rs, lane, vb, nb);
 #ifndef RING_EXP_NOFOLD
-    ring_fold_units<U, GATHER>(a, lds, cnt, exc_n, exc, va, na, pk, sbits, status);
+    ring_fold_units<U, GATHER>(a, lds, cnt, exc_n, exc, va, na, pk, sbits, lo32, status);
 #else
     for (int u = 0; u < U; u++) if (va[u].x == 0x01234567u && na[u] == 3) status |= 8u;
 #endif
     if (!live_b) break;
     live_a = ring_stream_next(a, hrow, C, base, rs, lane, va, na);
 #ifndef RING_EXP_NOFOLD
-    ring_fold_units<U, GATHER>(a, lds, cnt, exc_n, exc, vb, nb, pk, sbits, status);
+    ring_fold_units<U, GATHER>(a, lds, cnt, exc_n, exc, vb, nb, pk, sbits, lo32, status);
 #else
     for (int u = 0; u < U; u++) if (vb[u].x == 0x01234567u && nb[u] == 3) status |= 8u;
 #endif
@@ -875,7 +949,8 @@ __global__ __launch_bounds__(kRingReduceBlock) void k_ring_reduce(RingReduceArgs
     const uint8_t *acc = lds + ag.lds_off;
     if (ag.acc_kind == 4) {  // nibbles [K][128 B] -> u8 [G][256], 16 registers per thread (+ the exceptions)
       u32x4 *out = reinterpret_cast<u32x4 *>(static_cast<uint8_t *>(ag.acc) + kbase * 256);
-      for (long long t = tid; t < nkeys * 16; t += kRingReduceBlock) {
+      unsigned long long *sums = reinterpret_cast<unsigned long long *>(static_cast<uint8_t *>(ag.acc) + a.G * 256);
+      for (long long t = tid; t < nkeys * 16; t += kRingReduceBlock) {  // a key's 16 threads: 16 consecutive lanes
         const unsigned long long x = reinterpret_cast<const unsigned long long *>(acc)[t];
         uint32_t w[4] = {0, 0, 0, 0};
 #pragma unroll
@@ -896,6 +971,22 @@ __global__ __launch_bounds__(kRingReduceBlock) void k_ring_reduce(RingReduceArgs
         o.z = w[2];
         o.w = w[3];
         out[t] = o;
+        if (a.hll_sums) {  // HyperLogLog.cardinality's exact fixed-point sum and zero count (k_group_final kind 9)
+          unsigned long long sv = 0;
+          uint32_t z = 0;
+#pragma unroll
+          for (int j = 0; j < 16; j++) {
+            const uint32_t v = (w[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+            sv += 1ull << (32 - v);
+            z += v == 0u;
+          }
+#pragma unroll
+          for (int o2 = 8; o2 > 0; o2 >>= 1) {
+            sv += __shfl_xor(sv, o2, 16);
+            z += __shfl_xor(z, o2, 16);
+          }
+          if ((t & 15) == 0) sums[kbase + (t >> 4)] = sv | ((unsigned long long)z << 48);
+        }
       }
     } else {
       unsigned long long *out = static_cast<unsigned long long *>(ag.acc);
@@ -920,7 +1011,7 @@ __global__ __launch_bounds__(kRingReduceBlock) void k_ring_reduce(RingReduceArgs
 
 }  // namespace
 
-size_t ring_lds_bytes(int P) { return (size_t)P * (kRingBucket * 8 + 4 + 4) + 16; }
+size_t ring_lds_bytes(int P) { return (size_t)P * (kRingBucketStride * 8 + 4 + 4) + 16; }
 
 void launch_group_ring(const RingArgs &a, hipStream_t stream) {
   if (a.nblk <= 0 || a.total_chunks <= 0) return;

@@ -259,11 +259,17 @@ __global__ void k_group_final(const unsigned long long *__restrict__ counts, con
         case 1: v = static_cast<const double *>(f.acc[g])[k]; break;
         case 2:
         case 3: v = decode_ordered_d(static_cast<const unsigned long long *>(f.acc[g])[k]); break;
-        case 4: {
-          const u32x4 *r = reinterpret_cast<const u32x4 *>(static_cast<const uint8_t *>(f.acc[g]) + k * 256);
+        case 4:
+        case 9: {
           unsigned long long s = 0;
           uint32_t z = 0;
-          for (int q = 0; q < 16; q++) {
+          if (f.kind[g] == 9) {  // the reduce's packed sums
+            const unsigned long long x = static_cast<const unsigned long long *>(f.acc[g])[k];
+            s = x & ((1ull << 48) - 1ull);
+            z = (uint32_t)(x >> 48);
+          }
+          const u32x4 *r = reinterpret_cast<const u32x4 *>(static_cast<const uint8_t *>(f.acc[g]) + k * 256);
+          for (int q = 0; f.kind[g] == 4 && q < 16; q++) {
             const u32x4 w4 = r[q];
             const uint32_t w[4] = {w4.x, w4.y, w4.z, w4.w};
 #pragma unroll

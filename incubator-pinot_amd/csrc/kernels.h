@@ -384,7 +384,8 @@ struct RingReduceArgs {
   int32_t P, shift, n_aggs, nblk;
   int32_t lds_bytes, lds_zero_bytes;
   int32_t cnt_off, hist_off, exc_off;  // LDS: counts u32 [K], hist row u32 [nblk], exceptions (count + entries)
-  int32_t reserved;
+  int32_t hll_sums;  // 1: each HLL aggregation's array holds u64 [G] after its registers: Σ 2^(32 - register) in bits
+                     // 0..47, the zero registers' count in bits 48..63 (k_group_final kind 9 reads them, not the registers)
   long long G;
   unsigned long long *counts;
   uint32_t *status;
@@ -424,7 +425,7 @@ void launch_compact_keys_ordered(long long G, const unsigned long long *counts, 
 // 4 HLL u8 registers [G][256], 5 the count; acc: the accumulator the function reads (its primary's for aliases).
 struct GroupFinalArgs {
   int32_t n;
-  int32_t kind[kMaxGroupAggs];
+  int32_t kind[kMaxGroupAggs];  // accumulator kinds; 9: an HLL's packed register sums (RingReduceArgs.hll_sums)
   const void *acc[kMaxGroupAggs];
   double *out_values[kMaxGroupAggs];
   long long *out_card[kMaxGroupAggs];

@@ -14,6 +14,7 @@
 #include <cstring>
 
 #include "engine.h"
+#include "transcode.h"
 
 namespace pinot {
 
@@ -60,9 +61,22 @@ static void upload_dictionary(Engine &e, ColumnData &c) {
   }
 }
 
+// A raw (no-dictionary) column as a dictionary column: numeric ones on the device (transcode.hip), STRING on the host;
+// the bytes are the host path's either way (tests/test_gpu_raw.py compares them).
+bool transcode_column(Engine &e, const pinot_column_desc &d, int32_t num_docs, TranscodedColumn &tc) {
+  const int w = raw_numeric_width(d, num_docs);
+  if (!w || !e.raw_device) return transcode_raw(d, num_docs, tc);
+  std::vector<uint64_t> uniq;
+  transcode_numeric_device(d.forward_index, (uint64_t)std::max(num_docs, 0), w, d.data_type, e.stream, uniq,
+                           tc.forward_index);
+  transcoded_numeric_finish(d, uniq.data(), (int64_t)uniq.size(), tc);
+  e.raw_device_columns++;
+  return true;
+}
+
 static void register_column(Engine &e, SegmentData &seg, const pinot_column_desc &d_in) {
   TranscodedColumn tc;
-  const bool raw = transcode_raw(d_in, seg.num_docs, tc);  // no-dictionary column: one-time host transcoding
+  const bool raw = transcode_column(e, d_in, seg.num_docs, tc);  // no-dictionary column: one-time transcoding
   const pinot_column_desc &d = raw ? tc.desc : d_in;
   auto cp = std::make_unique<ColumnData>();
   ColumnData &c = *cp;

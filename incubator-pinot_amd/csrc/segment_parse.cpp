@@ -621,22 +621,51 @@ bool transcode_raw(const pinot_column_desc &d, int32_t num_docs, TranscodedColum
   return transcode_raw_threads(d, num_docs, out, 0);
 }
 
-bool transcode_raw_threads(const pinot_column_desc &d, int32_t num_docs, TranscodedColumn &out, size_t threads) {
-  if (d.encoding == PINOT_ENCODING_DICTIONARY) return false;
-  const size_t T = transcode_threads((uint64_t)std::max(num_docs, 0), threads);
+int raw_numeric_width(const pinot_column_desc &d, int32_t num_docs) {
+  if (d.encoding == PINOT_ENCODING_DICTIONARY) return 0;
   const std::string name = d.name ? d.name : "";
   require(d.encoding == PINOT_ENCODING_RAW, PINOT_ERR_BAD_ARG, name + ": unknown column encoding");
   require(!d.multi_value, PINOT_ERR_UNSUPPORTED, name + ": raw multi-value columns are not served");
   require(!d.bloom_filter && !d.create_bloom_filter, PINOT_ERR_UNSUPPORTED,
           name + ": bloom filters are not supported for no-dictionary columns");  // BloomFilterHandler.java:117-118
-  if (d.data_type == PINOT_STRING) return transcode_raw_string(d, num_docs, out, T);
+  if (d.data_type == PINOT_STRING) return 0;
   require(d.data_type >= PINOT_INT && d.data_type <= PINOT_DOUBLE, PINOT_ERR_BAD_ARG, name + ": data type");
   const int w = (d.data_type == PINOT_INT || d.data_type == PINOT_FLOAT) ? 4 : 8;
   const uint64_t n = (uint64_t)std::max(num_docs, 0);
   require(d.forward_index && d.forward_index_len >= n * (uint64_t)w, PINOT_ERR_BAD_ARG,
           name + ": raw forward index shorter than numDocs values");
+  return w;
+}
+
+void transcoded_numeric_finish(const pinot_column_desc &d, const uint64_t *uniq, int64_t card, TranscodedColumn &out) {
+  const std::string name = d.name ? d.name : "";
+  require(card < (1ll << 31), PINOT_ERR_UNSUPPORTED, name + ": more than 2^31 distinct values");
+  const int w = (d.data_type == PINOT_INT || d.data_type == PINOT_FLOAT) ? 4 : 8;
+  out.dictionary.resize((size_t)card * w);
+  for (int64_t j = 0; j < card; j++) {  // invert the key back to the BE value bytes
+    uint64_t k = uniq[j], v;
+    switch (d.data_type) {
+      case PINOT_INT: v = (k ^ 0x80000000ull) & 0xFFFFFFFFull; break;
+      case PINOT_LONG: v = k ^ 0x8000000000000000ull; break;
+      case PINOT_FLOAT: v = (k & 0x80000000ull) ? (k & 0x7FFFFFFFull) : (~k & 0xFFFFFFFFull); break;
+      default: v = (k & 0x8000000000000000ull) ? (k & 0x7FFFFFFFFFFFFFFFull) : ~k; break;
+    }
+    for (int b = 0; b < w; b++) out.dictionary[(size_t)j * w + b] = (uint8_t)(v >> (8 * (w - 1 - b)));
+  }
+  out.desc = pinot_column_desc{};
+  out.desc.cardinality = (int32_t)card;
+  out.desc.bits_per_value = num_bits_per_value(std::max<int64_t>(card - 1, 0));
+  finish_transcoded(d, out);
+}
+
+bool transcode_raw_threads(const pinot_column_desc &d, int32_t num_docs, TranscodedColumn &out, size_t threads) {
+  if (d.encoding == PINOT_ENCODING_DICTIONARY) return false;
+  const size_t T = transcode_threads((uint64_t)std::max(num_docs, 0), threads);
+  const int w = raw_numeric_width(d, num_docs);
+  if (d.data_type == PINOT_STRING) return transcode_raw_string(d, num_docs, out, T);
+  const uint64_t n = (uint64_t)std::max(num_docs, 0);
   // sort keys: order-preserving u64 images of the values (sign flip for ints, IEEE total order for floats with
-  // NaN canonicalised, as Double.compare orders them)
+  // NaN canonicalised, as Double.compare orders them); transcode.hip's k_raw_keys forms the same keys
   auto key = [&](uint64_t i) -> uint64_t {
     const uint8_t *p = d.forward_index + i * w;
     uint64_t v = 0;
@@ -662,20 +691,9 @@ bool transcode_raw_threads(const pinot_column_desc &d, int32_t num_docs, Transco
     for (uint64_t i = lo; i < hi; i++) keys[i] = key(i);
   });
   const std::vector<uint64_t> uniq = sorted_unique(keys, T);
-  require(uniq.size() < (1ull << 31), PINOT_ERR_UNSUPPORTED, name + ": more than 2^31 distinct values");
   const int64_t card = (int64_t)uniq.size();
+  require(card < (1ll << 31), PINOT_ERR_UNSUPPORTED, std::string(d.name ? d.name : "") + ": more than 2^31 distinct values");
   const int bits = num_bits_per_value(std::max<int64_t>(card - 1, 0));
-  out.dictionary.resize((size_t)card * w);
-  for (int64_t j = 0; j < card; j++) {  // invert the key back to the BE value bytes
-    uint64_t k = uniq[j], v;
-    switch (d.data_type) {
-      case PINOT_INT: v = (k ^ 0x80000000ull) & 0xFFFFFFFFull; break;
-      case PINOT_LONG: v = k ^ 0x8000000000000000ull; break;
-      case PINOT_FLOAT: v = (k & 0x80000000ull) ? (k & 0x7FFFFFFFull) : (~k & 0xFFFFFFFFull); break;
-      default: v = (k & 0x8000000000000000ull) ? (k & 0x7FFFFFFFFFFFFFFFull) : ~k; break;
-    }
-    for (int b = 0; b < w; b++) out.dictionary[(size_t)j * w + b] = (uint8_t)(v >> (8 * (w - 1 - b)));
-  }
   std::vector<uint32_t> ids(n);
   run_threads(T, [&](size_t t) {
     uint64_t lo, hi;
@@ -684,10 +702,7 @@ bool transcode_raw_threads(const pinot_column_desc &d, int32_t num_docs, Transco
       ids[i] = (uint32_t)(std::lower_bound(uniq.begin(), uniq.end(), keys[i]) - uniq.begin());
   });
   pack_ids(ids, bits, out.forward_index, T);
-  out.desc = pinot_column_desc{};
-  out.desc.cardinality = (int32_t)card;
-  out.desc.bits_per_value = bits;
-  finish_transcoded(d, out);
+  transcoded_numeric_finish(d, uniq.data(), card, out);
   return true;
 }
 

@@ -46,7 +46,7 @@ EXPORTED_SYMBOLS = [
     "pinot_gpu_last_kernel_ms", "pinot_gpu_engine_stat", "pinot_segment_read_raw_forward_index",
     "pinot_gpu_server_create", "pinot_gpu_server_unique_id", "pinot_gpu_server_create_rank", "pinot_gpu_server_destroy",
     "pinot_gpu_server_num_engines", "pinot_gpu_server_engine", "pinot_gpu_server_aggregate", "pinot_gpu_server_group_by",
-    "pinot_gpu_server_last_phases",
+    "pinot_gpu_server_last_phases", "pinot_gpu_transcode_raw",
 ]
 
 
@@ -172,6 +172,8 @@ def load(path=None):
         "pinot_gpu_segment_register": (i32, [P, C.POINTER(SegmentDesc), C.POINTER(i64)]),
         "pinot_gpu_segment_release": (i32, [P, i64]),
         "pinot_gpu_segment_validate": (i32, [C.POINTER(SegmentDesc)]),
+        "pinot_gpu_transcode_raw": (i32, [P, C.POINTER(ColumnDesc), i32, i32, C.POINTER(i32), C.POINTER(i32), P, u64,
+                                          C.POINTER(u64), P, u64, C.POINTER(u64)]),
         "pinot_gpu_segment_load": (i32, [P, C.c_char_p, C.POINTER(i64)]),
         "pinot_gpu_segment_acquire": (i32, [P, C.c_char_p, C.POINTER(i64), C.POINTER(i32)]),
         "pinot_gpu_segment_attach_star_tree": (i32, [P, i64, C.POINTER(StarTreeDesc)]),

@@ -285,6 +285,21 @@ class GpuEngine:
         check(self.lib.pinot_gpu_segment_register(self.ptr, C.byref(desc), C.byref(h)))
         return GpuSegment(self, h.value, seg.name, seg.num_docs)
 
+    def transcode_raw(self, seg: Segment, column: str, on_device: bool = True):
+        """pinot_gpu_transcode_raw: a raw column's dictionary form as registration builds it — (cardinality,
+        bits per value, dictionary bytes, packed forward-index bytes); on the GPU when on_device (numeric columns)."""
+        desc, _keep = segment_desc(seg)
+        names = list(seg.columns)
+        d = desc.columns[names.index(column)]
+        card, bits = C.c_int32(), C.c_int32()
+        dl, fl = C.c_uint64(), C.c_uint64()
+        args = (self.ptr, C.byref(d), seg.num_docs, int(on_device), C.byref(card), C.byref(bits))
+        check(self.lib.pinot_gpu_transcode_raw(*args, None, 0, C.byref(dl), None, 0, C.byref(fl)))
+        dic = C.create_string_buffer(max(dl.value, 1))
+        fwd = C.create_string_buffer(max(fl.value, 1))
+        check(self.lib.pinot_gpu_transcode_raw(*args, dic, dl.value, C.byref(dl), fwd, fl.value, C.byref(fl)))
+        return card.value, bits.value, dic.raw[:dl.value], fwd.raw[:fl.value]
+
     def load(self, index_dir: str) -> GpuSegment:
         """pinot_gpu_segment_load: a Pinot segment directory (v1/v2 files or v3 columns.psf) straight to HBM."""
         h = C.c_int64()

@@ -19,11 +19,15 @@ if "memory_copies" in tables:
     for r in c.execute("select start, end, %s from memory_copies" % (sz or "0")):
         rows.append((r[0], r[1], "C %d bytes" % (r[2] or 0)))
 rows.sort()
-marks = [i for i, r in enumerate(rows) if "GB_COUNT" in r[2] or "k_group_query<2" in r[2]]
-first = marks[-1] if marks else max(0, len(rows) - 40)
-prev = rows[first][0]
-t0 = prev
-for s, e, what in rows[first:]:
-    print("%9.1f us  gap %8.1f  dur %8.1f  %s" % ((s - t0) / 1e3, (s - prev) / 1e3, (e - s) / 1e3, what))
-    prev = e
+marks = [i for i, r in enumerate(rows) if "GB_COUNT" in r[2] or "k_group_query<2" in r[2] or "k_group_ring" in r[2]]
+# the last three queries' windows (each from its ring / COUNT pass to the next one)
+starts = marks[-3:] if marks else [max(0, len(rows) - 40)]
+for wi, first in enumerate(starts):
+    last = starts[wi + 1] if wi + 1 < len(starts) else len(rows)
+    prev = rows[first][0]
+    t0 = prev
+    print("---- query window %d" % wi)
+    for s, e, what in rows[first:last]:
+        print("%9.1f us  gap %8.1f  dur %8.1f  %s" % ((s - t0) / 1e3, (s - prev) / 1e3, (e - s) / 1e3, what))
+        prev = e
 print("tables:", ", ".join(tables))

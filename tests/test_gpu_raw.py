@@ -228,3 +228,33 @@ def test_large_raw_columns_threaded_transcode(engine):
     finally:
         gr.release()
         gd.release()
+
+
+@pytest.mark.parametrize("n", [1, 2, 777, 65537, 2_000_000])
+def test_device_transcode_matches_host(engine, n):
+    """Registration's device transcode of raw numeric columns (transcode.hip: radix sort of value keys, distinct count,
+    MSB-first packing) gives the host path's bytes exactly: dictionary, cardinality, bit width, forward index — for
+    INT / LONG / FLOAT / DOUBLE with negative values, -0.0 beside 0.0, NaN and infinities, single-value and
+    all-distinct columns."""
+    rng = np.random.default_rng(990 + n)
+    dbl = np.round(rng.normal(0, 1e3, n), 1)
+    dbl[rng.random(n) < 0.01] = -0.0
+    dbl[rng.random(n) < 0.005] = np.nan
+    dbl[rng.random(n) < 0.005] = np.inf
+    flt = rng.normal(0, 10, n).astype(np.float32)
+    flt[rng.random(n) < 0.01] = np.float32(-np.inf)
+    cols = {"i": ("INT", rng.integers(-2 ** 31, 2 ** 31, n).astype(np.int32)),
+            "l": ("LONG", rng.integers(-5, 5, n).astype(np.int64) * 10 ** 15),
+            "f": ("FLOAT", flt),
+            "d": ("DOUBLE", dbl),
+            "one": ("INT", np.full(n, 7, np.int32)),
+            "all": ("LONG", np.arange(n, dtype=np.int64) * 3 - n)}
+    seg = build_segment("tc", cols, raw_columns=tuple(cols), allow_sorted=False)
+    before = engine.stat("raw.device_columns")
+    for c in cols:
+        dev = engine.transcode_raw(seg, c, on_device=True)
+        host = engine.transcode_raw(seg, c, on_device=False)
+        assert dev[:2] == host[:2], c
+        assert dev[2] == host[2], c
+        assert dev[3] == host[3], c
+    assert engine.stat("raw.device_columns") == before + len(cols)

@@ -267,8 +267,9 @@ class Job:
             return lambda: self.ex.process_query(q, self.segs)
         if self.path == "engine":
             # what the server hands the broker: the group-by trimmed on the device (CombineGroupByOperator's
-            # AggregationGroupByTrimmingService, TOP 10 -> 5,000 groups per function) serialized as DataTable bytes
-            return lambda: self.ex.process_query_datatable(q, self.segs, trim=True)
+            # AggregationGroupByTrimmingService, TOP 10 -> 5,000 groups per function) serialized as DataTable bytes,
+            # handed on as a view of the native buffer (as a transport would send it; no Python-side copy)
+            return lambda: self.ex.process_query_datatable(q, self.segs, trim=True, zero_copy=True)
         return lambda: self.ex.process_query(q, self.segs, as_result=True)
 
     def set_config(self, cfg):

@@ -382,8 +382,9 @@ std::vector<uint8_t> group_by_datatable(const pinot_query &q, const GroupByResul
     Fn &F = fns[i];
     F.m = fn_groups && fn_groups[i] ? fn_num_groups[i] : n;
     F.sel = fn_groups && fn_groups[i] ? fn_groups[i] : nullptr;
-    for (int64_t j = 0; F.sel && j < F.m; j++)
-      require(F.sel[j] >= 0 && F.sel[j] < n, PINOT_ERR_BAD_ARG, "group index out of range");
+    bool in_range = true;
+    for (int64_t j = 0; F.sel && j < F.m; j++) in_range = in_range && F.sel[j] >= 0 && F.sel[j] < n;
+    require(in_range, PINOT_ERR_BAD_ARG, "group index out of range");
     F.f = sv_function(r.functions[i]);
     F.vtype = F.f == PINOT_AGG_COUNT ? OBJ_LONG : F.f == PINOT_AGG_AVG ? OBJ_AVG_PAIR
               : F.f == PINOT_AGG_DISTINCTCOUNTHLL ? OBJ_HLL : OBJ_DOUBLE;

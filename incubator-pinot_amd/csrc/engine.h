@@ -303,6 +303,8 @@ struct Engine {
   uint64_t arena_dev_gen = 0;
   bool arena_dev_valid = false;
   PinnedBuffer host_result;   // staging of the reduced results (D2H)
+  PinnedBuffer d2h_small;     // pinned landing of the group-by's small status reads (a pageable target makes each copy
+                              // a staged, synchronous one: ~20-35 us apiece)
   DeviceBuffer fused_ctl;     // k_scan_query: u32 arrival counter + [kMaxHll][256] HLL registers, kept zeroed
   MappedBuffer fused_result;  // k_scan_query's last block writes the reduced per-segment slots + HLL here
 
@@ -360,6 +362,7 @@ struct DenseOut {
   // hll_ser_off[fn], copied back with the other arrays
   std::shared_ptr<DeviceBuffer> hll_ser;
   std::vector<size_t> hll_ser_off;
+  int32_t *key_ids = nullptr;       // device-trimmed results: [n][gcols] global ids of each kept key (trim.h)
   // compact read-back (dense, non-hashed key spaces of >= 64 K groups): the non-empty keys as a bitmap over [0, G),
   // counts and HLL cardinalities as u32 (overflow flag -> the 64-bit arrays), widened on the host
   const uint64_t *key_bits = nullptr;
@@ -373,6 +376,29 @@ struct DenseOut {
 // The single-value function whose intermediate result / merge / final result a multi-value function shares
 // (CountMVAggregationFunction extends CountAggregationFunction, etc.).
 inline int sv_function(int f) { return f >= PINOT_AGG_COUNTMV && f <= PINOT_AGG_DISTINCTCOUNTHLLMV ? f - PINOT_AGG_COUNTMV : f; }
+
+// A pinned host vector whose resize leaves new elements uninitialised (a D2H copy fills them: no zero pass over
+// megabytes first).
+template <typename T>
+struct PinnedNoInitAllocator : PinnedAllocator<T> {
+  template <typename U>
+  struct rebind {
+    using other = PinnedNoInitAllocator<U>;
+  };
+  PinnedNoInitAllocator() = default;
+  template <typename U>
+  PinnedNoInitAllocator(const PinnedNoInitAllocator<U> &) {}
+  template <typename U>
+  void construct(U *p) noexcept {
+    ::new (static_cast<void *>(p)) U;
+  }
+  template <typename U, typename... A>
+  void construct(U *p, A &&...a) {
+    ::new (static_cast<void *>(p)) U(std::forward<A>(a)...);
+  }
+};
+template <typename T>
+using HostVecNoInit = std::vector<T, PinnedNoInitAllocator<T>>;
 
 struct GroupByResult {
   GroupByResult() = default;
@@ -409,7 +435,7 @@ struct GroupByResult {
   std::vector<HllPart> hll_parts;
   // device-trimmed results (pinot_gpu_group_by_top): per HLL function its groups' HyperLogLog.getBytes, [n][180] B
   // (empty: not prepared; the DataTable writer then packs the registers itself)
-  std::vector<HostVec<uint8_t>> hll_bytes;
+  std::vector<HostVecNoInit<uint8_t>> hll_bytes;
   mutable std::vector<uint8_t> datatable;  // pinot_datatable_group_by's bytes
 };
 // all groups' u8 HLL registers of function fn ([groups][256]) into host memory, from the device parts or the host copy

@@ -2308,9 +2308,11 @@ class TaskPool {
       std::lock_guard<std::mutex> lk(mu_);
       job_ = job;
       gen_++;
+      gen_seen_.store(gen_, std::memory_order_release);
     }
     cv_.notify_all();
     work(*job);  // the caller takes tasks too
+    for (int spin = 0; spin < kSpin && job->done.load(std::memory_order_acquire) != n; spin++) pause();
     std::unique_lock<std::mutex> lk(mu_);
     done_cv_.wait(lk, [&] { return job->done.load() == n; });
     job_.reset();
@@ -2339,9 +2341,14 @@ class TaskPool {
       }
     }
   }
+  // A worker that finished a job spins briefly before sleeping: the host phases issue their parallel passes a few
+  // microseconds apart, and a condition-variable wake costs tens of microseconds per pass.
+  static constexpr int kSpin = 20000;  // ~50-100 us of pause instructions
+  static void pause() { __builtin_ia32_pause(); }
   void loop() {
     uint64_t seen = 0;
     for (;;) {
+      for (int spin = 0; spin < kSpin && gen_seen_.load(std::memory_order_acquire) == seen; spin++) pause();
       std::shared_ptr<Job> j;
       {
         std::unique_lock<std::mutex> lk(mu_);
@@ -2357,6 +2364,7 @@ class TaskPool {
   std::condition_variable cv_, done_cv_;
   std::shared_ptr<Job> job_;
   uint64_t gen_ = 0;
+  std::atomic<uint64_t> gen_seen_{0};  // gen_, readable without the lock (the spin)
 };
 }  // namespace
 
@@ -2707,19 +2715,21 @@ struct DenseGroups {
   std::vector<const void *> hll_sum;  // per accumulator: the HLL's packed register sums (k_group_final kind 9), or null
 };
 
+// extra(pinned) issues the caller's own small D2H reads into pinned[0, 4096) (read back after the wait).
 unsigned long long compact_dense(Engine &e, const unsigned long long *counts, int64_t G, long long *&keys_dev,
-                                 const std::function<void()> &extra) {
+                                 const std::function<void(uint8_t *)> &extra, size_t extra_bytes = 0) {
   const size_t cscr = compact_keys_scratch_bytes(G);
   e.group_final.reserve(G * 8 + 64 + cscr);
   keys_dev = e.group_final.get<long long>();
   auto *n_dev = reinterpret_cast<unsigned long long *>(e.group_final.get<uint8_t>() + G * 8);
   launch_compact_keys_ordered(G, counts, keys_dev, n_dev, e.group_final.get<uint8_t>() + G * 8 + 64, cscr, e.stream);
   PINOT_HIP(hipGetLastError());
-  unsigned long long n = 0;
-  PINOT_HIP(hipMemcpyAsync(&n, n_dev, 8, hipMemcpyDeviceToHost, e.stream));
-  if (extra) extra();
+  e.d2h_small.reserve(64 + std::max<size_t>(extra_bytes, 4096));
+  auto *hn = e.d2h_small.get<unsigned long long>();
+  PINOT_HIP(hipMemcpyAsync(hn, n_dev, 8, hipMemcpyDeviceToHost, e.stream));
+  if (extra) extra(e.d2h_small.get<uint8_t>() + 64);
   wait_stream(e);
-  return n;
+  return *hn;
 }
 
 // Device half of build_dense_result: the final arrays of the n non-empty groups in the host result's layout
@@ -2758,7 +2768,11 @@ DenseOut dense_outputs(Engine &e, const DenseGroups &d, const long long *keys_de
   const bool compact = compact_ok && e.compact_d2h && !d.hashed && n >= (1u << 16) && d.ks->G > 0;
   const size_t key_words = compact ? (size_t)((d.ks->G + 63) / 64) : 0;
   const size_t compact_bytes = compact ? key_words * 8 + n * 4 * (1 + n_card) + 64 : 0;
-  e.group_out.reserve(n8 * (2 + na + n_card) + 256 + compact_bytes);
+  // a subset's keys also as per-column global ids (no division in the DataTable writer), after the arrays
+  const int nc = q.num_group_by;
+  const bool digits = serialize_hll && !d.hashed && nc <= kDigitsMaxCols && (size_t)d.ks->gcard.size() == (size_t)nc;
+  const size_t digit_bytes = digits ? n * nc * 4 + 16 : 0;
+  e.group_out.reserve(n8 * (2 + na + n_card) + 256 + compact_bytes + digit_bytes);
   GroupFinalArgs f{};
   f.n = na;
   f.out_keys = e.group_out.get<long long>();
@@ -2812,6 +2826,14 @@ DenseOut dense_outputs(Engine &e, const DenseGroups &d, const long long *keys_de
   }
   launch_group_final(d.counts, keys_dev, (long long)n, f, e.stream);
   PINOT_HIP(hipGetLastError());
+  if (digits) {
+    KeyDigits kd{};
+    kd.nc = nc;
+    for (int j = 0; j < nc; j++) kd.card[j] = d.ks->gcard[j];
+    o.key_ids = reinterpret_cast<int32_t *>(reinterpret_cast<uint8_t *>(f.out_counts + n) + n8 * (na + n_card));
+    launch_key_digits(keys_dev, (long long)n, d.key_base, kd, o.key_ids, e.stream);
+    PINOT_HIP(hipGetLastError());
+  }
   if (n_hll && gather_hll) {  // registers stay on the device until asked for; buffers are recycled once released
     const size_t need = (size_t)n_hll * n * 256 + 16;
     for (auto &b : e.hll_pool)
@@ -2998,6 +3020,28 @@ std::unique_ptr<GroupByResult> dense_fetch(Engine &e, const pinot_query &q, cons
     if (o.derive[i] == -1) copies.emplace_back(res->values[i].data(), o.values[i]);
     if (o.kind[i] == 4) copies.emplace_back(res->hll_card[i].data(), o.cards[i]);
   }
+  const size_t id_bytes = o.key_ids ? n * (size_t)q.num_group_by * 4 : 0;
+  if (o.key_ids) res->key_ids.resize(n * (size_t)q.num_group_by);
+  if (n8 < (1u << 20)) {  // small arrays are pageable (HostVec): one copy of the arrays' device span into pinned
+                          // staging, then host copies (a pageable D2H target is a staged, synchronous copy apiece)
+    const uint8_t *lo = static_cast<const uint8_t *>(copies[0].second), *hi = lo;
+    for (auto &c : copies) {
+      lo = std::min(lo, static_cast<const uint8_t *>(c.second));
+      hi = std::max(hi, static_cast<const uint8_t *>(c.second) + n8);
+    }
+    if (o.key_ids) {  // right after the arrays (dense_outputs)
+      lo = std::min(lo, reinterpret_cast<const uint8_t *>(o.key_ids));
+      hi = std::max(hi, reinterpret_cast<const uint8_t *>(o.key_ids) + id_bytes);
+    }
+    e.group_host.reserve((size_t)(hi - lo));
+    PINOT_HIP(hipMemcpyAsync(e.group_host.get(), lo, (size_t)(hi - lo), hipMemcpyDeviceToHost, e.stream));
+    wait_stream(e);
+    for (auto &c : copies)
+      memcpy(c.first, e.group_host.get<uint8_t>() + (static_cast<const uint8_t *>(c.second) - lo), n8);
+    if (o.key_ids)
+      memcpy(res->key_ids.data(), e.group_host.get<uint8_t>() + (reinterpret_cast<const uint8_t *>(o.key_ids) - lo), id_bytes);
+    copies.clear();
+  }
   const int ns = (n8 >= (1u << 20)) ? std::min<int>(e.d2h_streams, (int)copies.size()) : 1;
   if (ns > 1) {
     while ((int)e.copy_streams.size() < ns - 1) {
@@ -3014,6 +3058,8 @@ std::unique_ptr<GroupByResult> dense_fetch(Engine &e, const pinot_query &q, cons
     hipStream_t st = k == 0 ? e.stream : e.copy_streams[k - 1];
     PINOT_HIP(hipMemcpyAsync(copies[j].first, copies[j].second, n8, hipMemcpyDeviceToHost, st));
   }
+  if (o.key_ids && !copies.empty())
+    PINOT_HIP(hipMemcpyAsync(res->key_ids.data(), o.key_ids, id_bytes, hipMemcpyDeviceToHost, e.stream));
   for (int k = 0; k < ns - 1; k++) PINOT_HIP(hipStreamSynchronize(e.copy_streams[k]));
   wait_stream(e);
   bool any_derived = false;
@@ -3081,11 +3127,13 @@ const long long *device_trim(Engine &e, const DenseGroups &d, const long long *k
   PINOT_HIP(hipGetLastError());
   // the union holds at most na x T groups: its count and flags in one round trip
   const size_t max_u = std::min<size_t>((size_t)n, (size_t)na * (size_t)T);
-  unsigned long long nu = 0;
-  HostVec<uint32_t> hf(max_u);
-  PINOT_HIP(hipMemcpyAsync(&nu, n_dev, 8, hipMemcpyDeviceToHost, e.stream));
-  PINOT_HIP(hipMemcpyAsync(hf.data(), uflags, max_u * 4, hipMemcpyDeviceToHost, e.stream));
+  e.d2h_small.reserve(64 + max_u * 4);
+  auto *pin = e.d2h_small.get<uint8_t>();
+  PINOT_HIP(hipMemcpyAsync(pin, n_dev, 8, hipMemcpyDeviceToHost, e.stream));
+  PINOT_HIP(hipMemcpyAsync(pin + 64, uflags, max_u * 4, hipMemcpyDeviceToHost, e.stream));
   wait_stream(e);
+  const unsigned long long nu = *reinterpret_cast<const unsigned long long *>(pin);
+  const uint32_t *hf = reinterpret_cast<const uint32_t *>(pin + 64);
   require(nu <= max_u, PINOT_ERR_DEVICE, "trim union larger than its functions' lists");
   kept.assign(na, {});
   for (int i = 0; i < na; i++) kept[i].reserve((size_t)T);
@@ -3614,11 +3662,16 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
   uint32_t verify_err = 0;
   long long *keys_dev = nullptr;
   uint32_t rs[4] = {0, 0, 0, 0};
-  const unsigned long long n = compact_dense(e, counts, ks.G, keys_dev, [&] {
-    PINOT_HIP(hipMemcpyAsync(hmatched.data(), matched, S * 8, hipMemcpyDeviceToHost, e.stream));
-    if (ks.hashed) PINOT_HIP(hipMemcpyAsync(&verify_err, a.verify_err, 4, hipMemcpyDeviceToHost, e.stream));
-    if (ring_status) PINOT_HIP(hipMemcpyAsync(rs, ring_status, 16, hipMemcpyDeviceToHost, e.stream));
-  });
+  uint8_t *small = nullptr;
+  const unsigned long long n = compact_dense(e, counts, ks.G, keys_dev, [&](uint8_t *pin) {
+    small = pin;  // [0, 8S) matched, then 16 B of ring status, then the verify flag
+    PINOT_HIP(hipMemcpyAsync(pin, matched, S * 8, hipMemcpyDeviceToHost, e.stream));
+    if (ring_status) PINOT_HIP(hipMemcpyAsync(pin + S * 8, ring_status, 16, hipMemcpyDeviceToHost, e.stream));
+    if (ks.hashed) PINOT_HIP(hipMemcpyAsync(pin + S * 8 + 16, a.verify_err, 4, hipMemcpyDeviceToHost, e.stream));
+  }, S * 8 + 32);
+  memcpy(hmatched.data(), small, S * 8);
+  if (ring_status) memcpy(rs, small + S * 8, 16);
+  if (ks.hashed) memcpy(&verify_err, small + S * 8 + 16, 4);
   if (rs[0]) return ring_fallback();
   if (verify_err) {  // 64-bit fingerprint collision: retry with another seed
     require(attempt < 3, PINOT_ERR_DEVICE, "group-key fingerprint collisions persist");
@@ -4619,7 +4672,7 @@ DenseOut slice_outputs(Engine &e, const pinot_query &q, const std::vector<int> &
   ga.acc_bytes_per_key.assign(acc_kind.size(), 0);
   const std::vector<int> alias(acc_kind.size(), -1);
   long long *keys_dev = nullptr;
-  const unsigned long long n = G > 0 ? compact_dense(e, counts, G, keys_dev, nullptr) : 0;
+  const unsigned long long n = G > 0 ? compact_dense(e, counts, G, keys_dev, {}) : 0;
   DenseGroups dg{&q, &ks, &ga, &ga, &alias, counts, accs, key_base, nullptr};
   return dense_outputs(e, dg, keys_dev, n);
 }

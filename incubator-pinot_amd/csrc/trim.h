@@ -24,4 +24,14 @@ size_t trim_radix_scratch_bytes(long long n, int nf);
 void launch_trim_radix(const TrimFn *fns, int nf, const long long *counts, long long n, long long T, uint32_t *flags,
                        void *scratch, size_t scratch_bytes, hipStream_t stream);
 
+// ids[i][j] = global id of group column j in key keys[i] + key_base (mixed radix, column 0 least significant:
+// DictionaryBasedGroupKeyGenerator's raw key): the kept groups' key tuples, so the DataTable writer does no division.
+constexpr int kDigitsMaxCols = 16;
+struct KeyDigits {
+  long long card[kDigitsMaxCols];
+  int32_t nc;
+};
+void launch_key_digits(const long long *keys, long long n, long long key_base, const KeyDigits &kd, int32_t *ids,
+                       hipStream_t stream);
+
 }  // namespace pinot

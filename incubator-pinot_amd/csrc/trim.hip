@@ -1,10 +1,13 @@
 // Radix selection of the server trim's kept groups (trim.h): no sort of the group arrays.
 //
+//   k_trim_andor   the keys materialised once, with each block's AND / OR of them (a digit no key varies in is known
+//                  without a histogram)
 //   k_trim_round   round r (digit bits [56 - 8r, 64 - 8r)): every block histograms the digit of the keys that match
-//                  the prefix found so far, per function, in LDS, then adds its histogram to the global one; the last
-//                  block to finish picks the digit holding the remaining rank, extends the prefix, and clears the
-//                  histogram for the next round. After eight rounds the prefix is the trimSize-th key K and the rank
-//                  is how many ties of K in group order precede it.
+//                  the prefix found so far, per function, in LDS, then adds it into one of kTrimCopies global copies
+//                  (a single copy puts every block's adds on the same 256 addresses: memory-side atomics serialise);
+//   k_trim_pick    one block: the copies summed, the digit holding the remaining rank picked, the prefix extended.
+//                  After eight rounds the prefix is the trimSize-th key K and the rank is how many ties of K in group
+//                  order precede it.
 //   k_trim_ties    per block of 1024 groups, the ties of K per function.
 //   k_trim_flags   per group, the functions keeping it: key < K, or key == K with fewer than rank + 1 earlier ties
 //                  (the block's own earlier ties from an LDS scan, the earlier blocks' from k_trim_ties).
@@ -23,11 +26,13 @@ namespace {
 constexpr int kTrimBlock = 256;
 constexpr int kTrimPerThread = 4;                     // k_trim_ties / k_trim_flags: consecutive groups per thread
 constexpr int kTrimTile = kTrimBlock * kTrimPerThread;  // groups per block
+constexpr size_t kTrimStateBytes = 512;
+constexpr int kTrimCopies = 32;  // global histogram copies (block b adds into copy b % kTrimCopies)
 
 struct TrimState {
   unsigned long long prefix[kTrimMaxFns];
   unsigned long long rank[kTrimMaxFns];  // 0-based rank of the trimSize-th key among the keys matching the prefix
-  uint32_t done;                         // blocks finished in the current round
+  unsigned long long kand[kTrimMaxFns], kor[kTrimMaxFns];  // AND / OR of every key: a digit no key varies in is known
 };
 
 struct TrimArgs {
@@ -36,10 +41,12 @@ struct TrimArgs {
   const long long *counts;
   long long n;
   TrimState *st;
-  uint32_t *hist;  // [nf][256]
+  uint32_t *hist;              // [kTrimCopies][nf][256]
+  unsigned long long *keys;    // [nf][n]: every group's key per function (k_trim_andor writes them)
+  unsigned long long *bandor;  // [blocks][nf][2]: each block's AND / OR
 };
 
-__device__ __forceinline__ unsigned long long trim_key(const TrimArgs &a, int f, long long i) {
+__device__ __forceinline__ unsigned long long trim_key_of(const TrimArgs &a, int f, long long i) {
   double v = a.fn[f].vals[i];
   if (a.fn[f].avg) v = v / (double)a.counts[i];
   if (v == 0.0) v = 0.0;
@@ -48,53 +55,171 @@ __device__ __forceinline__ unsigned long long trim_key(const TrimArgs &a, int f,
   return a.fn[f].asc ? o : ~o;
 }
 
+__device__ __forceinline__ unsigned long long trim_key(const TrimArgs &a, int f, long long i) {
+  return a.keys[(size_t)f * a.n + i];
+}
+
 __global__ void k_trim_init(TrimArgs a, long long T) {
-  for (int i = threadIdx.x; i < a.nf * 256; i += blockDim.x) a.hist[i] = 0;
+  for (int i = threadIdx.x; i < kTrimCopies * a.nf * 256; i += blockDim.x) a.hist[i] = 0;
   if (threadIdx.x < kTrimMaxFns) {
     a.st->prefix[threadIdx.x] = 0;
     a.st->rank[threadIdx.x] = (unsigned long long)(T - 1);
   }
-  if (threadIdx.x == 0) a.st->done = 0;
+}
+
+// The keys, materialised (AVG's division once), and each block's AND / OR of them; kTrimPerThread groups per thread,
+// their loads issued together.
+__global__ __launch_bounds__(kTrimBlock) void k_trim_andor(TrimArgs a) {
+  __shared__ unsigned long long sx[kTrimBlock / 64], so[kTrimBlock / 64];
+  const long long i0 = (long long)blockIdx.x * kTrimTile + threadIdx.x;
+  for (int f = 0; f < a.nf; f++) {
+    unsigned long long k[kTrimPerThread], x = ~0ull, o = 0ull;
+#pragma unroll
+    for (int j = 0; j < kTrimPerThread; j++) {
+      const long long i = i0 + (long long)j * kTrimBlock;
+      k[j] = i < a.n ? trim_key_of(a, f, i) : 0ull;
+    }
+#pragma unroll
+    for (int j = 0; j < kTrimPerThread; j++) {
+      const long long i = i0 + (long long)j * kTrimBlock;
+      if (i < a.n) {
+        a.keys[(size_t)f * a.n + i] = k[j];
+        x &= k[j];
+        o |= k[j];
+      }
+    }
+    for (int m = 32; m > 0; m >>= 1) {
+      x &= __shfl_xor(x, m);
+      o |= __shfl_xor(o, m);
+    }
+    if ((threadIdx.x & 63) == 0) {
+      sx[threadIdx.x >> 6] = x;
+      so[threadIdx.x >> 6] = o;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int w = 1; w < kTrimBlock / 64; w++) {
+        x &= sx[w];
+        o |= so[w];
+      }
+      a.bandor[((size_t)blockIdx.x * a.nf + f) * 2] = x;
+      a.bandor[((size_t)blockIdx.x * a.nf + f) * 2 + 1] = o;
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(kTrimBlock) void k_trim_andor_reduce(TrimArgs a, int blocks) {
+  __shared__ unsigned long long sx[kTrimBlock / 64], so[kTrimBlock / 64];
+  for (int f = 0; f < a.nf; f++) {
+    unsigned long long x = ~0ull, o = 0ull;
+    for (int b = threadIdx.x; b < blocks; b += kTrimBlock) {
+      x &= a.bandor[((size_t)b * a.nf + f) * 2];
+      o |= a.bandor[((size_t)b * a.nf + f) * 2 + 1];
+    }
+    for (int m = 32; m > 0; m >>= 1) {
+      x &= __shfl_xor(x, m);
+      o |= __shfl_xor(o, m);
+    }
+    if ((threadIdx.x & 63) == 0) {
+      sx[threadIdx.x >> 6] = x;
+      so[threadIdx.x >> 6] = o;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int w = 1; w < kTrimBlock / 64; w++) {
+        x &= sx[w];
+        o |= so[w];
+      }
+      a.st->kand[f] = x;
+      a.st->kor[f] = o;
+    }
+    __syncthreads();
+  }
+}
+
+__device__ __forceinline__ uint32_t trim_vary(const TrimArgs &a, int shift) {
+  uint32_t vary = 0;  // functions whose keys differ in this digit (the others' digit is every key's)
+  for (int f = 0; f < a.nf; f++)
+    if (((a.st->kand[f] ^ a.st->kor[f]) >> shift) & 255ull) vary |= 1u << f;
+  return vary;
 }
 
 __global__ __launch_bounds__(kTrimBlock) void k_trim_round(TrimArgs a, int round) {
   __shared__ uint32_t h[kTrimMaxFns][256];
-  __shared__ bool last;
   const int tid = threadIdx.x;
+  const int shift = 56 - 8 * round;
+  const uint32_t vary = trim_vary(a, shift);
+  if (!vary) return;
   for (int i = tid; i < a.nf * 256; i += kTrimBlock) h[i >> 8][i & 255] = 0;
   __syncthreads();
-  const int shift = 56 - 8 * round;
   unsigned long long pre[kTrimMaxFns];
   for (int f = 0; f < a.nf; f++) pre[f] = round ? a.st->prefix[f] >> (shift + 8) : 0ull;
-  for (long long i = (long long)blockIdx.x * kTrimBlock + tid; i < a.n; i += (long long)gridDim.x * kTrimBlock)
-    for (int f = 0; f < a.nf; f++) {
-      const unsigned long long k = trim_key(a, f, i);
-      if (round == 0 || (k >> (shift + 8)) == pre[f]) atomicAdd(&h[f][(k >> shift) & 255u], 1u);
+  const long long i0 = (long long)blockIdx.x * kTrimTile + tid;
+  for (int f = 0; f < a.nf; f++) {
+    if (!((vary >> f) & 1u)) continue;
+    unsigned long long kk[kTrimPerThread];
+#pragma unroll
+    for (int j = 0; j < kTrimPerThread; j++) {  // every load first
+      const long long i = i0 + (long long)j * kTrimBlock;
+      kk[j] = i < a.n ? trim_key(a, f, i) : 0ull;
     }
+#pragma unroll
+    for (int j = 0; j < kTrimPerThread; j++) {
+      const unsigned long long k = kk[j];
+      const bool in = i0 + (long long)j * kTrimBlock < a.n && (round == 0 || (k >> (shift + 8)) == pre[f]);
+      const uint32_t d = (uint32_t)(k >> shift) & 255u;
+      // the wave's most common case first: every lane holding the first active lane's digit in one add
+      const unsigned long long act = __ballot(in);
+      bool done = !in;
+      if (act) {
+        const uint32_t d0 = (uint32_t)__shfl((int)d, (int)__builtin_ctzll(act), 64);
+        const unsigned long long same = __ballot(in && d == d0);
+        if (in && d == d0) {
+          done = true;
+          if ((tid & 63) == (int)__builtin_ctzll(same)) atomicAdd(&h[f][d0], (uint32_t)__popcll(same));
+        }
+      }
+      if (!done) atomicAdd(&h[f][d], 1u);
+    }
+  }
   __syncthreads();
+  uint32_t *g = a.hist + (size_t)(blockIdx.x % kTrimCopies) * a.nf * 256;
   for (int i = tid; i < a.nf * 256; i += kTrimBlock)
-    if (h[i >> 8][i & 255]) atomicAdd(a.hist + i, h[i >> 8][i & 255]);
-  __threadfence();
+    if (h[i >> 8][i & 255]) atomicAdd(g + i, h[i >> 8][i & 255]);
+}
+
+// One block after each round: per function the digit holding the remaining rank (its copies summed), the prefix
+// extended; the copies zeroed for the next round.
+__global__ __launch_bounds__(kTrimBlock) void k_trim_pick(TrimArgs a, int round) {
+  __shared__ uint32_t c[kTrimMaxFns][256];
+  const int tid = threadIdx.x;
+  const int shift = 56 - 8 * round;
+  const uint32_t vary = trim_vary(a, shift);
+  for (int i = tid; i < a.nf * 256; i += kTrimBlock) {
+    uint32_t t = 0;
+    for (int r = 0; r < kTrimCopies; r++) {
+      t += a.hist[(size_t)r * a.nf * 256 + i];
+      a.hist[(size_t)r * a.nf * 256 + i] = 0;
+    }
+    c[i >> 8][i & 255] = t;
+  }
   __syncthreads();
-  if (tid == 0) last = atomicAdd(&a.st->done, 1u) == gridDim.x - 1;
-  __syncthreads();
-  if (!last) return;
-  __threadfence();
-  if (tid < a.nf) {  // one thread per function: the digit holding the remaining rank
+  if (tid < a.nf) {
     const int f = tid;
     unsigned long long r = a.st->rank[f], cum = 0;
     int d = 0;
-    for (; d < 256; d++) {
-      const unsigned long long c = __hip_atomic_load(a.hist + f * 256 + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (r < cum + c) break;
-      cum += c;
+    if ((vary >> f) & 1u) {
+      for (; d < 255; d++) {
+        if (r < cum + c[f][d]) break;
+        cum += c[f][d];
+      }
+    } else {
+      d = (int)((a.st->kand[f] >> shift) & 255ull);  // every key's digit: the rank stays
     }
-    a.st->prefix[f] |= (unsigned long long)(d < 256 ? d : 255) << shift;
+    a.st->prefix[f] |= (unsigned long long)d << shift;
     a.st->rank[f] = r - cum;
   }
-  __syncthreads();
-  for (int i = tid; i < a.nf * 256; i += kTrimBlock) a.hist[i] = 0;
-  if (tid == 0) a.st->done = 0;
 }
 
 __global__ __launch_bounds__(kTrimBlock) void k_trim_ties(TrimArgs a, uint32_t *ties) {
@@ -163,11 +288,32 @@ __global__ __launch_bounds__(kTrimBlock) void k_trim_flags(TrimArgs a, const uin
     if (i0 + j < a.n) flags[i0 + j] = m[j];
 }
 
+__global__ void k_key_digits(const long long *__restrict__ keys, long long n, long long key_base, KeyDigits kd,
+                             int32_t *__restrict__ ids) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    unsigned long long k = (unsigned long long)(keys[i] + key_base);
+    for (int j = 0; j < kd.nc; j++) {
+      const unsigned long long c = (unsigned long long)kd.card[j];
+      ids[i * kd.nc + j] = (int32_t)(k % c);
+      k /= c;
+    }
+  }
+}
+
 }  // namespace
+
+void launch_key_digits(const long long *keys, long long n, long long key_base, const KeyDigits &kd, int32_t *ids,
+                       hipStream_t stream) {
+  if (n <= 0) return;
+  const int grid = (int)std::min<long long>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_key_digits, dim3(grid), dim3(256), 0, stream, keys, n, key_base, kd, ids);
+}
 
 size_t trim_radix_scratch_bytes(long long n, int nf) {
   const long long blocks = (n + kTrimTile - 1) / kTrimTile;
-  return 256 + (size_t)nf * 256 * 4 + (size_t)nf * blocks * 4 + 256;
+  auto up = [](size_t b) { return (b + 255) / 256 * 256; };
+  return kTrimStateBytes + up((size_t)kTrimCopies * nf * 256 * 4) + up((size_t)nf * blocks * 4) +
+         up((size_t)blocks * nf * 16) + (size_t)nf * n * 8 + 256;
 }
 
 void launch_trim_radix(const TrimFn *fns, int nf, const long long *counts, long long n, long long T, uint32_t *flags,
@@ -181,16 +327,28 @@ void launch_trim_radix(const TrimFn *fns, int nf, const long long *counts, long 
   a.counts = counts;
   a.n = n;
   uint8_t *p = static_cast<uint8_t *>(scratch);
+  auto up = [](size_t b) { return (b + 255) / 256 * 256; };
+  const long long blocks = (n + kTrimTile - 1) / kTrimTile;
   a.st = reinterpret_cast<TrimState *>(p);
-  a.hist = reinterpret_cast<uint32_t *>(p + 256);
-  auto *ties = reinterpret_cast<uint32_t *>(p + 256 + (size_t)nf * 256 * 4);
-  static_assert(sizeof(TrimState) <= 256, "trim state");
+  p += kTrimStateBytes;
+  a.hist = reinterpret_cast<uint32_t *>(p);
+  p += up((size_t)kTrimCopies * nf * 256 * 4);
+  auto *ties = reinterpret_cast<uint32_t *>(p);
+  p += up((size_t)nf * blocks * 4);
+  a.bandor = reinterpret_cast<unsigned long long *>(p);
+  p += up((size_t)blocks * nf * 16);
+  a.keys = reinterpret_cast<unsigned long long *>(p);
+  static_assert(sizeof(TrimState) <= kTrimStateBytes, "trim state");
+  const unsigned grid = (unsigned)blocks;  // one tile of kTrimTile groups per block in every pass
   hipLaunchKernelGGL(k_trim_init, dim3(1), dim3(kTrimBlock), 0, stream, a, T);
-  const int grid = (int)std::min<long long>((n + kTrimBlock * 16 - 1) / (kTrimBlock * 16), 1024);
-  for (int r = 0; r < 8; r++) hipLaunchKernelGGL(k_trim_round, dim3(grid), dim3(kTrimBlock), 0, stream, a, r);
-  const unsigned blocks = (unsigned)((n + kTrimTile - 1) / kTrimTile);
-  hipLaunchKernelGGL(k_trim_ties, dim3(blocks), dim3(kTrimBlock), 0, stream, a, ties);
-  hipLaunchKernelGGL(k_trim_flags, dim3(blocks), dim3(kTrimBlock), 0, stream, a, ties, flags);
+  hipLaunchKernelGGL(k_trim_andor, dim3(grid), dim3(kTrimBlock), 0, stream, a);
+  hipLaunchKernelGGL(k_trim_andor_reduce, dim3(1), dim3(kTrimBlock), 0, stream, a, (int)blocks);
+  for (int r = 0; r < 8; r++) {
+    hipLaunchKernelGGL(k_trim_round, dim3(grid), dim3(kTrimBlock), 0, stream, a, r);
+    hipLaunchKernelGGL(k_trim_pick, dim3(1), dim3(kTrimBlock), 0, stream, a, r);
+  }
+  hipLaunchKernelGGL(k_trim_ties, dim3(grid), dim3(kTrimBlock), 0, stream, a, ties);
+  hipLaunchKernelGGL(k_trim_flags, dim3(grid), dim3(kTrimBlock), 0, stream, a, ties, flags);
 }
 
 }  // namespace pinot

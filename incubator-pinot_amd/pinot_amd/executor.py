@@ -476,9 +476,10 @@ class GroupByResult:
                                          cards.ctypes.data_as(C.c_void_p)))
         return regs[:n], cards[:n]
 
-    def data_table(self, marshal, stats, trim_top_n=None, server=None):
+    def data_table(self, marshal, stats, trim_top_n=None, server=None, zero_copy=False):
         """DataTable bytes of this result (pinot_datatable_group_by), each function's map trimmed to its own top
-        groups (AggregationGroupByTrimmingService) when trim_top_n is given."""
+        groups (AggregationGroupByTrimmingService) when trim_top_n is given. zero_copy: a read-only memoryview of the
+        result's own buffer (it keeps this result alive), as a transport would hand the native bytes on."""
         na = len(self.query["aggregations"])
         groups = nums = None
         if trim_top_n is not None:
@@ -488,7 +489,13 @@ class GroupByResult:
         data, size = C.c_void_p(), C.c_uint64()
         check(self.lib.pinot_datatable_group_by(C.byref(marshal.q), self.ptr, groups, nums, C.byref(stats), server,
                                                 C.byref(data), C.byref(size)))
-        return C.string_at(data, size.value) if size.value else b""
+        if not size.value:
+            return b""
+        if zero_copy:
+            view = (C.c_ubyte * size.value).from_address(data.value)
+            view.owner = self  # the bytes live in the native result until it is freed
+            return memoryview(view).cast("B").toreadonly()
+        return C.string_at(data, size.value)
 
     def to_map(self, trim_top_n=None):
         """{string_key: [intermediate result per function]} (the CombineGroupByOperator result map).
@@ -715,7 +722,7 @@ class ServerQueryExecutor:
             res = [_agg_value(sv_name(a["function"]), out[i]) for i, a in enumerate(query["aggregations"])]
         return res, _stats(stats)
 
-    def process_query_datatable(self, query, segments, trim=True, server=None):
+    def process_query_datatable(self, query, segments, trim=True, server=None, zero_copy=False):
         """`processQuery` as the server answers the broker: the combined result as DataTable bytes
         (IntermediateResultsBlock.getDataTable -> DataTableImplV2.toBytes, built natively by pinot_datatable_*).
         Group-by maps are trimmed per function like CombineGroupByOperator when `trim`; `server` =
@@ -753,7 +760,7 @@ class ServerQueryExecutor:
             if total is not None:
                 stats.num_total_raw_docs = total
             res = GroupByResult(lib, out, query)
-            return res.data_table(m, stats, top_n, srv), _stats(stats)
+            return res.data_table(m, stats, top_n, srv, zero_copy), _stats(stats)
         n = len(query["aggregations"])
         out = (_lib.AggResult * n)()
         check(lib.pinot_gpu_aggregate(self.engine.ptr, handles, len(segments), C.byref(m.q), out, C.byref(stats)))

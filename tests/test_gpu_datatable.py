@@ -102,6 +102,8 @@ def test_group_by_datatable_trimmed_per_function_and_limit_flag(engine):
                                       float(mins[j]))
     exp, _ = O.execute_server([seg], q, num_groups_limit=50_000)
     assert len(exp) == len(keys)
+    view, _ = ex.process_query_datatable(q, [g], trim=True, zero_copy=True)  # the native buffer, no copy
+    assert isinstance(view, memoryview) and view.readonly and bytes(view) == data
     g.release()
 
 

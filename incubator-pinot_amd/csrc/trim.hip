@@ -27,7 +27,7 @@ constexpr int kTrimBlock = 256;
 constexpr int kTrimPerThread = 4;                     // k_trim_ties / k_trim_flags: consecutive groups per thread
 constexpr int kTrimTile = kTrimBlock * kTrimPerThread;  // groups per block
 constexpr size_t kTrimStateBytes = 512;
-constexpr int kTrimCopies = 32;  // global histogram copies (block b adds into copy b % kTrimCopies)
+constexpr int kTrimCopies = 16;  // global histogram copies (block b adds into copy b % kTrimCopies)
 
 struct TrimState {
   unsigned long long prefix[kTrimMaxFns];
@@ -191,15 +191,20 @@ __global__ __launch_bounds__(kTrimBlock) void k_trim_round(TrimArgs a, int round
 
 // One block after each round: per function the digit holding the remaining rank (its copies summed), the prefix
 // extended; the copies zeroed for the next round.
-__global__ __launch_bounds__(kTrimBlock) void k_trim_pick(TrimArgs a, int round) {
+constexpr int kTrimPickBlock = 1024;
+__global__ __launch_bounds__(kTrimPickBlock) void k_trim_pick(TrimArgs a, int round) {
   __shared__ uint32_t c[kTrimMaxFns][256];
   const int tid = threadIdx.x;
   const int shift = 56 - 8 * round;
   const uint32_t vary = trim_vary(a, shift);
-  for (int i = tid; i < a.nf * 256; i += kTrimBlock) {
+  for (int i = tid; i < a.nf * 256; i += kTrimPickBlock) {  // one (function, digit) per thread, its copies loaded at once
+    uint32_t v[kTrimCopies];
+#pragma unroll
+    for (int r = 0; r < kTrimCopies; r++) v[r] = a.hist[(size_t)r * a.nf * 256 + i];
     uint32_t t = 0;
+#pragma unroll
     for (int r = 0; r < kTrimCopies; r++) {
-      t += a.hist[(size_t)r * a.nf * 256 + i];
+      t += v[r];
       a.hist[(size_t)r * a.nf * 256 + i] = 0;
     }
     c[i >> 8][i & 255] = t;
@@ -345,7 +350,7 @@ void launch_trim_radix(const TrimFn *fns, int nf, const long long *counts, long 
   hipLaunchKernelGGL(k_trim_andor_reduce, dim3(1), dim3(kTrimBlock), 0, stream, a, (int)blocks);
   for (int r = 0; r < 8; r++) {
     hipLaunchKernelGGL(k_trim_round, dim3(grid), dim3(kTrimBlock), 0, stream, a, r);
-    hipLaunchKernelGGL(k_trim_pick, dim3(1), dim3(kTrimBlock), 0, stream, a, r);
+    hipLaunchKernelGGL(k_trim_pick, dim3(1), dim3(kTrimPickBlock), 0, stream, a, r);
   }
   hipLaunchKernelGGL(k_trim_ties, dim3(grid), dim3(kTrimBlock), 0, stream, a, ties);
   hipLaunchKernelGGL(k_trim_flags, dim3(grid), dim3(kTrimBlock), 0, stream, a, ties, flags);

@@ -18,5 +18,6 @@ for wl in $wls; do
   cp profiles/traffic_$wl.json $out/
   python3 scripts/pmc_summary.py $out/pmc_${wl}_FETCH_SIZE/run_results.db > $out/pmc_${wl}_summary.txt
   python3 scripts/pmc_summary.py $out/pmc_${wl}_WRITE_SIZE/run_results.db >> $out/pmc_${wl}_summary.txt
+  rm -f $out/pmc_${wl}_FETCH_SIZE/run_results.db $out/pmc_${wl}_WRITE_SIZE/run_results.db
   cat $out/traffic_$wl.log
 done

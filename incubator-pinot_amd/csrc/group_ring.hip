@@ -716,9 +716,14 @@ __device__ __forceinline__ void ring_fold(const RingReduceArgs &a, uint8_t *lds,
   for (int g = 0; g < a.n_aggs; g++) {
     const GroupAggDev &ag = a.aggs[g];
     if (ag.acc_kind == 5) continue;
+    // a slot outside the streamed range holds whatever the region's memory held (an earlier query's records): its
+    // dictId indexes nothing, so the gathers below read entry 0 for it
     uint32_t id[N];
 #pragma unroll
-    for (int u = 0; u < N; u++) id[u] = (uint32_t)((rec[u] >> ag.field_shift) & ((1ull << ag.bits) - 1ull));
+    for (int u = 0; u < N; u++) {
+      id[u] = (uint32_t)((rec[u] >> ag.field_shift) & ((1ull << ag.bits) - 1ull));
+      if constexpr (GATHER) id[u] = ok[u] ? id[u] : 0u;
+    }
     uint8_t *acc = lds + ag.lds_off;
     if (ag.acc_kind == 0) {
       unsigned long long v[N];  // affine: Σ dictId here, Σ value = base * count + step * Σ dictId at the end
@@ -870,12 +875,15 @@ __global__ __launch_bounds__(kRingReduceBlock) void k_ring_reduce(RingReduceArgs
       unsigned long long *m = reinterpret_cast<unsigned long long *>(lds + a.aggs[g].lds_off);
       for (int i = tid; i < K; i += kRingReduceBlock) m[i] = ~0ull;
     }
-  __shared__ uint32_t s_n, s_C;
+  __shared__ uint32_t s_n, s_C, s_over;
   if (tid == 0) {
     s_n = 0;
     s_C = *a.region;
+    s_over = *a.status & 1u;
   }
   __syncthreads();
+  // a region overflowed: its counts name slots never written this query (the host answers on the counted plan)
+  if (s_over) return;
   {
     uint32_t part = 0;
     for (int i = tid; i < a.nblk; i += kRingReduceBlock) {

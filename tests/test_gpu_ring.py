@@ -178,3 +178,19 @@ def test_ring_skewed_keys_fall_back():
     ran, fell = _run(e, q, [g], [seg])
     assert (ran, fell) == (1, 1)
     e.close()
+
+
+def test_ring_sparse_query_after_wide_records():
+    """A sparse query after a dense one on the same engine: the record buffer's slots beyond each region's streamed
+    range still hold the first query's records (another field layout), and the reduce's dictionary / HLL-LUT gathers
+    must not index by them (non-affine LONG dictionary: the HLL reads its LUT)."""
+    segs = [_mixed_segment("s0", 200_000, 31, np.arange(0, 100), np.arange(0, 100)),
+            _mixed_segment("s1", 150_000, 32, np.arange(0, 100), np.arange(0, 100))]
+    e = GpuEngine(0, "group.mode=partition;group.ring=1")
+    gsegs = [e.register(s) for s in segs]
+    for text in ("SELECT SUM(dv), MAX(lv) FROM t GROUP BY k1, k2",
+                 "SELECT DISTINCTCOUNTHLL(lv), SUM(lv) FROM t WHERE f < 1 AND h > 30000 GROUP BY k2, k1",
+                 "SELECT DISTINCTCOUNTHLL(lv) FROM t WHERE f = 3 OR h < 70 GROUP BY k1, k2"):
+        ran, fell = _run(e, compile_pql(text), gsegs, segs)
+        assert (ran, fell) == (1, 0)
+    e.close()

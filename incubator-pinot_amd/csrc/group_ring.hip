@@ -251,15 +251,30 @@ __device__ __forceinline__ RingColsDev ring_cols(const RingArgs &a, const GroupS
   return k;
 }
 
-// Lane-owns-quarter decode that hands each of the lane's 16 values to f.put<J>(v) as it is extracted (no 16-value
-// array: the decoders' registers go to the raw dwords of the columns in flight). The raw dwords pass through an empty
-// volatile asm first, so the compiler cannot hoist the byte swaps of every width of the switch above it.
-template <int B, typename F>
+// Values J0 .. JE - 1 of a lane's quarter (group_lq.h decode_quarter_apply over a sub-range).
+template <int B, int J, int JE, typename F>
+__device__ __forceinline__ void ring_quarter_apply(const uint32_t (&D)[(B + 1) / 2 + 1], F &f) {
+  constexpr int q = J * B, k = q >> 5, o = q & 31;
+  constexpr uint32_t mask = (uint32_t)((1ull << B) - 1ull);
+  if constexpr (o + B <= 32) f.template put<J>((D[k] >> (32 - o - B)) & mask);
+  else f.template put<J>(__builtin_amdgcn_alignbit(D[k], D[k + 1], 64 - o - B) & mask);
+  if constexpr (J + 1 < JE) ring_quarter_apply<B, J + 1, JE>(D, f);
+}
+
+// Lane-owns-quarter decode that hands values J0 .. JE - 1 of the lane's 16 to f.put<J>(v) as they are extracted (no
+// 16-value array: the decoders' registers go to the raw dwords of the columns in flight); only the dwords those values
+// span are byte-swapped. The raw dwords pass through an empty volatile asm first, so the compiler cannot hoist the byte
+// swaps of every width of the switch above it.
+template <int B, int J0, int JE, typename F>
 __device__ __forceinline__ void ring_decode_b(const uint32_t (&Rin)[12], int64_t qi, F &f) {
   constexpr int N = (B + 1) / 2 + (B & 1);
+  // the dwords the values span (odd widths: + the 16-bit shift of odd quarters), as sources of the last alignbit too
+  constexpr int LO = (J0 * B) >> 5, HI = ((JE * B + 15) >> 5) + 2 < N ? ((JE * B + 15) >> 5) + 2 : N;
   uint32_t D[(B + 1) / 2 + 1];
 #pragma unroll
-  for (int i = 0; i < N; i++) {
+  for (int i = 0; i < (B + 1) / 2 + 1; i++) D[i] = 0;
+#pragma unroll
+  for (int i = LO; i < HI; i++) {
     uint32_t r = Rin[i];
     asm volatile("" : "+v"(r));
     D[i] = bswap32(r);
@@ -267,15 +282,15 @@ __device__ __forceinline__ void ring_decode_b(const uint32_t (&Rin)[12], int64_t
   if constexpr (B & 1) {
     if (qi & 1) {
 #pragma unroll
-      for (int i = 0; i + 1 < N; i++) D[i] = __builtin_amdgcn_alignbit(D[i], D[i + 1], 16);
+      for (int i = LO; i + 1 < HI; i++) D[i] = __builtin_amdgcn_alignbit(D[i], D[i + 1], 16);
     }
   }
-  decode_quarter_apply<B, 0>(D, f);
+  ring_quarter_apply<B, J0, JE>(D, f);
 }
 
-template <typename F>
+template <int J0, int JE, typename F>
 __device__ __forceinline__ void ring_decode(const uint32_t (&R)[12], int bits, int64_t qi, F &f) {
-#define PINOT_RD(B) ring_decode_b<B>(R, qi, f)
+#define PINOT_RD(B) ring_decode_b<B, J0, JE>(R, qi, f)
   switch (bits) {  // widths up to kGroupLwMaxBits (plan_ring checks)
     case 1: PINOT_RD(1); break;   case 2: PINOT_RD(2); break;   case 3: PINOT_RD(3); break;   case 4: PINOT_RD(4); break;
     case 5: PINOT_RD(5); break;   case 6: PINOT_RD(6); break;   case 7: PINOT_RD(7); break;   case 8: PINOT_RD(8); break;
@@ -377,7 +392,7 @@ __device__ __forceinline__ void ring_load_raw(const uint8_t *fwd, int bits, int6
 // range (or a chunk with no candidate doc) requests nothing and decodes to no record.
 template <int NF, bool WORDS>
 struct RingDecoder {
-  int64_t c0, nq;
+  int64_t c0, nq, g_end;  // g_end: the first global chunk past segment g
   int wave, g;
   RingSeg sg;
   RingColsDev k;
@@ -389,8 +404,9 @@ struct RingDecoder {
   uint32_t word_bits;    // the lane's 16 candidate docs (pre / filter words, tail)
   uint32_t F[NF > 0 ? NF : 1][12];
   uint32_t RA[kRingGroupCols][12], RB[kRingAggCols][12];
-  // the decoded quarter
-  uint32_t act;
+  // the decoded quarter (act_next / skip_next: the requested quarter's filter between its two decode halves)
+  uint32_t act, act_next;
+  bool skip_next;
   unsigned long long rec[16];
 
   __device__ __forceinline__ void init(const RingArgs &a, int64_t c0_, int64_t nq_, int wave_, int lane) {
@@ -398,9 +414,11 @@ struct RingDecoder {
     nq = nq_;
     wave = wave_;
     g = -1;
+    g_end = 0;
     seg_matched = 0;
     live = false;
-    act = 0;
+    act = act_next = 0;
+    skip_next = true;
 #pragma unroll
     for (int j = 0; j < 16; j++) rec[j] = 0;
   }
@@ -412,8 +430,9 @@ struct RingDecoder {
     const int64_t c = c0 + (qg >> 2);
     const int q = (int)(qg & 3);
     const int lane = threadIdx.x & 63;
-    const int gn = ring_segment(a, c, g < 0 ? 0 : g);
-    if (gn != g) {  // uniform: the descriptors change with the segment only
+    if (g < 0 || c >= g_end) {  // uniform: the descriptors change with the segment only
+      const int gn = ring_segment(a, c, g < 0 ? 0 : g);
+      g_end = gn + 1 < a.nsegs ? load_const(a.cstart + gn + 1) : INT64_MAX;
       if (!WORDS && g >= 0) ring_add_matched(a, g, seg_matched, lane);
       seg_matched = 0;
       g = gn;
@@ -467,16 +486,13 @@ struct RingDecoder {
       if (k.bits[kRingGroupCols + cc]) ring_load_raw(k.fwd[kRingGroupCols + cc], k.bits[kRingGroupCols + cc], qi, RB[cc]);
   }
 
-  __device__ __forceinline__ void decode(const RingArgs &a, int lane, uint32_t &status) {
-    act = live ? word_bits : 0u;
-    if (!__any(act != 0)) {  // uniform: nothing to insert
-      act = 0;
-      return;
-    }
+  // Records J0 .. JE - 1 of the requested quarter (keys, then the aggregated fields).
+  template <int J0, int JE>
+  __device__ __forceinline__ void decode_records(const RingArgs &a) {
 #ifdef RING_EXP_NODEC
     {  // experiment: records of pseudo-random keys, no column data
 #pragma unroll
-      for (int j = 0; j < 16; j++) {
+      for (int j = J0; j < JE; j++) {
         unsigned long long z = (unsigned long long)(qi * 16 + j) + 0x9E3779B97F4A7C15ull;
         z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
         z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
@@ -486,36 +502,57 @@ struct RingDecoder {
       return;
     }
 #endif
+    uint32_t key[16];
+#pragma unroll
+    for (int j = J0; j < JE; j++) key[j] = 0;
+#pragma unroll
+    for (int cc = 0; cc < kRingGroupCols; cc++) {
+      if (!k.bits[cc]) continue;
+      RingKeyFold f{key, k.remap[cc], k.stride[cc]};
+      ring_decode<J0, JE>(RA[cc], k.bits[cc], qi, f);
+    }
+    const uint32_t lmask = (1u << a.shift) - 1u;
+#pragma unroll
+    for (int j = J0; j < JE; j++)
+      rec[j] = (unsigned long long)(key[j] & lmask) | ((unsigned long long)(key[j] >> a.shift) << kRecPShift);
+#pragma unroll
+    for (int cc = 0; cc < kRingAggCols; cc++) {
+      if (!k.bits[kRingGroupCols + cc]) continue;
+      RingFieldFold f{rec, k.fsh[kRingGroupCols + cc]};
+      ring_decode<J0, JE>(RB[cc], k.bits[kRingGroupCols + cc], qi, f);
+    }
+  }
+
+  // First half of the requested quarter's decode (while the flushers empty round 0's buckets): its filter (every doc)
+  // into act_next and records 0 .. 7, whose round-0 entries of the current pass are already in the buckets.
+  __device__ __forceinline__ void decode_front(const RingArgs &a) {
+    act_next = live ? word_bits : 0u;
+    skip_next = !__any(act_next != 0);  // uniform: nothing to insert
+    if (skip_next) {
+      act_next = 0;
+      return;
+    }
+#ifndef RING_EXP_NODEC
     if constexpr (NF > 0) {
 #pragma unroll
       for (int i = 0; i < NF; i++)
         if (i < sg.n_leaves) {
           uint32_t m = 0;
           RingLeafFold f{st[i], m};
-          ring_decode(F[i], st[i].bits, qi, f);
-          act &= (st[i].negate ? ~m : m) & 0xFFFFu;
+          ring_decode<0, 16>(F[i], st[i].bits, qi, f);
+          act_next &= (st[i].negate ? ~m : m) & 0xFFFFu;
         }
     }
-    if constexpr (!WORDS) seg_matched += __popc(act);
-    uint32_t key[16];
-#pragma unroll
-    for (int j = 0; j < 16; j++) key[j] = 0;
-#pragma unroll
-    for (int cc = 0; cc < kRingGroupCols; cc++) {
-      if (!k.bits[cc]) continue;
-      RingKeyFold f{key, k.remap[cc], k.stride[cc]};
-      ring_decode(RA[cc], k.bits[cc], qi, f);
-    }
-    const uint32_t lmask = (1u << a.shift) - 1u;
-#pragma unroll
-    for (int j = 0; j < 16; j++)
-      rec[j] = (unsigned long long)(key[j] & lmask) | ((unsigned long long)(key[j] >> a.shift) << kRecPShift);
-#pragma unroll
-    for (int cc = 0; cc < kRingAggCols; cc++) {
-      if (!k.bits[kRingGroupCols + cc]) continue;
-      RingFieldFold f{rec, k.fsh[kRingGroupCols + cc]};
-      ring_decode(RB[cc], k.bits[kRingGroupCols + cc], qi, f);
-    }
+#endif
+    if constexpr (!WORDS) seg_matched += __popc(act_next);
+    decode_records<0, kRingRoundRecs>(a);
+  }
+
+  // Second half (while the flushers empty round 1's buckets): records 8 .. 15; the quarter becomes the current one.
+  __device__ __forceinline__ void decode_back(const RingArgs &a) {
+    act = act_next;
+    if (skip_next) return;
+    if constexpr (kRingRoundRecs < 16) decode_records<kRingRoundRecs, 16>(a);
   }
 
   __device__ __forceinline__ void finish(const RingArgs &a, int lane) {
@@ -528,9 +565,10 @@ struct RingDecoder {
 //
 // The block walks its quarters in passes: in pass t decoder wave w takes quarter 4 c0 + 8 t + w of the block's range
 // (none past its end: that wave inserts nothing). A pass inserts the wave's 16 records per lane in two rounds of
-// [insert phase | barrier | flush phase | barrier]; during the second flush phase the decoders decode the next pass's
-// quarter (its raw dwords requested a pass earlier) and request the one after it. Every wave executes the same
-// barriers.
+// [insert phase | barrier | flush phase | barrier]; during the first flush phase the decoders evaluate the filter of the
+// next pass's quarter (its raw dwords requested a pass earlier) and decode its records 0 .. 7 (the slots round 0 just
+// emptied), during the second its records 8 .. 15, then request the quarter after it: the decode's VALU work fills
+// both flush phases. Every wave executes the same barriers.
 template <int NF, bool WORDS>
 __global__ __launch_bounds__(kRingBlock) void k_group_ring(RingArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -597,7 +635,8 @@ __global__ __launch_bounds__(kRingBlock) void k_group_ring(RingArgs a) {
     RingDecoder<NF, WORDS> d;
     d.init(a, c0, nq, wave, lane);
     d.load(a, 0);  // pass 0's raw dwords
-    d.decode(a, lane, status);
+    d.decode_front(a);
+    d.decode_back(a);
     d.load(a, 1);  // in flight during pass 0's rounds
 #ifdef RING_EXP_TIMING
     uint64_t ti = 0, tb = 0, td = 0, tl = 0, tt = 0;
@@ -609,23 +648,29 @@ __global__ __launch_bounds__(kRingBlock) void k_group_ring(RingArgs a) {
       ring_insert<0>(a, L, d.act, d.rec, region0, C);
 #endif
       RT_ADD(ti, x0);
-      RT_MARK(x2);
       if constexpr (kRingRoundRecs < 16) {
         __syncthreads();  // inserts of round 0 done
+        // the next pass's quarter: filter and records 0 .. 7 decoded meanwhile the flushers empty round 0's buckets
+        RT_MARK(x1);
+        d.decode_front(a);
+        RT_ADD(td, x1);
         __syncthreads();  // flush done
+        RT_MARK(x2);
 #ifndef RING_EXP_NOINS
         ring_insert<kRingRoundRecs>(a, L, d.act, d.rec, region0, C);
 #else
         if (d.rec[3] == 0x0123456789ull && d.act == 7) status |= 8u;
 #endif
+        RT_ADD(ti, x2);
       }
-      RT_ADD(ti, x2);
       RT_MARK(x3);
       __syncthreads();  // inserts of round 1 done
       RT_ADD(tb, x3);
-      // the next pass's quarter decoded meanwhile the flushers empty the buckets, then the one after it requested
+      // records 8 .. 15 of the next pass's quarter decoded meanwhile the flushers empty round 1's buckets, then the
+      // quarter after it requested
       RT_MARK(x4);
-      d.decode(a, lane, status);
+      if constexpr (kRingRoundRecs == 16) d.decode_front(a);
+      d.decode_back(a);
       RT_ADD(td, x4);
       RT_MARK(x5);
       d.load(a, t + 2);

@@ -799,18 +799,24 @@ __device__ __forceinline__ void ring_fold(const RingReduceArgs &a, uint8_t *lds,
 #endif
       uint32_t *word[N], old[N], rk[N];
       int sh[N];
+      uint32_t over = 0;  // records whose rank exceeds the nibble: the exception list (rare)
 #pragma unroll
       for (int u = 0; u < N; u++) {
         const uint32_t idx = k[u] * 256 + (h[u] >> 8), rank = h[u] & 0xFFu;
         word[u] = reinterpret_cast<uint32_t *>(acc) + (idx >> 3);
         sh[u] = (int)(idx & 7) * 4;
         rk[u] = ok[u] ? min(rank, 15u) : 0u;
-        if (ok[u] && rank > 15u) {
-          const uint32_t e = atomicAdd(exc_n, 1u);
-          if (e < (uint32_t)kRingExceptions) exc[e] = (k[u] << 13) | ((h[u] >> 8) << 5) | rank;
-          else status |= 4u;
-        }
+        over |= (ok[u] && rank > 15u) ? (1u << u) : 0u;
         old[u] = *word[u];
+      }
+      if (__any(over != 0)) {  // uniform, rare: out of the register reads' way (no branch or wait between them)
+#pragma unroll
+        for (int u = 0; u < N; u++)
+          if ((over >> u) & 1u) {
+            const uint32_t e = atomicAdd(exc_n, 1u);
+            if (e < (uint32_t)kRingExceptions) exc[e] = (k[u] << 13) | ((h[u] >> 8) << 5) | (h[u] & 0xFFu);
+            else status |= 4u;
+          }
       }
 #pragma unroll
       for (int u = 0; u < N; u++) {

@@ -132,6 +132,10 @@ __device__ __forceinline__ void ring_insert(const RingArgs &a, const RingLds &L,
   }
 }
 
+// A flushed 16-B piece of a region: a plain store, so L2 merges a region's two 64-B halves into one line before it
+// writes the line back (measured 2 % faster than non-temporal stores, r05p).
+__device__ __forceinline__ void ring_store(u32x4 v, u32x4 *dst) { *dst = v; }
+
 // Flush phase (flusher waves only, between two block barriers): every bucket holding 8 or more entries moves its
 // oldest half (entries head .. head + 7: one aligned 64-B piece of LDS) to the front of its region at the partition's
 // front cursor (64-B aligned: regions start 128-B aligned and the front advances by 8 records), then the head moves
@@ -171,7 +175,7 @@ __device__ __forceinline__ void ring_flush_phase(const RingArgs &a, const RingLd
 #endif
       u32x4 *dst = reinterpret_cast<u32x4 *>(region0 + (size_t)p * a.nblk * C + front[k]);
 #pragma unroll
-      for (int r = 0; r < 4; r++) __builtin_nontemporal_store(x[k][r] & m, dst + r);
+      for (int r = 0; r < 4; r++) ring_store(x[k][r] & m, dst + r);
     } else if (front[k] + 8u > C) {
       status |= 1u;  // region full: the query falls back to the counted plan
     }
@@ -183,7 +187,7 @@ __device__ __forceinline__ void ring_flush_phase(const RingArgs &a, const RingLd
       if (front[k] + 8u <= C) {
         u32x4 *dst = reinterpret_cast<u32x4 *>(region0 + (size_t)p * a.nblk * C + front[k]);
 #pragma unroll
-        for (int r = 0; r < 4; r++) __builtin_nontemporal_store(src[r] & m, dst + r);
+        for (int r = 0; r < 4; r++) ring_store(src[r] & m, dst + r);
       } else {
         status |= 1u;
       }

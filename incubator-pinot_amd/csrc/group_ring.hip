@@ -42,7 +42,11 @@ using namespace dev;
 
 constexpr int kRingBlock = 768;                             // one block of 12 waves per CU (the buckets take the LDS)
 constexpr int kRingWaves = kRingBlock / 64;
+#ifdef RING_EXP_FLUSH_WAVES
+constexpr int kRingFlushWaves = RING_EXP_FLUSH_WAVES;        // experiment: another decoder / flusher split
+#else
 constexpr int kRingFlushWaves = 4;                           // waves 8..11: the flush phases (one per SIMD)
+#endif
 constexpr int kRingDecWaves = kRingWaves - kRingFlushWaves;  // waves 0..7: filter, decode, insert (two per SIMD)
 #ifdef RING_EXP_ONEROUND
 constexpr int kRingRoundRecs = 16;                           // experiment: one insert phase per pass

@@ -301,14 +301,24 @@ class Job:
             self.dist.destroy_process_group()
 
 
-def timed_steps(job, step, steps, warmup):
-    """W untimed warm-ups, then exactly K steps bracketed by barrier + device sync; max over ranks."""
+def timed_steps(job, step, steps, warmup, warmup_s=0.0):
+    """W untimed warm-ups (continued, still untimed, until they have run warmup_s seconds: the GPU's clocks ramp over
+    the first few hundred ms of work on some boxes), then exactly K steps bracketed by barrier + device sync; max over
+    ranks. Returns the extra warm-up steps too."""
     import torch
     # the harness's own collector pauses stay out of the timed steps (the C-ABI call has none); collected before the
     # warm-ups so the timed steps follow them with no idle gap on the device
     gc.collect()
     gc.disable()
+    tw = time.perf_counter()
     for _ in range(warmup):
+        step()
+    # the extra count from the W warm-ups' pace, the same on every rank (a step may hold collectives)
+    extra = 0
+    if warmup > 0:
+        spent = time.perf_counter() - tw
+        extra = int(min(5000.0, job.max_over_ranks(max(0.0, (warmup_s - spent) / (spent / warmup)))) + 0.999)
+    for _ in range(extra):
         step()
     job.barrier()
     torch.cuda.synchronize()
@@ -327,6 +337,7 @@ def timed_steps(job, step, steps, warmup):
     job.barrier()
     elapsed = time.perf_counter() - t0
     gc.enable()
+    timed_steps.extra_warmup = extra
     return job.max_over_ranks(elapsed), (step_ms, dev_ms), abi_ms, res, st
 
 
@@ -356,7 +367,7 @@ def measure(job, args, workload):
     text = WORKLOAD_QUERY[workload]
     step = job.step_fn(text, gb)
     steps = args.steps if workload == args.workload else args.c4_steps
-    elapsed, (step_ms, dev_ms), abi_ms, res, st = timed_steps(job, step, steps, args.warmup)
+    elapsed, (step_ms, dev_ms), abi_ms, res, st = timed_steps(job, step, steps, args.warmup, args.warmup_seconds)
     ms_per_step = elapsed * 1000.0 / steps
     value = job.total_rows * steps / elapsed
     reps = max(3, min(steps, 10))
@@ -406,6 +417,7 @@ def measure(job, args, workload):
         "n_gpus": job.n_gpus,
         "steps": steps,
         "warmup": args.warmup,
+        "warmup_extra_steps": getattr(timed_steps, "extra_warmup", 0),  # untimed, to reach --warmup-seconds
         "ms_per_step": ms_per_step,
         "p50_query_ms": float(np.median(step_ms)),
         "p50_c_abi_ms": float(np.median(abi_ms)),
@@ -487,6 +499,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--warmup-seconds", type=float, default=0.3,
+                    help="keep warming up (untimed) until the warm-ups have run this long (clock ramp-up)")
     ap.add_argument("--workload", default="config2", choices=("config2", "config4", "lds"))
     ap.add_argument("--no-config4", action="store_true", help="config2 line without the embedded config-4 object")
     ap.add_argument("--no-lds", action="store_true", help="config2 line without the embedded LDS group-by object")
@@ -527,12 +541,12 @@ def main():
     if args.workload == "config2" and not args.no_config4:
         c4 = measure(job, args, "config4")
         keep = ("value", "unit", "ms_per_step", "p50_query_ms", "p50_c_abi_ms", "step_ms_detail", "steps", "warmup",
-                "dtype", "config", "roofline", "merge_phases_ms", "result", "verify", "plan")
+                "warmup_extra_steps", "dtype", "config", "roofline", "merge_phases_ms", "result", "verify", "plan")
         out["config4"] = {k: c4[k] for k in keep if k in c4}
     if args.workload == "config2" and not args.no_lds:
         lds = measure(job, args, "lds")
-        keep = ("value", "unit", "ms_per_step", "p50_query_ms", "step_ms_detail", "steps", "dtype", "config",
-                "roofline", "result", "verify", "plan")
+        keep = ("value", "unit", "ms_per_step", "p50_query_ms", "step_ms_detail", "steps", "warmup_extra_steps", "dtype",
+                "config", "roofline", "result", "verify", "plan")
         out["lds_group_by"] = {k: lds[k] for k in keep if k in lds}
     cpu_ok = rank == 0 and world == 1 and job.n_gpus == 1 and not args.no_cpu_baseline
     if cpu_ok:

@@ -265,12 +265,11 @@ class Job:
         q = self.ex.prepare(query_text)  # compiled + marshalled once; every step still prunes, plans and runs
         if not group_by:
             return lambda: self.ex.process_query(q, self.segs)
-        if self.path == "engine":
-            # what the server hands the broker: the group-by trimmed on the device (CombineGroupByOperator's
-            # AggregationGroupByTrimmingService, TOP 10 -> 5,000 groups per function) serialized as DataTable bytes,
-            # handed on as a view of the native buffer (as a transport would send it; no Python-side copy)
-            return lambda: self.ex.process_query_datatable(q, self.segs, trim=True, zero_copy=True)
-        return lambda: self.ex.process_query(q, self.segs, as_result=True)
+        # what the server hands the broker: the group-by trimmed on the device (CombineGroupByOperator's
+        # AggregationGroupByTrimmingService, TOP 10 -> 5,000 groups per function; on the multi-GPU server each rank
+        # trims its own key range before the gather to rank 0) serialized as DataTable bytes, handed on as a view of
+        # the native buffer (as a transport would send it; no Python-side copy)
+        return lambda: self.ex.process_query_datatable(q, self.segs, trim=True, zero_copy=True)
 
     def set_config(self, cfg):
         for e in self.engines:
@@ -448,9 +447,9 @@ def measure(job, args, workload):
         out["plan"] = {"instance": inst, "name": "ring" if inst == 90000 else
                        "counted" if inst // 10000 in (3, 6) else "lds" if inst // 10000 == 1 else "other"}
     if gb:
-        if job.path == "engine":  # the timed step returned DataTable bytes; the full result once for the check
-            out["datatable_bytes"] = len(res)
-            res, _ = job.ex.group_by_result(job.ex.prepare(text), job.segs)
+        # the timed step returned DataTable bytes (rank 0's); the full result once for the check
+        out["datatable_bytes"] = len(res)
+        res, _ = job.ex.group_by_result(job.ex.prepare(text), job.segs)
         n_groups = res.num_groups()
         counts, sums = res.function_values(1 if c4 else 2)  # AVG(d8): per-group counts and sums
         chk, _ = job.ex.process_query(job.ex.prepare("SELECT COUNT(*), SUM(d8) FROM fact WHERE d2 < 800"), job.segs)

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define PINOT_GPU_ABI_VERSION 13
+#define PINOT_GPU_ABI_VERSION 14
 
 /* ------------------------------------------------------------------ status */
 typedef enum {
@@ -403,8 +403,8 @@ pinot_status pinot_datatable_aggregation(const pinot_query *query, const pinot_a
                                          uint8_t *buf, uint64_t buf_len, uint64_t *out_len);
 /* Group-by result (getAggregationGroupByResultDataTable :272-292): one row per function, its map restricted to
  * fn_groups[fn] (fn_num_groups[fn] group indexes, e.g. pinot_groupby_trim's output) when fn_groups and
- * fn_groups[fn] are non-NULL. The bytes are owned by the result (*data valid until the next call on it or
- * pinot_groupby_free). */
+ * fn_groups[fn] are non-NULL. The bytes are owned by the result: each call's *data stays valid until
+ * pinot_groupby_free (a later call on the same result writes a new buffer). */
 pinot_status pinot_datatable_group_by(const pinot_query *query, const pinot_groupby_result *result,
                                       const int64_t *const *fn_groups, const int64_t *fn_num_groups,
                                       const pinot_exec_stats *stats, const pinot_datatable_server *server,
@@ -501,6 +501,17 @@ pinot_status pinot_gpu_server_aggregate(pinot_server *server, const pinot_segmen
                                         const pinot_query *query, pinot_agg_result *out, pinot_exec_stats *stats);
 pinot_status pinot_gpu_server_group_by(pinot_server *server, const pinot_segment_ref *segments, int32_t num_segments,
                                        const pinot_query *query, pinot_groupby_result **out, pinot_exec_stats *stats);
+/* (ABI >= 14) The server's trimmed answer, as pinot_gpu_group_by_top is the engine's: CombineGroupByOperator's
+ * AggregationGroupByTrimmingService (CombineGroupByOperator.java:184-187, AggregationGroupByTrimmingService.java:71-116)
+ * across the GPUs. After the reduce-scatter each rank owns a disjoint key range; the ranks all-gather their ranges'
+ * group counts, and when the merged map exceeds 4 x trimSize (trimSize = max(5 * top_n, 5000)) each rank keeps only its
+ * range's trimSize best groups per function before the gather to rank 0, which picks each function's trimSize best
+ * among them (the merged map's best, the ranges being disjoint). The result is device-trimmed (pinot_groupby_trim
+ * returns each function's list; top_n must match). With server.gather=0 and several ranks, or AvgMV functions, the
+ * result is returned untrimmed. */
+pinot_status pinot_gpu_server_group_by_top(pinot_server *server, const pinot_segment_ref *segments,
+                                           int32_t num_segments, const pinot_query *query, int32_t top_n,
+                                           pinot_groupby_result **out, pinot_exec_stats *stats);
 /* Host wall time (ms) of the phases of the server's last query as its first engine's rank ran it (n <= 8 values):
  *   [0] local work (aggregation: prune + plan + run; group-by: prune + dictionaries)  [1] all-gather of the ranks'
  *   headers (aggregation: of their results) + the global key space  [2] group-by partials on the device

@@ -150,6 +150,8 @@ void parse_config(Engine &e, const char *cfg) {
     else if (k == "group.bucket") e.group_bucket = v == "1" || v == "true";
     else if (k == "group.ring") e.group_ring = v == "1" || v == "true";
     else if (k == "group.ring_qfilter") e.group_ring_qfilter = v == "1" || v == "true";
+    else if (k == "group.ring_hll") e.group_ring_hll = v == "1" || v == "true";
+    else if (k == "group.ring_rec6") e.group_ring_rec6 = v == "1" || v == "true";
     else if (k == "raw.device") e.raw_device = v == "1" || v == "true";
     else if (k == "group.aligned") e.group_aligned = v == "1" || v == "true";
     else if (k == "group.lds_block") {
@@ -170,6 +172,7 @@ void parse_config(Engine &e, const char *cfg) {
       require(e.group_split >= -1 && e.group_split <= 8, PINOT_ERR_BAD_ARG, "group.split: -1 (auto) .. 8");
     }
     else if (k == "debug.host_phases") e.host_phases = v == "1" || v == "true";
+    else if (k == "host.spin") set_host_spin(std::stoi(v));
     else if (k == "exec.nt") e.use_nt = v == "1" || v == "true";
     else if (k == "exec.pipe") e.use_pipe = v == "1" || v == "true";
     else if (k == "stats.exact") e.stats_exact = v == "1" || v == "true";
@@ -591,9 +594,9 @@ pinot_status pinot_datatable_group_by(const pinot_query *query, const pinot_grou
     require(query->num_aggregations == (int32_t)result->functions.size(), PINOT_ERR_BAD_ARG,
             "query and result disagree on the aggregations");
     require(!fn_groups || fn_num_groups, PINOT_ERR_BAD_ARG, "fn_groups without fn_num_groups");
-    result->datatable = group_by_datatable(*query, *result, fn_groups, fn_num_groups, *stats, server);
-    *data = result->datatable.data();
-    *len = result->datatable.size();
+    result->datatables.push_back(group_by_datatable(*query, *result, fn_groups, fn_num_groups, *stats, server));
+    *data = result->datatables.back().data();
+    *len = result->datatables.back().size();
   });
 }
 
@@ -794,19 +797,32 @@ pinot_status pinot_gpu_server_aggregate(pinot_server *server, const pinot_segmen
   });
 }
 
-pinot_status pinot_gpu_server_group_by(pinot_server *server, const pinot_segment_ref *segments, int32_t num_segments,
-                                       const pinot_query *query, pinot_groupby_result **out, pinot_exec_stats *stats) {
+static pinot_status server_group_by_call(pinot_server *server, const pinot_segment_ref *segments, int32_t num_segments,
+                                         const pinot_query *query, int32_t top_n, pinot_groupby_result **out,
+                                         pinot_exec_stats *stats) {
   return guard([&] {
     require(server && server->impl && out, PINOT_ERR_BAD_ARG, "null argument");
     check_query(query);
     require(query->num_group_by >= 1, PINOT_ERR_BAD_ARG, "aggregation-only query passed to pinot_gpu_server_group_by");
+    require(top_n >= 0, PINOT_ERR_BAD_ARG, "top_n must be >= 0");
     const auto t0 = std::chrono::steady_clock::now();
-    auto r = server_group_by(*server->impl, server_refs(segments, num_segments), *query, stats);
+    auto r = server_group_by(*server->impl, server_refs(segments, num_segments), *query, stats, top_n);
     if (stats) stats->host_ms = elapsed_ms(t0);
     auto *res = new pinot_groupby_result();
     static_cast<GroupByResult &>(*res) = std::move(*r);
     *out = res;
   });
+}
+
+pinot_status pinot_gpu_server_group_by(pinot_server *server, const pinot_segment_ref *segments, int32_t num_segments,
+                                       const pinot_query *query, pinot_groupby_result **out, pinot_exec_stats *stats) {
+  return server_group_by_call(server, segments, num_segments, query, 0, out, stats);
+}
+
+pinot_status pinot_gpu_server_group_by_top(pinot_server *server, const pinot_segment_ref *segments, int32_t num_segments,
+                                           const pinot_query *query, int32_t top_n, pinot_groupby_result **out,
+                                           pinot_exec_stats *stats) {
+  return server_group_by_call(server, segments, num_segments, query, top_n, out, stats);
 }
 
 pinot_status pinot_gpu_server_prune_segments(pinot_server *server, const pinot_segment_ref *segments,
@@ -857,7 +873,11 @@ pinot_status pinot_gpu_engine_stat(pinot_engine *engine, const char *name, int64
     if (n == "group.ring_queries") *value = engine->ring_queries;
     else if (n == "group.ring_fallbacks") *value = engine->ring_fallbacks;
     else if (n == "group.ring_qfilter_queries") *value = engine->ring_qfilter_queries;
+    else if (n == "group.ring_rec_bytes") *value = engine->ring_last_rec_bytes;
+    else if (n == "group.ring_hll_slot") *value = engine->ring_last_hll_slot;
+    else if (n == "group.ring_last_status") *value = engine->ring_last_status;
     else if (n == "raw.device_columns") *value = engine->raw_device_columns;
+    else if (n == "raw.host_fallbacks") *value = engine->raw_host_fallbacks;
     else if (n == "group.last_instance") *value = engine->last_group_instance;
     else if (n == "exec.last_pre_segments") *value = engine->last_pre_segments;
     else require(false, PINOT_ERR_BAD_ARG, "unknown engine stat");

@@ -48,6 +48,7 @@ struct ColumnData {
   std::vector<std::string> dict_str;   // STRING values (unpadded)
   std::vector<int32_t> sorted_start, sorted_end;  // sorted columns
   std::vector<int32_t> inv_dir;        // per dictId [dir[i], dir[i+1]) into containers
+  std::vector<uint16_t> inv_keys;      // per container its roaring key (the fused plan's per-key container lists)
   std::vector<uint64_t> inv_bytes;     // serialized roaring bytes per dictId (cost model)
   // INT/LONG dictionary that is an arithmetic progression value(id) = affine_base + affine_step * id:
   // SUM/AVG then need Σ dictId only (no dictionary gather)
@@ -270,11 +271,17 @@ struct Engine {
                               // 0: the counted plan (COUNT -> scan -> EMIT2 -> k_partition_reduce)
   bool raw_device = true;     // raw.device: raw numeric columns transcoded on the device at registration (transcode.h)
   int64_t raw_device_columns = 0;  // columns the device transcoded
+  int64_t raw_host_fallbacks = 0;  // raw numeric columns transcoded on the host for want of free HBM
+  bool group_ring_hll = true;      // group.ring_hll: the ring scatter computes HLL (register, rank) fields (affine columns)
+  bool group_ring_rec6 = true;     // group.ring_rec6: 6-byte ring records when the fields fit 48 bits
   bool group_ring_qfilter = true;  // group.ring_qfilter: the ring kernel evaluates simple filters itself (else GB_FILTER)
   int32_t trim_top_n = 0;      // per call (pinot_gpu_group_by_top): trim the group-by on the device for this TOP n
   int64_t ring_queries = 0;    // group-bys launched on the ring plan
   int64_t last_group_instance = 0;  // the last fused group-by's main kernel instance (group.last_instance)
   int64_t last_pre_segments = 0;  // segments of the last fused query whose filter needed a `pre` bitset (launch sequence)
+  int64_t ring_last_rec_bytes = 0;  // the last ring query's record bytes (6 / 8) and its scatter-side HLL field (0 / 1)
+  int64_t ring_last_hll_slot = 0;
+  int64_t ring_last_status = 0;   // the status bits that sent the last fallen-back ring query to the counted plan
   int64_t ring_qfilter_queries = 0;  // ... of them with the filter evaluated inside k_group_ring (no GB_FILTER pass)
   int64_t ring_fallbacks = 0;  // ring-plan queries re-answered on the counted plan (a region overflowed: skewed keys)
   int num_cus = 256;          // multiProcessorCount of the device
@@ -436,10 +443,15 @@ struct GroupByResult {
   // device-trimmed results (pinot_gpu_group_by_top): per HLL function its groups' HyperLogLog.getBytes, [n][180] B
   // (empty: not prepared; the DataTable writer then packs the registers itself)
   std::vector<HostVecNoInit<uint8_t>> hll_bytes;
-  mutable std::vector<uint8_t> datatable;  // pinot_datatable_group_by's bytes
+  // pinot_datatable_group_by's bytes, one buffer per call: every pointer handed out stays valid until the result is
+  // freed (a caller may hold a zero-copy view of an earlier call's bytes)
+  mutable std::deque<std::vector<uint8_t>> datatables;
 };
 // all groups' u8 HLL registers of function fn ([groups][256]) into host memory, from the device parts or the host copy
 void group_by_hll_registers(const GroupByResult &r, int fn, uint8_t *registers, bool pinned_dst = false);
+// Host task pool (executor.cpp): pause instructions its threads spin after a job before sleeping (engine key host.spin).
+void set_host_spin(int pauses);
+
 // DataTable bytes (datatable.cpp)
 std::vector<uint8_t> aggregation_datatable(const pinot_query &q, const pinot_agg_result *r, const pinot_exec_stats &s,
                                            const pinot_datatable_server *srv);
@@ -514,8 +526,9 @@ int server_num_engines(const ServerImpl &s);
 Engine *server_engine(ServerImpl &s, int i);
 void server_aggregate(ServerImpl &s, const std::vector<SegmentRef> &refs, const pinot_query &q, pinot_agg_result *out,
                       pinot_exec_stats *stats);
+// top_n > 0: the server's trimmed answer (pinot_gpu_server_group_by_top)
 std::unique_ptr<GroupByResult> server_group_by(ServerImpl &s, const std::vector<SegmentRef> &refs, const pinot_query &q,
-                                               pinot_exec_stats *stats);
+                                               pinot_exec_stats *stats, int32_t top_n = 0);
 
 // the multi-device partial step of one engine (executor.cpp): dense partials over [0, G) of the given key space
 // into counts / accs (allow_admission: per-segment num.groups.limit admission inside the partial, when the caller
@@ -554,6 +567,18 @@ void exec_group_by_mv_partial(Engine &e, const std::vector<SegmentData *> &segs,
 // of the non-empty keys (one sync for their count) and the group outputs on the device
 DenseOut slice_outputs(Engine &e, const pinot_query &q, const std::vector<int> &acc_kind, unsigned long long *counts,
                        const std::vector<void *> &accs, int64_t G, int64_t key_base);
+// slice_outputs in two halves (a server's trimmed answer all-gathers the ranges' group counts between them): the
+// range's ordered non-empty keys (device) and their count, then the outputs of those keys — top_n > 0: of the range's
+// trimSize best groups per function only (AggregationGroupByTrimmingService, every group when the range holds no
+// more), with each kept group's mask of the functions that keep it in `flags`
+unsigned long long slice_compact(Engine &e, const unsigned long long *counts, int64_t G, long long *&keys_dev);
+DenseOut slice_outputs_keys(Engine &e, const pinot_query &q, const std::vector<int> &acc_kind, unsigned long long *counts,
+                            const std::vector<void *> &accs, int64_t G, int64_t key_base, const long long *keys_dev,
+                            unsigned long long n, int32_t top_n, std::vector<uint32_t> &flags);
+// The server trim over the ranges' candidates (flags: per gathered group, the functions whose range trim kept it):
+// each function keeps its trimSize best candidates — the merged map's trimSize best, as every group's range kept the
+// range's best — and the result becomes a device-trimmed one (fn_kept, trimmed_top_n, merged_groups).
+void server_trim_select(GroupByResult &r, int32_t top_n, const std::vector<uint32_t> &flags, int64_t merged_groups);
 // the device arrays of n gathered groups, in e's gather buffers, laid out as slice_outputs lays them out
 DenseOut slice_alloc(Engine &e, const pinot_query &q, const std::vector<int> &acc_kind, unsigned long long n);
 // the gatherable arrays of a DenseOut in a fixed order: (device pointer, bytes per group)

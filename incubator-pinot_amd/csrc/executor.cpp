@@ -78,9 +78,15 @@ struct FilterStep {
   int mode = CM_WRITE;
   int dst = 0, src = 0;
   int join = JOIN_NEW;  // fused leaves: how the leaf joins the filter program (FusedJoin)
+  // ROARING with more than kMaxFusedRoaringIds dictIds: the ids' containers listed per roaring key (arena: the key
+  // directory [keys + 1] at key_off, the container indices at list_off) so the fused kernels OR a chunk's containers
+  // without a search per id; 0 keys = not built (such a leaf is expanded to the `pre` bitset)
+  int keys = 0;
+  size_t key_off = 0, list_off = 0;
 };
 
-constexpr int kMaxFusedRoaringIds = 256;  // bitmap leaves with more dictIds are expanded to a `pre` bitset
+constexpr int kMaxFusedRoaringIds = 256;      // bitmap leaves with more dictIds need their per-key container list
+constexpr int64_t kMaxFusedRoaringList = 1 << 18;  // ... of at most this many containers (arena bytes), else `pre`
 
 struct SegPlan {
   SegmentData *seg = nullptr;
@@ -122,12 +128,13 @@ class Compiler {
   // at most kMaxFusedRoaringIds dictIds) — or an AND / OR of such leaves (OrBlockDocIdSet.java:78-120).
   // Deeper subtrees, wider scans (> max_fused_bits: the group kernel's 16 wave stages are small) and long
   // bitmap lists are built into slot 0 = the kernel's `pre` bitset by the launch sequence.
-  void run_fused(const FilterTreeInput *tree, int max_fused_bits = 32) {
+  void run_fused(const FilterTreeInput *tree, int max_fused_bits = 32, int max_stack = kMaxFusedStack) {
     FilterNode root = plan_filter(seg_, tree);
     if (root.type == FilterNode::EMPTY) { sp_.empty = true; return; }
     if (root.type == FilterNode::MATCH_ALL) { sp_.match_all = true; return; }
     next_slot_ = 1;
     max_fused_bits_ = max_fused_bits;
+    max_stack_ = max_stack;
     std::vector<const FilterNode *> conj;
     if (root.type == FilterNode::AND) {
       for (const auto &c : root.children) conj.push_back(&c);
@@ -164,7 +171,50 @@ class Compiler {
   bool fusable(const FilterStep &st) const {
     if (st.kind == FilterStep::SCAN) return seg_.cols[st.col]->bits <= max_fused_bits_;
     if (st.kind == FilterStep::RANGES) return true;
-    return st.kind == FilterStep::ROARING && st.n <= kMaxFusedRoaringIds;
+    return st.kind == FilterStep::ROARING && (st.n <= kMaxFusedRoaringIds || st.keys > 0);
+  }
+  // The registers a term's postfix program holds below its running term (gen_term): a child combined into a running
+  // term of another operator is pushed. first_need: as a node's first child (it starts the running term); join_need:
+  // as a later child joining with operator op.
+  static int first_need(const FilterNode &n) {
+    if (n.type != FilterNode::AND && n.type != FilterNode::OR) return 0;
+    const int op = n.type == FilterNode::OR ? JOIN_OR : JOIN_AND;
+    int need = 0, best = -1;
+    size_t first = 0;
+    for (size_t i = 0; i < n.children.size(); i++) {  // the costliest joiner goes first (it then costs first_need)
+      const int j = join_need(n.children[i], op);
+      if (j > best) best = j, first = i;
+    }
+    for (size_t i = 0; i < n.children.size(); i++)
+      need = std::max(need, i == first ? first_need(n.children[i]) : join_need(n.children[i], op));
+    return need;
+  }
+  static int join_need(const FilterNode &n, int op) {
+    if (n.type != FilterNode::AND && n.type != FilterNode::OR) return 0;
+    const int nop = n.type == FilterNode::OR ? JOIN_OR : JOIN_AND;
+    if (nop == op) {  // the same operator: its children join the running term directly
+      int need = 0;
+      for (const auto &c : n.children) need = std::max(need, join_need(c, op));
+      return need;
+    }
+    return 1 + first_need(n);
+  }
+  // The tree with every node's costliest joiner first (AND / OR children commute): the deepest subtree starts the
+  // running term instead of being pushed, so a chain of nested terms of any depth needs no register stack and a
+  // bushy tree needs its Strahler number's worth (FilterOperatorUtils.java:74-122 builds either shape).
+  static FilterNode deepest_first(const FilterNode &n) {
+    if (n.type != FilterNode::AND && n.type != FilterNode::OR) return n;
+    FilterNode r = n;
+    const int op = n.type == FilterNode::OR ? JOIN_OR : JOIN_AND;
+    for (auto &c : r.children) c = deepest_first(c);
+    int best = -1;
+    size_t first = 0;
+    for (size_t i = 0; i < r.children.size(); i++) {
+      const int j = join_need(r.children[i], op);
+      if (j > best) best = j, first = i;
+    }
+    if (first) std::rotate(r.children.begin(), r.children.begin() + first, r.children.begin() + first + 1);
+    return r;
   }
   // An AND / OR tree of fusable leaves -> one term of the fused program, in postfix over the kernel's register stack
   // (JOIN_PUSH / FUSED_OP: a child whose operator differs from its parent's is built above the parent's running
@@ -199,11 +249,12 @@ class Compiler {
     }
     return true;
   }
-  bool fuse_term(const FilterNode &n) {
+  bool fuse_term(const FilterNode &n0) {
     const int64_t scans_before = sp_.scan_leaves;
     std::vector<FilterStep> steps;
     int depth = 0, max_depth = 0;
-    if (!gen_term(n, GEN_START, -1, steps, depth, max_depth) || max_depth > kMaxFusedStack) {
+    const FilterNode n = deepest_first(n0);
+    if (!gen_term(n, GEN_START, -1, steps, depth, max_depth) || max_depth > max_stack_) {
       sp_.scan_leaves = scans_before;  // eval() plans these leaves again
       return false;
     }
@@ -285,6 +336,7 @@ class Compiler {
         st.n = (int)ids.size();
         st.negate = excl ? 1 : 0;
         st.off = ar_.add(ids.data(), ids.size() * 4);
+        if (st.n > kMaxFusedRoaringIds) key_list(c, ids, st);
         return st;
       }
     }
@@ -300,6 +352,25 @@ class Compiler {
     }
     scan_leaf(c, ev, st);
     return st;
+  }
+  // The ids' containers bucketed by roaring key (counting sort over the keys): a chunk's containers are then the
+  // key's slice of the list. Skipped (st.keys stays 0) when the list would exceed kMaxFusedRoaringList entries.
+  void key_list(const ColumnData &c, const std::vector<int32_t> &ids, FilterStep &st) {
+    int64_t total = 0;
+    for (int32_t id : ids) total += c.inv_dir[id + 1] - c.inv_dir[id];
+    if (total > kMaxFusedRoaringList) return;
+    const int keys = (int)(((int64_t)seg_.num_docs + 65535) >> 16);
+    std::vector<int32_t> dir(keys + 2, 0), list((size_t)std::max<int64_t>(total, 1));
+    for (int32_t id : ids)
+      for (int32_t j = c.inv_dir[id]; j < c.inv_dir[id + 1]; j++)
+        if (c.inv_keys[j] < keys) dir[c.inv_keys[j] + 2]++;
+    for (int k = 0; k < keys; k++) dir[k + 2] += dir[k + 1];
+    for (int32_t id : ids)
+      for (int32_t j = c.inv_dir[id]; j < c.inv_dir[id + 1]; j++)
+        if (c.inv_keys[j] < keys) list[dir[c.inv_keys[j] + 1]++] = j;
+    st.keys = keys;
+    st.key_off = ar_.add(dir.data(), (size_t)(keys + 1) * 4);
+    st.list_off = ar_.add(list.data(), list.size() * 4);
   }
   void scan_leaf(const ColumnData &c, const Evaluator &ev, FilterStep &st) {
     sp_.scan_leaves++;
@@ -337,6 +408,7 @@ class Compiler {
   }
 
   int max_fused_bits_ = 32;
+  int max_stack_ = kMaxFusedStack;
   Engine &e_;
   SegPlan &sp_;
   Arena &ar_;
@@ -689,6 +761,12 @@ FusedStep fused_leaf_step(const SegmentData &s, const FilterStep &l, const uint8
       st.aux1 = c.inv_dir_dev.get();
       st.table = arena + l.off;
       st.lo = (uint32_t)l.n;
+      if (l.n > kMaxFusedRoaringIds) {  // the per-key container list (key_list)
+        st.ops = 1;
+        st.aux1 = arena + l.key_off;
+        st.table = arena + l.list_off;
+        st.lo = (uint32_t)l.keys;
+      }
       break;
     default:
       st.fwd = c.fwd.get<uint8_t>();
@@ -2290,7 +2368,11 @@ namespace {
 namespace {
 // Persistent host workers for the result fills (spawning threads per call cost ~0.1 ms per call, several calls per
 // query). One job at a time: a second concurrent caller (another engine's thread in the multi-GPU server) runs its
-// tasks on threads of its own instead of waiting.
+// tasks on threads of its own instead of waiting. g_pool_spin: the pause instructions a pool thread spins after a job
+// before it sleeps (engine key host.spin; process-wide, the pool is shared by every engine). Short by default, so an
+// idle server's host cores sleep between queries.
+std::atomic<int> g_pool_spin{2000};
+
 class TaskPool {
  public:
   static TaskPool &get() {
@@ -2312,7 +2394,8 @@ class TaskPool {
     }
     cv_.notify_all();
     work(*job);  // the caller takes tasks too
-    for (int spin = 0; spin < kSpin && job->done.load(std::memory_order_acquire) != n; spin++) pause();
+    const int spin_n = g_pool_spin.load(std::memory_order_relaxed);
+    for (int spin = 0; spin < spin_n && job->done.load(std::memory_order_acquire) != n; spin++) pause();
     std::unique_lock<std::mutex> lk(mu_);
     done_cv_.wait(lk, [&] { return job->done.load() == n; });
     job_.reset();
@@ -2341,14 +2424,14 @@ class TaskPool {
       }
     }
   }
-  // A worker that finished a job spins briefly before sleeping: the host phases issue their parallel passes a few
-  // microseconds apart, and a condition-variable wake costs tens of microseconds per pass.
-  static constexpr int kSpin = 20000;  // ~50-100 us of pause instructions
+  // A worker that finished a job spins briefly before sleeping (host.spin pause instructions): the host phases issue
+  // their parallel passes a few microseconds apart, and a condition-variable wake costs tens of microseconds per pass.
   static void pause() { __builtin_ia32_pause(); }
   void loop() {
     uint64_t seen = 0;
     for (;;) {
-      for (int spin = 0; spin < kSpin && gen_seen_.load(std::memory_order_acquire) == seen; spin++) pause();
+      const int spin_n = g_pool_spin.load(std::memory_order_relaxed);
+      for (int spin = 0; spin < spin_n && gen_seen_.load(std::memory_order_acquire) == seen; spin++) pause();
       std::shared_ptr<Job> j;
       {
         std::unique_lock<std::mutex> lk(mu_);
@@ -2369,6 +2452,12 @@ class TaskPool {
 }  // namespace
 
 size_t host_threads() { return std::min<size_t>(16, TaskPool::get().threads()); }
+
+}  // namespace
+
+void set_host_spin(int pauses) { g_pool_spin.store(std::max(0, pauses), std::memory_order_relaxed); }
+
+namespace {
 
 void parallel_tasks(size_t n, const std::function<void(size_t)> &fn) {
   if (n <= 1) {
@@ -2502,11 +2591,14 @@ GroupPlan plan_group(const std::vector<SegmentData *> &segs, const pinot_query &
 // partitions of K <= 1024 keys number at most kRingMaxPartitions (k_group_ring's LDS rings), read through the
 // lane-owns-quarter decoder (<= 4 columns of <= 20 bits) with records of <= 53 bits.
 constexpr size_t kRingReduceLds = 160 * 1024;
+constexpr int kRingHllFieldBits = 13;  // register (8 bits, log2m = 8) << 5 | rank (<= 25)
 struct RingPlan {
   bool on = false;
   int shift = 0;
   int64_t P = 0;
+  int rec_bytes = 8;                     // 6 when the record fields fit 48 bits (group.ring_rec6)
   std::vector<int> field_shift, lds_off;
+  std::vector<int> hll_form;             // per aggregation: 1 = the HLL whose field the scatter computes (at most one)
   int cnt_off = 0, hist_off = 0, exc_off = 0, lds_bytes = 0;
   uint32_t cap = 0;        // records per region the allocation holds
   int64_t nblk = 0;
@@ -2543,6 +2635,28 @@ RingPlan plan_ring(const Engine &e, const std::vector<SegmentData *> &segs, cons
   const int64_t K = (int64_t)1 << s;
   rp.P = (ks.G + K - 1) / K;
   if (rp.P > kRingMaxPartitions || ring_lds_bytes((int)rp.P) > kRingReduceLds) return rp;
+  // HLL (register, rank) computed by the scatter's flushers (group.ring_hll): a column only HLL aggregations read,
+  // over an affine INT / LONG dictionary (identical on every segment: plan_group's condition) with every value in
+  // [0, 2^32) (the reduce's lo32 test), leaves the block as register << 5 | rank (13 bits) in its field (at least 13
+  // bits wide) instead of its dictId, so the reduce does no hashing
+  rp.hll_form.assign(na, 0);
+  for (int a = 0; a < na && e.group_ring_hll; a++) {
+    if (gx.acc_kind[a] != 4) continue;
+    const std::string c = agg_column(q.aggregations[a]);
+    bool only_hll = true;
+    for (int b = 0; b < na; b++)
+      if (gx.acc_kind[b] != 5 && gx.acc_kind[b] != 4 && agg_column(q.aggregations[b]) == c) only_hll = false;
+    const ColumnData &cd = *segs[0]->column(c);
+    if (!only_hll || !cd.affine || !e.use_affine || (cd.data_type != PINOT_INT && cd.data_type != PINOT_LONG) ||
+        cd.bits > kGroupLwMaxBits)
+      continue;
+    const long long top = cd.affine_base + cd.affine_step * (long long)((1ull << cd.bits) - 1ull);
+    const bool lo32 = cd.affine_base >= 0 && cd.affine_step >= 0 && cd.bits < 32 && top < (1ll << 32);
+    if (lo32) {
+      rp.hll_form[a] = 1;
+      break;  // one such column per query (RingArgs.hll)
+    }
+  }
   // record layout: [s bits local key | one field per distinct aggregated column]
   rp.field_shift.assign(na, 0);
   std::map<std::string, int> col_field;
@@ -2553,11 +2667,12 @@ RingPlan plan_ring(const Engine &e, const std::vector<SegmentData *> &segs, cons
     auto it = col_field.find(c);
     if (it == col_field.end()) {
       it = col_field.emplace(c, bits).first;
-      bits += segs[0]->column(c)->bits;
+      bits += rp.hll_form[a] ? std::max(kRingHllFieldBits, segs[0]->column(c)->bits) : segs[0]->column(c)->bits;
     }
     rp.field_shift[a] = it->second;
   }
   if (bits > 53) return rp;
+  rp.rec_bytes = bits <= 48 && e.group_ring_rec6 ? 6 : 8;
   // regions: every doc of the largest block matching, keys spread evenly (+ slack; beyond it the counted plan answers)
   const int64_t max_docs = (total_chunks + (int64_t)nblk - 1) / (int64_t)nblk * 4096;
   const uint32_t cap = ring_region_records((uint64_t)max_docs, K, ks.G, UINT32_MAX);
@@ -3100,10 +3215,13 @@ std::unique_ptr<GroupByResult> build_dense_result(Engine &e, const DenseGroups &
 // trimSize best groups (getSorter :160-176: MIN ascending, the others descending; AVG by sum / count, HLL by
 // cardinality; ties in ascending raw key order); the result holds the union of the kept groups and each function's
 // list. Returns the union's keys (device) and sets n to its size; `kept` stays empty when nothing is trimmed.
+// min_groups >= 0: trim above that many groups instead of 4 x trimSize (a server rank's pre-trim of its own key range,
+// server.cpp); flags_out: each kept group's bit mask of the functions that keep it.
 const long long *device_trim(Engine &e, const DenseGroups &d, const long long *keys_dev, unsigned long long &n,
-                             int32_t top_n, std::vector<std::vector<int64_t>> &kept) {
+                             int32_t top_n, std::vector<std::vector<int64_t>> &kept, int64_t min_groups = -1,
+                             std::vector<uint32_t> *flags_out = nullptr) {
   const int64_t T = std::max<int64_t>(5 * (int64_t)top_n, 5000);
-  if ((int64_t)n <= 4 * T || d.hashed) return keys_dev;
+  if ((int64_t)n <= (min_groups >= 0 ? min_groups : 4 * T) || d.hashed) return keys_dev;
   const pinot_query &q = *d.q;
   const int na = q.num_aggregations;
   const DenseOut o = dense_outputs(e, d, keys_dev, n, false, false);  // comparable values of every group, no registers
@@ -3139,6 +3257,7 @@ const long long *device_trim(Engine &e, const DenseGroups &d, const long long *k
   for (int i = 0; i < na; i++) kept[i].reserve((size_t)T);
   for (unsigned long long g = 0; g < nu; g++)
     for (uint32_t x = hf[g]; x; x &= x - 1u) kept[__builtin_ctz(x)].push_back((int64_t)g);
+  if (flags_out) flags_out->assign(hf, hf + nu);
   n = nu;
   return ukeys;
 }
@@ -3191,7 +3310,7 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
   std::vector<SegPlan> plans(S);
   for (size_t si = 0; si < S; si++) {
     plans[si].seg = segs[si];
-    Compiler(e, plans[si], ar).run_fused(tree.get(), kGroupMaxFusedLeafBits);
+    Compiler(e, plans[si], ar).run_fused(tree.get(), kGroupMaxFusedLeafBits, kMaxFusedStackGroup);
   }
   e.last_pre_segments = 0;
   for (auto &p : plans) e.last_pre_segments += p.has_pre && !p.empty;
@@ -3462,7 +3581,7 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     uint8_t *pb = e.group_part.get<uint8_t>();
     auto *hist = reinterpret_cast<uint32_t *>(pb);
     ring_status = reinterpret_cast<uint32_t *>(pb + hist_b);
-    e.group_records.reserve((size_t)rp.P * nblk * rp.cap * 8 + 64);
+    e.group_records.reserve((size_t)rp.P * nblk * rp.cap * rp.rec_bytes + 64);
     // the filter: a top-level conjunction of <= kRingMaxQuarterLeaves scan leaves (RANGE / LUT, <= 20 bits) is
     // evaluated by the ring kernel itself on each quarter; any other program runs first as GB_FILTER
     int nf = 0;
@@ -3507,13 +3626,23 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     ra.nblk = (int32_t)nblk;
     ra.cap = rp.cap;
     ra.nf = nf;
-    ra.records = e.group_records.get<unsigned long long>();
+    ra.records = e.group_records.get<uint8_t>();
+    ra.rec_bytes = rp.rec_bytes;
+    for (int i = 0; i < na; i++)
+      if (rp.hll_form[i]) {  // the flushers' HLL field (segment 0's dictionary: identical on every segment)
+        ra.hll = 1;
+        ra.hll_shift = rp.field_shift[i];
+        ra.hll_bits = gaggs[i].bits;
+        ra.hll_base = (uint32_t)gaggs[i].affine_base;
+        ra.hll_step = (uint32_t)gaggs[i].affine_step;
+      }
     ra.hist = hist;
     ra.status = ring_status;
     ra.region = ring_status + 1;
     ra.matched = matched;  // the quarter-form filter counts each segment's matching docs (GB_FILTER does otherwise)
     RingReduceArgs rr{};
     rr.records = ra.records;
+    rr.rec_bytes = rp.rec_bytes;
     rr.hist = hist;
     rr.region = ra.region;
     rr.P = (int32_t)rp.P;
@@ -3531,11 +3660,17 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     for (int i = 0; i < na; i++) {
       rr.aggs[i] = gaggs[i];  // segment 0's dictionary / LUT: identical on every segment (checked by plan_group)
       rr.aggs[i].lds_off = rp.lds_off[i];
+      if (rp.hll_form[i]) {
+        rr.hll_pre |= 1 << i;
+        rr.aggs[i].bits = kRingHllFieldBits;
+      }
     }
     require(a.pf_nc > 0, PINOT_ERR_DEVICE, "ring plan without its column list");
     PINOT_HIP(hipMemsetAsync(ring_status, 0, 256, e.stream));
     e.ring_queries++;
     if (nf >= 0) e.ring_qfilter_queries++;
+    e.ring_last_rec_bytes = rp.rec_bytes;
+    e.ring_last_hll_slot = ra.hll;
     e.last_group_instance = kRingInstanceCode;
     t.timed(1, [&] {
       if (nf < 0) launch_group_query(af, e.stream);
@@ -3644,7 +3779,10 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     if (ring_status) PINOT_HIP(hipMemcpyAsync(rs, ring_status, 16, hipMemcpyDeviceToHost, e.stream));
     PINOT_HIP(hipEventRecord(e.ev_stop, e.stream));
     wait_stream(e);
-    if (rs[0]) return ring_fallback();
+    if (rs[0]) {
+      e.ring_last_status = rs[0];
+      return ring_fallback();
+    }
     float pms = 0;
     PINOT_HIP(hipEventElapsedTime(&pms, e.ev_start, e.ev_stop));
     t.collect();
@@ -3672,7 +3810,10 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
   memcpy(hmatched.data(), small, S * 8);
   if (ring_status) memcpy(rs, small + S * 8, 16);
   if (ks.hashed) memcpy(&verify_err, small + S * 8 + 16, 4);
-  if (rs[0]) return ring_fallback();
+  if (rs[0]) {
+    e.ring_last_status = rs[0];
+    return ring_fallback();
+  }
   if (verify_err) {  // 64-bit fingerprint collision: retry with another seed
     require(attempt < 3, PINOT_ERR_DEVICE, "group-key fingerprint collisions persist");
     return exec_group_by_fused(e, segs, q, ks_in, ga, stats, attempt + 1);
@@ -4665,16 +4806,73 @@ void inter_segment_cap(std::vector<uint32_t> &bm, size_t S, int64_t words, int64
 
 DenseOut slice_outputs(Engine &e, const pinot_query &q, const std::vector<int> &acc_kind, unsigned long long *counts,
                        const std::vector<void *> &accs, int64_t G, int64_t key_base) {
+  long long *keys_dev = nullptr;
+  const unsigned long long n = slice_compact(e, counts, G, keys_dev);
+  std::vector<uint32_t> flags;
+  return slice_outputs_keys(e, q, acc_kind, counts, accs, G, key_base, keys_dev, n, 0, flags);
+}
+
+unsigned long long slice_compact(Engine &e, const unsigned long long *counts, int64_t G, long long *&keys_dev) {
+  keys_dev = nullptr;
+  return G > 0 ? compact_dense(e, counts, G, keys_dev, {}) : 0;
+}
+
+DenseOut slice_outputs_keys(Engine &e, const pinot_query &q, const std::vector<int> &acc_kind, unsigned long long *counts,
+                            const std::vector<void *> &accs, int64_t G, int64_t key_base, const long long *keys_dev,
+                            unsigned long long n, int32_t top_n, std::vector<uint32_t> &flags) {
   KeySpace ks;
   ks.G = G;
   GroupAccs ga;
   ga.acc_kind = acc_kind;
   ga.acc_bytes_per_key.assign(acc_kind.size(), 0);
   const std::vector<int> alias(acc_kind.size(), -1);
-  long long *keys_dev = nullptr;
-  const unsigned long long n = G > 0 ? compact_dense(e, counts, G, keys_dev, {}) : 0;
   DenseGroups dg{&q, &ks, &ga, &ga, &alias, counts, accs, key_base, nullptr};
+  flags.clear();
+  if (top_n > 0 && n > 0) {  // this range's trimSize best groups per function (every group when it holds no more)
+    const int64_t T = std::max<int64_t>(5 * (int64_t)top_n, 5000);
+    std::vector<std::vector<int64_t>> kept;
+    const long long *ukeys = device_trim(e, dg, keys_dev, n, top_n, kept, T, &flags);
+    if (ukeys != keys_dev) return dense_outputs(e, dg, ukeys, n, true, false);
+    flags.assign((size_t)n, (uint32_t)((1ull << q.num_aggregations) - 1));
+  }
   return dense_outputs(e, dg, keys_dev, n);
+}
+
+void server_trim_select(GroupByResult &r, int32_t top_n, const std::vector<uint32_t> &flags, int64_t merged_groups) {
+  const int64_t n = (int64_t)r.raw_keys.size();
+  require((int64_t)flags.size() == n, PINOT_ERR_DEVICE, "server trim: candidate flags of another size");
+  const int64_t T = std::max<int64_t>(5 * (int64_t)top_n, 5000);
+  const int na = (int)r.functions.size();
+  r.fn_kept.assign(na, {});
+  for (int fn = 0; fn < na; fn++) {
+    std::vector<int64_t> idx;
+    for (int64_t g = 0; g < n; g++)
+      if ((flags[g] >> fn) & 1u) idx.push_back(g);
+    if ((int64_t)idx.size() > T) {  // GroupByResult::trim's order: the function's value, ties by raw key (group order)
+      const int f = sv_function(r.functions[fn]);
+      const HostVec<int64_t> &cnt = r.counts[r.counts_shared ? 0 : fn];
+      auto val = [&](int64_t g) -> double {
+        switch (f) {
+          case PINOT_AGG_COUNT: return (double)cnt[g];
+          case PINOT_AGG_AVG: return cnt[g] ? r.values[fn][g] / (double)cnt[g] : -INFINITY;
+          case PINOT_AGG_DISTINCTCOUNTHLL: return (double)r.hll_card[fn][g];
+          default: return r.values[fn][g];
+        }
+      };
+      const bool asc = f == PINOT_AGG_MIN;
+      auto better = [&](int64_t a, int64_t b) {
+        const double va = val(a), vb = val(b);
+        if (va != vb) return asc ? va < vb : va > vb;
+        return a < b;
+      };
+      std::nth_element(idx.begin(), idx.begin() + T, idx.end(), better);
+      idx.resize(T);
+      std::sort(idx.begin(), idx.end());
+    }
+    r.fn_kept[fn] = std::move(idx);
+  }
+  r.trimmed_top_n = top_n;
+  r.merged_groups = merged_groups;
 }
 
 DenseOut slice_alloc(Engine &e, const pinot_query &q, const std::vector<int> &acc_kind, unsigned long long n) {

@@ -234,7 +234,7 @@ __device__ __forceinline__ unsigned long long eval_chunk(const FusedStep *__rest
                                                          int n_folds, uint64_t mask, FoldAcc &A, HllRegs *hll,
                                                          int64_t w, int64_t nwords, int32_t num_docs, int lane,
                                                          Src &&src) {
-  mask = eval_filter<G>(steps, n_leaves, mask, w, nwords, num_docs, lane, src);
+  mask = eval_filter<G, 32, kMaxFusedStack>(steps, n_leaves, mask, w, nwords, num_docs, lane, src);
   const unsigned long long cnt = __popcll(mask);
   for (int i = 0; i < n_folds; i++) {
     if (!__any(mask != 0)) break;

@@ -195,16 +195,55 @@ __device__ __forceinline__ uint64_t ranges_word(const int32_t *__restrict__ r, i
 
 __device__ __forceinline__ uint32_t ld16(const uint8_t *p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8); }
 
+// The 64 docs [first, first + 64) (low 16 bits) of one roaring container, as a word.
+__device__ __forceinline__ uint64_t container_word(const uint8_t *payload, const RoaringContainer &c, uint32_t first) {
+  const uint8_t *p = payload + c.payload_offset;
+  uint64_t x = 0;
+  if (c.type == 1) {  // bitmap container: 1024 LE u64 words
+    const uint8_t *q = p + (first >> 3);
+    x = (uint64_t)ld16(q) | ((uint64_t)ld16(q + 2) << 16) | ((uint64_t)ld16(q + 4) << 32) | ((uint64_t)ld16(q + 6) << 48);
+  } else if (c.type == 0) {  // sorted u16 array
+    int a = 0, b = (int)c.cardinality;
+    while (a < b) {
+      const int m = (a + b) >> 1;
+      if (ld16(p + 2 * m) < first) a = m + 1;
+      else b = m;
+    }
+    for (; a < (int)c.cardinality; a++) {
+      const uint32_t v = ld16(p + 2 * a);
+      if (v >= first + 64) break;
+      x |= 1ull << (v - first);
+    }
+  } else {  // run container: (start, length - 1) pairs
+    for (uint32_t k = 0; k < c.cardinality; k++) {
+      const uint32_t s0 = ld16(p + 4 * k), e0 = s0 + ld16(p + 4 * k + 2);
+      if (s0 >= first + 64) break;
+      if (e0 < first) continue;
+      x |= bits_between((int)(max(s0, first) - first), (int)(min(e0, first + 63) - first));
+    }
+  }
+  return x;
+}
+
 __device__ __forceinline__ uint64_t roaring_word(const FusedStep &st, int64_t w) {
   const uint8_t *payload = st.fwd;
   const RoaringContainer *conts = static_cast<const RoaringContainer *>(st.aux0);
-  const int32_t *dir = static_cast<const int32_t *>(st.aux1);
-  const int32_t *ids = static_cast<const int32_t *>(st.table);
   // a chunk's 64 words lie in one 1024-word roaring key: the key, each id's container search and the container header
   // are wave-uniform (scalar loads); only the word inside the container is per lane
   const uint32_t key = (uint32_t)__builtin_amdgcn_readfirstlane((int)(w >> 10));
   const uint32_t first = (uint32_t)(w & 1023) * 64;    // the word's first low-16 doc
   uint64_t x = 0;
+  if (st.ops) {  // many dictIds: their containers listed per key (aux1 = key directory, table = container indices)
+    const int32_t *kdir = static_cast<const int32_t *>(st.aux1);
+    const int32_t *list = static_cast<const int32_t *>(st.table);
+    if (key < st.lo) {
+      const int l1 = load_const(kdir + key + 1);
+      for (int l = load_const(kdir + key); l < l1; l++) x |= container_word(payload, load_const(conts + load_const(list + l)), first);
+    }
+    return st.negate ? ~x : x;
+  }
+  const int32_t *dir = static_cast<const int32_t *>(st.aux1);
+  const int32_t *ids = static_cast<const int32_t *>(st.table);
   for (int i = 0; i < (int)st.lo; i++) {
     const int id = load_const(ids + i);
     int l = load_const(dir + id), r = load_const(dir + id + 1);
@@ -217,31 +256,7 @@ __device__ __forceinline__ uint64_t roaring_word(const FusedStep &st, int64_t w)
     if (l >= end) continue;
     const RoaringContainer c = load_const(conts + l);
     if (c.key != key) continue;
-    const uint8_t *p = payload + c.payload_offset;
-    if (c.type == 1) {  // bitmap container: 1024 LE u64 words
-      const uint8_t *q = p + (first >> 3);
-      x |= (uint64_t)ld16(q) | ((uint64_t)ld16(q + 2) << 16) | ((uint64_t)ld16(q + 4) << 32) |
-           ((uint64_t)ld16(q + 6) << 48);
-    } else if (c.type == 0) {  // sorted u16 array
-      int a = 0, b = (int)c.cardinality;
-      while (a < b) {
-        const int m = (a + b) >> 1;
-        if (ld16(p + 2 * m) < first) a = m + 1;
-        else b = m;
-      }
-      for (; a < (int)c.cardinality; a++) {
-        const uint32_t v = ld16(p + 2 * a);
-        if (v >= first + 64) break;
-        x |= 1ull << (v - first);
-      }
-    } else {  // run container: (start, length - 1) pairs
-      for (uint32_t k = 0; k < c.cardinality; k++) {
-        const uint32_t s0 = ld16(p + 4 * k), e0 = s0 + ld16(p + 4 * k + 2);
-        if (s0 >= first + 64) break;
-        if (e0 < first) continue;
-        x |= bits_between((int)(max(s0, first) - first), (int)(min(e0, first + 63) - first));
-      }
-    }
+    x |= container_word(payload, c, first);
   }
   return st.negate ? ~x : x;
 }
@@ -257,12 +272,13 @@ __device__ __forceinline__ uint64_t leaf_word(const FusedStep &st, int i, int64_
 }
 
 // The filter program of a chunk: terms AND-ed into `mask` (early exit once the wave's mask is empty). A term is an
-// AND / OR tree in postfix over a register stack (s0..s2 below the running term): nested subtrees of the filter
-// (FilterOperatorUtils.java:74-122 builds them with AndFilterOperator / OrFilterOperator) stay in registers.
-template <bool G, int MAXB = 32, typename Src>
+// AND / OR tree in postfix over a register stack (STACK entries s0.. below the running term; the planner starts each node's term
+// with its deepest child, so only bushy trees push): nested subtrees of the filter (FilterOperatorUtils.java:74-122
+// builds them with AndFilterOperator / OrFilterOperator) stay in registers.
+template <bool G, int MAXB = 32, int STACK = kMaxFusedStackGroup, typename Src>
 __device__ __forceinline__ uint64_t eval_filter(const FusedStep *__restrict__ steps, int n_leaves, uint64_t mask,
                                                 int64_t w, int64_t nwords, int32_t num_docs, int lane, Src &&src) {
-  uint64_t term = ~0ull, s0 = 0, s1 = 0, s2 = 0;
+  uint64_t term = ~0ull, s0 = 0, s1 = 0, s2 = 0, s3 = 0;
   bool pending = false;
   for (int i = 0; i < n_leaves; i++) {
     const FusedStep st = load_const(steps + i);
@@ -270,6 +286,7 @@ __device__ __forceinline__ uint64_t eval_filter(const FusedStep *__restrict__ st
       term = st.join == JOIN_OR ? (s0 | term) : (s0 & term);
       s0 = s1;
       s1 = s2;
+      if constexpr (STACK >= 4) s2 = s3;
       continue;
     }
     if (st.join == JOIN_NEW) {
@@ -283,6 +300,7 @@ __device__ __forceinline__ uint64_t eval_filter(const FusedStep *__restrict__ st
     else if (st.join == JOIN_OR) term |= x;
     else if (st.join == JOIN_AND) term &= x;
     else {  // JOIN_PUSH
+      if constexpr (STACK >= 4) s3 = s2;
       s2 = s1;
       s1 = s0;
       s0 = term;

@@ -22,6 +22,8 @@
 // keys) sets a status bit and the host answers the query on the counted plan instead (executor.cpp).
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "fused_common.h"
 #include "group_lq.h"
 #include "group_ring.h"
@@ -42,17 +44,9 @@ using namespace dev;
 
 constexpr int kRingBlock = 768;                             // one block of 12 waves per CU (the buckets take the LDS)
 constexpr int kRingWaves = kRingBlock / 64;
-#ifdef RING_EXP_FLUSH_WAVES
-constexpr int kRingFlushWaves = RING_EXP_FLUSH_WAVES;        // experiment: another decoder / flusher split
-#else
 constexpr int kRingFlushWaves = 4;                           // waves 8..11: the flush phases (one per SIMD)
-#endif
 constexpr int kRingDecWaves = kRingWaves - kRingFlushWaves;  // waves 0..7: filter, decode, insert (two per SIMD)
-#ifdef RING_EXP_ONEROUND
-constexpr int kRingRoundRecs = 16;                           // experiment: one insert phase per pass
-#else
 constexpr int kRingRoundRecs = 8;                            // records per decoder lane between two flush phases
-#endif
 constexpr int kRingBucket = 16;                              // entries per partition bucket (two 64-B halves)
 // Bucket stride in entries: 144 B = 36 dwords, so the flushers' 16-B reads of consecutive partitions start on distinct
 // banks (a 128-B stride puts every lane of a ds_read_b128 group on the same four banks) and an insert's 8-B write lands
@@ -62,20 +56,55 @@ constexpr int kRecPShift = 53;                               // bucket entries c
 constexpr int kRingBackBits = 12;                            // hist: front count (20 bits) | back count << 20
 static_assert(16 % kRingRoundRecs == 0, "whole rounds per pass");
 
-// RING_EXP_TIMING (experiment builds only): per-wave shader-clock totals of each phase, printed by a few blocks.
-#ifdef RING_EXP_TIMING
-// the shader clock, ordered against the memory operations around it (its wait also drains pending LDS operations)
-__device__ __forceinline__ uint64_t rt_cycles() {
-  uint64_t x;
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(x) : : "memory");
-  return x;
+// stream-lib MurmurHash.hashLong + HyperLogLog (register << 8 | rank): hll.cpp's murmur_hash_long / hll_register_rank
+__device__ __forceinline__ uint32_t murmur_hash_long_g(long long data) {
+  constexpr uint32_t kM = 0x5bd1e995u;
+  const unsigned long long d = (unsigned long long)data;
+  uint32_t h = 0;
+  uint32_t k = (uint32_t)d * kM;
+  k ^= k >> 24;
+  h ^= k * kM;
+  k = (uint32_t)(d >> 32) * kM;
+  k ^= k >> 24;
+  h *= kM;
+  h ^= k * kM;
+  h ^= h >> 13;
+  h *= kM;
+  h ^= h >> 15;
+  return h;
 }
-#define RT_MARK(v) const uint64_t v = rt_cycles()
-#define RT_ADD(acc, from) acc += rt_cycles() - (from)
-#else
-#define RT_MARK(v)
-#define RT_ADD(acc, from)
-#endif
+
+// murmur_hash_long_g of a value in [0, 2^32): the high word's block multiplies h by kM once more
+__device__ __forceinline__ uint32_t murmur_hash_lo32_g(uint32_t lo) {
+  constexpr uint32_t kM = 0x5bd1e995u, kMM = kM * kM;
+  uint32_t k = lo * kM;
+  k ^= k >> 24;
+  uint32_t h = k * kMM;
+  h ^= h >> 13;
+  h *= kM;
+  h ^= h >> 15;
+  return h;
+}
+
+__device__ __forceinline__ uint32_t hll_register_rank_g(uint32_t h) {
+  return ((h >> 24) << 8) | (uint32_t)(__builtin_clz((h << 8) | 129u) + 1);
+}
+
+// The record field of an HLL aggregation whose (register, rank) the scatter computes (RingArgs.hll): the value
+// base + step * dictId (< 2^32) of an affine dictionary hashed as stream-lib does, kept as register << 5 | rank (13 bits)
+__device__ __forceinline__ uint32_t hll_field_g(uint32_t id, uint32_t base, uint32_t step) {
+  const uint32_t h = murmur_hash_lo32_g(base + step * id);
+  return ((h >> 24) << 5) | (uint32_t)(__builtin_clz((h << 8) | 129u) + 1);
+}
+
+// A record on its way out of the block (a flush, the final partial flush, a bucket-overflow write): its HLL field's
+// dictId replaced by hll_field_g of it. The flusher waves do this between their barriers, so the hash costs the
+// decoders nothing (they wait at barriers far less than the flushers, round 5).
+__device__ __forceinline__ unsigned long long ring_hll_out(const RingArgs &a, unsigned long long r) {
+  const unsigned long long m = ((1ull << a.hll_bits) - 1ull) << a.hll_shift;
+  const uint32_t id = (uint32_t)((r & m) >> a.hll_shift);
+  return (r & ~m) | ((unsigned long long)hll_field_g(id, a.hll_base, a.hll_step) << a.hll_shift);
+}
 
 struct RingLds {
   unsigned long long *bkt;  // [P][16] bucket entries: record | partition << 53
@@ -95,36 +124,40 @@ __device__ __forceinline__ RingLds ring_lds(uint8_t *lds, int P) {
 
 __device__ __forceinline__ uint32_t rec_part(unsigned long long r) { return (uint32_t)(r >> kRecPShift) & 1023u; }
 
+// Record i of a region array of RB-byte records (RB = 6: the low 48 bits, as three 16-bit stores).
+template <int RB>
+__device__ __forceinline__ void store_rec(uint8_t *base, size_t i, unsigned long long v) {
+  if constexpr (RB == 8) {
+    reinterpret_cast<unsigned long long *>(base)[i] = v;
+  } else {
+    uint16_t *d = reinterpret_cast<uint16_t *>(base + i * 6);
+    d[0] = (uint16_t)v;
+    d[1] = (uint16_t)(v >> 16);
+    d[2] = (uint16_t)(v >> 32);
+  }
+}
+
 // Insert phase: record j of each of the lane's kRingRoundRecs records (J0 ..) claims the next entry of its partition's
 // bucket (one LDS add returns the claim index and the head) and is written at (head + claim) mod 16. No flush runs
 // during an insert phase (block barriers on both sides), so a claim below 16 always finds its entry free; a claim of
 // 16 or more (a bucket that received more than 9 records in one round; rare) goes to the back of its region instead.
-template <int J0>
+template <int RB, bool HLL, int J0>
 __device__ __forceinline__ void ring_insert(const RingArgs &a, const RingLds &L, uint32_t act,
-                                            const unsigned long long (&rec)[16], unsigned long long *region0,
+                                            const unsigned long long (&rec)[16], uint8_t *region0,
                                             uint32_t C) {
   uint32_t old[kRingRoundRecs], p[kRingRoundRecs];
 #pragma unroll
   for (int j = 0; j < kRingRoundRecs; j++) {
     const bool on = (act >> (J0 + j)) & 1u;
     p[j] = on ? rec_part(rec[J0 + j]) : 0u;  // branch-free: an inactive record adds 0 to partition 0's counter
-#ifdef RING_EXP_RACY
-    old[j] = L.ctr[p[j]];  // experiment: a non-atomic claim (wrong results; timing only)
-    L.ctr[p[j]] = old[j] + (on ? 1u : 0u);
-#else
     old[j] = atomicAdd(L.ctr + p[j], on ? 1u : 0u);
-#endif
   }
   uint32_t over = 0;
 #pragma unroll
   for (int j = 0; j < kRingRoundRecs; j++) {
     const bool on = (act >> (J0 + j)) & 1u;
     const uint32_t s = old[j] & 0xFFFFu, h = old[j] >> 16;
-#ifdef RING_EXP_NOWRITE
-    if (on && s < (uint32_t)kRingBucket && rec[J0 + j] == 0x0123456789ABCDEFull)  // experiment: no bucket writes
-#else
     if (on && s < (uint32_t)kRingBucket)
-#endif
       L.bkt[p[j] * kRingBucketStride + ((h + s) & (kRingBucket - 1))] = rec[J0 + j];
     over |= (on && s >= (uint32_t)kRingBucket) ? (1u << j) : 0u;
   }
@@ -133,14 +166,32 @@ __device__ __forceinline__ void ring_insert(const RingArgs &a, const RingLds &L,
     for (int j = 0; j < kRingRoundRecs; j++)
       if ((over >> j) & 1u) {
         const uint32_t k = atomicAdd(L.back + p[j], 1u);
-        if (k < C) region0[((size_t)p[j] * a.nblk + 1) * C - 1 - k] = rec[J0 + j] & ((1ull << kRecPShift) - 1ull);
+        if (k < C) {
+          unsigned long long r = rec[J0 + j] & ((1ull << kRecPShift) - 1ull);
+          if constexpr (HLL) r = ring_hll_out(a, r);
+          store_rec<RB>(region0, ((size_t)p[j] * a.nblk + 1) * C - 1 - k, r);
+        }
       }
   }
 }
 
 // A flushed 16-B piece of a region: a plain store, so L2 merges a region's two 64-B halves into one line before it
 // writes the line back (measured 2 % faster than non-temporal stores, r05p).
-__device__ __forceinline__ void ring_store(u32x4 v, u32x4 *dst) { *dst = v; }
+// RB = 6: two 8-B entries (x, y | z, w; the record in the low 48 bits of each) packed into 12 B. (sizeof(u32x3a) is 16:
+// never index an array of them, address 12-B units in bytes.)
+typedef uint32_t u32x3a __attribute__((ext_vector_type(3), aligned(4)));
+template <int RB>
+__device__ __forceinline__ void ring_store(u32x4 v, uint8_t *dst) {
+  if constexpr (RB == 8) {
+    *reinterpret_cast<u32x4 *>(dst) = v;
+  } else {
+    u32x3a z;
+    z.x = v.x;
+    z.y = (v.y & 0xFFFFu) | (v.z << 16);
+    z.z = (v.z >> 16) | (v.w << 16);
+    *reinterpret_cast<u32x3a *>(dst) = z;
+  }
+}
 
 // Flush phase (flusher waves only, between two block barriers): every bucket holding 8 or more entries moves its
 // oldest half (entries head .. head + 7: one aligned 64-B piece of LDS) to the front of its region at the partition's
@@ -151,8 +202,8 @@ __device__ __forceinline__ void ring_store(u32x4 v, u32x4 *dst) { *dst = v; }
 // share the CU's vector-memory path with the decoders' loads, so fewer store instructions per flushed byte let the
 // loads issue sooner (k_group_ring 5.59 -> 5.09 ms against one lane storing each of its halves, r05s).
 constexpr int kRingListPerWave = 64 * 2 * 2;  // 2 partitions per lane per batch, <= 2 halves each
-template <int KP>
-__device__ __forceinline__ void ring_flush_phase(const RingArgs &a, const RingLds &L, unsigned long long *region0,
+template <int RB, bool HLL, int KP>
+__device__ __forceinline__ void ring_flush_phase(const RingArgs &a, const RingLds &L, uint8_t *region0,
                                                  uint32_t C, int fw, int lane, uint32_t (&front)[KP],
                                                  uint32_t &status) {
   uint32_t *list = L.list + fw * kRingListPerWave;
@@ -199,12 +250,18 @@ __device__ __forceinline__ void ring_flush_phase(const RingArgs &a, const RingLd
       const uint32_t ent = list[i];
       const uint32_t p = (ent >> 21) & 1023u, fr = ent & 0xFFFFFu, hh = ((ent >> 20) & 1u) * 8u;
       const u32x4 x = reinterpret_cast<const u32x4 *>(L.bkt + p * kRingBucketStride + hh)[sub];
-#ifdef RING_EXP_NOFLUSH
-      if ((ent >> 31) && x.x == 0x9E3779B9u && x.y == 0x7F4A7C15u)
-#else
-      if (ent >> 31)
-#endif
-        ring_store(x & m, reinterpret_cast<u32x4 *>(region0 + (size_t)p * a.nblk * C + fr) + sub);
+      if (ent >> 31) {
+        u32x4 y = x & m;
+        if constexpr (HLL) {
+          const unsigned long long r0 = ring_hll_out(a, ((unsigned long long)y.y << 32) | y.x),
+                                   r1 = ring_hll_out(a, ((unsigned long long)y.w << 32) | y.z);
+          y.x = (uint32_t)r0;
+          y.y = (uint32_t)(r0 >> 32);
+          y.z = (uint32_t)r1;
+          y.w = (uint32_t)(r1 >> 32);
+        }
+        ring_store<RB>(y, region0 + ((size_t)p * a.nblk * C + fr) * RB + sub * (2 * RB));
+      }
     }
     __builtin_amdgcn_wave_barrier();  // the list is rewritten by the next batch
   }
@@ -258,7 +315,7 @@ __device__ __forceinline__ RingColsDev ring_cols(const RingArgs &a, const GroupS
   }
 #pragma unroll
   for (int c = 0; c < kRingAggCols; c++)
-    if (a.n_gcols + c < a.nc) {
+    if (a.n_gcols + c < a.nc && a.pf_agg[a.n_gcols + c] >= 0) {
       const GroupAggDev ag = load_const(a.aggs + sg.first_agg + a.pf_agg[a.n_gcols + c]);
       k.fwd[kRingGroupCols + c] = ag.fwd;
       k.bits[kRingGroupCols + c] = ag.bits;
@@ -337,6 +394,7 @@ struct RingFieldFold {  // record |= dictId << field shift
   }
 };
 
+
 // The fields of a quarter-form scan leaf (FusedStep) the decoders keep in scalar registers.
 struct RingLeaf {
   const uint8_t *fwd;
@@ -390,7 +448,6 @@ struct RingSeg {
 // loads let the register allocator reuse a pending load's destination on the other path, and every later write of that
 // register then waits for all outstanding loads (vmcnt(0) between the columns' loads). The bytes past the quarter's
 // ceil(B / 2) + 1 dwords stay inside the forward index's padding and hit lines the wave reads anyway.
-typedef uint32_t u32x3a __attribute__((ext_vector_type(3), aligned(4)));
 __device__ __forceinline__ void ring_load_raw(const uint8_t *fwd, int bits, int64_t qi, uint32_t (&R)[12]) {
   // 11 dwords: the most a quarter of <= 20 bits spans (a dead 12th dword would be a pending load's destination the
   // allocator hands out again, and that write waits for every load)
@@ -473,24 +530,6 @@ struct RingDecoder {
     }
     word_bits = (uint32_t)(word >> (16 * (lane & 3))) & 0xFFFFu;
     qi = ch * 256 + 64 * q + lane;
-#ifdef RING_EXP_NODEC
-    return;  // experiment: no column loads (decode() makes synthetic records)
-#endif
-#ifdef RING_EXP_NOLOAD
-    {  // experiment: no column loads; the decode runs on opaque per-quarter values
-#pragma unroll
-      for (int i = 0; i < 12; i++) {
-        uint32_t v = (uint32_t)qi * 0x9E3779B1u + (uint32_t)i * 0x85EBCA77u;
-        v ^= v >> 15;
-        v *= 0x2C1B3C6Du;
-        asm volatile("" : "+v"(v));
-#pragma unroll
-        for (int f = 0; f < (NF > 0 ? NF : 1); f++) F[f][i] = v;
-        RA[0][i] = v * 3u; RA[1][i] = v * 5u; RB[0][i] = v * 7u; RB[1][i] = v * 11u;
-      }
-      return;
-    }
-#endif
 #pragma unroll
     for (int i = 0; i < NF; i++)
       if (i < sg.n_leaves) ring_load_raw(st[i].fwd, st[i].bits, qi, F[i]);
@@ -505,19 +544,6 @@ struct RingDecoder {
   // Records J0 .. JE - 1 of the requested quarter (keys, then the aggregated fields).
   template <int J0, int JE>
   __device__ __forceinline__ void decode_records(const RingArgs &a) {
-#ifdef RING_EXP_NODEC
-    {  // experiment: records of pseudo-random keys, no column data
-#pragma unroll
-      for (int j = J0; j < JE; j++) {
-        unsigned long long z = (unsigned long long)(qi * 16 + j) + 0x9E3779B97F4A7C15ull;
-        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-        const uint32_t key = (uint32_t)((z ^ (z >> 31)) % (uint64_t)a.G);
-        rec[j] = (unsigned long long)(key & ((1u << a.shift) - 1u)) | ((unsigned long long)(key >> a.shift) << kRecPShift);
-      }
-      return;
-    }
-#endif
     uint32_t key[16];
 #pragma unroll
     for (int j = J0; j < JE; j++) key[j] = 0;
@@ -548,7 +574,6 @@ struct RingDecoder {
       act_next = 0;
       return;
     }
-#ifndef RING_EXP_NODEC
     if constexpr (NF > 0) {
 #pragma unroll
       for (int i = 0; i < NF; i++)
@@ -559,7 +584,6 @@ struct RingDecoder {
           act_next &= (st[i].negate ? ~m : m) & 0xFFFFu;
         }
     }
-#endif
     if constexpr (!WORDS) seg_matched += __popc(act_next);
     decode_records<0, kRingRoundRecs>(a);
   }
@@ -585,7 +609,7 @@ struct RingDecoder {
 // next pass's quarter (its raw dwords requested a pass earlier) and decode its records 0 .. 7 (the slots round 0 just
 // emptied), during the second its records 8 .. 15, then request the quarter after it: the decode's VALU work fills
 // both flush phases. Every wave executes the same barriers.
-template <int NF, bool WORDS>
+template <int NF, bool WORDS, int RB, bool HLL>
 __global__ __launch_bounds__(kRingBlock) void k_group_ring(RingArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -599,7 +623,7 @@ __global__ __launch_bounds__(kRingBlock) void k_group_ring(RingArgs a) {
   __syncthreads();
   const uint32_t C = a.cap;
   if (b == 0 && tid == 0) *a.region = C;
-  unsigned long long *region0 = a.records + (size_t)b * C;  // region (p, b) at ((p * nblk + b) * C)
+  uint8_t *region0 = a.records + (size_t)b * C * RB;  // region (p, b): records ((p * nblk + b) * C ...) of RB bytes
   uint32_t status = 0;
   const int64_t c0 = a.total_chunks * b / a.nblk, c1 = a.total_chunks * (b + 1) / a.nblk;
   const int64_t nq = (c1 - c0) * 4;  // the block's quarters
@@ -610,29 +634,13 @@ __global__ __launch_bounds__(kRingBlock) void k_group_ring(RingArgs a) {
     uint32_t front[KP];
 #pragma unroll
     for (int k = 0; k < KP; k++) front[k] = 0;
-#ifdef RING_EXP_TIMING
-    uint64_t tb = 0, tf = 0, tt = 0;
-#endif
     for (int64_t t = 0; t < npass; t++)
 #pragma unroll 1
       for (int r = 0; r < 16 / kRingRoundRecs; r++) {
-        RT_MARK(x0);
-        RT_MARK(xt);
         __syncthreads();  // inserts of the round done
-        RT_ADD(tb, x0);
-        RT_MARK(x1);
-        ring_flush_phase<KP>(a, L, region0, C, fw, lane, front, status);
-        RT_ADD(tf, x1);
-        RT_MARK(x2);
+        ring_flush_phase<RB, HLL, KP>(a, L, region0, C, fw, lane, front, status);
         __syncthreads();  // flushes done (and the decoders' next quarter decoded)
-        RT_ADD(tb, x2);
-        RT_ADD(tt, xt);
       }
-#ifdef RING_EXP_TIMING
-    if ((b == 0 || b == a.nblk / 2) && lane == 0)
-      printf("ring-timing block %d flusher %d: total %llu barrier %llu flush %llu passes %lld\n", b, fw,
-             (unsigned long long)tt, (unsigned long long)tb, (unsigned long long)tf, (long long)npass);
-#endif
     // the partial buckets (< 8 entries) to their fronts, then each region's counts
 #pragma unroll
     for (int k = 0; k < KP; k++) {
@@ -641,8 +649,11 @@ __global__ __launch_bounds__(kRingBlock) void k_group_ring(RingArgs a) {
       const uint32_t c = L.ctr[p], n = min(c & 0xFFFFu, (uint32_t)kRingBucket), h = c >> 16, nb = L.back[p];
       for (uint32_t i = 0; i < n; i++)
         if (front[k] + i < C)
-          region0[(size_t)p * a.nblk * C + front[k] + i] =
-              L.bkt[p * kRingBucketStride + ((h + i) & (kRingBucket - 1))] & ((1ull << kRecPShift) - 1ull);
+        {
+          unsigned long long r = L.bkt[p * kRingBucketStride + ((h + i) & (kRingBucket - 1))] & ((1ull << kRecPShift) - 1ull);
+          if constexpr (HLL) r = ring_hll_out(a, r);
+          store_rec<RB>(region0, (size_t)p * a.nblk * C + front[k] + i, r);
+        }
       const uint32_t f = front[k] + n;
       if (f + nb > C || f >= (1u << (32 - kRingBackBits)) || nb >= (1u << kRingBackBits)) status |= 1u;
       a.hist[(size_t)p * a.nblk + b] = min(f, (1u << (32 - kRingBackBits)) - 1u) | (min(nb, (1u << kRingBackBits) - 1u) << (32 - kRingBackBits));
@@ -654,62 +665,31 @@ __global__ __launch_bounds__(kRingBlock) void k_group_ring(RingArgs a) {
     d.decode_front(a);
     d.decode_back(a);
     d.load(a, 1);  // in flight during pass 0's rounds
-#ifdef RING_EXP_TIMING
-    uint64_t ti = 0, tb = 0, td = 0, tl = 0, tt = 0;
-#endif
     for (int64_t t = 0; t < npass; t++) {
-      RT_MARK(xt);
-      RT_MARK(x0);
-#ifndef RING_EXP_NOINS
-      ring_insert<0>(a, L, d.act, d.rec, region0, C);
-#endif
-      RT_ADD(ti, x0);
+      ring_insert<RB, HLL, 0>(a, L, d.act, d.rec, region0, C);
       if constexpr (kRingRoundRecs < 16) {
         __syncthreads();  // inserts of round 0 done
         // the next pass's quarter: filter and records 0 .. 7 decoded meanwhile the flushers empty round 0's buckets
-        RT_MARK(x1);
         d.decode_front(a);
-        RT_ADD(td, x1);
         __syncthreads();  // flush done
-        RT_MARK(x2);
-#ifndef RING_EXP_NOINS
-        ring_insert<kRingRoundRecs>(a, L, d.act, d.rec, region0, C);
-#else
-        if (d.rec[3] == 0x0123456789ull && d.act == 7) status |= 8u;
-#endif
-        RT_ADD(ti, x2);
+        ring_insert<RB, HLL, kRingRoundRecs>(a, L, d.act, d.rec, region0, C);
       }
-      RT_MARK(x3);
       __syncthreads();  // inserts of round 1 done
-      RT_ADD(tb, x3);
       // records 8 .. 15 of the next pass's quarter decoded meanwhile the flushers empty round 1's buckets, then the
       // quarter after it requested
-      RT_MARK(x4);
       if constexpr (kRingRoundRecs == 16) d.decode_front(a);
       d.decode_back(a);
-      RT_ADD(td, x4);
-      RT_MARK(x5);
       d.load(a, t + 2);
-      RT_ADD(tl, x5);
-      RT_MARK(x6);
       __syncthreads();  // flush done
-      RT_ADD(tb, x6);
-      RT_ADD(tt, xt);
     }
     d.finish(a, lane);
-#ifdef RING_EXP_TIMING
-    if ((b == 0 || b == a.nblk / 2) && lane == 0)
-      printf("ring-timing block %d decoder %d: total %llu insert %llu barrier %llu decode %llu load %llu\n", b, wave,
-             (unsigned long long)tt, (unsigned long long)ti, (unsigned long long)tb, (unsigned long long)td,
-             (unsigned long long)tl);
-#endif
   }
   if (status) atomicOr(a.status, status);
 }
 
 // ----------------------------------------------------------------------------------------------------- reduce
 constexpr int kRingReduceBlock = 1024;
-constexpr int kRingReduceUnroll = 4;   // 16-B loads (two records each) per lane and step
+constexpr int kRingReduceUnroll = 4;   // 16-B / 12-B loads (two records each) per lane and step
 constexpr int kRingExceptions = 512;   // HLL ranks > 15 per partition (nibble registers saturate at 15)
 
 __device__ __forceinline__ unsigned long long ordered_bits_g(double d) {
@@ -723,40 +703,6 @@ __device__ __forceinline__ double dict_value_g(const void *dict, int value_kind,
     case 1: return (double)static_cast<const long long *>(dict)[id];
     default: return static_cast<const double *>(dict)[id];
   }
-}
-
-// stream-lib MurmurHash.hashLong + HyperLogLog (register << 8 | rank): hll.cpp's murmur_hash_long / hll_register_rank
-__device__ __forceinline__ uint32_t murmur_hash_long_g(long long data) {
-  constexpr uint32_t kM = 0x5bd1e995u;
-  const unsigned long long d = (unsigned long long)data;
-  uint32_t h = 0;
-  uint32_t k = (uint32_t)d * kM;
-  k ^= k >> 24;
-  h ^= k * kM;
-  k = (uint32_t)(d >> 32) * kM;
-  k ^= k >> 24;
-  h *= kM;
-  h ^= k * kM;
-  h ^= h >> 13;
-  h *= kM;
-  h ^= h >> 15;
-  return h;
-}
-
-// murmur_hash_long_g of a value in [0, 2^32): the high word's block multiplies h by kM once more
-__device__ __forceinline__ uint32_t murmur_hash_lo32_g(uint32_t lo) {
-  constexpr uint32_t kM = 0x5bd1e995u, kMM = kM * kM;
-  uint32_t k = lo * kM;
-  k ^= k >> 24;
-  uint32_t h = k * kMM;
-  h ^= h >> 13;
-  h *= kM;
-  h ^= h >> 15;
-  return h;
-}
-
-__device__ __forceinline__ uint32_t hll_register_rank_g(uint32_t h) {
-  return ((h >> 24) << 8) | (uint32_t)(__builtin_clz((h << 8) | 129u) + 1);
 }
 
 // GATHER = false: every aggregation is a COUNT, an affine-dictionary SUM / AVG or an affine-dictionary HLL (the host
@@ -800,19 +746,17 @@ __device__ __forceinline__ void ring_fold(const RingReduceArgs &a, uint8_t *lds,
       for (int u = 0; u < N; u++)
         if (ok[u]) atomicAdd(reinterpret_cast<unsigned long long *>(acc) + k[u], v[u]);
     } else if (ag.acc_kind == 4) {  // 4-bit registers: max by CAS on the containing dword
-#ifdef RING_EXP_NOHLL
-      continue;  // experiment: no HLL fold
-#endif
-      uint32_t h[N];
+      uint32_t h[N];  // register << 8 | rank
+      if ((a.hll_pre >> g) & 1) {  // the scatter's field: register << 5 | rank
 #pragma unroll
-      for (int u = 0; u < N; u++)
-#ifdef RING_EXP_CHEAPHASH
-        h[u] = hll_register_rank_g(id[u] * 0x9E3779B1u);  // experiment: one multiply instead of the hash
-#else
-        h[u] = (GATHER && !ag.affine) ? (uint32_t)gload<uint16_t>(ag.hll_lut + id[u])
-               : lo32 ? hll_register_rank_g(murmur_hash_lo32_g((uint32_t)ag.affine_base + (uint32_t)ag.affine_step * id[u]))
-                      : hll_register_rank_g(murmur_hash_long_g(ag.affine_base + ag.affine_step * (long long)id[u]));
-#endif
+        for (int u = 0; u < N; u++) h[u] = ((id[u] >> 5) << 8) | (id[u] & 31u);
+      } else {
+#pragma unroll
+        for (int u = 0; u < N; u++)
+          h[u] = (GATHER && !ag.affine) ? (uint32_t)gload<uint16_t>(ag.hll_lut + id[u])
+                 : lo32 ? hll_register_rank_g(murmur_hash_lo32_g((uint32_t)ag.affine_base + (uint32_t)ag.affine_step * id[u]))
+                        : hll_register_rank_g(murmur_hash_long_g(ag.affine_base + ag.affine_step * (long long)id[u]));
+      }
       uint32_t *word[N], old[N], rk[N];
       int sh[N];
       uint32_t over = 0;  // records whose rank exceeds the nibble: the exception list (rare)
@@ -859,9 +803,13 @@ __device__ __forceinline__ void ring_fold(const RingReduceArgs &a, uint8_t *lds,
   }
 }
 
-template <int U, bool GATHER>
+// A 16-B (RB = 8) or 12-B (RB = 6) unit of two consecutive records.
+template <int RB>
+using RingUnit = typename std::conditional<RB == 8, u32x4, u32x3a>::type;
+
+template <int RB, int U, bool GATHER>
 __device__ __forceinline__ void ring_fold_units(const RingReduceArgs &a, uint8_t *lds, uint32_t *cnt, uint32_t *exc_n,
-                                                uint32_t *exc, const u32x4 (&v)[U], const uint32_t (&n)[U], int pk,
+                                                uint32_t *exc, const RingUnit<RB> (&v)[U], const uint32_t (&n)[U], int pk,
                                                 int sbits, bool lo32, uint32_t &status) {
   unsigned long long rec[2 * U];
   bool ok[2 * U];
@@ -869,10 +817,15 @@ __device__ __forceinline__ void ring_fold_units(const RingReduceArgs &a, uint8_t
   for (int u = 0; u < U; u++) {
     // the loaded set passes through an empty asm here, in straight-line code: the compiler waits for exactly these
     // loads (the other set's stay in flight); a first use inside the fold's runtime loops would wait for every load
-    u32x4 x = v[u];
+    RingUnit<RB> x = v[u];
     asm volatile("" : "+v"(x));
-    rec[2 * u] = ((unsigned long long)x.y << 32) | x.x;
-    rec[2 * u + 1] = ((unsigned long long)x.w << 32) | x.z;
+    if constexpr (RB == 8) {
+      rec[2 * u] = ((unsigned long long)x.y << 32) | x.x;
+      rec[2 * u + 1] = ((unsigned long long)x.w << 32) | x.z;
+    } else {
+      rec[2 * u] = ((unsigned long long)(x.y & 0xFFFFu) << 32) | x.x;
+      rec[2 * u + 1] = ((unsigned long long)x.z << 16) | (x.y >> 16);
+    }
     ok[2 * u] = n[u] & 1u;
     ok[2 * u + 1] = (n[u] >> 1) & 1u;
   }
@@ -892,9 +845,10 @@ struct RingStream {
 // wave's next non-empty range when this one is done (wave w: regions w, w + 16, ..., each front then back); v >= nblk
 // once the stream is exhausted (loads then stay in bounds and count no record). cnt[u]: bit 0 / 1 = record 2i / 2i + 1
 // of the unit is in the range.
+template <int RB>
 __device__ __forceinline__ bool ring_stream_next(const RingReduceArgs &a, const uint32_t *hrow, uint32_t C,
-                                                 const unsigned long long *base, RingStream &rs, int lane,
-                                                 u32x4 (&v)[kRingReduceUnroll], uint32_t (&cnt)[kRingReduceUnroll]) {
+                                                 const uint8_t *base, RingStream &rs, int lane,
+                                                 RingUnit<RB> (&v)[kRingReduceUnroll], uint32_t (&cnt)[kRingReduceUnroll]) {
   while (rs.i >= rs.u1) {  // uniform
     if (rs.part == 0) {
       rs.part = 1;
@@ -911,7 +865,8 @@ __device__ __forceinline__ bool ring_stream_next(const RingReduceArgs &a, const 
     rs.u1 = (rs.s0 + rs.n + 1) >> 1;
   }
   const bool live = rs.v < a.nblk;
-  const u32x4 *src = reinterpret_cast<const u32x4 *>(base + (size_t)(live ? rs.v : 0) * C);
+  // byte addressing: a 3-vector's sizeof is 16, so unit i of the 12-B units is at 12 i, not at src + i
+  const uint8_t *src = base + (size_t)(live ? rs.v : 0) * C * RB;
 #pragma unroll
   for (int u = 0; u < kRingReduceUnroll; u++) {
     const uint32_t idx = rs.i + (uint32_t)(u * 64 + lane);
@@ -919,13 +874,14 @@ __device__ __forceinline__ bool ring_stream_next(const RingReduceArgs &a, const 
     const uint32_t r0 = 2 * idx;
     cnt[u] = ok ? ((r0 >= rs.s0 && r0 < rs.s0 + rs.n) ? 1u : 0u) | ((r0 + 1 >= rs.s0 && r0 + 1 < rs.s0 + rs.n) ? 2u : 0u)
                 : 0u;
-    v[u] = __builtin_nontemporal_load(src + (ok ? idx : 0u));  // unconditional (a branch would cost the counted wait)
+    v[u] = __builtin_nontemporal_load(  // unconditional (a branch would cost the counted wait)
+        reinterpret_cast<const RingUnit<RB> *>(src + (size_t)(ok ? idx : 0u) * (2 * RB)));
   }
   rs.i += 64 * kRingReduceUnroll;
   return live;
 }
 
-template <bool GATHER>
+template <bool GATHER, int RB>
 __global__ __launch_bounds__(kRingReduceBlock) void k_ring_reduce(RingReduceArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int tid = threadIdx.x;
@@ -979,7 +935,7 @@ __global__ __launch_bounds__(kRingReduceBlock) void k_ring_reduce(RingReduceArgs
       lo32 = lo32 && ag.affine && ag.affine_base >= 0 && ag.affine_step >= 0 && ag.bits < 32 && top < (1ll << 32);
     }
   uint32_t status = 0;
-  const unsigned long long *base = a.records + (size_t)p * a.nblk * C;
+  const uint8_t *base = a.records + (size_t)p * a.nblk * C * RB;
   // wave w streams record ranges w, w + 16, ... (each region's front and back): 16-B loads (two records) per lane,
   // kRingReduceUnroll loads per lane and step, the next step's loads issued before this step's records are folded
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -990,23 +946,15 @@ __global__ __launch_bounds__(kRingReduceBlock) void k_ring_reduce(RingReduceArgs
   rs.i = 0;
   rs.u1 = 0;
   // two register sets, unrolled by two (no copies: a copy of a set still in flight would wait for its loads)
-  u32x4 va[U], vb[U];
+  RingUnit<RB> va[U], vb[U];
   uint32_t na[U], nb[U];
-  bool live_a = ring_stream_next(a, hrow, C, base, rs, lane, va, na);
+  bool live_a = ring_stream_next<RB>(a, hrow, C, base, rs, lane, va, na);
   while (live_a) {  // uniform; every load unconditional (an exhausted stream loads unit 0 with no record counted)
-    const bool live_b = ring_stream_next(a, hrow, C, base, rs, lane, vb, nb);
-#ifndef RING_EXP_NOFOLD
-    ring_fold_units<U, GATHER>(a, lds, cnt, exc_n, exc, va, na, pk, sbits, lo32, status);
-#else
-    for (int u = 0; u < U; u++) if (va[u].x == 0x01234567u && na[u] == 3) status |= 8u;
-#endif
+    const bool live_b = ring_stream_next<RB>(a, hrow, C, base, rs, lane, vb, nb);
+    ring_fold_units<RB, U, GATHER>(a, lds, cnt, exc_n, exc, va, na, pk, sbits, lo32, status);
     if (!live_b) break;
-    live_a = ring_stream_next(a, hrow, C, base, rs, lane, va, na);
-#ifndef RING_EXP_NOFOLD
-    ring_fold_units<U, GATHER>(a, lds, cnt, exc_n, exc, vb, nb, pk, sbits, lo32, status);
-#else
-    for (int u = 0; u < U; u++) if (vb[u].x == 0x01234567u && nb[u] == 3) status |= 8u;
-#endif
+    live_a = ring_stream_next<RB>(a, hrow, C, base, rs, lane, va, na);
+    ring_fold_units<RB, U, GATHER>(a, lds, cnt, exc_n, exc, vb, nb, pk, sbits, lo32, status);
   }
   __syncthreads();
   const long long kbase = (long long)p * K;
@@ -1094,10 +1042,22 @@ void launch_group_ring(const RingArgs &a, hipStream_t stream) {
   if (a.nblk <= 0 || a.total_chunks <= 0) return;
   const size_t lds = ring_lds_bytes(a.P);
   const dim3 grid((unsigned)a.nblk), block(kRingBlock);
-  if (a.nf < 0) hipLaunchKernelGGL((k_group_ring<0, true>), grid, block, lds, stream, a);
-  else if (a.nf == 0) hipLaunchKernelGGL((k_group_ring<0, false>), grid, block, lds, stream, a);
-  else if (a.nf == 1) hipLaunchKernelGGL((k_group_ring<1, false>), grid, block, lds, stream, a);
-  else hipLaunchKernelGGL((k_group_ring<2, false>), grid, block, lds, stream, a);
+  // instances: the filter form (GB_FILTER words / 0-2 quarter-form leaves) x record bytes x the flushers' HLL field
+#define PINOT_RING(NF, W)                                                                                   \
+  do {                                                                                                      \
+    if (a.rec_bytes == 6) {                                                                                 \
+      if (a.hll) hipLaunchKernelGGL((k_group_ring<NF, W, 6, true>), grid, block, lds, stream, a);           \
+      else hipLaunchKernelGGL((k_group_ring<NF, W, 6, false>), grid, block, lds, stream, a);                \
+    } else {                                                                                                \
+      if (a.hll) hipLaunchKernelGGL((k_group_ring<NF, W, 8, true>), grid, block, lds, stream, a);           \
+      else hipLaunchKernelGGL((k_group_ring<NF, W, 8, false>), grid, block, lds, stream, a);                \
+    }                                                                                                       \
+  } while (0)
+  if (a.nf < 0) PINOT_RING(0, true);
+  else if (a.nf == 0) PINOT_RING(0, false);
+  else if (a.nf == 1) PINOT_RING(1, false);
+  else PINOT_RING(2, false);
+#undef PINOT_RING
 }
 
 void launch_ring_reduce(const RingReduceArgs &a, hipStream_t stream) {
@@ -1107,8 +1067,15 @@ void launch_ring_reduce(const RingReduceArgs &a, hipStream_t stream) {
     const int k = a.aggs[g].acc_kind;
     gather = gather || k == 1 || k == 2 || k == 3 || ((k == 0 || k == 4) && !a.aggs[g].affine);
   }
-  if (gather) hipLaunchKernelGGL(k_ring_reduce<true>, dim3((unsigned)a.P), dim3(kRingReduceBlock), (size_t)a.lds_bytes, stream, a);
-  else hipLaunchKernelGGL(k_ring_reduce<false>, dim3((unsigned)a.P), dim3(kRingReduceBlock), (size_t)a.lds_bytes, stream, a);
+  const dim3 grid((unsigned)a.P), block(kRingReduceBlock);
+  const size_t lds = (size_t)a.lds_bytes;
+  if (a.rec_bytes == 6) {
+    if (gather) hipLaunchKernelGGL((k_ring_reduce<true, 6>), grid, block, lds, stream, a);
+    else hipLaunchKernelGGL((k_ring_reduce<false, 6>), grid, block, lds, stream, a);
+  } else {
+    if (gather) hipLaunchKernelGGL((k_ring_reduce<true, 8>), grid, block, lds, stream, a);
+    else hipLaunchKernelGGL((k_ring_reduce<false, 8>), grid, block, lds, stream, a);
+  }
 }
 
 int ring_reduce_exceptions() { return kRingExceptions; }

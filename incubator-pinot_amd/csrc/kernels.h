@@ -147,7 +147,9 @@ enum FusedKind : int32_t {
   FK_LEAF_RANGE = 0, FK_LEAF_LUT64 = 1, FK_LEAF_LUT = 2, FK_FOLD = 3,
   FK_LEAF_RANGES = 4,   // sorted-index leaf: inclusive [start, end] doc ranges (table, n = lo)
   FK_LEAF_ROARING = 5,  // bitmap-index leaf: OR of the dictIds' roaring bitmaps (fwd = payload, aux0 = containers,
-                        // aux1 = per-dictId container directory, table = dictIds, n = lo), negate = exclusive
+                        // aux1 = per-dictId container directory, table = dictIds, n = lo), negate = exclusive;
+                        // ops = 1 (more than 256 dictIds): aux1 = per-key directory [lo + 1] into table = the dictIds'
+                        // container indices bucketed by roaring key (lo = keys)
   FK_OP = 6             // nested AND / OR: term = (popped entry) op term, op in `join` (JOIN_AND / JOIN_OR)
 };
 // How a leaf joins the filter program (the top-level conjunction of terms, a term = an AND / OR tree of leaves in
@@ -155,7 +157,8 @@ enum FusedKind : int32_t {
 // into the running term, JOIN_PUSH pushes the running term onto a register stack and starts a nested one (an FK_OP
 // step pops it and combines). kMaxFusedStack entries below the running term.
 enum FusedJoin : int32_t { JOIN_NEW = 0, JOIN_OR = 1, JOIN_AND = 2, JOIN_PUSH = 3 };
-constexpr int kMaxFusedStack = 3;
+constexpr int kMaxFusedStack = 4;       // k_scan_query's register stack
+constexpr int kMaxFusedStackGroup = 3;  // the group-by kernels' (one 64-bit entry less: their registers are spoken for)
 enum FoldOps : int32_t { FOLD_IDSUM = 1, FOLD_MINMAX = 2, FOLD_DICT32 = 4, FOLD_HLL = 8 };
 constexpr int kMaxFusedFolds = 6;                      // distinct aggregated columns per query
 constexpr int kMaxFusedSlots = 1 + 2 * kMaxFusedFolds; // slot 0 count; fold f: 1 + 2f sum, 2 + 2f min/max
@@ -370,7 +373,13 @@ struct RingArgs {
   int32_t shift, nblk;            // nblk: blocks of the launch (one per CU): block b owns chunks [T b / nblk, T (b+1) / nblk)
   uint32_t cap;                   // C: records per region
   int32_t nf;                     // < 0: the filter words; else at most nf scan leaves evaluated per quarter
-  unsigned long long *records;    // [P][nblk][C] (local key | dictId fields)
+  int32_t rec_bytes;              // 8, or 6 when the record fields fit 48 bits (the low 48 bits of each record stored)
+  int32_t hll;                    // 1: the records leave the block with the field [hll_shift, + hll_bits) (an HLL column's
+                                  // dictId, over an affine dictionary base + step * id with values in [0, 2^32)) replaced
+                                  // by register << 5 | rank of its value (the flushers hash; the reduce does not)
+  int32_t hll_shift, hll_bits;
+  uint32_t hll_base, hll_step;
+  uint8_t *records;               // [P][nblk][C] records of rec_bytes (local key | fields)
   uint32_t *hist;                 // [P][nblk] records claimed per region (> C: overflow)
   uint32_t *status;               // |= 1 a region overflowed, 2 a spin bound was hit, 4 HLL exception list full
   uint32_t *region;               // C, written by block 0 (read by k_ring_reduce)
@@ -378,7 +387,9 @@ struct RingArgs {
 };
 constexpr int kRingMaxQuarterLeaves = 2;
 struct RingReduceArgs {
-  const unsigned long long *records;
+  const uint8_t *records;            // RingArgs.records
+  int32_t rec_bytes;
+  int32_t hll_pre;                   // bit g: aggregation g's field is the scatter's HLL register << 5 | rank
   const uint32_t *hist;
   const uint32_t *region;
   int32_t P, shift, n_aggs, nblk;

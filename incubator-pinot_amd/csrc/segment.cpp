@@ -66,6 +66,15 @@ static void upload_dictionary(Engine &e, ColumnData &c) {
 bool transcode_column(Engine &e, const pinot_column_desc &d, int32_t num_docs, TranscodedColumn &tc) {
   const int w = raw_numeric_width(d, num_docs);
   if (!w || !e.raw_device) return transcode_raw(d, num_docs, tc);
+  {  // the device transcode's scratch (~n (w + 44) B) must leave room in HBM: else the host path (counted)
+    const size_t need = transcode_numeric_device_bytes((uint64_t)std::max(num_docs, 0), w, e.stream);
+    size_t free_b = 0, total_b = 0;
+    PINOT_HIP(hipMemGetInfo(&free_b, &total_b));
+    if ((double)need > 0.5 * (double)free_b) {
+      e.raw_host_fallbacks++;
+      return transcode_raw(d, num_docs, tc);
+    }
+  }
   std::vector<uint64_t> uniq;
   transcode_numeric_device(d.forward_index, (uint64_t)std::max(num_docs, 0), w, d.data_type, e.stream, uniq,
                            tc.forward_index);
@@ -103,6 +112,8 @@ static void register_column(Engine &e, SegmentData &seg, const pinot_column_desc
   }
   if (!c.is_sorted && c.has_inverted) {
     const std::vector<RoaringContainer> &conts = idx.containers;
+    c.inv_keys.resize(conts.size());
+    for (size_t i = 0; i < conts.size(); i++) c.inv_keys[i] = conts[i].key;
     upload(c.inv_payload, d.inverted_index, d.inverted_index_len, padded(d.inverted_index_len), e.stream);
     upload(c.inv_containers, conts.data(), conts.size() * sizeof(RoaringContainer),
            std::max<size_t>(conts.size() * sizeof(RoaringContainer), 16), e.stream);

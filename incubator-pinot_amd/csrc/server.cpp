@@ -26,10 +26,13 @@
 #include "collective.h"
 
 #include <algorithm>
+#include <atomic>
 #include <climits>
+#include <cmath>
 #include <cstring>
 #include <sstream>
 #include <thread>
+#include <unordered_map>
 
 #include "engine.h"
 
@@ -234,6 +237,121 @@ void fail_together(const std::vector<Status> &all, int my_rank, const char *what
       throw Error((pinot_status)all[r].status, std::string(what) + ": rank " + std::to_string(r) + " failed: " + all[r].msg);
 }
 
+// ---- hashed key spaces across ranks (LONG_MAP / ARRAY_MAP holders, SV or MV group columns)
+// One segment's groups as they travel to rank 0: key string, then per function its count (docs, or entries for the
+// MV functions), value and, for DISTINCTCOUNTHLL / DISTINCTCOUNTHLLMV, the 256 registers.
+bool is_hll_fn(int f) { return f == PINOT_AGG_DISTINCTCOUNTHLL || f == PINOT_AGG_DISTINCTCOUNTHLLMV; }
+
+void put_groups(Writer &w, const GroupByResult &r) {
+  const int64_t n = (int64_t)r.raw_keys.size();
+  const int na = (int)r.functions.size();
+  std::vector<std::vector<uint8_t>> regs(na);
+  for (int f = 0; f < na; f++)
+    if (is_hll_fn(r.functions[f]) && n) {
+      regs[f].resize((size_t)n * 256);
+      group_by_hll_registers(r, f, regs[f].data());
+    }
+  w.i64(n);
+  for (int64_t g = 0; g < n; g++) {
+    w.str(r.key(g));
+    for (int f = 0; f < na; f++) {
+      w.i64(r.counts[r.counts_shared ? 0 : f][g]);
+      w.f64(r.values[f].empty() ? 0.0 : r.values[f][g]);
+      if (!regs[f].empty()) w.raw(regs[f].data() + (size_t)g * 256, 256);
+    }
+  }
+}
+
+// CombineGroupByOperator's merge (CombineGroupByOperator.java:142-161) of every rank's segments' groups, in rank then
+// segment order, by group-key string: a key new to the merged map enters only while the map holds fewer than `cap`
+// keys (2 x num.groups.limit, :80,147); each function merges as its AggregationFunction.merge does (counts and sums
+// add, AvgPair adds both, MIN / MAX, HyperLogLog register max). The result's keys are its one "column" of strings.
+std::unique_ptr<GroupByResult> merge_rank_groups(const pinot_query &q, const std::vector<std::vector<uint8_t>> &blobs,
+                                                 const std::vector<size_t> &offsets, int64_t cap) {
+  const int na = q.num_aggregations;
+  std::vector<int> fn(na);
+  for (int a = 0; a < na; a++) fn[a] = q.aggregations[a].function;
+  std::unordered_map<std::string, int64_t> at;
+  std::vector<std::string> keys;
+  std::vector<std::vector<int64_t>> cnt(na);
+  std::vector<std::vector<double>> val(na);
+  std::vector<std::vector<uint8_t>> reg(na);
+  for (size_t r = 0; r < blobs.size(); r++) {
+    Reader rd{blobs[r]};
+    rd.p = offsets[r];
+    const int64_t nseg = rd.i64();
+    for (int64_t s = 0; s < nseg; s++) {
+      const int64_t n = rd.i64();
+      for (int64_t g = 0; g < n; g++) {
+        const std::string k = rd.str();
+        auto it = at.find(k);
+        int64_t i = -1;
+        if (it != at.end()) {
+          i = it->second;
+        } else if ((int64_t)keys.size() < cap) {
+          i = (int64_t)keys.size();
+          at.emplace(k, i);
+          keys.push_back(k);
+          for (int a = 0; a < na; a++) {
+            const int f = sv_function(fn[a]);
+            cnt[a].push_back(0);
+            val[a].push_back(f == PINOT_AGG_MIN ? INFINITY : f == PINOT_AGG_MAX ? -INFINITY : 0.0);
+            if (is_hll_fn(fn[a])) reg[a].resize(reg[a].size() + 256, 0);
+          }
+        }
+        for (int a = 0; a < na; a++) {
+          const int64_t c = rd.i64();
+          const double v = rd.f64();
+          uint8_t x[256];
+          if (is_hll_fn(fn[a])) rd.raw(x, 256);
+          if (i < 0) continue;  // the merged map is full: the key is dropped
+          cnt[a][i] += c;
+          const int f = sv_function(fn[a]);
+          if (f == PINOT_AGG_MIN) val[a][i] = std::min(val[a][i], v);
+          else if (f == PINOT_AGG_MAX) val[a][i] = std::max(val[a][i], v);
+          else if (f == PINOT_AGG_SUM || f == PINOT_AGG_AVG) val[a][i] += v;
+          if (is_hll_fn(fn[a]))
+            for (int j = 0; j < 256; j++) reg[a][(size_t)i * 256 + j] = std::max(reg[a][(size_t)i * 256 + j], x[j]);
+        }
+      }
+    }
+  }
+  // ascending key strings (the reference's map order is a hash order; the DataTable writer keeps this one)
+  const int64_t n = (int64_t)keys.size();
+  std::vector<int64_t> ord(n);
+  for (int64_t g = 0; g < n; g++) ord[g] = g;
+  std::sort(ord.begin(), ord.end(), [&](int64_t x, int64_t y) { return keys[x] < keys[y]; });
+  auto out = empty_group_result(q);
+  out->counts_shared = false;
+  out->gcard = {n};
+  out->gvalues.assign(1, std::vector<std::string>((size_t)n));
+  out->raw_keys.resize(n);
+  for (int a = 0; a < na; a++) {
+    out->counts[a].resize(n);
+    out->values[a].resize(n);
+    if (is_hll_fn(fn[a])) {
+      out->hll[a].resize((size_t)n * 256);
+      out->hll_card[a].resize(n);
+    }
+  }
+  for (int64_t g = 0; g < n; g++) {
+    const int64_t i = ord[g];
+    out->raw_keys[g] = g;
+    out->gvalues[0][g] = std::move(keys[i]);
+    for (int a = 0; a < na; a++) {
+      out->counts[a][g] = cnt[a][i];
+      out->values[a][g] = val[a][i];
+      if (is_hll_fn(fn[a])) {
+        memcpy(out->hll[a].data() + (size_t)g * 256, reg[a].data() + (size_t)i * 256, 256);
+        out->hll_card[a][g] = hll_cardinality(out->hll[a].data() + (size_t)g * 256);
+        out->values[a][g] = (double)out->hll_card[a][g];
+      }
+    }
+  }
+  out->merged_groups = n;
+  return out;
+}
+
 // This rank's segments for the query: its refs resolved on its engine, pruned (pinot_query.pruners, the server's
 // SegmentPrunerService), and the docs of all of them (totalDocs counts pruned segments, :214-215).
 std::vector<SegmentData *> rank_segments(Engine &e, size_t engine_index, const std::vector<SegmentRef> &refs,
@@ -368,7 +486,7 @@ void server_aggregate(ServerImpl &s, const std::vector<SegmentRef> &refs, const 
 
 // ------------------------------------------------------------------ group-by
 std::unique_ptr<GroupByResult> server_group_by(ServerImpl &s, const std::vector<SegmentRef> &refs, const pinot_query &q0,
-                                               pinot_exec_stats *stats) {
+                                               pinot_exec_stats *stats, int32_t top_n) {
   std::lock_guard<std::mutex> lk(s.mu);
   for (const SegmentRef &r : refs)
     require(r.engine >= 0 && r.engine < (int)s.engines.size(), PINOT_ERR_BAD_ARG, "segment ref: no such engine");
@@ -389,6 +507,7 @@ std::unique_ptr<GroupByResult> server_group_by(ServerImpl &s, const std::vector<
   const size_t E = s.engines.size();
   std::vector<std::unique_ptr<GroupByResult>> res(E);
   std::vector<pinot_exec_stats> tot(E);
+  std::atomic<bool> hashed_result{false};  // rank 0 holds the merged hashed result (the others an empty one)
   for_engines(s, [&](size_t i) {
     Engine &e = *s.engines[i];
     Collective &c = *s.comms[i];
@@ -443,8 +562,64 @@ std::unique_ptr<GroupByResult> server_group_by(ServerImpl &s, const std::vector<
     if (!gkinds.empty()) ks = global_key_space(segs, q, rank_dicts);  // identical on every rank (same inputs)
     ph.mark(1);
     const int64_t limit = q.num_groups_limit > 0 ? q.num_groups_limit : e.num_groups_limit;
-    require(!ks.hashed, PINOT_ERR_UNSUPPORTED,
-            "multi-GPU group-by needs a dense key space (LONG_MAP / ARRAY_MAP shapes: one GPU)");
+    if (ks.hashed) {
+      // LONG_MAP / ARRAY_MAP key spaces (SV or MV): no dense partials to reduce-scatter. Each rank runs its segments'
+      // group-bys one segment at a time (each segment's holder applies its own num.groups.limit admission,
+      // DictionaryBasedGroupKeyGenerator.java:293-302, 459-470), the segments' groups travel to rank 0 by key string,
+      // and rank 0 merges them as CombineGroupByOperator does (merge_rank_groups)
+      pinot_exec_stats st{};
+      Writer wh;
+      std::vector<uint8_t> groups;
+      my = capture([&] {
+        std::lock_guard<std::mutex> el(e.mu);
+        DeadlineScope ds(e, q.timeout_ms);
+        Writer w;
+        w.i64((int64_t)segs.size());
+        for (SegmentData *sg : segs) {
+          pinot_exec_stats s1{};
+          auto r = exec_group_by(e, std::vector<SegmentData *>{sg}, q0, &s1);
+          st.num_docs_scanned += s1.num_docs_scanned;
+          st.num_entries_scanned_in_filter += s1.num_entries_scanned_in_filter;
+          st.num_entries_scanned_post_filter += s1.num_entries_scanned_post_filter;
+          st.num_segments_processed += s1.num_segments_processed;
+          st.num_segments_matched += s1.num_segments_matched;
+          st.device_ms += s1.device_ms;
+          put_groups(w, *r);
+        }
+        groups = std::move(w.b);
+      });
+      put_status(wh, my);
+      put_stats(wh, st);
+      wh.raw(groups.data(), groups.size());
+      const auto all_h = c.all_gather_host(wh.b, e.stream);
+      sts.clear();
+      std::vector<size_t> offs;
+      for (const auto &blob : all_h) {
+        Reader rd{blob};
+        sts.push_back(get_status(rd));
+        add_stats(rd, tot[i]);
+        offs.push_back(rd.p);
+      }
+      tot[i].num_total_raw_docs = total_docs;
+      fail_together(sts, me, "group-by");
+      ph.mark(2);
+      if (me == 0 || !s.gather) {
+        const int64_t trim_size = std::max<int64_t>(5 * (int64_t)top_n, 5000);
+        if (me == 0) {
+          res[i] = merge_rank_groups(q0, all_h, offs, 2 * limit);
+          const int64_t n = (int64_t)res[i]->raw_keys.size();
+          if (top_n > 0 && n > 4 * trim_size)
+            server_trim_select(*res[i], top_n, std::vector<uint32_t>((size_t)n, 0xFFFFFFFFu), n);
+        } else {
+          res[i] = empty_group_result(q0);
+        }
+      } else {
+        res[i] = empty_group_result(q0);
+      }
+      ph.mark(6);
+      hashed_result = true;
+      return;
+    }
     if (gkinds.empty() || ks.G == 0) {  // no rank holds a segment after pruning: no group
       res[i] = empty_group_result(q);
       tot[i].num_total_raw_docs = total_docs;
@@ -568,26 +743,61 @@ std::unique_ptr<GroupByResult> server_group_by(ServerImpl &s, const std::vector<
     c.group_end();
     if (e.timing) PINOT_HIP(hipStreamSynchronize(e.stream));  // the merge's device time on its own
     ph.mark(4);
-    // D: owner finalize of this rank's key range, then the gather to rank 0
+    // D: owner finalize of this rank's key range, then the gather to rank 0. A trimmed answer (top_n: the server's
+    // AggregationGroupByTrimmingService, CombineGroupByOperator.java:184-187) first learns the merged map's size (every
+    // range's non-empty keys); above 4 x trimSize each rank keeps its range's trimSize best groups per function — the
+    // merged map's best are among them, the ranges being disjoint — so only those leave the owner ranks
     const int64_t base = (int64_t)me * slice;
     const int64_t g = std::max<int64_t>(0, std::min<int64_t>(slice, G - base));
     std::vector<void *> sl(na, nullptr);
     for (int a = 0; a < na; a++)
       if (accs[a]) sl[a] = static_cast<uint8_t *>(accs[a]) + (size_t)base * acc_unit(gkinds[a]);
-    const DenseOut own = slice_outputs(e, q, gkinds, counts + base, sl, g, base);
+    long long *keys_dev = nullptr;
+    const unsigned long long nr = slice_compact(e, counts + base, g, keys_dev);
+    // (not with hidden CountMV functions: those leave the function list after the merge; the caller's trim applies)
+    const bool top = top_n > 0 && (s.gather || R == 1) && hidden.empty();
+    int64_t merged = (int64_t)nr;
+    if (top && R > 1) {
+      Writer wg;
+      wg.i64((int64_t)nr);
+      const auto all_g = c.all_gather_host(wg.b, e.stream);
+      merged = 0;
+      for (int r = 0; r < R; r++) {
+        Reader rd{all_g[r]};
+        merged += rd.i64();
+      }
+    }
+    const int64_t trim_size = std::max<int64_t>(5 * (int64_t)top_n, 5000);
+    const bool trim = top && merged > 4 * trim_size;
+    std::vector<uint32_t> flags;
+    const DenseOut own = slice_outputs_keys(e, q, gkinds, counts + base, sl, g, base, keys_dev, nr, trim ? top_n : 0, flags);
     ph.mark(5);
     if (!s.gather || R == 1) {
       res[i] = slice_result(e, q, ks.gcard, ks.gvalues, own);
+      if (trim) server_trim_select(*res[i], top_n, flags, merged);
       ph.mark(6);
       return;
     }
     Writer wn;
     wn.i64((int64_t)own.n);
+    if (trim) {
+      std::vector<uint8_t> fb(flags.size() * 4);
+      if (!fb.empty()) memcpy(fb.data(), flags.data(), fb.size());
+      wn.bytes(fb);
+    }
     const auto all_n = c.all_gather_host(wn.b, e.stream);
     std::vector<size_t> prefix(R + 1, 0);
+    std::vector<uint32_t> all_flags;
     for (int r = 0; r < R; r++) {
       Reader rd{all_n[r]};
       prefix[r + 1] = prefix[r] + (size_t)rd.i64();
+      if (trim) {
+        const std::vector<uint8_t> fb = rd.bytes();
+        require(fb.size() == (prefix[r + 1] - prefix[r]) * 4, PINOT_ERR_DEVICE, "server trim: flags of another size");
+        const size_t at = all_flags.size();
+        all_flags.resize(at + fb.size() / 4);
+        if (!fb.empty()) memcpy(all_flags.data() + at, fb.data(), fb.size());
+      }
     }
     const DenseOut root = me == 0 ? slice_alloc(e, q, gkinds, prefix[R]) : DenseOut{};
     const auto send = slice_arrays(own);
@@ -602,6 +812,7 @@ std::unique_ptr<GroupByResult> server_group_by(ServerImpl &s, const std::vector<
     c.group_end();
     if (me == 0) {
       res[i] = slice_result(e, q, ks.gcard, ks.gvalues, root);
+      if (trim) server_trim_select(*res[i], top_n, all_flags, merged);
     } else {
       DenseOut none;
       none.kind = gkinds;
@@ -611,6 +822,10 @@ std::unique_ptr<GroupByResult> server_group_by(ServerImpl &s, const std::vector<
     ph.mark(6);
   });
   std::unique_ptr<GroupByResult> out = std::move(res[0]);
+  if (hashed_result) {  // merged on rank 0 with the query's own functions (no hidden CountMV)
+    if (stats) *stats = tot[0];
+    return out;
+  }
   if (!s.gather && E > 1) {  // one process, several GPUs, key ranges kept apart: concatenate them (ascending)
     for (size_t i = 1; i < E; i++) {
       GroupByResult &x = *res[i];

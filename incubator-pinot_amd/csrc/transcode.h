@@ -16,5 +16,7 @@ namespace pinot {
 // num_bits_per_value(card - 1) bits in fwd (FixedBitIntReaderWriter, the host pack_ids bytes).
 void transcode_numeric_device(const uint8_t *raw, uint64_t n, int w, int data_type, hipStream_t stream,
                               std::vector<uint64_t> &uniq, std::vector<uint8_t> &fwd);
+// HBM the device transcode of n values of w bytes allocates (its scratch buffer, hipcub's temporaries included).
+size_t transcode_numeric_device_bytes(uint64_t n, int w, hipStream_t stream);
 
 }  // namespace pinot

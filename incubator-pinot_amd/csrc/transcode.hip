@@ -77,20 +77,42 @@ unsigned grid_for(uint64_t n) { return (unsigned)std::max<uint64_t>(1, std::min<
 
 }  // namespace
 
+namespace {
+struct TranscodeSizes {
+  size_t a8, a4, raw_b, tmp_b;
+  size_t total() const { return raw_b + 3 * a8 + 5 * a4 + tmp_b + 256; }
+};
+
+TranscodeSizes transcode_sizes(uint64_t n, int w, hipStream_t stream) {
+  TranscodeSizes z;
+  z.a8 = (n * 8 + 255) / 256 * 256;
+  z.a4 = (n * 4 + 255) / 256 * 256;
+  z.raw_b = (n * (uint64_t)w + 255) / 256 * 256;
+  size_t sort_b = 0, scan_b = 0;
+  PINOT_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_b, (const unsigned long long *)nullptr,
+                                               (unsigned long long *)nullptr, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                                               (int)n, 0, w * 8, stream));
+  PINOT_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, scan_b, (const uint32_t *)nullptr, (uint32_t *)nullptr, (int)n, stream));
+  z.tmp_b = std::max(sort_b, scan_b);
+  return z;
+}
+}  // namespace
+
+size_t transcode_numeric_device_bytes(uint64_t n, int w, hipStream_t stream) {
+  if (n == 0 || n >= (1ull << 31)) return 0;
+  return transcode_sizes(n, w, stream).total();
+}
+
 void transcode_numeric_device(const uint8_t *raw, uint64_t n, int w, int data_type, hipStream_t stream,
                               std::vector<uint64_t> &uniq, std::vector<uint8_t> &fwd) {
   uniq.clear();
   fwd.clear();
   if (n == 0) return;
   require(n < (1ull << 31), PINOT_ERR_UNSUPPORTED, "device transcode over 2^31 docs");
-  const size_t a8 = (n * 8 + 255) / 256 * 256, a4 = (n * 4 + 255) / 256 * 256;
-  size_t sort_b = 0, scan_b = 0;
-  PINOT_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_b, (const unsigned long long *)nullptr,
-                                               (unsigned long long *)nullptr, (const uint32_t *)nullptr, (uint32_t *)nullptr,
-                                               (int)n, 0, w * 8, stream));
-  PINOT_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, scan_b, (const uint32_t *)nullptr, (uint32_t *)nullptr, (int)n, stream));
-  const size_t raw_b = (n * (uint64_t)w + 255) / 256 * 256;
-  DeviceBuffer buf(raw_b + 3 * a8 + 5 * a4 + std::max(sort_b, scan_b) + 256);
+  const TranscodeSizes z = transcode_sizes(n, w, stream);
+  const size_t a8 = z.a8, a4 = z.a4, raw_b = z.raw_b;
+  size_t sort_b = z.tmp_b, scan_b = z.tmp_b;
+  DeviceBuffer buf(z.total());
   uint8_t *p = buf.get<uint8_t>();
   uint8_t *d_raw = p;
   auto *keys = reinterpret_cast<unsigned long long *>(p + raw_b);

@@ -244,19 +244,37 @@ __global__ __launch_bounds__(kTrimBlock) void k_trim_ties(TrimArgs a, uint32_t *
   if (tid < a.nf) ties[(size_t)tid * gridDim.x + blockIdx.x] = s[tid];
 }
 
+// ties[f][*] -> its exclusive prefix sums in place (one block per function): the ties of K in each block's earlier
+// blocks, read by k_trim_flags (linear in the blocks, whatever the group count).
+__global__ __launch_bounds__(kTrimBlock) void k_trim_tie_scan(uint32_t *ties, unsigned blocks) {
+  __shared__ uint32_t scan[kTrimBlock];
+  const int tid = threadIdx.x;
+  uint32_t *t = ties + (size_t)blockIdx.x * blocks;
+  uint32_t carry = 0;
+  for (unsigned c0 = 0; c0 < blocks; c0 += kTrimBlock) {
+    const unsigned i = c0 + (unsigned)tid;
+    const uint32_t v = i < blocks ? t[i] : 0u;
+    scan[tid] = v;
+    __syncthreads();
+    for (int o = 1; o < kTrimBlock; o <<= 1) {
+      const uint32_t x = tid >= o ? scan[tid - o] : 0u;
+      __syncthreads();
+      scan[tid] += x;
+      __syncthreads();
+    }
+    if (i < blocks) t[i] = carry + scan[tid] - v;
+    carry += scan[kTrimBlock - 1];
+    __syncthreads();
+  }
+}
+
 __global__ __launch_bounds__(kTrimBlock) void k_trim_flags(TrimArgs a, const uint32_t *__restrict__ ties,
                                                            uint32_t *__restrict__ flags) {
   __shared__ uint32_t scan[kTrimBlock];
   __shared__ unsigned long long base[kTrimMaxFns];
   const int tid = threadIdx.x;
   const unsigned b = blockIdx.x;
-  if (tid < a.nf) base[tid] = 0;
-  __syncthreads();
-  for (int f = 0; f < a.nf; f++) {  // ties of K in the earlier blocks
-    unsigned long long c = 0;
-    for (unsigned j = tid; j < b; j += kTrimBlock) c += ties[(size_t)f * gridDim.x + j];
-    if (c) atomicAdd(&base[f], c);
-  }
+  if (tid < a.nf) base[tid] = ties[(size_t)tid * gridDim.x + b];  // ties of K in the earlier blocks (k_trim_tie_scan)
   __syncthreads();
   const long long i0 = (long long)b * kTrimTile + (long long)tid * kTrimPerThread;
   uint32_t m[kTrimPerThread] = {};
@@ -353,6 +371,7 @@ void launch_trim_radix(const TrimFn *fns, int nf, const long long *counts, long 
     hipLaunchKernelGGL(k_trim_pick, dim3(1), dim3(kTrimPickBlock), 0, stream, a, r);
   }
   hipLaunchKernelGGL(k_trim_ties, dim3(grid), dim3(kTrimBlock), 0, stream, a, ties);
+  hipLaunchKernelGGL(k_trim_tie_scan, dim3((unsigned)nf), dim3(kTrimBlock), 0, stream, ties, grid);
   hipLaunchKernelGGL(k_trim_flags, dim3(grid), dim3(kTrimBlock), 0, stream, a, ties, flags);
 }
 

@@ -46,7 +46,7 @@ EXPORTED_SYMBOLS = [
     "pinot_gpu_last_kernel_ms", "pinot_gpu_engine_stat", "pinot_segment_read_raw_forward_index",
     "pinot_gpu_server_create", "pinot_gpu_server_unique_id", "pinot_gpu_server_create_rank", "pinot_gpu_server_destroy",
     "pinot_gpu_server_num_engines", "pinot_gpu_server_engine", "pinot_gpu_server_aggregate", "pinot_gpu_server_group_by",
-    "pinot_gpu_server_last_phases", "pinot_gpu_transcode_raw",
+    "pinot_gpu_server_last_phases", "pinot_gpu_transcode_raw", "pinot_gpu_server_group_by_top",
 ]
 
 
@@ -228,6 +228,8 @@ def load(path=None):
                                              C.POINTER(ExecStats)]),
         "pinot_gpu_server_group_by": (i32, [P, C.POINTER(SegmentRef), i32, C.POINTER(Query), C.POINTER(P),
                                             C.POINTER(ExecStats)]),
+        "pinot_gpu_server_group_by_top": (i32, [P, C.POINTER(SegmentRef), i32, C.POINTER(Query), i32, C.POINTER(P),
+                                                C.POINTER(ExecStats)]),
         "pinot_gpu_server_last_phases": (i32, [P, C.POINTER(C.c_double), i32]),
     }
     for name, (res, args) in sig.items():

@@ -604,16 +604,49 @@ class ServerExecutor:
             arr[i].handle = s.handle
         return arr
 
+    def _query(self, query):
+        if isinstance(query, PreparedQuery):
+            return query.query, query.marshal
+        if isinstance(query, str):
+            query = compile_pql(query)
+        return query, self._marshal(query)
+
+    def group_by_result(self, query, segments, top_n=None):
+        """(native result, stats) of the merged group-by; top_n: the server's trimmed answer
+        (pinot_gpu_server_group_by_top: each rank trims its own key range before the gather to rank 0)."""
+        res, stats, _ = self._group_by(query, segments, top_n)
+        return res, _stats(stats)
+
+    def _group_by(self, query, segments, top_n):
+        query, m = self._query(query)
+        lib = self.server.lib
+        stats = _lib.ExecStats()
+        out = C.c_void_p()
+        refs = self._refs(segments)
+        if top_n:
+            check(lib.pinot_gpu_server_group_by_top(self.server.ptr, refs, len(segments), C.byref(m.q), top_n,
+                                                    C.byref(out), C.byref(stats)))
+        else:
+            check(lib.pinot_gpu_server_group_by(self.server.ptr, refs, len(segments), C.byref(m.q), C.byref(out),
+                                                C.byref(stats)))
+        return GroupByResult(lib, out, query), stats, m
+
+    def process_query_datatable(self, query, segments, trim=True, server=None, zero_copy=False):
+        """The server's answer to the broker as DataTable bytes (rank 0's; the other ranks' results are empty):
+        group-bys trimmed per function on the device across the ranks when `trim`."""
+        query, m = self._query(query)
+        if not query.get("group_by"):
+            raise ValueError("process_query_datatable on the multi-GPU server serves group-by queries")
+        top_n = query["group_by"].get("top_n", 10) if trim else None
+        res, stats, m = self._group_by(PreparedQuery(query, m), segments, top_n)
+        srv = C.byref(_lib.DataTableServer(*server)) if server else None
+        return res.data_table(m, stats, top_n, srv, zero_copy), _stats(stats)
+
     def process_query(self, query, segments, trim=True, as_result=False):
         """Every rank calls this with its own segments (possibly none): pruning (the executor's pruners, carried in
         the query) and the merge across GPUs / ranks happen inside the library, where a failure on any rank fails
         every rank with the same status instead of leaving peers in a collective."""
-        if isinstance(query, PreparedQuery):
-            query, m = query.query, query.marshal
-        else:
-            if isinstance(query, str):
-                query = compile_pql(query)
-            m = self._marshal(query)
+        query, m = self._query(query)
         lib = self.server.lib
         refs = self._refs(segments)
         stats = _lib.ExecStats()

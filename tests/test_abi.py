@@ -30,7 +30,7 @@ def test_library_exports_header_symbols():
 
 def test_abi_version_and_error_path_without_gpu():
     lib = _lib.load()
-    assert lib.pinot_gpu_abi_version() == 13
+    assert lib.pinot_gpu_abi_version() == 14
     if lib.pinot_gpu_device_count() == 0:
         ptr = ctypes.c_void_p()
         st = lib.pinot_gpu_engine_create(0, None, ctypes.byref(ptr))

@@ -104,6 +104,18 @@ def test_group_by_datatable_trimmed_per_function_and_limit_flag(engine):
     assert len(exp) == len(keys)
     view, _ = ex.process_query_datatable(q, [g], trim=True, zero_copy=True)  # the native buffer, no copy
     assert isinstance(view, memoryview) and view.readonly and bytes(view) == data
+    # two zero-copy views of one result (trimmed, then untrimmed): the second call must not free the first's bytes
+    from pinot_amd import _lib
+    from pinot_amd.executor import QueryMarshal
+    m = QueryMarshal(q, 50_000, ex.max_init, ex.timeout_ms)
+    v1 = res.data_table(m, _lib.ExecStats(), 10, None, True)
+    c1 = bytes(v1)
+    v2 = res.data_table(m, _lib.ExecStats(), None, None, True)
+    c2 = bytes(v2)
+    assert len(c2) > len(c1) and bytes(v1) == c1 and bytes(v2) == c2
+    assert D.decode(c1)["cells"][0][1].keys() <= D.decode(c2)["cells"][0][1].keys()
+    del res
+    assert bytes(v1) == c1  # the views keep the result (and its buffers) alive
     g.release()
 
 

@@ -365,3 +365,92 @@ def test_loopback_mv_group_by(K):
             assert len(exp) == 2 * limit  # the cap binds
         _check(q, got, exp)
     srv.close()
+
+
+def _wide_segments(rng, n, nseg):
+    """Segments of ~60,000 group keys (more than 4 x trimSize at TOP 10): the server trim binds."""
+    return [build_segment("wide%d" % i, {
+        "k": ("INT", rng.integers(0, 60_000, n).tolist()),
+        "j": ("INT", rng.integers(0, 3, n).tolist()),
+        "m": ("INT", rng.integers(-5000, 1_000_000, n).tolist()),
+        "h": ("INT", rng.integers(0, 50, n).tolist())}) for i in range(nseg)]
+
+
+@pytest.mark.parametrize("K", [2, 3, 8])
+def test_loopback_trimmed_server_answer(K):
+    """pinot_gpu_server_group_by_top: each rank trims its own key range (its trimSize best groups per function) before
+    the gather, rank 0 picks each function's trimSize best among them. The DataTable equals the one-engine device-trimmed
+    answer over the same segments (itself checked against the host trim), every kept value equals the oracle's merged
+    map, and below 4 x trimSize groups nothing is trimmed."""
+    import datatable as D
+    from pinot_amd import GpuEngine, ServerQueryExecutor
+    rng = np.random.default_rng(500 + K)
+    host = _wide_segments(rng, 60_000, 5)
+    srv = GpuServer([0] * K, "server.loopback=1")
+    gsegs = [srv.engines[i % K].register(s) for i, s in enumerate(host)]
+    ex = ServerExecutor(srv, num_groups_limit=1_000_000)
+    eng = GpuEngine(0)
+    esegs = [eng.register(s) for s in host]
+    ee = ServerQueryExecutor(eng, num_groups_limit=1_000_000)
+    for text, trimmed in (("SELECT COUNT(*), SUM(m), MIN(m), AVG(m), DISTINCTCOUNTHLL(h) FROM t GROUP BY k TOP 10", True),
+                          ("SELECT MAX(m), COUNT(*) FROM t WHERE h < 10 GROUP BY k, j TOP 20", True),
+                          ("SELECT SUM(m), COUNT(*) FROM t WHERE k < 15000 GROUP BY k TOP 10", False)):
+        q = compile_pql(text)
+        data, st = ex.process_query_datatable(q, gsegs, trim=True)
+        ref, _ = ee.process_query_datatable(q, esegs, trim=True)
+        d, r = D.decode(data), D.decode(ref)
+        assert d["cells"] == r["cells"], text
+        md = dict(d["metadata"])
+        assert md.get("numGroupsLimitReached") == dict(r["metadata"]).get("numGroupsLimitReached")
+        exp, _ = O.execute_server(host, q, num_groups_limit=1_000_000)
+        T = max(5 * q["group_by"].get("top_n", 10), 5000)
+        for i, (a, row) in enumerate(zip(q["aggregations"], d["cells"])):
+            got = row[1]
+            assert len(got) == (T if trimmed else len(exp)), (text, i)
+            f = a["function"].upper()
+            for k, v in list(got.items())[:300]:
+                e = exp[k][i]
+                if f == "AVG":
+                    assert v[1] == e[1] and abs(v[0] - e[0]) <= 1e-9 * max(1.0, abs(e[0]))
+                elif f == "DISTINCTCOUNTHLL":
+                    assert v == [int(x) for x in e.reg]  # the registers (HyperLogLog.getBytes decoded)
+                else:
+                    assert v == e, (text, k, f)
+        # the untrimmed merged result still holds every group
+        res, _ = ex.group_by_result(q, gsegs)
+        assert res.num_groups() == len(exp)
+        del res
+    srv.close()
+    eng.close()
+
+
+@pytest.mark.parametrize("K", [2, 3, 8])
+def test_loopback_hashed_key_space(K):
+    """Group-bys over key spaces past the dense limit (LONG_MAP / ARRAY_MAP holders; MV and SV group columns) across K
+    ranks: each rank runs its segments' group-bys (each segment's holder admission applied locally), rank 0 merges
+    the segments' groups by key string in rank then segment order (CombineGroupByOperator.java:142-161) with the
+    2 x num.groups.limit cap — equal to the oracle over the segments in that order, with and without the cap
+    binding (DictionaryBasedGroupKeyGenerator.java:459-470)."""
+    from test_gpu_mv import hashed_mv_segment, _check as _check_mv
+    rng = np.random.default_rng(900 + K)
+    host = [hashed_mv_segment(rng, 12000, "hk%d" % i) for i in range(4)]
+    srv = GpuServer([0] * K, "server.loopback=1")
+    gsegs = [srv.engines[i % K].register(s) for i, s in enumerate(host)]
+    order = [host[i] for r in range(K) for i in range(len(host)) if i % K == r]  # the server's merge order
+    aggs = [{"function": "COUNT", "column": "*"}, {"function": "SUMMV", "column": "tags"},
+            {"function": "AVGMV", "column": "tags"}, {"function": "SUM", "column": "m"},
+            {"function": "DISTINCTCOUNTHLLMV", "column": "tags"}, {"function": "MIN", "column": "m"}]
+    for cols, limit, thr in ((["hv", "hs"], None, None), (["hs", "m", "g"], None, None), (["hv", "hs"], 500, 10)):
+        q = {"aggregations": aggs, "filter": {"operator": "RANGE", "column": "m", "values": ["[-500\t\t900)"]},
+             "group_by": {"columns": cols, "top_n": 10}}
+        ex = ServerExecutor(srv, num_groups_limit=limit or 100000, max_init_group_holder_capacity=thr or 10000)
+        got, st = ex.process_query(q, gsegs, trim=False)
+        okw = {} if limit is None else {"num_groups_limit": limit, "array_threshold": thr}
+        exp, scanned = O.execute_server(order, q, **okw)
+        assert st.num_docs_scanned == scanned and st.num_total_raw_docs == 4 * 12000
+        assert len(exp) > (2 * limit if limit else 10000) // 2
+        _check_mv(q, got, exp)
+        # the trimmed answer (TOP 10 -> 5,000 per function when more than 20,000 groups) keeps each function's best
+        data, _ = ex.process_query_datatable(q, gsegs, trim=True)
+        assert b"sumMV_tags" in data
+    srv.close()

@@ -319,6 +319,67 @@ def test_wide_bitmap_leaf_in_registers():
     e.close()
 
 
+def _leaf(col, op, vals):
+    return {"operator": op, "column": col, "values": vals}
+
+
+def test_depth5_tree_with_1000_id_bitmap_leaf_fused():
+    """A filter nested five levels deep (AND / OR alternating, a bushy level among them) with a 1,000-dictId IN on a
+    bitmap-indexed column at the bottom: the planner starts each term with its deepest child, and the wide bitmap leaf
+    ORs its containers listed per roaring key inside the launch — no segment takes the dense-bitset launch sequence
+    (exec.last_pre_segments == 0) — for the aggregation kernel and the group-by kernel, equal to the oracle
+    (FilterOperatorUtils.java:74-122, BitmapBasedFilterOperator.java:69-84)."""
+    rng = np.random.default_rng(2300)
+    segs = []
+    for i, n in enumerate((200_000, 131_073)):
+        segs.append(build_segment("deep%d" % i, {
+            "b": ("INT", rng.integers(0, 4000, n).tolist()),
+            "a": ("INT", rng.integers(0, 100, n).tolist()),
+            "c": ("INT", rng.integers(0, 50, n).tolist()),
+            "d": ("INT", rng.integers(0, 10, n).tolist()),
+            "f": ("INT", rng.integers(0, 30, n).tolist()),
+            "g": ("INT", rng.integers(0, 7, n).tolist()),
+            "m": ("INT", rng.integers(-1000, 100000, n).tolist())}, inverted_columns=("b",)))
+    ids = "\t\t".join(str(v) for v in sorted(rng.choice(4000, 1000, replace=False)))
+    wide = _leaf("b", "IN", [ids])
+    deep = {"operator": "AND", "children": [
+        _leaf("a", "RANGE", ["[5\t\t95)"]),
+        {"operator": "OR", "children": [
+            _leaf("c", "RANGE", ["[0\t\t3)"]),
+            {"operator": "AND", "children": [
+                _leaf("d", "NOT_IN", ["9"]),
+                {"operator": "OR", "children": [
+                    {"operator": "AND", "children": [_leaf("g", "IN", ["1\t\t2"]), _leaf("f", "RANGE", ["[0\t\t20)"])]},
+                    {"operator": "AND", "children": [
+                        _leaf("f", "RANGE", ["[10\t\t30)"]),
+                        {"operator": "OR", "children": [wide, _leaf("g", "EQUALITY", ["5"])]}]}]}]}]}]}
+    bushy = {"operator": "OR", "children": [  # every level holds two composite children (needs the register stack)
+        {"operator": "AND", "children": [
+            {"operator": "OR", "children": [_leaf("a", "RANGE", ["[0\t\t10)"]), _leaf("c", "EQUALITY", ["4"])]},
+            {"operator": "OR", "children": [_leaf("d", "IN", ["1\t\t2"]), wide]}]},
+        {"operator": "AND", "children": [
+            {"operator": "OR", "children": [_leaf("f", "RANGE", ["[0\t\t5)"]), _leaf("g", "EQUALITY", ["3"])]},
+            {"operator": "OR", "children": [_leaf("a", "RANGE", ["[50\t\t60)"]), _leaf("d", "NOT_IN", ["0\t\t1"])]}]}]}
+    e = GpuEngine(0, "filter.force=index")
+    gsegs = [e.register(s) for s in segs]
+    ex = ServerQueryExecutor(e)
+    for tree in (deep, bushy, {"operator": "AND", "children": [wide, _leaf("a", "RANGE", ["[0\t\t50)"])]}):
+        q = {"aggregations": [{"function": "COUNT", "column": "*"}, {"function": "SUM", "column": "m"},
+                              {"function": "MAX", "column": "m"}], "filter": tree, "group_by": None}
+        got, st = ex.process_query(q, gsegs)
+        exp, scanned = O.execute_server(segs, q)
+        assert st.num_docs_scanned == scanned and got == exp, tree
+        assert e.stat("exec.last_pre_segments") == 0, tree
+        qg = dict(q, group_by={"columns": ["g"], "top_n": 10})
+        gotg, stg = ex.process_query(qg, gsegs, trim=False)
+        expg, scg = O.execute_server(segs, qg)
+        assert stg.num_docs_scanned == scg and set(gotg) == set(expg)
+        for k in expg:
+            assert gotg[k][0] == expg[k][0] and gotg[k][1] == expg[k][1] and gotg[k][2] == expg[k][2], k
+        assert e.stat("exec.last_pre_segments") == 0, tree
+    e.close()
+
+
 @pytest.mark.parametrize("seed", range(6))
 def test_random_aggregations(engine, seed):
     rng = np.random.default_rng(200 + seed)

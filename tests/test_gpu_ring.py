@@ -62,14 +62,19 @@ def _run(e, q, gsegs, host, limit=1 << 22, qfilter=None):
     return e.stat("group.ring_queries") - before[0], e.stat("group.ring_fallbacks") - before[1]
 
 
-def test_ring_config4_shape():
+@pytest.mark.parametrize("hll,rec6", [(1, 1), (0, 1), (1, 0), (0, 0)])
+def test_ring_config4_shape(hll, rec6):
     """Config 4's query and table at 2 x 2M docs: 1M keys in 977 partitions of 1024, SUM / AVG over the 20-bit d8
-    (count packed beside the dictId sum), HLL over the 16-bit d5 (~120 ranks > 15 across the groups)."""
-    e = GpuEngine(0, "group.ring=1")
+    (count packed beside the dictId sum), HLL over the 16-bit d5 (~120 ranks > 15 across the groups). hll: the
+    scatter computes d5's HLL (register, rank) field (else the reduce hashes d5's dictId); rec6: 6-byte records (the
+    10-bit local key + 20-bit d8 + 13-bit HLL field or 16-bit d5 dictId fit 48 bits)."""
+    e = GpuEngine(0, "group.ring=1;group.ring_hll=%d;group.ring_rec6=%d" % (hll, rec6))
     gsegs = [e.register_synthetic("fact_%d" % s, 2_000_000, CONFIG_COLUMNS, BASE_SEED + s) for s in range(2)]
     host = [synth.make_segment("fact_%d" % s, 2_000_000, CONFIG_COLUMNS, BASE_SEED + s) for s in range(2)]
     ran, fell = _run(e, compile_pql(CONFIG4), gsegs, host, limit=1_000_000, qfilter=True)
-    assert (ran, fell) == (1, 0)
+    assert (ran, fell) == (1, 0), "ring status %d" % e.stat("group.ring_last_status")
+    assert e.stat("group.ring_rec_bytes") == (6 if rec6 else 8)
+    assert e.stat("group.ring_hll_slot") == hll
     # the same query with the filter as GB_FILTER's words
     e.set_config("group.ring_qfilter=0")
     ran, fell = _run(e, compile_pql(CONFIG4), gsegs, host, limit=1_000_000, qfilter=False)
@@ -114,6 +119,8 @@ def _mixed_segment(name, n, seed, k1_vals, k2_vals, sorted_ts=False):
     "SELECT MIN(dv), MAX(lv) FROM t WHERE f < 70 GROUP BY k1, k2",
     "SELECT SUM(dv), COUNT(*) FROM t WHERE f >= 10 GROUP BY k2, k1",
     "SELECT SUM(lv), DISTINCTCOUNTHLL(h) FROM t WHERE f <> 5 GROUP BY k1, k2",
+    "SELECT DISTINCTCOUNTHLL(h), COUNT(*) FROM t WHERE f > 3 GROUP BY k2, k1",
+    "SELECT DISTINCTCOUNTHLL(h), MAX(h) FROM t GROUP BY k1, k2",
 ])
 def test_ring_remap_ragged_kinds(text):
     """Three segments of different sizes whose group dictionaries differ (remapped to the union key space), every
@@ -193,4 +200,29 @@ def test_ring_sparse_query_after_wide_records():
                  "SELECT DISTINCTCOUNTHLL(lv) FROM t WHERE f = 3 OR h < 70 GROUP BY k1, k2"):
         ran, fell = _run(e, compile_pql(text), gsegs, segs)
         assert (ran, fell) == (1, 0)
+    e.close()
+
+
+def test_ring_record_forms():
+    """The record width and the scatter-side HLL field by shape (1M keys: 10-bit local keys): two 20-bit aggregated
+    columns beside the local key exceed 48 bits (8-byte records), an HLL over an affine dictionary with values >= 2^32 keeps its dictId (the reduce
+    hashes the 64-bit value), an HLL beside a SUM of the same column keeps its dictId."""
+    n = 600_000
+    rng = np.random.default_rng(41)
+    cols = {"k1": ("INT", rng.integers(0, 1000, n).tolist()), "k2": ("INT", rng.integers(0, 1000, n).tolist()),
+            "x": ("INT", rng.permutation(1 << 20)[:n].tolist()),   # 600,000 distinct values: 20-bit dictIds
+            "y": ("INT", rng.permutation(1 << 20)[:n].tolist()),
+            "big": ("LONG", ((1 << 33) + 5 * rng.integers(0, 4000, n)).tolist()),
+            "h": ("INT", (3 * rng.integers(0, 9000, n)).tolist()),
+            "f": ("INT", rng.integers(0, 10, n).tolist())}
+    segs = [build_segment("rf0", cols)]
+    e = GpuEngine(0, "group.mode=partition;group.ring=1")
+    gsegs = [e.register(s) for s in segs]
+    for text, rb, hs in (("SELECT SUM(x), MAX(y) FROM t WHERE f < 8 GROUP BY k1, k2", 8, 0),
+                         ("SELECT SUM(x), DISTINCTCOUNTHLL(h) FROM t WHERE f < 8 GROUP BY k1, k2", 6, 1),
+                         ("SELECT DISTINCTCOUNTHLL(big), COUNT(*) FROM t WHERE f < 9 GROUP BY k1, k2", 6, 0),
+                         ("SELECT DISTINCTCOUNTHLL(h), SUM(h) FROM t GROUP BY k2, k1", 6, 0)):
+        ran, fell = _run(e, compile_pql(text), gsegs, segs)
+        assert (ran, fell) == (1, 0), text
+        assert (e.stat("group.ring_rec_bytes"), e.stat("group.ring_hll_slot")) == (rb, hs), text
     e.close()

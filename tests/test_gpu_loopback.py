@@ -367,7 +367,7 @@ def test_loopback_mv_group_by(K):
     srv.close()
 
 
-def _wide_segments(rng, n, nseg):
+def _trim_segments(rng, n, nseg):
     """Segments of ~60,000 group keys (more than 4 x trimSize at TOP 10): the server trim binds."""
     return [build_segment("wide%d" % i, {
         "k": ("INT", rng.integers(0, 60_000, n).tolist()),
@@ -385,7 +385,7 @@ def test_loopback_trimmed_server_answer(K):
     import datatable as D
     from pinot_amd import GpuEngine, ServerQueryExecutor
     rng = np.random.default_rng(500 + K)
-    host = _wide_segments(rng, 60_000, 5)
+    host = _trim_segments(rng, 60_000, 5)
     srv = GpuServer([0] * K, "server.loopback=1")
     gsegs = [srv.engines[i % K].register(s) for i, s in enumerate(host)]
     ex = ServerExecutor(srv, num_groups_limit=1_000_000)

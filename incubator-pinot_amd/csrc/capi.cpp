@@ -151,6 +151,7 @@ void parse_config(Engine &e, const char *cfg) {
     else if (k == "group.ring") e.group_ring = v == "1" || v == "true";
     else if (k == "group.ring_qfilter") e.group_ring_qfilter = v == "1" || v == "true";
     else if (k == "group.ring_hll") e.group_ring_hll = v == "1" || v == "true";
+    else if (k == "group.lds_qfilter") e.group_lds_qfilter = v == "1" || v == "true";
     else if (k == "group.ring_rec6") e.group_ring_rec6 = v == "1" || v == "true";
     else if (k == "raw.device") e.raw_device = v == "1" || v == "true";
     else if (k == "group.aligned") e.group_aligned = v == "1" || v == "true";

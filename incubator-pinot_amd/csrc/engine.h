@@ -272,8 +272,9 @@ struct Engine {
   bool raw_device = true;     // raw.device: raw numeric columns transcoded on the device at registration (transcode.h)
   int64_t raw_device_columns = 0;  // columns the device transcoded
   int64_t raw_host_fallbacks = 0;  // raw numeric columns transcoded on the host for want of free HBM
+  bool group_lds_qfilter = true;   // group.lds_qfilter: the LDS group-by evaluates a one-leaf filter per quarter
   bool group_ring_hll = true;      // group.ring_hll: the ring scatter computes HLL (register, rank) fields (affine columns)
-  bool group_ring_rec6 = true;     // group.ring_rec6: 6-byte ring records when the fields fit 48 bits
+  bool group_ring_rec6 = false;    // group.ring_rec6: 6-byte ring records when the fields fit 48 bits (measured slower)
   bool group_ring_qfilter = true;  // group.ring_qfilter: the ring kernel evaluates simple filters itself (else GB_FILTER)
   int32_t trim_top_n = 0;      // per call (pinot_gpu_group_by_top): trim the group-by on the device for this TOP n
   int64_t ring_queries = 0;    // group-bys launched on the ring plan

@@ -1684,6 +1684,25 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     a.verify_err = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(matched) + S * 8 + 16);
   }
   if (gp.mode == GB_LDS) a.emit_block = e.group_lds_block;  // block size of the lane-owns-quarter GB_LDS instance
+  // GB_LDS with <= 3 read columns: a filter of at most one scan leaf per segment (<= 12 bits) evaluated per quarter
+  // from its own lane-owns-quarter loads (GroupArgs.qfilter): no LDS chunk staging
+  if (gp.mode == GB_LDS && a.lw == 2 && a.pf_nc > 0 && a.pf_nc <= 3 && a.emit_block != 256 && e.group_lds_qfilter &&
+      !pin) {
+    bool qf = true;
+    for (const GroupSegment &g : gsegs) {
+      if (g.nwords == 0) continue;
+      qf = qf && g.n_leaves <= 1;
+      for (int i = 0; i < g.n_leaves && qf; i++) {
+        const FusedStep &l = leaves[g.first_leaf + i];
+        qf = l.join == JOIN_NEW && l.bits <= kGroupMaxFusedLeafBits &&
+             (l.kind == FK_LEAF_RANGE || l.kind == FK_LEAF_LUT64 || l.kind == FK_LEAF_LUT);
+      }
+    }
+    if (qf) {
+      a.qfilter = 1;
+      a.stage_bytes = 0;
+    }
+  }
   int64_t max_chunks = 1;  // chunks in the largest segment window
   for (const GroupSegment &g : gsegs) max_chunks = std::max<int64_t>(max_chunks, g.ch_end - g.ch_begin);
   const int64_t resident = (int64_t)group_query_blocks_per_cu(a) * e.num_cus;

@@ -889,6 +889,94 @@ __device__ __forceinline__ void lq_process(const GroupArgs &a, const GroupSegmen
   }
 }
 
+// A lane's raw dwords of a quarter of a column of <= 12 bits (7 dwords at most: two 16-B loads).
+__device__ __forceinline__ void load_raw_lq8(const uint8_t *fwd, int bits, int64_t qi, uint32_t (&R)[8]) {
+  const uint32_t *p = reinterpret_cast<const uint32_t *>(fwd) + ((qi * bits) >> 1);
+  const u32x4a x0 = gload<u32x4a>(p), x1 = gload<u32x4a>(p + 4);
+  R[0] = x0.x; R[1] = x0.y; R[2] = x0.z; R[3] = x0.w;
+  R[4] = x1.x; R[5] = x1.y; R[6] = x1.z; R[7] = x1.w;
+}
+
+// The predicate bits (bit j = value j) of a quarter-form scan leaf (FusedStep of <= 12 bits) over a lane's 16 values.
+struct LeafQuarterBits {
+  const FusedStep &st;
+  uint32_t m;
+  template <int J>
+  __device__ __forceinline__ void put(uint32_t id) {
+    uint32_t x;
+    if (st.kind == FK_LEAF_RANGE) x = id - st.lo < st.span ? 1u : 0u;
+    else if (st.kind == FK_LEAF_LUT64) x = (uint32_t)(st.lut64 >> (id & 63u)) & 1u;
+    else x = (gload<uint32_t>(static_cast<const uint32_t *>(st.table) + (id >> 5)) >> (id & 31u)) & 1u;
+    m |= x << J;
+  }
+};
+
+template <int B>
+__device__ __forceinline__ uint32_t leaf_quarter_b(const FusedStep &st, const uint32_t (&Rin)[8], int64_t qi) {
+  constexpr int N = (B + 1) / 2 + (B & 1);
+  static_assert(N <= 8, "leaf quarter");
+  uint32_t R[N];
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    R[i] = Rin[i];
+    asm volatile("" : "+v"(R[i]));
+  }
+  uint32_t D[(B + 1) / 2 + 1];
+  if constexpr (B & 1) {
+    const bool odd = qi & 1;
+#pragma unroll
+    for (int i = 0; i + 1 < N; i++) D[i] = odd ? __builtin_amdgcn_alignbit(bswap32(R[i]), bswap32(R[i + 1]), 16) : bswap32(R[i]);
+    D[N - 1] = bswap32(R[N - 1]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < N; i++) D[i] = bswap32(R[i]);
+  }
+  LeafQuarterBits f{st, 0u};
+  decode_quarter_apply<B, 0>(D, f);
+  return (st.negate ? ~f.m : f.m) & 0xFFFFu;
+}
+
+__device__ __forceinline__ uint32_t leaf_quarter(const FusedStep &st, const uint32_t (&R)[8], int64_t qi) {
+  uint32_t m = 0xFFFFu;
+#define PINOT_LQF(B) m = leaf_quarter_b<B>(st, R, qi)
+  PINOT_WIDTH_SWITCH_12(st.bits, PINOT_LQF)
+#undef PINOT_LQF
+  return m;
+}
+
+// GB_LDS with the filter in quarter form (GroupArgs.qfilter): per quarter the leaf's raw dwords are loaded with the
+// group and aggregated columns', the leaf evaluated from registers, the matching docs counted (numDocsScanned), then
+// the sink. `mask` holds the `pre` words only.
+template <int MODE, int NCOL>
+__device__ __forceinline__ void group_chunk_lq_qf(const GroupArgs &a, const GroupSegment &sg, const FusedStep *leaves,
+                                                  int64_t ch, uint64_t mask, int lane, uint32_t *plds,
+                                                  unsigned long long &matched) {
+  const int64_t q0 = ch * 256 + lane;
+#pragma unroll 1
+  for (int q = 0; q < 4; q++) {
+    const int src = 16 * q + (lane >> 2);
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)mask, src, 64);
+    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(mask >> 32), src, 64);
+    uint32_t m = (((lane & 2) ? hi : lo) >> (16 * (lane & 1))) & 0xFFFFu;
+    if (!__any(m != 0)) continue;
+    const LqCols k = lq_cols<MODE>(a, sg);
+    const int64_t qi = q0 + 64 * q;
+    const bool leaf = sg.n_leaves > 0;  // uniform
+    FusedStep st{};
+    uint32_t F[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (leaf) {
+      st = load_const(leaves);
+      load_raw_lq8(st.fwd, st.bits, qi, F);
+    }
+    uint32_t R[NCOL][12];
+    lq_load<NCOL>(k, qi, R);
+    if (leaf) m &= leaf_quarter(st, F, qi);
+    matched += (unsigned long long)__popc(m);
+    if (!__any(m != 0)) continue;
+    lq_process<MODE, NCOL>(a, sg, k, R, qi, m, lane, plds);
+  }
+}
+
 template <int MODE, int NCOL = kGroupPfCols>
 __device__ __forceinline__ void group_chunk_lq(const GroupArgs &a, const GroupSegment &sg, int64_t ch, uint64_t mask,
                                                int lane, uint32_t *plds) {
@@ -1022,6 +1110,11 @@ __global__ __launch_bounds__(BLK, MINW) void k_group_query(GroupArgs a) {
     if (ch >= nchunks) break;  // uniform
     uint64_t mask;
     const int64_t w = ch * 64 + lane;
+    if constexpr (PATH == 5) {  // GB_LDS, quarter-form filter: the `pre` words here, the leaf per quarter
+      mask = chunk_word(sg.pre, sg.nwords, sg.num_docs, ch, lane);
+      if (__any(mask != 0)) group_chunk_lq_qf<MODE, 3>(a, sg, leaves, ch, mask, lane, plds, matched);
+      continue;
+    }
     if constexpr (MODE == GB_EMIT2) {  // the filter words the COUNT pass wrote
       mask = w < sg.nwords ? a.filter_out[(size_t)g * a.filter_stride + w] : 0ull;
     } else {
@@ -1089,6 +1182,7 @@ static void with_group_kernel(const GroupArgs &a, V &&v) {
     case GB_GLOBAL: PINOT_GQ(GB_GLOBAL, 0, kGroupBlock, 1); break;
     case GB_LDS:
       if (lh && a.emit_block == 256) PINOT_GQ(GB_LDS, 3, 256, 3);  // 3 blocks of 4 waves per CU
+      else if (lh && a.pf_nc <= 3 && a.qfilter) PINOT_GQ(GB_LDS, 5, kGroupLwEmitBlock, 4);
       else if (lh && a.pf_nc <= 3) PINOT_GQ(GB_LDS, 4, kGroupLwEmitBlock, 4);
       else if (lh) PINOT_GQ(GB_LDS, 3, kGroupLwEmitBlock, 4);  // 4 waves per SIMD: 2 blocks per CU
       else PINOT_GQ(GB_LDS, 0, kGroupBlock, 1);

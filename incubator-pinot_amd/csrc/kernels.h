@@ -334,6 +334,10 @@ struct GroupArgs {
   // GB_LDS lane-owns-quarter: the doc count rides in the high bits of aggregation lds_pack's affine dictId sum
   // ((1 << lds_sbits) + dictId per doc: one LDS atomic for both); -1 = separate u32 counts
   int32_t lds_pack, lds_sbits;
+  // GB_LDS lane-owns-quarter, <= 3 read columns: every segment's filter is at most one scan leaf of <= 12 bits (RANGE /
+  // LUT64 / LUT, AND-ed with `pre`), evaluated on each quarter from its own lane-owns-quarter loads beside the group and
+  // aggregated columns' (no LDS chunk staging and no wait for it; stage_bytes = 0)
+  int32_t qfilter;
 };
 constexpr int kGroupPfCols = 4;
 constexpr int kGroupLwMaxBits = 20;  // widest column the lane-owns-word decode handles

@@ -62,7 +62,7 @@ def _run(e, q, gsegs, host, limit=1 << 22, qfilter=None):
     return e.stat("group.ring_queries") - before[0], e.stat("group.ring_fallbacks") - before[1]
 
 
-@pytest.mark.parametrize("hll,rec6", [(1, 1), (0, 1), (1, 0), (0, 0)])
+@pytest.mark.parametrize("hll,rec6", [(1, 0), (0, 0), (1, 1), (0, 1)])
 def test_ring_config4_shape(hll, rec6):
     """Config 4's query and table at 2 x 2M docs: 1M keys in 977 partitions of 1024, SUM / AVG over the 20-bit d8
     (count packed beside the dictId sum), HLL over the 16-bit d5 (~120 ranks > 15 across the groups). hll: the
@@ -204,7 +204,7 @@ def test_ring_sparse_query_after_wide_records():
 
 
 def test_ring_record_forms():
-    """The record width and the scatter-side HLL field by shape (1M keys: 10-bit local keys): two 20-bit aggregated
+    """The record width (group.ring_rec6=1) and the flushers' HLL field by shape (1M keys: 10-bit local keys): two 20-bit aggregated
     columns beside the local key exceed 48 bits (8-byte records), an HLL over an affine dictionary with values >= 2^32 keeps its dictId (the reduce
     hashes the 64-bit value), an HLL beside a SUM of the same column keeps its dictId."""
     n = 600_000
@@ -216,7 +216,7 @@ def test_ring_record_forms():
             "h": ("INT", (3 * rng.integers(0, 9000, n)).tolist()),
             "f": ("INT", rng.integers(0, 10, n).tolist())}
     segs = [build_segment("rf0", cols)]
-    e = GpuEngine(0, "group.mode=partition;group.ring=1")
+    e = GpuEngine(0, "group.mode=partition;group.ring=1;group.ring_rec6=1")  # 6-byte records where they fit
     gsegs = [e.register(s) for s in segs]
     for text, rb, hs in (("SELECT SUM(x), MAX(y) FROM t WHERE f < 8 GROUP BY k1, k2", 8, 0),
                          ("SELECT SUM(x), DISTINCTCOUNTHLL(h) FROM t WHERE f < 8 GROUP BY k1, k2", 6, 1),

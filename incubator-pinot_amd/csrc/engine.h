@@ -272,7 +272,8 @@ struct Engine {
   bool raw_device = true;     // raw.device: raw numeric columns transcoded on the device at registration (transcode.h)
   int64_t raw_device_columns = 0;  // columns the device transcoded
   int64_t raw_host_fallbacks = 0;  // raw numeric columns transcoded on the host for want of free HBM
-  bool group_lds_qfilter = true;   // group.lds_qfilter: the LDS group-by evaluates a one-leaf filter per quarter
+  bool group_lds_qfilter = false;  // group.lds_qfilter: the LDS group-by evaluates a one-leaf filter per quarter
+                                   // (measured slower than the staged chunk filter: 1.47 vs 1.15 ms, off by default)
   bool group_ring_hll = true;      // group.ring_hll: the ring scatter computes HLL (register, rank) fields (affine columns)
   bool group_ring_rec6 = false;    // group.ring_rec6: 6-byte ring records when the fields fit 48 bits (measured slower)
   bool group_ring_qfilter = true;  // group.ring_qfilter: the ring kernel evaluates simple filters itself (else GB_FILTER)

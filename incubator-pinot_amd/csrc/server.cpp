@@ -755,7 +755,7 @@ std::unique_ptr<GroupByResult> server_group_by(ServerImpl &s, const std::vector<
     long long *keys_dev = nullptr;
     const unsigned long long nr = slice_compact(e, counts + base, g, keys_dev);
     // (not with hidden CountMV functions: those leave the function list after the merge; the caller's trim applies)
-    const bool top = top_n > 0 && (s.gather || R == 1) && hidden.empty();
+    const bool top = top_n > 0 && (s.gather || R == 1) && na == q0.num_aggregations;
     int64_t merged = (int64_t)nr;
     if (top && R > 1) {
       Writer wg;

@@ -300,15 +300,17 @@ def test_query_timeout_status():
 # ------------------------------------------------------------------ the LDS-privatised group-by (bench `lds_group_by`)
 LDS_QUERIES = [
     # the bench's lds_group_by query: 1,600 keys, COUNT + SUM / AVG of the 20-bit d8 (count packed beside the dictId
-    # sum); 3 read columns and a one-leaf filter -> the quarter-form filter instance (k_group_query<GB_LDS, 5, 512, 4>)
-    ("SELECT COUNT(*), SUM(d8), AVG(d8) FROM fact WHERE d2 < 800 GROUP BY d0, d1 TOP 10", 1 * 10000 + 5 * 1000 + 512),
-    # the same without the quarter-form filter (the chunk staged in LDS): k_group_query<GB_LDS, 4, 512, 4>
-    ("SELECT COUNT(*), SUM(d8), AVG(d8) FROM fact WHERE d2 < 800 GROUP BY d0, d1 TOP 10 |group.lds_qfilter=0",
+    # sum); 3 read columns -> the <= 3-column lane-owns-quarter GB_LDS instance (k_group_query<GB_LDS, 4, 512, 4>)
+    ("SELECT COUNT(*), SUM(d8), AVG(d8) FROM fact WHERE d2 < 800 GROUP BY d0, d1 TOP 10", 1 * 10000 + 4 * 1000 + 512),
+    # group.lds_qfilter=1: a one-leaf filter evaluated per quarter from its own loads (k_group_query<GB_LDS, 5, 512, 4>;
+    # measured slower, off by default); two leaves stay staged (PATH 4); no filter: the `pre` words only (PATH 5)
+    ("SELECT COUNT(*), SUM(d8), AVG(d8) FROM fact WHERE d2 < 800 GROUP BY d0, d1 TOP 10 |group.lds_qfilter=1",
+     1 * 10000 + 5 * 1000 + 512),
+    ("SELECT COUNT(*), SUM(d8) FROM fact WHERE d2 < 800 AND d3 > 100 GROUP BY d0, d1 TOP 10 |group.lds_qfilter=1",
      1 * 10000 + 4 * 1000 + 512),
-    # two filter leaves: staged (PATH 4); no filter: the quarter-form instance with the `pre` words only (PATH 5)
-    ("SELECT COUNT(*), SUM(d8) FROM fact WHERE d2 < 800 AND d3 > 100 GROUP BY d0, d1 TOP 10", 1 * 10000 + 4 * 1000 + 512),
-    ("SELECT COUNT(*), SUM(d8) FROM fact GROUP BY d0, d1 TOP 10", 1 * 10000 + 5 * 1000 + 512),
-    ("SELECT COUNT(*), MAX(d8) FROM fact WHERE d0 IN (1, 4, 9) GROUP BY d1, d0 TOP 10", 1 * 10000 + 5 * 1000 + 512),
+    ("SELECT COUNT(*), SUM(d8) FROM fact GROUP BY d0, d1 TOP 10 |group.lds_qfilter=1", 1 * 10000 + 5 * 1000 + 512),
+    ("SELECT COUNT(*), MAX(d8) FROM fact WHERE d0 IN (1, 4, 9) GROUP BY d1, d0 TOP 10 |group.lds_qfilter=1",
+     1 * 10000 + 5 * 1000 + 512),
     # MIN / MAX: 4 read columns -> the general lane-owns-quarter instance (k_group_query<GB_LDS, 3, 512, 4>)
     ("SELECT MIN(d8), MAX(d3), COUNT(*) FROM fact WHERE d2 < 800 GROUP BY d0, d1 TOP 10", 1 * 10000 + 3 * 1000 + 512),
     ("SELECT MAX(d3), SUM(d8), AVG(d8) FROM fact WHERE d2 < 800 GROUP BY d0, d1 TOP 10", 1 * 10000 + 3 * 1000 + 512),

@@ -416,9 +416,13 @@ def test_loopback_trimmed_server_answer(K):
                     assert v == [int(x) for x in e.reg]  # the registers (HyperLogLog.getBytes decoded)
                 else:
                     assert v == e, (text, k, f)
-        # the untrimmed merged result still holds every group
+        # the untrimmed merged result still holds every group; the trimmed one only the kept union (rank 0 got no more)
         res, _ = ex.group_by_result(q, gsegs)
         assert res.num_groups() == len(exp)
+        del res
+        res, _ = ex.group_by_result(q, gsegs, top_n=q["group_by"].get("top_n", 10))
+        n_aggs = len(q["aggregations"])
+        assert (res.num_groups() <= n_aggs * T) if trimmed else (res.num_groups() == len(exp))
         del res
     srv.close()
     eng.close()

@@ -420,9 +420,14 @@ def test_loopback_trimmed_server_answer(K):
         res, _ = ex.group_by_result(q, gsegs)
         assert res.num_groups() == len(exp)
         del res
-        res, _ = ex.group_by_result(q, gsegs, top_n=q["group_by"].get("top_n", 10))
+        top = q["group_by"].get("top_n", 10)
+        res, _ = ex.group_by_result(q, gsegs, top_n=top)
         n_aggs = len(q["aggregations"])
-        assert (res.num_groups() <= n_aggs * T) if trimmed else (res.num_groups() == len(exp))
+        if trimmed:  # at most every rank's per-function candidates reached rank 0; each function keeps T of them
+            assert res.num_groups() <= min(len(exp), K * n_aggs * T)
+            assert all(len(res.trimmed_groups(top, i)) == T for i in range(n_aggs))
+        else:
+            assert res.num_groups() == len(exp)
         del res
     srv.close()
     eng.close()

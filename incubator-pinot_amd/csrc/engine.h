@@ -547,7 +547,10 @@ struct AdmissionIO {
 void exec_group_by_partial_ks(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q,
                               const std::vector<int64_t> &gcard, const std::vector<std::vector<std::string>> &gvalues,
                               const std::vector<std::vector<std::vector<int32_t>>> &remap, int64_t *counts_dev,
-                              void *const *accs_dev, pinot_exec_stats *stats, AdmissionIO *aio = nullptr);
+                              void *const *accs_dev, pinot_exec_stats *stats, AdmissionIO *aio = nullptr,
+                              bool hll_sum_room = false, bool *hll_sums_written = nullptr);
+// (hll_sum_room: each HLL array holds u64 [G] after its registers, where the ring plan leaves the packed register
+// sums — set in *hll_sums_written — so a one-rank owner finalize reads cardinalities without the registers)
 // CombineGroupByOperator's cap over [S][words] admitted bitmaps in segment order: keys enter until `cap` are in
 void inter_segment_cap(std::vector<uint32_t> &bm, size_t S, int64_t words, int64_t cap);
 // Multi-value group-by (MV group columns or *MV functions): the extended function list (a hidden CountMV after the
@@ -572,11 +575,14 @@ DenseOut slice_outputs(Engine &e, const pinot_query &q, const std::vector<int> &
 // slice_outputs in two halves (a server's trimmed answer all-gathers the ranges' group counts between them): the
 // range's ordered non-empty keys (device) and their count, then the outputs of those keys — top_n > 0: of the range's
 // trimSize best groups per function only (AggregationGroupByTrimmingService, every group when the range holds no
-// more), with each kept group's mask of the functions that keep it in `flags`
+// more), with each kept group's mask of the functions that keep it in `flags`. gcard (the whole key space's, the
+// range being all of it): the DataTable's per-column ids and serialized HLLs made on the device as the engine's own
+// result has them; hll_sum: per aggregation, the ring plan's packed register sums (or null)
 unsigned long long slice_compact(Engine &e, const unsigned long long *counts, int64_t G, long long *&keys_dev);
 DenseOut slice_outputs_keys(Engine &e, const pinot_query &q, const std::vector<int> &acc_kind, unsigned long long *counts,
                             const std::vector<void *> &accs, int64_t G, int64_t key_base, const long long *keys_dev,
-                            unsigned long long n, int32_t top_n, std::vector<uint32_t> &flags);
+                            unsigned long long n, int32_t top_n, std::vector<uint32_t> &flags,
+                            const std::vector<int64_t> *gcard = nullptr, const std::vector<const void *> *hll_sum = nullptr);
 // The server trim over the ranges' candidates (flags: per gathered group, the functions whose range trim kept it):
 // each function keeps its trimSize best candidates — the merged map's trimSize best, as every group's range kept the
 // range's best — and the result becomes a device-trimmed one (fn_kept, trimmed_top_n, merged_groups).

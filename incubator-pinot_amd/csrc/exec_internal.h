@@ -471,6 +471,8 @@ struct GroupAccs {
 struct PartialOut {
   int64_t *counts;
   void *const *accs;
+  bool hll_sum_room = false;         // HLL arrays: u64 [G] after the registers for the ring plan's register sums
+  bool *hll_sums_written = nullptr;  // set: the ring plan left them
 };
 
 // Dense accumulators of one key range [key_base, key_base + G) -> result (the one-GPU group-by's back half, and the

@@ -1852,7 +1852,7 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     rr.G = ks.G;
     rr.counts = counts;
     rr.status = ring_status;
-    rr.hll_sums = po ? 0 : 1;  // the engine's HLL arrays have room for the sums; a caller's partial arrays do not
+    rr.hll_sums = po && !po->hll_sum_room ? 0 : 1;  // the engine's HLL arrays have room for the sums (a caller's if said)
     for (int i = 0; i < na; i++) {
       rr.aggs[i] = gaggs[i];  // segment 0's dictionary / LUT: identical on every segment (checked by plan_group)
       rr.aggs[i].lds_off = rp.lds_off[i];
@@ -1964,9 +1964,10 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
   }
 
   if (po) {  // partial: the dense accumulators are the caller's (u8 HLL registers included), no compaction
+    const bool sums = ring_status && po->hll_sum_room;
     for (int i = 0; i < na; i++)
       if (alias[i] >= 0 && ga.acc_kind[i] != 5 && po->accs[i] != po->accs[alias[i]])
-        PINOT_HIP(hipMemcpyAsync(po->accs[i], po->accs[alias[i]], ks.G * (ga.acc_kind[i] == 4 ? 256 : 8),
+        PINOT_HIP(hipMemcpyAsync(po->accs[i], po->accs[alias[i]], ks.G * (ga.acc_kind[i] == 4 ? (sums ? 264 : 256) : 8),
                                  hipMemcpyDeviceToDevice, e.stream));
     PINOT_HIP(hipGetLastError());
     std::vector<unsigned long long> hm(S);
@@ -1985,6 +1986,7 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     std::vector<int64_t> seg_counts(S);
     for (size_t si = 0; si < S; si++) seg_counts[si] = plans[si].empty ? 0 : (int64_t)hm[si];
     fill_stats(q, plans, seg_counts, pms, stats);
+    if (po->hll_sums_written) *po->hll_sums_written = sums;
     return nullptr;
   }
 

@@ -235,7 +235,8 @@ bool admission_cap_can_bind(const std::vector<SegmentData *> &segs, const pinot_
 void exec_group_by_partial_ks(Engine &e, const std::vector<SegmentData *> &segs, const pinot_query &q,
                               const std::vector<int64_t> &gcard, const std::vector<std::vector<std::string>> &gvalues,
                               const std::vector<std::vector<std::vector<int32_t>>> &remap, int64_t *counts_dev,
-                              void *const *accs_dev, pinot_exec_stats *stats, AdmissionIO *aio) {
+                              void *const *accs_dev, pinot_exec_stats *stats, AdmissionIO *aio, bool hll_sum_room,
+                              bool *hll_sums_written) {
   require(e.use_fused, PINOT_ERR_UNSUPPORTED, "multi-GPU group-by runs on the fused path (exec.fused=1)");
   KeySpace ks;
   ks.gcard = gcard;
@@ -245,7 +246,8 @@ void exec_group_by_partial_ks(Engine &e, const std::vector<SegmentData *> &segs,
   for (auto g : gcard) ks.G *= g;
   GroupAccs ga = group_acc_kinds(*segs[0], q);
   std::vector<void *> no_accs(q.num_aggregations, nullptr);  // export: the partial arrays are never touched
-  const PartialOut po{counts_dev, accs_dev ? accs_dev : no_accs.data()};
+  if (hll_sums_written) *hll_sums_written = false;
+  const PartialOut po{counts_dev, accs_dev ? accs_dev : no_accs.data(), hll_sum_room && accs_dev, hll_sums_written};
   exec_group_by_fused(e, segs, q, ks, ga, stats, 0, &po, nullptr, true, aio);
 }
 
@@ -268,23 +270,27 @@ unsigned long long slice_compact(Engine &e, const unsigned long long *counts, in
 
 DenseOut slice_outputs_keys(Engine &e, const pinot_query &q, const std::vector<int> &acc_kind, unsigned long long *counts,
                             const std::vector<void *> &accs, int64_t G, int64_t key_base, const long long *keys_dev,
-                            unsigned long long n, int32_t top_n, std::vector<uint32_t> &flags) {
+                            unsigned long long n, int32_t top_n, std::vector<uint32_t> &flags,
+                            const std::vector<int64_t> *gcard, const std::vector<const void *> *hll_sum) {
   KeySpace ks;
   ks.G = G;
+  if (gcard) ks.gcard = *gcard;
   GroupAccs ga;
   ga.acc_kind = acc_kind;
   ga.acc_bytes_per_key.assign(acc_kind.size(), 0);
   const std::vector<int> alias(acc_kind.size(), -1);
   DenseGroups dg{&q, &ks, &ga, &ga, &alias, counts, accs, key_base, nullptr};
+  if (hll_sum) dg.hll_sum = *hll_sum;
+  const bool serialize = gcard != nullptr;  // a trimmed subset only, as build_dense_result does
   flags.clear();
   if (top_n > 0 && n > 0) {  // this range's trimSize best groups per function (every group when it holds no more)
     const int64_t T = std::max<int64_t>(5 * (int64_t)top_n, 5000);
     std::vector<std::vector<int64_t>> kept;
     const long long *ukeys = device_trim(e, dg, keys_dev, n, top_n, kept, T, &flags);
-    if (ukeys != keys_dev) return dense_outputs(e, dg, ukeys, n, true, false);
+    if (ukeys != keys_dev) return dense_outputs(e, dg, ukeys, n, true, false, serialize);
     flags.assign((size_t)n, (uint32_t)((1ull << q.num_aggregations) - 1));
   }
-  return dense_outputs(e, dg, keys_dev, n);
+  return dense_outputs(e, dg, keys_dev, n);  // (every group: the host writes the DataTable, as the engine's does)
 }
 
 void server_trim_select(GroupByResult &r, int32_t top_n, const std::vector<uint32_t> &flags, int64_t merged_groups) {

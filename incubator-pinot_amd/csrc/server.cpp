@@ -688,11 +688,18 @@ std::unique_ptr<GroupByResult> server_group_by(ServerImpl &s, const std::vector<
     unsigned long long *counts = nullptr;
     std::vector<void *> accs(na, nullptr);
     pinot_exec_stats st{};
+    // one rank: its range is the whole merged map, so the ring plan's packed HLL register sums (u64 [G] after each
+    // HLL's registers) stay valid through D — the finalize then reads cardinalities as the engine's does
+    const bool sum_room = R == 1 && !mv;
+    bool sums_written = false;
+    auto acc_bytes = [&](int a) {
+      return ((size_t)Gp * acc_unit(gkinds[a]) + (sum_room && gkinds[a] == 4 ? (size_t)Gp * 8 : 0) + 255) / 256 * 256;
+    };
     my = capture([&] {
       std::lock_guard<std::mutex> el(e.mu);
       DeadlineScope ds(e, q.timeout_ms);
       size_t bytes = ((size_t)Gp * 8 + 255) / 256 * 256 + 256;
-      for (int a = 0; a < na; a++) bytes += ((size_t)Gp * acc_unit(gkinds[a]) + 255) / 256 * 256;
+      for (int a = 0; a < na; a++) bytes += acc_bytes(a);
       s.partial[i].reserve(bytes);
       uint8_t *p = s.partial[i].get<uint8_t>();
       counts = reinterpret_cast<unsigned long long *>(p);
@@ -700,7 +707,7 @@ std::unique_ptr<GroupByResult> server_group_by(ServerImpl &s, const std::vector<
       for (int a = 0; a < na; a++) {
         if (gkinds[a] == 5) continue;
         accs[a] = p;
-        p += ((size_t)Gp * acc_unit(gkinds[a]) + 255) / 256 * 256;
+        p += acc_bytes(a);
       }
       const int64_t from = segs.empty() ? 0 : G;
       PINOT_HIP(hipMemsetAsync(counts + from, 0, (size_t)(Gp - from) * 8, e.stream));
@@ -715,7 +722,7 @@ std::unique_ptr<GroupByResult> server_group_by(ServerImpl &s, const std::vector<
                                  &st);
       else if (!segs.empty())
         exec_group_by_partial_ks(e, segs, q, ks.gcard, ks.gvalues, ks.remap, reinterpret_cast<int64_t *>(counts),
-                                 accs.data(), &st, admit.mode ? &admit : nullptr);
+                                 accs.data(), &st, admit.mode ? &admit : nullptr, sum_room, &sums_written);
       PINOT_HIP(hipStreamSynchronize(e.stream));
     });
     ph.mark(2);
@@ -770,9 +777,15 @@ std::unique_ptr<GroupByResult> server_group_by(ServerImpl &s, const std::vector<
     const int64_t trim_size = std::max<int64_t>(5 * (int64_t)top_n, 5000);
     const bool trim = top && merged > 4 * trim_size;
     std::vector<uint32_t> flags;
-    const DenseOut own = slice_outputs_keys(e, q, gkinds, counts + base, sl, g, base, keys_dev, nr, trim ? top_n : 0, flags);
+    std::vector<const void *> sums;
+    if (sums_written)
+      for (int a = 0; a < na; a++)
+        sums.push_back(gkinds[a] == 4 && accs[a] ? static_cast<const uint8_t *>(accs[a]) + (size_t)G * 256 : nullptr);
+    const bool one = !s.gather || R == 1;  // this rank's outputs are the answer's (nothing gathered after them)
+    const DenseOut own = slice_outputs_keys(e, q, gkinds, counts + base, sl, g, base, keys_dev, nr, trim ? top_n : 0, flags,
+                                            R == 1 && !mv ? &ks.gcard : nullptr, sums_written ? &sums : nullptr);
     ph.mark(5);
-    if (!s.gather || R == 1) {
+    if (one) {
       res[i] = slice_result(e, q, ks.gcard, ks.gvalues, own);
       if (trim) server_trim_select(*res[i], top_n, flags, merged);
       ph.mark(6);

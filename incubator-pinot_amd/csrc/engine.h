@@ -589,6 +589,9 @@ DenseOut slice_outputs_keys(Engine &e, const pinot_query &q, const std::vector<i
 void server_trim_select(GroupByResult &r, int32_t top_n, const std::vector<uint32_t> &flags, int64_t merged_groups);
 // the device arrays of n gathered groups, in e's gather buffers, laid out as slice_outputs lays them out
 DenseOut slice_alloc(Engine &e, const pinot_query &q, const std::vector<int> &acc_kind, unsigned long long n);
+// rank 0's gathered trimmed answer, after the gather on the same stream: the DataTable's per-column ids and serialized
+// HLLs on the device, as dense_outputs makes them for a one-GPU trimmed result
+void slice_serialize(Engine &e, const pinot_query &q, const std::vector<int64_t> &gcard, DenseOut &o);
 // the gatherable arrays of a DenseOut in a fixed order: (device pointer, bytes per group)
 std::vector<std::pair<void *, size_t>> slice_arrays(const DenseOut &o);
 // host half: the D2H into a result

@@ -345,7 +345,8 @@ DenseOut slice_alloc(Engine &e, const pinot_query &q, const std::vector<int> &ac
     if (acc_kind[i] == 4) o.derive[i] = -2;
   }
   const size_t n8 = n * 8;
-  e.group_gather.reserve(n8 * (2 + na + n_card) + 256);
+  // (+ room after the arrays for the key tuples of slice_serialize)
+  e.group_gather.reserve(n8 * (2 + na + n_card) + 256 + n * (size_t)q.num_group_by * 4 + 16);
   o.keys = e.group_gather.get<long long>();
   o.counts = o.keys + n;
   double *v = reinterpret_cast<double *>(o.counts + n);
@@ -370,6 +371,38 @@ DenseOut slice_alloc(Engine &e, const pinot_query &q, const std::vector<int> &ac
       if (acc_kind[i] == 4) o.hll_off[i] = (size_t)(h++) * n * 256;
   }
   return o;
+}
+
+void launch_hll_getbytes(const uint8_t *regs, long long n, uint8_t *out, hipStream_t stream);  // hll_serde.hip
+
+void slice_serialize(Engine &e, const pinot_query &q, const std::vector<int64_t> &gcard, DenseOut &o) {
+  const unsigned long long n = o.n;
+  const int na = q.num_aggregations, nc = q.num_group_by;
+  if (!n) return;
+  int n_card = 0;
+  for (int i = 0; i < na; i++) n_card += o.kind[i] == 4;
+  if (nc <= kDigitsMaxCols && (int)gcard.size() == nc) {  // the gathered keys are global raw keys (key base 0)
+    KeyDigits kd{};
+    kd.nc = nc;
+    for (int j = 0; j < nc; j++) kd.card[j] = gcard[j];
+    o.key_ids = reinterpret_cast<int32_t *>(reinterpret_cast<uint8_t *>(o.keys) + n * 8 * (size_t)(2 + na + n_card));
+    launch_key_digits(o.keys, (long long)n, 0, kd, o.key_ids, e.stream);
+  }
+  if (o.hll && n_card) {
+    const size_t need = (size_t)n_card * n * 180 + 16;
+    if (!e.hll_ser || e.hll_ser.use_count() > 1 || e.hll_ser->size() < need)
+      e.hll_ser = std::make_shared<DeviceBuffer>(need + need / 4);
+    o.hll_ser = e.hll_ser;
+    o.hll_ser_off.assign(na, 0);
+    int s = 0;
+    for (int i = 0; i < na; i++)
+      if (o.kind[i] == 4) {
+        o.hll_ser_off[i] = (size_t)(s++) * n * 180;
+        launch_hll_getbytes(o.hll->get<uint8_t>() + o.hll_off[i], (long long)n, o.hll_ser->get<uint8_t>() + o.hll_ser_off[i],
+                            e.stream);
+      }
+  }
+  PINOT_HIP(hipGetLastError());
 }
 
 std::vector<std::pair<void *, size_t>> slice_arrays(const DenseOut &o) {

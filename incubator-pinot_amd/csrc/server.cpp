@@ -812,7 +812,7 @@ std::unique_ptr<GroupByResult> server_group_by(ServerImpl &s, const std::vector<
         if (!fb.empty()) memcpy(all_flags.data() + at, fb.data(), fb.size());
       }
     }
-    const DenseOut root = me == 0 ? slice_alloc(e, q, gkinds, prefix[R]) : DenseOut{};
+    DenseOut root = me == 0 ? slice_alloc(e, q, gkinds, prefix[R]) : DenseOut{};
     const auto send = slice_arrays(own);
     const auto recv = me == 0 ? slice_arrays(root) : std::vector<std::pair<void *, size_t>>(send.size(), {nullptr, 0});
     c.group_start();
@@ -824,6 +824,7 @@ std::unique_ptr<GroupByResult> server_group_by(ServerImpl &s, const std::vector<
     }
     c.group_end();
     if (me == 0) {
+      if (trim && !mv) slice_serialize(e, q, ks.gcard, root);  // the trimmed answer's DataTable pieces, on the device
       res[i] = slice_result(e, q, ks.gcard, ks.gvalues, root);
       if (trim) server_trim_select(*res[i], top_n, all_flags, merged);
     } else {

@@ -87,6 +87,37 @@ def test_ring_config4_shape(hll, rec6):
     e.close()
 
 
+def test_ring_one_rank_server_answer():
+    """The multi-GPU server with one rank on config 4's query at 2 x 2M docs (server.cpp): its partial runs the ring
+    plan and keeps the packed HLL register sums in the partial arrays, the owner finalize reads the cardinalities from
+    them, and the trimmed answer's key ids and serialized HLLs are made on the device. The untrimmed server arrays equal
+    the oracle's; the trimmed DataTable's cells equal the engine path's."""
+    import datatable as D
+    from pinot_amd import GpuServer, ServerExecutor
+    host = [synth.make_segment("fact_%d" % s, 2_000_000, CONFIG_COLUMNS, BASE_SEED + s) for s in range(2)]
+    srv = GpuServer([0], "group.ring=1")
+    e0 = srv.engines[0]
+    gsegs = [e0.register_synthetic("fact_%d" % s, 2_000_000, CONFIG_COLUMNS, BASE_SEED + s) for s in range(2)]
+    ex = ServerExecutor(srv, num_groups_limit=1_000_000)
+    q = compile_pql(CONFIG4)
+    exp = O.execute_group_by_arrays(host, q, num_groups_limit=1_000_000)
+    before = e0.stat("group.ring_queries"), e0.stat("group.ring_fallbacks")
+    res, st = ex.group_by_result(q, gsegs)
+    assert (e0.stat("group.ring_queries") - before[0], e0.stat("group.ring_fallbacks") - before[1]) == (1, 0)
+    assert e0.stat("group.ring_hll_slot") == 1
+    _assert_group_arrays(res, exp, q)
+    del res
+    data, _ = ex.process_query_datatable(q, gsegs, trim=True)
+    e = GpuEngine(0, "group.ring=1")
+    esegs = [e.register_synthetic("fact_%d" % s, 2_000_000, CONFIG_COLUMNS, BASE_SEED + s) for s in range(2)]
+    ref, _ = ServerQueryExecutor(e, num_groups_limit=1_000_000).process_query_datatable(q, esegs, trim=True)
+    d, r = D.decode(data), D.decode(ref)
+    assert d["cells"] == r["cells"]
+    assert all(len(row[1]) == 5000 for row in d["cells"])
+    e.close()
+    srv.close()
+
+
 _POOL = np.random.default_rng(77)
 LV_POOL = _POOL.integers(-(1 << 40), 1 << 40, 3000) * 7
 DV_POOL = (_POOL.standard_normal(2000) * 1e6).round(3)

@@ -1972,10 +1972,14 @@ std::unique_ptr<GroupByResult> exec_group_by_fused(Engine &e, const std::vector<
     PINOT_HIP(hipGetLastError());
     std::vector<unsigned long long> hm(S);
     uint32_t rs[4] = {0, 0, 0, 0};
-    PINOT_HIP(hipMemcpyAsync(hm.data(), matched, S * 8, hipMemcpyDeviceToHost, e.stream));
-    if (ring_status) PINOT_HIP(hipMemcpyAsync(rs, ring_status, 16, hipMemcpyDeviceToHost, e.stream));
+    e.d2h_small.reserve(S * 8 + 64);  // pinned: asynchronous copies, one wait
+    uint8_t *pin = e.d2h_small.get<uint8_t>();
+    PINOT_HIP(hipMemcpyAsync(pin, matched, S * 8, hipMemcpyDeviceToHost, e.stream));
+    if (ring_status) PINOT_HIP(hipMemcpyAsync(pin + S * 8, ring_status, 16, hipMemcpyDeviceToHost, e.stream));
     PINOT_HIP(hipEventRecord(e.ev_stop, e.stream));
     wait_stream(e);
+    memcpy(hm.data(), pin, S * 8);
+    if (ring_status) memcpy(rs, pin + S * 8, 16);
     if (rs[0]) {
       e.ring_last_status = rs[0];
       return ring_fallback();

@@ -38,6 +38,16 @@
 
 namespace pinot {
 
+// The last group-by's global key space of one local engine (phase A's union dictionaries, global values and local
+// remaps), reused while its inputs are the same: this rank's segments (process-unique ids: their dictionaries never
+// change), the group columns and every rank's exchanged dictionaries, byte for byte.
+struct KeySpaceCache {
+  std::vector<uint64_t> uids;
+  std::vector<std::string> cols;
+  std::vector<std::vector<uint8_t>> dicts;
+  std::shared_ptr<const GlobalKeySpace> ks;
+};
+
 struct ServerImpl {
   std::vector<std::unique_ptr<pinot_engine>> engines;  // local GPUs (local engine i is rank rank0 + i)
   std::vector<std::unique_ptr<Collective>> comms;      // one per local engine (destroyed before the engines)
@@ -46,6 +56,7 @@ struct ServerImpl {
   bool gather = true;                                  // group-by: the whole result on rank 0
   std::mutex mu;                                       // one server call at a time (engines are locked too)
   std::vector<DeviceBuffer> partial;                   // per engine: dense group-by partials
+  std::vector<KeySpaceCache> ks_cache;                 // per engine
   double phase_ms[kServerPhases] = {};                 // last query, local engine 0's rank (server_last_phases)
 };
 
@@ -53,6 +64,22 @@ namespace {
 
 using Clock = std::chrono::steady_clock;
 double ms_since(Clock::time_point t) { return std::chrono::duration<double, std::milli>(Clock::now() - t).count(); }
+
+std::shared_ptr<const GlobalKeySpace> key_space_cached(KeySpaceCache &c, const std::vector<SegmentData *> &segs,
+                                                       const pinot_query &q,
+                                                       const std::vector<std::vector<uint8_t>> &dicts) {
+  std::vector<uint64_t> uids;
+  for (const SegmentData *sg : segs) uids.push_back(sg->uid);
+  std::vector<std::string> cols;
+  for (int j = 0; j < q.num_group_by; j++) cols.emplace_back(q.group_by[j]);
+  if (c.ks && c.uids == uids && c.cols == cols && c.dicts == dicts) return c.ks;
+  auto ks = std::make_shared<const GlobalKeySpace>(global_key_space(segs, q, dicts));
+  c.uids = std::move(uids);
+  c.cols = std::move(cols);
+  c.dicts = dicts;
+  c.ks = ks;
+  return ks;
+}
 
 // phase timer of local engine 0 (the other engines' threads pass nullptr)
 struct Phases {
@@ -508,6 +535,7 @@ std::unique_ptr<GroupByResult> server_group_by(ServerImpl &s, const std::vector<
   std::vector<std::unique_ptr<GroupByResult>> res(E);
   std::vector<pinot_exec_stats> tot(E);
   std::atomic<bool> hashed_result{false};  // rank 0 holds the merged hashed result (the others an empty one)
+  if (s.ks_cache.size() < E) s.ks_cache.resize(E);
   for_engines(s, [&](size_t i) {
     Engine &e = *s.engines[i];
     Collective &c = *s.comms[i];
@@ -558,8 +586,10 @@ std::unique_ptr<GroupByResult> server_group_by(ServerImpl &s, const std::vector<
     }
     fail_together(sts, me, "group-by");
     require(kinds_agree, PINOT_ERR_UNSUPPORTED, "multi-GPU group-by: ranks disagree on the aggregated columns' types");
-    GlobalKeySpace ks;
-    if (!gkinds.empty()) ks = global_key_space(segs, q, rank_dicts);  // identical on every rank (same inputs)
+    // identical on every rank (same inputs)
+    const std::shared_ptr<const GlobalKeySpace> ksp =
+        gkinds.empty() ? std::make_shared<const GlobalKeySpace>() : key_space_cached(s.ks_cache[i], segs, q, rank_dicts);
+    const GlobalKeySpace &ks = *ksp;
     ph.mark(1);
     const int64_t limit = q.num_groups_limit > 0 ? q.num_groups_limit : e.num_groups_limit;
     if (ks.hashed) {

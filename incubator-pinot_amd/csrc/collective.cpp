@@ -57,13 +57,31 @@ std::shared_ptr<Hub> loopback_hub(const uint8_t *id, int nranks, int timeout_ms,
 
 std::vector<std::vector<uint8_t>> Collective::all_gather_host(const std::vector<uint8_t> &mine, hipStream_t st) {
   if (nranks_ == 1) return {mine};
-  std::vector<int64_t> sizes(nranks_);
+  // one fixed-size round carries every rank's size and, when it fits, its payload (the control messages of an
+  // aggregation or a group-by phase do): a second round only for payloads beyond the inline room. Every rank knows
+  // every size after the first round, so all take the second one together.
+  constexpr size_t kInline = 4096;
+  std::vector<uint8_t> block(kInline, 0), first(kInline * (size_t)nranks_);
   const int64_t sz = (int64_t)mine.size();
-  all_gather_fixed_host(&sz, 8, reinterpret_cast<uint8_t *>(sizes.data()), st);
+  memcpy(block.data(), &sz, 8);
+  if (!mine.empty() && mine.size() <= kInline - 8) memcpy(block.data() + 8, mine.data(), mine.size());
+  all_gather_fixed_host(block.data(), kInline, first.data(), st);
+  std::vector<int64_t> sizes(nranks_);
   int64_t mx = 0;
-  for (int64_t s : sizes) mx = std::max(mx, s);
+  for (int r = 0; r < nranks_; r++) {
+    memcpy(&sizes[r], first.data() + (size_t)r * kInline, 8);
+    require(sizes[r] >= 0, PINOT_ERR_DEVICE, "server communicator: bad control payload size");
+    mx = std::max(mx, sizes[r]);
+  }
   std::vector<std::vector<uint8_t>> out(nranks_);
   if (mx == 0) return out;
+  if (mx <= (int64_t)(kInline - 8)) {
+    for (int r = 0; r < nranks_; r++) {
+      const auto at = first.begin() + (size_t)r * kInline + 8;
+      out[r].assign(at, at + sizes[r]);
+    }
+    return out;
+  }
   std::vector<uint8_t> padded(mx, 0), all((size_t)mx * nranks_);
   if (!mine.empty()) memcpy(padded.data(), mine.data(), mine.size());
   all_gather_fixed_host(padded.data(), (size_t)mx, all.data(), st);

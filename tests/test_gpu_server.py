@@ -86,6 +86,26 @@ def test_server_one_gpu_union_dictionaries():
     srv.close()
 
 
+def test_server_key_space_reuse_across_segment_sets():
+    """Phase A's global key space is reused while its inputs match (server.cpp KeySpaceCache): the same server answers
+    over one segment set, a subset of it, a set with other dictionaries (segments registered later, one of them after
+    an unregister) and the first set again, each equal to the oracle's."""
+    rng = np.random.default_rng(12)
+    host = _segments(rng, 20000, 3)
+    other = _segments(np.random.default_rng(13), 15000, 2)
+    srv = GpuServer([0])
+    e0 = srv.engines[0]
+    gsegs = [e0.register(s) for s in host]
+    _check(srv, gsegs, host)
+    _check(srv, gsegs[:2], host[:2])
+    gsegs[2].release()
+    osegs = [e0.register(s) for s in other]
+    _check(srv, osegs, other)
+    _check(srv, gsegs[:2] + osegs[:1], host[:2] + other[:1])
+    _check(srv, gsegs[:2], host[:2])
+    srv.close()
+
+
 def test_server_multi_process_form_one_rank():
     rng = np.random.default_rng(12)
     host = _segments(rng, 15000, 2)

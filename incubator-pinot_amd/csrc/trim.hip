@@ -210,20 +210,41 @@ __global__ __launch_bounds__(kTrimPickBlock) void k_trim_pick(TrimArgs a, int ro
     c[i >> 8][i & 255] = t;
   }
   __syncthreads();
-  if (tid < a.nf) {
-    const int f = tid;
-    unsigned long long r = a.st->rank[f], cum = 0;
-    int d = 0;
+  // wave f finds function f's digit: the first d (<= 255) whose inclusive count prefix exceeds the remaining rank, cum
+  // the count below it (a wave scan over four digits per lane instead of one thread's 255-step walk)
+  const int wv = tid >> 6, lane = tid & 63;
+  if (wv < a.nf) {
+    const int f = wv;
+    const unsigned long long r = a.st->rank[f];
     if ((vary >> f) & 1u) {
-      for (; d < 255; d++) {
-        if (r < cum + c[f][d]) break;
-        cum += c[f][d];
+      uint32_t c4[4];
+      unsigned long long s = 0;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        c4[k] = c[f][4 * lane + k];
+        s += c4[k];
       }
-    } else {
-      d = (int)((a.st->kand[f] >> shift) & 255ull);  // every key's digit: the rank stays
+      unsigned long long inc = s;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const unsigned long long y = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += y;
+      }
+      const unsigned long long hit = __ballot(r < inc);
+      const int L = hit ? (int)__builtin_ctzll(hit) : 63;
+      if (lane == L) {
+        unsigned long long cum = inc - s;
+        int d = 4 * lane;
+        for (int k = 0; k < 4 && d < 255; k++, d++) {
+          if (r < cum + c4[k]) break;
+          cum += c4[k];
+        }
+        a.st->prefix[f] |= (unsigned long long)d << shift;
+        a.st->rank[f] = r - cum;
+      }
+    } else if (lane == 0) {  // every key's digit: the rank stays
+      a.st->prefix[f] |= ((a.st->kand[f] >> shift) & 255ull) << shift;
     }
-    a.st->prefix[f] |= (unsigned long long)d << shift;
-    a.st->rank[f] = r - cum;
   }
 }
 
